@@ -1,0 +1,19 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, 'tests', 'golden')):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line('markers', 'gpu: needs an MI355X (HIP) device')
+    config.addinivalue_line('markers', 'slow: long-running CPU test')
+
+
+def golden(name):
+    import numpy as np
+    return np.load(os.path.join(ROOT, 'tests', 'golden', name))

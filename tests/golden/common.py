@@ -1,0 +1,143 @@
+"""Input builders shared by the golden generator and the tests.
+
+Large inputs and upstream gradients are NOT stored in the fixtures: they are regenerated
+bit-identically from CPU `torch.Generator` seeds here (same torch build in the build container
+and on the GPU box), and every fixture stores a checksum of them so that drift is detected.
+"""
+import numpy as np
+import torch
+
+from vfdepth_amd import config as C
+from vfdepth_amd import synth
+from vfdepth_amd.rotation import axis_angle_to_matrix
+
+
+def seeded_randn(shape, seed):
+    return torch.randn(tuple(shape), generator=torch.Generator().manual_seed(int(seed)))
+
+
+def checksum(t):
+    t = t.detach().double()
+    return np.array([t.sum().item(), (t * t).sum().item(), float(t.numel())])
+
+
+def random_mask(gen, shape):
+    """Binary self-occlusion mask (bottom 15 % invalid) with one fractional, antialiased row."""
+    m = torch.ones(shape)
+    H = shape[-2]
+    cut = int(round(H * 0.85))
+    m[..., cut:, :] = 0.0
+    m[..., cut - 1, :] = torch.rand(tuple(shape[:-2]) + (shape[-1],), generator=gen)
+    return m
+
+
+# ------------------------------------------------------------------------------------ fusion
+def fusion_cfg():
+    return C.surround_fusion_cfg(height=96, width=160, batch_size=2, fusion_feat_in_dim=8,
+                                 voxel_size=[16, 16, 6], voxel_unit_size=[6.0, 6.0, 5.0],
+                                 voxel_str_p=[-45.0, -45.0, -12.5], voxel_pre_dim=[8],
+                                 proj_d_bins=6)
+
+
+def fusion_case():
+    cfg = fusion_cfg()
+    gen = torch.Generator().manual_seed(11)
+    B, N, Cf = 2, 6, 8
+    batch = synth.make_batch(cfg, seed=3)
+    d = {'K': batch[('K', 3)], 'invK': batch[('inv_K', 3)], 'E': batch['extrinsics']}
+    d['Einv'] = torch.inverse(d['E'])
+    d['mask'] = random_mask(gen, (B, N, 1, 96, 160))
+    d['feats'] = torch.randn(B, N, Cf, 12, 20, generator=gen)
+    seeds = {'g_vox': 101, 'g_pose': 102, 'vleaf': 103, 'g_proj': 104}
+    return cfg, d, seeds
+
+
+# ------------------------------------------------------------------------------------ view synthesis
+VIEW_B, VIEW_H, VIEW_W = 2, 24, 40
+
+
+def view_case(skip_sample=False):
+    B, H, W = VIEW_B, VIEW_H, VIEW_W
+    seed = 22 if skip_sample else 21
+    cfg = C.surround_fusion_cfg(height=H, width=W, batch_size=B)
+    gen = torch.Generator().manual_seed(seed)
+    batch = synth.make_batch(cfg, seed=seed)
+    batch['extrinsics_inv'] = torch.inverse(batch['extrinsics'])
+    K0 = synth.rig_intrinsics(6, H, W)
+    gt = synth.ground_plane_depth(K0, synth.rig_extrinsics(6), H, W, 1.5, 60.0)
+    depth = gt.unsqueeze(0).repeat(B, 1, 1, 1, 1) * (0.8 + 0.4 * torch.rand(B, 6, 1, H, W, generator=gen))
+    batch['mask'] = random_mask(gen, (B, 6, 1, H, W))
+    poses = {}
+    for f in (-1, 1):
+        aa = 0.02 * torch.randn(B, 1, 3, generator=gen)
+        tr = 0.5 * torch.randn(B, 1, 3, generator=gen)
+        if skip_sample:
+            tr[1] = 500.0            # sample 1: temporal warps leave the image -> empty overlap
+        T = torch.eye(4).repeat(B, 1, 1)
+        T[:, :3, :3] = axis_angle_to_matrix(aa)[:, 0]
+        T[:, :3, 3] = tr[:, 0]
+        for c in range(6):
+            # per-camera variation, as distribute_pose would produce
+            Tc = T.clone()
+            Tc[:, :3, 3] += 0.05 * c
+            poses[(c, f)] = Tc
+    if skip_sample:
+        depth[1] = 0.02              # sample 1: spatial warps fall outside the neighbours
+    return cfg, batch, depth, poses
+
+
+VIEW_IMG_KEYS = [('color', -1, 0), ('color', 1, 0), ('overlap', 0, 0), ('overlap', -1, 0), ('overlap', 1, 0)]
+VIEW_MSK_KEYS = [('color_mask', -1, 0), ('color_mask', 1, 0), ('overlap_mask', 0, 0),
+                 ('overlap_mask', -1, 0), ('overlap_mask', 1, 0)]
+
+
+def key_name(k):
+    return '_'.join(str(x) for x in k)
+
+
+# ------------------------------------------------------------------------------------ losses
+def loss_case():
+    """Synthetic warped planes around the target so every loss branch is exercised."""
+    B, H, W = VIEW_B, VIEW_H, VIEW_W
+    cfg = C.surround_fusion_cfg(height=H, width=W, batch_size=B)
+    gen = torch.Generator().manual_seed(31)
+    batch = synth.make_batch(cfg, seed=31)
+    batch['mask'] = random_mask(gen, (B, 6, 1, H, W))
+    planes = {}
+    for c in range(6):
+        tgt = batch[('color', 0, 0)][:, c]
+        for k in VIEW_IMG_KEYS:
+            noise = torch.rand(B, 3, H, W, generator=gen) - 0.5
+            amp = 0.05 + 0.3 * torch.rand(B, 1, 1, 1, generator=gen)
+            img = (tgt + amp * noise).clamp(0, 1)
+            # a block of exact zeros (out-of-image warp) and of NaN-filled 2.0
+            img[:, :, :3, :5] = 0.0
+            img[:, :, -2:, -4:] = 2.0
+            planes[(c,) + k] = img
+        for f in (0, -1, 1):
+            m = (torch.rand(B, 1, H, W, generator=gen) > 0.3).float()
+            m = m + (torch.rand(B, 1, H, W, generator=gen) > 0.7).float()     # overlap masks reach 2
+            planes[(c, 'overlap_mask', f, 0)] = m
+        planes[(c, 'disp', 0)] = 0.2 + 0.6 * torch.rand(B, 1, H, W, generator=gen)
+    return cfg, batch, planes
+
+
+# ------------------------------------------------------------------------------------ full step
+STEP_SEED = 7
+
+
+def step_cfg():
+    return C.surround_fusion_cfg(height=96, width=160, batch_size=1, voxel_size=[40, 40, 10],
+                                 voxel_unit_size=[2.5, 2.5, 3.0], voxel_str_p=[-50.0, -50.0, -15.0],
+                                 proj_d_bins=16, focal_length_scale=30)
+
+
+def mono_cfg():
+    return C.mono_cfg(batch_size=1)
+
+
+PARAM_GRADS = ['depth_net.decoder.decoder.0.0.weight', 'depth_net.fusion_net.conv_overlap.0.weight',
+               'depth_net.fusion_net.conv_non_overlap.0.bias', 'depth_net.fusion_net.reduce_dim.0.bias',
+               'depth_net.conv1x1.0.bias', 'pose_net.pose_decoder.net.3.weight',
+               'pose_net.fusion_net.reduce_dim.0.bias', 'pose_net.conv1x1.0.bias',
+               'depth_net.depth_decoder.decoder.10.conv.conv.weight', 'pose_net.pose_decoder.net.3.bias']

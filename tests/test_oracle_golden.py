@@ -1,0 +1,131 @@
+"""Pin the CPU oracle against golden vectors produced by the real reference (CPU only).
+
+The oracle (`oracle/vfd_oracle.py`) restates the hot path with explicit index arithmetic; here it
+must reproduce the reference's own outputs and gradients (fixtures from
+`tests/golden/gen_golden.py`).  Tolerances: fp32 math in a different operation order, so
+1e-5 absolute / 1e-4 relative on values; gradients 1e-4 relative to their scale.
+"""
+import numpy as np
+import pytest
+import torch
+
+import common as G
+from conftest import golden
+from oracle import vfd_oracle as O
+
+
+def close(a, b, rtol=1e-4, atol=1e-5, what=''):
+    a = a.detach().cpu().double().numpy() if torch.is_tensor(a) else np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    assert a.shape == b.shape, f'{what}: shape {a.shape} vs {b.shape}'
+    err = np.abs(a - b)
+    tol = atol + rtol * np.abs(b)
+    bad = err > tol
+    assert not bad.any(), f'{what}: {bad.sum()} / {bad.size} off, max err {err.max():.3g}'
+
+
+def grad_close(a, b, what='', rel=1e-4):
+    a = a.detach().double().numpy()
+    b = np.asarray(b, np.float64)
+    scale = max(np.abs(b).max(), 1e-12)
+    err = np.abs(a - b).max() / scale
+    assert err < rel, f'{what}: max err {err:.3g} of scale {scale:.3g}'
+
+
+def test_fusion_inputs_reproducible():
+    fx = golden('fusion_small.npz')
+    _, d, _ = G.fusion_case()
+    for k, t in (('feats', d['feats']), ('mask', d['mask']), ('K', d['K']), ('E', d['E'])):
+        np.testing.assert_array_equal(G.checksum(t), fx['cs_' + k])
+
+
+def test_fusion_depth_mode():
+    fx = golden('fusion_small.npz')
+    cfg, d, seeds = G.fusion_case()
+    spec = O.VoxelSpec(cfg)
+    feats = d['feats'].clone().requires_grad_(True)
+    w_no, b_no = [torch.tensor(fx[k]).requires_grad_(True) for k in ('w_no', 'b_no')]
+    w_o, b_o = [torch.tensor(fx[k]).requires_grad_(True) for k in ('w_o', 'b_o')]
+    vox = O.fuse_depth(spec, feats, d['mask'], d['K'], d['Einv'], w_no, b_no, w_o, b_o)
+    close(vox, fx['vox'], what='voxel features')
+    (vox * G.seeded_randn(vox.shape, seeds['g_vox'])).sum().backward()
+    grad_close(feats.grad, fx['d_feats_depth'], 'd feats')
+    for t, k in ((w_no, 'd_w_no'), (b_no, 'd_b_no'), (w_o, 'd_w_o'), (b_o, 'd_b_o')):
+        grad_close(t.grad, fx[k], k)
+    cnt = np.stack([(np.abs(fx['vox']) > 0).any(1)])
+    assert cnt.mean() > 0.05  # fixture exercises non-empty fusion
+
+
+def test_fusion_pose_mode():
+    fx = golden('fusion_small.npz')
+    cfg, d, seeds = G.fusion_case()
+    spec = O.VoxelSpec(cfg)
+    feats = d['feats'].clone().requires_grad_(True)
+    v = O.fuse_pose(spec, feats, d['mask'], d['K'], d['Einv'])
+    close(v, fx['vpose'], what='pose voxels')
+    (v * G.seeded_randn(v.shape, seeds['g_pose'])).sum().backward()
+    grad_close(feats.grad, fx['d_feats_pose'], 'd feats (pose)')
+
+
+def test_voxel_projection():
+    fx = golden('fusion_small.npz')
+    cfg, d, seeds = G.fusion_case()
+    spec = O.VoxelSpec(cfg)
+    vleaf = G.seeded_randn(fx['vox'].shape, seeds['vleaf']).requires_grad_(True)
+    proj = torch.stack(O.project_voxels(spec, vleaf, d['invK'], d['E']), 1)
+    close(proj, fx['proj'], what='frustum features')
+    (proj * G.seeded_randn(proj.shape, seeds['g_proj'])).sum().backward()
+    grad_close(vleaf.grad, fx['d_vleaf'], 'd voxel')
+
+
+@pytest.mark.parametrize('name,skip', [('view_small.npz', False), ('view_skip.npz', True)])
+def test_view_rendering(name, skip):
+    fx = golden(name)
+    cfg, batch, depth, poses = G.view_case(skip)
+    np.testing.assert_array_equal(G.checksum(depth), fx['cs_depth'])
+    for c in range(6):
+        d = depth[:, c].clone().requires_grad_(True)
+        Ts = {f: poses[(c, f)].clone().requires_grad_(True) for f in (-1, 1)}
+        out = {('depth', 0): d, ('cam_T_cam', 0, -1): Ts[-1], ('cam_T_cam', 0, 1): Ts[1]}
+        O.view_rendering(batch, out, c, O.relative_poses(batch, out, c, cfg), cfg)
+        loss = 0
+        for i, k in enumerate(G.VIEW_IMG_KEYS):
+            close(out[k], fx[f'{G.key_name(k)}_c{c}'], what=f'{k} cam {c}')
+            loss = loss + (out[k] * G.seeded_randn(out[k].shape, 500 + 10 * c + i)).sum()
+        for k in G.VIEW_MSK_KEYS:
+            close(out[k], fx[f'{G.key_name(k)}_c{c}'], what=f'{k} cam {c}')
+        loss.backward()
+        grad_close(d.grad, fx[f'd_depth_c{c}'], f'd depth cam {c}', rel=2e-4)
+        for f in (-1, 1):
+            grad_close(Ts[f].grad, fx[f'd_T_{f}_c{c}'], f'd T{f} cam {c}', rel=2e-4)
+
+
+def test_losses():
+    fx = golden('loss_small.npz')
+    cfg, batch, planes = G.loss_case()
+    for c in range(6):
+        out, leaves = {}, {}
+        for k in G.VIEW_IMG_KEYS:
+            leaves[k] = planes[(c,) + k].clone().requires_grad_(True)
+            out[k] = leaves[k]
+        for f in (0, -1, 1):
+            out[('overlap_mask', f, 0)] = planes[(c, 'overlap_mask', f, 0)].clone()
+        disp = planes[(c, 'disp', 0)].clone().requires_grad_(True)
+        out[('disp', 0)] = disp
+        cl, terms = O.cam_loss(batch, out, c, cfg, torch.tensor(fx[f'noise_c{c}']))
+        close(cl, fx[f'cam_loss_c{c}'], what=f'cam loss {c}')
+        for k in ('reproj_loss', 'spatio_loss', 'spatio_tempo_loss', 'smooth'):
+            close(terms[k], fx[f'{k}_c{c}'], what=f'{k} {c}')
+        close(out[('reproj_loss', 0)], fx[f'reproj_plane_c{c}'], what='reproj plane')
+        close(out[('reproj_mask', 0)], fx[f'reproj_mask_c{c}'], what='reproj mask')
+        close(out[('overlap_mask', 0, 0)], fx[f'spatio_mask_c{c}'], what='spatio mask')
+        cl.backward()
+        for k in G.VIEW_IMG_KEYS:
+            grad_close(leaves[k].grad, fx[f'd_{G.key_name(k)}_c{c}'], f'd {k} cam {c}')
+        grad_close(disp.grad, fx[f'd_disp_c{c}'], f'd disp cam {c}')
+
+
+def test_depth_metrics():
+    fx = golden('metrics.npz')
+    errs = O.depth_errors(torch.tensor(fx['pred']), torch.tensor(fx['gt']))
+    close(torch.stack([e.double() for e in errs]), fx['errs'], rtol=1e-5, atol=1e-7, what='depth errors')

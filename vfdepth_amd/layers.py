@@ -1,0 +1,292 @@
+"""Dense CNN layers around the hot path (they stay on MIOpen / hipBLASLt via PyTorch-ROCm).
+
+* `conv2d_block` / `conv1d_block`: the reference's conv + (BN|Identity) + act Sequential builders
+  (`/root/reference/network/blocks.py:41-84`); kept as `nn.Sequential(conv, norm, act)` so
+  state-dict keys (`….0.weight`) line up with reference checkpoints.
+* `pack_cam_feat` / `unpack_cam_feat` / `upsample` (`blocks.py:6-38`).
+* `ResnetEncoder`, `PoseDecoder`, `MonoDepthDecoder`: the third-party packnet-sfm / monodepth2
+  layers that the reference imports from an un-vendored submodule
+  (`/root/reference/external/layers/__init__.py:2-4`).  Restated from their published
+  architecture (ResNet-18/34/50 with an n-image first conv, input normalised
+  `(x-0.45)/0.225`; squeeze → two 3×3 → 1×1 pose head scaled ×0.01; 5-level
+  reflect-padded ELU decoder).  Parameter names follow torchvision's ResNet so an
+  ImageNet or reference-trained state dict loads unchanged.
+"""
+from collections import OrderedDict
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+# ----------------------------------------------------------------------------- reference blocks
+def _activation(nonlin):
+    if nonlin == 'LRU':
+        return nn.LeakyReLU(0.1, inplace=True)
+    if nonlin == 'ELU':
+        return nn.ELU(inplace=True)
+    return nn.Identity()
+
+
+def conv2d_block(cin, cout, kernel_size=3, stride=1, dilation=1, nonlin='LRU',
+                 padding_mode='reflect', norm=False):
+    pad = ((kernel_size - 1) * dilation) // 2
+    conv = nn.Conv2d(cin, cout, kernel_size, stride=stride, dilation=dilation, padding=pad,
+                     bias=not norm, padding_mode=padding_mode)
+    return nn.Sequential(conv, nn.BatchNorm2d(cout) if norm else nn.Identity(), _activation(nonlin))
+
+
+def conv1d_block(cin, cout, kernel_size=3, stride=1, dilation=1, nonlin='LRU',
+                 padding_mode='reflect', norm=False):
+    pad = ((kernel_size - 1) * dilation) // 2
+    conv = nn.Conv1d(cin, cout, kernel_size, stride=stride, dilation=dilation, padding=pad,
+                     bias=not norm, padding_mode=padding_mode)
+    return nn.Sequential(conv, nn.BatchNorm1d(cout) if norm else nn.Identity(), _activation(nonlin))
+
+
+def pack_cam_feat(x):
+    """[B, N, ...] -> [B*N, ...] (dicts are packed in place)."""
+    if isinstance(x, dict):
+        for k in list(x.keys()):
+            v = x[k]
+            x[k] = v.reshape(v.shape[0] * v.shape[1], *v.shape[2:])
+        return x
+    return x.reshape(x.shape[0] * x.shape[1], *x.shape[2:])
+
+
+def unpack_cam_feat(x, b, n_cam):
+    """[B*N, ...] -> [B, N, ...] (dicts are unpacked in place)."""
+    if isinstance(x, dict):
+        for k in list(x.keys()):
+            v = x[k]
+            x[k] = v.view(b, n_cam, *v.shape[1:])
+        return x
+    return x.view(b, n_cam, *x.shape[1:])
+
+
+def upsample(x):
+    return F.interpolate(x, scale_factor=2, mode='nearest')
+
+
+# ----------------------------------------------------------------------------- ResNet encoder
+class BasicBlock(nn.Module):
+    expansion = 1
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None):
+        super().__init__()
+        self.conv1 = nn.Conv2d(inplanes, planes, 3, stride, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.relu = nn.ReLU(inplace=True)
+        self.conv2 = nn.Conv2d(planes, planes, 3, 1, 1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.downsample = downsample
+
+    def forward(self, x):
+        idt = x if self.downsample is None else self.downsample(x)
+        y = self.relu(self.bn1(self.conv1(x)))
+        y = self.bn2(self.conv2(y))
+        return self.relu(y + idt)
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None):
+        super().__init__()
+        self.conv1 = nn.Conv2d(inplanes, planes, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.conv2 = nn.Conv2d(planes, planes, 3, stride, 1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.conv3 = nn.Conv2d(planes, planes * 4, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(planes * 4)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = downsample
+
+    def forward(self, x):
+        idt = x if self.downsample is None else self.downsample(x)
+        y = self.relu(self.bn1(self.conv1(x)))
+        y = self.relu(self.bn2(self.conv2(y)))
+        y = self.bn3(self.conv3(y))
+        return self.relu(y + idt)
+
+
+_RESNET_SPECS = {18: (BasicBlock, [2, 2, 2, 2]), 34: (BasicBlock, [3, 4, 6, 3]),
+                 50: (Bottleneck, [3, 4, 6, 3])}
+
+
+class ResNetTrunk(nn.Module):
+    """torchvision-named ResNet trunk with a `3*num_input_images`-channel stem."""
+
+    def __init__(self, num_layers, num_input_images=1):
+        super().__init__()
+        block, counts = _RESNET_SPECS[num_layers]
+        self.inplanes = 64
+        self.conv1 = nn.Conv2d(3 * num_input_images, 64, 7, 2, 3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        self.relu = nn.ReLU(inplace=True)
+        self.maxpool = nn.MaxPool2d(3, 2, 1)
+        self.layer1 = self._stage(block, 64, counts[0], 1)
+        self.layer2 = self._stage(block, 128, counts[1], 2)
+        self.layer3 = self._stage(block, 256, counts[2], 2)
+        self.layer4 = self._stage(block, 512, counts[3], 2)
+        self.fc = nn.Linear(512 * block.expansion, 1000)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode='fan_out', nonlinearity='relu')
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+
+    def _stage(self, block, planes, n, stride):
+        down = None
+        if stride != 1 or self.inplanes != planes * block.expansion:
+            down = nn.Sequential(nn.Conv2d(self.inplanes, planes * block.expansion, 1, stride, bias=False),
+                                 nn.BatchNorm2d(planes * block.expansion))
+        blocks = [block(self.inplanes, planes, stride, down)]
+        self.inplanes = planes * block.expansion
+        blocks += [block(self.inplanes, planes) for _ in range(1, n)]
+        return nn.Sequential(*blocks)
+
+
+class ResnetEncoder(nn.Module):
+    """Five-level ResNet feature pyramid (1/2 … 1/32) — packnet/monodepth2 `ResnetEncoder`."""
+
+    def __init__(self, num_layers, pretrained=False, num_input_images=1):
+        super().__init__()
+        if num_layers not in _RESNET_SPECS:
+            raise ValueError(f'{num_layers} is not a valid number of resnet layers')
+        if pretrained:
+            # no network access: ImageNet weights cannot be fetched; callers load their own.
+            import warnings
+            warnings.warn('weights_init=True requested but pretrained ImageNet weights are not '
+                          'available offline; using seeded random init')
+        self.num_ch_enc = np.array([64, 64, 128, 256, 512])
+        if num_layers > 34:
+            self.num_ch_enc[1:] *= 4
+        self.encoder = ResNetTrunk(num_layers, num_input_images)
+
+    def forward(self, image):
+        e = self.encoder
+        x = (image - 0.45) / 0.225
+        f0 = e.relu(e.bn1(e.conv1(x)))
+        f1 = e.layer1(e.maxpool(f0))
+        f2 = e.layer2(f1)
+        f3 = e.layer3(f2)
+        f4 = e.layer4(f3)
+        self.features = [f0, f1, f2, f3, f4]
+        return self.features
+
+
+# ----------------------------------------------------------------------------- decoders
+class PoseDecoder(nn.Module):
+    """squeeze(1×1, ReLU) → 3×3 → 3×3 → 1×1 → spatial mean × 0.01 → (axis-angle, translation)."""
+
+    def __init__(self, num_ch_enc, num_input_features, num_frames_to_predict_for=None, stride=1):
+        super().__init__()
+        self.num_ch_enc = num_ch_enc
+        self.num_input_features = num_input_features
+        if num_frames_to_predict_for is None:
+            num_frames_to_predict_for = num_input_features - 1
+        self.num_frames_to_predict_for = num_frames_to_predict_for
+        self.convs = OrderedDict()
+        self.convs['squeeze'] = nn.Conv2d(int(num_ch_enc[-1]), 256, 1)
+        self.convs[('pose', 0)] = nn.Conv2d(num_input_features * 256, 256, 3, stride, 1)
+        self.convs[('pose', 1)] = nn.Conv2d(256, 256, 3, stride, 1)
+        self.convs[('pose', 2)] = nn.Conv2d(256, 6 * num_frames_to_predict_for, 1)
+        self.relu = nn.ReLU()
+        self.net = nn.ModuleList(list(self.convs.values()))
+
+    def forward(self, input_features):
+        last = [feats[-1] for feats in input_features]
+        x = torch.cat([self.relu(self.convs['squeeze'](f)) for f in last], 1)
+        for i in range(3):
+            x = self.convs[('pose', i)](x)
+            if i < 2:
+                x = self.relu(x)
+        x = 0.01 * x.mean(3).mean(2).view(-1, self.num_frames_to_predict_for, 1, 6)
+        return x[..., :3], x[..., 3:]
+
+
+class _Conv3x3(nn.Module):
+    def __init__(self, cin, cout):
+        super().__init__()
+        self.pad = nn.ReflectionPad2d(1)
+        self.conv = nn.Conv2d(int(cin), int(cout), 3)
+
+    def forward(self, x):
+        return self.conv(self.pad(x))
+
+
+class _ConvBlock(nn.Module):
+    def __init__(self, cin, cout):
+        super().__init__()
+        self.conv = _Conv3x3(cin, cout)
+        self.nonlin = nn.ELU(inplace=True)
+
+    def forward(self, x):
+        return self.nonlin(self.conv(x))
+
+
+class MonoDepthDecoder(nn.Module):
+    """Five-level monodepth2 decoder used by the fsm baseline (`network/mono_depthnet.py:19`)."""
+
+    def __init__(self, num_ch_enc, scales=range(4), num_output_channels=1, use_skips=True):
+        super().__init__()
+        self.num_output_channels = num_output_channels
+        self.use_skips = use_skips
+        self.scales = scales
+        self.num_ch_enc = num_ch_enc
+        self.num_ch_dec = np.array([16, 32, 64, 128, 256])
+        self.convs = OrderedDict()
+        for i in range(4, -1, -1):
+            cin = num_ch_enc[-1] if i == 4 else self.num_ch_dec[i + 1]
+            self.convs[('upconv', i, 0)] = _ConvBlock(cin, self.num_ch_dec[i])
+            cin = self.num_ch_dec[i] + (num_ch_enc[i - 1] if (use_skips and i > 0) else 0)
+            self.convs[('upconv', i, 1)] = _ConvBlock(cin, self.num_ch_dec[i])
+        for s in scales:
+            self.convs[('dispconv', s)] = _Conv3x3(self.num_ch_dec[s], num_output_channels)
+        self.decoder = nn.ModuleList(list(self.convs.values()))
+        self.sigmoid = nn.Sigmoid()
+
+    def forward(self, input_features):
+        out = {}
+        x = input_features[-1]
+        for i in range(4, -1, -1):
+            x = upsample(self.convs[('upconv', i, 0)](x))
+            if self.use_skips and i > 0:
+                x = torch.cat([x, input_features[i - 1]], 1)
+            x = self.convs[('upconv', i, 1)](x)
+            if i in self.scales:
+                out[('disp', i)] = self.sigmoid(self.convs[('dispconv', i)](x))
+        return out
+
+
+def seeded_state_dict(module, seed=0):
+    """Deterministic, machine-independent weights for parity runs (no checkpoint download).
+
+    Conv/linear weights ~ U(-a, a) with a = sqrt(3 / fan_in) (unit-variance pre-activations),
+    biases ~ U(-0.05, 0.05), BatchNorm affine (1, 0) and running stats (0, 1).  Values are drawn
+    from one CPU `torch.Generator` in sorted-key order, so any model with the same parameter
+    names and shapes (this package's or the reference's) receives identical tensors.
+    """
+    gen = torch.Generator().manual_seed(int(seed))
+    sd = module.state_dict()
+    out = OrderedDict()
+    for key in sorted(sd.keys()):
+        t = sd[key]
+        if key.endswith('num_batches_tracked'):
+            out[key] = torch.zeros_like(t)
+        elif key.endswith('running_mean'):
+            out[key] = torch.zeros_like(t)
+        elif key.endswith('running_var'):
+            out[key] = torch.ones_like(t)
+        elif t.dim() == 1 and ('bn' in key or 'downsample.1' in key):
+            out[key] = torch.ones_like(t) if key.endswith('weight') else torch.zeros_like(t)
+        elif t.dim() >= 2:
+            fan_in = int(np.prod(t.shape[1:]))
+            a = (3.0 / fan_in) ** 0.5
+            out[key] = (torch.rand(t.shape, generator=gen, dtype=torch.float64) * 2 - 1).mul_(a).to(t.dtype)
+        else:
+            out[key] = ((torch.rand(t.shape, generator=gen, dtype=torch.float64) * 2 - 1) * 0.05).to(t.dtype)
+    return out

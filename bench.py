@@ -1,0 +1,235 @@
+#!/usr/bin/env python
+"""VFDepth 6-camera training-step benchmark (BASELINE.json metric) on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+One step = process_batch (pose nets x2, depth net, view synthesis, losses) + backward + Adam on
+one synthetic DDAD-shaped batch that is already resident in HBM.  K timed steps between
+barriers + device syncs, max over ranks; rank 0 prints ONE JSON line.  `value` = iterations
+summed over ranks per second (batch per rank as configured; weak scaling).
+
+roofline: the hot-path kernel with the largest device time in the timed steps, timed with HIP
+events around each of its launches on its stream (C-ABI hook), against its algorithmic bytes
+per launch ("Roofline accounting").  cpu_baseline: the CPU oracle (oracle/, a
+restatement of the reference step) timed for a bounded sample on this host's cores (rank 0).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from vfdepth_amd import _lib  # noqa: E402
+from vfdepth_amd import config as C  # noqa: E402
+from vfdepth_amd import synth  # noqa: E402
+from vfdepth_amd.layers import seeded_state_dict  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def make_cfg(config, batch=None):
+    if config == 2:
+        cfg = C.surround_fusion_cfg(batch_size=batch or 1)
+        name = '6-cam DDAD 384x640 fusion, voxel 100x100x20, D=50, fp32'
+    elif config == 3:
+        cfg = C.surround_fusion_cfg(batch_size=batch or 2)
+        name = '6-cam DDAD 384x640 fusion, B=2/GPU, fp32 (bf16 features not yet enabled)'
+    elif config == 4:
+        cfg = C.surround_fusion_cfg(batch_size=batch or 1, height=352, width=640, max_depth=80.0,
+                                    cameras=list(C.NUSC_CAMERAS))
+        name = 'NuScenes 6-cam 352x640 fusion, fp32'
+    elif config == 5:
+        cfg = C.surround_fusion_cfg(batch_size=batch or 4, height=640, width=960, voxel_size=[200, 200, 20],
+                                    voxel_unit_size=[0.5, 0.5, 1.5])
+        name = '6-cam 640x960, voxel 200x200x20 @0.5m, B=4/GPU, fp32'
+    else:
+        raise SystemExit(f'unknown config {config}')
+    return cfg, name
+
+
+def shapes(cfg):
+    m, t = cfg['model'], cfg['training']
+    lvl = m['fusion_level']
+    H, W = t['height'], t['width']
+    X, Y, Z = m['voxel_size']
+    return dict(B=t['batch_size'], N=cfg['data']['num_cams'], C=m['fusion_feat_in_dim'], Cv=m['voxel_pre_dim'][-1],
+                H=H, W=W, h=H // 2 ** (lvl + 1), w=W // 2 ** (lvl + 1), X=X, Y=Y, Z=Z, V=X * Y * Z,
+                D=m['proj_d_bins'], T=len(t['frame_ids']) - 1, F=len(t['frame_ids']))
+
+
+def algorithmic_bytes(kernel, s):
+    """Compulsory HBM bytes of ONE launch at the kernel's own boundary (fp32 = 4 B)."""
+    B, N, C, Cv, p, P = s['B'], s['N'], s['C'], s['Cv'], s['h'] * s['w'], s['H'] * s['W']
+    V, Z, Y, X, D, T, F = s['V'], s['Z'], s['Y'], s['X'], s['D'], s['T'], s['F']
+    pose_out = B * (C + 1) * Z * (Y + 2) * (X + 2)
+    proj_out = B * N * Cv * D * (s['h'] + 2) * (s['w'] + 2)
+    planes = {
+        'mask_downsample': B * N * (P + p),
+        'fuse_depth_fwd': B * N * p * (2 * Cv + 1) + B * V * Cv,
+        'fuse_depth_bwd': 2 * B * V * Cv + B * N * p + B * N * p * 2 * Cv,
+        'fuse_pose_fwd': B * N * C * p + B * N * p + pose_out,
+        'fuse_pose_bwd': pose_out + B * N * p + B * N * C * p,
+        'voxel_project_fwd': B * V * Cv + proj_out,
+        'voxel_project_bwd': proj_out + B * V * Cv,
+        'view_stats': B * N * P * (1 + 3 * (T + 1) + 1),
+        'view_apply': B * N * P * (1 + 3 * (T + 1) + 1) + B * N * P * (4 * T + 4 * F),
+        'view_bwd': B * N * P * (1 + 3 * (T + 1) + 1) + B * N * P * 3 * (T + F) + B * N * P,
+        'photo_fwd': B * N * P * (3 + 6 * T + 4 * F + 1) + B * N * P * 3 + B * N * P // 4,
+        'photo_bwd': B * N * P * (3 + 3 * T + 4 * F + 1) + B * N * P // 4 + B * N * P * 3 * (T + F),
+        'smooth_fwd': B * N * P * 4,
+        'smooth_bwd': B * N * P * 5,
+    }
+    return planes[kernel] * 4
+
+
+def cpu_baseline(cfg, seconds_budget=60.0):
+    """Oracle step (forward + losses + backward + Adam) on the host CPU, batch 1."""
+    from oracle import vfd_oracle as O
+    from vfdepth_amd.network import FusedDepthNet, FusedPoseNet
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    torch.set_num_threads(threads)
+    dn, pn = FusedDepthNet(cfg), FusedPoseNet(cfg)
+    dn.load_state_dict(seeded_state_dict(dn, seed=7))
+    pn.load_state_dict(seeded_state_dict(pn, seed=7))
+    nets = O.nets_from_modules(dn, pn)
+    opt = torch.optim.Adam(list(dn.parameters()) + list(pn.parameters()), 1e-4)
+    inputs = synth.make_batch(cfg, seed=1234, batch_size=1)
+    N, T = cfg['data']['num_cams'], len(cfg['training']['frame_ids']) - 1
+    H, W = cfg['training']['height'], cfg['training']['width']
+    noise = [1e-5 * torch.randn(1, T, H, W) for _ in range(N)]
+    t0 = time.perf_counter()
+    opt.zero_grad(set_to_none=True)
+    _, losses = O.process_batch(nets, inputs, cfg, noise)
+    losses['total_loss'].backward()
+    opt.step()
+    dt = time.perf_counter() - t0
+    return {'value': 1.0 / dt, 'unit': 'iters/s', 'cores': threads, 'kind': 'port',
+            'sample': f'1 full step (fwd+loss+bwd+Adam) of the oracle at the same config, B=1, '
+                      f'{dt:.1f} s on {threads} host threads (torch CPU)'}
+
+
+def load_traffic(config):
+    path = os.path.join(ROOT, 'profiles', f'traffic_config{config}.json')
+    if os.path.isfile(path):
+        with open(path) as fh:
+            return json.load(fh)
+    return {}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=5)
+    ap.add_argument('--config', type=int, default=2)
+    ap.add_argument('--batch', type=int, default=None)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--kernel-table', action='store_true', help='print per-kernel times to stderr')
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        dist.init_process_group('nccl', init_method='env://')
+    torch.cuda.set_device(local)
+    _lib.load()
+
+    from vfdepth_amd.vfdepth import VFDepthAlgo
+    cfg, name = make_cfg(args.config, args.batch)
+    cfg['ddp'].update({'ddp_enable': world > 1, 'world_size': world, 'gpus': list(range(world))})
+    torch.manual_seed(42 + rank)
+    algo = VFDepthAlgo(cfg, local)
+    for mname, m in algo.models.items():
+        inner = m.module if hasattr(m, 'module') else m
+        inner.load_state_dict(seeded_state_dict(inner, seed=7))
+    algo.set_train()
+    batch = synth.make_batch(cfg, seed=1234 + rank, device=f'cuda:{local}')
+
+    def step():
+        algo.optimizer.zero_grad(set_to_none=True)
+        _, losses = algo.process_batch(dict(batch), local)
+        losses['total_loss'].backward()
+        algo.optimizer.step()
+        return losses
+
+    for i in range(args.warmup):
+        step()
+        if rank == 0 and i == 0:
+            print(f'[bench] first step done ({name})', file=sys.stderr, flush=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    _lib.prof_enable('all')
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        losses = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    prof = _lib.prof_read()
+    _lib.prof_enable('off')
+    if world > 1:
+        t = torch.tensor([elapsed], device=f'cuda:{local}')
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+
+    s = shapes(cfg)
+    dom = max(prof, key=lambda k: prof[k][1])
+    n_launch, ms = prof[dom]
+    avg_s = ms / 1e3 / n_launch
+    alg = algorithmic_bytes(dom, s)
+    achieved = alg / avg_s / 1e9
+    traffic = load_traffic(args.config).get(dom)
+    if args.kernel_table:
+        for k, (n, t) in sorted(prof.items(), key=lambda kv: -kv[1][1]):
+            ab = algorithmic_bytes(k, s)
+            print(f'[bench] {k:20s} {n:4d} launches {t / n * 1e3:9.1f} us/launch  '
+                  f'{ab / (t / n / 1e3) / 1e9:8.1f} GB/s alg  ({ab / 1e6:.1f} MB/launch)', file=sys.stderr)
+        print(f'[bench] hot-path kernels {sum(t for _, t in prof.values()) / args.steps:.2f} ms/step of '
+              f'{elapsed / args.steps * 1e3:.2f} ms/step; loss {float(losses["total_loss"]):.5f}', file=sys.stderr)
+    base = None
+    if world == 1 and not args.no_cpu_baseline:
+        base = cpu_baseline(cfg)
+    out = {
+        'metric': '6-cam 384x640 train iters/sec (DDAD-shaped, volumetric fusion)',
+        'value': world * args.steps / elapsed,
+        'unit': 'iters/s',
+        'n_gpus': world,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': elapsed / args.steps * 1e3,
+        'higher_is_better': True,
+        'scaling': 'weak',
+        'vs_baseline': None,
+        'dtype': 'fp32',
+        'data': 'synthetic DDAD-shaped batches (seeded), seeded random-init weights',
+        'config': {'workload': name, 'config_id': args.config, 'batch_per_gpu': s['B'], 'cameras': s['N'],
+                   'image': [s['H'], s['W']], 'voxels': [s['X'], s['Y'], s['Z']], 'depth_bins': s['D'],
+                   'parallelism': f'dp{world}'},
+        'roofline': {'kernel': dom, 'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                     'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic, 'alg_bytes_per_launch': alg,
+                     'avg_launch_us': avg_s * 1e6, 'launches': n_launch},
+        'hot_path_ms_per_step': sum(t for _, t in prof.values()) / args.steps,
+        'cpu_baseline': base,
+    }
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,173 @@
+/*
+ * vfd_capi.h — C ABI of the MI355X (gfx950) hot-path kernels of the VFDepth training step.
+ *
+ * The reference (tronglh241/VFDepth) is pure PyTorch: its hot path is a set of ATen calls
+ * behind Python module APIs.  Each entry point below replaces the ATen call chain named in
+ * its comment (paths relative to /root/reference).  Conventions:
+ *   - all tensors are raw device pointers, fp32, contiguous in the layouts stated, allocated
+ *     and owned by the caller (PyTorch's caching allocator); kernels never allocate;
+ *   - `stream` is a hipStream_t (the caller's current stream); every call is asynchronous;
+ *   - return 0 on success, a negative vfd_status on a bad descriptor or launch failure, with
+ *     a message in vfd_last_error() (thread-local);
+ *   - outputs the kernel accumulates into with atomics are zeroed inside the call;
+ *   - "workspace" buffers are scratch of at least the *_workspace_bytes() size.
+ * Layout symbols: B batch, N cameras, C feature channels, Cv voxel channels, (h, w) fusion-level
+ * feature map, (H, W) image, (X, Y, Z) voxel counts, V = X*Y*Z (x fastest), D depth bins.
+ */
+#ifndef VFD_CAPI_H
+#define VFD_CAPI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum vfd_status { VFD_OK = 0, VFD_EINVAL = -1, VFD_ELAUNCH = -2 };
+
+int vfd_version(void);
+const char* vfd_last_error(void);
+
+/* ------------------------------------------------------------------ volumetric fusion */
+typedef struct vfd_voxel_desc {
+  int32_t B, N;          /* batch, cameras                                               */
+  int32_t C;             /* image feature channels  (model.fusion_feat_in_dim)          */
+  int32_t Cv;            /* voxel feature channels  (model.voxel_pre_dim[-1]), <= 128    */
+  int32_t h, w;          /* feature map at the fusion level (H, W / 2^(fusion_level+1))  */
+  int32_t H, W;          /* full-resolution mask                                         */
+  int32_t X, Y, Z;       /* voxel counts (model.voxel_size)                              */
+  int32_t D;             /* frustum depth bins (model.proj_d_bins)                       */
+  float str[3];          /* model.voxel_str_p                                            */
+  float len[3];          /* voxel_end_p - voxel_str_p                                    */
+  float z_scale;         /* model.voxel_size[0]: divisor of the appended depth feature   */
+  int32_t pad_out;       /* 1: outputs consumed by a 3x3 reflect conv are written padded */
+  const float* axis_x;   /* [X] voxel centres (torch.linspace fp32), device              */
+  const float* axis_y;   /* [Y]                                                          */
+  const float* axis_z;   /* [Z]                                                          */
+  const float* dbins;    /* [D] frustum depths (torch.linspace fp32), device             */
+  const int32_t* group;  /* [N] overlap group of each camera (0: {0,3,4}, 1: {1,2,5})    */
+} vfd_voxel_desc;
+
+/* F.interpolate(mask, [h, w], 'bilinear', align_corners=True)
+ * (network/volumetric_fusionnet.py:129).  mask [B*N, H, W] -> mask_lo [B*N, h, w]. */
+int vfd_mask_downsample(const vfd_voxel_desc* d, const float* mask, float* mask_lo, void* stream);
+
+/* K1 — depth-mode unprojection + overlap/non-overlap 1x1 MLP + LeakyReLU + masks
+ * (volumetric_fusionnet.py:116-158, 166-230).  The 1x1 conv's feature columns are folded
+ * into the per-camera maps by the caller: P[b,n,pix,0:Cv] = W_no[:, :C] f,
+ * P[b,n,pix,Cv:2Cv] = W_o[:, g(n)(C+1) : g(n)(C+1)+C] f   (P: [B, N, h*w, 2*Cv]).
+ * wz [3, Cv] = depth-feature columns (W_no[:,C], W_o[:,C], W_o[:,2C+1]); b_no, b_o [Cv].
+ * K [B,N,4,4] at the fusion scale, Einv [B,N,4,4].  Output vox [B, V, Cv] (channels-last). */
+int vfd_fuse_depth_fwd(const vfd_voxel_desc* d, const float* P, const float* mask_lo,
+                       const float* K, const float* Einv, const float* wz, const float* b_no,
+                       const float* b_o, float* vox, void* stream);
+size_t vfd_fuse_depth_bwd_workspace(const vfd_voxel_desc* d);
+/* d_vox [B,V,Cv], vox (forward output).  dP [B,N,h*w,2*Cv] (zeroed here);
+ * d_wzb [5, Cv] = d wz (3 rows), d b_no, d b_o. */
+int vfd_fuse_depth_bwd(const vfd_voxel_desc* d, const float* d_vox, const float* vox,
+                       const float* mask_lo, const float* K, const float* Einv, float* dP,
+                       float* d_wzb, void* workspace, size_t ws_bytes, void* stream);
+
+/* K2 — pose-mode unprojection, mean over valid cameras (volumetric_fusionnet.py:116-162).
+ * feats [B,N,C,h,w] -> out [B, (C+1)*Z, Y(+2), X(+2)] (channel = c*Z + z; +2 when pad_out:
+ * reflect-padded for the stride-2 3x3 conv of reduce_dim, :339-342). */
+int vfd_fuse_pose_fwd(const vfd_voxel_desc* d, const float* feats, const float* mask_lo,
+                      const float* K, const float* Einv, float* out, void* stream);
+/* d_out in the forward's output layout -> d_feats [B,N,C,h,w] (zeroed here). */
+int vfd_fuse_pose_bwd(const vfd_voxel_desc* d, const float* d_out, const float* mask_lo,
+                      const float* K, const float* Einv, float* d_feats, void* stream);
+
+/* K3 — voxel -> camera-frustum trilinear resampling (volumetric_fusionnet.py:232-262).
+ * vox [B,V,Cv], invK, E [B,N,4,4] (fusion scale) -> out [B*N, Cv*D, h(+2), w(+2)]
+ * (channel = c*D + d; padded for the reflect 3x3 conv of reduce_dim when pad_out). */
+int vfd_voxel_project_fwd(const vfd_voxel_desc* d, const float* vox, const float* invK,
+                          const float* E, float* out, void* stream);
+/* d_out (forward layout) -> d_vox [B,V,Cv] (zeroed here). */
+int vfd_voxel_project_bwd(const vfd_voxel_desc* d, const float* d_out, const float* invK,
+                          const float* E, float* d_vox, void* stream);
+
+/* ------------------------------------------------------------------ view synthesis (K4) */
+typedef struct vfd_view_desc {
+  int32_t B, N, H, W;
+  int32_t n_warp;        /* warps per target camera                                      */
+  int32_t n_temporal;    /* T = len(frame_ids) - 1 temporal warps (warps 0..T-1)         */
+  int32_t n_overlap;     /* overlap slots: len(frame_ids) when spatial terms are on, else 0 */
+  int32_t intensity_align;
+  int32_t cam_begin;     /* target cameras cam_begin .. cam_begin+cam_count-1 are rendered */
+  int32_t cam_count;     /* (per-target arrays are [B, cam_count, ...])                  */
+  const float* color[4]; /* per frame slot (frame_ids order) [B, N, 3, H, W]             */
+  const int32_t* warp_tab; /* [N, n_warp, 3] device: frame slot, source camera, overlap slot (-1: temporal) */
+} vfd_view_desc;
+
+/* Projection.forward + get_virtual_image + get_norm_image_single + overlap accumulation
+ * (models/geometry/geometry_util.py:52-82, view_rendering.py:30-82, 118-198) for every target
+ * camera and warp in three fused passes.  With Nt = cam_count target cameras:
+ * depth [B,Nt,H,W], invK [B,Nt,4,4] (scale 0), M [B,Nt,n_warp,3,4] = (K_src @ T)[:3],
+ * mask [B,N,H,W] (all cameras).
+ * Outputs: color [B,Nt,T,3,H,W], cmask [B,Nt,T,H,W], ovl [B,Nt,F,3,H,W], omask [B,Nt,F,H,W];
+ * coef [B,Nt,n_warp,4] (w_mean, w_std, s_mean, s_std; w_std < 0: warp left unnormalised). */
+size_t vfd_view_workspace_bytes(const vfd_view_desc* d);
+int vfd_view_fwd(const vfd_view_desc* d, const float* depth, const float* invK, const float* M,
+                 const float* mask, float* color, float* cmask, float* ovl, float* omask,
+                 float* coef, void* workspace, size_t ws_bytes, void* stream);
+/* g_color [B,Nt,T,3,H,W], g_ovl [B,Nt,F,3,H,W] (nullable) -> d_depth [B,Nt,H,W], d_M [B,Nt,n_warp,3,4]. */
+int vfd_view_bwd(const vfd_view_desc* d, const float* depth, const float* invK, const float* M,
+                 const float* mask, const float* coef, const float* g_color, const float* g_ovl,
+                 float* d_depth, float* d_M, void* workspace, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------ photometric losses (K5) */
+typedef struct vfd_photo_desc {
+  int32_t B, N, H, W;
+  int32_t T;             /* temporal frames (frame_ids[1:])                              */
+  int32_t F;             /* overlap slots (0 = SingleCamLoss)                            */
+  int32_t cam_begin;     /* target cameras cam_begin .. cam_begin+cam_count-1            */
+  int32_t cam_count;
+  uint64_t seed;         /* identity-noise RNG seed, used when `noise` is NULL            */
+  float noise_scale;     /* 1e-5 (single_cam_loss.py:8)                                  */
+  const float* ident[4]; /* identity sources per temporal frame [B, N, 3, H, W]          */
+} vfd_photo_desc;
+
+/* compute_photometric_loss / compute_ssim_loss / auto-mask / masked means for every camera
+ * (models/losses/loss_util.py:6-78, single_cam_loss.py:17-55, multi_cam_loss.py:16-59).
+ * With Nt = cam_count: target [B,N,3,H,W] and ref_mask [B,N,H,W] (all cameras);
+ * color [B,Nt,T,3,H,W]; ovl [B,Nt,F,3,H,W]; omask [B,Nt,F,H,W]; noise [Nt,B,T,H,W] or NULL.
+ * Outputs: reproj [B,Nt,H,W] (automask * min reprojection), automask [B,Nt,H,W],
+ * spatio_mask [B,Nt,H,W], sel [B,Nt,H,W] uint8 (argmin bits, saved for backward),
+ * sums [Nt, 6] double (S_reproj, M_reproj, S_spatio, M_spatio, S_st, M_st),
+ * losses [Nt, 3] float (reproj, spatio, spatio-temporal masked means). */
+size_t vfd_photo_workspace_bytes(const vfd_photo_desc* d);
+int vfd_photo_fwd(const vfd_photo_desc* d, const float* target, const float* color,
+                  const float* ovl, const float* ref_mask, const float* omask, const float* noise,
+                  float* reproj, float* automask, float* spatio_mask, uint8_t* sel, double* sums,
+                  float* losses, void* workspace, size_t ws_bytes, void* stream);
+/* gcoef [Nt, 3] = upstream grad / (mask sum + 1e-8) per term -> d_color, d_ovl (overwritten). */
+int vfd_photo_bwd(const vfd_photo_desc* d, const float* target, const float* color,
+                  const float* ovl, const float* ref_mask, const float* omask, const uint8_t* sel,
+                  const float* gcoef, float* d_color, float* d_ovl, void* stream);
+
+/* Edge-aware smoothness of disp / mean(disp) (loss_util.py:28-40, single_cam_loss.py:57-65).
+ * disp [B,N,H,W], color [B,N,3,H,W] -> sums [B*N, 3] double (sum disp, Sx, Sy), loss [N]. */
+size_t vfd_smooth_workspace_bytes(int B, int N, int H, int W);
+int vfd_smooth_fwd(int B, int N, int H, int W, const float* disp, const float* color,
+                   double* sums, float* loss, void* workspace, size_t ws_bytes, void* stream);
+/* g [N] upstream grads -> d_disp [B,N,H,W] (overwritten). */
+int vfd_smooth_bwd(int B, int N, int H, int W, const float* disp, const float* color,
+                   const double* sums, const float* g, float* d_disp, void* stream);
+
+/* ------------------------------------------------------------------ measurement hooks */
+/* Record HIP events around every launch of kernel `kernel_id` (see vfd_kernel_name; -1 = all,
+ * -2 = off) on the launching stream.  vfd_prof_read: launches and summed ms of everything
+ * recorded; vfd_prof_read_kernels: the same per kernel id into arrays of `count` entries.
+ * Both reset the record. */
+#define VFD_PROF_ALL (-1)
+#define VFD_KERNEL_COUNT 14
+const char* vfd_kernel_name(int kernel_id);
+int vfd_prof_enable(int kernel_id);
+int vfd_prof_read(int* launches, double* total_ms);
+int vfd_prof_read_kernels(int count, int* launches, double* total_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VFD_CAPI_H */

@@ -565,3 +565,21 @@ def process_batch(nets, inputs, cfg, noise):
     losses = {k: sum(v) / len(v) for k, v in logs.items()}
     losses['total_loss'] = total / N
     return outputs, losses
+
+
+class _Nets:
+    pass
+
+
+def nets_from_modules(depth_net, pose_net):
+    """Adapter: dense layers of depth/pose networks that use the reference's attribute names
+    (FusedDepthNet.encoder/conv1x1/fusion_net/decoder, FusedPoseNet.…/pose_decoder)."""
+    n = _Nets()
+    n.depth_encoder, n.depth_conv1x1 = depth_net.encoder, depth_net.conv1x1
+    n.depth_reduce_dim, n.depth_decoder = depth_net.fusion_net.reduce_dim, depth_net.decoder
+    n.pose_encoder, n.pose_conv1x1 = pose_net.encoder, pose_net.conv1x1
+    n.pose_reduce_dim, n.pose_decoder = pose_net.fusion_net.reduce_dim, pose_net.pose_decoder
+    fn = depth_net.fusion_net
+    n.w_no, n.b_no = fn.conv_non_overlap[0].weight, fn.conv_non_overlap[0].bias
+    n.w_o, n.b_o = fn.conv_overlap[0].weight, fn.conv_overlap[0].bias
+    return n

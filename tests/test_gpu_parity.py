@@ -1,0 +1,294 @@
+"""GPU parity: the HIP hot path against the reference's golden vectors (and the CPU oracle).
+
+Every test calls the product through its C ABI (vfdepth_amd.kernels -> libvfd_hip.so).
+Tolerance (BASELINE.json north_star): fp32 per-pixel 1e-4.  Values are compared with
+|a - b| <= 1e-4 + 1e-4 |b|; gradients with max |a - b| <= 2e-4 x max |b| (they are sums of
+many atomically accumulated fp32 terms in a different order than the reference's).
+Discontinuities (nearest-mask lookups, OOB tests, argmin ties) are evaluated with the
+reference's operation order, so no mismatch allowance is made for them.
+"""
+import numpy as np
+import pytest
+import torch
+
+import common as G
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device('cuda:0')
+ATOL = RTOL = 1e-4
+
+
+def close(a, b, what, atol=ATOL, rtol=RTOL):
+    a = a.detach().float().cpu().numpy() if torch.is_tensor(a) else np.asarray(a)
+    b = b.detach().float().cpu().numpy() if torch.is_tensor(b) else np.asarray(b)
+    assert a.shape == b.shape, f'{what}: shape {a.shape} vs {b.shape}'
+    err = np.abs(a.astype(np.float64) - b)
+    bad = err > atol + rtol * np.abs(b)
+    assert not bad.any(), f'{what}: {int(bad.sum())}/{bad.size} off, max err {err.max():.3g}'
+
+
+def gclose(a, b, what, rel=2e-4):
+    a = a.detach().double().cpu().numpy()
+    b = np.asarray(b.detach().cpu().numpy() if torch.is_tensor(b) else b, np.float64)
+    assert a.shape == b.shape, f'{what}: shape {a.shape} vs {b.shape}'
+    scale = max(np.abs(b).max(), 1e-12)
+    err = np.abs(a - b).max() / scale
+    assert err < rel, f'{what}: max rel err {err:.3g} (scale {scale:.3g})'
+
+
+def to_dev(d):
+    return {k: (v.to(DEV) if torch.is_tensor(v) else v) for k, v in d.items()}
+
+
+@pytest.fixture(scope='module', autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip('no HIP device')
+    from vfdepth_amd import _lib
+    _lib.load()
+
+
+# ------------------------------------------------------------------------------------ fusion
+def _fusion_net(model):
+    from vfdepth_amd.fusion import VFNet
+    cfg, d, seeds = G.fusion_case()
+    fx = golden('fusion_small.npz')
+    net = VFNet(cfg, d['feats'].shape[2], 32, model=model).to(DEV)
+    if model == 'depth':
+        with torch.no_grad():
+            net.conv_non_overlap[0].weight.copy_(torch.tensor(fx['w_no']))
+            net.conv_non_overlap[0].bias.copy_(torch.tensor(fx['b_no']))
+            net.conv_overlap[0].weight.copy_(torch.tensor(fx['w_o']))
+            net.conv_overlap[0].bias.copy_(torch.tensor(fx['b_o']))
+    inputs = {('K', 3): d['K'].to(DEV), ('inv_K', 3): d['invK'].to(DEV), 'extrinsics': d['E'].to(DEV),
+              'extrinsics_inv': d['Einv'].to(DEV), 'mask': d['mask'].to(DEV)}
+    return cfg, d, seeds, fx, net, inputs
+
+
+def test_mask_downsample():
+    from oracle import vfd_oracle as O
+    from vfdepth_amd import kernels as KN
+    cfg, d, _ = G.fusion_case()
+    space = KN.VoxelSpace(cfg, DEV)
+    lo = KN.mask_lowres(space, d['mask'].to(DEV))
+    ref = O.resize_bilinear_ac(d['mask'].flatten(0, 1), space.h, space.w).view_as(lo)
+    close(lo, ref, 'mask 1/8', atol=1e-6, rtol=1e-6)
+
+
+def test_fuse_depth_forward_backward():
+    cfg, d, seeds, fx, net, inputs = _fusion_net('depth')
+    feats = d['feats'].to(DEV).requires_grad_(True)
+    vox = net.backproject_depth(inputs, feats)                               # [B, V, Cv]
+    close(vox.permute(0, 2, 1), fx['vox'], 'K1 voxel features')
+    g = G.seeded_randn(fx['vox'].shape, seeds['g_vox']).to(DEV)              # [B, Cv, V]
+    (vox.permute(0, 2, 1) * g).sum().backward()
+    gclose(feats.grad, fx['d_feats_depth'], 'K1 d feats')
+    gclose(net.conv_non_overlap[0].weight.grad, fx['d_w_no'], 'K1 d W_no')
+    gclose(net.conv_non_overlap[0].bias.grad, fx['d_b_no'], 'K1 d b_no')
+    gclose(net.conv_overlap[0].weight.grad, fx['d_w_o'], 'K1 d W_o')
+    gclose(net.conv_overlap[0].bias.grad, fx['d_b_o'], 'K1 d b_o')
+
+
+def test_fuse_pose_forward_backward():
+    from vfdepth_amd import kernels as KN
+    cfg, d, seeds, fx, net, inputs = _fusion_net('pose')
+    space = net.space(DEV)
+    feats = d['feats'].to(DEV).requires_grad_(True)
+    out = KN.FusePose.apply(space, feats, KN.mask_lowres(space, inputs['mask']), inputs[('K', 3)],
+                            inputs['extrinsics_inv'])
+    B, C1 = out.shape[0], feats.shape[2] + 1
+    inner = out[:, :, 1:-1, 1:-1].reshape(B, C1, space.Z, space.Y, space.X).reshape(B, C1, -1)
+    close(inner, fx['vpose'], 'K2 pose voxels')
+    # reflect halo holds the mirrored interior (what the stride-2 reflect conv reads)
+    close(out[:, :, 0, 1:-1], out[:, :, 2, 1:-1], 'K2 top halo', atol=0, rtol=0)
+    close(out[:, :, 1:-1, -1], out[:, :, 1:-1, -3], 'K2 right halo', atol=0, rtol=0)
+    g = G.seeded_randn(fx['vpose'].shape, seeds['g_pose']).to(DEV)
+    (inner * g).sum().backward()
+    gclose(feats.grad, fx['d_feats_pose'], 'K2 d feats')
+
+
+def test_voxel_project_forward_backward():
+    from vfdepth_amd import kernels as KN
+    cfg, d, seeds, fx, net, inputs = _fusion_net('depth')
+    space = net.space(DEV)
+    vleaf = G.seeded_randn(fx['vox'].shape, seeds['vleaf']).to(DEV)       # [B, Cv, V]
+    v = vleaf.permute(0, 2, 1).contiguous().requires_grad_(True)
+    out = KN.VoxelProject.apply(space, v, inputs[('inv_K', 3)], inputs['extrinsics'])
+    B, N = inputs['extrinsics'].shape[:2]
+    inner = out[:, :, 1:-1, 1:-1].reshape(B, N, *out.shape[1:2], space.h, space.w)
+    close(inner, fx['proj'], 'K3 frustum features')
+    g = G.seeded_randn(fx['proj'].shape, seeds['g_proj']).to(DEV)
+    (inner * g).sum().backward()
+    gclose(v.grad.permute(0, 2, 1), fx['d_vleaf'], 'K3 d voxel')
+
+
+def test_voxel_project_padding_matches_reflect_conv():
+    """Writing the reflect-padded layout then conv(padding=0) == reference conv(padding_mode='reflect')."""
+    from vfdepth_amd import kernels as KN
+    cfg, d, seeds, fx, net, inputs = _fusion_net('depth')
+    space = net.space(DEV)
+    v = G.seeded_randn(fx['vox'].shape, seeds['vleaf']).to(DEV).permute(0, 2, 1).contiguous()
+    out = KN.VoxelProject.apply(space, v, inputs[('inv_K', 3)], inputs['extrinsics'])
+    ref = torch.nn.functional.pad(out[:, :, 1:-1, 1:-1], (1, 1, 1, 1), mode='reflect')
+    close(out, ref, 'reflect halo', atol=0, rtol=0)
+
+
+# ------------------------------------------------------------------------------------ view synthesis
+@pytest.mark.parametrize('name,skip', [('view_small.npz', False), ('view_skip.npz', True)])
+def test_view_synthesis(name, skip):
+    from vfdepth_amd.geometry import Pose, ViewRendering
+    fx = golden(name)
+    cfg, batch, depth, poses = G.view_case(skip)
+    batch = to_dev(batch)
+    vr, pose = ViewRendering(cfg, 0), Pose(cfg)
+    d = depth.to(DEV).requires_grad_(True)
+    outputs = {('cam', c): {} for c in range(6)}
+    Ts = {}
+    for c in range(6):
+        for f in (-1, 1):
+            Ts[(c, f)] = poses[(c, f)].to(DEV).requires_grad_(True)
+            outputs[('cam', c)][('cam_T_cam', 0, f)] = Ts[(c, f)]
+        outputs[('cam', c)][('depth', 0)] = d[:, c]
+    rel = {c: pose.compute_relative_cam_poses(batch, outputs, c) for c in range(6)}
+    vr.render_all(batch, outputs, rel, {0: d[:, :, 0]})
+    loss = 0
+    for c in range(6):
+        out = outputs[('cam', c)]
+        for i, k in enumerate(G.VIEW_IMG_KEYS):
+            close(out[k], fx[f'{G.key_name(k)}_c{c}'], f'{k} cam {c}')
+            loss = loss + (out[k] * G.seeded_randn(out[k].shape, 500 + 10 * c + i).to(DEV)).sum()
+        for k in G.VIEW_MSK_KEYS:
+            close(out[k], fx[f'{G.key_name(k)}_c{c}'], f'{k} cam {c}', atol=0, rtol=0)
+    loss.backward()
+    for c in range(6):
+        gclose(d.grad[:, c], fx[f'd_depth_c{c}'], f'd depth cam {c}')
+        for f in (-1, 1):
+            gclose(Ts[(c, f)].grad, fx[f'd_T_{f}_c{c}'], f'd T{f} cam {c}')
+
+
+def test_view_synthesis_per_camera_api():
+    """ViewRendering.forward(inputs, outputs, cam, rel) (reference per-camera API) == batched path."""
+    from vfdepth_amd.geometry import Pose, ViewRendering
+    fx = golden('view_small.npz')
+    cfg, batch, depth, poses = G.view_case(False)
+    batch = to_dev(batch)
+    vr, pose = ViewRendering(cfg, 0), Pose(cfg)
+    for c in (0, 3):
+        out = {('depth', 0): depth[:, c].to(DEV)}
+        for f in (-1, 1):
+            out[('cam_T_cam', 0, f)] = poses[(c, f)].to(DEV)
+        outputs = {('cam', c): out}
+        vr(batch, outputs, c, pose.compute_relative_cam_poses(batch, outputs, c))
+        for k in G.VIEW_IMG_KEYS:
+            close(out[k], fx[f'{G.key_name(k)}_c{c}'], f'{k} cam {c} (per-camera API)')
+
+
+# ------------------------------------------------------------------------------------ losses
+def _loss_inputs():
+    cfg, batch, planes = G.loss_case()
+    batch = to_dev(batch)
+    return cfg, batch, planes
+
+
+def test_losses_per_camera_api():
+    from vfdepth_amd.losses import MultiCamLoss
+    fx = golden('loss_small.npz')
+    cfg, batch, planes = _loss_inputs()
+    batch['extrinsics_inv'] = torch.inverse(batch['extrinsics'])
+    loss_fn = MultiCamLoss(cfg, 0)
+    for c in range(6):
+        out, leaves = {}, {}
+        for k in G.VIEW_IMG_KEYS:
+            leaves[k] = planes[(c,) + k].to(DEV).requires_grad_(True)
+            out[k] = leaves[k]
+        for f in (0, -1, 1):
+            out[('overlap_mask', f, 0)] = planes[(c, 'overlap_mask', f, 0)].to(DEV)
+        disp = planes[(c, 'disp', 0)].to(DEV).requires_grad_(True)
+        out[('disp', 0)] = disp
+        out[('depth', 0)] = 1.0 / disp.detach()
+        noise = torch.tensor(fx[f'noise_c{c}']).to(DEV).unsqueeze(0)
+        cl, ld = loss_fn(batch, {('cam', c): out}, c, noise=noise)
+        close(cl, fx[f'cam_loss_c{c}'], f'cam loss {c}')
+        for k in ('reproj_loss', 'spatio_loss', 'spatio_tempo_loss', 'smooth'):
+            close(ld[k], fx[f'{k}_c{c}'], f'{k} cam {c}')
+        close(out[('reproj_loss', 0)], fx[f'reproj_plane_c{c}'], 'reproj plane')
+        close(out[('reproj_mask', 0)], fx[f'reproj_mask_c{c}'], 'reproj mask', atol=0, rtol=0)
+        close(out[('overlap_mask', 0, 0)], fx[f'spatio_mask_c{c}'], 'spatio mask', atol=0, rtol=0)
+        cl.backward()
+        for k in G.VIEW_IMG_KEYS:
+            gclose(leaves[k].grad, fx[f'd_{G.key_name(k)}_c{c}'], f'd {k} cam {c}')
+        gclose(disp.grad, fx[f'd_disp_c{c}'], f'd disp cam {c}')
+
+
+def test_losses_all_cameras():
+    """Batched forward_all over the six cameras == per-camera reference values."""
+    from vfdepth_amd.losses import MultiCamLoss
+    fx = golden('loss_small.npz')
+    cfg, batch, planes = _loss_inputs()
+    loss_fn = MultiCamLoss(cfg, 0)
+    T, F = 2, 3
+    color = torch.stack([torch.stack([planes[(c,) + k] for k in G.VIEW_IMG_KEYS[:T]], 1) for c in range(6)], 1)
+    ovl = torch.stack([torch.stack([planes[(c,) + k] for k in G.VIEW_IMG_KEYS[T:]], 1) for c in range(6)], 1)
+    omask = torch.stack([torch.stack([planes[(c, 'overlap_mask', f, 0)][:, 0] for f in (0, -1, 1)], 1)
+                         for c in range(6)], 1)
+    disp = torch.stack([planes[(c, 'disp', 0)][:, 0] for c in range(6)], 1)
+    color, ovl, disp = (t.to(DEV).requires_grad_(True) for t in (color, ovl, disp))
+    omask = omask.to(DEV)
+    noise = torch.stack([torch.tensor(fx[f'noise_c{c}']) for c in range(6)]).to(DEV)
+    outputs = {('cam', c): {} for c in range(6)}
+    total, logs = loss_fn.forward_all(batch, outputs, {0: (color, None, ovl, omask)}, {0: disp},
+                                      {0: 1.0 / disp.detach()}, noise=noise)
+    ref_total = np.mean([float(fx[f'cam_loss_c{c}']) for c in range(6)])
+    close(total, np.float32(ref_total), 'total loss')
+    for k in ('reproj_loss', 'spatio_loss', 'spatio_tempo_loss', 'smooth'):
+        close(logs[k], np.float32(np.mean([float(fx[f'{k}_c{c}']) for c in range(6)])), k)
+    total.backward()
+    for c in range(6):
+        for i, k in enumerate(G.VIEW_IMG_KEYS):
+            grad = color.grad[:, c, i] if i < T else ovl.grad[:, c, i - T]
+            gclose(grad * 6, fx[f'd_{G.key_name(k)}_c{c}'], f'd {k} cam {c} (batched)')
+        gclose(disp.grad[:, c].unsqueeze(1) * 6, fx[f'd_disp_c{c}'], f'd disp cam {c} (batched)')
+
+
+# ------------------------------------------------------------------------------------ full step
+def _step(cfg_fn, fixture, seed_inputs):
+    from vfdepth_amd import synth
+    from vfdepth_amd.layers import seeded_state_dict
+    from vfdepth_amd.vfdepth import VFDepthAlgo
+    fx = golden(fixture)
+    cfg = cfg_fn()
+    algo = VFDepthAlgo(cfg, 0)
+    for m in algo.models.values():
+        m.load_state_dict(seeded_state_dict(m, seed=G.STEP_SEED))
+    algo.set_train()
+    inputs = synth.make_batch(cfg, seed=seed_inputs, with_depth=True)
+    np.testing.assert_array_equal(G.checksum(inputs[('color', 0, 0)]), fx['cs_color'])
+    N = cfg['data']['num_cams']
+    noise = torch.stack([torch.tensor(fx[f'noise_c{c}']) for c in range(N)]).to(DEV)
+    outputs, losses = algo.process_batch(inputs, 0, noise=noise)
+    losses['total_loss'].backward()
+    return cfg, fx, algo, outputs, losses
+
+
+@pytest.mark.parametrize('which', ['fusion', 'mono'])
+def test_full_step_against_reference(which):
+    cfg_fn, fixture, seed = (G.step_cfg, 'step_small.npz', 5) if which == 'fusion' else (G.mono_cfg, 'mono_small.npz', 6)
+    cfg, fx, algo, outputs, losses = _step(cfg_fn, fixture, seed)
+    for k in [k for k in fx.files if k.startswith('loss_')]:
+        close(losses[k[5:]], fx[k], k)
+    for c in range(cfg['data']['num_cams']):
+        close(outputs[('cam', c)][('depth', 0)], fx[f'depth_c{c}'], f'depth cam {c}')
+        for f in cfg['training']['frame_ids'][1:]:
+            close(outputs[('cam', c)][('cam_T_cam', 0, f)], fx[f'cam_T_cam_{f}_c{c}'], f'T{f} cam {c}', atol=1e-5)
+    for key in [k for k in fx.files if k.startswith('c0_')]:
+        parts = key[3:].split('_')
+        name = '_'.join(p for p in parts if not p.lstrip('-').isdigit())
+        nums = tuple(int(p) for p in parts if p.lstrip('-').isdigit())
+        close(outputs[('cam', 0)][(name,) + nums], fx[key], key)
+    named = {}
+    for mname, m in algo.models.items():
+        for pname, p in m.named_parameters():
+            named[f'{mname}.{pname}'] = p
+    for key in [k for k in fx.files if k.startswith('grad__')]:
+        gclose(named[key[6:]].grad, fx[key], key, rel=1e-3)

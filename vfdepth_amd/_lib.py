@@ -1,0 +1,127 @@
+"""ctypes binding of `libvfd_hip.so` (C ABI declared in include/vfd_capi.h).
+
+The library is loaded after `torch` so that it binds to the HIP runtime PyTorch-ROCm already
+loaded (same SONAME, one device context).  There is no fallback: if the library is missing or
+fails to load, every hot-path op raises.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL: shares torch's libamdhip64)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get('VFD_LIB', os.path.join(_HERE, 'libvfd_hip.so'))
+
+c_int, c_float, c_double, c_size_t, c_void_p = ctypes.c_int32, ctypes.c_float, ctypes.c_double, ctypes.c_size_t, ctypes.c_void_p
+c_fp = ctypes.c_void_p      # device pointers are passed as integers
+
+
+class VoxelDesc(ctypes.Structure):
+    _fields_ = [('B', c_int), ('N', c_int), ('C', c_int), ('Cv', c_int), ('h', c_int), ('w', c_int),
+                ('H', c_int), ('W', c_int), ('X', c_int), ('Y', c_int), ('Z', c_int), ('D', c_int),
+                ('str', c_float * 3), ('len', c_float * 3), ('z_scale', c_float), ('pad_out', c_int),
+                ('axis_x', c_fp), ('axis_y', c_fp), ('axis_z', c_fp), ('dbins', c_fp), ('group', c_fp)]
+
+
+class ViewDesc(ctypes.Structure):
+    _fields_ = [('B', c_int), ('N', c_int), ('H', c_int), ('W', c_int), ('n_warp', c_int),
+                ('n_temporal', c_int), ('n_overlap', c_int), ('intensity_align', c_int),
+                ('cam_begin', c_int), ('cam_count', c_int), ('color', c_fp * 4), ('warp_tab', c_fp)]
+
+
+class PhotoDesc(ctypes.Structure):
+    _fields_ = [('B', c_int), ('N', c_int), ('H', c_int), ('W', c_int), ('T', c_int), ('F', c_int),
+                ('cam_begin', c_int), ('cam_count', c_int), ('seed', ctypes.c_uint64),
+                ('noise_scale', c_float), ('ident', c_fp * 4)]
+
+
+_SIGS = {
+    'vfd_version': (c_int, []),
+    'vfd_last_error': (ctypes.c_char_p, []),
+    'vfd_kernel_name': (ctypes.c_char_p, [c_int]),
+    'vfd_prof_enable': (c_int, [c_int]),
+    'vfd_prof_read': (c_int, [ctypes.POINTER(c_int), ctypes.POINTER(c_double)]),
+    'vfd_prof_read_kernels': (c_int, [c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_double)]),
+    'vfd_mask_downsample': (c_int, [ctypes.POINTER(VoxelDesc), c_fp, c_fp, c_void_p]),
+    'vfd_fuse_depth_fwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 8 + [c_void_p]),
+    'vfd_fuse_depth_bwd_workspace': (c_size_t, [ctypes.POINTER(VoxelDesc)]),
+    'vfd_fuse_depth_bwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 8 + [c_size_t, c_void_p]),
+    'vfd_fuse_pose_fwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 5 + [c_void_p]),
+    'vfd_fuse_pose_bwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 5 + [c_void_p]),
+    'vfd_voxel_project_fwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 4 + [c_void_p]),
+    'vfd_voxel_project_bwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 4 + [c_void_p]),
+    'vfd_view_workspace_bytes': (c_size_t, [ctypes.POINTER(ViewDesc)]),
+    'vfd_view_fwd': (c_int, [ctypes.POINTER(ViewDesc)] + [c_fp] * 10 + [c_size_t, c_void_p]),
+    'vfd_view_bwd': (c_int, [ctypes.POINTER(ViewDesc)] + [c_fp] * 10 + [c_size_t, c_void_p]),
+    'vfd_photo_workspace_bytes': (c_size_t, [ctypes.POINTER(PhotoDesc)]),
+    'vfd_photo_fwd': (c_int, [ctypes.POINTER(PhotoDesc)] + [c_fp] * 13 + [c_size_t, c_void_p]),
+    'vfd_photo_bwd': (c_int, [ctypes.POINTER(PhotoDesc)] + [c_fp] * 9 + [c_void_p]),
+    'vfd_smooth_workspace_bytes': (c_size_t, [c_int] * 4),
+    'vfd_smooth_fwd': (c_int, [c_int] * 4 + [c_fp] * 5 + [c_size_t, c_void_p]),
+    'vfd_smooth_bwd': (c_int, [c_int] * 4 + [c_fp] * 5 + [c_void_p]),
+}
+
+EXPORTED = sorted(_SIGS)
+_lib = None
+_load_error = None
+
+
+def load():
+    """Load (once) and return the library; raise with the reason if unavailable."""
+    global _lib, _load_error
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f'{LIB_PATH} not built: run `python -m vfdepth_amd.build` (hipcc, gfx950)')
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(status, what):
+    if status != 0:
+        msg = load().vfd_last_error().decode(errors='replace')
+        raise RuntimeError(f'{what} failed ({status}): {msg}')
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+KERNEL_IDS = {
+    'mask_downsample': 0, 'fuse_depth_fwd': 1, 'fuse_depth_bwd': 2, 'fuse_pose_fwd': 3, 'fuse_pose_bwd': 4,
+    'voxel_project_fwd': 5, 'voxel_project_bwd': 6, 'view_stats': 7, 'view_apply': 8, 'view_bwd': 9,
+    'photo_fwd': 10, 'photo_bwd': 11, 'smooth_fwd': 12, 'smooth_bwd': 13,
+}
+
+
+def prof_enable(kernel='all'):
+    """Time launches of `kernel` (name, id, 'all' or 'off') with HIP events on their stream."""
+    if kernel == 'all':
+        kid = -1
+    elif kernel == 'off':
+        kid = -2
+    else:
+        kid = KERNEL_IDS[kernel] if isinstance(kernel, str) else int(kernel)
+    load().vfd_prof_enable(kid)
+
+
+def prof_read():
+    """{kernel name: (launches, total ms)} of everything recorded since prof_enable; resets."""
+    n = len(KERNEL_IDS)
+    cnt = (c_int * n)()
+    ms = (c_double * n)()
+    load().vfd_prof_read_kernels(n, cnt, ms)
+    names = {v: k for k, v in KERNEL_IDS.items()}
+    return {names[i]: (cnt[i], ms[i]) for i in range(n) if cnt[i]}

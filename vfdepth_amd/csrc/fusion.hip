@@ -1,0 +1,784 @@
+// Volumetric fusion kernels for gfx950 (reference: network/volumetric_fusionnet.py).
+//
+//  mask_downsample    F.interpolate(mask, [h,w], bilinear, align_corners=True)          (:129)
+//  K1 fuse_depth      unproject -> bilinear gather -> overlap/non-overlap 1x1 MLP -> LReLU
+//                     -> count masks, voxel-major output [B,V,Cv]                   (:116-230)
+//  K2 fuse_pose       unproject -> bilinear gather -> mean over valid cameras, written in
+//                     the (reflect-padded) NCHW layout the stride-2 conv reads        (:116-162)
+//  K3 voxel_project   frustum points -> trilinear gather of [B,V,Cv] -> [B*N,Cv*D,h,w]
+//                     (reflect-padded for the 3x3 conv)                             (:232-262)
+//
+// Geometry (voxel<->camera) is recomputed in every kernel from K / E (a few dozen FLOPs per
+// point) instead of being stored: it costs no HBM traffic and keeps forward and backward
+// decisions bit-identical.  All arithmetic follows the reference's operation order with
+// -ffp-contract=off so that validity tests at the boundaries agree with the CPU reference.
+#include "vfd_common.h"
+
+namespace vfd {
+
+// ------------------------------------------------------------------------------ geometry
+struct VoxCam {
+  float ix, iy;   // unnormalised sample position in the h x w map (ATen align_corners=True)
+  float z;        // camera-frame depth of the voxel centre
+  bool valid;     // in front, inside the image, not self-occluded
+};
+
+// volumetric_fusionnet.py:132-140, 166-195
+__device__ __forceinline__ VoxCam voxel_to_camera(const float* __restrict__ Kc, const float* __restrict__ Ei,
+                                                  float x, float y, float z,
+                                                  const float* __restrict__ mlo, int h, int w) {
+  float l0 = Ei[0] * x + Ei[1] * y + Ei[2] * z + Ei[3];
+  float l1 = Ei[4] * x + Ei[5] * y + Ei[6] * z + Ei[7];
+  float l2 = Ei[8] * x + Ei[9] * y + Ei[10] * z + Ei[11];
+  float c0 = Kc[0] * l0 + Kc[1] * l1 + Kc[2] * l2;
+  float c1 = Kc[4] * l0 + Kc[5] * l1 + Kc[6] * l2;
+  float c2 = Kc[8] * l0 + Kc[9] * l1 + Kc[10] * l2;
+  float den = c2 + 1e-8f;
+  float u = c0 / den, v = c1 / den;
+  VoxCam r;
+  r.z = l2;
+  bool fin = finitef(u) && finitef(v);
+  if (!fin) {   // the reference clamps to +-2w (always out of range) or propagates NaN; both -> invalid
+    r.ix = r.iy = -1e9f;
+    r.valid = false;
+    return r;
+  }
+  float gx = (u / (float)(w - 1) - 0.5f) * 2.f;
+  float gy = (v / (float)(h - 1) - 0.5f) * 2.f;
+  r.ix = unnorm_ac(gx, w);
+  r.iy = unnorm_ac(gy, h);
+  bool oob = (gx > 1.f) || (gx < -1.f) || (gy > 1.f) || (gy < -1.f);
+  int ni = nearest_index(r.ix, r.iy, w, h);
+  float occ = ni >= 0 ? mlo[ni] : 0.f;
+  r.valid = (occ > 0.5f) && (l2 > 0.f) && !oob;
+  return r;
+}
+
+// A valid (voxel, camera) pair as the gather/scatter loops need it.
+struct Tap {
+  int cam;
+  int base;        // y0 * w + x0
+  float w[4];      // ATen corner weights, 0 for out-of-range corners
+  unsigned in;     // in-range bit per corner (nw, ne, sw, se)
+  float z;
+};
+
+__device__ __forceinline__ Tap make_tap(int cam, const VoxCam& g, int h, int w) {
+  Bilinear b = bilinear_taps(g.ix, g.iy, w, h);
+  Tap t;
+  t.cam = cam;
+  t.base = b.y0 * w + b.x0;
+  t.in = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    t.w[k] = b.in[k] ? b.w[k] : 0.f;
+    t.in |= (b.in[k] ? 1u : 0u) << k;
+  }
+  t.z = g.z;
+  return t;
+}
+
+__device__ __forceinline__ int tap_offset(int k, int w) { return (k & 1) + (k >> 1) * w; }
+
+__device__ __forceinline__ int rdl(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
+__device__ __forceinline__ float rdlf(float v, int lane) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+__device__ __forceinline__ unsigned rdlu(unsigned v, int lane) {
+  return (unsigned)__builtin_amdgcn_readlane((int)v, lane);
+}
+
+// ------------------------------------------------------------------------------ mask downsample
+__global__ void mask_downsample_k(const float* __restrict__ src, float* __restrict__ dst,
+                                  int BN, int H, int W, int h, int w) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= BN * h * w) return;
+  int x = i % w, y = (i / w) % h, n = i / (w * h);
+  const float* s = src + (size_t)n * H * W;
+  float sy = h > 1 ? (float)(H - 1) / (float)(h - 1) : 0.f;
+  float sx = w > 1 ? (float)(W - 1) / (float)(w - 1) : 0.f;
+  int y0, x0, y1, x1;
+  float ly, lx;
+  if (h == H) { y0 = y1 = y; ly = 0.f; } else {
+    float fy = sy * (float)y;
+    y0 = min((int)floorf(fy), H - 1);
+    ly = fminf(fmaxf(fy - (float)y0, 0.f), 1.f);
+    y1 = y0 + (y0 < H - 1 ? 1 : 0);
+  }
+  if (w == W) { x0 = x1 = x; lx = 0.f; } else {
+    float fx = sx * (float)x;
+    x0 = min((int)floorf(fx), W - 1);
+    lx = fminf(fmaxf(fx - (float)x0, 0.f), 1.f);
+    x1 = x0 + (x0 < W - 1 ? 1 : 0);
+  }
+  float h0 = 1.f - ly, w0 = 1.f - lx;
+  float top = w0 * s[y0 * W + x0] + lx * s[y0 * W + x1];
+  float bot = w0 * s[y1 * W + x0] + lx * s[y1 * W + x1];
+  dst[i] = h0 * top + ly * bot;
+}
+
+// ------------------------------------------------------------------------------ K1 forward
+// One wave owns 64 consecutive voxels.  Phase 1: lane i resolves voxel i's cameras.  Phase 2:
+// the wave walks the 64 voxels; for each, every lane produces one output channel from the
+// folded per-camera maps P (pixel-major rows of 2*Cv floats: 256-B coalesced tap reads).
+template <int CPL>
+__global__ __launch_bounds__(256) void fuse_depth_fwd_k(vfd_voxel_desc d, const float* __restrict__ P,
+                                                        const float* __restrict__ mlo,
+                                                        const float* __restrict__ K,
+                                                        const float* __restrict__ Einv,
+                                                        const float* __restrict__ wz,
+                                                        const float* __restrict__ b_no,
+                                                        const float* __restrict__ b_o,
+                                                        float* __restrict__ vox) {
+  const int lane = threadIdx.x & 63;
+  const int V = d.X * d.Y * d.Z;
+  const int b = blockIdx.y;
+  const int v0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
+  if (v0 >= V) return;
+  const int hw = d.h * d.w;
+  const int v = v0 + lane;
+  int cnt = 0;
+  Tap t0{}, t1{};
+  if (v < V) {
+    float x = d.axis_x[v % d.X], y = d.axis_y[(v / d.X) % d.Y], z = d.axis_z[v / (d.X * d.Y)];
+    for (int c = 0; c < d.N; ++c) {
+      const int bc = b * d.N + c;
+      VoxCam g = voxel_to_camera(K + bc * 16, Einv + bc * 16, x, y, z, mlo + (size_t)bc * hw, d.h, d.w);
+      if (g.valid) {
+        if (cnt == 0) t0 = make_tap(c, g, d.h, d.w);
+        else if (cnt == 1) t1 = make_tap(c, g, d.h, d.w);
+        ++cnt;
+      }
+    }
+  }
+  const int twoCv = 2 * d.Cv;
+  const int nvox = min(64, V - v0);
+  float wzr[CPL][3], bno[CPL], bo[CPL];
+#pragma unroll
+  for (int k = 0; k < CPL; ++k) {
+    int ch = lane + 64 * k;
+    bool on = ch < d.Cv;
+    wzr[k][0] = on ? wz[ch] : 0.f;
+    wzr[k][1] = on ? wz[d.Cv + ch] : 0.f;
+    wzr[k][2] = on ? wz[2 * d.Cv + ch] : 0.f;
+    bno[k] = on ? b_no[ch] : 0.f;
+    bo[k] = on ? b_o[ch] : 0.f;
+  }
+  for (int j = 0; j < nvox; ++j) {
+    const int cj = rdl(cnt, j);
+    float* out = vox + ((size_t)b * V + v0 + j) * d.Cv;
+    if (cj != 1 && cj != 2) {
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) {
+        int ch = lane + 64 * k;
+        if (ch < d.Cv) out[ch] = 0.f;
+      }
+      continue;
+    }
+    const int off = (cj == 1) ? 0 : d.Cv;
+    float acc[CPL];
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) acc[k] = 0.f;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if (s >= cj) break;
+      const Tap& tl = s == 0 ? t0 : t1;
+      const int cam = rdl(tl.cam, j);
+      const int base = rdl(tl.base, j);
+      const unsigned in = rdlu(tl.in, j);
+      const float zt = rdlf(tl.z, j);
+      const float* Pc = P + (size_t)(b * d.N + cam) * hw * twoCv + off;
+      float val[CPL];
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) val[k] = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (!(in >> q & 1u)) continue;
+        const float wq = rdlf(tl.w[q], j);
+        const float* row = Pc + (size_t)(base + tap_offset(q, d.w)) * twoCv;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+          int ch = lane + 64 * k;
+          if (ch < d.Cv) val[k] += row[ch] * wq;
+        }
+      }
+      const int zrow = (cj == 1) ? 0 : 1 + d.group[cam];
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) acc[k] += val[k] + wzr[k][zrow] * (zt / d.z_scale);
+    }
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+      int ch = lane + 64 * k;
+      if (ch < d.Cv) {
+        float pre = acc[k] + (cj == 1 ? bno[k] : bo[k]);
+        out[ch] = pre > 0.f ? pre : pre * 0.1f;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------ K1 backward
+// Same voxel walk; lanes are channels, so every scatter into dP is a 256-B contiguous row of
+// f32 atomics (the full-rate atomic shape on gfx950).  Depth-column and bias gradients are
+// reduced per lane and written as per-wave partials (summed by fuse_depth_reduce_k).
+template <int CPL>
+__global__ __launch_bounds__(256) void fuse_depth_bwd_k(vfd_voxel_desc d, const float* __restrict__ dvox,
+                                                        const float* __restrict__ vox,
+                                                        const float* __restrict__ mlo,
+                                                        const float* __restrict__ K,
+                                                        const float* __restrict__ Einv,
+                                                        float* __restrict__ dP,
+                                                        float* __restrict__ partial) {
+  const int lane = threadIdx.x & 63;
+  const int V = d.X * d.Y * d.Z;
+  const int b = blockIdx.y;
+  const int wave_id = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int v0 = wave_id * 64;
+  const int n_waves = (V + 63) / 64;
+  float* part = partial + ((size_t)b * n_waves + wave_id) * 5 * d.Cv;
+  float red[CPL][5];
+#pragma unroll
+  for (int k = 0; k < CPL; ++k)
+#pragma unroll
+    for (int r = 0; r < 5; ++r) red[k][r] = 0.f;
+  if (v0 < V) {
+    const int hw = d.h * d.w;
+    const int v = v0 + lane;
+    int cnt = 0;
+    Tap t0{}, t1{};
+    if (v < V) {
+      float x = d.axis_x[v % d.X], y = d.axis_y[(v / d.X) % d.Y], z = d.axis_z[v / (d.X * d.Y)];
+      for (int c = 0; c < d.N; ++c) {
+        const int bc = b * d.N + c;
+        VoxCam g = voxel_to_camera(K + bc * 16, Einv + bc * 16, x, y, z, mlo + (size_t)bc * hw, d.h, d.w);
+        if (g.valid) {
+          if (cnt == 0) t0 = make_tap(c, g, d.h, d.w);
+          else if (cnt == 1) t1 = make_tap(c, g, d.h, d.w);
+          ++cnt;
+        }
+      }
+    }
+    const int twoCv = 2 * d.Cv;
+    const int nvox = min(64, V - v0);
+    for (int j = 0; j < nvox; ++j) {
+      const int cj = rdl(cnt, j);
+      if (cj != 1 && cj != 2) continue;
+      const size_t vrow = ((size_t)b * V + v0 + j) * d.Cv;
+      float dpre[CPL];
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) {
+        int ch = lane + 64 * k;
+        dpre[k] = 0.f;
+        if (ch < d.Cv) {
+          float o = vox[vrow + ch];
+          dpre[k] = dvox[vrow + ch] * (o > 0.f ? 1.f : 0.1f);
+          red[k][3 + (cj - 1)] += dpre[k];
+        }
+      }
+      const int off = (cj == 1) ? 0 : d.Cv;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        if (s >= cj) break;
+        const Tap& tl = s == 0 ? t0 : t1;
+        const int cam = rdl(tl.cam, j);
+        const int base = rdl(tl.base, j);
+        const unsigned in = rdlu(tl.in, j);
+        const float zt = rdlf(tl.z, j);
+        float* Pc = dP + (size_t)(b * d.N + cam) * hw * twoCv + off;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (!(in >> q & 1u)) continue;
+          const float wq = rdlf(tl.w[q], j);
+          float* row = Pc + (size_t)(base + tap_offset(q, d.w)) * twoCv;
+#pragma unroll
+          for (int k = 0; k < CPL; ++k) {
+            int ch = lane + 64 * k;
+            if (ch < d.Cv) atomicAdd(row + ch, wq * dpre[k]);
+          }
+        }
+        const int zrow = (cj == 1) ? 0 : 1 + d.group[cam];
+        const float zf = zt / d.z_scale;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+          // select the row without dynamic register indexing
+          float c = dpre[k] * zf;
+          red[k][0] += zrow == 0 ? c : 0.f;
+          red[k][1] += zrow == 1 ? c : 0.f;
+          red[k][2] += zrow == 2 ? c : 0.f;
+        }
+      }
+    }
+  }
+  if (v0 < V) {
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+      int ch = lane + 64 * k;
+      if (ch < d.Cv)
+#pragma unroll
+        for (int r = 0; r < 5; ++r) part[r * d.Cv + ch] = red[k][r];
+    }
+  }
+}
+
+__global__ void fuse_depth_reduce_k(const float* __restrict__ partial, int n_rows, int n_out,
+                                    float* __restrict__ out) {
+  // out[i] = sum_r partial[r, i]  (fixed order, double accumulation)
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_out) return;
+  double s = 0.0;
+  for (int r = 0; r < n_rows; ++r) s += (double)partial[(size_t)r * n_out + i];
+  out[i] = (float)s;
+}
+
+// ------------------------------------------------------------------------------ K2 forward
+// Lanes are voxels (x fastest) so every channel row of the NCHW output is a coalesced store;
+// the per-camera maps (B*N*C*h*w floats, L2/MALL resident) are gathered per lane.
+
+__device__ __forceinline__ void pad_sets(int i, int n, bool pad, int* idx, int* cnt) {
+  // positions of source index i in a reflect-padded (+2) axis: {i+1} U {0 if i==1} U {n+1 if i==n-2}
+  if (!pad) { idx[0] = i; *cnt = 1; return; }
+  int c = 0;
+  idx[c++] = i + 1;
+  if (i == 1) idx[c++] = 0;
+  if (i == n - 2) idx[c++] = n + 1;
+  *cnt = c;
+}
+
+template <int NC>
+__global__ __launch_bounds__(256) void fuse_pose_fwd_k(vfd_voxel_desc d, const float* __restrict__ feats,
+                                                       const float* __restrict__ mlo,
+                                                       const float* __restrict__ K,
+                                                       const float* __restrict__ Einv,
+                                                       float* __restrict__ out) {
+  const int V = d.X * d.Y * d.Z;
+  const int b = blockIdx.y;
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= V) return;
+  const int hw = d.h * d.w;
+  const int xi = v % d.X, yi = (v / d.X) % d.Y, zi = v / (d.X * d.Y);
+  const float x = d.axis_x[xi], y = d.axis_y[yi], z = d.axis_z[zi];
+  Tap taps[NC];
+  bool val[NC];
+  int cnt = 0;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int bc = b * NC + c;
+    VoxCam g = voxel_to_camera(K + bc * 16, Einv + bc * 16, x, y, z, mlo + (size_t)bc * hw, d.h, d.w);
+    val[c] = g.valid;
+    taps[c] = make_tap(c, g, d.h, d.w);
+    cnt += g.valid ? 1 : 0;
+  }
+  const float denom = (float)cnt + 1e-7f;
+  const int P = d.pad_out ? 2 : 0;
+  const int Yo = d.Y + P, Xo = d.X + P;
+  int rows[3], cols[3], nr, nc;
+  pad_sets(yi, d.Y, d.pad_out, rows, &nr);
+  pad_sets(xi, d.X, d.pad_out, cols, &nc);
+  float* ob = out + (size_t)b * (d.C + 1) * d.Z * Yo * Xo;
+  for (int ch = 0; ch <= d.C; ++ch) {
+    float acc = 0.f;
+    if (ch < d.C) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        if (!val[c]) continue;
+        const float* f = feats + ((size_t)(b * NC + c) * d.C + ch) * hw + taps[c].base;
+        float vv = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (taps[c].in >> q & 1u) vv += f[tap_offset(q, d.w)] * taps[c].w[q];
+        acc += vv;
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+        if (val[c]) acc += taps[c].z / d.z_scale;
+    }
+    const float o = acc / denom;
+    float* plane = ob + ((size_t)ch * d.Z + zi) * Yo * Xo;
+    for (int a = 0; a < nr; ++a)
+      for (int c2 = 0; c2 < nc; ++c2) plane[rows[a] * Xo + cols[c2]] = o;
+  }
+}
+
+// ------------------------------------------------------------------------------ K2 backward
+template <int NC>
+__global__ __launch_bounds__(256) void fuse_pose_bwd_k(vfd_voxel_desc d, const float* __restrict__ dout,
+                                                       const float* __restrict__ mlo,
+                                                       const float* __restrict__ K,
+                                                       const float* __restrict__ Einv,
+                                                       float* __restrict__ dfeats) {
+  const int V = d.X * d.Y * d.Z;
+  const int b = blockIdx.y;
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= V) return;
+  const int hw = d.h * d.w;
+  const int xi = v % d.X, yi = (v / d.X) % d.Y, zi = v / (d.X * d.Y);
+  const float x = d.axis_x[xi], y = d.axis_y[yi], z = d.axis_z[zi];
+  Tap taps[NC];
+  bool val[NC];
+  int cnt = 0;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int bc = b * NC + c;
+    VoxCam g = voxel_to_camera(K + bc * 16, Einv + bc * 16, x, y, z, mlo + (size_t)bc * hw, d.h, d.w);
+    val[c] = g.valid;
+    taps[c] = make_tap(c, g, d.h, d.w);
+    cnt += g.valid ? 1 : 0;
+  }
+  if (cnt == 0) return;
+  const float denom = (float)cnt + 1e-7f;
+  const int P = d.pad_out ? 2 : 0;
+  const int Yo = d.Y + P, Xo = d.X + P;
+  int rows[3], cols[3], nr, nc;
+  pad_sets(yi, d.Y, d.pad_out, rows, &nr);
+  pad_sets(xi, d.X, d.pad_out, cols, &nc);
+  const float* gb = dout + (size_t)b * (d.C + 1) * d.Z * Yo * Xo;
+  for (int ch = 0; ch < d.C; ++ch) {
+    const float* plane = gb + ((size_t)ch * d.Z + zi) * Yo * Xo;
+    float g = 0.f;
+    for (int a = 0; a < nr; ++a)
+      for (int c2 = 0; c2 < nc; ++c2) g += plane[rows[a] * Xo + cols[c2]];
+    g = g / denom;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      if (!val[c]) continue;
+      float* f = dfeats + ((size_t)(b * NC + c) * d.C + ch) * hw + taps[c].base;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (taps[c].in >> q & 1u) atomicAdd(f + tap_offset(q, d.w), g * taps[c].w[q]);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------ K3 geometry
+struct Tri {
+  int x0, y0, z0;
+  float w[8];     // tnw, tne, tsw, tse, bnw, bne, bsw, bse
+  unsigned in;
+};
+
+// volumetric_fusionnet.py:245-260 + ATen grid_sampler_3d weights
+__device__ __forceinline__ Tri frustum_sample(const vfd_voxel_desc& d, const float* __restrict__ iK,
+                                              const float* __restrict__ E, int px, int py, float dep) {
+  float fx = (float)px, fy = (float)py;
+  float r0 = iK[0] * fx + iK[1] * fy + iK[2];
+  float r1 = iK[4] * fx + iK[5] * fy + iK[6];
+  float r2 = iK[8] * fx + iK[9] * fy + iK[10];
+  float p0 = dep * r0, p1 = dep * r1, p2 = dep * r2;
+  float w0 = E[0] * p0 + E[1] * p1 + E[2] * p2 + E[3];
+  float w1 = E[4] * p0 + E[5] * p1 + E[6] * p2 + E[7];
+  float w2 = E[8] * p0 + E[9] * p1 + E[10] * p2 + E[11];
+  float gx = (w0 - d.str[0]) / d.len[0] * 2.f - 1.f;
+  float gy = (w1 - d.str[1]) / d.len[1] * 2.f - 1.f;
+  float gz = (w2 - d.str[2]) / d.len[2] * 2.f - 1.f;
+  float ix = unnorm_ac(gx, d.X), iy = unnorm_ac(gy, d.Y), iz = unnorm_ac(gz, d.Z);
+  Tri t;
+  t.in = 0;
+  if (!(finitef(ix) && finitef(iy) && finitef(iz))) {
+    t.x0 = t.y0 = t.z0 = -4;
+    for (int k = 0; k < 8; ++k) t.w[k] = 0.f;
+    return t;
+  }
+  float fx0 = floorf(ix), fy0 = floorf(iy), fz0 = floorf(iz);
+  float fx1 = fx0 + 1.f, fy1 = fy0 + 1.f, fz1 = fz0 + 1.f;
+  float ax[2] = {fx1 - ix, ix - fx0}, ay[2] = {fy1 - iy, iy - fy0}, az[2] = {fz1 - iz, iz - fz0};
+  t.x0 = (int)fminf(fmaxf(fx0, -4.f), (float)d.X + 4.f);
+  t.y0 = (int)fminf(fmaxf(fy0, -4.f), (float)d.Y + 4.f);
+  t.z0 = (int)fminf(fmaxf(fz0, -4.f), (float)d.Z + 4.f);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    int dx = k & 1, dy = (k >> 1) & 1, dz = k >> 2;
+    int xx = t.x0 + dx, yy = t.y0 + dy, zz = t.z0 + dz;
+    bool ok = xx >= 0 && xx < d.X && yy >= 0 && yy < d.Y && zz >= 0 && zz < d.Z;
+    t.w[k] = ax[dx] * ay[dy] * az[dz];
+    t.in |= (ok ? 1u : 0u) << k;
+  }
+  return t;
+}
+
+__device__ __forceinline__ int tri_index(const vfd_voxel_desc& d, const Tri& t, int k) {
+  return ((t.z0 + (k >> 2)) * d.Y + (t.y0 + ((k >> 1) & 1))) * d.X + (t.x0 + (k & 1));
+}
+
+// ------------------------------------------------------------------------------ K3 forward
+// Lanes are frustum pixels (coalesced stores of every output channel row); each lane reads
+// its 8 voxel rows as float4 vectors of the channels-last voxel grid (K1's output layout).
+template <int CV>
+__global__ __launch_bounds__(256) void voxel_project_fwd_k(vfd_voxel_desc d, const float* __restrict__ vox,
+                                                           const float* __restrict__ invK,
+                                                           const float* __restrict__ E,
+                                                           float* __restrict__ out) {
+  const int hw = d.h * d.w;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const int dep_i = blockIdx.y;
+  const int bc = blockIdx.z;           // b * N + cam
+  if (p >= hw) return;
+  const int b = bc / d.N;
+  const int px = p % d.w, py = p / d.w;
+  Tri t = frustum_sample(d, invK + bc * 16, E + bc * 16, px, py, d.dbins[dep_i]);
+  const int V = d.X * d.Y * d.Z;
+  const float* vb = vox + (size_t)b * V * CV;
+  float acc[CV];
+#pragma unroll
+  for (int c = 0; c < CV; ++c) acc[c] = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    if (!(t.in >> k & 1u)) continue;
+    const float4* row = reinterpret_cast<const float4*>(vb + (size_t)tri_index(d, t, k) * CV);
+    const float wk = t.w[k];
+#pragma unroll
+    for (int c4 = 0; c4 < CV / 4; ++c4) {
+      float4 q = row[c4];
+      acc[4 * c4 + 0] += q.x * wk;
+      acc[4 * c4 + 1] += q.y * wk;
+      acc[4 * c4 + 2] += q.z * wk;
+      acc[4 * c4 + 3] += q.w * wk;
+    }
+  }
+  const int P = d.pad_out ? 2 : 0;
+  const int ho = d.h + P, wo = d.w + P;
+  int rows[3], cols[3], nr, nc;
+  pad_sets(py, d.h, d.pad_out, rows, &nr);
+  pad_sets(px, d.w, d.pad_out, cols, &nc);
+  float* ob = out + (size_t)bc * CV * d.D * ho * wo;
+#pragma unroll
+  for (int c = 0; c < CV; ++c) {
+    float* plane = ob + ((size_t)c * d.D + dep_i) * ho * wo;
+    for (int a = 0; a < nr; ++a)
+      for (int c2 = 0; c2 < nc; ++c2) plane[rows[a] * wo + cols[c2]] = acc[c];
+  }
+}
+
+// ------------------------------------------------------------------------------ K3 backward
+// A block owns 64 consecutive frustum pixels at one depth bin.  The (reflect-folded) gradient
+// tile [Cv x 64] is staged through LDS with coalesced row loads, then each wave walks 16
+// samples with lanes = channels: consecutive samples that fall in the same voxel cell are
+// merged in registers (runs are long in the near field) and flushed as 256-B rows of f32
+// atomics into the channels-last voxel gradient.
+template <int CV>
+__global__ __launch_bounds__(256) void voxel_project_bwd_k(vfd_voxel_desc d, const float* __restrict__ dout,
+                                                           const float* __restrict__ invK,
+                                                           const float* __restrict__ E,
+                                                           float* __restrict__ dvox) {
+  constexpr int TP = 64;                        // pixels per block
+  constexpr int CPL = (CV + 63) / 64;
+  __shared__ float tile[CV][TP + 1];
+  const int hw = d.h * d.w;
+  const int p0 = blockIdx.x * TP;
+  const int dep_i = blockIdx.y;
+  const int bc = blockIdx.z;
+  const int b = bc / d.N;
+  const int P = d.pad_out ? 2 : 0;
+  const int ho = d.h + P, wo = d.w + P;
+  const float* gb = dout + (size_t)bc * CV * d.D * ho * wo;
+  for (int i = threadIdx.x; i < CV * TP; i += blockDim.x) {
+    const int c = i / TP, j = i % TP, p = p0 + j;
+    float g = 0.f;
+    if (p < hw) {
+      const int px = p % d.w, py = p / d.w;
+      int rows[3], cols[3], nr, nc;
+      pad_sets(py, d.h, d.pad_out, rows, &nr);
+      pad_sets(px, d.w, d.pad_out, cols, &nc);
+      const float* plane = gb + ((size_t)c * d.D + dep_i) * ho * wo;
+      for (int a = 0; a < nr; ++a)
+        for (int c2 = 0; c2 < nc; ++c2) g += plane[rows[a] * wo + cols[c2]];
+    }
+    tile[c][j] = g;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int V = d.X * d.Y * d.Z;
+  float* vb = dvox + (size_t)b * V * CV;
+  float acc[CPL][8];
+  Tri cur;
+  cur.in = 0;
+  cur.x0 = cur.y0 = cur.z0 = -100;
+  bool open = false;
+  auto flush = [&]() {
+    if (!open) return;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (!(cur.in >> k & 1u)) continue;
+      float* row = vb + (size_t)tri_index(d, cur, k) * CV;
+#pragma unroll
+      for (int q = 0; q < CPL; ++q) {
+        int c = lane + 64 * q;
+        if (c < CV) atomicAdd(row + c, acc[q][k]);
+      }
+    }
+  };
+  for (int jj = 0; jj < TP / 4; ++jj) {
+    const int j = wv * (TP / 4) + jj;
+    const int p = p0 + j;
+    if (p >= hw) break;
+    Tri t = frustum_sample(d, invK + bc * 16, E + bc * 16, p % d.w, p / d.w, d.dbins[dep_i]);
+    if (t.in == 0) continue;
+    const bool same = open && t.x0 == cur.x0 && t.y0 == cur.y0 && t.z0 == cur.z0;
+    if (!same) {
+      flush();
+      cur = t;
+      open = true;
+#pragma unroll
+      for (int q = 0; q < CPL; ++q)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[q][k] = 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) {
+      int c = lane + 64 * q;
+      float g = c < CV ? tile[c][j] : 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[q][k] += g * t.w[k];
+    }
+  }
+  flush();
+}
+
+}  // namespace vfd
+
+// ================================================================================== C ABI
+using namespace vfd;
+
+static int check_voxel_desc(const vfd_voxel_desc* d) {
+  VFD_REQUIRE(d != nullptr, "null descriptor");
+  VFD_REQUIRE(d->B > 0 && d->N > 0 && d->N <= 8, "bad B/N (%d, %d)", d->B, d->N);
+  VFD_REQUIRE(d->h > 1 && d->w > 1 && d->X > 1 && d->Y > 1 && d->Z > 1, "bad map / voxel sizes");
+  VFD_REQUIRE(d->axis_x && d->axis_y && d->axis_z, "voxel axes not set");
+  return VFD_OK;
+}
+
+extern "C" {
+
+int vfd_mask_downsample(const vfd_voxel_desc* d, const float* mask, float* mask_lo, void* stream) {
+  int st = check_voxel_desc(d);
+  if (st) return st;
+  hipStream_t s = (hipStream_t)stream;
+  ProfScope ps(K_MASK_DOWN, s);
+  const int n = d->B * d->N * d->h * d->w;
+  mask_downsample_k<<<cdiv(n, 256), 256, 0, s>>>(mask, mask_lo, d->B * d->N, d->H, d->W, d->h, d->w);
+  return fail_launch("mask_downsample");
+}
+
+int vfd_fuse_depth_fwd(const vfd_voxel_desc* d, const float* P, const float* mask_lo, const float* K,
+                       const float* Einv, const float* wz, const float* b_no, const float* b_o,
+                       float* vox, void* stream) {
+  int st = check_voxel_desc(d);
+  if (st) return st;
+  VFD_REQUIRE(d->Cv > 0 && d->Cv <= 128, "Cv=%d unsupported (<=128)", d->Cv);
+  VFD_REQUIRE(d->group != nullptr, "camera groups not set");
+  hipStream_t s = (hipStream_t)stream;
+  const int V = d->X * d->Y * d->Z;
+  dim3 grid(cdiv(cdiv(V, 64), 4), d->B);
+  ProfScope ps(K_FUSE_DEPTH_FWD, s);
+  if (d->Cv <= 64)
+    fuse_depth_fwd_k<1><<<grid, 256, 0, s>>>(*d, P, mask_lo, K, Einv, wz, b_no, b_o, vox);
+  else
+    fuse_depth_fwd_k<2><<<grid, 256, 0, s>>>(*d, P, mask_lo, K, Einv, wz, b_no, b_o, vox);
+  return fail_launch("fuse_depth_fwd");
+}
+
+size_t vfd_fuse_depth_bwd_workspace(const vfd_voxel_desc* d) {
+  const int V = d->X * d->Y * d->Z;
+  return (size_t)d->B * cdiv(V, 64) * 5 * d->Cv * sizeof(float);
+}
+
+int vfd_fuse_depth_bwd(const vfd_voxel_desc* d, const float* d_vox, const float* vox, const float* mask_lo,
+                       const float* K, const float* Einv, float* dP, float* d_wzb, void* ws, size_t ws_bytes,
+                       void* stream) {
+  int st = check_voxel_desc(d);
+  if (st) return st;
+  VFD_REQUIRE(d->Cv > 0 && d->Cv <= 128, "Cv=%d unsupported (<=128)", d->Cv);
+  VFD_REQUIRE(ws_bytes >= vfd_fuse_depth_bwd_workspace(d), "workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const int V = d->X * d->Y * d->Z;
+  (void)hipMemsetAsync(dP, 0, (size_t)d->B * d->N * d->h * d->w * 2 * d->Cv * sizeof(float), s);
+  dim3 grid(cdiv(cdiv(V, 64), 4), d->B);
+  float* partial = (float*)ws;
+  {
+    ProfScope ps(K_FUSE_DEPTH_BWD, s);
+    if (d->Cv <= 64)
+      fuse_depth_bwd_k<1><<<grid, 256, 0, s>>>(*d, d_vox, vox, mask_lo, K, Einv, dP, partial);
+    else
+      fuse_depth_bwd_k<2><<<grid, 256, 0, s>>>(*d, d_vox, vox, mask_lo, K, Einv, dP, partial);
+  }
+  st = fail_launch("fuse_depth_bwd");
+  if (st) return st;
+  // pad waves beyond V wrote nothing: zero-initialise by reducing only real rows
+  const int rows = d->B * (int)cdiv(V, 64);
+  fuse_depth_reduce_k<<<cdiv(5 * d->Cv, 256), 256, 0, s>>>(partial, rows, 5 * d->Cv, d_wzb);
+  return fail_launch("fuse_depth_reduce");
+}
+
+int vfd_fuse_pose_fwd(const vfd_voxel_desc* d, const float* feats, const float* mask_lo, const float* K,
+                      const float* Einv, float* out, void* stream) {
+  int st = check_voxel_desc(d);
+  if (st) return st;
+  hipStream_t s = (hipStream_t)stream;
+  const int V = d->X * d->Y * d->Z;
+  ProfScope ps(K_FUSE_POSE_FWD, s);
+  dim3 grid(cdiv(V, 256), d->B);
+  switch (d->N) {
+#define VFD_CASE(n) case n: fuse_pose_fwd_k<n><<<grid, 256, 0, s>>>(*d, feats, mask_lo, K, Einv, out); break;
+    VFD_CASE(1) VFD_CASE(2) VFD_CASE(3) VFD_CASE(4) VFD_CASE(5) VFD_CASE(6) VFD_CASE(7) VFD_CASE(8)
+#undef VFD_CASE
+  }
+  return fail_launch("fuse_pose_fwd");
+}
+
+int vfd_fuse_pose_bwd(const vfd_voxel_desc* d, const float* d_out, const float* mask_lo, const float* K,
+                      const float* Einv, float* d_feats, void* stream) {
+  int st = check_voxel_desc(d);
+  if (st) return st;
+  hipStream_t s = (hipStream_t)stream;
+  const int V = d->X * d->Y * d->Z;
+  (void)hipMemsetAsync(d_feats, 0, (size_t)d->B * d->N * d->C * d->h * d->w * sizeof(float), s);
+  ProfScope ps(K_FUSE_POSE_BWD, s);
+  dim3 grid(cdiv(V, 256), d->B);
+  switch (d->N) {
+#define VFD_CASE(n) case n: fuse_pose_bwd_k<n><<<grid, 256, 0, s>>>(*d, d_out, mask_lo, K, Einv, d_feats); break;
+    VFD_CASE(1) VFD_CASE(2) VFD_CASE(3) VFD_CASE(4) VFD_CASE(5) VFD_CASE(6) VFD_CASE(7) VFD_CASE(8)
+#undef VFD_CASE
+  }
+  return fail_launch("fuse_pose_bwd");
+}
+
+int vfd_voxel_project_fwd(const vfd_voxel_desc* d, const float* vox, const float* invK, const float* E,
+                          float* out, void* stream) {
+  int st = check_voxel_desc(d);
+  if (st) return st;
+  VFD_REQUIRE(d->dbins != nullptr && d->D > 0, "depth bins not set");
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid(cdiv(d->h * d->w, 256), d->D, d->B * d->N);
+  ProfScope ps(K_VPROJ_FWD, s);
+  switch (d->Cv) {
+    case 8: voxel_project_fwd_k<8><<<grid, 256, 0, s>>>(*d, vox, invK, E, out); break;
+    case 16: voxel_project_fwd_k<16><<<grid, 256, 0, s>>>(*d, vox, invK, E, out); break;
+    case 32: voxel_project_fwd_k<32><<<grid, 256, 0, s>>>(*d, vox, invK, E, out); break;
+    case 64: voxel_project_fwd_k<64><<<grid, 256, 0, s>>>(*d, vox, invK, E, out); break;
+    default: set_error("voxel_project: Cv=%d unsupported (8/16/32/64)", d->Cv); return VFD_EINVAL;
+  }
+  return fail_launch("voxel_project_fwd");
+}
+
+int vfd_voxel_project_bwd(const vfd_voxel_desc* d, const float* d_out, const float* invK, const float* E,
+                          float* d_vox, void* stream) {
+  int st = check_voxel_desc(d);
+  if (st) return st;
+  VFD_REQUIRE(d->dbins != nullptr && d->D > 0, "depth bins not set");
+  hipStream_t s = (hipStream_t)stream;
+  const size_t V = (size_t)d->X * d->Y * d->Z;
+  (void)hipMemsetAsync(d_vox, 0, (size_t)d->B * V * d->Cv * sizeof(float), s);
+  dim3 grid(cdiv(d->h * d->w, 64), d->D, d->B * d->N);
+  ProfScope ps(K_VPROJ_BWD, s);
+  switch (d->Cv) {
+    case 8: voxel_project_bwd_k<8><<<grid, 256, 0, s>>>(*d, d_out, invK, E, d_vox); break;
+    case 16: voxel_project_bwd_k<16><<<grid, 256, 0, s>>>(*d, d_out, invK, E, d_vox); break;
+    case 32: voxel_project_bwd_k<32><<<grid, 256, 0, s>>>(*d, d_out, invK, E, d_vox); break;
+    case 64: voxel_project_bwd_k<64><<<grid, 256, 0, s>>>(*d, d_out, invK, E, d_vox); break;
+    default: set_error("voxel_project: Cv=%d unsupported (8/16/32/64)", d->Cv); return VFD_EINVAL;
+  }
+  return fail_launch("voxel_project_bwd");
+}
+
+}  // extern "C"

@@ -1,0 +1,124 @@
+// Shared helpers of the gfx950 hot-path kernels: error reporting, launch-time profiling hook,
+// ATen-compatible sampling arithmetic, wave64 reductions.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string>
+
+#include "vfd_capi.h"
+
+namespace vfd {
+
+// ---------------------------------------------------------------- error reporting
+void set_error(const char* fmt, ...);
+int fail_launch(const char* what);   // reads hipGetLastError, returns VFD_ELAUNCH or VFD_OK
+
+#define VFD_REQUIRE(cond, ...)            \
+  do {                                    \
+    if (!(cond)) {                        \
+      ::vfd::set_error(__VA_ARGS__);      \
+      return VFD_EINVAL;                  \
+    }                                     \
+  } while (0)
+
+// ---------------------------------------------------------------- profiling hook
+enum KernelId {
+  K_MASK_DOWN = 0, K_FUSE_DEPTH_FWD, K_FUSE_DEPTH_BWD, K_FUSE_POSE_FWD, K_FUSE_POSE_BWD,
+  K_VPROJ_FWD, K_VPROJ_BWD, K_VIEW_STATS, K_VIEW_APPLY, K_VIEW_BWD, K_PHOTO_FWD, K_PHOTO_BWD,
+  K_SMOOTH_FWD, K_SMOOTH_BWD, K_COUNT
+};
+void prof_begin(int id, hipStream_t s);
+void prof_end(int id, hipStream_t s);
+
+struct ProfScope {
+  int id;
+  hipStream_t s;
+  ProfScope(int i, hipStream_t st) : id(i), s(st) { prof_begin(id, s); }
+  ~ProfScope() { prof_end(id, s); }
+};
+
+// ---------------------------------------------------------------- device math
+constexpr int WAVE = 64;
+
+__device__ __forceinline__ float unnorm_ac(float g, int size) {
+  // ATen grid_sampler_unnormalize, align_corners=True: ((g + 1) / 2) * (size - 1)
+  return ((g + 1.f) / 2.f) * (float)(size - 1);
+}
+
+__device__ __forceinline__ int reflect1(int i, int n) {
+  // ReflectionPad(1) source index of padded-relative coordinate i in [-1, n]
+  return i < 0 ? -i : (i >= n ? 2 * n - 2 - i : i);
+}
+
+__device__ __forceinline__ bool finitef(float x) { return __builtin_isfinite(x); }
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, WAVE);
+  return v;
+}
+
+// Bilinear tap set with ATen's corner weights (grid_sampler_2d, zeros padding).
+struct Bilinear {
+  int x0, y0;
+  float w[4];     // nw, ne, sw, se
+  bool in[4];
+  bool finite;
+};
+
+__device__ __forceinline__ Bilinear bilinear_taps(float ix, float iy, int Wd, int Hd) {
+  Bilinear b;
+  b.finite = finitef(ix) && finitef(iy);
+  if (!b.finite) {
+    b.x0 = b.y0 = 0;
+    for (int k = 0; k < 4; ++k) { b.w[k] = 0.f; b.in[k] = false; }
+    return b;
+  }
+  float fx0 = floorf(ix), fy0 = floorf(iy);
+  float fx1 = fx0 + 1.f, fy1 = fy0 + 1.f;
+  b.w[0] = (fx1 - ix) * (fy1 - iy);
+  b.w[1] = (ix - fx0) * (fy1 - iy);
+  b.w[2] = (fx1 - ix) * (iy - fy0);
+  b.w[3] = (ix - fx0) * (iy - fy0);
+  // clamp before the int conversion: far-away coordinates must not overflow
+  fx0 = fminf(fmaxf(fx0, -2.f), (float)Wd + 1.f);
+  fy0 = fminf(fmaxf(fy0, -2.f), (float)Hd + 1.f);
+  b.x0 = (int)fx0;
+  b.y0 = (int)fy0;
+  bool xin0 = b.x0 >= 0 && b.x0 < Wd, xin1 = b.x0 + 1 >= 0 && b.x0 + 1 < Wd;
+  bool yin0 = b.y0 >= 0 && b.y0 < Hd, yin1 = b.y0 + 1 >= 0 && b.y0 + 1 < Hd;
+  b.in[0] = xin0 && yin0;
+  b.in[1] = xin1 && yin0;
+  b.in[2] = xin0 && yin1;
+  b.in[3] = xin1 && yin1;
+  return b;
+}
+
+// Nearest tap (round half to even, as ATen); returns -1 when out of range / non-finite.
+__device__ __forceinline__ int nearest_index(float ix, float iy, int Wd, int Hd) {
+  if (!(finitef(ix) && finitef(iy))) return -1;
+  float rx = rintf(ix), ry = rintf(iy);
+  if (rx < 0.f || rx > (float)(Wd - 1) || ry < 0.f || ry > (float)(Hd - 1)) return -1;
+  return (int)ry * Wd + (int)rx;
+}
+
+// counter-based normal variates for the identity-loss tie-break noise
+__device__ __forceinline__ uint32_t mix32(uint64_t x) {
+  x ^= x >> 33; x *= 0xff51afd7ed558ccdULL;
+  x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL;
+  x ^= x >> 33;
+  return (uint32_t)x;
+}
+__device__ __forceinline__ float hash_normal(uint64_t seed, uint64_t idx) {
+  uint32_t a = mix32(seed * 0x9E3779B97F4A7C15ULL + 2 * idx + 1);
+  uint32_t b = mix32(seed * 0xD1B54A32D192ED03ULL + 2 * idx + 2);
+  float u1 = ((float)(a >> 8) + 1.f) * (1.f / 16777217.f);   // (0, 1]
+  float u2 = (float)(b >> 8) * (1.f / 16777216.f);
+  return sqrtf(-2.f * logf(u1)) * cosf(6.2831853071795864f * u2);
+}
+
+inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
+
+}  // namespace vfd

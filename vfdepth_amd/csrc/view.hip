@@ -1,0 +1,450 @@
+// K4 — fused view synthesis for gfx950 (reference: models/geometry/geometry_util.py:33-82,
+// models/geometry/view_rendering.py:30-82, 118-198).
+//
+// Per target camera the reference runs 8 independent warps (2 temporal, 3 frames x 2 spatial
+// neighbours), each a backproject -> matmul -> divide -> grid_sample(bilinear) + grid_sample
+// (nearest) -> NaN fix -> OOB mask -> (intensity alignment: two masked global reductions) chain,
+// ~15 ATen launches and ~20 full-resolution intermediates per warp.  Here every pixel
+// back-projects its depth once and evaluates all warps in registers:
+//   view_stats_k    per-warp moments for intensity alignment (fp64 block partials)
+//   view_finalize_k means / stds / batch-wide "empty overlap" skip per warp
+//   view_apply_k    normalised warps, temporal planes, overlap sums -> the 20 output planes
+//   view_bwd_k      d depth (all warps summed per pixel, no atomics) and d (K T)[:3] partials
+// Source images (3 frames x N cameras) stay L2/MALL resident; nothing but inputs and the
+// output planes touches HBM.
+#include "vfd_common.h"
+
+namespace vfd {
+
+constexpr int VPPT = 4;          // pixels per thread in the reduction kernels
+constexpr int VBLK = 256;
+
+struct WarpEntry {
+  int fslot, src, oslot;         // frame slot, source camera (-1: unused), overlap slot (-1: temporal)
+};
+
+// Index conventions: bt = blockIdx.y = b * cam_count + target slot (per-target arrays);
+// br = b * N + cam (whole-rig arrays: colours, masks).
+struct Target {
+  int bt, b, cam;
+  size_t br;
+};
+__device__ __forceinline__ Target target_of(const vfd_view_desc& d) {
+  Target t;
+  t.bt = blockIdx.y;
+  t.b = t.bt / d.cam_count;
+  t.cam = d.cam_begin + t.bt % d.cam_count;
+  t.br = (size_t)t.b * d.N + t.cam;
+  return t;
+}
+
+__device__ __forceinline__ WarpEntry warp_entry(const vfd_view_desc& d, int cam, int w) {
+  const int* t = d.warp_tab + (cam * d.n_warp + w) * 3;
+  return {t[0], t[1], t[2]};
+}
+
+// Back-projected point of pixel p (geometry_util.py:56-64).
+__device__ __forceinline__ void backproject(const float* __restrict__ iK, float depth, int x, int y,
+                                            float* X, float* ray) {
+  float fx = (float)x, fy = (float)y;
+  ray[0] = iK[0] * fx + iK[1] * fy + iK[2];
+  ray[1] = iK[4] * fx + iK[5] * fy + iK[6];
+  ray[2] = iK[8] * fx + iK[9] * fy + iK[10];
+  X[0] = depth * ray[0];
+  X[1] = depth * ray[1];
+  X[2] = depth * ray[2];
+}
+
+struct WarpSample {
+  float a, b, den;       // uvw numerators and w + 1e-7
+  float ix, iy;
+  float img[3];
+  float cm;              // (~OOB) * nearest(mask)
+  Bilinear bl;
+};
+
+// reproject (geometry_util.py:66-81) + get_virtual_image (view_rendering.py:61-82)
+__device__ __forceinline__ WarpSample warp_sample(const float* __restrict__ Mw, const float* X,
+                                                  const float* __restrict__ img, const float* __restrict__ msk,
+                                                  int H, int W) {
+  WarpSample s;
+  s.a = Mw[0] * X[0] + Mw[1] * X[1] + Mw[2] * X[2] + Mw[3];
+  s.b = Mw[4] * X[0] + Mw[5] * X[1] + Mw[6] * X[2] + Mw[7];
+  float c = Mw[8] * X[0] + Mw[9] * X[1] + Mw[10] * X[2] + Mw[11];
+  s.den = c + 1e-7f;
+  float u = s.a / s.den, v = s.b / s.den;
+  float gx = (u / (float)(W - 1) - 0.5f) * 2.f;
+  float gy = (v / (float)(H - 1) - 0.5f) * 2.f;
+  s.ix = unnorm_ac(gx, W);
+  s.iy = unnorm_ac(gy, H);
+  s.bl = bilinear_taps(s.ix, s.iy, W, H);
+  const int HW = H * W;
+  if (!s.bl.finite) {
+    s.img[0] = s.img[1] = s.img[2] = 2.f;   // NaN -> 2.0 (view_rendering.py:73-75)
+    s.cm = 0.f;
+    return s;
+  }
+  const int base = s.bl.y0 * W + s.bl.x0;
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch) {
+    const float* pl = img + ch * HW;
+    float acc = 0.f;
+    if (s.bl.in[0]) acc += pl[base] * s.bl.w[0];
+    if (s.bl.in[1]) acc += pl[base + 1] * s.bl.w[1];
+    if (s.bl.in[2]) acc += pl[base + W] * s.bl.w[2];
+    if (s.bl.in[3]) acc += pl[base + W + 1] * s.bl.w[3];
+    s.img[ch] = acc;
+  }
+  int ni = nearest_index(s.ix, s.iy, W, H);
+  float mv = ni >= 0 ? msk[ni] : 0.f;
+  bool oob = (gx > 1.f) || (gx < -1.f) || (gy > 1.f) || (gy < -1.f);
+  s.cm = (oob ? 0.f : 1.f) * mv;
+  return s;
+}
+
+template <typename T>
+__device__ __forceinline__ T block_sum(T v, T* lds) {
+  // 256-thread block, returns the total in thread 0
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();
+  if (lane == 0) lds[w] = v;
+  __syncthreads();
+  T t = 0;
+  if (threadIdx.x == 0) t = lds[0] + lds[1] + lds[2] + lds[3];
+  return t;
+}
+
+// ------------------------------------------------------------------------------ stats
+// partial layout [B*N][nblk][n_warp*5 + 2] doubles:
+//   per warp: count(3 per masked pixel), sum w*m, sum r*m, sum w, sum w^2 ; per camera: sum r, sum r^2
+__global__ __launch_bounds__(VBLK) void view_stats_k(vfd_view_desc d, const float* __restrict__ depth,
+                                                     const float* __restrict__ invK, const float* __restrict__ M,
+                                                     const float* __restrict__ mask, double* __restrict__ partial) {
+  __shared__ double lds[4];
+  const Target tg = target_of(d);
+  const int bn = tg.bt, b = tg.b, cam = tg.cam;
+  const int HW = d.H * d.W;
+  const int nblk = gridDim.x;
+  const int stride = d.n_warp * 5 + 2;
+  double* out = partial + ((size_t)bn * nblk + blockIdx.x) * stride;
+  const float* ref = d.color[0] + tg.br * 3 * HW;
+  const float* rmask = mask + tg.br * HW;
+  float X[VPPT][3];
+  int pix[VPPT];
+#pragma unroll
+  for (int k = 0; k < VPPT; ++k) {
+    pix[k] = blockIdx.x * VBLK * VPPT + k * VBLK + threadIdx.x;
+    float ray[3];
+    if (pix[k] < HW) backproject(invK + bn * 16, depth[(size_t)bn * HW + pix[k]], pix[k] % d.W, pix[k] / d.W, X[k], ray);
+  }
+  {
+    double sr = 0.0, sr2 = 0.0;
+#pragma unroll
+    for (int k = 0; k < VPPT; ++k) {
+      if (pix[k] >= HW) continue;
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) {
+        double r = ref[ch * HW + pix[k]];
+        sr += r;
+        sr2 += r * r;
+      }
+    }
+    double t0 = block_sum(sr, lds);
+    if (threadIdx.x == 0) out[d.n_warp * 5] = t0;
+    double t1 = block_sum(sr2, lds);
+    if (threadIdx.x == 0) out[d.n_warp * 5 + 1] = t1;
+  }
+  for (int w = 0; w < d.n_warp; ++w) {
+    const WarpEntry e = warp_entry(d, cam, w);
+    double acc[5] = {0, 0, 0, 0, 0};
+    if (e.src >= 0) {
+      const size_t sbn = (size_t)b * d.N + e.src;
+      const float* img = d.color[e.fslot] + sbn * 3 * HW;
+      const float* msk = mask + sbn * HW;
+      const float* Mw = M + ((size_t)bn * d.n_warp + w) * 12;
+#pragma unroll
+      for (int k = 0; k < VPPT; ++k) {
+        if (pix[k] >= HW) continue;
+        WarpSample s = warp_sample(Mw, X[k], img, msk, d.H, d.W);
+        const bool m = (rmask[pix[k]] * s.cm) != 0.f;
+        const double mf = m ? 1.0 : 0.0;
+        acc[0] += 3.0 * mf;
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+          const double wv = s.img[ch], rv = ref[ch * HW + pix[k]];
+          acc[1] += wv * mf;
+          acc[2] += rv * mf;
+          acc[3] += wv;
+          acc[4] += wv * wv;
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      double t = block_sum(acc[i], lds);
+      if (threadIdx.x == 0) out[w * 5 + i] = t;
+    }
+  }
+}
+
+// coef [B,N,n_warp,4] = (w_mean, w_std, s_mean, s_std); w_std = -1 marks a skipped warp
+// (any sample of the batch without overlap -> warp returned unnormalised, view_rendering.py:50-53)
+__global__ void view_finalize_k(vfd_view_desc d, const double* __restrict__ partial, int nblk,
+                                float* __restrict__ coef) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;   // target slot * n_warp + w
+  if (i >= d.cam_count * d.n_warp) return;
+  const int cam = i / d.n_warp, w = i % d.n_warp;          // cam = target slot here
+  const int stride = d.n_warp * 5 + 2;
+  const double n_all = 3.0 * d.H * d.W;
+  bool skip = false;
+  for (int b = 0; b < d.B; ++b) {
+    const size_t bn = (size_t)b * d.cam_count + cam;
+    double s[5] = {0, 0, 0, 0, 0}, sr = 0, sr2 = 0;
+    for (int k = 0; k < nblk; ++k) {
+      const double* p = partial + (bn * nblk + k) * stride;
+      for (int j = 0; j < 5; ++j) s[j] += p[w * 5 + j];
+      sr += p[d.n_warp * 5];
+      sr2 += p[d.n_warp * 5 + 1];
+    }
+    if (s[0] == 0.0) skip = true;
+    const double mw = s[1] / (s[0] + 1e-8);
+    const double ms = s[2] / (s[0] + 1e-8);
+    double vw = (s[4] - 2.0 * mw * s[3] + n_all * mw * mw) / n_all;
+    double vs = (sr2 - 2.0 * ms * sr + n_all * ms * ms) / n_all;
+    vw = vw < 0.0 ? 0.0 : vw;
+    vs = vs < 0.0 ? 0.0 : vs;
+    float* c = coef + (bn * d.n_warp + w) * 4;
+    c[0] = (float)mw;
+    c[1] = sqrtf((float)vw + 1e-16f);
+    c[2] = (float)ms;
+    c[3] = sqrtf((float)vs + 1e-16f);
+  }
+  if (skip || !d.intensity_align) {
+    for (int b = 0; b < d.B; ++b) coef[(((size_t)b * d.cam_count + cam) * d.n_warp + w) * 4 + 1] = -1.f;
+  }
+}
+
+// ------------------------------------------------------------------------------ apply
+__global__ __launch_bounds__(VBLK) void view_apply_k(vfd_view_desc d, const float* __restrict__ depth,
+                                                     const float* __restrict__ invK, const float* __restrict__ M,
+                                                     const float* __restrict__ mask, const float* __restrict__ coef,
+                                                     float* __restrict__ color, float* __restrict__ cmask,
+                                                     float* __restrict__ ovl, float* __restrict__ omask) {
+  const Target tg = target_of(d);
+  const int bn = tg.bt, b = tg.b, cam = tg.cam;
+  const int HW = d.H * d.W;
+  const int p = blockIdx.x * VBLK + threadIdx.x;
+  if (p >= HW) return;
+  float X[3], ray[3];
+  backproject(invK + bn * 16, depth[(size_t)bn * HW + p], p % d.W, p / d.W, X, ray);
+  const int T = d.n_temporal, F = d.n_overlap;
+  // temporal warps: their own planes
+  for (int w = 0; w < d.n_warp; ++w) {
+    const WarpEntry e = warp_entry(d, cam, w);
+    if (e.src < 0 || e.oslot >= 0) continue;
+    const size_t sbn = (size_t)b * d.N + e.src;
+    const float* cf = coef + ((size_t)bn * d.n_warp + w) * 4;
+    WarpSample s = warp_sample(M + ((size_t)bn * d.n_warp + w) * 12, X, d.color[e.fslot] + sbn * 3 * HW,
+                               mask + sbn * HW, d.H, d.W);
+    float* co = color + (((size_t)bn * T + w) * 3) * HW;
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+      float o = s.img[ch];
+      if (cf[1] >= 0.f) o = ((o - cf[0]) / (cf[1] + 1e-8f) * cf[3] + cf[2]) * s.cm;
+      co[ch * HW + p] = o;
+    }
+    cmask[((size_t)bn * T + w) * HW + p] = s.cm;
+  }
+  // overlap slots: sum over the spatial neighbours in table order
+  for (int slot = 0; slot < F; ++slot) {
+    float acc[3] = {0.f, 0.f, 0.f}, macc = 0.f;
+    for (int w = 0; w < d.n_warp; ++w) {
+      const WarpEntry e = warp_entry(d, cam, w);
+      if (e.src < 0 || e.oslot != slot) continue;
+      const size_t sbn = (size_t)b * d.N + e.src;
+      const float* cf = coef + ((size_t)bn * d.n_warp + w) * 4;
+      WarpSample s = warp_sample(M + ((size_t)bn * d.n_warp + w) * 12, X, d.color[e.fslot] + sbn * 3 * HW,
+                                 mask + sbn * HW, d.H, d.W);
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) {
+        float o = s.img[ch];
+        if (cf[1] >= 0.f) o = ((o - cf[0]) / (cf[1] + 1e-8f) * cf[3] + cf[2]) * s.cm;
+        acc[ch] = acc[ch] + o;
+      }
+      macc = macc + s.cm;
+    }
+    float* oo = ovl + (((size_t)bn * F + slot) * 3) * HW;
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) oo[ch * HW + p] = acc[ch];
+    omask[((size_t)bn * F + slot) * HW + p] = macc;
+  }
+}
+
+// ------------------------------------------------------------------------------ backward
+// partial layout [B*N][nblk][n_warp][12] floats (d (K T)[:3] per warp).
+__global__ __launch_bounds__(VBLK) void view_bwd_k(vfd_view_desc d, const float* __restrict__ depth,
+                                                   const float* __restrict__ invK, const float* __restrict__ M,
+                                                   const float* __restrict__ mask, const float* __restrict__ coef,
+                                                   const float* __restrict__ g_color, const float* __restrict__ g_ovl,
+                                                   float* __restrict__ d_depth, float* __restrict__ partial) {
+  __shared__ float lds[4];
+  const Target tg = target_of(d);
+  const int bn = tg.bt, b = tg.b, cam = tg.cam;
+  const int HW = d.H * d.W;
+  const int nblk = gridDim.x;
+  const int T = d.n_temporal, F = d.n_overlap;
+  float X[VPPT][3], ray[VPPT][3], dd[VPPT];
+  int pix[VPPT];
+#pragma unroll
+  for (int k = 0; k < VPPT; ++k) {
+    pix[k] = blockIdx.x * VBLK * VPPT + k * VBLK + threadIdx.x;
+    dd[k] = 0.f;
+    if (pix[k] < HW) backproject(invK + bn * 16, depth[(size_t)bn * HW + pix[k]], pix[k] % d.W, pix[k] / d.W, X[k], ray[k]);
+  }
+  for (int w = 0; w < d.n_warp; ++w) {
+    const WarpEntry e = warp_entry(d, cam, w);
+    float dM[12];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) dM[i] = 0.f;
+    const float* gsrc = nullptr;
+    if (e.src >= 0) {
+      gsrc = e.oslot < 0 ? (g_color ? g_color + (((size_t)bn * T + w) * 3) * HW : nullptr)
+                         : (g_ovl ? g_ovl + (((size_t)bn * F + e.oslot) * 3) * HW : nullptr);
+    }
+    if (gsrc) {
+      const size_t sbn = (size_t)b * d.N + e.src;
+      const float* img = d.color[e.fslot] + sbn * 3 * HW;
+      const float* Mw = M + ((size_t)bn * d.n_warp + w) * 12;
+      const float* cf = coef + ((size_t)bn * d.n_warp + w) * 4;
+      const bool norm = cf[1] >= 0.f;
+#pragma unroll
+      for (int k = 0; k < VPPT; ++k) {
+        if (pix[k] >= HW) continue;
+        WarpSample s = warp_sample(Mw, X[k], img, mask + sbn * HW, d.H, d.W);
+        if (!s.bl.finite) continue;
+        const int base = s.bl.y0 * d.W + s.bl.x0;
+        const float x0 = floorf(s.ix), y0 = floorf(s.iy);
+        const float x1 = x0 + 1.f, y1 = y0 + 1.f;
+        float gix = 0.f, giy = 0.f;
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+          float g = gsrc[ch * HW + pix[k]];
+          if (norm) g = g * s.cm * cf[3] / (cf[1] + 1e-8f);
+          const float* pl = img + ch * HW;
+          if (s.bl.in[0]) { float v = pl[base]; gix -= v * (y1 - s.iy) * g; giy -= v * (x1 - s.ix) * g; }
+          if (s.bl.in[1]) { float v = pl[base + 1]; gix += v * (y1 - s.iy) * g; giy -= v * (s.ix - x0) * g; }
+          if (s.bl.in[2]) { float v = pl[base + d.W]; gix -= v * (s.iy - y0) * g; giy += v * (x1 - s.ix) * g; }
+          if (s.bl.in[3]) { float v = pl[base + d.W + 1]; gix += v * (s.iy - y0) * g; giy += v * (s.ix - x0) * g; }
+        }
+        // grid_sampler unnormalise -> (u/(W-1) - 0.5)*2 -> a/den
+        const float dgx = gix * ((float)(d.W - 1) / 2.f);
+        const float dgy = giy * ((float)(d.H - 1) / 2.f);
+        const float du = dgx * 2.f / (float)(d.W - 1);
+        const float dv = dgy * 2.f / (float)(d.H - 1);
+        const float da = du / s.den, db = dv / s.den;
+        const float dden = -(du * s.a + dv * s.b) / (s.den * s.den);
+        const float Xh[4] = {X[k][0], X[k][1], X[k][2], 1.f};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          dM[j] += da * Xh[j];
+          dM[4 + j] += db * Xh[j];
+          dM[8 + j] += dden * Xh[j];
+        }
+        float dX0 = da * Mw[0] + db * Mw[4] + dden * Mw[8];
+        float dX1 = da * Mw[1] + db * Mw[5] + dden * Mw[9];
+        float dX2 = da * Mw[2] + db * Mw[6] + dden * Mw[10];
+        dd[k] += dX0 * ray[k][0] + dX1 * ray[k][1] + dX2 * ray[k][2];
+      }
+    }
+    float* out = partial + (((size_t)bn * nblk + blockIdx.x) * d.n_warp + w) * 12;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      float t = block_sum(dM[i], lds);
+      if (threadIdx.x == 0) out[i] = t;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < VPPT; ++k)
+    if (pix[k] < HW) d_depth[(size_t)bn * HW + pix[k]] = dd[k];
+}
+
+__global__ void view_bwd_reduce_k(const float* __restrict__ partial, int nblk, int n_warp, int BN,
+                                  float* __restrict__ dM) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;    // (bn * n_warp + w) * 12 + j
+  if (i >= BN * n_warp * 12) return;
+  const int j = i % 12, w = (i / 12) % n_warp, bn = i / (12 * n_warp);
+  double s = 0.0;
+  for (int k = 0; k < nblk; ++k) s += (double)partial[(((size_t)bn * nblk + k) * n_warp + w) * 12 + j];
+  dM[i] = (float)s;
+}
+
+}  // namespace vfd
+
+// ================================================================================== C ABI
+using namespace vfd;
+
+static int check_view(const vfd_view_desc* d) {
+  VFD_REQUIRE(d != nullptr, "null descriptor");
+  VFD_REQUIRE(d->B > 0 && d->N > 0 && d->H > 1 && d->W > 1, "bad view sizes");
+  VFD_REQUIRE(d->n_warp > 0 && d->n_warp <= 16, "n_warp=%d unsupported", d->n_warp);
+  VFD_REQUIRE(d->n_temporal >= 0 && d->n_temporal <= 3 && d->n_overlap >= 0 && d->n_overlap <= 4, "bad frame counts");
+  VFD_REQUIRE(d->warp_tab != nullptr && d->color[0] != nullptr, "warp table / colour not set");
+  VFD_REQUIRE(d->cam_count > 0 && d->cam_begin >= 0 && d->cam_begin + d->cam_count <= d->N, "bad target range");
+  return VFD_OK;
+}
+
+static unsigned view_red_blocks(const vfd_view_desc* d) { return cdiv((size_t)d->H * d->W, VBLK * VPPT); }
+
+extern "C" {
+
+size_t vfd_view_workspace_bytes(const vfd_view_desc* d) {
+  const size_t nblk = view_red_blocks(d);
+  const size_t stats = (size_t)d->B * d->cam_count * nblk * (d->n_warp * 5 + 2) * sizeof(double);
+  const size_t bwd = (size_t)d->B * d->cam_count * nblk * d->n_warp * 12 * sizeof(float);
+  return stats > bwd ? stats : bwd;
+}
+
+int vfd_view_fwd(const vfd_view_desc* d, const float* depth, const float* invK, const float* M, const float* mask,
+                 float* color, float* cmask, float* ovl, float* omask, float* coef, void* ws, size_t ws_bytes,
+                 void* stream) {
+  int st = check_view(d);
+  if (st) return st;
+  VFD_REQUIRE(ws_bytes >= vfd_view_workspace_bytes(d), "workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const unsigned nblk = view_red_blocks(d);
+  {
+    ProfScope ps(K_VIEW_STATS, s);
+    view_stats_k<<<dim3(nblk, d->B * d->cam_count), VBLK, 0, s>>>(*d, depth, invK, M, mask, (double*)ws);
+  }
+  if ((st = fail_launch("view_stats"))) return st;
+  view_finalize_k<<<cdiv(d->cam_count * d->n_warp, 64), 64, 0, s>>>(*d, (const double*)ws, nblk, coef);
+  if ((st = fail_launch("view_finalize"))) return st;
+  {
+    ProfScope ps(K_VIEW_APPLY, s);
+    view_apply_k<<<dim3(cdiv((size_t)d->H * d->W, VBLK), d->B * d->cam_count), VBLK, 0, s>>>(*d, depth, invK, M, mask, coef,
+                                                                                     color, cmask, ovl, omask);
+  }
+  return fail_launch("view_apply");
+}
+
+int vfd_view_bwd(const vfd_view_desc* d, const float* depth, const float* invK, const float* M, const float* mask,
+                 const float* coef, const float* g_color, const float* g_ovl, float* d_depth, float* d_M, void* ws,
+                 size_t ws_bytes, void* stream) {
+  int st = check_view(d);
+  if (st) return st;
+  VFD_REQUIRE(ws_bytes >= vfd_view_workspace_bytes(d), "workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const unsigned nblk = view_red_blocks(d);
+  {
+    ProfScope ps(K_VIEW_BWD, s);
+    view_bwd_k<<<dim3(nblk, d->B * d->cam_count), VBLK, 0, s>>>(*d, depth, invK, M, mask, coef, g_color, g_ovl, d_depth,
+                                                        (float*)ws);
+  }
+  if ((st = fail_launch("view_bwd"))) return st;
+  const int n = d->B * d->cam_count * d->n_warp * 12;
+  view_bwd_reduce_k<<<cdiv(n, 256), 256, 0, s>>>((const float*)ws, nblk, d->n_warp, d->B * d->cam_count, d_M);
+  return fail_launch("view_bwd_reduce");
+}
+
+}  // extern "C"

@@ -1,0 +1,119 @@
+"""`VFNet` — surround-view volumetric fusion on the gfx950 kernels.
+
+Drop-in for `/root/reference/network/volumetric_fusionnet.py:11-343`: same constructor
+(`VFNet(cfg, feat_in_dim, feat_out_dim, model='depth'|'pose')`), same parameters and
+state-dict keys (`conv_overlap.0.*`, `conv_non_overlap.0.*`, `reduce_dim.{0,3}.*`), same
+`forward(inputs, feats_agg)` contract (depth: dict with 'proj_feat' [B*N, out, h, w];
+pose: BEV feature map).  What changes is how it is computed:
+
+* depth mode: the 1x1 convs' feature columns are folded into the per-camera maps by one
+  batched GEMM (W·bilinear(F) = bilinear(W·F)), K1 gathers 64 folded channels per valid
+  (voxel, camera) pair and applies depth column, bias, LeakyReLU and the count masks in
+  registers — no [B,6,257,V] intermediates;
+* K3 resamples the voxel grid on all camera frustums in one launch and writes the
+  reflect-padded layout `reduce_dim`'s first conv reads (no separate F.pad pass); the six
+  cameras' `reduce_dim` runs as one batched conv;
+* pose mode: K2 writes the camera-mean voxel features straight into the reflect-padded
+  [B, (C+1)Z, Y+2, X+2] map of the stride-2 conv.
+"""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import kernels as KN
+from .layers import conv1d_block, conv2d_block, pack_cam_feat
+
+
+class VFNet(nn.Module):
+    def __init__(self, cfg, feat_in_dim, feat_out_dim, model='depth'):
+        super().__init__()
+        self.cfg = cfg
+        m, t = cfg['model'], cfg['training']
+        self.model = model
+        self.num_cams = int(cfg['data']['num_cams'])
+        self.fusion_level = int(m['fusion_level'])
+        self.feat_in_dim = int(feat_in_dim)
+        self.voxel_size = [int(v) for v in m['voxel_size']]
+        self.proj_d_bins = int(m['proj_d_bins'])
+        self.aug_depth = bool(t.get('aug_depth', False))
+        self.syn_visualize = bool(cfg.get('eval', {}).get('syn_visualize', False))
+        x_dim, y_dim, z_dim = self.voxel_size
+        self.z_dim, self.y_dim, self.x_dim = z_dim, y_dim, x_dim
+        self.n_voxels = x_dim * y_dim * z_dim
+        if model == 'depth':
+            pre = list(m['voxel_pre_dim'])
+            self.v_dim_o = [(feat_in_dim + 1) * 2] + pre
+            self.v_dim_no = [feat_in_dim + 1] + pre
+            self.conv_overlap = conv1d_block(self.v_dim_o[0], self.v_dim_o[1], kernel_size=1)
+            self.conv_non_overlap = conv1d_block(self.v_dim_no[0], self.v_dim_no[1], kernel_size=1)
+            enc_dims, stride = self.proj_d_bins * self.v_dim_o[-1], 1
+            if KN.overlap_group_table(self.num_cams) is None:
+                raise NotImplementedError(f'overlap fusion needs 3 or 6 cameras, got {self.num_cams}')
+        else:
+            enc_dims, stride = (feat_in_dim + 1) * z_dim, 2
+        self.stride = stride
+        self.reduce_dim = nn.Sequential(*conv2d_block(enc_dims, 256, kernel_size=3, stride=stride).children(),
+                                        *conv2d_block(256, feat_out_dim, kernel_size=3, stride=stride).children())
+        self._space = None
+
+    # ------------------------------------------------------------------ helpers
+    def space(self, device):
+        if self._space is None or self._space.device != torch.device(device):
+            self._space = KN.VoxelSpace(self.cfg, device)
+        return self._space
+
+    def _mask_lowres(self, inputs, space):
+        key = ('_vfd_mask_lo', space.h, space.w)
+        if key not in inputs:
+            inputs[key] = KN.mask_lowres(space, inputs['mask'])
+        return inputs[key]
+
+    def _reduce(self, x_padded):
+        """reduce_dim with the first conv reading the kernel's reflect-padded output."""
+        c0, c1 = self.reduce_dim[0], self.reduce_dim[3]
+        x = F.leaky_relu(F.conv2d(x_padded, c0.weight, c0.bias, stride=self.stride), 0.1, inplace=True)
+        return F.leaky_relu(c1(x), 0.1, inplace=True)
+
+    def folded_weights(self):
+        """Per-camera [N, 2Cv, C] feature columns of (W_no, W_o[group]) and the [3, Cv] depth columns."""
+        C = self.feat_in_dim
+        w_no = self.conv_non_overlap[0].weight[:, :, 0]
+        w_o = self.conv_overlap[0].weight[:, :, 0]
+        groups = KN.overlap_group_table(self.num_cams)
+        halves = [w_o[:, :C], w_o[:, C + 1:2 * C + 1]]
+        wf = torch.stack([torch.cat([w_no[:, :C], halves[g]], 0) for g in groups], 0)
+        wz = torch.stack([w_no[:, C], w_o[:, C], w_o[:, 2 * C + 1]], 0)
+        return wf, wz
+
+    # ------------------------------------------------------------------ forward
+    def backproject_depth(self, inputs, feats_agg):
+        """K1: [B,N,C,h,w] -> voxel features [B, V, Cv] (channels-last)."""
+        space = self.space(feats_agg.device)
+        B, N, C, h, w = feats_agg.shape
+        wf, wz = self.folded_weights()
+        P = torch.einsum('bncp,nkc->bnpk', feats_agg.reshape(B, N, C, h * w), wf).contiguous()
+        K = inputs['K', self.fusion_level + 1]
+        return KN.FuseDepth.apply(space, P, self._mask_lowres(inputs, space), K, inputs['extrinsics_inv'],
+                                  wz, self.conv_non_overlap[0].bias, self.conv_overlap[0].bias)
+
+    def project_voxel_into_image(self, voxel_feat, inv_K, extrinsics):
+        """K3 + reduce_dim: voxel features [B,V,Cv] -> [B*N, feat_out, h, w]."""
+        space = self.space(voxel_feat.device)
+        return self._reduce(KN.VoxelProject.apply(space, voxel_feat, inv_K, extrinsics))
+
+    def forward(self, inputs, feats_agg):
+        if self.aug_depth or self.syn_visualize:
+            raise NotImplementedError('depth-synthesis / visualisation branches are out of scope of this build')
+        space = self.space(feats_agg.device)
+        fusion_dict = {('cam', c): {} for c in range(self.num_cams)}
+        if self.model == 'depth':
+            vox = self.backproject_depth(inputs, feats_agg)
+            fusion_dict['proj_feat'] = self.project_voxel_into_image(
+                vox, inputs['inv_K', self.fusion_level + 1], inputs['extrinsics'])
+            return fusion_dict
+        K = inputs['K', self.fusion_level + 1]
+        vox = KN.FusePose.apply(space, feats_agg, self._mask_lowres(inputs, space), K, inputs['extrinsics_inv'])
+        return self._reduce(vox)
+
+
+__all__ = ['VFNet', 'pack_cam_feat']

@@ -1,0 +1,155 @@
+"""Camera geometry and view synthesis (reference `/root/reference/models/geometry/`).
+
+* `vec_to_matrix`, `Pose` — pose assembly (geometry_util.py:8-30, pose.py:7-96); tiny 4x4 math,
+  stays in PyTorch (autograd carries the pose-net gradient).
+* `ViewRendering` — the K4 kernels.  `forward(inputs, outputs, cam, rel_pose_dict)` keeps the
+  reference's per-camera API; `render_all(inputs, outputs, rel_poses)` renders every camera's
+  warps in one fused launch sequence and is what `VFDepthAlgo` uses.
+"""
+import torch
+import torch.nn as nn
+
+from . import kernels as KN
+from .rotation import axis_angle_to_matrix
+
+
+def vec_to_matrix(rot_angle, trans_vec, invert=False):
+    """Axis-angle [B,1,3] + translation [B,1,3] -> [B,4,4]; invert -> R^T @ T(-t)."""
+    b = rot_angle.shape[0]
+    R = torch.eye(4, device=rot_angle.device, dtype=rot_angle.dtype).repeat(b, 1, 1)
+    Tm = torch.eye(4, device=rot_angle.device, dtype=rot_angle.dtype).repeat(b, 1, 1)
+    R[:, :3, :3] = axis_angle_to_matrix(rot_angle).squeeze(1)
+    t = trans_vec.clone().contiguous().view(-1, 3, 1)
+    if invert:
+        R = R.transpose(1, 2)
+        t = -1 * t
+    Tm[:, :3, 3:] = t
+    return torch.matmul(R, Tm) if invert else torch.matmul(Tm, R)
+
+
+class Pose:
+    """Multi-camera pose handling (pose.py:7-96)."""
+
+    def __init__(self, cfg):
+        t, dt = cfg['training'], cfg['data']
+        self.pose_model = cfg['model']['pose_model']
+        self.frame_ids = list(t['frame_ids'])
+        self.num_cams = int(dt['num_cams'])
+        self.rel_cam_list = dt['rel_cam_list']
+        self.spatio, self.spatio_temporal = bool(t['spatio']), bool(t['spatio_temporal'])
+
+    def compute_pose(self, net, inputs):
+        if self.pose_model == 'fusion':
+            pose = self.get_single_pose(net, inputs, None)
+            return self.distribute_pose(pose, inputs['extrinsics'], inputs['extrinsics_inv'])
+        return {('cam', c): self.get_single_pose(net, inputs, c) for c in range(self.num_cams)}
+
+    def get_single_pose(self, net, inputs, cam):
+        out = {}
+        for f in self.frame_ids[1:]:
+            pair = [-1, 0] if f < 0 else [0, 1]
+            axisangle, translation = net(inputs, pair, cam)
+            out[('cam_T_cam', 0, f)] = vec_to_matrix(axisangle[:, 0], translation[:, 0], invert=(f < 0))
+        return out
+
+    def distribute_pose(self, poses, exts, exts_inv):
+        """Canonical (camera 0) motion -> every camera: E_c^-1 E_0 T E_0^-1 E_c."""
+        out = {('cam', c): {} for c in range(self.num_cams)}
+        ref_ext, ref_inv = exts[:, 0], exts_inv[:, 0]
+        for f in self.frame_ids[1:]:
+            T = poses['cam_T_cam', 0, f].float()
+            for c in range(self.num_cams):
+                out[('cam', c)][('cam_T_cam', 0, f)] = exts_inv[:, c] @ ref_ext @ T @ ref_inv @ exts[:, c]
+        return out
+
+    def compute_relative_cam_poses(self, inputs, outputs, cam):
+        ref_ext = inputs['extrinsics'][:, cam]
+        view = outputs[('cam', cam)]
+        rel = {}
+        if self.spatio:
+            for s in self.rel_cam_list[cam]:
+                if s < self.num_cams:
+                    rel[(0, s)] = torch.matmul(inputs['extrinsics_inv'][:, s], ref_ext)
+        if self.spatio_temporal:
+            for f in self.frame_ids[1:]:
+                for s in self.rel_cam_list[cam]:
+                    if s < self.num_cams:
+                        rel[(f, s)] = torch.matmul(rel[(0, s)], view[('cam_T_cam', 0, f)])
+        return rel
+
+
+class ViewRendering(nn.Module):
+    """Warped colour / overlap synthesis on the K4 kernels (view_rendering.py:9-243)."""
+
+    def __init__(self, cfg, rank):
+        super().__init__()
+        t, dt = cfg['training'], cfg['data']
+        self.cfg = cfg
+        self.rank = rank
+        self.scales = list(t['scales'])
+        self.frame_ids = list(t['frame_ids'])
+        self.num_cams = int(dt['num_cams'])
+        self.aug_depth = bool(t.get('aug_depth', False))
+        self._plan = None
+
+    def plan(self, device):
+        if self._plan is None or self._plan.tab.device != torch.device(device):
+            self._plan = KN.ViewPlan(self.cfg, device)
+        return self._plan
+
+    def warp_matrices(self, inputs, outputs, rel_poses, cams):
+        """(K_src @ T)[:3] per (target camera, warp) in the plan's order -> [B, len(cams), n_warp, 3, 4]."""
+        plan = self.plan(inputs[('K', 0)].device)
+        K = inputs[('K', 0)]
+        B = K.shape[0]
+        eye = torch.eye(4, device=K.device, dtype=K.dtype).expand(B, 4, 4)
+        rows = []
+        for c in cams:
+            mats = []
+            for w in range(plan.n_warp):
+                if w >= len(plan.entries[c]):
+                    mats.append(eye[:, :3, :])
+                    continue
+                fslot, src, oslot = plan.entries[c][w]
+                f = self.frame_ids[fslot]
+                T = outputs[('cam', c)][('cam_T_cam', 0, f)] if oslot < 0 else rel_poses[c][(f, src)]
+                mats.append(torch.matmul(K[:, src], T)[:, :3, :])
+            rows.append(torch.stack(mats, 1))
+        return torch.stack(rows, 1)
+
+    def _render(self, inputs, outputs, rel_poses, cam_begin, cam_count, depth_all=None):
+        """Render cameras [cam_begin, +cam_count); returns {scale: (color, cmask, ovl, omask)}."""
+        if self.aug_depth:
+            raise NotImplementedError('depth-synthesis branch (aug_depth) is out of scope of this build')
+        plan = self.plan(inputs[('K', 0)].device)
+        cams = list(range(cam_begin, cam_begin + cam_count))
+        colors = [inputs[('color', f, 0)] for f in self.frame_ids]
+        mask = inputs['mask'][:, :, 0]
+        invK = inputs[('inv_K', 0)][:, cam_begin:cam_begin + cam_count]
+        packed = {}
+        for scale in self.scales:
+            if depth_all is not None and scale in depth_all:
+                depth = depth_all[scale]
+            else:
+                depth = torch.stack([outputs[('cam', c)][('depth', scale)][:, 0] for c in cams], 1)
+            M = self.warp_matrices(inputs, outputs, rel_poses, cams)
+            color, cmask, ovl, omask = KN.ViewSynthesis.apply(plan, cam_begin, depth, invK, M, mask, *colors)
+            for i, c in enumerate(cams):
+                view = outputs[('cam', c)]
+                for ti, f in enumerate(self.frame_ids[1:]):
+                    view[('color', f, scale)] = color[:, i, ti]
+                    view[('color_mask', f, scale)] = cmask[:, i, ti].unsqueeze(1)
+                for fi, f in enumerate(self.frame_ids[:plan.F]):
+                    view[('overlap', f, scale)] = ovl[:, i, fi]
+                    view[('overlap_mask', f, scale)] = omask[:, i, fi].unsqueeze(1)
+            packed[scale] = (color, cmask, ovl, omask)
+        return packed
+
+    def render_all(self, inputs, outputs, rel_poses, depth_all=None):
+        """Every camera in one launch sequence; rel_poses[c] = compute_relative_cam_poses(.., c).
+        depth_all: optional {scale: [B, N, H, W]} depth (avoids re-stacking the per-camera views)."""
+        return self._render(inputs, outputs, rel_poses, 0, self.num_cams, depth_all)
+
+    def forward(self, inputs, outputs, cam, rel_pose_dict):
+        """Reference per-camera API (view_rendering.py:118)."""
+        self._render(inputs, outputs, {cam: rel_pose_dict}, cam, 1)

@@ -1,0 +1,384 @@
+"""Autograd wrappers of the gfx950 hot-path kernels (C ABI in include/vfd_capi.h).
+
+Each op is a `torch.autograd.Function` whose forward and backward are single C-ABI calls on the
+current HIP stream.  Inputs must be fp32 HIP tensors; there is no CPU or ATen fallback — a
+missing library or a non-HIP tensor raises.
+"""
+import ctypes
+
+import torch
+
+from . import _lib as L
+
+
+def _dev(t, what):
+    if not torch.is_tensor(t) or not t.is_cuda:
+        raise RuntimeError(f'{what}: the VFDepth hot path runs only on a HIP device (got '
+                           f'{"non-tensor" if not torch.is_tensor(t) else t.device})')
+    if t.dtype != torch.float32:
+        t = t.float()
+    return t.contiguous()
+
+
+def _ws(nbytes, device):
+    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
+
+
+# =============================================================================================
+# Voxel space (constant grids of VFNet, volumetric_fusionnet.py:15-40, 67-103)
+# =============================================================================================
+def overlap_group_table(n_cams):
+    """Camera -> overlap group (volumetric_fusionnet.py:217-225); None if overlap is undefined."""
+    if n_cams == 6:
+        return [0, 1, 1, 0, 0, 1]
+    if n_cams == 3:
+        return [0, 1, 1]
+    return None
+
+
+class VoxelSpace:
+    """Device-resident voxel axes / depth bins / camera groups + descriptor factory."""
+
+    def __init__(self, cfg, device):
+        m, t = cfg['model'], cfg['training']
+        self.size = [int(v) for v in m['voxel_size']]
+        unit = [float(v) for v in m['voxel_unit_size']]
+        self.str_p = [float(v) for v in m['voxel_str_p']]
+        self.end_p = [self.str_p[i] + unit[i] * (self.size[i] - 1) for i in range(3)]
+        self.X, self.Y, self.Z = self.size
+        self.V = self.X * self.Y * self.Z
+        lvl = int(m['fusion_level'])
+        self.H, self.W = int(t['height']), int(t['width'])
+        self.h, self.w = self.H // 2 ** (lvl + 1), self.W // 2 ** (lvl + 1)
+        self.D = int(m['proj_d_bins'])
+        self.z_scale = float(m['voxel_size'][0])
+        self.n_cams = int(cfg['data']['num_cams'])
+        self.device = torch.device(device)
+        axes = [torch.linspace(self.str_p[i], self.end_p[i], self.size[i]) for i in range(3)]
+        self.axes = [a.to(self.device) for a in axes]
+        self.dbins = torch.linspace(m['proj_d_str'], m['proj_d_end'], self.D).to(self.device)
+        grp = overlap_group_table(self.n_cams) or [0] * self.n_cams
+        self.group = torch.tensor(grp, dtype=torch.int32, device=self.device)
+
+    def desc(self, B, N, C=0, Cv=0, pad_out=1):
+        d = L.VoxelDesc()
+        d.B, d.N, d.C, d.Cv = B, N, C, Cv
+        d.h, d.w, d.H, d.W = self.h, self.w, self.H, self.W
+        d.X, d.Y, d.Z, d.D = self.X, self.Y, self.Z, self.D
+        for i in range(3):
+            d.str[i] = self.str_p[i]
+            d.len[i] = self.end_p[i] - self.str_p[i]
+        d.z_scale = self.z_scale
+        d.pad_out = pad_out
+        d.axis_x, d.axis_y, d.axis_z = (a.data_ptr() for a in self.axes)
+        d.dbins = self.dbins.data_ptr()
+        d.group = self.group.data_ptr()
+        return d
+
+
+def mask_lowres(space, mask):
+    """mask [B,N,1,H,W] -> [B,N,h,w] (bilinear, align_corners=True); no gradient."""
+    lib = L.load()
+    mask = _dev(mask, 'mask')
+    B, N = mask.shape[:2]
+    out = torch.empty(B, N, space.h, space.w, device=mask.device)
+    d = space.desc(B, N)
+    L.check(lib.vfd_mask_downsample(ctypes.byref(d), mask.data_ptr(), out.data_ptr(), L.stream()), 'mask_downsample')
+    return out
+
+
+class FuseDepth(torch.autograd.Function):
+    """K1: P [B,N,hw,2Cv] (folded 1x1-conv maps) -> voxel features [B,V,Cv] (channels-last)."""
+
+    @staticmethod
+    def forward(ctx, space, P, mask_lo, K, Einv, wz, b_no, b_o):
+        lib = L.load()
+        P, mask_lo, K, Einv = (_dev(t, n) for t, n in ((P, 'P'), (mask_lo, 'mask'), (K, 'K'), (Einv, 'Einv')))
+        wz, b_no, b_o = (_dev(t, 'fusion params') for t in (wz, b_no, b_o))
+        B, N, hw, two_cv = P.shape
+        Cv = two_cv // 2
+        if hw != space.h * space.w:
+            raise ValueError(f'feature map {hw} px does not match voxel space {space.h}x{space.w}')
+        vox = torch.empty(B, space.V, Cv, device=P.device)
+        d = space.desc(B, N, Cv=Cv)
+        L.check(lib.vfd_fuse_depth_fwd(ctypes.byref(d), P.data_ptr(), mask_lo.data_ptr(), K.data_ptr(),
+                                       Einv.data_ptr(), wz.data_ptr(), b_no.data_ptr(), b_o.data_ptr(),
+                                       vox.data_ptr(), L.stream()), 'fuse_depth_fwd')
+        ctx.space, ctx.shape = space, (B, N, hw, Cv)
+        ctx.save_for_backward(vox, mask_lo, K, Einv)
+        return vox
+
+    @staticmethod
+    def backward(ctx, g):
+        lib = L.load()
+        vox, mask_lo, K, Einv = ctx.saved_tensors
+        B, N, hw, Cv = ctx.shape
+        g = _dev(g, 'grad')
+        d = ctx.space.desc(B, N, Cv=Cv)
+        dP = torch.empty(B, N, hw, 2 * Cv, device=g.device)
+        dwzb = torch.empty(5, Cv, device=g.device)
+        nbytes = lib.vfd_fuse_depth_bwd_workspace(ctypes.byref(d))
+        ws = _ws(nbytes, g.device)
+        L.check(lib.vfd_fuse_depth_bwd(ctypes.byref(d), g.data_ptr(), vox.data_ptr(), mask_lo.data_ptr(),
+                                       K.data_ptr(), Einv.data_ptr(), dP.data_ptr(), dwzb.data_ptr(),
+                                       ws.data_ptr(), nbytes, L.stream()), 'fuse_depth_bwd')
+        return None, dP, None, None, None, dwzb[:3], dwzb[3], dwzb[4]
+
+
+class FusePose(torch.autograd.Function):
+    """K2: feats [B,N,C,h,w] -> mean voxel features, reflect-padded NCHW [B,(C+1)Z,Y+2,X+2]."""
+
+    @staticmethod
+    def forward(ctx, space, feats, mask_lo, K, Einv):
+        lib = L.load()
+        feats, mask_lo, K, Einv = (_dev(t, n) for t, n in ((feats, 'feats'), (mask_lo, 'mask'), (K, 'K'), (Einv, 'Einv')))
+        B, N, C = feats.shape[:3]
+        out = torch.empty(B, (C + 1) * space.Z, space.Y + 2, space.X + 2, device=feats.device)
+        d = space.desc(B, N, C=C)
+        L.check(lib.vfd_fuse_pose_fwd(ctypes.byref(d), feats.data_ptr(), mask_lo.data_ptr(), K.data_ptr(),
+                                      Einv.data_ptr(), out.data_ptr(), L.stream()), 'fuse_pose_fwd')
+        ctx.space, ctx.shape = space, tuple(feats.shape)
+        ctx.save_for_backward(mask_lo, K, Einv)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        lib = L.load()
+        mask_lo, K, Einv = ctx.saved_tensors
+        B, N, C = ctx.shape[:3]
+        g = _dev(g, 'grad')
+        dfeats = torch.empty(ctx.shape, device=g.device)
+        d = ctx.space.desc(B, N, C=C)
+        L.check(lib.vfd_fuse_pose_bwd(ctypes.byref(d), g.data_ptr(), mask_lo.data_ptr(), K.data_ptr(),
+                                      Einv.data_ptr(), dfeats.data_ptr(), L.stream()), 'fuse_pose_bwd')
+        return None, dfeats, None, None, None
+
+
+class VoxelProject(torch.autograd.Function):
+    """K3: voxel features [B,V,Cv] -> frustum features, reflect-padded [B*N, Cv*D, h+2, w+2]."""
+
+    @staticmethod
+    def forward(ctx, space, vox, invK, E):
+        lib = L.load()
+        vox, invK, E = (_dev(t, n) for t, n in ((vox, 'voxel'), (invK, 'inv_K'), (E, 'extrinsics')))
+        B, V, Cv = vox.shape
+        N = E.shape[1]
+        out = torch.empty(B * N, Cv * space.D, space.h + 2, space.w + 2, device=vox.device)
+        d = space.desc(B, N, Cv=Cv)
+        L.check(lib.vfd_voxel_project_fwd(ctypes.byref(d), vox.data_ptr(), invK.data_ptr(), E.data_ptr(),
+                                          out.data_ptr(), L.stream()), 'voxel_project_fwd')
+        ctx.space, ctx.shape = space, (B, N, V, Cv)
+        ctx.save_for_backward(invK, E)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        lib = L.load()
+        invK, E = ctx.saved_tensors
+        B, N, V, Cv = ctx.shape
+        g = _dev(g, 'grad')
+        dvox = torch.empty(B, V, Cv, device=g.device)
+        d = ctx.space.desc(B, N, Cv=Cv)
+        L.check(lib.vfd_voxel_project_bwd(ctypes.byref(d), g.data_ptr(), invK.data_ptr(), E.data_ptr(),
+                                          dvox.data_ptr(), L.stream()), 'voxel_project_bwd')
+        return None, dvox, None, None
+
+
+# =============================================================================================
+# View synthesis (K4)
+# =============================================================================================
+class ViewPlan:
+    """Warp table of every target camera (view_rendering.py:118-198 enumeration order).
+
+    Warps of camera c: first the temporal warps (frame_ids[1:], source = c), then — when the
+    spatial terms are on — for every frame slot of frame_ids the neighbours rel_cam_list[c] that
+    exist (< num_cams).  Each entry: (frame slot, source camera, overlap slot or -1).
+    """
+
+    def __init__(self, cfg, device):
+        t, dt = cfg['training'], cfg['data']
+        self.frames = list(t['frame_ids'])
+        self.N = int(dt['num_cams'])
+        self.T = len(self.frames) - 1
+        spatial = bool(t['spatio'] or t['spatio_temporal'])
+        if spatial and not (t['spatio'] and t['spatio_temporal']):
+            raise KeyError('the reference needs spatio and spatio_temporal together '
+                           '(pose.py:66-96 builds (0, cam) before the temporal entries)')
+        self.F = len(self.frames) if spatial else 0
+        self.intensity_align = bool(t['intensity_align'])
+        rel = dt['rel_cam_list']
+        self.entries = []
+        for c in range(self.N):
+            ent = [(1 + i, c, -1) for i in range(self.T)]
+            if spatial:
+                for fs in range(len(self.frames)):
+                    for s in rel[c]:
+                        if s < self.N:
+                            ent.append((fs, s, fs))
+            self.entries.append(ent)
+        self.n_warp = max(len(e) for e in self.entries)
+        tab = torch.full((self.N, self.n_warp, 3), -1, dtype=torch.int32)
+        for c, ent in enumerate(self.entries):
+            for w, e in enumerate(ent):
+                tab[c, w] = torch.tensor(e, dtype=torch.int32)
+        self.tab = tab.to(device)
+
+    def desc(self, B, H, W, colors, cam_begin=0, cam_count=None):
+        d = L.ViewDesc()
+        d.B, d.N, d.H, d.W = B, self.N, H, W
+        d.n_warp, d.n_temporal, d.n_overlap = self.n_warp, self.T, self.F
+        d.intensity_align = int(self.intensity_align)
+        d.cam_begin = cam_begin
+        d.cam_count = self.N - cam_begin if cam_count is None else cam_count
+        for i, c in enumerate(colors):
+            d.color[i] = c.data_ptr()
+        d.warp_tab = self.tab.data_ptr()
+        return d
+
+
+class ViewSynthesis(torch.autograd.Function):
+    """K4: every warp of cameras [cam_begin, cam_begin+Nt) -> (color, color_mask, overlap, overlap_mask).
+
+    depth [B,Nt,H,W], invK [B,Nt,4,4], M [B,Nt,n_warp,3,4] = (K_src @ T)[:3], mask [B,N,H,W],
+    colors: one [B,N,3,H,W] tensor per frame slot.  Gradients flow to depth and M.
+    """
+
+    @staticmethod
+    def forward(ctx, plan, cam_begin, depth, invK, M, mask, *colors):
+        lib = L.load()
+        depth, invK, M, mask = (_dev(t, n) for t, n in ((depth, 'depth'), (invK, 'inv_K'), (M, 'KT'), (mask, 'mask')))
+        colors = [_dev(c, 'color') for c in colors]
+        B, Nt, H, W = depth.shape
+        d = plan.desc(B, H, W, colors, cam_begin, Nt)
+        dev = depth.device
+        color = torch.empty(B, Nt, plan.T, 3, H, W, device=dev)
+        cmask = torch.empty(B, Nt, plan.T, H, W, device=dev)
+        ovl = torch.empty(B, Nt, max(plan.F, 1), 3, H, W, device=dev)
+        omask = torch.empty(B, Nt, max(plan.F, 1), H, W, device=dev)
+        coef = torch.empty(B, Nt, plan.n_warp, 4, device=dev)
+        nbytes = lib.vfd_view_workspace_bytes(ctypes.byref(d))
+        ws = _ws(nbytes, dev)
+        L.check(lib.vfd_view_fwd(ctypes.byref(d), depth.data_ptr(), invK.data_ptr(), M.data_ptr(), mask.data_ptr(),
+                                 color.data_ptr(), cmask.data_ptr(), ovl.data_ptr(), omask.data_ptr(),
+                                 coef.data_ptr(), ws.data_ptr(), nbytes, L.stream()), 'view_fwd')
+        ctx.plan, ctx.cam_begin = plan, cam_begin
+        ctx.save_for_backward(depth, invK, M, mask, coef, *colors)
+        ctx.mark_non_differentiable(cmask, omask)
+        if plan.F == 0:
+            ovl, omask = ovl[:, :, :0], omask[:, :, :0]
+        return color, cmask, ovl, omask
+
+    @staticmethod
+    def backward(ctx, g_color, g_cmask, g_ovl, g_omask):
+        lib = L.load()
+        depth, invK, M, mask, coef, *colors = ctx.saved_tensors
+        plan = ctx.plan
+        B, Nt, H, W = depth.shape
+        d = plan.desc(B, H, W, colors, ctx.cam_begin, Nt)
+        g_color = _dev(g_color, 'grad') if g_color is not None else None
+        g_ovl = _dev(g_ovl, 'grad') if (g_ovl is not None and plan.F > 0) else None
+        d_depth = torch.empty_like(depth)
+        d_M = torch.empty_like(M)
+        nbytes = lib.vfd_view_workspace_bytes(ctypes.byref(d))
+        ws = _ws(nbytes, depth.device)
+        L.check(lib.vfd_view_bwd(ctypes.byref(d), depth.data_ptr(), invK.data_ptr(), M.data_ptr(), mask.data_ptr(),
+                                 coef.data_ptr(), L.ptr(g_color), L.ptr(g_ovl), d_depth.data_ptr(), d_M.data_ptr(),
+                                 ws.data_ptr(), nbytes, L.stream()), 'view_bwd')
+        return (None, None, d_depth, None, d_M, None) + (None,) * len(colors)
+
+
+# =============================================================================================
+# Photometric losses (K5) and smoothness
+# =============================================================================================
+class PhotoLoss(torch.autograd.Function):
+    """K5: masked reprojection / spatial / spatio-temporal losses of cameras [cam_begin, +Nt).
+
+    Returns (losses [Nt,3] (differentiable), reproj plane, auto-mask, spatial mask) with planes
+    [B,Nt,H,W].  `noise` ([Nt,B,T,H,W], already scaled like `1e-5 * randn`) or None for the
+    in-kernel counter RNG seeded by `seed`.
+    """
+
+    @staticmethod
+    def forward(ctx, plan, cam_begin, seed, noise, target, ref_mask, color, ovl, omask, *idents):
+        lib = L.load()
+        target, ref_mask, color = (_dev(t, n) for t, n in ((target, 'target'), (ref_mask, 'mask'), (color, 'color')))
+        ovl, omask = _dev(ovl, 'overlap'), _dev(omask, 'overlap mask')
+        idents = [_dev(t, 'identity source') for t in idents]
+        if noise is not None:
+            noise = _dev(noise, 'noise')
+        B, Nt, T, _, H, W = color.shape
+        dev = color.device
+        d = PhotoLoss.desc(plan, B, H, W, cam_begin, Nt, seed, noise is not None, idents)
+        reproj = torch.empty(B, Nt, H, W, device=dev)
+        automask = torch.empty_like(reproj)
+        spatio = torch.zeros_like(reproj) if plan.F > 0 else torch.empty(0, device=dev)
+        sel = torch.empty(B, Nt, H, W, dtype=torch.uint8, device=dev)
+        sums = torch.empty(Nt, 6, dtype=torch.float64, device=dev)
+        losses = torch.empty(Nt, 3, device=dev)
+        nbytes = lib.vfd_photo_workspace_bytes(ctypes.byref(d))
+        ws = _ws(nbytes, dev)
+        L.check(lib.vfd_photo_fwd(ctypes.byref(d), target.data_ptr(), color.data_ptr(), L.ptr(ovl),
+                                  ref_mask.data_ptr(), L.ptr(omask), L.ptr(noise), reproj.data_ptr(),
+                                  automask.data_ptr(), L.ptr(spatio) if plan.F > 0 else None, sel.data_ptr(),
+                                  sums.data_ptr(), losses.data_ptr(), ws.data_ptr(), nbytes, L.stream()), 'photo_fwd')
+        ctx.plan, ctx.cam_begin, ctx.seed, ctx.n_id = plan, cam_begin, seed, len(idents)
+        ctx.save_for_backward(target, ref_mask, color, ovl, omask, sel, sums, *idents)
+        ctx.mark_non_differentiable(reproj, automask, spatio)
+        return losses, reproj, automask, spatio
+
+    @staticmethod
+    def desc(plan, B, H, W, cam_begin, Nt, seed, has_noise, idents):
+        d = L.PhotoDesc()
+        d.B, d.N, d.H, d.W = B, plan.N, H, W
+        d.T, d.F = plan.T, plan.F
+        d.cam_begin, d.cam_count = cam_begin, Nt
+        d.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        d.noise_scale = 1.0 if has_noise else 1e-5
+        for i, t in enumerate(idents):
+            d.ident[i] = t.data_ptr()
+        return d
+
+    @staticmethod
+    def backward(ctx, g_losses, g_reproj, g_auto, g_spatio):
+        lib = L.load()
+        target, ref_mask, color, ovl, omask, sel, sums, *idents = ctx.saved_tensors
+        plan = ctx.plan
+        B, Nt, T, _, H, W = color.shape
+        d = PhotoLoss.desc(plan, B, H, W, ctx.cam_begin, Nt, ctx.seed, True, idents)
+        msum = sums[:, 1::2].float()                                   # M_reproj, M_spatio, M_st
+        gcoef = (_dev(g_losses, 'grad') / (msum + 1e-8)).contiguous()
+        d_color = torch.empty_like(color)
+        d_ovl = torch.empty_like(ovl)
+        L.check(lib.vfd_photo_bwd(ctypes.byref(d), target.data_ptr(), color.data_ptr(), L.ptr(ovl),
+                                  ref_mask.data_ptr(), L.ptr(omask), sel.data_ptr(), gcoef.data_ptr(),
+                                  d_color.data_ptr(), L.ptr(d_ovl), L.stream()), 'photo_bwd')
+        return (None, None, None, None, None, None, d_color, d_ovl if plan.F > 0 else None, None) + (None,) * ctx.n_id
+
+
+class Smoothness(torch.autograd.Function):
+    """Edge-aware smoothness of disp / mean(disp): disp [B,Nt,H,W], color [B,Nt,3,H,W] -> [Nt]."""
+
+    @staticmethod
+    def forward(ctx, disp, color):
+        lib = L.load()
+        disp, color = _dev(disp, 'disp'), _dev(color, 'color')
+        B, Nt, H, W = disp.shape
+        sums = torch.empty(B * Nt, 3, dtype=torch.float64, device=disp.device)
+        loss = torch.empty(Nt, device=disp.device)
+        nbytes = lib.vfd_smooth_workspace_bytes(B, Nt, H, W)
+        ws = _ws(nbytes, disp.device)
+        L.check(lib.vfd_smooth_fwd(B, Nt, H, W, disp.data_ptr(), color.data_ptr(), sums.data_ptr(), loss.data_ptr(),
+                                   ws.data_ptr(), nbytes, L.stream()), 'smooth_fwd')
+        ctx.save_for_backward(disp, color, sums)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        lib = L.load()
+        disp, color, sums = ctx.saved_tensors
+        B, Nt, H, W = disp.shape
+        g = _dev(g, 'grad')
+        d_disp = torch.empty_like(disp)
+        L.check(lib.vfd_smooth_bwd(B, Nt, H, W, disp.data_ptr(), color.data_ptr(), sums.data_ptr(), g.data_ptr(),
+                                   d_disp.data_ptr(), L.stream()), 'smooth_bwd')
+        return d_disp, None

@@ -1,0 +1,147 @@
+"""Depth / pose networks around VFNet (dense layers on MIOpen, fusion on the HIP kernels).
+
+Mirrors `/root/reference/network/{fusion_depthnet,fusion_posenet,mono_depthnet,mono_posenet}.py`
+module-for-module (attribute names and state-dict keys included) so reference checkpoints load.
+"""
+from collections import OrderedDict
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .fusion import VFNet
+from .layers import (MonoDepthDecoder, PoseDecoder, ResnetEncoder, conv2d_block, pack_cam_feat,
+                     unpack_cam_feat, upsample)
+
+
+def _aggregate(encoder, conv1x1, images, lvl, B, N):
+    """Encoder pyramid -> levels >= lvl resized to level lvl, concatenated, 1x1 conv -> [B,N,C,h,w]
+    (fusion_depthnet.py:53-65, fusion_posenet.py:55-67)."""
+    feats = encoder(images)
+    hh, ww = feats[lvl].shape[-2:]
+    stack = [feats[lvl]] + [F.interpolate(f, [hh, ww], mode='bilinear', align_corners=True) for f in feats[lvl + 1:]]
+    agg = conv1x1(torch.cat(stack, 1))
+    return feats, unpack_cam_feat(agg, B, N)
+
+
+class FusionDepthDecoder(nn.Module):
+    """Decoder from the fusion level up to full resolution (fusion_depthnet.py:97-145)."""
+
+    def __init__(self, level_in, num_ch_enc, num_ch_dec, scales=range(2), use_skips=False):
+        super().__init__()
+        self.num_output_channels = 1
+        self.scales = scales
+        self.use_skips = use_skips
+        self.level_in = level_in
+        self.num_ch_enc = num_ch_enc
+        self.num_ch_dec = num_ch_dec
+        self.convs = OrderedDict()
+        for i in range(level_in, -1, -1):
+            cin = num_ch_enc[-1] if i == level_in else num_ch_dec[i + 1]
+            self.convs[('upconv', i, 0)] = conv2d_block(int(cin), num_ch_dec[i], kernel_size=3, nonlin='ELU')
+            cin = num_ch_dec[i] + (num_ch_enc[i - 1] if (use_skips and i > 0) else 0)
+            self.convs[('upconv', i, 1)] = conv2d_block(int(cin), num_ch_dec[i], kernel_size=3, nonlin='ELU')
+        for s in scales:
+            self.convs[('dispconv', s)] = conv2d_block(num_ch_dec[s], self.num_output_channels, 3, nonlin=None)
+        self.decoder = nn.ModuleList(list(self.convs.values()))
+        self.sigmoid = nn.Sigmoid()
+
+    def forward(self, input_features):
+        out = {}
+        x = input_features[-1]
+        for i in range(self.level_in, -1, -1):
+            x = upsample(self.convs[('upconv', i, 0)](x))
+            if self.use_skips and i > 0:
+                x = torch.cat([x, input_features[i - 1]], 1)
+            x = self.convs[('upconv', i, 1)](x)
+            if i in self.scales:
+                out[('disp', i)] = self.sigmoid(self.convs[('dispconv', i)](x))
+        return out
+
+
+class FusedDepthNet(nn.Module):
+    """ResNet encoder -> 1/8 aggregation -> VFNet(depth) -> decoder (fusion_depthnet.py:12-94)."""
+
+    def __init__(self, cfg):
+        super().__init__()
+        m, t = cfg['model'], cfg['training']
+        self.num_cams = int(cfg['data']['num_cams'])
+        self.fusion_level = lvl = int(m['fusion_level'])
+        self.scales = list(t['scales'])
+        self.encoder = ResnetEncoder(int(m['num_layers']), bool(m['weights_init']), 1)
+        del self.encoder.encoder.fc
+        enc_dim = int(sum(self.encoder.num_ch_enc[lvl:]))
+        self.conv1x1 = conv2d_block(enc_dim, int(m['fusion_feat_in_dim']), kernel_size=1, padding_mode='reflect')
+        out_dim = int(self.encoder.num_ch_enc[lvl])
+        self.fusion_net = VFNet(cfg, int(m['fusion_feat_in_dim']), out_dim, model='depth')
+        self.decoder = FusionDepthDecoder(lvl, self.encoder.num_ch_enc[:lvl + 1], [16, 32, 64, 128, 256],
+                                          self.scales, use_skips=bool(m['use_skips']))
+
+    def forward(self, inputs):
+        outputs = {('cam', c): {} for c in range(self.num_cams)}
+        imgs = inputs[('color_aug', 0, 0)]
+        B, N = imgs.shape[:2]
+        feats, agg = _aggregate(self.encoder, self.conv1x1, pack_cam_feat(imgs), self.fusion_level, B, N)
+        fusion = self.fusion_net(inputs, agg)
+        disp = self.decoder(feats[:self.fusion_level] + [fusion['proj_feat']])
+        for k, v in disp.items():
+            v = v.view(B, N, *v.shape[1:])
+            for c in range(N):
+                outputs[('cam', c)][k] = v[:, c]
+        outputs['_packed'] = disp
+        return outputs
+
+
+class FusedPoseNet(nn.Module):
+    """Canonical motion from the fused BEV volume (fusion_posenet.py:10-72)."""
+
+    def __init__(self, cfg):
+        super().__init__()
+        m = cfg['model']
+        self.num_cams = int(cfg['data']['num_cams'])
+        self.fusion_level = lvl = int(m['fusion_level'])
+        self.encoder = ResnetEncoder(int(m['num_layers']), bool(m['weights_init']), 2)
+        del self.encoder.encoder.fc
+        enc_dim = int(sum(self.encoder.num_ch_enc[lvl:]))
+        self.conv1x1 = conv2d_block(enc_dim, int(m['fusion_feat_in_dim']), kernel_size=1, padding_mode='reflect')
+        out_dim = int(self.encoder.num_ch_enc[lvl])
+        self.fusion_net = VFNet(cfg, int(m['fusion_feat_in_dim']), out_dim, model='pose')
+        self.pose_decoder = PoseDecoder(num_ch_enc=[out_dim], num_input_features=1,
+                                        num_frames_to_predict_for=1, stride=2)
+
+    def forward(self, inputs, frame_ids, _cam=None):
+        imgs = torch.cat([inputs[('color_aug', frame_ids[0], 0)], inputs[('color_aug', frame_ids[1], 0)]], 2)
+        B, N = imgs.shape[:2]
+        _, agg = _aggregate(self.encoder, self.conv1x1, pack_cam_feat(imgs), self.fusion_level, B, N)
+        bev = self.fusion_net(inputs, agg)
+        axis_angle, translation = self.pose_decoder([[bev]])
+        return axis_angle, torch.clamp(translation, -4.0, 4.0)
+
+
+class MonoDepthNet(nn.Module):
+    """fsm baseline depth net (mono_depthnet.py:7-25)."""
+
+    def __init__(self, cfg):
+        super().__init__()
+        self.depth_encoder = ResnetEncoder(cfg['model']['num_layers'], cfg['model']['weights_init'], 1)
+        del self.depth_encoder.encoder.fc
+        self.depth_decoder = MonoDepthDecoder(self.depth_encoder.num_ch_enc, cfg['training']['scales'])
+
+    def forward(self, images):
+        return self.depth_decoder(self.depth_encoder(images))
+
+
+class MonoPoseNet(nn.Module):
+    """fsm baseline pose net (mono_posenet.py:8-29)."""
+
+    def __init__(self, cfg):
+        super().__init__()
+        self.pose_encoder = ResnetEncoder(cfg['model']['num_layers'], cfg['model']['weights_init'], num_input_images=2)
+        del self.pose_encoder.encoder.fc
+        self.pose_decoder = PoseDecoder(self.pose_encoder.num_ch_enc, num_input_features=1,
+                                        num_frames_to_predict_for=1)
+
+    def forward(self, inputs, frame_ids, cam):
+        x = torch.cat([inputs['color_aug', f, 0][:, cam] for f in frame_ids], 1)
+        axis_angle, translation = self.pose_decoder([self.pose_encoder(x)])
+        return axis_angle, torch.clamp(translation, -4.0, 4.0)

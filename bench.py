@@ -70,12 +70,16 @@ def algorithmic_bytes(kernel, s):
     V, Z, Y, X, D, T, F = s['V'], s['Z'], s['Y'], s['X'], s['D'], s['T'], s['F']
     pose_out = B * (C + 1) * Z * (Y + 2) * (X + 2)
     proj_out = B * N * Cv * D * (s['h'] + 2) * (s['w'] + 2)
+    h, w = s['h'], s['w']
+    agg_levels = (h // 2) * (w // 2) + (h // 4) * (w // 4)
     planes = {
         'mask_downsample': B * N * (P + p),
+        'fusion_plan': B * N * p + B * V * 8,                     # mask in, ~one 32-B entry per voxel out
+        'aggregate': B * N * C * (2 * p + agg_levels),
         'fuse_depth_fwd': B * N * p * (2 * Cv + 1) + B * V * Cv,
         'fuse_depth_bwd': 2 * B * V * Cv + B * N * p + B * N * p * 2 * Cv,
-        'fuse_pose_fwd': B * N * C * p + B * N * p + pose_out,
-        'fuse_pose_bwd': pose_out + B * N * p + B * N * C * p,
+        'fuse_pose_fwd': B * N * C * p + B * V * 8 + pose_out,
+        'fuse_pose_bwd': pose_out + B * V * 8 + B * N * C * p,
         'voxel_project_fwd': B * V * Cv + proj_out,
         'voxel_project_bwd': proj_out + B * V * Cv,
         'view_stats': B * N * P * (1 + 3 * (T + 1) + 1),

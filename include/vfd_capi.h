@@ -69,14 +69,22 @@ int vfd_fuse_depth_bwd(const vfd_voxel_desc* d, const float* d_vox, const float*
                        const float* mask_lo, const float* K, const float* Einv, float* dP,
                        float* d_wzb, void* workspace, size_t ws_bytes, void* stream);
 
+/* Fusion plan (volumetric_fusionnet.py:132-140, 166-195): for every (batch, camera) the compacted
+ * list of voxels the camera sees (32-B entries: voxel | valid-camera count | in-range taps, corner
+ * pixel, bilinear fractions, camera depth, mean denominator) and its length in counts [B*N].
+ * Built once per step from K (fusion scale), Einv and mask_lo; shared by every pose-mode call. */
+size_t vfd_fusion_plan_bytes(const vfd_voxel_desc* d);
+int vfd_fusion_plan(const vfd_voxel_desc* d, const float* mask_lo, const float* K, const float* Einv,
+                    void* plan, int* counts, void* stream);
+
 /* K2 — pose-mode unprojection, mean over valid cameras (volumetric_fusionnet.py:116-162).
  * feats [B,N,C,h,w] -> out [B, (C+1)*Z, Y(+2), X(+2)] (channel = c*Z + z; +2 when pad_out:
  * reflect-padded for the stride-2 3x3 conv of reduce_dim, :339-342). */
-int vfd_fuse_pose_fwd(const vfd_voxel_desc* d, const float* feats, const float* mask_lo,
-                      const float* K, const float* Einv, float* out, void* stream);
-/* d_out in the forward's output layout -> d_feats [B,N,C,h,w] (zeroed here). */
-int vfd_fuse_pose_bwd(const vfd_voxel_desc* d, const float* d_out, const float* mask_lo,
-                      const float* K, const float* Einv, float* d_feats, void* stream);
+int vfd_fuse_pose_fwd(const vfd_voxel_desc* d, const void* plan, const int* counts, const float* feats,
+                      float* out, void* stream);
+/* d_out in the forward's output layout -> d_feats [B,N,C,h,w] (every element written). */
+int vfd_fuse_pose_bwd(const vfd_voxel_desc* d, const void* plan, const int* counts, const float* d_out,
+                      float* d_feats, void* stream);
 
 /* K3 — voxel -> camera-frustum trilinear resampling (volumetric_fusionnet.py:232-262).
  * vox [B,V,Cv], invK, E [B,N,4,4] (fusion scale) -> out [B*N, Cv*D, h(+2), w(+2)]
@@ -155,13 +163,22 @@ int vfd_smooth_fwd(int B, int N, int H, int W, const float* disp, const float* c
 int vfd_smooth_bwd(int B, int N, int H, int W, const float* disp, const float* color,
                    const double* sums, const float* g, float* d_disp, void* stream);
 
+/* ------------------------------------------------------------------ feature aggregation */
+/* LReLU_0.1(base + sum_k up_align_corners(level_k) + bias) at the fusion level
+ * (network/fusion_depthnet.py:53-63: 1x1 conv of the concatenated, upsampled pyramid, with the
+ * conv applied per level by the caller).  base/out [BN, C, h, w]; levels[k] [BN, C, level_hw[2k],
+ * level_hw[2k+1]] (host array of device pointers), n_levels <= 3; bias [C]. */
+int vfd_aggregate_fwd(int BN, int C, int h, int w, const float* base, int n_levels,
+                      const float* const* levels, const int* level_hw, const float* bias, float* out,
+                      void* stream);
+
 /* ------------------------------------------------------------------ measurement hooks */
 /* Record HIP events around every launch of kernel `kernel_id` (see vfd_kernel_name; -1 = all,
  * -2 = off) on the launching stream.  vfd_prof_read: launches and summed ms of everything
  * recorded; vfd_prof_read_kernels: the same per kernel id into arrays of `count` entries.
  * Both reset the record. */
 #define VFD_PROF_ALL (-1)
-#define VFD_KERNEL_COUNT 14
+#define VFD_KERNEL_COUNT 16
 const char* vfd_kernel_name(int kernel_id);
 int vfd_prof_enable(int kernel_id);
 int vfd_prof_read(int* launches, double* total_ms);

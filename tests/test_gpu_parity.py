@@ -95,8 +95,8 @@ def test_fuse_pose_forward_backward():
     cfg, d, seeds, fx, net, inputs = _fusion_net('pose')
     space = net.space(DEV)
     feats = d['feats'].to(DEV).requires_grad_(True)
-    out = KN.FusePose.apply(space, feats, KN.mask_lowres(space, inputs['mask']), inputs[('K', 3)],
-                            inputs['extrinsics_inv'])
+    plan = KN.FusionPlan(space, KN.mask_lowres(space, inputs['mask']), inputs[('K', 3)], inputs['extrinsics_inv'])
+    out = KN.FusePose.apply(space, plan, feats)
     B, C1 = out.shape[0], feats.shape[2] + 1
     inner = out[:, :, 1:-1, 1:-1].reshape(B, C1, space.Z, space.Y, space.X).reshape(B, C1, -1)
     close(inner, fx['vpose'], 'K2 pose voxels')
@@ -266,26 +266,63 @@ def _step(cfg_fn, fixture, seed_inputs):
     np.testing.assert_array_equal(G.checksum(inputs[('color', 0, 0)]), fx['cs_color'])
     N = cfg['data']['num_cams']
     noise = torch.stack([torch.tensor(fx[f'noise_c{c}']) for c in range(N)]).to(DEV)
-    outputs, losses = algo.process_batch(inputs, 0, noise=noise)
+    outputs, losses = algo.process_batch(inputs, 0, noise=noise)     # moves `inputs` to the device in place
     losses['total_loss'].backward()
-    return cfg, fx, algo, outputs, losses
+    return cfg, fx, algo, inputs, outputs, losses
+
+
+def automask_flips(cfg, inputs, outputs, fx):
+    """Pixels of camera 0 whose auto-mask decision differs from the reference's.
+
+    The auto-mask is argmin([min reprojection, min identity + 1e-5 noise]) — a discontinuous
+    function of the depth.  A decision may legitimately flip where the two candidates are within
+    fp32 resolution of the upstream (conv-network) computation.  Each flip must therefore be
+    explained by a margin |reprojection - identity| below the 1e-4 tolerance (recomputed with
+    the CPU oracle from this run's warped images), and flips must stay rare (<= 1e-3 of pixels).
+    """
+    from oracle import vfd_oracle as O
+    ref_mask_plane = torch.tensor(fx['c0_reproj_mask_0'])
+    got = outputs[('cam', 0)][('reproj_mask', 0)].detach().cpu()
+    ref_bin = (ref_mask_plane != 0)
+    got_bin = (got != 0)
+    flips = ref_bin != got_bin
+    n = int(flips.sum())
+    if n == 0:
+        return flips.to(DEV)
+    assert n <= 1e-3 * flips.numel(), f'{n} auto-mask flips'
+    frames = cfg['training']['frame_ids']
+    target = inputs[('color', 0, 0)][:, 0].cpu()
+    rep = torch.cat([O.photometric(outputs[('cam', 0)][('color', f, 0)].detach().cpu(), target) for f in frames[1:]], 1)
+    idn = torch.cat([O.photometric(inputs[('color', f, 0)][:, 0].cpu(), target) for f in frames[1:]], 1)
+    idn = idn + torch.tensor(fx['noise_c0'])
+    margin = (rep.min(1, keepdim=True).values - idn.min(1, keepdim=True).values).abs()
+    worst = float(margin[flips].max())
+    assert worst <= 1e-4, f'auto-mask flip with margin {worst:.3g} > 1e-4'
+    return flips.to(DEV)
 
 
 @pytest.mark.parametrize('which', ['fusion', 'mono'])
 def test_full_step_against_reference(which):
     cfg_fn, fixture, seed = (G.step_cfg, 'step_small.npz', 5) if which == 'fusion' else (G.mono_cfg, 'mono_small.npz', 6)
-    cfg, fx, algo, outputs, losses = _step(cfg_fn, fixture, seed)
+    cfg, fx, algo, inputs, outputs, losses = _step(cfg_fn, fixture, seed)
     for k in [k for k in fx.files if k.startswith('loss_')]:
         close(losses[k[5:]], fx[k], k)
     for c in range(cfg['data']['num_cams']):
         close(outputs[('cam', c)][('depth', 0)], fx[f'depth_c{c}'], f'depth cam {c}')
         for f in cfg['training']['frame_ids'][1:]:
             close(outputs[('cam', c)][('cam_T_cam', 0, f)], fx[f'cam_T_cam_{f}_c{c}'], f'T{f} cam {c}', atol=1e-5)
+    flips = automask_flips(cfg, inputs, outputs, fx)
     for key in [k for k in fx.files if k.startswith('c0_')]:
         parts = key[3:].split('_')
         name = '_'.join(p for p in parts if not p.lstrip('-').isdigit())
         nums = tuple(int(p) for p in parts if p.lstrip('-').isdigit())
-        close(outputs[('cam', 0)][(name,) + nums], fx[key], key)
+        got = outputs[('cam', 0)][(name,) + nums]
+        if name in ('reproj_loss', 'reproj_mask'):
+            keep = ~flips
+            got, ref = got[keep], torch.tensor(fx[key])[keep.cpu()]
+            close(got, ref, key + ' (outside explained auto-mask flips)')
+        else:
+            close(got, fx[key], key)
     named = {}
     for mname, m in algo.models.items():
         for pname, p in m.named_parameters():

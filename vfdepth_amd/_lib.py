@@ -46,8 +46,10 @@ _SIGS = {
     'vfd_fuse_depth_fwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 8 + [c_void_p]),
     'vfd_fuse_depth_bwd_workspace': (c_size_t, [ctypes.POINTER(VoxelDesc)]),
     'vfd_fuse_depth_bwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 8 + [c_size_t, c_void_p]),
-    'vfd_fuse_pose_fwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 5 + [c_void_p]),
-    'vfd_fuse_pose_bwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 5 + [c_void_p]),
+    'vfd_fusion_plan_bytes': (c_size_t, [ctypes.POINTER(VoxelDesc)]),
+    'vfd_fusion_plan': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 5 + [c_void_p]),
+    'vfd_fuse_pose_fwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 4 + [c_void_p]),
+    'vfd_fuse_pose_bwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 4 + [c_void_p]),
     'vfd_voxel_project_fwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 4 + [c_void_p]),
     'vfd_voxel_project_bwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 4 + [c_void_p]),
     'vfd_view_workspace_bytes': (c_size_t, [ctypes.POINTER(ViewDesc)]),
@@ -56,6 +58,7 @@ _SIGS = {
     'vfd_photo_workspace_bytes': (c_size_t, [ctypes.POINTER(PhotoDesc)]),
     'vfd_photo_fwd': (c_int, [ctypes.POINTER(PhotoDesc)] + [c_fp] * 13 + [c_size_t, c_void_p]),
     'vfd_photo_bwd': (c_int, [ctypes.POINTER(PhotoDesc)] + [c_fp] * 9 + [c_void_p]),
+    'vfd_aggregate_fwd': (c_int, [c_int] * 4 + [c_fp, c_int, ctypes.POINTER(c_fp), ctypes.POINTER(c_int), c_fp, c_fp, c_void_p]),
     'vfd_smooth_workspace_bytes': (c_size_t, [c_int] * 4),
     'vfd_smooth_fwd': (c_int, [c_int] * 4 + [c_fp] * 5 + [c_size_t, c_void_p]),
     'vfd_smooth_bwd': (c_int, [c_int] * 4 + [c_fp] * 5 + [c_void_p]),
@@ -102,7 +105,8 @@ def stream():
 KERNEL_IDS = {
     'mask_downsample': 0, 'fuse_depth_fwd': 1, 'fuse_depth_bwd': 2, 'fuse_pose_fwd': 3, 'fuse_pose_bwd': 4,
     'voxel_project_fwd': 5, 'voxel_project_bwd': 6, 'view_stats': 7, 'view_apply': 8, 'view_bwd': 9,
-    'photo_fwd': 10, 'photo_bwd': 11, 'smooth_fwd': 12, 'smooth_bwd': 13,
+    'photo_fwd': 10, 'photo_bwd': 11, 'smooth_fwd': 12, 'smooth_bwd': 13, 'fusion_plan': 14,
+    'aggregate': 15,
 }
 
 

@@ -320,134 +320,199 @@ __global__ __launch_bounds__(256) void fuse_depth_bwd_k(vfd_voxel_desc d, const 
   }
 }
 
-__global__ void fuse_depth_reduce_k(const float* __restrict__ partial, int n_rows, int n_out,
-                                    float* __restrict__ out) {
-  // out[i] = sum_r partial[r, i]  (fixed order, double accumulation)
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_out) return;
+__global__ __launch_bounds__(256) void fuse_depth_reduce_k(const float* __restrict__ partial, int n_rows, int n_out,
+                                                           float* __restrict__ out) {
+  // out[i] = sum_r partial[r, i]: one block per output, fp64 accumulation, fixed order
+  __shared__ double lds[4];
+  const int i = blockIdx.x;
   double s = 0.0;
-  for (int r = 0; r < n_rows; ++r) s += (double)partial[(size_t)r * n_out + i];
-  out[i] = (float)s;
+  for (int r = threadIdx.x; r < n_rows; r += blockDim.x) s += (double)partial[(size_t)r * n_out + i];
+  s = block_sum_all(s, lds);
+  if (threadIdx.x == 0) out[i] = (float)s;
 }
 
-// ------------------------------------------------------------------------------ K2 forward
-// Lanes are voxels (x fastest) so every channel row of the NCHW output is a coalesced store;
-// the per-camera maps (B*N*C*h*w floats, L2/MALL resident) are gathered per lane.
+// ------------------------------------------------------------------------------ fusion plan
+// One pass over the voxel grid per step: for every (batch, camera) the compacted list of voxels
+// that camera sees, with the tap data every fusion kernel needs.  The geometry depends only on
+// K, E and the mask, so the two pose-net calls (forward and backward) share one plan.
+struct PlanEntry {
+  uint32_t meta;     // voxel index (bits 0-23) | count of valid cameras (24-27) | in-range taps (28-31)
+  int32_t base;      // y0 * w + x0
+  float fx, fy;      // ix - x0, iy - y0 (exact in fp32; weights are rebuilt bit-identically)
+  float z;           // camera-frame depth of the voxel
+  float den;         // count + 1e-7 (pose-mode mean denominator, volumetric_fusionnet.py:162)
+  float pad[2];
+};
+static_assert(sizeof(PlanEntry) == 32, "plan entry must stay 32 B");
 
-__device__ __forceinline__ void pad_sets(int i, int n, bool pad, int* idx, int* cnt) {
-  // positions of source index i in a reflect-padded (+2) axis: {i+1} U {0 if i==1} U {n+1 if i==n-2}
-  if (!pad) { idx[0] = i; *cnt = 1; return; }
-  int c = 0;
-  idx[c++] = i + 1;
-  if (i == 1) idx[c++] = 0;
-  if (i == n - 2) idx[c++] = n + 1;
-  *cnt = c;
+__device__ __forceinline__ void entry_weights(const PlanEntry& e, float* w) {
+  const float ax = 1.f - e.fx, ay = 1.f - e.fy;     // == x1 - ix, y1 - iy exactly
+  w[0] = ax * ay;
+  w[1] = e.fx * ay;
+  w[2] = ax * e.fy;
+  w[3] = e.fx * e.fy;
 }
 
 template <int NC>
-__global__ __launch_bounds__(256) void fuse_pose_fwd_k(vfd_voxel_desc d, const float* __restrict__ feats,
-                                                       const float* __restrict__ mlo,
-                                                       const float* __restrict__ K,
-                                                       const float* __restrict__ Einv,
-                                                       float* __restrict__ out) {
+__global__ __launch_bounds__(256) void fusion_plan_k(vfd_voxel_desc d, const float* __restrict__ mlo,
+                                                     const float* __restrict__ K, const float* __restrict__ Einv,
+                                                     PlanEntry* __restrict__ plan, int* __restrict__ counts) {
+  __shared__ int wave_cnt[4];
+  __shared__ int block_base;
   const int V = d.X * d.Y * d.Z;
   const int b = blockIdx.y;
   const int v = blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= V) return;
   const int hw = d.h * d.w;
-  const int xi = v % d.X, yi = (v / d.X) % d.Y, zi = v / (d.X * d.Y);
-  const float x = d.axis_x[xi], y = d.axis_y[yi], z = d.axis_z[zi];
-  Tap taps[NC];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   bool val[NC];
+  VoxCam g[NC];
   int cnt = 0;
+  if (v < V) {
+    const float x = d.axis_x[v % d.X], y = d.axis_y[(v / d.X) % d.Y], z = d.axis_z[v / (d.X * d.Y)];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int bc = b * NC + c;
+      g[c] = voxel_to_camera(K + bc * 16, Einv + bc * 16, x, y, z, mlo + (size_t)bc * hw, d.h, d.w);
+      val[c] = g[c].valid;
+      cnt += val[c] ? 1 : 0;
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) val[c] = false;
+  }
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
-    const int bc = b * NC + c;
-    VoxCam g = voxel_to_camera(K + bc * 16, Einv + bc * 16, x, y, z, mlo + (size_t)bc * hw, d.h, d.w);
-    val[c] = g.valid;
-    taps[c] = make_tap(c, g, d.h, d.w);
-    cnt += g.valid ? 1 : 0;
+    const unsigned long long m = __ballot(val[c]);
+    const int before = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) wave_cnt[wv] = __popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int tot = wave_cnt[0] + wave_cnt[1] + wave_cnt[2] + wave_cnt[3];
+      block_base = tot ? atomicAdd(counts + b * NC + c, tot) : 0;
+    }
+    __syncthreads();
+    if (val[c]) {
+      int off = block_base + before;
+      for (int k = 0; k < wv; ++k) off += wave_cnt[k];
+      Bilinear bl = bilinear_taps(g[c].ix, g[c].iy, d.w, d.h);
+      PlanEntry e;
+      unsigned in = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) in |= (bl.in[k] ? 1u : 0u) << k;
+      e.meta = (uint32_t)v | ((uint32_t)cnt << 24) | (in << 28);
+      e.base = bl.y0 * d.w + bl.x0;
+      e.fx = g[c].ix - floorf(g[c].ix);
+      e.fy = g[c].iy - floorf(g[c].iy);
+      e.z = g[c].z;
+      e.den = (float)cnt + 1e-7f;
+      e.pad[0] = e.pad[1] = 0.f;
+      plan[((size_t)b * NC + c) * V + off] = e;
+    }
+    __syncthreads();
   }
-  const float denom = (float)cnt + 1e-7f;
+}
+
+// ------------------------------------------------------------------------------ K2 forward
+// Camera-major scatter over the plan: a workgroup owns (batch, camera, G channels, list slice).
+// Feature planes of one camera/channel group stay L2 resident; voxels seen by one camera are
+// stored directly, voxels seen by >= 2 cameras are accumulated with f32 atomics (7.8 % of the
+// grid at config 2).  Output is pre-zeroed (voxels no camera sees stay 0 as in the reference).
+constexpr int POSE_G = 8;
+
+__global__ __launch_bounds__(256) void fuse_pose_fwd_k(vfd_voxel_desc d, const PlanEntry* __restrict__ plan,
+                                                       const int* __restrict__ counts,
+                                                       const float* __restrict__ feats, float* __restrict__ out) {
+  const int V = d.X * d.Y * d.Z;
+  const int bc = blockIdx.z, b = bc / d.N;
+  const int ch0 = blockIdx.y * POSE_G;
+  const int n = counts[bc];
+  const int hw = d.h * d.w;
   const int P = d.pad_out ? 2 : 0;
   const int Yo = d.Y + P, Xo = d.X + P;
-  int rows[3], cols[3], nr, nc;
-  pad_sets(yi, d.Y, d.pad_out, rows, &nr);
-  pad_sets(xi, d.X, d.pad_out, cols, &nc);
+  const PlanEntry* list = plan + (size_t)bc * V;
   float* ob = out + (size_t)b * (d.C + 1) * d.Z * Yo * Xo;
-  for (int ch = 0; ch <= d.C; ++ch) {
-    float acc = 0.f;
-    if (ch < d.C) {
-#pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        if (!val[c]) continue;
-        const float* f = feats + ((size_t)(b * NC + c) * d.C + ch) * hw + taps[c].base;
-        float vv = 0.f;
+  const float* fb = feats + (size_t)bc * d.C * hw;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const PlanEntry e = list[i];
+    const int v = e.meta & 0xFFFFFF, cnt = (e.meta >> 24) & 15;
+    const unsigned in = e.meta >> 28;
+    const int xi = v % d.X, yi = (v / d.X) % d.Y, zi = v / (d.X * d.Y);
+    int rows[3], cols[3], nr, nc;
+    pad_sets(yi, d.Y, d.pad_out, rows, &nr);
+    pad_sets(xi, d.X, d.pad_out, cols, &nc);
+    float w[4];
+    entry_weights(e, w);
+    for (int k = 0; k < POSE_G; ++k) {
+      const int ch = ch0 + k;
+      if (ch > d.C) break;
+      float val;
+      if (ch < d.C) {
+        const float* f = fb + (size_t)ch * hw + e.base;
+        val = 0.f;
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          if (taps[c].in >> q & 1u) vv += f[tap_offset(q, d.w)] * taps[c].w[q];
-        acc += vv;
+          if (in >> q & 1u) val += f[tap_offset(q, d.w)] * w[q];
+      } else {
+        val = e.z / d.z_scale;
       }
-    } else {
-#pragma unroll
-      for (int c = 0; c < NC; ++c)
-        if (val[c]) acc += taps[c].z / d.z_scale;
+      const float o = val / e.den;
+      float* plane = ob + ((size_t)ch * d.Z + zi) * Yo * Xo;
+      for (int a = 0; a < nr; ++a)
+        for (int c2 = 0; c2 < nc; ++c2) {
+          float* dst = plane + rows[a] * Xo + cols[c2];
+          if (cnt == 1) *dst = o;
+          else atomicAdd(dst, o);
+        }
     }
-    const float o = acc / denom;
-    float* plane = ob + ((size_t)ch * d.Z + zi) * Yo * Xo;
-    for (int a = 0; a < nr; ++a)
-      for (int c2 = 0; c2 < nc; ++c2) plane[rows[a] * Xo + cols[c2]] = o;
   }
 }
 
 // ------------------------------------------------------------------------------ K2 backward
-template <int NC>
-__global__ __launch_bounds__(256) void fuse_pose_bwd_k(vfd_voxel_desc d, const float* __restrict__ dout,
-                                                       const float* __restrict__ mlo,
-                                                       const float* __restrict__ K,
-                                                       const float* __restrict__ Einv,
-                                                       float* __restrict__ dfeats) {
+// LDS-privatised gather: a workgroup owns (batch, camera, POSE_BG channels) and accumulates the
+// gradient of those channel planes in LDS with ds_add_f32 while walking the camera's plan; each
+// plane is then written once with coalesced stores (no global atomics, no pre-zeroing).
+__global__ __launch_bounds__(256) void fuse_pose_bwd_k(vfd_voxel_desc d, const PlanEntry* __restrict__ plan,
+                                                       const int* __restrict__ counts,
+                                                       const float* __restrict__ dout, float* __restrict__ dfeats,
+                                                       int G) {
+  extern __shared__ __attribute__((aligned(16))) float acc[];     // [G][h*w]
   const int V = d.X * d.Y * d.Z;
-  const int b = blockIdx.y;
-  const int v = blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= V) return;
+  const int bc = blockIdx.y, b = bc / d.N;
+  const int ch0 = blockIdx.x * G;
   const int hw = d.h * d.w;
-  const int xi = v % d.X, yi = (v / d.X) % d.Y, zi = v / (d.X * d.Y);
-  const float x = d.axis_x[xi], y = d.axis_y[yi], z = d.axis_z[zi];
-  Tap taps[NC];
-  bool val[NC];
-  int cnt = 0;
-#pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    const int bc = b * NC + c;
-    VoxCam g = voxel_to_camera(K + bc * 16, Einv + bc * 16, x, y, z, mlo + (size_t)bc * hw, d.h, d.w);
-    val[c] = g.valid;
-    taps[c] = make_tap(c, g, d.h, d.w);
-    cnt += g.valid ? 1 : 0;
-  }
-  if (cnt == 0) return;
-  const float denom = (float)cnt + 1e-7f;
+  const int gch = min(G, d.C - ch0);
+  for (int i = threadIdx.x; i < G * hw; i += blockDim.x) acc[i] = 0.f;
+  __syncthreads();
+  const int n = counts[bc];
   const int P = d.pad_out ? 2 : 0;
   const int Yo = d.Y + P, Xo = d.X + P;
-  int rows[3], cols[3], nr, nc;
-  pad_sets(yi, d.Y, d.pad_out, rows, &nr);
-  pad_sets(xi, d.X, d.pad_out, cols, &nc);
+  const PlanEntry* list = plan + (size_t)bc * V;
   const float* gb = dout + (size_t)b * (d.C + 1) * d.Z * Yo * Xo;
-  for (int ch = 0; ch < d.C; ++ch) {
-    const float* plane = gb + ((size_t)ch * d.Z + zi) * Yo * Xo;
-    float g = 0.f;
-    for (int a = 0; a < nr; ++a)
-      for (int c2 = 0; c2 < nc; ++c2) g += plane[rows[a] * Xo + cols[c2]];
-    g = g / denom;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      if (!val[c]) continue;
-      float* f = dfeats + ((size_t)(b * NC + c) * d.C + ch) * hw + taps[c].base;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const PlanEntry e = list[i];
+    const int v = e.meta & 0xFFFFFF;
+    const unsigned in = e.meta >> 28;
+    const int xi = v % d.X, yi = (v / d.X) % d.Y, zi = v / (d.X * d.Y);
+    int rows[3], cols[3], nr, nc;
+    pad_sets(yi, d.Y, d.pad_out, rows, &nr);
+    pad_sets(xi, d.X, d.pad_out, cols, &nc);
+    float w[4];
+    entry_weights(e, w);
+    for (int k = 0; k < gch; ++k) {
+      const float* plane = gb + ((size_t)(ch0 + k) * d.Z + zi) * Yo * Xo;
+      float g = 0.f;
+      for (int a = 0; a < nr; ++a)
+        for (int c2 = 0; c2 < nc; ++c2) g += plane[rows[a] * Xo + cols[c2]];
+      g = g / e.den;
+      float* ak = acc + k * hw + e.base;
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        if (taps[c].in >> q & 1u) atomicAdd(f + tap_offset(q, d.w), g * taps[c].w[q]);
+        if (in >> q & 1u) atomicAdd(ak + tap_offset(q, d.w), g * w[q]);
     }
   }
+  __syncthreads();
+  float* db = dfeats + ((size_t)bc * d.C + ch0) * hw;
+  for (int i = threadIdx.x; i < gch * hw; i += blockDim.x) db[i] = acc[i];
 }
 
 // ------------------------------------------------------------------------------ K3 geometry
@@ -706,40 +771,62 @@ int vfd_fuse_depth_bwd(const vfd_voxel_desc* d, const float* d_vox, const float*
   if (st) return st;
   // pad waves beyond V wrote nothing: zero-initialise by reducing only real rows
   const int rows = d->B * (int)cdiv(V, 64);
-  fuse_depth_reduce_k<<<cdiv(5 * d->Cv, 256), 256, 0, s>>>(partial, rows, 5 * d->Cv, d_wzb);
+  fuse_depth_reduce_k<<<5 * d->Cv, 256, 0, s>>>(partial, rows, 5 * d->Cv, d_wzb);
   return fail_launch("fuse_depth_reduce");
 }
 
-int vfd_fuse_pose_fwd(const vfd_voxel_desc* d, const float* feats, const float* mask_lo, const float* K,
-                      const float* Einv, float* out, void* stream) {
+size_t vfd_fusion_plan_bytes(const vfd_voxel_desc* d) {
+  return (size_t)d->B * d->N * d->X * d->Y * d->Z * sizeof(PlanEntry);
+}
+
+int vfd_fusion_plan(const vfd_voxel_desc* d, const float* mask_lo, const float* K, const float* Einv, void* plan,
+                    int* counts, void* stream) {
   int st = check_voxel_desc(d);
   if (st) return st;
+  VFD_REQUIRE((size_t)d->X * d->Y * d->Z < (1u << 24), "voxel grid too large for the plan (%d x %d x %d)", d->X, d->Y, d->Z);
   hipStream_t s = (hipStream_t)stream;
   const int V = d->X * d->Y * d->Z;
-  ProfScope ps(K_FUSE_POSE_FWD, s);
+  (void)hipMemsetAsync(counts, 0, (size_t)d->B * d->N * sizeof(int), s);
   dim3 grid(cdiv(V, 256), d->B);
+  ProfScope ps(K_FUSION_PLAN, s);
   switch (d->N) {
-#define VFD_CASE(n) case n: fuse_pose_fwd_k<n><<<grid, 256, 0, s>>>(*d, feats, mask_lo, K, Einv, out); break;
+#define VFD_CASE(n) case n: fusion_plan_k<n><<<grid, 256, 0, s>>>(*d, mask_lo, K, Einv, (PlanEntry*)plan, counts); break;
     VFD_CASE(1) VFD_CASE(2) VFD_CASE(3) VFD_CASE(4) VFD_CASE(5) VFD_CASE(6) VFD_CASE(7) VFD_CASE(8)
 #undef VFD_CASE
   }
+  return fail_launch("fusion_plan");
+}
+
+int vfd_fuse_pose_fwd(const vfd_voxel_desc* d, const void* plan, const int* counts, const float* feats, float* out,
+                      void* stream) {
+  int st = check_voxel_desc(d);
+  if (st) return st;
+  hipStream_t s = (hipStream_t)stream;
+  const int P = d->pad_out ? 2 : 0;
+  (void)hipMemsetAsync(out, 0, (size_t)d->B * (d->C + 1) * d->Z * (d->Y + P) * (d->X + P) * sizeof(float), s);
+  dim3 grid(16, cdiv(d->C + 1, POSE_G), d->B * d->N);
+  ProfScope ps(K_FUSE_POSE_FWD, s);
+  fuse_pose_fwd_k<<<grid, 256, 0, s>>>(*d, (const PlanEntry*)plan, counts, feats, out);
   return fail_launch("fuse_pose_fwd");
 }
 
-int vfd_fuse_pose_bwd(const vfd_voxel_desc* d, const float* d_out, const float* mask_lo, const float* K,
-                      const float* Einv, float* d_feats, void* stream) {
+static int pose_bwd_group(const vfd_voxel_desc* d) {
+  // channels per workgroup so that G * h * w floats fit in ~64 KB of LDS (2 workgroups / CU)
+  int g = (64 * 1024) / (d->h * d->w * (int)sizeof(float));
+  return g < 1 ? 1 : (g > 8 ? 8 : g);
+}
+
+int vfd_fuse_pose_bwd(const vfd_voxel_desc* d, const void* plan, const int* counts, const float* d_out,
+                      float* d_feats, void* stream) {
   int st = check_voxel_desc(d);
   if (st) return st;
+  const int G = pose_bwd_group(d);
+  const size_t lds = (size_t)G * d->h * d->w * sizeof(float);
+  VFD_REQUIRE(lds <= 160 * 1024, "feature map %dx%d too large for the LDS-privatised backward", d->h, d->w);
   hipStream_t s = (hipStream_t)stream;
-  const int V = d->X * d->Y * d->Z;
-  (void)hipMemsetAsync(d_feats, 0, (size_t)d->B * d->N * d->C * d->h * d->w * sizeof(float), s);
+  dim3 grid(cdiv(d->C, G), d->B * d->N);
   ProfScope ps(K_FUSE_POSE_BWD, s);
-  dim3 grid(cdiv(V, 256), d->B);
-  switch (d->N) {
-#define VFD_CASE(n) case n: fuse_pose_bwd_k<n><<<grid, 256, 0, s>>>(*d, d_out, mask_lo, K, Einv, d_feats); break;
-    VFD_CASE(1) VFD_CASE(2) VFD_CASE(3) VFD_CASE(4) VFD_CASE(5) VFD_CASE(6) VFD_CASE(7) VFD_CASE(8)
-#undef VFD_CASE
-  }
+  fuse_pose_bwd_k<<<grid, 256, lds, s>>>(*d, (const PlanEntry*)plan, counts, d_out, d_feats, G);
   return fail_launch("fuse_pose_bwd");
 }
 

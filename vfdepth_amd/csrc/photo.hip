@@ -173,14 +173,23 @@ __global__ __launch_bounds__(256) void photo_fwd_k(vfd_photo_desc d, const float
   }
 }
 
-__global__ void photo_finalize_k(vfd_photo_desc d, const double* __restrict__ partial, int nblk,
-                                 double* __restrict__ sums, float* __restrict__ losses) {
-  const int cam = blockIdx.x * blockDim.x + threadIdx.x;      // target slot
-  if (cam >= d.cam_count) return;
-  double s[6] = {0, 0, 0, 0, 0, 0};
-  for (int b = 0; b < d.B; ++b)
-    for (int k = 0; k < nblk; ++k)
-      for (int i = 0; i < 6; ++i) s[i] += partial[(((size_t)b * d.cam_count + cam) * nblk + k) * 6 + i];
+__global__ __launch_bounds__(256) void photo_finalize_k(vfd_photo_desc d, const double* __restrict__ partial, int nblk,
+                                                        double* __restrict__ sums, float* __restrict__ losses) {
+  // one block per target camera: fp64 block reductions over batch x tiles
+  __shared__ double lds[4];
+  const int cam = blockIdx.x;
+  const int rows = d.B * nblk;
+  double s[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    double acc = 0.0;
+    for (int r = threadIdx.x; r < rows; r += blockDim.x) {
+      const int b = r / nblk, k = r % nblk;
+      acc += partial[(((size_t)b * d.cam_count + cam) * nblk + k) * 6 + i];
+    }
+    s[i] = block_sum_all(acc, lds);
+  }
+  if (threadIdx.x != 0) return;
   for (int i = 0; i < 6; ++i) sums[cam * 6 + i] = s[i];
   // compute_masked_loss: (loss * mask).sum() / (mask.sum() + 1e-8), fp32 like the reference
   losses[cam * 3 + 0] = (float)s[0] / ((float)s[1] + 1e-8f);
@@ -382,22 +391,28 @@ __global__ __launch_bounds__(SBLK) void smooth_fwd_k(int B, int N, int H, int W,
   }
 }
 
-__global__ void smooth_finalize_k(int B, int N, int H, int W, const double* __restrict__ partial, int nblk,
-                                  double* __restrict__ sums, float* __restrict__ loss) {
-  const int cam = blockIdx.x * blockDim.x + threadIdx.x;
-  if (cam >= N) return;
+__global__ __launch_bounds__(256) void smooth_finalize_k(int B, int N, int H, int W, const double* __restrict__ partial,
+                                                         int nblk, double* __restrict__ sums, float* __restrict__ loss) {
+  // one block per camera
+  __shared__ double lds[4];
+  const int cam = blockIdx.x;
   const double nx = (double)B * H * (W - 1), ny = (double)B * (H - 1) * W;
   double tot = 0.0;
   for (int b = 0; b < B; ++b) {
     const size_t bn = (size_t)b * N + cam;
-    double s[3] = {0, 0, 0};
-    for (int k = 0; k < nblk; ++k)
-      for (int i = 0; i < 3; ++i) s[i] += partial[(bn * nblk + k) * 3 + i];
-    for (int i = 0; i < 3; ++i) sums[bn * 3 + i] = s[i];
-    const double m = (double)(float)(s[0] / ((double)H * W)) + 1e-8;
-    tot += s[1] / (m * nx) + s[2] / (m * ny);
+    double s[3];
+    for (int i = 0; i < 3; ++i) {
+      double acc = 0.0;
+      for (int k = threadIdx.x; k < nblk; k += blockDim.x) acc += partial[(bn * nblk + k) * 3 + i];
+      s[i] = block_sum_all(acc, lds);
+    }
+    if (threadIdx.x == 0) {
+      for (int i = 0; i < 3; ++i) sums[bn * 3 + i] = s[i];
+      const double m = (double)(float)(s[0] / ((double)H * W)) + 1e-8;
+      tot += s[1] / (m * nx) + s[2] / (m * ny);
+    }
   }
-  loss[cam] = (float)tot;
+  if (threadIdx.x == 0) loss[cam] = (float)tot;
 }
 
 __global__ __launch_bounds__(SBLK) void smooth_bwd_k(int B, int N, int H, int W, const float* __restrict__ disp,
@@ -469,7 +484,7 @@ int vfd_photo_fwd(const vfd_photo_desc* d, const float* target, const float* col
                                      sel, (double*)ws);
   }
   if ((st = fail_launch("photo_fwd"))) return st;
-  photo_finalize_k<<<cdiv(d->cam_count, 64), 64, 0, s>>>(*d, (const double*)ws, g.x * g.y, sums, losses);
+  photo_finalize_k<<<d->cam_count, 256, 0, s>>>(*d, (const double*)ws, g.x * g.y, sums, losses);
   return fail_launch("photo_finalize");
 }
 
@@ -504,7 +519,7 @@ int vfd_smooth_fwd(int B, int N, int H, int W, const float* disp, const float* c
   }
   int st = fail_launch("smooth_fwd");
   if (st) return st;
-  smooth_finalize_k<<<cdiv(N, 64), 64, 0, s>>>(B, N, H, W, (const double*)ws, nblk, sums, loss);
+  smooth_finalize_k<<<N, 256, 0, s>>>(B, N, H, W, (const double*)ws, nblk, sums, loss);
   return fail_launch("smooth_finalize");
 }
 

@@ -26,7 +26,7 @@ int fail_launch(const char* what);   // reads hipGetLastError, returns VFD_ELAUN
 enum KernelId {
   K_MASK_DOWN = 0, K_FUSE_DEPTH_FWD, K_FUSE_DEPTH_BWD, K_FUSE_POSE_FWD, K_FUSE_POSE_BWD,
   K_VPROJ_FWD, K_VPROJ_BWD, K_VIEW_STATS, K_VIEW_APPLY, K_VIEW_BWD, K_PHOTO_FWD, K_PHOTO_BWD,
-  K_SMOOTH_FWD, K_SMOOTH_BWD, K_COUNT
+  K_SMOOTH_FWD, K_SMOOTH_BWD, K_FUSION_PLAN, K_AGGREGATE, K_COUNT
 };
 void prof_begin(int id, hipStream_t s);
 void prof_end(int id, hipStream_t s);
@@ -52,6 +52,17 @@ __device__ __forceinline__ int reflect1(int i, int n) {
 }
 
 __device__ __forceinline__ bool finitef(float x) { return __builtin_isfinite(x); }
+
+// Positions of source index i along an axis of length n in a reflect-padded (+1 each side) copy:
+// {i+1}, plus 0 when i == 1 and n+1 when i == n-2 (ReflectionPad(1)).  Without padding: {i}.
+__device__ __forceinline__ void pad_sets(int i, int n, bool pad, int* idx, int* cnt) {
+  if (!pad) { idx[0] = i; *cnt = 1; return; }
+  int c = 0;
+  idx[c++] = i + 1;
+  if (i == 1) idx[c++] = 0;
+  if (i == n - 2) idx[c++] = n + 1;
+  *cnt = c;
+}
 
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
@@ -117,6 +128,16 @@ __device__ __forceinline__ float hash_normal(uint64_t seed, uint64_t idx) {
   float u1 = ((float)(a >> 8) + 1.f) * (1.f / 16777217.f);   // (0, 1]
   float u2 = (float)(b >> 8) * (1.f / 16777216.f);
   return sqrtf(-2.f * logf(u1)) * cosf(6.2831853071795864f * u2);
+}
+
+// Sum over a 256-thread block; the total is returned to every thread.  `lds` holds >= 4 T.
+template <typename T>
+__device__ __forceinline__ T block_sum_all(T v, T* lds) {
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return lds[0] + lds[1] + lds[2] + lds[3];
 }
 
 inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }

@@ -190,37 +190,40 @@ __global__ __launch_bounds__(VBLK) void view_stats_k(vfd_view_desc d, const floa
 
 // coef [B,N,n_warp,4] = (w_mean, w_std, s_mean, s_std); w_std = -1 marks a skipped warp
 // (any sample of the batch without overlap -> warp returned unnormalised, view_rendering.py:50-53)
-__global__ void view_finalize_k(vfd_view_desc d, const double* __restrict__ partial, int nblk,
-                                float* __restrict__ coef) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;   // target slot * n_warp + w
-  if (i >= d.cam_count * d.n_warp) return;
-  const int cam = i / d.n_warp, w = i % d.n_warp;          // cam = target slot here
+__global__ __launch_bounds__(256) void view_finalize_k(vfd_view_desc d, const double* __restrict__ partial, int nblk,
+                                                       float* __restrict__ coef) {
+  // one block per (target slot, warp): fp64 block reductions over the stats partials
+  __shared__ double lds[4];
+  const int cam = blockIdx.x / d.n_warp, w = blockIdx.x % d.n_warp;
   const int stride = d.n_warp * 5 + 2;
   const double n_all = 3.0 * d.H * d.W;
   bool skip = false;
   for (int b = 0; b < d.B; ++b) {
     const size_t bn = (size_t)b * d.cam_count + cam;
-    double s[5] = {0, 0, 0, 0, 0}, sr = 0, sr2 = 0;
-    for (int k = 0; k < nblk; ++k) {
-      const double* p = partial + (bn * nblk + k) * stride;
-      for (int j = 0; j < 5; ++j) s[j] += p[w * 5 + j];
-      sr += p[d.n_warp * 5];
-      sr2 += p[d.n_warp * 5 + 1];
+    double s[7];
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      const int col = j < 5 ? w * 5 + j : d.n_warp * 5 + (j - 5);
+      double acc = 0.0;
+      for (int k = threadIdx.x; k < nblk; k += blockDim.x) acc += partial[(bn * nblk + k) * stride + col];
+      s[j] = block_sum_all(acc, lds);
     }
-    if (s[0] == 0.0) skip = true;
-    const double mw = s[1] / (s[0] + 1e-8);
-    const double ms = s[2] / (s[0] + 1e-8);
-    double vw = (s[4] - 2.0 * mw * s[3] + n_all * mw * mw) / n_all;
-    double vs = (sr2 - 2.0 * ms * sr + n_all * ms * ms) / n_all;
-    vw = vw < 0.0 ? 0.0 : vw;
-    vs = vs < 0.0 ? 0.0 : vs;
-    float* c = coef + (bn * d.n_warp + w) * 4;
-    c[0] = (float)mw;
-    c[1] = sqrtf((float)vw + 1e-16f);
-    c[2] = (float)ms;
-    c[3] = sqrtf((float)vs + 1e-16f);
+    if (threadIdx.x == 0) {
+      if (s[0] == 0.0) skip = true;
+      const double mw = s[1] / (s[0] + 1e-8);
+      const double ms = s[2] / (s[0] + 1e-8);
+      double vw = (s[4] - 2.0 * mw * s[3] + n_all * mw * mw) / n_all;
+      double vs = (s[6] - 2.0 * ms * s[5] + n_all * ms * ms) / n_all;
+      vw = vw < 0.0 ? 0.0 : vw;
+      vs = vs < 0.0 ? 0.0 : vs;
+      float* c = coef + (bn * d.n_warp + w) * 4;
+      c[0] = (float)mw;
+      c[1] = sqrtf((float)vw + 1e-16f);
+      c[2] = (float)ms;
+      c[3] = sqrtf((float)vs + 1e-16f);
+    }
   }
-  if (skip || !d.intensity_align) {
+  if (threadIdx.x == 0 && (skip || !d.intensity_align)) {
     for (int b = 0; b < d.B; ++b) coef[(((size_t)b * d.cam_count + cam) * d.n_warp + w) * 4 + 1] = -1.f;
   }
 }
@@ -369,14 +372,16 @@ __global__ __launch_bounds__(VBLK) void view_bwd_k(vfd_view_desc d, const float*
     if (pix[k] < HW) d_depth[(size_t)bn * HW + pix[k]] = dd[k];
 }
 
-__global__ void view_bwd_reduce_k(const float* __restrict__ partial, int nblk, int n_warp, int BN,
-                                  float* __restrict__ dM) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;    // (bn * n_warp + w) * 12 + j
-  if (i >= BN * n_warp * 12) return;
+__global__ __launch_bounds__(256) void view_bwd_reduce_k(const float* __restrict__ partial, int nblk, int n_warp,
+                                                         float* __restrict__ dM) {
+  // one block per output (bn, w, j): fp64 block reduction over the per-block partials
+  __shared__ double lds[4];
+  const int i = blockIdx.x;
   const int j = i % 12, w = (i / 12) % n_warp, bn = i / (12 * n_warp);
   double s = 0.0;
-  for (int k = 0; k < nblk; ++k) s += (double)partial[(((size_t)bn * nblk + k) * n_warp + w) * 12 + j];
-  dM[i] = (float)s;
+  for (int k = threadIdx.x; k < nblk; k += blockDim.x) s += (double)partial[(((size_t)bn * nblk + k) * n_warp + w) * 12 + j];
+  s = block_sum_all(s, lds);
+  if (threadIdx.x == 0) dM[i] = (float)s;
 }
 
 }  // namespace vfd
@@ -418,7 +423,7 @@ int vfd_view_fwd(const vfd_view_desc* d, const float* depth, const float* invK, 
     view_stats_k<<<dim3(nblk, d->B * d->cam_count), VBLK, 0, s>>>(*d, depth, invK, M, mask, (double*)ws);
   }
   if ((st = fail_launch("view_stats"))) return st;
-  view_finalize_k<<<cdiv(d->cam_count * d->n_warp, 64), 64, 0, s>>>(*d, (const double*)ws, nblk, coef);
+  view_finalize_k<<<d->cam_count * d->n_warp, 256, 0, s>>>(*d, (const double*)ws, nblk, coef);
   if ((st = fail_launch("view_finalize"))) return st;
   {
     ProfScope ps(K_VIEW_APPLY, s);
@@ -443,7 +448,7 @@ int vfd_view_bwd(const vfd_view_desc* d, const float* depth, const float* invK, 
   }
   if ((st = fail_launch("view_bwd"))) return st;
   const int n = d->B * d->cam_count * d->n_warp * 12;
-  view_bwd_reduce_k<<<cdiv(n, 256), 256, 0, s>>>((const float*)ws, nblk, d->n_warp, d->B * d->cam_count, d_M);
+  view_bwd_reduce_k<<<n, 256, 0, s>>>((const float*)ws, nblk, d->n_warp, d_M);
   return fail_launch("view_bwd_reduce");
 }
 

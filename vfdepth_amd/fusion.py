@@ -68,6 +68,13 @@ class VFNet(nn.Module):
             inputs[key] = KN.mask_lowres(space, inputs['mask'])
         return inputs[key]
 
+    def _plan(self, inputs, space):
+        key = ('_vfd_plan', space.h, space.w, tuple(self.voxel_size))
+        if key not in inputs:
+            inputs[key] = KN.FusionPlan(space, self._mask_lowres(inputs, space), inputs['K', self.fusion_level + 1],
+                                        inputs['extrinsics_inv'])
+        return inputs[key]
+
     def _reduce(self, x_padded):
         """reduce_dim with the first conv reading the kernel's reflect-padded output."""
         c0, c1 = self.reduce_dim[0], self.reduce_dim[3]
@@ -111,8 +118,7 @@ class VFNet(nn.Module):
             fusion_dict['proj_feat'] = self.project_voxel_into_image(
                 vox, inputs['inv_K', self.fusion_level + 1], inputs['extrinsics'])
             return fusion_dict
-        K = inputs['K', self.fusion_level + 1]
-        vox = KN.FusePose.apply(space, feats_agg, self._mask_lowres(inputs, space), K, inputs['extrinsics_inv'])
+        vox = KN.FusePose.apply(space, self._plan(inputs, space), feats_agg)
         return self._reduce(vox)
 
 

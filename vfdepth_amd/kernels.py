@@ -125,33 +125,49 @@ class FuseDepth(torch.autograd.Function):
         return None, dP, None, None, None, dwzb[:3], dwzb[3], dwzb[4]
 
 
+class FusionPlan:
+    """Per-(batch, camera) compacted list of visible voxels with their tap data (device buffers).
+
+    Built once per step from K (fusion scale), E^-1 and the 1/8 mask; every pose-mode fusion call
+    of the step (forward and backward) reuses it (the geometry does not depend on features)."""
+
+    def __init__(self, space, mask_lo, K, Einv):
+        lib = L.load()
+        mask_lo, K, Einv = (_dev(t, n) for t, n in ((mask_lo, 'mask'), (K, 'K'), (Einv, 'Einv')))
+        self.B, self.N = mask_lo.shape[:2]
+        d = space.desc(self.B, self.N)
+        nbytes = lib.vfd_fusion_plan_bytes(ctypes.byref(d))
+        self.buf = torch.empty(nbytes, dtype=torch.uint8, device=mask_lo.device)
+        self.counts = torch.empty(self.B * self.N, dtype=torch.int32, device=mask_lo.device)
+        L.check(lib.vfd_fusion_plan(ctypes.byref(d), mask_lo.data_ptr(), K.data_ptr(), Einv.data_ptr(),
+                                    self.buf.data_ptr(), self.counts.data_ptr(), L.stream()), 'fusion_plan')
+
+
 class FusePose(torch.autograd.Function):
     """K2: feats [B,N,C,h,w] -> mean voxel features, reflect-padded NCHW [B,(C+1)Z,Y+2,X+2]."""
 
     @staticmethod
-    def forward(ctx, space, feats, mask_lo, K, Einv):
+    def forward(ctx, space, plan, feats):
         lib = L.load()
-        feats, mask_lo, K, Einv = (_dev(t, n) for t, n in ((feats, 'feats'), (mask_lo, 'mask'), (K, 'K'), (Einv, 'Einv')))
+        feats = _dev(feats, 'feats')
         B, N, C = feats.shape[:3]
         out = torch.empty(B, (C + 1) * space.Z, space.Y + 2, space.X + 2, device=feats.device)
         d = space.desc(B, N, C=C)
-        L.check(lib.vfd_fuse_pose_fwd(ctypes.byref(d), feats.data_ptr(), mask_lo.data_ptr(), K.data_ptr(),
-                                      Einv.data_ptr(), out.data_ptr(), L.stream()), 'fuse_pose_fwd')
-        ctx.space, ctx.shape = space, tuple(feats.shape)
-        ctx.save_for_backward(mask_lo, K, Einv)
+        L.check(lib.vfd_fuse_pose_fwd(ctypes.byref(d), plan.buf.data_ptr(), plan.counts.data_ptr(),
+                                      feats.data_ptr(), out.data_ptr(), L.stream()), 'fuse_pose_fwd')
+        ctx.space, ctx.plan, ctx.shape = space, plan, tuple(feats.shape)
         return out
 
     @staticmethod
     def backward(ctx, g):
         lib = L.load()
-        mask_lo, K, Einv = ctx.saved_tensors
         B, N, C = ctx.shape[:3]
         g = _dev(g, 'grad')
         dfeats = torch.empty(ctx.shape, device=g.device)
         d = ctx.space.desc(B, N, C=C)
-        L.check(lib.vfd_fuse_pose_bwd(ctypes.byref(d), g.data_ptr(), mask_lo.data_ptr(), K.data_ptr(),
-                                      Einv.data_ptr(), dfeats.data_ptr(), L.stream()), 'fuse_pose_bwd')
-        return None, dfeats, None, None, None
+        L.check(lib.vfd_fuse_pose_bwd(ctypes.byref(d), ctx.plan.buf.data_ptr(), ctx.plan.counts.data_ptr(),
+                                      g.data_ptr(), dfeats.data_ptr(), L.stream()), 'fuse_pose_bwd')
+        return None, None, dfeats
 
 
 class VoxelProject(torch.autograd.Function):
@@ -382,3 +398,33 @@ class Smoothness(torch.autograd.Function):
         L.check(lib.vfd_smooth_bwd(B, Nt, H, W, disp.data_ptr(), color.data_ptr(), sums.data_ptr(), g.data_ptr(),
                                    d_disp.data_ptr(), L.stream()), 'smooth_bwd')
         return d_disp, None
+
+
+# =============================================================================================
+# Fusion-level feature aggregation (fusion_depthnet.py:53-63)
+# =============================================================================================
+class AggregateUp(torch.autograd.Function):
+    """LReLU_0.1(base + sum_k up_align_corners(level_k) + bias), NCHW; levels are upsampled to base's size."""
+
+    @staticmethod
+    def forward(ctx, base, bias, *levels):
+        lib = L.load()
+        base, bias = _dev(base, 'aggregate base'), _dev(bias, 'bias')
+        levels = [_dev(t, 'aggregate level') for t in levels]
+        BN, C, h, w = base.shape
+        out = torch.empty_like(base)
+        ptrs = (L.c_fp * max(len(levels), 1))(*[t.data_ptr() for t in levels])
+        hw = (L.c_int * max(2 * len(levels), 1))(*[v for t in levels for v in t.shape[-2:]])
+        L.check(lib.vfd_aggregate_fwd(BN, C, h, w, base.data_ptr(), len(levels), ptrs, hw, bias.data_ptr(),
+                                      out.data_ptr(), L.stream()), 'aggregate_fwd')
+        ctx.save_for_backward(out)
+        ctx.level_shapes = [tuple(t.shape) for t in levels]
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        out, = ctx.saved_tensors
+        d = g * torch.where(out > 0, 1.0, 0.1)
+        grads = [torch.ops.aten.upsample_bilinear2d_backward(d, list(out.shape[-2:]), list(shp), True, None, None)
+                 for shp in ctx.level_shapes]
+        return (d, d.sum((0, 2, 3))) + tuple(grads)

@@ -9,18 +9,25 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import kernels as KN
 from .fusion import VFNet
 from .layers import (MonoDepthDecoder, PoseDecoder, ResnetEncoder, conv2d_block, pack_cam_feat,
                      unpack_cam_feat, upsample)
 
 
 def _aggregate(encoder, conv1x1, images, lvl, B, N):
-    """Encoder pyramid -> levels >= lvl resized to level lvl, concatenated, 1x1 conv -> [B,N,C,h,w]
-    (fusion_depthnet.py:53-65, fusion_posenet.py:55-67)."""
+    """Encoder pyramid -> fusion-level aggregate [B,N,C,h,w] (fusion_depthnet.py:53-65,
+    fusion_posenet.py:55-67): LReLU(conv1x1(cat(f_lvl, up(f_lvl+1), ...))) evaluated as
+    LReLU(W_lvl f_lvl + sum up(W_k f_k) + b) — each slice of the 1x1 conv at its own resolution,
+    one fused upsample-add-bias-LReLU kernel (same parameters, same result up to fp32 rounding)."""
     feats = encoder(images)
-    hh, ww = feats[lvl].shape[-2:]
-    stack = [feats[lvl]] + [F.interpolate(f, [hh, ww], mode='bilinear', align_corners=True) for f in feats[lvl + 1:]]
-    agg = conv1x1(torch.cat(stack, 1))
+    conv = conv1x1[0]
+    off, parts = 0, []
+    for f in feats[lvl:]:
+        c = f.shape[1]
+        parts.append(F.conv2d(f, conv.weight[:, off:off + c]))
+        off += c
+    agg = KN.AggregateUp.apply(parts[0], conv.bias, *parts[1:])
     return feats, unpack_cam_feat(agg, B, N)
 
 

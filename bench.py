@@ -136,6 +136,8 @@ def main():
     ap.add_argument('--batch', type=int, default=None)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--kernel-table', action='store_true', help='print per-kernel times to stderr')
+    ap.add_argument('--conv-autotune', type=int, default=0,
+                    help='1: let MIOpen benchmark conv algorithms per shape (torch.backends.cudnn.benchmark)')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -144,6 +146,7 @@ def main():
     if world > 1:
         dist.init_process_group('nccl', init_method='env://')
     torch.cuda.set_device(local)
+    torch.backends.cudnn.benchmark = bool(args.conv_autotune)
     _lib.load()
 
     from vfdepth_amd.vfdepth import VFDepthAlgo

@@ -136,6 +136,7 @@ def main():
     ap.add_argument('--batch', type=int, default=None)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--kernel-table', action='store_true', help='print per-kernel times to stderr')
+    ap.add_argument('--graph', type=int, default=1, help='1: replay the step as a captured HIP graph (single GPU)')
     ap.add_argument('--conv-autotune', type=int, default=0,
                     help='1: let MIOpen benchmark conv algorithms per shape (torch.backends.cudnn.benchmark)')
     args = ap.parse_args()
@@ -160,22 +161,27 @@ def main():
     algo.set_train()
     batch = synth.make_batch(cfg, seed=1234 + rank, device=f'cuda:{local}')
 
-    def step():
-        algo.optimizer.zero_grad(set_to_none=True)
-        _, losses = algo.process_batch(dict(batch), local)
-        losses['total_loss'].backward()
-        algo.optimizer.step()
-        return losses
+    def eager_step():
+        return algo.train_step(dict(batch))
 
+    use_graph = bool(args.graph) and world == 1
     for i in range(args.warmup):
-        step()
+        eager_step()
         if rank == 0 and i == 0:
             print(f'[bench] first step done ({name})', file=sys.stderr, flush=True)
+    step = eager_step
+    if use_graph:
+        algo.set_optimizer(capturable=True)
+        step = algo.graphed_train_step(batch, warmup=2)
+        for _ in range(2):
+            step()
+        print('[bench] captured the training step as a HIP graph', file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    _lib.prof_enable('all')
+    if not use_graph:
+        _lib.prof_enable('all')
     t0 = time.perf_counter()
     for _ in range(args.steps):
         losses = step()
@@ -184,7 +190,18 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    prof = _lib.prof_read()
+    if use_graph:
+        # per-kernel device times: the same kernels launched eagerly (graph replays carry no host
+        # hooks); kernel durations do not depend on how the launch was issued
+        torch.cuda.synchronize()
+        _lib.prof_enable('all')
+        for _ in range(min(args.steps, 5)):
+            eager_step()
+        torch.cuda.synchronize()
+        prof = _lib.prof_read()
+        prof = {k: (n * args.steps // min(args.steps, 5), t * args.steps / min(args.steps, 5)) for k, (n, t) in prof.items()}
+    else:
+        prof = _lib.prof_read()
     _lib.prof_enable('off')
     if world > 1:
         t = torch.tensor([elapsed], device=f'cuda:{local}')
@@ -231,6 +248,7 @@ def main():
                      'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic, 'alg_bytes_per_launch': alg,
                      'avg_launch_us': avg_s * 1e6, 'launches': n_launch},
         'hot_path_ms_per_step': sum(t for _, t in prof.values()) / args.steps,
+        'execution': 'hip-graph replay of the whole step' if use_graph else 'eager',
         'cpu_baseline': base,
     }
     print(json.dumps(out), flush=True)

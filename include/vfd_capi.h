@@ -132,6 +132,7 @@ typedef struct vfd_photo_desc {
   int32_t cam_begin;     /* target cameras cam_begin .. cam_begin+cam_count-1            */
   int32_t cam_count;
   uint64_t seed;         /* identity-noise RNG seed, used when `noise` is NULL            */
+  const int64_t* step;   /* optional device step counter mixed into the seed (graph replay) */
   float noise_scale;     /* 1e-5 (single_cam_loss.py:8)                                  */
   const float* ident[4]; /* identity sources per temporal frame [B, N, 3, H, W]          */
 } vfd_photo_desc;

@@ -14,4 +14,8 @@ if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after smoke rc=$rc"; exit
 timeout -k 10 600 python bench.py --steps 10 --warmup 3 --kernel-table --no-cpu-baseline > gpurun_out/bench.log 2> gpurun_out/bench.err
 rc=$?
 echo "bench rc=$rc" >> gpurun_out/bench.err
+if [ $rc -ne 0 ]; then exit $rc; fi
+timeout -k 10 600 python bench.py --steps 10 --warmup 3 --graph 0 --no-cpu-baseline > gpurun_out/bench_eager.log 2> gpurun_out/bench_eager.err
+rc=$?
+echo "bench rc=$rc" >> gpurun_out/bench_eager.err
 exit $rc

@@ -1,0 +1,38 @@
+"""Host-side (non-kernel) pieces of the product on CPU: depth metrics, 4x4 inverse, config."""
+import numpy as np
+import torch
+
+from conftest import golden
+
+
+def test_cal_depth_error_matches_reference_fixture():
+    from vfdepth_amd.metrics import cal_depth_error
+    fx = golden('metrics.npz')
+    errs = cal_depth_error(torch.tensor(fx['pred']), torch.tensor(fx['gt']))
+    np.testing.assert_allclose([float(e) for e in errs], fx['errs'], rtol=1e-6, atol=1e-7)
+
+
+def test_compute_depth_losses_median_scaling():
+    """A prediction that is the GT times a constant has zero median-scaled error (logger.py:227-231)
+    and the metric error of that constant."""
+    from vfdepth_amd.metrics import compute_depth_losses
+    g = torch.Generator().manual_seed(0)
+    B, N, H, W = 1, 2, 8, 12
+    gt = 1.0 + 50 * torch.rand(B, N, 1, H, W, generator=g)
+    mask = torch.ones(B, N, 1, H, W)
+    mask[..., :2, :] = 0
+    outputs = {('cam', c): {('depth', 0): gt[:, c] * 0.5} for c in range(N)}
+    metric, median, scales = compute_depth_losses({'depth': gt, 'mask': mask}, outputs, N, 0.0, 200.0,
+                                                  return_scales=True)
+    assert scales == [2.0, 2.0]
+    assert abs(float(metric['abs_rel']) - 0.5) < 1e-6
+    assert float(median['abs_rel']) < 1e-6 and float(median['a1']) == 1.0
+
+
+def test_inverse4x4_matches_lu_inverse():
+    from vfdepth_amd import synth
+    from vfdepth_amd.geometry import inverse4x4
+    E = torch.from_numpy(synth.rig_extrinsics(6)).float()[None].repeat(2, 1, 1, 1)
+    np.testing.assert_allclose(inverse4x4(E).numpy(), torch.inverse(E).numpy(), atol=1e-6)
+    A = torch.randn(64, 4, 4, dtype=torch.float64) + 3 * torch.eye(4, dtype=torch.float64)
+    np.testing.assert_allclose((inverse4x4(A) @ A).numpy(), np.broadcast_to(np.eye(4), (64, 4, 4)), atol=1e-10)

@@ -31,7 +31,7 @@ class ViewDesc(ctypes.Structure):
 
 class PhotoDesc(ctypes.Structure):
     _fields_ = [('B', c_int), ('N', c_int), ('H', c_int), ('W', c_int), ('T', c_int), ('F', c_int),
-                ('cam_begin', c_int), ('cam_count', c_int), ('seed', ctypes.c_uint64),
+                ('cam_begin', c_int), ('cam_count', c_int), ('seed', ctypes.c_uint64), ('step', c_fp),
                 ('noise_scale', c_float), ('ident', c_fp * 4)]
 
 

@@ -132,7 +132,8 @@ __global__ __launch_bounds__(256) void photo_fwd_k(vfd_photo_desc d, const float
     for (int f = 0; f < T; ++f) {
       const size_t ni = (((size_t)tg.slot * d.B + b) * T + f) * HW + p;
       const size_t hi = (((size_t)tg.cam * d.B + b) * T + f) * HW + p;
-      const float nz = noise ? d.noise_scale * noise[ni] : d.noise_scale * hash_normal(d.seed, hi);
+      const uint64_t seed = d.step ? d.seed ^ ((uint64_t)(*d.step) * 0x9E3779B97F4A7C15ULL) : d.seed;
+      const float nz = noise ? d.noise_scale * noise[ni] : d.noise_scale * hash_normal(seed, hi);
       const float v = photo(T + f) + nz;
       if (f == 0 || v < idn) idn = v;
     }

@@ -13,6 +13,32 @@ from . import kernels as KN
 from .rotation import axis_angle_to_matrix
 
 
+def inverse4x4(m):
+    """Batched general 4x4 inverse by cofactors (torch ops only: capturable in a HIP graph, no
+    solver workspace).  Replaces torch.inverse on the extrinsics (vfdepth.py:211); for the rigid
+    camera transforms the two agree to fp32 rounding."""
+    a = m.reshape(-1, 4, 4)
+    a00, a01, a02, a03 = a[:, 0, 0], a[:, 0, 1], a[:, 0, 2], a[:, 0, 3]
+    a10, a11, a12, a13 = a[:, 1, 0], a[:, 1, 1], a[:, 1, 2], a[:, 1, 3]
+    a20, a21, a22, a23 = a[:, 2, 0], a[:, 2, 1], a[:, 2, 2], a[:, 2, 3]
+    a30, a31, a32, a33 = a[:, 3, 0], a[:, 3, 1], a[:, 3, 2], a[:, 3, 3]
+    s0, s1, s2 = a00 * a11 - a10 * a01, a00 * a12 - a10 * a02, a00 * a13 - a10 * a03
+    s3, s4, s5 = a01 * a12 - a11 * a02, a01 * a13 - a11 * a03, a02 * a13 - a12 * a03
+    c5, c4, c3 = a22 * a33 - a32 * a23, a21 * a33 - a31 * a23, a21 * a32 - a31 * a22
+    c2, c1, c0 = a20 * a33 - a30 * a23, a20 * a32 - a30 * a22, a20 * a31 - a30 * a21
+    det = s0 * c5 - s1 * c4 + s2 * c3 + s3 * c2 - s4 * c1 + s5 * c0
+    inv = torch.stack([
+        a11 * c5 - a12 * c4 + a13 * c3, -a01 * c5 + a02 * c4 - a03 * c3,
+        a31 * s5 - a32 * s4 + a33 * s3, -a21 * s5 + a22 * s4 - a23 * s3,
+        -a10 * c5 + a12 * c2 - a13 * c1, a00 * c5 - a02 * c2 + a03 * c1,
+        -a30 * s5 + a32 * s2 - a33 * s1, a20 * s5 - a22 * s2 + a23 * s1,
+        a10 * c4 - a11 * c2 + a13 * c0, -a00 * c4 + a01 * c2 - a03 * c0,
+        a30 * s4 - a31 * s2 + a33 * s0, -a20 * s4 + a21 * s2 - a23 * s0,
+        -a10 * c3 + a11 * c1 - a12 * c0, a00 * c3 - a01 * c1 + a02 * c0,
+        -a30 * s3 + a31 * s1 - a32 * s0, a20 * s3 - a21 * s1 + a22 * s0], -1)
+    return (inv / det.unsqueeze(-1)).reshape(m.shape)
+
+
 def vec_to_matrix(rot_angle, trans_vec, invert=False):
     """Axis-angle [B,1,3] + translation [B,1,3] -> [B,4,4]; invert -> R^T @ T(-t)."""
     b = rot_angle.shape[0]

@@ -316,6 +316,7 @@ class PhotoLoss(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, plan, cam_begin, seed, noise, target, ref_mask, color, ovl, omask, *idents):
+        # seed: int, or (int, int64 device counter) — the counter is read by the kernel (graph replay)
         lib = L.load()
         target, ref_mask, color = (_dev(t, n) for t, n in ((target, 'target'), (ref_mask, 'mask'), (color, 'color')))
         ovl, omask = _dev(ovl, 'overlap'), _dev(omask, 'overlap mask')
@@ -348,6 +349,9 @@ class PhotoLoss(torch.autograd.Function):
         d.B, d.N, d.H, d.W = B, plan.N, H, W
         d.T, d.F = plan.T, plan.F
         d.cam_begin, d.cam_count = cam_begin, Nt
+        if isinstance(seed, tuple):
+            seed, counter = seed
+            d.step = counter.data_ptr()
         d.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         d.noise_scale = 1.0 if has_noise else 1e-5
         for i, t in enumerate(idents):

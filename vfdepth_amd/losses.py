@@ -31,6 +31,7 @@ class SingleCamLoss(nn.Module):
             setattr(self, k, v)
         self._plan = None
         self.noise_mode = 'device'     # 'device': in-kernel counter RNG; 'cpu_global': reference RNG stream
+        self.device_seed = False       # True: seed counter on the device (required under graph capture)
         self._seed = int(torch.initial_seed()) & 0xFFFFFFFF
         self._calls = 0
 
@@ -40,9 +41,17 @@ class SingleCamLoss(nn.Module):
             self._plan = KN.ViewPlan(self.cfg, device)
         return self._plan
 
-    def next_seed(self):
+    def next_seed(self, device=None):
+        """Identity-noise seed of the next call: a host counter in eager mode; with a device the
+        counter lives on the device and is advanced by a kernel (so a captured graph draws fresh
+        noise on every replay)."""
         self._calls += 1
-        return (self._seed << 20) ^ self._calls
+        if device is None:
+            return (self._seed << 20) ^ self._calls
+        if getattr(self, '_counter', None) is None or self._counter.device != torch.device(device):
+            self._counter = torch.zeros(1, dtype=torch.int64, device=device)
+        self._counter += 1
+        return ((self._seed << 20) ^ self._calls, self._counter)
 
     def draw_noise(self, B, H, W, cams, device):
         """Identity-loss noise exactly as the reference draws it: CPU global RNG, camera by camera
@@ -103,7 +112,8 @@ class SingleCamLoss(nn.Module):
             color, _, ovl, omask = packed[scale]
             B, _, _, _, H, W = color.shape
             nz = self._noise(B, H, W, range(N), color.device, noise)
-            losses, reproj, automask, spatio = KN.PhotoLoss.apply(plan, 0, self.next_seed(), nz, target, ref_mask,
+            seed = self.next_seed(color.device) if self.device_seed else self.next_seed()
+            losses, reproj, automask, spatio = KN.PhotoLoss.apply(plan, 0, seed, nz, target, ref_mask,
                                                                   color, ovl, omask, *idents)
             smooth = KN.Smoothness.apply(disp_all[scale], inputs[('color', 0, scale)])
             per_cam = losses[:, 0] + self.disparity_smoothness * smooth / (2 ** scale)

@@ -23,7 +23,7 @@ import torch.optim as optim
 from torch.utils.data import DataLoader
 
 from .config import flatten
-from .geometry import Pose, ViewRendering
+from .geometry import Pose, ViewRendering, inverse4x4
 from .losses import MultiCamLoss, SingleCamLoss
 from .network import FusedDepthNet, FusedPoseNet, MonoDepthNet, MonoPoseNet
 from .synth import SyntheticSurroundDataset
@@ -89,12 +89,12 @@ class VFDepthAlgo:
                                                   batch_size=self.batch_size, shuffle=False, drop_last=True)
         self.num_total_steps = len(ds) // (self.batch_size * self.world_size) * self.num_epochs
 
-    def set_optimizer(self):
+    def set_optimizer(self, capturable=False):
         params = []
         for m in self.models.values():
             params += list(m.parameters())
         fused = self.device.type == 'cuda'
-        self.optimizer = optim.Adam(params, self.learning_rate, fused=fused)
+        self.optimizer = optim.Adam(params, self.learning_rate, fused=fused, capturable=capturable and fused)
         self.lr_scheduler = optim.lr_scheduler.StepLR(self.optimizer, self.scheduler_step_size, 0.1)
 
     # ------------------------------------------------------------------ base-model API
@@ -154,7 +154,7 @@ class VFDepthAlgo:
         return outputs, losses
 
     def estimate_vfdepth(self, inputs):
-        inputs['extrinsics_inv'] = torch.inverse(inputs['extrinsics'])
+        inputs['extrinsics_inv'] = inverse4x4(inputs['extrinsics'])
         outputs = {('cam', c): {} for c in range(self.num_cams)}
         pose_pred = self.predict_pose(inputs)
         depth_feats = self.predict_depth(inputs)
@@ -218,6 +218,59 @@ class VFDepthAlgo:
         losses = dict(logs)
         losses['total_loss'] = total
         return losses
+
+    # ------------------------------------------------------------------ HIP graph
+    def train_step(self, inputs):
+        """zero_grad -> process_batch -> backward -> optimizer step (vfdepth_trainer.py:63-66)."""
+        self.optimizer.zero_grad(set_to_none=True)
+        _, losses = self.process_batch(inputs, self.rank)
+        losses['total_loss'].backward()
+        self.optimizer.step()
+        return losses
+
+    def graphed_train_step(self, batch, warmup=3):
+        """Capture one whole training step (forward, losses, backward, Adam) in a HIP graph.
+
+        Returns step(new_batch=None) -> losses: copies new_batch (same shapes) into the static
+        input buffers and replays the graph: ~2000 kernel launches per step become one.  Needs a
+        capturable optimizer (set_optimizer(capturable=True)); single process (no DDP)."""
+        if self.ddp_enable:
+            raise NotImplementedError('graph capture of the DDP step is not supported; use train_step')
+        static = {k: (v.to(self.device) if torch.is_tensor(v) else v) for k, v in batch.items()}
+        self.losses.device_seed = True
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                self.train_step(dict(static))
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        self.optimizer.zero_grad(set_to_none=True)
+        with torch.cuda.graph(graph):
+            _, static_losses = self.process_batch(dict(static), self.rank)
+            static_losses['total_loss'].backward()
+            self.optimizer.step()
+
+        def step(new_batch=None):
+            if new_batch is not None:
+                for k, v in new_batch.items():
+                    if torch.is_tensor(v) and torch.is_tensor(static.get(k)):
+                        static[k].copy_(v, non_blocking=True)
+            graph.replay()
+            return static_losses
+
+        step.graph = graph
+        return step
+
+    def compute_depth_metrics(self, inputs, outputs, vis_scale=False):
+        """Abs.Rel & co. against inputs['depth'] (Logger.compute_depth_losses, logger.py:193-247)."""
+        from .metrics import compute_depth_losses
+        ev = self.cfg.get('eval', {})
+        lo, hi = float(ev.get('eval_min_depth', 0.0)), float(ev.get('eval_max_depth', 200.0))
+        metric, median, scales = compute_depth_losses(inputs, outputs, self.num_cams, lo, hi, return_scales=True)
+        if vis_scale:
+            print(f'          | median scale = {scales}')
+        return metric, median
 
     def pred_cam_imgs(self, inputs, outputs, cam):
         """Reference per-camera API (vfdepth.py:315-320)."""

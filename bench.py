@@ -15,15 +15,23 @@ per launch ("Roofline accounting").  cpu_baseline: the CPU oracle (or
 restatement of the reference step) timed for a bounded sample on this host's cores (rank 0).
 """
 import argparse
+import faulthandler
 import json
 import os
 import sys
 import time
 
-import torch
-import torch.distributed as dist
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
+# MIOpen's user find/perf database: a committed one (tuned on MI355X) makes conv-solver choice
+# reproducible and skips the per-shape search on a fresh box.  Must be set before MIOpen loads.
+if os.path.isdir(os.path.join(ROOT, 'miopen_db')):
+    os.environ.setdefault('MIOPEN_USER_DB_PATH', os.path.join(ROOT, 'miopen_db'))
+
+import threading  # noqa: E402
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
 sys.path.insert(0, ROOT)
 
 from vfdepth_amd import _lib  # noqa: E402
@@ -136,10 +144,19 @@ def main():
     ap.add_argument('--batch', type=int, default=None)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--kernel-table', action='store_true', help='print per-kernel times to stderr')
-    ap.add_argument('--graph', type=int, default=1, help='1: replay the step as a captured HIP graph (single GPU)')
+    ap.add_argument('--graph', type=int, default=0, help='1: replay the step as a captured HIP graph (single GPU)')
     ap.add_argument('--conv-autotune', type=int, default=0,
                     help='1: let MIOpen benchmark conv algorithms per shape (torch.backends.cudnn.benchmark)')
+    ap.add_argument('--channels-last', type=int, default=0, help='1: NHWC memory format for the dense nets')
     args = ap.parse_args()
+    faulthandler.enable()
+    t_start = time.time()
+    done = threading.Event()
+
+    def heartbeat():     # warm-up (MIOpen kernel compiles / solver search) can be silent for minutes
+        while not done.wait(60):
+            print(f'[bench] ... {time.time() - t_start:.0f} s', file=sys.stderr, flush=True)
+    threading.Thread(target=heartbeat, daemon=True).start()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
@@ -159,23 +176,27 @@ def main():
         inner = m.module if hasattr(m, 'module') else m
         inner.load_state_dict(seeded_state_dict(inner, seed=7))
     algo.set_train()
+    if args.channels_last:
+        for m in algo.models.values():
+            m.to(memory_format=torch.channels_last)
     batch = synth.make_batch(cfg, seed=1234 + rank, device=f'cuda:{local}')
 
     def eager_step():
         return algo.train_step(dict(batch))
 
     use_graph = bool(args.graph) and world == 1
-    for i in range(args.warmup):
-        eager_step()
-        if rank == 0 and i == 0:
-            print(f'[bench] first step done ({name})', file=sys.stderr, flush=True)
     step = eager_step
     if use_graph:
+        # warm-up runs inside graphed_train_step (side stream), then the capture, then replays
         algo.set_optimizer(capturable=True)
-        step = algo.graphed_train_step(batch, warmup=2)
-        for _ in range(2):
-            step()
-        print('[bench] captured the training step as a HIP graph', file=sys.stderr, flush=True)
+        step = algo.graphed_train_step(batch, warmup=max(args.warmup - 1, 1))
+        print(f'[bench] captured the training step as a HIP graph ({name})', file=sys.stderr, flush=True)
+        step()
+    else:
+        for i in range(args.warmup):
+            eager_step()
+            if rank == 0 and i == 0:
+                print(f'[bench] first step done ({name})', file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -251,6 +272,7 @@ def main():
         'execution': 'hip-graph replay of the whole step' if use_graph else 'eager',
         'cpu_baseline': base,
     }
+    done.set()
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

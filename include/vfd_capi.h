@@ -78,10 +78,12 @@ int vfd_fusion_plan(const vfd_voxel_desc* d, const float* mask_lo, const float* 
                     void* plan, int* counts, void* stream);
 
 /* K2 — pose-mode unprojection, mean over valid cameras (volumetric_fusionnet.py:116-162).
- * feats [B,N,C,h,w] -> out [B, (C+1)*Z, Y(+2), X(+2)] (channel = c*Z + z; +2 when pad_out:
- * reflect-padded for the stride-2 3x3 conv of reduce_dim, :339-342). */
-int vfd_fuse_pose_fwd(const vfd_voxel_desc* d, const void* plan, const int* counts, const float* feats,
-                      float* out, void* stream);
+ * Voxel-major gather: every output element is written exactly once (no pre-zeroing, no atomics).
+ * feats_cl [B,N,h*w,C] (channels-last), mask_lo [B*N,h,w], K / Einv [B,N,4,4] (fusion scale)
+ * -> out [B, (C+1)*Z, Y(+2), X(+2)] (channel = c*Z + z; +2 when pad_out: reflect-padded for
+ * the stride-2 3x3 conv of reduce_dim, :339-342). */
+int vfd_fuse_pose_fwd(const vfd_voxel_desc* d, const float* mask_lo, const float* K, const float* Einv,
+                      const float* feats_cl, float* out, void* stream);
 /* d_out in the forward's output layout -> d_feats [B,N,C,h,w] (every element written). */
 int vfd_fuse_pose_bwd(const vfd_voxel_desc* d, const void* plan, const int* counts, const float* d_out,
                       float* d_feats, void* stream);

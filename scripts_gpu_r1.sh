@@ -1,9 +1,10 @@
 #!/bin/bash
-# round-1 GPU session: parity tests, smoke, short bench.  Stops at any GPU fault / abort / timeout.
+# GPU session: parity tests, smoke, short eager bench with kernel table.  Stops at any GPU fault /
+# abort / timeout.
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
-timeout -k 10 900 python -m pytest tests -m gpu -q -rf -v > gpurun_out/gpu_tests.log 2>&1
+timeout -k 10 900 python -m pytest tests -m gpu -q -rf > gpurun_out/gpu_tests.log 2>&1
 rc=$?
 echo "pytest rc=$rc" >> gpurun_out/gpu_tests.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after pytest rc=$rc"; exit $rc; fi
@@ -14,8 +15,4 @@ if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after smoke rc=$rc"; exit
 timeout -k 10 600 python bench.py --steps 10 --warmup 3 --kernel-table --no-cpu-baseline > gpurun_out/bench.log 2> gpurun_out/bench.err
 rc=$?
 echo "bench rc=$rc" >> gpurun_out/bench.err
-if [ $rc -ne 0 ]; then exit $rc; fi
-timeout -k 10 600 python bench.py --steps 10 --warmup 3 --graph 0 --no-cpu-baseline > gpurun_out/bench_eager.log 2> gpurun_out/bench_eager.err
-rc=$?
-echo "bench rc=$rc" >> gpurun_out/bench_eager.err
 exit $rc

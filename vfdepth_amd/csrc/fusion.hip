@@ -413,72 +413,137 @@ __global__ __launch_bounds__(256) void fusion_plan_k(vfd_voxel_desc d, const flo
 }
 
 // ------------------------------------------------------------------------------ K2 forward
-// Camera-major scatter over the plan: a workgroup owns (batch, camera, G channels, list slice).
-// Feature planes of one camera/channel group stay L2 resident; voxels seen by one camera are
-// stored directly, voxels seen by >= 2 cameras are accumulated with f32 atomics (7.8 % of the
-// grid at config 2).  Output is pre-zeroed (voxels no camera sees stay 0 as in the reference).
-constexpr int POSE_G = 8;
+// Voxel-major gather (volumetric_fusionnet.py:116-162, pose branch).  A workgroup owns POSE_TV
+// consecutive voxels: (1) one thread per voxel projects it into every camera (same arithmetic as
+// the plan / the reference), (2) each wave takes voxels in turn with lanes = channels and reads
+// the four bilinear taps of every valid camera from the channels-last feature map (one
+// contiguous C-float row per tap), sums the cameras in order and divides by (count + 1e-7),
+// staging the [C+1][POSE_TV] result in LDS, (3) the tile is written to the reflect-padded NCHW
+// output with voxel-contiguous stores.  Every output element is written once: no memset, no
+// atomics, and the per-voxel camera sum runs in the reference's camera order.
+constexpr int POSE_TV = 32;
+constexpr int POSE_MAXC = 256;      // channels held per lane: ceil(C / 64) <= 4
 
-__global__ __launch_bounds__(256) void fuse_pose_fwd_k(vfd_voxel_desc d, const PlanEntry* __restrict__ plan,
-                                                       const int* __restrict__ counts,
+template <int NC>
+__global__ __launch_bounds__(256) void fuse_pose_fwd_k(vfd_voxel_desc d, const float* __restrict__ mlo,
+                                                       const float* __restrict__ K, const float* __restrict__ Einv,
                                                        const float* __restrict__ feats, float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) float tile[];      // [C+1][POSE_TV+1]
+  __shared__ int s_base[POSE_TV][NC];
+  __shared__ float s_w[POSE_TV][NC][4];
+  __shared__ int s_cam[POSE_TV][NC];
+  __shared__ unsigned s_in[POSE_TV][NC];
+  __shared__ int s_cnt[POSE_TV];
+  __shared__ float s_den[POSE_TV];
   const int V = d.X * d.Y * d.Z;
-  const int bc = blockIdx.z, b = bc / d.N;
-  const int ch0 = blockIdx.y * POSE_G;
-  const int n = counts[bc];
+  const int b = blockIdx.y;
+  const int v0 = blockIdx.x * POSE_TV;
   const int hw = d.h * d.w;
+  const int C = d.C;
+  const int TS = POSE_TV + 1;
+  if (threadIdx.x < POSE_TV) {
+    const int t = threadIdx.x, v = v0 + t;
+    int cnt = 0;
+    float zsum = 0.f;
+    if (v < V) {
+      const float x = d.axis_x[v % d.X], y = d.axis_y[(v / d.X) % d.Y], z = d.axis_z[v / (d.X * d.Y)];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int bc = b * NC + c;
+        const VoxCam g = voxel_to_camera(K + bc * 16, Einv + bc * 16, x, y, z, mlo + (size_t)bc * hw, d.h, d.w);
+        if (g.valid) {
+          const Tap tp = make_tap(c, g, d.h, d.w);
+          s_cam[t][cnt] = c;
+          s_base[t][cnt] = tp.base;
+          s_in[t][cnt] = tp.in;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) s_w[t][cnt][q] = tp.w[q];
+          zsum += g.z / d.z_scale;
+          ++cnt;
+        }
+      }
+    }
+    s_cnt[t] = cnt;
+    s_den[t] = (float)cnt + 1e-7f;
+    tile[C * TS + t] = zsum / ((float)cnt + 1e-7f);
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const float* fb = feats + (size_t)b * NC * hw * C;
+  for (int t = wv; t < POSE_TV; t += 4) {
+    const int cnt = s_cnt[t];
+    float acc[POSE_MAXC / 64];
+#pragma unroll
+    for (int k = 0; k < POSE_MAXC / 64; ++k) acc[k] = 0.f;
+    for (int j = 0; j < cnt; ++j) {
+      const int cam = s_cam[t][j], base = s_base[t][j];
+      const float* fc = fb + (size_t)cam * hw * C;
+      float val[POSE_MAXC / 64];
+#pragma unroll
+      for (int k = 0; k < POSE_MAXC / 64; ++k) val[k] = 0.f;
+      const unsigned in = s_in[t][j];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (!(in >> q & 1u)) continue;          // out-of-range corner: zeros padding
+        const float wq = s_w[t][j][q];
+        const float* row = fc + (size_t)(base + tap_offset(q, d.w)) * C;
+#pragma unroll
+        for (int k = 0; k < POSE_MAXC / 64; ++k) {
+          const int ch = lane + 64 * k;
+          if (ch < C) val[k] += row[ch] * wq;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < POSE_MAXC / 64; ++k) acc[k] += val[k];
+    }
+    const float den = s_den[t];
+#pragma unroll
+    for (int k = 0; k < POSE_MAXC / 64; ++k) {
+      const int ch = lane + 64 * k;
+      if (ch < C) tile[ch * TS + t] = acc[k] / den;
+    }
+  }
+  __syncthreads();
   const int P = d.pad_out ? 2 : 0;
   const int Yo = d.Y + P, Xo = d.X + P;
-  const PlanEntry* list = plan + (size_t)bc * V;
-  float* ob = out + (size_t)b * (d.C + 1) * d.Z * Yo * Xo;
-  const float* fb = feats + (size_t)bc * d.C * hw;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const PlanEntry e = list[i];
-    const int v = e.meta & 0xFFFFFF, cnt = (e.meta >> 24) & 15;
-    const unsigned in = e.meta >> 28;
+  float* ob = out + (size_t)b * (C + 1) * d.Z * Yo * Xo;
+  for (int idx = threadIdx.x; idx < (C + 1) * POSE_TV; idx += blockDim.x) {
+    const int ch = idx / POSE_TV, t = idx % POSE_TV, v = v0 + t;
+    if (v >= V) continue;
     const int xi = v % d.X, yi = (v / d.X) % d.Y, zi = v / (d.X * d.Y);
     int rows[3], cols[3], nr, nc;
     pad_sets(yi, d.Y, d.pad_out, rows, &nr);
     pad_sets(xi, d.X, d.pad_out, cols, &nc);
-    float w[4];
-    entry_weights(e, w);
-    for (int k = 0; k < POSE_G; ++k) {
-      const int ch = ch0 + k;
-      if (ch > d.C) break;
-      float val;
-      if (ch < d.C) {
-        const float* f = fb + (size_t)ch * hw + e.base;
-        val = 0.f;
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (in >> q & 1u) val += f[tap_offset(q, d.w)] * w[q];
-      } else {
-        val = e.z / d.z_scale;
-      }
-      const float o = val / e.den;
-      float* plane = ob + ((size_t)ch * d.Z + zi) * Yo * Xo;
-      for (int a = 0; a < nr; ++a)
-        for (int c2 = 0; c2 < nc; ++c2) {
-          float* dst = plane + rows[a] * Xo + cols[c2];
-          if (cnt == 1) *dst = o;
-          else atomicAdd(dst, o);
-        }
-    }
+    const float o = tile[ch * TS + t];
+    float* plane = ob + ((size_t)ch * d.Z + zi) * Yo * Xo;
+    for (int a = 0; a < nr; ++a)
+      for (int c2 = 0; c2 < nc; ++c2) plane[rows[a] * Xo + cols[c2]] = o;
   }
 }
 
 // ------------------------------------------------------------------------------ K2 backward
-// LDS-privatised gather: a workgroup owns (batch, camera, POSE_BG channels) and accumulates the
-// gradient of those channel planes in LDS with ds_add_f32 while walking the camera's plan; each
-// plane is then written once with coalesced stores (no global atomics, no pre-zeroing).
-__global__ __launch_bounds__(256) void fuse_pose_bwd_k(vfd_voxel_desc d, const PlanEntry* __restrict__ plan,
-                                                       const int* __restrict__ counts,
-                                                       const float* __restrict__ dout, float* __restrict__ dfeats,
-                                                       int G) {
+// LDS-privatised gather over the fusion plan: a workgroup owns (batch, camera, G channels) and
+// accumulates the gradient of those channel planes in LDS (ds_add_f32) while walking the
+// camera's plan, then writes each plane once (no global atomics, no pre-zeroing).  Each thread
+// keeps U plan entries in flight (independent loads), and workgroups are numbered so that all
+// groups of one camera land on the same XCD (its plan stays in that XCD's L2).
+constexpr int POSE_BWD_THREADS = 512;
+constexpr int POSE_BWD_U = 4;
+
+template <int G>
+__global__ __launch_bounds__(POSE_BWD_THREADS) void fuse_pose_bwd_k(vfd_voxel_desc d,
+                                                                    const PlanEntry* __restrict__ plan,
+                                                                    const int* __restrict__ counts,
+                                                                    const float* __restrict__ dout,
+                                                                    float* __restrict__ dfeats, int ngroups,
+                                                                    int ntasks) {
   extern __shared__ __attribute__((aligned(16))) float acc[];     // [G][h*w]
+  const int per_xcd = gridDim.x / 8;
+  const int task = (blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
+  if (task >= ntasks) return;
+  const int bc = task / ngroups, b = bc / d.N;
+  const int ch0 = (task % ngroups) * G;
   const int V = d.X * d.Y * d.Z;
-  const int bc = blockIdx.y, b = bc / d.N;
-  const int ch0 = blockIdx.x * G;
   const int hw = d.h * d.w;
   const int gch = min(G, d.C - ch0);
   for (int i = threadIdx.x; i < G * hw; i += blockDim.x) acc[i] = 0.f;
@@ -486,28 +551,62 @@ __global__ __launch_bounds__(256) void fuse_pose_bwd_k(vfd_voxel_desc d, const P
   const int n = counts[bc];
   const int P = d.pad_out ? 2 : 0;
   const int Yo = d.Y + P, Xo = d.X + P;
+  const size_t plane_sz = (size_t)d.Z * Yo * Xo;
   const PlanEntry* list = plan + (size_t)bc * V;
-  const float* gb = dout + (size_t)b * (d.C + 1) * d.Z * Yo * Xo;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    const PlanEntry e = list[i];
-    const int v = e.meta & 0xFFFFFF;
-    const unsigned in = e.meta >> 28;
-    const int xi = v % d.X, yi = (v / d.X) % d.Y, zi = v / (d.X * d.Y);
-    int rows[3], cols[3], nr, nc;
-    pad_sets(yi, d.Y, d.pad_out, rows, &nr);
-    pad_sets(xi, d.X, d.pad_out, cols, &nc);
-    float w[4];
-    entry_weights(e, w);
-    for (int k = 0; k < gch; ++k) {
-      const float* plane = gb + ((size_t)(ch0 + k) * d.Z + zi) * Yo * Xo;
-      float g = 0.f;
-      for (int a = 0; a < nr; ++a)
-        for (int c2 = 0; c2 < nc; ++c2) g += plane[rows[a] * Xo + cols[c2]];
-      g = g / e.den;
-      float* ak = acc + k * hw + e.base;
+  const float* gb = dout + (size_t)b * (d.C + 1) * plane_sz + (size_t)ch0 * plane_sz;
+  // Each thread walks its own contiguous segment of the list: the lanes of one instruction then
+  // hold voxels from 64 different parts of the grid, whose taps land on different pixels (the
+  // plan is voxel-ordered, so neighbouring entries would pile their ds_add_f32 onto the same
+  // LDS words and serialise); a lane's consecutive entries stay cache-line neighbours.
+  const int seg = cdiv(n, POSE_BWD_THREADS);
+  const int s0 = threadIdx.x * seg, s1 = min(n, s0 + seg);
+  for (int i0 = s0; i0 < s1; i0 += POSE_BWD_U) {
+    PlanEntry e[POSE_BWD_U];
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (in >> q & 1u) atomicAdd(ak + tap_offset(q, d.w), g * w[q]);
+    for (int u = 0; u < POSE_BWD_U; ++u) {
+      const int i = i0 + u;
+      if (i < s1) e[u] = list[i];
+      else e[u].meta = 0xFFFFFFFFu;
+    }
+    float g[POSE_BWD_U][G];
+#pragma unroll
+    for (int u = 0; u < POSE_BWD_U; ++u) {
+#pragma unroll
+      for (int k = 0; k < G; ++k) g[u][k] = 0.f;
+      if (e[u].meta == 0xFFFFFFFFu) continue;
+      const int v = e[u].meta & 0xFFFFFF;
+      const int xi = v % d.X, yi = (v / d.X) % d.Y, zi = v / (d.X * d.Y);
+      int rows[3], cols[3], nr, nc;
+      pad_sets(yi, d.Y, d.pad_out, rows, &nr);
+      pad_sets(xi, d.X, d.pad_out, cols, &nc);
+      const float* pz = gb + (size_t)zi * Yo * Xo;
+#pragma unroll
+      for (int k = 0; k < G; ++k) {
+        if (k < gch) {
+          const float* plane = pz + (size_t)k * plane_sz;
+          float s = 0.f;
+          for (int a = 0; a < nr; ++a)
+            for (int c2 = 0; c2 < nc; ++c2) s += plane[rows[a] * Xo + cols[c2]];
+          g[u][k] = s;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < POSE_BWD_U; ++u) {
+      if (e[u].meta == 0xFFFFFFFFu) continue;
+      const unsigned in = e[u].meta >> 28;
+      float w[4];
+      entry_weights(e[u], w);
+#pragma unroll
+      for (int k = 0; k < G; ++k) {
+        if (k < gch) {
+          const float gk = g[u][k] / e[u].den;
+          float* ak = acc + k * hw + e[u].base;
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (in >> q & 1u) atomicAdd(ak + tap_offset(q, d.w), gk * w[q]);
+        }
+      }
     }
   }
   __syncthreads();
@@ -797,23 +896,31 @@ int vfd_fusion_plan(const vfd_voxel_desc* d, const float* mask_lo, const float* 
   return fail_launch("fusion_plan");
 }
 
-int vfd_fuse_pose_fwd(const vfd_voxel_desc* d, const void* plan, const int* counts, const float* feats, float* out,
-                      void* stream) {
+int vfd_fuse_pose_fwd(const vfd_voxel_desc* d, const float* mask_lo, const float* K, const float* Einv,
+                      const float* feats_cl, float* out, void* stream) {
   int st = check_voxel_desc(d);
   if (st) return st;
+  VFD_REQUIRE(d->C >= 1 && d->C <= POSE_MAXC, "fuse_pose: C=%d outside [1, %d]", d->C, POSE_MAXC);
+  VFD_REQUIRE(d->N >= 1 && d->N <= 8, "fuse_pose: N=%d outside [1, 8]", d->N);
   hipStream_t s = (hipStream_t)stream;
-  const int P = d->pad_out ? 2 : 0;
-  (void)hipMemsetAsync(out, 0, (size_t)d->B * (d->C + 1) * d->Z * (d->Y + P) * (d->X + P) * sizeof(float), s);
-  dim3 grid(16, cdiv(d->C + 1, POSE_G), d->B * d->N);
+  const int V = d->X * d->Y * d->Z;
+  const size_t lds = (size_t)(d->C + 1) * (POSE_TV + 1) * sizeof(float);
+  dim3 grid(cdiv(V, POSE_TV), d->B);
   ProfScope ps(K_FUSE_POSE_FWD, s);
-  fuse_pose_fwd_k<<<grid, 256, 0, s>>>(*d, (const PlanEntry*)plan, counts, feats, out);
+  switch (d->N) {
+#define VFD_CASE(n) case n: fuse_pose_fwd_k<n><<<grid, 256, lds, s>>>(*d, mask_lo, K, Einv, feats_cl, out); break;
+    VFD_CASE(1) VFD_CASE(2) VFD_CASE(3) VFD_CASE(4) VFD_CASE(5) VFD_CASE(6) VFD_CASE(7) VFD_CASE(8)
+#undef VFD_CASE
+  }
   return fail_launch("fuse_pose_fwd");
 }
 
 static int pose_bwd_group(const vfd_voxel_desc* d) {
-  // channels per workgroup so that G * h * w floats fit in ~64 KB of LDS (2 workgroups / CU)
-  int g = (64 * 1024) / (d->h * d->w * (int)sizeof(float));
-  return g < 1 ? 1 : (g > 8 ? 8 : g);
+  // channels per workgroup: G * h * w floats within ~40 KB of LDS (several workgroups per CU)
+  const int per = d->h * d->w * (int)sizeof(float);
+  if (4 * per <= 40 * 1024) return 4;
+  if (2 * per <= 40 * 1024) return 2;
+  return 1;
 }
 
 int vfd_fuse_pose_bwd(const vfd_voxel_desc* d, const void* plan, const int* counts, const float* d_out,
@@ -822,11 +929,17 @@ int vfd_fuse_pose_bwd(const vfd_voxel_desc* d, const void* plan, const int* coun
   if (st) return st;
   const int G = pose_bwd_group(d);
   const size_t lds = (size_t)G * d->h * d->w * sizeof(float);
-  VFD_REQUIRE(lds <= 160 * 1024, "feature map %dx%d too large for the LDS-privatised backward", d->h, d->w);
+  VFD_REQUIRE(lds <= 64 * 1024, "feature map %dx%d too large for the LDS-privatised backward", d->h, d->w);
   hipStream_t s = (hipStream_t)stream;
-  dim3 grid(cdiv(d->C, G), d->B * d->N);
+  const int ngroups = cdiv(d->C, G);
+  const int ntasks = ngroups * d->B * d->N;
+  dim3 grid(8 * cdiv(ntasks, 8));
   ProfScope ps(K_FUSE_POSE_BWD, s);
-  fuse_pose_bwd_k<<<grid, 256, lds, s>>>(*d, (const PlanEntry*)plan, counts, d_out, d_feats, G);
+  switch (G) {
+    case 4: fuse_pose_bwd_k<4><<<grid, POSE_BWD_THREADS, lds, s>>>(*d, (const PlanEntry*)plan, counts, d_out, d_feats, ngroups, ntasks); break;
+    case 2: fuse_pose_bwd_k<2><<<grid, POSE_BWD_THREADS, lds, s>>>(*d, (const PlanEntry*)plan, counts, d_out, d_feats, ngroups, ntasks); break;
+    default: fuse_pose_bwd_k<1><<<grid, POSE_BWD_THREADS, lds, s>>>(*d, (const PlanEntry*)plan, counts, d_out, d_feats, ngroups, ntasks); break;
+  }
   return fail_launch("fuse_pose_bwd");
 }
 

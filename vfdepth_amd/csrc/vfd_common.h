@@ -140,6 +140,6 @@ __device__ __forceinline__ T block_sum_all(T v, T* lds) {
   return lds[0] + lds[1] + lds[2] + lds[3];
 }
 
-inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
+__host__ __device__ inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
 
 }  // namespace vfd

@@ -135,6 +135,7 @@ class FusionPlan:
         lib = L.load()
         mask_lo, K, Einv = (_dev(t, n) for t, n in ((mask_lo, 'mask'), (K, 'K'), (Einv, 'Einv')))
         self.B, self.N = mask_lo.shape[:2]
+        self.mask_lo, self.K, self.Einv = mask_lo, K, Einv
         d = space.desc(self.B, self.N)
         nbytes = lib.vfd_fusion_plan_bytes(ctypes.byref(d))
         self.buf = torch.empty(nbytes, dtype=torch.uint8, device=mask_lo.device)
@@ -151,10 +152,12 @@ class FusePose(torch.autograd.Function):
         lib = L.load()
         feats = _dev(feats, 'feats')
         B, N, C = feats.shape[:3]
+        feats_cl = feats.flatten(3).transpose(2, 3).contiguous()        # [B, N, h*w, C]
         out = torch.empty(B, (C + 1) * space.Z, space.Y + 2, space.X + 2, device=feats.device)
         d = space.desc(B, N, C=C)
-        L.check(lib.vfd_fuse_pose_fwd(ctypes.byref(d), plan.buf.data_ptr(), plan.counts.data_ptr(),
-                                      feats.data_ptr(), out.data_ptr(), L.stream()), 'fuse_pose_fwd')
+        L.check(lib.vfd_fuse_pose_fwd(ctypes.byref(d), plan.mask_lo.data_ptr(), plan.K.data_ptr(),
+                                      plan.Einv.data_ptr(), feats_cl.data_ptr(), out.data_ptr(), L.stream()),
+                'fuse_pose_fwd')
         ctx.space, ctx.plan, ctx.shape = space, plan, tuple(feats.shape)
         return out
 

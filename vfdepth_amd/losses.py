@@ -51,7 +51,7 @@ class SingleCamLoss(nn.Module):
         if getattr(self, '_counter', None) is None or self._counter.device != torch.device(device):
             self._counter = torch.zeros(1, dtype=torch.int64, device=device)
         self._counter += 1
-        return ((self._seed << 20) ^ self._calls, self._counter)
+        return (self._seed << 20, self._counter)
 
     def draw_noise(self, B, H, W, cams, device):
         """Identity-loss noise exactly as the reference draws it: CPU global RNG, camera by camera

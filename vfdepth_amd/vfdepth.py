@@ -191,7 +191,7 @@ class VFDepthAlgo:
     def compute_depth_maps(self, inputs, outputs, packed=None):
         """Per-camera depth (vfdepth.py:263-275); with the packed [B*N] decoder output the depth of
         all cameras is one elementwise op, kept as [B, N, H, W] for the kernels."""
-        self._disp_all, self._depth_all = {}, {}
+        disp_all, depth_all = outputs.setdefault('_disp_all', {}), outputs.setdefault('_depth_all', {})
         K0 = inputs[('K', 0)]
         B, N = K0.shape[:2]
         for scale in self.scales:
@@ -206,15 +206,15 @@ class VFDepthAlgo:
             lo, hi = 1 / self.max_depth, 1 / self.min_depth
             depth = 1 / (lo + (hi - lo) * disp_f)
             depth = depth * K0[:, :, 0:1, 0:1] / self.focal_length_scale
-            self._disp_all[scale] = disp
-            self._depth_all[scale] = depth
+            disp_all[scale] = disp
+            depth_all[scale] = depth
             for c in range(N):
                 outputs[('cam', c)][('depth', scale)] = depth[:, c].unsqueeze(1)
 
     def compute_losses(self, inputs, outputs, noise=None):
         rel = {c: self.pose.compute_relative_cam_poses(inputs, outputs, c) for c in range(self.num_cams)}
-        packed = self.view_rendering.render_all(inputs, outputs, rel, self._depth_all)
-        total, logs = self.losses.forward_all(inputs, outputs, packed, self._disp_all, self._depth_all, noise)
+        packed = self.view_rendering.render_all(inputs, outputs, rel, outputs['_depth_all'])
+        total, logs = self.losses.forward_all(inputs, outputs, packed, outputs['_disp_all'], outputs['_depth_all'], noise)
         losses = dict(logs)
         losses['total_loss'] = total
         return losses
@@ -247,7 +247,7 @@ class VFDepthAlgo:
         graph = torch.cuda.CUDAGraph()
         self.optimizer.zero_grad(set_to_none=True)
         with torch.cuda.graph(graph):
-            _, static_losses = self.process_batch(dict(static), self.rank)
+            static_outputs, static_losses = self.process_batch(dict(static), self.rank)
             static_losses['total_loss'].backward()
             self.optimizer.step()
 
@@ -260,6 +260,7 @@ class VFDepthAlgo:
             return static_losses
 
         step.graph = graph
+        step.outputs = static_outputs      # refreshed by every replay
         return step
 
     def compute_depth_metrics(self, inputs, outputs, vis_scale=False):

@@ -71,7 +71,8 @@ int vfd_fuse_depth_bwd(const vfd_voxel_desc* d, const float* d_vox, const float*
 
 /* Fusion plan (volumetric_fusionnet.py:132-140, 166-195): for every (batch, camera) the compacted
  * list of voxels the camera sees (32-B entries: voxel | valid-camera count | in-range taps, corner
- * pixel, bilinear fractions, camera depth, mean denominator) and its length in counts [B*N].
+ * pixel, bilinear fractions, camera depth, mean denominator) and its length in counts [B*N],
+ * plus its inverse index (per pixel, the (entry, tap) pairs that sample it; CSR).
  * Built once per step from K (fusion scale), Einv and mask_lo; shared by every pose-mode call. */
 size_t vfd_fusion_plan_bytes(const vfd_voxel_desc* d);
 int vfd_fusion_plan(const vfd_voxel_desc* d, const float* mask_lo, const float* K, const float* Einv,
@@ -84,9 +85,12 @@ int vfd_fusion_plan(const vfd_voxel_desc* d, const float* mask_lo, const float* 
  * the stride-2 3x3 conv of reduce_dim, :339-342). */
 int vfd_fuse_pose_fwd(const vfd_voxel_desc* d, const float* mask_lo, const float* K, const float* Einv,
                       const float* feats_cl, float* out, void* stream);
-/* d_out in the forward's output layout -> d_feats [B,N,C,h,w] (every element written). */
+/* d_out in the forward's output layout -> d_feats [B,N,C,h,w] (every element written).
+ * Atomic-free gather through the plan's per-pixel inverse index; the workspace holds the
+ * voxel-major [B, V, C] copy of d_out (vfd_fuse_pose_bwd_workspace bytes). */
+size_t vfd_fuse_pose_bwd_workspace(const vfd_voxel_desc* d);
 int vfd_fuse_pose_bwd(const vfd_voxel_desc* d, const void* plan, const int* counts, const float* d_out,
-                      float* d_feats, void* stream);
+                      float* d_feats, void* workspace, size_t ws_bytes, void* stream);
 
 /* K3 — voxel -> camera-frustum trilinear resampling (volumetric_fusionnet.py:232-262).
  * vox [B,V,Cv], invK, E [B,N,4,4] (fusion scale) -> out [B*N, Cv*D, h(+2), w(+2)]

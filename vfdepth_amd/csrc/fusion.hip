@@ -522,96 +522,183 @@ __global__ __launch_bounds__(256) void fuse_pose_fwd_k(vfd_voxel_desc d, const f
 }
 
 // ------------------------------------------------------------------------------ K2 backward
-// LDS-privatised gather over the fusion plan: a workgroup owns (batch, camera, G channels) and
-// accumulates the gradient of those channel planes in LDS (ds_add_f32) while walking the
-// camera's plan, then writes each plane once (no global atomics, no pre-zeroing).  Each thread
-// keeps U plan entries in flight (independent loads), and workgroups are numbered so that all
-// groups of one camera land on the same XCD (its plan stays in that XCD's L2).
-constexpr int POSE_BWD_THREADS = 512;
-constexpr int POSE_BWD_U = 4;
+// Atomic-free, pixel-major.  LDS float atomics cost ~3 cycles per lane on gfx950 (measured on
+// the scatter form of this kernel), so the backward is a gather:
+//   plan_index_k     once per step with the plan: per (batch, camera) CSR inverse index
+//                    pixel -> [(entry << 2) | tap] of every in-range bilinear tap;
+//   pose_grad_rows_k d_out (reflect-padded NCHW) -> voxel-major rows T[b][v][0:C] with the
+//                    padding copies folded back (one coalesced pass);
+//   fuse_pose_bwd_k  per pixel, lanes = channels: sum (T[voxel] / den) * w_tap over the pixel's
+//                    list (1-KB row loads), staged through LDS for coalesced NCHW stores.
+constexpr int PIDX_THREADS = 1024;
 
-template <int G>
-__global__ __launch_bounds__(POSE_BWD_THREADS) void fuse_pose_bwd_k(vfd_voxel_desc d,
-                                                                    const PlanEntry* __restrict__ plan,
-                                                                    const int* __restrict__ counts,
-                                                                    const float* __restrict__ dout,
-                                                                    float* __restrict__ dfeats, int ngroups,
-                                                                    int ntasks) {
-  extern __shared__ __attribute__((aligned(16))) float acc[];     // [G][h*w]
-  const int per_xcd = gridDim.x / 8;
-  const int task = (blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
-  if (task >= ntasks) return;
-  const int bc = task / ngroups, b = bc / d.N;
-  const int ch0 = (task % ngroups) * G;
-  const int V = d.X * d.Y * d.Z;
+__global__ __launch_bounds__(PIDX_THREADS) void plan_index_k(vfd_voxel_desc d, const PlanEntry* __restrict__ plan,
+                                                             const int* __restrict__ counts, int* __restrict__ row_ptr,
+                                                             int* __restrict__ csr) {
+  extern __shared__ int sm[];
   const int hw = d.h * d.w;
-  const int gch = min(G, d.C - ch0);
-  for (int i = threadIdx.x; i < G * hw; i += blockDim.x) acc[i] = 0.f;
+  int* cnt = sm;                 // [hw]
+  int* cur = sm + hw;            // [hw]
+  int* part = sm + 2 * hw;       // [PIDX_THREADS]
+  const int bc = blockIdx.x;
+  const int V = d.X * d.Y * d.Z;
+  const int t = threadIdx.x;
+  for (int i = t; i < hw; i += PIDX_THREADS) cnt[i] = 0;
   __syncthreads();
   const int n = counts[bc];
+  const PlanEntry* list = plan + (size_t)bc * V;
+  for (int i = t; i < n; i += PIDX_THREADS) {
+    const PlanEntry e = list[i];
+    const unsigned in = e.meta >> 28;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (in >> q & 1u) atomicAdd(&cnt[e.base + tap_offset(q, d.w)], 1);
+  }
+  __syncthreads();
+  // exclusive scan of cnt -> cur / row_ptr (chunk per thread, Hillis-Steele over the chunk sums)
+  const int chunk = (hw + PIDX_THREADS - 1) / PIDX_THREADS;
+  const int c0 = min(hw, t * chunk), c1 = min(hw, c0 + chunk);
+  int local = 0;
+  for (int i = c0; i < c1; ++i) local += cnt[i];
+  part[t] = local;
+  __syncthreads();
+  for (int off = 1; off < PIDX_THREADS; off <<= 1) {
+    const int v = t >= off ? part[t - off] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int run = part[t] - local;
+  int* rp = row_ptr + (size_t)bc * (hw + 1);
+  for (int i = c0; i < c1; ++i) {
+    cur[i] = run;
+    rp[i] = run;
+    run += cnt[i];
+  }
+  if (t == PIDX_THREADS - 1) rp[hw] = part[t];
+  __syncthreads();
+  int* cb = csr + (size_t)bc * 4 * V;
+  for (int i = t; i < n; i += PIDX_THREADS) {
+    const PlanEntry e = list[i];
+    const unsigned in = e.meta >> 28;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (in >> q & 1u) cb[atomicAdd(&cur[e.base + tap_offset(q, d.w)], 1)] = (i << 2) | q;
+  }
+}
+
+constexpr int PGR_CH = 64;     // channels per transpose tile
+
+__global__ __launch_bounds__(256) void pose_grad_rows_k(vfd_voxel_desc d, const float* __restrict__ dout,
+                                                        float* __restrict__ rows) {
+  extern __shared__ float tile[];        // [PGR_CH][X + 1]
+  const int c0 = blockIdx.x * PGR_CH;
+  const int zy = blockIdx.y, zi = zy / d.Y, yi = zy % d.Y;
+  const int b = blockIdx.z;
+  const int X = d.X, XS = d.X + 1;
   const int P = d.pad_out ? 2 : 0;
   const int Yo = d.Y + P, Xo = d.X + P;
   const size_t plane_sz = (size_t)d.Z * Yo * Xo;
+  const int nch = min(PGR_CH, d.C - c0);
+  int rws[3], nr;
+  pad_sets(yi, d.Y, d.pad_out, rws, &nr);
+  const float* gb = dout + (size_t)b * (d.C + 1) * plane_sz;
+  for (int i = threadIdx.x; i < nch * X; i += blockDim.x) {
+    const int c = i / X, xi = i % X;
+    int cols[3], nc;
+    pad_sets(xi, X, d.pad_out, cols, &nc);
+    const float* plane = gb + (size_t)(c0 + c) * plane_sz + (size_t)zi * Yo * Xo;
+    float g = 0.f;
+    for (int a = 0; a < nr; ++a)
+      for (int c2 = 0; c2 < nc; ++c2) g += plane[rws[a] * Xo + cols[c2]];
+    tile[c * XS + xi] = g;
+  }
+  __syncthreads();
+  float* rb = rows + ((size_t)b * d.X * d.Y * d.Z + (size_t)zy * X) * d.C + c0;
+  for (int i = threadIdx.x; i < X * nch; i += blockDim.x) {
+    const int xi = i / nch, c = i % nch;
+    rb[(size_t)xi * d.C + c] = tile[c * XS + xi];
+  }
+}
+
+constexpr int PBW_TP = 16;     // pixels per workgroup (4 per wave)
+constexpr int PBW_U = 4;       // list items in flight per wave
+
+__global__ __launch_bounds__(256) void fuse_pose_bwd_k(vfd_voxel_desc d, const PlanEntry* __restrict__ plan,
+                                                       const int* __restrict__ row_ptr, const int* __restrict__ csr,
+                                                       const float* __restrict__ rows, float* __restrict__ dfeats) {
+  extern __shared__ float otile[];       // [C][PBW_TP + 1]
+  constexpr int CPL = POSE_MAXC / 64;
+  const int hw = d.h * d.w;
+  const int V = d.X * d.Y * d.Z;
+  const int C = d.C;
+  const int bc = blockIdx.y, b = bc / d.N;
+  const int q0 = blockIdx.x * PBW_TP;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const PlanEntry* list = plan + (size_t)bc * V;
-  const float* gb = dout + (size_t)b * (d.C + 1) * plane_sz + (size_t)ch0 * plane_sz;
-  // Each thread walks its own contiguous segment of the list: the lanes of one instruction then
-  // hold voxels from 64 different parts of the grid, whose taps land on different pixels (the
-  // plan is voxel-ordered, so neighbouring entries would pile their ds_add_f32 onto the same
-  // LDS words and serialise); a lane's consecutive entries stay cache-line neighbours.
-  const int seg = cdiv(n, POSE_BWD_THREADS);
-  const int s0 = threadIdx.x * seg, s1 = min(n, s0 + seg);
-  for (int i0 = s0; i0 < s1; i0 += POSE_BWD_U) {
-    PlanEntry e[POSE_BWD_U];
+  const int* rp = row_ptr + (size_t)bc * (hw + 1);
+  const int* cb = csr + (size_t)bc * 4 * V;
+  const float* rb = rows + (size_t)b * V * C;
+  for (int pi = 0; pi < PBW_TP / 4; ++pi) {
+    const int ql = wv * (PBW_TP / 4) + pi;
+    const int q = q0 + ql;
+    float acc[CPL];
 #pragma unroll
-    for (int u = 0; u < POSE_BWD_U; ++u) {
-      const int i = i0 + u;
-      if (i < s1) e[u] = list[i];
-      else e[u].meta = 0xFFFFFFFFu;
-    }
-    float g[POSE_BWD_U][G];
+    for (int k = 0; k < CPL; ++k) acc[k] = 0.f;
+    if (q < hw) {
+      const int lo = rp[q], hi = rp[q + 1];
+      for (int j = lo; j < hi; j += PBW_U) {
+        float wt[PBW_U], den[PBW_U];
+        int vox[PBW_U];
 #pragma unroll
-    for (int u = 0; u < POSE_BWD_U; ++u) {
-#pragma unroll
-      for (int k = 0; k < G; ++k) g[u][k] = 0.f;
-      if (e[u].meta == 0xFFFFFFFFu) continue;
-      const int v = e[u].meta & 0xFFFFFF;
-      const int xi = v % d.X, yi = (v / d.X) % d.Y, zi = v / (d.X * d.Y);
-      int rows[3], cols[3], nr, nc;
-      pad_sets(yi, d.Y, d.pad_out, rows, &nr);
-      pad_sets(xi, d.X, d.pad_out, cols, &nc);
-      const float* pz = gb + (size_t)zi * Yo * Xo;
-#pragma unroll
-      for (int k = 0; k < G; ++k) {
-        if (k < gch) {
-          const float* plane = pz + (size_t)k * plane_sz;
-          float s = 0.f;
-          for (int a = 0; a < nr; ++a)
-            for (int c2 = 0; c2 < nc; ++c2) s += plane[rows[a] * Xo + cols[c2]];
-          g[u][k] = s;
+        for (int u = 0; u < PBW_U; ++u) {
+          wt[u] = 0.f;
+          den[u] = 1.f;
+          vox[u] = -1;
+          if (j + u < hi) {
+            const int it = cb[j + u];
+            const PlanEntry e = list[it >> 2];
+            float w[4];
+            entry_weights(e, w);
+            const int tap = it & 3;
+            wt[u] = tap == 0 ? w[0] : tap == 1 ? w[1] : tap == 2 ? w[2] : w[3];
+            den[u] = e.den;
+            vox[u] = (int)(e.meta & 0xFFFFFF);
+          }
         }
+        float g[PBW_U][CPL];
+#pragma unroll
+        for (int u = 0; u < PBW_U; ++u) {
+          const float* row = rb + (size_t)(vox[u] < 0 ? 0 : vox[u]) * C;
+#pragma unroll
+          for (int k = 0; k < CPL; ++k) {
+            const int ch = lane + 64 * k;
+            g[u][k] = (vox[u] >= 0 && ch < C) ? row[ch] : 0.f;
+          }
+        }
+        // reference order: d(mean) = g / den, then grid_sample's backward adds d(mean) * w
+#pragma unroll
+        for (int u = 0; u < PBW_U; ++u)
+          if (vox[u] >= 0) {
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) acc[k] += (g[u][k] / den[u]) * wt[u];
+          }
       }
     }
 #pragma unroll
-    for (int u = 0; u < POSE_BWD_U; ++u) {
-      if (e[u].meta == 0xFFFFFFFFu) continue;
-      const unsigned in = e[u].meta >> 28;
-      float w[4];
-      entry_weights(e[u], w);
-#pragma unroll
-      for (int k = 0; k < G; ++k) {
-        if (k < gch) {
-          const float gk = g[u][k] / e[u].den;
-          float* ak = acc + k * hw + e[u].base;
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            if (in >> q & 1u) atomicAdd(ak + tap_offset(q, d.w), gk * w[q]);
-        }
-      }
+    for (int k = 0; k < CPL; ++k) {
+      const int ch = lane + 64 * k;
+      if (ch < C) otile[ch * (PBW_TP + 1) + ql] = acc[k];
     }
   }
   __syncthreads();
-  float* db = dfeats + ((size_t)bc * d.C + ch0) * hw;
-  for (int i = threadIdx.x; i < gch * hw; i += blockDim.x) db[i] = acc[i];
+  const int np = min(PBW_TP, hw - q0);
+  float* db = dfeats + (size_t)bc * C * hw + q0;
+  for (int i = threadIdx.x; i < C * PBW_TP; i += blockDim.x) {
+    const int ch = i / PBW_TP, p = i % PBW_TP;
+    if (p < np) db[(size_t)ch * hw + p] = otile[ch * (PBW_TP + 1) + p];
+  }
 }
 
 // ------------------------------------------------------------------------------ K3 geometry
@@ -874,8 +961,16 @@ int vfd_fuse_depth_bwd(const vfd_voxel_desc* d, const float* d_vox, const float*
   return fail_launch("fuse_depth_reduce");
 }
 
-size_t vfd_fusion_plan_bytes(const vfd_voxel_desc* d) {
+// plan buffer: [B*N][V] PlanEntry | [B*N][hw+1] int row_ptr | [B*N][4V] int csr
+static size_t plan_entries_bytes(const vfd_voxel_desc* d) {
   return (size_t)d->B * d->N * d->X * d->Y * d->Z * sizeof(PlanEntry);
+}
+static size_t plan_rowptr_bytes(const vfd_voxel_desc* d) {
+  return ((size_t)d->B * d->N * (d->h * d->w + 1) * sizeof(int) + 255) / 256 * 256;
+}
+
+size_t vfd_fusion_plan_bytes(const vfd_voxel_desc* d) {
+  return plan_entries_bytes(d) + plan_rowptr_bytes(d) + (size_t)d->B * d->N * 4 * d->X * d->Y * d->Z * sizeof(int);
 }
 
 int vfd_fusion_plan(const vfd_voxel_desc* d, const float* mask_lo, const float* K, const float* Einv, void* plan,
@@ -893,6 +988,10 @@ int vfd_fusion_plan(const vfd_voxel_desc* d, const float* mask_lo, const float* 
     VFD_CASE(1) VFD_CASE(2) VFD_CASE(3) VFD_CASE(4) VFD_CASE(5) VFD_CASE(6) VFD_CASE(7) VFD_CASE(8)
 #undef VFD_CASE
   }
+  int* row_ptr = (int*)((char*)plan + plan_entries_bytes(d));
+  int* csr = (int*)((char*)row_ptr + plan_rowptr_bytes(d));
+  const size_t lds = (2 * (size_t)d->h * d->w + PIDX_THREADS) * sizeof(int);
+  plan_index_k<<<d->B * d->N, PIDX_THREADS, lds, s>>>(*d, (const PlanEntry*)plan, counts, row_ptr, csr);
   return fail_launch("fusion_plan");
 }
 
@@ -915,31 +1014,28 @@ int vfd_fuse_pose_fwd(const vfd_voxel_desc* d, const float* mask_lo, const float
   return fail_launch("fuse_pose_fwd");
 }
 
-static int pose_bwd_group(const vfd_voxel_desc* d) {
-  // channels per workgroup: G * h * w floats within ~40 KB of LDS (several workgroups per CU)
-  const int per = d->h * d->w * (int)sizeof(float);
-  if (4 * per <= 40 * 1024) return 4;
-  if (2 * per <= 40 * 1024) return 2;
-  return 1;
+size_t vfd_fuse_pose_bwd_workspace(const vfd_voxel_desc* d) {
+  return (size_t)d->B * d->X * d->Y * d->Z * d->C * sizeof(float);
 }
 
 int vfd_fuse_pose_bwd(const vfd_voxel_desc* d, const void* plan, const int* counts, const float* d_out,
-                      float* d_feats, void* stream) {
+                      float* d_feats, void* workspace, size_t ws_bytes, void* stream) {
   int st = check_voxel_desc(d);
   if (st) return st;
-  const int G = pose_bwd_group(d);
-  const size_t lds = (size_t)G * d->h * d->w * sizeof(float);
-  VFD_REQUIRE(lds <= 64 * 1024, "feature map %dx%d too large for the LDS-privatised backward", d->h, d->w);
+  (void)counts;
+  VFD_REQUIRE(d->C >= 1 && d->C <= POSE_MAXC, "fuse_pose: C=%d outside [1, %d]", d->C, POSE_MAXC);
+  VFD_REQUIRE(ws_bytes >= vfd_fuse_pose_bwd_workspace(d), "fuse_pose_bwd: workspace too small");
+  VFD_REQUIRE((2 * (size_t)d->h * d->w + PIDX_THREADS) * sizeof(int) <= 160 * 1024, "feature map %dx%d too large", d->h, d->w);
   hipStream_t s = (hipStream_t)stream;
-  const int ngroups = cdiv(d->C, G);
-  const int ntasks = ngroups * d->B * d->N;
-  dim3 grid(8 * cdiv(ntasks, 8));
+  const int hw = d->h * d->w;
+  const int* row_ptr = (const int*)((const char*)plan + plan_entries_bytes(d));
+  const int* csr = (const int*)((const char*)row_ptr + plan_rowptr_bytes(d));
+  float* rows = (float*)workspace;
   ProfScope ps(K_FUSE_POSE_BWD, s);
-  switch (G) {
-    case 4: fuse_pose_bwd_k<4><<<grid, POSE_BWD_THREADS, lds, s>>>(*d, (const PlanEntry*)plan, counts, d_out, d_feats, ngroups, ntasks); break;
-    case 2: fuse_pose_bwd_k<2><<<grid, POSE_BWD_THREADS, lds, s>>>(*d, (const PlanEntry*)plan, counts, d_out, d_feats, ngroups, ntasks); break;
-    default: fuse_pose_bwd_k<1><<<grid, POSE_BWD_THREADS, lds, s>>>(*d, (const PlanEntry*)plan, counts, d_out, d_feats, ngroups, ntasks); break;
-  }
+  pose_grad_rows_k<<<dim3(cdiv(d->C, PGR_CH), d->Y * d->Z, d->B), 256, (size_t)PGR_CH * (d->X + 1) * sizeof(float), s>>>(
+      *d, d_out, rows);
+  fuse_pose_bwd_k<<<dim3(cdiv(hw, PBW_TP), d->B * d->N), 256, (size_t)d->C * (PBW_TP + 1) * sizeof(float), s>>>(
+      *d, (const PlanEntry*)plan, row_ptr, csr, rows, d_feats);
   return fail_launch("fuse_pose_bwd");
 }
 

@@ -168,8 +168,11 @@ class FusePose(torch.autograd.Function):
         g = _dev(g, 'grad')
         dfeats = torch.empty(ctx.shape, device=g.device)
         d = ctx.space.desc(B, N, C=C)
+        nbytes = lib.vfd_fuse_pose_bwd_workspace(ctypes.byref(d))
+        ws = _ws(nbytes, g.device)
         L.check(lib.vfd_fuse_pose_bwd(ctypes.byref(d), ctx.plan.buf.data_ptr(), ctx.plan.counts.data_ptr(),
-                                      g.data_ptr(), dfeats.data_ptr(), L.stream()), 'fuse_pose_bwd')
+                                      g.data_ptr(), dfeats.data_ptr(), ws.data_ptr(), nbytes, L.stream()),
+                'fuse_pose_bwd')
         return None, None, dfeats
 
 

@@ -81,20 +81,20 @@ int vfd_fusion_plan(const vfd_voxel_desc* d, const float* mask_lo, const float* 
 /* K2 — pose-mode unprojection, mean over valid cameras (volumetric_fusionnet.py:116-162).
  * Voxel-major gather: every output element is written exactly once (no pre-zeroing, no atomics).
  * feats_cl [B,N,h*w,C] (channels-last), mask_lo [B*N,h,w], K / Einv [B,N,4,4] (fusion scale)
- * -> out [B, (C+1)*Z, Y(+2), X(+2)] (channel = c*Z + z; +2 when pad_out: reflect-padded for
- * the stride-2 3x3 conv of reduce_dim, :339-342). */
+ * -> out [B, Y(+2), X(+2), Z*(C+1)]: NHWC input of reduce_dim's stride-2 3x3 conv (:339-342),
+ * reflect-padded when pad_out, channel index z*(C+1) + c (the reference's c*Z + z order permuted;
+ * the conv weight's input channels are permuted the same way, so the convolution is unchanged). */
 int vfd_fuse_pose_fwd(const vfd_voxel_desc* d, const float* mask_lo, const float* K, const float* Einv,
                       const float* feats_cl, float* out, void* stream);
 /* d_out in the forward's output layout -> d_feats [B,N,C,h,w] (every element written).
- * Atomic-free gather through the plan's per-pixel inverse index; the workspace holds the
- * voxel-major [B, V, C] copy of d_out (vfd_fuse_pose_bwd_workspace bytes). */
-size_t vfd_fuse_pose_bwd_workspace(const vfd_voxel_desc* d);
+ * Atomic-free gather through the plan's per-pixel inverse index. */
 int vfd_fuse_pose_bwd(const vfd_voxel_desc* d, const void* plan, const int* counts, const float* d_out,
-                      float* d_feats, void* workspace, size_t ws_bytes, void* stream);
+                      float* d_feats, void* stream);
 
 /* K3 — voxel -> camera-frustum trilinear resampling (volumetric_fusionnet.py:232-262).
- * vox [B,V,Cv], invK, E [B,N,4,4] (fusion scale) -> out [B*N, Cv*D, h(+2), w(+2)]
- * (channel = c*D + d; padded for the reflect 3x3 conv of reduce_dim when pad_out). */
+ * vox [B,V,Cv] (Cv <= 64), invK, E [B,N,4,4] (fusion scale) -> out [B*N, h(+2), w(+2), D*Cv]:
+ * NHWC input of reduce_dim's first 3x3 conv, reflect-padded when pad_out, channel index
+ * d*Cv + c (the reference's c*D + d order permuted; the conv weight is permuted to match). */
 int vfd_voxel_project_fwd(const vfd_voxel_desc* d, const float* vox, const float* invK,
                           const float* E, float* out, void* stream);
 /* d_out (forward layout) -> d_vox [B,V,Cv] (zeroed here). */

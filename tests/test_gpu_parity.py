@@ -96,8 +96,8 @@ def test_fuse_pose_forward_backward():
     space = net.space(DEV)
     feats = d['feats'].to(DEV).requires_grad_(True)
     plan = KN.FusionPlan(space, KN.mask_lowres(space, inputs['mask']), inputs[('K', 3)], inputs['extrinsics_inv'])
-    out = KN.FusePose.apply(space, plan, feats)
-    B, C1 = out.shape[0], feats.shape[2] + 1
+    B, C1 = feats.shape[0], feats.shape[2] + 1
+    out = KN.pose_to_reference(KN.FusePose.apply(space, plan, feats), C1, space.Z)
     inner = out[:, :, 1:-1, 1:-1].reshape(B, C1, space.Z, space.Y, space.X).reshape(B, C1, -1)
     close(inner, fx['vpose'], 'K2 pose voxels')
     # reflect halo holds the mirrored interior (what the stride-2 reflect conv reads)
@@ -114,7 +114,8 @@ def test_voxel_project_forward_backward():
     space = net.space(DEV)
     vleaf = G.seeded_randn(fx['vox'].shape, seeds['vleaf']).to(DEV)       # [B, Cv, V]
     v = vleaf.permute(0, 2, 1).contiguous().requires_grad_(True)
-    out = KN.VoxelProject.apply(space, v, inputs[('inv_K', 3)], inputs['extrinsics'])
+    out = KN.proj_to_reference(KN.VoxelProject.apply(space, v, inputs[('inv_K', 3)], inputs['extrinsics']),
+                               v.shape[2], space.D)
     B, N = inputs['extrinsics'].shape[:2]
     inner = out[:, :, 1:-1, 1:-1].reshape(B, N, *out.shape[1:2], space.h, space.w)
     close(inner, fx['proj'], 'K3 frustum features')

@@ -413,14 +413,15 @@ __global__ __launch_bounds__(256) void fusion_plan_k(vfd_voxel_desc d, const flo
 }
 
 // ------------------------------------------------------------------------------ K2 forward
-// Voxel-major gather (volumetric_fusionnet.py:116-162, pose branch).  A workgroup owns POSE_TV
-// consecutive voxels: (1) one thread per voxel projects it into every camera (same arithmetic as
-// the plan / the reference), (2) each wave takes voxels in turn with lanes = channels and reads
-// the four bilinear taps of every valid camera from the channels-last feature map (one
-// contiguous C-float row per tap), sums the cameras in order and divides by (count + 1e-7),
-// staging the [C+1][POSE_TV] result in LDS, (3) the tile is written to the reflect-padded NCHW
-// output with voxel-contiguous stores.  Every output element is written once: no memset, no
-// atomics, and the per-voxel camera sum runs in the reference's camera order.
+// Voxel-major gather (volumetric_fusionnet.py:116-162, pose branch) into the channels-last input
+// of reduce_dim's stride-2 conv: out[b][y'][x'][z*(C+1) + c] (NHWC, z-major channels; the conv's
+// weight is permuted to match, so the convolution is the reference's).  A workgroup owns
+// POSE_TV consecutive voxels: (1) one thread per voxel projects it into every camera (the plan's
+// arithmetic), (2) each wave takes two voxels at a time with lanes = channels, reads the four
+// bilinear taps of every valid camera from the channels-last feature map (one contiguous C-float
+// row per tap), sums the cameras in the reference's order, divides by (count + 1e-7) and stores
+// the voxel's C+1 values as one contiguous row at each of its (reflect-padded) positions.  Every
+// output element is written exactly once: no memset, no atomics.
 constexpr int POSE_TV = 32;
 constexpr int POSE_MAXC = 256;      // channels held per lane: ceil(C / 64) <= 4
 
@@ -428,19 +429,19 @@ template <int NC>
 __global__ __launch_bounds__(256) void fuse_pose_fwd_k(vfd_voxel_desc d, const float* __restrict__ mlo,
                                                        const float* __restrict__ K, const float* __restrict__ Einv,
                                                        const float* __restrict__ feats, float* __restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) float tile[];      // [C+1][POSE_TV+1]
+  constexpr int CPL = POSE_MAXC / 64;
   __shared__ int s_base[POSE_TV][NC];
   __shared__ float s_w[POSE_TV][NC][4];
   __shared__ int s_cam[POSE_TV][NC];
   __shared__ unsigned s_in[POSE_TV][NC];
   __shared__ int s_cnt[POSE_TV];
   __shared__ float s_den[POSE_TV];
+  __shared__ float s_zf[POSE_TV];
   const int V = d.X * d.Y * d.Z;
   const int b = blockIdx.y;
   const int v0 = blockIdx.x * POSE_TV;
   const int hw = d.h * d.w;
-  const int C = d.C;
-  const int TS = POSE_TV + 1;
+  const int C = d.C, C1 = d.C + 1;
   if (threadIdx.x < POSE_TV) {
     const int t = threadIdx.x, v = v0 + t;
     int cnt = 0;
@@ -465,59 +466,82 @@ __global__ __launch_bounds__(256) void fuse_pose_fwd_k(vfd_voxel_desc d, const f
     }
     s_cnt[t] = cnt;
     s_den[t] = (float)cnt + 1e-7f;
-    tile[C * TS + t] = zsum / ((float)cnt + 1e-7f);
+    s_zf[t] = zsum / ((float)cnt + 1e-7f);
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const float* fb = feats + (size_t)b * NC * hw * C;
-  for (int t = wv; t < POSE_TV; t += 4) {
-    const int cnt = s_cnt[t];
-    float acc[POSE_MAXC / 64];
-#pragma unroll
-    for (int k = 0; k < POSE_MAXC / 64; ++k) acc[k] = 0.f;
-    for (int j = 0; j < cnt; ++j) {
-      const int cam = s_cam[t][j], base = s_base[t][j];
-      const float* fc = fb + (size_t)cam * hw * C;
-      float val[POSE_MAXC / 64];
-#pragma unroll
-      for (int k = 0; k < POSE_MAXC / 64; ++k) val[k] = 0.f;
-      const unsigned in = s_in[t][j];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (!(in >> q & 1u)) continue;          // out-of-range corner: zeros padding
-        const float wq = s_w[t][j][q];
-        const float* row = fc + (size_t)(base + tap_offset(q, d.w)) * C;
-#pragma unroll
-        for (int k = 0; k < POSE_MAXC / 64; ++k) {
-          const int ch = lane + 64 * k;
-          if (ch < C) val[k] += row[ch] * wq;
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < POSE_MAXC / 64; ++k) acc[k] += val[k];
-    }
-    const float den = s_den[t];
-#pragma unroll
-    for (int k = 0; k < POSE_MAXC / 64; ++k) {
-      const int ch = lane + 64 * k;
-      if (ch < C) tile[ch * TS + t] = acc[k] / den;
-    }
-  }
-  __syncthreads();
   const int P = d.pad_out ? 2 : 0;
   const int Yo = d.Y + P, Xo = d.X + P;
-  float* ob = out + (size_t)b * (C + 1) * d.Z * Yo * Xo;
-  for (int idx = threadIdx.x; idx < (C + 1) * POSE_TV; idx += blockDim.x) {
-    const int ch = idx / POSE_TV, t = idx % POSE_TV, v = v0 + t;
-    if (v >= V) continue;
-    const int xi = v % d.X, yi = (v / d.X) % d.Y, zi = v / (d.X * d.Y);
-    int rows[3], cols[3], nr, nc;
-    pad_sets(yi, d.Y, d.pad_out, rows, &nr);
-    pad_sets(xi, d.X, d.pad_out, cols, &nc);
-    const float o = tile[ch * TS + t];
-    float* plane = ob + ((size_t)ch * d.Z + zi) * Yo * Xo;
-    for (int a = 0; a < nr; ++a)
-      for (int c2 = 0; c2 < nc; ++c2) plane[rows[a] * Xo + cols[c2]] = o;
+  const size_t pix_stride = (size_t)d.Z * C1;
+  float* ob = out + (size_t)b * Yo * Xo * pix_stride;
+  for (int t0 = wv * 2; t0 < POSE_TV; t0 += 8) {
+    float acc[2][CPL];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) acc[u][k] = 0.f;
+    const int cmax = max(s_cnt[t0], s_cnt[t0 + 1]);
+    for (int j = 0; j < cmax; ++j) {
+      float val[2][CPL];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int t = t0 + u;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) val[u][k] = 0.f;
+        if (j >= s_cnt[t]) continue;
+        const float* fc = fb + (size_t)s_cam[t][j] * hw * C;
+        const int base = s_base[t][j];
+        const unsigned in = s_in[t][j];
+        // out-of-range taps (zeros padding) read pixel 0 with weight 0: branch-free loads
+        float f[4][CPL], wq[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const bool ok = (in >> q & 1u) != 0u;
+          wq[q] = ok ? s_w[t][j][q] : 0.f;
+          const float* row = fc + (size_t)(ok ? base + tap_offset(q, d.w) : 0) * C;
+#pragma unroll
+          for (int k = 0; k < CPL; ++k) {
+            const int ch = lane + 64 * k;
+            f[q][k] = row[ch < C ? ch : 0];
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int k = 0; k < CPL; ++k) val[u][k] += f[q][k] * wq[q];
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        if (j < s_cnt[t0 + u]) {
+#pragma unroll
+          for (int k = 0; k < CPL; ++k) acc[u][k] += val[u][k];
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int t = t0 + u, v = v0 + t;
+      if (v >= V) continue;
+      const float den = s_den[t];
+      const int xi = v % d.X, yi = (v / d.X) % d.Y, zi = v / (d.X * d.Y);
+      int rows[3], cols[3], nr, nc;
+      pad_sets(yi, d.Y, d.pad_out, rows, &nr);
+      pad_sets(xi, d.X, d.pad_out, cols, &nc);
+      float o[CPL];
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) o[k] = acc[u][k] / den;
+      const float zf = s_zf[t];
+      for (int a = 0; a < nr; ++a)
+        for (int c2 = 0; c2 < nc; ++c2) {
+          float* row = ob + ((size_t)rows[a] * Xo + cols[c2]) * pix_stride + (size_t)zi * C1;
+#pragma unroll
+          for (int k = 0; k < CPL; ++k) {
+            const int ch = lane + 64 * k;
+            if (ch < C) row[ch] = o[k];
+          }
+          if (lane == 0) row[C] = zf;
+        }
+    }
   }
 }
 
@@ -526,10 +550,9 @@ __global__ __launch_bounds__(256) void fuse_pose_fwd_k(vfd_voxel_desc d, const f
 // the scatter form of this kernel), so the backward is a gather:
 //   plan_index_k     once per step with the plan: per (batch, camera) CSR inverse index
 //                    pixel -> [(entry << 2) | tap] of every in-range bilinear tap;
-//   pose_grad_rows_k d_out (reflect-padded NCHW) -> voxel-major rows T[b][v][0:C] with the
-//                    padding copies folded back (one coalesced pass);
-//   fuse_pose_bwd_k  per pixel, lanes = channels: sum (T[voxel] / den) * w_tap over the pixel's
-//                    list (1-KB row loads), staged through LDS for coalesced NCHW stores.
+//   fuse_pose_bwd_k  per pixel, lanes = channels: sum (g[voxel] / den) * w_tap over the pixel's
+//                    list, g read as contiguous rows of the channels-last d_out (reflect-padding
+//                    copies folded back), staged through LDS for coalesced NCHW stores.
 constexpr int PIDX_THREADS = 1024;
 
 __global__ __launch_bounds__(PIDX_THREADS) void plan_index_k(vfd_voxel_desc d, const PlanEntry* __restrict__ plan,
@@ -587,59 +610,28 @@ __global__ __launch_bounds__(PIDX_THREADS) void plan_index_k(vfd_voxel_desc d, c
   }
 }
 
-constexpr int PGR_CH = 64;     // channels per transpose tile
-
-__global__ __launch_bounds__(256) void pose_grad_rows_k(vfd_voxel_desc d, const float* __restrict__ dout,
-                                                        float* __restrict__ rows) {
-  extern __shared__ float tile[];        // [PGR_CH][X + 1]
-  const int c0 = blockIdx.x * PGR_CH;
-  const int zy = blockIdx.y, zi = zy / d.Y, yi = zy % d.Y;
-  const int b = blockIdx.z;
-  const int X = d.X, XS = d.X + 1;
-  const int P = d.pad_out ? 2 : 0;
-  const int Yo = d.Y + P, Xo = d.X + P;
-  const size_t plane_sz = (size_t)d.Z * Yo * Xo;
-  const int nch = min(PGR_CH, d.C - c0);
-  int rws[3], nr;
-  pad_sets(yi, d.Y, d.pad_out, rws, &nr);
-  const float* gb = dout + (size_t)b * (d.C + 1) * plane_sz;
-  for (int i = threadIdx.x; i < nch * X; i += blockDim.x) {
-    const int c = i / X, xi = i % X;
-    int cols[3], nc;
-    pad_sets(xi, X, d.pad_out, cols, &nc);
-    const float* plane = gb + (size_t)(c0 + c) * plane_sz + (size_t)zi * Yo * Xo;
-    float g = 0.f;
-    for (int a = 0; a < nr; ++a)
-      for (int c2 = 0; c2 < nc; ++c2) g += plane[rws[a] * Xo + cols[c2]];
-    tile[c * XS + xi] = g;
-  }
-  __syncthreads();
-  float* rb = rows + ((size_t)b * d.X * d.Y * d.Z + (size_t)zy * X) * d.C + c0;
-  for (int i = threadIdx.x; i < X * nch; i += blockDim.x) {
-    const int xi = i / nch, c = i % nch;
-    rb[(size_t)xi * d.C + c] = tile[c * XS + xi];
-  }
-}
-
 constexpr int PBW_TP = 16;     // pixels per workgroup (4 per wave)
 constexpr int PBW_U = 4;       // list items in flight per wave
 
 __global__ __launch_bounds__(256) void fuse_pose_bwd_k(vfd_voxel_desc d, const PlanEntry* __restrict__ plan,
                                                        const int* __restrict__ row_ptr, const int* __restrict__ csr,
-                                                       const float* __restrict__ rows, float* __restrict__ dfeats) {
+                                                       const float* __restrict__ dout, float* __restrict__ dfeats) {
   extern __shared__ float otile[];       // [C][PBW_TP + 1]
   constexpr int CPL = POSE_MAXC / 64;
   const int hw = d.h * d.w;
   const int V = d.X * d.Y * d.Z;
-  const int C = d.C;
+  const int C = d.C, C1 = d.C + 1;
   const int bc = blockIdx.y, b = bc / d.N;
   const int q0 = blockIdx.x * PBW_TP;
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int P = d.pad_out ? 2 : 0;
+  const int Yo = d.Y + P, Xo = d.X + P;
+  const size_t pix_stride = (size_t)d.Z * C1;
   const PlanEntry* list = plan + (size_t)bc * V;
   const int* rp = row_ptr + (size_t)bc * (hw + 1);
   const int* cb = csr + (size_t)bc * 4 * V;
-  const float* rb = rows + (size_t)b * V * C;
+  const float* gb = dout + (size_t)b * Yo * Xo * pix_stride;
   for (int pi = 0; pi < PBW_TP / 4; ++pi) {
     const int ql = wv * (PBW_TP / 4) + pi;
     const int q = q0 + ql;
@@ -667,15 +659,36 @@ __global__ __launch_bounds__(256) void fuse_pose_bwd_k(vfd_voxel_desc d, const P
             vox[u] = (int)(e.meta & 0xFFFFFF);
           }
         }
+        // main row of every item first (all loads in flight), reflect-padding copies after
         float g[PBW_U][CPL];
+        int rows[PBW_U][3], cols[PBW_U][3], nr[PBW_U], nc[PBW_U], zoff[PBW_U];
 #pragma unroll
         for (int u = 0; u < PBW_U; ++u) {
-          const float* row = rb + (size_t)(vox[u] < 0 ? 0 : vox[u]) * C;
+          const int v = vox[u] < 0 ? 0 : vox[u];
+          const int xi = v % d.X, yi = (v / d.X) % d.Y, zi = v / (d.X * d.Y);
+          pad_sets(yi, d.Y, d.pad_out, rows[u], &nr[u]);
+          pad_sets(xi, d.X, d.pad_out, cols[u], &nc[u]);
+          zoff[u] = zi * C1;
+          const float* row = gb + ((size_t)rows[u][0] * Xo + cols[u][0]) * pix_stride + zoff[u];
 #pragma unroll
           for (int k = 0; k < CPL; ++k) {
             const int ch = lane + 64 * k;
-            g[u][k] = (vox[u] >= 0 && ch < C) ? row[ch] : 0.f;
+            g[u][k] = row[ch < C ? ch : 0];      // unconditional (voxel 0 for empty slots, weight 0)
           }
+        }
+#pragma unroll
+        for (int u = 0; u < PBW_U; ++u) {
+          if (vox[u] < 0 || nr[u] * nc[u] == 1) continue;
+          for (int a = 0; a < nr[u]; ++a)
+            for (int c2 = 0; c2 < nc[u]; ++c2) {
+              if (a == 0 && c2 == 0) continue;
+              const float* row = gb + ((size_t)rows[u][a] * Xo + cols[u][c2]) * pix_stride + zoff[u];
+#pragma unroll
+              for (int k = 0; k < CPL; ++k) {
+                const int ch = lane + 64 * k;
+                if (ch < C) g[u][k] += row[ch];
+              }
+            }
         }
         // reference order: d(mean) = g / den, then grid_sample's backward adds d(mean) * w
 #pragma unroll
@@ -752,138 +765,236 @@ __device__ __forceinline__ int tri_index(const vfd_voxel_desc& d, const Tri& t, 
 }
 
 // ------------------------------------------------------------------------------ K3 forward
-// Lanes are frustum pixels (coalesced stores of every output channel row); each lane reads
-// its 8 voxel rows as float4 vectors of the channels-last voxel grid (K1's output layout).
+// Frustum samples -> trilinear gather from the channels-last voxel grid (K1's output), written
+// into the channels-last input of reduce_dim's first conv: out[bc][y'][x'][d*Cv + c] (NHWC,
+// depth-major channels; the conv weight is permuted to match).  A workgroup owns 64 consecutive
+// pixels at one depth bin: one thread per sample computes the trilinear cell and weights into
+// LDS, then lanes = channels, so every corner read and every output write is one contiguous
+// Cv-float row; each wave keeps VP_U samples in flight.
+constexpr int VP_PX = 64;       // pixels per workgroup
+constexpr int VP_U = 4;         // samples in flight per wave
+
+struct TriLds {
+  int base[VP_PX];              // voxel index of corner 0 (may be out of range; see in)
+  unsigned in[VP_PX];
+  float w[VP_PX][8];
+};
+
+__device__ __forceinline__ void tri_to_lds(const vfd_voxel_desc& d, TriLds& tl, int j, const Tri& t) {
+  tl.base[j] = (t.z0 * d.Y + t.y0) * d.X + t.x0;
+  tl.in[j] = t.in;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) tl.w[j][k] = t.w[k];
+}
+
+__device__ __forceinline__ int corner_offset(const vfd_voxel_desc& d, int k) {
+  return (k & 1) + ((k >> 1) & 1) * d.X + (k >> 2) * d.X * d.Y;
+}
+
 template <int CV>
 __global__ __launch_bounds__(256) void voxel_project_fwd_k(vfd_voxel_desc d, const float* __restrict__ vox,
                                                            const float* __restrict__ invK,
                                                            const float* __restrict__ E,
                                                            float* __restrict__ out) {
+  __shared__ TriLds tl;
   const int hw = d.h * d.w;
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  const int dep_i = blockIdx.y;
-  const int bc = blockIdx.z;           // b * N + cam
-  if (p >= hw) return;
+  // XCD-aware numbering: workgroups are dealt to the 8 XCDs round-robin, so XCD k gets the
+  // contiguous task range [k*per, (k+1)*per) in (camera, depth bin, pixel chunk) order; the
+  // workgroups resident on one XCD then read one thin shell of the voxel grid from its L2
+  const int nchunk = (hw + VP_PX - 1) / VP_PX;
+  const int ntask = nchunk * d.D * d.B * d.N;
+  const int per = gridDim.x / 8;
+  const int task = (blockIdx.x % 8) * per + blockIdx.x / 8;
+  if (task >= ntask) return;
+  const int p0 = (task % nchunk) * VP_PX;
+  const int dep_i = (task / nchunk) % d.D;
+  const int bc = task / (nchunk * d.D);
   const int b = bc / d.N;
-  const int px = p % d.w, py = p / d.w;
-  Tri t = frustum_sample(d, invK + bc * 16, E + bc * 16, px, py, d.dbins[dep_i]);
+  const float dep = d.dbins[dep_i];
+  if (threadIdx.x < VP_PX) {
+    const int p = p0 + threadIdx.x;
+    Tri t;
+    t.in = 0;
+    t.x0 = t.y0 = t.z0 = 0;
+    if (p < hw) t = frustum_sample(d, invK + bc * 16, E + bc * 16, p % d.w, p / d.w, dep);
+    tri_to_lds(d, tl, threadIdx.x, t);
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int V = d.X * d.Y * d.Z;
   const float* vb = vox + (size_t)b * V * CV;
-  float acc[CV];
-#pragma unroll
-  for (int c = 0; c < CV; ++c) acc[c] = 0.f;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    if (!(t.in >> k & 1u)) continue;
-    const float4* row = reinterpret_cast<const float4*>(vb + (size_t)tri_index(d, t, k) * CV);
-    const float wk = t.w[k];
-#pragma unroll
-    for (int c4 = 0; c4 < CV / 4; ++c4) {
-      float4 q = row[c4];
-      acc[4 * c4 + 0] += q.x * wk;
-      acc[4 * c4 + 1] += q.y * wk;
-      acc[4 * c4 + 2] += q.z * wk;
-      acc[4 * c4 + 3] += q.w * wk;
-    }
-  }
   const int P = d.pad_out ? 2 : 0;
   const int ho = d.h + P, wo = d.w + P;
-  int rows[3], cols[3], nr, nc;
-  pad_sets(py, d.h, d.pad_out, rows, &nr);
-  pad_sets(px, d.w, d.pad_out, cols, &nc);
-  float* ob = out + (size_t)bc * CV * d.D * ho * wo;
+  const size_t pix_stride = (size_t)d.D * CV;
+  float* ob = out + (size_t)bc * ho * wo * pix_stride + (size_t)dep_i * CV;
+  const bool act = lane < CV;
+  for (int j0 = wv * (VP_PX / 4); j0 < (wv + 1) * (VP_PX / 4); j0 += VP_U) {
+    float acc[VP_U];
 #pragma unroll
-  for (int c = 0; c < CV; ++c) {
-    float* plane = ob + ((size_t)c * d.D + dep_i) * ho * wo;
-    for (int a = 0; a < nr; ++a)
-      for (int c2 = 0; c2 < nc; ++c2) plane[rows[a] * wo + cols[c2]] = acc[c];
+    for (int u = 0; u < VP_U; ++u) {
+      const int j = j0 + u;
+      const unsigned in = tl.in[j];
+      const int base = tl.base[j];
+      // branch-free: every corner is loaded (out-of-range ones from voxel 0 with weight 0, which
+      // adds +0: the reference's sum over in-range corners, same order), so all 8 loads of the
+      // VP_U samples are in flight before the first FMA
+      float v[8], w[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const bool ok = (in >> k & 1u) != 0u;
+        const int idx = ok ? base + corner_offset(d, k) : 0;
+        v[k] = vb[(size_t)idx * CV + (act ? lane : 0)];
+        w[k] = ok ? tl.w[j][k] : 0.f;
+      }
+      float a = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) a += v[k] * w[k];
+      acc[u] = a;
+    }
+#pragma unroll
+    for (int u = 0; u < VP_U; ++u) {
+      const int p = p0 + j0 + u;
+      if (p >= hw || !act) continue;
+      const int px = p % d.w, py = p / d.w;
+      int rows[3], cols[3], nr, nc;
+      pad_sets(py, d.h, d.pad_out, rows, &nr);
+      pad_sets(px, d.w, d.pad_out, cols, &nc);
+      for (int a = 0; a < nr; ++a)
+        for (int c2 = 0; c2 < nc; ++c2) ob[((size_t)rows[a] * wo + cols[c2]) * pix_stride + lane] = acc[u];
+    }
   }
 }
 
 // ------------------------------------------------------------------------------ K3 backward
-// A block owns 64 consecutive frustum pixels at one depth bin.  The (reflect-folded) gradient
-// tile [Cv x 64] is staged through LDS with coalesced row loads, then each wave walks 16
-// samples with lanes = channels: consecutive samples that fall in the same voxel cell are
-// merged in registers (runs are long in the near field) and flushed as 256-B rows of f32
-// atomics into the channels-last voxel gradient.
+// f32 atomics run at one chip-wide rate (~1.3 TB/s of added bytes), so this kernel is sized by
+// how many voxel rows it flushes.  A workgroup owns 64 consecutive pixels x VPB_TD depth bins;
+// per-sample cells and weights go to LDS, then each wave walks the 64 pixels of one depth bin
+// with lanes = channels, reading each sample's (reflect-folded) upstream gradient as one
+// contiguous row of the channels-last d_out.  The wave keeps the 8 corner accumulators of the
+// current cell in registers; on moving to a neighbouring cell the corners the two cells share
+// are carried over (remapped) instead of flushed, so a voxel row is flushed once per run of
+// samples around it rather than once per sample.
+constexpr int VPB_TD = 4;       // depth bins per workgroup (one per wave)
+constexpr int VPB_S = VP_PX * VPB_TD;
+
+struct CellLds {
+  short x0[VPB_S], y0[VPB_S], z0[VPB_S];
+  unsigned char in[VPB_S];
+  float w[VPB_S][8];
+};
+
 template <int CV>
 __global__ __launch_bounds__(256) void voxel_project_bwd_k(vfd_voxel_desc d, const float* __restrict__ dout,
                                                            const float* __restrict__ invK,
                                                            const float* __restrict__ E,
                                                            float* __restrict__ dvox) {
-  constexpr int TP = 64;                        // pixels per block
-  constexpr int CPL = (CV + 63) / 64;
-  __shared__ float tile[CV][TP + 1];
+  __shared__ CellLds cl;
   const int hw = d.h * d.w;
-  const int p0 = blockIdx.x * TP;
-  const int dep_i = blockIdx.y;
+  const int p0 = blockIdx.x * VP_PX;
+  const int d0 = blockIdx.y * VPB_TD;
   const int bc = blockIdx.z;
   const int b = bc / d.N;
-  const int P = d.pad_out ? 2 : 0;
-  const int ho = d.h + P, wo = d.w + P;
-  const float* gb = dout + (size_t)bc * CV * d.D * ho * wo;
-  for (int i = threadIdx.x; i < CV * TP; i += blockDim.x) {
-    const int c = i / TP, j = i % TP, p = p0 + j;
-    float g = 0.f;
-    if (p < hw) {
-      const int px = p % d.w, py = p / d.w;
-      int rows[3], cols[3], nr, nc;
-      pad_sets(py, d.h, d.pad_out, rows, &nr);
-      pad_sets(px, d.w, d.pad_out, cols, &nc);
-      const float* plane = gb + ((size_t)c * d.D + dep_i) * ho * wo;
-      for (int a = 0; a < nr; ++a)
-        for (int c2 = 0; c2 < nc; ++c2) g += plane[rows[a] * wo + cols[c2]];
-    }
-    tile[c][j] = g;
+  for (int i = threadIdx.x; i < VPB_S; i += blockDim.x) {
+    const int p = p0 + i % VP_PX, di = d0 + i / VP_PX;
+    Tri t;
+    t.in = 0;
+    t.x0 = t.y0 = t.z0 = 0;
+    if (p < hw && di < d.D) t = frustum_sample(d, invK + bc * 16, E + bc * 16, p % d.w, p / d.w, d.dbins[di]);
+    cl.x0[i] = (short)t.x0;
+    cl.y0[i] = (short)t.y0;
+    cl.z0[i] = (short)t.z0;
+    cl.in[i] = (unsigned char)t.in;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) cl.w[i][k] = t.w[k];
   }
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
+  const int dep_i = d0 + wv;
+  if (dep_i >= d.D) return;
+  const int P = d.pad_out ? 2 : 0;
+  const int ho = d.h + P, wo = d.w + P;
+  const size_t pix_stride = (size_t)d.D * CV;
+  const float* gb = dout + (size_t)bc * ho * wo * pix_stride + (size_t)dep_i * CV;
+  const bool act = lane < CV;
+  const int cl_lane = act ? lane : 0;
   const int V = d.X * d.Y * d.Z;
   float* vb = dvox + (size_t)b * V * CV;
-  float acc[CPL][8];
-  Tri cur;
-  cur.in = 0;
-  cur.x0 = cur.y0 = cur.z0 = -100;
-  bool open = false;
-  auto flush = [&]() {
-    if (!open) return;
+  const int XY = d.X * d.Y;
+  float acc[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      if (!(cur.in >> k & 1u)) continue;
-      float* row = vb + (size_t)tri_index(d, cur, k) * CV;
-#pragma unroll
-      for (int q = 0; q < CPL; ++q) {
-        int c = lane + 64 * q;
-        if (c < CV) atomicAdd(row + c, acc[q][k]);
-      }
-    }
+  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  int cx = 0, cy = 0, cz = 0;
+  unsigned cin = 0;
+  auto row_of = [&](int x, int y, int z, int k) {
+    return vb + (size_t)((z + (k >> 2)) * XY + (y + ((k >> 1) & 1)) * d.X + x + (k & 1)) * CV + cl_lane;
   };
-  for (int jj = 0; jj < TP / 4; ++jj) {
-    const int j = wv * (TP / 4) + jj;
-    const int p = p0 + j;
-    if (p >= hw) break;
-    Tri t = frustum_sample(d, invK + bc * 16, E + bc * 16, p % d.w, p / d.w, d.dbins[dep_i]);
-    if (t.in == 0) continue;
-    const bool same = open && t.x0 == cur.x0 && t.y0 == cur.y0 && t.z0 == cur.z0;
-    if (!same) {
-      flush();
-      cur = t;
-      open = true;
+  constexpr int CH = 16;                 // gradient rows prefetched per chunk
+  for (int j0 = 0; j0 < VP_PX; j0 += CH) {
+    float gs[CH];
 #pragma unroll
-      for (int q = 0; q < CPL; ++q)
-#pragma unroll
-        for (int k = 0; k < 8; ++k) acc[q][k] = 0.f;
+    for (int jj = 0; jj < CH; ++jj) {
+      const int p = min(p0 + j0 + jj, hw - 1);
+      const int px = p % d.w, py = p / d.w;
+      gs[jj] = gb[((size_t)(py + P / 2) * wo + px + P / 2) * pix_stride + cl_lane];
     }
 #pragma unroll
-    for (int q = 0; q < CPL; ++q) {
-      int c = lane + 64 * q;
-      float g = c < CV ? tile[c][j] : 0.f;
+    for (int jj = 0; jj < CH; ++jj) {
+      const int p = p0 + j0 + jj;
+      if (p >= hw) continue;
+      const int px = p % d.w, py = p / d.w;
+      int rows[3], cols[3], nr, nc;
+      pad_sets(py, d.h, d.pad_out, rows, &nr);
+      pad_sets(px, d.w, d.pad_out, cols, &nc);
+      if (nr * nc == 1) continue;
+      for (int a = 0; a < nr; ++a)
+        for (int c2 = 0; c2 < nc; ++c2)
+          if (a || c2) gs[jj] += gb[((size_t)rows[a] * wo + cols[c2]) * pix_stride + cl_lane];
+    }
+    for (int jj = 0; jj < CH; ++jj) {
+      const int i = wv * VP_PX + j0 + jj;
+      const int p = p0 + j0 + jj;
+      const unsigned in = cl.in[i];
+      if (p >= hw || in == 0) continue;
+      const int nx = cl.x0[i], ny = cl.y0[i], nz = cl.z0[i];
+      if (!(cin && nx == cx && ny == cy && nz == cz)) {
+        // switch cells: corners shared with the new cell move to its accumulator slot, the
+        // others are flushed (only in-range corners are real voxels)
+        const int dx = cx - nx, dy = cy - ny, dz = cz - nz;
+        float nacc[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) acc[q][k] += g * t.w[k];
+        for (int k = 0; k < 8; ++k) nacc[k] = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          if (!(cin >> k & 1u)) continue;
+          const int tx = (k & 1) + dx, ty = ((k >> 1) & 1) + dy, tz = (k >> 2) + dz;
+          const bool keep = tx >= 0 && tx <= 1 && ty >= 0 && ty <= 1 && tz >= 0 && tz <= 1;
+          if (keep) {
+            const int kt = tx + 2 * ty + 4 * tz;
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+              if (q == kt) nacc[q] += acc[k];
+          } else if (act) {
+            atomicAdd(row_of(cx, cy, cz, k), acc[k]);
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] = nacc[k];
+        cx = nx;
+        cy = ny;
+        cz = nz;
+        cin = in;
+      }
+      const float g = gs[jj];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += g * cl.w[i][k];
     }
   }
-  flush();
+  if (cin && act) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (cin >> k & 1u) atomicAdd(row_of(cx, cy, cz, k), acc[k]);
+  }
 }
 
 }  // namespace vfd
@@ -1003,39 +1114,30 @@ int vfd_fuse_pose_fwd(const vfd_voxel_desc* d, const float* mask_lo, const float
   VFD_REQUIRE(d->N >= 1 && d->N <= 8, "fuse_pose: N=%d outside [1, 8]", d->N);
   hipStream_t s = (hipStream_t)stream;
   const int V = d->X * d->Y * d->Z;
-  const size_t lds = (size_t)(d->C + 1) * (POSE_TV + 1) * sizeof(float);
   dim3 grid(cdiv(V, POSE_TV), d->B);
   ProfScope ps(K_FUSE_POSE_FWD, s);
   switch (d->N) {
-#define VFD_CASE(n) case n: fuse_pose_fwd_k<n><<<grid, 256, lds, s>>>(*d, mask_lo, K, Einv, feats_cl, out); break;
+#define VFD_CASE(n) case n: fuse_pose_fwd_k<n><<<grid, 256, 0, s>>>(*d, mask_lo, K, Einv, feats_cl, out); break;
     VFD_CASE(1) VFD_CASE(2) VFD_CASE(3) VFD_CASE(4) VFD_CASE(5) VFD_CASE(6) VFD_CASE(7) VFD_CASE(8)
 #undef VFD_CASE
   }
   return fail_launch("fuse_pose_fwd");
 }
 
-size_t vfd_fuse_pose_bwd_workspace(const vfd_voxel_desc* d) {
-  return (size_t)d->B * d->X * d->Y * d->Z * d->C * sizeof(float);
-}
-
 int vfd_fuse_pose_bwd(const vfd_voxel_desc* d, const void* plan, const int* counts, const float* d_out,
-                      float* d_feats, void* workspace, size_t ws_bytes, void* stream) {
+                      float* d_feats, void* stream) {
   int st = check_voxel_desc(d);
   if (st) return st;
   (void)counts;
   VFD_REQUIRE(d->C >= 1 && d->C <= POSE_MAXC, "fuse_pose: C=%d outside [1, %d]", d->C, POSE_MAXC);
-  VFD_REQUIRE(ws_bytes >= vfd_fuse_pose_bwd_workspace(d), "fuse_pose_bwd: workspace too small");
   VFD_REQUIRE((2 * (size_t)d->h * d->w + PIDX_THREADS) * sizeof(int) <= 160 * 1024, "feature map %dx%d too large", d->h, d->w);
   hipStream_t s = (hipStream_t)stream;
   const int hw = d->h * d->w;
   const int* row_ptr = (const int*)((const char*)plan + plan_entries_bytes(d));
   const int* csr = (const int*)((const char*)row_ptr + plan_rowptr_bytes(d));
-  float* rows = (float*)workspace;
   ProfScope ps(K_FUSE_POSE_BWD, s);
-  pose_grad_rows_k<<<dim3(cdiv(d->C, PGR_CH), d->Y * d->Z, d->B), 256, (size_t)PGR_CH * (d->X + 1) * sizeof(float), s>>>(
-      *d, d_out, rows);
   fuse_pose_bwd_k<<<dim3(cdiv(hw, PBW_TP), d->B * d->N), 256, (size_t)d->C * (PBW_TP + 1) * sizeof(float), s>>>(
-      *d, (const PlanEntry*)plan, row_ptr, csr, rows, d_feats);
+      *d, (const PlanEntry*)plan, row_ptr, csr, d_out, d_feats);
   return fail_launch("fuse_pose_bwd");
 }
 
@@ -1045,7 +1147,9 @@ int vfd_voxel_project_fwd(const vfd_voxel_desc* d, const float* vox, const float
   if (st) return st;
   VFD_REQUIRE(d->dbins != nullptr && d->D > 0, "depth bins not set");
   hipStream_t s = (hipStream_t)stream;
-  dim3 grid(cdiv(d->h * d->w, 256), d->D, d->B * d->N);
+  VFD_REQUIRE(d->Cv <= 64, "voxel_project: Cv=%d > 64", d->Cv);
+  const int ntask = cdiv(d->h * d->w, VP_PX) * d->D * d->B * d->N;
+  dim3 grid(8 * cdiv(ntask, 8));
   ProfScope ps(K_VPROJ_FWD, s);
   switch (d->Cv) {
     case 8: voxel_project_fwd_k<8><<<grid, 256, 0, s>>>(*d, vox, invK, E, out); break;
@@ -1063,9 +1167,10 @@ int vfd_voxel_project_bwd(const vfd_voxel_desc* d, const float* d_out, const flo
   if (st) return st;
   VFD_REQUIRE(d->dbins != nullptr && d->D > 0, "depth bins not set");
   hipStream_t s = (hipStream_t)stream;
+  VFD_REQUIRE(d->Cv <= 64, "voxel_project: Cv=%d > 64", d->Cv);
   const size_t V = (size_t)d->X * d->Y * d->Z;
   (void)hipMemsetAsync(d_vox, 0, (size_t)d->B * V * d->Cv * sizeof(float), s);
-  dim3 grid(cdiv(d->h * d->w, 64), d->D, d->B * d->N);
+  dim3 grid(cdiv(d->h * d->w, VP_PX), cdiv(d->D, VPB_TD), d->B * d->N);
   ProfScope ps(K_VPROJ_BWD, s);
   switch (d->Cv) {
     case 8: voxel_project_bwd_k<8><<<grid, 256, 0, s>>>(*d, d_out, invK, E, d_vox); break;

@@ -11,10 +11,13 @@ pose: BEV feature map).  What changes is how it is computed:
   (voxel, camera) pair and applies depth column, bias, LeakyReLU and the count masks in
   registers — no [B,6,257,V] intermediates;
 * K3 resamples the voxel grid on all camera frustums in one launch and writes the
-  reflect-padded layout `reduce_dim`'s first conv reads (no separate F.pad pass); the six
-  cameras' `reduce_dim` runs as one batched conv;
-* pose mode: K2 writes the camera-mean voxel features straight into the reflect-padded
-  [B, (C+1)Z, Y+2, X+2] map of the stride-2 conv.
+  reflect-padded, channels-last (NHWC) layout `reduce_dim`'s first conv reads (no F.pad pass,
+  no layout transposes); the six cameras' `reduce_dim` runs as one batched NHWC conv;
+* pose mode: K2 writes the camera-mean voxel features straight into the reflect-padded NHWC
+  [B, Y+2, X+2, Z(C+1)] map of the stride-2 conv.
+The two kernels order their channels voxel-row-major (z*(C+1)+c, d*Cv+c) so that every gather
+and store is a contiguous row; `_reduce` permutes the conv weight's input channels to match,
+which leaves the convolution (and the parameters / state dict) exactly the reference's.
 """
 import torch
 import torch.nn as nn
@@ -76,10 +79,17 @@ class VFNet(nn.Module):
         return inputs[key]
 
     def _reduce(self, x_padded):
-        """reduce_dim with the first conv reading the kernel's reflect-padded output."""
+        """reduce_dim with the first conv reading the kernel's channels-last, reflect-padded output
+        (padding 0; its weight's input channels permuted to the kernel's channel order).  Both
+        convs run channels-last (MIOpen NHWC implicit GEMM, no layout transposes); the result is
+        handed on in the usual contiguous NCHW layout."""
         c0, c1 = self.reduce_dim[0], self.reduce_dim[3]
-        x = F.leaky_relu(F.conv2d(x_padded, c0.weight, c0.bias, stride=self.stride), 0.1, inplace=True)
-        return F.leaky_relu(c1(x), 0.1, inplace=True)
+        if self.model == 'depth':
+            w0 = KN.proj_conv_weight(c0.weight, self.v_dim_o[-1], self.proj_d_bins)
+        else:
+            w0 = KN.pose_conv_weight(c0.weight, self.feat_in_dim + 1, self.z_dim)
+        x = F.leaky_relu(F.conv2d(x_padded, w0, c0.bias, stride=self.stride), 0.1, inplace=True)
+        return F.leaky_relu(c1(x), 0.1, inplace=True).contiguous()
 
     def folded_weights(self):
         """Per-camera [N, 2Cv, C] feature columns of (W_no, W_o[group]) and the [3, Cv] depth columns."""

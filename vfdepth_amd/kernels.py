@@ -144,8 +144,44 @@ class FusionPlan:
                                     self.buf.data_ptr(), self.counts.data_ptr(), L.stream()), 'fusion_plan')
 
 
+def _channels_last(t, what):
+    """Device fp32 tensor in channels-last (NHWC) memory order (no copy when it already is)."""
+    if not torch.is_tensor(t) or not t.is_cuda:
+        raise RuntimeError(f'{what}: the VFDepth hot path runs only on a HIP device')
+    if t.dtype != torch.float32:
+        t = t.float()
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+def pose_conv_weight(w, C1, Z):
+    """reduce_dim[0] weight [O, C1*Z, kh, kw] (reference channel c*Z + z) -> the z-major order
+    z*C1 + c of FusePose's output; differentiable (a view + one gather)."""
+    O = w.shape[0]
+    return w.view(O, C1, Z, *w.shape[2:]).transpose(1, 2).reshape(O, Z * C1, *w.shape[2:])
+
+
+def proj_conv_weight(w, Cv, D):
+    """reduce_dim[0] weight [O, Cv*D, kh, kw] (reference channel c*D + d) -> the depth-major
+    order d*Cv + c of VoxelProject's output."""
+    O = w.shape[0]
+    return w.view(O, Cv, D, *w.shape[2:]).transpose(1, 2).reshape(O, D * Cv, *w.shape[2:])
+
+
+def pose_to_reference(out, C1, Z):
+    """FusePose output -> the reference's [B, C1*Z, Y+2, X+2] channel order (tests, tools)."""
+    B, _, H, W = out.shape
+    return out.reshape(B, Z, C1, H, W).transpose(1, 2).reshape(B, C1 * Z, H, W)
+
+
+def proj_to_reference(out, Cv, D):
+    """VoxelProject output -> the reference's [B*N, Cv*D, h+2, w+2] channel order."""
+    BN, _, H, W = out.shape
+    return out.reshape(BN, D, Cv, H, W).transpose(1, 2).reshape(BN, Cv * D, H, W)
+
+
 class FusePose(torch.autograd.Function):
-    """K2: feats [B,N,C,h,w] -> mean voxel features, reflect-padded NCHW [B,(C+1)Z,Y+2,X+2]."""
+    """K2: feats [B,N,C,h,w] -> mean voxel features as the channels-last, reflect-padded input of
+    reduce_dim's stride-2 conv: logical [B, Z*(C+1), Y+2, X+2], channel z*(C+1) + c."""
 
     @staticmethod
     def forward(ctx, space, plan, feats):
@@ -153,7 +189,8 @@ class FusePose(torch.autograd.Function):
         feats = _dev(feats, 'feats')
         B, N, C = feats.shape[:3]
         feats_cl = feats.flatten(3).transpose(2, 3).contiguous()        # [B, N, h*w, C]
-        out = torch.empty(B, (C + 1) * space.Z, space.Y + 2, space.X + 2, device=feats.device)
+        out = torch.empty(B, (C + 1) * space.Z, space.Y + 2, space.X + 2, device=feats.device,
+                          memory_format=torch.channels_last)
         d = space.desc(B, N, C=C)
         L.check(lib.vfd_fuse_pose_fwd(ctypes.byref(d), plan.mask_lo.data_ptr(), plan.K.data_ptr(),
                                       plan.Einv.data_ptr(), feats_cl.data_ptr(), out.data_ptr(), L.stream()),
@@ -165,19 +202,17 @@ class FusePose(torch.autograd.Function):
     def backward(ctx, g):
         lib = L.load()
         B, N, C = ctx.shape[:3]
-        g = _dev(g, 'grad')
+        g = _channels_last(g, 'grad')
         dfeats = torch.empty(ctx.shape, device=g.device)
         d = ctx.space.desc(B, N, C=C)
-        nbytes = lib.vfd_fuse_pose_bwd_workspace(ctypes.byref(d))
-        ws = _ws(nbytes, g.device)
         L.check(lib.vfd_fuse_pose_bwd(ctypes.byref(d), ctx.plan.buf.data_ptr(), ctx.plan.counts.data_ptr(),
-                                      g.data_ptr(), dfeats.data_ptr(), ws.data_ptr(), nbytes, L.stream()),
-                'fuse_pose_bwd')
+                                      g.data_ptr(), dfeats.data_ptr(), L.stream()), 'fuse_pose_bwd')
         return None, None, dfeats
 
 
 class VoxelProject(torch.autograd.Function):
-    """K3: voxel features [B,V,Cv] -> frustum features, reflect-padded [B*N, Cv*D, h+2, w+2]."""
+    """K3: voxel features [B,V,Cv] -> frustum features as the channels-last, reflect-padded input
+    of reduce_dim's first conv: logical [B*N, D*Cv, h+2, w+2], channel d*Cv + c."""
 
     @staticmethod
     def forward(ctx, space, vox, invK, E):
@@ -185,7 +220,8 @@ class VoxelProject(torch.autograd.Function):
         vox, invK, E = (_dev(t, n) for t, n in ((vox, 'voxel'), (invK, 'inv_K'), (E, 'extrinsics')))
         B, V, Cv = vox.shape
         N = E.shape[1]
-        out = torch.empty(B * N, Cv * space.D, space.h + 2, space.w + 2, device=vox.device)
+        out = torch.empty(B * N, Cv * space.D, space.h + 2, space.w + 2, device=vox.device,
+                          memory_format=torch.channels_last)
         d = space.desc(B, N, Cv=Cv)
         L.check(lib.vfd_voxel_project_fwd(ctypes.byref(d), vox.data_ptr(), invK.data_ptr(), E.data_ptr(),
                                           out.data_ptr(), L.stream()), 'voxel_project_fwd')
@@ -198,7 +234,7 @@ class VoxelProject(torch.autograd.Function):
         lib = L.load()
         invK, E = ctx.saved_tensors
         B, N, V, Cv = ctx.shape
-        g = _dev(g, 'grad')
+        g = _channels_last(g, 'grad')
         dvox = torch.empty(B, V, Cv, device=g.device)
         d = ctx.space.desc(B, N, Cv=Cv)
         L.check(lib.vfd_voxel_project_bwd(ctypes.byref(d), g.data_ptr(), invK.data_ptr(), E.data_ptr(),

@@ -344,6 +344,14 @@ def test_graph_replay_matches_eager():
     from vfdepth_amd.vfdepth import VFDepthAlgo
     cfg = G.step_cfg()
     batch = synth.make_batch(cfg, seed=99, device=DEV)
+    # static scene (context frames = target frame): the identity loss is ~1e-5 everywhere, far
+    # below every reprojection loss, so no auto-mask decision sits near a tie and the two runs'
+    # different MIOpen rounding cannot flip one
+    for f in cfg['training']['frame_ids'][1:]:
+        for s in cfg['training']['scales']:
+            for key in ('color', 'color_aug'):
+                if (key, f, s) in batch:
+                    batch[(key, f, s)] = batch[(key, 0, s)].clone()
     algos, init = [], {}
     for _ in range(2):
         a = VFDepthAlgo(cfg, 0)
@@ -381,7 +389,7 @@ def test_graph_replay_matches_eager():
     # gradients; compare the gradients as one vector per net: ||g_graph - g_eager|| / ||g_eager||
     flips = sum(int((graphed.outputs[('cam', c)][('reproj_mask', 0)] != out_e[('cam', c)][('reproj_mask', 0)]).sum())
                 for c in range(cfg['data']['num_cams']))
-    assert flips <= 1e-3 * cfg['data']['num_cams'] * cfg['training']['height'] * cfg['training']['width']
+    assert flips == 0, f'{flips} auto-mask flips between graph replay and eager'
     for net in ('depth_net', 'pose_net'):
         pg = dict(algos[0].models[net].named_parameters())
         diff = ref = 0.0
@@ -389,7 +397,7 @@ def test_graph_replay_matches_eager():
             diff += float((pg[name].grad.double() - p.grad.double()).pow(2).sum())
             ref += float(p.grad.double().pow(2).sum())
         rel = (diff / ref) ** 0.5
-        assert rel < (1e-4 if flips == 0 else 1e-2), f'{net}: gradient rel diff {rel:.3g} ({flips} auto-mask flips)'
+        assert rel < 1e-3, f'{net}: gradient rel diff {rel:.3g} ({flips} auto-mask flips)'
     # a second replay draws fresh identity noise and keeps training
     l2 = graphed()
     assert torch.isfinite(l2['total_loss']).item()

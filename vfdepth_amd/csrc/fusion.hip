@@ -833,8 +833,9 @@ __global__ __launch_bounds__(256) void voxel_project_fwd_k(vfd_voxel_desc d, con
 #pragma unroll
     for (int u = 0; u < VP_U; ++u) {
       const int j = j0 + u;
-      const unsigned in = tl.in[j];
-      const int base = tl.base[j];
+      // per-sample values are wave-uniform: keep them (and the corner addresses) scalar
+      const unsigned in = (unsigned)__builtin_amdgcn_readfirstlane((int)tl.in[j]);
+      const int base = __builtin_amdgcn_readfirstlane(tl.base[j]);
       // branch-free: every corner is loaded (out-of-range ones from voxel 0 with weight 0, which
       // adds +0: the reference's sum over in-range corners, same order), so all 8 loads of the
       // VP_U samples are in flight before the first FMA
@@ -954,9 +955,11 @@ __global__ __launch_bounds__(256) void voxel_project_bwd_k(vfd_voxel_desc d, con
     for (int jj = 0; jj < CH; ++jj) {
       const int i = wv * VP_PX + j0 + jj;
       const int p = p0 + j0 + jj;
-      const unsigned in = cl.in[i];
+      const unsigned in = (unsigned)__builtin_amdgcn_readfirstlane((int)cl.in[i]);
       if (p >= hw || in == 0) continue;
-      const int nx = cl.x0[i], ny = cl.y0[i], nz = cl.z0[i];
+      const int nx = __builtin_amdgcn_readfirstlane((int)cl.x0[i]);
+      const int ny = __builtin_amdgcn_readfirstlane((int)cl.y0[i]);
+      const int nz = __builtin_amdgcn_readfirstlane((int)cl.z0[i]);
       if (!(cin && nx == cx && ny == cy && nz == cz)) {
         // switch cells: corners shared with the new cell move to its accumulator slot, the
         // others are flushed (only in-range corners are real voxels)

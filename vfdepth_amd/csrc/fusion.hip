@@ -341,7 +341,8 @@ struct PlanEntry {
   float fx, fy;      // ix - x0, iy - y0 (exact in fp32; weights are rebuilt bit-identically)
   float z;           // camera-frame depth of the voxel
   float den;         // count + 1e-7 (pose-mode mean denominator, volumetric_fusionnet.py:162)
-  float pad[2];
+  int16_t x0, y0;    // tap 0 (may be -1: zeros padding)
+  uint32_t pad;
 };
 static_assert(sizeof(PlanEntry) == 32, "plan entry must stay 32 B");
 
@@ -405,7 +406,9 @@ __global__ __launch_bounds__(256) void fusion_plan_k(vfd_voxel_desc d, const flo
       e.fy = g[c].iy - floorf(g[c].iy);
       e.z = g[c].z;
       e.den = (float)cnt + 1e-7f;
-      e.pad[0] = e.pad[1] = 0.f;
+      e.x0 = (int16_t)bl.x0;
+      e.y0 = (int16_t)bl.y0;
+      e.pad = 0;
       plan[((size_t)b * NC + c) * V + off] = e;
     }
     __syncthreads();
@@ -555,32 +558,80 @@ __global__ __launch_bounds__(256) void fuse_pose_fwd_k(vfd_voxel_desc d, const f
 //                    copies folded back), staged through LDS for coalesced NCHW stores.
 constexpr int PIDX_THREADS = 1024;
 
-__global__ __launch_bounds__(PIDX_THREADS) void plan_index_k(vfd_voxel_desc d, const PlanEntry* __restrict__ plan,
-                                                             const int* __restrict__ counts, int* __restrict__ row_ptr,
-                                                             int* __restrict__ csr) {
-  extern __shared__ int sm[];
-  const int hw = d.h * d.w;
-  int* cnt = sm;                 // [hw]
-  int* cur = sm + hw;            // [hw]
-  int* part = sm + 2 * hw;       // [PIDX_THREADS]
-  const int bc = blockIdx.x;
-  const int V = d.X * d.Y * d.Z;
-  const int t = threadIdx.x;
-  for (int i = t; i < hw; i += PIDX_THREADS) cnt[i] = 0;
-  __syncthreads();
-  const int n = counts[bc];
-  const PlanEntry* list = plan + (size_t)bc * V;
-  for (int i = t; i < n; i += PIDX_THREADS) {
-    const PlanEntry e = list[i];
-    const unsigned in = e.meta >> 28;
+// K2 backward = the transpose of a bilinear gather: every visible (voxel, camera) pair adds
+// w_q * g[voxel] / den to the 4 pixels of its tap footprint.  The pixel map is cut into 4x4
+// tiles; each tile owns the bucket of plan entries whose footprint touches it (an entry on a
+// tile border is listed by every tile it touches, its weights masked to that tile's taps), so a
+// workgroup reads each of its voxel rows from HBM exactly once, accumulates in registers
+// (16 pixels x C/64 channels per lane) and writes its tile with plain stores: no atomics, no
+// inverse pixel index, no re-reads through L2.
+constexpr int PT = 4;              // tile side (pixels)
+constexpr int PT2 = PT * PT;
+
+struct TileItem {
+  uint32_t pz;       // padded XY position in d_out (bits 0-19) | z (20-27) | reflect copies exist (bit 28)
+  float den;         // count + 1e-7 (volumetric_fusionnet.py:162)
+  float w[4];        // ATen bilinear weights of taps (x0,y0) (x0+1,y0) (x0,y0+1) (x0+1,y0+1); 0 outside the tile
+  int32_t lxy;       // tap 0 relative to the tile origin: (ly + 1) * 8 + (lx + 1), lx, ly in [-1, PT-1]
+  uint32_t pad;
+};
+static_assert(sizeof(TileItem) == 32, "tile item must stay 32 B");
+
+__device__ __forceinline__ int tiles_x(const vfd_voxel_desc& d) { return (d.w + PT - 1) / PT; }
+__device__ __forceinline__ int tiles_y(const vfd_voxel_desc& d) { return (d.h + PT - 1) / PT; }
+
+// Tiles touched by an entry's in-range taps: bit (ty - ty0) * 2 + (tx - tx0) over the 2x2 tile
+// block starting at (tx0, ty0) = tile of tap 0 (taps out of the map never count).
+__device__ __forceinline__ unsigned entry_tiles(const vfd_voxel_desc& d, const PlanEntry& e, int* tx0, int* ty0) {
+  const unsigned in = e.meta >> 28;
+  const int x0 = e.x0, y0 = e.y0;
+  // tap 0 may sit at x0 = -1 / y0 = -1 (left/top zeros padding): floor division
+  *tx0 = x0 >= 0 ? x0 / PT : -1;
+  *ty0 = y0 >= 0 ? y0 / PT : -1;
+  unsigned m = 0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (in >> q & 1u) atomicAdd(&cnt[e.base + tap_offset(q, d.w)], 1);
+  for (int q = 0; q < 4; ++q)
+    if (in >> q & 1u) {
+      const int x = x0 + (q & 1), y = y0 + (q >> 1);
+      m |= 1u << ((y / PT - *ty0) * 2 + (x / PT - *tx0));
+    }
+  return m;
+}
+
+// Tile counters see ~100 adders each; a workgroup first histograms its 256 entries in LDS and
+// then adds one count per touched tile (entries of one workgroup are neighbouring voxels, so
+// they touch a handful of tiles).
+__global__ __launch_bounds__(256) void plan_count_k(vfd_voxel_desc d, const PlanEntry* __restrict__ plan,
+                                                    const int* __restrict__ counts, int* __restrict__ tile_cnt) {
+  extern __shared__ int hist[];          // [nt]
+  const int bc = blockIdx.y;
+  const int V = d.X * d.Y * d.Z, ntx = tiles_x(d), nt = ntx * tiles_y(d);
+  const int n = counts[bc];
+  if ((int)(blockIdx.x * blockDim.x) >= n) return;     // whole workgroup beyond the list
+  for (int i = threadIdx.x; i < nt; i += blockDim.x) hist[i] = 0;
+  __syncthreads();
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const PlanEntry e = plan[(size_t)bc * V + i];
+    int tx0, ty0;
+    const unsigned m = entry_tiles(d, e, &tx0, &ty0);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      if (m >> t & 1u) atomicAdd(hist + (ty0 + (t >> 1)) * ntx + tx0 + (t & 1), 1);
   }
   __syncthreads();
-  // exclusive scan of cnt -> cur / row_ptr (chunk per thread, Hillis-Steele over the chunk sums)
-  const int chunk = (hw + PIDX_THREADS - 1) / PIDX_THREADS;
-  const int c0 = min(hw, t * chunk), c1 = min(hw, c0 + chunk);
+  for (int t = threadIdx.x; t < nt; t += blockDim.x)
+    if (hist[t]) atomicAdd(tile_cnt + (size_t)bc * nt + t, hist[t]);
+}
+
+__global__ __launch_bounds__(PIDX_THREADS) void plan_scan_k(vfd_voxel_desc d, int* __restrict__ tile_cnt,
+                                                            int* __restrict__ tile_ptr) {
+  __shared__ int part[PIDX_THREADS];
+  const int nt = tiles_x(d) * tiles_y(d);
+  const int bc = blockIdx.x, t = threadIdx.x;
+  int* cnt = tile_cnt + (size_t)bc * nt;
+  const int chunk = (nt + PIDX_THREADS - 1) / PIDX_THREADS;
+  const int c0 = min(nt, t * chunk), c1 = min(nt, c0 + chunk);
   int local = 0;
   for (int i = c0; i < c1; ++i) local += cnt[i];
   part[t] = local;
@@ -592,125 +643,196 @@ __global__ __launch_bounds__(PIDX_THREADS) void plan_index_k(vfd_voxel_desc d, c
     __syncthreads();
   }
   int run = part[t] - local;
-  int* rp = row_ptr + (size_t)bc * (hw + 1);
+  int* tp = tile_ptr + (size_t)bc * (nt + 1);
   for (int i = c0; i < c1; ++i) {
-    cur[i] = run;
-    rp[i] = run;
-    run += cnt[i];
+    const int c = cnt[i];
+    tp[i] = run;
+    cnt[i] = run;                 // becomes the fill cursor
+    run += c;
   }
-  if (t == PIDX_THREADS - 1) rp[hw] = part[t];
+  if (t == PIDX_THREADS - 1) tp[nt] = part[t];
+}
+
+__global__ __launch_bounds__(256) void plan_fill_k(vfd_voxel_desc d, const PlanEntry* __restrict__ plan,
+                                                   const int* __restrict__ counts, int* __restrict__ cursor,
+                                                   TileItem* __restrict__ items) {
+  extern __shared__ int lds[];           // [nt] local counts -> slot bases | [nt] local cursors
+  const int bc = blockIdx.y;
+  const int V = d.X * d.Y * d.Z, ntx = tiles_x(d), nt = ntx * tiles_y(d);
+  const int n = counts[bc];
+  if ((int)(blockIdx.x * blockDim.x) >= n) return;
+  int* lbase = lds;
+  int* lcur = lds + nt;
+  for (int t = threadIdx.x; t < nt; t += blockDim.x) lbase[t] = lcur[t] = 0;
   __syncthreads();
-  int* cb = csr + (size_t)bc * 4 * V;
-  for (int i = t; i < n; i += PIDX_THREADS) {
-    const PlanEntry e = list[i];
-    const unsigned in = e.meta >> 28;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool act = i < n;
+  PlanEntry e;
+  unsigned m = 0;
+  int tx0 = 0, ty0 = 0;
+  if (act) {
+    e = plan[(size_t)bc * V + i];
+    m = entry_tiles(d, e, &tx0, &ty0);
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (in >> q & 1u) cb[atomicAdd(&cur[e.base + tap_offset(q, d.w)], 1)] = (i << 2) | q;
+    for (int t = 0; t < 4; ++t)
+      if (m >> t & 1u) atomicAdd(lbase + (ty0 + (t >> 1)) * ntx + tx0 + (t & 1), 1);
+  }
+  __syncthreads();
+  int* cur = cursor + (size_t)bc * nt;
+  for (int t = threadIdx.x; t < nt; t += blockDim.x)
+    if (lbase[t]) lbase[t] = atomicAdd(cur + t, lbase[t]);
+  __syncthreads();
+  if (!act) return;
+  const unsigned in = e.meta >> 28;
+  const int v = (int)(e.meta & 0xFFFFFF);
+  const int xi = v % d.X, yi = (v / d.X) % d.Y, zi = v / (d.X * d.Y);
+  const int P1 = d.pad_out ? 1 : 0;
+  const bool fold = d.pad_out && (xi == 1 || xi == d.X - 2 || yi == 1 || yi == d.Y - 2);
+  TileItem it;
+  it.pz = (uint32_t)((yi + P1) * (d.X + 2 * P1) + xi + P1) | ((uint32_t)zi << 20) | ((fold ? 1u : 0u) << 28);
+  it.den = e.den;
+  it.pad = 0;
+  float w[4];
+  entry_weights(e, w);
+  const int x0 = e.x0, y0 = e.y0;
+  TileItem* ib = items + (size_t)bc * 4 * V;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    if (!(m >> t & 1u)) continue;
+    const int tx = tx0 + (t & 1), ty = ty0 + (t >> 1), tile = ty * ntx + tx;
+    const int lx = x0 - tx * PT, ly = y0 - ty * PT;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int px = lx + (q & 1), py = ly + (q >> 1);
+      const bool mine = (in >> q & 1u) && px >= 0 && px < PT && py >= 0 && py < PT;
+      it.w[q] = mine ? w[q] : 0.f;
+    }
+    it.lxy = (ly + 1) * 8 + (lx + 1);
+    ib[lbase[tile] + atomicAdd(lcur + tile, 1)] = it;
   }
 }
 
-constexpr int PBW_TP = 16;     // pixels per workgroup (4 per wave)
-constexpr int PBW_U = 4;       // list items in flight per wave
+#ifndef VFD_PBW_U
+#define VFD_PBW_U 8
+#endif
+constexpr int PBW_U = VFD_PBW_U;       // voxel rows (1 KB each) in flight per wave
 
-__global__ __launch_bounds__(256) void fuse_pose_bwd_k(vfd_voxel_desc d, const PlanEntry* __restrict__ plan,
-                                                       const int* __restrict__ row_ptr, const int* __restrict__ csr,
+__global__ __launch_bounds__(256) void fuse_pose_bwd_k(vfd_voxel_desc d, const int* __restrict__ tile_ptr,
+                                                       const TileItem* __restrict__ items,
                                                        const float* __restrict__ dout, float* __restrict__ dfeats) {
-  extern __shared__ float otile[];       // [C][PBW_TP + 1]
-  constexpr int CPL = POSE_MAXC / 64;
+  extern __shared__ float red[];         // [C][PT2 + 1]: one wave's tile, then the transposed sum
   const int hw = d.h * d.w;
   const int V = d.X * d.Y * d.Z;
   const int C = d.C, C1 = d.C + 1;
-  const int bc = blockIdx.y, b = bc / d.N;
-  const int q0 = blockIdx.x * PBW_TP;
+  const int ntx = tiles_x(d), nt = ntx * tiles_y(d);
+  // XCD-aware numbering: XCD k takes the contiguous task range [k*per, (k+1)*per) of
+  // (camera, tile), so neighbouring tiles' NCHW row segments merge in one L2
+  const int per = gridDim.x / 8;
+  const int task = (blockIdx.x % 8) * per + blockIdx.x / 8;
+  if (task >= nt * d.B * d.N) return;
+  const int bc = task / nt, b = bc / d.N, tile = task % nt;
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int P = d.pad_out ? 2 : 0;
   const int Yo = d.Y + P, Xo = d.X + P;
   const size_t pix_stride = (size_t)d.Z * C1;
-  const PlanEntry* list = plan + (size_t)bc * V;
-  const int* rp = row_ptr + (size_t)bc * (hw + 1);
-  const int* cb = csr + (size_t)bc * 4 * V;
+  const int* tp = tile_ptr + (size_t)bc * (nt + 1);
+  const TileItem* ib = items + (size_t)bc * 4 * V;
   const float* gb = dout + (size_t)b * Yo * Xo * pix_stride;
-  for (int pi = 0; pi < PBW_TP / 4; ++pi) {
-    const int ql = wv * (PBW_TP / 4) + pi;
-    const int q = q0 + ql;
-    float acc[CPL];
+  const int lo = __builtin_amdgcn_readfirstlane(tp[tile]), hi = __builtin_amdgcn_readfirstlane(tp[tile + 1]);
+  // register accumulators: one 16-pixel array per 64-channel group, indexed by the wave-uniform
+  // tap pixel (register-indexed moves, no scratch)
+  float a0[PT2], a1[PT2], a2[PT2], a3[PT2];
 #pragma unroll
-    for (int k = 0; k < CPL; ++k) acc[k] = 0.f;
-    if (q < hw) {
-      const int lo = rp[q], hi = rp[q + 1];
-      for (int j = lo; j < hi; j += PBW_U) {
-        float wt[PBW_U], den[PBW_U];
-        int vox[PBW_U];
+  for (int i = 0; i < PT2; ++i) a0[i] = a1[i] = a2[i] = a3[i] = 0.f;
+  int cho[4];
 #pragma unroll
-        for (int u = 0; u < PBW_U; ++u) {
-          wt[u] = 0.f;
-          den[u] = 1.f;
-          vox[u] = -1;
-          if (j + u < hi) {
-            const int it = cb[j + u];
-            const PlanEntry e = list[it >> 2];
-            float w[4];
-            entry_weights(e, w);
-            const int tap = it & 3;
-            wt[u] = tap == 0 ? w[0] : tap == 1 ? w[1] : tap == 2 ? w[2] : w[3];
-            den[u] = e.den;
-            vox[u] = (int)(e.meta & 0xFFFFFF);
-          }
-        }
-        // main row of every item first (all loads in flight), reflect-padding copies after
-        float g[PBW_U][CPL];
-        int rows[PBW_U][3], cols[PBW_U][3], nr[PBW_U], nc[PBW_U], zoff[PBW_U];
+  for (int k = 0; k < 4; ++k) cho[k] = min(lane + 64 * k, C - 1);
+  for (int j = lo + wv * PBW_U; j < hi; j += 4 * PBW_U) {
+    TileItem it[PBW_U];
+    float g[PBW_U][4];
 #pragma unroll
-        for (int u = 0; u < PBW_U; ++u) {
-          const int v = vox[u] < 0 ? 0 : vox[u];
-          const int xi = v % d.X, yi = (v / d.X) % d.Y, zi = v / (d.X * d.Y);
-          pad_sets(yi, d.Y, d.pad_out, rows[u], &nr[u]);
-          pad_sets(xi, d.X, d.pad_out, cols[u], &nc[u]);
-          zoff[u] = zi * C1;
-          const float* row = gb + ((size_t)rows[u][0] * Xo + cols[u][0]) * pix_stride + zoff[u];
+    for (int u = 0; u < PBW_U; ++u) {
+      it[u] = ib[min(j + u, hi - 1)];                     // tail slots re-read the last item (skipped below)
+      const float* row = gb + (size_t)(it[u].pz & 0xFFFFF) * pix_stride + ((it[u].pz >> 20) & 0xFF) * C1;
 #pragma unroll
-          for (int k = 0; k < CPL; ++k) {
-            const int ch = lane + 64 * k;
-            g[u][k] = row[ch < C ? ch : 0];      // unconditional (voxel 0 for empty slots, weight 0)
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < PBW_U; ++u) {
-          if (vox[u] < 0 || nr[u] * nc[u] == 1) continue;
-          for (int a = 0; a < nr[u]; ++a)
-            for (int c2 = 0; c2 < nc[u]; ++c2) {
-              if (a == 0 && c2 == 0) continue;
-              const float* row = gb + ((size_t)rows[u][a] * Xo + cols[u][c2]) * pix_stride + zoff[u];
-#pragma unroll
-              for (int k = 0; k < CPL; ++k) {
-                const int ch = lane + 64 * k;
-                if (ch < C) g[u][k] += row[ch];
-              }
-            }
-        }
-        // reference order: d(mean) = g / den, then grid_sample's backward adds d(mean) * w
-#pragma unroll
-        for (int u = 0; u < PBW_U; ++u)
-          if (vox[u] >= 0) {
-#pragma unroll
-            for (int k = 0; k < CPL; ++k) acc[k] += (g[u][k] / den[u]) * wt[u];
-          }
-      }
+      for (int k = 0; k < 4; ++k) g[u][k] = row[cho[k]];
     }
 #pragma unroll
-    for (int k = 0; k < CPL; ++k) {
-      const int ch = lane + 64 * k;
-      if (ch < C) otile[ch * (PBW_TP + 1) + ql] = acc[k];
+    for (int u = 0; u < PBW_U; ++u) {
+      if (j + u >= hi) continue;
+      if (it[u].pz >> 28) {                               // reflect-padding copies (grid border)
+        const int pos = it[u].pz & 0xFFFFF, zo = ((it[u].pz >> 20) & 0xFF) * C1;
+        const int xi = pos % Xo - P / 2, yi = pos / Xo - P / 2;
+        int rows[3], cols[3], nr, nc;
+        pad_sets(yi, d.Y, d.pad_out, rows, &nr);
+        pad_sets(xi, d.X, d.pad_out, cols, &nc);
+        for (int a = 0; a < nr; ++a)
+          for (int c2 = 0; c2 < nc; ++c2) {
+            if (a == 0 && c2 == 0) continue;
+            const float* row = gb + ((size_t)rows[a] * Xo + cols[c2]) * pix_stride + zo;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) g[u][k] += row[cho[k]];
+          }
+      }
+      const int lx = (it[u].lxy & 7) - 1, ly = (it[u].lxy >> 3) - 1;
+      // reference order: d(mean) = g / den, then grid_sample's backward adds d(mean) * w
+      float gd[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) gd[k] = g[u][k] / it[u].den;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (it[u].w[q] != 0.f) {
+          const int pl = __builtin_amdgcn_readfirstlane((ly + (q >> 1)) * PT + lx + (q & 1));
+          const float w = it[u].w[q];
+          a0[pl] += gd[0] * w;
+          a1[pl] += gd[1] * w;
+          a2[pl] += gd[2] * w;
+          a3[pl] += gd[3] * w;
+        }
+    }
+  }
+  // sum the four waves' tiles in a fixed order ((w0 + w1) + w2) + w3 through one [C][PT2+1]
+  // LDS tile, then write the tile NCHW with lanes along pixels
+  constexpr int LD = PT2 + 1;
+  for (int src = 1; src < 4; ++src) {
+    if (wv == src) {
+#pragma unroll
+      for (int i = 0; i < PT2; ++i) {
+        if (lane < C) red[lane * LD + i] = a0[i];
+        if (lane + 64 < C) red[(lane + 64) * LD + i] = a1[i];
+        if (lane + 128 < C) red[(lane + 128) * LD + i] = a2[i];
+        if (lane + 192 < C) red[(lane + 192) * LD + i] = a3[i];
+      }
+    }
+    __syncthreads();
+    if (wv == 0) {
+#pragma unroll
+      for (int i = 0; i < PT2; ++i) {
+        a0[i] += red[cho[0] * LD + i];
+        a1[i] += red[cho[1] * LD + i];
+        a2[i] += red[cho[2] * LD + i];
+        a3[i] += red[cho[3] * LD + i];
+      }
+    }
+    __syncthreads();
+  }
+  if (wv == 0) {
+#pragma unroll
+    for (int i = 0; i < PT2; ++i) {
+      if (lane < C) red[lane * LD + i] = a0[i];
+      if (lane + 64 < C) red[(lane + 64) * LD + i] = a1[i];
+      if (lane + 128 < C) red[(lane + 128) * LD + i] = a2[i];
+      if (lane + 192 < C) red[(lane + 192) * LD + i] = a3[i];
     }
   }
   __syncthreads();
-  const int np = min(PBW_TP, hw - q0);
-  float* db = dfeats + (size_t)bc * C * hw + q0;
-  for (int i = threadIdx.x; i < C * PBW_TP; i += blockDim.x) {
-    const int ch = i / PBW_TP, p = i % PBW_TP;
-    if (p < np) db[(size_t)ch * hw + p] = otile[ch * (PBW_TP + 1) + p];
+  const int tx = tile % ntx, ty = tile / ntx;
+  float* db = dfeats + (size_t)bc * C * hw;
+  for (int i = threadIdx.x; i < C * PT2; i += blockDim.x) {
+    const int ch = i / PT2, pl = i % PT2;
+    const int x = tx * PT + pl % PT, y = ty * PT + pl / PT;
+    if (x < d.w && y < d.h) db[(size_t)ch * hw + y * d.w + x] = red[ch * LD + pl];
   }
 }
 
@@ -1079,12 +1201,17 @@ int vfd_fuse_depth_bwd(const vfd_voxel_desc* d, const float* d_vox, const float*
 static size_t plan_entries_bytes(const vfd_voxel_desc* d) {
   return (size_t)d->B * d->N * d->X * d->Y * d->Z * sizeof(PlanEntry);
 }
+static int host_tiles(const vfd_voxel_desc* d) { return cdiv(d->w, PT) * cdiv(d->h, PT); }
 static size_t plan_rowptr_bytes(const vfd_voxel_desc* d) {
-  return ((size_t)d->B * d->N * (d->h * d->w + 1) * sizeof(int) + 255) / 256 * 256;
+  return ((size_t)d->B * d->N * (host_tiles(d) + 1) * sizeof(int) + 255) / 256 * 256;
+}
+static size_t plan_cursor_bytes(const vfd_voxel_desc* d) {
+  return ((size_t)d->B * d->N * host_tiles(d) * sizeof(int) + 255) / 256 * 256;
 }
 
 size_t vfd_fusion_plan_bytes(const vfd_voxel_desc* d) {
-  return plan_entries_bytes(d) + plan_rowptr_bytes(d) + (size_t)d->B * d->N * 4 * d->X * d->Y * d->Z * sizeof(int);
+  return plan_entries_bytes(d) + plan_rowptr_bytes(d) + plan_cursor_bytes(d) +
+         (size_t)d->B * d->N * 4 * d->X * d->Y * d->Z * sizeof(TileItem);
 }
 
 int vfd_fusion_plan(const vfd_voxel_desc* d, const float* mask_lo, const float* K, const float* Einv, void* plan,
@@ -1092,6 +1219,8 @@ int vfd_fusion_plan(const vfd_voxel_desc* d, const float* mask_lo, const float* 
   int st = check_voxel_desc(d);
   if (st) return st;
   VFD_REQUIRE((size_t)d->X * d->Y * d->Z < (1u << 24), "voxel grid too large for the plan (%d x %d x %d)", d->X, d->Y, d->Z);
+  VFD_REQUIRE((size_t)(d->X + 2) * (d->Y + 2) < (1u << 20) && d->Z < 256, "voxel grid too large for the pose index");
+  VFD_REQUIRE(2 * (size_t)host_tiles(d) * sizeof(int) <= 64 * 1024, "feature map %dx%d too large for the tile index", d->h, d->w);
   hipStream_t s = (hipStream_t)stream;
   const int V = d->X * d->Y * d->Z;
   (void)hipMemsetAsync(counts, 0, (size_t)d->B * d->N * sizeof(int), s);
@@ -1103,9 +1232,14 @@ int vfd_fusion_plan(const vfd_voxel_desc* d, const float* mask_lo, const float* 
 #undef VFD_CASE
   }
   int* row_ptr = (int*)((char*)plan + plan_entries_bytes(d));
-  int* csr = (int*)((char*)row_ptr + plan_rowptr_bytes(d));
-  const size_t lds = (2 * (size_t)d->h * d->w + PIDX_THREADS) * sizeof(int);
-  plan_index_k<<<d->B * d->N, PIDX_THREADS, lds, s>>>(*d, (const PlanEntry*)plan, counts, row_ptr, csr);
+  int* cursor = (int*)((char*)row_ptr + plan_rowptr_bytes(d));
+  TileItem* csr = (TileItem*)((char*)cursor + plan_cursor_bytes(d));
+  (void)hipMemsetAsync(cursor, 0, (size_t)d->B * d->N * host_tiles(d) * sizeof(int), s);
+  const dim3 egrid(cdiv(V, 256), d->B * d->N);
+  const size_t hist = (size_t)host_tiles(d) * sizeof(int);
+  plan_count_k<<<egrid, 256, hist, s>>>(*d, (const PlanEntry*)plan, counts, cursor);
+  plan_scan_k<<<d->B * d->N, PIDX_THREADS, 0, s>>>(*d, cursor, row_ptr);
+  plan_fill_k<<<egrid, 256, 2 * hist, s>>>(*d, (const PlanEntry*)plan, counts, cursor, csr);
   return fail_launch("fusion_plan");
 }
 
@@ -1133,14 +1267,14 @@ int vfd_fuse_pose_bwd(const vfd_voxel_desc* d, const void* plan, const int* coun
   if (st) return st;
   (void)counts;
   VFD_REQUIRE(d->C >= 1 && d->C <= POSE_MAXC, "fuse_pose: C=%d outside [1, %d]", d->C, POSE_MAXC);
-  VFD_REQUIRE((2 * (size_t)d->h * d->w + PIDX_THREADS) * sizeof(int) <= 160 * 1024, "feature map %dx%d too large", d->h, d->w);
   hipStream_t s = (hipStream_t)stream;
   const int hw = d->h * d->w;
   const int* row_ptr = (const int*)((const char*)plan + plan_entries_bytes(d));
-  const int* csr = (const int*)((const char*)row_ptr + plan_rowptr_bytes(d));
+  const TileItem* csr = (const TileItem*)((const char*)row_ptr + plan_rowptr_bytes(d) + plan_cursor_bytes(d));
   ProfScope ps(K_FUSE_POSE_BWD, s);
-  fuse_pose_bwd_k<<<dim3(cdiv(hw, PBW_TP), d->B * d->N), 256, (size_t)d->C * (PBW_TP + 1) * sizeof(float), s>>>(
-      *d, (const PlanEntry*)plan, row_ptr, csr, d_out, d_feats);
+  const int ntask = host_tiles(d) * d->B * d->N;
+  fuse_pose_bwd_k<<<dim3(8 * cdiv(ntask, 8)), 256, (size_t)(PT2 + 1) * d->C * sizeof(float), s>>>(
+      *d, row_ptr, csr, d_out, d_feats);
   return fail_launch("fuse_pose_bwd");
 }
 

@@ -14,11 +14,11 @@ import sys
 
 OPS = {
     'mask_downsample': ['mask_downsample_k'],
-    'fusion_plan': ['fusion_plan_k', 'plan_index_k'],
+    'fusion_plan': ['fusion_plan_k', 'plan_index_k', 'plan_count_k', 'plan_scan_k', 'plan_fill_k'],
     'fuse_depth_fwd': ['fuse_depth_fwd_k'],
     'fuse_depth_bwd': ['fuse_depth_bwd_k', 'fuse_depth_reduce_k'],
     'fuse_pose_fwd': ['fuse_pose_fwd_k'],
-    'fuse_pose_bwd': ['pose_grad_rows_k', 'fuse_pose_bwd_k'],
+    'fuse_pose_bwd': ['fuse_pose_bwd_k'],
     'voxel_project_fwd': ['voxel_project_fwd_k'],
     'voxel_project_bwd': ['voxel_project_bwd_k'],
     'view_stats': ['view_stats_k', 'view_finalize_k'],
@@ -54,7 +54,8 @@ def main():
     out = {'_meta': {'unit': 'bytes per op launch', 'fetch_correction': 2.0,
                      'source': 'rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes'}}
     for op, ks in OPS.items():
-        n = len(fetch.get(ks[0], []))
+        ks = [k for k in ks if k in fetch]          # kernels this build actually launches
+        n = len(fetch.get(ks[0], [])) if ks else 0
         if not n:
             continue
         f = sum(sum(fetch.get(k, [])) for k in ks) / n

@@ -889,17 +889,18 @@ __device__ __forceinline__ int tri_index(const vfd_voxel_desc& d, const Tri& t, 
 // ------------------------------------------------------------------------------ K3 forward
 // Frustum samples -> trilinear gather from the channels-last voxel grid (K1's output), written
 // into the channels-last input of reduce_dim's first conv: out[bc][y'][x'][d*Cv + c] (NHWC,
-// depth-major channels; the conv weight is permuted to match).  A workgroup owns 64 consecutive
-// pixels at one depth bin: one thread per sample computes the trilinear cell and weights into
-// LDS, then lanes = channels, so every corner read and every output write is one contiguous
-// Cv-float row; each wave keeps VP_U samples in flight.
-constexpr int VP_PX = 64;       // pixels per workgroup
-constexpr int VP_U = 4;         // samples in flight per wave
+// depth-major channels; the conv weight is permuted to match).  Samples are numbered
+// s = pixel * D + depth, the output order, so consecutive samples write consecutive Cv-rows.
+// A workgroup owns 64 consecutive samples: one thread per sample computes the cell and weights
+// into LDS, then each wave processes its 16 samples four at a time with lanes = (sample,
+// channel quad): every corner read and every output store is one float4 per lane (a 256-B row
+// per 16 lanes), and the per-sample index math runs on vector lanes (no scalar-unit loop).
+constexpr int VP_S = 64;        // samples per workgroup
 
 struct TriLds {
-  int base[VP_PX];              // voxel index of corner 0 (may be out of range; see in)
-  unsigned in[VP_PX];
-  float w[VP_PX][8];
+  int base[VP_S];               // voxel index of corner 0 (may be out of range; see in)
+  unsigned in[VP_S];
+  float w[VP_S][8];
 };
 
 __device__ __forceinline__ void tri_to_lds(const vfd_voxel_desc& d, TriLds& tl, int j, const Tri& t) {
@@ -918,72 +919,72 @@ __global__ __launch_bounds__(256) void voxel_project_fwd_k(vfd_voxel_desc d, con
                                                            const float* __restrict__ invK,
                                                            const float* __restrict__ E,
                                                            float* __restrict__ out) {
+  constexpr int QPS = CV / 4;           // float4 quads per sample row
+  constexpr int SPI = 64 / QPS;         // samples per wave instruction
   __shared__ TriLds tl;
-  const int hw = d.h * d.w;
-  // XCD-aware numbering: workgroups are dealt to the 8 XCDs round-robin, so XCD k gets the
-  // contiguous task range [k*per, (k+1)*per) in (camera, depth bin, pixel chunk) order; the
-  // workgroups resident on one XCD then read one thin shell of the voxel grid from its L2
-  const int nchunk = (hw + VP_PX - 1) / VP_PX;
-  const int ntask = nchunk * d.D * d.B * d.N;
+  const int S = d.h * d.w * d.D;        // samples per (batch, camera)
+  // XCD-aware numbering: XCD k takes the contiguous task range [k*per, (k+1)*per) — the
+  // workgroups resident on one XCD sweep neighbouring rays, which read one wedge of the grid
+  const int nchunk = (S + VP_S - 1) / VP_S;
+  const int ntask = nchunk * d.B * d.N;
   const int per = gridDim.x / 8;
   const int task = (blockIdx.x % 8) * per + blockIdx.x / 8;
   if (task >= ntask) return;
-  const int p0 = (task % nchunk) * VP_PX;
-  const int dep_i = (task / nchunk) % d.D;
-  const int bc = task / (nchunk * d.D);
-  const int b = bc / d.N;
-  const float dep = d.dbins[dep_i];
-  if (threadIdx.x < VP_PX) {
-    const int p = p0 + threadIdx.x;
+  const int bc = task / nchunk, b = bc / d.N;
+  const int s0 = (task % nchunk) * VP_S;
+  if (threadIdx.x < VP_S) {
+    const int sl = s0 + threadIdx.x;
     Tri t;
     t.in = 0;
     t.x0 = t.y0 = t.z0 = 0;
-    if (p < hw) t = frustum_sample(d, invK + bc * 16, E + bc * 16, p % d.w, p / d.w, dep);
+    if (sl < S) {
+      const int p = sl / d.D, di = sl % d.D;
+      t = frustum_sample(d, invK + bc * 16, E + bc * 16, p % d.w, p / d.w, d.dbins[di]);
+    }
     tri_to_lds(d, tl, threadIdx.x, t);
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int grp = lane / QPS, q = lane % QPS;
   const int V = d.X * d.Y * d.Z;
-  const float* vb = vox + (size_t)b * V * CV;
+  const float4* vb = reinterpret_cast<const float4*>(vox + (size_t)b * V * CV) + q;
   const int P = d.pad_out ? 2 : 0;
   const int ho = d.h + P, wo = d.w + P;
-  const size_t pix_stride = (size_t)d.D * CV;
-  float* ob = out + (size_t)bc * ho * wo * pix_stride + (size_t)dep_i * CV;
-  const bool act = lane < CV;
-  for (int j0 = wv * (VP_PX / 4); j0 < (wv + 1) * (VP_PX / 4); j0 += VP_U) {
-    float acc[VP_U];
+  float4* ob = reinterpret_cast<float4*>(out + (size_t)bc * ho * wo * d.D * CV) + q;
+  constexpr int SPW = VP_S / 4;          // samples per wave
 #pragma unroll
-    for (int u = 0; u < VP_U; ++u) {
-      const int j = j0 + u;
-      // per-sample values are wave-uniform: keep them (and the corner addresses) scalar
-      const unsigned in = (unsigned)__builtin_amdgcn_readfirstlane((int)tl.in[j]);
-      const int base = __builtin_amdgcn_readfirstlane(tl.base[j]);
-      // branch-free: every corner is loaded (out-of-range ones from voxel 0 with weight 0, which
-      // adds +0: the reference's sum over in-range corners, same order), so all 8 loads of the
-      // VP_U samples are in flight before the first FMA
-      float v[8], w[8];
+  for (int it = 0; it < (SPW + SPI - 1) / SPI; ++it) {
+    if (it * SPI + grp >= SPW) break;     // (only when a wave instruction spans > SPW samples)
+    const int j = wv * SPW + it * SPI + grp;                  // sample within the workgroup
+    const int sl = s0 + j;
+    const unsigned in = tl.in[j];
+    const int base = tl.base[j];
+    // branch-free: every corner is loaded (out-of-range ones from voxel 0 with weight 0, which
+    // adds +0: the reference's sum over in-range corners, same order)
+    float4 v[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const bool ok = (in >> k & 1u) != 0u;
-        const int idx = ok ? base + corner_offset(d, k) : 0;
-        v[k] = vb[(size_t)idx * CV + (act ? lane : 0)];
-        w[k] = ok ? tl.w[j][k] : 0.f;
-      }
-      float a = 0.f;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) a += v[k] * w[k];
-      acc[u] = a;
+    for (int k = 0; k < 8; ++k) {
+      const bool ok = (in >> k & 1u) != 0u;
+      v[k] = vb[(size_t)(ok ? base + corner_offset(d, k) : 0) * QPS];
     }
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int u = 0; u < VP_U; ++u) {
-      const int p = p0 + j0 + u;
-      if (p >= hw || !act) continue;
+    for (int k = 0; k < 8; ++k) {
+      const float w = (in >> k & 1u) ? tl.w[j][k] : 0.f;
+      acc.x += v[k].x * w;
+      acc.y += v[k].y * w;
+      acc.z += v[k].z * w;
+      acc.w += v[k].w * w;
+    }
+    if (sl < S) {
+      const int p = sl / d.D, di = sl % d.D;
       const int px = p % d.w, py = p / d.w;
       int rows[3], cols[3], nr, nc;
       pad_sets(py, d.h, d.pad_out, rows, &nr);
       pad_sets(px, d.w, d.pad_out, cols, &nc);
-      for (int a = 0; a < nr; ++a)
-        for (int c2 = 0; c2 < nc; ++c2) ob[((size_t)rows[a] * wo + cols[c2]) * pix_stride + lane] = acc[u];
+      for (int r = 0; r < nr; ++r)
+        for (int c2 = 0; c2 < nc; ++c2)
+          ob[(((size_t)rows[r] * wo + cols[c2]) * d.D + di) * QPS] = acc;
     }
   }
 }
@@ -997,6 +998,7 @@ __global__ __launch_bounds__(256) void voxel_project_fwd_k(vfd_voxel_desc d, con
 // current cell in registers; on moving to a neighbouring cell the corners the two cells share
 // are carried over (remapped) instead of flushed, so a voxel row is flushed once per run of
 // samples around it rather than once per sample.
+constexpr int VP_PX = 64;       // pixels per workgroup
 constexpr int VPB_TD = 4;       // depth bins per workgroup (one per wave)
 constexpr int VPB_S = VP_PX * VPB_TD;
 
@@ -1285,7 +1287,8 @@ int vfd_voxel_project_fwd(const vfd_voxel_desc* d, const float* vox, const float
   VFD_REQUIRE(d->dbins != nullptr && d->D > 0, "depth bins not set");
   hipStream_t s = (hipStream_t)stream;
   VFD_REQUIRE(d->Cv <= 64, "voxel_project: Cv=%d > 64", d->Cv);
-  const int ntask = cdiv(d->h * d->w, VP_PX) * d->D * d->B * d->N;
+  VFD_REQUIRE(((uintptr_t)vox & 15) == 0 && ((uintptr_t)out & 15) == 0, "voxel_project: 16-B aligned buffers required");
+  const int ntask = cdiv((size_t)d->h * d->w * d->D, VP_S) * d->B * d->N;
   dim3 grid(8 * cdiv(ntask, 8));
   ProfScope ps(K_VPROJ_FWD, s);
   switch (d->Cv) {

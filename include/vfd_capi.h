@@ -97,9 +97,13 @@ int vfd_fuse_pose_bwd(const vfd_voxel_desc* d, const void* plan, const int* coun
  * d*Cv + c (the reference's c*D + d order permuted; the conv weight is permuted to match). */
 int vfd_voxel_project_fwd(const vfd_voxel_desc* d, const float* vox, const float* invK,
                           const float* E, float* out, void* stream);
-/* d_out (forward layout) -> d_vox [B,V,Cv] (zeroed here). */
+/* Autograd of the trilinear gather (grid_sampler_3d_backward, volumetric_fusionnet.py:261-262):
+ * d_out (forward layout, reflect copies folded) -> d_vox [B,V,Cv] (fully written here).
+ * Counting sort of the frustum samples by voxel cell + brick-owned LDS accumulation; needs
+ * vfd_voxel_project_bwd_workspace(d) bytes of device workspace (no host sync, graph-safe). */
+size_t vfd_voxel_project_bwd_workspace(const vfd_voxel_desc* d);
 int vfd_voxel_project_bwd(const vfd_voxel_desc* d, const float* d_out, const float* invK,
-                          const float* E, float* d_vox, void* stream);
+                          const float* E, float* d_vox, void* ws, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------ view synthesis (K4) */
 typedef struct vfd_view_desc {

@@ -51,7 +51,8 @@ _SIGS = {
     'vfd_fuse_pose_fwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 5 + [c_void_p]),
     'vfd_fuse_pose_bwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 4 + [c_void_p]),
     'vfd_voxel_project_fwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 4 + [c_void_p]),
-    'vfd_voxel_project_bwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 4 + [c_void_p]),
+    'vfd_voxel_project_bwd_workspace': (c_size_t, [ctypes.POINTER(VoxelDesc)]),
+    'vfd_voxel_project_bwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 4 + [c_void_p, c_size_t, c_void_p]),
     'vfd_view_workspace_bytes': (c_size_t, [ctypes.POINTER(ViewDesc)]),
     'vfd_view_fwd': (c_int, [ctypes.POINTER(ViewDesc)] + [c_fp] * 10 + [c_size_t, c_void_p]),
     'vfd_view_bwd': (c_int, [ctypes.POINTER(ViewDesc)] + [c_fp] * 10 + [c_size_t, c_void_p]),

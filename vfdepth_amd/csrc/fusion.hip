@@ -990,137 +990,486 @@ __global__ __launch_bounds__(256) void voxel_project_fwd_k(vfd_voxel_desc d, con
 }
 
 // ------------------------------------------------------------------------------ K3 backward
-// f32 atomics run at one chip-wide rate (~1.3 TB/s of added bytes), so this kernel is sized by
-// how many voxel rows it flushes.  A workgroup owns 64 consecutive pixels x VPB_TD depth bins;
-// per-sample cells and weights go to LDS, then each wave walks the 64 pixels of one depth bin
-// with lanes = channels, reading each sample's (reflect-folded) upstream gradient as one
-// contiguous row of the channels-last d_out.  The wave keeps the 8 corner accumulators of the
-// current cell in registers; on moving to a neighbouring cell the corners the two cells share
-// are carried over (remapped) instead of flushed, so a voxel row is flushed once per run of
-// samples around it rather than once per sample.
-constexpr int VP_PX = 64;       // pixels per workgroup
-constexpr int VPB_TD = 4;       // depth bins per workgroup (one per wave)
-constexpr int VPB_S = VP_PX * VPB_TD;
+// The transpose of the trilinear gather: every frustum sample adds w_k * g to the 8 corners of
+// its voxel cell.  f32 atomics run at one chip-wide rate (~1.3 TB/s of added bytes, and LDS
+// float atomics at ~3 cycles per lane), so the backward is organised as an owner-computes
+// accumulation with no float atomics on the common path:
+//   vpb_count_k / vpb_fill_k  counting sort of the samples by cell (extended grid of
+//                             (X+1)(Y+1)(Z+1) cells, corner 0 in [-1, X-1] ...): one 16-B
+//                             entry {ix, iy, iz, sample} per in-range sample, cells contiguous
+//                             in x;
+//   vpb_brick_k / vpb_tasks_k voxel bricks of 8x8x4; a brick's wave for voxel layer zl owns the
+//                             samples of the 2 x 9 cell rows that touch that layer (18
+//                             contiguous entry ranges); bricks whose heaviest layer has more
+//                             than VB_S samples are split into parts (their voxels zeroed and
+//                             flushed with atomics);
+//   vpb_main_k                one workgroup per task, lanes = channels, 64 KB LDS brick
+//                             accumulator: each wave reads its samples' gradient rows (reflect
+//                             copies folded), merges runs of one cell in registers and flushes
+//                             the cell's 4 corners of its own layer into LDS with plain
+//                             read-add-write (no other wave writes that layer); the brick is
+//                             then written with plain stores.
+constexpr int VB_X = 8, VB_Y = 8;                  // voxel tile (one z layer) per wave task
+constexpr int VB_S = 1024;                         // samples per task part
+constexpr int VB_SCAN = 4096;                      // cells per block of the first scan level
 
-struct CellLds {
-  short x0[VPB_S], y0[VPB_S], z0[VPB_S];
-  unsigned char in[VPB_S];
-  float w[VPB_S][8];
+struct VpbGeom {
+  int CX, CY, CZ, ncell;                           // extended cell grid per batch
+  int nbx, nby, ntile;                             // tiles per batch: nbx * nby * Z
 };
+__host__ __device__ __forceinline__ VpbGeom vpb_geom(const vfd_voxel_desc& d) {
+  VpbGeom g;
+  g.CX = d.X + 1;
+  g.CY = d.Y + 1;
+  g.CZ = d.Z + 1;
+  g.ncell = g.CX * g.CY * g.CZ;
+  g.nbx = (d.X + VB_X - 1) / VB_X;
+  g.nby = (d.Y + VB_Y - 1) / VB_Y;
+  g.ntile = g.nbx * g.nby * d.Z;
+  return g;
+}
+
+// continuous grid coordinates of a frustum sample (the first half of frustum_sample)
+__device__ __forceinline__ void frustum_coords(const vfd_voxel_desc& d, const float* __restrict__ iK,
+                                               const float* __restrict__ E, int px, int py, float dep,
+                                               float* ix, float* iy, float* iz) {
+  float fx = (float)px, fy = (float)py;
+  float r0 = iK[0] * fx + iK[1] * fy + iK[2];
+  float r1 = iK[4] * fx + iK[5] * fy + iK[6];
+  float r2 = iK[8] * fx + iK[9] * fy + iK[10];
+  float p0 = dep * r0, p1 = dep * r1, p2 = dep * r2;
+  float w0 = E[0] * p0 + E[1] * p1 + E[2] * p2 + E[3];
+  float w1 = E[4] * p0 + E[5] * p1 + E[6] * p2 + E[7];
+  float w2 = E[8] * p0 + E[9] * p1 + E[10] * p2 + E[11];
+  float gx = (w0 - d.str[0]) / d.len[0] * 2.f - 1.f;
+  float gy = (w1 - d.str[1]) / d.len[1] * 2.f - 1.f;
+  float gz = (w2 - d.str[2]) / d.len[2] * 2.f - 1.f;
+  *ix = unnorm_ac(gx, d.X);
+  *iy = unnorm_ac(gy, d.Y);
+  *iz = unnorm_ac(gz, d.Z);
+}
+
+// extended-grid cell of a sample whose cell has at least one in-range corner, else -1
+__device__ __forceinline__ int vpb_cell(const vfd_voxel_desc& d, const VpbGeom& g, float ix, float iy, float iz) {
+  if (!(finitef(ix) && finitef(iy) && finitef(iz))) return -1;
+  const float fx0 = floorf(ix), fy0 = floorf(iy), fz0 = floorf(iz);
+  if (!(fx0 >= -1.f && fx0 <= (float)(d.X - 1) && fy0 >= -1.f && fy0 <= (float)(d.Y - 1) && fz0 >= -1.f &&
+        fz0 <= (float)(d.Z - 1)))
+    return -1;
+  return (((int)fz0 + 1) * g.CY + ((int)fy0 + 1)) * g.CX + ((int)fx0 + 1);
+}
+
+// Sort order inside the count / fill kernels: sl = depth * hw + pixel (pixels fastest, so a
+// wave's lanes are neighbouring pixels at one depth and often share a cell near the camera: the
+// lanes of a run of equal cells take their ranks with ONE counter atomic, issued by the run head).
+// The entry's sample id is s = (bc * hw + pixel) * D + depth (the order of the gradient rows).
+__global__ __launch_bounds__(256) void vpb_count_k(vfd_voxel_desc d, const float* __restrict__ invK,
+                                                   const float* __restrict__ E, int* __restrict__ cnt,
+                                                   int* __restrict__ rank) {
+  const VpbGeom g = vpb_geom(d);
+  const int bc = blockIdx.y, b = bc / d.N;
+  const int hw = d.h * d.w, hwD = hw * d.D;
+  const int sl = blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  int c = -1;
+  if (sl < hwD) {
+    const int di = sl / hw, p = sl % hw;
+    float ix, iy, iz;
+    frustum_coords(d, invK + bc * 16, E + bc * 16, p % d.w, p / d.w, d.dbins[di], &ix, &iy, &iz);
+    c = vpb_cell(d, g, ix, iy, iz);
+  }
+  const int prev = __shfl_up(c, 1, 64);
+  const bool head = lane == 0 || c != prev;
+  const unsigned long long hm = __ballot(head);
+  const unsigned long long le = lane == 63 ? ~0ull : ((2ull << lane) - 1);     // lanes <= lane
+  const int myhead = 63 - __clzll(hm & le);
+  const unsigned long long after = hm & ~le;
+  const int next = after ? __ffsll((long long)after) - 1 : 64;
+  int r = 0;
+  if (head && c >= 0) r = atomicAdd(cnt + (size_t)b * g.ncell + c, next - lane);
+  r = __shfl(r, myhead, 64) + lane - myhead;
+  if (sl < hwD) rank[(size_t)bc * hwD + sl] = c < 0 ? -1 : r;
+}
+
+// first scan level: exclusive prefix of VB_SCAN counts per block (16 per thread), block totals
+__global__ __launch_bounds__(256) void vpb_scan1_k(const int* __restrict__ cnt, int n, int* __restrict__ ptr,
+                                                   int* __restrict__ bsum) {
+  __shared__ int wsum[4];
+  const int base = blockIdx.x * VB_SCAN + threadIdx.x * 16;
+  int v[16], run = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    v[i] = base + i < n ? cnt[base + i] : 0;
+    run += v[i];
+  }
+  // inclusive wave scan of the per-thread totals
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int inc = run;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int t = __shfl_up(inc, off, 64);
+    if (lane >= off) inc += t;
+  }
+  if (lane == 63) wsum[wv] = inc;
+  __syncthreads();
+  int woff = 0;
+  for (int k = 0; k < wv; ++k) woff += wsum[k];
+  int ex = woff + inc - run;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    if (base + i < n) ptr[base + i] = ex;
+    ex += v[i];
+  }
+  if (threadIdx.x == 255) bsum[blockIdx.x] = woff + inc;
+}
+
+// second level: one workgroup, exclusive prefix of the block totals; boff[nblk] = grand total
+__global__ __launch_bounds__(1024) void vpb_scan2_k(const int* __restrict__ bsum, int nblk, int* __restrict__ boff) {
+  __shared__ int part[1024];
+  const int t = threadIdx.x;
+  const int chunk = (nblk + 1023) / 1024;
+  const int c0 = min(nblk, t * chunk), c1 = min(nblk, c0 + chunk);
+  int local = 0;
+  for (int i = c0; i < c1; ++i) local += bsum[i];
+  part[t] = local;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const int v = t >= off ? part[t - off] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int run = part[t] - local;
+  for (int i = c0; i < c1; ++i) {
+    boff[i] = run;
+    run += bsum[i];
+  }
+  if (t == 1023) boff[nblk] = part[t];
+}
+
+// start of cell i's entries (i == n: the total)
+__device__ __forceinline__ int vpb_ptr(const int* __restrict__ ptr, const int* __restrict__ boff, int n, int i) {
+  return i < n ? ptr[i] + boff[i / VB_SCAN] : boff[(n + VB_SCAN - 1) / VB_SCAN];
+}
+
+__global__ __launch_bounds__(256) void vpb_fill_k(vfd_voxel_desc d, const float* __restrict__ invK,
+                                                  const float* __restrict__ E, const int* __restrict__ rank,
+                                                  const int* __restrict__ ptr, const int* __restrict__ boff,
+                                                  float4* __restrict__ entries) {
+  const VpbGeom g = vpb_geom(d);
+  const int bc = blockIdx.y, b = bc / d.N;
+  const int hw = d.h * d.w, hwD = hw * d.D;
+  const int sl = blockIdx.x * blockDim.x + threadIdx.x;
+  if (sl >= hwD) return;
+  const int r = rank[(size_t)bc * hwD + sl];
+  if (r < 0) return;
+  const int di = sl / hw, p = sl % hw;
+  float ix, iy, iz;
+  frustum_coords(d, invK + bc * 16, E + bc * 16, p % d.w, p / d.w, d.dbins[di], &ix, &iy, &iz);
+  const int c = vpb_cell(d, g, ix, iy, iz);
+  const int n = d.B * g.ncell;
+  entries[vpb_ptr(ptr, boff, n, b * g.ncell + c) + r] =
+      make_float4(ix, iy, iz, __int_as_float((bc * hw + p) * d.D + di));
+}
+
+// Reflect-pad fold (pad_sets): the gradient of map pixel (px, py) is the sum of its copies in the
+// padded d_out.  Only pixels with a second copy (py in {1, h-2} or px in {1, w-2}) are folded,
+// into fb[bc][slot][D][CV]; slot = px (py == 1), w + px (py == h-2), 2w + py (px == 1),
+// 2w + h + py (px == w-2), first match wins.
+__device__ __forceinline__ int vpb_fold_slot(const vfd_voxel_desc& d, int px, int py) {
+  if (py == 1) return px;
+  if (py == d.h - 2) return d.w + px;
+  if (px == 1) return 2 * d.w + py;
+  if (px == d.w - 2) return 2 * d.w + d.h + py;
+  return -1;
+}
 
 template <int CV>
-__global__ __launch_bounds__(256) void voxel_project_bwd_k(vfd_voxel_desc d, const float* __restrict__ dout,
-                                                           const float* __restrict__ invK,
-                                                           const float* __restrict__ E,
-                                                           float* __restrict__ dvox) {
-  __shared__ CellLds cl;
-  const int hw = d.h * d.w;
-  const int p0 = blockIdx.x * VP_PX;
-  const int d0 = blockIdx.y * VPB_TD;
-  const int bc = blockIdx.z;
-  const int b = bc / d.N;
-  for (int i = threadIdx.x; i < VPB_S; i += blockDim.x) {
-    const int p = p0 + i % VP_PX, di = d0 + i / VP_PX;
-    Tri t;
-    t.in = 0;
-    t.x0 = t.y0 = t.z0 = 0;
-    if (p < hw && di < d.D) t = frustum_sample(d, invK + bc * 16, E + bc * 16, p % d.w, p / d.w, d.dbins[di]);
-    cl.x0[i] = (short)t.x0;
-    cl.y0[i] = (short)t.y0;
-    cl.z0[i] = (short)t.z0;
-    cl.in[i] = (unsigned char)t.in;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) cl.w[i][k] = t.w[k];
+__global__ __launch_bounds__(256) void vpb_fold_k(vfd_voxel_desc d, const float* __restrict__ dout,
+                                                  float* __restrict__ fb) {
+  const int nsl = 2 * (d.w + d.h);
+  const int bc = blockIdx.x / nsl, slot = blockIdx.x % nsl;
+  int px, py;
+  if (slot < d.w) { px = slot; py = 1; }
+  else if (slot < 2 * d.w) { px = slot - d.w; py = d.h - 2; }
+  else if (slot < 2 * d.w + d.h) { px = 1; py = slot - 2 * d.w; }
+  else { px = d.w - 2; py = slot - 2 * d.w - d.h; }
+  if (vpb_fold_slot(d, px, py) != slot) return;          // owned by an earlier slot
+  const int wo = d.w + 2, ho = d.h + 2;
+  int rows[3], cols[3], nr, nc;
+  pad_sets(py, d.h, true, rows, &nr);
+  pad_sets(px, d.w, true, cols, &nc);
+  const size_t rl = (size_t)d.D * CV;
+  const float4* src[9];
+  int ns = 0;
+  for (int a = 0; a < nr; ++a)
+    for (int c2 = 0; c2 < nc; ++c2)
+      src[ns++] = reinterpret_cast<const float4*>(dout + (((size_t)bc * ho + rows[a]) * wo + cols[c2]) * rl);
+  float4* dst = reinterpret_cast<float4*>(fb + ((size_t)bc * nsl + slot) * rl);
+  for (int i = threadIdx.x; i < (int)(rl / 4); i += blockDim.x) {
+    float4 s = src[0][i];
+    for (int k = 1; k < ns; ++k) {
+      const float4 v = src[k][i];
+      s.x += v.x;
+      s.y += v.y;
+      s.z += v.z;
+      s.w += v.w;
+    }
+    dst[i] = s;
   }
-  __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int wv = threadIdx.x >> 6;
-  const int dep_i = d0 + wv;
-  if (dep_i >= d.D) return;
-  const int P = d.pad_out ? 2 : 0;
-  const int ho = d.h + P, wo = d.w + P;
-  const size_t pix_stride = (size_t)d.D * CV;
-  const float* gb = dout + (size_t)bc * ho * wo * pix_stride + (size_t)dep_i * CV;
-  const bool act = lane < CV;
-  const int cl_lane = act ? lane : 0;
+}
+
+// entry range of cell row (z0, y0) of brick column [xb - 1, xb + 7] (clipped to the grid)
+__device__ __forceinline__ void vpb_segment(const vfd_voxel_desc& d, const VpbGeom& g, const int* __restrict__ ptr,
+                                            const int* __restrict__ boff, int b, int z0, int y0, int xb, int* s0,
+                                            int* s1) {
+  if (y0 < -1 || y0 > d.Y - 1 || z0 < -1 || z0 > d.Z - 1) {
+    *s0 = *s1 = 0;
+    return;
+  }
+  const int n = d.B * g.ncell;
+  const int base = b * g.ncell + ((z0 + 1) * g.CY + (y0 + 1)) * g.CX;
+  *s0 = vpb_ptr(ptr, boff, n, base + xb);
+  *s1 = vpb_ptr(ptr, boff, n, base + min(xb + VB_X, d.X) + 1);
+}
+
+// per tile (8x8 voxels of one z layer): its samples = the 2 x 9 cell rows touching the layer
+// -> number of parts; split tiles are zeroed here (their parts add with atomics).
+// grid = B * ntile, block = one wave (lanes 0..17 = the cell rows)
+template <int CV>
+__global__ __launch_bounds__(64) void vpb_tile_k(vfd_voxel_desc d, const int* __restrict__ ptr,
+                                                 const int* __restrict__ boff, int* __restrict__ parts,
+                                                 float* __restrict__ dvox) {
+  const VpbGeom g = vpb_geom(d);
+  const int tile = blockIdx.x, lane = threadIdx.x;
+  const int b = tile / g.ntile, tl = tile % g.ntile;
+  const int xb = (tl % g.nbx) * VB_X, yb = ((tl / g.nbx) % g.nby) * VB_Y, zl = tl / (g.nbx * g.nby);
+  int n = 0;
+  if (lane < 18) {
+    int s0, s1;
+    vpb_segment(d, g, ptr, boff, b, zl - 1 + lane / 9, yb - 1 + lane % 9, xb, &s0, &s1);
+    n = s1 - s0;
+  }
+  n = wave_sum(n);
+  const int np = max(1, (n + VB_S - 1) / VB_S);
+  if (lane == 0) parts[tile] = np;
+  if (np == 1) return;
   const int V = d.X * d.Y * d.Z;
-  float* vb = dvox + (size_t)b * V * CV;
-  const int XY = d.X * d.Y;
-  float acc[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
-  int cx = 0, cy = 0, cz = 0;
-  unsigned cin = 0;
-  auto row_of = [&](int x, int y, int z, int k) {
-    return vb + (size_t)((z + (k >> 2)) * XY + (y + ((k >> 1) & 1)) * d.X + x + (k & 1)) * CV + cl_lane;
-  };
-  constexpr int CH = 16;                 // gradient rows prefetched per chunk
-  for (int j0 = 0; j0 < VP_PX; j0 += CH) {
-    float gs[CH];
-#pragma unroll
-    for (int jj = 0; jj < CH; ++jj) {
-      const int p = min(p0 + j0 + jj, hw - 1);
-      const int px = p % d.w, py = p / d.w;
-      gs[jj] = gb[((size_t)(py + P / 2) * wo + px + P / 2) * pix_stride + cl_lane];
-    }
-#pragma unroll
-    for (int jj = 0; jj < CH; ++jj) {
-      const int p = p0 + j0 + jj;
-      if (p >= hw) continue;
-      const int px = p % d.w, py = p / d.w;
-      int rows[3], cols[3], nr, nc;
-      pad_sets(py, d.h, d.pad_out, rows, &nr);
-      pad_sets(px, d.w, d.pad_out, cols, &nc);
-      if (nr * nc == 1) continue;
-      for (int a = 0; a < nr; ++a)
-        for (int c2 = 0; c2 < nc; ++c2)
-          if (a || c2) gs[jj] += gb[((size_t)rows[a] * wo + cols[c2]) * pix_stride + cl_lane];
-    }
-    for (int jj = 0; jj < CH; ++jj) {
-      const int i = wv * VP_PX + j0 + jj;
-      const int p = p0 + j0 + jj;
-      const unsigned in = (unsigned)__builtin_amdgcn_readfirstlane((int)cl.in[i]);
-      if (p >= hw || in == 0) continue;
-      const int nx = __builtin_amdgcn_readfirstlane((int)cl.x0[i]);
-      const int ny = __builtin_amdgcn_readfirstlane((int)cl.y0[i]);
-      const int nz = __builtin_amdgcn_readfirstlane((int)cl.z0[i]);
-      if (!(cin && nx == cx && ny == cy && nz == cz)) {
-        // switch cells: corners shared with the new cell move to its accumulator slot, the
-        // others are flushed (only in-range corners are real voxels)
-        const int dx = cx - nx, dy = cy - ny, dz = cz - nz;
-        float nacc[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) nacc[k] = 0.f;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          if (!(cin >> k & 1u)) continue;
-          const int tx = (k & 1) + dx, ty = ((k >> 1) & 1) + dy, tz = (k >> 2) + dz;
-          const bool keep = tx >= 0 && tx <= 1 && ty >= 0 && ty <= 1 && tz >= 0 && tz <= 1;
-          if (keep) {
-            const int kt = tx + 2 * ty + 4 * tz;
-#pragma unroll
-            for (int q = 0; q < 8; ++q)
-              if (q == kt) nacc[q] += acc[k];
-          } else if (act) {
-            atomicAdd(row_of(cx, cy, cz, k), acc[k]);
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) acc[k] = nacc[k];
-        cx = nx;
-        cy = ny;
-        cz = nz;
-        cin = in;
-      }
-      const float g = gs[jj];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) acc[k] += g * cl.w[i][k];
-    }
+  constexpr int QPV = CV / 4;
+  for (int i = lane; i < VB_X * VB_Y * QPV; i += 64) {
+    const int q = i % QPV, v = i / QPV;
+    const int x = xb + v % VB_X, y = yb + v / VB_X;
+    if (x < d.X && y < d.Y)
+      reinterpret_cast<float4*>(dvox + ((size_t)b * V + (zl * d.Y + y) * d.X + x) * CV)[q] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  if (cin && act) {
+}
+
+// one workgroup: task list (int2 {tile, part | nparts << 16}), task count, main's work counter
+__global__ __launch_bounds__(1024) void vpb_tasks_k(const int* __restrict__ parts, int nb, int2* __restrict__ tasks,
+                                                    int* __restrict__ ctrl) {
+  __shared__ int part[1024];
+  const int t = threadIdx.x;
+  const int chunk = (nb + 1023) / 1024;
+  const int c0 = min(nb, t * chunk), c1 = min(nb, c0 + chunk);
+  int local = 0;
+  for (int i = c0; i < c1; ++i) local += parts[i];
+  part[t] = local;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const int v = t >= off ? part[t - off] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int run = part[t] - local;
+  for (int i = c0; i < c1; ++i) {
+    const int np = parts[i];
+    for (int q = 0; q < np; ++q) tasks[run + q] = make_int2(i, q | (np << 16));
+    run += np;
+  }
+  if (t == 1023) {
+    ctrl[0] = part[t];       // tasks
+    ctrl[1] = 0;             // work counter of vpb_main_k
+  }
+}
+
+// One wave = one independent worker: it takes tile tasks from the counter, accumulates its tile
+// in a private 16 KB LDS slab and writes it out (plain stores, or atomics for split tiles).
+template <int CV>
+__global__ __launch_bounds__(64) void vpb_main_k(vfd_voxel_desc d, const int* __restrict__ ptr,
+                                                 const int* __restrict__ boff, const float4* __restrict__ entries,
+                                                 const int2* __restrict__ tasks, int* __restrict__ ctrl,
+                                                 const float* __restrict__ dout, const float* __restrict__ fb,
+                                                 const float* __restrict__ zrow, float* __restrict__ dvox) {
+  constexpr int LAYER = VB_Y * VB_X * 64;
+  __shared__ float lacc[LAYER + 64];               // + one scratch row (masked corners)
+  const VpbGeom g = vpb_geom(d);
+  const int lane = threadIdx.x;
+  const int cl = lane < CV ? lane : 0;
+  const int hw = d.h * d.w, hwD = hw * d.D;
+  const int Pd = d.pad_out ? 1 : 0;
+  const int ho = d.h + 2 * Pd, wo = d.w + 2 * Pd;
+  const int nfold = 2 * (d.w + d.h);
+  const int V = d.X * d.Y * d.Z;
+  const int ntask = ctrl[0];
+  const long long fb_off = (long long)(fb - dout);   // fold rows addressed relative to dout
+  const long long zero_off = (long long)(zrow - dout);
+  float* trash = lacc + LAYER;
+  for (;;) {
+    int t = 0;
+    if (lane == 0) t = atomicAdd(ctrl + 1, 1);
+    t = __builtin_amdgcn_readfirstlane(t);
+    if (t >= ntask) break;
+    for (int i = lane; i < LAYER / 4; i += 64) reinterpret_cast<float4*>(lacc)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int2 tk = tasks[t];
+    const int tile = tk.x, part = tk.y & 0xFFFF, np = tk.y >> 16;
+    const int b = tile / g.ntile, tl = tile % g.ntile;
+    const int xb = (tl % g.nbx) * VB_X, yb = ((tl / g.nbx) % g.nby) * VB_Y, zl = tl / (g.nbx * g.nby);
+    {
+      // the wave's 18 entry ranges (lanes 0..17) and their running offsets
+      int s0 = 0, s1 = 0;
+      if (lane < 18) vpb_segment(d, g, ptr, boff, b, zl - 1 + lane / 9, yb - 1 + lane % 9, xb, &s0, &s1);
+      const int len = s1 - s0;
+      int inc = len;
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if (cin >> k & 1u) atomicAdd(row_of(cx, cy, cz, k), acc[k]);
+      for (int off = 1; off < 32; off <<= 1) {
+        const int tt = __shfl_up(inc, off, 64);
+        if (lane >= off) inc += tt;
+      }
+      const int total = __builtin_amdgcn_readlane(inc, 17);
+      const int lo = (int)((long long)total * part / np), hi = (int)((long long)total * (part + 1) / np);
+      // entry of list position gi (clamped into [lo, hi): the load is unconditional, so it stays
+      // in flight behind the row loads instead of forcing a wait inside a divergent branch)
+      auto entry_of = [&](int gi) {
+        gi = min(gi, hi - 1);
+        int seg = 0;
+#pragma unroll
+        for (int k = 0; k < 17; ++k) seg += gi >= __builtin_amdgcn_readlane(inc, k) ? 1 : 0;
+        const int ss = __shfl(s0, seg, 64), ex = __shfl(inc - len, seg, 64);
+        return entries[ss + gi - ex];
+      };
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+      int cur = -1;                  // current cell key (wave-uniform)
+      unsigned cmask = 0;            // its in-brick, in-grid corner mask
+      // branch-free: masked corners go to the wave's scratch row (their sums are exactly 0)
+      auto flush = [&]() {
+        const int lx = (cur & 15) - 1, ly = ((cur >> 4) & 15) - 1;
+        float* r0 = lacc + (ly * VB_X + lx) * 64;
+        float* p0 = (cmask & 1u) ? r0 : trash;
+        float* p1 = (cmask & 2u) ? r0 + 64 : trash;
+        float* p2 = (cmask & 4u) ? r0 + VB_X * 64 : trash;
+        float* p3 = (cmask & 8u) ? r0 + VB_X * 64 + 64 : trash;
+        const float v0 = p0[lane], v1 = p1[lane], v2 = p2[lane], v3 = p3[lane];
+        p0[lane] = v0 + a0;
+        p1[lane] = v1 + a1;
+        p2[lane] = v2 + a2;
+        p3[lane] = v3 + a3;
+        a0 = a1 = a2 = a3 = 0.f;
+      };
+      // Software pipeline over half-batches of 32 samples: the rows of the next half are in
+      // flight while the current half is accumulated (<= 64 loads outstanding: vmcnt's range).
+      struct Prm {
+        int key, m;
+        float w0, w1, w2, w3;
+        long long off;
+      };
+      auto setup = [&](const float4& e, int g0) {
+        Prm q;
+        const bool valid = g0 + lane < hi;
+        const float fx0 = floorf(e.x), fy0 = floorf(e.y), fz0 = floorf(e.z);
+        const float ax0 = fx0 + 1.f - e.x, ax1 = e.x - fx0, ay0 = fy0 + 1.f - e.y, ay1 = e.y - fy0;
+        const int x0 = (int)fx0, y0 = (int)fy0, z0 = (int)fz0;
+        const int dz = valid ? zl - z0 : 0;
+        const float az = dz ? e.z - fz0 : fz0 + 1.f - e.z;
+        // ATen trilinear weights (ax[dx] * ay[dy]) * az[dz], as in frustum_sample
+        q.w0 = ax0 * ay0 * az;
+        q.w1 = ax1 * ay0 * az;
+        q.w2 = ax0 * ay1 * az;
+        q.w3 = ax1 * ay1 * az;
+        const bool xin0 = x0 >= max(xb, 0), xin1 = x0 + 1 < min(xb + VB_X, d.X);
+        const bool yin0 = y0 >= max(yb, 0), yin1 = y0 + 1 < min(yb + VB_Y, d.Y);
+        q.m = valid ? (xin0 && yin0 ? 1 : 0) | (xin1 && yin0 ? 2 : 0) | (xin0 && yin1 ? 4 : 0) | (xin1 && yin1 ? 8 : 0)
+                    : 0;
+        // samples past the end: key -1 (one flush of the open cell, then nothing), a zero row
+        q.key = valid ? ((1 - dz) << 8) | ((y0 - yb + 1) << 4) | (x0 - xb + 1) : -1;
+        q.off = zero_off;
+        if (valid) {
+          const int s = __float_as_int(e.w);
+          const int bc = s / hwD, r = s % hwD;
+          const int p = r / d.D, di = r % d.D;
+          const int px = p % d.w, py = p / d.w;
+          const int fs = Pd ? vpb_fold_slot(d, px, py) : -1;
+          q.off = fs >= 0 ? fb_off + ((long long)(bc * nfold + fs) * d.D + di) * CV
+                          : ((long long)((bc * ho + py + Pd) * wo + px + Pd) * d.D + di) * CV;
+        }
+        return q;
+      };
+      auto load_half = [&](const Prm& q, int h, float* gr) {
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+          const int olo = __builtin_amdgcn_readlane((int)(q.off & 0xFFFFFFFF), h * 32 + j);
+          const int ohi = __builtin_amdgcn_readlane((int)(q.off >> 32), h * 32 + j);
+          const long long o = ((long long)ohi << 32) | (unsigned)olo;
+          gr[j] = dout[o + cl];
+        }
+      };
+      auto process_half = [&](const Prm& q, int h, const float* gr) {
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+          const int jj = h * 32 + j;
+          const float gj = gr[j];
+          const int kj = __builtin_amdgcn_readlane(q.key, jj);
+          if (kj != cur) {
+            flush();
+            cur = kj;
+            cmask = (unsigned)__builtin_amdgcn_readlane(q.m, jj);
+          }
+          a0 += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q.w0), jj)) * gj;
+          a1 += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q.w1), jj)) * gj;
+          a2 += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q.w2), jj)) * gj;
+          a3 += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q.w3), jj)) * gj;
+        }
+      };
+      if (lo < hi) {
+        float4 en = entry_of(lo + lane);
+        Prm P = setup(en, lo);
+        en = entry_of(lo + 64 + lane);
+        float grA[32], grB[32];
+        load_half(P, 0, grA);
+        // every load is unconditional (samples past the end read the zero row): a load under a
+        // branch makes the compiler's vmcnt accounting at the join wait for everything
+        for (int g0 = lo; g0 < hi; g0 += 64) {
+          load_half(P, 1, grB);
+          process_half(P, 0, grA);
+          const Prm Pn = setup(en, g0 + 64);
+          en = entry_of(g0 + 128 + lane);
+          load_half(Pn, 0, grA);
+          process_half(P, 1, grB);
+          P = Pn;
+        }
+      }
+      flush();
+    }
+    // ---- write the tile: lanes = (voxel, channel quad)
+    {
+      constexpr int QPV = CV / 4, VPI = 64 / QPV;
+      const int q = lane % QPV, vsub = lane / QPV;
+      for (int v0 = 0; v0 < VB_X * VB_Y; v0 += VPI) {
+        const int vl = v0 + vsub;
+        const int x = xb + vl % VB_X, y = yb + vl / VB_X;
+        if (x >= d.X || y >= d.Y) continue;
+        const float4 a = *reinterpret_cast<const float4*>(lacc + vl * 64 + q * 4);
+        float* dst = dvox + ((size_t)b * V + ((size_t)zl * d.Y + y) * d.X + x) * CV + q * 4;
+        if (np == 1) {
+          *reinterpret_cast<float4*>(dst) = a;
+        } else {
+          unsafeAtomicAdd(dst + 0, a.x);
+          unsafeAtomicAdd(dst + 1, a.y);
+          unsafeAtomicAdd(dst + 2, a.z);
+          unsafeAtomicAdd(dst + 3, a.w);
+        }
+      }
+    }
   }
 }
 
@@ -1301,23 +1650,84 @@ int vfd_voxel_project_fwd(const vfd_voxel_desc* d, const float* vox, const float
   return fail_launch("voxel_project_fwd");
 }
 
+constexpr int VPB_WORKERS = 2048;      // persistent waves (8 per CU: LDS 16.6 KB, <=256 VGPRs)
+
+struct VpbWs {
+  size_t cnt, zero, ptr, bsum, boff, rank, entries, fold, parts, tasks, ctrl, total;
+};
+static VpbWs vpb_ws(const vfd_voxel_desc* d) {
+  const VpbGeom g = vpb_geom(*d);
+  const size_t ncell = (size_t)d->B * g.ncell, nS = (size_t)d->B * d->N * d->h * d->w * d->D;
+  const size_t nblk = cdiv(ncell, VB_SCAN), nb = (size_t)d->B * g.ntile;
+  const size_t ntask_max = nb + cdiv(8 * nS, VB_S);
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  VpbWs w;
+  w.cnt = 0;
+  w.zero = ncell * 4;                  // one zero row of 64 floats right after the counters
+  w.ptr = w.cnt + al(ncell * 4 + 256);
+  w.bsum = w.ptr + al(ncell * 4);
+  w.boff = w.bsum + al(nblk * 4);
+  w.rank = w.boff + al((nblk + 1) * 4);
+  w.entries = w.rank + al(nS * 4);
+  w.fold = w.entries + al(nS * 16);
+  w.parts = w.fold + al((size_t)d->B * d->N * 2 * (d->w + d->h) * d->D * d->Cv * 4);
+  w.tasks = w.parts + al(nb * 4);
+  w.ctrl = w.tasks + al(ntask_max * 8);
+  w.total = w.ctrl + al(2 * 4);
+  return w;
+}
+
+size_t vfd_voxel_project_bwd_workspace(const vfd_voxel_desc* d) {
+  if (check_voxel_desc(d)) return 0;
+  return vpb_ws(d).total;
+}
+
 int vfd_voxel_project_bwd(const vfd_voxel_desc* d, const float* d_out, const float* invK, const float* E,
-                          float* d_vox, void* stream) {
+                          float* d_vox, void* ws, size_t ws_bytes, void* stream) {
   int st = check_voxel_desc(d);
   if (st) return st;
   VFD_REQUIRE(d->dbins != nullptr && d->D > 0, "depth bins not set");
   hipStream_t s = (hipStream_t)stream;
-  VFD_REQUIRE(d->Cv <= 64, "voxel_project: Cv=%d > 64", d->Cv);
-  const size_t V = (size_t)d->X * d->Y * d->Z;
-  (void)hipMemsetAsync(d_vox, 0, (size_t)d->B * V * d->Cv * sizeof(float), s);
-  dim3 grid(cdiv(d->h * d->w, VP_PX), cdiv(d->D, VPB_TD), d->B * d->N);
+  VFD_REQUIRE(d->Cv == 8 || d->Cv == 16 || d->Cv == 32 || d->Cv == 64, "voxel_project: Cv=%d unsupported (8/16/32/64)", d->Cv);
+  VFD_REQUIRE(((uintptr_t)d_vox & 15) == 0, "voxel_project: 16-B aligned d_vox required");
+  const VpbWs w = vpb_ws(d);
+  VFD_REQUIRE(ws != nullptr && ws_bytes >= w.total, "voxel_project_bwd: workspace %zu < %zu bytes", ws_bytes, w.total);
+  VFD_REQUIRE((size_t)d->B * d->N * d->h * d->w * d->D < (1u << 31) / 2, "voxel_project_bwd: too many samples");
+  const VpbGeom g = vpb_geom(*d);
+  char* base = (char*)ws;
+  int* cnt = (int*)(base + w.cnt);
+  int* ptr = (int*)(base + w.ptr);
+  int* bsum = (int*)(base + w.bsum);
+  int* boff = (int*)(base + w.boff);
+  int* rank = (int*)(base + w.rank);
+  float4* entries = (float4*)(base + w.entries);
+  float* fb = (float*)(base + w.fold);
+  const float* zrow = (const float*)(base + w.zero);
+  int* parts = (int*)(base + w.parts);
+  int2* tasks = (int2*)(base + w.tasks);
+  int* ctrl = (int*)(base + w.ctrl);
+  const int ncell = d->B * g.ncell, nblk = cdiv(ncell, VB_SCAN), nb = d->B * g.ntile;
+  const int hwD = d->h * d->w * d->D;
   ProfScope ps(K_VPROJ_BWD, s);
+  (void)hipMemsetAsync(cnt, 0, (size_t)ncell * 4 + 256, s);   // counters + zero row
+  dim3 sgrid(cdiv(hwD, 256), d->B * d->N);
+  vpb_count_k<<<sgrid, 256, 0, s>>>(*d, invK, E, cnt, rank);
+  vpb_scan1_k<<<nblk, 256, 0, s>>>(cnt, ncell, ptr, bsum);
+  vpb_scan2_k<<<1, 1024, 0, s>>>(bsum, nblk, boff);
+  vpb_fill_k<<<sgrid, 256, 0, s>>>(*d, invK, E, rank, ptr, boff, entries);
   switch (d->Cv) {
-    case 8: voxel_project_bwd_k<8><<<grid, 256, 0, s>>>(*d, d_out, invK, E, d_vox); break;
-    case 16: voxel_project_bwd_k<16><<<grid, 256, 0, s>>>(*d, d_out, invK, E, d_vox); break;
-    case 32: voxel_project_bwd_k<32><<<grid, 256, 0, s>>>(*d, d_out, invK, E, d_vox); break;
-    case 64: voxel_project_bwd_k<64><<<grid, 256, 0, s>>>(*d, d_out, invK, E, d_vox); break;
-    default: set_error("voxel_project: Cv=%d unsupported (8/16/32/64)", d->Cv); return VFD_EINVAL;
+#define VPB_LAUNCH(CVV)                                                                            \
+  case CVV:                                                                                        \
+    if (d->pad_out) vpb_fold_k<CVV><<<d->B * d->N * 2 * (d->w + d->h), 256, 0, s>>>(*d, d_out, fb); \
+    vpb_tile_k<CVV><<<nb, 64, 0, s>>>(*d, ptr, boff, parts, d_vox);                                \
+    vpb_tasks_k<<<1, 1024, 0, s>>>(parts, nb, tasks, ctrl);                                        \
+    vpb_main_k<CVV><<<VPB_WORKERS, 64, 0, s>>>(*d, ptr, boff, entries, tasks, ctrl, d_out, fb, zrow, d_vox); \
+    break;
+    VPB_LAUNCH(8)
+    VPB_LAUNCH(16)
+    VPB_LAUNCH(32)
+    VPB_LAUNCH(64)
+#undef VPB_LAUNCH
   }
   return fail_launch("voxel_project_bwd");
 }

@@ -237,8 +237,10 @@ class VoxelProject(torch.autograd.Function):
         g = _channels_last(g, 'grad')
         dvox = torch.empty(B, V, Cv, device=g.device)
         d = ctx.space.desc(B, N, Cv=Cv)
+        nbytes = lib.vfd_voxel_project_bwd_workspace(ctypes.byref(d))
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=g.device)
         L.check(lib.vfd_voxel_project_bwd(ctypes.byref(d), g.data_ptr(), invK.data_ptr(), E.data_ptr(),
-                                          dvox.data_ptr(), L.stream()), 'voxel_project_bwd')
+                                          dvox.data_ptr(), ws.data_ptr(), nbytes, L.stream()), 'voxel_project_bwd')
         return None, dvox, None, None
 
 

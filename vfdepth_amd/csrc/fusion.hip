@@ -12,6 +12,8 @@
 // point) instead of being stored: it costs no HBM traffic and keeps forward and backward
 // decisions bit-identical.  All arithmetic follows the reference's operation order with
 // -ffp-contract=off so that validity tests at the boundaries agree with the CPU reference.
+#include <algorithm>
+
 #include "vfd_common.h"
 
 namespace vfd {
@@ -1152,6 +1154,10 @@ __device__ __forceinline__ int vpb_ptr(const int* __restrict__ ptr, const int* _
   return i < n ? ptr[i] + boff[i / VB_SCAN] : boff[(n + VB_SCAN - 1) / VB_SCAN];
 }
 
+__device__ __forceinline__ int vpb_fold_slot(const vfd_voxel_desc& d, int px, int py);
+
+// entry = {ix, iy, iz, row}: row = the sample's gradient row (CV floats): bit 31 clear = row of
+// d_out, set = row of fbz (row 0 = a zero row, 1 + ... = folded rows of pixels with reflect copies)
 __global__ __launch_bounds__(256) void vpb_fill_k(vfd_voxel_desc d, const float* __restrict__ invK,
                                                   const float* __restrict__ E, const int* __restrict__ rank,
                                                   const int* __restrict__ ptr, const int* __restrict__ boff,
@@ -1164,12 +1170,16 @@ __global__ __launch_bounds__(256) void vpb_fill_k(vfd_voxel_desc d, const float*
   const int r = rank[(size_t)bc * hwD + sl];
   if (r < 0) return;
   const int di = sl / hw, p = sl % hw;
+  const int px = p % d.w, py = p / d.w;
   float ix, iy, iz;
-  frustum_coords(d, invK + bc * 16, E + bc * 16, p % d.w, p / d.w, d.dbins[di], &ix, &iy, &iz);
+  frustum_coords(d, invK + bc * 16, E + bc * 16, px, py, d.dbins[di], &ix, &iy, &iz);
   const int c = vpb_cell(d, g, ix, iy, iz);
   const int n = d.B * g.ncell;
-  entries[vpb_ptr(ptr, boff, n, b * g.ncell + c) + r] =
-      make_float4(ix, iy, iz, __int_as_float((bc * hw + p) * d.D + di));
+  const int Pd = d.pad_out ? 1 : 0;
+  const int fs = Pd ? vpb_fold_slot(d, px, py) : -1;
+  const unsigned row = fs >= 0 ? 0x80000000u | (unsigned)(1 + (bc * 2 * (d.w + d.h) + fs) * d.D + di)
+                               : (unsigned)(((bc * (d.h + 2 * Pd) + py + Pd) * (d.w + 2 * Pd) + px + Pd) * d.D + di);
+  entries[vpb_ptr(ptr, boff, n, b * g.ncell + c) + r] = make_float4(ix, iy, iz, __uint_as_float(row));
 }
 
 // Reflect-pad fold (pad_sets): the gradient of map pixel (px, py) is the sum of its copies in the
@@ -1299,21 +1309,15 @@ template <int CV>
 __global__ __launch_bounds__(64) void vpb_main_k(vfd_voxel_desc d, const int* __restrict__ ptr,
                                                  const int* __restrict__ boff, const float4* __restrict__ entries,
                                                  const int2* __restrict__ tasks, int* __restrict__ ctrl,
-                                                 const float* __restrict__ dout, const float* __restrict__ fb,
-                                                 const float* __restrict__ zrow, float* __restrict__ dvox) {
+                                                 const float* __restrict__ dout, const float* __restrict__ fbz,
+                                                 float* __restrict__ dvox) {
   constexpr int LAYER = VB_Y * VB_X * 64;
   __shared__ float lacc[LAYER + 64];               // + one scratch row (masked corners)
   const VpbGeom g = vpb_geom(d);
   const int lane = threadIdx.x;
   const int cl = lane < CV ? lane : 0;
-  const int hw = d.h * d.w, hwD = hw * d.D;
-  const int Pd = d.pad_out ? 1 : 0;
-  const int ho = d.h + 2 * Pd, wo = d.w + 2 * Pd;
-  const int nfold = 2 * (d.w + d.h);
   const int V = d.X * d.Y * d.Z;
   const int ntask = ctrl[0];
-  const long long fb_off = (long long)(fb - dout);   // fold rows addressed relative to dout
-  const long long zero_off = (long long)(zrow - dout);
   float* trash = lacc + LAYER;
   for (;;) {
     int t = 0;
@@ -1371,7 +1375,7 @@ __global__ __launch_bounds__(64) void vpb_main_k(vfd_voxel_desc d, const int* __
       struct Prm {
         int key, m;
         float w0, w1, w2, w3;
-        long long off;
+        unsigned row;
       };
       auto setup = [&](const float4& e, int g0) {
         Prm q;
@@ -1392,25 +1396,15 @@ __global__ __launch_bounds__(64) void vpb_main_k(vfd_voxel_desc d, const int* __
                     : 0;
         // samples past the end: key -1 (one flush of the open cell, then nothing), a zero row
         q.key = valid ? ((1 - dz) << 8) | ((y0 - yb + 1) << 4) | (x0 - xb + 1) : -1;
-        q.off = zero_off;
-        if (valid) {
-          const int s = __float_as_int(e.w);
-          const int bc = s / hwD, r = s % hwD;
-          const int p = r / d.D, di = r % d.D;
-          const int px = p % d.w, py = p / d.w;
-          const int fs = Pd ? vpb_fold_slot(d, px, py) : -1;
-          q.off = fs >= 0 ? fb_off + ((long long)(bc * nfold + fs) * d.D + di) * CV
-                          : ((long long)((bc * ho + py + Pd) * wo + px + Pd) * d.D + di) * CV;
-        }
+        q.row = valid ? __float_as_uint(e.w) : 0x80000000u;     // past the end: the zero row
         return q;
       };
       auto load_half = [&](const Prm& q, int h, float* gr) {
 #pragma unroll
         for (int j = 0; j < 32; ++j) {
-          const int olo = __builtin_amdgcn_readlane((int)(q.off & 0xFFFFFFFF), h * 32 + j);
-          const int ohi = __builtin_amdgcn_readlane((int)(q.off >> 32), h * 32 + j);
-          const long long o = ((long long)ohi << 32) | (unsigned)olo;
-          gr[j] = dout[o + cl];
+          const unsigned rj = (unsigned)__builtin_amdgcn_readlane((int)q.row, h * 32 + j);
+          const float* src = (rj >> 31) ? fbz : dout;      // wave-uniform: scalar select
+          gr[j] = src[(size_t)(rj & 0x7FFFFFFFu) * CV + cl];
         }
       };
       auto process_half = [&](const Prm& q, int h, const float* gr) {
@@ -1663,14 +1657,14 @@ static VpbWs vpb_ws(const vfd_voxel_desc* d) {
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   VpbWs w;
   w.cnt = 0;
-  w.zero = ncell * 4;                  // one zero row of 64 floats right after the counters
-  w.ptr = w.cnt + al(ncell * 4 + 256);
+  w.zero = al(ncell * 4);              // one zero row of 64 floats right after the counters,
+  w.fold = w.zero + (size_t)d->Cv * 4;  // then the folded rows (fbz = zero row + fold rows)
+  w.ptr = al(w.fold + (size_t)d->B * d->N * 2 * (d->w + d->h) * d->D * d->Cv * 4);
   w.bsum = w.ptr + al(ncell * 4);
   w.boff = w.bsum + al(nblk * 4);
   w.rank = w.boff + al((nblk + 1) * 4);
   w.entries = w.rank + al(nS * 4);
-  w.fold = w.entries + al(nS * 16);
-  w.parts = w.fold + al((size_t)d->B * d->N * 2 * (d->w + d->h) * d->D * d->Cv * 4);
+  w.parts = w.entries + al(nS * 16);
   w.tasks = w.parts + al(nb * 4);
   w.ctrl = w.tasks + al(ntask_max * 8);
   w.total = w.ctrl + al(2 * 4);
@@ -1708,8 +1702,10 @@ int vfd_voxel_project_bwd(const vfd_voxel_desc* d, const float* d_out, const flo
   int* ctrl = (int*)(base + w.ctrl);
   const int ncell = d->B * g.ncell, nblk = cdiv(ncell, VB_SCAN), nb = d->B * g.ntile;
   const int hwD = d->h * d->w * d->D;
+  const size_t dout_rows = (size_t)d->B * d->N * (d->h + 2 * (d->pad_out ? 1 : 0)) * (d->w + 2 * (d->pad_out ? 1 : 0)) * d->D;
+  VFD_REQUIRE(dout_rows < (1ull << 31), "voxel_project_bwd: d_out has too many rows for 31-bit row indices");
   ProfScope ps(K_VPROJ_BWD, s);
-  (void)hipMemsetAsync(cnt, 0, (size_t)ncell * 4 + 256, s);   // counters + zero row
+  (void)hipMemsetAsync(cnt, 0, w.fold, s);   // counters + zero row
   dim3 sgrid(cdiv(hwD, 256), d->B * d->N);
   vpb_count_k<<<sgrid, 256, 0, s>>>(*d, invK, E, cnt, rank);
   vpb_scan1_k<<<nblk, 256, 0, s>>>(cnt, ncell, ptr, bsum);
@@ -1721,7 +1717,7 @@ int vfd_voxel_project_bwd(const vfd_voxel_desc* d, const float* d_out, const flo
     if (d->pad_out) vpb_fold_k<CVV><<<d->B * d->N * 2 * (d->w + d->h), 256, 0, s>>>(*d, d_out, fb); \
     vpb_tile_k<CVV><<<nb, 64, 0, s>>>(*d, ptr, boff, parts, d_vox);                                \
     vpb_tasks_k<<<1, 1024, 0, s>>>(parts, nb, tasks, ctrl);                                        \
-    vpb_main_k<CVV><<<VPB_WORKERS, 64, 0, s>>>(*d, ptr, boff, entries, tasks, ctrl, d_out, fb, zrow, d_vox); \
+    vpb_main_k<CVV><<<VPB_WORKERS, 64, 0, s>>>(*d, ptr, boff, entries, tasks, ctrl, d_out, zrow, d_vox); \
     break;
     VPB_LAUNCH(8)
     VPB_LAUNCH(16)

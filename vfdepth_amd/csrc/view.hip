@@ -115,49 +115,72 @@ __device__ __forceinline__ T block_sum(T v, T* lds) {
   return t;
 }
 
+// Reduce N values (N a power of two <= 64) over the 64 lanes of a wave without LDS or barriers:
+// full butterflies for offsets >= N, then value-halving butterflies (each lane keeps half of its
+// values); lane L ends with the wave total of v[L % N].
+template <int N>
+__device__ __forceinline__ float wave_reduce_n(float (&v)[N]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 32; o >= N; o >>= 1)
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] += __shfl_xor(v[i], o, 64);
+#pragma unroll
+  for (int o = N / 2; o >= 1; o >>= 1) {
+    const bool up = (lane & o) != 0;
+#pragma unroll
+    for (int i = 0; i < o; ++i) {
+      const float a = v[i], b = v[i + o];
+      v[i] = (up ? b : a) + __shfl_xor(up ? a : b, o, 64);
+    }
+  }
+  return v[0];
+}
+
 // ------------------------------------------------------------------------------ stats
-// partial layout [B*N][nblk][n_warp*5 + 2] doubles:
-//   per warp: count(3 per masked pixel), sum w*m, sum r*m, sum w, sum w^2 ; per camera: sum r, sum r^2
+// partial layout [B*N][nblk * 4 waves][n_warp*8 + 2] floats (per-wave sums, fp32 over 256 pixels):
+//   per warp (8 slots): count(3 per masked pixel), sum w*m, sum r*m, sum w, sum w^2, 0, 0, 0;
+//   per camera: sum r, sum r^2.  No barriers: every wave writes its own row.
 __global__ __launch_bounds__(VBLK) void view_stats_k(vfd_view_desc d, const float* __restrict__ depth,
                                                      const float* __restrict__ invK, const float* __restrict__ M,
-                                                     const float* __restrict__ mask, double* __restrict__ partial) {
-  __shared__ double lds[4];
+                                                     const float* __restrict__ mask, float* __restrict__ partial) {
   const Target tg = target_of(d);
   const int bn = tg.bt, b = tg.b, cam = tg.cam;
   const int HW = d.H * d.W;
-  const int nblk = gridDim.x;
-  const int stride = d.n_warp * 5 + 2;
-  double* out = partial + ((size_t)bn * nblk + blockIdx.x) * stride;
+  const int nrow = gridDim.x * (VBLK / 64);
+  const int stride = d.n_warp * 8 + 2;
+  const int lane = threadIdx.x & 63;
+  float* out = partial + ((size_t)bn * nrow + blockIdx.x * (VBLK / 64) + (threadIdx.x >> 6)) * stride;
   const float* ref = d.color[0] + tg.br * 3 * HW;
   const float* rmask = mask + tg.br * HW;
-  float X[VPPT][3];
+  float X[VPPT][3], rv[VPPT][3], rm[VPPT];
   int pix[VPPT];
 #pragma unroll
   for (int k = 0; k < VPPT; ++k) {
     pix[k] = blockIdx.x * VBLK * VPPT + k * VBLK + threadIdx.x;
     float ray[3];
-    if (pix[k] < HW) backproject(invK + bn * 16, depth[(size_t)bn * HW + pix[k]], pix[k] % d.W, pix[k] / d.W, X[k], ray);
+    const bool in = pix[k] < HW;
+    const int pk = in ? pix[k] : 0;
+    backproject(invK + bn * 16, depth[(size_t)bn * HW + pk], pk % d.W, pk / d.W, X[k], ray);
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) rv[k][ch] = in ? ref[ch * HW + pk] : 0.f;
+    rm[k] = rmask[pk];
   }
   {
-    double sr = 0.0, sr2 = 0.0;
+    float v[2] = {0.f, 0.f};
 #pragma unroll
-    for (int k = 0; k < VPPT; ++k) {
-      if (pix[k] >= HW) continue;
+    for (int k = 0; k < VPPT; ++k)
 #pragma unroll
       for (int ch = 0; ch < 3; ++ch) {
-        double r = ref[ch * HW + pix[k]];
-        sr += r;
-        sr2 += r * r;
+        v[0] += rv[k][ch];
+        v[1] += rv[k][ch] * rv[k][ch];
       }
-    }
-    double t0 = block_sum(sr, lds);
-    if (threadIdx.x == 0) out[d.n_warp * 5] = t0;
-    double t1 = block_sum(sr2, lds);
-    if (threadIdx.x == 0) out[d.n_warp * 5 + 1] = t1;
+    const float s = wave_reduce_n<2>(v);
+    if (lane < 2) out[d.n_warp * 8 + lane] = s;
   }
   for (int w = 0; w < d.n_warp; ++w) {
     const WarpEntry e = warp_entry(d, cam, w);
-    double acc[5] = {0, 0, 0, 0, 0};
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (e.src >= 0) {
       const size_t sbn = (size_t)b * d.N + e.src;
       const float* img = d.color[e.fslot] + sbn * 3 * HW;
@@ -167,35 +190,31 @@ __global__ __launch_bounds__(VBLK) void view_stats_k(vfd_view_desc d, const floa
       for (int k = 0; k < VPPT; ++k) {
         if (pix[k] >= HW) continue;
         WarpSample s = warp_sample(Mw, X[k], img, msk, d.H, d.W);
-        const bool m = (rmask[pix[k]] * s.cm) != 0.f;
-        const double mf = m ? 1.0 : 0.0;
-        acc[0] += 3.0 * mf;
+        const float mf = (rm[k] * s.cm) != 0.f ? 1.f : 0.f;
+        acc[0] += 3.f * mf;
 #pragma unroll
         for (int ch = 0; ch < 3; ++ch) {
-          const double wv = s.img[ch], rv = ref[ch * HW + pix[k]];
+          const float wv = s.img[ch];
           acc[1] += wv * mf;
-          acc[2] += rv * mf;
+          acc[2] += rv[k][ch] * mf;
           acc[3] += wv;
           acc[4] += wv * wv;
         }
       }
     }
-#pragma unroll
-    for (int i = 0; i < 5; ++i) {
-      double t = block_sum(acc[i], lds);
-      if (threadIdx.x == 0) out[w * 5 + i] = t;
-    }
+    const float s = wave_reduce_n<8>(acc);
+    if (lane < 8) out[w * 8 + lane] = s;
   }
 }
 
 // coef [B,N,n_warp,4] = (w_mean, w_std, s_mean, s_std); w_std = -1 marks a skipped warp
 // (any sample of the batch without overlap -> warp returned unnormalised, view_rendering.py:50-53)
-__global__ __launch_bounds__(256) void view_finalize_k(vfd_view_desc d, const double* __restrict__ partial, int nblk,
+__global__ __launch_bounds__(256) void view_finalize_k(vfd_view_desc d, const float* __restrict__ partial, int nblk,
                                                        float* __restrict__ coef) {
   // one block per (target slot, warp): fp64 block reductions over the stats partials
   __shared__ double lds[4];
   const int cam = blockIdx.x / d.n_warp, w = blockIdx.x % d.n_warp;
-  const int stride = d.n_warp * 5 + 2;
+  const int stride = d.n_warp * 8 + 2;
   const double n_all = 3.0 * d.H * d.W;
   bool skip = false;
   for (int b = 0; b < d.B; ++b) {
@@ -203,9 +222,9 @@ __global__ __launch_bounds__(256) void view_finalize_k(vfd_view_desc d, const do
     double s[7];
 #pragma unroll
     for (int j = 0; j < 7; ++j) {
-      const int col = j < 5 ? w * 5 + j : d.n_warp * 5 + (j - 5);
+      const int col = j < 5 ? w * 8 + j : d.n_warp * 8 + (j - 5);
       double acc = 0.0;
-      for (int k = threadIdx.x; k < nblk; k += blockDim.x) acc += partial[(bn * nblk + k) * stride + col];
+      for (int k = threadIdx.x; k < nblk; k += blockDim.x) acc += (double)partial[(bn * nblk + k) * stride + col];
       s[j] = block_sum_all(acc, lds);
     }
     if (threadIdx.x == 0) {
@@ -285,17 +304,18 @@ __global__ __launch_bounds__(VBLK) void view_apply_k(vfd_view_desc d, const floa
 }
 
 // ------------------------------------------------------------------------------ backward
-// partial layout [B*N][nblk][n_warp][12] floats (d (K T)[:3] per warp).
+// partial layout [B*N][nblk * 4 waves][n_warp][16] floats (d (K T)[:3] per warp in slots 0..11).
 __global__ __launch_bounds__(VBLK) void view_bwd_k(vfd_view_desc d, const float* __restrict__ depth,
                                                    const float* __restrict__ invK, const float* __restrict__ M,
                                                    const float* __restrict__ mask, const float* __restrict__ coef,
                                                    const float* __restrict__ g_color, const float* __restrict__ g_ovl,
                                                    float* __restrict__ d_depth, float* __restrict__ partial) {
-  __shared__ float lds[4];
   const Target tg = target_of(d);
   const int bn = tg.bt, b = tg.b, cam = tg.cam;
   const int HW = d.H * d.W;
-  const int nblk = gridDim.x;
+  const int nrow = gridDim.x * (VBLK / 64);
+  const int row = blockIdx.x * (VBLK / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   const int T = d.n_temporal, F = d.n_overlap;
   float X[VPPT][3], ray[VPPT][3], dd[VPPT];
   int pix[VPPT];
@@ -307,9 +327,9 @@ __global__ __launch_bounds__(VBLK) void view_bwd_k(vfd_view_desc d, const float*
   }
   for (int w = 0; w < d.n_warp; ++w) {
     const WarpEntry e = warp_entry(d, cam, w);
-    float dM[12];
+    float dM[16];
 #pragma unroll
-    for (int i = 0; i < 12; ++i) dM[i] = 0.f;
+    for (int i = 0; i < 16; ++i) dM[i] = 0.f;
     const float* gsrc = nullptr;
     if (e.src >= 0) {
       gsrc = e.oslot < 0 ? (g_color ? g_color + (((size_t)bn * T + w) * 3) * HW : nullptr)
@@ -360,12 +380,8 @@ __global__ __launch_bounds__(VBLK) void view_bwd_k(vfd_view_desc d, const float*
         dd[k] += dX0 * ray[k][0] + dX1 * ray[k][1] + dX2 * ray[k][2];
       }
     }
-    float* out = partial + (((size_t)bn * nblk + blockIdx.x) * d.n_warp + w) * 12;
-#pragma unroll
-    for (int i = 0; i < 12; ++i) {
-      float t = block_sum(dM[i], lds);
-      if (threadIdx.x == 0) out[i] = t;
-    }
+    const float sm = wave_reduce_n<16>(dM);
+    if (lane < 12) partial[(((size_t)bn * nrow + row) * d.n_warp + w) * 16 + lane] = sm;
   }
 #pragma unroll
   for (int k = 0; k < VPPT; ++k)
@@ -379,7 +395,7 @@ __global__ __launch_bounds__(256) void view_bwd_reduce_k(const float* __restrict
   const int i = blockIdx.x;
   const int j = i % 12, w = (i / 12) % n_warp, bn = i / (12 * n_warp);
   double s = 0.0;
-  for (int k = threadIdx.x; k < nblk; k += blockDim.x) s += (double)partial[(((size_t)bn * nblk + k) * n_warp + w) * 12 + j];
+  for (int k = threadIdx.x; k < nblk; k += blockDim.x) s += (double)partial[(((size_t)bn * nblk + k) * n_warp + w) * 16 + j];
   s = block_sum_all(s, lds);
   if (threadIdx.x == 0) dM[i] = (float)s;
 }
@@ -404,9 +420,9 @@ static unsigned view_red_blocks(const vfd_view_desc* d) { return cdiv((size_t)d-
 extern "C" {
 
 size_t vfd_view_workspace_bytes(const vfd_view_desc* d) {
-  const size_t nblk = view_red_blocks(d);
-  const size_t stats = (size_t)d->B * d->cam_count * nblk * (d->n_warp * 5 + 2) * sizeof(double);
-  const size_t bwd = (size_t)d->B * d->cam_count * nblk * d->n_warp * 12 * sizeof(float);
+  const size_t nrow = (size_t)view_red_blocks(d) * (VBLK / 64);
+  const size_t stats = (size_t)d->B * d->cam_count * nrow * (d->n_warp * 8 + 2) * sizeof(float);
+  const size_t bwd = (size_t)d->B * d->cam_count * nrow * d->n_warp * 16 * sizeof(float);
   return stats > bwd ? stats : bwd;
 }
 
@@ -420,10 +436,10 @@ int vfd_view_fwd(const vfd_view_desc* d, const float* depth, const float* invK, 
   const unsigned nblk = view_red_blocks(d);
   {
     ProfScope ps(K_VIEW_STATS, s);
-    view_stats_k<<<dim3(nblk, d->B * d->cam_count), VBLK, 0, s>>>(*d, depth, invK, M, mask, (double*)ws);
+    view_stats_k<<<dim3(nblk, d->B * d->cam_count), VBLK, 0, s>>>(*d, depth, invK, M, mask, (float*)ws);
   }
   if ((st = fail_launch("view_stats"))) return st;
-  view_finalize_k<<<d->cam_count * d->n_warp, 256, 0, s>>>(*d, (const double*)ws, nblk, coef);
+  view_finalize_k<<<d->cam_count * d->n_warp, 256, 0, s>>>(*d, (const float*)ws, nblk * (VBLK / 64), coef);
   if ((st = fail_launch("view_finalize"))) return st;
   {
     ProfScope ps(K_VIEW_APPLY, s);
@@ -448,7 +464,7 @@ int vfd_view_bwd(const vfd_view_desc* d, const float* depth, const float* invK, 
   }
   if ((st = fail_launch("view_bwd"))) return st;
   const int n = d->B * d->cam_count * d->n_warp * 12;
-  view_bwd_reduce_k<<<n, 256, 0, s>>>((const float*)ws, nblk, d->n_warp, d_M);
+  view_bwd_reduce_k<<<n, 256, 0, s>>>((const float*)ws, nblk * (VBLK / 64), d->n_warp, d_M);
   return fail_launch("view_bwd_reduce");
 }
 

@@ -199,158 +199,187 @@ __global__ __launch_bounds__(256) void photo_finalize_k(vfd_photo_desc d, const 
 }
 
 // ------------------------------------------------------------------------------ backward
-// LDS: images with a +2 reflect halo (pitch TS+4): target + T colours + F overlaps (3 ch each);
-// per-pixel masks with a +1 halo (pitch TS+2); coefficient planes of the current image.
+// Register sliding window, no LDS: a wave owns one image k and a strip of 64 columns (60 output
+// columns + a 2-column halo each side) x PB_R rows and walks it top to bottom, one input row per
+// step: lanes = columns (coalesced row loads), horizontal neighbours by lane shuffles, the last
+// three rows of window sums / coefficient sums kept in registers (ring unrolled by 3).
+//   step i: load row i (reflect-padded) -> horizontal 3-sums of (p, t, pp, tt, pt);
+//           window at m = i-1 -> SSIM chain coefficients (A, B, C) * dL/dphoto(m), summed over
+//           the transposed horizontal window (x2 on the reflect-folded neighbour);
+//           gradient at q = i-2 = vertical transposed sum (A + 2 p B + t C) / 9 + L1 term.
+// The transposed window sums carry the reflect fold: the neighbour term counts twice at
+// q == 1 and q == n-2 (loss_util.py:43-67 pads by reflection before the 3x3 pools).
+constexpr int PB_R = 32;        // output rows per strip
+constexpr int PB_OC = 60;       // output columns per wave
+
+// lane L <- lane L-1 / L+1 of the wave (DPP wave_shr:1 / wave_shl:1: a VALU modifier, no LDS);
+// the end lanes receive 0 (they only feed halo lanes)
+__device__ __forceinline__ float from_left(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float from_right(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xF, 0xF, false));
+}
+
+struct PRow {
+  float hm[3][5];               // horizontal window sums of p, t, p^2, t^2, p*t per channel
+  float cf[3][3];               // transposed horizontal sums of A, B, C per channel
+  float p[3], t[3];             // the pixel's own values
+  float g;                      // dL/dphoto at the pixel
+};
+
 __global__ __launch_bounds__(256) void photo_bwd_k(vfd_photo_desc d, const float* __restrict__ target,
                                                    const float* __restrict__ color, const float* __restrict__ ovl,
                                                    const float* __restrict__ ref_mask, const float* __restrict__ omask,
                                                    const uint8_t* __restrict__ sel, const float* __restrict__ gcoef,
                                                    float* __restrict__ d_color, float* __restrict__ d_ovl) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  constexpr int QT = TS + 4, QA = QT * QT;      // image tiles, halo 2
-  constexpr int MT = TS + 2, MA = MT * MT;      // mask / coefficient tiles, halo 1
   const int T = d.T, F = d.F;
   const int n_img = T + F;
   const PTarget tg = ptarget_of(d);
   const int bn = tg.bt, cam = tg.slot;
   const size_t br = tg.br;
   const int H = d.H, W = d.W, HW = H * W;
-  const int ty0 = blockIdx.y * TS, tx0 = blockIdx.x * TS;
-  float* img = smem;                                   // (1 + n_img) * 3 * QA
-  float* mrm = img + (1 + n_img) * 3 * QA;             // ref mask       MA
-  float* mom = mrm + MA;                               // overlap masks  F * MA
-  float* msel = mom + F * MA;                          // selection      MA (as float)
-  float* coef = msel + MA;                             // 9 * MA: (A, B, C) x 3 channels
-  for (int i = threadIdx.x; i < QA; i += blockDim.x) {
-    const int ly = i / QT, lx = i % QT;
-    const int gy = min(max(reflect1(ty0 + ly - 2, H), 0), H - 1);
-    const int gx = min(max(reflect1(tx0 + lx - 2, W), 0), W - 1);
-    const size_t off = (size_t)gy * W + gx;
-#pragma unroll
-    for (int ch = 0; ch < 3; ++ch) img[ch * QA + i] = target[(br * 3 + ch) * HW + off];
-    for (int k = 0; k < n_img; ++k) {
-      const float* src = k < T ? color + (((size_t)bn * T + k) * 3) * HW : ovl + (((size_t)bn * F + (k - T)) * 3) * HW;
-#pragma unroll
-      for (int ch = 0; ch < 3; ++ch) img[(3 + 3 * k + ch) * QA + i] = src[(size_t)ch * HW + off];
-    }
-  }
-  for (int i = threadIdx.x; i < MA; i += blockDim.x) {
-    const int gy = ty0 + i / MT - 1, gx = tx0 + i % MT - 1;
-    const bool in = gy >= 0 && gy < H && gx >= 0 && gx < W;
-    const size_t p = (size_t)gy * W + gx;
-    mrm[i] = in ? ref_mask[br * HW + p] : 0.f;
-    for (int s = 0; s < F; ++s) mom[s * MA + i] = in ? omask[((size_t)bn * F + s) * HW + p] : 0.f;
-    msel[i] = in ? (float)sel[(size_t)bn * HW + p] : -1.f;
-  }
-  __syncthreads();
+  const int nsx = (W + PB_OC - 1) / PB_OC, nsy = (H + PB_R - 1) / PB_R;
+  const int task = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (task >= n_img * nsx * nsy) return;                 // whole wave; no barriers below
+  const int k = task % n_img, sx = (task / n_img) % nsx, sy = task / (n_img * nsx);
+  const int lane = threadIdx.x & 63;
+  const int c = sx * PB_OC - 2 + lane;
+  const bool col_in = c >= 0 && c < W;
+  const bool out_lane = lane >= 2 && lane < 2 + PB_OC && col_in;
+  const int cr = min(max(c < 0 ? -c : (c > W - 1 ? 2 * (W - 1) - c : c), 0), W - 1);
+  const int cc = min(max(c, 0), W - 1);                  // clamped real column (masks)
+  const int r0 = sy * PB_R, r1 = min(r0 + PB_R, H);
+  const float* P = k < T ? color + (((size_t)bn * T + k) * 3) * HW : ovl + (((size_t)bn * F + (k - T)) * 3) * HW;
+  const float* Tg = target + br * 3 * HW;
+  float* dst = k < T ? d_color + (((size_t)bn * T + k) * 3) * HW : d_ovl + (((size_t)bn * F + (k - T)) * 3) * HW;
   const float gR = gcoef[cam * 3 + 0], gS = gcoef[cam * 3 + 1], gT = gcoef[cam * 3 + 2];
-  const int qy = threadIdx.x / TS, qx = threadIdx.x % TS;      // output pixel in tile
-  const int gy = ty0 + qy, gx = tx0 + qx;
-  const bool inside = gy < H && gx < W;
-  // row / column multisets of windows touching q, with the reflect fold
-  int rows[5], cols[5], nr = 0, nc = 0;
-  if (inside) {
-    for (int dy = -1; dy <= 1; ++dy) if (gy + dy >= 0 && gy + dy < H) rows[nr++] = gy + dy;
-    if (gy == 1) rows[nr++] = 0;
-    if (gy == H - 2) rows[nr++] = H - 1;
-    for (int dx = -1; dx <= 1; ++dx) if (gx + dx >= 0 && gx + dx < W) cols[nc++] = gx + dx;
-    if (gx == 1) cols[nc++] = 0;
-    if (gx == W - 2) cols[nc++] = W - 1;
-  }
-  for (int k = 0; k < n_img; ++k) {
-    // ---- dL/dphoto at every output pixel of the +1 halo, then SSIM chain coefficients
-    for (int i = threadIdx.x; i < MA; i += blockDim.x) {
-      const int my = i / MT, mx = i % MT;
-      float gph = 0.f;
-      const float sv = msel[i];
-      if (sv >= 0.f) {
-        const int sb = (int)sv;
-        const float rm = mrm[i];
-        const float am = ((sb & 4) ? 1.f : 0.f) * rm;
-        if (k < T) {
-          if ((sb & 3) == k) gph = gR * am;
-        } else if (k == T) {
-          gph = gS * (rm * mom[i]);
-        } else {
-          const int f = k - T - 1;
-          if (((sb >> 3) & 3) == f) {
-            float mst = 0.f;
-            for (int ff = 0; ff < T; ++ff) {
-              const float pm = rm * mom[(1 + ff) * MA + i] * am;
-              mst = ff == 0 ? pm : fmaxf(mst, pm);
-            }
-            gph = gT * mst;
-          }
+  const float wl = c == 1 ? 2.f : 1.f, wr = c == W - 2 ? 2.f : 1.f;
+  const uint8_t* selb = sel + (size_t)bn * HW;
+  const float* rmb = ref_mask + br * HW;
+  const float* omb = omask + (size_t)bn * F * HW;
+
+  // dL/dphoto_k at real pixel (m, c) (0 outside the map)
+  auto gph_at = [&](int m) {
+    float gph = 0.f;
+    if (m >= 0 && m < H && col_in) {
+      const size_t pm = (size_t)m * W + cc;
+      const int sb = selb[pm];
+      const float rm = rmb[pm];
+      const float am = ((sb & 4) ? 1.f : 0.f) * rm;
+      if (k < T) {
+        if ((sb & 3) == k) gph = gR * am;
+      } else if (k == T) {
+        gph = gS * (rm * omb[pm]);
+      } else if (((sb >> 3) & 3) == k - T - 1) {
+        float mst = 0.f;
+        for (int ff = 0; ff < T; ++ff) {
+          const float pmv = rm * omb[(size_t)(1 + ff) * HW + pm] * am;
+          mst = ff == 0 ? pmv : fmaxf(mst, pmv);
         }
+        gph = gT * mst;
       }
+    }
+    return gph;
+  };
+
+  auto step = [&](int i, PRow& nw, PRow& o1, PRow& o2) {
+    if (i > r1 + 1) return;
+    // ---- (1) input row i of the reflect-padded images
+    if (i >= -1 && i <= H) {
+      const int ri = i < 0 ? -i : (i > H - 1 ? 2 * (H - 1) - i : i);
+      const size_t off = (size_t)ri * W + cr;
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) {
+        const float p = P[(size_t)ch * HW + off], tv = Tg[(size_t)ch * HW + off];
+        nw.p[ch] = p;
+        nw.t[ch] = tv;
+        const float pl = from_left(p), pr = from_right(p);
+        const float tl = from_left(tv), tr = from_right(tv);
+        nw.hm[ch][0] = pl + p + pr;
+        nw.hm[ch][1] = tl + tv + tr;
+        nw.hm[ch][2] = pl * pl + p * p + pr * pr;
+        nw.hm[ch][3] = tl * tl + tv * tv + tr * tr;
+        nw.hm[ch][4] = pl * tl + p * tv + pr * tr;
+      }
+    } else {
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) {
+        nw.p[ch] = nw.t[ch] = 0.f;
+#pragma unroll
+        for (int q = 0; q < 5; ++q) nw.hm[ch][q] = 0.f;
+      }
+    }
+    // ---- (2) window centred at m = i - 1 -> coefficient sums of row m (slot o1)
+    {
+      const int m = i - 1;
+      const float gph = gph_at(m);
+      o1.g = gph;
 #pragma unroll
       for (int ch = 0; ch < 3; ++ch) {
         float A = 0.f, Bc = 0.f, Cc = 0.f;
         if (gph != 0.f) {
-          const float* P = img + (3 + 3 * k + ch) * QA;
-          const float* Tt = img + ch * QA;
-          const Moments m = window(P, Tt, QT, my + 1, mx + 1);
-          const float mpt = m.mp * m.mt, mp2 = m.mp * m.mp, mt2 = m.mt * m.mt;
-          const float A1 = 2.f * mpt + C1, A2 = 2.f * (m.spt - mpt) + C2;
-          const float B1 = mp2 + mt2 + C1, B2 = (m.spp - mp2) + (m.stt - mt2) + C2;
-          const float Dn = B1 * B2 + 1e-8f;
-          const float ssim = (A1 * A2) / Dn;
-          const float lv = (1.f - ssim) / 2.f;
+          // window means: sums * (1/9) (the backward's arithmetic need not repeat the forward's
+          // division; the clamp test below sits on ssim, far from rounding at +-1)
+          constexpr float inv9 = 1.f / 9.f;
+          const float mp = (o2.hm[ch][0] + o1.hm[ch][0] + nw.hm[ch][0]) * inv9;
+          const float mt = (o2.hm[ch][1] + o1.hm[ch][1] + nw.hm[ch][1]) * inv9;
+          const float spp = (o2.hm[ch][2] + o1.hm[ch][2] + nw.hm[ch][2]) * inv9;
+          const float stt = (o2.hm[ch][3] + o1.hm[ch][3] + nw.hm[ch][3]) * inv9;
+          const float spt = (o2.hm[ch][4] + o1.hm[ch][4] + nw.hm[ch][4]) * inv9;
+          const float mpt = mp * mt, mp2 = mp * mp, mt2 = mt * mt;
+          const float A1 = 2.f * mpt + C1, A2 = 2.f * (spt - mpt) + C2;
+          const float B1 = mp2 + mt2 + C1, B2 = (spp - mp2) + (stt - mt2) + C2;
+          const float rDn = 1.f / (B1 * B2 + 1e-8f);
+          const float ssim = (A1 * A2) * rDn;
+          const float lv = (1.f - ssim) * 0.5f;
           if (lv >= 0.f && lv <= 1.f) {
-            const float g = gph * (0.85f / 3.f) * -0.5f;
-            A = g * ((2.f * m.mt * (A2 - A1)) / Dn - ssim * (2.f * m.mp * (B2 - B1)) / Dn);
-            Bc = g * (-ssim * B1 / Dn);
-            Cc = g * (2.f * A1 / Dn);
+            const float g = gph * (0.85f / 3.f) * -0.5f * rDn;
+            A = g * (2.f * mt * (A2 - A1) - ssim * (2.f * mp * (B2 - B1)));
+            Bc = g * (-ssim * B1);
+            Cc = g * (2.f * A1);
           }
         }
-        coef[(ch * 3 + 0) * MA + i] = A;
-        coef[(ch * 3 + 1) * MA + i] = Bc;
-        coef[(ch * 3 + 2) * MA + i] = Cc;
+        o1.cf[ch][0] = from_left(A) * wl + A + from_right(A) * wr;
+        o1.cf[ch][1] = from_left(Bc) * wl + Bc + from_right(Bc) * wr;
+        o1.cf[ch][2] = from_left(Cc) * wl + Cc + from_right(Cc) * wr;
       }
     }
-    __syncthreads();
-    if (inside) {
-      const int ci = (qy + 2) * QT + qx + 2;
-      const int mi = (qy + 1) * MT + qx + 1;
-      // dL/dphoto at q itself for the L1 term
-      float gq = 0.f;
-      {
-        const float sv = msel[mi];
-        const int sb = (int)sv;
-        const float rm = mrm[mi];
-        const float am = ((sb & 4) ? 1.f : 0.f) * rm;
-        if (k < T) {
-          if ((sb & 3) == k) gq = gR * am;
-        } else if (k == T) {
-          gq = gS * (rm * mom[mi]);
-        } else if (((sb >> 3) & 3) == k - T - 1) {
-          float mst = 0.f;
-          for (int ff = 0; ff < T; ++ff) {
-            const float pm = rm * mom[(1 + ff) * MA + mi] * am;
-            mst = ff == 0 ? pm : fmaxf(mst, pm);
-          }
-          gq = gT * mst;
-        }
-      }
-      float* dst = k < T ? d_color + (((size_t)bn * T + k) * 3) * HW : d_ovl + (((size_t)bn * F + (k - T)) * 3) * HW;
+    // ---- (3) gradient at real row q = i - 2: rows q-1 (slot nw, not yet reused), q (o2), q+1 (o1)
+    const int q = i - 2;
+    if (q >= r0 && q < r1) {
+      const float vl = q == 1 ? 2.f : 1.f, vr = q == H - 2 ? 2.f : 1.f;
+      const size_t off = (size_t)q * W + cc;
 #pragma unroll
       for (int ch = 0; ch < 3; ++ch) {
-        float sA = 0.f, sB = 0.f, sC = 0.f;
-        for (int a = 0; a < nr; ++a)
-          for (int c2 = 0; c2 < nc; ++c2) {
-            const int m = (rows[a] - ty0 + 1) * MT + (cols[c2] - tx0 + 1);
-            sA += coef[(ch * 3 + 0) * MA + m];
-            sB += coef[(ch * 3 + 1) * MA + m];
-            sC += coef[(ch * 3 + 2) * MA + m];
-          }
-        const float pv = img[(3 + 3 * k + ch) * QA + ci], tv = img[ch * QA + ci];
-        float g = (sA + 2.f * pv * sB + tv * sC) / 9.f;
+        const float sA = nw.cf[ch][0] * vl + o2.cf[ch][0] + o1.cf[ch][0] * vr;
+        const float sB = nw.cf[ch][1] * vl + o2.cf[ch][1] + o1.cf[ch][1] * vr;
+        const float sC = nw.cf[ch][2] * vl + o2.cf[ch][2] + o1.cf[ch][2] * vr;
+        const float pv = o2.p[ch], tv = o2.t[ch];
+        float g = (sA + 2.f * pv * sB + tv * sC) * (1.f / 9.f);
         const float diff = tv - pv;
-        g += gq * (0.15f / 3.f) * (diff > 0.f ? -1.f : (diff < 0.f ? 1.f : 0.f));
-        dst[(size_t)ch * HW + (size_t)gy * W + gx] = g;
+        g += o2.g * (0.15f / 3.f) * (diff > 0.f ? -1.f : (diff < 0.f ? 1.f : 0.f));
+        if (out_lane) dst[(size_t)ch * HW + off] = g;
       }
     }
-    __syncthreads();
+  };
+
+  PRow R0, R1, R2;
+  for (PRow* r : {&R0, &R1, &R2}) {
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+#pragma unroll
+      for (int q = 0; q < 5; ++q) r->hm[ch][q] = 0.f;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) r->cf[ch][q] = 0.f;
+      r->p[ch] = r->t[ch] = 0.f;
+    }
+    r->g = 0.f;
+  }
+  for (int i = r0 - 2; i <= r1 + 1; i += 3) {
+    step(i, R0, R2, R1);
+    step(i + 1, R1, R0, R2);
+    step(i + 2, R2, R1, R0);
   }
 }
 
@@ -495,12 +524,11 @@ int vfd_photo_bwd(const vfd_photo_desc* d, const float* target, const float* col
   int st = check_photo(d);
   if (st) return st;
   hipStream_t s = (hipStream_t)stream;
-  dim3 g = photo_grid(d);
   const int n_img = d->T + d->F;
-  const int QA = (TS + 4) * (TS + 4), MA = (TS + 2) * (TS + 2);
-  const size_t lds = ((size_t)(1 + n_img) * 3 * QA + (size_t)(2 + d->F) * MA + 9 * MA) * sizeof(float);
+  const int ntask = n_img * cdiv(d->W, PB_OC) * cdiv(d->H, PB_R);
   ProfScope ps(K_PHOTO_BWD, s);
-  photo_bwd_k<<<g, 256, lds, s>>>(*d, target, color, ovl, ref_mask, omask, sel, gcoef, d_color, d_ovl);
+  photo_bwd_k<<<dim3(cdiv(ntask, 4), 1, d->B * d->cam_count), 256, 0, s>>>(*d, target, color, ovl, ref_mask, omask, sel,
+                                                                       gcoef, d_color, d_ovl);
   return fail_launch("photo_bwd");
 }
 

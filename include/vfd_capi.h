@@ -87,7 +87,9 @@ int vfd_fusion_plan(const vfd_voxel_desc* d, const float* mask_lo, const float* 
 int vfd_fuse_pose_fwd(const vfd_voxel_desc* d, const float* mask_lo, const float* K, const float* Einv,
                       const float* feats_cl, float* out, void* stream);
 /* d_out in the forward's output layout -> d_feats [B,N,C,h,w] (every element written).
- * Atomic-free gather through the plan's per-pixel inverse index. */
+ * Atomic-free gather over the plan's 4x4-pixel tile buckets, pulled from the plan's task queue
+ * (heavy tiles split by channel group); the call resets the queue's work counter inside `plan`,
+ * so calls sharing one plan must be stream-ordered. */
 int vfd_fuse_pose_bwd(const vfd_voxel_desc* d, const void* plan, const int* counts, const float* d_out,
                       float* d_feats, void* stream);
 

@@ -572,7 +572,7 @@ constexpr int PT2 = PT * PT;
 
 struct TileItem {
   uint32_t pz;       // padded XY position in d_out (bits 0-19) | z (20-27) | reflect copies exist (bit 28)
-  float den;         // count + 1e-7 (volumetric_fusionnet.py:162)
+  float rden;        // 1 / (count + 1e-7) (volumetric_fusionnet.py:162)
   float w[4];        // ATen bilinear weights of taps (x0,y0) (x0+1,y0) (x0,y0+1) (x0+1,y0+1); 0 outside the tile
   int32_t lxy;       // tap 0 relative to the tile origin: (ly + 1) * 8 + (lx + 1), lx, ly in [-1, PT-1]
   uint32_t pad;
@@ -692,7 +692,7 @@ __global__ __launch_bounds__(256) void plan_fill_k(vfd_voxel_desc d, const PlanE
   const bool fold = d.pad_out && (xi == 1 || xi == d.X - 2 || yi == 1 || yi == d.Y - 2);
   TileItem it;
   it.pz = (uint32_t)((yi + P1) * (d.X + 2 * P1) + xi + P1) | ((uint32_t)zi << 20) | ((fold ? 1u : 0u) << 28);
-  it.den = e.den;
+  it.rden = 1.f / e.den;
   it.pad = 0;
   float w[4];
   entry_weights(e, w);
@@ -714,6 +714,62 @@ __global__ __launch_bounds__(256) void plan_fill_k(vfd_voxel_desc d, const PlanE
   }
 }
 
+// Load balance of the backward: tiles at the horizon collect ~10x the mean item count.  Tiles
+// with more than PBW_SPLIT items are split into one workgroup per 64-channel group (disjoint
+// outputs: no combine step), and those tasks are queued first; the kernel pulls tasks from a
+// counter.  tasks[i] = {bc * nt + tile, group | 1 << 8} for a split tile (POSE_MAXC / 64 groups,
+// independent of C: the plan is built without it; groups beyond C are skipped), {bc * nt + tile,
+// 0 | 0xFF << 8} for a whole tile.
+constexpr int PBW_SPLIT = 384;
+
+__global__ __launch_bounds__(1024) void plan_task_k(vfd_voxel_desc d, const int* __restrict__ tile_ptr,
+                                                    int2* __restrict__ tasks, int* __restrict__ ctrl) {
+  __shared__ int part[1024];
+  __shared__ int n_heavy_tasks;
+  const int nt = tiles_x(d) * tiles_y(d);
+  const int M = d.B * d.N * nt;
+  constexpr int ng = POSE_MAXC / 64;
+  const int t = threadIdx.x;
+  const int chunk = (M + 1023) / 1024;
+  const int c0 = min(M, t * chunk), c1 = min(M, c0 + chunk);
+  auto heavy = [&](int i) {
+    const int bc = i / nt, tile = i % nt;
+    const int* tp = tile_ptr + (size_t)bc * (nt + 1);
+    return tp[tile + 1] - tp[tile] > PBW_SPLIT;
+  };
+  for (int pass = 0; pass < 2; ++pass) {           // pass 0: heavy tiles (ng tasks), 1: light
+    int local = 0;
+    for (int i = c0; i < c1; ++i) {
+      const bool h = heavy(i);
+      local += pass == 0 ? (h ? ng : 0) : (h ? 0 : 1);
+    }
+    __syncthreads();
+    part[t] = local;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+      const int v = t >= off ? part[t - off] : 0;
+      __syncthreads();
+      part[t] += v;
+      __syncthreads();
+    }
+    int run = part[t] - local + (pass == 1 ? n_heavy_tasks : 0);
+    for (int i = c0; i < c1; ++i) {
+      const bool h = heavy(i);
+      if (pass == 0 && h) {
+        for (int g = 0; g < ng; ++g) tasks[run++] = make_int2(i, g | (1 << 8));
+      } else if (pass == 1 && !h) {
+        tasks[run++] = make_int2(i, 0 | (0xFF << 8));
+      }
+    }
+    __syncthreads();
+    if (t == 1023) {
+      if (pass == 0) n_heavy_tasks = part[t];
+      else ctrl[0] = n_heavy_tasks + part[t];
+    }
+    __syncthreads();
+  }
+}
+
 #ifndef VFD_PBW_U
 #define VFD_PBW_U 8
 #endif
@@ -721,120 +777,135 @@ constexpr int PBW_U = VFD_PBW_U;       // voxel rows (1 KB each) in flight per w
 
 __global__ __launch_bounds__(256) void fuse_pose_bwd_k(vfd_voxel_desc d, const int* __restrict__ tile_ptr,
                                                        const TileItem* __restrict__ items,
+                                                       const int2* __restrict__ tasks, int* __restrict__ ctrl,
                                                        const float* __restrict__ dout, float* __restrict__ dfeats) {
   extern __shared__ float red[];         // [C][PT2 + 1]: one wave's tile, then the transposed sum
+  __shared__ int task_l;
   const int hw = d.h * d.w;
   const int V = d.X * d.Y * d.Z;
   const int C = d.C, C1 = d.C + 1;
   const int ntx = tiles_x(d), nt = ntx * tiles_y(d);
-  // XCD-aware numbering: XCD k takes the contiguous task range [k*per, (k+1)*per) of
-  // (camera, tile), so neighbouring tiles' NCHW row segments merge in one L2
-  const int per = gridDim.x / 8;
-  const int task = (blockIdx.x % 8) * per + blockIdx.x / 8;
-  if (task >= nt * d.B * d.N) return;
-  const int bc = task / nt, b = bc / d.N, tile = task % nt;
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int P = d.pad_out ? 2 : 0;
   const int Yo = d.Y + P, Xo = d.X + P;
   const size_t pix_stride = (size_t)d.Z * C1;
-  const int* tp = tile_ptr + (size_t)bc * (nt + 1);
-  const TileItem* ib = items + (size_t)bc * 4 * V;
-  const float* gb = dout + (size_t)b * Yo * Xo * pix_stride;
-  const int lo = __builtin_amdgcn_readfirstlane(tp[tile]), hi = __builtin_amdgcn_readfirstlane(tp[tile + 1]);
-  // register accumulators: one 16-pixel array per 64-channel group, indexed by the wave-uniform
-  // tap pixel (register-indexed moves, no scratch)
-  float a0[PT2], a1[PT2], a2[PT2], a3[PT2];
+  const int ntask = ctrl[0];
+  constexpr int LD = PT2 + 1;
+  for (;;) {
+    __syncthreads();
+    if (threadIdx.x == 0) task_l = atomicAdd(ctrl + 1, 1);
+    __syncthreads();
+    const int task = task_l;
+    if (task >= ntask) break;
+    const int2 tk = tasks[task];
+    const int bc = tk.x / nt, b = bc / d.N, tile = tk.x % nt;
+    const int g0 = tk.y & 0xFF;                      // channel groups [g0, g0 + ng) of 64
+    const int ng = min(tk.y >> 8, (C + 63) / 64 - g0);
+    if (ng <= 0) continue;                           // a split group beyond C (workgroup-uniform)
+    const int* tp = tile_ptr + (size_t)bc * (nt + 1);
+    const TileItem* ib = items + (size_t)bc * 4 * V;
+    const float* gb = dout + (size_t)b * Yo * Xo * pix_stride;
+    const int lo = __builtin_amdgcn_readfirstlane(tp[tile]), hi = __builtin_amdgcn_readfirstlane(tp[tile + 1]);
+    // register accumulators: one 16-pixel array per 64-channel group, indexed by the wave-uniform
+    // tap pixel (register-indexed moves, no scratch)
+    float a0[PT2], a1[PT2], a2[PT2], a3[PT2];
 #pragma unroll
-  for (int i = 0; i < PT2; ++i) a0[i] = a1[i] = a2[i] = a3[i] = 0.f;
-  int cho[4];
+    for (int i = 0; i < PT2; ++i) a0[i] = a1[i] = a2[i] = a3[i] = 0.f;
+    int cho[4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) cho[k] = min(lane + 64 * k, C - 1);
-  for (int j = lo + wv * PBW_U; j < hi; j += 4 * PBW_U) {
-    TileItem it[PBW_U];
-    float g[PBW_U][4];
+    for (int k = 0; k < 4; ++k) cho[k] = min(lane + 64 * (g0 + k), C - 1);
+    for (int j = lo + wv * PBW_U; j < hi; j += 4 * PBW_U) {
+      TileItem it[PBW_U];
+      float g[PBW_U][4];
 #pragma unroll
-    for (int u = 0; u < PBW_U; ++u) {
-      it[u] = ib[min(j + u, hi - 1)];                     // tail slots re-read the last item (skipped below)
-      const float* row = gb + (size_t)(it[u].pz & 0xFFFFF) * pix_stride + ((it[u].pz >> 20) & 0xFF) * C1;
+      for (int u = 0; u < PBW_U; ++u) {
+        it[u] = ib[min(j + u, hi - 1)];                     // tail slots re-read the last item (skipped below)
+        const float* row = gb + (size_t)(it[u].pz & 0xFFFFF) * pix_stride + ((it[u].pz >> 20) & 0xFF) * C1;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) g[u][k] = row[cho[k]];
-    }
+        for (int k = 0; k < 4; ++k) g[u][k] = k < ng ? row[cho[k]] : 0.f;
+      }
 #pragma unroll
-    for (int u = 0; u < PBW_U; ++u) {
-      if (j + u >= hi) continue;
-      if (it[u].pz >> 28) {                               // reflect-padding copies (grid border)
-        const int pos = it[u].pz & 0xFFFFF, zo = ((it[u].pz >> 20) & 0xFF) * C1;
-        const int xi = pos % Xo - P / 2, yi = pos / Xo - P / 2;
-        int rows[3], cols[3], nr, nc;
-        pad_sets(yi, d.Y, d.pad_out, rows, &nr);
-        pad_sets(xi, d.X, d.pad_out, cols, &nc);
-        for (int a = 0; a < nr; ++a)
-          for (int c2 = 0; c2 < nc; ++c2) {
-            if (a == 0 && c2 == 0) continue;
-            const float* row = gb + ((size_t)rows[a] * Xo + cols[c2]) * pix_stride + zo;
+      for (int u = 0; u < PBW_U; ++u) {
+        if (j + u >= hi) continue;
+        if (it[u].pz >> 28) {                               // reflect-padding copies (grid border)
+          const int pos = it[u].pz & 0xFFFFF, zo = ((it[u].pz >> 20) & 0xFF) * C1;
+          const int xi = pos % Xo - P / 2, yi = pos / Xo - P / 2;
+          int rows[3], cols[3], nr, nc;
+          pad_sets(yi, d.Y, d.pad_out, rows, &nr);
+          pad_sets(xi, d.X, d.pad_out, cols, &nc);
+          for (int a = 0; a < nr; ++a)
+            for (int c2 = 0; c2 < nc; ++c2) {
+              if (a == 0 && c2 == 0) continue;
+              const float* row = gb + ((size_t)rows[a] * Xo + cols[c2]) * pix_stride + zo;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) g[u][k] += row[cho[k]];
+              for (int k = 0; k < 4; ++k)
+                if (k < ng) g[u][k] += row[cho[k]];
+            }
+        }
+        const int lx = (it[u].lxy & 7) - 1, ly = (it[u].lxy >> 3) - 1;
+        // d(mean) = g / den (as g * (1/den)), then grid_sample's backward adds d(mean) * w
+        float gd[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) gd[k] = g[u][k] * it[u].rden;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (it[u].w[q] != 0.f) {
+            const int pl = __builtin_amdgcn_readfirstlane((ly + (q >> 1)) * PT + lx + (q & 1));
+            const float w = it[u].w[q];
+            a0[pl] += gd[0] * w;
+            if (ng > 1) {
+              a1[pl] += gd[1] * w;
+              a2[pl] += gd[2] * w;
+              a3[pl] += gd[3] * w;
+            }
           }
       }
-      const int lx = (it[u].lxy & 7) - 1, ly = (it[u].lxy >> 3) - 1;
-      // reference order: d(mean) = g / den, then grid_sample's backward adds d(mean) * w
-      float gd[4];
+    }
+    // sum the four waves' tiles in a fixed order ((w0 + w1) + w2) + w3 through one [C][PT2+1]
+    // LDS tile (rows = the task's channels), then write the tile NCHW with lanes along pixels
+    const int cbase = 64 * g0, cn = min(C - cbase, 64 * ng);
+    for (int src = 1; src < 4; ++src) {
+      if (wv == src) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) gd[k] = g[u][k] / it[u].den;
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (it[u].w[q] != 0.f) {
-          const int pl = __builtin_amdgcn_readfirstlane((ly + (q >> 1)) * PT + lx + (q & 1));
-          const float w = it[u].w[q];
-          a0[pl] += gd[0] * w;
-          a1[pl] += gd[1] * w;
-          a2[pl] += gd[2] * w;
-          a3[pl] += gd[3] * w;
+        for (int i = 0; i < PT2; ++i) {
+          if (lane < cn) red[lane * LD + i] = a0[i];
+          if (lane + 64 < cn) red[(lane + 64) * LD + i] = a1[i];
+          if (lane + 128 < cn) red[(lane + 128) * LD + i] = a2[i];
+          if (lane + 192 < cn) red[(lane + 192) * LD + i] = a3[i];
         }
-    }
-  }
-  // sum the four waves' tiles in a fixed order ((w0 + w1) + w2) + w3 through one [C][PT2+1]
-  // LDS tile, then write the tile NCHW with lanes along pixels
-  constexpr int LD = PT2 + 1;
-  for (int src = 1; src < 4; ++src) {
-    if (wv == src) {
-#pragma unroll
-      for (int i = 0; i < PT2; ++i) {
-        if (lane < C) red[lane * LD + i] = a0[i];
-        if (lane + 64 < C) red[(lane + 64) * LD + i] = a1[i];
-        if (lane + 128 < C) red[(lane + 128) * LD + i] = a2[i];
-        if (lane + 192 < C) red[(lane + 192) * LD + i] = a3[i];
       }
+      __syncthreads();
+      if (wv == 0) {
+#pragma unroll
+        for (int i = 0; i < PT2; ++i) {
+          a0[i] += red[min(lane, cn - 1) * LD + i];
+          if (ng > 1) {
+            a1[i] += red[min(lane + 64, cn - 1) * LD + i];
+            a2[i] += red[min(lane + 128, cn - 1) * LD + i];
+            a3[i] += red[min(lane + 192, cn - 1) * LD + i];
+          }
+        }
+      }
+      __syncthreads();
     }
-    __syncthreads();
     if (wv == 0) {
 #pragma unroll
       for (int i = 0; i < PT2; ++i) {
-        a0[i] += red[cho[0] * LD + i];
-        a1[i] += red[cho[1] * LD + i];
-        a2[i] += red[cho[2] * LD + i];
-        a3[i] += red[cho[3] * LD + i];
+        if (lane < cn) red[lane * LD + i] = a0[i];
+        if (lane + 64 < cn) red[(lane + 64) * LD + i] = a1[i];
+        if (lane + 128 < cn) red[(lane + 128) * LD + i] = a2[i];
+        if (lane + 192 < cn) red[(lane + 192) * LD + i] = a3[i];
       }
     }
     __syncthreads();
-  }
-  if (wv == 0) {
-#pragma unroll
-    for (int i = 0; i < PT2; ++i) {
-      if (lane < C) red[lane * LD + i] = a0[i];
-      if (lane + 64 < C) red[(lane + 64) * LD + i] = a1[i];
-      if (lane + 128 < C) red[(lane + 128) * LD + i] = a2[i];
-      if (lane + 192 < C) red[(lane + 192) * LD + i] = a3[i];
+    const int tx = tile % ntx, ty = tile / ntx;
+    float* db = dfeats + ((size_t)bc * C + cbase) * hw;
+    for (int i = threadIdx.x; i < cn * PT2; i += blockDim.x) {
+      const int ch = i / PT2, pl = i % PT2;
+      const int x = tx * PT + pl % PT, y = ty * PT + pl / PT;
+      if (x < d.w && y < d.h) db[(size_t)ch * hw + y * d.w + x] = red[ch * LD + pl];
     }
-  }
-  __syncthreads();
-  const int tx = tile % ntx, ty = tile / ntx;
-  float* db = dfeats + (size_t)bc * C * hw;
-  for (int i = threadIdx.x; i < C * PT2; i += blockDim.x) {
-    const int ch = i / PT2, pl = i % PT2;
-    const int x = tx * PT + pl % PT, y = ty * PT + pl / PT;
-    if (x < d.w && y < d.h) db[(size_t)ch * hw + y * d.w + x] = red[ch * LD + pl];
   }
 }
 
@@ -1554,9 +1625,16 @@ static size_t plan_cursor_bytes(const vfd_voxel_desc* d) {
   return ((size_t)d->B * d->N * host_tiles(d) * sizeof(int) + 255) / 256 * 256;
 }
 
+static size_t plan_items_bytes(const vfd_voxel_desc* d) {
+  return (size_t)d->B * d->N * 4 * d->X * d->Y * d->Z * sizeof(TileItem);
+}
+static size_t plan_tasks_bytes(const vfd_voxel_desc* d) {     // independent of C (see plan_task_k)
+  return ((size_t)d->B * d->N * host_tiles(d) * (POSE_MAXC / 64) * sizeof(int2) + 255) / 256 * 256;
+}
+
 size_t vfd_fusion_plan_bytes(const vfd_voxel_desc* d) {
-  return plan_entries_bytes(d) + plan_rowptr_bytes(d) + plan_cursor_bytes(d) +
-         (size_t)d->B * d->N * 4 * d->X * d->Y * d->Z * sizeof(TileItem);
+  return plan_entries_bytes(d) + plan_rowptr_bytes(d) + plan_cursor_bytes(d) + plan_items_bytes(d) +
+         plan_tasks_bytes(d) + 256;
 }
 
 int vfd_fusion_plan(const vfd_voxel_desc* d, const float* mask_lo, const float* K, const float* Einv, void* plan,
@@ -1585,6 +1663,9 @@ int vfd_fusion_plan(const vfd_voxel_desc* d, const float* mask_lo, const float* 
   plan_count_k<<<egrid, 256, hist, s>>>(*d, (const PlanEntry*)plan, counts, cursor);
   plan_scan_k<<<d->B * d->N, PIDX_THREADS, 0, s>>>(*d, cursor, row_ptr);
   plan_fill_k<<<egrid, 256, 2 * hist, s>>>(*d, (const PlanEntry*)plan, counts, cursor, csr);
+  int2* tasks = (int2*)((char*)csr + plan_items_bytes(d));
+  int* ctrl = (int*)((char*)tasks + plan_tasks_bytes(d));
+  plan_task_k<<<1, 1024, 0, s>>>(*d, row_ptr, tasks, ctrl);
   return fail_launch("fusion_plan");
 }
 
@@ -1616,10 +1697,13 @@ int vfd_fuse_pose_bwd(const vfd_voxel_desc* d, const void* plan, const int* coun
   const int hw = d->h * d->w;
   const int* row_ptr = (const int*)((const char*)plan + plan_entries_bytes(d));
   const TileItem* csr = (const TileItem*)((const char*)row_ptr + plan_rowptr_bytes(d) + plan_cursor_bytes(d));
+  const int2* tasks = (const int2*)((const char*)csr + plan_items_bytes(d));
+  int* ctrl = (int*)((char*)tasks + plan_tasks_bytes(d));      // {task count, work counter}
   ProfScope ps(K_FUSE_POSE_BWD, s);
-  const int ntask = host_tiles(d) * d->B * d->N;
-  fuse_pose_bwd_k<<<dim3(8 * cdiv(ntask, 8)), 256, (size_t)(PT2 + 1) * d->C * sizeof(float), s>>>(
-      *d, row_ptr, csr, d_out, d_feats);
+  (void)hipMemsetAsync(ctrl + 1, 0, sizeof(int), s);
+  const int ntask = host_tiles(d) * d->B * d->N * (POSE_MAXC / 64);
+  fuse_pose_bwd_k<<<dim3(std::min(ntask, 1024)), 256, (size_t)(PT2 + 1) * d->C * sizeof(float), s>>>(
+      *d, row_ptr, csr, tasks, ctrl, d_out, d_feats);
   return fail_launch("fuse_pose_bwd");
 }
 

@@ -42,6 +42,21 @@ from vfdepth_amd.layers import seeded_state_dict  # noqa: E402
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
 
+def max_over_ranks(elapsed, world, device):
+    """The slowest rank's time (the job's time): all-reduce MAX over the process group."""
+    if world <= 1:
+        return elapsed
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t)
+
+
+def job_throughput(elapsed, steps, world, batch_per_rank=1):
+    """Whole-job iterations/s: every rank runs `steps` iterations of `batch_per_rank` samples
+    (weak scaling); divided by the slowest rank's time."""
+    return steps * world * batch_per_rank / elapsed
+
+
 def make_cfg(config, batch=None):
     if config == 2:
         cfg = C.surround_fusion_cfg(batch_size=batch or 1)
@@ -201,8 +216,6 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    if not use_graph:
-        _lib.prof_enable('all')
     t0 = time.perf_counter()
     for _ in range(args.steps):
         losses = step()
@@ -211,23 +224,19 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if use_graph:
-        # per-kernel device times: the same kernels launched eagerly (graph replays carry no host
-        # hooks); kernel durations do not depend on how the launch was issued
-        torch.cuda.synchronize()
-        _lib.prof_enable('all')
-        for _ in range(min(args.steps, 5)):
-            eager_step()
-        torch.cuda.synchronize()
-        prof = _lib.prof_read()
-        prof = {k: (n * args.steps // min(args.steps, 5), t * args.steps / min(args.steps, 5)) for k, (n, t) in prof.items()}
-    else:
-        prof = _lib.prof_read()
+    # per-kernel device times: HIP events around each hot-path launch on its stream, recorded in
+    # a few eager steps right after the timed region (the timed steps carry no profiling hooks;
+    # graph replays could not fire them); kernel durations do not depend on how they were issued
+    n_prof = min(args.steps, 5)
+    torch.cuda.synchronize()
+    _lib.prof_enable('all')
+    for _ in range(n_prof):
+        losses = eager_step()
+    torch.cuda.synchronize()
+    prof = _lib.prof_read()
     _lib.prof_enable('off')
-    if world > 1:
-        t = torch.tensor([elapsed], device=f'cuda:{local}')
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t)
+    prof = {k: (n * args.steps // n_prof, t * args.steps / n_prof) for k, (n, t) in prof.items()}
+    elapsed = max_over_ranks(elapsed, world, f'cuda:{local}')
     if rank != 0:
         dist.destroy_process_group()
         return
@@ -251,7 +260,7 @@ def main():
         base = cpu_baseline(cfg)
     out = {
         'metric': '6-cam 384x640 train iters/sec (DDAD-shaped, volumetric fusion)',
-        'value': world * args.steps / elapsed,
+        'value': job_throughput(elapsed, args.steps, world),
         'unit': 'iters/s',
         'n_gpus': world,
         'steps': args.steps,

@@ -66,9 +66,13 @@ class VFDepthAlgo:
         if self.ddp_enable:
             from torch.nn.parallel import DistributedDataParallel as DDP
             group = dist.new_group(list(range(self.world_size)))
+            on_gpu = self.device.type == 'cuda'
             for k, v in models.items():
-                v = torch.nn.SyncBatchNorm.convert_sync_batchnorm(v, group)
-                models[k] = DDP(v, device_ids=[self.device.index], broadcast_buffers=True)
+                # torch's SyncBatchNorm only runs on GPU modules: the gloo/CPU rehearsal keeps
+                # per-rank BatchNorm, the GPU path converts exactly as the reference does
+                if on_gpu:
+                    v = torch.nn.SyncBatchNorm.convert_sync_batchnorm(v, group)
+                models[k] = DDP(v, device_ids=[self.device.index] if on_gpu else None, broadcast_buffers=True)
         return models
 
     def prepare_dataset(self, cfg, rank):
@@ -80,8 +84,10 @@ class VFDepthAlgo:
         opts = {'batch_size': self.batch_size, 'shuffle': not self.ddp_enable, 'num_workers': self.num_workers,
                 'pin_memory': True, 'drop_last': True}
         if self.ddp_enable:
+            # rank may be a device (CPU rehearsal): the sampler wants the process rank
+            prank = rank if isinstance(rank, int) else (dist.get_rank() if dist.is_initialized() else 0)
             self.train_sampler = torch.utils.data.distributed.DistributedSampler(
-                ds, num_replicas=self.world_size, rank=rank, shuffle=True)
+                ds, num_replicas=self.world_size, rank=prank, shuffle=True)
             opts['sampler'] = self.train_sampler
         self._dataloaders['train'] = DataLoader(ds, **opts)
         if rank == 0:

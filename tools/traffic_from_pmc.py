@@ -14,13 +14,14 @@ import sys
 
 OPS = {
     'mask_downsample': ['mask_downsample_k'],
-    'fusion_plan': ['fusion_plan_k', 'plan_index_k', 'plan_count_k', 'plan_scan_k', 'plan_fill_k'],
+    'fusion_plan': ['fusion_plan_k', 'plan_index_k', 'plan_count_k', 'plan_scan_k', 'plan_fill_k', 'plan_task_k'],
     'fuse_depth_fwd': ['fuse_depth_fwd_k'],
     'fuse_depth_bwd': ['fuse_depth_bwd_k', 'fuse_depth_reduce_k'],
     'fuse_pose_fwd': ['fuse_pose_fwd_k'],
     'fuse_pose_bwd': ['fuse_pose_bwd_k'],
     'voxel_project_fwd': ['voxel_project_fwd_k'],
-    'voxel_project_bwd': ['voxel_project_bwd_k'],
+    'voxel_project_bwd': ['vpb_count_k', 'vpb_scan1_k', 'vpb_scan2_k', 'vpb_fill_k', 'vpb_fold_k', 'vpb_tile_k',
+                          'vpb_tasks_k', 'vpb_main_k'],
     'view_stats': ['view_stats_k', 'view_finalize_k'],
     'view_apply': ['view_apply_k'],
     'view_bwd': ['view_bwd_k', 'view_bwd_reduce_k'],

@@ -219,6 +219,138 @@ __global__ __launch_bounds__(256) void fuse_depth_fwd_k(vfd_voxel_desc d, const 
   }
 }
 
+// Latency-tolerant variant for Cv in {16, 32, 64}: phase 1 (lane = voxel) writes each voxel's
+// taps to LDS; phase 2 runs lanes = (voxel, channel quad), 64 / (Cv/4) voxels per instruction,
+// branch-free: every voxel issues its 8 float4 corner reads (out-of-range corners and the missing
+// second tap read a valid row with weight 0, which adds +0: the same per-channel operation
+// sequence as fuse_depth_fwd_k), so two groups of voxels have all their loads in flight.
+struct VoxRec {
+  int cnt, cam[2], base[2];
+  float w[2][4], z[2];
+};
+
+template <int CV>
+__global__ __launch_bounds__(256) void fuse_depth_fwd_q_k(vfd_voxel_desc d, const float* __restrict__ P,
+                                                          const float* __restrict__ mlo,
+                                                          const float* __restrict__ K,
+                                                          const float* __restrict__ Einv,
+                                                          const float* __restrict__ wz,
+                                                          const float* __restrict__ b_no,
+                                                          const float* __restrict__ b_o,
+                                                          float* __restrict__ vox) {
+  constexpr int QPV = CV / 4, VPI = 64 / QPV;      // quads per voxel, voxels per instruction
+  __shared__ VoxRec rec_l[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int V = d.X * d.Y * d.Z;
+  const int b = blockIdx.y;
+  const int v0 = (blockIdx.x * 4 + wv) * 64;
+  if (v0 >= V) return;                               // whole wave; the block has no barrier
+  const int hw = d.h * d.w;
+  {
+    const int v = v0 + lane;
+    VoxRec r;
+    r.cnt = 0;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      r.cam[s] = 0;
+      r.base[s] = 0;
+      r.z[s] = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) r.w[s][q] = 0.f;
+    }
+    if (v < V) {
+      const float x = d.axis_x[v % d.X], y = d.axis_y[(v / d.X) % d.Y], z = d.axis_z[v / (d.X * d.Y)];
+      for (int c = 0; c < d.N; ++c) {
+        const int bc = b * d.N + c;
+        VoxCam g = voxel_to_camera(K + bc * 16, Einv + bc * 16, x, y, z, mlo + (size_t)bc * hw, d.h, d.w);
+        if (g.valid) {
+          // (explicit slots: a runtime slot index would put the record in scratch)
+          if (r.cnt == 0) {
+            const Tap tp = make_tap(c, g, d.h, d.w);
+            r.cam[0] = r.cam[1] = c;          // slot 1 defaults to a valid row (weight 0)
+            r.base[0] = r.base[1] = tp.base;
+            r.z[0] = tp.z;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) r.w[0][q] = tp.w[q];
+          } else if (r.cnt == 1) {
+            const Tap tp = make_tap(c, g, d.h, d.w);
+            r.cam[1] = c;
+            r.base[1] = tp.base;
+            r.z[1] = tp.z;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) r.w[1][q] = tp.w[q];
+          }
+          ++r.cnt;
+        }
+      }
+    }
+    rec_l[wv][lane] = r;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_s_waitcnt(0xc07f);                // lgkmcnt(0): the wave's LDS records are visible
+  const int g = lane / QPV, q4 = lane % QPV;
+  const int ch0 = q4 * 4;
+  const float4 bno = *reinterpret_cast<const float4*>(b_no + ch0);
+  const float4 bo = *reinterpret_cast<const float4*>(b_o + ch0);
+  const float4 wz0 = *reinterpret_cast<const float4*>(wz + ch0);
+  const float4 wz1 = *reinterpret_cast<const float4*>(wz + CV + ch0);
+  const float4 wz2 = *reinterpret_cast<const float4*>(wz + 2 * CV + ch0);
+  const int twoCv = 2 * CV;
+  const int nvox = min(64, V - v0);
+  for (int j0 = 0; j0 < nvox; j0 += VPI) {
+    const int j = j0 + g;
+    const VoxRec& r = rec_l[wv][min(j, 63)];
+    const int cnt = j < nvox ? r.cnt : 0;
+    const bool live = cnt == 1 || cnt == 2;
+    const int off = cnt == 2 ? CV : 0;
+    float4 v[2][4];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int cam = r.cam[s];
+      const float* Pc = P + (size_t)(b * d.N + cam) * hw * twoCv + off + ch0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int pix = min(max(r.base[s] + tap_offset(q, d.w), 0), hw - 1);
+        v[s][q] = *reinterpret_cast<const float4*>(Pc + (size_t)pix * twoCv);
+      }
+    }
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bool tap = s < cnt && live;
+      float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float wq = tap ? r.w[s][q] : 0.f;
+        val.x += v[s][q].x * wq;
+        val.y += v[s][q].y * wq;
+        val.z += v[s][q].z * wq;
+        val.w += v[s][q].w * wq;
+      }
+      const int zrow = (cnt == 1) ? 0 : 1 + d.group[r.cam[s]];
+      const float4 wzr = zrow == 0 ? wz0 : (zrow == 1 ? wz1 : wz2);
+      const float zf = tap ? r.z[s] / d.z_scale : 0.f;
+      if (tap) {
+        acc.x += val.x + wzr.x * zf;
+        acc.y += val.y + wzr.y * zf;
+        acc.z += val.z + wzr.z * zf;
+        acc.w += val.w + wzr.w * zf;
+      }
+    }
+    const float4 bb = cnt == 1 ? bno : bo;
+    float4 o;
+    o.x = acc.x + bb.x;
+    o.y = acc.y + bb.y;
+    o.z = acc.z + bb.z;
+    o.w = acc.w + bb.w;
+    o.x = live ? (o.x > 0.f ? o.x : o.x * 0.1f) : 0.f;
+    o.y = live ? (o.y > 0.f ? o.y : o.y * 0.1f) : 0.f;
+    o.z = live ? (o.z > 0.f ? o.z : o.z * 0.1f) : 0.f;
+    o.w = live ? (o.w > 0.f ? o.w : o.w * 0.1f) : 0.f;
+    if (j < nvox) *reinterpret_cast<float4*>(vox + ((size_t)b * V + v0 + j) * CV + ch0) = o;
+  }
+}
+
 // ------------------------------------------------------------------------------ K1 backward
 // Same voxel walk; lanes are channels, so every scatter into dP is a 256-B contiguous row of
 // f32 atomics (the full-rate atomic shape on gfx950).  Depth-column and bias gradients are
@@ -1574,7 +1706,15 @@ int vfd_fuse_depth_fwd(const vfd_voxel_desc* d, const float* P, const float* mas
   const int V = d->X * d->Y * d->Z;
   dim3 grid(cdiv(cdiv(V, 64), 4), d->B);
   ProfScope ps(K_FUSE_DEPTH_FWD, s);
-  if (d->Cv <= 64)
+  const bool al = ((uintptr_t)P & 15) == 0 && ((uintptr_t)vox & 15) == 0 && ((uintptr_t)wz & 15) == 0 &&
+                  ((uintptr_t)b_no & 15) == 0 && ((uintptr_t)b_o & 15) == 0;
+  if (al && d->Cv == 64)
+    fuse_depth_fwd_q_k<64><<<grid, 256, 0, s>>>(*d, P, mask_lo, K, Einv, wz, b_no, b_o, vox);
+  else if (al && d->Cv == 32)
+    fuse_depth_fwd_q_k<32><<<grid, 256, 0, s>>>(*d, P, mask_lo, K, Einv, wz, b_no, b_o, vox);
+  else if (al && d->Cv == 16)
+    fuse_depth_fwd_q_k<16><<<grid, 256, 0, s>>>(*d, P, mask_lo, K, Einv, wz, b_no, b_o, vox);
+  else if (d->Cv <= 64)
     fuse_depth_fwd_k<1><<<grid, 256, 0, s>>>(*d, P, mask_lo, K, Einv, wz, b_no, b_o, vox);
   else
     fuse_depth_fwd_k<2><<<grid, 256, 0, s>>>(*d, P, mask_lo, K, Einv, wz, b_no, b_o, vox);

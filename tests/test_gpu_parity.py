@@ -560,19 +560,36 @@ def test_graph_replay_matches_eager():
     flips = sum(int((graphed.outputs[('cam', c)][('reproj_mask', 0)] != out_e[('cam', c)][('reproj_mask', 0)]).sum())
                 for c in range(cfg['data']['num_cams']))
     assert flips == 0, f'{flips} auto-mask flips between graph replay and eager'
-    for net in ('depth_net', 'pose_net'):
-        pg = dict(algos[0].models[net].named_parameters())
+    # the fusion kernels sum some terms in atomic order (K2 forward cnt>=2 voxels, the plan's
+    # bucket order), so two eager steps differ too: the replay must agree with eager to 1e-3 or
+    # to within 4x the eager-vs-eager spread, whichever is looser
+    g_e1 = {net: {n: p.grad.detach().clone() for n, p in algos[1].models[net].named_parameters()}
+            for net in ('depth_net', 'pose_net')}
+    algos[1].optimizer.zero_grad(set_to_none=True)
+    _, le2 = algos[1].process_batch(dict(batch), 0)
+    le2['total_loss'].backward()
+    torch.cuda.synchronize()
+
+    def rel_diff(ga, gb):
         diff = ref = 0.0
-        for name, p in algos[1].models[net].named_parameters():
-            diff += float((pg[name].grad.double() - p.grad.double()).pow(2).sum())
-            ref += float(p.grad.double().pow(2).sum())
+        for name, g in gb.items():
+            diff += float((ga[name].double() - g.double()).pow(2).sum())
+            ref += float(g.double().pow(2).sum())
+        return diff, ref
+
+    for net in ('depth_net', 'pose_net'):
+        pg = {n: p.grad for n, p in algos[0].models[net].named_parameters()}
+        diff, ref = rel_diff(pg, g_e1[net])
         if ref == 0.0:
             # static scene: the identity term wins every auto-mask decision, so no temporal warp
             # (the pose net's only path into the loss) contributes — both runs must agree on that
             assert diff == 0.0, f'{net}: eager gradient is zero but the replay\'s is not ({diff:.3g})'
             continue
         rel = (diff / ref) ** 0.5
-        assert rel < 1e-3, f'{net}: gradient rel diff {rel:.3g} ({flips} auto-mask flips)'
+        d2, r2 = rel_diff({n: p.grad for n, p in algos[1].models[net].named_parameters()}, g_e1[net])
+        spread = (d2 / r2) ** 0.5
+        assert rel < max(1e-3, 4.0 * spread), \
+            f'{net}: gradient rel diff {rel:.3g} (eager-vs-eager {spread:.3g}, {flips} auto-mask flips)'
     # a second replay draws fresh identity noise and keeps training
     l2 = graphed()
     assert torch.isfinite(l2['total_loss']).item()

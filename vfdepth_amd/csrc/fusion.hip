@@ -13,6 +13,7 @@
 // decisions bit-identical.  All arithmetic follows the reference's operation order with
 // -ffp-contract=off so that validity tests at the boundaries agree with the CPU reference.
 #include <algorithm>
+#include <type_traits>
 
 #include "vfd_common.h"
 
@@ -711,6 +712,12 @@ struct TileItem {
 };
 static_assert(sizeof(TileItem) == 32, "tile item must stay 32 B");
 
+// Inside a tile, items are bucketed by their 2x2 footprint position (lx, ly) in [-1, PT-1]^2
+// (PSUB = 25 sub-keys), so the backward sums runs of equal footprints in fixed registers and
+// touches the pixel-indexed accumulators once per run.
+constexpr int PSUB = (PT + 1) * (PT + 1);
+__host__ __device__ __forceinline__ int sub_key(int lx, int ly) { return (ly + 1) * (PT + 1) + lx + 1; }
+
 __device__ __forceinline__ int tiles_x(const vfd_voxel_desc& d) { return (d.w + PT - 1) / PT; }
 __device__ __forceinline__ int tiles_y(const vfd_voxel_desc& d) { return (d.h + PT - 1) / PT; }
 
@@ -737,12 +744,12 @@ __device__ __forceinline__ unsigned entry_tiles(const vfd_voxel_desc& d, const P
 // they touch a handful of tiles).
 __global__ __launch_bounds__(256) void plan_count_k(vfd_voxel_desc d, const PlanEntry* __restrict__ plan,
                                                     const int* __restrict__ counts, int* __restrict__ tile_cnt) {
-  extern __shared__ int hist[];          // [nt]
+  extern __shared__ int hist[];          // [nt * PSUB]
   const int bc = blockIdx.y;
-  const int V = d.X * d.Y * d.Z, ntx = tiles_x(d), nt = ntx * tiles_y(d);
+  const int V = d.X * d.Y * d.Z, ntx = tiles_x(d), nt = ntx * tiles_y(d), nk = nt * PSUB;
   const int n = counts[bc];
   if ((int)(blockIdx.x * blockDim.x) >= n) return;     // whole workgroup beyond the list
-  for (int i = threadIdx.x; i < nt; i += blockDim.x) hist[i] = 0;
+  for (int i = threadIdx.x; i < nk; i += blockDim.x) hist[i] = 0;
   __syncthreads();
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) {
@@ -751,17 +758,20 @@ __global__ __launch_bounds__(256) void plan_count_k(vfd_voxel_desc d, const Plan
     const unsigned m = entry_tiles(d, e, &tx0, &ty0);
 #pragma unroll
     for (int t = 0; t < 4; ++t)
-      if (m >> t & 1u) atomicAdd(hist + (ty0 + (t >> 1)) * ntx + tx0 + (t & 1), 1);
+      if (m >> t & 1u) {
+        const int tx = tx0 + (t & 1), ty = ty0 + (t >> 1);
+        atomicAdd(hist + (ty * ntx + tx) * PSUB + sub_key(e.x0 - tx * PT, e.y0 - ty * PT), 1);
+      }
   }
   __syncthreads();
-  for (int t = threadIdx.x; t < nt; t += blockDim.x)
-    if (hist[t]) atomicAdd(tile_cnt + (size_t)bc * nt + t, hist[t]);
+  for (int t = threadIdx.x; t < nk; t += blockDim.x)
+    if (hist[t]) atomicAdd(tile_cnt + (size_t)bc * nk + t, hist[t]);
 }
 
 __global__ __launch_bounds__(PIDX_THREADS) void plan_scan_k(vfd_voxel_desc d, int* __restrict__ tile_cnt,
                                                             int* __restrict__ tile_ptr) {
   __shared__ int part[PIDX_THREADS];
-  const int nt = tiles_x(d) * tiles_y(d);
+  const int nt = tiles_x(d) * tiles_y(d) * PSUB;     // (tile, sub-key) buckets
   const int bc = blockIdx.x, t = threadIdx.x;
   int* cnt = tile_cnt + (size_t)bc * nt;
   const int chunk = (nt + PIDX_THREADS - 1) / PIDX_THREADS;
@@ -790,14 +800,14 @@ __global__ __launch_bounds__(PIDX_THREADS) void plan_scan_k(vfd_voxel_desc d, in
 __global__ __launch_bounds__(256) void plan_fill_k(vfd_voxel_desc d, const PlanEntry* __restrict__ plan,
                                                    const int* __restrict__ counts, int* __restrict__ cursor,
                                                    TileItem* __restrict__ items) {
-  extern __shared__ int lds[];           // [nt] local counts -> slot bases | [nt] local cursors
+  extern __shared__ int lds[];           // [nk] local counts -> slot bases | [nk] local cursors
   const int bc = blockIdx.y;
-  const int V = d.X * d.Y * d.Z, ntx = tiles_x(d), nt = ntx * tiles_y(d);
+  const int V = d.X * d.Y * d.Z, ntx = tiles_x(d), nt = ntx * tiles_y(d), nk = nt * PSUB;
   const int n = counts[bc];
   if ((int)(blockIdx.x * blockDim.x) >= n) return;
   int* lbase = lds;
-  int* lcur = lds + nt;
-  for (int t = threadIdx.x; t < nt; t += blockDim.x) lbase[t] = lcur[t] = 0;
+  int* lcur = lds + nk;
+  for (int t = threadIdx.x; t < nk; t += blockDim.x) lbase[t] = lcur[t] = 0;
   __syncthreads();
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   const bool act = i < n;
@@ -809,11 +819,14 @@ __global__ __launch_bounds__(256) void plan_fill_k(vfd_voxel_desc d, const PlanE
     m = entry_tiles(d, e, &tx0, &ty0);
 #pragma unroll
     for (int t = 0; t < 4; ++t)
-      if (m >> t & 1u) atomicAdd(lbase + (ty0 + (t >> 1)) * ntx + tx0 + (t & 1), 1);
+      if (m >> t & 1u) {
+        const int tx = tx0 + (t & 1), ty = ty0 + (t >> 1);
+        atomicAdd(lbase + (ty * ntx + tx) * PSUB + sub_key(e.x0 - tx * PT, e.y0 - ty * PT), 1);
+      }
   }
   __syncthreads();
-  int* cur = cursor + (size_t)bc * nt;
-  for (int t = threadIdx.x; t < nt; t += blockDim.x)
+  int* cur = cursor + (size_t)bc * nk;
+  for (int t = threadIdx.x; t < nk; t += blockDim.x)
     if (lbase[t]) lbase[t] = atomicAdd(cur + t, lbase[t]);
   __syncthreads();
   if (!act) return;
@@ -842,7 +855,8 @@ __global__ __launch_bounds__(256) void plan_fill_k(vfd_voxel_desc d, const PlanE
       it.w[q] = mine ? w[q] : 0.f;
     }
     it.lxy = (ly + 1) * 8 + (lx + 1);
-    ib[lbase[tile] + atomicAdd(lcur + tile, 1)] = it;
+    const int key = tile * PSUB + sub_key(lx, ly);
+    ib[lbase[key] + atomicAdd(lcur + key, 1)] = it;
   }
 }
 
@@ -866,8 +880,8 @@ __global__ __launch_bounds__(1024) void plan_task_k(vfd_voxel_desc d, const int*
   const int c0 = min(M, t * chunk), c1 = min(M, c0 + chunk);
   auto heavy = [&](int i) {
     const int bc = i / nt, tile = i % nt;
-    const int* tp = tile_ptr + (size_t)bc * (nt + 1);
-    return tp[tile + 1] - tp[tile] > PBW_SPLIT;
+    const int* tp = tile_ptr + (size_t)bc * (nt * PSUB + 1);
+    return tp[(tile + 1) * PSUB] - tp[tile * PSUB] > PBW_SPLIT;
   };
   for (int pass = 0; pass < 2; ++pass) {           // pass 0: heavy tiles (ng tasks), 1: light
     int local = 0;
@@ -911,7 +925,9 @@ __global__ __launch_bounds__(256) void fuse_pose_bwd_k(vfd_voxel_desc d, const i
                                                        const TileItem* __restrict__ items,
                                                        const int2* __restrict__ tasks, int* __restrict__ ctrl,
                                                        const float* __restrict__ dout, float* __restrict__ dfeats) {
-  extern __shared__ float red[];         // [C][PT2 + 1]: one wave's tile, then the transposed sum
+  // one LDS copy of the tile per wave: [pixel][POSE_MAXC + 1] (odd pitch: conflict-free sweeps)
+  constexpr int LDP = POSE_MAXC + 1;
+  __shared__ float acc_l[4 * PT2 * LDP];
   __shared__ int task_l;
   const int hw = d.h * d.w;
   const int V = d.X * d.Y * d.Z;
@@ -923,10 +939,11 @@ __global__ __launch_bounds__(256) void fuse_pose_bwd_k(vfd_voxel_desc d, const i
   const int Yo = d.Y + P, Xo = d.X + P;
   const size_t pix_stride = (size_t)d.Z * C1;
   const int ntask = ctrl[0];
-  constexpr int LD = PT2 + 1;
+  float* wacc = acc_l + wv * PT2 * LDP;
   for (;;) {
     __syncthreads();
     if (threadIdx.x == 0) task_l = atomicAdd(ctrl + 1, 1);
+    for (int i = threadIdx.x; i < 4 * PT2 * LDP; i += 256) acc_l[i] = 0.f;
     __syncthreads();
     const int task = task_l;
     if (task >= ntask) break;
@@ -935,108 +952,112 @@ __global__ __launch_bounds__(256) void fuse_pose_bwd_k(vfd_voxel_desc d, const i
     const int g0 = tk.y & 0xFF;                      // channel groups [g0, g0 + ng) of 64
     const int ng = min(tk.y >> 8, (C + 63) / 64 - g0);
     if (ng <= 0) continue;                           // a split group beyond C (workgroup-uniform)
-    const int* tp = tile_ptr + (size_t)bc * (nt + 1);
+    const int* tp = tile_ptr + (size_t)bc * (nt * PSUB + 1);
     const TileItem* ib = items + (size_t)bc * 4 * V;
     const float* gb = dout + (size_t)b * Yo * Xo * pix_stride;
-    const int lo = __builtin_amdgcn_readfirstlane(tp[tile]), hi = __builtin_amdgcn_readfirstlane(tp[tile + 1]);
-    // register accumulators: one 16-pixel array per 64-channel group, indexed by the wave-uniform
-    // tap pixel (register-indexed moves, no scratch)
-    float a0[PT2], a1[PT2], a2[PT2], a3[PT2];
-#pragma unroll
-    for (int i = 0; i < PT2; ++i) a0[i] = a1[i] = a2[i] = a3[i] = 0.f;
+    const int lo = __builtin_amdgcn_readfirstlane(tp[tile * PSUB]);
+    const int hi = __builtin_amdgcn_readfirstlane(tp[tile * PSUB + PSUB]);
     int cho[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) cho[k] = min(lane + 64 * (g0 + k), C - 1);
-    for (int j = lo + wv * PBW_U; j < hi; j += 4 * PBW_U) {
-      TileItem it[PBW_U];
-      float g[PBW_U][4];
+    // the item walk, specialised on the group count so every load is unconditional (a load
+    // under a branch makes the compiler's waitcnt at the join wait for everything in flight)
+    auto walk = [&](auto ngc) {
+      constexpr int NG = decltype(ngc)::value;
+      // the open footprint run: tap sums per (tap, group) in fixed registers; flushed into the
+      // pixel-indexed accumulators when the run ends (out-of-tile taps have weight 0: skipped)
+      float tq[4][NG];
 #pragma unroll
-      for (int u = 0; u < PBW_U; ++u) {
-        it[u] = ib[min(j + u, hi - 1)];                     // tail slots re-read the last item (skipped below)
-        const float* row = gb + (size_t)(it[u].pz & 0xFFFFF) * pix_stride + ((it[u].pz >> 20) & 0xFF) * C1;
+      for (int q = 0; q < 4; ++q)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) g[u][k] = k < ng ? row[cho[k]] : 0.f;
-      }
+        for (int k = 0; k < NG; ++k) tq[q][k] = 0.f;
+      int cur = -1;
+      auto flush = [&]() {
+        if (cur < 0) return;
+        const int lx = (cur & 7) - 1, ly = (cur >> 3) - 1;
 #pragma unroll
-      for (int u = 0; u < PBW_U; ++u) {
-        if (j + u >= hi) continue;
-        if (it[u].pz >> 28) {                               // reflect-padding copies (grid border)
-          const int pos = it[u].pz & 0xFFFFF, zo = ((it[u].pz >> 20) & 0xFF) * C1;
-          const int xi = pos % Xo - P / 2, yi = pos / Xo - P / 2;
-          int rows[3], cols[3], nr, nc;
-          pad_sets(yi, d.Y, d.pad_out, rows, &nr);
-          pad_sets(xi, d.X, d.pad_out, cols, &nc);
-          for (int a = 0; a < nr; ++a)
-            for (int c2 = 0; c2 < nc; ++c2) {
-              if (a == 0 && c2 == 0) continue;
-              const float* row = gb + ((size_t)rows[a] * Xo + cols[c2]) * pix_stride + zo;
+        for (int q = 0; q < 4; ++q) {
+          const int px = lx + (q & 1), py = ly + (q >> 1);
+          if (px >= 0 && px < PT && py >= 0 && py < PT) {
+            float* r = wacc + (py * PT + px) * LDP + lane;
 #pragma unroll
-              for (int k = 0; k < 4; ++k)
-                if (k < ng) g[u][k] += row[cho[k]];
-            }
-        }
-        const int lx = (it[u].lxy & 7) - 1, ly = (it[u].lxy >> 3) - 1;
-        // d(mean) = g / den (as g * (1/den)), then grid_sample's backward adds d(mean) * w
-        float gd[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) gd[k] = g[u][k] * it[u].rden;
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (it[u].w[q] != 0.f) {
-            const int pl = __builtin_amdgcn_readfirstlane((ly + (q >> 1)) * PT + lx + (q & 1));
-            const float w = it[u].w[q];
-            a0[pl] += gd[0] * w;
-            if (ng > 1) {
-              a1[pl] += gd[1] * w;
-              a2[pl] += gd[2] * w;
-              a3[pl] += gd[3] * w;
-            }
+            for (int k = 0; k < NG; ++k) r[64 * k] += tq[q][k];
           }
-      }
-    }
-    // sum the four waves' tiles in a fixed order ((w0 + w1) + w2) + w3 through one [C][PT2+1]
-    // LDS tile (rows = the task's channels), then write the tile NCHW with lanes along pixels
-    const int cbase = 64 * g0, cn = min(C - cbase, 64 * ng);
-    for (int src = 1; src < 4; ++src) {
-      if (wv == src) {
 #pragma unroll
-        for (int i = 0; i < PT2; ++i) {
-          if (lane < cn) red[lane * LD + i] = a0[i];
-          if (lane + 64 < cn) red[(lane + 64) * LD + i] = a1[i];
-          if (lane + 128 < cn) red[(lane + 128) * LD + i] = a2[i];
-          if (lane + 192 < cn) red[(lane + 192) * LD + i] = a3[i];
+          for (int k = 0; k < NG; ++k) tq[q][k] = 0.f;
         }
-      }
-      __syncthreads();
-      if (wv == 0) {
+      };
+      for (int j = lo + wv * PBW_U; j < hi; j += 4 * PBW_U) {
+        // lane-parallel item fetch (lane u < PBW_U holds item j + u), broadcast by readlane: the
+        // batch's items cost one vector load each instead of a block of SGPRs
+        const TileItem mine = ib[min(j + (lane & (PBW_U - 1)), hi - 1)];  // tail slots re-read the last item
+        TileItem it[PBW_U];
 #pragma unroll
-        for (int i = 0; i < PT2; ++i) {
-          a0[i] += red[min(lane, cn - 1) * LD + i];
-          if (ng > 1) {
-            a1[i] += red[min(lane + 64, cn - 1) * LD + i];
-            a2[i] += red[min(lane + 128, cn - 1) * LD + i];
-            a3[i] += red[min(lane + 192, cn - 1) * LD + i];
+        for (int u = 0; u < PBW_U; ++u) {
+          it[u].pz = (uint32_t)__builtin_amdgcn_readlane((int)mine.pz, u);
+          it[u].rden = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine.rden), u));
+#pragma unroll
+          for (int q = 0; q < 4; ++q) it[u].w[q] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine.w[q]), u));
+          it[u].lxy = __builtin_amdgcn_readlane(mine.lxy, u);
+        }
+        float g[PBW_U][NG];
+#pragma unroll
+        for (int u = 0; u < PBW_U; ++u) {
+          const float* row = gb + (size_t)(it[u].pz & 0xFFFFF) * pix_stride + ((it[u].pz >> 20) & 0xFF) * C1;
+#pragma unroll
+          for (int k = 0; k < NG; ++k) g[u][k] = row[cho[k]];
+        }
+#pragma unroll
+        for (int u = 0; u < PBW_U; ++u) {
+          if (j + u >= hi) continue;
+          if (it[u].pz >> 28) {                               // reflect-padding copies (grid border)
+            // pad_sets with constant indices (a runtime-indexed set would live in scratch)
+            const int pos = it[u].pz & 0xFFFFF, zo = ((it[u].pz >> 20) & 0xFF) * C1;
+            const int xi = pos % Xo - P / 2, yi = pos / Xo - P / 2;
+            const int ry[3] = {yi + 1, 0, d.Y + 1}, cx[3] = {xi + 1, 0, d.X + 1};
+            const bool vy[3] = {true, yi == 1, yi == d.Y - 2}, vx[3] = {true, xi == 1, xi == d.X - 2};
+#pragma unroll
+            for (int a = 0; a < 3; ++a)
+#pragma unroll
+              for (int c2 = 0; c2 < 3; ++c2) {
+                if ((a == 0 && c2 == 0) || !vy[a] || !vx[c2]) continue;
+                const float* row = gb + ((size_t)ry[a] * Xo + cx[c2]) * pix_stride + zo;
+#pragma unroll
+                for (int k = 0; k < NG; ++k) g[u][k] += row[cho[k]];
+              }
+          }
+          if (it[u].lxy != cur) {
+            flush();
+            cur = it[u].lxy;
+          }
+          // d(mean) = g / den (as g * (1/den)), then grid_sample's backward adds d(mean) * w
+#pragma unroll
+          for (int k = 0; k < NG; ++k) {
+            const float gd = g[u][k] * it[u].rden;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) tq[q][k] = __builtin_fmaf(gd, it[u].w[q], tq[q][k]);
           }
         }
       }
-      __syncthreads();
-    }
-    if (wv == 0) {
-#pragma unroll
-      for (int i = 0; i < PT2; ++i) {
-        if (lane < cn) red[lane * LD + i] = a0[i];
-        if (lane + 64 < cn) red[(lane + 64) * LD + i] = a1[i];
-        if (lane + 128 < cn) red[(lane + 128) * LD + i] = a2[i];
-        if (lane + 192 < cn) red[(lane + 192) * LD + i] = a3[i];
-      }
+      flush();
+    };
+    switch (ng) {
+      case 1: walk(std::integral_constant<int, 1>{}); break;
+      case 2: walk(std::integral_constant<int, 2>{}); break;
+      case 3: walk(std::integral_constant<int, 3>{}); break;
+      default: walk(std::integral_constant<int, 4>{}); break;
     }
     __syncthreads();
+    // ((w0 + w1) + w2) + w3, written NCHW with threads along the tile's pixels
+    const int cbase = 64 * g0, cn = min(C - cbase, 64 * ng);
     const int tx = tile % ntx, ty = tile / ntx;
     float* db = dfeats + ((size_t)bc * C + cbase) * hw;
     for (int i = threadIdx.x; i < cn * PT2; i += blockDim.x) {
       const int ch = i / PT2, pl = i % PT2;
       const int x = tx * PT + pl % PT, y = ty * PT + pl / PT;
-      if (x < d.w && y < d.h) db[(size_t)ch * hw + y * d.w + x] = red[ch * LD + pl];
+      const int o = pl * LDP + ch;
+      const float v = ((acc_l[o] + acc_l[PT2 * LDP + o]) + acc_l[2 * PT2 * LDP + o]) + acc_l[3 * PT2 * LDP + o];
+      if (x < d.w && y < d.h) db[(size_t)ch * hw + y * d.w + x] = v;
     }
   }
 }
@@ -1759,10 +1780,10 @@ static size_t plan_entries_bytes(const vfd_voxel_desc* d) {
 }
 static int host_tiles(const vfd_voxel_desc* d) { return cdiv(d->w, PT) * cdiv(d->h, PT); }
 static size_t plan_rowptr_bytes(const vfd_voxel_desc* d) {
-  return ((size_t)d->B * d->N * (host_tiles(d) + 1) * sizeof(int) + 255) / 256 * 256;
+  return ((size_t)d->B * d->N * (host_tiles(d) * PSUB + 1) * sizeof(int) + 255) / 256 * 256;
 }
 static size_t plan_cursor_bytes(const vfd_voxel_desc* d) {
-  return ((size_t)d->B * d->N * host_tiles(d) * sizeof(int) + 255) / 256 * 256;
+  return ((size_t)d->B * d->N * host_tiles(d) * PSUB * sizeof(int) + 255) / 256 * 256;
 }
 
 static size_t plan_items_bytes(const vfd_voxel_desc* d) {
@@ -1783,7 +1804,7 @@ int vfd_fusion_plan(const vfd_voxel_desc* d, const float* mask_lo, const float* 
   if (st) return st;
   VFD_REQUIRE((size_t)d->X * d->Y * d->Z < (1u << 24), "voxel grid too large for the plan (%d x %d x %d)", d->X, d->Y, d->Z);
   VFD_REQUIRE((size_t)(d->X + 2) * (d->Y + 2) < (1u << 20) && d->Z < 256, "voxel grid too large for the pose index");
-  VFD_REQUIRE(2 * (size_t)host_tiles(d) * sizeof(int) <= 64 * 1024, "feature map %dx%d too large for the tile index", d->h, d->w);
+  VFD_REQUIRE(2 * (size_t)host_tiles(d) * PSUB * sizeof(int) <= 160 * 1024, "feature map %dx%d too large for the tile index", d->h, d->w);
   hipStream_t s = (hipStream_t)stream;
   const int V = d->X * d->Y * d->Z;
   (void)hipMemsetAsync(counts, 0, (size_t)d->B * d->N * sizeof(int), s);
@@ -1797,9 +1818,13 @@ int vfd_fusion_plan(const vfd_voxel_desc* d, const float* mask_lo, const float* 
   int* row_ptr = (int*)((char*)plan + plan_entries_bytes(d));
   int* cursor = (int*)((char*)row_ptr + plan_rowptr_bytes(d));
   TileItem* csr = (TileItem*)((char*)cursor + plan_cursor_bytes(d));
-  (void)hipMemsetAsync(cursor, 0, (size_t)d->B * d->N * host_tiles(d) * sizeof(int), s);
+  (void)hipMemsetAsync(cursor, 0, (size_t)d->B * d->N * host_tiles(d) * PSUB * sizeof(int), s);
   const dim3 egrid(cdiv(V, 256), d->B * d->N);
-  const size_t hist = (size_t)host_tiles(d) * sizeof(int);
+  const size_t hist = (size_t)host_tiles(d) * PSUB * sizeof(int);
+  if (2 * hist > 64 * 1024) {
+    (void)hipFuncSetAttribute((const void*)plan_count_k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hist);
+    (void)hipFuncSetAttribute((const void*)plan_fill_k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(2 * hist));
+  }
   plan_count_k<<<egrid, 256, hist, s>>>(*d, (const PlanEntry*)plan, counts, cursor);
   plan_scan_k<<<d->B * d->N, PIDX_THREADS, 0, s>>>(*d, cursor, row_ptr);
   plan_fill_k<<<egrid, 256, 2 * hist, s>>>(*d, (const PlanEntry*)plan, counts, cursor, csr);
@@ -1842,8 +1867,7 @@ int vfd_fuse_pose_bwd(const vfd_voxel_desc* d, const void* plan, const int* coun
   ProfScope ps(K_FUSE_POSE_BWD, s);
   (void)hipMemsetAsync(ctrl + 1, 0, sizeof(int), s);
   const int ntask = host_tiles(d) * d->B * d->N * (POSE_MAXC / 64);
-  fuse_pose_bwd_k<<<dim3(std::min(ntask, 1024)), 256, (size_t)(PT2 + 1) * d->C * sizeof(float), s>>>(
-      *d, row_ptr, csr, tasks, ctrl, d_out, d_feats);
+  fuse_pose_bwd_k<<<dim3(std::min(ntask, 512)), 256, 0, s>>>(*d, row_ptr, csr, tasks, ctrl, d_out, d_feats);
   return fail_launch("fuse_pose_bwd");
 }
 

@@ -1235,7 +1235,11 @@ __global__ __launch_bounds__(256) void voxel_project_fwd_k(vfd_voxel_desc d, con
 //                             the cell's 4 corners of its own layer into LDS with plain
 //                             read-add-write (no other wave writes that layer); the brick is
 //                             then written with plain stores.
-constexpr int VB_X = 8, VB_Y = 8;                  // voxel tile (one z layer) per wave task
+#ifndef VFD_VPB_PQ
+#define VFD_VPB_PQ 8
+#endif
+constexpr int VB_X = 8, VB_Y = 4;                  // voxel tile (one z layer) per wave task
+constexpr int VB_RY = VB_Y + 1, VB_NSEG = 2 * VB_RY;   // cell rows per layer, entry ranges per tile
 constexpr int VB_S = 1024;                         // samples per task part
 constexpr int VB_SCAN = 4096;                      // cells per block of the first scan level
 
@@ -1479,9 +1483,9 @@ __global__ __launch_bounds__(64) void vpb_tile_k(vfd_voxel_desc d, const int* __
   const int b = tile / g.ntile, tl = tile % g.ntile;
   const int xb = (tl % g.nbx) * VB_X, yb = ((tl / g.nbx) % g.nby) * VB_Y, zl = tl / (g.nbx * g.nby);
   int n = 0;
-  if (lane < 18) {
+  if (lane < VB_NSEG) {
     int s0, s1;
-    vpb_segment(d, g, ptr, boff, b, zl - 1 + lane / 9, yb - 1 + lane % 9, xb, &s0, &s1);
+    vpb_segment(d, g, ptr, boff, b, zl - 1 + lane / VB_RY, yb - 1 + lane % VB_RY, xb, &s0, &s1);
     n = s1 - s0;
   }
   n = wave_sum(n);
@@ -1556,7 +1560,7 @@ __global__ __launch_bounds__(64) void vpb_main_k(vfd_voxel_desc d, const int* __
     {
       // the wave's 18 entry ranges (lanes 0..17) and their running offsets
       int s0 = 0, s1 = 0;
-      if (lane < 18) vpb_segment(d, g, ptr, boff, b, zl - 1 + lane / 9, yb - 1 + lane % 9, xb, &s0, &s1);
+      if (lane < VB_NSEG) vpb_segment(d, g, ptr, boff, b, zl - 1 + lane / VB_RY, yb - 1 + lane % VB_RY, xb, &s0, &s1);
       const int len = s1 - s0;
       int inc = len;
 #pragma unroll
@@ -1564,7 +1568,7 @@ __global__ __launch_bounds__(64) void vpb_main_k(vfd_voxel_desc d, const int* __
         const int tt = __shfl_up(inc, off, 64);
         if (lane >= off) inc += tt;
       }
-      const int total = __builtin_amdgcn_readlane(inc, 17);
+      const int total = __builtin_amdgcn_readlane(inc, VB_NSEG - 1);
       const int lo = (int)((long long)total * part / np), hi = (int)((long long)total * (part + 1) / np);
       // entry of list position gi (clamped into [lo, hi): the load is unconditional, so it stays
       // in flight behind the row loads instead of forcing a wait inside a divergent branch)
@@ -1572,7 +1576,7 @@ __global__ __launch_bounds__(64) void vpb_main_k(vfd_voxel_desc d, const int* __
         gi = min(gi, hi - 1);
         int seg = 0;
 #pragma unroll
-        for (int k = 0; k < 17; ++k) seg += gi >= __builtin_amdgcn_readlane(inc, k) ? 1 : 0;
+        for (int k = 0; k < VB_NSEG - 1; ++k) seg += gi >= __builtin_amdgcn_readlane(inc, k) ? 1 : 0;
         const int ss = __shfl(s0, seg, 64), ex = __shfl(inc - len, seg, 64);
         return entries[ss + gi - ex];
       };
@@ -1623,18 +1627,19 @@ __global__ __launch_bounds__(64) void vpb_main_k(vfd_voxel_desc d, const int* __
         q.row = valid ? __float_as_uint(e.w) : 0x80000000u;     // past the end: the zero row
         return q;
       };
-      auto load_half = [&](const Prm& q, int h, float* gr) {
+      constexpr int PQ = VFD_VPB_PQ;    // samples per pipeline stage (64 / PQ stages per batch)
+      auto load_part = [&](const Prm& q, int h, float* gr) {
 #pragma unroll
-        for (int j = 0; j < 32; ++j) {
-          const unsigned rj = (unsigned)__builtin_amdgcn_readlane((int)q.row, h * 32 + j);
+        for (int j = 0; j < PQ; ++j) {
+          const unsigned rj = (unsigned)__builtin_amdgcn_readlane((int)q.row, h * PQ + j);
           const float* src = (rj >> 31) ? fbz : dout;      // wave-uniform: scalar select
           gr[j] = src[(size_t)(rj & 0x7FFFFFFFu) * CV + cl];
         }
       };
-      auto process_half = [&](const Prm& q, int h, const float* gr) {
+      auto process_part = [&](const Prm& q, int h, const float* gr) {
 #pragma unroll
-        for (int j = 0; j < 32; ++j) {
-          const int jj = h * 32 + j;
+        for (int j = 0; j < PQ; ++j) {
+          const int jj = h * PQ + j;
           const float gj = gr[j];
           const int kj = __builtin_amdgcn_readlane(q.key, jj);
           if (kj != cur) {
@@ -1649,20 +1654,27 @@ __global__ __launch_bounds__(64) void vpb_main_k(vfd_voxel_desc d, const int* __
         }
       };
       if (lo < hi) {
+        constexpr int NST = 64 / PQ;
         float4 en = entry_of(lo + lane);
         Prm P = setup(en, lo);
         en = entry_of(lo + 64 + lane);
-        float grA[32], grB[32];
-        load_half(P, 0, grA);
+        float gr[2][PQ];
+        load_part(P, 0, gr[0]);
         // every load is unconditional (samples past the end read the zero row): a load under a
         // branch makes the compiler's vmcnt accounting at the join wait for everything
         for (int g0 = lo; g0 < hi; g0 += 64) {
-          load_half(P, 1, grB);
-          process_half(P, 0, grA);
-          const Prm Pn = setup(en, g0 + 64);
-          en = entry_of(g0 + 128 + lane);
-          load_half(Pn, 0, grA);
-          process_half(P, 1, grB);
+          Prm Pn = P;
+#pragma unroll
+          for (int st = 0; st < NST; ++st) {
+            if (st + 1 < NST) {
+              load_part(P, st + 1, gr[(st + 1) & 1]);
+            } else {
+              Pn = setup(en, g0 + 64);
+              en = entry_of(g0 + 128 + lane);
+              load_part(Pn, 0, gr[(st + 1) & 1]);
+            }
+            process_part(P, st, gr[st & 1]);
+          }
           P = Pn;
         }
       }
@@ -1892,7 +1904,7 @@ int vfd_voxel_project_fwd(const vfd_voxel_desc* d, const float* vox, const float
   return fail_launch("voxel_project_fwd");
 }
 
-constexpr int VPB_WORKERS = 2048;      // persistent waves (8 per CU: LDS 16.6 KB, <=256 VGPRs)
+constexpr int VPB_WORKERS = 5120;      // persistent waves (20 per CU: LDS 8.4 KB, <=96 VGPRs)
 
 struct VpbWs {
   size_t cnt, zero, ptr, bsum, boff, rank, entries, fold, parts, tasks, ctrl, total;

@@ -1245,7 +1245,7 @@ constexpr int VB_SCAN = 4096;                      // cells per block of the fir
 
 struct VpbGeom {
   int CX, CY, CZ, ncell;                           // extended cell grid per batch
-  int nbx, nby, ntile;                             // tiles per batch: nbx * nby * Z
+  int nbx, nby, ntile;                             // tiles per batch: nbx * nby * ceil(Z / 2) layer pairs
 };
 __host__ __device__ __forceinline__ VpbGeom vpb_geom(const vfd_voxel_desc& d) {
   VpbGeom g;
@@ -1255,7 +1255,7 @@ __host__ __device__ __forceinline__ VpbGeom vpb_geom(const vfd_voxel_desc& d) {
   g.ncell = g.CX * g.CY * g.CZ;
   g.nbx = (d.X + VB_X - 1) / VB_X;
   g.nby = (d.Y + VB_Y - 1) / VB_Y;
-  g.ntile = g.nbx * g.nby * d.Z;
+  g.ntile = g.nbx * g.nby * ((d.Z + 1) / 2);
   return g;
 }
 
@@ -1474,6 +1474,15 @@ __device__ __forceinline__ void vpb_segment(const vfd_voxel_desc& d, const VpbGe
 // per tile (8x8 voxels of one z layer): its samples = the 2 x 9 cell rows touching the layer
 // -> number of parts; split tiles are zeroed here (their parts add with atomics).
 // grid = B * ntile, block = one wave (lanes 0..17 = the cell rows)
+// Entry range k (< VB_NSEG) of the wave for layer zl = 2 zp + w of a layer-pair tile: the cell
+// layer both waves share (z0 = 2 zp) comes first, so the pair reads those rows at the same time
+// (one L1/L2 fetch), then the wave's own outer layer (2 zp - 1 or 2 zp + 1).
+__device__ __forceinline__ int vpb_seg_z0(int zp, int w, int k) {
+  return k < VB_RY ? 2 * zp : (w == 0 ? 2 * zp - 1 : 2 * zp + 1);
+}
+
+// per layer-pair tile: samples of each layer's wave -> number of parts; split tiles are zeroed
+// here (their parts add with atomics).  grid = B * ntile, block = one wave
 template <int CV>
 __global__ __launch_bounds__(64) void vpb_tile_k(vfd_voxel_desc d, const int* __restrict__ ptr,
                                                  const int* __restrict__ boff, int* __restrict__ parts,
@@ -1481,23 +1490,27 @@ __global__ __launch_bounds__(64) void vpb_tile_k(vfd_voxel_desc d, const int* __
   const VpbGeom g = vpb_geom(d);
   const int tile = blockIdx.x, lane = threadIdx.x;
   const int b = tile / g.ntile, tl = tile % g.ntile;
-  const int xb = (tl % g.nbx) * VB_X, yb = ((tl / g.nbx) % g.nby) * VB_Y, zl = tl / (g.nbx * g.nby);
-  int n = 0;
-  if (lane < VB_NSEG) {
-    int s0, s1;
-    vpb_segment(d, g, ptr, boff, b, zl - 1 + lane / VB_RY, yb - 1 + lane % VB_RY, xb, &s0, &s1);
-    n = s1 - s0;
+  const int xb = (tl % g.nbx) * VB_X, yb = ((tl / g.nbx) % g.nby) * VB_Y, zp = tl / (g.nbx * g.nby);
+  int n0 = 0, n1 = 0;
+  if (lane < 2 * VB_NSEG) {
+    const int w = lane / VB_NSEG, k = lane % VB_NSEG;
+    if (2 * zp + w < d.Z) {
+      int s0, s1;
+      vpb_segment(d, g, ptr, boff, b, vpb_seg_z0(zp, w, k), yb - 1 + k % VB_RY, xb, &s0, &s1);
+      (w == 0 ? n0 : n1) = s1 - s0;
+    }
   }
-  n = wave_sum(n);
-  const int np = max(1, (n + VB_S - 1) / VB_S);
+  n0 = wave_sum(n0);
+  n1 = wave_sum(n1);
+  const int np = max(1, (max(n0, n1) + VB_S - 1) / VB_S);
   if (lane == 0) parts[tile] = np;
   if (np == 1) return;
   const int V = d.X * d.Y * d.Z;
   constexpr int QPV = CV / 4;
-  for (int i = lane; i < VB_X * VB_Y * QPV; i += 64) {
-    const int q = i % QPV, v = i / QPV;
+  for (int i = lane; i < 2 * VB_X * VB_Y * QPV; i += 64) {
+    const int q = i % QPV, v = (i / QPV) % (VB_X * VB_Y), zl = 2 * zp + i / (QPV * VB_X * VB_Y);
     const int x = xb + v % VB_X, y = yb + v / VB_X;
-    if (x < d.X && y < d.Y)
+    if (x < d.X && y < d.Y && zl < d.Z)
       reinterpret_cast<float4*>(dvox + ((size_t)b * V + (zl * d.Y + y) * d.X + x) * CV)[q] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
@@ -1534,33 +1547,37 @@ __global__ __launch_bounds__(1024) void vpb_tasks_k(const int* __restrict__ part
 // One wave = one independent worker: it takes tile tasks from the counter, accumulates its tile
 // in a private 16 KB LDS slab and writes it out (plain stores, or atomics for split tiles).
 template <int CV>
-__global__ __launch_bounds__(64) void vpb_main_k(vfd_voxel_desc d, const int* __restrict__ ptr,
-                                                 const int* __restrict__ boff, const float4* __restrict__ entries,
-                                                 const int2* __restrict__ tasks, int* __restrict__ ctrl,
-                                                 const float* __restrict__ dout, const float* __restrict__ fbz,
-                                                 float* __restrict__ dvox) {
+__global__ __launch_bounds__(128) void vpb_main_k(vfd_voxel_desc d, const int* __restrict__ ptr,
+                                                  const int* __restrict__ boff, const float4* __restrict__ entries,
+                                                  const int2* __restrict__ tasks, int* __restrict__ ctrl,
+                                                  const float* __restrict__ dout, const float* __restrict__ fbz,
+                                                  float* __restrict__ dvox) {
   constexpr int LAYER = VB_Y * VB_X * 64;
-  __shared__ float lacc[LAYER + 64];               // + one scratch row (masked corners)
+  __shared__ float lacc_l[2][LAYER + 64];          // per wave: its layer + one scratch row (masked corners)
+  __shared__ int task_l;
   const VpbGeom g = vpb_geom(d);
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int cl = lane < CV ? lane : 0;
   const int V = d.X * d.Y * d.Z;
   const int ntask = ctrl[0];
+  float* lacc = lacc_l[wv];
   float* trash = lacc + LAYER;
   for (;;) {
-    int t = 0;
-    if (lane == 0) t = atomicAdd(ctrl + 1, 1);
-    t = __builtin_amdgcn_readfirstlane(t);
-    if (t >= ntask) break;
+    __syncthreads();
+    if (threadIdx.x == 0) task_l = atomicAdd(ctrl + 1, 1);
     for (int i = lane; i < LAYER / 4; i += 64) reinterpret_cast<float4*>(lacc)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    __syncthreads();
+    const int t = task_l;
+    if (t >= ntask) break;
     const int2 tk = tasks[t];
     const int tile = tk.x, part = tk.y & 0xFFFF, np = tk.y >> 16;
     const int b = tile / g.ntile, tl = tile % g.ntile;
-    const int xb = (tl % g.nbx) * VB_X, yb = ((tl / g.nbx) % g.nby) * VB_Y, zl = tl / (g.nbx * g.nby);
-    {
-      // the wave's 18 entry ranges (lanes 0..17) and their running offsets
+    const int xb = (tl % g.nbx) * VB_X, yb = ((tl / g.nbx) % g.nby) * VB_Y, zp = tl / (g.nbx * g.nby);
+    const int zl = 2 * zp + wv;                      // this wave's voxel layer
+    if (zl < d.Z) {
+      // the wave's entry ranges (lanes 0 .. VB_NSEG-1) and their running offsets
       int s0 = 0, s1 = 0;
-      if (lane < VB_NSEG) vpb_segment(d, g, ptr, boff, b, zl - 1 + lane / VB_RY, yb - 1 + lane % VB_RY, xb, &s0, &s1);
+      if (lane < VB_NSEG) vpb_segment(d, g, ptr, boff, b, vpb_seg_z0(zp, wv, lane), yb - 1 + lane % VB_RY, xb, &s0, &s1);
       const int len = s1 - s0;
       int inc = len;
 #pragma unroll
@@ -1681,7 +1698,7 @@ __global__ __launch_bounds__(64) void vpb_main_k(vfd_voxel_desc d, const int* __
       flush();
     }
     // ---- write the tile: lanes = (voxel, channel quad)
-    {
+    if (zl < d.Z) {
       constexpr int QPV = CV / 4, VPI = 64 / QPV;
       const int q = lane % QPV, vsub = lane / QPV;
       for (int v0 = 0; v0 < VB_X * VB_Y; v0 += VPI) {
@@ -1977,7 +1994,7 @@ int vfd_voxel_project_bwd(const vfd_voxel_desc* d, const float* d_out, const flo
     if (d->pad_out) vpb_fold_k<CVV><<<d->B * d->N * 2 * (d->w + d->h), 256, 0, s>>>(*d, d_out, fb); \
     vpb_tile_k<CVV><<<nb, 64, 0, s>>>(*d, ptr, boff, parts, d_vox);                                \
     vpb_tasks_k<<<1, 1024, 0, s>>>(parts, nb, tasks, ctrl);                                        \
-    vpb_main_k<CVV><<<VPB_WORKERS, 64, 0, s>>>(*d, ptr, boff, entries, tasks, ctrl, d_out, zrow, d_vox); \
+    vpb_main_k<CVV><<<VPB_WORKERS / 2, 128, 0, s>>>(*d, ptr, boff, entries, tasks, ctrl, d_out, zrow, d_vox); \
     break;
     VPB_LAUNCH(8)
     VPB_LAUNCH(16)

@@ -1293,13 +1293,13 @@ __device__ __forceinline__ int vpb_cell(const vfd_voxel_desc& d, const VpbGeom& 
 // wave's lanes are neighbouring pixels at one depth and often share a cell near the camera: the
 // lanes of a run of equal cells take their ranks with ONE counter atomic, issued by the run head).
 // The entry's sample id is s = (bc * hw + pixel) * D + depth (the order of the gradient rows).
-__global__ __launch_bounds__(256) void vpb_count_k(vfd_voxel_desc d, const float* __restrict__ invK,
-                                                   const float* __restrict__ E, int* __restrict__ cnt,
-                                                   int* __restrict__ rank) {
+__device__ __forceinline__ void vpb_count(const vfd_voxel_desc& d, const float* __restrict__ invK,
+                                          const float* __restrict__ E, int* __restrict__ cnt,
+                                          int* __restrict__ rank, int bc, int blk) {
   const VpbGeom g = vpb_geom(d);
-  const int bc = blockIdx.y, b = bc / d.N;
+  const int b = bc / d.N;
   const int hw = d.h * d.w, hwD = hw * d.D;
-  const int sl = blockIdx.x * blockDim.x + threadIdx.x;
+  const int sl = blk * blockDim.x + threadIdx.x;
   const int lane = threadIdx.x & 63;
   int c = -1;
   if (sl < hwD) {
@@ -1423,10 +1423,10 @@ __device__ __forceinline__ int vpb_fold_slot(const vfd_voxel_desc& d, int px, in
 }
 
 template <int CV>
-__global__ __launch_bounds__(256) void vpb_fold_k(vfd_voxel_desc d, const float* __restrict__ dout,
-                                                  float* __restrict__ fb) {
+__device__ __forceinline__ void vpb_fold(const vfd_voxel_desc& d, const float* __restrict__ dout,
+                                         float* __restrict__ fb, int fblk) {
   const int nsl = 2 * (d.w + d.h);
-  const int bc = blockIdx.x / nsl, slot = blockIdx.x % nsl;
+  const int bc = fblk / nsl, slot = fblk % nsl;
   int px, py;
   if (slot < d.w) { px = slot; py = 1; }
   else if (slot < 2 * d.w) { px = slot - d.w; py = d.h - 2; }
@@ -1455,6 +1455,18 @@ __global__ __launch_bounds__(256) void vpb_fold_k(vfd_voxel_desc d, const float*
     }
     dst[i] = s;
   }
+}
+
+// One launch for the two independent first steps: blocks [0, nc) count samples per cell (latency-
+// bound returning atomics), blocks [nc, nc + nf) fold the reflect copies of d_out (streaming);
+// they overlap on the chip instead of running back to back.
+template <int CV>
+__global__ __launch_bounds__(256) void vpb_count_fold_k(vfd_voxel_desc d, const float* __restrict__ invK,
+                                                        const float* __restrict__ E, int* __restrict__ cnt,
+                                                        int* __restrict__ rank, int cpb, int nc,
+                                                        const float* __restrict__ dout, float* __restrict__ fb) {
+  if ((int)blockIdx.x < nc) vpb_count(d, invK, E, cnt, rank, blockIdx.x / cpb, blockIdx.x % cpb);
+  else vpb_fold<CV>(d, dout, fb, blockIdx.x - nc);
 }
 
 // entry range of cell row (z0, y0) of brick column [xb - 1, xb + 7] (clipped to the grid)
@@ -1984,14 +1996,15 @@ int vfd_voxel_project_bwd(const vfd_voxel_desc* d, const float* d_out, const flo
   ProfScope ps(K_VPROJ_BWD, s);
   (void)hipMemsetAsync(cnt, 0, w.fold, s);   // counters + zero row
   dim3 sgrid(cdiv(hwD, 256), d->B * d->N);
-  vpb_count_k<<<sgrid, 256, 0, s>>>(*d, invK, E, cnt, rank);
-  vpb_scan1_k<<<nblk, 256, 0, s>>>(cnt, ncell, ptr, bsum);
-  vpb_scan2_k<<<1, 1024, 0, s>>>(bsum, nblk, boff);
-  vpb_fill_k<<<sgrid, 256, 0, s>>>(*d, invK, E, rank, ptr, boff, entries);
+  const int cpb = cdiv(hwD, 256), nc = cpb * d->B * d->N;
+  const int nf = d->pad_out ? d->B * d->N * 2 * (d->w + d->h) : 0;
   switch (d->Cv) {
 #define VPB_LAUNCH(CVV)                                                                            \
   case CVV:                                                                                        \
-    if (d->pad_out) vpb_fold_k<CVV><<<d->B * d->N * 2 * (d->w + d->h), 256, 0, s>>>(*d, d_out, fb); \
+    vpb_count_fold_k<CVV><<<nc + nf, 256, 0, s>>>(*d, invK, E, cnt, rank, cpb, nc, d_out, fb);     \
+    vpb_scan1_k<<<nblk, 256, 0, s>>>(cnt, ncell, ptr, bsum);                                       \
+    vpb_scan2_k<<<1, 1024, 0, s>>>(bsum, nblk, boff);                                              \
+    vpb_fill_k<<<sgrid, 256, 0, s>>>(*d, invK, E, rank, ptr, boff, entries);                       \
     vpb_tile_k<CVV><<<nb, 64, 0, s>>>(*d, ptr, boff, parts, d_vox);                                \
     vpb_tasks_k<<<1, 1024, 0, s>>>(parts, nb, tasks, ctrl);                                        \
     vpb_main_k<CVV><<<VPB_WORKERS / 2, 128, 0, s>>>(*d, ptr, boff, entries, tasks, ctrl, d_out, zrow, d_vox); \

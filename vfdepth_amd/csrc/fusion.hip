@@ -1797,16 +1797,14 @@ int vfd_fuse_depth_bwd(const vfd_voxel_desc* d, const float* d_vox, const float*
   VFD_REQUIRE(ws_bytes >= vfd_fuse_depth_bwd_workspace(d), "workspace too small");
   hipStream_t s = (hipStream_t)stream;
   const int V = d->X * d->Y * d->Z;
+  ProfScope ps(K_FUSE_DEPTH_BWD, s);         // the op: zero dP, scatter, partial reduction
   (void)hipMemsetAsync(dP, 0, (size_t)d->B * d->N * d->h * d->w * 2 * d->Cv * sizeof(float), s);
   dim3 grid(cdiv(cdiv(V, 64), 4), d->B);
   float* partial = (float*)ws;
-  {
-    ProfScope ps(K_FUSE_DEPTH_BWD, s);
-    if (d->Cv <= 64)
-      fuse_depth_bwd_k<1><<<grid, 256, 0, s>>>(*d, d_vox, vox, mask_lo, K, Einv, dP, partial);
-    else
-      fuse_depth_bwd_k<2><<<grid, 256, 0, s>>>(*d, d_vox, vox, mask_lo, K, Einv, dP, partial);
-  }
+  if (d->Cv <= 64)
+    fuse_depth_bwd_k<1><<<grid, 256, 0, s>>>(*d, d_vox, vox, mask_lo, K, Einv, dP, partial);
+  else
+    fuse_depth_bwd_k<2><<<grid, 256, 0, s>>>(*d, d_vox, vox, mask_lo, K, Einv, dP, partial);
   st = fail_launch("fuse_depth_bwd");
   if (st) return st;
   // pad waves beyond V wrote nothing: zero-initialise by reducing only real rows

@@ -508,11 +508,9 @@ int vfd_photo_fwd(const vfd_photo_desc* d, const float* target, const float* col
   dim3 g = photo_grid(d);
   const int n_img = 2 * d->T + d->F;
   const size_t lds = (size_t)(3 + 3 * n_img) * (TS + 2) * (TS + 2) * sizeof(float);
-  {
-    ProfScope ps(K_PHOTO_FWD, s);
-    photo_fwd_k<<<g, 256, lds, s>>>(*d, target, color, ovl, ref_mask, omask, noise, reproj, automask, spatio_mask,
-                                     sel, (double*)ws);
-  }
+  ProfScope ps(K_PHOTO_FWD, s);              // the op: maps + block partials + their reduction
+  photo_fwd_k<<<g, 256, lds, s>>>(*d, target, color, ovl, ref_mask, omask, noise, reproj, automask, spatio_mask,
+                                   sel, (double*)ws);
   if ((st = fail_launch("photo_fwd"))) return st;
   photo_finalize_k<<<d->cam_count, 256, 0, s>>>(*d, (const double*)ws, g.x * g.y, sums, losses);
   return fail_launch("photo_finalize");
@@ -542,10 +540,8 @@ int vfd_smooth_fwd(int B, int N, int H, int W, const float* disp, const float* c
   VFD_REQUIRE(ws_bytes >= vfd_smooth_workspace_bytes(B, N, H, W), "workspace too small");
   hipStream_t s = (hipStream_t)stream;
   const unsigned nblk = cdiv((size_t)H * W, SBLK * SPPT);
-  {
-    ProfScope ps(K_SMOOTH_FWD, s);
-    smooth_fwd_k<<<dim3(nblk, B * N), SBLK, 0, s>>>(B, N, H, W, disp, color, (double*)ws);
-  }
+  ProfScope ps(K_SMOOTH_FWD, s);             // the op: block partials + their reduction
+  smooth_fwd_k<<<dim3(nblk, B * N), SBLK, 0, s>>>(B, N, H, W, disp, color, (double*)ws);
   int st = fail_launch("smooth_fwd");
   if (st) return st;
   smooth_finalize_k<<<N, 256, 0, s>>>(B, N, H, W, (const double*)ws, nblk, sums, loss);

@@ -16,7 +16,10 @@
 
 namespace vfd {
 
-constexpr int VPPT = 4;          // pixels per thread in the reduction kernels
+#ifndef VFD_VPPT
+#define VFD_VPPT 1
+#endif
+constexpr int VPPT = VFD_VPPT;   // pixels per thread in the reduction kernels
 constexpr int VBLK = 256;
 
 struct WarpEntry {
@@ -138,7 +141,8 @@ __device__ __forceinline__ float wave_reduce_n(float (&v)[N]) {
 }
 
 // ------------------------------------------------------------------------------ stats
-// partial layout [B*N][nblk * 4 waves][n_warp*8 + 2] floats (per-wave sums, fp32 over 256 pixels):
+// partial layout [B*N][n_warp*8 + 2][nblk * 4 waves] floats (per-wave sums; column-major so each
+// reduction reads one contiguous column):
 //   per warp (8 slots): count(3 per masked pixel), sum w*m, sum r*m, sum w, sum w^2, 0, 0, 0;
 //   per camera: sum r, sum r^2.  No barriers: every wave writes its own row.
 __global__ __launch_bounds__(VBLK) void view_stats_k(vfd_view_desc d, const float* __restrict__ depth,
@@ -150,7 +154,9 @@ __global__ __launch_bounds__(VBLK) void view_stats_k(vfd_view_desc d, const floa
   const int nrow = gridDim.x * (VBLK / 64);
   const int stride = d.n_warp * 8 + 2;
   const int lane = threadIdx.x & 63;
-  float* out = partial + ((size_t)bn * nrow + blockIdx.x * (VBLK / 64) + (threadIdx.x >> 6)) * stride;
+  // column-major partials: column c of camera slot bn is partial[(bn * stride + c) * nrow + row]
+  const int row = blockIdx.x * (VBLK / 64) + (threadIdx.x >> 6);
+  float* out = partial + (size_t)bn * stride * nrow + row;
   const float* ref = d.color[0] + tg.br * 3 * HW;
   const float* rmask = mask + tg.br * HW;
   float X[VPPT][3], rv[VPPT][3], rm[VPPT];
@@ -176,7 +182,7 @@ __global__ __launch_bounds__(VBLK) void view_stats_k(vfd_view_desc d, const floa
         v[1] += rv[k][ch] * rv[k][ch];
       }
     const float s = wave_reduce_n<2>(v);
-    if (lane < 2) out[d.n_warp * 8 + lane] = s;
+    if (lane < 2) out[(size_t)(d.n_warp * 8 + lane) * nrow] = s;
   }
   for (int w = 0; w < d.n_warp; ++w) {
     const WarpEntry e = warp_entry(d, cam, w);
@@ -203,31 +209,35 @@ __global__ __launch_bounds__(VBLK) void view_stats_k(vfd_view_desc d, const floa
       }
     }
     const float s = wave_reduce_n<8>(acc);
-    if (lane < 8) out[w * 8 + lane] = s;
+    if (lane < 8) out[(size_t)(w * 8 + lane) * nrow] = s;
   }
 }
 
 // coef [B,N,n_warp,4] = (w_mean, w_std, s_mean, s_std); w_std = -1 marks a skipped warp
 // (any sample of the batch without overlap -> warp returned unnormalised, view_rendering.py:50-53)
-__global__ __launch_bounds__(256) void view_finalize_k(vfd_view_desc d, const float* __restrict__ partial, int nblk,
+__global__ __launch_bounds__(512) void view_finalize_k(vfd_view_desc d, const float* __restrict__ partial, int nblk,
                                                        float* __restrict__ coef) {
-  // one block per (target slot, warp): fp64 block reductions over the stats partials
-  __shared__ double lds[4];
+  // one block per (target slot, warp); wave j < 7 reduces column j (contiguous, fp64) in parallel
+  __shared__ double sl[8];
   const int cam = blockIdx.x / d.n_warp, w = blockIdx.x % d.n_warp;
   const int stride = d.n_warp * 8 + 2;
   const double n_all = 3.0 * d.H * d.W;
+  const int lane = threadIdx.x & 63, j = threadIdx.x >> 6;
   bool skip = false;
   for (int b = 0; b < d.B; ++b) {
     const size_t bn = (size_t)b * d.cam_count + cam;
-    double s[7];
-#pragma unroll
-    for (int j = 0; j < 7; ++j) {
+    if (j < 7) {
       const int col = j < 5 ? w * 8 + j : d.n_warp * 8 + (j - 5);
+      const float* pc = partial + (bn * stride + col) * nblk;
       double acc = 0.0;
-      for (int k = threadIdx.x; k < nblk; k += blockDim.x) acc += (double)partial[(bn * nblk + k) * stride + col];
-      s[j] = block_sum_all(acc, lds);
+      for (int k = lane; k < nblk; k += 64) acc += (double)pc[k];
+      acc = wave_sum(acc);
+      if (lane == 0) sl[j] = acc;
     }
+    __syncthreads();
     if (threadIdx.x == 0) {
+      double s[7];
+      for (int i = 0; i < 7; ++i) s[i] = sl[i];
       if (s[0] == 0.0) skip = true;
       const double mw = s[1] / (s[0] + 1e-8);
       const double ms = s[2] / (s[0] + 1e-8);
@@ -241,6 +251,7 @@ __global__ __launch_bounds__(256) void view_finalize_k(vfd_view_desc d, const fl
       c[2] = (float)ms;
       c[3] = sqrtf((float)vs + 1e-16f);
     }
+    __syncthreads();
   }
   if (threadIdx.x == 0 && (skip || !d.intensity_align)) {
     for (int b = 0; b < d.B; ++b) coef[(((size_t)b * d.cam_count + cam) * d.n_warp + w) * 4 + 1] = -1.f;
@@ -304,7 +315,8 @@ __global__ __launch_bounds__(VBLK) void view_apply_k(vfd_view_desc d, const floa
 }
 
 // ------------------------------------------------------------------------------ backward
-// partial layout [B*N][nblk * 4 waves][n_warp][16] floats (d (K T)[:3] per warp in slots 0..11).
+// partial layout [B*N][n_warp][16][nblk * 4 waves] floats (d (K T)[:3] per warp in slots 0..11,
+// column-major for contiguous reductions).
 __global__ __launch_bounds__(VBLK) void view_bwd_k(vfd_view_desc d, const float* __restrict__ depth,
                                                    const float* __restrict__ invK, const float* __restrict__ M,
                                                    const float* __restrict__ mask, const float* __restrict__ coef,
@@ -381,7 +393,7 @@ __global__ __launch_bounds__(VBLK) void view_bwd_k(vfd_view_desc d, const float*
       }
     }
     const float sm = wave_reduce_n<16>(dM);
-    if (lane < 12) partial[(((size_t)bn * nrow + row) * d.n_warp + w) * 16 + lane] = sm;
+    if (lane < 12) partial[(((size_t)bn * d.n_warp + w) * 16 + lane) * nrow + row] = sm;
   }
 #pragma unroll
   for (int k = 0; k < VPPT; ++k)
@@ -395,7 +407,7 @@ __global__ __launch_bounds__(256) void view_bwd_reduce_k(const float* __restrict
   const int i = blockIdx.x;
   const int j = i % 12, w = (i / 12) % n_warp, bn = i / (12 * n_warp);
   double s = 0.0;
-  for (int k = threadIdx.x; k < nblk; k += blockDim.x) s += (double)partial[(((size_t)bn * nblk + k) * n_warp + w) * 16 + j];
+  for (int k = threadIdx.x; k < nblk; k += blockDim.x) s += (double)partial[(((size_t)bn * n_warp + w) * 16 + j) * nblk + k];
   s = block_sum_all(s, lds);
   if (threadIdx.x == 0) dM[i] = (float)s;
 }
@@ -435,11 +447,11 @@ int vfd_view_fwd(const vfd_view_desc* d, const float* depth, const float* invK, 
   hipStream_t s = (hipStream_t)stream;
   const unsigned nblk = view_red_blocks(d);
   {
-    ProfScope ps(K_VIEW_STATS, s);
+    ProfScope ps(K_VIEW_STATS, s);          // the op: per-wave partials + their reduction
     view_stats_k<<<dim3(nblk, d->B * d->cam_count), VBLK, 0, s>>>(*d, depth, invK, M, mask, (float*)ws);
+    if ((st = fail_launch("view_stats"))) return st;
+    view_finalize_k<<<d->cam_count * d->n_warp, 512, 0, s>>>(*d, (const float*)ws, nblk * (VBLK / 64), coef);
   }
-  if ((st = fail_launch("view_stats"))) return st;
-  view_finalize_k<<<d->cam_count * d->n_warp, 256, 0, s>>>(*d, (const float*)ws, nblk * (VBLK / 64), coef);
   if ((st = fail_launch("view_finalize"))) return st;
   {
     ProfScope ps(K_VIEW_APPLY, s);
@@ -458,13 +470,13 @@ int vfd_view_bwd(const vfd_view_desc* d, const float* depth, const float* invK, 
   hipStream_t s = (hipStream_t)stream;
   const unsigned nblk = view_red_blocks(d);
   {
-    ProfScope ps(K_VIEW_BWD, s);
+    ProfScope ps(K_VIEW_BWD, s);            // the op: per-wave partials + their reduction
     view_bwd_k<<<dim3(nblk, d->B * d->cam_count), VBLK, 0, s>>>(*d, depth, invK, M, mask, coef, g_color, g_ovl, d_depth,
                                                         (float*)ws);
+    if ((st = fail_launch("view_bwd"))) return st;
+    const int n = d->B * d->cam_count * d->n_warp * 12;
+    view_bwd_reduce_k<<<n, 256, 0, s>>>((const float*)ws, nblk * (VBLK / 64), d->n_warp, d_M);
   }
-  if ((st = fail_launch("view_bwd"))) return st;
-  const int n = d->B * d->cam_count * d->n_warp * 12;
-  view_bwd_reduce_k<<<n, 256, 0, s>>>((const float*)ws, nblk * (VBLK / 64), d->n_warp, d_M);
   return fail_launch("view_bwd_reduce");
 }
 

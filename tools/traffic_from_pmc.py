@@ -18,7 +18,7 @@ OPS = {
     'fuse_depth_fwd': ['fuse_depth_fwd_k'],
     'fuse_depth_bwd': ['fuse_depth_bwd_k', 'fuse_depth_reduce_k'],
     'fuse_pose_fwd': ['fuse_pose_fwd_k'],
-    'fuse_pose_bwd': ['fuse_pose_bwd_k'],
+    'fuse_pose_bwd': ['pose_fold_k', 'fuse_pose_bwd_k', 'pose_combine_k'],
     'voxel_project_fwd': ['voxel_project_fwd_k'],
     'voxel_project_bwd': ['vpb_count_fold_k', 'vpb_scan1_k', 'vpb_scan2_k', 'vpb_fill_k', 'vpb_fold_k', 'vpb_tile_k',
                           'vpb_tasks_k', 'vpb_main_k'],

@@ -703,8 +703,18 @@ constexpr int PIDX_THREADS = 1024;
 constexpr int PT = 4;              // tile side (pixels)
 constexpr int PT2 = PT * PT;
 
+// Reflect-pad fold slot of a border voxel (xi in {1, X-2} or yi in {1, Y-2}; -1 otherwise):
+// slot = xi (yi == 1), X + xi (yi == Y-2), 2X + yi (xi == 1), 2X + Y + yi (xi == X-2).
+__host__ __device__ __forceinline__ int pose_fold_slot(int xi, int yi, int X, int Y) {
+  if (yi == 1) return xi;
+  if (yi == Y - 2) return X + xi;
+  if (xi == 1) return 2 * X + yi;
+  if (xi == X - 2) return 2 * X + Y + yi;
+  return -1;
+}
+
 struct TileItem {
-  uint32_t pz;       // padded XY position in d_out (bits 0-19) | z (20-27) | reflect copies exist (bit 28)
+  uint32_t pz;       // d_out row (padded position * Z + z), or bit 31 | fold-buffer row (slot * Z + z)
   float rden;        // 1 / (count + 1e-7) (volumetric_fusionnet.py:162)
   float w[4];        // ATen bilinear weights of taps (x0,y0) (x0+1,y0) (x0,y0+1) (x0+1,y0+1); 0 outside the tile
   int32_t lxy;       // tap 0 relative to the tile origin: (ly + 1) * 8 + (lx + 1), lx, ly in [-1, PT-1]
@@ -836,7 +846,8 @@ __global__ __launch_bounds__(256) void plan_fill_k(vfd_voxel_desc d, const PlanE
   const int P1 = d.pad_out ? 1 : 0;
   const bool fold = d.pad_out && (xi == 1 || xi == d.X - 2 || yi == 1 || yi == d.Y - 2);
   TileItem it;
-  it.pz = (uint32_t)((yi + P1) * (d.X + 2 * P1) + xi + P1) | ((uint32_t)zi << 20) | ((fold ? 1u : 0u) << 28);
+  it.pz = fold ? (1u << 31) | (uint32_t)(pose_fold_slot(xi, yi, d.X, d.Y) * d.Z + zi)
+               : (uint32_t)(((yi + P1) * (d.X + 2 * P1) + xi + P1) * d.Z + zi);
   it.rden = 1.f / e.den;
   it.pad = 0;
   float w[4];
@@ -860,35 +871,46 @@ __global__ __launch_bounds__(256) void plan_fill_k(vfd_voxel_desc d, const PlanE
   }
 }
 
-// Load balance of the backward: tiles at the horizon collect ~10x the mean item count.  Tiles
-// with more than PBW_SPLIT items are split into one workgroup per 64-channel group (disjoint
-// outputs: no combine step), and those tasks are queued first; the kernel pulls tasks from a
-// counter.  tasks[i] = {bc * nt + tile, group | 1 << 8} for a split tile (POSE_MAXC / 64 groups,
-// independent of C: the plan is built without it; groups beyond C are skipped), {bc * nt + tile,
-// 0 | 0xFF << 8} for a whole tile.
-constexpr int PBW_SPLIT = 384;
+// Load balance of the backward: tiles at the horizon collect ~4x the mean item count.  A tile
+// with more than PBW_SPLIT items is split into S <= PBW_MAXS item ranges ("parts", ~PBW_PART
+// items each); each part writes its partial tile into a pool slot and a second launch sums the
+// S slots in part order into d_feats (deterministic: no float atomics; an in-launch hand-off to
+// the last part measured slower: its serial cross-XCD slot reads stretch the tail).  Split
+// tiles are queued first.
+//   tasks[i]  = {bc * nt + tile, lo, hi, meta}: items [lo, hi) of the (bc) item block;
+//               meta = -1 for a whole tile, else the part's pool slot
+//   combos[k] = {bc * nt + tile, first slot, S, 0} for the k-th split tile
+//   ctrl      = {task count, split-tile count}
+// When the pool runs out, the remaining heavy tiles run whole (correct, just slower).
+#ifndef VFD_PBW_SPLIT
+#define VFD_PBW_SPLIT 128
+#endif
+#ifndef VFD_PBW_PART
+#define VFD_PBW_PART 104
+#endif
+constexpr int PBW_SPLIT = VFD_PBW_SPLIT;
+constexpr int PBW_PART = VFD_PBW_PART;
+constexpr int PBW_MAXS = 8;
+constexpr int PBW_POOL = 8192;         // part slots of PT2 x POSE_MAXC floats (128 MB)
 
 __global__ __launch_bounds__(1024) void plan_task_k(vfd_voxel_desc d, const int* __restrict__ tile_ptr,
-                                                    int2* __restrict__ tasks, int* __restrict__ ctrl) {
+                                                    int4* __restrict__ tasks, int4* __restrict__ combos,
+                                                    int* __restrict__ ctrl) {
   __shared__ int part[1024];
-  __shared__ int n_heavy_tasks;
+  __shared__ int total;
   const int nt = tiles_x(d) * tiles_y(d);
   const int M = d.B * d.N * nt;
-  constexpr int ng = POSE_MAXC / 64;
   const int t = threadIdx.x;
   const int chunk = (M + 1023) / 1024;
   const int c0 = min(M, t * chunk), c1 = min(M, c0 + chunk);
-  auto heavy = [&](int i) {
+  auto range = [&](int i, int& lo, int& hi) {
     const int bc = i / nt, tile = i % nt;
     const int* tp = tile_ptr + (size_t)bc * (nt * PSUB + 1);
-    return tp[(tile + 1) * PSUB] - tp[tile * PSUB] > PBW_SPLIT;
+    lo = tp[tile * PSUB];
+    hi = tp[(tile + 1) * PSUB];
   };
-  for (int pass = 0; pass < 2; ++pass) {           // pass 0: heavy tiles (ng tasks), 1: light
-    int local = 0;
-    for (int i = c0; i < c1; ++i) {
-      const bool h = heavy(i);
-      local += pass == 0 ? (h ? ng : 0) : (h ? 0 : 1);
-    }
+  auto want = [](int n) { return n > PBW_SPLIT ? min(PBW_MAXS, (n + PBW_PART - 1) / PBW_PART) : 0; };
+  auto scan = [&](int local) {                     // exclusive prefix over threads; total -> `total`
     __syncthreads();
     part[t] = local;
     __syncthreads();
@@ -898,21 +920,57 @@ __global__ __launch_bounds__(1024) void plan_task_k(vfd_voxel_desc d, const int*
       part[t] += v;
       __syncthreads();
     }
-    int run = part[t] - local + (pass == 1 ? n_heavy_tasks : 0);
-    for (int i = c0; i < c1; ++i) {
-      const bool h = heavy(i);
-      if (pass == 0 && h) {
-        for (int g = 0; g < ng; ++g) tasks[run++] = make_int2(i, g | (1 << 8));
-      } else if (pass == 1 && !h) {
-        tasks[run++] = make_int2(i, 0 | (0xFF << 8));
-      }
-    }
+    if (t == 1023) total = part[t];
     __syncthreads();
-    if (t == 1023) {
-      if (pass == 0) n_heavy_tasks = part[t];
-      else ctrl[0] = n_heavy_tasks + part[t];
+    return part[t] - local;
+  };
+  int lo, hi;
+  // pass 0: pool slots wanted
+  int local = 0;
+  for (int i = c0; i < c1; ++i) { range(i, lo, hi); local += want(hi - lo); }
+  const int slot0 = scan(local);
+  auto fits = [](int s, int sl) { return s > 0 && sl + s <= PBW_POOL; };
+  // pass 1: split tiles (their slots fit the pool): parts and combine entries
+  int nsplit = 0;
+  local = 0;
+  for (int i = c0, sl = slot0; i < c1; ++i) {
+    range(i, lo, hi);
+    const int s = want(hi - lo);
+    if (fits(s, sl)) { local += s; ++nsplit; }
+    sl += s;
+  }
+  int run = scan(local);
+  const int n_parts = total;
+  int crun = scan(nsplit);
+  const int n_combo = total;
+  for (int i = c0, sl = slot0; i < c1; ++i) {
+    range(i, lo, hi);
+    const int n = hi - lo, s = want(n);
+    if (fits(s, sl)) {
+      for (int p = 0; p < s; ++p)
+        tasks[run++] = make_int4(i, lo + (int)((long long)n * p / s), lo + (int)((long long)n * (p + 1) / s), sl + p);
+      combos[crun++] = make_int4(i, sl, s, 0);
     }
-    __syncthreads();
+    sl += s;
+  }
+  // pass 2: whole tiles
+  local = 0;
+  for (int i = c0, sl = slot0; i < c1; ++i) {
+    range(i, lo, hi);
+    const int s = want(hi - lo);
+    if (!fits(s, sl)) local += 1;
+    sl += s;
+  }
+  run = n_parts + scan(local);
+  for (int i = c0, sl = slot0; i < c1; ++i) {
+    range(i, lo, hi);
+    const int s = want(hi - lo);
+    if (!fits(s, sl)) tasks[run++] = make_int4(i, lo, hi, -1);
+    sl += s;
+  }
+  if (t == 0) {
+    ctrl[0] = n_parts + total;
+    ctrl[1] = n_combo;
   }
 }
 
@@ -921,143 +979,259 @@ __global__ __launch_bounds__(1024) void plan_task_k(vfd_voxel_desc d, const int*
 #endif
 constexpr int PBW_U = VFD_PBW_U;       // voxel rows (1 KB each) in flight per wave
 
-__global__ __launch_bounds__(256) void fuse_pose_bwd_k(vfd_voxel_desc d, const int* __restrict__ tile_ptr,
-                                                       const TileItem* __restrict__ items,
-                                                       const int2* __restrict__ tasks, int* __restrict__ ctrl,
-                                                       const float* __restrict__ dout, float* __restrict__ dfeats) {
-  // one LDS copy of the tile per wave: [pixel][POSE_MAXC + 1] (odd pitch: conflict-free sweeps)
-  constexpr int LDP = POSE_MAXC + 1;
-  __shared__ float acc_l[4 * PT2 * LDP];
-  __shared__ int task_l;
-  const int hw = d.h * d.w;
-  const int V = d.X * d.Y * d.Z;
+// Reflect-pad fold of the pose output's gradient: a voxel with xi in {1, X-2} or yi in {1, Y-2}
+// has copies in the padded map; their sum goes to a compact buffer (row = (b * nslot + slot) * Z
+// + z, C + 1 floats), so the backward's row reads carry no data-dependent extra loads.
+__global__ __launch_bounds__(256) void pose_fold_k(vfd_voxel_desc d, const float* __restrict__ dout,
+                                                   float* __restrict__ fb) {
+  const int nslot = 2 * (d.X + d.Y);
+  const int slot = blockIdx.x % nslot, b = blockIdx.x / nslot;
+  int xi, yi;
+  if (slot < d.X) { xi = slot; yi = 1; }
+  else if (slot < 2 * d.X) { xi = slot - d.X; yi = d.Y - 2; }
+  else if (slot < 2 * d.X + d.Y) { xi = 1; yi = slot - 2 * d.X; }
+  else { xi = d.X - 2; yi = slot - 2 * d.X - d.Y; }
+  if (pose_fold_slot(xi, yi, d.X, d.Y) != slot) return;     // owned by an earlier slot
+  // a padded position's Z rows are contiguous: sum the (up to 4) copies' Z * (C + 1) floats
+  const int n = d.Z * (d.C + 1), Xo = d.X + 2;
+  const float* gb = dout + (size_t)b * (d.Y + 2) * Xo * n;
+  const int ex = xi == 1 ? 0 : (xi == d.X - 2 ? d.X + 1 : -1);   // x-mirror column (padded)
+  const int ey = yi == 1 ? 0 : (yi == d.Y - 2 ? d.Y + 1 : -1);
+  const float* p0 = gb + ((size_t)(yi + 1) * Xo + xi + 1) * n;
+  const float* p1 = gb + ((size_t)(yi + 1) * Xo + max(ex, 0)) * n;
+  const float* p2 = gb + ((size_t)max(ey, 0) * Xo + xi + 1) * n;
+  const float* p3 = gb + ((size_t)max(ey, 0) * Xo + max(ex, 0)) * n;
+  const float f1 = ex >= 0 ? 1.f : 0.f, f2 = ey >= 0 ? 1.f : 0.f, f3 = f1 * f2;
+  float* dst = fb + ((size_t)b * nslot + slot) * n;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    // ((primary + x-copy) + y-copy) + xy-copy, absent copies weighted 0 (loads stay in range)
+    float s = p0[i];
+    s += f1 * p1[i];
+    s += f2 * p2[i];
+    s += f3 * p3[i];
+    dst[i] = s;
+  }
+}
+
+#ifdef VFD_PBW_TRACE
+// diagnostic build only: per wave task {start, end, items | split << 24, cu | group << 32} (100 MHz clock)
+__device__ unsigned long long g_pbw_trace[16384 * 4];
+extern "C" int vfd_pbw_trace_read(void* dst, size_t bytes) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_pbw_trace), bytes, 0, hipMemcpyDeviceToHost);
+}
+#endif
+
+// One single-wave workgroup per task (a tile, or a part of a split tile); each lane owns four
+// consecutive channels, so one 16-B-per-lane load brings a whole gradient row (C <= 256
+// channels, 1 KiB) per wave-instruction.  The wave walks the task's items in batches of PBW_U
+// (records fetched lane-parallel four batches ahead and broadcast by readlane, rows loaded one
+// batch ahead), sums each footprint run in registers and flushes it into its LDS tile
+// [PT2 + 1][256] (row PT2 takes taps outside the tile).  Rows start at any 4-B offset (C + 1
+// floats per row): the 16-B loads run unaligned, which gfx9's unaligned access mode allows.
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void fuse_pose_bwd_k(vfd_voxel_desc d, const int4* __restrict__ tasks,
+                                                      const int* __restrict__ ctrl, const TileItem* __restrict__ items,
+                                                      const float* __restrict__ dout, const float* __restrict__ fbuf,
+                                                      float* __restrict__ pool, float* __restrict__ dfeats) {
+  constexpr int U = PBW_U;
+  constexpr int PR = PT2 + 1;
+  __shared__ float4 acc_l[PR * 64];
+  const int lane = threadIdx.x;
+  const int wt = blockIdx.x;
+  if (wt >= ctrl[0]) return;
+#ifdef VFD_PBW_TRACE
+  const unsigned long long t_start = wall_clock64();
+#endif
   const int C = d.C, C1 = d.C + 1;
-  const int ntx = tiles_x(d), nt = ntx * tiles_y(d);
-  const int lane = threadIdx.x & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int4 rec = tasks[wt];
+  const int bct = rec.x, lo = rec.y, hi = rec.z, meta = rec.w;
+  const int nt = tiles_x(d) * tiles_y(d), ntx = tiles_x(d);
+  const int bc = bct / nt, b = bc / d.N, tile = bct % nt;
+  const int V = d.X * d.Y * d.Z, hw = d.h * d.w;
   const int P = d.pad_out ? 2 : 0;
-  const int Yo = d.Y + P, Xo = d.X + P;
-  const size_t pix_stride = (size_t)d.Z * C1;
-  const int ntask = ctrl[0];
-  float* wacc = acc_l + wv * PT2 * LDP;
-  for (;;) {
-    __syncthreads();
-    if (threadIdx.x == 0) task_l = atomicAdd(ctrl + 1, 1);
-    for (int i = threadIdx.x; i < 4 * PT2 * LDP; i += 256) acc_l[i] = 0.f;
-    __syncthreads();
-    const int task = task_l;
-    if (task >= ntask) break;
-    const int2 tk = tasks[task];
-    const int bc = tk.x / nt, b = bc / d.N, tile = tk.x % nt;
-    const int g0 = tk.y & 0xFF;                      // channel groups [g0, g0 + ng) of 64
-    const int ng = min(tk.y >> 8, (C + 63) / 64 - g0);
-    if (ng <= 0) continue;                           // a split group beyond C (workgroup-uniform)
-    const int* tp = tile_ptr + (size_t)bc * (nt * PSUB + 1);
-    const TileItem* ib = items + (size_t)bc * 4 * V;
-    const float* gb = dout + (size_t)b * Yo * Xo * pix_stride;
-    const int lo = __builtin_amdgcn_readfirstlane(tp[tile * PSUB]);
-    const int hi = __builtin_amdgcn_readfirstlane(tp[tile * PSUB + PSUB]);
-    int cho[4];
+  const float* gb = dout + (size_t)b * (d.Y + P) * (d.X + P) * d.Z * C1;
+  const float* fb = fbuf + (size_t)b * 2 * (d.X + d.Y) * d.Z * C1;
+  const TileItem* ib = items + (size_t)bc * 4 * V;
+  const int cq = min(lane, C / 4 - 1) * 4;         // this lane's first channel (idle lanes re-read)
+  float4* wacc = acc_l + lane;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) cho[k] = min(lane + 64 * (g0 + k), C - 1);
-    // the item walk, specialised on the group count so every load is unconditional (a load
-    // under a branch makes the compiler's waitcnt at the join wait for everything in flight)
-    auto walk = [&](auto ngc) {
-      constexpr int NG = decltype(ngc)::value;
-      // the open footprint run: tap sums per (tap, group) in fixed registers; flushed into the
-      // pixel-indexed accumulators when the run ends (out-of-tile taps have weight 0: skipped)
-      float tq[4][NG];
+  for (int p = 0; p < PT2; ++p) wacc[64 * p] = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 tq[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
+  for (int q = 0; q < 4; ++q) tq[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+  int cur = -1;
+  auto flush = [&]() {
+    if (cur < 0) return;
+    const int lx = (cur & 7) - 1, ly = (cur >> 3) - 1;
+    int o[4];
+    float4 v[4];
 #pragma unroll
-        for (int k = 0; k < NG; ++k) tq[q][k] = 0.f;
-      int cur = -1;
-      auto flush = [&]() {
-        if (cur < 0) return;
-        const int lx = (cur & 7) - 1, ly = (cur >> 3) - 1;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int px = lx + (q & 1), py = ly + (q >> 1);
-          if (px >= 0 && px < PT && py >= 0 && py < PT) {
-            float* r = wacc + (py * PT + px) * LDP + lane;
-#pragma unroll
-            for (int k = 0; k < NG; ++k) r[64 * k] += tq[q][k];
-          }
-#pragma unroll
-          for (int k = 0; k < NG; ++k) tq[q][k] = 0.f;
-        }
-      };
-      for (int j = lo + wv * PBW_U; j < hi; j += 4 * PBW_U) {
-        // lane-parallel item fetch (lane u < PBW_U holds item j + u), broadcast by readlane: the
-        // batch's items cost one vector load each instead of a block of SGPRs
-        const TileItem mine = ib[min(j + (lane & (PBW_U - 1)), hi - 1)];  // tail slots re-read the last item
-        TileItem it[PBW_U];
-#pragma unroll
-        for (int u = 0; u < PBW_U; ++u) {
-          it[u].pz = (uint32_t)__builtin_amdgcn_readlane((int)mine.pz, u);
-          it[u].rden = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine.rden), u));
-#pragma unroll
-          for (int q = 0; q < 4; ++q) it[u].w[q] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine.w[q]), u));
-          it[u].lxy = __builtin_amdgcn_readlane(mine.lxy, u);
-        }
-        float g[PBW_U][NG];
-#pragma unroll
-        for (int u = 0; u < PBW_U; ++u) {
-          const float* row = gb + (size_t)(it[u].pz & 0xFFFFF) * pix_stride + ((it[u].pz >> 20) & 0xFF) * C1;
-#pragma unroll
-          for (int k = 0; k < NG; ++k) g[u][k] = row[cho[k]];
-        }
-#pragma unroll
-        for (int u = 0; u < PBW_U; ++u) {
-          if (j + u >= hi) continue;
-          if (it[u].pz >> 28) {                               // reflect-padding copies (grid border)
-            // pad_sets with constant indices (a runtime-indexed set would live in scratch)
-            const int pos = it[u].pz & 0xFFFFF, zo = ((it[u].pz >> 20) & 0xFF) * C1;
-            const int xi = pos % Xo - P / 2, yi = pos / Xo - P / 2;
-            const int ry[3] = {yi + 1, 0, d.Y + 1}, cx[3] = {xi + 1, 0, d.X + 1};
-            const bool vy[3] = {true, yi == 1, yi == d.Y - 2}, vx[3] = {true, xi == 1, xi == d.X - 2};
-#pragma unroll
-            for (int a = 0; a < 3; ++a)
-#pragma unroll
-              for (int c2 = 0; c2 < 3; ++c2) {
-                if ((a == 0 && c2 == 0) || !vy[a] || !vx[c2]) continue;
-                const float* row = gb + ((size_t)ry[a] * Xo + cx[c2]) * pix_stride + zo;
-#pragma unroll
-                for (int k = 0; k < NG; ++k) g[u][k] += row[cho[k]];
-              }
-          }
-          if (it[u].lxy != cur) {
-            flush();
-            cur = it[u].lxy;
-          }
-          // d(mean) = g / den (as g * (1/den)), then grid_sample's backward adds d(mean) * w
-#pragma unroll
-          for (int k = 0; k < NG; ++k) {
-            const float gd = g[u][k] * it[u].rden;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) tq[q][k] = __builtin_fmaf(gd, it[u].w[q], tq[q][k]);
-          }
-        }
-      }
-      flush();
-    };
-    switch (ng) {
-      case 1: walk(std::integral_constant<int, 1>{}); break;
-      case 2: walk(std::integral_constant<int, 2>{}); break;
-      case 3: walk(std::integral_constant<int, 3>{}); break;
-      default: walk(std::integral_constant<int, 4>{}); break;
+    for (int q = 0; q < 4; ++q) {
+      const int px = lx + (q & 1), py = ly + (q >> 1);
+      o[q] = 64 * ((px >= 0 && px < PT && py >= 0 && py < PT) ? py * PT + px : PT2);
+      v[q] = wacc[o[q]];
     }
-    __syncthreads();
-    // ((w0 + w1) + w2) + w3, written NCHW with threads along the tile's pixels
-    const int cbase = 64 * g0, cn = min(C - cbase, 64 * ng);
-    const int tx = tile % ntx, ty = tile / ntx;
-    float* db = dfeats + ((size_t)bc * C + cbase) * hw;
-    for (int i = threadIdx.x; i < cn * PT2; i += blockDim.x) {
-      const int ch = i / PT2, pl = i % PT2;
-      const int x = tx * PT + pl % PT, y = ty * PT + pl / PT;
-      const int o = pl * LDP + ch;
-      const float v = ((acc_l[o] + acc_l[PT2 * LDP + o]) + acc_l[2 * PT2 * LDP + o]) + acc_l[3 * PT2 * LDP + o];
-      if (x < d.w && y < d.h) db[(size_t)ch * hw + y * d.w + x] = v;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      wacc[o[q]] = make_float4(v[q].x + tq[q].x, v[q].y + tq[q].y, v[q].z + tq[q].z, v[q].w + tq[q].w);
+      tq[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  // lane-parallel record fetch of a group of 3 batches: lane i < 3U holds item jb + i; tail
+  // slots re-read the last item and get 1/den = 0 when consumed (they add nothing and keep its
+  // footprint: no flush).  A fetched record is never touched before its use (any VALU op on it
+  // would wait for it).
+  constexpr int GI = 3 * U;                        // items per record group
+  auto fetch = [&](int jb) { return ib[min(jb + (lane < GI ? lane : 0), hi - 1)]; };
+  // the item's gradient row: its own padded position, or the folded sum of its reflect copies
+  // (bit 31): a wave-uniform pointer select, so every row load is unconditional
+  // (buffer loads: the row offset is a scalar soffset and the lane's channel offset a constant
+  // voffset, so an item costs no VGPR address arithmetic)
+  const __amdgpu_buffer_rsrc_t rs_g = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)gb, 0, (int)((size_t)(d.Y + P) * (d.X + P) * d.Z * C1 * sizeof(float)), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_f = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)fb, 0, (int)((size_t)2 * (d.X + d.Y) * d.Z * C1 * sizeof(float)), 0x00020000);
+  const int voff = cq * (int)sizeof(float);
+  auto issue = [&](const TileItem& m, int k, float4 (&gr)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)m.pz, k * U + u);
+      const int soff = (int)((r & 0x7FFFFFFFu) * (uint32_t)C1 * (uint32_t)sizeof(float));
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128((r >> 31) ? rs_f : rs_g, voff, soff, 0);
+      gr[u] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+    }
+  };
+  auto consume = [&](int jb, const TileItem& m, int k, const float4 (&gr)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int lxy = __builtin_amdgcn_readlane(m.lxy, k * U + u);
+      if (lxy != cur) {
+        flush();
+        cur = lxy;
+      }
+      // d(mean) = g / den (as g * (1/den)), then grid_sample's backward adds d(mean) * w
+      const float rden = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(m.rden), k * U + u));
+      const float r = jb + u < hi ? rden : 0.f;
+      const float4 gd = make_float4(gr[u].x * r, gr[u].y * r, gr[u].z * r, gr[u].w * r);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(m.w[q]), k * U + u));
+        tq[q].x = __builtin_fmaf(gd.x, w, tq[q].x);
+        tq[q].y = __builtin_fmaf(gd.y, w, tq[q].y);
+        tq[q].z = __builtin_fmaf(gd.z, w, tq[q].z);
+        tq[q].w = __builtin_fmaf(gd.w, w, tq[q].w);
+      }
+    }
+  };
+  // rows: a 3-slot ring, two batches in flight beyond the one being summed; records: the
+  // current and the next group, alternating between two registers (no copies)
+  float4 s0[U], s1[U], s2[U];
+  auto group = [&](int jg, const TileItem& Rc, const TileItem& Rn) {
+    issue(Rc, 2, s2);
+    consume(jg, Rc, 0, s0);
+    issue(Rn, 0, s0);
+    consume(jg + U, Rc, 1, s1);
+    issue(Rn, 1, s1);
+    consume(jg + 2 * U, Rc, 2, s2);
+  };
+  TileItem R0 = fetch(lo), R1 = fetch(lo + GI);
+  issue(R0, 0, s0);
+  issue(R0, 1, s1);
+  for (int j = lo;; j += 2 * GI) {
+    group(j, R0, R1);
+    if (j + GI >= hi) break;
+    R0 = fetch(j + 2 * GI);
+    group(j + GI, R1, R0);
+    if (j + 2 * GI >= hi) break;
+    R1 = fetch(j + 3 * GI);
+  }
+  flush();
+#ifdef VFD_PBW_TRACE
+  if (lane == 0 && wt < 16384) {
+    unsigned long long* r = g_pbw_trace + 4 * wt;
+    r[0] = t_start;
+    r[1] = wall_clock64();
+    r[2] = (unsigned long long)(hi - lo) | ((unsigned long long)(meta >= 0) << 24);
+    r[3] = (unsigned long long)__smid();
+  }
+#endif
+  if (meta >= 0) {                                 // a split tile's part: its pool slot
+    float4* ps = reinterpret_cast<float4*>(pool + (size_t)meta * PT2 * POSE_MAXC) + lane;
+    if (4 * lane < C) {
+#pragma unroll
+      for (int p = 0; p < PT2; ++p) ps[p * (POSE_MAXC / 4)] = wacc[64 * p];
+    }
+    return;
+  }
+  // NCHW: each lane writes 4 x-consecutive pixels of one channel per store (ch = lane + 64 k)
+  const float* tl = reinterpret_cast<const float*>(acc_l);      // [PR][256] floats
+  const int tx = tile % ntx, ty = tile / ntx;
+  const int x0 = tx * PT;
+  float* db = dfeats + (size_t)bc * C * hw;
+  const bool vec = (d.w % 4) == 0 && x0 + PT <= d.w;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int ch = lane + 64 * k;
+    if (ch >= C) break;
+#pragma unroll
+    for (int py = 0; py < PT; ++py) {
+      const int y = ty * PT + py;
+      if (y >= d.h) break;
+      float v[PT];
+#pragma unroll
+      for (int px = 0; px < PT; ++px) v[px] = tl[(py * PT + px) * 256 + ch];
+      float* dst = db + (size_t)ch * hw + (size_t)y * d.w + x0;
+      if (vec) {
+        *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+#pragma unroll
+        for (int px = 0; px < PT; ++px)
+          if (x0 + px < d.w) dst[px] = v[px];
+      }
+    }
+  }
+}
+
+// Split tiles: the S part slots summed in part order.  A workgroup takes split tiles in turn;
+// thread = channel, one tile row at a time with all S x 4 slot loads of the row in flight, each
+// channel's 4 pixels of the row written as one 16-B store.
+__global__ __launch_bounds__(256) void pose_combine_k(vfd_voxel_desc d, const int4* __restrict__ combos,
+                                                      const int* __restrict__ ctrl, const float* __restrict__ pool,
+                                                      float* __restrict__ dfeats) {
+  const int nt = tiles_x(d) * tiles_y(d), ntx = tiles_x(d);
+  const int hw = d.h * d.w;
+  const int ch = threadIdx.x;                      // 256 threads = POSE_MAXC channels
+  const int ncombo = ctrl[1];
+  const bool vec = (d.w % 4) == 0;
+  for (int k = blockIdx.x; k < ncombo; k += gridDim.x) {
+    const int4 cb = combos[k];
+    const int bc = cb.x / nt, tile = cb.x % nt;
+    const int x0 = (tile % ntx) * PT, y0 = (tile / ntx) * PT;
+    if (ch >= d.C) continue;
+    const float* p0 = pool + (size_t)cb.y * PT2 * POSE_MAXC + ch;
+    float* db = dfeats + ((size_t)bc * d.C + ch) * hw;
+    for (int py = 0; py < PT && y0 + py < d.h; ++py) {
+      // every slot load unconditional (absent parts re-read the last slot and add +0)
+      float v[PBW_MAXS][PT];
+#pragma unroll
+      for (int s = 0; s < PBW_MAXS; ++s)
+#pragma unroll
+        for (int px = 0; px < PT; ++px)
+          v[s][px] = p0[((size_t)min(s, cb.z - 1) * PT2 + py * PT + px) * POSE_MAXC];
+      float a[PT];
+#pragma unroll
+      for (int px = 0; px < PT; ++px) {
+        a[px] = v[0][px];
+#pragma unroll
+        for (int s = 1; s < PBW_MAXS; ++s) a[px] += (s < cb.z ? 1.f : 0.f) * v[s][px];   // part order
+      }
+      float* dst = db + (size_t)(y0 + py) * d.w + x0;
+      if (vec && x0 + PT <= d.w) {
+        *reinterpret_cast<float4*>(dst) = make_float4(a[0], a[1], a[2], a[3]);
+      } else {
+#pragma unroll
+        for (int px = 0; px < PT; ++px)
+          if (x0 + px < d.w) dst[px] = a[px];
+      }
     }
   }
 }
@@ -1829,12 +2003,18 @@ static size_t plan_items_bytes(const vfd_voxel_desc* d) {
   return (size_t)d->B * d->N * 4 * d->X * d->Y * d->Z * sizeof(TileItem);
 }
 static size_t plan_tasks_bytes(const vfd_voxel_desc* d) {     // independent of C (see plan_task_k)
-  return ((size_t)d->B * d->N * host_tiles(d) * (POSE_MAXC / 64) * sizeof(int2) + 255) / 256 * 256;
+  return ((size_t)(d->B * d->N * host_tiles(d) + PBW_POOL + PBW_POOL / 2) * sizeof(int4) + 255) / 256 * 256;
 }
+
+static size_t plan_fold_bytes(const vfd_voxel_desc* d) {       // K2 backward's folded border rows
+  return ((size_t)d->B * 2 * (d->X + d->Y) * d->Z * (POSE_MAXC + 1) * sizeof(float) + 255) / 256 * 256;
+}
+
+static constexpr size_t PLAN_POOL_BYTES = (size_t)PBW_POOL * PT2 * POSE_MAXC * sizeof(float);
 
 size_t vfd_fusion_plan_bytes(const vfd_voxel_desc* d) {
   return plan_entries_bytes(d) + plan_rowptr_bytes(d) + plan_cursor_bytes(d) + plan_items_bytes(d) +
-         plan_tasks_bytes(d) + 256;
+         plan_tasks_bytes(d) + 256 + plan_fold_bytes(d) + PLAN_POOL_BYTES;
 }
 
 int vfd_fusion_plan(const vfd_voxel_desc* d, const float* mask_lo, const float* K, const float* Einv, void* plan,
@@ -1867,9 +2047,10 @@ int vfd_fusion_plan(const vfd_voxel_desc* d, const float* mask_lo, const float* 
   plan_count_k<<<egrid, 256, hist, s>>>(*d, (const PlanEntry*)plan, counts, cursor);
   plan_scan_k<<<d->B * d->N, PIDX_THREADS, 0, s>>>(*d, cursor, row_ptr);
   plan_fill_k<<<egrid, 256, 2 * hist, s>>>(*d, (const PlanEntry*)plan, counts, cursor, csr);
-  int2* tasks = (int2*)((char*)csr + plan_items_bytes(d));
+  int4* tasks = (int4*)((char*)csr + plan_items_bytes(d));
   int* ctrl = (int*)((char*)tasks + plan_tasks_bytes(d));
-  plan_task_k<<<1, 1024, 0, s>>>(*d, row_ptr, tasks, ctrl);
+  int4* combos = tasks + (d->B * d->N * host_tiles(d) + PBW_POOL);
+  plan_task_k<<<1, 1024, 0, s>>>(*d, row_ptr, tasks, combos, ctrl);
   return fail_launch("fusion_plan");
 }
 
@@ -1896,17 +2077,21 @@ int vfd_fuse_pose_bwd(const vfd_voxel_desc* d, const void* plan, const int* coun
   int st = check_voxel_desc(d);
   if (st) return st;
   (void)counts;
-  VFD_REQUIRE(d->C >= 1 && d->C <= POSE_MAXC, "fuse_pose: C=%d outside [1, %d]", d->C, POSE_MAXC);
+  VFD_REQUIRE(d->C >= 4 && d->C <= POSE_MAXC && d->C % 4 == 0, "fuse_pose_bwd: C=%d must be a multiple of 4 in [4, %d]", d->C, POSE_MAXC);
   hipStream_t s = (hipStream_t)stream;
   const int hw = d->h * d->w;
   const int* row_ptr = (const int*)((const char*)plan + plan_entries_bytes(d));
   const TileItem* csr = (const TileItem*)((const char*)row_ptr + plan_rowptr_bytes(d) + plan_cursor_bytes(d));
-  const int2* tasks = (const int2*)((const char*)csr + plan_items_bytes(d));
-  int* ctrl = (int*)((char*)tasks + plan_tasks_bytes(d));      // {task count, work counter}
+  const int4* tasks = (const int4*)((const char*)csr + plan_items_bytes(d));
+  const int* ctrl = (const int*)((const char*)tasks + plan_tasks_bytes(d));   // {tasks, split tiles}
+  const int4* combos = tasks + (d->B * d->N * host_tiles(d) + PBW_POOL);
+  float* fbuf = (float*)((char*)ctrl + 256);                   // folded border rows (plan scratch)
+  float* pool = (float*)((char*)fbuf + plan_fold_bytes(d));    // split tiles' partials
   ProfScope ps(K_FUSE_POSE_BWD, s);
-  (void)hipMemsetAsync(ctrl + 1, 0, sizeof(int), s);
-  const int ntask = host_tiles(d) * d->B * d->N * (POSE_MAXC / 64);
-  fuse_pose_bwd_k<<<dim3(std::min(ntask, 512)), 256, 0, s>>>(*d, row_ptr, csr, tasks, ctrl, d_out, d_feats);
+  if (d->pad_out) pose_fold_k<<<d->B * 2 * (d->X + d->Y), 256, 0, s>>>(*d, d_out, fbuf);
+  const int ntask_max = host_tiles(d) * d->B * d->N + PBW_POOL;
+  fuse_pose_bwd_k<<<ntask_max, 64, 0, s>>>(*d, tasks, ctrl, csr, d_out, fbuf, pool, d_feats);
+  pose_combine_k<<<std::min(PBW_POOL / 2, host_tiles(d) * d->B * d->N), 256, 0, s>>>(*d, combos, ctrl, pool, d_feats);
   return fail_launch("fuse_pose_bwd");
 }
 

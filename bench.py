@@ -62,8 +62,8 @@ def make_cfg(config, batch=None):
         cfg = C.surround_fusion_cfg(batch_size=batch or 1)
         name = '6-cam DDAD 384x640 fusion, voxel 100x100x20, D=50, fp32'
     elif config == 3:
-        cfg = C.surround_fusion_cfg(batch_size=batch or 2)
-        name = '6-cam DDAD 384x640 fusion, B=2/GPU, fp32 (bf16 features not yet enabled)'
+        cfg = C.surround_fusion_cfg(batch_size=batch or 2, net_precision='bf16')
+        name = '6-cam DDAD 384x640 fusion, B=2/GPU, bf16 nets (MIOpen), fp32 fusion/geometry/loss kernels'
     elif config == 4:
         cfg = C.surround_fusion_cfg(batch_size=batch or 1, height=352, width=640, max_depth=80.0,
                                     cameras=list(C.NUSC_CAMERAS))
@@ -165,6 +165,8 @@ def main():
     ap.add_argument('--channels-last', type=int, default=0, help='1: NHWC memory format for the dense nets')
     args = ap.parse_args()
     faulthandler.enable()
+    if os.environ.get('VFD_BENCH_TRACEBACK'):     # diagnostics: dump every thread's stack periodically
+        faulthandler.dump_traceback_later(float(os.environ['VFD_BENCH_TRACEBACK']), repeat=True)
     t_start = time.time()
     done = threading.Event()
 
@@ -273,7 +275,7 @@ def main():
         'data': 'synthetic DDAD-shaped batches (seeded), seeded random-init weights',
         'config': {'workload': name, 'config_id': args.config, 'batch_per_gpu': s['B'], 'cameras': s['N'],
                    'image': [s['H'], s['W']], 'voxels': [s['X'], s['Y'], s['Z']], 'depth_bins': s['D'],
-                   'parallelism': f'dp{world}'},
+                   'parallelism': f'dp{world}', 'net_precision': cfg['training']['net_precision']},
         'roofline': {'kernel': dom, 'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic, 'alg_bytes_per_launch': alg,
                      'avg_launch_us': avg_s * 1e6, 'launches': n_launch},

@@ -7,6 +7,8 @@ many atomically accumulated fp32 terms in a different order than the reference's
 Discontinuities (nearest-mask lookups, OOB tests, argmin ties) are evaluated with the
 reference's operation order, so no mismatch allowance is made for them.
 """
+import math
+
 import numpy as np
 import pytest
 import torch
@@ -594,3 +596,40 @@ def test_graph_replay_matches_eager():
     # a second replay draws fresh identity noise and keeps training
     l2 = graphed()
     assert torch.isfinite(l2['total_loss']).item()
+
+
+def test_bf16_nets_step_tracks_fp32():
+    """Config 3's mixed precision (`net_precision='bf16'`): the dense nets run under bf16 autocast,
+    the HIP fusion / geometry / loss kernels stay fp32.  Same weights and inputs as the fp32 step:
+    the HIP ops must still receive fp32 tensors, the nets must hand back fp32 depths and poses, and
+    the losses / gradients must track the fp32 step within bf16 resolution (8 mantissa bits
+    through ~40 layers: 5e-2 relative on the losses, gradient cosine > 0.9 per net)."""
+    from vfdepth_amd import synth
+    from vfdepth_amd.layers import seeded_state_dict
+    from vfdepth_amd.vfdepth import VFDepthAlgo
+    runs = {}
+    for prec in ('fp32', 'bf16'):
+        cfg = G.step_cfg()
+        cfg['training']['net_precision'] = prec
+        algo = VFDepthAlgo(cfg, 0)
+        for m in algo.models.values():
+            m.load_state_dict(seeded_state_dict(m, seed=G.STEP_SEED))
+        algo.set_train()
+        inputs = synth.make_batch(cfg, seed=5)
+        noise = torch.zeros(6, 1, 2, cfg['training']['height'], cfg['training']['width'], device=DEV)
+        outputs, losses = algo.process_batch(inputs, 0, noise=noise)
+        losses['total_loss'].backward()
+        torch.cuda.synchronize()
+        assert outputs[('cam', 0)][('depth', 0)].dtype == torch.float32
+        assert outputs[('cam', 0)][('cam_T_cam', 0, -1)].dtype == torch.float32
+        grads = {n: torch.cat([p.grad.flatten() for p in m.parameters() if p.grad is not None])
+                 for n, m in algo.models.items()}
+        runs[prec] = ({k: float(v) for k, v in losses.items() if torch.is_tensor(v) and v.numel() == 1}, grads)
+    (l32, g32), (l16, g16) = runs['fp32'], runs['bf16']
+    for k in ('total_loss', 'reproj_loss', 'spatio_loss', 'spatio_tempo_loss'):
+        assert math.isfinite(l16[k]), k
+        assert abs(l16[k] - l32[k]) <= 5e-2 * abs(l32[k]) + 1e-6, f'{k}: bf16 {l16[k]} vs fp32 {l32[k]}'
+    for n in g32:
+        assert torch.isfinite(g16[n]).all(), n
+        cos = float(torch.nn.functional.cosine_similarity(g16[n].double(), g32[n].double(), dim=0))
+        assert cos > 0.9, f'{n}: gradient cosine {cos:.3f} between the bf16 and fp32 steps'

@@ -36,3 +36,16 @@ def test_inverse4x4_matches_lu_inverse():
     np.testing.assert_allclose(inverse4x4(E).numpy(), torch.inverse(E).numpy(), atol=1e-6)
     A = torch.randn(64, 4, 4, dtype=torch.float64) + 3 * torch.eye(4, dtype=torch.float64)
     np.testing.assert_allclose((inverse4x4(A) @ A).numpy(), np.broadcast_to(np.eye(4), (64, 4, 4)), atol=1e-10)
+
+
+def test_net_precision_flag():
+    """`net_precision` (config 3's bf16 nets) is validated at construction; fp32 is the default."""
+    import pytest
+    from vfdepth_amd import config as C
+    from vfdepth_amd.network import FusedDepthNet, FusedPoseNet
+    assert C.surround_fusion_cfg()['training']['net_precision'] == 'fp32'
+    cfg = C.surround_fusion_cfg(net_precision='bf16')
+    assert FusedDepthNet(cfg).bf16 and FusedPoseNet(cfg).bf16
+    from vfdepth_amd.vfdepth import VFDepthAlgo
+    with pytest.raises(ValueError):
+        VFDepthAlgo(C.surround_fusion_cfg(net_precision='fp16'), 'cpu')

@@ -104,6 +104,9 @@ def surround_fusion_cfg(**over):
             'min_depth': 1.5, 'max_depth': 200.0,
             'spatio': True, 'spatio_temporal': True, 'intensity_align': True,
             'focal_length_scale': 300, 'aug_depth': False, 'aug_angle': [15, 15, 40],
+            # build-only: precision of the dense nets (encoders/decoders/reduce_dim on MIOpen);
+            # 'bf16' = autocast for config 3, the HIP fusion/geometry/loss kernels stay fp32
+            'net_precision': 'fp32',
         },
         'loss': {'disparity_smoothness': 0.001, 'spatio_coeff': 0.03,
                  'spatio_tempo_coeff': 0.1, 'pose_loss_coeff': 0.0},

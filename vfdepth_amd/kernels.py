@@ -20,6 +20,12 @@ def _dev(t, what):
     return t.contiguous()
 
 
+# Under bf16 autocast (net_precision='bf16', config 3) the fusion ops take fp32 inputs and run
+# with autocast off; their gradients are cast back to the callers' dtypes by autograd.
+_amp_fwd = torch.amp.custom_fwd(device_type='cuda', cast_inputs=torch.float32)
+_amp_bwd = torch.amp.custom_bwd(device_type='cuda')
+
+
 def _ws(nbytes, device):
     return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
 
@@ -91,6 +97,7 @@ class FuseDepth(torch.autograd.Function):
     """K1: P [B,N,hw,2Cv] (folded 1x1-conv maps) -> voxel features [B,V,Cv] (channels-last)."""
 
     @staticmethod
+    @_amp_fwd
     def forward(ctx, space, P, mask_lo, K, Einv, wz, b_no, b_o):
         lib = L.load()
         P, mask_lo, K, Einv = (_dev(t, n) for t, n in ((P, 'P'), (mask_lo, 'mask'), (K, 'K'), (Einv, 'Einv')))
@@ -109,6 +116,7 @@ class FuseDepth(torch.autograd.Function):
         return vox
 
     @staticmethod
+    @_amp_bwd
     def backward(ctx, g):
         lib = L.load()
         vox, mask_lo, K, Einv = ctx.saved_tensors
@@ -184,6 +192,7 @@ class FusePose(torch.autograd.Function):
     reduce_dim's stride-2 conv: logical [B, Z*(C+1), Y+2, X+2], channel z*(C+1) + c."""
 
     @staticmethod
+    @_amp_fwd
     def forward(ctx, space, plan, feats):
         lib = L.load()
         feats = _dev(feats, 'feats')
@@ -199,6 +208,7 @@ class FusePose(torch.autograd.Function):
         return out
 
     @staticmethod
+    @_amp_bwd
     def backward(ctx, g):
         lib = L.load()
         B, N, C = ctx.shape[:3]
@@ -215,6 +225,7 @@ class VoxelProject(torch.autograd.Function):
     of reduce_dim's first conv: logical [B*N, D*Cv, h+2, w+2], channel d*Cv + c."""
 
     @staticmethod
+    @_amp_fwd
     def forward(ctx, space, vox, invK, E):
         lib = L.load()
         vox, invK, E = (_dev(t, n) for t, n in ((vox, 'voxel'), (invK, 'inv_K'), (E, 'extrinsics')))
@@ -230,6 +241,7 @@ class VoxelProject(torch.autograd.Function):
         return out
 
     @staticmethod
+    @_amp_bwd
     def backward(ctx, g):
         lib = L.load()
         invK, E = ctx.saved_tensors
@@ -455,6 +467,7 @@ class AggregateUp(torch.autograd.Function):
     """LReLU_0.1(base + sum_k up_align_corners(level_k) + bias), NCHW; levels are upsampled to base's size."""
 
     @staticmethod
+    @_amp_fwd
     def forward(ctx, base, bias, *levels):
         lib = L.load()
         base, bias = _dev(base, 'aggregate base'), _dev(bias, 'bias')
@@ -470,6 +483,7 @@ class AggregateUp(torch.autograd.Function):
         return out
 
     @staticmethod
+    @_amp_bwd
     def backward(ctx, g):
         out, = ctx.saved_tensors
         d = g * torch.where(out > 0, 1.0, 0.1)

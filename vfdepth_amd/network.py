@@ -31,6 +31,14 @@ def _aggregate(encoder, conv1x1, images, lvl, B, N):
     return feats, unpack_cam_feat(agg, B, N)
 
 
+def net_autocast(module, x):
+    """bf16 autocast around a fusion net's body when `net_precision == 'bf16'` (config 3): the
+    MIOpen convs run in bf16, the HIP ops cast their inputs back to fp32
+    (`custom_fwd(cast_inputs=float32)`), and the nets return fp32 disparities / poses, so the
+    geometry and losses always run in fp32."""
+    return torch.autocast(device_type='cuda', dtype=torch.bfloat16, enabled=module.bf16 and x.is_cuda)
+
+
 class FusionDepthDecoder(nn.Module):
     """Decoder from the fusion level up to full resolution (fusion_depthnet.py:97-145)."""
 
@@ -83,14 +91,17 @@ class FusedDepthNet(nn.Module):
         self.fusion_net = VFNet(cfg, int(m['fusion_feat_in_dim']), out_dim, model='depth')
         self.decoder = FusionDepthDecoder(lvl, self.encoder.num_ch_enc[:lvl + 1], [16, 32, 64, 128, 256],
                                           self.scales, use_skips=bool(m['use_skips']))
+        self.bf16 = t.get('net_precision', 'fp32') == 'bf16'
 
     def forward(self, inputs):
         outputs = {('cam', c): {} for c in range(self.num_cams)}
         imgs = inputs[('color_aug', 0, 0)]
         B, N = imgs.shape[:2]
-        feats, agg = _aggregate(self.encoder, self.conv1x1, pack_cam_feat(imgs), self.fusion_level, B, N)
-        fusion = self.fusion_net(inputs, agg)
-        disp = self.decoder(feats[:self.fusion_level] + [fusion['proj_feat']])
+        with net_autocast(self, imgs):
+            feats, agg = _aggregate(self.encoder, self.conv1x1, pack_cam_feat(imgs), self.fusion_level, B, N)
+            fusion = self.fusion_net(inputs, agg)
+            disp = self.decoder(feats[:self.fusion_level] + [fusion['proj_feat']])
+        disp = {k: v.float() for k, v in disp.items()}
         for k, v in disp.items():
             v = v.view(B, N, *v.shape[1:])
             for c in range(N):
@@ -115,14 +126,16 @@ class FusedPoseNet(nn.Module):
         self.fusion_net = VFNet(cfg, int(m['fusion_feat_in_dim']), out_dim, model='pose')
         self.pose_decoder = PoseDecoder(num_ch_enc=[out_dim], num_input_features=1,
                                         num_frames_to_predict_for=1, stride=2)
+        self.bf16 = cfg['training'].get('net_precision', 'fp32') == 'bf16'
 
     def forward(self, inputs, frame_ids, _cam=None):
         imgs = torch.cat([inputs[('color_aug', frame_ids[0], 0)], inputs[('color_aug', frame_ids[1], 0)]], 2)
         B, N = imgs.shape[:2]
-        _, agg = _aggregate(self.encoder, self.conv1x1, pack_cam_feat(imgs), self.fusion_level, B, N)
-        bev = self.fusion_net(inputs, agg)
-        axis_angle, translation = self.pose_decoder([[bev]])
-        return axis_angle, torch.clamp(translation, -4.0, 4.0)
+        with net_autocast(self, imgs):
+            _, agg = _aggregate(self.encoder, self.conv1x1, pack_cam_feat(imgs), self.fusion_level, B, N)
+            bev = self.fusion_net(inputs, agg)
+            axis_angle, translation = self.pose_decoder([[bev]])
+        return axis_angle.float(), torch.clamp(translation.float(), -4.0, 4.0)
 
 
 class MonoDepthNet(nn.Module):

@@ -42,6 +42,8 @@ class VFDepthAlgo:
         for k, v in flatten(cfg).items():
             setattr(self, k, v)
         self.device = torch.device(f'cuda:{rank}') if isinstance(rank, int) else torch.device(rank)
+        if getattr(self, 'net_precision', 'fp32') not in ('fp32', 'bf16'):
+            raise ValueError(f'net_precision must be fp32 or bf16, got {self.net_precision!r}')
         self.prepare_dataset(cfg, rank)
         self.models = self.prepare_model(cfg, rank)
         self.losses = self.init_losses(cfg, rank)

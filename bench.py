@@ -71,7 +71,7 @@ def make_cfg(config, batch=None):
     elif config == 5:
         cfg = C.surround_fusion_cfg(batch_size=batch or 4, height=640, width=960, voxel_size=[200, 200, 20],
                                     voxel_unit_size=[0.5, 0.5, 1.5])
-        name = '6-cam 640x960, voxel 200x200x20 @0.5m, B=4/GPU, fp32'
+        name = f'6-cam 640x960, voxel 200x200x20 @0.5m, B={batch or 4}/GPU, fp32'
     else:
         raise SystemExit(f'unknown config {config}')
     return cfg, name
@@ -105,6 +105,7 @@ def algorithmic_bytes(kernel, s):
         'fuse_pose_bwd': pose_out + B * V * 8 + B * N * C * p,
         'voxel_project_fwd': B * V * Cv + proj_out,
         'voxel_project_bwd': proj_out + B * V * Cv,
+        'voxel_project_plan': 4 * B * N * p * D,                  # one 16-B sorted entry per frustum sample
         'view_stats': B * N * P * (1 + 3 * (T + 1) + 1),
         'view_apply': B * N * P * (1 + 3 * (T + 1) + 1) + B * N * P * (4 * T + 4 * F),
         'view_bwd': B * N * P * (1 + 3 * (T + 1) + 1) + B * N * P * 3 * (T + F) + B * N * P,

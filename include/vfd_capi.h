@@ -101,8 +101,18 @@ int vfd_voxel_project_fwd(const vfd_voxel_desc* d, const float* vox, const float
                           const float* E, float* out, void* stream);
 /* Autograd of the trilinear gather (grid_sampler_3d_backward, volumetric_fusionnet.py:261-262):
  * d_out (forward layout, reflect copies folded) -> d_vox [B,V,Cv] (fully written here).
- * Counting sort of the frustum samples by voxel cell + brick-owned LDS accumulation; needs
- * vfd_voxel_project_bwd_workspace(d) bytes of device workspace (no host sync, graph-safe). */
+ * Two phases: (1) vfd_voxel_project_plan — geometry only (invK, E, depth bins): counting sort of
+ * the frustum samples by voxel cell, tile parts, task list, into a device buffer of
+ * vfd_voxel_project_plan_bytes(d) bytes; independent of d_out, so it can run on a side stream
+ * while the forward's dense layers run; (2) vfd_voxel_project_bwd_planned — fold the reflect
+ * copies of d_out and accumulate each voxel tile in LDS from the sorted samples.  A plan serves any
+ * number of backward calls with the same descriptor / geometry.  vfd_voxel_project_bwd does both
+ * in one call (workspace = the plan buffer).  No host sync; graph-safe. */
+size_t vfd_voxel_project_plan_bytes(const vfd_voxel_desc* d);
+int vfd_voxel_project_plan(const vfd_voxel_desc* d, const float* invK, const float* E, void* plan,
+                           size_t plan_bytes, void* stream);
+int vfd_voxel_project_bwd_planned(const vfd_voxel_desc* d, const float* d_out, void* plan,
+                                  size_t plan_bytes, float* d_vox, void* stream);
 size_t vfd_voxel_project_bwd_workspace(const vfd_voxel_desc* d);
 int vfd_voxel_project_bwd(const vfd_voxel_desc* d, const float* d_out, const float* invK,
                           const float* E, float* d_vox, void* ws, size_t ws_bytes, void* stream);

@@ -126,6 +126,37 @@ def test_voxel_project_forward_backward():
     gclose(v.grad.permute(0, 2, 1), fx['d_vleaf'], 'K3 d voxel')
 
 
+def test_voxel_project_bwd_one_call_and_plan_reuse():
+    """The one-call C entry (`vfd_voxel_project_bwd`: plan + backward) and a plan reused for a
+    second backward agree bit for bit with the split plan / planned-backward path the op uses."""
+    import ctypes
+    from vfdepth_amd import _lib as L
+    from vfdepth_amd import kernels as KN
+    cfg, d, seeds, fx, net, inputs = _fusion_net('depth')
+    space = net.space(DEV)
+    lib = L.load()
+    v = G.seeded_randn(fx['vox'].shape, seeds['vleaf']).to(DEV).permute(0, 2, 1).contiguous().requires_grad_(True)
+    invK, E = inputs[('inv_K', 3)].contiguous(), inputs['extrinsics'].contiguous()
+    out = KN.VoxelProject.apply(space, v, invK, E)
+    g = torch.randn(out.shape, device=DEV).contiguous(memory_format=torch.channels_last)
+    out.backward(g)
+    B, V, Cv = v.shape
+    desc = space.desc(B, E.shape[1], Cv=Cv)
+    nbytes = lib.vfd_voxel_project_bwd_workspace(ctypes.byref(desc))
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=DEV)
+    one = torch.empty(B, V, Cv, device=DEV)
+    L.check(lib.vfd_voxel_project_bwd(ctypes.byref(desc), g.data_ptr(), invK.data_ptr(), E.data_ptr(), one.data_ptr(),
+                                      ws.data_ptr(), nbytes, L.stream()), 'voxel_project_bwd')
+    again = torch.empty(B, V, Cv, device=DEV)
+    L.check(lib.vfd_voxel_project_bwd_planned(ctypes.byref(desc), g.data_ptr(), ws.data_ptr(), nbytes,
+                                              again.data_ptr(), L.stream()), 'voxel_project_bwd_planned')
+    torch.cuda.synchronize()
+    # split tiles add their parts with atomics (order-dependent rounding): compare at 1e-6 of max
+    scale = float(v.grad.abs().max())
+    assert float((one - v.grad).abs().max()) <= 1e-6 * scale
+    assert float((again - v.grad).abs().max()) <= 1e-6 * scale
+
+
 def test_voxel_project_padding_matches_reflect_conv():
     """Writing the reflect-padded layout then conv(padding=0) == reference conv(padding_mode='reflect')."""
     from vfdepth_amd import kernels as KN

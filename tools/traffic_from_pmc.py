@@ -20,8 +20,8 @@ OPS = {
     'fuse_pose_fwd': ['fuse_pose_fwd_k'],
     'fuse_pose_bwd': ['pose_fold_k', 'fuse_pose_bwd_k', 'pose_combine_k'],
     'voxel_project_fwd': ['voxel_project_fwd_k'],
-    'voxel_project_bwd': ['vpb_count_fold_k', 'vpb_scan1_k', 'vpb_scan2_k', 'vpb_fill_k', 'vpb_fold_k', 'vpb_tile_k',
-                          'vpb_tasks_k', 'vpb_main_k'],
+    'voxel_project_plan': ['vpb_count_k', 'vpb_scan1_k', 'vpb_scan2_k', 'vpb_fill_k', 'vpb_tile_k', 'vpb_tasks_k'],
+    'voxel_project_bwd': ['vpb_fold_zero_k', 'vpb_main_k'],
     'view_stats': ['view_stats_k', 'view_finalize_k'],
     'view_apply': ['view_apply_k'],
     'view_bwd': ['view_bwd_k', 'view_bwd_reduce_k'],

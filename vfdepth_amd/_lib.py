@@ -51,6 +51,9 @@ _SIGS = {
     'vfd_fuse_pose_fwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 5 + [c_void_p]),
     'vfd_fuse_pose_bwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 4 + [c_void_p]),
     'vfd_voxel_project_fwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 4 + [c_void_p]),
+    'vfd_voxel_project_plan_bytes': (c_size_t, [ctypes.POINTER(VoxelDesc)]),
+    'vfd_voxel_project_plan': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 2 + [c_void_p, c_size_t, c_void_p]),
+    'vfd_voxel_project_bwd_planned': (c_int, [ctypes.POINTER(VoxelDesc), c_fp, c_void_p, c_size_t, c_fp, c_void_p]),
     'vfd_voxel_project_bwd_workspace': (c_size_t, [ctypes.POINTER(VoxelDesc)]),
     'vfd_voxel_project_bwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 4 + [c_void_p, c_size_t, c_void_p]),
     'vfd_view_workspace_bytes': (c_size_t, [ctypes.POINTER(ViewDesc)]),
@@ -107,7 +110,7 @@ KERNEL_IDS = {
     'mask_downsample': 0, 'fuse_depth_fwd': 1, 'fuse_depth_bwd': 2, 'fuse_pose_fwd': 3, 'fuse_pose_bwd': 4,
     'voxel_project_fwd': 5, 'voxel_project_bwd': 6, 'view_stats': 7, 'view_apply': 8, 'view_bwd': 9,
     'photo_fwd': 10, 'photo_bwd': 11, 'smooth_fwd': 12, 'smooth_bwd': 13, 'fusion_plan': 14,
-    'aggregate': 15,
+    'aggregate': 15, 'voxel_project_plan': 16,
 }
 
 

@@ -1414,7 +1414,10 @@ __global__ __launch_bounds__(256) void voxel_project_fwd_k(vfd_voxel_desc d, con
 #endif
 constexpr int VB_X = 8, VB_Y = 4;                  // voxel tile (one z layer) per wave task
 constexpr int VB_RY = VB_Y + 1, VB_NSEG = 2 * VB_RY;   // cell rows per layer, entry ranges per tile
-constexpr int VB_S = 1024;                         // samples per task part
+#ifndef VFD_VPB_S
+#define VFD_VPB_S 1024
+#endif
+constexpr int VB_S = VFD_VPB_S;                    // samples per task part
 constexpr int VB_SCAN = 4096;                      // cells per block of the first scan level
 
 struct VpbGeom {
@@ -1631,16 +1634,42 @@ __device__ __forceinline__ void vpb_fold(const vfd_voxel_desc& d, const float* _
   }
 }
 
-// One launch for the two independent first steps: blocks [0, nc) count samples per cell (latency-
-// bound returning atomics), blocks [nc, nc + nf) fold the reflect copies of d_out (streaming);
-// they overlap on the chip instead of running back to back.
+// plan phase: count samples per cell (latency-bound returning atomics)
+__global__ __launch_bounds__(256) void vpb_count_k(vfd_voxel_desc d, const float* __restrict__ invK,
+                                                   const float* __restrict__ E, int* __restrict__ cnt,
+                                                   int* __restrict__ rank, int cpb) {
+  vpb_count(d, invK, E, cnt, rank, blockIdx.x / cpb, blockIdx.x % cpb);
+}
+
+// backward phase, one launch: blocks [0, nf) fold the reflect copies of d_out (streaming), blocks
+// [nf, nf + nb) zero the voxels of split tiles (their parts add with atomics), block nf + nb
+// resets main's work counter
 template <int CV>
-__global__ __launch_bounds__(256) void vpb_count_fold_k(vfd_voxel_desc d, const float* __restrict__ invK,
-                                                        const float* __restrict__ E, int* __restrict__ cnt,
-                                                        int* __restrict__ rank, int cpb, int nc,
-                                                        const float* __restrict__ dout, float* __restrict__ fb) {
-  if ((int)blockIdx.x < nc) vpb_count(d, invK, E, cnt, rank, blockIdx.x / cpb, blockIdx.x % cpb);
-  else vpb_fold<CV>(d, dout, fb, blockIdx.x - nc);
+__global__ __launch_bounds__(256) void vpb_fold_zero_k(vfd_voxel_desc d, const float* __restrict__ dout,
+                                                       float* __restrict__ fb, int nf, const int* __restrict__ parts,
+                                                       int nb, int* __restrict__ ctrl, float* __restrict__ dvox) {
+  const int blk = blockIdx.x;
+  if (blk < nf) {
+    vpb_fold<CV>(d, dout, fb, blk);
+    return;
+  }
+  const int tile = blk - nf;
+  if (tile >= nb) {
+    if (threadIdx.x == 0) ctrl[1] = 0;
+    return;
+  }
+  if (parts[tile] <= 1) return;
+  const VpbGeom g = vpb_geom(d);
+  const int b = tile / g.ntile, tl = tile % g.ntile;
+  const int xb = (tl % g.nbx) * VB_X, yb = ((tl / g.nbx) % g.nby) * VB_Y, zp = tl / (g.nbx * g.nby);
+  const int V = d.X * d.Y * d.Z;
+  constexpr int QPV = CV / 4;
+  for (int i = threadIdx.x; i < 2 * VB_X * VB_Y * QPV; i += blockDim.x) {
+    const int q = i % QPV, v = (i / QPV) % (VB_X * VB_Y), zl = 2 * zp + i / (QPV * VB_X * VB_Y);
+    const int x = xb + v % VB_X, y = yb + v / VB_X;
+    if (x < d.X && y < d.Y && zl < d.Z)
+      reinterpret_cast<float4*>(dvox + ((size_t)b * V + (zl * d.Y + y) * d.X + x) * CV)[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
 }
 
 // entry range of cell row (z0, y0) of brick column [xb - 1, xb + 7] (clipped to the grid)
@@ -1657,9 +1686,6 @@ __device__ __forceinline__ void vpb_segment(const vfd_voxel_desc& d, const VpbGe
   *s1 = vpb_ptr(ptr, boff, n, base + min(xb + VB_X, d.X) + 1);
 }
 
-// per tile (8x8 voxels of one z layer): its samples = the 2 x 9 cell rows touching the layer
-// -> number of parts; split tiles are zeroed here (their parts add with atomics).
-// grid = B * ntile, block = one wave (lanes 0..17 = the cell rows)
 // Entry range k (< VB_NSEG) of the wave for layer zl = 2 zp + w of a layer-pair tile: the cell
 // layer both waves share (z0 = 2 zp) comes first, so the pair reads those rows at the same time
 // (one L1/L2 fetch), then the wave's own outer layer (2 zp - 1 or 2 zp + 1).
@@ -1667,12 +1693,10 @@ __device__ __forceinline__ int vpb_seg_z0(int zp, int w, int k) {
   return k < VB_RY ? 2 * zp : (w == 0 ? 2 * zp - 1 : 2 * zp + 1);
 }
 
-// per layer-pair tile: samples of each layer's wave -> number of parts; split tiles are zeroed
-// here (their parts add with atomics).  grid = B * ntile, block = one wave
-template <int CV>
+// per layer-pair tile: samples of each layer's wave -> number of parts (split tiles are zeroed by
+// vpb_fold_zero_k in the backward phase).  grid = B * ntile, block = one wave
 __global__ __launch_bounds__(64) void vpb_tile_k(vfd_voxel_desc d, const int* __restrict__ ptr,
-                                                 const int* __restrict__ boff, int* __restrict__ parts,
-                                                 float* __restrict__ dvox) {
+                                                 const int* __restrict__ boff, int* __restrict__ parts) {
   const VpbGeom g = vpb_geom(d);
   const int tile = blockIdx.x, lane = threadIdx.x;
   const int b = tile / g.ntile, tl = tile % g.ntile;
@@ -1690,15 +1714,6 @@ __global__ __launch_bounds__(64) void vpb_tile_k(vfd_voxel_desc d, const int* __
   n1 = wave_sum(n1);
   const int np = max(1, (max(n0, n1) + VB_S - 1) / VB_S);
   if (lane == 0) parts[tile] = np;
-  if (np == 1) return;
-  const int V = d.X * d.Y * d.Z;
-  constexpr int QPV = CV / 4;
-  for (int i = lane; i < 2 * VB_X * VB_Y * QPV; i += 64) {
-    const int q = i % QPV, v = (i / QPV) % (VB_X * VB_Y), zl = 2 * zp + i / (QPV * VB_X * VB_Y);
-    const int x = xb + v % VB_X, y = yb + v / VB_X;
-    if (x < d.X && y < d.Y && zl < d.Z)
-      reinterpret_cast<float4*>(dvox + ((size_t)b * V + (zl * d.Y + y) * d.X + x) * CV)[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
 }
 
 // one workgroup: task list (int2 {tile, part | nparts << 16}), task count, main's work counter
@@ -2116,7 +2131,10 @@ int vfd_voxel_project_fwd(const vfd_voxel_desc* d, const float* vox, const float
   return fail_launch("voxel_project_fwd");
 }
 
-constexpr int VPB_WORKERS = 5120;      // persistent waves (20 per CU: LDS 8.4 KB, <=96 VGPRs)
+#ifndef VFD_VPB_WORKERS
+#define VFD_VPB_WORKERS 5120
+#endif
+constexpr int VPB_WORKERS = VFD_VPB_WORKERS;      // persistent waves (20 per CU: LDS 8.4 KB, <=96 VGPRs)
 
 struct VpbWs {
   size_t cnt, zero, ptr, bsum, boff, rank, entries, fold, parts, tasks, ctrl, total;
@@ -2143,54 +2161,73 @@ static VpbWs vpb_ws(const vfd_voxel_desc* d) {
   return w;
 }
 
-size_t vfd_voxel_project_bwd_workspace(const vfd_voxel_desc* d) {
-  if (check_voxel_desc(d)) return 0;
-  return vpb_ws(d).total;
-}
-
-int vfd_voxel_project_bwd(const vfd_voxel_desc* d, const float* d_out, const float* invK, const float* E,
-                          float* d_vox, void* ws, size_t ws_bytes, void* stream) {
+// The geometry-only half of the backward (the counting sort of the frustum samples by voxel cell,
+// the tile parts and the task list) depends on invK / E / the depth bins, not on d_out: it is its
+// own call so the caller can build it while the forward's dense layers run (side stream).
+static int vpb_check(const vfd_voxel_desc* d) {
   int st = check_voxel_desc(d);
   if (st) return st;
   VFD_REQUIRE(d->dbins != nullptr && d->D > 0, "depth bins not set");
-  hipStream_t s = (hipStream_t)stream;
   VFD_REQUIRE(d->Cv == 8 || d->Cv == 16 || d->Cv == 32 || d->Cv == 64, "voxel_project: Cv=%d unsupported (8/16/32/64)", d->Cv);
-  VFD_REQUIRE(((uintptr_t)d_vox & 15) == 0, "voxel_project: 16-B aligned d_vox required");
-  const VpbWs w = vpb_ws(d);
-  VFD_REQUIRE(ws != nullptr && ws_bytes >= w.total, "voxel_project_bwd: workspace %zu < %zu bytes", ws_bytes, w.total);
   VFD_REQUIRE((size_t)d->B * d->N * d->h * d->w * d->D < (1u << 31) / 2, "voxel_project_bwd: too many samples");
-  const VpbGeom g = vpb_geom(*d);
-  char* base = (char*)ws;
-  int* cnt = (int*)(base + w.cnt);
-  int* ptr = (int*)(base + w.ptr);
-  int* bsum = (int*)(base + w.bsum);
-  int* boff = (int*)(base + w.boff);
-  int* rank = (int*)(base + w.rank);
-  float4* entries = (float4*)(base + w.entries);
-  float* fb = (float*)(base + w.fold);
-  const float* zrow = (const float*)(base + w.zero);
-  int* parts = (int*)(base + w.parts);
-  int2* tasks = (int2*)(base + w.tasks);
-  int* ctrl = (int*)(base + w.ctrl);
-  const int ncell = d->B * g.ncell, nblk = cdiv(ncell, VB_SCAN), nb = d->B * g.ntile;
-  const int hwD = d->h * d->w * d->D;
   const size_t dout_rows = (size_t)d->B * d->N * (d->h + 2 * (d->pad_out ? 1 : 0)) * (d->w + 2 * (d->pad_out ? 1 : 0)) * d->D;
   VFD_REQUIRE(dout_rows < (1ull << 31), "voxel_project_bwd: d_out has too many rows for 31-bit row indices");
-  ProfScope ps(K_VPROJ_BWD, s);
-  (void)hipMemsetAsync(cnt, 0, w.fold, s);   // counters + zero row
-  dim3 sgrid(cdiv(hwD, 256), d->B * d->N);
-  const int cpb = cdiv(hwD, 256), nc = cpb * d->B * d->N;
+  return VFD_OK;
+}
+
+struct VpbPtrs {
+  int *cnt, *ptr, *bsum, *boff, *rank, *parts, *ctrl;
+  float4* entries;
+  float* fb;
+  const float* zrow;
+  int2* tasks;
+};
+
+static VpbPtrs vpb_ptrs(const VpbWs& w, void* ws) {
+  char* base = (char*)ws;
+  VpbPtrs p;
+  p.cnt = (int*)(base + w.cnt);
+  p.ptr = (int*)(base + w.ptr);
+  p.bsum = (int*)(base + w.bsum);
+  p.boff = (int*)(base + w.boff);
+  p.rank = (int*)(base + w.rank);
+  p.entries = (float4*)(base + w.entries);
+  p.fb = (float*)(base + w.fold);
+  p.zrow = (const float*)(base + w.zero);
+  p.parts = (int*)(base + w.parts);
+  p.tasks = (int2*)(base + w.tasks);
+  p.ctrl = (int*)(base + w.ctrl);
+  return p;
+}
+
+static void vpb_plan_launch(const vfd_voxel_desc* d, const float* invK, const float* E, void* ws, hipStream_t s) {
+  const VpbWs w = vpb_ws(d);
+  const VpbGeom g = vpb_geom(*d);
+  const VpbPtrs p = vpb_ptrs(w, ws);
+  const int ncell = d->B * g.ncell, nblk = cdiv(ncell, VB_SCAN), nb = d->B * g.ntile;
+  const int hwD = d->h * d->w * d->D;
+  (void)hipMemsetAsync(p.cnt, 0, w.fold, s);   // counters + zero row
+  const int cpb = cdiv(hwD, 256);
+  vpb_count_k<<<cpb * d->B * d->N, 256, 0, s>>>(*d, invK, E, p.cnt, p.rank, cpb);
+  vpb_scan1_k<<<nblk, 256, 0, s>>>(p.cnt, ncell, p.ptr, p.bsum);
+  vpb_scan2_k<<<1, 1024, 0, s>>>(p.bsum, nblk, p.boff);
+  vpb_fill_k<<<dim3(cpb, d->B * d->N), 256, 0, s>>>(*d, invK, E, p.rank, p.ptr, p.boff, p.entries);
+  vpb_tile_k<<<nb, 64, 0, s>>>(*d, p.ptr, p.boff, p.parts);
+  vpb_tasks_k<<<1, 1024, 0, s>>>(p.parts, nb, p.tasks, p.ctrl);
+}
+
+static void vpb_bwd_launch(const vfd_voxel_desc* d, const float* d_out, void* ws, float* d_vox, hipStream_t s) {
+  const VpbWs w = vpb_ws(d);
+  const VpbGeom g = vpb_geom(*d);
+  const VpbPtrs p = vpb_ptrs(w, ws);
+  const int nb = d->B * g.ntile;
   const int nf = d->pad_out ? d->B * d->N * 2 * (d->w + d->h) : 0;
   switch (d->Cv) {
-#define VPB_LAUNCH(CVV)                                                                            \
-  case CVV:                                                                                        \
-    vpb_count_fold_k<CVV><<<nc + nf, 256, 0, s>>>(*d, invK, E, cnt, rank, cpb, nc, d_out, fb);     \
-    vpb_scan1_k<<<nblk, 256, 0, s>>>(cnt, ncell, ptr, bsum);                                       \
-    vpb_scan2_k<<<1, 1024, 0, s>>>(bsum, nblk, boff);                                              \
-    vpb_fill_k<<<sgrid, 256, 0, s>>>(*d, invK, E, rank, ptr, boff, entries);                       \
-    vpb_tile_k<CVV><<<nb, 64, 0, s>>>(*d, ptr, boff, parts, d_vox);                                \
-    vpb_tasks_k<<<1, 1024, 0, s>>>(parts, nb, tasks, ctrl);                                        \
-    vpb_main_k<CVV><<<VPB_WORKERS / 2, 128, 0, s>>>(*d, ptr, boff, entries, tasks, ctrl, d_out, zrow, d_vox); \
+#define VPB_LAUNCH(CVV)                                                                                         \
+  case CVV:                                                                                                     \
+    vpb_fold_zero_k<CVV><<<nf + nb + 1, 256, 0, s>>>(*d, d_out, p.fb, nf, p.parts, nb, p.ctrl, d_vox);            \
+    vpb_main_k<CVV><<<VPB_WORKERS / 2, 128, 0, s>>>(*d, p.ptr, p.boff, p.entries, p.tasks, p.ctrl, d_out, p.zrow, \
+                                                     d_vox);                                                    \
     break;
     VPB_LAUNCH(8)
     VPB_LAUNCH(16)
@@ -2198,6 +2235,51 @@ int vfd_voxel_project_bwd(const vfd_voxel_desc* d, const float* d_out, const flo
     VPB_LAUNCH(64)
 #undef VPB_LAUNCH
   }
+}
+
+size_t vfd_voxel_project_plan_bytes(const vfd_voxel_desc* d) {
+  if (vpb_check(d)) return 0;
+  return vpb_ws(d).total;
+}
+
+size_t vfd_voxel_project_bwd_workspace(const vfd_voxel_desc* d) { return vfd_voxel_project_plan_bytes(d); }
+
+int vfd_voxel_project_plan(const vfd_voxel_desc* d, const float* invK, const float* E, void* plan,
+                           size_t plan_bytes, void* stream) {
+  int st = vpb_check(d);
+  if (st) return st;
+  VFD_REQUIRE(plan != nullptr && plan_bytes >= vpb_ws(d).total, "voxel_project_plan: buffer %zu < %zu bytes",
+              plan_bytes, vpb_ws(d).total);
+  hipStream_t s = (hipStream_t)stream;
+  ProfScope ps(K_VPROJ_PLAN, s);
+  vpb_plan_launch(d, invK, E, plan, s);
+  return fail_launch("voxel_project_plan");
+}
+
+int vfd_voxel_project_bwd_planned(const vfd_voxel_desc* d, const float* d_out, void* plan, size_t plan_bytes,
+                                  float* d_vox, void* stream) {
+  int st = vpb_check(d);
+  if (st) return st;
+  VFD_REQUIRE(((uintptr_t)d_vox & 15) == 0, "voxel_project: 16-B aligned d_vox required");
+  VFD_REQUIRE(plan != nullptr && plan_bytes >= vpb_ws(d).total, "voxel_project_bwd: plan %zu < %zu bytes",
+              plan_bytes, vpb_ws(d).total);
+  hipStream_t s = (hipStream_t)stream;
+  ProfScope ps(K_VPROJ_BWD, s);
+  vpb_bwd_launch(d, d_out, plan, d_vox, s);
+  return fail_launch("voxel_project_bwd");
+}
+
+int vfd_voxel_project_bwd(const vfd_voxel_desc* d, const float* d_out, const float* invK, const float* E,
+                          float* d_vox, void* ws, size_t ws_bytes, void* stream) {
+  int st = vpb_check(d);
+  if (st) return st;
+  VFD_REQUIRE(((uintptr_t)d_vox & 15) == 0, "voxel_project: 16-B aligned d_vox required");
+  VFD_REQUIRE(ws != nullptr && ws_bytes >= vpb_ws(d).total, "voxel_project_bwd: workspace %zu < %zu bytes", ws_bytes,
+              vpb_ws(d).total);
+  hipStream_t s = (hipStream_t)stream;
+  ProfScope ps(K_VPROJ_BWD, s);
+  vpb_plan_launch(d, invK, E, ws, s);
+  vpb_bwd_launch(d, d_out, ws, d_vox, s);
   return fail_launch("voxel_project_bwd");
 }
 

@@ -5,6 +5,7 @@ current HIP stream.  Inputs must be fp32 HIP tensors; there is no CPU or ATen fa
 missing library or a non-HIP tensor raises.
 """
 import ctypes
+import os
 
 import torch
 
@@ -133,11 +134,29 @@ class FuseDepth(torch.autograd.Function):
         return None, dP, None, None, None, dwzb[:3], dwzb[3], dwzb[4]
 
 
+def _side_stream(device):
+    """Stream for the geometry-only plans (K2 fusion plan, K3 backward plan).  Default: the current
+    stream (in order).  VFD_SIDE_PLANS=1 puts them on a side stream that overlaps the dense layers;
+    measured on MI355X at config 2 that is SLOWER (44.2-44.4 vs 41.9-42.1 ms/step: the plan
+    kernels co-running with MIOpen's implicit-GEMM convs cost those more than the plans take)."""
+    if os.environ.get('VFD_SIDE_PLANS', '0') != '1':
+        return torch.cuda.current_stream(device)
+    key = torch.device(device).index
+    st = _SIDE_STREAMS.get(key)
+    if st is None:
+        st = _SIDE_STREAMS[key] = torch.cuda.Stream(device=device)
+    return st
+
+
+_SIDE_STREAMS = {}
+
+
 class FusionPlan:
     """Per-(batch, camera) compacted list of visible voxels with their tap data (device buffers).
 
     Built once per step from K (fusion scale), E^-1 and the 1/8 mask; every pose-mode fusion call
-    of the step (forward and backward) reuses it (the geometry does not depend on features)."""
+    of the step reuses it (the geometry does not depend on features).  Only the backward reads the
+    buffers (built on `_side_stream`'s stream); `wait()` joins that stream."""
 
     def __init__(self, space, mask_lo, K, Einv):
         lib = L.load()
@@ -146,10 +165,21 @@ class FusionPlan:
         self.mask_lo, self.K, self.Einv = mask_lo, K, Einv
         d = space.desc(self.B, self.N)
         nbytes = lib.vfd_fusion_plan_bytes(ctypes.byref(d))
-        self.buf = torch.empty(nbytes, dtype=torch.uint8, device=mask_lo.device)
-        self.counts = torch.empty(self.B * self.N, dtype=torch.int32, device=mask_lo.device)
-        L.check(lib.vfd_fusion_plan(ctypes.byref(d), mask_lo.data_ptr(), K.data_ptr(), Einv.data_ptr(),
-                                    self.buf.data_ptr(), self.counts.data_ptr(), L.stream()), 'fusion_plan')
+        main, self.side = torch.cuda.current_stream(mask_lo.device), _side_stream(mask_lo.device)
+        self.side.wait_stream(main)
+        with torch.cuda.stream(self.side):
+            self.buf = torch.empty(nbytes, dtype=torch.uint8, device=mask_lo.device)
+            self.counts = torch.empty(self.B * self.N, dtype=torch.int32, device=mask_lo.device)
+            L.check(lib.vfd_fusion_plan(ctypes.byref(d), mask_lo.data_ptr(), K.data_ptr(), Einv.data_ptr(),
+                                        self.buf.data_ptr(), self.counts.data_ptr(), L.stream()), 'fusion_plan')
+        for t in (self.buf, self.counts):
+            t.record_stream(main)
+        for t in (mask_lo, K, Einv):
+            t.record_stream(self.side)
+
+    def wait(self):
+        """Make the current stream wait for the plan (before any kernel that reads its buffers)."""
+        torch.cuda.current_stream(self.buf.device).wait_stream(self.side)
 
 
 def _channels_last(t, what):
@@ -215,6 +245,7 @@ class FusePose(torch.autograd.Function):
         g = _channels_last(g, 'grad')
         dfeats = torch.empty(ctx.shape, device=g.device)
         d = ctx.space.desc(B, N, C=C)
+        ctx.plan.wait()
         L.check(lib.vfd_fuse_pose_bwd(ctypes.byref(d), ctx.plan.buf.data_ptr(), ctx.plan.counts.data_ptr(),
                                       g.data_ptr(), dfeats.data_ptr(), L.stream()), 'fuse_pose_bwd')
         return None, None, dfeats
@@ -222,7 +253,12 @@ class FusePose(torch.autograd.Function):
 
 class VoxelProject(torch.autograd.Function):
     """K3: voxel features [B,V,Cv] -> frustum features as the channels-last, reflect-padded input
-    of reduce_dim's first conv: logical [B*N, D*Cv, h+2, w+2], channel d*Cv + c."""
+    of reduce_dim's first conv: logical [B*N, D*Cv, h+2, w+2], channel d*Cv + c.
+
+    When the voxels need a gradient, the forward also builds the backward's geometry-only plan
+    (`vfd_voxel_project_plan`: the frustum samples sorted by voxel cell; see `_side_stream` for
+    where it runs); the backward joins that stream and runs only the d_out-dependent part
+    (`vfd_voxel_project_bwd_planned`)."""
 
     @staticmethod
     @_amp_fwd
@@ -237,22 +273,33 @@ class VoxelProject(torch.autograd.Function):
         L.check(lib.vfd_voxel_project_fwd(ctypes.byref(d), vox.data_ptr(), invK.data_ptr(), E.data_ptr(),
                                           out.data_ptr(), L.stream()), 'voxel_project_fwd')
         ctx.space, ctx.shape = space, (B, N, V, Cv)
-        ctx.save_for_backward(invK, E)
+        ctx.plan = ctx.side = None
+        if ctx.needs_input_grad[1]:
+            nbytes = lib.vfd_voxel_project_plan_bytes(ctypes.byref(d))
+            main, side = torch.cuda.current_stream(vox.device), _side_stream(vox.device)
+            side.wait_stream(main)                  # invK / E are ready
+            with torch.cuda.stream(side):
+                plan = torch.empty(nbytes, dtype=torch.uint8, device=vox.device)
+                L.check(lib.vfd_voxel_project_plan(ctypes.byref(d), invK.data_ptr(), E.data_ptr(), plan.data_ptr(),
+                                                   nbytes, L.stream()), 'voxel_project_plan')
+            plan.record_stream(main)                # consumed on the main stream by the backward
+            invK.record_stream(side)
+            E.record_stream(side)
+            ctx.plan, ctx.side = plan, side
         return out
 
     @staticmethod
     @_amp_bwd
     def backward(ctx, g):
         lib = L.load()
-        invK, E = ctx.saved_tensors
         B, N, V, Cv = ctx.shape
         g = _channels_last(g, 'grad')
         dvox = torch.empty(B, V, Cv, device=g.device)
         d = ctx.space.desc(B, N, Cv=Cv)
-        nbytes = lib.vfd_voxel_project_bwd_workspace(ctypes.byref(d))
-        ws = torch.empty(nbytes, dtype=torch.uint8, device=g.device)
-        L.check(lib.vfd_voxel_project_bwd(ctypes.byref(d), g.data_ptr(), invK.data_ptr(), E.data_ptr(),
-                                          dvox.data_ptr(), ws.data_ptr(), nbytes, L.stream()), 'voxel_project_bwd')
+        torch.cuda.current_stream(g.device).wait_stream(ctx.side)
+        L.check(lib.vfd_voxel_project_bwd_planned(ctypes.byref(d), g.data_ptr(), ctx.plan.data_ptr(),
+                                                  ctx.plan.numel(), dvox.data_ptr(), L.stream()), 'voxel_project_bwd')
+        ctx.plan = None
         return None, dvox, None, None
 
 

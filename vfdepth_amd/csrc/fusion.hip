@@ -395,6 +395,35 @@ __global__ __launch_bounds__(256) void fuse_depth_bwd_k(vfd_voxel_desc d, const 
     }
     const int twoCv = 2 * d.Cv;
     const int nvox = min(64, V - v0);
+    // Run merging: consecutive voxels of the walk whose camera slot hits the same (camera, base
+    // pixel, column half, in-range corners) add their weighted gradients in registers; a run
+    // issues one row of atomics per in-range corner instead of one per voxel.
+    float racc[2][4][CPL];
+    int rkey[2] = {-1, -1};          // wave-uniform run keys per camera slot
+    unsigned rin[2] = {0u, 0u};
+    float* rrow[2] = {dP, dP};
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) racc[s][q][k] = 0.f;
+    auto flush = [&](int s) {
+      if (rkey[s] < 0) return;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (rin[s] >> q & 1u) {
+          float* row = rrow[s] + (size_t)tap_offset(q, d.w) * twoCv;
+#pragma unroll
+          for (int k = 0; k < CPL; ++k) {
+            int ch = lane + 64 * k;
+            if (ch < d.Cv) atomicAdd(row + ch, racc[s][q][k]);
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) racc[s][q][k] = 0.f;
+      }
+    };
     for (int j = 0; j < nvox; ++j) {
       const int cj = rdl(cnt, j);
       if (cj != 1 && cj != 2) continue;
@@ -419,17 +448,18 @@ __global__ __launch_bounds__(256) void fuse_depth_bwd_k(vfd_voxel_desc d, const 
         const int base = rdl(tl.base, j);
         const unsigned in = rdlu(tl.in, j);
         const float zt = rdlf(tl.z, j);
-        float* Pc = dP + (size_t)(b * d.N + cam) * hw * twoCv + off;
+        const int key = ((base * 16 + (int)in) * 2 + (cj == 1 ? 0 : 1)) * 8 + cam;
+        if (key != rkey[s]) {
+          flush(s);
+          rkey[s] = key;
+          rin[s] = in;
+          rrow[s] = dP + ((size_t)(b * d.N + cam) * hw + base) * twoCv + off;
+        }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          if (!(in >> q & 1u)) continue;
           const float wq = rdlf(tl.w[q], j);
-          float* row = Pc + (size_t)(base + tap_offset(q, d.w)) * twoCv;
 #pragma unroll
-          for (int k = 0; k < CPL; ++k) {
-            int ch = lane + 64 * k;
-            if (ch < d.Cv) atomicAdd(row + ch, wq * dpre[k]);
-          }
+          for (int k = 0; k < CPL; ++k) racc[s][q][k] += wq * dpre[k];
         }
         const int zrow = (cj == 1) ? 0 : 1 + d.group[cam];
         const float zf = zt / d.z_scale;
@@ -443,6 +473,8 @@ __global__ __launch_bounds__(256) void fuse_depth_bwd_k(vfd_voxel_desc d, const 
         }
       }
     }
+    flush(0);
+    flush(1);
   }
   if (v0 < V) {
 #pragma unroll

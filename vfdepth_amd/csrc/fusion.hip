@@ -395,11 +395,12 @@ __global__ __launch_bounds__(256) void fuse_depth_bwd_k(vfd_voxel_desc d, const 
     }
     const int twoCv = 2 * d.Cv;
     const int nvox = min(64, V - v0);
-    // Run merging: consecutive voxels of the walk whose camera slot hits the same (camera, base
-    // pixel, column half, in-range corners) add their weighted gradients in registers; a run
-    // issues one row of atomics per in-range corner instead of one per voxel.
+    // Run merging: consecutive voxels of the walk whose camera slot hits the same (camera, column
+    // half) footprint, or one shifted by one pixel along the row, add their weighted gradients in
+    // registers; atomics are issued only for tap rows that leave the footprint.
     float racc[2][4][CPL];
-    int rkey[2] = {-1, -1};          // wave-uniform run keys per camera slot
+    int rside[2] = {-1, -1};         // wave-uniform run state per camera slot: (column half, camera),
+    int rbase[2] = {0, 0};           // -1 = no open run; base pixel (may be negative at the border)
     unsigned rin[2] = {0u, 0u};
     float* rrow[2] = {dP, dP};
 #pragma unroll
@@ -408,8 +409,23 @@ __global__ __launch_bounds__(256) void fuse_depth_bwd_k(vfd_voxel_desc d, const 
       for (int q = 0; q < 4; ++q)
 #pragma unroll
         for (int k = 0; k < CPL; ++k) racc[s][q][k] = 0.f;
+    // flush one tap column (0: corners 0/2, 1: corners 1/3) of slot s
+    auto flush_col = [&](int s, int col) {
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const int q = col + 2 * r;
+        if (rin[s] >> q & 1u) {
+          float* row = rrow[s] + (size_t)tap_offset(q, d.w) * twoCv;
+#pragma unroll
+          for (int k = 0; k < CPL; ++k) {
+            int ch = lane + 64 * k;
+            if (ch < d.Cv) atomicAdd(row + ch, racc[s][q][k]);
+          }
+        }
+      }
+    };
     auto flush = [&](int s) {
-      if (rkey[s] < 0) return;
+      if (rside[s] < 0) return;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         if (rin[s] >> q & 1u) {
@@ -448,13 +464,40 @@ __global__ __launch_bounds__(256) void fuse_depth_bwd_k(vfd_voxel_desc d, const 
         const int base = rdl(tl.base, j);
         const unsigned in = rdlu(tl.in, j);
         const float zt = rdlf(tl.z, j);
-        const int key = ((base * 16 + (int)in) * 2 + (cj == 1 ? 0 : 1)) * 8 + cam;
-        if (key != rkey[s]) {
+        // run key: (camera, column half) + base pixel; a base one pixel to the right / left keeps
+        // the shared tap column in registers (flush only the column that leaves the footprint)
+        const int side = (cj == 1 ? 0 : 1) * 8 + cam;
+        const int rb = rbase[s], rs = rside[s];
+        const unsigned ri = rin[s];
+        // a retained column keeps its accumulators only if its in-range bits agree (a base can
+        // name two pixels at the row ends: x0 = -1 of row y0 and x0 = w-1 of row y0-1)
+        if (side == rs && base == rb + 1 && ((ri >> 1) & 5u) == (in & 5u)) {
+          flush_col(s, 0);
+#pragma unroll
+          for (int k = 0; k < CPL; ++k) {
+            racc[s][0][k] = racc[s][1][k];
+            racc[s][2][k] = racc[s][3][k];
+            racc[s][1][k] = 0.f;
+            racc[s][3][k] = 0.f;
+          }
+        } else if (side == rs && base == rb - 1 && (ri & 5u) == ((in >> 1) & 5u)) {
+          flush_col(s, 1);
+#pragma unroll
+          for (int k = 0; k < CPL; ++k) {
+            racc[s][1][k] = racc[s][0][k];
+            racc[s][3][k] = racc[s][2][k];
+            racc[s][0][k] = 0.f;
+            racc[s][2][k] = 0.f;
+          }
+        } else if (!(side == rs && base == rb && ri == in)) {
           flush(s);
-          rkey[s] = key;
-          rin[s] = in;
-          rrow[s] = dP + ((size_t)(b * d.N + cam) * hw + base) * twoCv + off;
         }
+        // the new footprint's in-range bits describe every accumulator (checked above for the
+        // retained column; the other column starts at zero)
+        rside[s] = side;
+        rbase[s] = base;
+        rin[s] = in;
+        rrow[s] = dP + ((size_t)(b * d.N + cam) * hw + base) * twoCv + off;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const float wq = rdlf(tl.w[q], j);
@@ -1014,10 +1057,14 @@ constexpr int PBW_U = VFD_PBW_U;       // voxel rows (1 KB each) in flight per w
 // Reflect-pad fold of the pose output's gradient: a voxel with xi in {1, X-2} or yi in {1, Y-2}
 // has copies in the padded map; their sum goes to a compact buffer (row = (b * nslot + slot) * Z
 // + z, C + 1 floats), so the backward's row reads carry no data-dependent extra loads.
+// grid = B * nslot * POSE_FOLD_SPLIT: each slot's Z * (C + 1) floats are split over
+// POSE_FOLD_SPLIT workgroups (a slot per workgroup leaves 400 workgroups on 256 CUs, latency-bound)
+constexpr int POSE_FOLD_SPLIT = 4;
 __global__ __launch_bounds__(256) void pose_fold_k(vfd_voxel_desc d, const float* __restrict__ dout,
-                                                   float* __restrict__ fb) {
+                                                   float* __restrict__ fb, int aligned16) {
   const int nslot = 2 * (d.X + d.Y);
-  const int slot = blockIdx.x % nslot, b = blockIdx.x / nslot;
+  const int part = blockIdx.x % POSE_FOLD_SPLIT, sb = blockIdx.x / POSE_FOLD_SPLIT;
+  const int slot = sb % nslot, b = sb / nslot;
   int xi, yi;
   if (slot < d.X) { xi = slot; yi = 1; }
   else if (slot < 2 * d.X) { xi = slot - d.X; yi = d.Y - 2; }
@@ -1035,8 +1082,25 @@ __global__ __launch_bounds__(256) void pose_fold_k(vfd_voxel_desc d, const float
   const float* p3 = gb + ((size_t)max(ey, 0) * Xo + max(ex, 0)) * n;
   const float f1 = ex >= 0 ? 1.f : 0.f, f2 = ey >= 0 ? 1.f : 0.f, f3 = f1 * f2;
   float* dst = fb + ((size_t)b * nslot + slot) * n;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    // ((primary + x-copy) + y-copy) + xy-copy, absent copies weighted 0 (loads stay in range)
+  // ((primary + x-copy) + y-copy) + xy-copy, absent copies weighted 0 (loads stay in range)
+  if ((n & 3) == 0 && aligned16) {          // rows start 16-B aligned: float4 lanes
+    const int n4 = n >> 2, c4 = (n4 + POSE_FOLD_SPLIT - 1) / POSE_FOLD_SPLIT;
+    const int e4 = min(n4, (part + 1) * c4);
+    const float4 *q0 = reinterpret_cast<const float4*>(p0), *q1 = reinterpret_cast<const float4*>(p1);
+    const float4 *q2 = reinterpret_cast<const float4*>(p2), *q3 = reinterpret_cast<const float4*>(p3);
+    for (int i = part * c4 + threadIdx.x; i < e4; i += blockDim.x) {
+      const float4 a = q0[i], bx = q1[i], by = q2[i], bxy = q3[i];
+      float4 r;
+      r.x = ((a.x + f1 * bx.x) + f2 * by.x) + f3 * bxy.x;
+      r.y = ((a.y + f1 * bx.y) + f2 * by.y) + f3 * bxy.y;
+      r.z = ((a.z + f1 * bx.z) + f2 * by.z) + f3 * bxy.z;
+      r.w = ((a.w + f1 * bx.w) + f2 * by.w) + f3 * bxy.w;
+      reinterpret_cast<float4*>(dst)[i] = r;
+    }
+    return;
+  }
+  const int cn = (n + POSE_FOLD_SPLIT - 1) / POSE_FOLD_SPLIT, e = min(n, (part + 1) * cn);
+  for (int i = part * cn + threadIdx.x; i < e; i += blockDim.x) {
     float s = p0[i];
     s += f1 * p1[i];
     s += f2 * p2[i];
@@ -2135,7 +2199,8 @@ int vfd_fuse_pose_bwd(const vfd_voxel_desc* d, const void* plan, const int* coun
   float* fbuf = (float*)((char*)ctrl + 256);                   // folded border rows (plan scratch)
   float* pool = (float*)((char*)fbuf + plan_fold_bytes(d));    // split tiles' partials
   ProfScope ps(K_FUSE_POSE_BWD, s);
-  if (d->pad_out) pose_fold_k<<<d->B * 2 * (d->X + d->Y), 256, 0, s>>>(*d, d_out, fbuf);
+  if (d->pad_out) pose_fold_k<<<d->B * 2 * (d->X + d->Y) * POSE_FOLD_SPLIT, 256, 0, s>>>(
+      *d, d_out, fbuf, (((uintptr_t)d_out | (uintptr_t)fbuf) & 15) == 0);
   const int ntask_max = host_tiles(d) * d->B * d->N + PBW_POOL;
   fuse_pose_bwd_k<<<ntask_max, 64, 0, s>>>(*d, tasks, ctrl, csr, d_out, fbuf, pool, d_feats);
   pose_combine_k<<<std::min(PBW_POOL / 2, host_tiles(d) * d->B * d->N), 256, 0, s>>>(*d, combos, ctrl, pool, d_feats);

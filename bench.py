@@ -138,7 +138,14 @@ def cpu_baseline(cfg, seconds_budget=60.0):
     losses['total_loss'].backward()
     opt.step()
     dt = time.perf_counter() - t0
+    cpu_model = ''
+    try:
+        with open('/proc/cpuinfo') as fh:
+            cpu_model = next((l.split(':', 1)[1].strip() for l in fh if l.startswith('model name')), '')
+    except OSError:
+        pass
     return {'value': 1.0 / dt, 'unit': 'iters/s', 'cores': threads, 'kind': 'port',
+            'cpu_model': cpu_model, 'torch_threads': torch.get_num_threads(),
             'sample': f'1 full step (fwd+loss+bwd+Adam) of the oracle at the same config, B=1, '
                       f'{dt:.1f} s on {threads} host threads (torch CPU)'}
 

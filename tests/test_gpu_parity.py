@@ -664,3 +664,47 @@ def test_bf16_nets_step_tracks_fp32():
         assert torch.isfinite(g16[n]).all(), n
         cos = float(torch.nn.functional.cosine_similarity(g16[n].double(), g32[n].double(), dim=0))
         assert cos > 0.9, f'{n}: gradient cosine {cos:.3f} between the bf16 and fp32 steps'
+
+
+@pytest.mark.parametrize('config', [2, 4, 5])
+def test_fusion_adjoint_at_full_size(config):
+    """Size-independent property at BASELINE.json's full sizes (configs 2, 4, 5 at B=1), where the
+    oracle is too slow: K2 (pose fusion, affine in the features) and K3 (voxel -> frustum, linear)
+    backward kernels are the exact adjoints of their forward kernels,
+    <fwd(x) - fwd(0), g> == <x, bwd(g)>, reflect-pad copies and zero padding included.  Inner
+    products in fp64 over fp32 values; tolerance 1e-5 of sum |fwd(x) * g| (fp32 rounding of the
+    per-element sums in the two kernels)."""
+    import bench
+    from vfdepth_amd import kernels as KN
+    from vfdepth_amd import synth
+    from vfdepth_amd.geometry import inverse4x4
+    cfg, _ = bench.make_cfg(config, 1)
+    space = KN.VoxelSpace(cfg, DEV)
+    b = synth.make_batch(cfg, seed=3, device=DEV)
+    lvl = cfg['model']['fusion_level'] + 1
+    Einv = inverse4x4(b['extrinsics'])
+    mask_lo = KN.mask_lowres(space, b['mask'])
+    gen = torch.Generator(device=DEV).manual_seed(config)
+    C, Cv = cfg['model']['fusion_feat_in_dim'], cfg['model']['voxel_pre_dim'][-1]
+
+    def check(lhs_terms, rhs, what):
+        lhs = float(lhs_terms.double().sum())
+        scale = float(lhs_terms.double().abs().sum())
+        assert abs(lhs - rhs) <= 1e-5 * scale, f'{what}: <Ax, g> {lhs} vs <x, A^T g> {rhs} (scale {scale})'
+
+    # K2: features [B, N, C, h, w] -> padded pose volume (affine: the depth channel is constant)
+    plan = KN.FusionPlan(space, mask_lo, b['K', lvl], Einv)
+    feats = torch.randn(1, 6, C, space.h, space.w, device=DEV, generator=gen, requires_grad=True)
+    out = KN.FusePose.apply(space, plan, feats)
+    with torch.no_grad():
+        out0 = KN.FusePose.apply(space, plan, torch.zeros_like(feats))
+    g = torch.randn(out.shape, device=DEV, generator=gen)
+    out.backward(g)
+    check((out.detach() - out0) * g, float((feats.detach().double() * feats.grad.double()).sum()), 'K2')
+    del out, out0, g, feats
+    # K3: voxels [B, V, Cv] -> frustum features (linear)
+    vox = torch.randn(1, space.V, Cv, device=DEV, generator=gen, requires_grad=True)
+    out = KN.VoxelProject.apply(space, vox, b['inv_K', lvl], b['extrinsics'])
+    g = torch.randn(out.shape, device=DEV, generator=gen).contiguous(memory_format=torch.channels_last)
+    out.backward(g)
+    check(out.detach() * g, float((vox.detach().double() * vox.grad.double()).sum()), 'K3')

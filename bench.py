@@ -88,22 +88,24 @@ def shapes(cfg):
 
 
 def algorithmic_bytes(kernel, s):
-    """Compulsory HBM bytes of ONE launch at the kernel's own boundary (fp32 = 4 B)."""
+    """Compulsory HBM bytes of ONE launch at the kernel's own boundary (fp32 = 4 B), with the
+    unpadded tensor sizes of SURVEY.md §8(d) (the reflect-pad halos the K2/K3 kernels also write
+    for the consumer convs are NOT counted: they are extra work, not algorithmic bytes)."""
     B, N, C, Cv, p, P = s['B'], s['N'], s['C'], s['Cv'], s['h'] * s['w'], s['H'] * s['W']
-    V, Z, Y, X, D, T, F = s['V'], s['Z'], s['Y'], s['X'], s['D'], s['T'], s['F']
-    pose_out = B * (C + 1) * Z * (Y + 2) * (X + 2)
-    proj_out = B * N * Cv * D * (s['h'] + 2) * (s['w'] + 2)
+    V, D, T, F = s['V'], s['D'], s['T'], s['F']
+    pose_out = B * (C + 1) * V                                    # [B, C+1, V] mean voxel features
+    proj_out = B * N * Cv * D * p                                 # [B*N, Cv*D, h, w] frustum features
     h, w = s['h'], s['w']
     agg_levels = (h // 2) * (w // 2) + (h // 4) * (w // 4)
     planes = {
         'mask_downsample': B * N * (P + p),
         'fusion_plan': B * N * p + B * V * 8,                     # mask in, ~one 32-B entry per voxel out
         'aggregate': B * N * C * (2 * p + agg_levels),
-        'fuse_depth_fwd': B * N * p * (2 * Cv + 1) + B * V * Cv,
+        'fuse_depth_fwd': B * N * p * (2 * Cv + 1) + B * V * Cv,  # folded maps + 1/8 mask in, voxels out
         'fuse_depth_bwd': 2 * B * V * Cv + B * N * p + B * N * p * 2 * Cv,
-        'fuse_pose_fwd': B * N * C * p + B * V * 8 + pose_out,
-        'fuse_pose_bwd': pose_out + B * V * 8 + B * N * C * p,
-        'voxel_project_fwd': B * V * Cv + proj_out,
+        'fuse_pose_fwd': B * N * C * p + B * N * p + pose_out,    # SURVEY §8(d) K2 per call
+        'fuse_pose_bwd': pose_out + B * N * C * p,
+        'voxel_project_fwd': B * V * Cv + proj_out,               # SURVEY §8(d) K3
         'voxel_project_bwd': proj_out + B * V * Cv,
         'voxel_project_plan': 4 * B * N * p * D,                  # one 16-B sorted entry per frustum sample
         'view_stats': B * N * P * (1 + 3 * (T + 1) + 1),
@@ -117,11 +119,22 @@ def algorithmic_bytes(kernel, s):
     return planes[kernel] * 4
 
 
-def cpu_baseline(cfg, seconds_budget=60.0):
-    """Oracle step (forward + losses + backward + Adam) on the host CPU, batch 1."""
+def cpu_threads():
+    """all cores of this process's affinity mask — capped by OMP_NUM_THREADS when
+    the host sets it (the GPU pool gives each 1-GPU job a 16-thread CPU share and exports
+    OMP_NUM_THREADS=16; `sched_getaffinity` there shows the whole machine)."""
+    aff = len(os.sched_getaffinity(0))
+    cap = os.environ.get('OMP_NUM_THREADS')
+    return (min(aff, int(cap)) if cap and cap.isdigit() and int(cap) > 0 else aff), aff
+
+
+def cpu_baseline(cfg, timed_steps=3, warmup_steps=1):
+    """The CPU oracle's training step (forward + losses + backward + Adam; oracle/vfd_oracle.py,
+    the reference's algorithm restated on torch CPU) at the per-GPU batch shape, B=1:
+    `warmup_steps` untimed + `timed_steps` timed (1 + 3 for config 2)."""
     from oracle import vfd_oracle as O
     from vfdepth_amd.network import FusedDepthNet, FusedPoseNet
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    threads, aff = cpu_threads()
     torch.set_num_threads(threads)
     dn, pn = FusedDepthNet(cfg), FusedPoseNet(cfg)
     dn.load_state_dict(seeded_state_dict(dn, seed=7))
@@ -132,12 +145,18 @@ def cpu_baseline(cfg, seconds_budget=60.0):
     N, T = cfg['data']['num_cams'], len(cfg['training']['frame_ids']) - 1
     H, W = cfg['training']['height'], cfg['training']['width']
     noise = [1e-5 * torch.randn(1, T, H, W) for _ in range(N)]
-    t0 = time.perf_counter()
-    opt.zero_grad(set_to_none=True)
-    _, losses = O.process_batch(nets, inputs, cfg, noise)
-    losses['total_loss'].backward()
-    opt.step()
-    dt = time.perf_counter() - t0
+    times = []
+    for i in range(warmup_steps + timed_steps):
+        t0 = time.perf_counter()
+        opt.zero_grad(set_to_none=True)
+        _, losses = O.process_batch(nets, inputs, cfg, noise)
+        losses['total_loss'].backward()
+        opt.step()
+        if i >= warmup_steps:
+            times.append(time.perf_counter() - t0)
+        print(f'[bench] cpu baseline step {i + 1}/{warmup_steps + timed_steps}: '
+              f'{time.perf_counter() - t0:.1f} s', file=sys.stderr, flush=True)
+    dt = sum(times) / len(times)
     cpu_model = ''
     try:
         with open('/proc/cpuinfo') as fh:
@@ -145,9 +164,52 @@ def cpu_baseline(cfg, seconds_budget=60.0):
     except OSError:
         pass
     return {'value': 1.0 / dt, 'unit': 'iters/s', 'cores': threads, 'kind': 'port',
-            'cpu_model': cpu_model, 'torch_threads': torch.get_num_threads(),
-            'sample': f'1 full step (fwd+loss+bwd+Adam) of the oracle at the same config, B=1, '
-                      f'{dt:.1f} s on {threads} host threads (torch CPU)'}
+            'cpu_model': cpu_model, 'torch_threads': torch.get_num_threads(), 'affinity_cores': aff,
+            'step_s': [round(t, 2) for t in times],
+            'sample': f'{warmup_steps} warm-up + {timed_steps} timed full steps (fwd+loss+bwd+Adam) of the '
+                      f'CPU oracle at the same config, B=1, mean {dt:.1f} s/step on {threads} threads '
+                      f'(torch CPU; affinity {aff} cores, capped by OMP_NUM_THREADS); the reference\'s '
+                      f'train.py:17-20 pins OMP/MKL to 1 thread'}
+
+
+def parity_check(device):
+    """BASELINE.md §3 'Reported: parity': one training step of the reduced 6-camera fusion
+    config (tests/golden/step_small.npz: the reference's own outputs on the same seeded weights,
+    inputs and identity noise) through the HIP path, compared with the reference: max |Δ| of the
+    depth maps and of every loss scalar, and the Abs.Rel / median-scaled metrics
+    (Logger.compute_depth_losses) against tests/golden/depth_metrics.npz."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, 'tests', 'golden'))
+    import common as G
+    from vfdepth_amd.vfdepth import VFDepthAlgo
+    gold = os.path.join(ROOT, 'tests', 'golden')
+    fx = np.load(os.path.join(gold, 'step_small.npz'))
+    fm = np.load(os.path.join(gold, 'depth_metrics.npz'))
+    cfg = G.step_cfg()
+    algo = VFDepthAlgo(cfg, device.index)
+    for m in algo.models.values():
+        m.load_state_dict(seeded_state_dict(m, seed=G.STEP_SEED))
+    algo.set_train()
+    inputs = synth.make_batch(cfg, seed=5, with_depth=True)
+    N = cfg['data']['num_cams']
+    noise = torch.stack([torch.tensor(fx[f'noise_c{c}']) for c in range(N)]).to(device)
+    outputs, losses = algo.process_batch(inputs, device.index, noise=noise)
+    losses['total_loss'].backward()
+    torch.cuda.synchronize()
+    d_depth = max(float((outputs[('cam', c)][('depth', 0)].cpu() - torch.tensor(fx[f'depth_c{c}'])).abs().max())
+                  for c in range(N))
+    rel_depth = max(float(((outputs[('cam', c)][('depth', 0)].cpu() - torch.tensor(fx[f'depth_c{c}'])).abs()
+                           / torch.tensor(fx[f'depth_c{c}']).abs()).max()) for c in range(N))
+    d_loss = {k[5:]: abs(float(losses[k[5:]]) - float(fx[k])) for k in fx.files if k.startswith('loss_')}
+    metric, median = algo.compute_depth_metrics(inputs, outputs)
+    absrel = {'metric': float(metric['abs_rel']), 'median': float(median['abs_rel']),
+              'ref_metric': float(fm['step_metric_abs_rel']), 'ref_median': float(fm['step_median_abs_rel'])}
+    return {'config': 'reduced 6-cam fusion step (96x160, voxels 40x40x10, D=16) vs the reference\'s outputs',
+            'max_abs_diff_depth': d_depth, 'max_rel_diff_depth': rel_depth,
+            'max_abs_diff_loss': max(d_loss.values()), 'loss_keys': len(d_loss),
+            'abs_rel': absrel,
+            'abs_rel_equal_1e-4': abs(absrel['metric'] - absrel['ref_metric']) <= 1e-4 * absrel['ref_metric']
+            and abs(absrel['median'] - absrel['ref_median']) <= 1e-4 * absrel['ref_median']}
 
 
 def load_traffic(config):
@@ -156,6 +218,20 @@ def load_traffic(config):
         with open(path) as fh:
             return json.load(fh)
     return {}
+
+
+def launch_ranks(n):
+    """Run this script on n ranks (torch.distributed.run, rendezvous on 127.0.0.1) as a child
+    process; return its exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={n}',
+           '--master-addr', '127.0.0.1', '--master-port', str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    print(f'[bench] launching {n} ranks: {" ".join(cmd)}', file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
 
 
 def main():
@@ -171,7 +247,14 @@ def main():
     ap.add_argument('--conv-autotune', type=int, default=0,
                     help='1: let MIOpen benchmark conv algorithms per shape (torch.backends.cudnn.benchmark)')
     ap.add_argument('--channels-last', type=int, default=0, help='1: NHWC memory format for the dense nets')
+    ap.add_argument('--cpu-steps', type=int, default=3, help='timed CPU-baseline steps (after 1 warm-up)')
+    ap.add_argument('--no-parity', action='store_true')
     args = ap.parse_args()
+    if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
+        # `bench.py --gpus N` on its own: one rank per GPU, launched like the reference's
+        # mp.spawn (train.py:59-61) — here torch.distributed.run as a CHILD process (this parent
+        # has not touched the GPU; it never execs), and its exit code is ours
+        return launch_ranks(args.gpus)
     faulthandler.enable()
     if os.environ.get('VFD_BENCH_TRACEBACK'):     # diagnostics: dump every thread's stack periodically
         faulthandler.dump_traceback_later(float(os.environ['VFD_BENCH_TRACEBACK']), repeat=True)
@@ -186,6 +269,8 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world != args.gpus:
+        raise SystemExit(f'bench.py --gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU')
     if world > 1:
         dist.init_process_group('nccl', init_method='env://')
     torch.cuda.set_device(local)
@@ -249,7 +334,7 @@ def main():
     elapsed = max_over_ranks(elapsed, world, f'cuda:{local}')
     if rank != 0:
         dist.destroy_process_group()
-        return
+        return 0
 
     s = shapes(cfg)
     dom = max(prof, key=lambda k: prof[k][1])
@@ -265,9 +350,15 @@ def main():
                   f'{ab / (t / n / 1e3) / 1e9:8.1f} GB/s alg  ({ab / 1e6:.1f} MB/launch)', file=sys.stderr)
         print(f'[bench] hot-path kernels {sum(t for _, t in prof.values()) / args.steps:.2f} ms/step of '
               f'{elapsed / args.steps * 1e3:.2f} ms/step; loss {float(losses["total_loss"]):.5f}', file=sys.stderr)
+    # aggregate over every hot-path op of the step (per-kernel and aggregate)
+    agg_bytes = sum(algorithmic_bytes(k, s) * n for k, (n, _) in prof.items())
+    agg_s = sum(t for _, t in prof.values()) / 1e3
+    parity = None
+    if not args.no_parity:
+        parity = parity_check(torch.device(f'cuda:{local}'))
     base = None
     if world == 1 and not args.no_cpu_baseline:
-        base = cpu_baseline(cfg)
+        base = cpu_baseline(cfg, timed_steps=args.cpu_steps)
     out = {
         'metric': '6-cam 384x640 train iters/sec (DDAD-shaped, volumetric fusion)',
         'value': job_throughput(elapsed, args.steps, world),
@@ -279,7 +370,7 @@ def main():
         'higher_is_better': True,
         'scaling': 'weak',
         'vs_baseline': None,
-        'dtype': 'fp32',
+        'dtype': 'fp32' if cfg['training']['net_precision'] == 'fp32' else 'bf16 dense nets, fp32 hot-path kernels',
         'data': 'synthetic DDAD-shaped batches (seeded), seeded random-init weights',
         'config': {'workload': name, 'config_id': args.config, 'batch_per_gpu': s['B'], 'cameras': s['N'],
                    'image': [s['H'], s['W']], 'voxels': [s['X'], s['Y'], s['Z']], 'depth_bins': s['D'],
@@ -287,15 +378,22 @@ def main():
         'roofline': {'kernel': dom, 'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic, 'alg_bytes_per_launch': alg,
                      'avg_launch_us': avg_s * 1e6, 'launches': n_launch},
+        'roofline_aggregate': {'bound': 'hbm', 'achieved': agg_bytes / agg_s / 1e9, 'peak': HBM_PEAK_GBS,
+                               'unit': 'GB/s', 'frac': agg_bytes / agg_s / 1e9 / HBM_PEAK_GBS,
+                               'alg_bytes_per_step': agg_bytes / args.steps,
+                               'kernel_ms_per_step': agg_s * 1e3 / args.steps,
+                               'what': 'every hot-path op of the step (K1-K5, plans, aggregation)'},
         'hot_path_ms_per_step': sum(t for _, t in prof.values()) / args.steps,
         'execution': 'hip-graph replay of the whole step' if use_graph else 'eager',
+        'parity': parity,
         'cpu_baseline': base,
     }
     done.set()
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == '__main__':
-    main()
+    sys.exit(main())

@@ -86,6 +86,31 @@ def view_case(skip_sample=False):
     return cfg, batch, depth, poses
 
 
+def view_case_cfg(cfg, seed):
+    """view_case at any configuration (full BASELINE sizes): batch with a fractional mask row,
+    ground-plane depth x U(0.8, 1.2), small random per-camera motions."""
+    t = cfg['training']
+    B, N, H, W = t['batch_size'], cfg['data']['num_cams'], t['height'], t['width']
+    gen = torch.Generator().manual_seed(seed)
+    batch = synth.make_batch(cfg, seed=seed)
+    batch['extrinsics_inv'] = torch.inverse(batch['extrinsics'])
+    gt = synth.ground_plane_depth(synth.rig_intrinsics(N, H, W), synth.rig_extrinsics(N), H, W, 1.5, 60.0)
+    depth = gt.unsqueeze(0).repeat(B, 1, 1, 1, 1) * (0.8 + 0.4 * torch.rand(B, N, 1, H, W, generator=gen))
+    batch['mask'] = random_mask(gen, (B, N, 1, H, W))
+    poses = {}
+    for f in t['frame_ids'][1:]:
+        aa = 0.02 * torch.randn(B, 1, 3, generator=gen)
+        tr = 0.5 * torch.randn(B, 1, 3, generator=gen)
+        T = torch.eye(4).repeat(B, 1, 1)
+        T[:, :3, :3] = axis_angle_to_matrix(aa)[:, 0]
+        T[:, :3, 3] = tr[:, 0]
+        for c in range(N):
+            Tc = T.clone()
+            Tc[:, :3, 3] += 0.05 * c
+            poses[(c, f)] = Tc
+    return batch, depth, poses
+
+
 VIEW_IMG_KEYS = [('color', -1, 0), ('color', 1, 0), ('overlap', 0, 0), ('overlap', -1, 0), ('overlap', 1, 0)]
 VIEW_MSK_KEYS = [('color_mask', -1, 0), ('color_mask', 1, 0), ('overlap_mask', 0, 0),
                  ('overlap_mask', -1, 0), ('overlap_mask', 1, 0)]
@@ -120,6 +145,27 @@ def loss_case():
             planes[(c, 'overlap_mask', f, 0)] = m
         planes[(c, 'disp', 0)] = 0.2 + 0.6 * torch.rand(B, 1, H, W, generator=gen)
     return cfg, batch, planes
+
+
+# ------------------------------------------------------------------------------------ depth metrics
+def depth_metric_case():
+    """(cfg, inputs, outputs) for Logger.compute_depth_losses: 6 cameras, B=2, GT 48x80 with
+    lidar holes (0) and far returns, fractional mask, predictions at 96x160."""
+    B, N, h, w = 2, 6, 48, 80
+    cfg = C.surround_fusion_cfg(height=2 * h, width=2 * w, batch_size=B)
+    gen = torch.Generator().manual_seed(41)
+    K0 = synth.rig_intrinsics(N, h, w)
+    gt = synth.ground_plane_depth(K0, synth.rig_extrinsics(N), h, w, 1.5, 250.0)
+    gt = gt.unsqueeze(0).repeat(B, 1, 1, 1, 1)
+    gt = gt * (torch.rand(B, N, 1, h, w, generator=gen) > 0.1).float()          # lidar holes
+    mask = torch.ones(B, N, 1, h, w)
+    mask[..., int(h * 0.85):, :] = 0.0
+    mask[..., int(h * 0.85) - 1, :] = torch.rand(B, N, 1, w, generator=gen)      # antialiased row
+    pred = torch.nn.functional.interpolate(gt.clamp(min=1.0).flatten(0, 1), [2 * h, 2 * w], mode='nearest')
+    pred = pred.view(B, N, 1, 2 * h, 2 * w) * (0.6 + 0.8 * torch.rand(B, N, 1, 2 * h, 2 * w, generator=gen))
+    inputs = {'depth': gt, 'mask': mask}
+    outputs = {('cam', c): {('depth', 0): pred[:, c].contiguous()} for c in range(N)}
+    return cfg, inputs, outputs
 
 
 # ------------------------------------------------------------------------------------ full step

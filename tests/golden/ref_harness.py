@@ -49,7 +49,7 @@ def available():
 
 def load():
     """Return a namespace with the reference classes/functions needed for fixtures."""
-    if _LOADED:
+    if 'ns' in _LOADED:
         return _LOADED['ns']
     from vfdepth_amd import layers as L
     from vfdepth_amd import rotation as R
@@ -111,6 +111,42 @@ def load():
                                fusion_depthnet=fus_d, fusion_posenet=fus_p)
     _LOADED['ns'] = ns
     return ns
+
+
+def load_logger():
+    """The reference's `utils/logger.py` module (for `Logger.compute_depth_losses`, logger.py:193-247).
+
+    Loaded under a synthetic package `ref_utils` rooted at the reference's `utils/` (its relative
+    imports `.visualize` / `.misc` resolve there); `tensorboardX` is not installed, so a stand-in
+    module with an inert `SummaryWriter` is registered first (no writer is ever constructed)."""
+    if 'logger' in _LOADED:
+        return _LOADED['logger']
+    tbx = _register('tensorboardX', types.ModuleType('tensorboardX'))
+
+    class SummaryWriter:            # never instantiated: compute_depth_losses does not log
+        def __init__(self, *a, **k):
+            raise RuntimeError('tensorboardX stand-in')
+    tbx.SummaryWriter = SummaryWriter
+    _pkg('ref_utils', os.path.join(REF, 'utils'))
+    _load('ref_utils.misc', 'utils/misc.py')
+    _load('ref_utils.visualize', 'utils/visualize.py')
+    mod = _load('ref_utils.logger', 'utils/logger.py')
+    _LOADED['logger'] = mod
+    return mod
+
+
+def reference_depth_losses(cfg, inputs, outputs):
+    """`Logger(cfg, use_tb=False).compute_depth_losses(inputs, outputs)` of the reference, with
+    the log directory redirected to a temporary one (the constructor creates it)."""
+    import copy
+    import tempfile
+    lg = load_logger()
+    cfg = copy.deepcopy(cfg)
+    with tempfile.TemporaryDirectory() as tmp:
+        cfg['data']['log_path'] = tmp
+        cfg['eval']['eval_visualize'] = False
+        logger = lg.Logger(cfg, use_tb=False)
+        return logger.compute_depth_losses(inputs, outputs)
 
 
 def build_algo(cfg):

@@ -1,0 +1,407 @@
+"""GPU parity at BASELINE.json's FULL sizes against the CPU oracle (configs 2-5).
+
+The golden fixtures (test_gpu_parity.py) pin every kernel against the reference's own outputs at
+reduced sizes; here the same kernels run at the shapes the bench measures — 6 cameras at
+384x640 (config 2/3), 352x640 (config 4), the 100x100x20 and 200x200x20 voxel grids with C=256 /
+Cv=64 / D=50 — and are compared with the oracle (oracle/vfd_oracle.py, itself pinned by those
+fixtures) on identical inputs:
+
+* K4 view synthesis + K5 photometric losses, forward and backward, all six cameras;
+* K1 depth fusion forward (+ backward at config 2), K2 pose fusion and K3 voxel->frustum forward;
+* a config-3 step (B=2 per GPU) with fp32 nets against the oracle's whole step, and with bf16
+  nets, where every hot-path op's output is checked against the oracle on that op's own inputs.
+
+Tolerance (north_star): fp32 per-pixel |a-b| <= 1e-4 + 1e-4|b|; gradients max |a-b| <= 2e-4 max|b|,
+away from the loss's discrete decisions (argmin auto-mask, temporal min, spatio-temporal min), which
+the fp32 GPU and CPU evaluations may resolve differently within 1e-5 of a tie.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import common as G
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device('cuda:0')
+
+
+@pytest.fixture(scope='module', autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip('no HIP device')
+    from vfdepth_amd import _lib
+    _lib.load()
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+
+
+def close(a, b, what, atol=1e-4, rtol=1e-4, where=None):
+    a = a.detach().float().cpu() if torch.is_tensor(a) else torch.as_tensor(a)
+    b = b.detach().float().cpu() if torch.is_tensor(b) else torch.as_tensor(b)
+    assert a.shape == b.shape, f'{what}: shape {tuple(a.shape)} vs {tuple(b.shape)}'
+    err = (a.double() - b.double()).abs()
+    bad = err > atol + rtol * b.double().abs()
+    if where is not None:
+        bad &= where
+    assert not bool(bad.any()), f'{what}: {int(bad.sum())}/{bad.numel()} off, max err {float(err.max()):.3g}'
+
+
+def gclose(a, b, what, rel=2e-4, where=None):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    assert a.shape == b.shape, f'{what}: shape {tuple(a.shape)} vs {tuple(b.shape)}'
+    if where is not None:
+        a, b = a[where], b[where]
+    scale = max(float(b.abs().max()), 1e-12)
+    err = float((a - b).abs().max()) / scale
+    assert err < rel, f'{what}: max rel err {err:.3g} (scale {scale:.3g})'
+
+
+def full_cfg(config, batch=1):
+    import bench
+    cfg, _ = bench.make_cfg(config, batch)
+    return cfg
+
+
+def to_dev(d):
+    return {k: (v.to(DEV) if torch.is_tensor(v) else v) for k, v in d.items()}
+
+
+# ------------------------------------------------------------------------------------ K4 + K5
+def _near_decisions(O, target, planes, idents, noise, frames, margin=1e-5):
+    """[B,1,H,W] pixels within `margin` of one of the loss's discrete decisions (temporal min,
+    auto-mask argmin, spatio-temporal min), dilated by the 3x3 SSIM window."""
+    rep = torch.cat([O.photometric(planes[('color', f, 0)], target) for f in frames[1:]], 1)
+    idn = torch.cat([O.photometric(i, target) for i in idents], 1) + noise
+    st = torch.cat([O.photometric(planes[('overlap', f, 0)], target) for f in frames[1:]], 1)
+
+    def tie(m):
+        return m < margin
+    near = tie(rep.max(1, keepdim=True).values - rep.min(1, keepdim=True).values)
+    near |= tie((rep.min(1, keepdim=True).values - idn.min(1, keepdim=True).values).abs())
+    near |= tie(st.max(1, keepdim=True).values - st.min(1, keepdim=True).values)
+    return F.max_pool2d(near.float(), 3, 1, 1) > 0
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize('config', [2, 4])
+def test_view_synthesis_and_losses_full_size(config):
+    """K4 (Projection + get_virtual_image + intensity alignment + overlap sums, every warp of
+    all six cameras) and K5 (SSIM/photometric, auto-mask, masked means, spatial and
+    spatio-temporal terms, smoothness) at 384x640 / 352x640, forward and backward, against the
+    oracle (view_rendering.py:118-243, loss_util.py:6-78, multi_cam_loss.py:16-138)."""
+    from oracle import vfd_oracle as O
+    from vfdepth_amd.geometry import Pose, ViewRendering
+    from vfdepth_amd.losses import MultiCamLoss
+    cfg = full_cfg(config)
+    t = cfg['training']
+    N, frames, H, W = cfg['data']['num_cams'], t['frame_ids'], t['height'], t['width']
+    batch, depth, poses = G.view_case_cfg(cfg, seed=60 + config)
+    keys = G.VIEW_IMG_KEYS
+    # ---- K4, oracle
+    d_leaf = depth.clone().requires_grad_(True)
+    T_leaf = {k: v.clone().requires_grad_(True) for k, v in poses.items()}
+    ref = {}
+    loss = 0.0
+    for c in range(N):
+        co = {('depth', 0): d_leaf[:, c]}
+        for f in frames[1:]:
+            co[('cam_T_cam', 0, f)] = T_leaf[(c, f)]
+        O.view_rendering(batch, co, c, O.relative_poses(batch, co, c, cfg), cfg)
+        ref[c] = co
+        for i, k in enumerate(keys):
+            loss = loss + (co[k] * G.seeded_randn(co[k].shape, 700 + 10 * c + i)).sum()
+    loss.backward()
+    # ---- K4, product
+    bd = to_dev(batch)
+    vr, pose = ViewRendering(cfg, 0), Pose(cfg)
+    d = depth.to(DEV).requires_grad_(True)
+    Ts = {k: v.to(DEV).requires_grad_(True) for k, v in poses.items()}
+    outputs = {('cam', c): {} for c in range(N)}
+    for c in range(N):
+        for f in frames[1:]:
+            outputs[('cam', c)][('cam_T_cam', 0, f)] = Ts[(c, f)]
+    rel = {c: pose.compute_relative_cam_poses(bd, outputs, c) for c in range(N)}
+    vr.render_all(bd, outputs, rel, {0: d[:, :, 0]})
+    gloss = 0.0
+    for c in range(N):
+        out = outputs[('cam', c)]
+        for i, k in enumerate(keys):
+            close(out[k], ref[c][k], f'{k} cam {c}')
+            gloss = gloss + (out[k] * G.seeded_randn(out[k].shape, 700 + 10 * c + i).to(DEV)).sum()
+        for k in G.VIEW_MSK_KEYS:
+            close(out[k], ref[c][k], f'{k} cam {c}', atol=0, rtol=0)
+    gloss.backward()
+    for c in range(N):
+        gclose(d.grad[:, c], d_leaf.grad[:, c], f'd depth cam {c}')
+        for f in frames[1:]:
+            gclose(Ts[(c, f)].grad, T_leaf[(c, f)].grad, f'd T{f} cam {c}', rel=1e-3)
+    del d, Ts, outputs, gloss
+    # ---- K5 on the oracle's planes (identical inputs on both sides)
+    B = depth.shape[0]
+    gen = torch.Generator().manual_seed(80 + config)
+    disp = 0.2 + 0.6 * F.avg_pool2d(torch.rand(B * N, 1, H, W, generator=gen), 9, 1, 4).view(B, N, H, W)
+    noise = 1e-5 * torch.randn(N, B, len(frames) - 1, H, W, generator=gen)
+    planes = {c: {k: ref[c][k].detach().clone() for k in keys} for c in range(N)}
+    omask = {c: {f: ref[c][('overlap_mask', f, 0)].detach().clone() for f in frames} for c in range(N)}
+    leaves = {c: {k: planes[c][k].clone().requires_grad_(True) for k in keys} for c in range(N)}
+    disp_leaf = disp.clone().requires_grad_(True)
+    total, terms = 0.0, {}
+    for c in range(N):
+        co = dict(leaves[c])
+        for f in frames:
+            co[('overlap_mask', f, 0)] = omask[c][f].clone()
+        co[('disp', 0)] = disp_leaf[:, c:c + 1]
+        cl, tm = O.cam_loss(batch, co, c, cfg, noise[c])
+        total = total + cl
+        for k, v in tm.items():
+            terms.setdefault(k, []).append(float(v))
+    total = total / N
+    total.backward()
+    loss_fn = MultiCamLoss(cfg, 0)
+    T_, F_ = len(frames) - 1, len(frames)
+    color = torch.stack([torch.stack([planes[c][k] for k in keys[:T_]], 1) for c in range(N)], 1)
+    ovl = torch.stack([torch.stack([planes[c][k] for k in keys[T_:]], 1) for c in range(N)], 1)
+    om = torch.stack([torch.stack([omask[c][f][:, 0] for f in frames], 1) for c in range(N)], 1)
+    color, ovl, gd = (x.to(DEV).requires_grad_(True) for x in (color, ovl, disp))
+    outputs = {('cam', c): {} for c in range(N)}
+    gt, logs = loss_fn.forward_all(bd, outputs, {0: (color, None, ovl, om.to(DEV))}, {0: gd}, {0: 1.0 / gd.detach()},
+                                   noise=noise.to(DEV))
+    close(gt, total, 'total loss')
+    for k in ('reproj_loss', 'spatio_loss', 'spatio_tempo_loss', 'smooth'):
+        close(logs[k], np.mean(terms[k]), k)
+    gt.backward()
+    for c in range(N):
+        keep = ~_near_decisions(O, batch[('color', 0, 0)][:, c], planes[c],
+                                [batch[('color', f, 0)][:, c] for f in frames[1:]], noise[c], frames)
+        n_near = int((~keep).sum())
+        assert n_near < 0.01 * keep.numel(), f'cam {c}: {n_near} px near a decision'
+        for i, k in enumerate(keys):
+            g = color.grad[:, c, i] if i < T_ else ovl.grad[:, c, i - T_]
+            gclose(g, leaves[c][k].grad, f'd {k} cam {c}', where=keep.expand_as(g))
+        gclose(gd.grad[:, c:c + 1], disp_leaf.grad[:, c:c + 1], f'd disp cam {c}', where=keep)
+
+
+# ------------------------------------------------------------------------------------ K1 / K2 / K3
+def _fusion_inputs(cfg, seed):
+    from vfdepth_amd import synth
+    batch = synth.make_batch(cfg, seed=seed)
+    lvl = int(cfg['model']['fusion_level']) + 1
+    gen = torch.Generator().manual_seed(seed)
+    batch['mask'] = G.random_mask(gen, tuple(batch['mask'].shape))
+    Einv = torch.inverse(batch['extrinsics'])
+    return batch, lvl, Einv
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize('config', [2, 5])
+def test_fuse_depth_full_size(config):
+    """K1 (depth-mode backproject_into_voxel + the overlap / non-overlap 1x1 MLPs,
+    volumetric_fusionnet.py:116-230) on the full grid: 100x100x20 (config 2) and 200x200x20
+    (config 5), C=256 -> Cv=64, forward against the oracle; backward too at config 2."""
+    from oracle import vfd_oracle as O
+    from vfdepth_amd.fusion import VFNet
+    from vfdepth_amd.layers import seeded_state_dict
+    cfg = full_cfg(config)
+    spec = O.VoxelSpec(cfg)
+    batch, lvl, Einv = _fusion_inputs(cfg, 90 + config)
+    C = int(cfg['model']['fusion_feat_in_dim'])
+    feats = G.seeded_randn((1, 6, C, spec.h, spec.w), 91 + config)
+    net = VFNet(cfg, C, 128, model='depth')
+    net.load_state_dict(seeded_state_dict(net, seed=92))
+    c_no, c_o = net.conv_non_overlap[0], net.conv_overlap[0]
+    grad = config == 2
+    fr = feats.clone().requires_grad_(grad)
+    ref = O.fuse_depth(spec, fr, batch['mask'], batch[('K', lvl)], Einv, c_no.weight, c_no.bias, c_o.weight, c_o.bias)
+    if grad:
+        g = G.seeded_randn(ref.shape, 93)
+        (ref * g).sum().backward()
+        ref_grads = {k: p.grad.clone() for k, p in net.named_parameters() if p.grad is not None}
+        net.zero_grad(set_to_none=True)
+    ref = ref.detach()
+    gnet = net.to(DEV)
+    inputs = {('K', lvl): batch[('K', lvl)].to(DEV), 'extrinsics_inv': Einv.to(DEV), 'mask': batch['mask'].to(DEV)}
+    fg = feats.to(DEV).requires_grad_(grad)
+    vox = gnet.backproject_depth(inputs, fg)                       # [B, V, Cv]
+    close(vox.permute(0, 2, 1), ref, f'K1 voxel features (config {config})')
+    n_seen = int(((ref != 0).sum(1) > 0).sum())
+    assert n_seen > 0.1 * spec.V, f'only {n_seen} of {spec.V} voxels carry features'
+    if grad:
+        (vox.permute(0, 2, 1) * g.to(DEV)).sum().backward()
+        gclose(fg.grad, fr.grad, 'K1 d feats')
+        for k, p in gnet.named_parameters():
+            if k in ref_grads:
+                gclose(p.grad, ref_grads[k], f'K1 d {k}')
+
+
+@pytest.mark.timeout(900)
+def test_fuse_pose_and_voxel_project_full_size():
+    """K2 (pose-mode fusion, volumetric_fusionnet.py:116-162) and K3 (project_voxel_into_image,
+    :232-262) forward at config 2: 6 cameras, 100x100x20 voxels, C=256, Cv=64, D=50."""
+    from oracle import vfd_oracle as O
+    from vfdepth_amd import kernels as KN
+    cfg = full_cfg(2)
+    spec = O.VoxelSpec(cfg)
+    batch, lvl, Einv = _fusion_inputs(cfg, 95)
+    C, Cv = int(cfg['model']['fusion_feat_in_dim']), int(cfg['model']['voxel_pre_dim'][-1])
+    feats = G.seeded_randn((1, 6, C, spec.h, spec.w), 96)
+    ref = O.fuse_pose(spec, feats, batch['mask'], batch[('K', lvl)], Einv)               # [B, C+1, V]
+    space = KN.VoxelSpace(cfg, DEV)
+    mask_lo = KN.mask_lowres(space, batch['mask'].to(DEV))
+    plan = KN.FusionPlan(space, mask_lo, batch[('K', lvl)].to(DEV), Einv.to(DEV), build=False)
+    out = KN.pose_to_reference(KN.FusePose.apply(space, plan, feats.to(DEV)), C + 1, space.Z)
+    inner = out[:, :, 1:-1, 1:-1].reshape(1, C + 1, space.Z, space.Y, space.X).reshape(1, C + 1, -1)
+    close(inner, ref, 'K2 pose voxels (config 2)')
+    del out, inner, ref
+    vox = G.seeded_randn((1, Cv, spec.V), 97)
+    refs = O.project_voxels(spec, vox, batch[('inv_K', lvl)], batch['extrinsics'])          # N x [B, Cv*D, h, w]
+    out = KN.proj_to_reference(KN.VoxelProject.apply(space, vox.permute(0, 2, 1).contiguous().to(DEV),
+                                                     batch[('inv_K', lvl)].to(DEV), batch['extrinsics'].to(DEV)),
+                               Cv, space.D)
+    for c in range(6):
+        close(out[c, :, 1:-1, 1:-1], refs[c][0], f'K3 frustum features cam {c} (config 2)')
+
+
+# ------------------------------------------------------------------------------------ config 3
+class OpRecorder:
+    """Record the inputs and outputs of the step's hot-path ops (K1 via VFNet.backproject_depth,
+    K2 FusePose, K3 VoxelProject) during a GPU step, for an op-by-op oracle check."""
+
+    def __init__(self):
+        from vfdepth_amd import kernels as KN
+        from vfdepth_amd.fusion import VFNet
+        self.calls = {'k1': [], 'k2': [], 'k3': []}
+        self._saved = [(owner, name, owner.__dict__.get(name)) for owner, name in
+                       ((VFNet, 'backproject_depth'), (KN.FusePose, 'apply'), (KN.VoxelProject, 'apply'))]
+        rec = self
+        k1, k2, k3 = VFNet.backproject_depth, KN.FusePose.apply, KN.VoxelProject.apply
+
+        def backproject_depth(net, inputs, feats):
+            out = k1(net, inputs, feats)
+            rec.calls['k1'].append((net, inputs['mask'], inputs[('K', net.fusion_level + 1)], inputs['extrinsics_inv'],
+                                    feats.detach().float(), out.detach()))
+            return out
+
+        def fuse_pose(space, plan, feats):
+            out = k2(space, plan, feats)
+            rec.calls['k2'].append((feats.detach().float(), out.detach()))
+            return out
+
+        def voxel_project(space, vox, invK, E):
+            out = k3(space, vox, invK, E)
+            rec.calls['k3'].append((vox.detach().float(), invK, E, out.detach()))
+            return out
+        VFNet.backproject_depth = backproject_depth
+        KN.FusePose.apply = staticmethod(fuse_pose)
+        KN.VoxelProject.apply = staticmethod(voxel_project)
+
+    def restore(self):
+        for owner, name, orig in self._saved:
+            if orig is None:
+                delattr(owner, name)            # inherited (autograd.Function.apply)
+            else:
+                setattr(owner, name, orig)
+
+
+def _check_recorded_ops(O, cfg, rec, inputs_cpu):
+    """Each recorded K1/K2/K3 call against the oracle on that call's own (fp32) inputs."""
+    from vfdepth_amd import kernels as KN
+    spec = O.VoxelSpec(cfg)
+    lvl = int(cfg['model']['fusion_level']) + 1
+    mask, K, Einv = inputs_cpu['mask'], inputs_cpu[('K', lvl)], torch.inverse(inputs_cpu['extrinsics'])
+    C, Cv, Z = int(cfg['model']['fusion_feat_in_dim']), int(cfg['model']['voxel_pre_dim'][-1]), spec.Z
+    assert len(rec.calls['k1']) == 1 and len(rec.calls['k2']) == 2 and len(rec.calls['k3']) == 1
+    net, _, _, _, feats, vox = rec.calls['k1'][0]
+    c_no, c_o = net.conv_non_overlap[0], net.conv_overlap[0]
+    with torch.no_grad():
+        ref = O.fuse_depth(spec, feats.cpu(), mask, K, Einv, c_no.weight.cpu(), c_no.bias.cpu(),
+                           c_o.weight.cpu(), c_o.bias.cpu())
+    close(vox.permute(0, 2, 1), ref, 'K1 in the step')
+    for i, (feats, out) in enumerate(rec.calls['k2']):
+        with torch.no_grad():
+            ref = O.fuse_pose(spec, feats.cpu(), mask, K, Einv)
+        B = ref.shape[0]
+        got = KN.pose_to_reference(out, C + 1, Z)[:, :, 1:-1, 1:-1].reshape(B, C + 1, -1)
+        close(got, ref, f'K2 call {i} in the step')
+    vox, invK, E, out = rec.calls['k3'][0]
+    B = vox.shape[0]
+    with torch.no_grad():
+        refs = O.project_voxels(spec, vox.cpu().permute(0, 2, 1), invK.cpu(), E.cpu())
+    got = KN.proj_to_reference(out, Cv, spec.D).view(B, 6, Cv * spec.D, spec.h + 2, spec.w + 2)
+    for c in range(6):
+        close(got[:, c, :, 1:-1, 1:-1], refs[c], f'K3 cam {c} in the step')
+
+
+def _check_loss_path(O, cfg, inputs_cpu, outputs, losses, noise):
+    """K4 + K5 of the step against the oracle evaluated on the step's own depth maps and poses."""
+    N, frames = cfg['data']['num_cams'], cfg['training']['frame_ids']
+    ci = dict(inputs_cpu)
+    ci['extrinsics_inv'] = torch.inverse(ci['extrinsics'])
+    total, terms = 0.0, {}
+    with torch.no_grad():
+        for c in range(N):
+            go = outputs[('cam', c)]
+            co = {('disp', 0): go[('disp', 0)].detach().float().cpu(),
+                  ('depth', 0): go[('depth', 0)].detach().float().cpu()}
+            for f in frames[1:]:
+                co[('cam_T_cam', 0, f)] = go[('cam_T_cam', 0, f)].detach().cpu()
+            O.view_rendering(ci, co, c, O.relative_poses(ci, co, c, cfg), cfg)
+            for k in G.VIEW_IMG_KEYS:
+                close(go[k], co[k], f'{k} cam {c} in the step')
+            cl, tm = O.cam_loss(ci, co, c, cfg, noise[c].cpu())
+            total = total + cl
+            for k, v in tm.items():
+                terms.setdefault(k, []).append(float(v))
+    close(losses['total_loss'], total / N, 'total loss (oracle on the step\'s depths and poses)')
+    for k in ('reproj_loss', 'spatio_loss', 'spatio_tempo_loss', 'smooth'):
+        close(losses[k], np.mean(terms[k]), f'{k} (oracle on the step\'s depths and poses)')
+
+
+@pytest.mark.timeout(1200)
+@pytest.mark.parametrize('prec', ['fp32', 'bf16'])
+def test_config3_step_b2(prec):
+    """Config 3 (6-cam 384x640, B=2 per GPU).  fp32 nets: the whole GPU step (depth maps, poses,
+    losses) against the oracle's whole step with the same modules and weights.  bf16 nets
+    (config 3's precision): every hot-path op of the step against the oracle on that op's own
+    inputs (K1, both K2 calls, K3), and K4 + K5 on the step's own depth maps and poses."""
+    from oracle import vfd_oracle as O
+    from vfdepth_amd import synth
+    from vfdepth_amd.layers import seeded_state_dict
+    from vfdepth_amd.network import FusedDepthNet, FusedPoseNet
+    from vfdepth_amd.vfdepth import VFDepthAlgo
+    cfg = full_cfg(3, 2)
+    cfg['training']['net_precision'] = prec
+    N, frames, H, W = cfg['data']['num_cams'], cfg['training']['frame_ids'], cfg['training']['height'], cfg['training']['width']
+    inputs = synth.make_batch(cfg, seed=33)
+    cpu_inputs = {k: v.clone() if torch.is_tensor(v) else v for k, v in inputs.items()}
+    noise = 1e-5 * torch.randn(N, 2, len(frames) - 1, H, W, generator=torch.Generator().manual_seed(34))
+    algo = VFDepthAlgo(cfg, 0)
+    for m in algo.models.values():
+        m.load_state_dict(seeded_state_dict(m, seed=G.STEP_SEED))
+    algo.set_train()
+    rec = OpRecorder()
+    try:
+        outputs, losses = algo.process_batch(inputs, 0, noise=noise.to(DEV))
+        losses['total_loss'].backward()
+        torch.cuda.synchronize()
+    finally:
+        rec.restore()
+    assert torch.isfinite(losses['total_loss']).item()
+    _check_recorded_ops(O, cfg, rec, cpu_inputs)
+    _check_loss_path(O, cfg, cpu_inputs, outputs, losses, noise)
+    if prec != 'fp32':
+        return
+    dn, pn = FusedDepthNet(cfg), FusedPoseNet(cfg)
+    dn.load_state_dict(seeded_state_dict(dn, seed=G.STEP_SEED))
+    pn.load_state_dict(seeded_state_dict(pn, seed=G.STEP_SEED))
+    dn.train()
+    pn.train()
+    with torch.no_grad():
+        o_out, o_loss = O.process_batch(O.nets_from_modules(dn, pn), cpu_inputs, cfg, [n for n in noise])
+    for c in range(N):
+        close(outputs[('cam', c)][('depth', 0)], o_out[('cam', c)][('depth', 0)], f'depth cam {c} vs oracle step')
+        for f in frames[1:]:
+            close(outputs[('cam', c)][('cam_T_cam', 0, f)], o_out[('cam', c)][('cam_T_cam', 0, f)],
+                  f'T{f} cam {c} vs oracle step', atol=1e-5)
+    for k in ('total_loss', 'reproj_loss', 'spatio_loss', 'spatio_tempo_loss', 'smooth'):
+        close(losses[k], o_loss[k], f'{k} vs oracle step')

@@ -29,6 +29,40 @@ def test_compute_depth_losses_median_scaling():
     assert float(median['abs_rel']) < 1e-6 and float(median['a1']) == 1.0
 
 
+def _metric_fixture(fx, prefix):
+    names = ['abs_rel', 'sq_rel', 'rms', 'log_rms', 'a1', 'a2', 'a3']
+    return ({k: float(fx[f'{prefix}_metric_{k}']) for k in names},
+            {k: float(fx[f'{prefix}_median_{k}']) for k in names})
+
+
+def test_compute_depth_losses_matches_reference_logger():
+    """Logger.compute_depth_losses (logger.py:193-247) of the reference, run on the same inputs
+    (tests/golden/depth_metrics.npz): resize of a 2x prediction, clamping, lidar holes, fractional
+    mask, median scaling, two eval ranges; and the reference step's own depth maps vs the
+    synthetic ground-plane GT (the Abs.Rel half of BASELINE.json's metric)."""
+    import common as G
+    from vfdepth_amd import synth
+    from vfdepth_amd.metrics import METRIC_NAMES, compute_depth_losses
+    fx = golden('depth_metrics.npz')
+    assert METRIC_NAMES == ['abs_rel', 'sq_rel', 'rms', 'log_rms', 'a1', 'a2', 'a3']
+    for case, (lo, hi) in (('unit', (0.0, 200.0)), ('unit_nusc', (1.5, 80.0))):
+        cfg, inputs, outputs = G.depth_metric_case()
+        np.testing.assert_allclose(G.checksum(inputs['depth']), fx['cs_unit_gt'], rtol=1e-12)
+        metric, median = compute_depth_losses(inputs, outputs, 6, lo, hi)
+        ref_metric, ref_median = _metric_fixture(fx, case)
+        for k in METRIC_NAMES:
+            np.testing.assert_allclose(float(metric[k]), ref_metric[k], rtol=1e-6, atol=1e-7, err_msg=f'{case} {k}')
+            np.testing.assert_allclose(float(median[k]), ref_median[k], rtol=1e-6, atol=1e-7, err_msg=f'{case} {k}')
+    cfg = G.step_cfg()
+    inputs = synth.make_batch(cfg, seed=5, with_depth=True)
+    outputs = {('cam', c): {('depth', 0): torch.tensor(fx[f'step_depth_c{c}'])} for c in range(6)}
+    metric, median = compute_depth_losses(inputs, outputs, 6, 0.0, 200.0)
+    ref_metric, ref_median = _metric_fixture(fx, 'step')
+    for k in METRIC_NAMES:
+        np.testing.assert_allclose(float(metric[k]), ref_metric[k], rtol=1e-6, atol=1e-7, err_msg=f'step {k}')
+        np.testing.assert_allclose(float(median[k]), ref_median[k], rtol=1e-6, atol=1e-7, err_msg=f'step {k}')
+
+
 def test_inverse4x4_matches_lu_inverse():
     from vfdepth_amd import synth
     from vfdepth_amd.geometry import inverse4x4

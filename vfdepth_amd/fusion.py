@@ -27,6 +27,43 @@ from . import kernels as KN
 from .layers import conv1d_block, conv2d_block, pack_cam_feat
 
 
+class _GeometryCache:
+    """Step-scoped geometry products (1/8 mask, K2 fusion plan) shared by the three VFNet calls
+    of a step (two pose calls, one depth call).
+
+    Keyed on the IDENTITY and version of the input tensors they derive from, not on the
+    `inputs` dict: DDP re-packs a module's positional inputs into a fresh dict every call
+    (`torch.distributed.utils._recursive_to`), so anything cached inside `inputs` would be lost
+    and rebuilt per call.  One entry per tag holds strong references to its key tensors (their
+    addresses cannot be reused while cached); the next step's tensors replace it."""
+
+    def __init__(self):
+        self.entries = {}
+
+    def get(self, tag, tensors, build):
+        e = self.entries.get(tag)
+        vers = tuple(t._version for t in tensors)
+        if e is not None and len(e[0]) == len(tensors) and all(a is b for a, b in zip(e[0], tensors)) \
+                and e[1] == vers:
+            return e[2]
+        self.entries.pop(tag, None)
+        val = build()
+        self.entries[tag] = (tuple(tensors), vers, val)
+        return val
+
+    def clear(self):
+        self.entries.clear()
+
+
+_GEOMETRY_CACHE = _GeometryCache()
+
+
+def begin_step():
+    """Drop the previous step's geometry products (VFDepthAlgo.process_batch calls this first, so
+    every step builds its own 1/8 mask and fusion plan even when a batch tensor is reused)."""
+    _GEOMETRY_CACHE.clear()
+
+
 class VFNet(nn.Module):
     def __init__(self, cfg, feat_in_dim, feat_out_dim, model='depth'):
         super().__init__()
@@ -54,6 +91,10 @@ class VFNet(nn.Module):
                 raise NotImplementedError(f'overlap fusion needs 3 or 6 cameras, got {self.num_cams}')
         else:
             enc_dims, stride = (feat_in_dim + 1) * z_dim, 2
+            if feat_in_dim % 4 or not 0 < feat_in_dim <= 256:
+                # K2's backward moves channel quads (fusion.hip, vfd_fuse_pose_bwd): refuse at
+                # construction instead of failing mid-step
+                raise ValueError(f'pose fusion needs fusion_feat_in_dim % 4 == 0 and <= 256, got {feat_in_dim}')
         self.stride = stride
         self.reduce_dim = nn.Sequential(*conv2d_block(enc_dims, 256, kernel_size=3, stride=stride).children(),
                                         *conv2d_block(256, feat_out_dim, kernel_size=3, stride=stride).children())
@@ -66,17 +107,16 @@ class VFNet(nn.Module):
         return self._space
 
     def _mask_lowres(self, inputs, space):
-        key = ('_vfd_mask_lo', space.h, space.w)
-        if key not in inputs:
-            inputs[key] = KN.mask_lowres(space, inputs['mask'])
-        return inputs[key]
+        return _GEOMETRY_CACHE.get(('mask_lo', space.h, space.w), (inputs['mask'],),
+                                   lambda: KN.mask_lowres(space, inputs['mask']))
 
     def _plan(self, inputs, space):
-        key = ('_vfd_plan', space.h, space.w, tuple(self.voxel_size))
-        if key not in inputs:
-            inputs[key] = KN.FusionPlan(space, self._mask_lowres(inputs, space), inputs['K', self.fusion_level + 1],
-                                        inputs['extrinsics_inv'])
-        return inputs[key]
+        K, Einv = inputs['K', self.fusion_level + 1], inputs['extrinsics_inv']
+        mask_lo = self._mask_lowres(inputs, space)
+        # buffers built by the first forward that needs a gradient (FusePose), shared by both
+        # pose calls of the step
+        return _GEOMETRY_CACHE.get(('plan', space.h, space.w, tuple(self.voxel_size)), (mask_lo, K, Einv),
+                                   lambda: KN.FusionPlan(space, mask_lo, K, Einv, build=False))
 
     def _reduce(self, x_padded):
         """reduce_dim with the first conv reading the kernel's channels-last, reflect-padded output
@@ -108,7 +148,10 @@ class VFNet(nn.Module):
         space = self.space(feats_agg.device)
         B, N, C, h, w = feats_agg.shape
         wf, wz = self.folded_weights()
-        P = torch.einsum('bncp,nkc->bnpk', feats_agg.reshape(B, N, C, h * w), wf).contiguous()
+        # the fold is part of K1's algebra (it replaces the reference's fp32 1x1 convs after the
+        # gather): fp32 even when the dense nets run under bf16 autocast (config 3)
+        with torch.autocast(device_type='cuda', enabled=False):
+            P = torch.einsum('bncp,nkc->bnpk', feats_agg.float().reshape(B, N, C, h * w), wf.float()).contiguous()
         K = inputs['K', self.fusion_level + 1]
         return KN.FuseDepth.apply(space, P, self._mask_lowres(inputs, space), K, inputs['extrinsics_inv'],
                                   wz, self.conv_non_overlap[0].bias, self.conv_overlap[0].bias)

@@ -12,10 +12,19 @@ import torch
 from . import _lib as L
 
 
-def _dev(t, what):
+def _check_device(t, what):
     if not torch.is_tensor(t) or not t.is_cuda:
         raise RuntimeError(f'{what}: the VFDepth hot path runs only on a HIP device (got '
                            f'{"non-tensor" if not torch.is_tensor(t) else t.device})')
+    if t.device.index is not None and t.device.index != torch.cuda.current_device():
+        # every launch goes on the current device's stream (_lib.stream): a tensor of another
+        # device would be read through the wrong context
+        raise RuntimeError(f'{what}: tensor on {t.device} but the current HIP device is '
+                           f'cuda:{torch.cuda.current_device()} (torch.cuda.set_device first)')
+
+
+def _dev(t, what):
+    _check_device(t, what)
     if t.dtype != torch.float32:
         t = t.float()
     return t.contiguous()
@@ -156,14 +165,25 @@ class FusionPlan:
 
     Built once per step from K (fusion scale), E^-1 and the 1/8 mask; every pose-mode fusion call
     of the step reuses it (the geometry does not depend on features).  Only the backward reads the
-    buffers (built on `_side_stream`'s stream); `wait()` joins that stream."""
+    buffers, so they are built on demand (`build()`: by the first forward that needs a gradient;
+    a no-grad evaluation step never allocates them), on `_side_stream`'s stream; `wait()` joins
+    that stream."""
 
-    def __init__(self, space, mask_lo, K, Einv):
-        lib = L.load()
+    def __init__(self, space, mask_lo, K, Einv, build=True):
         mask_lo, K, Einv = (_dev(t, n) for t, n in ((mask_lo, 'mask'), (K, 'K'), (Einv, 'Einv')))
         self.B, self.N = mask_lo.shape[:2]
         self.mask_lo, self.K, self.Einv = mask_lo, K, Einv
-        d = space.desc(self.B, self.N)
+        self.space = space
+        self.buf = None
+        if build:
+            self.build()
+
+    def build(self):
+        if self.buf is not None:
+            return self
+        lib = L.load()
+        mask_lo, K, Einv = self.mask_lo, self.K, self.Einv
+        d = self.space.desc(self.B, self.N)
         nbytes = lib.vfd_fusion_plan_bytes(ctypes.byref(d))
         main, self.side = torch.cuda.current_stream(mask_lo.device), _side_stream(mask_lo.device)
         self.side.wait_stream(main)
@@ -176,6 +196,7 @@ class FusionPlan:
             t.record_stream(main)
         for t in (mask_lo, K, Einv):
             t.record_stream(self.side)
+        return self
 
     def wait(self):
         """Make the current stream wait for the plan (before any kernel that reads its buffers)."""
@@ -184,8 +205,7 @@ class FusionPlan:
 
 def _channels_last(t, what):
     """Device fp32 tensor in channels-last (NHWC) memory order (no copy when it already is)."""
-    if not torch.is_tensor(t) or not t.is_cuda:
-        raise RuntimeError(f'{what}: the VFDepth hot path runs only on a HIP device')
+    _check_device(t, what)
     if t.dtype != torch.float32:
         t = t.float()
     return t.contiguous(memory_format=torch.channels_last)
@@ -235,6 +255,8 @@ class FusePose(torch.autograd.Function):
                                       plan.Einv.data_ptr(), feats_cl.data_ptr(), out.data_ptr(), L.stream()),
                 'fuse_pose_fwd')
         ctx.space, ctx.plan, ctx.shape = space, plan, tuple(feats.shape)
+        if ctx.needs_input_grad[2]:
+            plan.build()            # the backward's index (kept in the order the step issued it)
         return out
 
     @staticmethod
@@ -245,7 +267,7 @@ class FusePose(torch.autograd.Function):
         g = _channels_last(g, 'grad')
         dfeats = torch.empty(ctx.shape, device=g.device)
         d = ctx.space.desc(B, N, C=C)
-        ctx.plan.wait()
+        ctx.plan.build().wait()
         L.check(lib.vfd_fuse_pose_bwd(ctypes.byref(d), ctx.plan.buf.data_ptr(), ctx.plan.counts.data_ptr(),
                                       g.data_ptr(), dfeats.data_ptr(), L.stream()), 'fuse_pose_bwd')
         return None, None, dfeats

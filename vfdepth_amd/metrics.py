@@ -11,7 +11,7 @@ from collections import defaultdict
 import torch
 import torch.nn.functional as F
 
-METRIC_NAMES = ['abs_rel', 'sq_rel', 'rmse', 'rmse_log', 'a1', 'a2', 'a3']   # logger.py:_metric_names
+METRIC_NAMES = ['abs_rel', 'sq_rel', 'rms', 'log_rms', 'a1', 'a2', 'a3']   # logger.py:76 _metric_names
 
 
 def cal_depth_error(pred, target):

@@ -22,6 +22,7 @@ import torch.nn.functional as F
 import torch.optim as optim
 from torch.utils.data import DataLoader
 
+from . import fusion
 from .config import flatten
 from .geometry import Pose, ViewRendering, inverse4x4
 from .losses import MultiCamLoss, SingleCamLoss
@@ -42,6 +43,9 @@ class VFDepthAlgo:
         for k, v in flatten(cfg).items():
             setattr(self, k, v)
         self.device = torch.device(f'cuda:{rank}') if isinstance(rank, int) else torch.device(rank)
+        if self.device.type == 'cuda':
+            # the C-ABI ops launch on the current device's stream: make it this rank's device
+            torch.cuda.set_device(self.device)
         if getattr(self, 'net_precision', 'fp32') not in ('fp32', 'bf16'):
             raise ValueError(f'net_precision must be fp32 or bf16, got {self.net_precision!r}')
         self.prepare_dataset(cfg, rank)
@@ -102,7 +106,11 @@ class VFDepthAlgo:
         for m in self.models.values():
             params += list(m.parameters())
         fused = self.device.type == 'cuda'
-        self.optimizer = optim.Adam(params, self.learning_rate, fused=fused, capturable=capturable and fused)
+        capturable = capturable and fused
+        # a captured step reads the learning rate from device memory: a tensor lr, which
+        # StepLR updates in place (fill_), so the scheduler's decay reaches graph replays
+        lr = torch.tensor(float(self.learning_rate), device=self.device) if capturable else self.learning_rate
+        self.optimizer = optim.Adam(params, lr, fused=fused, capturable=capturable)
         self.lr_scheduler = optim.lr_scheduler.StepLR(self.optimizer, self.scheduler_step_size, 0.1)
 
     # ------------------------------------------------------------------ base-model API
@@ -133,7 +141,10 @@ class VFDepthAlgo:
         torch.save(self.optimizer.state_dict(), os.path.join(path, f'{_OPTIMIZER_NAME}.pth'))
 
     def load_weights(self):
+        """base_model.py:58-93: filtered state-dict load per model; the Adam state only in train
+        mode, and a param-group mismatch (ValueError) keeps a fresh optimizer, as the reference."""
         assert os.path.isdir(self.load_weights_dir), f'\tCannot find {self.load_weights_dir}'
+        print(f'Loading a model from {self.load_weights_dir}')
         for name in self.models_to_load:
             path = os.path.join(self.load_weights_dir, f'{name}.pth')
             model = self.models[name]
@@ -141,15 +152,23 @@ class VFDepthAlgo:
             src = torch.load(path, map_location=self.device, weights_only=True)
             own.update({k: v for k, v in src.items() if k in own})
             model.load_state_dict(own)
+        if self.mode != 'train':
+            return
         opt = os.path.join(self.load_weights_dir, f'{_OPTIMIZER_NAME}.pth')
-        if os.path.isfile(opt):
+        if not os.path.isfile(opt):
+            print(f'\tCannot find {_OPTIMIZER_NAME} weights, so the optimizer will be randomly initialized')
+            return
+        try:
             self.optimizer.load_state_dict(torch.load(opt, map_location=self.device, weights_only=True))
+        except ValueError:
+            print(f'\tCannnot load {_OPTIMIZER_NAME} - the optimizer will be randomly initialized')
 
     # ------------------------------------------------------------------ step
     def process_batch(self, inputs, rank, noise=None):
         """Move the batch to the device, estimate poses/depths, render and score every camera.
 
         `noise` (optional, [N, B, T, H, W]) overrides the identity-loss noise (parity tests)."""
+        fusion.begin_step()
         for key, ipt in list(inputs.items()):
             if key in _NO_DEVICE_KEYS or not torch.is_tensor(ipt) and not isinstance(ipt, list):
                 continue

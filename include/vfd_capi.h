@@ -117,6 +117,19 @@ size_t vfd_voxel_project_bwd_workspace(const vfd_voxel_desc* d);
 int vfd_voxel_project_bwd(const vfd_voxel_desc* d, const float* d_out, const float* invK,
                           const float* E, float* d_vox, void* ws, size_t ws_bytes, void* stream);
 
+/* K3C — K3 fused into reduce_dim's first 3x3 conv (volumetric_fusionnet.py:59-60, 232-267; depth
+ * mode): out = LeakyReLU_0.1(conv3x3_reflect(frustum samples of vox) + bias) as an fp32 MFMA
+ * implicit GEMM; the [B*N, Cv*D, h, w] frustum features are generated per (pixel tile, depth bin)
+ * in LDS and never written.  vox [B,V,Cv] (Cv = 64), invK, E [B,N,4,4] (fusion scale),
+ * Wq = the conv weight [O, Cv*D, 3, 3] in fragment order [D, 3, 3, Cv/4, O, 2, 2]
+ * (reference channel c*D + d with c = 4q + 2h + s), bias [O], out_channels O = 256 ->
+ * out [B*N, h+2, w+2, O]: reflect-padded NHWC input of reduce_dim's second conv.  D <= 64.
+ * Workspace: per-workgroup partial tiles (summed in a fixed order: deterministic). */
+size_t vfd_proj_conv_fwd_workspace(const vfd_voxel_desc* d);
+int vfd_proj_conv_fwd(const vfd_voxel_desc* d, const float* vox, const float* invK, const float* E,
+                      const float* Wq, const float* bias, int out_channels, float* out, void* workspace,
+                      size_t ws_bytes, void* stream);
+
 /* ------------------------------------------------------------------ view synthesis (K4) */
 typedef struct vfd_view_desc {
   int32_t B, N, H, W;
@@ -201,7 +214,7 @@ int vfd_aggregate_fwd(int BN, int C, int h, int w, const float* base, int n_leve
  * recorded; vfd_prof_read_kernels: the same per kernel id into arrays of `count` entries.
  * Both reset the record. */
 #define VFD_PROF_ALL (-1)
-#define VFD_KERNEL_COUNT 16
+#define VFD_KERNEL_COUNT 18
 const char* vfd_kernel_name(int kernel_id);
 int vfd_prof_enable(int kernel_id);
 int vfd_prof_read(int* launches, double* total_ms);

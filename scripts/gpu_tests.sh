@@ -5,7 +5,10 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 OUT=gpurun_out/tests
 mkdir -p $OUT
 export PYTHONUNBUFFERED=1
+# optional: K='expr' selects tests by keyword
 SEL=${@:-tests}
-timeout -k 10 1500 python -u -m pytest $SEL -m gpu -v -rf --timeout 900 --timeout-method thread > $OUT/tests.log 2>&1
+KARG=()
+[ -n "$K" ] && KARG=(-k "$K")
+timeout -k 10 1500 python -u -m pytest $SEL "${KARG[@]}" -m gpu -v -rf --timeout 900 --timeout-method thread > $OUT/tests.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> $OUT/tests.log
 exit $rc

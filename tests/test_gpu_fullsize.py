@@ -75,12 +75,34 @@ def _near_decisions(O, target, planes, idents, noise, frames, margin=1e-5):
     idn = torch.cat([O.photometric(i, target) for i in idents], 1) + noise
     st = torch.cat([O.photometric(planes[('overlap', f, 0)], target) for f in frames[1:]], 1)
 
-    def tie(m):
-        return m < margin
+    def tie(m):     # exact ties resolve identically on both sides (equal inputs, first index wins)
+        return (m > 0) & (m < margin)
     near = tie(rep.max(1, keepdim=True).values - rep.min(1, keepdim=True).values)
     near |= tie((rep.min(1, keepdim=True).values - idn.min(1, keepdim=True).values).abs())
     near |= tie(st.max(1, keepdim=True).values - st.min(1, keepdim=True).values)
     return F.max_pool2d(near.float(), 3, 1, 1) > 0
+
+
+def _near_grid_lines(O, batch, depth_c, co, c, cfg, tol=2e-3):
+    """[B,1,H,W] pixels where some warp of camera c samples within `tol` pixels of an integer
+    grid line of its source image (or of the OOB border).  The bilinear sample's slope w.r.t.
+    the coordinate jumps there (floor changes: d/dx = v1 - v0 on one side, v0 - v-1 on the
+    other), so fp32-rounding differences in the coordinate legitimately flip d img / d depth."""
+    H, W = depth_c.shape[-2:]
+    frames = cfg['training']['frame_ids']
+    invK, K = batch[('inv_K', 0)][:, c], batch[('K', 0)]
+    pts = O.backproject(invK, depth_c)
+    warps = [(K[:, c], co[('cam_T_cam', 0, f)]) for f in frames[1:]]
+    rel = O.relative_poses(batch, co, c, cfg)
+    warps += [(K[:, s], T) for (f, s), T in rel.items()]
+    near = torch.zeros(depth_c.shape[0], H * W, dtype=torch.bool)
+    for Ks, T in warps:
+        gx, gy = O.reproject(Ks, T, pts, H, W)
+        for g, n in ((gx, W), (gy, H)):
+            ix = ((g + 1) / 2) * (n - 1)
+            fr = ix - torch.floor(ix)
+            near |= (fr < tol) | (fr > 1 - tol)
+    return near.view(-1, 1, H, W)
 
 
 @pytest.mark.timeout(900)
@@ -98,19 +120,25 @@ def test_view_synthesis_and_losses_full_size(config):
     N, frames, H, W = cfg['data']['num_cams'], t['frame_ids'], t['height'], t['width']
     batch, depth, poses = G.view_case_cfg(cfg, seed=60 + config)
     keys = G.VIEW_IMG_KEYS
-    # ---- K4, oracle
+    # ---- K4, oracle.  The backward is checked with a random linear functional of the planes
+    # whose weights are zero on pixels that sample near a source grid line (_near_grid_lines),
+    # so d depth and d T compare the same decision-free function on both sides.
     d_leaf = depth.clone().requires_grad_(True)
     T_leaf = {k: v.clone().requires_grad_(True) for k, v in poses.items()}
-    ref = {}
+    ref, gw = {}, {}
     loss = 0.0
     for c in range(N):
         co = {('depth', 0): d_leaf[:, c]}
         for f in frames[1:]:
             co[('cam_T_cam', 0, f)] = T_leaf[(c, f)]
+        with torch.no_grad():
+            grid = _near_grid_lines(O, batch, depth[:, c], co, c, cfg)
+        assert float(grid.float().mean()) < 0.1, f'cam {c}: {float(grid.float().mean()):.3f} of px near a grid line'
         O.view_rendering(batch, co, c, O.relative_poses(batch, co, c, cfg), cfg)
         ref[c] = co
         for i, k in enumerate(keys):
-            loss = loss + (co[k] * G.seeded_randn(co[k].shape, 700 + 10 * c + i)).sum()
+            gw[(c, i)] = G.seeded_randn(co[k].shape, 700 + 10 * c + i) * (~grid).float()
+            loss = loss + (co[k] * gw[(c, i)]).sum()
     loss.backward()
     # ---- K4, product
     bd = to_dev(batch)
@@ -128,7 +156,7 @@ def test_view_synthesis_and_losses_full_size(config):
         out = outputs[('cam', c)]
         for i, k in enumerate(keys):
             close(out[k], ref[c][k], f'{k} cam {c}')
-            gloss = gloss + (out[k] * G.seeded_randn(out[k].shape, 700 + 10 * c + i).to(DEV)).sum()
+            gloss = gloss + (out[k] * gw[(c, i)].to(DEV)).sum()
         for k in G.VIEW_MSK_KEYS:
             close(out[k], ref[c][k], f'{k} cam {c}', atol=0, rtol=0)
     gloss.backward()
@@ -270,11 +298,13 @@ class OpRecorder:
     def __init__(self):
         from vfdepth_amd import kernels as KN
         from vfdepth_amd.fusion import VFNet
-        self.calls = {'k1': [], 'k2': [], 'k3': []}
+        self.calls = {'k1': [], 'k2': [], 'k3': [], 'k3c': []}
         self._saved = [(owner, name, owner.__dict__.get(name)) for owner, name in
-                       ((VFNet, 'backproject_depth'), (KN.FusePose, 'apply'), (KN.VoxelProject, 'apply'))]
+                       ((VFNet, 'backproject_depth'), (KN.FusePose, 'apply'), (KN.VoxelProject, 'apply'),
+                        (KN.ProjConv, 'apply'))]
         rec = self
         k1, k2, k3 = VFNet.backproject_depth, KN.FusePose.apply, KN.VoxelProject.apply
+        k3c = KN.ProjConv.apply
 
         def backproject_depth(net, inputs, feats):
             out = k1(net, inputs, feats)
@@ -291,9 +321,14 @@ class OpRecorder:
             out = k3(space, vox, invK, E)
             rec.calls['k3'].append((vox.detach().float(), invK, E, out.detach()))
             return out
+        def proj_conv(space, vox, invK, E, w0, bias):
+            out = k3c(space, vox, invK, E, w0, bias)
+            rec.calls['k3c'].append((vox.detach().float(), invK, E, w0.detach(), bias.detach(), out.detach()))
+            return out
         VFNet.backproject_depth = backproject_depth
         KN.FusePose.apply = staticmethod(fuse_pose)
         KN.VoxelProject.apply = staticmethod(voxel_project)
+        KN.ProjConv.apply = staticmethod(proj_conv)
 
     def restore(self):
         for owner, name, orig in self._saved:
@@ -310,7 +345,8 @@ def _check_recorded_ops(O, cfg, rec, inputs_cpu):
     lvl = int(cfg['model']['fusion_level']) + 1
     mask, K, Einv = inputs_cpu['mask'], inputs_cpu[('K', lvl)], torch.inverse(inputs_cpu['extrinsics'])
     C, Cv, Z = int(cfg['model']['fusion_feat_in_dim']), int(cfg['model']['voxel_pre_dim'][-1]), spec.Z
-    assert len(rec.calls['k1']) == 1 and len(rec.calls['k2']) == 2 and len(rec.calls['k3']) == 1
+    assert len(rec.calls['k1']) == 1 and len(rec.calls['k2']) == 2
+    assert len(rec.calls['k3']) + len(rec.calls['k3c']) == 1
     net, _, _, _, feats, vox = rec.calls['k1'][0]
     c_no, c_o = net.conv_non_overlap[0], net.conv_overlap[0]
     with torch.no_grad():
@@ -323,13 +359,24 @@ def _check_recorded_ops(O, cfg, rec, inputs_cpu):
         B = ref.shape[0]
         got = KN.pose_to_reference(out, C + 1, Z)[:, :, 1:-1, 1:-1].reshape(B, C + 1, -1)
         close(got, ref, f'K2 call {i} in the step')
-    vox, invK, E, out = rec.calls['k3'][0]
-    B = vox.shape[0]
-    with torch.no_grad():
-        refs = O.project_voxels(spec, vox.cpu().permute(0, 2, 1), invK.cpu(), E.cpu())
-    got = KN.proj_to_reference(out, Cv, spec.D).view(B, 6, Cv * spec.D, spec.h + 2, spec.w + 2)
-    for c in range(6):
-        close(got[:, c, :, 1:-1, 1:-1], refs[c], f'K3 cam {c} in the step')
+    if rec.calls['k3']:
+        vox, invK, E, out = rec.calls['k3'][0]
+        B = vox.shape[0]
+        with torch.no_grad():
+            refs = O.project_voxels(spec, vox.cpu().permute(0, 2, 1), invK.cpu(), E.cpu())
+        got = KN.proj_to_reference(out, Cv, spec.D).view(B, 6, Cv * spec.D, spec.h + 2, spec.w + 2)
+        for c in range(6):
+            close(got[:, c, :, 1:-1, 1:-1], refs[c], f'K3 cam {c} in the step')
+    else:
+        # K3C: the oracle's frustum features through the reference's reflect conv + LeakyReLU (CPU)
+        vox, invK, E, w0, bias, out = rec.calls['k3c'][0]
+        B = vox.shape[0]
+        with torch.no_grad():
+            refs = O.project_voxels(spec, vox.cpu().permute(0, 2, 1), invK.cpu(), E.cpu())
+            got = out.view(B, 6, *out.shape[1:])
+            for c in range(6):
+                y = F.conv2d(F.pad(refs[c], (1, 1, 1, 1), mode='reflect'), w0.cpu(), bias.cpu())
+                close(got[:, c, :, 1:-1, 1:-1], F.leaky_relu(y, 0.1), f'K3C cam {c} in the step')
 
 
 def _check_loss_path(O, cfg, inputs_cpu, outputs, losses, noise):
@@ -405,3 +452,43 @@ def test_config3_step_b2(prec):
                   f'T{f} cam {c} vs oracle step', atol=1e-5)
     for k in ('total_loss', 'reproj_loss', 'spatio_loss', 'spatio_tempo_loss', 'smooth'):
         close(losses[k], o_loss[k], f'{k} vs oracle step')
+
+
+# ------------------------------------------------------------------------------------ K3C
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize('config', ['small', 2, 5])
+def test_proj_conv_matches_k3_plus_conv(config):
+    """K3C (K3 fused into reduce_dim's first conv, fp32 MFMA implicit GEMM) against the unfused
+    path it replaces — K3 (pinned by the golden fixtures) + the reflect-padded 3x3 conv + bias +
+    LeakyReLU (volumetric_fusionnet.py:59-60, 232-267) — forward (every reflect-halo copy too) and
+    backward (d voxels, d weight, d bias).  'small': the reduced step config (12x20 feature map:
+    partial pixel tiles, D=16); 2: 48x80, D=50; 5: 80x120 (partial column tiles), 200x200x20."""
+    from vfdepth_amd import kernels as KN
+    from vfdepth_amd import synth
+    cfg = G.step_cfg() if config == 'small' else full_cfg(config)
+    space = KN.VoxelSpace(cfg, DEV)
+    b = synth.make_batch(cfg, seed=71, batch_size=1, device=DEV)
+    lvl = cfg['model']['fusion_level'] + 1
+    invK, E = b['inv_K', lvl], b['extrinsics']
+    gen = torch.Generator(device=DEV).manual_seed(72)
+    Cv, D, O = 64, space.D, 256
+    vox = torch.randn(1, space.V, Cv, device=DEV, generator=gen)
+    w0 = torch.randn(O, Cv * D, 3, 3, device=DEV, generator=gen) * (Cv * D * 9) ** -0.5
+    bias = 0.1 * torch.randn(O, device=DEV, generator=gen)
+    leaves = [t.clone().requires_grad_(True) for t in (vox, w0, bias)]
+    y = KN.ProjConv.apply(space, leaves[0], invK, E, leaves[1], leaves[2])
+    refs = [t.clone().requires_grad_(True) for t in (vox, w0, bias)]
+    x = KN.VoxelProject.apply(space, refs[0], invK, E)
+    pre = F.conv2d(x, KN.proj_conv_weight(refs[1], Cv, D), refs[2])
+    # LeakyReLU with the fused kernel's own sign decisions: a pre-activation within fp32 rounding
+    # of 0 may take the other branch in the two GEMM summation orders (the kink: slope 1 vs 0.1),
+    # which the forward tolerates but would move the gradient by 0.9 g there
+    pos = y.detach()[:, :, 1:-1, 1:-1] > 0
+    y_ref = F.pad(torch.where(pos, pre, 0.1 * pre), (1, 1, 1, 1), mode='reflect')
+    close(y, y_ref, f'K3C output (config {config})')
+    close(F.leaky_relu(pre, 0.1), y[:, :, 1:-1, 1:-1], f'K3C output vs its own LeakyReLU (config {config})')
+    g = torch.randn(y.shape, device=DEV, generator=gen)
+    (y * g).sum().backward()
+    (y_ref * g).sum().backward()
+    for name, a, r in zip(('d voxels', 'd weight', 'd bias'), leaves, refs):
+        gclose(a.grad, r.grad, f'K3C {name} (config {config})')

@@ -1,0 +1,74 @@
+"""Time K3C (K3 fused into reduce_dim's first conv) against K3 + MIOpen conv at config 2.
+
+    python tools/micro_projconv.py [--config 2] [--iters 20]
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+if os.path.isdir(os.path.join(ROOT, 'miopen_db')):
+    os.environ.setdefault('MIOPEN_USER_DB_PATH', os.path.join(ROOT, 'miopen_db'))
+
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+
+def timed(fn, iters):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+
+def main():
+    import bench
+    from vfdepth_amd import _lib
+    from vfdepth_amd import kernels as KN
+    from vfdepth_amd import synth
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--config', type=int, default=2)
+    ap.add_argument('--iters', type=int, default=20)
+    a = ap.parse_args()
+    _lib.load()
+    cfg, _ = bench.make_cfg(a.config, 1)
+    dev = torch.device('cuda:0')
+    space = KN.VoxelSpace(cfg, dev)
+    b = synth.make_batch(cfg, seed=71, device=dev)
+    lvl = cfg['model']['fusion_level'] + 1
+    invK, E = b['inv_K', lvl], b['extrinsics']
+    B, N = E.shape[:2]
+    Cv, D, O = 64, space.D, 256
+    vox = torch.randn(B, space.V, Cv, device=dev)
+    w0 = torch.randn(O, Cv * D, 3, 3, device=dev) * (Cv * D * 9) ** -0.5
+    bias = 0.1 * torch.randn(O, device=dev)
+    flop = 2.0 * B * N * space.h * space.w * O * Cv * D * 9
+    with torch.no_grad():
+        t_fused = timed(lambda: KN.ProjConv.apply(space, vox, invK, E, w0, bias), a.iters)
+        wp = KN.proj_conv_weight(w0, Cv, D)
+        t_k3 = timed(lambda: KN.VoxelProject.apply(space, vox, invK, E), a.iters)
+        x = KN.VoxelProject.apply(space, vox, invK, E)
+        t_conv = timed(lambda: F.leaky_relu(F.conv2d(x, wp, bias), 0.1), a.iters)
+        _lib.prof_enable('proj_conv_fwd')
+        for _ in range(a.iters):
+            KN.ProjConv.apply(space, vox, invK, E, w0, bias)
+        torch.cuda.synchronize()
+        prof = _lib.prof_read()
+        _lib.prof_enable('off')
+        n, ms = prof.get('proj_conv_fwd', (1, float('nan')))
+        y = KN.ProjConv.apply(space, vox, invK, E, w0, bias)
+        ref = F.pad(F.leaky_relu(F.conv2d(x, wp, bias), 0.1), (1, 1, 1, 1), mode='reflect')
+        err = float((y - ref).abs().max()) / float(ref.abs().max())
+    print(f'config {a.config}: K3C fused {t_fused:.3f} ms (kernel {ms / n:.3f} ms, {flop / (ms / n) / 1e9:.1f} TFLOP/s); '
+          f'K3 {t_k3:.3f} ms + MIOpen conv {t_conv:.3f} ms = {t_k3 + t_conv:.3f} ms; max rel err {err:.2e}', flush=True)
+
+
+if __name__ == '__main__':
+    main()

@@ -63,6 +63,8 @@ _SIGS = {
     'vfd_photo_fwd': (c_int, [ctypes.POINTER(PhotoDesc)] + [c_fp] * 13 + [c_size_t, c_void_p]),
     'vfd_photo_bwd': (c_int, [ctypes.POINTER(PhotoDesc)] + [c_fp] * 9 + [c_void_p]),
     'vfd_aggregate_fwd': (c_int, [c_int] * 4 + [c_fp, c_int, ctypes.POINTER(c_fp), ctypes.POINTER(c_int), c_fp, c_fp, c_void_p]),
+    'vfd_proj_conv_fwd_workspace': (c_size_t, [ctypes.POINTER(VoxelDesc)]),
+    'vfd_proj_conv_fwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 5 + [c_int, c_fp, c_fp, c_size_t, c_void_p]),
     'vfd_smooth_workspace_bytes': (c_size_t, [c_int] * 4),
     'vfd_smooth_fwd': (c_int, [c_int] * 4 + [c_fp] * 5 + [c_size_t, c_void_p]),
     'vfd_smooth_bwd': (c_int, [c_int] * 4 + [c_fp] * 5 + [c_void_p]),
@@ -110,7 +112,7 @@ KERNEL_IDS = {
     'mask_downsample': 0, 'fuse_depth_fwd': 1, 'fuse_depth_bwd': 2, 'fuse_pose_fwd': 3, 'fuse_pose_bwd': 4,
     'voxel_project_fwd': 5, 'voxel_project_bwd': 6, 'view_stats': 7, 'view_apply': 8, 'view_bwd': 9,
     'photo_fwd': 10, 'photo_bwd': 11, 'smooth_fwd': 12, 'smooth_bwd': 13, 'fusion_plan': 14,
-    'aggregate': 15, 'voxel_project_plan': 16,
+    'aggregate': 15, 'voxel_project_plan': 16, 'proj_conv_fwd': 17,
 }
 
 

@@ -1,0 +1,365 @@
+// K3C — voxel -> frustum trilinear resampling FUSED into reduce_dim's first 3x3 conv, as an
+// fp32 MFMA implicit GEMM (network/volumetric_fusionnet.py:59-60, 232-267, depth mode).
+//
+// The reference materialises, per camera, the frustum features X[Cv*D, h, w] (trilinear samples of
+// the voxel grid on D depth planes) and convolves them (3x3, reflect padding, Cv*D -> O = 256)
+// followed by LeakyReLU(0.1).  Here X is never written to HBM:
+//
+//   Y[n, y, x, o] = lrelu(bias[o] + sum_{d, c, ky, kx} W[o, c*D + d, ky, kx] * Xp[n, y+ky, x+kx, d, c])
+//
+// is an implicit GEMM with M = pixels (B*N*h*w), N = O output channels, K = D * Cv * 9, whose
+// A operand (pixels x k) is generated on the fly: for one (pixel tile, depth bin d) "atom" the
+// workgroup gathers the Cv-channel trilinear samples of the tile's reflect-padded halo into LDS
+// (8 voxel rows per sample from the channels-last [B, V, Cv] grid, the K3 arithmetic exactly), then
+// runs the 9 taps x Cv channels of that depth bin on v_mfma_f32_32x32x2_f32 (exact fp32 FMA chains:
+// the reference's fp32 conv up to summation order).  B operands (weights) are read straight from
+// L2 / Infinity Cache in a fragment-ordered copy of W (`vfd_proj_conv_weight_layout`).
+//
+// Work split ("stream-K"): the B*N * tiles * D atoms, tile-major, are cut into equal contiguous
+// ranges, one per workgroup (one resident per CU): a range covers at most two tiles, whose partial
+// sums go to a per-(workgroup, slot) buffer in MFMA fragment order; `pcv_reduce_k` sums each tile's
+// partials in workgroup order (deterministic), adds the bias, applies the LeakyReLU and writes the
+// reflect-padded NHWC input of reduce_dim's second conv.
+#include "vfd_common.h"
+
+namespace vfd {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int PC_CV = 64;                       // voxel channels (voxel_pre_dim[-1])
+constexpr int PC_O = 256;                       // output channels (reduce_dim[0])
+constexpr int PC_TR = 8, PC_TC = 16;            // pixel tile: 8 rows x 16 columns = 128 pixels
+constexpr int PC_PIX = PC_TR * PC_TC;
+constexpr int PC_HR = PC_TR + 2, PC_HC = PC_TC + 2;
+constexpr int PC_NPOS = PC_HR * PC_HC;          // 180 halo positions
+constexpr int PC_XS = PC_CV + 4;                // LDS floats per halo position (16-B aligned rows)
+constexpr int PC_WAVES = 4;                     // each wave: 128 pixels x 64 output channels
+constexpr int PC_FRAG = PC_PIX * PC_O;          // floats of one tile's partial (fragment order)
+constexpr int PC_WG_PER_CU = 1;
+
+struct PcGeom {
+  int tr, tc, tiles_img, ntile, natom, ngroup;
+};
+
+__host__ __device__ inline PcGeom pc_geom(const vfd_voxel_desc& d, int ngroup) {
+  PcGeom g;
+  g.tr = (d.h + PC_TR - 1) / PC_TR;
+  g.tc = (d.w + PC_TC - 1) / PC_TC;
+  g.tiles_img = g.tr * g.tc;
+  g.ntile = d.B * d.N * g.tiles_img;
+  g.natom = g.ntile * d.D;
+  g.ngroup = ngroup;
+  return g;
+}
+
+// first atom of workgroup g (ranges are [lo(g), lo(g+1)))
+__host__ __device__ inline int pc_lo(const PcGeom& g, int grp) {
+  return (int)(((long long)grp * g.natom) / g.ngroup);
+}
+
+__device__ __forceinline__ int pc_reflect(int i, int n) {
+  // reflect-pad(1) source row of padded-relative index i in [-1, n]; rows of a partial tile that
+  // lie beyond the image are clamped (their outputs are never stored)
+  if (i < 0) return 1 < n ? 1 : 0;
+  if (i >= n) return i == n ? (n >= 2 ? n - 2 : 0) : n - 1;
+  return i;
+}
+
+// Workgroup = 8 waves, one per CU: waves 0-3 are the MFMA "compute" waves (each 128 pixels x 64
+// output channels, 8 f32x16 accumulators), waves 4-7 the "gather" waves, which build the NEXT
+// atom's halo samples into the other half of a double-buffered LDS image while the compute waves
+// run the current one (one barrier per atom).  Compute waves therefore never stall on the voxel
+// gather; each keeps its SIMD's matrix pipe busy alone, with the weight fragments prefetched
+// PC_PF iterations ahead from L2 / Infinity Cache.
+constexpr int PC_THREADS = 512;
+#ifndef VFD_PC_PF
+#define VFD_PC_PF 4
+#endif
+constexpr int PC_PF = VFD_PC_PF;                // weight-fragment prefetch distance (iterations)
+constexpr int PC_ITERS = 9 * (PC_CV / 4);       // (tap, channel quad) iterations per atom
+
+// gather waves: halo samples of atom (tile origin y0/x0, depth dep) into one LDS image
+__device__ __forceinline__ void pc_gather(const vfd_voxel_desc& d, float* __restrict__ xs,
+                                          const float* __restrict__ vox_b, const float* __restrict__ iK,
+                                          const float* __restrict__ E, int y0, int x0, float dep, int gw) {
+  // lanes = (position, channel quad): 16 quads per 64-channel row, 4 positions per wave
+  // instruction; each lane evaluates its position's trilinear cell itself (no cross-wave sync)
+  const int lane = threadIdx.x & 63;
+  const int q = lane & 15, sub = lane >> 4;
+  const float4* vb = reinterpret_cast<const float4*>(vox_b) + q;
+  for (int p = gw * 4 + sub; p < PC_NPOS; p += 16) {
+    const int hr = p / PC_HC, hc = p - hr * PC_HC;
+    const int py = pc_reflect(y0 + hr - 1, d.h), px = pc_reflect(x0 + hc - 1, d.w);
+    const Tri t = frustum_sample(d, iK, E, px, py, dep);
+    const int base = (t.z0 * d.Y + t.y0) * d.X + t.x0;
+    float4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const bool ok = (t.in >> k & 1u) != 0u;
+      v[k] = vb[(size_t)(ok ? base + corner_offset(d, k) : 0) * (PC_CV / 4)];
+    }
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {           // K3's arithmetic: corner order, weight 0 when out of range
+      const float w = (t.in >> k & 1u) ? t.w[k] : 0.f;
+      acc.x += v[k].x * w;
+      acc.y += v[k].y * w;
+      acc.z += v[k].z * w;
+      acc.w += v[k].w * w;
+    }
+    *reinterpret_cast<float4*>(&xs[p * PC_XS + 4 * q]) = acc;
+  }
+}
+
+struct PcAtom {
+  int t, di, bc, y0, x0;
+};
+
+__device__ __forceinline__ PcAtom pc_atom(const vfd_voxel_desc& d, const PcGeom& g, int atom) {
+  PcAtom a;
+  a.t = atom / d.D;
+  a.di = atom - a.t * d.D;
+  a.bc = a.t / g.tiles_img;
+  const int ti = a.t - a.bc * g.tiles_img;
+  a.y0 = (ti / g.tc) * PC_TR;
+  a.x0 = (ti % g.tc) * PC_TC;
+  return a;
+}
+
+// Weight layout Wq (fragment order): [D][9 taps][Cv/4 = 16 quads][O][2 (h)][2 (s)], where the
+// reference channel is c*D + d with c = 4*quad + 2*h + s.  For iteration i = tap*16 + quad of
+// depth bin d, lane l of output block ob reads the float2 (s = 0, 1) at float2 index
+// (d*144 + i)*2*O + (ob*32 + (l & 31))*2 + (l >> 5).
+__global__ __launch_bounds__(PC_THREADS, 2) void pcv_main_k(vfd_voxel_desc d, PcGeom g,
+                                                           const float* __restrict__ vox,
+                                                           const float* __restrict__ invK,
+                                                           const float* __restrict__ E,
+                                                           const float* __restrict__ Wq,
+                                                           float* __restrict__ partial) {
+  __shared__ float xs[2][PC_NPOS * PC_XS];
+  const int grp = blockIdx.x;
+  const int a_lo = pc_lo(g, grp), a_hi = pc_lo(g, grp + 1);
+  if (a_lo >= a_hi) return;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int V = d.X * d.Y * d.Z;
+  const bool compute = wv < PC_WAVES;
+  // prologue: the gather waves build the first atom
+  if (!compute) {
+    const PcAtom a = pc_atom(d, g, a_lo);
+    pc_gather(d, xs[0], vox + (size_t)(a.bc / d.N) * V * PC_CV, invK + a.bc * 16, E + a.bc * 16, a.y0, a.x0,
+              d.dbins[a.di], wv - PC_WAVES);
+  }
+  __syncthreads();
+  if (!compute) {
+    // producer: atom a+1 into the other buffer while the compute waves run atom a
+    for (int atom = a_lo; atom < a_hi; ++atom) {
+#ifdef VFD_PC_NOGATHER
+      if (false) {                                    // experiment: no gather after the first atom
+#else
+      if (atom + 1 < a_hi) {
+#endif
+        const PcAtom a = pc_atom(d, g, atom + 1);
+        pc_gather(d, xs[(atom + 1 - a_lo) & 1], vox + (size_t)(a.bc / d.N) * V * PC_CV, invK + a.bc * 16,
+                  E + a.bc * 16, a.y0, a.x0, d.dbins[a.di], wv - PC_WAVES);
+      }
+      __syncthreads();
+    }
+    return;
+  }
+  const int li = lane & 31, lh = lane >> 5;
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  // A-fragment LDS offsets of the wave's 4 pixel blocks at tap (0, 0), channel 2*lh
+  int aoff[4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const int ip = 32 * a + li;                      // tile pixel of this lane's A row
+    aoff[a] = ((ip >> 4) * PC_HC + (ip & 15)) * PC_XS + 2 * lh;
+  }
+  const float2* wlane = reinterpret_cast<const float2*>(Wq) + (size_t)(wv * 64 + li) * 2 + lh;
+  // weight fragments of the flattened (atom, iteration) stream, PC_PF iterations ahead
+  float2 bq[PC_PF][2];
+  int pf_atom = a_lo, pf_it = 0;
+  auto prefetch = [&](int slot) {
+    if (pf_atom < a_hi) {
+#ifdef VFD_PC_SAMEW
+      const int di = 0;                               // experiment: every atom reads bin 0's weights
+#else
+      const int di = pf_atom % d.D;
+#endif
+      const float2* w = wlane + ((size_t)di * PC_ITERS + pf_it) * (2 * PC_O);
+      bq[slot][0] = w[0];
+      bq[slot][1] = w[64];
+      if (++pf_it == PC_ITERS) { pf_it = 0; ++pf_atom; }
+    }
+  };
+#pragma unroll
+  for (int k = 0; k < PC_PF; ++k) prefetch(k);
+  int slot = 0;
+  int tile = a_lo / d.D;
+  for (int atom = a_lo; atom < a_hi; ++atom) {
+    const int t = atom / d.D;
+    if (t != tile) {                                  // flush the finished tile's partial
+      float* dst = partial + ((size_t)grp * 2 + slot) * PC_FRAG + (size_t)wv * (PC_FRAG / PC_WAVES);
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            dst[((a * 2 + b) * 16 + r) * 64 + lane] = acc[a][b][r];
+            acc[a][b][r] = 0.f;
+          }
+      slot = 1;
+      tile = t;
+    }
+    const float* xb = xs[(atom - a_lo) & 1];
+    // A fragments software-pipelined one iteration ahead (LDS latency off the MFMA path)
+    float2 afc[4], afn[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) afc[a] = *reinterpret_cast<const float2*>(&xb[aoff[a]]);
+#pragma unroll 1
+    for (int tap = 0; tap < 9; ++tap) {
+      const int ky = tap / 3, kx = tap - 3 * ky;
+      const float* xt = xb + (ky * PC_HC + kx) * PC_XS;
+      const int tn = tap + 1, kyn = tn / 3, kxn = tn - 3 * kyn;
+      const float* xn = xb + (kyn * PC_HC + kxn) * PC_XS;         // next tap (unused after tap 8)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int ring = q % PC_PF;                   // 16 % PC_PF == 0: static ring slots
+        const float2 b0 = bq[ring][0], b1 = bq[ring][1];
+        prefetch(ring);
+        if (q < 15) {
+#pragma unroll
+          for (int a = 0; a < 4; ++a) afn[a] = *reinterpret_cast<const float2*>(&xt[aoff[a] + 4 * (q + 1)]);
+        } else if (tap < 8) {
+#pragma unroll
+          for (int a = 0; a < 4; ++a) afn[a] = *reinterpret_cast<const float2*>(&xn[aoff[a]]);
+        }
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int a = 0; a < 4; ++a) {
+            const float av = s ? afc[a].y : afc[a].x;
+            acc[a][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, s ? b0.y : b0.x, acc[a][0], 0, 0, 0);
+            acc[a][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, s ? b1.y : b1.x, acc[a][1], 0, 0, 0);
+          }
+#pragma unroll
+        for (int a = 0; a < 4; ++a) afc[a] = afn[a];
+      }
+    }
+    __syncthreads();                                  // buffer handed back to the gather waves
+  }
+  float* dst = partial + ((size_t)grp * 2 + slot) * PC_FRAG + (size_t)wv * (PC_FRAG / PC_WAVES);
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dst[((a * 2 + b) * 16 + r) * 64 + lane] = acc[a][b][r];
+}
+
+// Sum of each tile's partials (in workgroup order) + bias, LeakyReLU(0.1), stored into the
+// reflect-padded NHWC map out [B*N, h+2, w+2, O] (the input of reduce_dim's second conv).
+constexpr int PC_MAXC = 72;     // contributors of one tile (<= D + 1, D <= 64)
+__global__ __launch_bounds__(256) void pcv_reduce_k(vfd_voxel_desc d, PcGeom g, const float* __restrict__ partial,
+                                                    const float* __restrict__ bias, float* __restrict__ out) {
+  __shared__ int contrib[PC_MAXC];
+  __shared__ int ncontrib;
+  const int t = blockIdx.x;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int a0 = t * d.D, a1 = a0 + d.D;
+  if (threadIdx.x == 0) {
+    // workgroups whose atom range meets [a0, a1), in order; the first is the one containing a0
+    int gg = (int)(((long long)a0 * g.ngroup) / g.natom);
+    while (gg > 0 && pc_lo(g, gg) > a0) --gg;
+    while (pc_lo(g, gg + 1) <= a0) ++gg;
+    int n = 0;
+    for (; gg < g.ngroup && n < PC_MAXC; ++gg) {
+      const int lo = pc_lo(g, gg), hi = pc_lo(g, gg + 1);
+      if (lo >= a1) break;
+      if (hi <= a0 || lo >= hi) continue;
+      contrib[n++] = gg * 2 + (lo >= a0 ? 0 : 1);   // slot 0 iff the tile is the group's first
+    }
+    ncontrib = n;
+  }
+  __syncthreads();
+  const int nc = ncontrib;
+  const int bc = t / g.tiles_img, ti = t - bc * g.tiles_img;
+  const int y0 = (ti / g.tc) * PC_TR, x0 = (ti % g.tc) * PC_TC;
+  const int ho = d.h + 2, wo = d.w + 2;
+  float* ob = out + (size_t)bc * ho * wo * PC_O;
+  for (int f = 0; f < 4 * 2 * 16; ++f) {
+    const int a = f >> 5, bb = (f >> 4) & 1, r = f & 15;
+    float s = 0.f;
+    for (int k = 0; k < nc; ++k)
+      s += partial[(size_t)contrib[k] * PC_FRAG + (size_t)wv * (PC_FRAG / PC_WAVES) + (f * 64 + lane)];
+    // fragment -> (pixel, channel): C/D layout of v_mfma_f32_32x32x2_f32
+    const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    const int ip = 32 * a + row;
+    const int o = wv * 64 + bb * 32 + (lane & 31);
+    const int py = y0 + (ip >> 4), px = x0 + (ip & 15);
+    if (py >= d.h || px >= d.w) continue;
+    float v = s + bias[o];
+    v = v > 0.f ? v : v * 0.1f;
+    int rows[3], cols[3], nr, ncol;
+    pad_sets(py, d.h, true, rows, &nr);
+    pad_sets(px, d.w, true, cols, &ncol);
+    for (int i = 0; i < nr; ++i)
+      for (int j = 0; j < ncol; ++j) ob[((size_t)rows[i] * wo + cols[j]) * PC_O + o] = v;
+  }
+}
+
+static int pc_resident() {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    cus = 256;
+  return cus * PC_WG_PER_CU;
+}
+
+// Workgroup count: a multiple of the resident capacity, large enough that no range exceeds D
+// atoms (so a range touches at most two tiles: partial slots 0 and 1).
+static PcGeom pc_plan(const vfd_voxel_desc& d) {
+  PcGeom g = pc_geom(d, 1);
+  const int res = pc_resident();
+  const int need = (g.natom + d.D - 1) / d.D;
+  g.ngroup = res * ((need + res - 1) / res);
+  return g;
+}
+
+}  // namespace vfd
+
+using namespace vfd;
+
+extern "C" {
+
+size_t vfd_proj_conv_fwd_workspace(const vfd_voxel_desc* d) {
+  if (!d || d->D <= 0 || d->h <= 0 || d->w <= 0) return 0;
+  return (size_t)pc_plan(*d).ngroup * 2 * PC_FRAG * sizeof(float);
+}
+
+int vfd_proj_conv_fwd(const vfd_voxel_desc* d, const float* vox, const float* invK, const float* E,
+                      const float* Wq, const float* bias, int out_channels, float* out, void* ws,
+                      size_t ws_bytes, void* stream) {
+  VFD_REQUIRE(d && vox && invK && E && Wq && bias && out, "proj_conv_fwd: null argument");
+  VFD_REQUIRE(d->Cv == PC_CV, "proj_conv_fwd: Cv must be %d (got %d)", PC_CV, d->Cv);
+  VFD_REQUIRE(out_channels == PC_O, "proj_conv_fwd: output channels must be %d (got %d)", PC_O, out_channels);
+  VFD_REQUIRE(d->B > 0 && d->N > 0 && d->h >= 2 && d->w >= 2 && d->D > 0 && d->D <= 64,
+              "proj_conv_fwd: bad shape (h, w >= 2, 0 < D <= 64)");
+  VFD_REQUIRE(ws && ws_bytes >= vfd_proj_conv_fwd_workspace(d), "proj_conv_fwd: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  ProfScope ps(K_PROJ_CONV_FWD, s);
+  const PcGeom g = pc_plan(*d);
+  float* partial = (float*)ws;
+  pcv_main_k<<<g.ngroup, PC_THREADS, 0, s>>>(*d, g, vox, invK, E, Wq, partial);
+  pcv_reduce_k<<<g.ntile, 256, 0, s>>>(*d, g, partial, bias, out);
+  return fail_launch("proj_conv_fwd");
+}
+
+}  // extern "C"

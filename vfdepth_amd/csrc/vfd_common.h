@@ -26,7 +26,7 @@ int fail_launch(const char* what);   // reads hipGetLastError, returns VFD_ELAUN
 enum KernelId {
   K_MASK_DOWN = 0, K_FUSE_DEPTH_FWD, K_FUSE_DEPTH_BWD, K_FUSE_POSE_FWD, K_FUSE_POSE_BWD,
   K_VPROJ_FWD, K_VPROJ_BWD, K_VIEW_STATS, K_VIEW_APPLY, K_VIEW_BWD, K_PHOTO_FWD, K_PHOTO_BWD,
-  K_SMOOTH_FWD, K_SMOOTH_BWD, K_FUSION_PLAN, K_AGGREGATE, K_VPROJ_PLAN, K_COUNT
+  K_SMOOTH_FWD, K_SMOOTH_BWD, K_FUSION_PLAN, K_AGGREGATE, K_VPROJ_PLAN, K_PROJ_CONV_FWD, K_COUNT
 };
 void prof_begin(int id, hipStream_t s);
 void prof_end(int id, hipStream_t s);
@@ -138,6 +138,60 @@ __device__ __forceinline__ T block_sum_all(T v, T* lds) {
   if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = v;
   __syncthreads();
   return lds[0] + lds[1] + lds[2] + lds[3];
+}
+
+// ---------------------------------------------------------------- K3 geometry (frustum samples)
+struct Tri {
+  int x0, y0, z0;
+  float w[8];     // tnw, tne, tsw, tse, bnw, bne, bsw, bse
+  unsigned in;
+};
+
+// volumetric_fusionnet.py:245-260 + ATen grid_sampler_3d weights
+__device__ __forceinline__ Tri frustum_sample(const vfd_voxel_desc& d, const float* __restrict__ iK,
+                                              const float* __restrict__ E, int px, int py, float dep) {
+  float fx = (float)px, fy = (float)py;
+  float r0 = iK[0] * fx + iK[1] * fy + iK[2];
+  float r1 = iK[4] * fx + iK[5] * fy + iK[6];
+  float r2 = iK[8] * fx + iK[9] * fy + iK[10];
+  float p0 = dep * r0, p1 = dep * r1, p2 = dep * r2;
+  float w0 = E[0] * p0 + E[1] * p1 + E[2] * p2 + E[3];
+  float w1 = E[4] * p0 + E[5] * p1 + E[6] * p2 + E[7];
+  float w2 = E[8] * p0 + E[9] * p1 + E[10] * p2 + E[11];
+  float gx = (w0 - d.str[0]) / d.len[0] * 2.f - 1.f;
+  float gy = (w1 - d.str[1]) / d.len[1] * 2.f - 1.f;
+  float gz = (w2 - d.str[2]) / d.len[2] * 2.f - 1.f;
+  float ix = unnorm_ac(gx, d.X), iy = unnorm_ac(gy, d.Y), iz = unnorm_ac(gz, d.Z);
+  Tri t;
+  t.in = 0;
+  if (!(finitef(ix) && finitef(iy) && finitef(iz))) {
+    t.x0 = t.y0 = t.z0 = -4;
+    for (int k = 0; k < 8; ++k) t.w[k] = 0.f;
+    return t;
+  }
+  float fx0 = floorf(ix), fy0 = floorf(iy), fz0 = floorf(iz);
+  float fx1 = fx0 + 1.f, fy1 = fy0 + 1.f, fz1 = fz0 + 1.f;
+  float ax[2] = {fx1 - ix, ix - fx0}, ay[2] = {fy1 - iy, iy - fy0}, az[2] = {fz1 - iz, iz - fz0};
+  t.x0 = (int)fminf(fmaxf(fx0, -4.f), (float)d.X + 4.f);
+  t.y0 = (int)fminf(fmaxf(fy0, -4.f), (float)d.Y + 4.f);
+  t.z0 = (int)fminf(fmaxf(fz0, -4.f), (float)d.Z + 4.f);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    int dx = k & 1, dy = (k >> 1) & 1, dz = k >> 2;
+    int xx = t.x0 + dx, yy = t.y0 + dy, zz = t.z0 + dz;
+    bool ok = xx >= 0 && xx < d.X && yy >= 0 && yy < d.Y && zz >= 0 && zz < d.Z;
+    t.w[k] = ax[dx] * ay[dy] * az[dz];
+    t.in |= (ok ? 1u : 0u) << k;
+  }
+  return t;
+}
+
+__device__ __forceinline__ int tri_index(const vfd_voxel_desc& d, const Tri& t, int k) {
+  return ((t.z0 + (k >> 2)) * d.Y + (t.y0 + ((k >> 1) & 1))) * d.X + (t.x0 + (k & 1));
+}
+
+__device__ __forceinline__ int corner_offset(const vfd_voxel_desc& d, int k) {
+  return (k & 1) + ((k >> 1) & 1) * d.X + (k >> 2) * d.X * d.Y;
 }
 
 __host__ __device__ inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }

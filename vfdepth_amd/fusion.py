@@ -19,6 +19,8 @@ The two kernels order their channels voxel-row-major (z*(C+1)+c, d*Cv+c) so that
 and store is a contiguous row; `_reduce` permutes the conv weight's input channels to match,
 which leaves the convolution (and the parameters / state dict) exactly the reference's.
 """
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -156,9 +158,22 @@ class VFNet(nn.Module):
         return KN.FuseDepth.apply(space, P, self._mask_lowres(inputs, space), K, inputs['extrinsics_inv'],
                                   wz, self.conv_non_overlap[0].bias, self.conv_overlap[0].bias)
 
+    def fused_projection(self, voxel_feat):
+        """K3C (K3 fused into reduce_dim's first conv, fp32 MFMA) applies: 64 voxel channels, 256
+        conv outputs, <= 64 depth bins, fp32 nets (under bf16 autocast the conv runs on MIOpen's
+        bf16 path instead), not disabled by VFD_PROJ_CONV=0."""
+        c0 = self.reduce_dim[0]
+        return (os.environ.get('VFD_PROJ_CONV', '1') != '0' and voxel_feat.shape[-1] == 64
+                and c0.out_channels == 256 and self.proj_d_bins <= 64
+                and not torch.is_autocast_enabled('cuda'))
+
     def project_voxel_into_image(self, voxel_feat, inv_K, extrinsics):
         """K3 + reduce_dim: voxel features [B,V,Cv] -> [B*N, feat_out, h, w]."""
         space = self.space(voxel_feat.device)
+        if self.fused_projection(voxel_feat):
+            c0, c1 = self.reduce_dim[0], self.reduce_dim[3]
+            y0 = KN.ProjConv.apply(space, voxel_feat, inv_K, extrinsics, c0.weight, c0.bias)
+            return F.leaky_relu(F.conv2d(y0, c1.weight, c1.bias), 0.1, inplace=True).contiguous()
         return self._reduce(KN.VoxelProject.apply(space, voxel_feat, inv_K, extrinsics))
 
     def forward(self, inputs, feats_agg):

@@ -325,6 +325,82 @@ class VoxelProject(torch.autograd.Function):
         return None, dvox, None, None
 
 
+def proj_conv_weight_fragments(w, Cv, D):
+    """reduce_dim[0] weight [O, Cv*D, 3, 3] (reference channel c*D + d) -> the fused kernel's
+    fragment-ordered copy [D, 3, 3, Cv/4, O, 2, 2] (c = 4q + 2h + s; projconv.hip, pcv_main_k)."""
+    O = w.shape[0]
+    return w.reshape(O, Cv // 4, 2, 2, D, 3, 3).permute(4, 5, 6, 1, 0, 2, 3).contiguous()
+
+
+class ProjConv(torch.autograd.Function):
+    """K3C: voxel features [B,V,Cv] -> LeakyReLU(conv3x3_reflect(frustum samples) + bias): K3's
+    trilinear resampling fused into reduce_dim's first conv (fp32 MFMA implicit GEMM; the
+    [B*N, Cv*D, h, w] frustum features never reach HBM).  Output: the reflect-padded
+    channels-last input of reduce_dim's second conv, logical [B*N, O, h+2, w+2].
+
+    Backward: the frustum features are recomputed by K3, then MIOpen's data / weight gradients and
+    K3's planned backward give d voxel, d weight, d bias."""
+
+    @staticmethod
+    @_amp_fwd
+    def forward(ctx, space, vox, invK, E, w0, bias):
+        lib = L.load()
+        vox, invK, E = (_dev(t, n) for t, n in ((vox, 'voxel'), (invK, 'inv_K'), (E, 'extrinsics')))
+        w0, bias = _dev(w0, 'reduce_dim weight'), _dev(bias, 'reduce_dim bias')
+        B, V, Cv = vox.shape
+        N, O = E.shape[1], w0.shape[0]
+        wq = proj_conv_weight_fragments(w0, Cv, space.D)
+        out = torch.empty(B * N, O, space.h + 2, space.w + 2, device=vox.device, memory_format=torch.channels_last)
+        d = space.desc(B, N, Cv=Cv)
+        nbytes = lib.vfd_proj_conv_fwd_workspace(ctypes.byref(d))
+        ws = _ws(nbytes, vox.device)
+        L.check(lib.vfd_proj_conv_fwd(ctypes.byref(d), vox.data_ptr(), invK.data_ptr(), E.data_ptr(), wq.data_ptr(),
+                                      bias.data_ptr(), O, out.data_ptr(), ws.data_ptr(), nbytes, L.stream()),
+                'proj_conv_fwd')
+        ctx.space, ctx.shape = space, (B, N, V, Cv, O)
+        ctx.plan = None
+        if ctx.needs_input_grad[1]:
+            nbytes = lib.vfd_voxel_project_plan_bytes(ctypes.byref(d))
+            ctx.plan = torch.empty(nbytes, dtype=torch.uint8, device=vox.device)
+            L.check(lib.vfd_voxel_project_plan(ctypes.byref(d), invK.data_ptr(), E.data_ptr(), ctx.plan.data_ptr(),
+                                               nbytes, L.stream()), 'voxel_project_plan')
+        ctx.save_for_backward(vox, invK, E, w0, out)
+        return out
+
+    @staticmethod
+    @_amp_bwd
+    def backward(ctx, g):
+        lib = L.load()
+        vox, invK, E, w0, out = ctx.saved_tensors
+        space = ctx.space
+        B, N, V, Cv, O = ctx.shape
+        d = space.desc(B, N, Cv=Cv)
+        g = _channels_last(g, 'grad')
+        # adjoint of the reflect padding, then of the LeakyReLU (its sign from the output)
+        g_in = torch.ops.aten.reflection_pad2d_backward(g, out[:, :, 1:-1, 1:-1], [1, 1, 1, 1])
+        inner = out[:, :, 1:-1, 1:-1]
+        g_pre = g_in * torch.where(inner > 0, 1.0, 0.1)
+        x = torch.empty(B * N, Cv * space.D, space.h + 2, space.w + 2, device=g.device,
+                        memory_format=torch.channels_last)
+        L.check(lib.vfd_voxel_project_fwd(ctypes.byref(d), vox.data_ptr(), invK.data_ptr(), E.data_ptr(),
+                                          x.data_ptr(), L.stream()), 'voxel_project_fwd (recompute)')
+        w_perm = proj_conv_weight(w0, Cv, space.D)
+        mask = (ctx.needs_input_grad[1], ctx.needs_input_grad[4], ctx.needs_input_grad[5])
+        dx, dw, db = torch.ops.aten.convolution_backward(g_pre, x, w_perm, [O], [1, 1], [0, 0], [1, 1], False,
+                                                         [0, 0], 1, [mask[0], mask[1], mask[2]])
+        dvox = dw0 = None
+        if mask[0]:
+            dx = _channels_last(dx, 'd frustum features')
+            dvox = torch.empty(B, V, Cv, device=g.device)
+            L.check(lib.vfd_voxel_project_bwd_planned(ctypes.byref(d), dx.data_ptr(), ctx.plan.data_ptr(),
+                                                      ctx.plan.numel(), dvox.data_ptr(), L.stream()),
+                    'voxel_project_bwd')
+        if mask[1]:
+            dw0 = dw.reshape(O, space.D, Cv, 3, 3).transpose(1, 2).reshape(O, Cv * space.D, 3, 3)
+        ctx.plan = None
+        return None, dvox, None, None, dw0, db if mask[2] else None
+
+
 # =============================================================================================
 # View synthesis (K4)
 # =============================================================================================

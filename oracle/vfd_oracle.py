@@ -404,6 +404,74 @@ def to_depth(disp, K0, cfg):
     return d * K0[:, 0:1, 0:1].unsqueeze(2) / t['focal_length_scale']
 
 
+def augment_extrinsics(E, aug_angle, angle):
+    """A17 (volumetric_fusionnet.py:269-287): a random rotation applied in front of every camera's
+    extrinsics.  `angle` [B, N, 3] stands for the reference's `torch.rand(b, cam, 3)` draw;
+    (angle - 0.5) * aug_angle[i] is used as an axis-angle in RADIANS (the config's values are
+    called degrees, the reference feeds them to axis_angle_to_matrix unchanged)."""
+    a = (angle - 0.5) * torch.tensor([float(v) for v in aug_angle], dtype=angle.dtype)
+    T = torch.eye(4, dtype=E.dtype).repeat(*E.shape[:2], 1, 1)
+    T[:, :, :3, :3] = axis_angle_to_matrix(a).to(E.dtype)
+    return T @ E
+
+
+def virtual_depth(src_depth, src_mask, src_invK, tar_depth, tar_invK, src_K, T, min_depth, max_depth):
+    """A17 (view_rendering.py:84-116): the source depth map, expressed in the novel view's camera
+    (z of T @ backproject(src)), backward-warped into the novel view through the novel view's own
+    depth; NaN -> 2.0, masks by nearest lookup, OOB and the [min, max] range (out-of-range values
+    replaced by the bound: no gradient through them).  -> depth [B,1,H,W], mask [B,1,H,W]."""
+    B, _, H, W = src_depth.shape
+    z = torch.matmul(T[:, :3, :], backproject(src_invK, src_depth)).reshape(B, 3, H, W)[:, 2:3]
+    gx, gy = reproject(src_K, torch.inverse(T), backproject(tar_invK, tar_depth), H, W)
+    d = sample2d(z, gx, gy, 'bilinear')
+    m = sample2d(src_mask, gx, gy, 'nearest')
+    d = torch.where(torch.isnan(d), torch.full_like(d, 2.0), d)
+    m = torch.where(torch.isnan(m), torch.zeros_like(m), m)
+    bad = ((gx > 1) | (gx < -1) | (gy > 1) | (gy < -1)).unsqueeze(1)
+    vmin = d > min_depth
+    d = torch.where(vmin, d, torch.full_like(d, min_depth))
+    vmax = d < max_depth
+    d = torch.where(vmax, d, torch.full_like(d, max_depth))
+    mask = (~bad).to(d.dtype) * m * vmin.to(d.dtype) * vmax.to(d.dtype)
+    return d.view(B, 1, H, W), mask.view(B, 1, H, W)
+
+
+def depth_synthesis(inputs, outputs, cam, cfg):
+    """A17 (view_rendering.py:201-241): tform_depth / tform_depth_mask lists of camera `cam`
+    (sources rel_cam_list[cam] + [cam], each warped into the augmented view of `cam`)."""
+    t = cfg['training']
+    N = cfg['data']['num_cams']
+    aug_ext = inputs['extrinsics_aug'][:, cam]
+    aug_inv = torch.inverse(aug_ext)
+    ref_K, ref_invK = inputs[('K', 0)][:, cam], inputs[('inv_K', 0)][:, cam]
+    view = outputs[('cam', cam)]
+    depths, masks = [], []
+    for src in list(cfg['data']['rel_cam_list'][cam]) + [cam]:
+        if src >= N:
+            continue
+        rel = torch.matmul(aug_inv, inputs['extrinsics'][:, src])
+        d, m = virtual_depth(outputs[('cam', src)][('depth', 0)], inputs['mask'][:, src],
+                             inputs[('inv_K', 0)][:, src], view[('depth', 0, 'aug')], ref_invK,
+                             inputs[('K', 0)][:, src], rel, t['min_depth'], t['max_depth'])
+        depths.append(d)
+        masks.append(m)
+    view[('tform_depth', 0)] = depths
+    view[('tform_depth_mask', 0)] = masks
+
+
+def depth_synthesis_loss(view):
+    """A17 (depth_synthesis_loss.py:15-45): consistency clamp(|a - t| / (a + t + 1e-8), 0, 1),
+    masked mean pooled over all sources; plain gradient smoothness of disp_aug / mean."""
+    aug = view[('depth', 0, 'aug')]
+    pl = torch.cat([torch.clamp((aug - d).abs() / (aug + d + 1e-8), 0., 1.) for d in view[('tform_depth', 0)]], 0)
+    pm = torch.cat(list(view[('tform_depth_mask', 0)]), 0)
+    con = masked_mean(pl, pm)
+    disp = view[('disp', 0, 'aug')]
+    nd = disp / (disp.mean(2, True).mean(3, True) + 1e-8)
+    sm = (nd[..., :-1] - nd[..., 1:]).abs().mean() + (nd[..., :-1, :] - nd[..., 1:, :]).abs().mean()
+    return con, sm
+
+
 # =============================================================================================
 # Losses (reference models/losses/*)
 # =============================================================================================
@@ -498,13 +566,15 @@ def depth_errors(pred, gt):
 # =============================================================================================
 # Whole step (A1/A2/A4/A5 restated around caller-supplied dense layers)
 # =============================================================================================
-def process_batch(nets, inputs, cfg, noise):
+def process_batch(nets, inputs, cfg, noise, aug_angles=None):
     """Restated `VFDepthAlgo.process_batch` (vfdepth.py:191-313) for the fusion configs.
 
     `nets` supplies the dense (non-hot-path) layers as callables/tensors shared with the
     product via one state dict: pose_encoder, pose_conv1x1, pose_reduce_dim, pose_decoder,
     depth_encoder, depth_conv1x1, depth_reduce_dim, depth_decoder, w_no, b_no, w_o, b_o.
-    `noise[cam]` is the identity-loss noise for camera `cam`.
+    `noise[cam]` is the identity-loss noise for camera `cam`; with training.aug_depth,
+    `aug_angles` [B, N, 3] stands for augment_extrinsics' torch.rand draw (depth synthesis:
+    volumetric_fusionnet.py:313-317, fusion_depthnet.py:79-86, depth_synthesis_loss.py).
     Returns (outputs, losses) in the reference schema.
     """
     t = cfg['training']
@@ -541,11 +611,23 @@ def process_batch(nets, inputs, cfg, noise):
     proj = project_voxels(spec, vox, invK_l, E)
     proj = torch.stack([nets.depth_reduce_dim(p) for p in proj], 1).reshape(B * N, -1, spec.h, spec.w)
     disp = nets.depth_decoder(feats[:lvl] + [proj])
+    aug = bool(t.get('aug_depth', False))
+    if aug:
+        inputs['extrinsics_aug'] = augment_extrinsics(E, t['aug_angle'], aug_angles)
+        proj_aug = project_voxels(spec, vox, invK_l, inputs['extrinsics_aug'])
+        proj_aug = torch.stack([nets.depth_reduce_dim(p) for p in proj_aug], 1).reshape(B * N, -1, spec.h, spec.w)
+        disp_aug = nets.depth_decoder(feats[:lvl] + [proj_aug])
     for c in range(N):
         for k, v in disp.items():
             outputs[('cam', c)][k] = v.view(B, N, *v.shape[1:])[:, c]
         for s in t['scales']:
             outputs[('cam', c)][('depth', s)] = to_depth(outputs[('cam', c)][('disp', s)], inputs[('K', 0)][:, c], cfg)
+        if aug:
+            for k, v in disp_aug.items():
+                outputs[('cam', c)][k + ('aug',)] = v.view(B, N, *v.shape[1:])[:, c]
+            for s in t['scales']:
+                outputs[('cam', c)][('depth', s, 'aug')] = to_depth(outputs[('cam', c)][('disp', s, 'aug')],
+                                                                    inputs[('K', 0)][:, c], cfg)
 
     total = 0.0
     logs = {}
@@ -553,6 +635,13 @@ def process_batch(nets, inputs, cfg, noise):
         rp = relative_poses(inputs, outputs[('cam', c)], c, cfg)
         view_rendering(inputs, outputs[('cam', c)], c, rp, cfg)
         cl, terms = cam_loss(inputs, outputs[('cam', c)], c, cfg, noise[c])
+        if aug:
+            lc = cfg['loss']
+            depth_synthesis(inputs, outputs, c, cfg)
+            con, sm = depth_synthesis_loss(outputs[('cam', c)])
+            syn = lc['depth_con_coeff'] * con + lc['depth_sm_coeff'] * sm
+            cl = cl + syn
+            terms.update({'depth_loss': syn, 'depth_sm_loss': sm, 'depth_con_loss': con, 'cam_loss': cl})
         total = total + cl
         d = outputs[('cam', c)][('depth', 0)].detach()
         terms.update({'depth/mean': d.mean(), 'depth/max': d.max(), 'depth/min': d.min()})

@@ -5,3 +5,4 @@ for v in base samew nogather pf8 pf2; do
   echo "== $v" >> gpurun_out/pcvar.log
   VFD_LIB=$L timeout -k 10 120 python tools/micro_projconv.py 2>&1 | grep -v amdgpu.ids >> gpurun_out/pcvar.log || exit 1
 done
+timeout -k 10 300 python tools/micro_convbwd.py > gpurun_out/convbwd.log 2>&1

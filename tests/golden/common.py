@@ -178,6 +178,38 @@ def step_cfg():
                                  proj_d_bins=16, focal_length_scale=30)
 
 
+def step_aug_cfg():
+    """The reduced step config with the depth-synthesis branch (ddad_surround_fusion_augdepth.yaml:
+    aug_depth, aug_angle [15, 15, 40], depth_con_coeff 0.03, depth_sm_coeff 0.05)."""
+    cfg = step_cfg()
+    cfg['training']['aug_depth'] = True
+    cfg['loss'].update({'depth_con_coeff': 0.03, 'depth_sm_coeff': 0.05})
+    return cfg
+
+
+def virtual_depth_case():
+    """Inputs of ViewRendering.get_virtual_depth (view_rendering.py:84-116): B=2, 24x40, a source
+    camera warped into a rotated novel view of a neighbouring camera; depth ranges that exercise
+    the [min, max] clamps and the OOB / mask rules."""
+    B, H, W = 2, 24, 40
+    gen = torch.Generator().manual_seed(51)
+    K = torch.from_numpy(synth.rig_intrinsics(6, H, W)).float()
+    E = torch.from_numpy(synth.rig_extrinsics(6)).float()
+    gt = synth.ground_plane_depth(K.double().numpy(), E.double().numpy(), H, W, 1.5, 60.0)
+    src, tar = 0, 0                  # the `[cam]` source of view_rendering.py:210 (neighbours: step fixture)
+    src_depth = gt[src].unsqueeze(0).repeat(B, 1, 1, 1) * (0.7 + 0.6 * torch.rand(B, 1, H, W, generator=gen))
+    tar_depth = gt[tar].unsqueeze(0).repeat(B, 1, 1, 1) * (0.7 + 0.6 * torch.rand(B, 1, H, W, generator=gen))
+    src_mask = random_mask(gen, (B, 1, H, W))
+    aa = 0.3 * (torch.rand(B, 1, 3, generator=gen) - 0.5)
+    Rm = torch.eye(4).repeat(B, 1, 1)
+    Rm[:, :3, :3] = axis_angle_to_matrix(aa)[:, 0]
+    E_aug = Rm @ E[tar]
+    T = torch.inverse(E_aug) @ E[src]
+    return {'src_depth': src_depth, 'src_mask': src_mask, 'src_invK': torch.inverse(K[src]).repeat(B, 1, 1),
+            'tar_depth': tar_depth, 'tar_invK': torch.inverse(K[tar]).repeat(B, 1, 1),
+            'src_K': K[src].repeat(B, 1, 1), 'T': T, 'min_depth': 1.5, 'max_depth': 40.0}
+
+
 def mono_cfg():
     return C.mono_cfg(batch_size=1)
 

@@ -1,0 +1,102 @@
+"""The DDP path of the fusion step on the GPU (reference models/vfdepth.py:56-71, utils/ddp.py:10-29):
+an NCCL (= RCCL) process group of world size 1 on the MI355X, `VFDepthAlgo` with ddp_enable on
+the fusion config — SyncBatchNorm conversion, both nets DDP-wrapped, the pose net called twice
+per step through DDP, backward through DDP's reducer — against the same step without DDP."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+
+import common as G
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device('cuda:0')
+
+
+@pytest.fixture(scope='module')
+def nccl_group():
+    if not torch.cuda.is_available():
+        pytest.skip('no HIP device')
+    from vfdepth_amd import _lib
+    _lib.load()
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    os.environ.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+    dist.init_process_group('nccl', init_method=f'tcp://127.0.0.1:{port}', rank=0, world_size=1)
+    yield
+    dist.destroy_process_group()
+
+
+def _step(ddp, inputs, noise):
+    from vfdepth_amd.layers import seeded_state_dict
+    from vfdepth_amd.vfdepth import VFDepthAlgo
+    cfg = G.step_cfg()
+    cfg['ddp'].update({'ddp_enable': ddp, 'world_size': 1, 'gpus': [0]})
+    algo = VFDepthAlgo(cfg, 0)
+    for m in algo.models.values():
+        inner = m.module if hasattr(m, 'module') else m
+        inner.load_state_dict(seeded_state_dict(inner, seed=G.STEP_SEED))
+    algo.set_train()
+    outputs, losses = algo.process_batch({k: v.clone() if torch.is_tensor(v) else v for k, v in inputs.items()},
+                                         0, noise=noise)
+    losses['total_loss'].backward()
+    torch.cuda.synchronize()
+    grads = {}
+    for name, m in algo.models.items():
+        inner = m.module if hasattr(m, 'module') else m
+        grads[name] = {k: p.grad.detach().clone() for k, p in inner.named_parameters() if p.grad is not None}
+    return algo, outputs, losses, grads
+
+
+def _rel(ga, gb):
+    num = sum(float((ga[k].double() - gb[k].double()).pow(2).sum()) for k in gb)
+    den = sum(float(gb[k].double().pow(2).sum()) for k in gb)
+    return (num / max(den, 1e-300)) ** 0.5
+
+
+def test_ddp_fusion_step_world1_matches_plain(nccl_group):
+    from torch.nn.parallel import DistributedDataParallel as DDP
+    from vfdepth_amd import kernels as KN
+    from vfdepth_amd import synth
+    cfg = G.step_cfg()
+    inputs = synth.make_batch(cfg, seed=5, device=DEV)
+    fx = __import__('conftest').golden('step_small.npz')
+    noise = torch.stack([torch.tensor(fx[f'noise_c{c}']) for c in range(6)]).to(DEV)
+    # geometry products built once per step even though DDP re-packs the inputs dict per call
+    builds = {'plan': 0, 'mask': 0}
+    orig_build, orig_mask = KN.FusionPlan.build, KN.mask_lowres
+
+    def counting_build(self):
+        if self.buf is None:
+            builds['plan'] += 1
+        return orig_build(self)
+
+    def counting_mask(space, mask):
+        builds['mask'] += 1
+        return orig_mask(space, mask)
+    KN.FusionPlan.build, KN.mask_lowres = counting_build, counting_mask
+    try:
+        algo, out_d, loss_d, grad_d = _step(True, inputs, noise)
+    finally:
+        KN.FusionPlan.build, KN.mask_lowres = orig_build, orig_mask
+    assert builds == {'plan': 1, 'mask': 1}, builds
+    assert all(isinstance(m, DDP) for m in algo.models.values())
+    for m in algo.models.values():
+        mods = list(m.module.modules())
+        assert not any(type(x) is torch.nn.BatchNorm2d for x in mods), 'BatchNorm2d left unconverted'
+        assert any(isinstance(x, torch.nn.SyncBatchNorm) for x in mods)
+    _, out_p, loss_p, grad_p = _step(False, inputs, noise)
+    _, _, _, grad_p2 = _step(False, inputs, noise)
+    for k in ('total_loss', 'reproj_loss', 'spatio_loss', 'spatio_tempo_loss', 'smooth'):
+        a, b = float(loss_d[k]), float(loss_p[k])
+        assert abs(a - b) <= 1e-5 * abs(b) + 1e-7, f'{k}: DDP {a} vs plain {b}'
+    for c in range(6):
+        dd, dp = out_d[('cam', c)][('depth', 0)], out_p[('cam', c)][('depth', 0)]
+        assert float((dd - dp).abs().max()) <= 1e-5 * float(dp.abs().max()), f'depth cam {c}'
+    for net in ('depth_net', 'pose_net'):
+        spread = _rel(grad_p2[net], grad_p[net])        # eager-vs-eager (atomic-order) spread
+        rel = _rel(grad_d[net], grad_p[net])
+        assert rel <= max(1e-5, 4.0 * spread), f'{net}: DDP vs plain gradient rel diff {rel:.3g} (spread {spread:.3g})'

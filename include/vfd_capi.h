@@ -159,6 +159,26 @@ int vfd_view_bwd(const vfd_view_desc* d, const float* depth, const float* invK, 
                  const float* mask, const float* coef, const float* g_color, const float* g_ovl,
                  float* d_depth, float* d_M, void* workspace, size_t ws_bytes, void* stream);
 
+/* ------------------------------------------------------------------ depth synthesis (aug_depth) */
+typedef struct vfd_depthsyn_desc {
+  int32_t B, N, H, W;
+  int32_t S;             /* source slots per target camera (rel_cam_list[c] + [c])          */
+  float min_depth, max_depth;   /* training.min_depth / max_depth                          */
+  const int32_t* src_tab;       /* [N, S] device: source camera of each slot (-1: absent)  */
+} vfd_depthsyn_desc;
+
+/* get_virtual_depth for every (target camera, source slot) (view_rendering.py:84-116, 201-241):
+ * aug_depth [B,N,H,W] (depth at the augmented view of each camera), depth [B,N,H,W] (each
+ * camera's depth), mask [B,N,H,W], invK [B,N,4,4] (scale 0), M [B,N,S,3,4] = (K_src @ T^-1)[:3],
+ * zrow [B,N,S,4] = T[2, :] with T = E_aug[c]^-1 E[src]  ->  tform_depth, tform_mask [B,N,S,H,W]. */
+int vfd_depth_syn_fwd(const vfd_depthsyn_desc* d, const float* aug_depth, const float* depth, const float* mask,
+                      const float* invK, const float* M, const float* zrow, float* tform_depth, float* tform_mask,
+                      void* stream);
+/* g [B,N,S,H,W] (d tform_depth) -> d_aug [B,N,H,W] (written), d_depth [B,N,H,W] (zeroed here, atomics). */
+int vfd_depth_syn_bwd(const vfd_depthsyn_desc* d, const float* aug_depth, const float* depth, const float* mask,
+                      const float* invK, const float* M, const float* zrow, const float* g, float* d_aug,
+                      float* d_depth, void* stream);
+
 /* ------------------------------------------------------------------ photometric losses (K5) */
 typedef struct vfd_photo_desc {
   int32_t B, N, H, W;
@@ -214,7 +234,7 @@ int vfd_aggregate_fwd(int BN, int C, int h, int w, const float* base, int n_leve
  * recorded; vfd_prof_read_kernels: the same per kernel id into arrays of `count` entries.
  * Both reset the record. */
 #define VFD_PROF_ALL (-1)
-#define VFD_KERNEL_COUNT 18
+#define VFD_KERNEL_COUNT 20
 const char* vfd_kernel_name(int kernel_id);
 int vfd_prof_enable(int kernel_id);
 int vfd_prof_read(int* launches, double* total_ms);

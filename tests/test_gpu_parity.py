@@ -708,3 +708,61 @@ def test_fusion_adjoint_at_full_size(config):
     g = torch.randn(out.shape, device=DEV, generator=gen).contiguous(memory_format=torch.channels_last)
     out.backward(g)
     check(out.detach() * g, float((vox.detach().double() * vox.grad.double()).sum()), 'K3')
+
+
+# ------------------------------------------------------------------------------------ depth synthesis
+def test_depth_synthesis_kernel_against_reference():
+    """get_virtual_depth (view_rendering.py:84-116) through the C ABI (vfd_depth_syn_fwd/bwd)
+    against the reference's fixture: warped depth, mask (exact), d source depth, d target depth."""
+    from vfdepth_amd import kernels as KN
+    fx = golden('virtual_depth.npz')
+    c = G.virtual_depth_case()
+    B = c['src_depth'].shape[0]
+    T = c['T'].to(DEV)
+    M = (c['src_K'].to(DEV) @ torch.inverse(T))[:, :3, :].reshape(B, 1, 1, 3, 4).contiguous()
+    zrow = T[:, 2, :].reshape(B, 1, 1, 4).contiguous()
+    tab = torch.zeros(1, 1, dtype=torch.int32, device=DEV)
+    sd = c['src_depth'].to(DEV).requires_grad_(True)           # [B,1,H,W]: camera 0 as the source
+    td = c['tar_depth'].to(DEV).requires_grad_(True)           # camera 0's augmented view
+    invK = c['tar_invK'].to(DEV).reshape(B, 1, 4, 4)
+    d, m = KN.DepthSynthesis.apply(tab, c['min_depth'], c['max_depth'], td, sd, c['src_mask'].to(DEV)[:, 0:1],
+                                   invK, M, zrow)
+    close(d[:, :, 0], fx['depth'], 'warped depth')
+    close(m[:, :, 0], fx['mask'], 'warped mask', atol=0, rtol=0)
+    (d[:, :, 0] * G.seeded_randn(fx['depth'].shape, 61).to(DEV)).sum().backward()
+    gclose(sd.grad, fx['d_src_depth'], 'd source depth')
+    gclose(td.grad, fx['d_tar_depth'], 'd augmented-view depth')
+
+
+def test_full_step_depth_synthesis_against_reference():
+    """The aug_depth step (ddad_surround_fusion_augdepth.yaml: augment_extrinsics, second K3C +
+    decoder pass, depth synthesis, DepthSynLoss) against the reference's step fixture: every loss
+    key, the augmented depths and every camera's warped source depths / masks."""
+    from vfdepth_amd import synth
+    from vfdepth_amd.layers import seeded_state_dict
+    from vfdepth_amd.vfdepth import VFDepthAlgo
+    fx = golden('step_aug_small.npz')
+    cfg = G.step_aug_cfg()
+    algo = VFDepthAlgo(cfg, 0)
+    for m in algo.models.values():
+        m.load_state_dict(seeded_state_dict(m, seed=G.STEP_SEED))
+    algo.set_train()
+    inputs = synth.make_batch(cfg, seed=5, with_depth=True)
+    noise = torch.stack([torch.tensor(fx[f'noise_c{c}']) for c in range(6)]).to(DEV)
+    torch.manual_seed(1234)               # the augmentation angles: the reference's CPU draw
+    outputs, losses = algo.process_batch(inputs, 0, noise=noise)
+    losses['total_loss'].backward()
+    close(inputs['extrinsics_aug'], fx['extrinsics_aug'], 'extrinsics_aug', atol=1e-5, rtol=1e-5)
+    for k in [k for k in fx.files if k.startswith('loss_')]:
+        close(losses[k[5:]], fx[k], k)
+    for c in range(6):
+        o = outputs[('cam', c)]
+        close(o[('depth', 0)], fx[f'depth_c{c}'], f'depth cam {c}')
+        close(o[('depth', 0, 'aug')], fx[f'depth_aug_c{c}'], f'aug depth cam {c}')
+        for j, (dd, mm) in enumerate(zip(o[('tform_depth', 0)], o[('tform_depth_mask', 0)])):
+            ref_d, ref_m = fx[f'tform_depth_c{c}_{j}'], fx[f'tform_mask_c{c}_{j}']
+            err = (dd.detach().cpu().double() - torch.tensor(ref_d).double()).abs()
+            off = err > 1e-4 + 1e-4 * torch.tensor(ref_d).double().abs()
+            # samples across a depth discontinuity move with fp32 coordinate rounding: rare
+            assert float(off.float().mean()) <= 1e-3, f'tform depth cam {c} src {j}: {int(off.sum())} off'
+            assert float((mm.detach().cpu() != torch.tensor(ref_m)).float().mean()) <= 1e-3, f'tform mask {c} {j}'

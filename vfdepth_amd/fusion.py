@@ -27,6 +27,7 @@ import torch.nn.functional as F
 
 from . import kernels as KN
 from .layers import conv1d_block, conv2d_block, pack_cam_feat
+from .rotation import axis_angle_to_matrix
 
 
 class _GeometryCache:
@@ -78,6 +79,7 @@ class VFNet(nn.Module):
         self.voxel_size = [int(v) for v in m['voxel_size']]
         self.proj_d_bins = int(m['proj_d_bins'])
         self.aug_depth = bool(t.get('aug_depth', False))
+        self.aug_angle = [float(v) for v in t.get('aug_angle', [15, 15, 40])]
         self.syn_visualize = bool(cfg.get('eval', {}).get('syn_visualize', False))
         x_dim, y_dim, z_dim = self.voxel_size
         self.z_dim, self.y_dim, self.x_dim = z_dim, y_dim, x_dim
@@ -176,15 +178,34 @@ class VFNet(nn.Module):
             return F.leaky_relu(F.conv2d(y0, c1.weight, c1.bias), 0.1, inplace=True).contiguous()
         return self._reduce(KN.VoxelProject.apply(space, voxel_feat, inv_K, extrinsics))
 
+    def augment_extrinsics(self, ext):
+        """Random rotation in front of every camera (volumetric_fusionnet.py:269-287): the angles
+        are the reference's `torch.rand(b, cam, 3)` draw on the CPU global generator, scaled by
+        `aug_angle` (used as radians, as the reference does); no gradient."""
+        with torch.no_grad():
+            b, cam = ext.shape[:2]
+            angle = torch.rand(b, cam, 3)
+            for i in range(3):
+                angle[:, :, i] = (angle[:, :, i] - 0.5) * self.aug_angle[i]
+            tform = torch.eye(4).repeat(b, cam, 1, 1)
+            tform[:, :, :3, :3] = axis_angle_to_matrix(angle)
+            return tform.to(device=ext.device, dtype=ext.dtype) @ ext
+
     def forward(self, inputs, feats_agg):
-        if self.aug_depth or self.syn_visualize:
-            raise NotImplementedError('depth-synthesis / visualisation branches are out of scope of this build')
+        if self.syn_visualize:
+            raise NotImplementedError('synthesis visualisation (eval.syn_visualize) is out of scope of this build')
         space = self.space(feats_agg.device)
         fusion_dict = {('cam', c): {} for c in range(self.num_cams)}
         if self.model == 'depth':
             vox = self.backproject_depth(inputs, feats_agg)
-            fusion_dict['proj_feat'] = self.project_voxel_into_image(
-                vox, inputs['inv_K', self.fusion_level + 1], inputs['extrinsics'])
+            inv_K = inputs['inv_K', self.fusion_level + 1]
+            fusion_dict['proj_feat'] = self.project_voxel_into_image(vox, inv_K, inputs['extrinsics'])
+            if self.aug_depth:
+                # depth synthesis at a novel view (volumetric_fusionnet.py:313-317); the augmented
+                # extrinsics also travel in the returned dict (DDP re-packs `inputs` per call)
+                ext_aug = self.augment_extrinsics(inputs['extrinsics'])
+                inputs['extrinsics_aug'] = fusion_dict['extrinsics_aug'] = ext_aug
+                fusion_dict['proj_feat_aug'] = self.project_voxel_into_image(vox, inv_K, ext_aug)
             return fusion_dict
         vox = KN.FusePose.apply(space, self._plan(inputs, space), feats_agg)
         return self._reduce(vox)

@@ -145,8 +145,6 @@ class ViewRendering(nn.Module):
 
     def _render(self, inputs, outputs, rel_poses, cam_begin, cam_count, depth_all=None):
         """Render cameras [cam_begin, +cam_count); returns {scale: (color, cmask, ovl, omask)}."""
-        if self.aug_depth:
-            raise NotImplementedError('depth-synthesis branch (aug_depth) is out of scope of this build')
         plan = self.plan(inputs[('K', 0)].device)
         cams = list(range(cam_begin, cam_begin + cam_count))
         colors = [inputs[('color', f, 0)] for f in self.frame_ids]
@@ -176,6 +174,55 @@ class ViewRendering(nn.Module):
         depth_all: optional {scale: [B, N, H, W]} depth (avoids re-stacking the per-camera views)."""
         return self._render(inputs, outputs, rel_poses, 0, self.num_cams, depth_all)
 
+    # ------------------------------------------------------------------ depth synthesis
+    def depth_sources(self, device):
+        """[N, S] source cameras of each target's augmented view: rel_cam_list[c] + [c], present
+        cameras only (view_rendering.py:210-213), padded with -1."""
+        key = ('_ds_tab', str(device))
+        if getattr(self, '_ds_key', None) != key:
+            rel = self.cfg['data']['rel_cam_list']
+            lists = [[s for s in list(rel[c]) + [c] if s < self.num_cams] for c in range(self.num_cams)]
+            S = max(len(x) for x in lists)
+            tab = torch.full((self.num_cams, S), -1, dtype=torch.int32)
+            for c, x in enumerate(lists):
+                tab[c, :len(x)] = torch.tensor(x, dtype=torch.int32)
+            self._ds_lists, self._ds_tab, self._ds_key = lists, tab.to(device), key
+        return self._ds_lists, self._ds_tab
+
+    def render_depth_synthesis(self, inputs, outputs, depth, aug_depth, cams=None):
+        """Depth of every source camera warped into the augmented view of each target camera
+        (view_rendering.py:200-241): depth, aug_depth [B, N, H, W] (scale 0) -> the packed
+        (tform_depth, tform_mask) [B, N, S, H, W]; the per-camera lists go to
+        outputs[('cam', c)][('tform_depth', 0)] / [('tform_depth_mask', 0)]."""
+        t = self.cfg['training']
+        lists, tab = self.depth_sources(depth.device)
+        E, E_aug, K = inputs['extrinsics'], inputs['extrinsics_aug'], inputs[('K', 0)]
+        aug_inv = inverse4x4(E_aug)
+        B, N = E.shape[:2]
+        S = tab.shape[1]
+        eye = torch.eye(4, device=E.device, dtype=E.dtype).expand(B, 4, 4)
+        Ms, zs = [], []
+        for c in range(N):
+            for j in range(S):
+                src = lists[c][j] if j < len(lists[c]) else c
+                T = aug_inv[:, c] @ E[:, src] if j < len(lists[c]) else eye
+                Ms.append((K[:, src] @ inverse4x4(T))[:, :3, :])
+                zs.append(T[:, 2, :])
+        M = torch.stack(Ms, 1).view(B, N, S, 3, 4)
+        zrow = torch.stack(zs, 1).view(B, N, S, 4)
+        tform, tmask = KN.DepthSynthesis.apply(tab, t['min_depth'], t['max_depth'], aug_depth, depth,
+                                               inputs['mask'][:, :, 0], inputs[('inv_K', 0)], M, zrow)
+        for c in (range(N) if cams is None else cams):
+            view = outputs[('cam', c)]
+            view[('tform_depth', 0)] = [tform[:, c, j:j + 1] for j in range(len(lists[c]))]
+            view[('tform_depth_mask', 0)] = [tmask[:, c, j:j + 1] for j in range(len(lists[c]))]
+        return tform, tmask
+
     def forward(self, inputs, outputs, cam, rel_pose_dict):
         """Reference per-camera API (view_rendering.py:118)."""
         self._render(inputs, outputs, {cam: rel_pose_dict}, cam, 1)
+        if self.aug_depth:
+            N = self.num_cams
+            depth = torch.stack([outputs[('cam', c)][('depth', 0)][:, 0] for c in range(N)], 1)
+            aug = torch.stack([outputs[('cam', c)][('depth', 0, 'aug')][:, 0] for c in range(N)], 1)
+            self.render_depth_synthesis(inputs, outputs, depth, aug, cams=[cam])

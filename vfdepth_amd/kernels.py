@@ -504,6 +504,53 @@ class ViewSynthesis(torch.autograd.Function):
         return (None, None, d_depth, None, d_M, None) + (None,) * len(colors)
 
 
+class DepthSynthesis(torch.autograd.Function):
+    """get_virtual_depth of every (target camera, source slot) (view_rendering.py:84-116,
+    201-241) in one launch: aug_depth, depth, mask [B,N,H,W], invK [B,N,4,4], M [B,N,S,3,4] =
+    (K_src @ T^-1)[:3], zrow [B,N,S,4] = T[2] -> (tform_depth, tform_mask) [B,N,S,H,W].
+    Gradients flow to aug_depth (sample coordinates) and depth (sampled values)."""
+
+    @staticmethod
+    def forward(ctx, src_tab, min_depth, max_depth, aug_depth, depth, mask, invK, M, zrow):
+        lib = L.load()
+        aug_depth, depth, mask, invK, M, zrow = (_dev(t, n) for t, n in (
+            (aug_depth, 'aug depth'), (depth, 'depth'), (mask, 'mask'), (invK, 'inv_K'), (M, 'KT'), (zrow, 'T')))
+        B, N, H, W = depth.shape
+        S = src_tab.shape[1]
+        d = DepthSynthesis.desc(src_tab, min_depth, max_depth, B, N, H, W)
+        out_d = torch.empty(B, N, S, H, W, device=depth.device)
+        out_m = torch.empty_like(out_d)
+        L.check(lib.vfd_depth_syn_fwd(ctypes.byref(d), aug_depth.data_ptr(), depth.data_ptr(), mask.data_ptr(),
+                                      invK.data_ptr(), M.data_ptr(), zrow.data_ptr(), out_d.data_ptr(),
+                                      out_m.data_ptr(), L.stream()), 'depth_syn_fwd')
+        ctx.src_tab, ctx.range = src_tab, (min_depth, max_depth)
+        ctx.save_for_backward(aug_depth, depth, mask, invK, M, zrow)
+        ctx.mark_non_differentiable(out_m)
+        return out_d, out_m
+
+    @staticmethod
+    def desc(src_tab, min_depth, max_depth, B, N, H, W):
+        d = L.DepthSynDesc()
+        d.B, d.N, d.H, d.W, d.S = B, N, H, W, src_tab.shape[1]
+        d.min_depth, d.max_depth = float(min_depth), float(max_depth)
+        d.src_tab = src_tab.data_ptr()
+        return d
+
+    @staticmethod
+    def backward(ctx, g, _g_mask):
+        lib = L.load()
+        aug_depth, depth, mask, invK, M, zrow = ctx.saved_tensors
+        B, N, H, W = depth.shape
+        d = DepthSynthesis.desc(ctx.src_tab, *ctx.range, B, N, H, W)
+        g = _dev(g, 'grad')
+        d_aug = torch.empty_like(aug_depth)
+        d_depth = torch.empty_like(depth)
+        L.check(lib.vfd_depth_syn_bwd(ctypes.byref(d), aug_depth.data_ptr(), depth.data_ptr(), mask.data_ptr(),
+                                      invK.data_ptr(), M.data_ptr(), zrow.data_ptr(), g.data_ptr(), d_aug.data_ptr(),
+                                      d_depth.data_ptr(), L.stream()), 'depth_syn_bwd')
+        return None, None, None, d_aug, d_depth, None, None, None, None
+
+
 # =============================================================================================
 # Photometric losses (K5) and smoothness
 # =============================================================================================

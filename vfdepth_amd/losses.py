@@ -197,3 +197,46 @@ class SingleCamLoss(nn.Module):
 class MultiCamLoss(SingleCamLoss):
     """Spatial + spatio-temporal terms on top of the temporal loss (multi_cam_loss.py:9-138)."""
     multi = True
+
+
+class DepthSynLoss(MultiCamLoss):
+    """MultiCamLoss + the depth-synthesis terms (depth_synthesis_loss.py:8-91): consistency between
+    each camera's augmented-view depth and the source depths warped into that view,
+    clamp(|a - t| / (a + t + 1e-8), 0, 1) as one masked mean over all sources, and plain-gradient
+    smoothness of disp_aug / mean; weighted by depth_con_coeff / depth_sm_coeff."""
+
+    @staticmethod
+    def syn_terms(aug_depth, tform, tmask, disp_aug):
+        """aug_depth, disp_aug [B, N, H, W]; tform, tmask [B, N, S, H, W] -> (con [N], sm [N])."""
+        a = aug_depth.unsqueeze(2)
+        pl = torch.clamp((a - tform).abs() / (a + tform + 1e-8), 0., 1.)
+        con = (pl * tmask).sum((0, 2, 3, 4)) / (tmask.sum((0, 2, 3, 4)) + 1e-8)
+        nd = disp_aug / (disp_aug.mean((2, 3), keepdim=True) + 1e-8)
+        sm = (nd[..., :-1] - nd[..., 1:]).abs().mean((0, 2, 3)) + (nd[..., :-1, :] - nd[..., 1:, :]).abs().mean((0, 2, 3))
+        return con, sm
+
+    def forward_all(self, inputs, outputs, packed, disp_all, depth_all, noise=None):
+        total, logs = super().forward_all(inputs, outputs, packed, disp_all, depth_all, noise)
+        tform, tmask = outputs['_tform']
+        con, sm = self.syn_terms(outputs['_depth_aug_all'][0], tform, tmask, outputs['_disp_aug_all'][0])
+        syn = self.depth_con_coeff * con + self.depth_sm_coeff * sm
+        total = total + syn.sum() / self.num_cams
+        logs['depth_loss'] = syn.detach().mean()
+        logs['depth_sm_loss'] = sm.detach().mean()
+        logs['depth_con_loss'] = con.detach().mean()
+        logs['cam_loss'] = total.detach()
+        return total, logs
+
+    def forward(self, inputs, outputs, cam, noise=None):
+        cam_loss, loss_dict = super().forward(inputs, outputs, cam, noise)
+        view = outputs[('cam', cam)]
+        aug = view[('depth', 0, 'aug')]
+        tform = torch.stack(view[('tform_depth', 0)], 1)[:, :, 0].unsqueeze(1)
+        tmask = torch.stack(view[('tform_depth_mask', 0)], 1)[:, :, 0].unsqueeze(1)
+        con, sm = self.syn_terms(aug, tform, tmask, view[('disp', 0, 'aug')])
+        syn = self.depth_con_coeff * con[0] + self.depth_sm_coeff * sm[0]
+        cam_loss = cam_loss + syn / len(self.scales)
+        loss_dict.update({'depth_loss': syn.detach(), 'depth_sm_loss': sm[0].detach(),
+                          'depth_con_loss': con[0].detach(), 'cam_loss': cam_loss.detach()})
+        return cam_loss, loss_dict
+

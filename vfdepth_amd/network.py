@@ -101,12 +101,20 @@ class FusedDepthNet(nn.Module):
             feats, agg = _aggregate(self.encoder, self.conv1x1, pack_cam_feat(imgs), self.fusion_level, B, N)
             fusion = self.fusion_net(inputs, agg)
             disp = self.decoder(feats[:self.fusion_level] + [fusion['proj_feat']])
-        disp = {k: v.float() for k, v in disp.items()}
-        for k, v in disp.items():
-            v = v.view(B, N, *v.shape[1:])
-            for c in range(N):
-                outputs[('cam', c)][k] = v[:, c]
-        outputs['_packed'] = disp
+            # depth synthesis: a second decoder pass on the augmented view (fusion_depthnet.py:79-86)
+            disp_aug = (self.decoder(feats[:self.fusion_level] + [fusion['proj_feat_aug']])
+                        if 'proj_feat_aug' in fusion else None)
+        for tag, dd, suffix in (('_packed', disp, ()), ('_packed_aug', disp_aug, ('aug',))):
+            if dd is None:
+                continue
+            dd = {k: v.float() for k, v in dd.items()}
+            for k, v in dd.items():
+                v = v.view(B, N, *v.shape[1:])
+                for c in range(N):
+                    outputs[('cam', c)][k + suffix] = v[:, c]
+            outputs[tag] = dd
+        if 'extrinsics_aug' in fusion:
+            outputs['_extrinsics_aug'] = fusion['extrinsics_aug']
         return outputs
 
 

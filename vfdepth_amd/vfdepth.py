@@ -25,7 +25,7 @@ from torch.utils.data import DataLoader
 from . import fusion
 from .config import flatten
 from .geometry import Pose, ViewRendering, inverse4x4
-from .losses import MultiCamLoss, SingleCamLoss
+from .losses import DepthSynLoss, MultiCamLoss, SingleCamLoss
 from .network import FusedDepthNet, FusedPoseNet, MonoDepthNet, MonoPoseNet
 from .synth import SyntheticSurroundDataset
 
@@ -59,7 +59,7 @@ class VFDepthAlgo:
     # ------------------------------------------------------------------ construction
     def init_losses(self, cfg, rank):
         if self.aug_depth:
-            raise NotImplementedError('depth-synthesis loss (aug_depth) is out of scope of this build')
+            return DepthSynLoss(cfg, rank)
         if self.spatio_temporal or self.spatio:
             return MultiCamLoss(cfg, rank)
         return SingleCamLoss(cfg, rank)
@@ -186,10 +186,13 @@ class VFDepthAlgo:
         pose_pred = self.predict_pose(inputs)
         depth_feats = self.predict_depth(inputs)
         packed = depth_feats.pop('_packed', None)
+        packed_aug = depth_feats.pop('_packed_aug', None)
+        if '_extrinsics_aug' in depth_feats:          # written by VFNet (travels through DDP)
+            inputs['extrinsics_aug'] = depth_feats.pop('_extrinsics_aug')
         for c in range(self.num_cams):
             outputs[('cam', c)].update(pose_pred[('cam', c)])
             outputs[('cam', c)].update(depth_feats[('cam', c)])
-        self.compute_depth_maps(inputs, outputs, packed)
+        self.compute_depth_maps(inputs, outputs, packed, packed_aug)
         return outputs
 
     def _net(self, name):
@@ -215,32 +218,41 @@ class VFDepthAlgo:
         depth = 1 / (lo + (hi - lo) * disp_in)
         return depth * K_in[:, 0:1, 0:1].unsqueeze(2) / self.focal_length_scale      # (depth * fx) / fls
 
-    def compute_depth_maps(self, inputs, outputs, packed=None):
-        """Per-camera depth (vfdepth.py:263-275); with the packed [B*N] decoder output the depth of
-        all cameras is one elementwise op, kept as [B, N, H, W] for the kernels."""
-        disp_all, depth_all = outputs.setdefault('_disp_all', {}), outputs.setdefault('_depth_all', {})
+    def compute_depth_maps(self, inputs, outputs, packed=None, packed_aug=None):
+        """Per-camera depth (vfdepth.py:263-275), and the augmented view's (aug_depth); with the
+        packed [B*N] decoder output the depth of all cameras is one elementwise op, kept as
+        [B, N, H, W] for the kernels."""
         K0 = inputs[('K', 0)]
         B, N = K0.shape[:2]
-        for scale in self.scales:
-            if packed is not None and ('disp', scale) in packed:
-                disp = packed[('disp', scale)].view(B, N, *packed[('disp', scale)].shape[1:])[:, :, 0]
-            else:
-                disp = torch.stack([outputs[('cam', c)][('disp', scale)][:, 0] for c in range(N)], 1)
-            if tuple(disp.shape[-2:]) != (self.height, self.width):
-                disp_f = F.interpolate(disp, [self.height, self.width], mode='bilinear', align_corners=False)
-            else:
-                disp_f = disp
-            lo, hi = 1 / self.max_depth, 1 / self.min_depth
-            depth = 1 / (lo + (hi - lo) * disp_f)
-            depth = depth * K0[:, :, 0:1, 0:1] / self.focal_length_scale
-            disp_all[scale] = disp
-            depth_all[scale] = depth
-            for c in range(N):
-                outputs[('cam', c)][('depth', scale)] = depth[:, c].unsqueeze(1)
+        variants = [('', packed)] + ([('aug', packed_aug)] if self.aug_depth else [])
+        for tag, pk in variants:
+            sfx = (tag,) if tag else ()
+            disp_all = outputs.setdefault('_disp_aug_all' if tag else '_disp_all', {})
+            depth_all = outputs.setdefault('_depth_aug_all' if tag else '_depth_all', {})
+            for scale in self.scales:
+                key = ('disp', scale)
+                if pk is not None and key in pk:
+                    disp = pk[key].view(B, N, *pk[key].shape[1:])[:, :, 0]
+                else:
+                    disp = torch.stack([outputs[('cam', c)][key + sfx][:, 0] for c in range(N)], 1)
+                if tuple(disp.shape[-2:]) != (self.height, self.width):
+                    disp_f = F.interpolate(disp, [self.height, self.width], mode='bilinear', align_corners=False)
+                else:
+                    disp_f = disp
+                lo, hi = 1 / self.max_depth, 1 / self.min_depth
+                depth = 1 / (lo + (hi - lo) * disp_f)
+                depth = depth * K0[:, :, 0:1, 0:1] / self.focal_length_scale
+                disp_all[scale] = disp
+                depth_all[scale] = depth
+                for c in range(N):
+                    outputs[('cam', c)][('depth', scale) + sfx] = depth[:, c].unsqueeze(1)
 
     def compute_losses(self, inputs, outputs, noise=None):
         rel = {c: self.pose.compute_relative_cam_poses(inputs, outputs, c) for c in range(self.num_cams)}
         packed = self.view_rendering.render_all(inputs, outputs, rel, outputs['_depth_all'])
+        if self.aug_depth:
+            outputs['_tform'] = self.view_rendering.render_depth_synthesis(
+                inputs, outputs, outputs['_depth_all'][0], outputs['_depth_aug_all'][0])
         total, logs = self.losses.forward_all(inputs, outputs, packed, outputs['_disp_all'], outputs['_depth_all'], noise)
         losses = dict(logs)
         losses['total_loss'] = total

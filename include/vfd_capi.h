@@ -124,11 +124,13 @@ int vfd_voxel_project_bwd(const vfd_voxel_desc* d, const float* d_out, const flo
  * Wq = the conv weight [O, Cv*D, 3, 3] in fragment order [D, 3, 3, Cv/4, O, 2, 2]
  * (reference channel c*D + d with c = 4q + 2h + s), bias [O], out_channels O = 256 ->
  * out [B*N, h+2, w+2, O]: reflect-padded NHWC input of reduce_dim's second conv.  D <= 64.
+ * x_out (nullable): also write the frustum features themselves as [B*N, h+2, w+2, D*Cv] (channel
+ * d*Cv + c, reflect-padded NHWC: K3's padded output layout) for the conv's backward.
  * Workspace: per-workgroup partial tiles (summed in a fixed order: deterministic). */
 size_t vfd_proj_conv_fwd_workspace(const vfd_voxel_desc* d);
 int vfd_proj_conv_fwd(const vfd_voxel_desc* d, const float* vox, const float* invK, const float* E,
-                      const float* Wq, const float* bias, int out_channels, float* out, void* workspace,
-                      size_t ws_bytes, void* stream);
+                      const float* Wq, const float* bias, int out_channels, float* out, float* x_out,
+                      void* workspace, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------ view synthesis (K4) */
 typedef struct vfd_view_desc {

@@ -487,6 +487,8 @@ def test_proj_conv_matches_k3_plus_conv(config):
     y_ref = F.pad(torch.where(pos, pre, 0.1 * pre), (1, 1, 1, 1), mode='reflect')
     close(y, y_ref, f'K3C output (config {config})')
     close(F.leaky_relu(pre, 0.1), y[:, :, 1:-1, 1:-1], f'K3C output vs its own LeakyReLU (config {config})')
+    # the frustum features the kernel writes for the backward (K3's padded layout, halo included)
+    close(y.grad_fn.saved_tensors[2], x.detach(), f'K3C frustum-feature side output (config {config})')
     g = torch.randn(y.shape, device=DEV, generator=gen)
     (y * g).sum().backward()
     (y_ref * g).sum().backward()

@@ -66,8 +66,16 @@ def main():
         y = KN.ProjConv.apply(space, vox, invK, E, w0, bias)
         ref = F.pad(F.leaky_relu(F.conv2d(x, wp, bias), 0.1), (1, 1, 1, 1), mode='reflect')
         err = float((y - ref).abs().max()) / float(ref.abs().max())
+    # with a voxel gradient: the kernel also writes the frustum features (K3's output) as a side output
+    vg = vox.clone().requires_grad_(True)
+    t_side = timed(lambda: KN.ProjConv.apply(space, vg, invK, E, w0, bias), a.iters)
+    y2 = KN.ProjConv.apply(space, vg, invK, E, w0, bias)
+    xs = y2.grad_fn.saved_tensors[2]
+    xerr = float((xs - x).abs().max())
     print(f'config {a.config}: K3C fused {t_fused:.3f} ms (kernel {ms / n:.3f} ms, {flop / (ms / n) / 1e9:.1f} TFLOP/s); '
-          f'K3 {t_k3:.3f} ms + MIOpen conv {t_conv:.3f} ms = {t_k3 + t_conv:.3f} ms; max rel err {err:.2e}', flush=True)
+          f'with side output {t_side:.3f} ms; '
+          f'K3 {t_k3:.3f} ms + MIOpen conv {t_conv:.3f} ms = {t_k3 + t_conv:.3f} ms; max rel err {err:.2e}; '
+          f'side output max |dx| {xerr:.2e}', flush=True)
 
 
 if __name__ == '__main__':

@@ -78,37 +78,78 @@ constexpr int PC_THREADS = 512;
 constexpr int PC_PF = VFD_PC_PF;                // weight-fragment prefetch distance (iterations)
 constexpr int PC_ITERS = 9 * (PC_CV / 4);       // (tap, channel quad) iterations per atom
 
-// gather waves: halo samples of atom (tile origin y0/x0, depth dep) into one LDS image
-__device__ __forceinline__ void pc_gather(const vfd_voxel_desc& d, float* __restrict__ xs,
+// gather waves: halo samples of atom (tile origin y0/x0, depth bin di) into one LDS image, and —
+// when `xo` is given — the tile's own (interior) samples into the padded NHWC frustum-feature map
+// the conv's backward reads (K3's output layout; written once, reflect copies included).
+constexpr int PC_GPOS = (PC_NPOS + 15) / 16 * 4;   // halo positions per gather wave (48)
+
+struct PcTri {
+  int base;
+  unsigned in;
+  float w[8];
+};
+
+__device__ __forceinline__ void pc_gather(const vfd_voxel_desc& d, float* __restrict__ xs, PcTri* __restrict__ tw,
                                           const float* __restrict__ vox_b, const float* __restrict__ iK,
-                                          const float* __restrict__ E, int y0, int x0, float dep, int gw) {
-  // lanes = (position, channel quad): 16 quads per 64-channel row, 4 positions per wave
-  // instruction; each lane evaluates its position's trilinear cell itself (no cross-wave sync)
+                                          const float* __restrict__ E, int y0, int x0, int di, int gw,
+                                          float* __restrict__ xo) {
   const int lane = threadIdx.x & 63;
+  // (1) the wave's positions p = gw*4 + (k & 3) + 16*(k >> 2): lane k evaluates slot k's trilinear
+  //     cell once (wave-private LDS slice, no workgroup barrier)
+  if (lane < PC_GPOS) {
+    const int p = gw * 4 + (lane & 3) + 16 * (lane >> 2);
+    if (p < PC_NPOS) {
+      const int hr = p / PC_HC, hc = p - hr * PC_HC;
+      const int py = pc_reflect(y0 + hr - 1, d.h), px = pc_reflect(x0 + hc - 1, d.w);
+      const Tri t = frustum_sample(d, iK, E, px, py, d.dbins[di]);
+      tw[lane].base = (t.z0 * d.Y + t.y0) * d.X + t.x0;
+      tw[lane].in = t.in;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) tw[lane].w[k] = t.w[k];
+    }
+  }
+  __threadfence_block();
+  __builtin_amdgcn_wave_barrier();
+  // (2) lanes = (position, channel quad): 16 quads per 64-channel row, 4 positions per instruction
   const int q = lane & 15, sub = lane >> 4;
   const float4* vb = reinterpret_cast<const float4*>(vox_b) + q;
-  for (int p = gw * 4 + sub; p < PC_NPOS; p += 16) {
-    const int hr = p / PC_HC, hc = p - hr * PC_HC;
-    const int py = pc_reflect(y0 + hr - 1, d.h), px = pc_reflect(x0 + hc - 1, d.w);
-    const Tri t = frustum_sample(d, iK, E, px, py, dep);
-    const int base = (t.z0 * d.Y + t.y0) * d.X + t.x0;
+  const int ho = d.h + 2, wo = d.w + 2;
+  for (int it = 0; it < PC_GPOS / 4; ++it) {
+    const int p = gw * 4 + sub + 16 * it;
+    if (p >= PC_NPOS) break;
+    const PcTri& t = tw[it * 4 + sub];
+    const unsigned in = t.in;
+    const int base = t.base;
     float4 v[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const bool ok = (t.in >> k & 1u) != 0u;
+      const bool ok = (in >> k & 1u) != 0u;
       v[k] = vb[(size_t)(ok ? base + corner_offset(d, k) : 0) * (PC_CV / 4)];
     }
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {           // K3's arithmetic: corner order, weight 0 when out of range
-      const float w = (t.in >> k & 1u) ? t.w[k] : 0.f;
+      const float w = (in >> k & 1u) ? t.w[k] : 0.f;
       acc.x += v[k].x * w;
       acc.y += v[k].y * w;
       acc.z += v[k].z * w;
       acc.w += v[k].w * w;
     }
     *reinterpret_cast<float4*>(&xs[p * PC_XS + 4 * q]) = acc;
+    if (xo) {
+      const int hr = p / PC_HC, hc = p - hr * PC_HC;
+      const int py = y0 + hr - 1, px = x0 + hc - 1;
+      if (hr >= 1 && hr <= PC_TR && hc >= 1 && hc <= PC_TC && py < d.h && px < d.w) {
+        int rows[3], cols[3], nr, nc;
+        pad_sets(py, d.h, true, rows, &nr);
+        pad_sets(px, d.w, true, cols, &nc);
+        for (int r = 0; r < nr; ++r)
+          for (int c = 0; c < nc; ++c)
+            *reinterpret_cast<float4*>(xo + (((size_t)rows[r] * wo + cols[c]) * d.D + di) * PC_CV + 4 * q) = acc;
+      }
+    }
   }
+  (void)ho;
 }
 
 struct PcAtom {
@@ -135,8 +176,10 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pcv_main_k(vfd_voxel_desc d, Pc
                                                            const float* __restrict__ invK,
                                                            const float* __restrict__ E,
                                                            const float* __restrict__ Wq,
-                                                           float* __restrict__ partial) {
+                                                           float* __restrict__ partial,
+                                                           float* __restrict__ xout) {
   __shared__ float xs[2][PC_NPOS * PC_XS];
+  __shared__ PcTri tri[PC_WAVES][PC_GPOS];
   const int grp = blockIdx.x;
   const int a_lo = pc_lo(g, grp), a_hi = pc_lo(g, grp + 1);
   if (a_lo >= a_hi) return;
@@ -144,24 +187,23 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pcv_main_k(vfd_voxel_desc d, Pc
   const int V = d.X * d.Y * d.Z;
   const bool compute = wv < PC_WAVES;
   // prologue: the gather waves build the first atom
-  if (!compute) {
-    const PcAtom a = pc_atom(d, g, a_lo);
-    pc_gather(d, xs[0], vox + (size_t)(a.bc / d.N) * V * PC_CV, invK + a.bc * 16, E + a.bc * 16, a.y0, a.x0,
-              d.dbins[a.di], wv - PC_WAVES);
-  }
+  auto gather = [&](int atom, float* dst) {
+    const PcAtom a = pc_atom(d, g, atom);
+    float* xo = xout ? xout + (size_t)a.bc * (d.h + 2) * (d.w + 2) * d.D * PC_CV : nullptr;
+    pc_gather(d, dst, tri[wv - PC_WAVES], vox + (size_t)(a.bc / d.N) * V * PC_CV, invK + a.bc * 16,
+              E + a.bc * 16, a.y0, a.x0, a.di, wv - PC_WAVES, xo);
+  };
+  if (!compute) gather(a_lo, xs[0]);
   __syncthreads();
   if (!compute) {
     // producer: atom a+1 into the other buffer while the compute waves run atom a
     for (int atom = a_lo; atom < a_hi; ++atom) {
 #ifdef VFD_PC_NOGATHER
-      if (false) {                                    // experiment: no gather after the first atom
+      if (false)                                      // experiment: no gather after the first atom
 #else
-      if (atom + 1 < a_hi) {
+      if (atom + 1 < a_hi)
 #endif
-        const PcAtom a = pc_atom(d, g, atom + 1);
-        pc_gather(d, xs[(atom + 1 - a_lo) & 1], vox + (size_t)(a.bc / d.N) * V * PC_CV, invK + a.bc * 16,
-                  E + a.bc * 16, a.y0, a.x0, d.dbins[a.di], wv - PC_WAVES);
-      }
+        gather(atom + 1, xs[(atom + 1 - a_lo) & 1]);
       __syncthreads();
     }
     return;
@@ -345,7 +387,7 @@ size_t vfd_proj_conv_fwd_workspace(const vfd_voxel_desc* d) {
 }
 
 int vfd_proj_conv_fwd(const vfd_voxel_desc* d, const float* vox, const float* invK, const float* E,
-                      const float* Wq, const float* bias, int out_channels, float* out, void* ws,
+                      const float* Wq, const float* bias, int out_channels, float* out, float* x_out, void* ws,
                       size_t ws_bytes, void* stream) {
   VFD_REQUIRE(d && vox && invK && E && Wq && bias && out, "proj_conv_fwd: null argument");
   VFD_REQUIRE(d->Cv == PC_CV, "proj_conv_fwd: Cv must be %d (got %d)", PC_CV, d->Cv);
@@ -357,7 +399,7 @@ int vfd_proj_conv_fwd(const vfd_voxel_desc* d, const float* vox, const float* in
   ProfScope ps(K_PROJ_CONV_FWD, s);
   const PcGeom g = pc_plan(*d);
   float* partial = (float*)ws;
-  pcv_main_k<<<g.ngroup, PC_THREADS, 0, s>>>(*d, g, vox, invK, E, Wq, partial);
+  pcv_main_k<<<g.ngroup, PC_THREADS, 0, s>>>(*d, g, vox, invK, E, Wq, partial, x_out);
   pcv_reduce_k<<<g.ntile, 256, 0, s>>>(*d, g, partial, bias, out);
   return fail_launch("proj_conv_fwd");
 }

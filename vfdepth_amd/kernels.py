@@ -325,6 +325,11 @@ class VoxelProject(torch.autograd.Function):
         return None, dvox, None, None
 
 
+# reduce_dim[0]'s data gradient in K3C's backward: 'nhwc' (one MIOpen call on the channels-last
+# tensors) or 'nchw' (the data gradient on NCHW copies of the small tensors; tools/micro_convbwd.py)
+_DGRAD_LAYOUT = os.environ.get('VFD_DGRAD_LAYOUT', 'nhwc')
+
+
 def proj_conv_weight_fragments(w, Cv, D):
     """reduce_dim[0] weight [O, Cv*D, 3, 3] (reference channel c*D + d) -> the fused kernel's
     fragment-ordered copy [D, 3, 3, Cv/4, O, 2, 2] (c = 4q + 2h + s; projconv.hip, pcv_main_k)."""
@@ -338,8 +343,9 @@ class ProjConv(torch.autograd.Function):
     [B*N, Cv*D, h, w] frustum features never reach HBM).  Output: the reflect-padded
     channels-last input of reduce_dim's second conv, logical [B*N, O, h+2, w+2].
 
-    Backward: the frustum features are recomputed by K3, then MIOpen's data / weight gradients and
-    K3's planned backward give d voxel, d weight, d bias."""
+    When a gradient is needed the kernel also writes the frustum features themselves (K3's padded
+    channels-last layout) as a side output, so the backward is exactly the unfused one: MIOpen's
+    data / weight gradients and K3's planned backward give d voxel, d weight, d bias."""
 
     @staticmethod
     @_amp_fwd
@@ -351,11 +357,15 @@ class ProjConv(torch.autograd.Function):
         N, O = E.shape[1], w0.shape[0]
         wq = proj_conv_weight_fragments(w0, Cv, space.D)
         out = torch.empty(B * N, O, space.h + 2, space.w + 2, device=vox.device, memory_format=torch.channels_last)
+        need_x = ctx.needs_input_grad[1] or ctx.needs_input_grad[4]
+        x = (torch.empty(B * N, Cv * space.D, space.h + 2, space.w + 2, device=vox.device,
+                         memory_format=torch.channels_last) if need_x else None)
         d = space.desc(B, N, Cv=Cv)
         nbytes = lib.vfd_proj_conv_fwd_workspace(ctypes.byref(d))
         ws = _ws(nbytes, vox.device)
         L.check(lib.vfd_proj_conv_fwd(ctypes.byref(d), vox.data_ptr(), invK.data_ptr(), E.data_ptr(), wq.data_ptr(),
-                                      bias.data_ptr(), O, out.data_ptr(), ws.data_ptr(), nbytes, L.stream()),
+                                      bias.data_ptr(), O, out.data_ptr(), x.data_ptr() if need_x else None,
+                                      ws.data_ptr(), nbytes, L.stream()),
                 'proj_conv_fwd')
         ctx.space, ctx.shape = space, (B, N, V, Cv, O)
         ctx.plan = None
@@ -364,14 +374,14 @@ class ProjConv(torch.autograd.Function):
             ctx.plan = torch.empty(nbytes, dtype=torch.uint8, device=vox.device)
             L.check(lib.vfd_voxel_project_plan(ctypes.byref(d), invK.data_ptr(), E.data_ptr(), ctx.plan.data_ptr(),
                                                nbytes, L.stream()), 'voxel_project_plan')
-        ctx.save_for_backward(vox, invK, E, w0, out)
+        ctx.save_for_backward(w0, out, x)
         return out
 
     @staticmethod
     @_amp_bwd
     def backward(ctx, g):
         lib = L.load()
-        vox, invK, E, w0, out = ctx.saved_tensors
+        w0, out, x = ctx.saved_tensors
         space = ctx.space
         B, N, V, Cv, O = ctx.shape
         d = space.desc(B, N, Cv=Cv)
@@ -379,15 +389,22 @@ class ProjConv(torch.autograd.Function):
         # adjoint of the reflect padding, then of the LeakyReLU (its sign from the output)
         g_in = torch.ops.aten.reflection_pad2d_backward(g, out[:, :, 1:-1, 1:-1], [1, 1, 1, 1])
         inner = out[:, :, 1:-1, 1:-1]
-        g_pre = g_in * torch.where(inner > 0, 1.0, 0.1)
-        x = torch.empty(B * N, Cv * space.D, space.h + 2, space.w + 2, device=g.device,
-                        memory_format=torch.channels_last)
-        L.check(lib.vfd_voxel_project_fwd(ctypes.byref(d), vox.data_ptr(), invK.data_ptr(), E.data_ptr(),
-                                          x.data_ptr(), L.stream()), 'voxel_project_fwd (recompute)')
+        g_pre = (g_in * torch.where(inner > 0, 1.0, 0.1)).contiguous(memory_format=torch.channels_last)
+        if x is None:   # only the bias gradient was asked for
+            x = torch.empty(B * N, Cv * space.D, space.h + 2, space.w + 2, device=g.device,
+                            memory_format=torch.channels_last)
         w_perm = proj_conv_weight(w0, Cv, space.D)
         mask = (ctx.needs_input_grad[1], ctx.needs_input_grad[4], ctx.needs_input_grad[5])
-        dx, dw, db = torch.ops.aten.convolution_backward(g_pre, x, w_perm, [O], [1, 1], [0, 0], [1, 1], False,
-                                                         [0, 0], 1, [mask[0], mask[1], mask[2]])
+        cb = torch.ops.aten.convolution_backward
+        args = ([O], [1, 1], [0, 0], [1, 1], False, [0, 0], 1)
+        if _DGRAD_LAYOUT == 'nchw' and mask[0]:
+            # MIOpen's NCHW data-gradient solver (the NHWC one is ~1.5x slower at this shape);
+            # the input tensor only supplies shape / memory format to the data gradient
+            shape_only = torch.empty(x.shape, device=x.device)
+            dx = cb(g_pre.contiguous(), shape_only, w_perm.contiguous(), *args, [True, False, False])[0]
+            _, dw, db = cb(g_pre, x, w_perm, *args, [False, mask[1], mask[2]])
+        else:
+            dx, dw, db = cb(g_pre, x, w_perm, *args, [mask[0], mask[1], mask[2]])
         dvox = dw0 = None
         if mask[0]:
             dx = _channels_last(dx, 'd frustum features')

@@ -78,7 +78,12 @@ class VFDepthAlgo:
                 # per-rank BatchNorm, the GPU path converts exactly as the reference does
                 if on_gpu:
                     v = torch.nn.SyncBatchNorm.convert_sync_batchnorm(v, group)
-                models[k] = DDP(v, device_ids=[self.device.index] if on_gpu else None, broadcast_buffers=True)
+                # broadcast_buffers as the reference (vfdepth.py:70) — except at world size 1, where
+                # the broadcast is a self-copy whose in-place version bump on the BatchNorm running
+                # stats (saved by MIOpen's batch-norm backward) breaks the second pose-net call of
+                # the step; at world > 1 SyncBatchNorm's synchronised path saves no running stats
+                models[k] = DDP(v, device_ids=[self.device.index] if on_gpu else None,
+                                broadcast_buffers=self.world_size > 1)
         return models
 
     def prepare_dataset(self, cfg, rank):

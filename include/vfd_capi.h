@@ -132,6 +132,16 @@ int vfd_proj_conv_fwd(const vfd_voxel_desc* d, const float* vox, const float* in
                       const float* Wq, const float* bias, int out_channels, float* out, float* x_out,
                       void* workspace, size_t ws_bytes, void* stream);
 
+/* K3C data gradient (volumetric_fusionnet.py:59-60, 265 backward): d of reduce_dim's first conv
+ * w.r.t. its reflect-padded input, dx [B*N, h+2, w+2, D*Cv] (channel d*Cv + c: the layout
+ * vfd_voxel_project_bwd_planned reads) from g_pre [B*N, h, w, O = 256] (d pre-activation, NHWC)
+ * and Wd = the weight [O, Cv*D, 3, 3] as [9 flipped taps][O/4][np][2][2] (np = D*Cv rounded up
+ * to 256, zero-padded).  fp32 MFMA, stream-K with a fixed-order partial sum (deterministic).
+ * Workspace 0 = shape unsupported (Cv != 64, D > 64, or the padded rows of a tile exceed LDS). */
+size_t vfd_proj_conv_dgrad_workspace(const vfd_voxel_desc* d);
+int vfd_proj_conv_dgrad(const vfd_voxel_desc* d, const float* g_pre, const float* Wd, float* dx, void* workspace,
+                        size_t ws_bytes, void* stream);
+
 /* ------------------------------------------------------------------ view synthesis (K4) */
 typedef struct vfd_view_desc {
   int32_t B, N, H, W;
@@ -236,7 +246,7 @@ int vfd_aggregate_fwd(int BN, int C, int h, int w, const float* base, int n_leve
  * recorded; vfd_prof_read_kernels: the same per kernel id into arrays of `count` entries.
  * Both reset the record. */
 #define VFD_PROF_ALL (-1)
-#define VFD_KERNEL_COUNT 20
+#define VFD_KERNEL_COUNT 21
 const char* vfd_kernel_name(int kernel_id);
 int vfd_prof_enable(int kernel_id);
 int vfd_prof_read(int* launches, double* total_ms);

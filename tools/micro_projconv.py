@@ -76,6 +76,41 @@ def main():
           f'with side output {t_side:.3f} ms; '
           f'K3 {t_k3:.3f} ms + MIOpen conv {t_conv:.3f} ms = {t_k3 + t_conv:.3f} ms; max rel err {err:.2e}; '
           f'side output max |dx| {xerr:.2e}', flush=True)
+    # data gradient: the MFMA kernel vs MIOpen's (channels-last) data gradient
+    import ctypes
+    lib = _lib.load()
+    h, w = space.h, space.w
+    g_pre = torch.randn(B * N, O, h, w, device=dev).contiguous(memory_format=torch.channels_last)
+    d = space.desc(B, N, Cv=Cv)
+    nbytes = lib.vfd_proj_conv_dgrad_workspace(ctypes.byref(d))
+    if not nbytes:
+        print('dgrad kernel: shape unsupported', flush=True)
+        return
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    dx = torch.empty(B * N, Cv * D, h + 2, w + 2, device=dev, memory_format=torch.channels_last)
+
+    def dgrad():
+        wd = KN.proj_conv_dgrad_weight(w0, Cv, D)
+        _lib.check(lib.vfd_proj_conv_dgrad(ctypes.byref(d), g_pre.data_ptr(), wd.data_ptr(), dx.data_ptr(),
+                                           ws.data_ptr(), nbytes, _lib.stream()), 'proj_conv_dgrad')
+    xcl = x.contiguous(memory_format=torch.channels_last)
+    cb = torch.ops.aten.convolution_backward
+    args = ([O], [1, 1], [0, 0], [1, 1], False, [0, 0], 1)
+    t_dg = timed(dgrad, a.iters)
+    t_mi = timed(lambda: cb(g_pre, xcl, wp, *args, [True, False, False]), a.iters)
+    t_wg = timed(lambda: cb(g_pre, xcl, wp, *args, [False, True, True]), a.iters)
+    _lib.prof_enable('proj_conv_dgrad')
+    for _ in range(a.iters):
+        dgrad()
+    torch.cuda.synchronize()
+    prof = _lib.prof_read()
+    _lib.prof_enable('off')
+    n2, ms2 = prof.get('proj_conv_dgrad', (1, float('nan')))
+    dgrad()
+    ref = cb(g_pre, xcl, wp, *args, [True, False, False])[0]
+    derr = float((dx - ref).abs().max()) / float(ref.abs().max())
+    print(f'config {a.config}: dgrad kernel {t_dg:.3f} ms (kernel {ms2 / n2:.3f} ms, {flop / (ms2 / n2) / 1e9:.1f} TFLOP/s, '
+          f'weight copy incl.); MIOpen dgrad {t_mi:.3f} ms, MIOpen wgrad {t_wg:.3f} ms; max rel err {derr:.2e}', flush=True)
 
 
 if __name__ == '__main__':

@@ -375,6 +375,269 @@ static PcGeom pc_plan(const vfd_voxel_desc& d) {
   return g;
 }
 
+// =============================================================================================
+// K3C data gradient — reduce_dim's first conv, backward w.r.t. its reflect-padded input (the
+// frustum features K3's backward consumes), as an fp32 MFMA GEMM over the padded grid:
+//
+//   dXp[bc, Y, X, n] = sum_{ty, tx, o} G[bc, Y - ty, X - tx, o] * W[o, n, ty, tx]
+//
+// G = d pre-activation [B*N, h, w, O] (zero outside the h x w grid), n = d*Cv + c (K3's channel
+// order).  M = padded positions (row-major, 128 per tile), N = D*Cv (256 per tile, zero-padded
+// weights past D*Cv), K = 9 taps x O.  An atom = (tile, 32-channel chunk of O): the loader waves
+// stage the chunk's G rows under the tile (<= hrows rows x (w + 4) columns, zero margins) in LDS
+// while the compute waves run the previous atom's 9 taps x 8 channel quads (same wave roles and
+// fragment pipeline as the forward).  Stream-K over atoms: a tile whole inside one workgroup's
+// range is stored directly; the (at most two) split tiles of a range go to partial slots that
+// `pcd_reduce_k` sums in workgroup order (deterministic).
+constexpr int PD_OC = 32;                       // O channels per atom
+constexpr int PD_XS = PD_OC + 4;                // LDS floats per staged position
+constexpr int PD_N = PC_WAVES * 64;             // n per tile
+constexpr int PD_CHUNKS = PC_O / PD_OC;         // atoms per tile
+constexpr int PD_ITERS = 9 * (PD_OC / 4);       // (tap, quad) iterations per atom
+constexpr int PD_LDS_MAX = 160 * 1024;
+
+struct PdGeom {
+  int nbc, h, w, wo, npix, mtiles, ntot, np, ntile, natom, ngroup, hrows, cols, lds_floats;
+};
+
+__host__ __device__ inline int pd_lo(const PdGeom& g, int grp) {
+  return (int)(((long long)grp * g.natom) / g.ngroup);
+}
+
+struct PdTile {
+  int nt, bc, mt, m0, ymin;
+};
+
+// tile order: n-tile outermost (a workgroup's consecutive tiles share the n-tile's weights)
+__device__ __forceinline__ PdTile pd_tile(const PdGeom& g, int t) {
+  PdTile r;
+  r.mt = t % g.mtiles;
+  const int rest = t / g.mtiles;
+  r.bc = rest % g.nbc;
+  r.nt = rest / g.nbc;
+  r.m0 = r.mt * PC_PIX;
+  r.ymin = r.m0 / g.wo;
+  return r;
+}
+
+// loader waves (tid 0..255): G rows ymin-2 .. ymin-2+hrows-1, columns -2 .. w+1, channels of chunk ch
+__device__ __forceinline__ void pd_stage(const PdGeom& g, float* __restrict__ dst, const float* __restrict__ gp,
+                                         int atom, int tid) {
+  const int t = atom / PD_CHUNKS, ch = atom - t * PD_CHUNKS;
+  const PdTile tl = pd_tile(g, t);
+  const int npos = g.hrows * g.cols;
+  const int q = tid & 7;
+  const float* src = gp + (size_t)tl.bc * g.h * g.w * PC_O + ch * PD_OC + 4 * q;
+  for (int p0 = tid >> 3; p0 < npos; p0 += 4 * 32) {
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int p = p0 + 32 * u;
+      const int hr = p / g.cols, c = p - hr * g.cols;
+      const int y = tl.ymin - 2 + hr, x = c - 2;
+      v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (p < npos && y >= 0 && y < g.h && x >= 0 && x < g.w)
+        v[u] = *reinterpret_cast<const float4*>(src + ((size_t)y * g.w + x) * PC_O);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int p = p0 + 32 * u;
+      if (p < npos) *reinterpret_cast<float4*>(dst + p * PD_XS + 4 * q) = v[u];
+    }
+  }
+}
+
+// Weight layout Wd: [9 taps (flipped: tap' = (2-ty)*3 + (2-tx))][O/4 quads][np][2 (h)][2 (s)],
+// o = 4*quad + 2*h + s, n = d*Cv + c (zero for n >= D*Cv).
+__global__ __launch_bounds__(PC_THREADS, 2) void pcd_main_k(PdGeom g, const float* __restrict__ gp,
+                                                           const float* __restrict__ Wd,
+                                                           float* __restrict__ dx,
+                                                           float* __restrict__ partial) {
+  extern __shared__ float pd_lds[];
+  const int grp = blockIdx.x;
+  const int a_lo = pd_lo(g, grp), a_hi = pd_lo(g, grp + 1);
+  if (a_lo >= a_hi) return;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const bool compute = wv < PC_WAVES;
+  if (!compute) pd_stage(g, pd_lds, gp, a_lo, threadIdx.x - 64 * PC_WAVES);
+  __syncthreads();
+  if (!compute) {
+    for (int atom = a_lo; atom < a_hi; ++atom) {
+      if (atom + 1 < a_hi)
+        pd_stage(g, pd_lds + ((atom + 1 - a_lo) & 1) * g.lds_floats, gp, atom + 1, threadIdx.x - 64 * PC_WAVES);
+      __syncthreads();
+    }
+    return;
+  }
+  const int li = lane & 31, lh = lane >> 5;
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  const float2* wlane = reinterpret_cast<const float2*>(Wd) + (size_t)(wv * 64 + li) * 2 + lh;
+  float2 bq[PC_PF][2];
+  int pf_atom = a_lo, pf_it = 0;
+  auto prefetch = [&](int slot) {
+    if (pf_atom < a_hi) {
+      const int t = pf_atom / PD_CHUNKS, ch = pf_atom - t * PD_CHUNKS;
+      const int nt = t / (g.mtiles * g.nbc);
+      const int tap = pf_it >> 3, q = pf_it & 7;
+      const float2* w = wlane + ((size_t)(tap * (PC_O / 4) + ch * (PD_OC / 4) + q) * g.np + nt * PD_N) * 2;
+      bq[slot][0] = w[0];
+      bq[slot][1] = w[64];
+      if (++pf_it == PD_ITERS) { pf_it = 0; ++pf_atom; }
+    }
+  };
+#pragma unroll
+  for (int k = 0; k < PC_PF; ++k) prefetch(k);
+  for (int atom = a_lo; atom < a_hi; ++atom) {
+    const int t = atom / PD_CHUNKS, ch = atom - t * PD_CHUNKS;
+    const PdTile tl = pd_tile(g, t);
+    int aoff[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      int m = tl.m0 + 32 * a + li;
+      m = m < g.npix ? m : g.npix - 1;                 // rows past the grid: computed, never stored
+      const int Y = m / g.wo, X = m - Y * g.wo;
+      aoff[a] = ((Y - tl.ymin) * g.cols + X) * PD_XS + 2 * lh;
+    }
+    const float* xb = pd_lds + ((atom - a_lo) & 1) * g.lds_floats;
+    float2 afc[4], afn[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) afc[a] = *reinterpret_cast<const float2*>(&xb[aoff[a]]);
+#pragma unroll 1
+    for (int tap = 0; tap < 9; ++tap) {
+      const int ky = tap / 3, kx = tap - 3 * ky;
+      const float* xt = xb + (ky * g.cols + kx) * PD_XS;
+      const int tn = tap + 1, kyn = tn / 3, kxn = tn - 3 * kyn;
+      const float* xn = xb + (kyn * g.cols + kxn) * PD_XS;
+#pragma unroll
+      for (int q = 0; q < PD_OC / 4; ++q) {
+        const int ring = q % PC_PF;
+        const float2 b0 = bq[ring][0], b1 = bq[ring][1];
+        prefetch(ring);
+        if (q < PD_OC / 4 - 1) {
+#pragma unroll
+          for (int a = 0; a < 4; ++a) afn[a] = *reinterpret_cast<const float2*>(&xt[aoff[a] + 4 * (q + 1)]);
+        } else if (tap < 8) {
+#pragma unroll
+          for (int a = 0; a < 4; ++a) afn[a] = *reinterpret_cast<const float2*>(&xn[aoff[a]]);
+        }
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int a = 0; a < 4; ++a) {
+            const float av = s ? afc[a].y : afc[a].x;
+            acc[a][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, s ? b0.y : b0.x, acc[a][0], 0, 0, 0);
+            acc[a][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, s ? b1.y : b1.x, acc[a][1], 0, 0, 0);
+          }
+#pragma unroll
+        for (int a = 0; a < 4; ++a) afc[a] = afn[a];
+      }
+    }
+    __syncthreads();                                  // buffer handed back to the loader waves
+    if (ch == PD_CHUNKS - 1 || atom == a_hi - 1) {
+      const int ts = t * PD_CHUNKS;
+      if (ts >= a_lo && ts + PD_CHUNKS <= a_hi) {     // whole tile in this range: store
+        float* ob = dx + (size_t)tl.bc * g.npix * g.ntot;
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            const int n = tl.nt * PD_N + wv * 64 + b * 32 + li;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int m = tl.m0 + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * lh;
+              if (m < g.npix && n < g.ntot) ob[(size_t)m * g.ntot + n] = acc[a][b][r];
+              acc[a][b][r] = 0.f;
+            }
+          }
+      } else {                                        // split tile: partial slot
+        const int slot = t == a_lo / PD_CHUNKS ? 0 : 1;
+        float* dst = partial + ((size_t)grp * 2 + slot) * PC_FRAG + (size_t)wv * (PC_FRAG / PC_WAVES);
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              dst[((a * 2 + b) * 16 + r) * 64 + lane] = acc[a][b][r];
+              acc[a][b][r] = 0.f;
+            }
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void pcd_reduce_k(PdGeom g, const float* __restrict__ partial,
+                                                    float* __restrict__ dx) {
+  __shared__ int contrib[PC_MAXC];
+  __shared__ int ncontrib;
+  const int t = blockIdx.x;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int a0 = t * PD_CHUNKS, a1 = a0 + PD_CHUNKS;
+  if (threadIdx.x == 0) {
+    int gg = (int)(((long long)a0 * g.ngroup) / g.natom);
+    while (gg > 0 && pd_lo(g, gg) > a0) --gg;
+    while (pd_lo(g, gg + 1) <= a0) ++gg;
+    int n = 0;
+    if (pd_lo(g, gg + 1) < a1) {                      // split: every group meeting the tile, in order
+      for (; gg < g.ngroup && n < PC_MAXC; ++gg) {
+        const int lo = pd_lo(g, gg), hi = pd_lo(g, gg + 1);
+        if (lo >= a1) break;
+        if (hi <= a0 || lo >= hi) continue;
+        contrib[n++] = gg * 2 + (t == lo / PD_CHUNKS ? 0 : 1);
+      }
+    }
+    ncontrib = n;
+  }
+  __syncthreads();
+  const int nc = ncontrib;
+  if (nc == 0) return;                                // stored directly by its workgroup
+  const PdTile tl = pd_tile(g, t);
+  float* ob = dx + (size_t)tl.bc * g.npix * g.ntot;
+  for (int f = 0; f < 4 * 2 * 16; ++f) {
+    const int a = f >> 5, bb = (f >> 4) & 1, r = f & 15;
+    float s = 0.f;
+    for (int k = 0; k < nc; ++k)
+      s += partial[(size_t)contrib[k] * PC_FRAG + (size_t)wv * (PC_FRAG / PC_WAVES) + (f * 64 + lane)];
+    const int m = tl.m0 + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    const int n = tl.nt * PD_N + wv * 64 + bb * 32 + (lane & 31);
+    if (m < g.npix && n < g.ntot) ob[(size_t)m * g.ntot + n] = s;
+  }
+}
+
+// one workgroup per CU, ranges of >= PD_CHUNKS atoms (a tile meets at most two groups per side)
+static PdGeom pd_plan(const vfd_voxel_desc& d) {
+  PdGeom g;
+  g.nbc = d.B * d.N;
+  g.h = d.h;
+  g.w = d.w;
+  g.wo = d.w + 2;
+  g.npix = (d.h + 2) * g.wo;
+  g.mtiles = (g.npix + PC_PIX - 1) / PC_PIX;
+  g.ntot = d.D * PC_CV;
+  g.np = (g.ntot + PD_N - 1) / PD_N * PD_N;
+  g.ntile = (g.np / PD_N) * g.nbc * g.mtiles;
+  g.natom = g.ntile * PD_CHUNKS;
+  g.hrows = 3 + (g.wo + PC_PIX - 2) / g.wo;           // rows under 128 consecutive positions + 2
+  g.cols = d.w + 4;
+  g.lds_floats = g.hrows * g.cols * PD_XS;
+  const int res = pc_resident();
+  const int most = g.natom / PD_CHUNKS;
+  g.ngroup = most < res ? (most > 0 ? most : 1) : res;
+  return g;
+}
+
+static bool pd_supported(const vfd_voxel_desc& d) {
+  if (d.Cv != PC_CV || d.B <= 0 || d.N <= 0 || d.h < 2 || d.w < 2 || d.D <= 0 || d.D > 64) return false;
+  const PdGeom g = pd_plan(d);
+  return (size_t)2 * g.lds_floats * sizeof(float) <= PD_LDS_MAX;
+}
+
 }  // namespace vfd
 
 using namespace vfd;
@@ -402,6 +665,32 @@ int vfd_proj_conv_fwd(const vfd_voxel_desc* d, const float* vox, const float* in
   pcv_main_k<<<g.ngroup, PC_THREADS, 0, s>>>(*d, g, vox, invK, E, Wq, partial, x_out);
   pcv_reduce_k<<<g.ntile, 256, 0, s>>>(*d, g, partial, bias, out);
   return fail_launch("proj_conv_fwd");
+}
+
+size_t vfd_proj_conv_dgrad_workspace(const vfd_voxel_desc* d) {
+  if (!d || !pd_supported(*d)) return 0;
+  return (size_t)pd_plan(*d).ngroup * 2 * PC_FRAG * sizeof(float);
+}
+
+int vfd_proj_conv_dgrad(const vfd_voxel_desc* d, const float* g_pre, const float* Wd, float* dx, void* ws,
+                        size_t ws_bytes, void* stream) {
+  VFD_REQUIRE(d && g_pre && Wd && dx, "proj_conv_dgrad: null argument");
+  VFD_REQUIRE(pd_supported(*d), "proj_conv_dgrad: unsupported shape (Cv = %d, 0 < D <= 64, padded rows in LDS)", PC_CV);
+  VFD_REQUIRE(ws && ws_bytes >= vfd_proj_conv_dgrad_workspace(d), "proj_conv_dgrad: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  ProfScope ps(K_PROJ_CONV_DGRAD, s);
+  const PdGeom g = pd_plan(*d);
+  float* partial = (float*)ws;
+  const size_t lds = (size_t)2 * g.lds_floats * sizeof(float);
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(pcd_main_k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                        PD_LDS_MAX);
+    attr = true;
+  }
+  pcd_main_k<<<g.ngroup, PC_THREADS, lds, s>>>(g, g_pre, Wd, dx, partial);
+  pcd_reduce_k<<<g.ntile, 256, 0, s>>>(g, partial, dx);
+  return fail_launch("proj_conv_dgrad");
 }
 
 }  // extern "C"

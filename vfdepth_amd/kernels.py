@@ -8,6 +8,7 @@ import ctypes
 import os
 
 import torch
+import torch.nn.functional as F
 
 from . import _lib as L
 
@@ -337,6 +338,22 @@ def proj_conv_weight_fragments(w, Cv, D):
     return w.reshape(O, Cv // 4, 2, 2, D, 3, 3).permute(4, 5, 6, 1, 0, 2, 3).contiguous()
 
 
+def proj_conv_dgrad_weight(w, Cv, D):
+    """reduce_dim[0] weight [O, Cv*D, 3, 3] (reference channel c*D + d) -> the data-gradient
+    kernel's copy [9 flipped taps, O/4, np, 2, 2] (o = 4q + 2h + s; n = d*Cv + c zero-padded to a
+    multiple of 256; projconv.hip, pcd_main_k)."""
+    O = w.shape[0]
+    n = Cv * D
+    npad = (n + 255) // 256 * 256
+    wd = w.reshape(O, Cv, D, 3, 3).flip(3, 4).permute(3, 4, 0, 2, 1).reshape(9, O, n)
+    if npad != n:
+        wd = F.pad(wd, (0, npad - n))
+    return wd.reshape(9, O // 4, 2, 2, npad).permute(0, 1, 4, 2, 3).contiguous()
+
+
+_PC_DGRAD = os.environ.get('VFD_PC_DGRAD', '1') != '0'
+
+
 class ProjConv(torch.autograd.Function):
     """K3C: voxel features [B,V,Cv] -> LeakyReLU(conv3x3_reflect(frustum samples) + bias): K3's
     trilinear resampling fused into reduce_dim's first conv (fp32 MFMA implicit GEMM; the
@@ -397,7 +414,22 @@ class ProjConv(torch.autograd.Function):
         mask = (ctx.needs_input_grad[1], ctx.needs_input_grad[4], ctx.needs_input_grad[5])
         cb = torch.ops.aten.convolution_backward
         args = ([O], [1, 1], [0, 0], [1, 1], False, [0, 0], 1)
-        if _DGRAD_LAYOUT == 'nchw' and mask[0]:
+        dx = None
+        if mask[0] and _PC_DGRAD:
+            nbytes = lib.vfd_proj_conv_dgrad_workspace(ctypes.byref(d))
+            if nbytes:
+                # the fused data gradient (fp32 MFMA, projconv.hip); MIOpen then only does d weight
+                wd = proj_conv_dgrad_weight(w0, Cv, space.D)
+                dx = torch.empty(B * N, Cv * space.D, space.h + 2, space.w + 2, device=g.device,
+                                 memory_format=torch.channels_last)
+                ws = _ws(nbytes, g.device)
+                L.check(lib.vfd_proj_conv_dgrad(ctypes.byref(d), g_pre.data_ptr(), wd.data_ptr(), dx.data_ptr(),
+                                                ws.data_ptr(), nbytes, L.stream()), 'proj_conv_dgrad')
+        if dx is not None:
+            dw = db = None
+            if mask[1] or mask[2]:
+                _, dw, db = cb(g_pre, x, w_perm, *args, [False, mask[1], mask[2]])
+        elif _DGRAD_LAYOUT == 'nchw' and mask[0]:
             # MIOpen's NCHW data-gradient solver (the NHWC one is ~1.5x slower at this shape);
             # the input tensor only supplies shape / memory format to the data gradient
             shape_only = torch.empty(x.shape, device=x.device)

@@ -117,17 +117,27 @@ def algorithmic_bytes(kernel, s):
         'smooth_fwd': B * N * P * 4,
         'smooth_bwd': B * N * P * 5,
         'proj_conv_fwd': B * V * Cv + B * N * p * 256,            # voxels in, reduce_dim[0] output out
+        'proj_conv_dgrad': B * N * p * 256 + proj_out,            # d pre-activation in, d frustum features out
+        'pad_conv_fwd': pose_out + B * 256 * pose_hw(s),          # BEV map in, reduce_dim[0] out
         'depth_syn_fwd': B * N * P * 3 + 2 * B * N * 3 * P,        # depths + mask in, 3 sources x (depth, mask) out
         'depth_syn_bwd': B * N * P * 3 + B * N * 3 * P + 2 * B * N * P,
     }
     return planes[kernel] * 4
 
 
+def pose_hw(s):
+    """Output pixels of the pose reduce_dim's first conv (3x3 stride 2 on the padded Y x X map)."""
+    return ((s['Y'] - 1) // 2 + 1) * ((s['X'] - 1) // 2 + 1)
+
+
 def mfma_flops(kernel, s):
     """Dense fp32 MFMA flops of one launch of the matrix-bound ops (None for the HBM-bound ones):
-    K3C = reduce_dim's first conv, 2 * pixels * 256 * (Cv * D * 9)."""
-    if kernel == 'proj_conv_fwd':
+    K3C = reduce_dim's first conv, 2 * pixels * 256 * (Cv * D * 9); its data gradient the same;
+    K2C = the pose reduce_dim's first conv."""
+    if kernel in ('proj_conv_fwd', 'proj_conv_dgrad'):
         return 2.0 * s['B'] * s['N'] * s['h'] * s['w'] * 256 * s['Cv'] * s['D'] * 9
+    if kernel == 'pad_conv_fwd':                                  # K2C, pose reduce_dim[0]: K = (C+1)*Z*9
+        return 2.0 * s['B'] * pose_hw(s) * 256 * (s['C'] + 1) * s['Z'] * 9
     return None
 
 

@@ -132,6 +132,26 @@ int vfd_proj_conv_fwd(const vfd_voxel_desc* d, const float* vox, const float* in
                       const float* Wq, const float* bias, int out_channels, float* out, float* x_out,
                       void* workspace, size_t ws_bytes, void* stream);
 
+/* ------------------------------------------------------------------ padded 3x3 conv (K2C) */
+typedef struct vfd_conv_desc {
+  int32_t B;             /* images                                                       */
+  int32_t H, W;          /* rows / columns of the (already reflect-padded) input         */
+  int32_t C;             /* input channels, a multiple of 4                              */
+  int32_t stride;        /* 1 or 2                                                       */
+  int32_t out_channels;  /* 256                                                          */
+} vfd_conv_desc;
+
+/* K2C — the pose fusion's reduce_dim[0] (volumetric_fusionnet.py:59-60, 338-343): out =
+ * LeakyReLU_0.1(conv3x3_stride(x) + bias) on the reflect-padded channels-last map K2 writes,
+ * x [B, H, W, C] -> out [B, Ho+2, Wo+2, 256] (Ho = (H-3)/stride + 1; reflect-padded NHWC input of
+ * reduce_dim's second conv).  Wf = the weight [256, C, 3, 3] (C in x's channel order) as
+ * [9 taps][Cpad/4][256][2][2] (c = 4q + 2h + s, Cpad = C rounded up to 16, zero-padded).  fp32
+ * MFMA, stream-K over 16-channel chunks, fixed-order partial sums (deterministic).
+ * Workspace 0 = shape unsupported. */
+size_t vfd_pad_conv_fwd_workspace(const vfd_conv_desc* d);
+int vfd_pad_conv_fwd(const vfd_conv_desc* d, const float* x, const float* Wf, const float* bias, float* out,
+                     void* workspace, size_t ws_bytes, void* stream);
+
 /* K3C data gradient (volumetric_fusionnet.py:59-60, 265 backward): d of reduce_dim's first conv
  * w.r.t. its reflect-padded input, dx [B*N, h+2, w+2, D*Cv] (channel d*Cv + c: the layout
  * vfd_voxel_project_bwd_planned reads) from g_pre [B*N, h, w, O = 256] (d pre-activation, NHWC)
@@ -246,7 +266,7 @@ int vfd_aggregate_fwd(int BN, int C, int h, int w, const float* base, int n_leve
  * recorded; vfd_prof_read_kernels: the same per kernel id into arrays of `count` entries.
  * Both reset the record. */
 #define VFD_PROF_ALL (-1)
-#define VFD_KERNEL_COUNT 21
+#define VFD_KERNEL_COUNT 22
 const char* vfd_kernel_name(int kernel_id);
 int vfd_prof_enable(int kernel_id);
 int vfd_prof_read(int* launches, double* total_ms);

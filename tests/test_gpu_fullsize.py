@@ -494,3 +494,35 @@ def test_proj_conv_matches_k3_plus_conv(config):
     (y_ref * g).sum().backward()
     for name, a, r in zip(('d voxels', 'd weight', 'd bias'), leaves, refs):
         gclose(a.grad, r.grad, f'K3C {name} (config {config})')
+
+
+# ------------------------------------------------------------------------------------ K2C
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize('shape', [(1, 5140, 102, 102, 2),     # config 2 pose: (C+1)*Z, padded 100x100 BEV
+                                   (2, 20, 13, 11, 2),         # odd sizes, partial channel chunk
+                                   (1, 44, 9, 30, 1),          # stride 1
+                                   (2, 1028, 22, 22, 2)])      # small-config pose shape, B=2
+def test_pad_conv_matches_conv(shape):
+    """K2C (the pose reduce_dim's first conv, volumetric_fusionnet.py:59-60, 338-343) against
+    F.conv2d on the same reflect-padded map + bias + LeakyReLU + the reflect pad of the next conv:
+    forward (every pad copy) and, through MIOpen's gradients on the kernel's output, backward."""
+    from vfdepth_amd import kernels as KN
+    B, C, H, W, s = shape
+    gen = torch.Generator(device=DEV).manual_seed(81)
+    x = torch.randn(B, C, H, W, device=DEV, generator=gen).contiguous(memory_format=torch.channels_last)
+    w = torch.randn(256, C, 3, 3, device=DEV, generator=gen) * (C * 9) ** -0.5
+    b = 0.1 * torch.randn(256, device=DEV, generator=gen)
+    assert KN.pad_conv_supported(x, s, 256)
+    leaves = [t.clone().requires_grad_(True) for t in (x, w, b)]
+    y = KN.PadConv.apply(leaves[0], leaves[1], leaves[2], s)
+    refs = [t.clone().requires_grad_(True) for t in (x, w, b)]
+    pre = F.conv2d(refs[0], refs[1], refs[2], stride=s)
+    pos = y.detach()[:, :, 1:-1, 1:-1] > 0          # the kernel's own LeakyReLU decisions (see K3C)
+    y_ref = F.pad(torch.where(pos, pre, 0.1 * pre), (1, 1, 1, 1), mode='reflect')
+    close(y, y_ref, f'K2C output {shape}')
+    close(F.leaky_relu(pre, 0.1), y[:, :, 1:-1, 1:-1], f'K2C output vs its own LeakyReLU {shape}')
+    g = torch.randn(y.shape, device=DEV, generator=gen)
+    (y * g).sum().backward()
+    (y_ref * g).sum().backward()
+    for name, a, r in zip(('d input', 'd weight', 'd bias'), leaves, refs):
+        gclose(a.grad, r.grad, f'K2C {name} {shape}')

@@ -40,6 +40,11 @@ class DepthSynDesc(ctypes.Structure):
                 ('min_depth', c_float), ('max_depth', c_float), ('src_tab', c_fp)]
 
 
+class ConvDesc(ctypes.Structure):
+    _fields_ = [('B', c_int), ('H', c_int), ('W', c_int), ('C', c_int), ('stride', c_int),
+                ('out_channels', c_int)]
+
+
 _SIGS = {
     'vfd_version': (c_int, []),
     'vfd_last_error': (ctypes.c_char_p, []),
@@ -72,6 +77,8 @@ _SIGS = {
     'vfd_proj_conv_fwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 5 + [c_int, c_fp, c_fp, c_fp, c_size_t, c_void_p]),
     'vfd_proj_conv_dgrad_workspace': (c_size_t, [ctypes.POINTER(VoxelDesc)]),
     'vfd_proj_conv_dgrad': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 4 + [c_size_t, c_void_p]),
+    'vfd_pad_conv_fwd_workspace': (c_size_t, [ctypes.POINTER(ConvDesc)]),
+    'vfd_pad_conv_fwd': (c_int, [ctypes.POINTER(ConvDesc)] + [c_fp] * 5 + [c_size_t, c_void_p]),
     'vfd_depth_syn_fwd': (c_int, [ctypes.POINTER(DepthSynDesc)] + [c_fp] * 8 + [c_void_p]),
     'vfd_depth_syn_bwd': (c_int, [ctypes.POINTER(DepthSynDesc)] + [c_fp] * 9 + [c_void_p]),
     'vfd_smooth_workspace_bytes': (c_size_t, [c_int] * 4),
@@ -122,7 +129,7 @@ KERNEL_IDS = {
     'voxel_project_fwd': 5, 'voxel_project_bwd': 6, 'view_stats': 7, 'view_apply': 8, 'view_bwd': 9,
     'photo_fwd': 10, 'photo_bwd': 11, 'smooth_fwd': 12, 'smooth_bwd': 13, 'fusion_plan': 14,
     'aggregate': 15, 'voxel_project_plan': 16, 'proj_conv_fwd': 17,
-    'depth_syn_fwd': 18, 'depth_syn_bwd': 19, 'proj_conv_dgrad': 20,
+    'depth_syn_fwd': 18, 'depth_syn_bwd': 19, 'proj_conv_dgrad': 20, 'pad_conv_fwd': 21,
 }
 
 

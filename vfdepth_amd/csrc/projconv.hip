@@ -309,6 +309,7 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pcv_main_k(vfd_voxel_desc d, Pc
 // Sum of each tile's partials (in workgroup order) + bias, LeakyReLU(0.1), stored into the
 // reflect-padded NHWC map out [B*N, h+2, w+2, O] (the input of reduce_dim's second conv).
 constexpr int PC_MAXC = 72;     // contributors of one tile (<= D + 1, D <= 64)
+constexpr int PC_FSL = 8;       // fragment slices per tile (grid.y of the reduce kernels)
 __global__ __launch_bounds__(256) void pcv_reduce_k(vfd_voxel_desc d, PcGeom g, const float* __restrict__ partial,
                                                     const float* __restrict__ bias, float* __restrict__ out) {
   __shared__ int contrib[PC_MAXC];
@@ -336,7 +337,8 @@ __global__ __launch_bounds__(256) void pcv_reduce_k(vfd_voxel_desc d, PcGeom g, 
   const int y0 = (ti / g.tc) * PC_TR, x0 = (ti % g.tc) * PC_TC;
   const int ho = d.h + 2, wo = d.w + 2;
   float* ob = out + (size_t)bc * ho * wo * PC_O;
-  for (int f = 0; f < 4 * 2 * 16; ++f) {
+  constexpr int FPS = 4 * 2 * 16 / PC_FSL;
+  for (int f = blockIdx.y * FPS; f < (blockIdx.y + 1) * FPS; ++f) {
     const int a = f >> 5, bb = (f >> 4) & 1, r = f & 15;
     float s = 0.f;
     for (int k = 0; k < nc; ++k)
@@ -572,38 +574,23 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pcd_main_k(PdGeom g, const floa
   }
 }
 
+// Ranges hold >= PD_CHUNKS atoms, so a split tile contains exactly one group boundary lo(g):
+// workgroup (g, slice) sums group g-1's and group g's partials of that tile, in that order.
 __global__ __launch_bounds__(256) void pcd_reduce_k(PdGeom g, const float* __restrict__ partial,
                                                     float* __restrict__ dx) {
-  __shared__ int contrib[PC_MAXC];
-  __shared__ int ncontrib;
-  const int t = blockIdx.x;
+  const int grp = blockIdx.x;
+  const int lo = pd_lo(g, grp);
+  if (grp == 0 || lo % PD_CHUNKS == 0) return;        // boundary on a tile edge: nothing split
+  const int t = lo / PD_CHUNKS;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int a0 = t * PD_CHUNKS, a1 = a0 + PD_CHUNKS;
-  if (threadIdx.x == 0) {
-    int gg = (int)(((long long)a0 * g.ngroup) / g.natom);
-    while (gg > 0 && pd_lo(g, gg) > a0) --gg;
-    while (pd_lo(g, gg + 1) <= a0) ++gg;
-    int n = 0;
-    if (pd_lo(g, gg + 1) < a1) {                      // split: every group meeting the tile, in order
-      for (; gg < g.ngroup && n < PC_MAXC; ++gg) {
-        const int lo = pd_lo(g, gg), hi = pd_lo(g, gg + 1);
-        if (lo >= a1) break;
-        if (hi <= a0 || lo >= hi) continue;
-        contrib[n++] = gg * 2 + (t == lo / PD_CHUNKS ? 0 : 1);
-      }
-    }
-    ncontrib = n;
-  }
-  __syncthreads();
-  const int nc = ncontrib;
-  if (nc == 0) return;                                // stored directly by its workgroup
+  const int c0 = (grp - 1) * 2 + (t == pd_lo(g, grp - 1) / PD_CHUNKS ? 0 : 1), c1 = grp * 2;
   const PdTile tl = pd_tile(g, t);
   float* ob = dx + (size_t)tl.bc * g.npix * g.ntot;
-  for (int f = 0; f < 4 * 2 * 16; ++f) {
+  constexpr int FPS = 4 * 2 * 16 / PC_FSL;
+  for (int f = blockIdx.y * FPS; f < (blockIdx.y + 1) * FPS; ++f) {
     const int a = f >> 5, bb = (f >> 4) & 1, r = f & 15;
-    float s = 0.f;
-    for (int k = 0; k < nc; ++k)
-      s += partial[(size_t)contrib[k] * PC_FRAG + (size_t)wv * (PC_FRAG / PC_WAVES) + (f * 64 + lane)];
+    const size_t off = (size_t)wv * (PC_FRAG / PC_WAVES) + (f * 64 + lane);
+    const float s = partial[(size_t)c0 * PC_FRAG + off] + partial[(size_t)c1 * PC_FRAG + off];
     const int m = tl.m0 + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
     const int n = tl.nt * PD_N + wv * 64 + bb * 32 + (lane & 31);
     if (m < g.npix && n < g.ntot) ob[(size_t)m * g.ntot + n] = s;
@@ -663,7 +650,7 @@ int vfd_proj_conv_fwd(const vfd_voxel_desc* d, const float* vox, const float* in
   const PcGeom g = pc_plan(*d);
   float* partial = (float*)ws;
   pcv_main_k<<<g.ngroup, PC_THREADS, 0, s>>>(*d, g, vox, invK, E, Wq, partial, x_out);
-  pcv_reduce_k<<<g.ntile, 256, 0, s>>>(*d, g, partial, bias, out);
+  pcv_reduce_k<<<dim3(g.ntile, PC_FSL), 256, 0, s>>>(*d, g, partial, bias, out);
   return fail_launch("proj_conv_fwd");
 }
 
@@ -684,12 +671,12 @@ int vfd_proj_conv_dgrad(const vfd_voxel_desc* d, const float* g_pre, const float
   const size_t lds = (size_t)2 * g.lds_floats * sizeof(float);
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(pcd_main_k), hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(pcd_main_k), hipFuncAttributeMaxDynamicSharedMemorySize,
                         PD_LDS_MAX);
     attr = true;
   }
   pcd_main_k<<<g.ngroup, PC_THREADS, lds, s>>>(g, g_pre, Wd, dx, partial);
-  pcd_reduce_k<<<g.ntile, 256, 0, s>>>(g, partial, dx);
+  pcd_reduce_k<<<dim3(g.ngroup, PC_FSL), 256, 0, s>>>(g, partial, dx);
   return fail_launch("proj_conv_dgrad");
 }
 

@@ -31,7 +31,7 @@ from .rotation import axis_angle_to_matrix
 
 
 class _GeometryCache:
-    """Step-scoped geometry products (1/8 mask, K2 fusion plan) shared by the three VFNet calls
+    """Step-scoped products (1/8 mask, K2 fusion plan, K2C weight copy) shared by the three VFNet calls
     of a step (two pose calls, one depth call).
 
     Keyed on the IDENTITY and version of the input tensors they derive from, not on the
@@ -132,8 +132,24 @@ class VFNet(nn.Module):
             w0 = KN.proj_conv_weight(c0.weight, self.v_dim_o[-1], self.proj_d_bins)
         else:
             w0 = KN.pose_conv_weight(c0.weight, self.feat_in_dim + 1, self.z_dim)
+            if self.pad_conv(x_padded):
+                # K2C: the first conv on MFMA (padconv.hip), written reflect-padded for the second
+                # the fragment copy of the weight is shared by the step's pose calls (same version)
+                wf = _GEOMETRY_CACHE.get(('pose_wf', id(c0.weight)), (c0.weight,),
+                                         lambda: KN.pose_conv_fragments(c0.weight, self.feat_in_dim + 1, self.z_dim))
+                y0 = KN.PadConv.apply(x_padded, w0, c0.bias, self.stride, wf)
+                return F.leaky_relu(F.conv2d(y0, c1.weight, c1.bias, stride=self.stride), 0.1,
+                                    inplace=True).contiguous()
         x = F.leaky_relu(F.conv2d(x_padded, w0, c0.bias, stride=self.stride), 0.1, inplace=True)
         return F.leaky_relu(c1(x), 0.1, inplace=True).contiguous()
+
+    def pad_conv(self, x_padded):
+        """K2C (the pose reduce_dim's first conv as an fp32 MFMA kernel) applies: 256 outputs, fp32
+        nets (under bf16 autocast MIOpen's bf16 path runs instead), a supported shape, not
+        disabled by VFD_PAD_CONV=0."""
+        return (os.environ.get('VFD_PAD_CONV', '1') != '0' and self.reduce_dim[0].out_channels == 256
+                and not torch.is_autocast_enabled('cuda') and x_padded.dtype == torch.float32
+                and KN.pad_conv_supported(x_padded, self.stride, 256))
 
     def folded_weights(self):
         """Per-camera [N, 2Cv, C] feature columns of (W_no, W_o[group]) and the [3, Cv] depth columns."""

@@ -354,6 +354,80 @@ def proj_conv_dgrad_weight(w, Cv, D):
 _PC_DGRAD = os.environ.get('VFD_PC_DGRAD', '1') != '0'
 
 
+def pad_conv_weight_fragments(w):
+    """Conv weight [O, C, 3, 3] (C in the input map's channel order) -> K2C's copy
+    [9 taps, Cpad/4, O, 2, 2] (c = 4q + 2h + s, Cpad = C rounded up to 16, zero-padded;
+    padconv.hip, ppc_main_k)."""
+    O, C = w.shape[:2]
+    cpad = (C + 15) // 16 * 16
+    wf = w.permute(2, 3, 1, 0).reshape(9, C, O)
+    if cpad != C:
+        wf = F.pad(wf, (0, 0, 0, cpad - C))
+    return wf.reshape(9, cpad // 4, 2, 2, O).permute(0, 1, 4, 2, 3).contiguous()
+
+
+def pose_conv_fragments(w, C1, Z):
+    """The pose reduce_dim[0] weight [O, C1*Z, 3, 3] (reference channel c*Z + z) straight to K2C's
+    fragment copy over FusePose's channel order z*C1 + c (= pad_conv_weight_fragments of
+    pose_conv_weight(w)); no gradient."""
+    O = w.shape[0]
+    with torch.no_grad():
+        return pad_conv_weight_fragments(w.detach().view(O, C1, Z, 3, 3).transpose(1, 2).reshape(O, Z * C1, 3, 3))
+
+
+def pad_conv_desc(x, stride, out_channels):
+    B, C, H, W = x.shape
+    return L.ConvDesc(B, H, W, C, stride, out_channels)
+
+
+def pad_conv_supported(x, stride, out_channels):
+    """K2C applies: fp32 NHWC-able map, C % 4 == 0, 256 outputs, rows of a tile fit in LDS."""
+    return bool(L.load().vfd_pad_conv_fwd_workspace(ctypes.byref(pad_conv_desc(x, stride, out_channels))))
+
+
+class PadConv(torch.autograd.Function):
+    """K2C: reflect-padded channels-last map x [B, C, H, W] -> LeakyReLU(conv3x3_stride(x) + bias)
+    as the reflect-padded channels-last input of the next reflect conv, logical
+    [B, 256, Ho+2, Wo+2] (fp32 MFMA, padconv.hip).  Backward: MIOpen's data / weight gradients of
+    the conv on the pre-activation gradient (pad adjoint + LeakyReLU slope from the output)."""
+
+    @staticmethod
+    @_amp_fwd
+    def forward(ctx, x, w, bias, stride, wf=None):
+        lib = L.load()
+        x = _channels_last(x, 'pad_conv input')
+        w, bias = _dev(w, 'pad_conv weight'), _dev(bias, 'pad_conv bias')
+        O = w.shape[0]
+        d = pad_conv_desc(x, stride, O)
+        nbytes = lib.vfd_pad_conv_fwd_workspace(ctypes.byref(d))
+        if not nbytes:
+            raise RuntimeError(f'pad_conv_fwd: unsupported shape {tuple(x.shape)}, stride {stride}, {O} outputs')
+        ho, wo = (x.shape[2] - 3) // stride + 1, (x.shape[3] - 3) // stride + 1
+        out = torch.empty(x.shape[0], O, ho + 2, wo + 2, device=x.device, memory_format=torch.channels_last)
+        if wf is None:
+            wf = pad_conv_weight_fragments(w)
+        ws = _ws(nbytes, x.device)
+        L.check(lib.vfd_pad_conv_fwd(ctypes.byref(d), x.data_ptr(), wf.data_ptr(), bias.data_ptr(), out.data_ptr(),
+                                     ws.data_ptr(), nbytes, L.stream()), 'pad_conv_fwd')
+        ctx.stride = stride
+        ctx.save_for_backward(x, w, out)
+        return out
+
+    @staticmethod
+    @_amp_bwd
+    def backward(ctx, g):
+        x, w, out = ctx.saved_tensors
+        g = _channels_last(g, 'grad')
+        inner = out[:, :, 1:-1, 1:-1]
+        g_in = torch.ops.aten.reflection_pad2d_backward(g, inner, [1, 1, 1, 1])
+        g_pre = (g_in * torch.where(inner > 0, 1.0, 0.1)).contiguous(memory_format=torch.channels_last)
+        mask = [ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]]
+        s = ctx.stride
+        dx, dw, db = torch.ops.aten.convolution_backward(g_pre, x, w, [w.shape[0]], [s, s], [0, 0], [1, 1],
+                                                         False, [0, 0], 1, mask)
+        return dx, dw, db, None, None
+
+
 class ProjConv(torch.autograd.Function):
     """K3C: voxel features [B,V,Cv] -> LeakyReLU(conv3x3_reflect(frustum samples) + bias): K3's
     trilinear resampling fused into reduce_dim's first conv (fp32 MFMA implicit GEMM; the

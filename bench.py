@@ -351,6 +351,7 @@ def main():
         losses = eager_step()
     torch.cuda.synchronize()
     prof = _lib.prof_read()
+    dense_bytes = {k: v * args.steps / n_prof for k, v in _lib.ALG_BYTES.items()}
     _lib.prof_enable('off')
     prof = {k: (n * args.steps // n_prof, t * args.steps / n_prof) for k, (n, t) in prof.items()}
     elapsed = max_over_ranks(elapsed, world, f'cuda:{local}')
@@ -370,20 +371,32 @@ def main():
             return {'kernel': k, 'bound': 'mfma', 'achieved': ach, 'peak': MFMA_F32_PEAK_TFS, 'unit': 'TFLOP/s',
                     'frac': ach / MFMA_F32_PEAK_TFS, 'traffic': traffic_tab.get(k), 'flops_per_launch': fl,
                     'avg_launch_us': avg_s * 1e6, 'launches': n_launch}
-        alg = algorithmic_bytes(k, s)
+        alg = dense_bytes[k] / n_launch if k in dense_bytes else algorithmic_bytes(k, s)
         ach = alg / avg_s / 1e9
         return {'kernel': k, 'bound': 'hbm', 'achieved': ach, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                 'frac': ach / HBM_PEAK_GBS, 'traffic': traffic_tab.get(k), 'alg_bytes_per_launch': alg,
                 'avg_launch_us': avg_s * 1e6, 'launches': n_launch}
+    dense = {k: prof.pop(k) for k in list(prof) if k in dense_bytes}     # fused dense-net kernels (BN)
     dom = max(prof, key=lambda k: prof[k][1])
     hbm_ops = [k for k in prof if mfma_flops(k, s) is None]
     dom_hbm = max(hbm_ops, key=lambda k: prof[k][1])
+    prof_all = dict(prof, **dense)
+
+    def roofline_any(k):
+        saved = prof.get(k)
+        prof[k] = prof_all[k]
+        try:
+            return roofline_of(k)
+        finally:
+            if saved is None:
+                del prof[k]
     if args.kernel_table:
-        for k, (n, t) in sorted(prof.items(), key=lambda kv: -kv[1][1]):
-            r = roofline_of(k)
+        for k, (n, t) in sorted(prof_all.items(), key=lambda kv: -kv[1][1]):
+            r = roofline_any(k)
             print(f'[bench] {k:20s} {n:4d} launches {t / n * 1e3:9.1f} us/launch  '
                   f'{r["achieved"]:8.1f} {r["unit"]} ({r["frac"]:.3f} of peak)', file=sys.stderr)
-        print(f'[bench] hot-path kernels {sum(t for _, t in prof.values()) / args.steps:.2f} ms/step of '
+        print(f'[bench] hot-path kernels {sum(t for _, t in prof.values()) / args.steps:.2f} ms/step, fused BN '
+              f'{sum(t for _, t in dense.values()) / args.steps:.2f} ms/step, of '
               f'{elapsed / args.steps * 1e3:.2f} ms/step; loss {float(losses["total_loss"]):.5f}', file=sys.stderr)
     # aggregate over every HBM-bound hot-path op of the step (per-kernel and aggregate)
     agg_bytes = sum(algorithmic_bytes(k, s) * prof[k][0] for k in hbm_ops)
@@ -418,6 +431,7 @@ def main():
                                'kernel_ms_per_step': agg_s * 1e3 / args.steps,
                                'what': 'every HBM-bound hot-path op of the step (K1-K5, plans, aggregation)'},
         'hot_path_ms_per_step': sum(t for _, t in prof.values()) / args.steps,
+        'dense_fused': {k: roofline_any(k) for k in dense},
         'execution': 'hip-graph replay of the whole step' if use_graph else 'eager',
         'parity': parity,
         'cpu_baseline': base,

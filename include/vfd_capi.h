@@ -132,6 +132,36 @@ int vfd_proj_conv_fwd(const vfd_voxel_desc* d, const float* vox, const float* in
                       const float* Wq, const float* bias, int out_channels, float* out, float* x_out,
                       void* workspace, size_t ws_bytes, void* stream);
 
+/* ------------------------------------------------------------------ fused BatchNorm (+res)(+ReLU) */
+/* Training-mode BatchNorm2d of the ResNet encoders (fusion_depthnet.py:24-36, fusion_posenet.py:
+ * 22-35; torchvision BasicBlock/Bottleneck/stem), fused with the block's residual add and ReLU:
+ * y = relu((x - mean) * invstd * gamma + beta [+ r]), NCHW fp32.  Statistics in fp64, per
+ * (channel, split) partials [C][S][2] summed in a fixed order.  SyncBatchNorm (DDP): vfd_bn_sum
+ * reduces the partials to [C][2] sums that the host all-reduces, then the apply passes take
+ * ns = 1 and the global element count. */
+typedef struct vfd_bn_desc {
+  int32_t N, C, HW;      /* images, channels, H*W                                        */
+  int32_t S;             /* splits per channel: vfd_bn_splits(desc)                      */
+  int32_t relu;          /* 1: ReLU after the (residual) add                              */
+  float eps, momentum;   /* nn.BatchNorm2d eps / momentum                                 */
+} vfd_bn_desc;
+
+int vfd_bn_splits(const vfd_bn_desc* d);
+int vfd_bn_fwd_stats(const vfd_bn_desc* d, const float* x, double* partial, void* stream);
+int vfd_bn_sum(const vfd_bn_desc* d, const double* partial, double* sums, void* stream);
+/* sums: the [C][S][2] partials (ns = S) or reduced [C][2] sums (ns = 1); residual / running stats
+ * nullable.  Writes y and the per-channel mean / invstd the backward reads. */
+int vfd_bn_fwd_apply(const vfd_bn_desc* d, const float* x, const float* residual, const double* sums, int ns,
+                     double count, const float* gamma, const float* beta, float* y, float* mean, float* invstd,
+                     float* running_mean, float* running_var, void* stream);
+/* g = d y; y = the forward's output (ReLU mask; unused without ReLU) */
+int vfd_bn_bwd_stats(const vfd_bn_desc* d, const float* g, const float* y, const float* x, const float* mean,
+                     double* partial, void* stream);
+/* dx, d residual, d gamma, d beta nullable (not requested) */
+int vfd_bn_bwd_apply(const vfd_bn_desc* d, const float* g, const float* y, const float* x, const double* sums,
+                     int ns, double count, const float* gamma, const float* mean, const float* invstd, float* dx,
+                     float* dresidual, float* dgamma, float* dbeta, void* stream);
+
 /* ------------------------------------------------------------------ padded 3x3 conv (K2C) */
 typedef struct vfd_conv_desc {
   int32_t B;             /* images                                                       */
@@ -266,7 +296,7 @@ int vfd_aggregate_fwd(int BN, int C, int h, int w, const float* base, int n_leve
  * recorded; vfd_prof_read_kernels: the same per kernel id into arrays of `count` entries.
  * Both reset the record. */
 #define VFD_PROF_ALL (-1)
-#define VFD_KERNEL_COUNT 22
+#define VFD_KERNEL_COUNT 24
 const char* vfd_kernel_name(int kernel_id);
 int vfd_prof_enable(int kernel_id);
 int vfd_prof_read(int* launches, double* total_ms);

@@ -526,3 +526,47 @@ def test_pad_conv_matches_conv(shape):
     (y_ref * g).sum().backward()
     for name, a, r in zip(('d input', 'd weight', 'd bias'), leaves, refs):
         gclose(a.grad, r.grad, f'K2C {name} {shape}')
+
+
+# ------------------------------------------------------------------------------------ fused BN
+@pytest.mark.parametrize('shape,res,relu', [((6, 64, 96, 160), True, True),      # layer1 block tail
+                                            ((6, 64, 192, 320), False, True),    # stem
+                                            ((6, 512, 12, 20), False, False),    # layer4 downsample BN
+                                            ((3, 8, 5, 7), True, True)])         # HW % 4 != 0
+def test_batchnorm_act_matches_torch(shape, res, relu):
+    """Fused training-mode BatchNorm (+ residual) (+ ReLU) (bnact.hip) against nn.BatchNorm2d.train()
+    + add + ReLU: output, running statistics, num_batches_tracked, and d input / gamma / beta /
+    residual."""
+    import copy
+    from vfdepth_amd.layers import bn_act
+    gen = torch.Generator(device=DEV).manual_seed(91)
+    x = 2.0 * torch.randn(shape, device=DEV, generator=gen) + 0.5
+    r = torch.randn(shape, device=DEV, generator=gen) if res else None
+    bn = torch.nn.BatchNorm2d(shape[1]).to(DEV).train()
+    with torch.no_grad():
+        bn.weight.copy_(1 + 0.1 * torch.randn(shape[1], device=DEV, generator=gen))
+        bn.bias.copy_(0.1 * torch.randn(shape[1], device=DEV, generator=gen))
+        bn.running_mean.copy_(0.2 * torch.randn(shape[1], device=DEV, generator=gen))
+    bn_ref = copy.deepcopy(bn)
+    xa, xr = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    ra = r.clone().requires_grad_(True) if res else None
+    rr = r.clone().requires_grad_(True) if res else None
+    y = bn_act(bn, xa, ra, relu)
+    yr = bn_ref(xr)
+    if res:
+        yr = yr + rr
+    if relu:
+        yr = torch.relu(yr)
+    assert y.grad_fn is not None and 'BatchNormAct' in type(y.grad_fn).__name__
+    close(y, yr, f'BN output {shape}', atol=2e-5, rtol=2e-5)
+    close(bn.running_mean, bn_ref.running_mean, 'running_mean', atol=1e-6, rtol=1e-6)
+    close(bn.running_var, bn_ref.running_var, 'running_var', atol=1e-6, rtol=1e-5)
+    assert int(bn.num_batches_tracked) == int(bn_ref.num_batches_tracked) == 1
+    g = torch.randn(shape, device=DEV, generator=gen)
+    (y * g).sum().backward()
+    (yr * g).sum().backward()
+    gclose(xa.grad, xr.grad, 'BN d input', rel=1e-4)
+    gclose(bn.weight.grad, bn_ref.weight.grad, 'BN d gamma', rel=1e-4)
+    gclose(bn.bias.grad, bn_ref.bias.grad, 'BN d beta', rel=1e-4)
+    if res:
+        gclose(ra.grad, rr.grad, 'BN d residual', rel=1e-6)

@@ -45,6 +45,11 @@ class ConvDesc(ctypes.Structure):
                 ('out_channels', c_int)]
 
 
+class BnDesc(ctypes.Structure):
+    _fields_ = [('N', c_int), ('C', c_int), ('HW', c_int), ('S', c_int), ('relu', c_int),
+                ('eps', c_float), ('momentum', c_float)]
+
+
 _SIGS = {
     'vfd_version': (c_int, []),
     'vfd_last_error': (ctypes.c_char_p, []),
@@ -77,6 +82,13 @@ _SIGS = {
     'vfd_proj_conv_fwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 5 + [c_int, c_fp, c_fp, c_fp, c_size_t, c_void_p]),
     'vfd_proj_conv_dgrad_workspace': (c_size_t, [ctypes.POINTER(VoxelDesc)]),
     'vfd_proj_conv_dgrad': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 4 + [c_size_t, c_void_p]),
+    'vfd_bn_splits': (c_int, [ctypes.POINTER(BnDesc)]),
+    'vfd_bn_fwd_stats': (c_int, [ctypes.POINTER(BnDesc), c_fp, c_fp, c_void_p]),
+    'vfd_bn_sum': (c_int, [ctypes.POINTER(BnDesc), c_fp, c_fp, c_void_p]),
+    'vfd_bn_fwd_apply': (c_int, [ctypes.POINTER(BnDesc), c_fp, c_fp, c_fp, c_int, c_double] + [c_fp] * 7 + [c_void_p]),
+    'vfd_bn_bwd_stats': (c_int, [ctypes.POINTER(BnDesc)] + [c_fp] * 5 + [c_void_p]),
+    'vfd_bn_bwd_apply': (c_int, [ctypes.POINTER(BnDesc), c_fp, c_fp, c_fp, c_fp, c_int, c_double] + [c_fp] * 7
+                         + [c_void_p]),
     'vfd_pad_conv_fwd_workspace': (c_size_t, [ctypes.POINTER(ConvDesc)]),
     'vfd_pad_conv_fwd': (c_int, [ctypes.POINTER(ConvDesc)] + [c_fp] * 5 + [c_size_t, c_void_p]),
     'vfd_depth_syn_fwd': (c_int, [ctypes.POINTER(DepthSynDesc)] + [c_fp] * 8 + [c_void_p]),
@@ -129,7 +141,7 @@ KERNEL_IDS = {
     'voxel_project_fwd': 5, 'voxel_project_bwd': 6, 'view_stats': 7, 'view_apply': 8, 'view_bwd': 9,
     'photo_fwd': 10, 'photo_bwd': 11, 'smooth_fwd': 12, 'smooth_bwd': 13, 'fusion_plan': 14,
     'aggregate': 15, 'voxel_project_plan': 16, 'proj_conv_fwd': 17,
-    'depth_syn_fwd': 18, 'depth_syn_bwd': 19, 'proj_conv_dgrad': 20, 'pad_conv_fwd': 21,
+    'depth_syn_fwd': 18, 'depth_syn_bwd': 19, 'proj_conv_dgrad': 20, 'pad_conv_fwd': 21, 'bn_fwd': 22, 'bn_bwd': 23,
 }
 
 
@@ -142,6 +154,17 @@ def prof_enable(kernel='all'):
     else:
         kid = KERNEL_IDS[kernel] if isinstance(kernel, str) else int(kernel)
     load().vfd_prof_enable(kid)
+    global PROF_ON
+    PROF_ON = kid != -2
+    if PROF_ON:
+        for k in ALG_BYTES:
+            ALG_BYTES[k] = 0
+
+
+# Algorithmic bytes of the shape-varying dense kernels (fused BN), accumulated by their Python
+# wrappers while profiling is on (bench.py's roofline of those kernels).
+PROF_ON = False
+ALG_BYTES = {'bn_fwd': 0, 'bn_bwd': 0}
 
 
 def prof_read():

@@ -1,0 +1,338 @@
+// Fused training-mode BatchNorm (+ residual) (+ ReLU) for the ResNet encoders of the fused depth /
+// pose nets (network/fusion_depthnet.py:24-36, fusion_posenet.py:22-35: torchvision BasicBlock /
+// Bottleneck + stem; under DDP their BN layers are SyncBatchNorm, models/vfdepth.py:68).
+//
+//   y = relu( (x - mean_c) * invstd_c * gamma_c + beta_c  [+ r] )        x, r, y: NCHW fp32
+//
+// MIOpen's BN kernel, the residual add and the ReLU are three HBM passes + launches per layer here
+// (plus three more for their backward); these kernels do one statistics pass and one apply pass
+// each way.  Statistics accumulate in fp64 (as the reference's CPU batch norm does), per
+// (channel, split) partials summed in a fixed order: deterministic.  For SyncBatchNorm the host
+// all-reduces the per-channel sums between the two passes (vfd_bn_sum).
+//
+// Work split: a channel's N*HW elements (N images of HW contiguous floats) are cut into S
+// equal float4-aligned ranges; block (split, channel) of every kernel owns one range.
+#include "vfd_common.h"
+
+namespace vfd {
+
+constexpr int BN_THREADS = 256;
+
+struct BnRange {
+  long long lo, hi;     // element range [lo, hi) of the channel's N*HW elements
+};
+
+__device__ __forceinline__ BnRange bn_range(const vfd_bn_desc& d, int split) {
+  const long long total = (long long)d.N * d.HW;
+  const long long chunk = ((total + d.S - 1) / d.S + 3) & ~3LL;
+  BnRange r;
+  r.lo = chunk * split;
+  r.hi = r.lo + chunk < total ? r.lo + chunk : total;
+  return r;
+}
+
+// element e of channel c -> offset in the NCHW tensor
+__device__ __forceinline__ size_t bn_off(const vfd_bn_desc& d, int c, long long e) {
+  const long long n = e / d.HW;
+  return ((size_t)n * d.C + c) * d.HW + (e - n * d.HW);
+}
+
+__device__ __forceinline__ double block_sum(double v, double* sh) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) sh[wv] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int i = 0; i < BN_THREADS / 64; ++i) s += sh[i];
+  return s;
+}
+
+// Visit every element of a range: f(offset_of_float4, 4 values) with float4 loads when HW % 4 == 0.
+template <typename F>
+__device__ __forceinline__ void bn_visit(const vfd_bn_desc& d, int c, BnRange r, F&& f) {
+  if ((d.HW & 3) == 0) {
+    for (long long e = r.lo + 4 * threadIdx.x; e < r.hi; e += 4 * BN_THREADS) f(bn_off(d, c, e), 4);
+  } else {
+    for (long long e = r.lo + threadIdx.x; e < r.hi; e += BN_THREADS) f(bn_off(d, c, e), 1);
+  }
+}
+
+// partial[(c*S + split)*2 + {0,1}] = sum x, sum x^2 over the range
+__global__ __launch_bounds__(BN_THREADS) void bn_stats_k(vfd_bn_desc d, const float* __restrict__ x,
+                                                         double* __restrict__ partial) {
+  __shared__ double sh[BN_THREADS / 64];
+  const int c = blockIdx.y, split = blockIdx.x;
+  double s1 = 0.0, s2 = 0.0;
+  bn_visit(d, c, bn_range(d, split), [&](size_t o, int n) {
+    if (n == 4) {
+      const float4 v = *reinterpret_cast<const float4*>(x + o);
+      const double a = v.x, b = v.y, e = v.z, f = v.w;
+      s1 += (a + b) + (e + f);
+      s2 += (a * a + b * b) + (e * e + f * f);
+    } else {
+      const double a = x[o];
+      s1 += a;
+      s2 += a * a;
+    }
+  });
+  s1 = block_sum(s1, sh);
+  s2 = block_sum(s2, sh);
+  if (threadIdx.x == 0) {
+    partial[((size_t)c * d.S + split) * 2] = s1;
+    partial[((size_t)c * d.S + split) * 2 + 1] = s2;
+  }
+}
+
+// sums[c*2 + k] = sum over splits of partial (fixed order); one thread per channel
+__global__ void bn_sum_k(vfd_bn_desc d, const double* __restrict__ partial, double* __restrict__ sums) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= d.C) return;
+  double a = 0.0, b = 0.0;
+  for (int s = 0; s < d.S; ++s) {
+    a += partial[((size_t)c * d.S + s) * 2];
+    b += partial[((size_t)c * d.S + s) * 2 + 1];
+  }
+  sums[c * 2] = a;
+  sums[c * 2 + 1] = b;
+}
+
+// per-channel sums of the block's channel: from the S partials, or (ns == 1) already reduced
+__device__ __forceinline__ void bn_channel_sums(const double* __restrict__ part, int ns, int c, double* a,
+                                                double* b) {
+  double s1 = 0.0, s2 = 0.0;
+  for (int s = 0; s < ns; ++s) {
+    s1 += part[((size_t)c * ns + s) * 2];
+    s2 += part[((size_t)c * ns + s) * 2 + 1];
+  }
+  *a = s1;
+  *b = s2;
+}
+
+// y = relu((x - mean) * invstd * gamma + beta [+ r]); block (0, c) also stores mean / invstd and
+// updates the running statistics (momentum, unbiased variance), as nn.BatchNorm2d.train() does.
+__global__ __launch_bounds__(BN_THREADS) void bn_apply_k(vfd_bn_desc d, const float* __restrict__ x,
+                                                         const float* __restrict__ r, const double* __restrict__ sums,
+                                                         int ns, double count, const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta, float* __restrict__ y,
+                                                         float* __restrict__ mean_out, float* __restrict__ invstd_out,
+                                                         float* __restrict__ run_mean, float* __restrict__ run_var) {
+  const int c = blockIdx.y, split = blockIdx.x;
+  double s1, s2;
+  bn_channel_sums(sums, ns, c, &s1, &s2);
+  const double mean_d = s1 / count;
+  double var_d = s2 / count - mean_d * mean_d;
+  var_d = var_d > 0.0 ? var_d : 0.0;
+  const float mean = (float)mean_d;
+  const float invstd = (float)(1.0 / sqrt(var_d + (double)d.eps));
+  if (split == 0 && threadIdx.x == 0) {
+    mean_out[c] = mean;
+    invstd_out[c] = invstd;
+    if (run_mean) {
+      const double unbiased = count > 1.0 ? var_d * count / (count - 1.0) : var_d;
+      run_mean[c] = (float)((1.0 - d.momentum) * run_mean[c] + d.momentum * mean_d);
+      run_var[c] = (float)((1.0 - d.momentum) * run_var[c] + d.momentum * unbiased);
+    }
+  }
+  const float sc = invstd * gamma[c];
+  const float sh = beta[c] - mean * sc;
+  const bool relu = d.relu != 0;
+  bn_visit(d, c, bn_range(d, split), [&](size_t o, int n) {
+    if (n == 4) {
+      float4 v = *reinterpret_cast<const float4*>(x + o);
+      v.x = v.x * sc + sh;
+      v.y = v.y * sc + sh;
+      v.z = v.z * sc + sh;
+      v.w = v.w * sc + sh;
+      if (r) {
+        const float4 q = *reinterpret_cast<const float4*>(r + o);
+        v.x += q.x;
+        v.y += q.y;
+        v.z += q.z;
+        v.w += q.w;
+      }
+      if (relu) {
+        v.x = fmaxf(v.x, 0.f);
+        v.y = fmaxf(v.y, 0.f);
+        v.z = fmaxf(v.z, 0.f);
+        v.w = fmaxf(v.w, 0.f);
+      }
+      *reinterpret_cast<float4*>(y + o) = v;
+    } else {
+      float v = x[o] * sc + sh;
+      if (r) v += r[o];
+      if (relu) v = fmaxf(v, 0.f);
+      y[o] = v;
+    }
+  });
+}
+
+// backward statistics: sum g', sum g' * (x - mean), g' = g * [y > 0] (relu) or g
+__global__ __launch_bounds__(BN_THREADS) void bn_bwd_stats_k(vfd_bn_desc d, const float* __restrict__ g,
+                                                             const float* __restrict__ y, const float* __restrict__ x,
+                                                             const float* __restrict__ mean_in,
+                                                             double* __restrict__ partial) {
+  __shared__ double sh[BN_THREADS / 64];
+  const int c = blockIdx.y, split = blockIdx.x;
+  const float mean = mean_in[c];
+  const bool relu = d.relu != 0;
+  double s1 = 0.0, s2 = 0.0;
+  bn_visit(d, c, bn_range(d, split), [&](size_t o, int n) {
+    if (n == 4) {
+      float4 gv = *reinterpret_cast<const float4*>(g + o);
+      const float4 xv = *reinterpret_cast<const float4*>(x + o);
+      if (relu) {
+        const float4 yv = *reinterpret_cast<const float4*>(y + o);
+        gv.x = yv.x > 0.f ? gv.x : 0.f;
+        gv.y = yv.y > 0.f ? gv.y : 0.f;
+        gv.z = yv.z > 0.f ? gv.z : 0.f;
+        gv.w = yv.w > 0.f ? gv.w : 0.f;
+      }
+      s1 += ((double)gv.x + (double)gv.y) + ((double)gv.z + (double)gv.w);
+      s2 += ((double)gv.x * (double)(xv.x - mean) + (double)gv.y * (double)(xv.y - mean)) +
+            ((double)gv.z * (double)(xv.z - mean) + (double)gv.w * (double)(xv.w - mean));
+    } else {
+      float gv = g[o];
+      if (relu && !(y[o] > 0.f)) gv = 0.f;
+      s1 += gv;
+      s2 += (double)gv * (double)(x[o] - mean);
+    }
+  });
+  s1 = block_sum(s1, sh);
+  s2 = block_sum(s2, sh);
+  if (threadIdx.x == 0) {
+    partial[((size_t)c * d.S + split) * 2] = s1;
+    partial[((size_t)c * d.S + split) * 2 + 1] = s2;
+  }
+}
+
+// dx = gamma * invstd * (g' - sum g'/n - (x - mean) * invstd^2 * sum g'(x - mean) / n); dr = g';
+// block (0, c) stores d gamma = invstd * sum g'(x - mean), d beta = sum g'
+__global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply_k(vfd_bn_desc d, const float* __restrict__ g,
+                                                             const float* __restrict__ y, const float* __restrict__ x,
+                                                             const double* __restrict__ sums, int ns, double count,
+                                                             const float* __restrict__ gamma,
+                                                             const float* __restrict__ mean_in,
+                                                             const float* __restrict__ invstd_in,
+                                                             float* __restrict__ dx, float* __restrict__ dr,
+                                                             float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  const int c = blockIdx.y, split = blockIdx.x;
+  double sg, sgx;
+  bn_channel_sums(sums, ns, c, &sg, &sgx);
+  const float mean = mean_in[c], invstd = invstd_in[c];
+  if (split == 0 && threadIdx.x == 0) {
+    if (dgamma) dgamma[c] = (float)(sgx * invstd);
+    if (dbeta) dbeta[c] = (float)sg;
+  }
+  const float k = gamma[c] * invstd;
+  const float mg = (float)(sg / count);
+  const float mx = (float)(sgx / count) * invstd * invstd;
+  const bool relu = d.relu != 0;
+  bn_visit(d, c, bn_range(d, split), [&](size_t o, int n) {
+    if (n == 4) {
+      float4 gv = *reinterpret_cast<const float4*>(g + o);
+      const float4 xv = *reinterpret_cast<const float4*>(x + o);
+      if (relu) {
+        const float4 yv = *reinterpret_cast<const float4*>(y + o);
+        gv.x = yv.x > 0.f ? gv.x : 0.f;
+        gv.y = yv.y > 0.f ? gv.y : 0.f;
+        gv.z = yv.z > 0.f ? gv.z : 0.f;
+        gv.w = yv.w > 0.f ? gv.w : 0.f;
+      }
+      if (dr) *reinterpret_cast<float4*>(dr + o) = gv;
+      if (dx) {
+        float4 o4;
+        o4.x = k * (gv.x - mg - (xv.x - mean) * mx);
+        o4.y = k * (gv.y - mg - (xv.y - mean) * mx);
+        o4.z = k * (gv.z - mg - (xv.z - mean) * mx);
+        o4.w = k * (gv.w - mg - (xv.w - mean) * mx);
+        *reinterpret_cast<float4*>(dx + o) = o4;
+      }
+    } else {
+      float gv = g[o];
+      if (relu && !(y[o] > 0.f)) gv = 0.f;
+      if (dr) dr[o] = gv;
+      if (dx) dx[o] = k * (gv - mg - (x[o] - mean) * mx);
+    }
+  });
+}
+
+}  // namespace vfd
+
+using namespace vfd;
+
+extern "C" {
+
+int vfd_bn_splits(const vfd_bn_desc* d) {
+  if (!d || d->N <= 0 || d->C <= 0 || d->HW <= 0) return 0;
+  // ~4096 blocks per pass, >= 2048 elements per block
+  const long long total = (long long)d->N * d->HW;
+  long long s = (4096 + d->C - 1) / d->C;
+  const long long most = (total + 2047) / 2048;
+  if (s > most) s = most;
+  if (s < 1) s = 1;
+  return (int)s;
+}
+
+static int bn_check(const vfd_bn_desc* d, const char* what) {
+  VFD_REQUIRE(d && d->N > 0 && d->C > 0 && d->HW > 0 && d->S > 0 && d->S == vfd_bn_splits(d),
+              "%s: bad descriptor (S must be vfd_bn_splits)", what);
+  return VFD_OK;
+}
+
+int vfd_bn_fwd_stats(const vfd_bn_desc* d, const float* x, double* partial, void* stream) {
+  if (int e = bn_check(d, "bn_fwd_stats")) return e;
+  VFD_REQUIRE(x && partial, "bn_fwd_stats: null argument");
+  hipStream_t s = (hipStream_t)stream;
+  ProfScope ps(K_BN_FWD, s);
+  bn_stats_k<<<dim3(d->S, d->C), BN_THREADS, 0, s>>>(*d, x, partial);
+  return fail_launch("bn_fwd_stats");
+}
+
+int vfd_bn_sum(const vfd_bn_desc* d, const double* partial, double* sums, void* stream) {
+  if (int e = bn_check(d, "bn_sum")) return e;
+  VFD_REQUIRE(partial && sums, "bn_sum: null argument");
+  hipStream_t s = (hipStream_t)stream;
+  bn_sum_k<<<(d->C + 255) / 256, 256, 0, s>>>(*d, partial, sums);
+  return fail_launch("bn_sum");
+}
+
+int vfd_bn_fwd_apply(const vfd_bn_desc* d, const float* x, const float* residual, const double* sums, int ns,
+                     double count, const float* gamma, const float* beta, float* y, float* mean, float* invstd,
+                     float* running_mean, float* running_var, void* stream) {
+  if (int e = bn_check(d, "bn_fwd_apply")) return e;
+  VFD_REQUIRE(x && sums && gamma && beta && y && mean && invstd && (ns == 1 || ns == d->S) && count > 0.0,
+              "bn_fwd_apply: bad argument");
+  VFD_REQUIRE(!running_mean == !running_var, "bn_fwd_apply: running mean / var must come together");
+  hipStream_t s = (hipStream_t)stream;
+  ProfScope ps(K_BN_FWD, s);
+  bn_apply_k<<<dim3(d->S, d->C), BN_THREADS, 0, s>>>(*d, x, residual, sums, ns, count, gamma, beta, y, mean, invstd,
+                                                     running_mean, running_var);
+  return fail_launch("bn_fwd_apply");
+}
+
+int vfd_bn_bwd_stats(const vfd_bn_desc* d, const float* g, const float* y, const float* x, const float* mean,
+                     double* partial, void* stream) {
+  if (int e = bn_check(d, "bn_bwd_stats")) return e;
+  VFD_REQUIRE(g && x && mean && partial && (y || !d->relu), "bn_bwd_stats: null argument");
+  hipStream_t s = (hipStream_t)stream;
+  ProfScope ps(K_BN_BWD, s);
+  bn_bwd_stats_k<<<dim3(d->S, d->C), BN_THREADS, 0, s>>>(*d, g, y, x, mean, partial);
+  return fail_launch("bn_bwd_stats");
+}
+
+int vfd_bn_bwd_apply(const vfd_bn_desc* d, const float* g, const float* y, const float* x, const double* sums,
+                     int ns, double count, const float* gamma, const float* mean, const float* invstd, float* dx,
+                     float* dresidual, float* dgamma, float* dbeta, void* stream) {
+  if (int e = bn_check(d, "bn_bwd_apply")) return e;
+  VFD_REQUIRE(g && x && sums && gamma && mean && invstd && (y || !d->relu) && (ns == 1 || ns == d->S) &&
+                  count > 0.0,
+              "bn_bwd_apply: bad argument");
+  hipStream_t s = (hipStream_t)stream;
+  ProfScope ps(K_BN_BWD, s);
+  bn_bwd_apply_k<<<dim3(d->S, d->C), BN_THREADS, 0, s>>>(*d, g, y, x, sums, ns, count, gamma, mean, invstd, dx,
+                                                         dresidual, dgamma, dbeta);
+  return fail_launch("bn_bwd_apply");
+}
+
+}  // extern "C"

@@ -805,3 +805,91 @@ class AggregateUp(torch.autograd.Function):
         grads = [torch.ops.aten.upsample_bilinear2d_backward(d, list(out.shape[-2:]), list(shp), True, None, None)
                  for shp in ctx.level_shapes]
         return (d, d.sum((0, 2, 3))) + tuple(grads)
+
+
+# =============================================================================================
+# Fused training-mode BatchNorm (+ residual) (+ ReLU) of the ResNet encoders (bnact.hip)
+# =============================================================================================
+def _bn_group(bn):
+    """SyncBatchNorm under an initialised process group of > 1 ranks -> that group, else None
+    (nn.SyncBatchNorm itself falls back to the local batch norm at world size 1)."""
+    import torch.distributed as dist
+    if not isinstance(bn, torch.nn.SyncBatchNorm) or not (dist.is_available() and dist.is_initialized()):
+        return None
+    pg = bn.process_group or dist.group.WORLD
+    return pg if dist.get_world_size(pg) > 1 else None
+
+
+def _bn_sync(lib, d, partial, pg, what, count=None):
+    """Per-channel [C, 2] fp64 sums reduced over the group (+ the global element count when the
+    local one is given: ranks may hold different batch sizes, as SyncBatchNorm allows)."""
+    import torch.distributed as dist
+    sums = torch.empty(d.C, 2, dtype=torch.float64, device=partial.device)
+    L.check(lib.vfd_bn_sum(ctypes.byref(d), partial.data_ptr(), sums.data_ptr(), L.stream()), what)
+    dist.all_reduce(sums, group=pg)
+    if count is None:
+        return sums, None
+    cnt = torch.tensor([float(count)], dtype=torch.float64, device=partial.device)
+    dist.all_reduce(cnt, group=pg)
+    return sums, float(cnt.item())
+
+
+class BatchNormAct(torch.autograd.Function):
+    """y = relu(batch_norm_train(x) [+ r]) for NCHW fp32 x (one statistics + one apply pass each
+    way; running statistics updated like nn.BatchNorm2d.train()).  `pg`: the SyncBatchNorm group
+    (None = local statistics)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, residual, running_mean, running_var, eps, momentum, relu, pg):
+        lib = L.load()
+        _check_device(x, 'batch norm input')
+        x = x.contiguous()
+        N, C, H, W = x.shape
+        d = L.BnDesc(N, C, H * W, 0, int(relu), float(eps), float(momentum))
+        d.S = lib.vfd_bn_splits(ctypes.byref(d))
+        r = residual.contiguous() if residual is not None else None
+        partial = torch.empty(C, d.S, 2, dtype=torch.float64, device=x.device)
+        L.check(lib.vfd_bn_fwd_stats(ctypes.byref(d), x.data_ptr(), partial.data_ptr(), L.stream()), 'bn_fwd_stats')
+        count, sums, ns = float(N * H * W), partial, d.S
+        if pg is not None:
+            (sums, count), ns = _bn_sync(lib, d, partial, pg, 'bn_sum', count), 1
+        y = torch.empty_like(x)
+        mean = torch.empty(C, device=x.device)
+        invstd = torch.empty(C, device=x.device)
+        L.check(lib.vfd_bn_fwd_apply(ctypes.byref(d), x.data_ptr(), r.data_ptr() if r is not None else None,
+                                     sums.data_ptr(), ns, count, gamma.data_ptr(), beta.data_ptr(), y.data_ptr(),
+                                     mean.data_ptr(), invstd.data_ptr(),
+                                     running_mean.data_ptr() if running_mean is not None else None,
+                                     running_var.data_ptr() if running_var is not None else None, L.stream()),
+                'bn_fwd_apply')
+        ctx.d, ctx.pg, ctx.count, ctx.has_res = (d.N, d.C, d.HW, d.S, d.relu, d.eps, d.momentum), pg, count, r is not None
+        if L.PROF_ON:                        # compulsory: x (+ r) in, y out
+            L.ALG_BYTES['bn_fwd'] += x.numel() * 4 * (2 + (r is not None))
+        ctx.save_for_backward(x, y, gamma, mean, invstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        lib = L.load()
+        x, y, gamma, mean, invstd = ctx.saved_tensors
+        d = L.BnDesc(*ctx.d)
+        g = g.contiguous()
+        partial = torch.empty(d.C, d.S, 2, dtype=torch.float64, device=g.device)
+        yp = y.data_ptr() if d.relu else None
+        L.check(lib.vfd_bn_bwd_stats(ctypes.byref(d), g.data_ptr(), yp, x.data_ptr(), mean.data_ptr(),
+                                     partial.data_ptr(), L.stream()), 'bn_bwd_stats')
+        sums, ns, count = partial, d.S, ctx.count
+        if ctx.pg is not None:
+            sums, ns = _bn_sync(lib, d, partial, ctx.pg, 'bn_sum')[0], 1
+        need = ctx.needs_input_grad
+        dx = torch.empty_like(x) if need[0] else None
+        dr = torch.empty_like(x) if ctx.has_res and need[3] else None
+        dgamma = torch.empty_like(gamma) if need[1] else None
+        dbeta = torch.empty_like(gamma) if need[2] else None
+        ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+        if L.PROF_ON:                        # compulsory: g, x (, y) in, dx (, dr) out
+            L.ALG_BYTES['bn_bwd'] += x.numel() * 4 * (2 + d.relu + (dx is not None) + (dr is not None))
+        L.check(lib.vfd_bn_bwd_apply(ctypes.byref(d), g.data_ptr(), yp, x.data_ptr(), sums.data_ptr(), ns, count,
+                                     gamma.data_ptr(), mean.data_ptr(), invstd.data_ptr(), ptr(dx), ptr(dr),
+                                     ptr(dgamma), ptr(dbeta), L.stream()), 'bn_bwd_apply')
+        return dx, dgamma, dbeta, dr, None, None, None, None, None, None

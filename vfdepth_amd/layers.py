@@ -12,6 +12,7 @@
   reflect-padded ELU decoder).  Parameter names follow torchvision's ResNet so an
   ImageNet or reference-trained state dict loads unchanged.
 """
+import os
 from collections import OrderedDict
 
 import numpy as np
@@ -70,6 +71,24 @@ def upsample(x):
 
 
 # ----------------------------------------------------------------------------- ResNet encoder
+def bn_act(bn, x, residual=None, relu=True):
+    """relu(bn(x) [+ residual]): one fused HIP kernel pair (bnact.hip, SyncBatchNorm-aware) for a
+    training-mode fp32 BatchNorm2d on the GPU; the module + torch ops otherwise (eval mode, bf16
+    autocast, CPU).  VFD_FUSED_BN=0 disables the fused path."""
+    if (bn.training and bn.track_running_stats and bn.affine and bn.momentum is not None and x.is_cuda
+            and x.dim() == 4 and x.dtype == torch.float32 and not torch.is_autocast_enabled('cuda')
+            and os.environ.get('VFD_FUSED_BN', '1') != '0'
+            and (residual is None or residual.shape == x.shape and residual.dtype == x.dtype)):
+        from . import kernels as KN
+        bn.num_batches_tracked.add_(1)
+        return KN.BatchNormAct.apply(x, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var,
+                                     bn.eps, bn.momentum, relu, KN._bn_group(bn))
+    y = bn(x)
+    if residual is not None:
+        y = y + residual
+    return F.relu(y, inplace=True) if relu else y
+
+
 class BasicBlock(nn.Module):
     expansion = 1
 
@@ -83,10 +102,9 @@ class BasicBlock(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
-        idt = x if self.downsample is None else self.downsample(x)
-        y = self.relu(self.bn1(self.conv1(x)))
-        y = self.bn2(self.conv2(y))
-        return self.relu(y + idt)
+        idt = x if self.downsample is None else bn_act(self.downsample[1], self.downsample[0](x), relu=False)
+        y = bn_act(self.bn1, self.conv1(x))
+        return bn_act(self.bn2, self.conv2(y), residual=idt)
 
 
 class Bottleneck(nn.Module):
@@ -104,11 +122,10 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
-        idt = x if self.downsample is None else self.downsample(x)
-        y = self.relu(self.bn1(self.conv1(x)))
-        y = self.relu(self.bn2(self.conv2(y)))
-        y = self.bn3(self.conv3(y))
-        return self.relu(y + idt)
+        idt = x if self.downsample is None else bn_act(self.downsample[1], self.downsample[0](x), relu=False)
+        y = bn_act(self.bn1, self.conv1(x))
+        y = bn_act(self.bn2, self.conv2(y))
+        return bn_act(self.bn3, self.conv3(y), residual=idt)
 
 
 _RESNET_SPECS = {18: (BasicBlock, [2, 2, 2, 2]), 34: (BasicBlock, [3, 4, 6, 3]),
@@ -169,7 +186,7 @@ class ResnetEncoder(nn.Module):
     def forward(self, image):
         e = self.encoder
         x = (image - 0.45) / 0.225
-        f0 = e.relu(e.bn1(e.conv1(x)))
+        f0 = bn_act(e.bn1, e.conv1(x))
         f1 = e.layer1(e.maxpool(f0))
         f2 = e.layer2(f1)
         f3 = e.layer3(f2)

@@ -83,3 +83,43 @@ def test_net_precision_flag():
     from vfdepth_amd.vfdepth import VFDepthAlgo
     with pytest.raises(ValueError):
         VFDepthAlgo(C.surround_fusion_cfg(net_precision='fp16'), 'cpu')
+
+
+def test_batched_pose_and_warp_matrices_match_per_camera():
+    """The batched pose distribution + warp-matrix chain (one gather + batched products) equals the
+    per-camera reference formulation (pose.py:66-96, view_rendering.py:118-198) bit for bit."""
+    import copy
+    import common as G
+    from vfdepth_amd.geometry import Pose, ViewRendering, inverse4x4
+    from vfdepth_amd.rotation import axis_angle_to_matrix
+    cfg = G.step_cfg()
+    N = cfg['data']['num_cams']
+    B = 2
+    gen = torch.Generator().manual_seed(5)
+    R = axis_angle_to_matrix(0.3 * torch.randn(B, N, 3, generator=gen))
+    E = torch.eye(4).repeat(B, N, 1, 1)
+    E[:, :, :3, :3] = R
+    E[:, :, :3, 3] = torch.randn(B, N, 3, generator=gen)
+    K = torch.eye(4).repeat(B, N, 1, 1)
+    K[:, :, 0, 0], K[:, :, 1, 1] = 200.0, 210.0
+    K[:, :, 0, 2], K[:, :, 1, 2] = 80.0, 48.0
+    inputs = {('K', 0): K, 'extrinsics': E, 'extrinsics_inv': inverse4x4(E)}
+    pose = Pose(cfg)
+    T = {}
+    for f in cfg['training']['frame_ids'][1:]:
+        Tf = torch.eye(4).repeat(B, 1, 1)
+        Tf[:, :3, :3] = axis_angle_to_matrix(0.05 * torch.randn(B, 3, generator=gen))
+        Tf[:, :3, 3] = 0.5 * torch.randn(B, 3, generator=gen)
+        T[('cam_T_cam', 0, f)] = Tf
+    out = pose.distribute_pose(T, E, inputs['extrinsics_inv'])
+    for f in cfg['training']['frame_ids'][1:]:
+        for c in range(N):
+            ref = inputs['extrinsics_inv'][:, c] @ E[:, 0] @ T['cam_T_cam', 0, f] @ inputs['extrinsics_inv'][:, 0] @ E[:, c]
+            assert torch.equal(out[('cam', c)][('cam_T_cam', 0, f)], ref)
+    outputs = copy.copy(out)
+    vr = ViewRendering(cfg, 0)
+    rel = {c: pose.compute_relative_cam_poses(inputs, outputs, c) for c in range(N)}
+    per_cam = vr.warp_matrices(inputs, outputs, rel, list(range(N)))
+    batched = vr.warp_matrices(inputs, outputs, None, list(range(N)))
+    assert batched.shape == per_cam.shape
+    assert torch.equal(batched, per_cam)

@@ -24,6 +24,7 @@ def main():
     ap.add_argument('--top', type=int, default=70)
     ap.add_argument('--config', type=int, default=2)
     ap.add_argument('--stacks', default='', help='comma-separated aten ops to attribute by Python stack')
+    ap.add_argument('--ops', default='', help='comma-separated aten ops to list by input shapes')
     a = ap.parse_args()
     torch.cuda.set_device(0)
     _lib.load()
@@ -45,6 +46,13 @@ def main():
     print(ka.table(sort_by='self_cuda_time_total', row_limit=a.top, max_name_column_width=40,
                    max_shapes_column_width=90))
     print(prof.key_averages().table(sort_by='self_cuda_time_total', row_limit=40, max_name_column_width=50))
+    if a.ops:
+        want = set(a.ops.split(','))
+        rows = [e for e in ka if e.key in want]
+        rows.sort(key=lambda e: -e.self_device_time_total)
+        for e in rows[:80]:
+            print(f'{e.key:22s} calls {e.count / a.steps:6.1f}/step  dev {e.self_device_time_total / a.steps / 1e3:7.3f} '
+                  f'ms/step  {str(e.input_shapes)[:160]}')
     if a.stacks:
         want = set(a.stacks.split(','))
         rows = [e for e in prof.key_averages(group_by_stack_n=8) if e.key in want]

@@ -79,13 +79,18 @@ class Pose:
         return out
 
     def distribute_pose(self, poses, exts, exts_inv):
-        """Canonical (camera 0) motion -> every camera: E_c^-1 E_0 T E_0^-1 E_c."""
+        """Canonical (camera 0) motion -> every camera: E_c^-1 E_0 T E_0^-1 E_c, all cameras in one
+        batched chain (the reference's left-to-right association).  The per-camera entries are
+        views of out['_cam_T_cam'][f] = [B, N, 4, 4], which the batched warp path consumes."""
         out = {('cam', c): {} for c in range(self.num_cams)}
-        ref_ext, ref_inv = exts[:, 0], exts_inv[:, 0]
+        out['_cam_T_cam'] = {}
+        ref_ext, ref_inv = exts[:, :1], exts_inv[:, :1]
         for f in self.frame_ids[1:]:
-            T = poses['cam_T_cam', 0, f].float()
+            T = poses['cam_T_cam', 0, f].float().unsqueeze(1)
+            P = exts_inv @ ref_ext @ T @ ref_inv @ exts
+            out['_cam_T_cam'][f] = P
             for c in range(self.num_cams):
-                out[('cam', c)][('cam_T_cam', 0, f)] = exts_inv[:, c] @ ref_ext @ T @ ref_inv @ exts[:, c]
+                out[('cam', c)][('cam_T_cam', 0, f)] = P[:, c]
         return out
 
     def compute_relative_cam_poses(self, inputs, outputs, cam):
@@ -124,7 +129,12 @@ class ViewRendering(nn.Module):
         return self._plan
 
     def warp_matrices(self, inputs, outputs, rel_poses, cams):
-        """(K_src @ T)[:3] per (target camera, warp) in the plan's order -> [B, len(cams), n_warp, 3, 4]."""
+        """(K_src @ T)[:3] per (target camera, warp) in the plan's order -> [B, len(cams), n_warp, 3, 4].
+        T: the temporal pose cam_T_cam[c][f], or the relative pose (E_src^-1 E_c) [@ cam_T_cam[c][f]]
+        (pose.py:66-96).  With the batched poses of the fusion pose model and rel_poses None,
+        every warp of every camera is one gather + three batched products."""
+        if rel_poses is None:
+            return self._warp_matrices_all(inputs, outputs)[:, cams[0]:cams[-1] + 1]
         plan = self.plan(inputs[('K', 0)].device)
         K = inputs[('K', 0)]
         B = K.shape[0]
@@ -143,6 +153,39 @@ class ViewRendering(nn.Module):
             rows.append(torch.stack(mats, 1))
         return torch.stack(rows, 1)
 
+    def _warp_index(self, plan, device):
+        """Per (camera, warp) of the plan: target, source, frame slot, and kind (0 temporal,
+        1 spatial at frame 0, 2 spatio-temporal, 3 padding) as device index tensors."""
+        key = (plan, str(device))
+        if getattr(self, '_widx_key', None) != key:
+            rows = []
+            for c in range(plan.N):
+                for w in range(plan.n_warp):
+                    if w >= len(plan.entries[c]):
+                        rows.append((c, c, 0, 3))
+                        continue
+                    fs, src, os_ = plan.entries[c][w]
+                    rows.append((c, src, fs, 0 if os_ < 0 else (1 if fs == 0 else 2)))
+            t = torch.tensor(rows, dtype=torch.long, device=device)
+            self._widx = (t[:, 0], t[:, 1], t[:, 2], t[:, 3])
+            self._widx_key = key
+        return self._widx
+
+    def _warp_matrices_all(self, inputs, outputs):
+        plan = self.plan(inputs[('K', 0)].device)
+        K, E, Einv = inputs[('K', 0)], inputs['extrinsics'], inputs['extrinsics_inv']
+        B, N = K.shape[:2]
+        tgt, src, fslot, kind = self._warp_index(plan, K.device)
+        eye = torch.eye(4, device=K.device, dtype=K.dtype)
+        P_all = outputs['_cam_T_cam']
+        Pst = torch.stack([eye.expand(B, N, 4, 4) if f == 0 else P_all[f] for f in self.frame_ids], 1)
+        Pw = Pst[:, fslot, tgt]                                           # [B, n, 4, 4]
+        R = Einv[:, src] @ E[:, tgt]                                      # rel pose (0, src)
+        T = torch.where((kind == 0).view(-1, 1, 1), Pw, R @ Pw)           # R @ I == R exactly
+        M = (K[:, src] @ T)[:, :, :3, :]
+        M = torch.where((kind == 3).view(-1, 1, 1), eye[:3], M)
+        return M.view(B, N, plan.n_warp, 3, 4)
+
     def _render(self, inputs, outputs, rel_poses, cam_begin, cam_count, depth_all=None):
         """Render cameras [cam_begin, +cam_count); returns {scale: (color, cmask, ovl, omask)}."""
         plan = self.plan(inputs[('K', 0)].device)
@@ -151,12 +194,12 @@ class ViewRendering(nn.Module):
         mask = inputs['mask'][:, :, 0]
         invK = inputs[('inv_K', 0)][:, cam_begin:cam_begin + cam_count]
         packed = {}
+        M = self.warp_matrices(inputs, outputs, rel_poses, cams)          # the same at every scale
         for scale in self.scales:
             if depth_all is not None and scale in depth_all:
                 depth = depth_all[scale]
             else:
                 depth = torch.stack([outputs[('cam', c)][('depth', scale)][:, 0] for c in cams], 1)
-            M = self.warp_matrices(inputs, outputs, rel_poses, cams)
             color, cmask, ovl, omask = KN.ViewSynthesis.apply(plan, cam_begin, depth, invK, M, mask, *colors)
             for i, c in enumerate(cams):
                 view = outputs[('cam', c)]

@@ -194,6 +194,8 @@ class VFDepthAlgo:
         packed_aug = depth_feats.pop('_packed_aug', None)
         if '_extrinsics_aug' in depth_feats:          # written by VFNet (travels through DDP)
             inputs['extrinsics_aug'] = depth_feats.pop('_extrinsics_aug')
+        if '_cam_T_cam' in pose_pred:                 # batched poses of the fusion pose model
+            outputs['_cam_T_cam'] = pose_pred['_cam_T_cam']
         for c in range(self.num_cams):
             outputs[('cam', c)].update(pose_pred[('cam', c)])
             outputs[('cam', c)].update(depth_feats[('cam', c)])
@@ -253,7 +255,9 @@ class VFDepthAlgo:
                     outputs[('cam', c)][('depth', scale) + sfx] = depth[:, c].unsqueeze(1)
 
     def compute_losses(self, inputs, outputs, noise=None):
-        rel = {c: self.pose.compute_relative_cam_poses(inputs, outputs, c) for c in range(self.num_cams)}
+        # with the batched fusion poses every warp matrix comes from one batched chain (rel None)
+        rel = (None if '_cam_T_cam' in outputs else
+               {c: self.pose.compute_relative_cam_poses(inputs, outputs, c) for c in range(self.num_cams)})
         packed = self.view_rendering.render_all(inputs, outputs, rel, outputs['_depth_all'])
         if self.aug_depth:
             outputs['_tform'] = self.view_rendering.render_depth_synthesis(

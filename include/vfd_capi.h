@@ -150,10 +150,11 @@ int vfd_bn_splits(const vfd_bn_desc* d);
 int vfd_bn_fwd_stats(const vfd_bn_desc* d, const float* x, double* partial, void* stream);
 int vfd_bn_sum(const vfd_bn_desc* d, const double* partial, double* sums, void* stream);
 /* sums: the [C][S][2] partials (ns = S) or reduced [C][2] sums (ns = 1); residual / running stats
- * nullable.  Writes y and the per-channel mean / invstd the backward reads. */
+ * / num_batches_tracked (int64, += 1) nullable.  Writes y and the per-channel mean / invstd the
+ * backward reads. */
 int vfd_bn_fwd_apply(const vfd_bn_desc* d, const float* x, const float* residual, const double* sums, int ns,
                      double count, const float* gamma, const float* beta, float* y, float* mean, float* invstd,
-                     float* running_mean, float* running_var, void* stream);
+                     float* running_mean, float* running_var, long long* num_batches_tracked, void* stream);
 /* g = d y; y = the forward's output (ReLU mask; unused without ReLU) */
 int vfd_bn_bwd_stats(const vfd_bn_desc* d, const float* g, const float* y, const float* x, const float* mean,
                      double* partial, void* stream);

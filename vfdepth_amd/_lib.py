@@ -85,7 +85,7 @@ _SIGS = {
     'vfd_bn_splits': (c_int, [ctypes.POINTER(BnDesc)]),
     'vfd_bn_fwd_stats': (c_int, [ctypes.POINTER(BnDesc), c_fp, c_fp, c_void_p]),
     'vfd_bn_sum': (c_int, [ctypes.POINTER(BnDesc), c_fp, c_fp, c_void_p]),
-    'vfd_bn_fwd_apply': (c_int, [ctypes.POINTER(BnDesc), c_fp, c_fp, c_fp, c_int, c_double] + [c_fp] * 7 + [c_void_p]),
+    'vfd_bn_fwd_apply': (c_int, [ctypes.POINTER(BnDesc), c_fp, c_fp, c_fp, c_int, c_double] + [c_fp] * 8 + [c_void_p]),
     'vfd_bn_bwd_stats': (c_int, [ctypes.POINTER(BnDesc)] + [c_fp] * 5 + [c_void_p]),
     'vfd_bn_bwd_apply': (c_int, [ctypes.POINTER(BnDesc), c_fp, c_fp, c_fp, c_fp, c_int, c_double] + [c_fp] * 7
                          + [c_void_p]),

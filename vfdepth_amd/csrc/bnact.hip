@@ -116,8 +116,10 @@ __global__ __launch_bounds__(BN_THREADS) void bn_apply_k(vfd_bn_desc d, const fl
                                                          int ns, double count, const float* __restrict__ gamma,
                                                          const float* __restrict__ beta, float* __restrict__ y,
                                                          float* __restrict__ mean_out, float* __restrict__ invstd_out,
-                                                         float* __restrict__ run_mean, float* __restrict__ run_var) {
+                                                         float* __restrict__ run_mean, float* __restrict__ run_var,
+                                                         long long* __restrict__ nbt) {
   const int c = blockIdx.y, split = blockIdx.x;
+  if (nbt && c == 0 && split == 0 && threadIdx.x == 0) nbt[0] += 1;   // num_batches_tracked
   double s1, s2;
   bn_channel_sums(sums, ns, c, &s1, &s2);
   const double mean_d = s1 / count;
@@ -299,7 +301,7 @@ int vfd_bn_sum(const vfd_bn_desc* d, const double* partial, double* sums, void* 
 
 int vfd_bn_fwd_apply(const vfd_bn_desc* d, const float* x, const float* residual, const double* sums, int ns,
                      double count, const float* gamma, const float* beta, float* y, float* mean, float* invstd,
-                     float* running_mean, float* running_var, void* stream) {
+                     float* running_mean, float* running_var, long long* num_batches_tracked, void* stream) {
   if (int e = bn_check(d, "bn_fwd_apply")) return e;
   VFD_REQUIRE(x && sums && gamma && beta && y && mean && invstd && (ns == 1 || ns == d->S) && count > 0.0,
               "bn_fwd_apply: bad argument");
@@ -307,7 +309,7 @@ int vfd_bn_fwd_apply(const vfd_bn_desc* d, const float* x, const float* residual
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_BN_FWD, s);
   bn_apply_k<<<dim3(d->S, d->C), BN_THREADS, 0, s>>>(*d, x, residual, sums, ns, count, gamma, beta, y, mean, invstd,
-                                                     running_mean, running_var);
+                                                     running_mean, running_var, num_batches_tracked);
   return fail_launch("bn_fwd_apply");
 }
 

@@ -840,7 +840,7 @@ class BatchNormAct(torch.autograd.Function):
     (None = local statistics)."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, residual, running_mean, running_var, eps, momentum, relu, pg):
+    def forward(ctx, x, gamma, beta, residual, running_mean, running_var, eps, momentum, relu, pg, nbt=None):
         lib = L.load()
         _check_device(x, 'batch norm input')
         x = x.contiguous()
@@ -860,7 +860,8 @@ class BatchNormAct(torch.autograd.Function):
                                      sums.data_ptr(), ns, count, gamma.data_ptr(), beta.data_ptr(), y.data_ptr(),
                                      mean.data_ptr(), invstd.data_ptr(),
                                      running_mean.data_ptr() if running_mean is not None else None,
-                                     running_var.data_ptr() if running_var is not None else None, L.stream()),
+                                     running_var.data_ptr() if running_var is not None else None,
+                                     nbt.data_ptr() if nbt is not None else None, L.stream()),
                 'bn_fwd_apply')
         ctx.d, ctx.pg, ctx.count, ctx.has_res = (d.N, d.C, d.HW, d.S, d.relu, d.eps, d.momentum), pg, count, r is not None
         if L.PROF_ON:                        # compulsory: x (+ r) in, y out
@@ -892,4 +893,4 @@ class BatchNormAct(torch.autograd.Function):
         L.check(lib.vfd_bn_bwd_apply(ctypes.byref(d), g.data_ptr(), yp, x.data_ptr(), sums.data_ptr(), ns, count,
                                      gamma.data_ptr(), mean.data_ptr(), invstd.data_ptr(), ptr(dx), ptr(dr),
                                      ptr(dgamma), ptr(dbeta), L.stream()), 'bn_bwd_apply')
-        return dx, dgamma, dbeta, dr, None, None, None, None, None, None
+        return dx, dgamma, dbeta, dr, None, None, None, None, None, None, None

@@ -80,9 +80,9 @@ def bn_act(bn, x, residual=None, relu=True):
             and os.environ.get('VFD_FUSED_BN', '1') != '0'
             and (residual is None or residual.shape == x.shape and residual.dtype == x.dtype)):
         from . import kernels as KN
-        bn.num_batches_tracked.add_(1)
         return KN.BatchNormAct.apply(x, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var,
-                                     bn.eps, bn.momentum, relu, KN._bn_group(bn))
+                                     bn.eps, bn.momentum, relu, KN._bn_group(bn),
+                                     bn.num_batches_tracked)      # += 1 inside the apply kernel
     y = bn(x)
     if residual is not None:
         y = y + residual

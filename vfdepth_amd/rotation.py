@@ -17,14 +17,32 @@ def axis_angle_to_quaternion(axis_angle):
     return torch.cat([torch.cos(half), axis_angle * k], dim=-1)
 
 
+# pytorch3d's quaternion_to_matrix entries as (product a, product b, sign of b, sign of the s-term)
+# over the 16 products q_x * q_y (x, y in r, i, j, k): m = [1|0] + sign_s * s * (P_a + sign_b * P_b)
+# — the same products and sums in the same order, so the values are identical; as gathers over one
+# outer product it is ~10 kernels each way instead of ~30 scalar-shaped ones.
+_QM_A = (10, 6, 7, 6, 5, 11, 7, 11, 5)          # jj, ij, ik, ij, ii, jk, ik, jk, ii
+_QM_B = (15, 12, 8, 12, 15, 4, 8, 4, 10)        # kk, kr, jr, kr, kk, ir, jr, ir, jj
+_QM_SB = (1., -1., 1., 1., 1., -1., -1., 1., 1.)
+_QM_SS = (-1., 1., 1., 1., -1., 1., 1., 1., -1.)
+_QM_BASE = (1., 0., 0., 0., 1., 0., 0., 0., 1.)
+_QM_CACHE = {}
+
+
+def _qm_consts(device, dtype):
+    key = (str(device), dtype)
+    if key not in _QM_CACHE:
+        mk = lambda v, dt=dtype: torch.tensor(v, device=device, dtype=dt)  # noqa: E731
+        _QM_CACHE[key] = (mk(_QM_A, torch.long), mk(_QM_B, torch.long), mk(_QM_SB), mk(_QM_SS), mk(_QM_BASE))
+    return _QM_CACHE[key]
+
+
 def quaternion_to_matrix(q):
-    r, i, j, k = torch.unbind(q, -1)
-    s = 2.0 / (q * q).sum(-1)
-    m = torch.stack((
-        1 - s * (j * j + k * k), s * (i * j - k * r), s * (i * k + j * r),
-        s * (i * j + k * r), 1 - s * (i * i + k * k), s * (j * k - i * r),
-        s * (i * k - j * r), s * (j * k + i * r), 1 - s * (i * i + j * j),
-    ), -1)
+    ia, ib, sb, ss, base = _qm_consts(q.device, q.dtype)
+    s = 2.0 / (q * q).sum(-1, keepdim=True)
+    P = (q.unsqueeze(-1) * q.unsqueeze(-2)).flatten(-2)
+    t = P.index_select(-1, ia) + sb * P.index_select(-1, ib)
+    m = base + ss * (s * t)
     return m.reshape(q.shape[:-1] + (3, 3))
 
 

@@ -2,6 +2,7 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
-bash scripts/gpu_bench.sh r2_bn --steps 10 --no-cpu-baseline --no-parity || exit 1
-VFD_FUSED_BN=0 bash scripts/gpu_bench.sh r2_nobn --steps 10 --no-cpu-baseline --no-parity || exit 1
-timeout -k 10 400 python tools/diag_ops.py > gpurun_out/ops.txt 2> gpurun_out/ops.err
+K="config3_step_b2 or full_step_gradient_chain" bash scripts/gpu_tests.sh tests/test_gpu_fullsize.py tests/test_gpu_parity.py || exit 1
+cp gpurun_out/tests/tests.log gpurun_out/tests_fix.log
+bash scripts/gpu_bench.sh r2_all --steps 20 --no-cpu-baseline || exit 1
+bash scripts/gpu_profile.sh r2

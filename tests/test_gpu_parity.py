@@ -478,8 +478,14 @@ def test_full_step_gradient_chain():
     disp = outputs['_disp_all'][0]
     disp.retain_grad()
     Ts = {(c, f): outputs[('cam', c)][('cam_T_cam', 0, f)] for c in range(N) for f in frames[1:]}
-    for t in Ts.values():
+    # the fusion pose model's per-camera poses are views of one [B, N, 4, 4] tensor per frame,
+    # which the batched warp path consumes: the gradient lands there
+    P_all = outputs.get('_cam_T_cam')
+    for t in (P_all.values() if P_all is not None else Ts.values()):
         t.retain_grad()
+
+    def t_grad(k):
+        return P_all[k[1]].grad[:, k[0]] if P_all is not None else Ts[k].grad
     losses['total_loss'].backward()
     # 1. loss path on the GPU's disparities / poses
     ci = dict(cpu_inputs)
@@ -503,8 +509,8 @@ def test_full_step_gradient_chain():
     print(f'loss path: {int(near.sum())} of {near.numel()} px within 1e-4 of a decision')
     fro, mx = _fro(disp.grad[keep.to(DEV)], d_leaf.grad[keep])
     assert fro < 1e-3 and mx < 1e-2, f'd loss / d disp (outside {int(near.sum())} near-tie px): fro {fro:.3g}, max {mx:.3g}'
-    for k, t in Ts.items():
-        fro, mx = _fro(t.grad, T_leaf[k].grad)
+    for k in Ts:
+        fro, mx = _fro(t_grad(k), T_leaf[k].grad)
         assert fro < 5e-3, f'd loss / d cam_T_cam{k}: fro {fro:.3g}'
     # 2. nets: inject the GPU's upstream gradients into the oracle step
     dn, pn = FusedDepthNet(cfg), FusedPoseNet(cfg)
@@ -517,7 +523,7 @@ def test_full_step_gradient_chain():
     o_out, _ = O.process_batch(O.nets_from_modules(dn, pn), cpu_inputs, cfg, [n for n in noise])
     hook.remove()
     tensors = [held['disp']] + [o_out[('cam', c)][('cam_T_cam', 0, f)] for (c, f) in Ts]
-    grads = [disp.grad.detach().cpu().reshape(held['disp'].shape)] + [t.grad.detach().cpu() for t in Ts.values()]
+    grads = [disp.grad.detach().cpu().reshape(held['disp'].shape)] + [t_grad(k).detach().cpu() for k in Ts]
     torch.autograd.backward(tensors, grads)
     # The ResNet encoders' train-mode BatchNorm backward cancels (dx = (g - mean g - x̂·mean g x̂)/σ):
     # on the CPU alone a 1e-7 relative input perturbation moves encoder gradients by up to 4e-3

@@ -47,6 +47,10 @@ typedef struct vfd_voxel_desc {
   const float* axis_z;   /* [Z]                                                          */
   const float* dbins;    /* [D] frustum depths (torch.linspace fp32), device             */
   const int32_t* group;  /* [N] overlap group of each camera (0: {0,3,4}, 1: {1,2,5})    */
+  int32_t deterministic; /* 1: every gradient sums in a fixed order (torch.backends.cudnn.  */
+                         /*    deterministic, as the reference's train.py:23 sets): the   */
+                         /*    fusion plan's buckets and K3's cell lists are ordered by   */
+                         /*    voxel / sample, and K3's heavy tiles are not split         */
 } vfd_voxel_desc;
 
 /* F.interpolate(mask, [h, w], 'bilinear', align_corners=True)
@@ -68,6 +72,12 @@ size_t vfd_fuse_depth_bwd_workspace(const vfd_voxel_desc* d);
 int vfd_fuse_depth_bwd(const vfd_voxel_desc* d, const float* d_vox, const float* vox,
                        const float* mask_lo, const float* K, const float* Einv, float* dP,
                        float* d_wzb, void* workspace, size_t ws_bytes, void* stream);
+/* K1 backward as an atomic-free gather over the fusion plan's tile buckets (the plan vfd_fusion_plan
+ * builds for the K2 backward; same arguments otherwise, Cv = 64): d P written with plain stores,
+ * summed in bucket order (deterministic once the buckets are, see vfd_fusion_plan_sort). */
+int vfd_fuse_depth_bwd_planned(const vfd_voxel_desc* d, const void* plan, const float* d_vox, const float* vox,
+                               const float* mask_lo, const float* K, const float* Einv, float* dP, float* d_wzb,
+                               void* workspace, size_t ws_bytes, void* stream);
 
 /* Fusion plan (volumetric_fusionnet.py:132-140, 166-195): for every (batch, camera) the compacted
  * list of voxels the camera sees (32-B entries: voxel | valid-camera count | in-range taps, corner

@@ -222,14 +222,17 @@ def _fusion_inputs(cfg, seed):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize('config', [2, 5])
-def test_fuse_depth_full_size(config):
+@pytest.mark.parametrize('config,k1', [(2, 'gather'), (2, 'scatter'), (5, 'gather')])
+def test_fuse_depth_full_size(config, k1, monkeypatch):
     """K1 (depth-mode backproject_into_voxel + the overlap / non-overlap 1x1 MLPs,
     volumetric_fusionnet.py:116-230) on the full grid: 100x100x20 (config 2) and 200x200x20
-    (config 5), C=256 -> Cv=64, forward against the oracle; backward too at config 2."""
+    (config 5), C=256 -> Cv=64, forward against the oracle; backward too at config 2, through the
+    atomic-free gather over the fusion plan (the default) and the atomic scatter."""
     from oracle import vfd_oracle as O
+    from vfdepth_amd import kernels as KN
     from vfdepth_amd.fusion import VFNet
     from vfdepth_amd.layers import seeded_state_dict
+    monkeypatch.setattr(KN, '_K1_GATHER', k1 == 'gather')
     cfg = full_cfg(config)
     spec = O.VoxelSpec(cfg)
     batch, lvl, Einv = _fusion_inputs(cfg, 90 + config)

@@ -20,7 +20,8 @@ class VoxelDesc(ctypes.Structure):
     _fields_ = [('B', c_int), ('N', c_int), ('C', c_int), ('Cv', c_int), ('h', c_int), ('w', c_int),
                 ('H', c_int), ('W', c_int), ('X', c_int), ('Y', c_int), ('Z', c_int), ('D', c_int),
                 ('str', c_float * 3), ('len', c_float * 3), ('z_scale', c_float), ('pad_out', c_int),
-                ('axis_x', c_fp), ('axis_y', c_fp), ('axis_z', c_fp), ('dbins', c_fp), ('group', c_fp)]
+                ('axis_x', c_fp), ('axis_y', c_fp), ('axis_z', c_fp), ('dbins', c_fp), ('group', c_fp),
+                ('deterministic', c_int)]
 
 
 class ViewDesc(ctypes.Structure):
@@ -61,6 +62,7 @@ _SIGS = {
     'vfd_fuse_depth_fwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 8 + [c_void_p]),
     'vfd_fuse_depth_bwd_workspace': (c_size_t, [ctypes.POINTER(VoxelDesc)]),
     'vfd_fuse_depth_bwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 8 + [c_size_t, c_void_p]),
+    'vfd_fuse_depth_bwd_planned': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 9 + [c_size_t, c_void_p]),
     'vfd_fusion_plan_bytes': (c_size_t, [ctypes.POINTER(VoxelDesc)]),
     'vfd_fusion_plan': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 5 + [c_void_p]),
     'vfd_fuse_pose_fwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 5 + [c_void_p]),

@@ -356,7 +356,7 @@ __global__ __launch_bounds__(256) void fuse_depth_fwd_q_k(vfd_voxel_desc d, cons
 // Same voxel walk; lanes are channels, so every scatter into dP is a 256-B contiguous row of
 // f32 atomics (the full-rate atomic shape on gfx950).  Depth-column and bias gradients are
 // reduced per lane and written as per-wave partials (summed by fuse_depth_reduce_k).
-template <int CPL>
+template <int CPL, bool SCATTER>
 __global__ __launch_bounds__(256) void fuse_depth_bwd_k(vfd_voxel_desc d, const float* __restrict__ dvox,
                                                         const float* __restrict__ vox,
                                                         const float* __restrict__ mlo,
@@ -419,7 +419,7 @@ __global__ __launch_bounds__(256) void fuse_depth_bwd_k(vfd_voxel_desc d, const 
 #pragma unroll
           for (int k = 0; k < CPL; ++k) {
             int ch = lane + 64 * k;
-            if (ch < d.Cv) atomicAdd(row + ch, racc[s][q][k]);
+            if (SCATTER && ch < d.Cv) atomicAdd(row + ch, racc[s][q][k]);
           }
         }
       }
@@ -433,7 +433,7 @@ __global__ __launch_bounds__(256) void fuse_depth_bwd_k(vfd_voxel_desc d, const 
 #pragma unroll
           for (int k = 0; k < CPL; ++k) {
             int ch = lane + 64 * k;
-            if (ch < d.Cv) atomicAdd(row + ch, racc[s][q][k]);
+            if (SCATTER && ch < d.Cv) atomicAdd(row + ch, racc[s][q][k]);
           }
         }
 #pragma unroll
@@ -806,7 +806,7 @@ struct TileItem {
   float rden;        // 1 / (count + 1e-7) (volumetric_fusionnet.py:162)
   float w[4];        // ATen bilinear weights of taps (x0,y0) (x0+1,y0) (x0,y0+1) (x0+1,y0+1); 0 outside the tile
   int32_t lxy;       // tap 0 relative to the tile origin: (ly + 1) * 8 + (lx + 1), lx, ly in [-1, PT-1]
-  uint32_t pad;
+  uint32_t vc;       // voxel index (bits 0-23) | its count of valid cameras (24-27): K1's gather backward
 };
 static_assert(sizeof(TileItem) == 32, "tile item must stay 32 B");
 
@@ -937,7 +937,7 @@ __global__ __launch_bounds__(256) void plan_fill_k(vfd_voxel_desc d, const PlanE
   it.pz = fold ? (1u << 31) | (uint32_t)(pose_fold_slot(xi, yi, d.X, d.Y) * d.Z + zi)
                : (uint32_t)(((yi + P1) * (d.X + 2 * P1) + xi + P1) * d.Z + zi);
   it.rden = 1.f / e.den;
-  it.pad = 0;
+  it.vc = e.meta & 0x0FFFFFFFu;
   float w[4];
   entry_weights(e, w);
   const int x0 = e.x0, y0 = e.y0;
@@ -957,6 +957,39 @@ __global__ __launch_bounds__(256) void plan_fill_k(vfd_voxel_desc d, const PlanE
     const int key = tile * PSUB + sub_key(lx, ly);
     ib[lbase[key] + atomicAdd(lcur + key, 1)] = it;
   }
+}
+
+// Deterministic mode: the fill above orders a bucket's items by atomic arrival.  plan_order_k
+// ranks every item within its (tile, sub-key) bucket by voxel index (unique in a bucket: an entry
+// lists a tile once) into `tmp`; plan_copy_k moves them back.  Buckets are short (tens of
+// items), so the rank is a plain count over the bucket.
+__global__ __launch_bounds__(256) void plan_order_k(vfd_voxel_desc d, const int* __restrict__ row_ptr,
+                                                    const TileItem* __restrict__ items, TileItem* __restrict__ tmp) {
+  const int bc = blockIdx.y;
+  const int V = d.X * d.Y * d.Z, nk = tiles_x(d) * tiles_y(d) * PSUB;
+  const int* tp = row_ptr + (size_t)bc * (nk + 1);
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= tp[nk]) return;
+  int lo = 0, hi = nk;                              // last bucket k with tp[k] <= i
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (tp[mid] <= i) lo = mid; else hi = mid;
+  }
+  const TileItem* ib = items + (size_t)bc * 4 * V;
+  const TileItem it = ib[i];
+  const uint32_t key = it.vc & 0xFFFFFFu;
+  int r = 0;
+  for (int j = tp[lo]; j < tp[lo + 1]; ++j) r += (ib[j].vc & 0xFFFFFFu) < key ? 1 : 0;
+  tmp[(size_t)bc * 4 * V + tp[lo] + r] = it;
+}
+
+__global__ __launch_bounds__(256) void plan_copy_k(vfd_voxel_desc d, const int* __restrict__ row_ptr,
+                                                   const TileItem* __restrict__ tmp, TileItem* __restrict__ items) {
+  const int bc = blockIdx.y;
+  const int V = d.X * d.Y * d.Z, nk = tiles_x(d) * tiles_y(d) * PSUB;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= row_ptr[(size_t)bc * (nk + 1) + nk]) return;
+  items[(size_t)bc * 4 * V + i] = tmp[(size_t)bc * 4 * V + i];
 }
 
 // Load balance of the backward: tiles at the horizon collect ~4x the mean item count.  A tile
@@ -1345,6 +1378,138 @@ __global__ __launch_bounds__(256) void pose_combine_k(vfd_voxel_desc d, const in
   }
 }
 
+// ------------------------------------------------------------------------------ K1 backward (gather)
+// The K1 backward's d P as a gather over the fusion plan's tile buckets (the K2 backward's index:
+// the geometry is the same): per (batch, camera, 4x4 pixel tile) task, lanes = the Cv = 64 voxel
+// channels; every item (a visible (voxel, camera) pair touching the tile) with a camera count of 1
+// or 2 adds w_tap * d pre-activation to its footprint's pixels in the non-overlap (count 1) or
+// overlap (count 2) half of the tile's d P rows, runs of equal footprints summed in registers.
+// No atomics; d P is written once with plain stores (split tiles through the pool + combine in
+// part order), so the result depends only on the item order of each bucket.
+constexpr int K1G_CV = 64;
+
+__global__ __launch_bounds__(64) void fuse_depth_bwd_gather_k(vfd_voxel_desc d, const int4* __restrict__ tasks,
+                                                              const int* __restrict__ ctrl,
+                                                              const TileItem* __restrict__ items,
+                                                              const float* __restrict__ dvox,
+                                                              const float* __restrict__ vox,
+                                                              float* __restrict__ pool, float* __restrict__ dP) {
+  constexpr int PR = PT2 + 1, ROW = 2 * K1G_CV;
+  constexpr int U = 8;
+  __shared__ float acc_l[PR * ROW];
+  const int lane = threadIdx.x;
+  const int wt = blockIdx.x;
+  if (wt >= ctrl[0]) return;
+  const int4 rec = tasks[wt];
+  const int bct = rec.x, lo = rec.y, hi = rec.z, meta = rec.w;
+  const int nt = tiles_x(d) * tiles_y(d), ntx = tiles_x(d);
+  const int bc = bct / nt, b = bc / d.N, tile = bct % nt;
+  const int V = d.X * d.Y * d.Z, hw = d.h * d.w;
+  const TileItem* ib = items + (size_t)bc * 4 * V;
+  const float* gv = dvox + (size_t)b * V * K1G_CV + lane;
+  const float* ov = vox + (size_t)b * V * K1G_CV + lane;
+#pragma unroll
+  for (int p = 0; p < PR; ++p) {
+    acc_l[p * ROW + lane] = 0.f;
+    acc_l[p * ROW + K1G_CV + lane] = 0.f;
+  }
+  float tq[2][4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) tq[h][q] = 0.f;
+  int cur = -1;
+  auto flush = [&]() {
+    if (cur < 0) return;
+    const int lx = (cur & 7) - 1, ly = (cur >> 3) - 1;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int px = lx + (q & 1), py = ly + (q >> 1);
+      float* a = acc_l + ((px >= 0 && px < PT && py >= 0 && py < PT) ? py * PT + px : PT2) * ROW + lane;
+      a[0] += tq[0][q];
+      a[K1G_CV] += tq[1][q];
+      tq[0][q] = tq[1][q] = 0.f;
+    }
+  };
+  // batches of U items: records lane-parallel (lane u < U holds item j + u), rows loaded for the
+  // whole batch before it is summed
+  for (int j = lo; j < hi; j += U) {
+    const TileItem m = ib[min(j + (lane < U ? lane : 0), hi - 1)];
+    float g[U], o[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t vc = (uint32_t)__builtin_amdgcn_readlane((int)m.vc, u);
+      const size_t row = (size_t)(vc & 0xFFFFFFu) * K1G_CV;
+      g[u] = gv[row];
+      o[u] = ov[row];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int lxy = __builtin_amdgcn_readlane(m.lxy, u);
+      const uint32_t vc = (uint32_t)__builtin_amdgcn_readlane((int)m.vc, u);
+      const int cnt = (int)(vc >> 24);
+      const bool live = j + u < hi && (cnt == 1 || cnt == 2);
+      if (lxy != cur) {
+        flush();
+        cur = lxy;
+      }
+      const float dpre = live ? g[u] * (o[u] > 0.f ? 1.f : 0.1f) : 0.f;
+      const float d0 = cnt == 2 ? 0.f : dpre, d1 = cnt == 2 ? dpre : 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(m.w[q]), u));
+        tq[0][q] += w * d0;
+        tq[1][q] += w * d1;
+      }
+    }
+  }
+  flush();
+  if (meta >= 0) {                                 // a split tile's part: its pool slot
+    float* ps = pool + (size_t)meta * PT2 * POSE_MAXC;
+#pragma unroll
+    for (int p = 0; p < PT2; ++p) {
+      ps[p * POSE_MAXC + lane] = acc_l[p * ROW + lane];
+      ps[p * POSE_MAXC + K1G_CV + lane] = acc_l[p * ROW + K1G_CV + lane];
+    }
+    return;
+  }
+  const int tx = tile % ntx, ty = tile / ntx;
+  float* db = dP + (size_t)bc * hw * ROW;
+#pragma unroll
+  for (int p = 0; p < PT2; ++p) {
+    const int x = tx * PT + p % PT, y = ty * PT + p / PT;
+    if (x >= d.w || y >= d.h) continue;
+    float* dst = db + ((size_t)y * d.w + x) * ROW;
+    dst[lane] = acc_l[p * ROW + lane];
+    dst[K1G_CV + lane] = acc_l[p * ROW + K1G_CV + lane];
+  }
+}
+
+// split tiles of the K1 gather: the S part slots summed in part order (thread = d P channel)
+__global__ __launch_bounds__(128) void fuse_depth_combine_k(vfd_voxel_desc d, const int4* __restrict__ combos,
+                                                            const int* __restrict__ ctrl,
+                                                            const float* __restrict__ pool, float* __restrict__ dP) {
+  constexpr int ROW = 2 * K1G_CV;
+  const int nt = tiles_x(d) * tiles_y(d), ntx = tiles_x(d);
+  const int hw = d.h * d.w;
+  const int ch = threadIdx.x;
+  const int ncombo = ctrl[1];
+  for (int k = blockIdx.x; k < ncombo; k += gridDim.x) {
+    const int4 cb = combos[k];
+    const int bc = cb.x / nt, tile = cb.x % nt;
+    const int x0 = (tile % ntx) * PT, y0 = (tile / ntx) * PT;
+    const float* p0 = pool + (size_t)cb.y * PT2 * POSE_MAXC + ch;
+    float* db = dP + (size_t)bc * hw * ROW + ch;
+    for (int p = 0; p < PT2; ++p) {
+      const int x = x0 + p % PT, y = y0 + p / PT;
+      if (x >= d.w || y >= d.h) continue;
+      float a = p0[(size_t)p * POSE_MAXC];
+      for (int s2 = 1; s2 < cb.z; ++s2) a += p0[((size_t)s2 * PT2 + p) * POSE_MAXC];
+      db[((size_t)y * d.w + x) * ROW] = a;
+    }
+  }
+}
+
 // K3 geometry (Tri, frustum_sample, tri_index, corner_offset): vfd_common.h
 
 // ------------------------------------------------------------------------------ K3 forward
@@ -1645,6 +1810,55 @@ __global__ __launch_bounds__(256) void vpb_fill_k(vfd_voxel_desc d, const float*
   entries[vpb_ptr(ptr, boff, n, b * g.ncell + c) + r] = make_float4(ix, iy, iz, __uint_as_float(row));
 }
 
+// Deterministic mode: the count kernel ranks a cell's samples by atomic arrival.  vpb_order_k
+// re-ranks every filled entry within its cell by its gradient row (one row per sample: unique)
+// and writes that rank back to the sample's slot of `rank`; a second vpb_fill_k then places the
+// entries in that order.
+__device__ __forceinline__ int vpb_row_sample(const vfd_voxel_desc& d, unsigned row, int* bc) {
+  const int Pd = d.pad_out ? 1 : 0, hw = d.h * d.w;
+  int px, py, di;
+  if (row >> 31) {
+    const int r = (int)(row & 0x7FFFFFFFu) - 1, nfs = 2 * (d.w + d.h);
+    di = r % d.D;
+    const int t = r / d.D, fs = t % nfs;
+    *bc = t / nfs;
+    if (fs < d.w) { px = fs; py = 1; }
+    else if (fs < 2 * d.w) { px = fs - d.w; py = d.h - 2; }
+    else if (fs < 2 * d.w + d.h) { px = 1; py = fs - 2 * d.w; }
+    else { px = d.w - 2; py = fs - 2 * d.w - d.h; }
+  } else {
+    const int r = (int)row;
+    di = r % d.D;
+    const int t = r / d.D, W2 = d.w + 2 * Pd, H2 = d.h + 2 * Pd;
+    px = t % W2 - Pd;
+    py = (t / W2) % H2 - Pd;
+    *bc = t / (W2 * H2);
+  }
+  return di * hw + py * d.w + px;                   // sl of the count / fill kernels
+}
+
+__global__ __launch_bounds__(256) void vpb_order_k(vfd_voxel_desc d, const int* __restrict__ ptr,
+                                                   const int* __restrict__ boff, const float4* __restrict__ entries,
+                                                   int* __restrict__ rank) {
+  const VpbGeom g = vpb_geom(d);
+  const int n = d.B * g.ncell;
+  const int total = vpb_ptr(ptr, boff, n, n);
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  int lo = 0, hi = n;                               // last cell c with start(c) <= i
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (vpb_ptr(ptr, boff, n, mid) <= i) lo = mid; else hi = mid;
+  }
+  const int s0 = vpb_ptr(ptr, boff, n, lo), s1 = vpb_ptr(ptr, boff, n, lo + 1);
+  const unsigned key = __float_as_uint(entries[i].w);
+  int r = 0;
+  for (int j = s0; j < s1; ++j) r += __float_as_uint(entries[j].w) < key ? 1 : 0;
+  int bc;
+  const int sl = vpb_row_sample(d, key, &bc);
+  rank[(size_t)bc * d.h * d.w * d.D + sl] = r;
+}
+
 // Reflect-pad fold (pad_sets): the gradient of map pixel (px, py) is the sum of its copies in the
 // padded d_out.  Only pixels with a second copy (py in {1, h-2} or px in {1, w-2}) are folded,
 // into fb[bc][slot][D][CV]; slot = px (py == 1), w + px (py == h-2), 2w + py (px == 1),
@@ -1770,7 +1984,8 @@ __global__ __launch_bounds__(64) void vpb_tile_k(vfd_voxel_desc d, const int* __
   }
   n0 = wave_sum(n0);
   n1 = wave_sum(n1);
-  const int np = max(1, (max(n0, n1) + VB_S - 1) / VB_S);
+  // deterministic mode: no split tiles (their parts would add with atomics)
+  const int np = d.deterministic ? 1 : max(1, (max(n0, n1) + VB_S - 1) / VB_S);
   if (lane == 0) parts[tile] = np;
 }
 
@@ -2049,9 +2264,9 @@ int vfd_fuse_depth_bwd(const vfd_voxel_desc* d, const float* d_vox, const float*
   dim3 grid(cdiv(cdiv(V, 64), 4), d->B);
   float* partial = (float*)ws;
   if (d->Cv <= 64)
-    fuse_depth_bwd_k<1><<<grid, 256, 0, s>>>(*d, d_vox, vox, mask_lo, K, Einv, dP, partial);
+    fuse_depth_bwd_k<1, true><<<grid, 256, 0, s>>>(*d, d_vox, vox, mask_lo, K, Einv, dP, partial);
   else
-    fuse_depth_bwd_k<2><<<grid, 256, 0, s>>>(*d, d_vox, vox, mask_lo, K, Einv, dP, partial);
+    fuse_depth_bwd_k<2, true><<<grid, 256, 0, s>>>(*d, d_vox, vox, mask_lo, K, Einv, dP, partial);
   st = fail_launch("fuse_depth_bwd");
   if (st) return st;
   // pad waves beyond V wrote nothing: zero-initialise by reducing only real rows
@@ -2086,8 +2301,10 @@ static size_t plan_fold_bytes(const vfd_voxel_desc* d) {       // K2 backward's 
 static constexpr size_t PLAN_POOL_BYTES = (size_t)PBW_POOL * PT2 * POSE_MAXC * sizeof(float);
 
 size_t vfd_fusion_plan_bytes(const vfd_voxel_desc* d) {
+  // deterministic mode: + an item array for the bucket ordering pass
   return plan_entries_bytes(d) + plan_rowptr_bytes(d) + plan_cursor_bytes(d) + plan_items_bytes(d) +
-         plan_tasks_bytes(d) + 256 + plan_fold_bytes(d) + PLAN_POOL_BYTES;
+         plan_tasks_bytes(d) + 256 + plan_fold_bytes(d) + PLAN_POOL_BYTES +
+         (d->deterministic ? plan_items_bytes(d) : 0);
 }
 
 int vfd_fusion_plan(const vfd_voxel_desc* d, const float* mask_lo, const float* K, const float* Einv, void* plan,
@@ -2120,6 +2337,12 @@ int vfd_fusion_plan(const vfd_voxel_desc* d, const float* mask_lo, const float* 
   plan_count_k<<<egrid, 256, hist, s>>>(*d, (const PlanEntry*)plan, counts, cursor);
   plan_scan_k<<<d->B * d->N, PIDX_THREADS, 0, s>>>(*d, cursor, row_ptr);
   plan_fill_k<<<egrid, 256, 2 * hist, s>>>(*d, (const PlanEntry*)plan, counts, cursor, csr);
+  if (d->deterministic) {
+    TileItem* tmp = (TileItem*)((char*)plan + vfd_fusion_plan_bytes(d) - plan_items_bytes(d));
+    const dim3 igrid(cdiv(4 * V, 256), d->B * d->N);
+    plan_order_k<<<igrid, 256, 0, s>>>(*d, row_ptr, csr, tmp);
+    plan_copy_k<<<igrid, 256, 0, s>>>(*d, row_ptr, tmp, csr);
+  }
   int4* tasks = (int4*)((char*)csr + plan_items_bytes(d));
   int* ctrl = (int*)((char*)tasks + plan_tasks_bytes(d));
   int4* combos = tasks + (d->B * d->N * host_tiles(d) + PBW_POOL);
@@ -2167,6 +2390,38 @@ int vfd_fuse_pose_bwd(const vfd_voxel_desc* d, const void* plan, const int* coun
   fuse_pose_bwd_k<<<ntask_max, 64, 0, s>>>(*d, tasks, ctrl, csr, d_out, fbuf, pool, d_feats);
   pose_combine_k<<<std::min(PBW_POOL / 2, host_tiles(d) * d->B * d->N), 256, 0, s>>>(*d, combos, ctrl, pool, d_feats);
   return fail_launch("fuse_pose_bwd");
+}
+
+int vfd_fuse_depth_bwd_planned(const vfd_voxel_desc* d, const void* plan, const float* d_vox, const float* vox,
+                               const float* mask_lo, const float* K, const float* Einv, float* dP, float* d_wzb,
+                               void* ws, size_t ws_bytes, void* stream) {
+  int st = check_voxel_desc(d);
+  if (st) return st;
+  VFD_REQUIRE(d->Cv == K1G_CV, "fuse_depth_bwd_planned: Cv=%d (the gather backward needs %d)", d->Cv, K1G_CV);
+  VFD_REQUIRE(plan && d_vox && vox && dP && d_wzb, "fuse_depth_bwd_planned: null argument");
+  VFD_REQUIRE(ws_bytes >= vfd_fuse_depth_bwd_workspace(d), "workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const int V = d->X * d->Y * d->Z;
+  const int* row_ptr = (const int*)((const char*)plan + plan_entries_bytes(d));
+  const TileItem* csr = (const TileItem*)((const char*)row_ptr + plan_rowptr_bytes(d) + plan_cursor_bytes(d));
+  const int4* tasks = (const int4*)((const char*)csr + plan_items_bytes(d));
+  const int* ctrl = (const int*)((const char*)tasks + plan_tasks_bytes(d));
+  const int4* combos = tasks + (d->B * d->N * host_tiles(d) + PBW_POOL);
+  float* pool = (float*)((char*)ctrl + 256 + plan_fold_bytes(d));
+  ProfScope ps(K_FUSE_DEPTH_BWD, s);
+  const int ntask_max = host_tiles(d) * d->B * d->N + PBW_POOL;
+  fuse_depth_bwd_gather_k<<<ntask_max, 64, 0, s>>>(*d, tasks, ctrl, csr, d_vox, vox, pool, dP);
+  fuse_depth_combine_k<<<std::min(PBW_POOL / 2, host_tiles(d) * d->B * d->N), 2 * K1G_CV, 0, s>>>(
+      *d, combos, ctrl, pool, dP);
+  // depth-column and bias gradients: the voxel walk without the scatter
+  dim3 grid(cdiv(cdiv(V, 64), 4), d->B);
+  float* partial = (float*)ws;
+  fuse_depth_bwd_k<1, false><<<grid, 256, 0, s>>>(*d, d_vox, vox, mask_lo, K, Einv, dP, partial);
+  st = fail_launch("fuse_depth_bwd_planned");
+  if (st) return st;
+  const int rows = d->B * (int)cdiv(V, 64);
+  fuse_depth_reduce_k<<<5 * d->Cv, 256, 0, s>>>(partial, rows, 5 * d->Cv, d_wzb);
+  return fail_launch("fuse_depth_reduce");
 }
 
 int vfd_voxel_project_fwd(const vfd_voxel_desc* d, const float* vox, const float* invK, const float* E,
@@ -2271,6 +2526,10 @@ static void vpb_plan_launch(const vfd_voxel_desc* d, const float* invK, const fl
   vpb_scan1_k<<<nblk, 256, 0, s>>>(p.cnt, ncell, p.ptr, p.bsum);
   vpb_scan2_k<<<1, 1024, 0, s>>>(p.bsum, nblk, p.boff);
   vpb_fill_k<<<dim3(cpb, d->B * d->N), 256, 0, s>>>(*d, invK, E, p.rank, p.ptr, p.boff, p.entries);
+  if (d->deterministic) {
+    vpb_order_k<<<cdiv((size_t)d->B * d->N * hwD, 256), 256, 0, s>>>(*d, p.ptr, p.boff, p.entries, p.rank);
+    vpb_fill_k<<<dim3(cpb, d->B * d->N), 256, 0, s>>>(*d, invK, E, p.rank, p.ptr, p.boff, p.entries);
+  }
   vpb_tile_k<<<nb, 64, 0, s>>>(*d, p.ptr, p.boff, p.parts);
   vpb_tasks_k<<<1, 1024, 0, s>>>(p.parts, nb, p.tasks, p.ctrl);
 }

@@ -173,8 +173,10 @@ class VFNet(nn.Module):
         with torch.autocast(device_type='cuda', enabled=False):
             P = torch.einsum('bncp,nkc->bnpk', feats_agg.float().reshape(B, N, C, h * w), wf.float()).contiguous()
         K = inputs['K', self.fusion_level + 1]
+        # the step's fusion plan (shared with the pose calls) indexes K1's atomic-free backward
         return KN.FuseDepth.apply(space, P, self._mask_lowres(inputs, space), K, inputs['extrinsics_inv'],
-                                  wz, self.conv_non_overlap[0].bias, self.conv_overlap[0].bias)
+                                  wz, self.conv_non_overlap[0].bias, self.conv_overlap[0].bias,
+                                  self._plan(inputs, space))
 
     def fused_projection(self, voxel_feat):
         """K3C (K3 fused into reduce_dim's first conv, fp32 MFMA) applies: 64 voxel channels, 256

@@ -90,7 +90,14 @@ class VoxelSpace:
         d.axis_x, d.axis_y, d.axis_z = (a.data_ptr() for a in self.axes)
         d.dbins = self.dbins.data_ptr()
         d.group = self.group.data_ptr()
+        d.deterministic = int(deterministic())
         return d
+
+
+def deterministic():
+    """Fixed-order gradient sums in the fusion kernels: on when torch.backends.cudnn.deterministic
+    is set (the reference's train.py:23-24 sets it, with benchmark off) or VFD_DETERMINISTIC=1."""
+    return bool(torch.backends.cudnn.deterministic) or os.environ.get('VFD_DETERMINISTIC', '0') == '1'
 
 
 def mask_lowres(space, mask):
@@ -104,12 +111,19 @@ def mask_lowres(space, mask):
     return out
 
 
+_K1_GATHER = os.environ.get('VFD_K1_GATHER', '1') != '0'
+
+
 class FuseDepth(torch.autograd.Function):
-    """K1: P [B,N,hw,2Cv] (folded 1x1-conv maps) -> voxel features [B,V,Cv] (channels-last)."""
+    """K1: P [B,N,hw,2Cv] (folded 1x1-conv maps) -> voxel features [B,V,Cv] (channels-last).
+
+    Backward: with the step's FusionPlan (`plan`, the K2 backward's tile index of the same
+    geometry) and Cv = 64, d P is an atomic-free gather over the plan's tile buckets
+    (`vfd_fuse_depth_bwd_planned`); otherwise the voxel-walk scatter with f32 atomics."""
 
     @staticmethod
     @_amp_fwd
-    def forward(ctx, space, P, mask_lo, K, Einv, wz, b_no, b_o):
+    def forward(ctx, space, P, mask_lo, K, Einv, wz, b_no, b_o, plan=None):
         lib = L.load()
         P, mask_lo, K, Einv = (_dev(t, n) for t, n in ((P, 'P'), (mask_lo, 'mask'), (K, 'K'), (Einv, 'Einv')))
         wz, b_no, b_o = (_dev(t, 'fusion params') for t in (wz, b_no, b_o))
@@ -123,6 +137,10 @@ class FuseDepth(torch.autograd.Function):
                                        Einv.data_ptr(), wz.data_ptr(), b_no.data_ptr(), b_o.data_ptr(),
                                        vox.data_ptr(), L.stream()), 'fuse_depth_fwd')
         ctx.space, ctx.shape = space, (B, N, hw, Cv)
+        ctx.plan = plan if (plan is not None and Cv == 64 and _K1_GATHER) else None
+        if ctx.plan is None and deterministic() and torch.is_grad_enabled():
+            raise RuntimeError('deterministic mode: the K1 backward needs the fusion plan gather (Cv = 64, '
+                               'VFD_K1_GATHER=1); the atomic scatter sums in arrival order')
         ctx.save_for_backward(vox, mask_lo, K, Einv)
         return vox
 
@@ -138,10 +156,18 @@ class FuseDepth(torch.autograd.Function):
         dwzb = torch.empty(5, Cv, device=g.device)
         nbytes = lib.vfd_fuse_depth_bwd_workspace(ctypes.byref(d))
         ws = _ws(nbytes, g.device)
-        L.check(lib.vfd_fuse_depth_bwd(ctypes.byref(d), g.data_ptr(), vox.data_ptr(), mask_lo.data_ptr(),
-                                       K.data_ptr(), Einv.data_ptr(), dP.data_ptr(), dwzb.data_ptr(),
-                                       ws.data_ptr(), nbytes, L.stream()), 'fuse_depth_bwd')
-        return None, dP, None, None, None, dwzb[:3], dwzb[3], dwzb[4]
+        if ctx.plan is not None:
+            plan, ctx.plan = ctx.plan.build(), None
+            plan.wait()
+            L.check(lib.vfd_fuse_depth_bwd_planned(ctypes.byref(d), plan.buf.data_ptr(), g.data_ptr(), vox.data_ptr(),
+                                                   mask_lo.data_ptr(), K.data_ptr(), Einv.data_ptr(), dP.data_ptr(),
+                                                   dwzb.data_ptr(), ws.data_ptr(), nbytes, L.stream()),
+                    'fuse_depth_bwd_planned')
+        else:
+            L.check(lib.vfd_fuse_depth_bwd(ctypes.byref(d), g.data_ptr(), vox.data_ptr(), mask_lo.data_ptr(),
+                                           K.data_ptr(), Einv.data_ptr(), dP.data_ptr(), dwzb.data_ptr(),
+                                           ws.data_ptr(), nbytes, L.stream()), 'fuse_depth_bwd')
+        return None, dP, None, None, None, dwzb[:3], dwzb[3], dwzb[4], None
 
 
 def _side_stream(device):

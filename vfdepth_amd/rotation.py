@@ -19,8 +19,8 @@ def axis_angle_to_quaternion(axis_angle):
 
 # pytorch3d's quaternion_to_matrix entries as (product a, product b, sign of b, sign of the s-term)
 # over the 16 products q_x * q_y (x, y in r, i, j, k): m = [1|0] + sign_s * s * (P_a + sign_b * P_b)
-# — the same products and sums in the same order, so the values are identical; as gathers over one
-# outer product it is ~10 kernels each way instead of ~30 scalar-shaped ones.
+# — the same products and sums in the same order, so the values are identical; as selections from
+# one outer product it is ~10 kernels each way instead of ~30 scalar-shaped ones.
 _QM_A = (10, 6, 7, 6, 5, 11, 7, 11, 5)          # jj, ij, ik, ij, ii, jk, ik, jk, ii
 _QM_B = (15, 12, 8, 12, 15, 4, 8, 4, 10)        # kk, kr, jr, kr, kk, ir, jr, ir, jj
 _QM_SB = (1., -1., 1., 1., 1., -1., -1., 1., 1.)
@@ -30,18 +30,25 @@ _QM_CACHE = {}
 
 
 def _qm_consts(device, dtype):
+    """0/1 selection matrices [16, 9] of the products (a matmul, not index_select: its backward is
+    a plain GEMM, deterministic, where index_select's scatters with atomics)."""
     key = (str(device), dtype)
     if key not in _QM_CACHE:
-        mk = lambda v, dt=dtype: torch.tensor(v, device=device, dtype=dt)  # noqa: E731
-        _QM_CACHE[key] = (mk(_QM_A, torch.long), mk(_QM_B, torch.long), mk(_QM_SB), mk(_QM_SS), mk(_QM_BASE))
+        sa = torch.zeros(16, 9, dtype=dtype)
+        sb = torch.zeros(16, 9, dtype=dtype)
+        for k, (a, b) in enumerate(zip(_QM_A, _QM_B)):
+            sa[a, k] = 1.0
+            sb[b, k] = _QM_SB[k]
+        mk = lambda v: torch.tensor(v, dtype=dtype, device=device)  # noqa: E731
+        _QM_CACHE[key] = (sa.to(device), sb.to(device), mk(_QM_SS), mk(_QM_BASE))
     return _QM_CACHE[key]
 
 
 def quaternion_to_matrix(q):
-    ia, ib, sb, ss, base = _qm_consts(q.device, q.dtype)
+    sa, sb, ss, base = _qm_consts(q.device, q.dtype)
     s = 2.0 / (q * q).sum(-1, keepdim=True)
     P = (q.unsqueeze(-1) * q.unsqueeze(-2)).flatten(-2)
-    t = P.index_select(-1, ia) + sb * P.index_select(-1, ib)
+    t = P @ sa + P @ sb           # selections are exact (x * 1 + zeros); sb carries the sign of b
     m = base + ss * (s * t)
     return m.reshape(q.shape[:-1] + (3, 3))
 

@@ -173,6 +173,18 @@ int vfd_bn_bwd_apply(const vfd_bn_desc* d, const float* g, const float* y, const
                      int ns, double count, const float* gamma, const float* mean, const float* invstd, float* dx,
                      float* dresidual, float* dgamma, float* dbeta, void* stream);
 
+/* ------------------------------------------------------------------ reflect padding (decoders) */
+/* nn.Conv2d(padding_mode='reflect', padding=1) of the decoders' 3x3 blocks (network/blocks.py):
+ * x [planes, h, w] -> y [planes, h+2, w+2] (NCHW fp32), and its backward as a fixed-order gather
+ * of each pixel's copies (deterministic, no atomics). */
+int vfd_reflect_pad1_fwd(const float* x, float* y, long long planes, int h, int w, void* stream);
+int vfd_reflect_pad1_bwd(const float* g, float* dx, long long planes, int h, int w, void* stream);
+/* backward of LeakyReLU(slope) + the one-pixel reflect pad for channels-last maps (the K3C / K2C
+ * outputs): g, out [n, h+2, w+2, C] (out = the padded forward output) -> gp [n, h, w, C] =
+ * (sum of g's copies) * (out > 0 ? 1 : slope); C % 4 == 0, 16-B aligned. */
+int vfd_lrelu_pad1_bwd_nhwc(const float* g, const float* out, float* gp, long long n_img, int h, int w, int C,
+                            float slope, void* stream);
+
 /* ------------------------------------------------------------------ padded 3x3 conv (K2C) */
 typedef struct vfd_conv_desc {
   int32_t B;             /* images                                                       */
@@ -300,6 +312,9 @@ int vfd_smooth_bwd(int B, int N, int H, int W, const float* disp, const float* c
 int vfd_aggregate_fwd(int BN, int C, int h, int w, const float* base, int n_levels,
                       const float* const* levels, const int* level_hw, const float* bias, float* out,
                       void* stream);
+/* backward of the align_corners bilinear upsample (the aggregation's levels): g [planes, h, w] ->
+ * dsrc [planes, hs, ws] as a fixed-order gather (deterministic, no atomics) */
+int vfd_upsample_ac_bwd(const float* g, float* dsrc, long long planes, int h, int w, int hs, int ws, void* stream);
 
 /* ------------------------------------------------------------------ measurement hooks */
 /* Record HIP events around every launch of kernel `kernel_id` (see vfd_kernel_name; -1 = all,
@@ -307,7 +322,7 @@ int vfd_aggregate_fwd(int BN, int C, int h, int w, const float* base, int n_leve
  * recorded; vfd_prof_read_kernels: the same per kernel id into arrays of `count` entries.
  * Both reset the record. */
 #define VFD_PROF_ALL (-1)
-#define VFD_KERNEL_COUNT 24
+#define VFD_KERNEL_COUNT 25
 const char* vfd_kernel_name(int kernel_id);
 int vfd_prof_enable(int kernel_id);
 int vfd_prof_read(int* launches, double* total_ms);

@@ -2,7 +2,6 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
-K="config3_step_b2 or full_step_gradient_chain" bash scripts/gpu_tests.sh tests/test_gpu_fullsize.py tests/test_gpu_parity.py || exit 1
-cp gpurun_out/tests/tests.log gpurun_out/tests_fix.log
-bash scripts/gpu_bench.sh r2_all --steps 20 --no-cpu-baseline || exit 1
-bash scripts/gpu_profile.sh r2
+K="fuse_depth or deterministic or full_step or graph_replay" bash scripts/gpu_tests.sh tests/test_gpu_parity.py tests/test_gpu_fullsize.py || exit 1
+cp gpurun_out/tests/tests.log gpurun_out/tests_det.log
+bash scripts/gpu_bench.sh r2_k1g --steps 10 --no-cpu-baseline --no-parity || exit 1

@@ -576,3 +576,33 @@ def test_batchnorm_act_matches_torch(shape, res, relu):
     gclose(bn.bias.grad, bn_ref.bias.grad, 'BN d beta', rel=1e-4)
     if res:
         gclose(ra.grad, rr.grad, 'BN d residual', rel=1e-6)
+
+
+# ------------------------------------------------------------------------------------ pads / upsample
+def test_reflect_pad_upsample_and_lrelu_pad_backward():
+    """The deterministic gather backwards against ATen's: one-pixel reflect pad (decoder convs),
+    LeakyReLU + reflect pad of the channels-last K3C / K2C outputs, and the aggregation's
+    align_corners bilinear upsample (24x40, 12x20, 6x10 -> 48x80, 256 channels)."""
+    from vfdepth_amd import kernels as KN
+    gen = torch.Generator(device=DEV).manual_seed(95)
+    x = torch.randn(6, 16, 37, 53, device=DEV, generator=gen, requires_grad=True)
+    xr = x.detach().clone().requires_grad_(True)
+    y = KN.ReflectPad1.apply(x)
+    yr = F.pad(xr, (1, 1, 1, 1), mode='reflect')
+    assert torch.equal(y, yr)
+    g = torch.randn(y.shape, device=DEV, generator=gen)
+    y.backward(g)
+    yr.backward(g)
+    close(x.grad, xr.grad, 'reflect pad backward', atol=1e-6, rtol=1e-6)
+    out = torch.randn(2, 64, 14, 22, device=DEV, generator=gen).contiguous(memory_format=torch.channels_last)
+    gp = torch.randn(out.shape, device=DEV, generator=gen).contiguous(memory_format=torch.channels_last)
+    inner = out[:, :, 1:-1, 1:-1]
+    ref = torch.ops.aten.reflection_pad2d_backward(gp, inner, [1, 1, 1, 1]) * torch.where(inner > 0, 1.0, 0.1)
+    close(KN.lrelu_pad_backward(gp, out), ref, 'LeakyReLU + reflect pad backward', atol=1e-6, rtol=1e-6)
+    lib = KN.L.load()
+    d = torch.randn(6, 256, 48, 80, device=DEV, generator=gen)
+    for hs, ws in ((24, 40), (12, 20), (6, 10)):
+        dl = torch.empty(6, 256, hs, ws, device=DEV)
+        KN.L.check(lib.vfd_upsample_ac_bwd(d.data_ptr(), dl.data_ptr(), 6 * 256, 48, 80, hs, ws, KN.L.stream()), 'up')
+        ref = torch.ops.aten.upsample_bilinear2d_backward(d, [48, 80], [6, 256, hs, ws], True, None, None)
+        close(dl, ref, f'upsample backward {hs}x{ws}', atol=1e-5, rtol=1e-5)

@@ -91,6 +91,10 @@ _SIGS = {
     'vfd_bn_bwd_stats': (c_int, [ctypes.POINTER(BnDesc)] + [c_fp] * 5 + [c_void_p]),
     'vfd_bn_bwd_apply': (c_int, [ctypes.POINTER(BnDesc), c_fp, c_fp, c_fp, c_fp, c_int, c_double] + [c_fp] * 7
                          + [c_void_p]),
+    'vfd_upsample_ac_bwd': (c_int, [c_fp, c_fp, ctypes.c_longlong] + [c_int] * 4 + [c_void_p]),
+    'vfd_reflect_pad1_fwd': (c_int, [c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_void_p]),
+    'vfd_reflect_pad1_bwd': (c_int, [c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_void_p]),
+    'vfd_lrelu_pad1_bwd_nhwc': (c_int, [c_fp, c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_int, c_float, c_void_p]),
     'vfd_pad_conv_fwd_workspace': (c_size_t, [ctypes.POINTER(ConvDesc)]),
     'vfd_pad_conv_fwd': (c_int, [ctypes.POINTER(ConvDesc)] + [c_fp] * 5 + [c_size_t, c_void_p]),
     'vfd_depth_syn_fwd': (c_int, [ctypes.POINTER(DepthSynDesc)] + [c_fp] * 8 + [c_void_p]),
@@ -143,7 +147,7 @@ KERNEL_IDS = {
     'voxel_project_fwd': 5, 'voxel_project_bwd': 6, 'view_stats': 7, 'view_apply': 8, 'view_bwd': 9,
     'photo_fwd': 10, 'photo_bwd': 11, 'smooth_fwd': 12, 'smooth_bwd': 13, 'fusion_plan': 14,
     'aggregate': 15, 'voxel_project_plan': 16, 'proj_conv_fwd': 17,
-    'depth_syn_fwd': 18, 'depth_syn_bwd': 19, 'proj_conv_dgrad': 20, 'pad_conv_fwd': 21, 'bn_fwd': 22, 'bn_bwd': 23,
+    'depth_syn_fwd': 18, 'depth_syn_bwd': 19, 'proj_conv_dgrad': 20, 'pad_conv_fwd': 21, 'bn_fwd': 22, 'bn_bwd': 23, 'reflect_pad': 24,
 }
 
 

@@ -59,6 +59,73 @@ __global__ __launch_bounds__(256) void aggregate_fwd_k(int BN, int C, int h, int
 
 using namespace vfd;
 
+namespace vfd {
+
+// source index / weight of output row y under align_corners=True resizing from n_src to n (the
+// forward's arithmetic: up_ac)
+__device__ __forceinline__ void up_axis(int n_src, int n, int y, int* y0, int* y1, float* l) {
+  if (n_src == n) { *y0 = *y1 = y; *l = 0.f; return; }
+  const float sy = n > 1 ? (float)(n_src - 1) / (float)(n - 1) : 0.f;
+  const float fy = sy * (float)y;
+  *y0 = min((int)floorf(fy), n_src - 1);
+  *l = fminf(fmaxf(fy - (float)*y0, 0.f), 1.f);
+  *y1 = *y0 + (*y0 < n_src - 1 ? 1 : 0);
+}
+
+// Backward of the align_corners bilinear upsample as a gather: every source pixel sums
+// w_y * w_x * g over the output pixels whose taps name it, in a fixed order (ATen's backward
+// scatters with atomics).  Candidate output rows / columns come from the scale, then the exact
+// forward taps decide.
+__global__ __launch_bounds__(256) void up_ac_bwd_k(const float* __restrict__ g, float* __restrict__ dsrc,
+                                                   long long planes, int h, int w, int hs, int ws) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= planes * hs * ws) return;
+  const int xs = (int)(i % ws);
+  const long long t = i / ws;
+  const int ys = (int)(t % hs);
+  const long long p = t / hs;
+  auto range = [](int s, int n_src, int n, int* lo, int* hi) {
+    if (n_src == n) { *lo = *hi = s; return; }
+    const float sc = n > 1 ? (float)(n_src - 1) / (float)(n - 1) : 0.f;
+    if (!(sc > 0.f)) { *lo = 0; *hi = n - 1; return; }
+    *lo = max(0, (int)floorf((float)(s - 1) / sc) - 1);
+    *hi = min(n - 1, (int)ceilf((float)(s + 1) / sc) + 1);
+  };
+  int ylo, yhi, xlo, xhi;
+  range(ys, hs, h, &ylo, &yhi);
+  range(xs, ws, w, &xlo, &xhi);
+  const float* gp = g + p * h * w;
+  float acc = 0.f;
+  for (int y = ylo; y <= yhi; ++y) {
+    int y0, y1;
+    float ly;
+    up_axis(hs, h, y, &y0, &y1, &ly);
+    const float wy = (y0 == ys ? 1.f - ly : 0.f) + (y1 == ys ? ly : 0.f);
+    if (wy == 0.f) continue;
+    for (int x = xlo; x <= xhi; ++x) {
+      int x0, x1;
+      float lx;
+      up_axis(ws, w, x, &x0, &x1, &lx);
+      const float wx = (x0 == xs ? 1.f - lx : 0.f) + (x1 == xs ? lx : 0.f);
+      if (wx != 0.f) acc += wy * wx * gp[(size_t)y * w + x];
+    }
+  }
+  dsrc[i] = acc;
+}
+
+}  // namespace vfd
+
+extern "C" int vfd_upsample_ac_bwd(const float* g, float* dsrc, long long planes, int h, int w, int hs, int ws,
+                                   void* stream) {
+  VFD_REQUIRE(g && dsrc && planes > 0 && h > 0 && w > 0 && hs > 0 && ws > 0 && hs <= h && ws <= w,
+              "upsample_ac_bwd: bad sizes");
+  hipStream_t s = (hipStream_t)stream;
+  vfd::ProfScope ps(vfd::K_AGGREGATE, s);
+  const long long n = planes * hs * ws;
+  vfd::up_ac_bwd_k<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(g, dsrc, planes, h, w, hs, ws);
+  return vfd::fail_launch("upsample_ac_bwd");
+}
+
 extern "C" int vfd_aggregate_fwd(int BN, int C, int h, int w, const float* base, int n_levels,
                                  const float* const* levels, const int* level_hw, const float* bias, float* out,
                                  void* stream) {

@@ -443,15 +443,24 @@ class PadConv(torch.autograd.Function):
     @_amp_bwd
     def backward(ctx, g):
         x, w, out = ctx.saved_tensors
-        g = _channels_last(g, 'grad')
-        inner = out[:, :, 1:-1, 1:-1]
-        g_in = torch.ops.aten.reflection_pad2d_backward(g, inner, [1, 1, 1, 1])
-        g_pre = (g_in * torch.where(inner > 0, 1.0, 0.1)).contiguous(memory_format=torch.channels_last)
+        g_pre = lrelu_pad_backward(g, out)
         mask = [ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]]
         s = ctx.stride
         dx, dw, db = torch.ops.aten.convolution_backward(g_pre, x, w, [w.shape[0]], [s, s], [0, 0], [1, 1],
                                                          False, [0, 0], 1, mask)
         return dx, dw, db, None, None
+
+
+def lrelu_pad_backward(g, out, slope=0.1):
+    """d pre-activation of LeakyReLU(slope) + reflect pad(1) from the channels-last gradient of the
+    padded output g and that output (fused, deterministic: reflectpad.hip) -> NHWC [n, C, h, w]."""
+    lib = L.load()
+    g = _channels_last(g, 'grad')
+    n, C, hp, wp = g.shape
+    gp = torch.empty(n, C, hp - 2, wp - 2, device=g.device, memory_format=torch.channels_last)
+    L.check(lib.vfd_lrelu_pad1_bwd_nhwc(g.data_ptr(), out.data_ptr(), gp.data_ptr(), n, hp - 2, wp - 2, C, slope,
+                                        L.stream()), 'lrelu_pad1_bwd_nhwc')
+    return gp
 
 
 class ProjConv(torch.autograd.Function):
@@ -502,11 +511,8 @@ class ProjConv(torch.autograd.Function):
         space = ctx.space
         B, N, V, Cv, O = ctx.shape
         d = space.desc(B, N, Cv=Cv)
-        g = _channels_last(g, 'grad')
-        # adjoint of the reflect padding, then of the LeakyReLU (its sign from the output)
-        g_in = torch.ops.aten.reflection_pad2d_backward(g, out[:, :, 1:-1, 1:-1], [1, 1, 1, 1])
-        inner = out[:, :, 1:-1, 1:-1]
-        g_pre = (g_in * torch.where(inner > 0, 1.0, 0.1)).contiguous(memory_format=torch.channels_last)
+        # adjoint of the reflect padding, then of the LeakyReLU (its sign from the output): one kernel
+        g_pre = lrelu_pad_backward(g, out)
         if x is None:   # only the bias gradient was asked for
             x = torch.empty(B * N, Cv * space.D, space.h + 2, space.w + 2, device=g.device,
                             memory_format=torch.channels_last)
@@ -826,10 +832,16 @@ class AggregateUp(torch.autograd.Function):
     @staticmethod
     @_amp_bwd
     def backward(ctx, g):
+        lib = L.load()
         out, = ctx.saved_tensors
-        d = g * torch.where(out > 0, 1.0, 0.1)
-        grads = [torch.ops.aten.upsample_bilinear2d_backward(d, list(out.shape[-2:]), list(shp), True, None, None)
-                 for shp in ctx.level_shapes]
+        d = (g * torch.where(out > 0, 1.0, 0.1)).contiguous()
+        BN, C, h, w = d.shape
+        grads = []
+        for shp in ctx.level_shapes:          # the upsample's adjoint as a gather (deterministic)
+            dl = torch.empty(shp, device=d.device)
+            L.check(lib.vfd_upsample_ac_bwd(d.data_ptr(), dl.data_ptr(), BN * C, h, w, shp[-2], shp[-1], L.stream()),
+                    'upsample_ac_bwd')
+            grads.append(dl)
         return (d, d.sum((0, 2, 3))) + tuple(grads)
 
 
@@ -920,3 +932,33 @@ class BatchNormAct(torch.autograd.Function):
                                      gamma.data_ptr(), mean.data_ptr(), invstd.data_ptr(), ptr(dx), ptr(dr),
                                      ptr(dgamma), ptr(dbeta), L.stream()), 'bn_bwd_apply')
         return dx, dgamma, dbeta, dr, None, None, None, None, None, None, None
+
+
+# =============================================================================================
+# Reflect padding by one pixel (the decoders' reflect 3x3 convs), deterministic backward
+# =============================================================================================
+class ReflectPad1(torch.autograd.Function):
+    """F.pad(x, (1, 1, 1, 1), mode='reflect') for NCHW fp32 x (reflectpad.hip); the backward
+    gathers each pixel's copies in a fixed order (ATen's scatters with atomics)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        lib = L.load()
+        _check_device(x, 'reflect pad input')
+        x = x.contiguous()
+        *lead, h, w = x.shape
+        y = torch.empty(*lead, h + 2, w + 2, device=x.device)
+        planes = x.numel() // (h * w)
+        L.check(lib.vfd_reflect_pad1_fwd(x.data_ptr(), y.data_ptr(), planes, h, w, L.stream()), 'reflect_pad1_fwd')
+        ctx.shape = tuple(x.shape)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        lib = L.load()
+        g = g.contiguous()
+        h, w = ctx.shape[-2:]
+        dx = torch.empty(ctx.shape, device=g.device)
+        planes = dx.numel() // (h * w)
+        L.check(lib.vfd_reflect_pad1_bwd(g.data_ptr(), dx.data_ptr(), planes, h, w, L.stream()), 'reflect_pad1_bwd')
+        return dx

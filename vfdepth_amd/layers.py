@@ -30,11 +30,25 @@ def _activation(nonlin):
     return nn.Identity()
 
 
+class ReflectConv2d(nn.Conv2d):
+    """nn.Conv2d(padding_mode='reflect') (same parameters and state-dict keys) whose one-pixel
+    reflect padding runs on the HIP pad kernels for fp32 GPU maps: a deterministic backward
+    (ATen's reflection_pad2d backward scatters with atomics) and one launch each way."""
+
+    def _conv_forward(self, x, weight, bias):
+        if (self.padding_mode == 'reflect' and tuple(self.padding) == (1, 1) and x.is_cuda and x.dim() == 4
+                and x.dtype == torch.float32 and x.shape[-1] >= 2 and x.shape[-2] >= 2
+                and not torch.is_autocast_enabled('cuda') and os.environ.get('VFD_REFLECT_PAD', '1') != '0'):
+            from . import kernels as KN
+            return F.conv2d(KN.ReflectPad1.apply(x), weight, bias, self.stride, 0, self.dilation, self.groups)
+        return super()._conv_forward(x, weight, bias)
+
+
 def conv2d_block(cin, cout, kernel_size=3, stride=1, dilation=1, nonlin='LRU',
                  padding_mode='reflect', norm=False):
     pad = ((kernel_size - 1) * dilation) // 2
-    conv = nn.Conv2d(cin, cout, kernel_size, stride=stride, dilation=dilation, padding=pad,
-                     bias=not norm, padding_mode=padding_mode)
+    conv = ReflectConv2d(cin, cout, kernel_size, stride=stride, dilation=dilation, padding=pad,
+                         bias=not norm, padding_mode=padding_mode)
     return nn.Sequential(conv, nn.BatchNorm2d(cout) if norm else nn.Identity(), _activation(nonlin))
 
 

@@ -46,6 +46,10 @@ class VFDepthAlgo:
         if self.device.type == 'cuda':
             # the C-ABI ops launch on the current device's stream: make it this rank's device
             torch.cuda.set_device(self.device)
+        if torch.backends.cudnn.deterministic:
+            # the reference's train.py:23 switch; MIOpen honours it only through this variable,
+            # read once per process at its first convolution (so set it before building models)
+            os.environ.setdefault('MIOPEN_DEBUG_CONVOLUTION_DETERMINISTIC', '1')
         if getattr(self, 'net_precision', 'fp32') not in ('fp32', 'bf16'):
             raise ValueError(f'net_precision must be fp32 or bf16, got {self.net_precision!r}')
         self.prepare_dataset(cfg, rank)

@@ -395,8 +395,8 @@ def main():
             r = roofline_any(k)
             print(f'[bench] {k:20s} {n:4d} launches {t / n * 1e3:9.1f} us/launch  '
                   f'{r["achieved"]:8.1f} {r["unit"]} ({r["frac"]:.3f} of peak)', file=sys.stderr)
-        print(f'[bench] hot-path kernels {sum(t for _, t in prof.values()) / args.steps:.2f} ms/step, fused BN '
-              f'{sum(t for _, t in dense.values()) / args.steps:.2f} ms/step, of '
+        print(f'[bench] hot-path kernels {sum(t for _, t in prof.values()) / args.steps:.2f} ms/step, fused dense '
+              f'{sum(t for _, t in dense.values()) / args.steps:.2f} ms/step (BN, pads, upsample bwd), of '
               f'{elapsed / args.steps * 1e3:.2f} ms/step; loss {float(losses["total_loss"]):.5f}', file=sys.stderr)
     # aggregate over every HBM-bound hot-path op of the step (per-kernel and aggregate)
     agg_bytes = sum(algorithmic_bytes(k, s) * prof[k][0] for k in hbm_ops)

@@ -322,7 +322,7 @@ int vfd_upsample_ac_bwd(const float* g, float* dsrc, long long planes, int h, in
  * recorded; vfd_prof_read_kernels: the same per kernel id into arrays of `count` entries.
  * Both reset the record. */
 #define VFD_PROF_ALL (-1)
-#define VFD_KERNEL_COUNT 25
+#define VFD_KERNEL_COUNT 26
 const char* vfd_kernel_name(int kernel_id);
 int vfd_prof_enable(int kernel_id);
 int vfd_prof_read(int* launches, double* total_ms);

@@ -120,7 +120,7 @@ extern "C" int vfd_upsample_ac_bwd(const float* g, float* dsrc, long long planes
   VFD_REQUIRE(g && dsrc && planes > 0 && h > 0 && w > 0 && hs > 0 && ws > 0 && hs <= h && ws <= w,
               "upsample_ac_bwd: bad sizes");
   hipStream_t s = (hipStream_t)stream;
-  vfd::ProfScope ps(vfd::K_AGGREGATE, s);
+  vfd::ProfScope ps(vfd::K_UPSAMPLE_BWD, s);
   const long long n = planes * hs * ws;
   vfd::up_ac_bwd_k<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(g, dsrc, planes, h, w, hs, ws);
   return vfd::fail_launch("upsample_ac_bwd");

@@ -460,6 +460,8 @@ def lrelu_pad_backward(g, out, slope=0.1):
     gp = torch.empty(n, C, hp - 2, wp - 2, device=g.device, memory_format=torch.channels_last)
     L.check(lib.vfd_lrelu_pad1_bwd_nhwc(g.data_ptr(), out.data_ptr(), gp.data_ptr(), n, hp - 2, wp - 2, C, slope,
                                         L.stream()), 'lrelu_pad1_bwd_nhwc')
+    if L.PROF_ON:                            # g in, the output's interior in, gp out
+        L.ALG_BYTES['reflect_pad'] += (g.numel() + 2 * gp.numel()) * 4
     return gp
 
 
@@ -841,6 +843,8 @@ class AggregateUp(torch.autograd.Function):
             dl = torch.empty(shp, device=d.device)
             L.check(lib.vfd_upsample_ac_bwd(d.data_ptr(), dl.data_ptr(), BN * C, h, w, shp[-2], shp[-1], L.stream()),
                     'upsample_ac_bwd')
+            if L.PROF_ON:
+                L.ALG_BYTES['upsample_bwd'] += (d.numel() + dl.numel()) * 4
             grads.append(dl)
         return (d, d.sum((0, 2, 3))) + tuple(grads)
 
@@ -950,6 +954,8 @@ class ReflectPad1(torch.autograd.Function):
         y = torch.empty(*lead, h + 2, w + 2, device=x.device)
         planes = x.numel() // (h * w)
         L.check(lib.vfd_reflect_pad1_fwd(x.data_ptr(), y.data_ptr(), planes, h, w, L.stream()), 'reflect_pad1_fwd')
+        if L.PROF_ON:
+            L.ALG_BYTES['reflect_pad'] += (x.numel() + y.numel()) * 4
         ctx.shape = tuple(x.shape)
         return y
 
@@ -961,4 +967,6 @@ class ReflectPad1(torch.autograd.Function):
         dx = torch.empty(ctx.shape, device=g.device)
         planes = dx.numel() // (h * w)
         L.check(lib.vfd_reflect_pad1_bwd(g.data_ptr(), dx.data_ptr(), planes, h, w, L.stream()), 'reflect_pad1_bwd')
+        if L.PROF_ON:
+            L.ALG_BYTES['reflect_pad'] += (g.numel() + dx.numel()) * 4
         return dx

@@ -313,8 +313,10 @@ int vfd_aggregate_fwd(int BN, int C, int h, int w, const float* base, int n_leve
                       const float* const* levels, const int* level_hw, const float* bias, float* out,
                       void* stream);
 /* backward of the align_corners bilinear upsample (the aggregation's levels): g [planes, h, w] ->
- * dsrc [planes, hs, ws] as a fixed-order gather (deterministic, no atomics) */
-int vfd_upsample_ac_bwd(const float* g, float* dsrc, long long planes, int h, int w, int hs, int ws, void* stream);
+ * dsrc [planes, hs, ws] as a separable fixed-order gather (deterministic, no atomics);
+ * tmp: [planes, h, ws] scratch */
+int vfd_upsample_ac_bwd(const float* g, float* dsrc, float* tmp, long long planes, int h, int w, int hs, int ws,
+                        void* stream);
 
 /* ------------------------------------------------------------------ measurement hooks */
 /* Record HIP events around every launch of kernel `kernel_id` (see vfd_kernel_name; -1 = all,

@@ -603,6 +603,8 @@ def test_reflect_pad_upsample_and_lrelu_pad_backward():
     d = torch.randn(6, 256, 48, 80, device=DEV, generator=gen)
     for hs, ws in ((24, 40), (12, 20), (6, 10)):
         dl = torch.empty(6, 256, hs, ws, device=DEV)
-        KN.L.check(lib.vfd_upsample_ac_bwd(d.data_ptr(), dl.data_ptr(), 6 * 256, 48, 80, hs, ws, KN.L.stream()), 'up')
+        tmp = torch.empty(6 * 256 * 48 * ws, device=DEV)
+        KN.L.check(lib.vfd_upsample_ac_bwd(d.data_ptr(), dl.data_ptr(), tmp.data_ptr(), 6 * 256, 48, 80, hs, ws,
+                                           KN.L.stream()), 'up')
         ref = torch.ops.aten.upsample_bilinear2d_backward(d, [48, 80], [6, 256, hs, ws], True, None, None)
         close(dl, ref, f'upsample backward {hs}x{ws}', atol=1e-5, rtol=1e-5)

@@ -72,57 +72,75 @@ __device__ __forceinline__ void up_axis(int n_src, int n, int y, int* y0, int* y
   *y1 = *y0 + (*y0 < n_src - 1 ? 1 : 0);
 }
 
-// Backward of the align_corners bilinear upsample as a gather: every source pixel sums
-// w_y * w_x * g over the output pixels whose taps name it, in a fixed order (ATen's backward
-// scatters with atomics).  Candidate output rows / columns come from the scale, then the exact
-// forward taps decide.
-__global__ __launch_bounds__(256) void up_ac_bwd_k(const float* __restrict__ g, float* __restrict__ dsrc,
-                                                   long long planes, int h, int w, int hs, int ws) {
+// Backward of the align_corners bilinear upsample as a separable gather (the forward weight of
+// source (ys, xs) for output (y, x) is wy(y, ys) * wx(x, xs)): pass 1 sums each output row over
+// the columns whose taps name xs, pass 2 sums those over the rows whose taps name ys; every sum
+// in a fixed order (ATen's backward scatters with atomics).  Candidate indices come from the
+// scale, then the forward's exact taps decide.
+__device__ __forceinline__ void up_range(int s, int n_src, int n, int* lo, int* hi) {
+  if (n_src == n) { *lo = *hi = s; return; }
+  const float sc = n > 1 ? (float)(n_src - 1) / (float)(n - 1) : 0.f;
+  if (!(sc > 0.f)) { *lo = 0; *hi = n - 1; return; }
+  *lo = max(0, (int)floorf((float)(s - 1) / sc) - 1);
+  *hi = min(n - 1, (int)ceilf((float)(s + 1) / sc) + 1);
+}
+
+__device__ __forceinline__ float up_weight(int n_src, int n, int y, int s) {
+  int y0, y1;
+  float l;
+  up_axis(n_src, n, y, &y0, &y1, &l);
+  return (y0 == s ? 1.f - l : 0.f) + (y1 == s ? l : 0.f);
+}
+
+// tmp[p][y][xs] = sum_x wx(x, xs) g[p][y][x]
+__global__ __launch_bounds__(256) void up_ac_bwd_x_k(const float* __restrict__ g, float* __restrict__ tmp,
+                                                     long long planes, int h, int w, int ws) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= planes * h * ws) return;
+  const int xs = (int)(i % ws);
+  const long long row = i / ws;                     // p * h + y
+  int lo, hi;
+  up_range(xs, ws, w, &lo, &hi);
+  const float* gr = g + row * w;
+  float acc = 0.f;
+  for (int x = lo; x <= hi; ++x) {
+    const float wx = up_weight(ws, w, x, xs);
+    if (wx != 0.f) acc += wx * gr[x];
+  }
+  tmp[i] = acc;
+}
+
+// dsrc[p][ys][xs] = sum_y wy(y, ys) tmp[p][y][xs]
+__global__ __launch_bounds__(256) void up_ac_bwd_y_k(const float* __restrict__ tmp, float* __restrict__ dsrc,
+                                                     long long planes, int h, int hs, int ws) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= planes * hs * ws) return;
   const int xs = (int)(i % ws);
   const long long t = i / ws;
   const int ys = (int)(t % hs);
   const long long p = t / hs;
-  auto range = [](int s, int n_src, int n, int* lo, int* hi) {
-    if (n_src == n) { *lo = *hi = s; return; }
-    const float sc = n > 1 ? (float)(n_src - 1) / (float)(n - 1) : 0.f;
-    if (!(sc > 0.f)) { *lo = 0; *hi = n - 1; return; }
-    *lo = max(0, (int)floorf((float)(s - 1) / sc) - 1);
-    *hi = min(n - 1, (int)ceilf((float)(s + 1) / sc) + 1);
-  };
-  int ylo, yhi, xlo, xhi;
-  range(ys, hs, h, &ylo, &yhi);
-  range(xs, ws, w, &xlo, &xhi);
-  const float* gp = g + p * h * w;
+  int lo, hi;
+  up_range(ys, hs, h, &lo, &hi);
+  const float* tp = tmp + p * h * ws + xs;
   float acc = 0.f;
-  for (int y = ylo; y <= yhi; ++y) {
-    int y0, y1;
-    float ly;
-    up_axis(hs, h, y, &y0, &y1, &ly);
-    const float wy = (y0 == ys ? 1.f - ly : 0.f) + (y1 == ys ? ly : 0.f);
-    if (wy == 0.f) continue;
-    for (int x = xlo; x <= xhi; ++x) {
-      int x0, x1;
-      float lx;
-      up_axis(ws, w, x, &x0, &x1, &lx);
-      const float wx = (x0 == xs ? 1.f - lx : 0.f) + (x1 == xs ? lx : 0.f);
-      if (wx != 0.f) acc += wy * wx * gp[(size_t)y * w + x];
-    }
+  for (int y = lo; y <= hi; ++y) {
+    const float wy = up_weight(hs, h, y, ys);
+    if (wy != 0.f) acc += wy * tp[(size_t)y * ws];
   }
   dsrc[i] = acc;
 }
 
 }  // namespace vfd
 
-extern "C" int vfd_upsample_ac_bwd(const float* g, float* dsrc, long long planes, int h, int w, int hs, int ws,
-                                   void* stream) {
-  VFD_REQUIRE(g && dsrc && planes > 0 && h > 0 && w > 0 && hs > 0 && ws > 0 && hs <= h && ws <= w,
+extern "C" int vfd_upsample_ac_bwd(const float* g, float* dsrc, float* tmp, long long planes, int h, int w, int hs,
+                                   int ws, void* stream) {
+  VFD_REQUIRE(g && dsrc && tmp && planes > 0 && h > 0 && w > 0 && hs > 0 && ws > 0 && hs <= h && ws <= w,
               "upsample_ac_bwd: bad sizes");
   hipStream_t s = (hipStream_t)stream;
   vfd::ProfScope ps(vfd::K_UPSAMPLE_BWD, s);
-  const long long n = planes * hs * ws;
-  vfd::up_ac_bwd_k<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(g, dsrc, planes, h, w, hs, ws);
+  const long long n1 = planes * h * ws, n2 = planes * hs * ws;
+  vfd::up_ac_bwd_x_k<<<(unsigned)((n1 + 255) / 256), 256, 0, s>>>(g, tmp, planes, h, w, ws);
+  vfd::up_ac_bwd_y_k<<<(unsigned)((n2 + 255) / 256), 256, 0, s>>>(tmp, dsrc, planes, h, hs, ws);
   return vfd::fail_launch("upsample_ac_bwd");
 }
 

@@ -1431,11 +1431,10 @@ __global__ __launch_bounds__(64) void fuse_depth_bwd_gather_k(vfd_voxel_desc d, 
       tq[0][q] = tq[1][q] = 0.f;
     }
   };
-  // batches of U items: records lane-parallel (lane u < U holds item j + u), rows loaded for the
-  // whole batch before it is summed
-  for (int j = lo; j < hi; j += U) {
-    const TileItem m = ib[min(j + (lane < U ? lane : 0), hi - 1)];
-    float g[U], o[U];
+  // batches of U items, software-pipelined: records fetched lane-parallel two batches ahead
+  // (lane u < U holds item j + u), the next batch's rows loaded while the current one is summed
+  auto fetch = [&](int j) { return ib[min(j + (lane < U ? lane : 0), hi - 1)]; };
+  auto load = [&](const TileItem& m, float (&g)[U], float (&o)[U]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t vc = (uint32_t)__builtin_amdgcn_readlane((int)m.vc, u);
@@ -1443,6 +1442,8 @@ __global__ __launch_bounds__(64) void fuse_depth_bwd_gather_k(vfd_voxel_desc d, 
       g[u] = gv[row];
       o[u] = ov[row];
     }
+  };
+  auto consume = [&](int j, const TileItem& m, const float (&g)[U], const float (&o)[U]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int lxy = __builtin_amdgcn_readlane(m.lxy, u);
@@ -1461,6 +1462,24 @@ __global__ __launch_bounds__(64) void fuse_depth_bwd_gather_k(vfd_voxel_desc d, 
         tq[0][q] += w * d0;
         tq[1][q] += w * d1;
       }
+    }
+  };
+  if (lo < hi) {
+    TileItem m0 = fetch(lo), m1 = fetch(lo + U);
+    float g0[U], o0[U], g1[U], o1[U];
+    load(m0, g0, o0);
+    for (int j = lo;; j += 2 * U) {
+      const TileItem m2 = fetch(j + 2 * U);
+      load(m1, g1, o1);
+      consume(j, m0, g0, o0);
+      if (j + U >= hi) break;
+      m0 = fetch(j + 3 * U);
+      load(m2, g0, o0);
+      consume(j + U, m1, g1, o1);
+      if (j + 2 * U >= hi) break;
+      m1 = m0;
+      m0 = m2;
+      // (g0, o0) hold batch j + 2U (m0), m1 the batch after it
     }
   }
   flush();

@@ -841,8 +841,9 @@ class AggregateUp(torch.autograd.Function):
         grads = []
         for shp in ctx.level_shapes:          # the upsample's adjoint as a gather (deterministic)
             dl = torch.empty(shp, device=d.device)
-            L.check(lib.vfd_upsample_ac_bwd(d.data_ptr(), dl.data_ptr(), BN * C, h, w, shp[-2], shp[-1], L.stream()),
-                    'upsample_ac_bwd')
+            tmp = torch.empty(BN * C * h * shp[-1], device=d.device)
+            L.check(lib.vfd_upsample_ac_bwd(d.data_ptr(), dl.data_ptr(), tmp.data_ptr(), BN * C, h, w, shp[-2], shp[-1],
+                                            L.stream()), 'upsample_ac_bwd')
             if L.PROF_ON:
                 L.ALG_BYTES['upsample_bwd'] += (d.numel() + dl.numel()) * 4
             grads.append(dl)

@@ -456,7 +456,10 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pcd_main_k(PdGeom g, const floa
                                                            float* __restrict__ dx,
                                                            float* __restrict__ partial) {
   extern __shared__ float pd_lds[];
-  const int grp = blockIdx.x;
+  // XCD-contiguous ranges: workgroups are dealt round-robin to the 8 XCDs, so logical group
+  // (blockIdx % 8) * (G / 8) + blockIdx / 8 gives each XCD one contiguous run of tiles — a
+  // 1-2 n-tile window of weights (2.4 MB each) that stays in that XCD's L2 while its M-tiles pass
+  const int grp = (g.ngroup % 8 == 0) ? (blockIdx.x % 8) * (g.ngroup / 8) + blockIdx.x / 8 : blockIdx.x;
   const int a_lo = pd_lo(g, grp), a_hi = pd_lo(g, grp + 1);
   if (a_lo >= a_hi) return;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;

@@ -3,8 +3,9 @@
     python tools/traffic_from_pmc.py <fetch_counter_collection.csv> <write_counter_collection.csv> > profiles/traffic_config2.json
 
 Per MI355X_MICROARCH.md (HBM / rocprofv3): FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950
-FETCH_SIZE reports 1/2 of the bytes of wide coalesced reads, so it is doubled here; WRITE_SIZE
-is taken as is.  Each op (a C-ABI call, as the bench's roofline names it) sums the kernels it
+FETCH_SIZE reports 1/2 of the bytes of coalesced reads — calibrated here for 4-, 8- and 16-B
+lanes alike on a known-byte probe (tools/probe_fetch.py: 0.5000 of 512 MiB for all three widths,
+profiles/r2/fetch_probe.json) — so it is doubled; WRITE_SIZE is taken as is.  Each op (a C-ABI call, as the bench's roofline names it) sums the kernels it
 launches; values are bytes per op launch, averaged over all launches in the run."""
 import collections
 import csv
@@ -14,13 +15,15 @@ import sys
 
 OPS = {
     'mask_downsample': ['mask_downsample_k'],
-    'fusion_plan': ['fusion_plan_k', 'plan_index_k', 'plan_count_k', 'plan_scan_k', 'plan_fill_k', 'plan_task_k'],
-    'fuse_depth_fwd': ['fuse_depth_fwd_k'],
-    'fuse_depth_bwd': ['fuse_depth_bwd_k', 'fuse_depth_reduce_k'],
+    'fusion_plan': ['fusion_plan_k', 'plan_index_k', 'plan_count_k', 'plan_scan_k', 'plan_fill_k', 'plan_order_k',
+                    'plan_copy_k', 'plan_task_k'],
+    'fuse_depth_fwd': ['fuse_depth_fwd_q_k', 'fuse_depth_fwd_k'],
+    'fuse_depth_bwd': ['fuse_depth_bwd_gather_k', 'fuse_depth_combine_k', 'fuse_depth_bwd_k', 'fuse_depth_reduce_k'],
     'fuse_pose_fwd': ['fuse_pose_fwd_k'],
     'fuse_pose_bwd': ['pose_fold_k', 'fuse_pose_bwd_k', 'pose_combine_k'],
     'voxel_project_fwd': ['voxel_project_fwd_k'],
-    'voxel_project_plan': ['vpb_count_k', 'vpb_scan1_k', 'vpb_scan2_k', 'vpb_fill_k', 'vpb_tile_k', 'vpb_tasks_k'],
+    'voxel_project_plan': ['vpb_count_k', 'vpb_scan1_k', 'vpb_scan2_k', 'vpb_fill_k', 'vpb_order_k', 'vpb_tile_k',
+                           'vpb_tasks_k'],
     'voxel_project_bwd': ['vpb_fold_zero_k', 'vpb_main_k'],
     'view_stats': ['view_stats_k', 'view_finalize_k'],
     'view_apply': ['view_apply_k'],
@@ -30,6 +33,11 @@ OPS = {
     'smooth_fwd': ['smooth_fwd_k', 'smooth_finalize_k'],
     'smooth_bwd': ['smooth_bwd_k'],
     'aggregate': ['aggregate_fwd_k'],
+    'proj_conv_fwd': ['pcv_main_k', 'pcv_reduce_k'],
+    'proj_conv_dgrad': ['pcd_main_k', 'pcd_reduce_k'],
+    'pad_conv_fwd': ['ppc_main_k', 'ppc_reduce_k'],
+    'depth_syn_fwd': ['depth_syn_fwd_k'],
+    'depth_syn_bwd': ['depth_syn_bwd_k'],
 }
 
 

@@ -21,9 +21,9 @@ struct PTarget {
   int bt, b, slot, cam;
   size_t br;
 };
-__device__ __forceinline__ PTarget ptarget_of(const vfd_photo_desc& d) {
+__device__ __forceinline__ PTarget ptarget_of(const vfd_photo_desc& d, int bz = -1) {
   PTarget t;
-  t.bt = blockIdx.z;
+  t.bt = bz >= 0 ? bz : (int)blockIdx.z;
   t.b = t.bt / d.cam_count;
   t.slot = t.bt % d.cam_count;
   t.cam = d.cam_begin + t.slot;
@@ -80,11 +80,16 @@ __global__ __launch_bounds__(256) void photo_fwd_k(vfd_photo_desc d, const float
   constexpr int PT = TS + 2, PA = PT * PT;
   const int T = d.T, F = d.F;
   const int n_img = 2 * T + F;
-  const PTarget tg = ptarget_of(d);
+  // XCD-contiguous tiles: workgroups are dealt round-robin to the 8 XCDs, so the linear tile
+  // index (L % 8) * (total / 8) + L / 8 hands each XCD a contiguous band of tile rows — a tile's
+  // halo rows and the cache lines it shares with its neighbours are then fetched into the same
+  // L2 once instead of once per XCD
+  const uint3 bi = xcd_tile();
+  const PTarget tg = ptarget_of(d, (int)bi.z);
   const int bn = tg.bt, b = tg.b;
   const size_t br = tg.br;
   const int H = d.H, W = d.W, HW = H * W;
-  const int ty0 = blockIdx.y * TS, tx0 = blockIdx.x * TS;
+  const int ty0 = bi.y * TS, tx0 = bi.x * TS;
   // ---- stage tiles (+1 reflect halo)
   for (int i = threadIdx.x; i < PA; i += blockDim.x) {
     const int ly = i / PT, lx = i % PT;
@@ -163,7 +168,7 @@ __global__ __launch_bounds__(256) void photo_fwd_k(vfd_photo_desc d, const float
     sel[(size_t)bn * HW + p] = (uint8_t)(ridx | (auto_bit ? 4 : 0) | (sidx << 3));
   }
   const int nblk = gridDim.x * gridDim.y;
-  const int blk = blockIdx.y * gridDim.x + blockIdx.x;
+  const int blk = bi.y * gridDim.x + bi.x;
   double* out = partial + ((size_t)bn * nblk + blk) * 6;
   for (int i = 0; i < 6; ++i) {
     double v = wave_sum(acc[i]);

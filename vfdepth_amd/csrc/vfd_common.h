@@ -64,6 +64,17 @@ __device__ __forceinline__ void pad_sets(int i, int n, bool pad, int* idx, int* 
   *cnt = c;
 }
 
+// XCD-contiguous workgroup numbering: the hardware deals workgroups round-robin (by linear id) to
+// the 8 XCDs, each with its own L2; remapping linear id L to (L % 8) * (total / 8) + L / 8 gives
+// each XCD one contiguous run of (x-fastest) tiles, so neighbouring tiles share that XCD's L2.
+// Identity when the grid is not a multiple of 8.
+__device__ __forceinline__ uint3 xcd_tile() {
+  const unsigned total = gridDim.x * gridDim.y * gridDim.z;
+  const unsigned L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  const unsigned t = (total % 8u == 0u) ? (L % 8u) * (total / 8u) + L / 8u : L;
+  return make_uint3(t % gridDim.x, (t / gridDim.x) % gridDim.y, t / (gridDim.x * gridDim.y));
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll

@@ -32,9 +32,9 @@ struct Target {
   int bt, b, cam;
   size_t br;
 };
-__device__ __forceinline__ Target target_of(const vfd_view_desc& d) {
+__device__ __forceinline__ Target target_of(const vfd_view_desc& d, int by) {
   Target t;
-  t.bt = blockIdx.y;
+  t.bt = by;
   t.b = t.bt / d.cam_count;
   t.cam = d.cam_begin + t.bt % d.cam_count;
   t.br = (size_t)t.b * d.N + t.cam;
@@ -148,14 +148,15 @@ __device__ __forceinline__ float wave_reduce_n(float (&v)[N]) {
 __global__ __launch_bounds__(VBLK) void view_stats_k(vfd_view_desc d, const float* __restrict__ depth,
                                                      const float* __restrict__ invK, const float* __restrict__ M,
                                                      const float* __restrict__ mask, float* __restrict__ partial) {
-  const Target tg = target_of(d);
+  const uint3 bi = xcd_tile();         // XCD-contiguous pixel blocks: a band of rows per XCD's L2
+  const Target tg = target_of(d, (int)bi.y);
   const int bn = tg.bt, b = tg.b, cam = tg.cam;
   const int HW = d.H * d.W;
   const int nrow = gridDim.x * (VBLK / 64);
   const int stride = d.n_warp * 8 + 2;
   const int lane = threadIdx.x & 63;
   // column-major partials: column c of camera slot bn is partial[(bn * stride + c) * nrow + row]
-  const int row = blockIdx.x * (VBLK / 64) + (threadIdx.x >> 6);
+  const int row = bi.x * (VBLK / 64) + (threadIdx.x >> 6);
   float* out = partial + (size_t)bn * stride * nrow + row;
   const float* ref = d.color[0] + tg.br * 3 * HW;
   const float* rmask = mask + tg.br * HW;
@@ -163,7 +164,7 @@ __global__ __launch_bounds__(VBLK) void view_stats_k(vfd_view_desc d, const floa
   int pix[VPPT];
 #pragma unroll
   for (int k = 0; k < VPPT; ++k) {
-    pix[k] = blockIdx.x * VBLK * VPPT + k * VBLK + threadIdx.x;
+    pix[k] = bi.x * VBLK * VPPT + k * VBLK + threadIdx.x;
     float ray[3];
     const bool in = pix[k] < HW;
     const int pk = in ? pix[k] : 0;
@@ -264,10 +265,11 @@ __global__ __launch_bounds__(VBLK) void view_apply_k(vfd_view_desc d, const floa
                                                      const float* __restrict__ mask, const float* __restrict__ coef,
                                                      float* __restrict__ color, float* __restrict__ cmask,
                                                      float* __restrict__ ovl, float* __restrict__ omask) {
-  const Target tg = target_of(d);
+  const uint3 bi = xcd_tile();
+  const Target tg = target_of(d, (int)bi.y);
   const int bn = tg.bt, b = tg.b, cam = tg.cam;
   const int HW = d.H * d.W;
-  const int p = blockIdx.x * VBLK + threadIdx.x;
+  const int p = bi.x * VBLK + threadIdx.x;
   if (p >= HW) return;
   float X[3], ray[3];
   backproject(invK + bn * 16, depth[(size_t)bn * HW + p], p % d.W, p / d.W, X, ray);
@@ -322,18 +324,19 @@ __global__ __launch_bounds__(VBLK) void view_bwd_k(vfd_view_desc d, const float*
                                                    const float* __restrict__ mask, const float* __restrict__ coef,
                                                    const float* __restrict__ g_color, const float* __restrict__ g_ovl,
                                                    float* __restrict__ d_depth, float* __restrict__ partial) {
-  const Target tg = target_of(d);
+  const uint3 bi = xcd_tile();
+  const Target tg = target_of(d, (int)bi.y);
   const int bn = tg.bt, b = tg.b, cam = tg.cam;
   const int HW = d.H * d.W;
   const int nrow = gridDim.x * (VBLK / 64);
-  const int row = blockIdx.x * (VBLK / 64) + (threadIdx.x >> 6);
+  const int row = bi.x * (VBLK / 64) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int T = d.n_temporal, F = d.n_overlap;
   float X[VPPT][3], ray[VPPT][3], dd[VPPT];
   int pix[VPPT];
 #pragma unroll
   for (int k = 0; k < VPPT; ++k) {
-    pix[k] = blockIdx.x * VBLK * VPPT + k * VBLK + threadIdx.x;
+    pix[k] = bi.x * VBLK * VPPT + k * VBLK + threadIdx.x;
     dd[k] = 0.f;
     if (pix[k] < HW) backproject(invK + bn * 16, depth[(size_t)bn * HW + pix[k]], pix[k] % d.W, pix[k] / d.W, X[k], ray[k]);
   }

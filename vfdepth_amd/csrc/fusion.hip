@@ -1178,8 +1178,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void fu
   constexpr int PR = PT2 + 1;
   __shared__ float4 acc_l[PR * 64];
   const int lane = threadIdx.x;
-  const int wt = blockIdx.x;
-  if (wt >= ctrl[0]) return;
+  const int wt = xcd_task(ctrl[0]);              // neighbouring tiles on one XCD (shared rows in its L2)
+  if (wt < 0) return;
 #ifdef VFD_PBW_TRACE
   const unsigned long long t_start = wall_clock64();
 #endif
@@ -1398,8 +1398,8 @@ __global__ __launch_bounds__(64) void fuse_depth_bwd_gather_k(vfd_voxel_desc d, 
   constexpr int U = 8;
   __shared__ float acc_l[PR * ROW];
   const int lane = threadIdx.x;
-  const int wt = blockIdx.x;
-  if (wt >= ctrl[0]) return;
+  const int wt = xcd_task(ctrl[0]);
+  if (wt < 0) return;
   const int4 rec = tasks[wt];
   const int bct = rec.x, lo = rec.y, hi = rec.z, meta = rec.w;
   const int nt = tiles_x(d) * tiles_y(d), ntx = tiles_x(d);
@@ -2406,7 +2406,7 @@ int vfd_fuse_pose_bwd(const vfd_voxel_desc* d, const void* plan, const int* coun
   if (d->pad_out) pose_fold_k<<<d->B * 2 * (d->X + d->Y) * POSE_FOLD_SPLIT, 256, 0, s>>>(
       *d, d_out, fbuf, (((uintptr_t)d_out | (uintptr_t)fbuf) & 15) == 0);
   const int ntask_max = host_tiles(d) * d->B * d->N + PBW_POOL;
-  fuse_pose_bwd_k<<<ntask_max, 64, 0, s>>>(*d, tasks, ctrl, csr, d_out, fbuf, pool, d_feats);
+  fuse_pose_bwd_k<<<128 * cdiv(ntask_max, 128), 64, 0, s>>>(*d, tasks, ctrl, csr, d_out, fbuf, pool, d_feats);
   pose_combine_k<<<std::min(PBW_POOL / 2, host_tiles(d) * d->B * d->N), 256, 0, s>>>(*d, combos, ctrl, pool, d_feats);
   return fail_launch("fuse_pose_bwd");
 }
@@ -2429,7 +2429,7 @@ int vfd_fuse_depth_bwd_planned(const vfd_voxel_desc* d, const void* plan, const 
   float* pool = (float*)((char*)ctrl + 256 + plan_fold_bytes(d));
   ProfScope ps(K_FUSE_DEPTH_BWD, s);
   const int ntask_max = host_tiles(d) * d->B * d->N + PBW_POOL;
-  fuse_depth_bwd_gather_k<<<ntask_max, 64, 0, s>>>(*d, tasks, ctrl, csr, d_vox, vox, pool, dP);
+  fuse_depth_bwd_gather_k<<<128 * cdiv(ntask_max, 128), 64, 0, s>>>(*d, tasks, ctrl, csr, d_vox, vox, pool, dP);
   fuse_depth_combine_k<<<std::min(PBW_POOL / 2, host_tiles(d) * d->B * d->N), 2 * K1G_CV, 0, s>>>(
       *d, combos, ctrl, pool, dP);
   // depth-column and bias gradients: the voxel walk without the scatter

@@ -75,6 +75,16 @@ __device__ __forceinline__ uint3 xcd_tile() {
   return make_uint3(t % gridDim.x, (t / gridDim.x) % gridDim.y, t / (gridDim.x * gridDim.y));
 }
 
+// Task index for a 1-D grid of single-task workgroups (grid a multiple of 128): runs of 16
+// consecutive tasks go to one XCD (the hardware deals workgroups round-robin to the 8 XCDs), so
+// neighbouring tiles share that XCD's L2, while dispatch still follows task order (the split
+// tiles' parts, queued first, start first on every XCD).  -1 = beyond the n tasks.
+__device__ __forceinline__ int xcd_task(int n) {
+  const int k = (int)(blockIdx.x % 8u), j = (int)(blockIdx.x / 8u);
+  const int t = ((j / 16) * 8 + k) * 16 + j % 16;
+  return t < n ? t : -1;
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll

@@ -173,6 +173,11 @@ int vfd_bn_bwd_apply(const vfd_bn_desc* d, const float* g, const float* y, const
                      int ns, double count, const float* gamma, const float* mean, const float* invstd, float* dx,
                      float* dresidual, float* dgamma, float* dbeta, void* stream);
 
+/* ------------------------------------------------------------------ geometry */
+/* batched 4x4 inverse of n row-major matrices (torch.inverse of the extrinsics, models/vfdepth.py:211):
+ * cofactors in geometry.inverse4x4's operation order (bit-identical to it), one thread per matrix */
+int vfd_inverse4x4(const float* m, float* out, int n, void* stream);
+
 /* ------------------------------------------------------------------ reflect padding (decoders) */
 /* nn.Conv2d(padding_mode='reflect', padding=1) of the decoders' 3x3 blocks (network/blocks.py):
  * x [planes, h, w] -> y [planes, h+2, w+2] (NCHW fp32), and its backward as a fixed-order gather

@@ -608,3 +608,20 @@ def test_reflect_pad_upsample_and_lrelu_pad_backward():
                                            KN.L.stream()), 'up')
         ref = torch.ops.aten.upsample_bilinear2d_backward(d, [48, 80], [6, 256, hs, ws], True, None, None)
         close(dl, ref, f'upsample backward {hs}x{ws}', atol=1e-5, rtol=1e-5)
+
+
+def test_inverse4x4_kernel_matches_torch_ops():
+    """The one-launch 4x4 inverse (geometry.hip) is bit-identical to the cofactor torch ops it
+    replaces (same operation order) and agrees with torch.linalg.inv to fp32 rounding."""
+    from vfdepth_amd import geometry
+    from vfdepth_amd.rotation import axis_angle_to_matrix
+    gen = torch.Generator().manual_seed(17)
+    E = torch.eye(4).repeat(3, 6, 1, 1)
+    E[..., :3, :3] = axis_angle_to_matrix(0.5 * torch.randn(3, 6, 3, generator=gen))
+    E[..., :3, 3] = 3 * torch.randn(3, 6, 3, generator=gen)
+    E[0, 0] = torch.randn(4, 4, generator=gen) + 4 * torch.eye(4)         # a general matrix too
+    Eg = E.to(DEV)
+    k = geometry.inverse4x4(Eg)                                          # kernel path
+    t = geometry.inverse4x4(Eg.clone().requires_grad_(True)).detach()    # torch-ops path (grad)
+    assert torch.equal(k, t)
+    close(k, torch.linalg.inv(E.double()).float(), '4x4 inverse vs linalg.inv', atol=1e-5, rtol=1e-5)

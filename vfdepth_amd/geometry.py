@@ -14,9 +14,16 @@ from .rotation import axis_angle_to_matrix
 
 
 def inverse4x4(m):
-    """Batched general 4x4 inverse by cofactors (torch ops only: capturable in a HIP graph, no
-    solver workspace).  Replaces torch.inverse on the extrinsics (vfdepth.py:211); for the rigid
-    camera transforms the two agree to fp32 rounding."""
+    """Batched general 4x4 inverse by cofactors (capturable in a HIP graph, no solver workspace).
+    Replaces torch.inverse on the extrinsics (vfdepth.py:211); for the rigid camera transforms the
+    two agree to fp32 rounding.  fp32 GPU tensors without a gradient run the one-launch HIP kernel
+    (`vfd_inverse4x4`, the same operation order: bit-identical); otherwise the torch ops below."""
+    if m.is_cuda and m.dtype == torch.float32 and not (m.requires_grad and torch.is_grad_enabled()):
+        from . import _lib as L
+        src = m.contiguous()
+        out = torch.empty_like(src)
+        L.check(L.load().vfd_inverse4x4(src.data_ptr(), out.data_ptr(), src.numel() // 16, L.stream()), 'inverse4x4')
+        return out
     a = m.reshape(-1, 4, 4)
     a00, a01, a02, a03 = a[:, 0, 0], a[:, 0, 1], a[:, 0, 2], a[:, 0, 3]
     a10, a11, a12, a13 = a[:, 1, 0], a[:, 1, 1], a[:, 1, 2], a[:, 1, 3]

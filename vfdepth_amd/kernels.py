@@ -518,7 +518,6 @@ class ProjConv(torch.autograd.Function):
         if x is None:   # only the bias gradient was asked for
             x = torch.empty(B * N, Cv * space.D, space.h + 2, space.w + 2, device=g.device,
                             memory_format=torch.channels_last)
-        w_perm = proj_conv_weight(w0, Cv, space.D)
         mask = (ctx.needs_input_grad[1], ctx.needs_input_grad[4], ctx.needs_input_grad[5])
         cb = torch.ops.aten.convolution_backward
         args = ([O], [1, 1], [0, 0], [1, 1], False, [0, 0], 1)
@@ -536,15 +535,17 @@ class ProjConv(torch.autograd.Function):
         if dx is not None:
             dw = db = None
             if mask[1] or mask[2]:
-                _, dw, db = cb(g_pre, x, w_perm, *args, [False, mask[1], mask[2]])
+                # the weight gradient reads only the weight's shape: w0 has it (no permuted copy)
+                _, dw, db = cb(g_pre, x, w0, *args, [False, mask[1], mask[2]])
         elif _DGRAD_LAYOUT == 'nchw' and mask[0]:
             # MIOpen's NCHW data-gradient solver (the NHWC one is ~1.5x slower at this shape);
             # the input tensor only supplies shape / memory format to the data gradient
+            w_perm = proj_conv_weight(w0, Cv, space.D)
             shape_only = torch.empty(x.shape, device=x.device)
             dx = cb(g_pre.contiguous(), shape_only, w_perm.contiguous(), *args, [True, False, False])[0]
-            _, dw, db = cb(g_pre, x, w_perm, *args, [False, mask[1], mask[2]])
+            _, dw, db = cb(g_pre, x, w0, *args, [False, mask[1], mask[2]])
         else:
-            dx, dw, db = cb(g_pre, x, w_perm, *args, [mask[0], mask[1], mask[2]])
+            dx, dw, db = cb(g_pre, x, proj_conv_weight(w0, Cv, space.D), *args, [mask[0], mask[1], mask[2]])
         dvox = dw0 = None
         if mask[0]:
             dx = _channels_last(dx, 'd frustum features')

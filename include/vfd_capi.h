@@ -178,6 +178,13 @@ int vfd_bn_bwd_apply(const vfd_bn_desc* d, const float* g, const float* y, const
  * cofactors in geometry.inverse4x4's operation order (bit-identical to it), one thread per matrix */
 int vfd_inverse4x4(const float* m, float* out, int n, void* stream);
 
+/* ------------------------------------------------------------------ ResNet stem max pool */
+/* MaxPool2d(3, 2, 1) of the encoders' stem, NCHW fp32: x [planes, h, w] -> y [planes, ho, wo]
+ * (ho = (h-1)/2 + 1) and the winning window position (0..8) per output as one byte; ATen's tie
+ * and NaN rules.  Backward: a fixed-order gather of the winners' gradients (no atomics). */
+int vfd_maxpool3s2_fwd(const float* x, float* y, uint8_t* arg, long long planes, int h, int w, void* stream);
+int vfd_maxpool3s2_bwd(const float* g, const uint8_t* arg, float* dx, long long planes, int h, int w, void* stream);
+
 /* ------------------------------------------------------------------ reflect padding (decoders) */
 /* nn.Conv2d(padding_mode='reflect', padding=1) of the decoders' 3x3 blocks (network/blocks.py):
  * x [planes, h, w] -> y [planes, h+2, w+2] (NCHW fp32), and its backward as a fixed-order gather
@@ -329,7 +336,7 @@ int vfd_upsample_ac_bwd(const float* g, float* dsrc, float* tmp, long long plane
  * recorded; vfd_prof_read_kernels: the same per kernel id into arrays of `count` entries.
  * Both reset the record. */
 #define VFD_PROF_ALL (-1)
-#define VFD_KERNEL_COUNT 26
+#define VFD_KERNEL_COUNT 27
 const char* vfd_kernel_name(int kernel_id);
 int vfd_prof_enable(int kernel_id);
 int vfd_prof_read(int* launches, double* total_ms);

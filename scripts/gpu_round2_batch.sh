@@ -2,8 +2,6 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
-K="fuse_pose or fuse_depth or full_step or deterministic" bash scripts/gpu_tests.sh tests/test_gpu_parity.py tests/test_gpu_fullsize.py || exit 1
+K="max_pool or batchnorm or reflect_pad or full_step or deterministic or aggregat" bash scripts/gpu_tests.sh tests/test_gpu_parity.py tests/test_gpu_fullsize.py || exit 1
 cp gpurun_out/tests/tests.log gpurun_out/tests_t.log
-bash scripts/gpu_bench.sh r2_xt --steps 20 --no-cpu-baseline --no-parity || exit 1
-cd /tmp
-timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $GRAFT_REPO_ROOT/gpurun_out/fetch -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-parity > /dev/null 2>&1
+bash scripts/gpu_bench.sh r2_idx --steps 20 --no-cpu-baseline --no-parity || exit 1

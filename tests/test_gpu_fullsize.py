@@ -610,6 +610,26 @@ def test_reflect_pad_upsample_and_lrelu_pad_backward():
         close(dl, ref, f'upsample backward {hs}x{ws}', atol=1e-5, rtol=1e-5)
 
 
+def test_stem_max_pool_matches_aten():
+    """MaxPool2d(3, 2, 1) with the one-byte argmax: forward bit-identical to ATen (ties of a ReLU
+    map's zeros go to the first maximum in scan order), backward equal to ATen's (fixed-order sum of
+    the <= 4 windows a pixel wins); odd and even sizes, the bench's stem shapes included."""
+    from vfdepth_amd import kernels as KN
+    gen = torch.Generator(device=DEV).manual_seed(41)
+    for shape in ((6, 64, 192, 320), (2, 64, 96, 160), (3, 5, 37, 53), (1, 2, 1, 1), (2, 3, 2, 7)):
+        x = torch.relu(torch.randn(shape, device=DEV, generator=gen)).requires_grad_(True)
+        if shape[-1] > 10:
+            x.data[:, :, ::3, ::2] = 0.5                                  # equal maxima in one window
+        xr = x.detach().clone().requires_grad_(True)
+        y = KN.MaxPool3s2.apply(x)
+        yr = F.max_pool2d(xr, 3, 2, 1)
+        assert torch.equal(y, yr), shape
+        g = torch.randn(y.shape, device=DEV, generator=gen)
+        y.backward(g)
+        yr.backward(g)
+        assert torch.equal(x.grad, xr.grad), shape
+
+
 def test_inverse4x4_kernel_matches_torch_ops():
     """The one-launch 4x4 inverse (geometry.hip) is bit-identical to the cofactor torch ops it
     replaces (same operation order) and agrees with torch.linalg.inv to fp32 rounding."""

@@ -95,39 +95,39 @@ __device__ __forceinline__ float up_weight(int n_src, int n, int y, int s) {
 // tmp[p][y][xs] = sum_x wx(x, xs) g[p][y][x]
 __global__ __launch_bounds__(256) void up_ac_bwd_x_k(const float* __restrict__ g, float* __restrict__ tmp,
                                                      long long planes, int h, int w, int ws) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= planes * h * ws) return;
-  const int xs = (int)(i % ws);
-  const long long row = i / ws;                     // p * h + y
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;       // (y, xs) of the plane
+  if (j >= h * ws) return;
+  const int y = j / ws, xs = j - y * ws;
   int lo, hi;
   up_range(xs, ws, w, &lo, &hi);
-  const float* gr = g + row * w;
-  float acc = 0.f;
-  for (int x = lo; x <= hi; ++x) {
-    const float wx = up_weight(ws, w, x, xs);
-    if (wx != 0.f) acc += wx * gr[x];
+  for (long long p = blockIdx.y; p < planes; p += gridDim.y) {
+    const float* gr = g + (p * h + y) * w;
+    float acc = 0.f;
+    for (int x = lo; x <= hi; ++x) {
+      const float wx = up_weight(ws, w, x, xs);
+      if (wx != 0.f) acc += wx * gr[x];
+    }
+    tmp[p * h * ws + j] = acc;
   }
-  tmp[i] = acc;
 }
 
 // dsrc[p][ys][xs] = sum_y wy(y, ys) tmp[p][y][xs]
 __global__ __launch_bounds__(256) void up_ac_bwd_y_k(const float* __restrict__ tmp, float* __restrict__ dsrc,
                                                      long long planes, int h, int hs, int ws) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= planes * hs * ws) return;
-  const int xs = (int)(i % ws);
-  const long long t = i / ws;
-  const int ys = (int)(t % hs);
-  const long long p = t / hs;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;       // (ys, xs) of the plane
+  if (j >= hs * ws) return;
+  const int ys = j / ws, xs = j - ys * ws;
   int lo, hi;
   up_range(ys, hs, h, &lo, &hi);
-  const float* tp = tmp + p * h * ws + xs;
-  float acc = 0.f;
-  for (int y = lo; y <= hi; ++y) {
-    const float wy = up_weight(hs, h, y, ys);
-    if (wy != 0.f) acc += wy * tp[(size_t)y * ws];
+  for (long long p = blockIdx.y; p < planes; p += gridDim.y) {
+    const float* tp = tmp + p * h * ws + xs;
+    float acc = 0.f;
+    for (int y = lo; y <= hi; ++y) {
+      const float wy = up_weight(hs, h, y, ys);
+      if (wy != 0.f) acc += wy * tp[(size_t)y * ws];
+    }
+    dsrc[p * hs * ws + j] = acc;
   }
-  dsrc[i] = acc;
 }
 
 }  // namespace vfd
@@ -138,9 +138,10 @@ extern "C" int vfd_upsample_ac_bwd(const float* g, float* dsrc, float* tmp, long
               "upsample_ac_bwd: bad sizes");
   hipStream_t s = (hipStream_t)stream;
   vfd::ProfScope ps(vfd::K_UPSAMPLE_BWD, s);
-  const long long n1 = planes * h * ws, n2 = planes * hs * ws;
-  vfd::up_ac_bwd_x_k<<<(unsigned)((n1 + 255) / 256), 256, 0, s>>>(g, tmp, planes, h, w, ws);
-  vfd::up_ac_bwd_y_k<<<(unsigned)((n2 + 255) / 256), 256, 0, s>>>(tmp, dsrc, planes, h, hs, ws);
+  VFD_REQUIRE((long long)h * w < (1LL << 31), "upsample_ac_bwd: plane too large");
+  const unsigned gy = (unsigned)(planes < 65535 ? planes : 65535);
+  vfd::up_ac_bwd_x_k<<<dim3((unsigned)((h * ws + 255) / 256), gy), 256, 0, s>>>(g, tmp, planes, h, w, ws);
+  vfd::up_ac_bwd_y_k<<<dim3((unsigned)((hs * ws + 255) / 256), gy), 256, 0, s>>>(tmp, dsrc, planes, h, hs, ws);
   return vfd::fail_launch("upsample_ac_bwd");
 }
 

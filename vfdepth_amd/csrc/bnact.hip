@@ -19,22 +19,23 @@ namespace vfd {
 constexpr int BN_THREADS = 256;
 
 struct BnRange {
-  long long lo, hi;     // element range [lo, hi) of the channel's N*HW elements
+  unsigned lo, hi;      // element range [lo, hi) of the channel's N*HW (< 2^31, host-checked) elements
 };
 
 __device__ __forceinline__ BnRange bn_range(const vfd_bn_desc& d, int split) {
-  const long long total = (long long)d.N * d.HW;
-  const long long chunk = ((total + d.S - 1) / d.S + 3) & ~3LL;
+  const unsigned total = (unsigned)d.N * (unsigned)d.HW;
+  const unsigned chunk = ((total + d.S - 1) / d.S + 3) & ~3u;
   BnRange r;
   r.lo = chunk * split;
   r.hi = r.lo + chunk < total ? r.lo + chunk : total;
   return r;
 }
 
-// element e of channel c -> offset in the NCHW tensor
-__device__ __forceinline__ size_t bn_off(const vfd_bn_desc& d, int c, long long e) {
-  const long long n = e / d.HW;
-  return ((size_t)n * d.C + c) * d.HW + (e - n * d.HW);
+// element e of channel c -> offset in the NCHW tensor (32-bit division: the 64-bit one is a long
+// software sequence per element)
+__device__ __forceinline__ size_t bn_off(const vfd_bn_desc& d, int c, unsigned e) {
+  const unsigned n = e / (unsigned)d.HW;
+  return ((size_t)n * d.C + c) * d.HW + (e - n * (unsigned)d.HW);
 }
 
 __device__ __forceinline__ double block_sum(double v, double* sh) {
@@ -52,9 +53,9 @@ __device__ __forceinline__ double block_sum(double v, double* sh) {
 template <typename F>
 __device__ __forceinline__ void bn_visit(const vfd_bn_desc& d, int c, BnRange r, F&& f) {
   if ((d.HW & 3) == 0) {
-    for (long long e = r.lo + 4 * threadIdx.x; e < r.hi; e += 4 * BN_THREADS) f(bn_off(d, c, e), 4);
+    for (unsigned e = r.lo + 4 * threadIdx.x; e < r.hi; e += 4 * BN_THREADS) f(bn_off(d, c, e), 4);
   } else {
-    for (long long e = r.lo + threadIdx.x; e < r.hi; e += BN_THREADS) f(bn_off(d, c, e), 1);
+    for (unsigned e = r.lo + threadIdx.x; e < r.hi; e += BN_THREADS) f(bn_off(d, c, e), 1);
   }
 }
 
@@ -279,6 +280,7 @@ int vfd_bn_splits(const vfd_bn_desc* d) {
 static int bn_check(const vfd_bn_desc* d, const char* what) {
   VFD_REQUIRE(d && d->N > 0 && d->C > 0 && d->HW > 0 && d->S > 0 && d->S == vfd_bn_splits(d),
               "%s: bad descriptor (S must be vfd_bn_splits)", what);
+  VFD_REQUIRE((long long)d->N * d->HW < (1LL << 31), "%s: more than 2^31 elements per channel", what);
   return VFD_OK;
 }
 

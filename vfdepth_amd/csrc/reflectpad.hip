@@ -14,32 +14,29 @@ __device__ __forceinline__ int rp_src(int i, int n) {       // padded index -> s
 __global__ __launch_bounds__(256) void reflect_pad_fwd_k(const float* __restrict__ x, float* __restrict__ y,
                                                          long long planes, int h, int w) {
   const int ho = h + 2, wo = w + 2;
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= planes * ho * wo) return;
-  const int X = (int)(i % wo);
-  const long long t = i / wo;
-  const int Y = (int)(t % ho);
-  const long long p = t / ho;
-  y[i] = x[(p * h + rp_src(Y, h)) * w + rp_src(X, w)];
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;       // pixel of the padded plane
+  if (j >= ho * wo) return;
+  const int Y = j / wo, X = j - Y * wo;
+  const int src = rp_src(Y, h) * w + rp_src(X, w);
+  for (long long p = blockIdx.y; p < planes; p += gridDim.y) y[p * ho * wo + j] = x[p * h * w + src];
 }
 
 __global__ __launch_bounds__(256) void reflect_pad_bwd_k(const float* __restrict__ g, float* __restrict__ dx,
                                                          long long planes, int h, int w) {
   const int wo = w + 2;
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= planes * h * w) return;
-  const int x = (int)(i % w);
-  const long long t = i / w;
-  const int yy = (int)(t % h);
-  const long long p = t / h;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;       // pixel of the plane
+  if (j >= h * w) return;
+  const int yy = j / w, x = j - yy * w;
   int rows[3], cols[3], nr, nc;
   pad_sets(yy, h, true, rows, &nr);
   pad_sets(x, w, true, cols, &nc);
-  const float* gp = g + p * (h + 2) * wo;
-  float s = 0.f;
-  for (int a = 0; a < nr; ++a)
-    for (int b = 0; b < nc; ++b) s += gp[rows[a] * wo + cols[b]];
-  dx[i] = s;
+  for (long long p = blockIdx.y; p < planes; p += gridDim.y) {
+    const float* gp = g + p * (h + 2) * wo;
+    float s = 0.f;
+    for (int a = 0; a < nr; ++a)
+      for (int b = 0; b < nc; ++b) s += gp[rows[a] * wo + cols[b]];
+    dx[p * h * w + j] = s;
+  }
 }
 
 // Backward of LeakyReLU(slope) followed by the one-pixel reflect pad, channels-last (the fused
@@ -48,15 +45,13 @@ __global__ __launch_bounds__(256) void reflect_pad_bwd_k(const float* __restrict
 __global__ __launch_bounds__(256) void lrelu_pad_bwd_nhwc_k(const float4* __restrict__ g, const float4* __restrict__ out,
                                                             float4* __restrict__ gp, long long n_img, int h, int w,
                                                             int c4, float slope) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_img * h * w * c4) return;
-  const int q = (int)(i % c4);
-  long long t = i / c4;
-  const int x = (int)(t % w);
-  t /= w;
-  const int yy = (int)(t % h);
-  const long long n = t / h;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;       // (pixel, float4) of image blockIdx.y
+  if (j >= h * w * c4) return;
+  const long long n = blockIdx.y;
+  const int pix = j / c4, q = j - pix * c4;
+  const int yy = pix / w, x = pix - yy * w;
   const int wo = w + 2;
+  const size_t i = (size_t)n * h * w * c4 + j;
   int rows[3], cols[3], nr, nc;
   pad_sets(yy, h, true, rows, &nr);
   pad_sets(x, w, true, cols, &nc);
@@ -85,20 +80,22 @@ using namespace vfd;
 extern "C" {
 
 int vfd_reflect_pad1_fwd(const float* x, float* y, long long planes, int h, int w, void* stream) {
-  VFD_REQUIRE(x && y && planes > 0 && h >= 2 && w >= 2, "reflect_pad1: bad arguments (h, w >= 2)");
+  VFD_REQUIRE(x && y && planes > 0 && h >= 2 && w >= 2 && (long long)(h + 2) * (w + 2) < (1LL << 31),
+              "reflect_pad1: bad arguments (h, w >= 2)");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_REFLECT_PAD, s);
-  const long long n = planes * (h + 2) * (w + 2);
-  reflect_pad_fwd_k<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(x, y, planes, h, w);
+  const dim3 grid((unsigned)(((h + 2) * (w + 2) + 255) / 256), (unsigned)(planes < 65535 ? planes : 65535));
+  reflect_pad_fwd_k<<<grid, 256, 0, s>>>(x, y, planes, h, w);
   return fail_launch("reflect_pad1_fwd");
 }
 
 int vfd_reflect_pad1_bwd(const float* g, float* dx, long long planes, int h, int w, void* stream) {
-  VFD_REQUIRE(g && dx && planes > 0 && h >= 2 && w >= 2, "reflect_pad1: bad arguments (h, w >= 2)");
+  VFD_REQUIRE(g && dx && planes > 0 && h >= 2 && w >= 2 && (long long)(h + 2) * (w + 2) < (1LL << 31),
+              "reflect_pad1: bad arguments (h, w >= 2)");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_REFLECT_PAD, s);
-  const long long n = planes * h * w;
-  reflect_pad_bwd_k<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(g, dx, planes, h, w);
+  const dim3 grid((unsigned)((h * w + 255) / 256), (unsigned)(planes < 65535 ? planes : 65535));
+  reflect_pad_bwd_k<<<grid, 256, 0, s>>>(g, dx, planes, h, w);
   return fail_launch("reflect_pad1_bwd");
 }
 
@@ -109,8 +106,9 @@ int vfd_lrelu_pad1_bwd_nhwc(const float* g, const float* out, float* gp, long lo
   VFD_REQUIRE((((uintptr_t)g | (uintptr_t)out | (uintptr_t)gp) & 15) == 0, "lrelu_pad1_bwd_nhwc: 16-B alignment");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_REFLECT_PAD, s);
-  const long long n = n_img * h * w * (C / 4);
-  lrelu_pad_bwd_nhwc_k<<<(unsigned)((n + 255) / 256), 256, 0, s>>>((const float4*)g, (const float4*)out, (float4*)gp,
+  VFD_REQUIRE(n_img < 65536 && (long long)h * w * C < (1LL << 31), "lrelu_pad1_bwd_nhwc: too large");
+  const dim3 grid((unsigned)(((long long)h * w * (C / 4) + 255) / 256), (unsigned)n_img);
+  lrelu_pad_bwd_nhwc_k<<<grid, 256, 0, s>>>((const float4*)g, (const float4*)out, (float4*)gp,
                                                                   n_img, h, w, C / 4, slope);
   return fail_launch("lrelu_pad1_bwd_nhwc");
 }

@@ -972,3 +972,43 @@ class ReflectPad1(torch.autograd.Function):
         if L.PROF_ON:
             L.ALG_BYTES['reflect_pad'] += (g.numel() + dx.numel()) * 4
         return dx
+
+
+# =============================================================================================
+# ResNet stem max pool (3x3, stride 2, padding 1) with a one-byte argmax and a gather backward
+# =============================================================================================
+class MaxPool3s2(torch.autograd.Function):
+    """F.max_pool2d(x, 3, 2, 1) for NCHW fp32 x (maxpool.hip): one byte of window index per
+    output instead of ATen's int64 indices; deterministic gather backward."""
+
+    @staticmethod
+    def forward(ctx, x):
+        lib = L.load()
+        _check_device(x, 'max pool input')
+        x = x.contiguous()
+        *lead, h, w = x.shape
+        ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+        y = torch.empty(*lead, ho, wo, device=x.device)
+        arg = torch.empty(*lead, ho, wo, dtype=torch.uint8, device=x.device)
+        planes = x.numel() // (h * w)
+        L.check(lib.vfd_maxpool3s2_fwd(x.data_ptr(), y.data_ptr(), arg.data_ptr(), planes, h, w, L.stream()),
+                'maxpool3s2_fwd')
+        if L.PROF_ON:
+            L.ALG_BYTES['maxpool'] += (x.numel() + y.numel()) * 4 + arg.numel()
+        ctx.shape = tuple(x.shape)
+        ctx.save_for_backward(arg)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        lib = L.load()
+        arg, = ctx.saved_tensors
+        g = g.contiguous()
+        h, w = ctx.shape[-2:]
+        dx = torch.empty(ctx.shape, device=g.device)
+        planes = dx.numel() // (h * w)
+        L.check(lib.vfd_maxpool3s2_bwd(g.data_ptr(), arg.data_ptr(), dx.data_ptr(), planes, h, w, L.stream()),
+                'maxpool3s2_bwd')
+        if L.PROF_ON:
+            L.ALG_BYTES['maxpool'] += (g.numel() + dx.numel()) * 4 + arg.numel()
+        return dx

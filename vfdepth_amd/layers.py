@@ -103,6 +103,17 @@ def bn_act(bn, x, residual=None, relu=True):
     return F.relu(y, inplace=True) if relu else y
 
 
+def max_pool_stem(pool, x):
+    """The stem's MaxPool2d(3, 2, 1): the HIP kernel pair for fp32 GPU maps (one-byte argmax,
+    gather backward), the module otherwise."""
+    if (x.is_cuda and x.dim() == 4 and x.dtype == torch.float32 and pool.kernel_size in (3, (3, 3))
+            and pool.stride in (2, (2, 2)) and pool.padding in (1, (1, 1)) and pool.dilation in (1, (1, 1))
+            and not pool.ceil_mode and os.environ.get('VFD_MAXPOOL', '1') != '0'):
+        from . import kernels as KN
+        return KN.MaxPool3s2.apply(x)
+    return pool(x)
+
+
 class BasicBlock(nn.Module):
     expansion = 1
 
@@ -201,7 +212,7 @@ class ResnetEncoder(nn.Module):
         e = self.encoder
         x = (image - 0.45) / 0.225
         f0 = bn_act(e.bn1, e.conv1(x))
-        f1 = e.layer1(e.maxpool(f0))
+        f1 = e.layer1(max_pool_stem(e.maxpool, f0))
         f2 = e.layer2(f1)
         f3 = e.layer3(f2)
         f4 = e.layer4(f3)

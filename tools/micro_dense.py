@@ -1,0 +1,76 @@
+"""Times the fused dense kernels against the ATen ops they replace, at the bench's shapes
+(config 2: 6 cameras, 384x640): stem max pool fwd/bwd, reflect pad fwd/bwd, align-corners
+upsample backward, BatchNorm+ReLU fwd/bwd.  Prints us/call and GB/s of the algorithmic bytes.
+
+    python tools/micro_dense.py
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+
+def timeit(fn, iters=20):
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / iters * 1e3
+
+
+def line(name, us, nbytes):
+    print(f'{name:44s} {us:8.1f} us  {nbytes / us / 1e3:8.1f} GB/s', flush=True)
+
+
+def main():
+    from vfdepth_amd import _lib as L
+    from vfdepth_amd import kernels as KN
+    torch.cuda.set_device(0)
+    lib = L.load()
+    dev = 'cuda:0'
+    x = torch.randn(6, 64, 192, 320, device=dev).relu_()
+    y = KN.MaxPool3s2.apply(x)
+    arg = torch.empty(y.shape, dtype=torch.uint8, device=dev)
+    g = torch.randn_like(y)
+    dx = torch.empty_like(x)
+    nb = x.numel() * 4 + y.numel() * 5
+    line('maxpool fwd (HIP)', timeit(lambda: lib.vfd_maxpool3s2_fwd(x.data_ptr(), y.data_ptr(), arg.data_ptr(), 384, 192, 320, L.stream())), nb)
+    line('maxpool bwd (HIP)', timeit(lambda: lib.vfd_maxpool3s2_bwd(g.data_ptr(), arg.data_ptr(), dx.data_ptr(), 384, 192, 320, L.stream())), nb)
+    yr, idx = F.max_pool2d(x, 3, 2, 1, return_indices=True)
+    line('maxpool fwd (ATen)', timeit(lambda: F.max_pool2d(x, 3, 2, 1, return_indices=True)), x.numel() * 4 + y.numel() * 12)
+    line('maxpool bwd (ATen)', timeit(lambda: torch.ops.aten.max_pool2d_with_indices_backward(g, x, [3, 3], [2, 2], [1, 1], [1, 1], False, idx)),
+         x.numel() * 4 + y.numel() * 12)
+    line('copy (reference stream)', timeit(lambda: dx.copy_(x)), x.numel() * 8)
+    for shape in ((6, 64, 96, 160), (6, 256, 24, 40), (6, 32, 192, 320)):
+        t = torch.randn(shape, device=dev)
+        n, c, h, w = shape
+        tp = torch.empty(n, c, h + 2, w + 2, device=dev)
+        nbp = (t.numel() + tp.numel()) * 4
+        line(f'reflect pad fwd {shape}', timeit(lambda: lib.vfd_reflect_pad1_fwd(t.data_ptr(), tp.data_ptr(), n * c, h, w, L.stream())), nbp)
+        line(f'reflect pad bwd {shape}', timeit(lambda: lib.vfd_reflect_pad1_bwd(tp.data_ptr(), t.data_ptr(), n * c, h, w, L.stream())), nbp)
+    d = torch.randn(6, 256, 48, 80, device=dev)
+    for hs, ws in ((24, 40), (12, 20), (6, 10)):
+        dl = torch.empty(6, 256, hs, ws, device=dev)
+        tmp = torch.empty(6 * 256 * 48 * ws, device=dev)
+        line(f'upsample bwd {hs}x{ws}', timeit(lambda: lib.vfd_upsample_ac_bwd(d.data_ptr(), dl.data_ptr(), tmp.data_ptr(), 6 * 256, 48, 80, hs, ws, L.stream())),
+             (d.numel() + dl.numel()) * 4)
+    for shape in ((6, 64, 192, 320), (6, 64, 96, 160), (6, 512, 12, 20)):
+        bn = torch.nn.BatchNorm2d(shape[1]).to(dev).train()
+        t = torch.randn(shape, device=dev, requires_grad=True)
+        from vfdepth_amd.layers import bn_act
+        out = bn_act(bn, t)
+        go = torch.randn_like(out)
+        line(f'bn+relu fwd {shape}', timeit(lambda: bn_act(bn, t)), t.numel() * 12)
+        line(f'bn+relu fwd+bwd {shape}', timeit(lambda: torch.autograd.grad(bn_act(bn, t), t, go)), t.numel() * 32)
+
+
+if __name__ == '__main__':
+    main()

@@ -103,10 +103,10 @@ __global__ __launch_bounds__(256) void up_ac_bwd_x_k(const float* __restrict__ g
   for (long long p = blockIdx.y; p < planes; p += gridDim.y) {
     const float* gr = g + (p * h + y) * w;
     float acc = 0.f;
-    for (int x = lo; x <= hi; ++x) {
-      const float wx = up_weight(ws, w, x, xs);
-      if (wx != 0.f) acc += wx * gr[x];
-    }
+    // unconditional loads (a zero weight adds nothing): a load behind the weight test waited for
+    // each candidate in turn
+#pragma unroll 4
+    for (int x = lo; x <= hi; ++x) acc += up_weight(ws, w, x, xs) * gr[x];
     tmp[p * h * ws + j] = acc;
   }
 }
@@ -122,10 +122,8 @@ __global__ __launch_bounds__(256) void up_ac_bwd_y_k(const float* __restrict__ t
   for (long long p = blockIdx.y; p < planes; p += gridDim.y) {
     const float* tp = tmp + p * h * ws + xs;
     float acc = 0.f;
-    for (int y = lo; y <= hi; ++y) {
-      const float wy = up_weight(hs, h, y, ys);
-      if (wy != 0.f) acc += wy * tp[(size_t)y * ws];
-    }
+#pragma unroll 4
+    for (int y = lo; y <= hi; ++y) acc += up_weight(hs, h, y, ys) * tp[(size_t)y * ws];
     dsrc[p * hs * ws + j] = acc;
   }
 }

@@ -26,35 +26,56 @@ struct VoxCam {
   bool valid;     // in front, inside the image, not self-occluded
 };
 
-// volumetric_fusionnet.py:132-140, 166-195
+// volumetric_fusionnet.py:132-140, 166-195, in two steps so a caller looping over the cameras can
+// put every camera's mask load in flight before it tests any: voxel_project (arithmetic only, the
+// nearest mask index) and voxel_finish (the validity test on the loaded mask value).
+struct VoxProj {
+  float ix, iy, z;
+  int ni;         // nearest mask index, -1 when out of range / non-finite
+  bool fin, oob;
+};
+
+__device__ __forceinline__ VoxProj voxel_project(const float* __restrict__ Kc, const float* __restrict__ Ei,
+                                                 float x, float y, float z, int h, int w) {
+  const float l0 = Ei[0] * x + Ei[1] * y + Ei[2] * z + Ei[3];
+  const float l1 = Ei[4] * x + Ei[5] * y + Ei[6] * z + Ei[7];
+  const float l2 = Ei[8] * x + Ei[9] * y + Ei[10] * z + Ei[11];
+  const float c0 = Kc[0] * l0 + Kc[1] * l1 + Kc[2] * l2;
+  const float c1 = Kc[4] * l0 + Kc[5] * l1 + Kc[6] * l2;
+  const float c2 = Kc[8] * l0 + Kc[9] * l1 + Kc[10] * l2;
+  const float den = c2 + 1e-8f;
+  const float u = c0 / den, v = c1 / den;
+  VoxProj p;
+  p.z = l2;
+  p.fin = finitef(u) && finitef(v);
+  const float gx = (u / (float)(w - 1) - 0.5f) * 2.f;
+  const float gy = (v / (float)(h - 1) - 0.5f) * 2.f;
+  p.ix = unnorm_ac(gx, w);
+  p.iy = unnorm_ac(gy, h);
+  p.oob = (gx > 1.f) || (gx < -1.f) || (gy > 1.f) || (gy < -1.f);
+  p.ni = p.fin ? nearest_index(p.ix, p.iy, w, h) : -1;
+  return p;
+}
+
+// mask index to load for a projection (element 0 when there is none; voxel_finish drops it)
+__device__ __forceinline__ int voxel_mask_index(const VoxProj& p) { return p.ni >= 0 ? p.ni : 0; }
+
+__device__ __forceinline__ VoxCam voxel_finish(const VoxProj& p, float occ_raw) {
+  VoxCam r;
+  r.z = p.z;
+  const float occ = p.ni >= 0 ? occ_raw : 0.f;
+  // non-finite: the reference clamps to +-2w (always out of range) or propagates NaN; both -> invalid
+  r.ix = p.fin ? p.ix : -1e9f;
+  r.iy = p.fin ? p.iy : -1e9f;
+  r.valid = p.fin && (occ > 0.5f) && (p.z > 0.f) && !p.oob;
+  return r;
+}
+
 __device__ __forceinline__ VoxCam voxel_to_camera(const float* __restrict__ Kc, const float* __restrict__ Ei,
                                                   float x, float y, float z,
                                                   const float* __restrict__ mlo, int h, int w) {
-  float l0 = Ei[0] * x + Ei[1] * y + Ei[2] * z + Ei[3];
-  float l1 = Ei[4] * x + Ei[5] * y + Ei[6] * z + Ei[7];
-  float l2 = Ei[8] * x + Ei[9] * y + Ei[10] * z + Ei[11];
-  float c0 = Kc[0] * l0 + Kc[1] * l1 + Kc[2] * l2;
-  float c1 = Kc[4] * l0 + Kc[5] * l1 + Kc[6] * l2;
-  float c2 = Kc[8] * l0 + Kc[9] * l1 + Kc[10] * l2;
-  float den = c2 + 1e-8f;
-  float u = c0 / den, v = c1 / den;
-  VoxCam r;
-  r.z = l2;
-  bool fin = finitef(u) && finitef(v);
-  if (!fin) {   // the reference clamps to +-2w (always out of range) or propagates NaN; both -> invalid
-    r.ix = r.iy = -1e9f;
-    r.valid = false;
-    return r;
-  }
-  float gx = (u / (float)(w - 1) - 0.5f) * 2.f;
-  float gy = (v / (float)(h - 1) - 0.5f) * 2.f;
-  r.ix = unnorm_ac(gx, w);
-  r.iy = unnorm_ac(gy, h);
-  bool oob = (gx > 1.f) || (gx < -1.f) || (gy > 1.f) || (gy < -1.f);
-  int ni = nearest_index(r.ix, r.iy, w, h);
-  float occ = ni >= 0 ? mlo[ni] : 0.f;
-  r.valid = (occ > 0.5f) && (l2 > 0.f) && !oob;
-  return r;
+  const VoxProj p = voxel_project(Kc, Ei, x, y, z, h, w);
+  return voxel_finish(p, mlo[voxel_mask_index(p)]);
 }
 
 // A valid (voxel, camera) pair as the gather/scatter loops need it.
@@ -580,10 +601,15 @@ __global__ __launch_bounds__(256) void fusion_plan_k(vfd_voxel_desc d, const flo
   int cnt = 0;
   if (v < V) {
     const float x = d.axis_x[v % d.X], y = d.axis_y[(v / d.X) % d.Y], z = d.axis_z[v / (d.X * d.Y)];
+    VoxProj pj[NC];
+    float occ[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) pj[c] = voxel_project(K + (b * NC + c) * 16, Einv + (b * NC + c) * 16, x, y, z, d.h, d.w);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) occ[c] = mlo[(size_t)(b * NC + c) * hw + voxel_mask_index(pj[c])];
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
-      const int bc = b * NC + c;
-      g[c] = voxel_to_camera(K + bc * 16, Einv + bc * 16, x, y, z, mlo + (size_t)bc * hw, d.h, d.w);
+      g[c] = voxel_finish(pj[c], occ[c]);
       val[c] = g[c].valid;
       cnt += val[c] ? 1 : 0;
     }
@@ -674,10 +700,15 @@ __global__ __launch_bounds__(256) void fuse_pose_fwd_k(vfd_voxel_desc d, const f
     float zsum = 0.f;
     if (v < V) {
       const float x = d.axis_x[v % d.X], y = d.axis_y[(v / d.X) % d.Y], z = d.axis_z[v / (d.X * d.Y)];
+      VoxProj pj[NC];
+      float occ[NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) pj[c] = voxel_project(K + (b * NC + c) * 16, Einv + (b * NC + c) * 16, x, y, z, d.h, d.w);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) occ[c] = mlo[(size_t)(b * NC + c) * hw + voxel_mask_index(pj[c])];
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
-        const int bc = b * NC + c;
-        const VoxCam g = voxel_to_camera(K + bc * 16, Einv + bc * 16, x, y, z, mlo + (size_t)bc * hw, d.h, d.w);
+        const VoxCam g = voxel_finish(pj[c], occ[c]);
         if (g.valid) {
           const Tap tp = make_tap(c, g, d.h, d.w);
           s_cam[t][cnt] = c;
@@ -868,23 +899,32 @@ __global__ __launch_bounds__(256) void plan_count_k(vfd_voxel_desc d, const Plan
 
 __global__ __launch_bounds__(PIDX_THREADS) void plan_scan_k(vfd_voxel_desc d, int* __restrict__ tile_cnt,
                                                             int* __restrict__ tile_ptr) {
-  __shared__ int part[PIDX_THREADS];
+  // exclusive scan of the bucket counts: wave prefix sums by lane shuffles + one cross-wave step
+  constexpr int NW = PIDX_THREADS / 64;
+  __shared__ int wsum[NW];
   const int nt = tiles_x(d) * tiles_y(d) * PSUB;     // (tile, sub-key) buckets
-  const int bc = blockIdx.x, t = threadIdx.x;
+  const int bc = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   int* cnt = tile_cnt + (size_t)bc * nt;
   const int chunk = (nt + PIDX_THREADS - 1) / PIDX_THREADS;
   const int c0 = min(nt, t * chunk), c1 = min(nt, c0 + chunk);
   int local = 0;
   for (int i = c0; i < c1; ++i) local += cnt[i];
-  part[t] = local;
-  __syncthreads();
-  for (int off = 1; off < PIDX_THREADS; off <<= 1) {
-    const int v = t >= off ? part[t - off] : 0;
-    __syncthreads();
-    part[t] += v;
-    __syncthreads();
+  int v = local;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int n = __shfl_up(v, off, 64);
+    if (lane >= off) v += n;
   }
-  int run = part[t] - local;
+  if (lane == 63) wsum[wv] = v;
+  __syncthreads();
+  int base = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < NW; ++k) {
+    const int sk = wsum[k];
+    base += k < wv ? sk : 0;
+    tot += sk;
+  }
+  int run = base + v - local;
   int* tp = tile_ptr + (size_t)bc * (nt + 1);
   for (int i = c0; i < c1; ++i) {
     const int c = cnt[i];
@@ -892,7 +932,7 @@ __global__ __launch_bounds__(PIDX_THREADS) void plan_scan_k(vfd_voxel_desc d, in
     cnt[i] = run;                 // becomes the fill cursor
     run += c;
   }
-  if (t == PIDX_THREADS - 1) tp[nt] = part[t];
+  if (t == PIDX_THREADS - 1) tp[nt] = tot;
 }
 
 __global__ __launch_bounds__(256) void plan_fill_k(vfd_voxel_desc d, const PlanEntry* __restrict__ plan,
@@ -1017,33 +1057,58 @@ constexpr int PBW_POOL = 8192;         // part slots of PT2 x POSE_MAXC floats (
 __global__ __launch_bounds__(1024) void plan_task_k(vfd_voxel_desc d, const int* __restrict__ tile_ptr,
                                                     int4* __restrict__ tasks, int4* __restrict__ combos,
                                                     int* __restrict__ ctrl) {
-  __shared__ int part[1024];
-  __shared__ int total;
+  // One workgroup: four exclusive scans over the (batch, camera, tile) list.  Scans are wave
+  // prefix sums by lane shuffles plus one cross-wave step (two barriers each), and a thread's
+  // tile ranges are read once into registers (the first version re-read them per pass and ran
+  // 1024-wide LDS scans: ~20 us of barriers and round trips for a few KB).
+  constexpr int TASK_T = 1024, TASK_W = TASK_T / 64, TASK_CACHE = 8;
+  __shared__ int wsum[TASK_W];
   const int nt = tiles_x(d) * tiles_y(d);
   const int M = d.B * d.N * nt;
-  const int t = threadIdx.x;
-  const int chunk = (M + 1023) / 1024;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int chunk = (M + TASK_T - 1) / TASK_T;
   const int c0 = min(M, t * chunk), c1 = min(M, c0 + chunk);
-  auto range = [&](int i, int& lo, int& hi) {
+  auto range_ld = [&](int i, int& lo, int& hi) {
     const int bc = i / nt, tile = i % nt;
     const int* tp = tile_ptr + (size_t)bc * (nt * PSUB + 1);
     lo = tp[tile * PSUB];
     hi = tp[(tile + 1) * PSUB];
   };
-  auto want = [](int n) { return n > PBW_SPLIT ? min(PBW_MAXS, (n + PBW_PART - 1) / PBW_PART) : 0; };
-  auto scan = [&](int local) {                     // exclusive prefix over threads; total -> `total`
-    __syncthreads();
-    part[t] = local;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {
-      const int v = t >= off ? part[t - off] : 0;
-      __syncthreads();
-      part[t] += v;
-      __syncthreads();
+  int clo[TASK_CACHE], chi[TASK_CACHE];
+#pragma unroll
+  for (int j = 0; j < TASK_CACHE; ++j)
+    if (c0 + j < c1) range_ld(c0 + j, clo[j], chi[j]);
+  auto range = [&](int i, int& lo, int& hi) {
+    const int j = i - c0;
+    if (j < TASK_CACHE) {
+#pragma unroll
+      for (int q = 0; q < TASK_CACHE; ++q)
+        if (q == j) { lo = clo[q]; hi = chi[q]; }
+    } else {
+      range_ld(i, lo, hi);
     }
-    if (t == 1023) total = part[t];
+  };
+  auto want = [](int n) { return n > PBW_SPLIT ? min(PBW_MAXS, (n + PBW_PART - 1) / PBW_PART) : 0; };
+  int total = 0;
+  auto scan = [&](int local) {                     // exclusive prefix over threads; sum -> `total`
+    int v = local;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int n = __shfl_up(v, off, 64);
+      if (lane >= off) v += n;
+    }
+    __syncthreads();                               // the previous scan's wsum reads are done
+    if (lane == 63) wsum[wv] = v;
     __syncthreads();
-    return part[t] - local;
+    int base = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < TASK_W; ++k) {
+      const int sk = wsum[k];
+      base += k < wv ? sk : 0;
+      tot += sk;
+    }
+    total = tot;
+    return base + v - local;
   };
   int lo, hi;
   // pass 0: pool slots wanted
@@ -1052,18 +1117,21 @@ __global__ __launch_bounds__(1024) void plan_task_k(vfd_voxel_desc d, const int*
   const int slot0 = scan(local);
   auto fits = [](int s, int sl) { return s > 0 && sl + s <= PBW_POOL; };
   // pass 1: split tiles (their slots fit the pool): parts and combine entries
-  int nsplit = 0;
+  int nsplit = 0, nwhole = 0;
   local = 0;
   for (int i = c0, sl = slot0; i < c1; ++i) {
     range(i, lo, hi);
     const int s = want(hi - lo);
-    if (fits(s, sl)) { local += s; ++nsplit; }
+    if (fits(s, sl)) { local += s; ++nsplit; } else { ++nwhole; }
     sl += s;
   }
   int run = scan(local);
   const int n_parts = total;
   int crun = scan(nsplit);
   const int n_combo = total;
+  int wrun = scan(nwhole);                         // pass 2 (whole tiles) goes after the parts
+  const int n_whole = total;
+  wrun += n_parts;
   for (int i = c0, sl = slot0; i < c1; ++i) {
     range(i, lo, hi);
     const int n = hi - lo, s = want(n);
@@ -1071,26 +1139,13 @@ __global__ __launch_bounds__(1024) void plan_task_k(vfd_voxel_desc d, const int*
       for (int p = 0; p < s; ++p)
         tasks[run++] = make_int4(i, lo + (int)((long long)n * p / s), lo + (int)((long long)n * (p + 1) / s), sl + p);
       combos[crun++] = make_int4(i, sl, s, 0);
+    } else {
+      tasks[wrun++] = make_int4(i, lo, hi, -1);
     }
     sl += s;
   }
-  // pass 2: whole tiles
-  local = 0;
-  for (int i = c0, sl = slot0; i < c1; ++i) {
-    range(i, lo, hi);
-    const int s = want(hi - lo);
-    if (!fits(s, sl)) local += 1;
-    sl += s;
-  }
-  run = n_parts + scan(local);
-  for (int i = c0, sl = slot0; i < c1; ++i) {
-    range(i, lo, hi);
-    const int s = want(hi - lo);
-    if (!fits(s, sl)) tasks[run++] = make_int4(i, lo, hi, -1);
-    sl += s;
-  }
   if (t == 0) {
-    ctrl[0] = n_parts + total;
+    ctrl[0] = n_parts + n_whole;
     ctrl[1] = n_combo;
   }
 }

@@ -19,23 +19,23 @@ __global__ __launch_bounds__(256) void maxpool_fwd_k(const float* __restrict__ x
   for (long long p = blockIdx.y; p < planes; p += gridDim.y) {
     const size_t i = (size_t)p * ho * wo + j;
     const float* xp = x + (size_t)p * h * w;
+    float v[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {                    // unconditional loads at clamped taps
+      const int yy = min(max(2 * oy - 1 + k / 3, 0), h - 1), xx = min(max(2 * ox - 1 + k % 3, 0), w - 1);
+      v[k] = xp[yy * w + xx];
+    }
     float best = -INFINITY;
     int bi = 4;                                      // centre (always inside the image)
     bool first = true;
 #pragma unroll
-    for (int ky = 0; ky < 3; ++ky) {
-      const int yy = 2 * oy - 1 + ky;
-      if (yy < 0 || yy >= h) continue;
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const int xx = 2 * ox - 1 + kx;
-        if (xx < 0 || xx >= w) continue;
-        const float v = xp[yy * w + xx];
-        if (first || v > best || isnan(v)) {
-          best = v;
-          bi = ky * 3 + kx;
-          first = false;
-        }
+    for (int k = 0; k < 9; ++k) {
+      const int yy = 2 * oy - 1 + k / 3, xx = 2 * ox - 1 + k % 3;
+      const bool ok = yy >= 0 && yy < h && xx >= 0 && xx < w;
+      if (ok && (first || v[k] > best || isnan(v[k]))) {
+        best = v[k];
+        bi = k;
+        first = false;
       }
     }
     y[i] = best;
@@ -43,27 +43,49 @@ __global__ __launch_bounds__(256) void maxpool_fwd_k(const float* __restrict__ x
   }
 }
 
+// One thread per 2x2 input block (rows 2i, 2i+1; columns 2j, 2j+1): the block's pixels are covered
+// by the output windows (i, j), (i, j+1), (i+1, j), (i+1, j+1) only (pixel 2i sits in window i's
+// centre row, pixel 2i+1 in window i's last row and window i+1's first), so 4 gradient and 4 index
+// loads serve 4 pixels; each pixel sums its winning windows in ATen's (row, column) order.
 __global__ __launch_bounds__(256) void maxpool_bwd_k(const float* __restrict__ g, const uint8_t* __restrict__ arg,
                                                      float* __restrict__ dx, long long planes, int h, int w, int ho,
                                                      int wo) {
+  const int hb = (h + 1) / 2, wb = (w + 1) / 2;
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= h * w) return;
-  const int yy = j / w, xx = j - yy * w;
-  // output rows / columns whose window (2o-1 .. 2o+1) contains the pixel, in increasing order:
-  // o in {p/2, p/2 + 1} (the second only for odd p)
-  const int oy0 = yy / 2, ox0 = xx / 2;
-  const bool y2 = (yy & 1) && oy0 + 1 < ho, x2 = (xx & 1) && ox0 + 1 < wo;
-  const int o00 = oy0 * wo + ox0;
-  const int k00 = (yy - 2 * oy0 + 1) * 3 + (xx - 2 * ox0 + 1);   // window position in (oy0, ox0)
+  if (j >= hb * wb) return;
+  const int bi = j / wb, bj = j - bi * wb;               // == output row / column of window (i, j)
+  const bool r1 = bi + 1 < ho, c1 = bj + 1 < wo;          // neighbouring windows exist
+  const int o = bi * wo + bj;
+  const int y0 = 2 * bi, x0 = 2 * bj;
+  const bool y1in = y0 + 1 < h, x1in = x0 + 1 < w;
   for (long long p = blockIdx.y; p < planes; p += gridDim.y) {
     const float* gp = g + (size_t)p * ho * wo;
     const uint8_t* ap = arg + (size_t)p * ho * wo;
-    float acc = 0.f;
-    if (ap[o00] == k00) acc += gp[o00];
-    if (x2 && ap[o00 + 1] == k00 - 2) acc += gp[o00 + 1];
-    if (y2 && ap[o00 + wo] == k00 - 6) acc += gp[o00 + wo];
-    if (y2 && x2 && ap[o00 + wo + 1] == k00 - 8) acc += gp[o00 + wo + 1];
-    dx[(size_t)p * h * w + j] = acc;
+    // unconditional loads at clamped offsets; windows past the edge get index 255 (never wins)
+    const int o01 = c1 ? o + 1 : o, o10 = r1 ? o + wo : o, o11 = (r1 && c1) ? o + wo + 1 : o;
+    const int l00 = ap[o], l01 = ap[o01], l10 = ap[o10], l11 = ap[o11];
+    const float g00 = gp[o], g01 = gp[o01], g10 = gp[o10], g11 = gp[o11];
+    const int a00 = l00, a01 = c1 ? l01 : 255, a10 = r1 ? l10 : 255, a11 = (r1 && c1) ? l11 : 255;
+    // window positions (ky * 3 + kx): pixel (2i, 2j) is (1,1) of (i,j); (2i, 2j+1) is (1,2) of
+    // (i,j) and (1,0) of (i,j+1); (2i+1, 2j) is (2,1) of (i,j) and (0,1) of (i+1,j); (2i+1, 2j+1)
+    // is (2,2) of (i,j), (2,0) of (i,j+1), (0,2) of (i+1,j) and (0,0) of (i+1,j+1)
+    float d00 = 0.f, d01 = 0.f, d10 = 0.f, d11 = 0.f;
+    if (a00 == 4) d00 += g00;
+    if (a00 == 5) d01 += g00;
+    if (a01 == 3) d01 += g01;
+    if (a00 == 7) d10 += g00;
+    if (a10 == 1) d10 += g10;
+    if (a00 == 8) d11 += g00;
+    if (a01 == 6) d11 += g01;
+    if (a10 == 2) d11 += g10;
+    if (a11 == 0) d11 += g11;
+    float* dp = dx + (size_t)p * h * w + (size_t)y0 * w + x0;
+    dp[0] = d00;
+    if (x1in) dp[1] = d01;
+    if (y1in) {
+      dp[w] = d10;
+      if (x1in) dp[w + 1] = d11;
+    }
   }
 }
 
@@ -89,7 +111,8 @@ int vfd_maxpool3s2_bwd(const float* g, const uint8_t* arg, float* dx, long long 
   vfd::ProfScope ps(vfd::K_MAXPOOL, s);
   const int ho = (h - 1) / 2 + 1, wo = (w - 1) / 2 + 1;
   const unsigned gy = (unsigned)(planes < 65535 ? planes : 65535);
-  vfd::maxpool_bwd_k<<<dim3((unsigned)((h * w + 255) / 256), gy), 256, 0, s>>>(g, arg, dx, planes, h, w, ho, wo);
+  const int nblk2 = ((h + 1) / 2) * ((w + 1) / 2);
+  vfd::maxpool_bwd_k<<<dim3((unsigned)((nblk2 + 255) / 256), gy), 256, 0, s>>>(g, arg, dx, planes, h, w, ho, wo);
   return vfd::fail_launch("maxpool3s2_bwd");
 }
 

@@ -13,6 +13,7 @@
 namespace vfd {
 
 constexpr int TS = 16;                  // tile side
+constexpr int PH_MAXI = 10;             // image slots 2T + F <= 2*3 + 4
 constexpr float C1 = 0.0001f;           // 0.01 ** 2
 constexpr float C2 = 0.0009f;           // 0.03 ** 2
 
@@ -91,20 +92,28 @@ __global__ __launch_bounds__(256) void photo_fwd_k(vfd_photo_desc d, const float
   const int H = d.H, W = d.W, HW = H * W;
   const int ty0 = bi.y * TS, tx0 = bi.x * TS;
   // ---- stage tiles (+1 reflect halo)
+  // every plane's value of an LDS position is loaded before any is stored, so the 3 + 3 n_img
+  // gathers of a thread are in flight together (a load -> store loop ran them as round trips)
   for (int i = threadIdx.x; i < PA; i += blockDim.x) {
     const int ly = i / PT, lx = i % PT;
     const int gy = min(reflect1(ty0 + ly - 1, H), H - 1), gx = min(reflect1(tx0 + lx - 1, W), W - 1);
     const size_t off = (size_t)gy * W + gx;
+    float v[3 + 3 * PH_MAXI];
 #pragma unroll
-    for (int ch = 0; ch < 3; ++ch) smem[ch * PA + i] = target[(br * 3 + ch) * HW + off];
-    for (int k = 0; k < n_img; ++k) {
+    for (int ch = 0; ch < 3; ++ch) v[ch] = target[(br * 3 + ch) * HW + off];
+#pragma unroll
+    for (int k = 0; k < PH_MAXI; ++k) {
+      const int kk = k < n_img ? k : 0;
       const float* src;
-      if (k < T) src = color + (((size_t)bn * T + k) * 3) * HW;
-      else if (k < 2 * T) src = d.ident[k - T] + (br * 3) * HW;
-      else src = ovl + (((size_t)bn * F + (k - 2 * T)) * 3) * HW;
+      if (kk < T) src = color + (((size_t)bn * T + kk) * 3) * HW;
+      else if (kk < 2 * T) src = d.ident[kk - T] + (br * 3) * HW;
+      else src = ovl + (((size_t)bn * F + (kk - 2 * T)) * 3) * HW;
 #pragma unroll
-      for (int ch = 0; ch < 3; ++ch) smem[(3 + 3 * k + ch) * PA + i] = src[(size_t)ch * HW + off];
+      for (int ch = 0; ch < 3; ++ch) v[3 + 3 * k + ch] = src[(size_t)ch * HW + off];
     }
+#pragma unroll
+    for (int k = 0; k < 3 + 3 * PH_MAXI; ++k)
+      if (k < 3 + 3 * n_img) smem[k * PA + i] = v[k];
   }
   __syncthreads();
   const int ly = threadIdx.x / TS + 1, lx = threadIdx.x % TS + 1;
@@ -264,39 +273,55 @@ __global__ __launch_bounds__(256) void photo_bwd_k(vfd_photo_desc d, const float
   const float* rmb = ref_mask + br * HW;
   const float* omb = omask + (size_t)bn * F * HW;
 
-  // dL/dphoto_k at real pixel (m, c) (0 outside the map)
-  auto gph_at = [&](int m) {
+  // All loads of a step (image row i, mask row i - 1) are unconditional at clamped addresses and
+  // sit in one basic block ahead of the arithmetic, so they are one memory round trip together
+  // (behind the row / selection branches they were three dependent ones, and a wave walks ~36 rows
+  // in sequence with only a few waves per SIMD to hide it).
+  const float* omp = F > 0 ? omb : rmb;                  // any readable plane when F == 0 (k < T)
+  auto step = [&](int i, PRow& nw, PRow& o1, PRow& o2) {
+    if (i > r1 + 1) return;
+    const int m = i - 1;
+    const size_t pm = (size_t)min(max(m, 0), H - 1) * W + cc;
+    const int sb = selb[pm];
+    const float rm = rmb[pm];
+    float om[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) om[j] = omp[(size_t)(F > 0 ? min(k == T ? 0 : 1 + j, F - 1) : 0) * HW + pm];
+    const int ri = min(max(i < 0 ? -i : (i > H - 1 ? 2 * (H - 1) - i : i), 0), H - 1);
+    const size_t roff = (size_t)ri * W + cr;
+    float pr_[3], tr_[3];
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+      pr_[ch] = P[(size_t)ch * HW + roff];
+      tr_[ch] = Tg[(size_t)ch * HW + roff];
+    }
+    // keep the loads here (the optimiser would sink each into the branch that reads it)
+    asm volatile("" ::"v"(sb), "v"(rm), "v"(om[0]), "v"(om[1]), "v"(om[2]));
+    asm volatile("" ::"v"(pr_[0]), "v"(pr_[1]), "v"(pr_[2]), "v"(tr_[0]), "v"(tr_[1]), "v"(tr_[2]));
+    // dL/dphoto_k at real pixel (m, c) (0 outside the map)
     float gph = 0.f;
     if (m >= 0 && m < H && col_in) {
-      const size_t pm = (size_t)m * W + cc;
-      const int sb = selb[pm];
-      const float rm = rmb[pm];
       const float am = ((sb & 4) ? 1.f : 0.f) * rm;
       if (k < T) {
         if ((sb & 3) == k) gph = gR * am;
       } else if (k == T) {
-        gph = gS * (rm * omb[pm]);
+        gph = gS * (rm * om[0]);
       } else if (((sb >> 3) & 3) == k - T - 1) {
         float mst = 0.f;
-        for (int ff = 0; ff < T; ++ff) {
-          const float pmv = rm * omb[(size_t)(1 + ff) * HW + pm] * am;
+#pragma unroll
+        for (int ff = 0; ff < 3; ++ff) {
+          if (ff >= T) break;
+          const float pmv = rm * om[ff] * am;
           mst = ff == 0 ? pmv : fmaxf(mst, pmv);
         }
         gph = gT * mst;
       }
     }
-    return gph;
-  };
-
-  auto step = [&](int i, PRow& nw, PRow& o1, PRow& o2) {
-    if (i > r1 + 1) return;
     // ---- (1) input row i of the reflect-padded images
     if (i >= -1 && i <= H) {
-      const int ri = i < 0 ? -i : (i > H - 1 ? 2 * (H - 1) - i : i);
-      const size_t off = (size_t)ri * W + cr;
 #pragma unroll
       for (int ch = 0; ch < 3; ++ch) {
-        const float p = P[(size_t)ch * HW + off], tv = Tg[(size_t)ch * HW + off];
+        const float p = pr_[ch], tv = tr_[ch];
         nw.p[ch] = p;
         nw.t[ch] = tv;
         const float pl = from_left(p), pr = from_right(p);
@@ -317,8 +342,6 @@ __global__ __launch_bounds__(256) void photo_bwd_k(vfd_photo_desc d, const float
     }
     // ---- (2) window centred at m = i - 1 -> coefficient sums of row m (slot o1)
     {
-      const int m = i - 1;
-      const float gph = gph_at(m);
       o1.g = gph;
 #pragma unroll
       for (int ch = 0; ch < 3; ++ch) {

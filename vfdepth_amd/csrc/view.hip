@@ -16,10 +16,7 @@
 
 namespace vfd {
 
-#ifndef VFD_VPPT
-#define VFD_VPPT 1
-#endif
-constexpr int VPPT = VFD_VPPT;   // pixels per thread in the reduction kernels
+constexpr int VPPT = 1;          // pixels per thread in the reduction kernels
 constexpr int VBLK = 256;
 
 struct WarpEntry {
@@ -66,43 +63,87 @@ struct WarpSample {
   Bilinear bl;
 };
 
-// reproject (geometry_util.py:66-81) + get_virtual_image (view_rendering.py:61-82)
-__device__ __forceinline__ WarpSample warp_sample(const float* __restrict__ Mw, const float* X,
-                                                  const float* __restrict__ img, const float* __restrict__ msk,
-                                                  int H, int W) {
+// A warp sample in three steps, so a kernel can put the gathers of several warps in flight before
+// it uses any of them (the gathers hit L2 / MALL; issued one by one behind branches they ran as
+// serial round trips):
+//   warp_geo    reproject (geometry_util.py:66-81) + grid_sample coordinates; no memory access
+//   warp_fetch  the 12 bilinear taps + the nearest mask value as unconditional loads (out-of-range
+//               and non-finite taps read element 0 and are dropped by warp_combine)
+//   warp_combine get_virtual_image (view_rendering.py:61-82): taps in fixed order, NaN -> 2.0, OOB mask
+struct WarpGeo {
+  float a, b, den, ix, iy;
+  Bilinear bl;
+  int ni;                // nearest tap, -1 when out of range / non-finite
+  bool oob;
+};
+
+struct WarpTex {
+  float v[3][4];         // channel x tap (nw, ne, sw, se)
+  float m;               // nearest mask value
+};
+
+__device__ __forceinline__ WarpGeo warp_geo(const float* __restrict__ Mw, const float* X, int H, int W) {
+  WarpGeo g;
+  g.a = Mw[0] * X[0] + Mw[1] * X[1] + Mw[2] * X[2] + Mw[3];
+  g.b = Mw[4] * X[0] + Mw[5] * X[1] + Mw[6] * X[2] + Mw[7];
+  const float c = Mw[8] * X[0] + Mw[9] * X[1] + Mw[10] * X[2] + Mw[11];
+  g.den = c + 1e-7f;
+  const float u = g.a / g.den, v = g.b / g.den;
+  const float gx = (u / (float)(W - 1) - 0.5f) * 2.f;
+  const float gy = (v / (float)(H - 1) - 0.5f) * 2.f;
+  g.ix = unnorm_ac(gx, W);
+  g.iy = unnorm_ac(gy, H);
+  g.bl = bilinear_taps(g.ix, g.iy, W, H);
+  g.ni = nearest_index(g.ix, g.iy, W, H);
+  g.oob = (gx > 1.f) || (gx < -1.f) || (gy > 1.f) || (gy < -1.f);
+  return g;
+}
+
+__device__ __forceinline__ void warp_fetch(const WarpGeo& g, const float* __restrict__ img,
+                                           const float* __restrict__ msk, int W, int HW, WarpTex& t) {
+  const int base = g.bl.y0 * W + g.bl.x0;
+  const int off[4] = {0, 1, W, W + 1};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int i = g.bl.in[k] ? base + off[k] : 0;
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) t.v[ch][k] = img[ch * HW + i];
+  }
+  t.m = msk[g.ni >= 0 ? g.ni : 0];
+}
+
+__device__ __forceinline__ WarpSample warp_combine(const WarpGeo& g, const WarpTex& t) {
   WarpSample s;
-  s.a = Mw[0] * X[0] + Mw[1] * X[1] + Mw[2] * X[2] + Mw[3];
-  s.b = Mw[4] * X[0] + Mw[5] * X[1] + Mw[6] * X[2] + Mw[7];
-  float c = Mw[8] * X[0] + Mw[9] * X[1] + Mw[10] * X[2] + Mw[11];
-  s.den = c + 1e-7f;
-  float u = s.a / s.den, v = s.b / s.den;
-  float gx = (u / (float)(W - 1) - 0.5f) * 2.f;
-  float gy = (v / (float)(H - 1) - 0.5f) * 2.f;
-  s.ix = unnorm_ac(gx, W);
-  s.iy = unnorm_ac(gy, H);
-  s.bl = bilinear_taps(s.ix, s.iy, W, H);
-  const int HW = H * W;
-  if (!s.bl.finite) {
+  s.a = g.a;
+  s.b = g.b;
+  s.den = g.den;
+  s.ix = g.ix;
+  s.iy = g.iy;
+  s.bl = g.bl;
+  if (!g.bl.finite) {
     s.img[0] = s.img[1] = s.img[2] = 2.f;   // NaN -> 2.0 (view_rendering.py:73-75)
     s.cm = 0.f;
     return s;
   }
-  const int base = s.bl.y0 * W + s.bl.x0;
 #pragma unroll
   for (int ch = 0; ch < 3; ++ch) {
-    const float* pl = img + ch * HW;
     float acc = 0.f;
-    if (s.bl.in[0]) acc += pl[base] * s.bl.w[0];
-    if (s.bl.in[1]) acc += pl[base + 1] * s.bl.w[1];
-    if (s.bl.in[2]) acc += pl[base + W] * s.bl.w[2];
-    if (s.bl.in[3]) acc += pl[base + W + 1] * s.bl.w[3];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc += g.bl.in[k] ? t.v[ch][k] * g.bl.w[k] : 0.f;
     s.img[ch] = acc;
   }
-  int ni = nearest_index(s.ix, s.iy, W, H);
-  float mv = ni >= 0 ? msk[ni] : 0.f;
-  bool oob = (gx > 1.f) || (gx < -1.f) || (gy > 1.f) || (gy < -1.f);
-  s.cm = (oob ? 0.f : 1.f) * mv;
+  const float mv = g.ni >= 0 ? t.m : 0.f;
+  s.cm = (g.oob ? 0.f : 1.f) * mv;
   return s;
+}
+
+__device__ __forceinline__ WarpSample warp_sample(const float* __restrict__ Mw, const float* X,
+                                                  const float* __restrict__ img, const float* __restrict__ msk,
+                                                  int H, int W) {
+  const WarpGeo g = warp_geo(Mw, X, H, W);
+  WarpTex t;
+  warp_fetch(g, img, msk, W, H * W, t);
+  return warp_combine(g, t);
 }
 
 template <typename T>
@@ -185,32 +226,42 @@ __global__ __launch_bounds__(VBLK) void view_stats_k(vfd_view_desc d, const floa
     const float s = wave_reduce_n<2>(v);
     if (lane < 2) out[(size_t)(d.n_warp * 8 + lane) * nrow] = s;
   }
-  for (int w = 0; w < d.n_warp; ++w) {
-    const WarpEntry e = warp_entry(d, cam, w);
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (e.src >= 0) {
-      const size_t sbn = (size_t)b * d.N + e.src;
-      const float* img = d.color[e.fslot] + sbn * 3 * HW;
-      const float* msk = mask + sbn * HW;
-      const float* Mw = M + ((size_t)bn * d.n_warp + w) * 12;
+  const bool live = pix[0] < HW;
+  for (int w0 = 0; w0 < d.n_warp; w0 += 2) {
+    // the gathers of two warps in flight together; a missing / unused warp reads camera 0
+    WarpEntry e[2];
+    WarpGeo g[2];
+    WarpTex t[2];
 #pragma unroll
-      for (int k = 0; k < VPPT; ++k) {
-        if (pix[k] >= HW) continue;
-        WarpSample s = warp_sample(Mw, X[k], img, msk, d.H, d.W);
-        const float mf = (rm[k] * s.cm) != 0.f ? 1.f : 0.f;
+    for (int j = 0; j < 2; ++j) {
+      const int w = w0 + j < d.n_warp ? w0 + j : w0;
+      e[j] = warp_entry(d, cam, w);
+      const int src = e[j].src >= 0 ? e[j].src : 0, fs = e[j].src >= 0 ? e[j].fslot : 0;
+      const size_t sbn = (size_t)b * d.N + src;
+      g[j] = warp_geo(M + ((size_t)bn * d.n_warp + w) * 12, X[0], d.H, d.W);
+      warp_fetch(g[j], d.color[fs] + sbn * 3 * HW, mask + sbn * HW, d.W, HW, t[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int w = w0 + j;
+      if (w >= d.n_warp) break;
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (e[j].src >= 0 && live) {
+        const WarpSample s = warp_combine(g[j], t[j]);
+        const float mf = (rm[0] * s.cm) != 0.f ? 1.f : 0.f;
         acc[0] += 3.f * mf;
 #pragma unroll
         for (int ch = 0; ch < 3; ++ch) {
           const float wv = s.img[ch];
           acc[1] += wv * mf;
-          acc[2] += rv[k][ch] * mf;
+          acc[2] += rv[0][ch] * mf;
           acc[3] += wv;
           acc[4] += wv * wv;
         }
       }
+      const float sm = wave_reduce_n<8>(acc);
+      if (lane < 8) out[(size_t)(w * 8 + lane) * nrow] = sm;
     }
-    const float s = wave_reduce_n<8>(acc);
-    if (lane < 8) out[(size_t)(w * 8 + lane) * nrow] = s;
   }
 }
 
@@ -338,42 +389,59 @@ __global__ __launch_bounds__(VBLK) void view_bwd_k(vfd_view_desc d, const float*
   for (int k = 0; k < VPPT; ++k) {
     pix[k] = bi.x * VBLK * VPPT + k * VBLK + threadIdx.x;
     dd[k] = 0.f;
-    if (pix[k] < HW) backproject(invK + bn * 16, depth[(size_t)bn * HW + pix[k]], pix[k] % d.W, pix[k] / d.W, X[k], ray[k]);
+    const int pk = pix[k] < HW ? pix[k] : 0;
+    backproject(invK + bn * 16, depth[(size_t)bn * HW + pk], pk % d.W, pk / d.W, X[k], ray[k]);
   }
-  for (int w = 0; w < d.n_warp; ++w) {
-    const WarpEntry e = warp_entry(d, cam, w);
-    float dM[16];
+  const bool live = pix[0] < HW;
+  const int pk = live ? pix[0] : 0;
+  constexpr int VB = 1;     // warps per batch (2 measured slower: 99 VGPRs cost occupancy)
+  for (int w0 = 0; w0 < d.n_warp; w0 += VB) {
+    // a warp's gathers (taps, mask, incoming gradient) in flight together
+    const float* gsrc[VB];
+    WarpGeo g[VB];
+    WarpTex t[VB];
+    float gv[VB][3];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) dM[i] = 0.f;
-    const float* gsrc = nullptr;
-    if (e.src >= 0) {
-      gsrc = e.oslot < 0 ? (g_color ? g_color + (((size_t)bn * T + w) * 3) * HW : nullptr)
-                         : (g_ovl ? g_ovl + (((size_t)bn * F + e.oslot) * 3) * HW : nullptr);
+    for (int j = 0; j < VB; ++j) {
+      const int w = w0 + j < d.n_warp ? w0 + j : w0;
+      const WarpEntry e = warp_entry(d, cam, w);
+      gsrc[j] = nullptr;
+      if (e.src >= 0)
+        gsrc[j] = e.oslot < 0 ? (g_color ? g_color + (((size_t)bn * T + w) * 3) * HW : nullptr)
+                              : (g_ovl ? g_ovl + (((size_t)bn * F + e.oslot) * 3) * HW : nullptr);
+      if (w0 + j >= d.n_warp) gsrc[j] = nullptr;
+      const int src = e.src >= 0 ? e.src : 0, fs = e.src >= 0 ? e.fslot : 0;
+      const size_t sbn = (size_t)b * d.N + src;
+      g[j] = warp_geo(M + ((size_t)bn * d.n_warp + w) * 12, X[0], d.H, d.W);
+      warp_fetch(g[j], d.color[fs] + sbn * 3 * HW, mask + sbn * HW, d.W, HW, t[j]);
+      const float* gp = gsrc[j] ? gsrc[j] : depth;   // any readable plane when unused
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) gv[j][ch] = gp[(gsrc[j] ? ch * HW : 0) + pk];
     }
-    if (gsrc) {
-      const size_t sbn = (size_t)b * d.N + e.src;
-      const float* img = d.color[e.fslot] + sbn * 3 * HW;
-      const float* Mw = M + ((size_t)bn * d.n_warp + w) * 12;
-      const float* cf = coef + ((size_t)bn * d.n_warp + w) * 4;
-      const bool norm = cf[1] >= 0.f;
 #pragma unroll
-      for (int k = 0; k < VPPT; ++k) {
-        if (pix[k] >= HW) continue;
-        WarpSample s = warp_sample(Mw, X[k], img, mask + sbn * HW, d.H, d.W);
-        if (!s.bl.finite) continue;
-        const int base = s.bl.y0 * d.W + s.bl.x0;
+    for (int j = 0; j < VB; ++j) {
+      const int w = w0 + j;
+      if (w >= d.n_warp) break;
+      float dM[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) dM[i] = 0.f;
+      if (gsrc[j] && live && g[j].bl.finite) {
+        const float* Mw = M + ((size_t)bn * d.n_warp + w) * 12;
+        const float* cf = coef + ((size_t)bn * d.n_warp + w) * 4;
+        const bool norm = cf[1] >= 0.f;
+        const WarpSample s = warp_combine(g[j], t[j]);
         const float x0 = floorf(s.ix), y0 = floorf(s.iy);
         const float x1 = x0 + 1.f, y1 = y0 + 1.f;
         float gix = 0.f, giy = 0.f;
 #pragma unroll
         for (int ch = 0; ch < 3; ++ch) {
-          float g = gsrc[ch * HW + pix[k]];
-          if (norm) g = g * s.cm * cf[3] / (cf[1] + 1e-8f);
-          const float* pl = img + ch * HW;
-          if (s.bl.in[0]) { float v = pl[base]; gix -= v * (y1 - s.iy) * g; giy -= v * (x1 - s.ix) * g; }
-          if (s.bl.in[1]) { float v = pl[base + 1]; gix += v * (y1 - s.iy) * g; giy -= v * (s.ix - x0) * g; }
-          if (s.bl.in[2]) { float v = pl[base + d.W]; gix -= v * (s.iy - y0) * g; giy += v * (x1 - s.ix) * g; }
-          if (s.bl.in[3]) { float v = pl[base + d.W + 1]; gix += v * (s.iy - y0) * g; giy += v * (s.ix - x0) * g; }
+          float gg = gv[j][ch];
+          if (norm) gg = gg * s.cm * cf[3] / (cf[1] + 1e-8f);
+          const float* v = t[j].v[ch];
+          if (s.bl.in[0]) { gix -= v[0] * (y1 - s.iy) * gg; giy -= v[0] * (x1 - s.ix) * gg; }
+          if (s.bl.in[1]) { gix += v[1] * (y1 - s.iy) * gg; giy -= v[1] * (s.ix - x0) * gg; }
+          if (s.bl.in[2]) { gix -= v[2] * (s.iy - y0) * gg; giy += v[2] * (x1 - s.ix) * gg; }
+          if (s.bl.in[3]) { gix += v[3] * (s.iy - y0) * gg; giy += v[3] * (s.ix - x0) * gg; }
         }
         // grid_sampler unnormalise -> (u/(W-1) - 0.5)*2 -> a/den
         const float dgx = gix * ((float)(d.W - 1) / 2.f);
@@ -382,21 +450,21 @@ __global__ __launch_bounds__(VBLK) void view_bwd_k(vfd_view_desc d, const float*
         const float dv = dgy * 2.f / (float)(d.H - 1);
         const float da = du / s.den, db = dv / s.den;
         const float dden = -(du * s.a + dv * s.b) / (s.den * s.den);
-        const float Xh[4] = {X[k][0], X[k][1], X[k][2], 1.f};
+        const float Xh[4] = {X[0][0], X[0][1], X[0][2], 1.f};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          dM[j] += da * Xh[j];
-          dM[4 + j] += db * Xh[j];
-          dM[8 + j] += dden * Xh[j];
+        for (int q = 0; q < 4; ++q) {
+          dM[q] += da * Xh[q];
+          dM[4 + q] += db * Xh[q];
+          dM[8 + q] += dden * Xh[q];
         }
-        float dX0 = da * Mw[0] + db * Mw[4] + dden * Mw[8];
-        float dX1 = da * Mw[1] + db * Mw[5] + dden * Mw[9];
-        float dX2 = da * Mw[2] + db * Mw[6] + dden * Mw[10];
-        dd[k] += dX0 * ray[k][0] + dX1 * ray[k][1] + dX2 * ray[k][2];
+        const float dX0 = da * Mw[0] + db * Mw[4] + dden * Mw[8];
+        const float dX1 = da * Mw[1] + db * Mw[5] + dden * Mw[9];
+        const float dX2 = da * Mw[2] + db * Mw[6] + dden * Mw[10];
+        dd[0] += dX0 * ray[0][0] + dX1 * ray[0][1] + dX2 * ray[0][2];
       }
+      const float sm = wave_reduce_n<16>(dM);
+      if (lane < 12) partial[(((size_t)bn * d.n_warp + w) * 16 + lane) * nrow + row] = sm;
     }
-    const float sm = wave_reduce_n<16>(dM);
-    if (lane < 12) partial[(((size_t)bn * d.n_warp + w) * 16 + lane) * nrow + row] = sm;
   }
 #pragma unroll
   for (int k = 0; k < VPPT; ++k)

@@ -38,6 +38,11 @@ OPS = {
     'pad_conv_fwd': ['ppc_main_k', 'ppc_reduce_k'],
     'depth_syn_fwd': ['depth_syn_fwd_k'],
     'depth_syn_bwd': ['depth_syn_bwd_k'],
+    'bn_fwd': ['bn_stats_k', 'bn_sum_k', 'bn_apply_k'],
+    'bn_bwd': ['bn_bwd_stats_k', 'bn_bwd_apply_k'],
+    'reflect_pad': ['reflect_pad_fwd_k', 'reflect_pad_bwd_k', 'lrelu_pad_bwd_nhwc_k'],
+    'upsample_bwd': ['up_ac_bwd_x_k', 'up_ac_bwd_y_k'],
+    'maxpool': ['maxpool_fwd_k', 'maxpool_bwd_k'],
 }
 
 

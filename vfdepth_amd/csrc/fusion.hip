@@ -1710,6 +1710,10 @@ __global__ __launch_bounds__(256) void voxel_project_fwd_k(vfd_voxel_desc d, con
 #define VFD_VPB_PQ 8
 #endif
 constexpr int VB_X = 8, VB_Y = 4;                  // voxel tile (one z layer) per wave task
+#ifndef VFD_VPB_LG
+#define VFD_VPB_LG 2          // 4 and 5 measured slower (219, 263 us vs 209 us at config 2)
+#endif
+constexpr int VB_LG = VFD_VPB_LG;                  // voxel layers (waves) per workgroup task
 constexpr int VB_RY = VB_Y + 1, VB_NSEG = 2 * VB_RY;   // cell rows per layer, entry ranges per tile
 #ifndef VFD_VPB_S
 #define VFD_VPB_S 1024
@@ -1729,8 +1733,33 @@ __host__ __device__ __forceinline__ VpbGeom vpb_geom(const vfd_voxel_desc& d) {
   g.ncell = g.CX * g.CY * g.CZ;
   g.nbx = (d.X + VB_X - 1) / VB_X;
   g.nby = (d.Y + VB_Y - 1) / VB_Y;
-  g.ntile = g.nbx * g.nby * ((d.Z + 1) / 2);
+  g.ntile = g.nbx * g.nby * ((d.Z + VB_LG - 1) / VB_LG);
   return g;
+}
+
+// Tile tl of a batch -> brick origin (xb, yb) and layer pair zp.  Layer pairs are the fastest
+// index: the tasks of one brick column are consecutive, so (with vpb_main_k's per-XCD task
+// ranges) neighbouring layer pairs run at about the same time on one XCD and the cell layer each
+// pair shares with the next (2 zp + 1) is fetched into that XCD's L2 once.
+#ifndef VFD_VPB_ZFAST
+#define VFD_VPB_ZFAST 1
+#endif
+#ifndef VFD_VPB_XCDQ
+#define VFD_VPB_XCDQ 0          // 1: per-XCD task ranges + stealing, 2: static per XCD (both measured slower)
+#endif
+__device__ __forceinline__ void vpb_tile_pos(const vfd_voxel_desc& d, const VpbGeom& g, int tl, int* xb, int* yb,
+                                             int* zp) {
+#if VFD_VPB_ZFAST
+  const int nzp = (d.Z + VB_LG - 1) / VB_LG;
+  *zp = tl % nzp;
+  const int r = tl / nzp;
+  *xb = (r % g.nbx) * VB_X;
+  *yb = (r / g.nbx) * VB_Y;
+#else
+  *xb = (tl % g.nbx) * VB_X;
+  *yb = ((tl / g.nbx) % g.nby) * VB_Y;
+  *zp = tl / (g.nbx * g.nby);
+#endif
 }
 
 // continuous grid coordinates of a frustum sample (the first half of frustum_sample)
@@ -2001,17 +2030,18 @@ __global__ __launch_bounds__(256) void vpb_fold_zero_k(vfd_voxel_desc d, const f
   }
   const int tile = blk - nf;
   if (tile >= nb) {
-    if (threadIdx.x == 0) ctrl[1] = 0;
+    if (threadIdx.x < 8) ctrl[8 + threadIdx.x] = 0;    // vpb_main_k's per-XCD work counters
     return;
   }
   if (parts[tile] <= 1) return;
   const VpbGeom g = vpb_geom(d);
   const int b = tile / g.ntile, tl = tile % g.ntile;
-  const int xb = (tl % g.nbx) * VB_X, yb = ((tl / g.nbx) % g.nby) * VB_Y, zp = tl / (g.nbx * g.nby);
+  int xb, yb, zp;
+  vpb_tile_pos(d, g, tl, &xb, &yb, &zp);
   const int V = d.X * d.Y * d.Z;
   constexpr int QPV = CV / 4;
-  for (int i = threadIdx.x; i < 2 * VB_X * VB_Y * QPV; i += blockDim.x) {
-    const int q = i % QPV, v = (i / QPV) % (VB_X * VB_Y), zl = 2 * zp + i / (QPV * VB_X * VB_Y);
+  for (int i = threadIdx.x; i < VB_LG * VB_X * VB_Y * QPV; i += blockDim.x) {
+    const int q = i % QPV, v = (i / QPV) % (VB_X * VB_Y), zl = VB_LG * zp + i / (QPV * VB_X * VB_Y);
     const int x = xb + v % VB_X, y = yb + v / VB_X;
     if (x < d.X && y < d.Y && zl < d.Z)
       reinterpret_cast<float4*>(dvox + ((size_t)b * V + (zl * d.Y + y) * d.X + x) * CV)[q] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -2032,11 +2062,16 @@ __device__ __forceinline__ void vpb_segment(const vfd_voxel_desc& d, const VpbGe
   *s1 = vpb_ptr(ptr, boff, n, base + min(xb + VB_X, d.X) + 1);
 }
 
-// Entry range k (< VB_NSEG) of the wave for layer zl = 2 zp + w of a layer-pair tile: the cell
-// layer both waves share (z0 = 2 zp) comes first, so the pair reads those rows at the same time
-// (one L1/L2 fetch), then the wave's own outer layer (2 zp - 1 or 2 zp + 1).
+// Entry range k (< VB_NSEG) of the wave for layer zl = VB_LG zp + w of a layer-group tile: the
+// cell layers of zl are z0 = zl - 1 (its samples weigh in with dz = 1) and z0 = zl (dz = 0); each
+// is shared with a neighbouring wave.  Even waves read z0 = zl first, odd waves z0 = zl - 1 first,
+// so waves (2k, 2k+1) read their shared layer in their first halves and (2k+1, 2k+2) in their
+// second halves: roughly at the same time, one L2 fetch for both.  Inside a group a cell layer is
+// fetched once, so a group of VB_LG layers reads VB_LG + 1 cell layers.
 __device__ __forceinline__ int vpb_seg_z0(int zp, int w, int k) {
-  return k < VB_RY ? 2 * zp : (w == 0 ? 2 * zp - 1 : 2 * zp + 1);
+  const int zl = VB_LG * zp + w;
+  const bool own_first = (w & 1) == 0;
+  return (k < VB_RY) == own_first ? zl : zl - 1;
 }
 
 // per layer-pair tile: samples of each layer's wave -> number of parts (split tiles are zeroed by
@@ -2046,20 +2081,24 @@ __global__ __launch_bounds__(64) void vpb_tile_k(vfd_voxel_desc d, const int* __
   const VpbGeom g = vpb_geom(d);
   const int tile = blockIdx.x, lane = threadIdx.x;
   const int b = tile / g.ntile, tl = tile % g.ntile;
-  const int xb = (tl % g.nbx) * VB_X, yb = ((tl / g.nbx) % g.nby) * VB_Y, zp = tl / (g.nbx * g.nby);
-  int n0 = 0, n1 = 0;
-  if (lane < 2 * VB_NSEG) {
+  int xb, yb, zp;
+  vpb_tile_pos(d, g, tl, &xb, &yb, &zp);
+  static_assert(VB_LG * VB_NSEG <= 64, "one lane per entry range");
+  int n = 0, wl = -1;
+  if (lane < VB_LG * VB_NSEG) {
     const int w = lane / VB_NSEG, k = lane % VB_NSEG;
-    if (2 * zp + w < d.Z) {
+    if (VB_LG * zp + w < d.Z) {
       int s0, s1;
       vpb_segment(d, g, ptr, boff, b, vpb_seg_z0(zp, w, k), yb - 1 + k % VB_RY, xb, &s0, &s1);
-      (w == 0 ? n0 : n1) = s1 - s0;
+      n = s1 - s0;
+      wl = w;
     }
   }
-  n0 = wave_sum(n0);
-  n1 = wave_sum(n1);
+  int nmax = 0;
+#pragma unroll
+  for (int w = 0; w < VB_LG; ++w) nmax = max(nmax, wave_sum(wl == w ? n : 0));
   // deterministic mode: no split tiles (their parts would add with atomics)
-  const int np = d.deterministic ? 1 : max(1, (max(n0, n1) + VB_S - 1) / VB_S);
+  const int np = d.deterministic ? 1 : max(1, (nmax + VB_S - 1) / VB_S);
   if (lane == 0) parts[tile] = np;
 }
 
@@ -2086,22 +2125,20 @@ __global__ __launch_bounds__(1024) void vpb_tasks_k(const int* __restrict__ part
     for (int q = 0; q < np; ++q) tasks[run + q] = make_int2(i, q | (np << 16));
     run += np;
   }
-  if (t == 1023) {
-    ctrl[0] = part[t];       // tasks
-    ctrl[1] = 0;             // work counter of vpb_main_k
-  }
+  if (t == 1023) ctrl[0] = part[t];                 // tasks
+  if (t < 8) ctrl[8 + t] = 0;                         // per-XCD work counters of vpb_main_k
 }
 
 // One wave = one independent worker: it takes tile tasks from the counter, accumulates its tile
 // in a private 16 KB LDS slab and writes it out (plain stores, or atomics for split tiles).
 template <int CV>
-__global__ __launch_bounds__(128) void vpb_main_k(vfd_voxel_desc d, const int* __restrict__ ptr,
+__global__ __launch_bounds__(64 * VB_LG) void vpb_main_k(vfd_voxel_desc d, const int* __restrict__ ptr,
                                                   const int* __restrict__ boff, const float4* __restrict__ entries,
                                                   const int2* __restrict__ tasks, int* __restrict__ ctrl,
                                                   const float* __restrict__ dout, const float* __restrict__ fbz,
                                                   float* __restrict__ dvox) {
   constexpr int LAYER = VB_Y * VB_X * 64;
-  __shared__ float lacc_l[2][LAYER + 64];          // per wave: its layer + one scratch row (masked corners)
+  __shared__ float lacc_l[VB_LG][LAYER + 64];      // per wave: its layer + one scratch row (masked corners)
   __shared__ int task_l;
   const VpbGeom g = vpb_geom(d);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -2110,18 +2147,47 @@ __global__ __launch_bounds__(128) void vpb_main_k(vfd_voxel_desc d, const int* _
   const int ntask = ctrl[0];
   float* lacc = lacc_l[wv];
   float* trash = lacc + LAYER;
-  for (;;) {
+  // Work queues: the task list is cut into 8 contiguous ranges, one per XCD (workgroups are dealt
+  // round-robin to the XCDs, so blockIdx % 8 names this one's); a worker drains its XCD's range in
+  // order, then steals from the others.  Counters past a range's end are harmless.
+  const int xcd = blockIdx.x & 7;
+  for (int iter = 0;; ++iter) {
     __syncthreads();
-    if (threadIdx.x == 0) task_l = atomicAdd(ctrl + 1, 1);
+    if (threadIdx.x == 0) {
+      int tk = -1;
+#if VFD_VPB_XCDQ == 0
+      tk = atomicAdd(ctrl + 8, 1);
+      if (tk >= ntask) tk = -1;
+#elif VFD_VPB_XCDQ == 2
+      {   // static: this XCD's range, round-robin over its workgroups (no atomics)
+        const int lo = (int)((long long)ntask * xcd / 8), hi = (int)((long long)ntask * (xcd + 1) / 8);
+        const int i = lo + (int)(blockIdx.x >> 3) + iter * (int)(gridDim.x >> 3);
+        tk = i < hi ? i : -1;
+      }
+#else
+      for (int k = 0; k < 8; ++k) {
+        const int qq = (xcd + k) & 7;
+        const int lo = (int)((long long)ntask * qq / 8), hi = (int)((long long)ntask * (qq + 1) / 8);
+        if (lo >= hi) continue;
+        const int i = atomicAdd(ctrl + 8 + qq, 1);
+        if (lo + i < hi) {
+          tk = lo + i;
+          break;
+        }
+      }
+#endif
+      task_l = tk;
+    }
     for (int i = lane; i < LAYER / 4; i += 64) reinterpret_cast<float4*>(lacc)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     __syncthreads();
     const int t = task_l;
-    if (t >= ntask) break;
+    if (t < 0) break;
     const int2 tk = tasks[t];
     const int tile = tk.x, part = tk.y & 0xFFFF, np = tk.y >> 16;
     const int b = tile / g.ntile, tl = tile % g.ntile;
-    const int xb = (tl % g.nbx) * VB_X, yb = ((tl / g.nbx) % g.nby) * VB_Y, zp = tl / (g.nbx * g.nby);
-    const int zl = 2 * zp + wv;                      // this wave's voxel layer
+    int xb, yb, zp;
+    vpb_tile_pos(d, g, tl, &xb, &yb, &zp);
+    const int zl = VB_LG * zp + wv;                  // this wave's voxel layer
     if (zl < d.Z) {
       // the wave's entry ranges (lanes 0 .. VB_NSEG-1) and their running offsets
       int s0 = 0, s1 = 0;
@@ -2545,7 +2611,7 @@ static VpbWs vpb_ws(const vfd_voxel_desc* d) {
   w.parts = w.entries + al(nS * 16);
   w.tasks = w.parts + al(nb * 4);
   w.ctrl = w.tasks + al(ntask_max * 8);
-  w.total = w.ctrl + al(2 * 4);
+  w.total = w.ctrl + al(16 * 4);
   return w;
 }
 
@@ -2618,7 +2684,7 @@ static void vpb_bwd_launch(const vfd_voxel_desc* d, const float* d_out, void* ws
 #define VPB_LAUNCH(CVV)                                                                                         \
   case CVV:                                                                                                     \
     vpb_fold_zero_k<CVV><<<nf + nb + 1, 256, 0, s>>>(*d, d_out, p.fb, nf, p.parts, nb, p.ctrl, d_vox);            \
-    vpb_main_k<CVV><<<VPB_WORKERS / 2, 128, 0, s>>>(*d, p.ptr, p.boff, p.entries, p.tasks, p.ctrl, d_out, p.zrow, \
+    vpb_main_k<CVV><<<VPB_WORKERS / VB_LG, 64 * VB_LG, 0, s>>>(*d, p.ptr, p.boff, p.entries, p.tasks, p.ctrl, d_out, p.zrow, \
                                                      d_vox);                                                    \
     break;
     VPB_LAUNCH(8)

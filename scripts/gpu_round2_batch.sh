@@ -1,10 +1,14 @@
 #!/bin/bash
+# Round-end validation: the whole -m gpu suite, smoke, the default bench (cpu baseline + parity),
+# a kernel-trace profile and PMC traffic passes.
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
-K="voxel or proj or full_step or deterministic" bash scripts/gpu_tests.sh tests/test_gpu_parity.py tests/test_gpu_fullsize.py || exit 1
-cp gpurun_out/tests/tests.log gpurun_out/tests_t.log
-bash scripts/gpu_bench.sh r2_vpb --steps 20 --no-cpu-baseline --no-parity || exit 1
+bash scripts/gpu_tests.sh tests/test_gpu_ddp.py || exit 1
+cp gpurun_out/tests/tests.log gpurun_out/tests_full.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke.log 2>&1 || exit 1
+timeout -k 10 600 python bench.py --kernel-table > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err || exit 1
+bash scripts/gpu_profile.sh r2final || exit 1
 OUT=$GRAFT_REPO_ROOT/gpurun_out/traffic
 mkdir -p $OUT
 cd /tmp

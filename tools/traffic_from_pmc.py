@@ -44,6 +44,14 @@ OPS = {
     'upsample_bwd': ['up_ac_bwd_x_k', 'up_ac_bwd_y_k'],
     'maxpool': ['maxpool_fwd_k', 'maxpool_bwd_k'],
 }
+# Ops timed as several separate C-ABI calls (one ProfScope each, the bench's launch unit): the
+# traffic is per call of any of these kernels, not per launch of the first one.
+ENTRY = {
+    'bn_fwd': ['bn_stats_k', 'bn_apply_k'],
+    'bn_bwd': ['bn_bwd_stats_k', 'bn_bwd_apply_k'],
+    'reflect_pad': ['reflect_pad_fwd_k', 'reflect_pad_bwd_k', 'lrelu_pad_bwd_nhwc_k'],
+    'maxpool': ['maxpool_fwd_k', 'maxpool_bwd_k'],
+}
 
 
 def kernel_of(name):
@@ -69,11 +77,12 @@ def main():
                      'source': 'rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes'}}
     for op, ks in OPS.items():
         ks = [k for k in ks if k in fetch]          # kernels this build actually launches
-        n = len(fetch.get(ks[0], [])) if ks else 0
+        entry = ENTRY.get(op, ks[:1])
+        n = sum(len(fetch.get(k, [])) for k in entry)
         if not n:
             continue
         f = sum(sum(fetch.get(k, [])) for k in ks) / n
-        w = sum(sum(write.get(k, [])) for k in ks) / max(len(write.get(ks[0], [])), 1)
+        w = sum(sum(write.get(k, [])) for k in ks) / max(sum(len(write.get(k, [])) for k in entry), 1)
         out[op] = round((2.0 * f + w) * 1024)
         out['_meta'][op] = {'fetch_kib': round(f, 1), 'write_kib': round(w, 1), 'launches': n}
     json.dump(out, sys.stdout, indent=1)

@@ -219,3 +219,28 @@ PARAM_GRADS = ['depth_net.decoder.decoder.0.0.weight', 'depth_net.fusion_net.con
                'depth_net.conv1x1.0.bias', 'pose_net.pose_decoder.net.3.weight',
                'pose_net.fusion_net.reduce_dim.0.bias', 'pose_net.conv1x1.0.bias',
                'depth_net.depth_decoder.decoder.10.conv.conv.weight', 'pose_net.pose_decoder.net.3.bias']
+
+
+# ------------------------------------------------------------------------------------ data path
+def data_align_case():
+    """A stacked 6-camera sample as the reference's DDAD/NuScenes readers hand it to
+    `align_dataset` (after the per-camera transforms and `stack_sample`): seeded images 40x64
+    (augmented + original, contexts -1 / +1), intrinsics [6,3,3] float64 with a skew term and
+    an off-centre principal point, extrinsics; plus a 97x151 'L' mask image for
+    `transform_mask_sample`."""
+    import numpy as np
+    import PIL.Image as pil
+    gen = torch.Generator().manual_seed(77)
+    N, H, W = 6, 40, 64
+    rgb = torch.rand(N, 3, H, W, generator=gen)
+    org = torch.rand(N, 3, H, W, generator=gen)
+    ctx = [torch.rand(N, 3, H, W, generator=gen) for _ in range(2)]
+    ctx_o = [torch.rand(N, 3, H, W, generator=gen) for _ in range(2)]
+    K = np.zeros((N, 3, 3))
+    for c in range(N):
+        K[c] = [[50.0 + 3 * c, 0.25 * c, 31.5 + c], [0.0, 48.0 + 2 * c, 19.25 - c], [0.0, 0.0, 1.0]]
+    sample = {'rgb': rgb, 'rgb_original': org, 'rgb_context': ctx, 'rgb_context_original': ctx_o,
+              'intrinsics': K, 'extrinsics': np.stack([np.eye(4)] * N), 'contexts': [-1, 1],
+              'splitname': 'train_0000000000'}
+    m = (torch.rand(97, 151, generator=gen) * 255).to(torch.uint8).numpy()
+    return sample, pil.fromarray(m, 'L'), [-1, 1], np.arange(4)

@@ -135,6 +135,41 @@ def load_logger():
     return mod
 
 
+def load_data_util():
+    """The reference's `dataset/data_util.py` (align_dataset, transform_mask_sample).
+
+    Its module-level `import torchvision.transforms` names an absent package: a stand-in whose
+    `Resize` / `ToTensor` are the plain PIL / numpy operations torchvision performs on PIL images,
+    and Pillow >= 10 no longer has `ANTIALIAS` (it was always an alias of `LANCZOS`), so the alias
+    is restored before the file runs.  `align_dataset` itself uses only numpy and F.interpolate."""
+    if 'data_util' in _LOADED:
+        return _LOADED['data_util']
+    import numpy as np
+    import PIL.Image as pil
+    if not hasattr(pil, 'ANTIALIAS'):
+        pil.ANTIALIAS = pil.LANCZOS
+    tv = _pkg('torchvision')
+    trm = _register('torchvision.transforms', types.ModuleType('torchvision.transforms'))
+
+    class Resize:
+        def __init__(self, size, interpolation=pil.BILINEAR):
+            self.size, self.interpolation = size, interpolation
+
+        def __call__(self, img):
+            return img.resize((self.size[1], self.size[0]), self.interpolation)
+
+    class ToTensor:
+        def __call__(self, img):
+            a = np.asarray(img)
+            a = a[:, :, None] if a.ndim == 2 else a
+            return torch.from_numpy(a.transpose(2, 0, 1).copy()).float().div(255.0)
+    trm.Resize, trm.ToTensor = Resize, ToTensor
+    tv.transforms = trm
+    mod = _load('ref_dataset_data_util', 'dataset/data_util.py')
+    _LOADED['data_util'] = mod
+    return mod
+
+
 def reference_depth_losses(cfg, inputs, outputs):
     """`Logger(cfg, use_tb=False).compute_depth_losses(inputs, outputs)` of the reference, with
     the log directory redirected to a temporary one (the constructor creates it)."""

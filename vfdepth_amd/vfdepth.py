@@ -90,12 +90,22 @@ class VFDepthAlgo:
                                 broadcast_buffers=self.world_size > 1)
         return models
 
+    def _dataset(self, cfg, mode, with_depth):
+        """The on-disk DDAD / NuScenes reader (`data.construct_dataset`, base_dataset.py:5-50) when
+        `data.data_path` names a dataset, else the synthetic DDAD-shaped generator."""
+        if str(cfg['data'].get('data_path', 'synthetic')) != 'synthetic':
+            from .data import augmentation, construct_dataset
+            return construct_dataset(cfg, 'train' if mode == 'train' else 'val', **augmentation(cfg, mode))
+        if mode == 'val':
+            return SyntheticSurroundDataset(cfg, length=8, seed=7, with_depth=True)
+        return SyntheticSurroundDataset(cfg, with_depth=with_depth)
+
     def prepare_dataset(self, cfg, rank):
         if self.mode == 'eval' or cfg['model'].get('mode') == 'eval':
-            self._dataloaders['eval'] = DataLoader(SyntheticSurroundDataset(cfg, with_depth=True),
+            self._dataloaders['eval'] = DataLoader(self._dataset(cfg, 'eval', True),
                                                    batch_size=self.eval_batch_size, shuffle=False, drop_last=True)
             return
-        ds = SyntheticSurroundDataset(cfg, with_depth=False)
+        ds = self._dataset(cfg, 'train', False)
         opts = {'batch_size': self.batch_size, 'shuffle': not self.ddp_enable, 'num_workers': self.num_workers,
                 'pin_memory': True, 'drop_last': True}
         if self.ddp_enable:
@@ -106,7 +116,7 @@ class VFDepthAlgo:
             opts['sampler'] = self.train_sampler
         self._dataloaders['train'] = DataLoader(ds, **opts)
         if rank == 0:
-            self._dataloaders['val'] = DataLoader(SyntheticSurroundDataset(cfg, length=8, seed=7, with_depth=True),
+            self._dataloaders['val'] = DataLoader(self._dataset(cfg, 'val', True),
                                                   batch_size=self.batch_size, shuffle=False, drop_last=True)
         self.num_total_steps = len(ds) // (self.batch_size * self.world_size) * self.num_epochs
 

@@ -194,6 +194,27 @@ int vfd_reflect_pad1_bwd(const float* g, float* dx, long long planes, int h, int
 /* backward of LeakyReLU(slope) + the one-pixel reflect pad for channels-last maps (the K3C / K2C
  * outputs): g, out [n, h+2, w+2, C] (out = the padded forward output) -> gp [n, h, w, C] =
  * (sum of g's copies) * (out > 0 ? 1 : slope); C % 4 == 0, 16-B aligned. */
+/* ------------------------------------------------------------------ weight relayouts (weights.hip) */
+/* Once-per-step copies of reduce_dim's first-conv weight w [O, C, 3, 3] for the MFMA kernels
+ * (volumetric_fusionnet.py:59-60; replace ATen permute/flip/pad chains):
+ *   mode 0: K2C fragments [9][ceil16(C)/4][O][2][2] over the map's channel order; C1 > 0 means the
+ *           map is z-major (z*C1 + c) and w is in the reference order c*Z + z (C = C1*Z);
+ *   mode 1: K3C forward fragments [D][9][Cv/4][O][2][2] (w channel c*D + d);
+ *   mode 2: K3C data-gradient copy [9 flipped taps][O/4][ceil256(Cv*D)][2][2] (n = d*Cv + c). */
+int vfd_weight_fragments(int mode, const float* w, float* dst, int O, int C, int C1, int Z, int Cv, int D,
+                         void* stream);
+/* dst[o][b][a][t] = w[o][a][b][t] (w [O][A][B][taps]): the pose weight between the reference channel
+ * order c*Z + z (A = C1, B = Z) and K2's map order z*C1 + c, and back for its gradient. */
+int vfd_weight_swap(const float* w, float* dst, int O, int A, int B, int taps, void* stream);
+
+/* ELU(alpha 1) [+ nearest 2x upsample (up = 1)] + the one-pixel reflect pad, NCHW fp32: the
+ * decoders' conv -> ELU -> upsample -> next reflect conv chain (fusion_depthnet.py:97-145,
+ * blocks.py:33-38 upsample, nn.Conv2d(padding_mode='reflect')) from the conv's pre-activation
+ * y [planes, h, w] straight to the next conv's padded input out [planes, (h<<up)+2, (w<<up)+2];
+ * backward dy = elu'(y) * (gather of the up-block's reflect copies of g), no atomics. */
+int vfd_elu_up_pad1_fwd(const float* y, float* out, long long planes, int h, int w, int up, void* stream);
+int vfd_elu_up_pad1_bwd(const float* g, const float* y, float* dy, long long planes, int h, int w, int up,
+                        void* stream);
 int vfd_lrelu_pad1_bwd_nhwc(const float* g, const float* out, float* gp, long long n_img, int h, int w, int C,
                             float slope, void* stream);
 

@@ -610,6 +610,73 @@ def test_reflect_pad_upsample_and_lrelu_pad_backward():
         close(dl, ref, f'upsample backward {hs}x{ws}', atol=1e-5, rtol=1e-5)
 
 
+def test_elu_upsample_pad_matches_aten():
+    """The decoders' fused ELU [+ nearest 2x upsample] + reflect pad against F.elu ->
+    F.interpolate(nearest) -> F.pad(reflect), forward and backward, at the config-2 decoder shapes
+    (6 x 16 x 192x320 -> 386x642, 6 x 16 x 384x640 -> 386x642 padded) and ragged ones; the
+    fused decoder against the module path on the same weights."""
+    from vfdepth_amd import kernels as KN
+    gen = torch.Generator(device=DEV).manual_seed(17)
+    for shape, up in (((6, 16, 192, 320), True), ((6, 16, 384, 640), False), ((2, 3, 5, 7), True),
+                      ((2, 3, 1, 1), True), ((1, 2, 2, 3), False)):
+        y = torch.randn(shape, device=DEV, generator=gen).requires_grad_(True)
+        yr = y.detach().clone().requires_grad_(True)
+        out = KN.EluUpPad.apply(y, up)
+        ref = F.elu(yr)
+        if up:
+            ref = F.interpolate(ref, scale_factor=2, mode='nearest')
+        ref = F.pad(ref, (1, 1, 1, 1), mode='reflect')
+        close(out, ref, f'elu_up_pad {shape} up={up}', atol=1e-6, rtol=1e-6)
+        g = torch.randn(out.shape, device=DEV, generator=gen)
+        out.backward(g)
+        ref.backward(g)
+        close(y.grad, yr.grad, f'elu_up_pad backward {shape} up={up}', atol=1e-5, rtol=1e-5)
+    import os
+    from vfdepth_amd import config as C
+    from vfdepth_amd.network import FusionDepthDecoder
+    dec = FusionDepthDecoder(2, [64, 64, 128], [16, 32, 64, 128, 256], [0], use_skips=False).to(DEV)
+    feats = [None, None, torch.randn(6, 128, 48, 80, device=DEV, generator=gen).requires_grad_(True)]
+    assert dec._fused_ok(feats[-1])
+    out_f = dec(feats)[('disp', 0)]
+    gd = torch.randn(out_f.shape, device=DEV, generator=gen)
+    gf, = torch.autograd.grad(out_f, feats[-1], gd)
+    os.environ['VFD_ELU_PAD'] = '0'
+    try:
+        out_m = dec(feats)[('disp', 0)]
+        gm, = torch.autograd.grad(out_m, feats[-1], gd)
+    finally:
+        del os.environ['VFD_ELU_PAD']
+    close(out_f, out_m, 'fused decoder disparity', atol=1e-5, rtol=1e-4)
+    close(gf, gm, 'fused decoder input gradient', atol=1e-5 * float(gm.abs().max()), rtol=1e-4)
+
+
+def test_weight_relayouts_match_torch_chains():
+    """weights.hip against the ATen permute / flip / pad chains it replaces (pure data movement:
+    bit-identical): K3C forward fragments, K3C data-gradient copy, K2C fragments over the pose map's
+    z-major order from the reference-order weight, and the channel-order swap both ways."""
+    import torch.nn.functional as F
+    from vfdepth_amd import kernels as KN
+    gen = torch.Generator(device=DEV).manual_seed(5)
+    O, Cv, D = 256, 64, 50
+    w = torch.randn(O, Cv * D, 3, 3, device=DEV, generator=gen)
+    ref = w.reshape(O, Cv // 4, 2, 2, D, 3, 3).permute(4, 5, 6, 1, 0, 2, 3).contiguous()
+    assert torch.equal(KN.proj_conv_weight_fragments(w, Cv, D), ref)
+    n, npad = Cv * D, (Cv * D + 255) // 256 * 256
+    wd = F.pad(w.reshape(O, Cv, D, 3, 3).flip(3, 4).permute(3, 4, 0, 2, 1).reshape(9, O, n), (0, npad - n))
+    ref = wd.reshape(9, O // 4, 2, 2, npad).permute(0, 1, 4, 2, 3).contiguous()
+    assert torch.equal(KN.proj_conv_dgrad_weight(w, Cv, D), ref)
+    for C1, Z in ((257, 20), (13, 3)):
+        wp = torch.randn(O, C1 * Z, 3, 3, device=DEV, generator=gen)
+        wz = wp.view(O, C1, Z, 3, 3).transpose(1, 2).reshape(O, Z * C1, 3, 3)
+        cpad = (C1 * Z + 15) // 16 * 16
+        wf = F.pad(wz.permute(2, 3, 1, 0).reshape(9, C1 * Z, O), (0, 0, 0, cpad - C1 * Z))
+        ref = wf.reshape(9, cpad // 4, 2, 2, O).permute(0, 1, 4, 2, 3).contiguous()
+        assert torch.equal(KN.pose_conv_fragments(wp, C1, Z), ref)
+        assert torch.equal(KN.pad_conv_weight_fragments(wz), ref)
+        assert torch.equal(KN.weight_swap(wp, C1, Z), wz)
+        assert torch.equal(KN.weight_swap(wz, Z, C1), wp)
+
+
 def test_stem_max_pool_matches_aten():
     """MaxPool2d(3, 2, 1) with the one-byte argmax: forward bit-identical to ATen (ties of a ReLU
     map's zeros go to the first maximum in scan order), backward equal to ATen's (fixed-order sum of

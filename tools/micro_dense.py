@@ -56,6 +56,22 @@ def main():
         nbp = (t.numel() + tp.numel()) * 4
         line(f'reflect pad fwd {shape}', timeit(lambda: lib.vfd_reflect_pad1_fwd(t.data_ptr(), tp.data_ptr(), n * c, h, w, L.stream())), nbp)
         line(f'reflect pad bwd {shape}', timeit(lambda: lib.vfd_reflect_pad1_bwd(tp.data_ptr(), t.data_ptr(), n * c, h, w, L.stream())), nbp)
+    # decoder ELU [+ nearest 2x] + reflect pad (config-2 decoder shapes) vs the ATen chain
+    for shape, up in (((6, 16, 192, 320), 1), ((6, 16, 384, 640), 0), ((6, 32, 96, 160), 1), ((6, 64, 48, 80), 1)):
+        n, c, h, w = shape
+        yy = torch.randn(shape, device=dev)
+        op = torch.empty(n, c, (h << up) + 2, (w << up) + 2, device=dev)
+        dyy = torch.empty_like(yy)
+        nbe = (yy.numel() + op.numel()) * 4
+        line(f'elu_up_pad fwd {shape} up={up}', timeit(lambda: lib.vfd_elu_up_pad1_fwd(yy.data_ptr(), op.data_ptr(), n * c, h, w, up, L.stream())), nbe)
+        line(f'elu_up_pad bwd {shape} up={up}', timeit(lambda: lib.vfd_elu_up_pad1_bwd(op.data_ptr(), yy.data_ptr(), dyy.data_ptr(), n * c, h, w, up, L.stream())), nbe + yy.numel() * 4)
+
+        def aten_chain():
+            a = F.elu(yy)
+            if up:
+                a = F.interpolate(a, scale_factor=2, mode='nearest')
+            return F.pad(a, (1, 1, 1, 1), mode='reflect')
+        line(f'  ATen elu->up->pad fwd {shape}', timeit(aten_chain), nbe)
     d = torch.randn(6, 256, 48, 80, device=dev)
     for hs, ws in ((24, 40), (12, 20), (6, 10)):
         dl = torch.empty(6, 256, hs, ws, device=dev)

@@ -1,42 +1,15 @@
 // Reflect padding by one pixel (nn.Conv2d(padding_mode='reflect', padding=1): the decoders'
-// 3x3 convs, network/blocks.py conv2d blocks) for NCHW fp32 maps, forward and backward.
-// The backward is a gather: every input pixel sums its (up to four) padded copies in a fixed
-// order (pad_sets), so it needs no atomics and is deterministic (ATen's reflection_pad2d
-// backward scatters with atomics).
+// 3x3 convs, network/blocks.py conv2d blocks) for NCHW fp32 maps, forward and backward, alone
+// or fused with the ELU [+ nearest 2x upsample] in front of it (elu_up_pad_*: the plain pad is
+// the <UP = 0, ACT = false> instance).  The backward is a gather: every input pixel sums its
+// (up to four) padded copies in a fixed order, so it needs no atomics and is deterministic
+// (ATen's reflection_pad2d backward scatters with atomics).
 #include "vfd_common.h"
 
 namespace vfd {
 
 __device__ __forceinline__ int rp_src(int i, int n) {       // padded index -> source index
   return i == 0 ? 1 : (i == n + 1 ? n - 2 : i - 1);
-}
-
-__global__ __launch_bounds__(256) void reflect_pad_fwd_k(const float* __restrict__ x, float* __restrict__ y,
-                                                         long long planes, int h, int w) {
-  const int ho = h + 2, wo = w + 2;
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;       // pixel of the padded plane
-  if (j >= ho * wo) return;
-  const int Y = j / wo, X = j - Y * wo;
-  const int src = rp_src(Y, h) * w + rp_src(X, w);
-  for (long long p = blockIdx.y; p < planes; p += gridDim.y) y[p * ho * wo + j] = x[p * h * w + src];
-}
-
-__global__ __launch_bounds__(256) void reflect_pad_bwd_k(const float* __restrict__ g, float* __restrict__ dx,
-                                                         long long planes, int h, int w) {
-  const int wo = w + 2;
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;       // pixel of the plane
-  if (j >= h * w) return;
-  const int yy = j / w, x = j - yy * w;
-  int rows[3], cols[3], nr, nc;
-  pad_sets(yy, h, true, rows, &nr);
-  pad_sets(x, w, true, cols, &nc);
-  for (long long p = blockIdx.y; p < planes; p += gridDim.y) {
-    const float* gp = g + p * (h + 2) * wo;
-    float s = 0.f;
-    for (int a = 0; a < nr; ++a)
-      for (int b = 0; b < nc; ++b) s += gp[rows[a] * wo + cols[b]];
-    dx[p * h * w + j] = s;
-  }
 }
 
 // Backward of LeakyReLU(slope) followed by the one-pixel reflect pad, channels-last (the fused
@@ -73,6 +46,143 @@ __global__ __launch_bounds__(256) void lrelu_pad_bwd_nhwc_k(const float4* __rest
   gp[i] = s;
 }
 
+
+// ELU(alpha 1) [+ nearest 2x upsample] + one-pixel reflect pad, NCHW: the decoders' chain
+// conv -> ELU -> upsample -> (next conv's) reflect pad (fusion_depthnet.py:97-145 conv2d blocks,
+// blocks.py upsample) in one pass from the conv's pre-activation y [planes, h, w] to the padded
+// input of the next conv [planes, Hu + 2, Wu + 2] (Hu = 2h or h).  out = elu(y) = expm1(y) for
+// y <= 0 (ATen's elu formula).  A thread writes EPT consecutive outputs of the flat padded plane
+// (one 16-B store when the plane size allows) for PPT planes (grid.y = plane groups), so the
+// index arithmetic is paid once per PPT * EPT outputs.
+constexpr int EPT = 4, PPT = 4;
+__device__ __forceinline__ float elu1(float v) { return v <= 0.f ? expm1f(v) : v; }
+
+template <int UP, bool ACT>
+__global__ __launch_bounds__(256) void elu_up_pad_fwd_k(const float* __restrict__ y, float* __restrict__ out,
+                                                        long long planes, int h, int w) {
+  const int Hu = h << UP, Wu = w << UP;
+  const int ho = Hu + 2, wo = Wu + 2, hwo = ho * wo;
+  const int j0 = (blockIdx.x * blockDim.x + threadIdx.x) * EPT;   // first flat output of the plane
+  if (j0 >= hwo) return;
+  int src[EPT];
+  int Y = j0 / wo, X = j0 - Y * wo;
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) {
+    src[e] = (rp_src(Y, Hu) >> UP) * w + (rp_src(X, Wu) >> UP);
+    if (++X == wo) { X = 0; ++Y; }
+  }
+  const bool vec = (hwo % EPT) == 0;                          // every thread's 4 outputs in one plane row-run
+  const long long p0 = (long long)blockIdx.y * PPT;
+#pragma unroll
+  for (int q = 0; q < PPT; ++q) {
+    const long long p = p0 + q;
+    if (p >= planes) break;
+    const float* yp = y + p * h * w;
+    float v[EPT];
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) v[e] = ACT ? elu1(yp[src[e]]) : yp[src[e]];
+    float* op = out + p * hwo + j0;
+    if (vec) {
+      *reinterpret_cast<float4*>(op) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < EPT; ++e)
+        if (j0 + e < hwo) op[e] = v[e];
+    }
+  }
+}
+
+// Its backward: dy = elu'(y) * (sum over the up-block's pixels of their reflect copies in g).
+// The padded rows covering the block {2sy, 2sy+1} are 2sy+1, 2sy+2 plus a mirror row when a
+// block pixel sits at 1 or Hu-2 (the rows of pad_sets of each pixel; the sets are disjoint),
+// likewise the columns: a fixed-order gather of <= 4 x 4 values, no atomics.  ELU' from the
+// output as ATen's elu_backward (is_result): out <= 0 ? g * (out + 1) : g.  A thread owns EPT
+// consecutive pixels of a row (16-B y / dy accesses when w % 4 == 0) for PPT planes.
+struct EupIdx {
+  int a, b, ma, mb;           // padded rows/cols: a, b (up only), mirrors of pixels 1 / n-2
+  float fma, fmb;             // 1 when that mirror exists (absent ones alias `a` and weigh 0)
+};
+template <int UP>
+__device__ __forceinline__ EupIdx eup_idx(int s, int n) {
+  const int Nu = n << UP, lo = s << UP, hi = lo + UP;        // the block's pixels lo..hi
+  EupIdx r;
+  r.a = lo + 1;
+  r.b = lo + 2;
+  const bool m1 = lo <= 1 && hi >= 1, m2 = lo <= Nu - 2 && hi >= Nu - 2;
+  r.fma = m1 ? 1.f : 0.f;
+  r.ma = m1 ? 0 : r.a;
+  r.fmb = m2 ? 1.f : 0.f;
+  r.mb = m2 ? Nu + 1 : r.a;
+  return r;
+}
+
+template <int UP>
+__device__ __forceinline__ float eup_row(const float* __restrict__ gr, const EupIdx& C) {
+  float t = gr[C.a];
+  if (UP) t += gr[C.b];
+  if (C.fma != 0.f || C.fmb != 0.f) t = (t + C.fma * gr[C.ma]) + C.fmb * gr[C.mb];
+  return t;
+}
+
+template <int UP, bool ACT>
+__global__ __launch_bounds__(256) void elu_up_pad_bwd_k(const float* __restrict__ g, const float* __restrict__ y,
+                                                        float* __restrict__ dy, long long planes, int h, int w) {
+  const int Hu = h << UP, Wu = w << UP;
+  const int wo = Wu + 2;
+  const int wq = (w + EPT - 1) / EPT;                        // thread groups per row
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= h * wq) return;
+  const int sy = j / wq, sx0 = (j - sy * wq) * EPT;
+  const EupIdx R = eup_idx<UP>(sy, h);
+  const bool rmir = R.fma != 0.f || R.fmb != 0.f;           // rare: border rows
+  EupIdx C[EPT];
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) C[e] = eup_idx<UP>(min(sx0 + e, w - 1), w);
+  const bool vec = (w % EPT) == 0;
+  const long long p0 = (long long)blockIdx.y * PPT;
+#pragma unroll 1
+  for (int q = 0; q < PPT; ++q) {
+    const long long p = p0 + q;
+    if (p >= planes) break;
+    const float* gp = g + p * (Hu + 2) * wo;
+    const float* ga = gp + (size_t)R.a * wo;
+    const float* gb = gp + (size_t)R.b * wo;
+    float s[EPT];
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) {
+      s[e] = eup_row<UP>(ga, C[e]);
+      if (UP) s[e] += eup_row<UP>(gb, C[e]);
+      if (rmir) {
+        s[e] += R.fma * eup_row<UP>(gp + (size_t)R.ma * wo, C[e]);
+        s[e] += R.fmb * eup_row<UP>(gp + (size_t)R.mb * wo, C[e]);
+      }
+    }
+    const size_t o = p * h * w + (size_t)sy * w + sx0;
+    float v[EPT] = {};
+    if (!ACT) {
+    } else if (vec) {
+      const float4 t = *reinterpret_cast<const float4*>(y + o);
+      v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < EPT; ++e) v[e] = y[o + (sx0 + e < w ? e : 0)];
+    }
+    float r[EPT];
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) {
+      const float ov = elu1(v[e]);
+      r[e] = !ACT ? s[e] : (ov <= 0.f ? s[e] * (ov + 1.f) : s[e]);
+    }
+    if (vec) {
+      *reinterpret_cast<float4*>(dy + o) = make_float4(r[0], r[1], r[2], r[3]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < EPT; ++e)
+        if (sx0 + e < w) dy[o + e] = r[e];
+    }
+  }
+}
+
 }  // namespace vfd
 
 using namespace vfd;
@@ -84,8 +194,9 @@ int vfd_reflect_pad1_fwd(const float* x, float* y, long long planes, int h, int 
               "reflect_pad1: bad arguments (h, w >= 2)");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_REFLECT_PAD, s);
-  const dim3 grid((unsigned)(((h + 2) * (w + 2) + 255) / 256), (unsigned)(planes < 65535 ? planes : 65535));
-  reflect_pad_fwd_k<<<grid, 256, 0, s>>>(x, y, planes, h, w);
+  VFD_REQUIRE(planes / PPT < 65535, "reflect_pad1: too many planes");
+  const dim3 grid((unsigned)(((h + 2) * (w + 2) + 256 * EPT - 1) / (256 * EPT)), (unsigned)((planes + PPT - 1) / PPT));
+  elu_up_pad_fwd_k<0, false><<<grid, 256, 0, s>>>(x, y, planes, h, w);
   return fail_launch("reflect_pad1_fwd");
 }
 
@@ -94,8 +205,9 @@ int vfd_reflect_pad1_bwd(const float* g, float* dx, long long planes, int h, int
               "reflect_pad1: bad arguments (h, w >= 2)");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_REFLECT_PAD, s);
-  const dim3 grid((unsigned)((h * w + 255) / 256), (unsigned)(planes < 65535 ? planes : 65535));
-  reflect_pad_bwd_k<<<grid, 256, 0, s>>>(g, dx, planes, h, w);
+  VFD_REQUIRE(planes / PPT < 65535, "reflect_pad1: too many planes");
+  const dim3 grid((unsigned)((h * ((w + EPT - 1) / EPT) + 255) / 256), (unsigned)((planes + PPT - 1) / PPT));
+  elu_up_pad_bwd_k<0, false><<<grid, 256, 0, s>>>(g, nullptr, dx, planes, h, w);
   return fail_launch("reflect_pad1_bwd");
 }
 
@@ -111,6 +223,32 @@ int vfd_lrelu_pad1_bwd_nhwc(const float* g, const float* out, float* gp, long lo
   lrelu_pad_bwd_nhwc_k<<<grid, 256, 0, s>>>((const float4*)g, (const float4*)out, (float4*)gp,
                                                                   n_img, h, w, C / 4, slope);
   return fail_launch("lrelu_pad1_bwd_nhwc");
+}
+
+int vfd_elu_up_pad1_fwd(const float* y, float* out, long long planes, int h, int w, int up, void* stream) {
+  VFD_REQUIRE(y && out && planes > 0 && planes / PPT < 65535 && h >= 1 && w >= 1 && (up == 0 || up == 1) && (h << up) >= 2 &&
+                  (w << up) >= 2 && (long long)((h << up) + 2) * ((w << up) + 2) < (1LL << 31),
+              "elu_up_pad1: bad arguments (up in {0, 1}, padded side >= 2)");
+  hipStream_t s = (hipStream_t)stream;
+  ProfScope ps(K_ELU_PAD, s);
+  const unsigned gx = (unsigned)((((h << up) + 2) * ((w << up) + 2) + 256 * EPT - 1) / (256 * EPT));
+  const dim3 grid(gx, (unsigned)((planes + PPT - 1) / PPT));
+  if (up) elu_up_pad_fwd_k<1, true><<<grid, 256, 0, s>>>(y, out, planes, h, w);
+  else elu_up_pad_fwd_k<0, true><<<grid, 256, 0, s>>>(y, out, planes, h, w);
+  return fail_launch("elu_up_pad1_fwd");
+}
+
+int vfd_elu_up_pad1_bwd(const float* g, const float* y, float* dy, long long planes, int h, int w, int up,
+                        void* stream) {
+  VFD_REQUIRE(g && y && dy && planes > 0 && planes / PPT < 65535 && h >= 1 && w >= 1 && (up == 0 || up == 1) && (h << up) >= 2 &&
+                  (w << up) >= 2 && (long long)((h << up) + 2) * ((w << up) + 2) < (1LL << 31),
+              "elu_up_pad1: bad arguments (up in {0, 1}, padded side >= 2)");
+  hipStream_t s = (hipStream_t)stream;
+  ProfScope ps(K_ELU_PAD, s);
+  const dim3 grid((unsigned)((h * ((w + EPT - 1) / EPT) + 255) / 256), (unsigned)((planes + PPT - 1) / PPT));
+  if (up) elu_up_pad_bwd_k<1, true><<<grid, 256, 0, s>>>(g, y, dy, planes, h, w);
+  else elu_up_pad_bwd_k<0, true><<<grid, 256, 0, s>>>(g, y, dy, planes, h, w);
+  return fail_launch("elu_up_pad1_bwd");
 }
 
 }  // extern "C"

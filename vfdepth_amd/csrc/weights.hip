@@ -1,0 +1,121 @@
+// Weight relayouts for the MFMA convolution kernels (once per step: the weights change at every
+// optimizer step).  Each replaces a chain of ATen permute / flip / pad / contiguous copies whose
+// element-wise gathers touch every 3x3 tap row of the source once per tap (~0.6 TB/s on the
+// 47 MB pose reduce_dim weight):  here a thread moves one (out-channel, in-channel) row of the 9
+// taps — a 36-byte contiguous read — to the 9 tap planes of the destination, where consecutive
+// lanes write consecutive floats.
+//
+//   mode 0  K2C fragments           dst[tap][q][o][h][s]     = w[o][chan(4q + 2h + s)][tap]
+//           (padconv.hip ppc_main_k; cz = 4q + 2h + s in the map's channel order, zero past C;
+//           chan(cz) = cz, or for the pose map's z-major order cz = z*C1 + c the reference
+//           channel c*Z + z — volumetric_fusionnet.py:160-162, 338-343)
+//   mode 1  K3C forward fragments   dst[d][tap][q][o][h][s]  = w[o][(4q + 2h + s)*D + d][tap]
+//           (projconv.hip pcv_main_k; reference channel c*D + d, :261-265)
+//   mode 2  K3C data-gradient copy  dst[8 - tap][oq][n][h][s] = w[4oq + 2h + s][c*D + d][tap]
+//           (projconv.hip pcd_main_k; n = d*Cv + c, zero for n >= Cv*D)
+//   swap    dst[o][b][a][t] = w[o][a][b][t]: the pose weight between the reference channel order
+//           (c*Z + z) and the map's (z*C1 + c), for MIOpen's data / weight gradients
+#include "vfd_common.h"
+
+namespace vfd {
+
+constexpr int WR_TAPS = 9;
+
+struct WrArgs {
+  int mode, O, C, C1, Z, Cv, D, cpad, npad, refperm;
+};
+
+__global__ __launch_bounds__(256) void weight_frag_k(WrArgs a, const float* __restrict__ w, float* __restrict__ dst,
+                                                     long long nrow) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;   // destination row (all taps)
+  if (t >= nrow) return;
+  const int s = (int)(t & 1), h = (int)((t >> 1) & 1);
+  long long src = -1;                     // source row (of 9 taps), -1: zero padding
+  long long plane = 0, off = 0;           // tap-plane stride, offset of tap 0 in dst
+  int flip = 0;
+  const int K = a.mode == 0 ? a.C : a.Cv * a.D;   // source in-channels per out-channel
+  if (a.mode == 0) {
+    const long long per = (long long)(a.cpad / 4) * a.O * 4;             // one tap plane
+    const int o = (int)((t >> 2) % a.O), q = (int)((t >> 2) / a.O);
+    const int cz = 4 * q + 2 * h + s;
+    if (cz < a.C) src = (long long)o * K + (a.refperm ? (long long)(cz % a.C1) * a.Z + cz / a.C1 : cz);
+    plane = per;
+    off = t;
+  } else if (a.mode == 1) {
+    const int Q = a.Cv / 4;
+    const long long per = (long long)Q * a.O * 4;
+    const long long r = t % per;
+    const int d = (int)(t / per);
+    const int o = (int)((r >> 2) % a.O), q = (int)((r >> 2) / a.O);
+    const int c = 4 * q + 2 * h + s;
+    src = (long long)o * K + (long long)c * a.D + d;
+    plane = per;
+    off = (long long)d * WR_TAPS * per + r;
+  } else {
+    const long long per = (long long)(a.O / 4) * a.npad * 4;
+    const int n = (int)((t >> 2) % a.npad), oq = (int)((t >> 2) / a.npad);
+    const int o = 4 * oq + 2 * h + s;
+    if (n < K) src = (long long)o * K + (long long)(n % a.Cv) * a.D + n / a.Cv;
+    plane = per;
+    off = t;
+    flip = 1;
+  }
+  float v[WR_TAPS];
+  const float* p = w + (src >= 0 ? src : 0) * WR_TAPS;
+#pragma unroll
+  for (int k = 0; k < WR_TAPS; ++k) v[k] = src >= 0 ? p[k] : 0.f;
+#pragma unroll
+  for (int k = 0; k < WR_TAPS; ++k) dst[off + (flip ? WR_TAPS - 1 - k : k) * plane] = v[k];
+}
+
+__global__ __launch_bounds__(256) void weight_swap_k(const float* __restrict__ w, float* __restrict__ dst, int O,
+                                                     int A, int Bn, int taps) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;   // destination row (o, b, a)
+  if (t >= (long long)O * A * Bn) return;
+  const int ai = (int)(t % A), bi = (int)((t / A) % Bn), o = (int)(t / ((long long)A * Bn));
+  const float* p = w + (((long long)o * A + ai) * Bn + bi) * taps;
+  float* q = dst + t * taps;
+  for (int k = 0; k < taps; ++k) q[k] = p[k];
+}
+
+}  // namespace vfd
+
+using namespace vfd;
+
+extern "C" {
+
+int vfd_weight_fragments(int mode, const float* w, float* dst, int O, int C, int C1, int Z, int Cv, int D,
+                         void* stream) {
+  VFD_REQUIRE(w && dst && O > 0 && O % 4 == 0, "weight_fragments: bad arguments");
+  WrArgs a{mode, O, C, C1, Z, Cv, D, 0, 0, 0};
+  long long nrow = 0;
+  if (mode == 0) {
+    VFD_REQUIRE(C > 0 && (C1 <= 0 || (Z > 0 && C1 * Z == C)), "weight_fragments: C = %d vs C1 * Z", C);
+    a.cpad = (C + 15) / 16 * 16;
+    a.refperm = C1 > 0 ? 1 : 0;
+    nrow = (long long)(a.cpad / 4) * O * 4;
+  } else if (mode == 1) {
+    VFD_REQUIRE(Cv > 0 && Cv % 4 == 0 && D > 0, "weight_fragments: Cv %% 4, D");
+    nrow = (long long)D * (Cv / 4) * O * 4;
+  } else if (mode == 2) {
+    VFD_REQUIRE(Cv > 0 && D > 0, "weight_fragments: Cv, D");
+    a.npad = (Cv * D + 255) / 256 * 256;
+    nrow = (long long)(O / 4) * a.npad * 4;
+  } else {
+    set_error("weight_fragments: mode %d", mode);
+    return VFD_EINVAL;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  weight_frag_k<<<(unsigned)((nrow + 255) / 256), 256, 0, s>>>(a, w, dst, nrow);
+  return fail_launch("weight_fragments");
+}
+
+int vfd_weight_swap(const float* w, float* dst, int O, int A, int B, int taps, void* stream) {
+  VFD_REQUIRE(w && dst && O > 0 && A > 0 && B > 0 && taps > 0, "weight_swap: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  const long long n = (long long)O * A * B;
+  weight_swap_k<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(w, dst, O, A, B, taps);
+  return fail_launch("weight_swap");
+}
+
+}  // extern "C"

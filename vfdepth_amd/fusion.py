@@ -131,15 +131,17 @@ class VFNet(nn.Module):
         if self.model == 'depth':
             w0 = KN.proj_conv_weight(c0.weight, self.v_dim_o[-1], self.proj_d_bins)
         else:
-            w0 = KN.pose_conv_weight(c0.weight, self.feat_in_dim + 1, self.z_dim)
+            C1, Z = self.feat_in_dim + 1, self.z_dim
             if self.pad_conv(x_padded):
-                # K2C: the first conv on MFMA (padconv.hip), written reflect-padded for the second
-                # the fragment copy of the weight is shared by the step's pose calls (same version)
+                # K2C: the first conv on MFMA (padconv.hip), written reflect-padded for the second;
+                # it takes the weight in the reference channel order (relayouts in weights.hip);
+                # the fragment copy is shared by the step's pose calls (same version)
                 wf = _GEOMETRY_CACHE.get(('pose_wf', id(c0.weight)), (c0.weight,),
-                                         lambda: KN.pose_conv_fragments(c0.weight, self.feat_in_dim + 1, self.z_dim))
-                y0 = KN.PadConv.apply(x_padded, w0, c0.bias, self.stride, wf)
+                                         lambda: KN.pose_conv_fragments(c0.weight, C1, Z))
+                y0 = KN.PadConv.apply(x_padded, c0.weight, c0.bias, self.stride, wf, (C1, Z))
                 return F.leaky_relu(F.conv2d(y0, c1.weight, c1.bias, stride=self.stride), 0.1,
                                     inplace=True).contiguous()
+            w0 = KN.pose_conv_weight(c0.weight, C1, Z)
         x = F.leaky_relu(F.conv2d(x_padded, w0, c0.bias, stride=self.stride), 0.1, inplace=True)
         return F.leaky_relu(c1(x), 0.1, inplace=True).contiguous()
 

@@ -357,11 +357,22 @@ class VoxelProject(torch.autograd.Function):
 _DGRAD_LAYOUT = os.environ.get('VFD_DGRAD_LAYOUT', 'nhwc')
 
 
+def _weight_fragments(mode, w, shape, C1=0, Z=0, Cv=0, D=0):
+    """One relayout launch (weights.hip) of a conv weight [O, C, 3, 3] into an MFMA kernel's copy."""
+    lib = L.load()
+    w = _dev(w.detach(), 'conv weight')
+    out = torch.empty(shape, device=w.device)
+    O, C = w.shape[:2]
+    L.check(lib.vfd_weight_fragments(mode, w.data_ptr(), out.data_ptr(), O, C, C1, Z, Cv, D, L.stream()),
+            'weight_fragments')
+    return out
+
+
 def proj_conv_weight_fragments(w, Cv, D):
     """reduce_dim[0] weight [O, Cv*D, 3, 3] (reference channel c*D + d) -> the fused kernel's
     fragment-ordered copy [D, 3, 3, Cv/4, O, 2, 2] (c = 4q + 2h + s; projconv.hip, pcv_main_k)."""
     O = w.shape[0]
-    return w.reshape(O, Cv // 4, 2, 2, D, 3, 3).permute(4, 5, 6, 1, 0, 2, 3).contiguous()
+    return _weight_fragments(1, w, (D, 3, 3, Cv // 4, O, 2, 2), Cv=Cv, D=D)
 
 
 def proj_conv_dgrad_weight(w, Cv, D):
@@ -369,36 +380,36 @@ def proj_conv_dgrad_weight(w, Cv, D):
     kernel's copy [9 flipped taps, O/4, np, 2, 2] (o = 4q + 2h + s; n = d*Cv + c zero-padded to a
     multiple of 256; projconv.hip, pcd_main_k)."""
     O = w.shape[0]
-    n = Cv * D
-    npad = (n + 255) // 256 * 256
-    wd = w.reshape(O, Cv, D, 3, 3).flip(3, 4).permute(3, 4, 0, 2, 1).reshape(9, O, n)
-    if npad != n:
-        wd = F.pad(wd, (0, npad - n))
-    return wd.reshape(9, O // 4, 2, 2, npad).permute(0, 1, 4, 2, 3).contiguous()
+    npad = (Cv * D + 255) // 256 * 256
+    return _weight_fragments(2, w, (9, O // 4, npad, 2, 2), Cv=Cv, D=D)
 
 
 _PC_DGRAD = os.environ.get('VFD_PC_DGRAD', '1') != '0'
 
 
-def pad_conv_weight_fragments(w):
-    """Conv weight [O, C, 3, 3] (C in the input map's channel order) -> K2C's copy
-    [9 taps, Cpad/4, O, 2, 2] (c = 4q + 2h + s, Cpad = C rounded up to 16, zero-padded;
-    padconv.hip, ppc_main_k)."""
+def pad_conv_weight_fragments(w, C1=0, Z=0):
+    """Conv weight [O, C, 3, 3] -> K2C's copy [9 taps, Cpad/4, O, 2, 2] (c = 4q + 2h + s over the
+    input map's channel order, Cpad = C rounded up to 16, zero-padded; padconv.hip, ppc_main_k).
+    C1, Z > 0: w is in the reference order c*Z + z and the map is K2's z-major z*C1 + c."""
     O, C = w.shape[:2]
     cpad = (C + 15) // 16 * 16
-    wf = w.permute(2, 3, 1, 0).reshape(9, C, O)
-    if cpad != C:
-        wf = F.pad(wf, (0, 0, 0, cpad - C))
-    return wf.reshape(9, cpad // 4, 2, 2, O).permute(0, 1, 4, 2, 3).contiguous()
+    return _weight_fragments(0, w, (9, cpad // 4, O, 2, 2), C1=C1, Z=Z)
 
 
 def pose_conv_fragments(w, C1, Z):
     """The pose reduce_dim[0] weight [O, C1*Z, 3, 3] (reference channel c*Z + z) straight to K2C's
-    fragment copy over FusePose's channel order z*C1 + c (= pad_conv_weight_fragments of
-    pose_conv_weight(w)); no gradient."""
-    O = w.shape[0]
-    with torch.no_grad():
-        return pad_conv_weight_fragments(w.detach().view(O, C1, Z, 3, 3).transpose(1, 2).reshape(O, Z * C1, 3, 3))
+    fragment copy over FusePose's channel order z*C1 + c; no gradient."""
+    return pad_conv_weight_fragments(w, C1, Z)
+
+
+def weight_swap(w, A, B):
+    """w [O, A*B, kh, kw] with channel a*B + b -> channel b*A + a (weights.hip, one launch)."""
+    lib = L.load()
+    w = _dev(w, 'conv weight').contiguous()
+    O, _, kh, kw = w.shape
+    out = torch.empty_like(w)
+    L.check(lib.vfd_weight_swap(w.data_ptr(), out.data_ptr(), O, A, B, kh * kw, L.stream()), 'weight_swap')
+    return out
 
 
 def pad_conv_desc(x, stride, out_channels):
@@ -419,7 +430,7 @@ class PadConv(torch.autograd.Function):
 
     @staticmethod
     @_amp_fwd
-    def forward(ctx, x, w, bias, stride, wf=None):
+    def forward(ctx, x, w, bias, stride, wf=None, perm=None):
         lib = L.load()
         x = _channels_last(x, 'pad_conv input')
         w, bias = _dev(w, 'pad_conv weight'), _dev(bias, 'pad_conv bias')
@@ -431,11 +442,11 @@ class PadConv(torch.autograd.Function):
         ho, wo = (x.shape[2] - 3) // stride + 1, (x.shape[3] - 3) // stride + 1
         out = torch.empty(x.shape[0], O, ho + 2, wo + 2, device=x.device, memory_format=torch.channels_last)
         if wf is None:
-            wf = pad_conv_weight_fragments(w)
+            wf = pad_conv_weight_fragments(w, *(perm or (0, 0)))
         ws = _ws(nbytes, x.device)
         L.check(lib.vfd_pad_conv_fwd(ctypes.byref(d), x.data_ptr(), wf.data_ptr(), bias.data_ptr(), out.data_ptr(),
                                      ws.data_ptr(), nbytes, L.stream()), 'pad_conv_fwd')
-        ctx.stride = stride
+        ctx.stride, ctx.perm = stride, perm
         ctx.save_for_backward(x, w, out)
         return out
 
@@ -446,9 +457,14 @@ class PadConv(torch.autograd.Function):
         g_pre = lrelu_pad_backward(g, out)
         mask = [ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]]
         s = ctx.stride
+        if ctx.perm:        # MIOpen works in the map's channel order: swap in, and the gradient back
+            C1, Z = ctx.perm
+            w = weight_swap(w, C1, Z)
         dx, dw, db = torch.ops.aten.convolution_backward(g_pre, x, w, [w.shape[0]], [s, s], [0, 0], [1, 1],
                                                          False, [0, 0], 1, mask)
-        return dx, dw, db, None, None
+        if ctx.perm and dw is not None:
+            dw = weight_swap(dw, Z, C1)
+        return dx, dw, db, None, None, None
 
 
 def lrelu_pad_backward(g, out, slope=0.1):
@@ -554,7 +570,7 @@ class ProjConv(torch.autograd.Function):
                                                       ctx.plan.numel(), dvox.data_ptr(), L.stream()),
                     'voxel_project_bwd')
         if mask[1]:
-            dw0 = dw.reshape(O, space.D, Cv, 3, 3).transpose(1, 2).reshape(O, Cv * space.D, 3, 3)
+            dw0 = weight_swap(dw, space.D, Cv)      # d*Cv + c -> the reference's c*D + d
         ctx.plan = None
         return None, dvox, None, None, dw0, db if mask[2] else None
 
@@ -972,6 +988,42 @@ class ReflectPad1(torch.autograd.Function):
         if L.PROF_ON:
             L.ALG_BYTES['reflect_pad'] += (g.numel() + dx.numel()) * 4
         return dx
+
+
+class EluUpPad(torch.autograd.Function):
+    """F.pad(upsample2x_nearest(elu(y)) if up else elu(y), (1, 1, 1, 1), mode='reflect') for NCHW
+    fp32 y in one pass (reflectpad.hip): the decoders' ELU -> upsample -> next reflect conv chain
+    without the ELU / upsample / cat / pad intermediates; backward is one gather kernel."""
+
+    @staticmethod
+    def forward(ctx, y, up):
+        lib = L.load()
+        _check_device(y, 'elu_up_pad input')
+        y = y.contiguous()
+        *lead, h, w = y.shape
+        u = 1 if up else 0
+        out = torch.empty(*lead, (h << u) + 2, (w << u) + 2, device=y.device)
+        planes = y.numel() // (h * w)
+        L.check(lib.vfd_elu_up_pad1_fwd(y.data_ptr(), out.data_ptr(), planes, h, w, u, L.stream()), 'elu_up_pad1_fwd')
+        if L.PROF_ON:
+            L.ALG_BYTES['elu_pad'] += (y.numel() + out.numel()) * 4
+        ctx.u = u
+        ctx.save_for_backward(y)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        lib = L.load()
+        y, = ctx.saved_tensors
+        g = g.contiguous()
+        h, w = y.shape[-2:]
+        dy = torch.empty_like(y)
+        planes = y.numel() // (h * w)
+        L.check(lib.vfd_elu_up_pad1_bwd(g.data_ptr(), y.data_ptr(), dy.data_ptr(), planes, h, w, ctx.u, L.stream()),
+                'elu_up_pad1_bwd')
+        if L.PROF_ON:
+            L.ALG_BYTES['elu_pad'] += (g.numel() + 2 * y.numel()) * 4
+        return dy, None
 
 
 # =============================================================================================

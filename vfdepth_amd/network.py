@@ -3,6 +3,7 @@
 Mirrors `/root/reference/network/{fusion_depthnet,fusion_posenet,mono_depthnet,mono_posenet}.py`
 module-for-module (attribute names and state-dict keys included) so reference checkpoints load.
 """
+import os
 from collections import OrderedDict
 
 import torch
@@ -61,7 +62,44 @@ class FusionDepthDecoder(nn.Module):
         self.decoder = nn.ModuleList(list(self.convs.values()))
         self.sigmoid = nn.Sigmoid()
 
+    def _fused_ok(self, x):
+        """The HIP chain applies: fp32 GPU maps outside autocast, no skip concatenation, and the
+        blocks are the stock (reflect conv 3x3, Identity, ELU(1.0)) — VFD_ELU_PAD=0 disables it."""
+        if not (x.is_cuda and x.dtype == torch.float32 and not torch.is_autocast_enabled('cuda')
+                and not self.use_skips and os.environ.get('VFD_ELU_PAD', '1') != '0'):
+            return False
+        for k, blk in self.convs.items():
+            conv, norm, act = blk
+            if not (isinstance(norm, nn.Identity) and conv.padding_mode == 'reflect' and conv.kernel_size == (3, 3)
+                    and conv.stride == (1, 1) and conv.padding == (1, 1) and conv.dilation == (1, 1)
+                    and conv.groups == 1):
+                return False
+            if k[0] == 'upconv' and not (isinstance(act, nn.ELU) and act.alpha == 1.0):
+                return False
+            if k[0] == 'dispconv' and not isinstance(act, nn.Identity):
+                return False
+        return True
+
+    def _forward_fused(self, input_features):
+        """The same decoder with each block's ELU, the nearest upsample and the next conv's reflect
+        pad done by one HIP kernel (`KN.EluUpPad`): every conv reads a padded map that the
+        previous block's kernel wrote (padding 0), the ELU / upsample / pad intermediates never
+        exist."""
+        out = {}
+        xp = KN.ReflectPad1.apply(input_features[-1])
+        for i in range(self.level_in, -1, -1):
+            c0 = self.convs[('upconv', i, 0)][0]
+            xp = KN.EluUpPad.apply(F.conv2d(xp, c0.weight, c0.bias), True)
+            c1 = self.convs[('upconv', i, 1)][0]
+            xp = KN.EluUpPad.apply(F.conv2d(xp, c1.weight, c1.bias), False)
+            if i in self.scales:
+                cd = self.convs[('dispconv', i)][0]
+                out[('disp', i)] = self.sigmoid(F.conv2d(xp, cd.weight, cd.bias))
+        return out
+
     def forward(self, input_features):
+        if self._fused_ok(input_features[-1]):
+            return self._forward_fused(input_features)
         out = {}
         x = input_features[-1]
         for i in range(self.level_in, -1, -1):

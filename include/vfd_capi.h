@@ -194,6 +194,18 @@ int vfd_reflect_pad1_bwd(const float* g, float* dx, long long planes, int h, int
 /* backward of LeakyReLU(slope) + the one-pixel reflect pad for channels-last maps (the K3C / K2C
  * outputs): g, out [n, h+2, w+2, C] (out = the padded forward output) -> gp [n, h, w, C] =
  * (sum of g's copies) * (out > 0 ? 1 : slope); C % 4 == 0, 16-B aligned. */
+/* One-launch BatchNorm(+residual)(+ReLU) forward / backward for channels of at most 8192 elements
+ * with local statistics (the small ResNet layers): one workgroup per channel computes the fp64
+ * statistics and applies them; same arguments and results as bn_fwd_stats + bn_fwd_apply /
+ * bn_bwd_stats + bn_bwd_apply (d->S unused).  vfd_bn1_fits: 1 when the shape qualifies. */
+int vfd_bn1_fits(const vfd_bn_desc* d);
+int vfd_bn1_fwd(const vfd_bn_desc* d, const float* x, const float* residual, const float* gamma, const float* beta,
+                float* y, float* mean, float* invstd, float* running_mean, float* running_var,
+                long long* num_batches_tracked, void* stream);
+int vfd_bn1_bwd(const vfd_bn_desc* d, const float* g, const float* y, const float* x, const float* gamma,
+                const float* mean, const float* invstd, float* dx, float* dresidual, float* dgamma, float* dbeta,
+                void* stream);
+
 /* ------------------------------------------------------------------ weight relayouts (weights.hip) */
 /* Once-per-step copies of reduce_dim's first-conv weight w [O, C, 3, 3] for the MFMA kernels
  * (volumetric_fusionnet.py:59-60; replace ATen permute/flip/pad chains):
@@ -214,7 +226,10 @@ int vfd_weight_swap(const float* w, float* dst, int O, int A, int B, int taps, v
  * backward dy = elu'(y) * (gather of the up-block's reflect copies of g), no atomics. */
 int vfd_elu_up_pad1_fwd(const float* y, float* out, long long planes, int h, int w, int up, void* stream);
 int vfd_elu_up_pad1_bwd(const float* g, const float* y, float* dy, long long planes, int h, int w, int up,
-                        void* stream);
+                        float* psum, void* stream);
+/* psum (optional, [planes][vfd_elu_up_pad1_bwd_blocks(h, w)]): per-block sums of dy per plane —
+ * the partials of the producing conv's bias gradient (summed in fixed order by the caller) */
+int vfd_elu_up_pad1_bwd_blocks(int h, int w);
 int vfd_lrelu_pad1_bwd_nhwc(const float* g, const float* out, float* gp, long long n_img, int h, int w, int C,
                             float slope, void* stream);
 

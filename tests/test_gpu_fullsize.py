@@ -538,6 +538,8 @@ def test_pad_conv_matches_conv(shape):
 @pytest.mark.parametrize('shape,res,relu', [((6, 64, 96, 160), True, True),      # layer1 block tail
                                             ((6, 64, 192, 320), False, True),    # stem
                                             ((6, 512, 12, 20), False, False),    # layer4 downsample BN
+                                            ((6, 128, 48, 80), True, True),      # layer2
+                                            ((6, 256, 24, 40), True, True),      # layer3 (one-launch path)
                                             ((3, 8, 5, 7), True, True)])         # HW % 4 != 0
 def test_batchnorm_act_matches_torch(shape, res, relu):
     """Fused training-mode BatchNorm (+ residual) (+ ReLU) (bnact.hip) against nn.BatchNorm2d.train()

@@ -97,10 +97,14 @@ _SIGS = {
     'vfd_upsample_ac_bwd': (c_int, [c_fp, c_fp, c_fp, ctypes.c_longlong] + [c_int] * 4 + [c_void_p]),
     'vfd_reflect_pad1_fwd': (c_int, [c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_void_p]),
     'vfd_reflect_pad1_bwd': (c_int, [c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_void_p]),
+    'vfd_bn1_fits': (c_int, [ctypes.POINTER(BnDesc)]),
+    'vfd_bn1_fwd': (c_int, [ctypes.POINTER(BnDesc)] + [c_fp] * 10 + [c_void_p]),
+    'vfd_bn1_bwd': (c_int, [ctypes.POINTER(BnDesc)] + [c_fp] * 10 + [c_void_p]),
     'vfd_weight_fragments': (c_int, [c_int, c_fp, c_fp] + [c_int] * 6 + [c_void_p]),
     'vfd_weight_swap': (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_void_p]),
     'vfd_elu_up_pad1_fwd': (c_int, [c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_int, c_void_p]),
-    'vfd_elu_up_pad1_bwd': (c_int, [c_fp, c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_int, c_void_p]),
+    'vfd_elu_up_pad1_bwd': (c_int, [c_fp, c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_int, c_fp, c_void_p]),
+    'vfd_elu_up_pad1_bwd_blocks': (c_int, [c_int, c_int]),
     'vfd_lrelu_pad1_bwd_nhwc': (c_int, [c_fp, c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_int, c_float, c_void_p]),
     'vfd_pad_conv_fwd_workspace': (c_size_t, [ctypes.POINTER(ConvDesc)]),
     'vfd_pad_conv_fwd': (c_int, [ctypes.POINTER(ConvDesc)] + [c_fp] * 5 + [c_size_t, c_void_p]),

@@ -260,6 +260,178 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply_k(vfd_bn_desc d, cons
   });
 }
 
+
+// ---- one-launch variants for channels of at most BN1_MAX elements (the 1/16 - 1/32 ResNet layers,
+// local statistics only): one workgroup per channel computes the statistics and then applies them
+// (the second sweep re-reads the channel from L2), so a layer is one launch each way instead of
+// two, and no partials round-trip through memory.  Fixed summation order: deterministic.
+constexpr int BN1_THREADS = 512;
+constexpr unsigned BN1_MAX = 8192;   // layer2 (23040 / channel) keeps the split path: its 128 channels alone would leave half the CUs idle
+
+__device__ __forceinline__ double block_sum1(double v, double* sh) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) sh[wv] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int i = 0; i < BN1_THREADS / 64; ++i) s += sh[i];
+  return s;
+}
+
+template <typename F>
+__device__ __forceinline__ void bn1_visit(const vfd_bn_desc& d, int c, F&& f) {
+  const unsigned total = (unsigned)d.N * (unsigned)d.HW;
+  if ((d.HW & 3) == 0) {
+    for (unsigned e = 4 * threadIdx.x; e < total; e += 4 * BN1_THREADS) f(bn_off(d, c, e), 4);
+  } else {
+    for (unsigned e = threadIdx.x; e < total; e += BN1_THREADS) f(bn_off(d, c, e), 1);
+  }
+}
+
+__global__ __launch_bounds__(BN1_THREADS) void bn1_fwd_k(vfd_bn_desc d, const float* __restrict__ x,
+                                                         const float* __restrict__ r, const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta, float* __restrict__ y,
+                                                         float* __restrict__ mean_out, float* __restrict__ invstd_out,
+                                                         float* __restrict__ run_mean, float* __restrict__ run_var,
+                                                         long long* __restrict__ nbt) {
+  __shared__ double sh[BN1_THREADS / 64];
+  const int c = blockIdx.x;
+  if (nbt && c == 0 && threadIdx.x == 0) nbt[0] += 1;
+  double s1 = 0.0, s2 = 0.0;
+  bn1_visit(d, c, [&](size_t o, int n) {
+    if (n == 4) {
+      const float4 v = *reinterpret_cast<const float4*>(x + o);
+      const double a = v.x, b = v.y, e = v.z, f = v.w;
+      s1 += (a + b) + (e + f);
+      s2 += (a * a + b * b) + (e * e + f * f);
+    } else {
+      const double a = x[o];
+      s1 += a;
+      s2 += a * a;
+    }
+  });
+  s1 = block_sum1(s1, sh);
+  s2 = block_sum1(s2, sh);
+  const double count = (double)d.N * d.HW;
+  const double mean_d = s1 / count;
+  double var_d = s2 / count - mean_d * mean_d;
+  var_d = var_d > 0.0 ? var_d : 0.0;
+  const float mean = (float)mean_d;
+  const float invstd = (float)(1.0 / sqrt(var_d + (double)d.eps));
+  if (threadIdx.x == 0) {
+    mean_out[c] = mean;
+    invstd_out[c] = invstd;
+    if (run_mean) {
+      const double unbiased = count > 1.0 ? var_d * count / (count - 1.0) : var_d;
+      run_mean[c] = (float)((1.0 - d.momentum) * run_mean[c] + d.momentum * mean_d);
+      run_var[c] = (float)((1.0 - d.momentum) * run_var[c] + d.momentum * unbiased);
+    }
+  }
+  const float sc = invstd * gamma[c];
+  const float shf = beta[c] - mean * sc;
+  const bool relu = d.relu != 0;
+  bn1_visit(d, c, [&](size_t o, int n) {
+    if (n == 4) {
+      float4 v = *reinterpret_cast<const float4*>(x + o);
+      v.x = v.x * sc + shf;
+      v.y = v.y * sc + shf;
+      v.z = v.z * sc + shf;
+      v.w = v.w * sc + shf;
+      if (r) {
+        const float4 q = *reinterpret_cast<const float4*>(r + o);
+        v.x += q.x;
+        v.y += q.y;
+        v.z += q.z;
+        v.w += q.w;
+      }
+      if (relu) {
+        v.x = fmaxf(v.x, 0.f);
+        v.y = fmaxf(v.y, 0.f);
+        v.z = fmaxf(v.z, 0.f);
+        v.w = fmaxf(v.w, 0.f);
+      }
+      *reinterpret_cast<float4*>(y + o) = v;
+    } else {
+      float v = x[o] * sc + shf;
+      if (r) v += r[o];
+      if (relu) v = fmaxf(v, 0.f);
+      y[o] = v;
+    }
+  });
+}
+
+__global__ __launch_bounds__(BN1_THREADS) void bn1_bwd_k(vfd_bn_desc d, const float* __restrict__ g,
+                                                         const float* __restrict__ y, const float* __restrict__ x,
+                                                         const float* __restrict__ gamma,
+                                                         const float* __restrict__ mean_in,
+                                                         const float* __restrict__ invstd_in, float* __restrict__ dx,
+                                                         float* __restrict__ dr, float* __restrict__ dgamma,
+                                                         float* __restrict__ dbeta) {
+  __shared__ double sh[BN1_THREADS / 64];
+  const int c = blockIdx.x;
+  const float mean = mean_in[c], invstd = invstd_in[c];
+  const bool relu = d.relu != 0;
+  double s1 = 0.0, s2 = 0.0;
+  bn1_visit(d, c, [&](size_t o, int n) {
+    if (n == 4) {
+      float4 gv = *reinterpret_cast<const float4*>(g + o);
+      const float4 xv = *reinterpret_cast<const float4*>(x + o);
+      if (relu) {
+        const float4 yv = *reinterpret_cast<const float4*>(y + o);
+        gv.x = yv.x > 0.f ? gv.x : 0.f;
+        gv.y = yv.y > 0.f ? gv.y : 0.f;
+        gv.z = yv.z > 0.f ? gv.z : 0.f;
+        gv.w = yv.w > 0.f ? gv.w : 0.f;
+      }
+      s1 += ((double)gv.x + (double)gv.y) + ((double)gv.z + (double)gv.w);
+      s2 += ((double)gv.x * (double)(xv.x - mean) + (double)gv.y * (double)(xv.y - mean)) +
+            ((double)gv.z * (double)(xv.z - mean) + (double)gv.w * (double)(xv.w - mean));
+    } else {
+      float gv = g[o];
+      if (relu && !(y[o] > 0.f)) gv = 0.f;
+      s1 += gv;
+      s2 += (double)gv * (double)(x[o] - mean);
+    }
+  });
+  const double sg = block_sum1(s1, sh), sgx = block_sum1(s2, sh);
+  if (threadIdx.x == 0) {
+    if (dgamma) dgamma[c] = (float)(sgx * invstd);
+    if (dbeta) dbeta[c] = (float)sg;
+  }
+  const double count = (double)d.N * d.HW;
+  const float k = gamma[c] * invstd;
+  const float mg = (float)(sg / count);
+  const float mx = (float)(sgx / count) * invstd * invstd;
+  bn1_visit(d, c, [&](size_t o, int n) {
+    if (n == 4) {
+      float4 gv = *reinterpret_cast<const float4*>(g + o);
+      const float4 xv = *reinterpret_cast<const float4*>(x + o);
+      if (relu) {
+        const float4 yv = *reinterpret_cast<const float4*>(y + o);
+        gv.x = yv.x > 0.f ? gv.x : 0.f;
+        gv.y = yv.y > 0.f ? gv.y : 0.f;
+        gv.z = yv.z > 0.f ? gv.z : 0.f;
+        gv.w = yv.w > 0.f ? gv.w : 0.f;
+      }
+      if (dr) *reinterpret_cast<float4*>(dr + o) = gv;
+      if (dx) {
+        float4 o4;
+        o4.x = k * (gv.x - mg - (xv.x - mean) * mx);
+        o4.y = k * (gv.y - mg - (xv.y - mean) * mx);
+        o4.z = k * (gv.z - mg - (xv.z - mean) * mx);
+        o4.w = k * (gv.w - mg - (xv.w - mean) * mx);
+        *reinterpret_cast<float4*>(dx + o) = o4;
+      }
+    } else {
+      float gv = g[o];
+      if (relu && !(y[o] > 0.f)) gv = 0.f;
+      if (dr) dr[o] = gv;
+      if (dx) dx[o] = k * (gv - mg - (x[o] - mean) * mx);
+    }
+  });
+}
+
 }  // namespace vfd
 
 using namespace vfd;
@@ -337,6 +509,33 @@ int vfd_bn_bwd_apply(const vfd_bn_desc* d, const float* g, const float* y, const
   bn_bwd_apply_k<<<dim3(d->S, d->C), BN_THREADS, 0, s>>>(*d, g, y, x, sums, ns, count, gamma, mean, invstd, dx,
                                                          dresidual, dgamma, dbeta);
   return fail_launch("bn_bwd_apply");
+}
+
+int vfd_bn1_fits(const vfd_bn_desc* d) {
+  return d && d->N > 0 && d->C > 0 && d->HW > 0 && (long long)d->N * d->HW <= (long long)BN1_MAX ? 1 : 0;
+}
+
+int vfd_bn1_fwd(const vfd_bn_desc* d, const float* x, const float* residual, const float* gamma, const float* beta,
+                float* y, float* mean, float* invstd, float* running_mean, float* running_var,
+                long long* num_batches_tracked, void* stream) {
+  VFD_REQUIRE(vfd_bn1_fits(d), "bn1_fwd: channel larger than %u elements", BN1_MAX);
+  VFD_REQUIRE(x && gamma && beta && y && mean && invstd && !running_mean == !running_var, "bn1_fwd: bad argument");
+  hipStream_t s = (hipStream_t)stream;
+  ProfScope ps(K_BN_FWD, s);
+  bn1_fwd_k<<<d->C, BN1_THREADS, 0, s>>>(*d, x, residual, gamma, beta, y, mean, invstd, running_mean, running_var,
+                                         num_batches_tracked);
+  return fail_launch("bn1_fwd");
+}
+
+int vfd_bn1_bwd(const vfd_bn_desc* d, const float* g, const float* y, const float* x, const float* gamma,
+                const float* mean, const float* invstd, float* dx, float* dresidual, float* dgamma, float* dbeta,
+                void* stream) {
+  VFD_REQUIRE(vfd_bn1_fits(d), "bn1_bwd: channel larger than %u elements", BN1_MAX);
+  VFD_REQUIRE(g && x && gamma && mean && invstd && (y || !d->relu), "bn1_bwd: bad argument");
+  hipStream_t s = (hipStream_t)stream;
+  ProfScope ps(K_BN_BWD, s);
+  bn1_bwd_k<<<d->C, BN1_THREADS, 0, s>>>(*d, g, y, x, gamma, mean, invstd, dx, dresidual, dgamma, dbeta);
+  return fail_launch("bn1_bwd");
 }
 
 }  // extern "C"

@@ -124,14 +124,19 @@ __device__ __forceinline__ float eup_row(const float* __restrict__ gr, const Eup
   return t;
 }
 
+// psum (optional): psum[p * gridDim.x + blockIdx.x] = the block's sum of dy over plane p (the
+// conv bias gradient's partials, summed in a fixed order by the caller: no ATen reduction pass)
 template <int UP, bool ACT>
 __global__ __launch_bounds__(256) void elu_up_pad_bwd_k(const float* __restrict__ g, const float* __restrict__ y,
-                                                        float* __restrict__ dy, long long planes, int h, int w) {
+                                                        float* __restrict__ dy, long long planes, int h, int w,
+                                                        float* __restrict__ psum) {
+  __shared__ float red[256 / 64];
   const int Hu = h << UP, Wu = w << UP;
   const int wo = Wu + 2;
   const int wq = (w + EPT - 1) / EPT;                        // thread groups per row
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= h * wq) return;
+  const int j0 = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = j0 < h * wq;                             // dead threads still join the block sums
+  const int j = live ? j0 : 0;
   const int sy = j / wq, sx0 = (j - sy * wq) * EPT;
   const EupIdx R = eup_idx<UP>(sy, h);
   const bool rmir = R.fma != 0.f || R.fmb != 0.f;           // rare: border rows
@@ -173,12 +178,24 @@ __global__ __launch_bounds__(256) void elu_up_pad_bwd_k(const float* __restrict_
       const float ov = elu1(v[e]);
       r[e] = !ACT ? s[e] : (ov <= 0.f ? s[e] * (ov + 1.f) : s[e]);
     }
-    if (vec) {
-      *reinterpret_cast<float4*>(dy + o) = make_float4(r[0], r[1], r[2], r[3]);
-    } else {
+    if (live) {
+      if (vec) {
+        *reinterpret_cast<float4*>(dy + o) = make_float4(r[0], r[1], r[2], r[3]);
+      } else {
 #pragma unroll
-      for (int e = 0; e < EPT; ++e)
-        if (sx0 + e < w) dy[o + e] = r[e];
+        for (int e = 0; e < EPT; ++e)
+          if (sx0 + e < w) dy[o + e] = r[e];
+      }
+    }
+    if (psum) {                                              // block-uniform branch
+      float t = 0.f;
+#pragma unroll
+      for (int e = 0; e < EPT; ++e) t += (live && sx0 + e < w) ? r[e] : 0.f;
+      t = wave_sum(t);
+      __syncthreads();
+      if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
+      __syncthreads();
+      if (threadIdx.x == 0) psum[p * gridDim.x + blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
     }
   }
 }
@@ -207,7 +224,7 @@ int vfd_reflect_pad1_bwd(const float* g, float* dx, long long planes, int h, int
   ProfScope ps(K_REFLECT_PAD, s);
   VFD_REQUIRE(planes / PPT < 65535, "reflect_pad1: too many planes");
   const dim3 grid((unsigned)((h * ((w + EPT - 1) / EPT) + 255) / 256), (unsigned)((planes + PPT - 1) / PPT));
-  elu_up_pad_bwd_k<0, false><<<grid, 256, 0, s>>>(g, nullptr, dx, planes, h, w);
+  elu_up_pad_bwd_k<0, false><<<grid, 256, 0, s>>>(g, nullptr, dx, planes, h, w, nullptr);
   return fail_launch("reflect_pad1_bwd");
 }
 
@@ -238,16 +255,18 @@ int vfd_elu_up_pad1_fwd(const float* y, float* out, long long planes, int h, int
   return fail_launch("elu_up_pad1_fwd");
 }
 
+int vfd_elu_up_pad1_bwd_blocks(int h, int w) { return (h * ((w + EPT - 1) / EPT) + 255) / 256; }
+
 int vfd_elu_up_pad1_bwd(const float* g, const float* y, float* dy, long long planes, int h, int w, int up,
-                        void* stream) {
+                        float* psum, void* stream) {
   VFD_REQUIRE(g && y && dy && planes > 0 && planes / PPT < 65535 && h >= 1 && w >= 1 && (up == 0 || up == 1) && (h << up) >= 2 &&
                   (w << up) >= 2 && (long long)((h << up) + 2) * ((w << up) + 2) < (1LL << 31),
               "elu_up_pad1: bad arguments (up in {0, 1}, padded side >= 2)");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_ELU_PAD, s);
   const dim3 grid((unsigned)((h * ((w + EPT - 1) / EPT) + 255) / 256), (unsigned)((planes + PPT - 1) / PPT));
-  if (up) elu_up_pad_bwd_k<1, true><<<grid, 256, 0, s>>>(g, y, dy, planes, h, w);
-  else elu_up_pad_bwd_k<0, true><<<grid, 256, 0, s>>>(g, y, dy, planes, h, w);
+  if (up) elu_up_pad_bwd_k<1, true><<<grid, 256, 0, s>>>(g, y, dy, planes, h, w, psum);
+  else elu_up_pad_bwd_k<0, true><<<grid, 256, 0, s>>>(g, y, dy, planes, h, w, psum);
   return fail_launch("elu_up_pad1_bwd");
 }
 

@@ -870,6 +870,9 @@ class AggregateUp(torch.autograd.Function):
 # =============================================================================================
 # Fused training-mode BatchNorm (+ residual) (+ ReLU) of the ResNet encoders (bnact.hip)
 # =============================================================================================
+_BN_ONE = os.environ.get('VFD_BN_ONE', '1') != '0'      # one-launch BN for small layers
+
+
 def _bn_group(bn):
     """SyncBatchNorm under an initialised process group of > 1 ranks -> that group, else None
     (nn.SyncBatchNorm itself falls back to the local batch norm at world size 1)."""
@@ -908,6 +911,20 @@ class BatchNormAct(torch.autograd.Function):
         d = L.BnDesc(N, C, H * W, 0, int(relu), float(eps), float(momentum))
         d.S = lib.vfd_bn_splits(ctypes.byref(d))
         r = residual.contiguous() if residual is not None else None
+        ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+        ctx.one = pg is None and _BN_ONE and bool(lib.vfd_bn1_fits(ctypes.byref(d)))
+        if ctx.one:       # small layer, local statistics: one launch (bnact.hip bn1_fwd_k)
+            y = torch.empty_like(x)
+            mean = torch.empty(C, device=x.device)
+            invstd = torch.empty(C, device=x.device)
+            L.check(lib.vfd_bn1_fwd(ctypes.byref(d), x.data_ptr(), ptr(r), gamma.data_ptr(), beta.data_ptr(),
+                                    y.data_ptr(), mean.data_ptr(), invstd.data_ptr(), ptr(running_mean),
+                                    ptr(running_var), ptr(nbt), L.stream()), 'bn1_fwd')
+            ctx.d, ctx.pg, ctx.count, ctx.has_res = (d.N, d.C, d.HW, d.S, d.relu, d.eps, d.momentum), pg, float(N * H * W), r is not None
+            if L.PROF_ON:
+                L.ALG_BYTES['bn_fwd'] += x.numel() * 4 * (2 + (r is not None))
+            ctx.save_for_backward(x, y, gamma, mean, invstd)
+            return y
         partial = torch.empty(C, d.S, 2, dtype=torch.float64, device=x.device)
         L.check(lib.vfd_bn_fwd_stats(ctypes.byref(d), x.data_ptr(), partial.data_ptr(), L.stream()), 'bn_fwd_stats')
         count, sums, ns = float(N * H * W), partial, d.S
@@ -935,6 +952,19 @@ class BatchNormAct(torch.autograd.Function):
         x, y, gamma, mean, invstd = ctx.saved_tensors
         d = L.BnDesc(*ctx.d)
         g = g.contiguous()
+        need = ctx.needs_input_grad
+        ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+        if ctx.one:
+            dx = torch.empty_like(x) if need[0] else None
+            dr = torch.empty_like(x) if ctx.has_res and need[3] else None
+            dgamma = torch.empty_like(gamma) if need[1] else None
+            dbeta = torch.empty_like(gamma) if need[2] else None
+            if L.PROF_ON:
+                L.ALG_BYTES['bn_bwd'] += x.numel() * 4 * (2 + d.relu + (dx is not None) + (dr is not None))
+            L.check(lib.vfd_bn1_bwd(ctypes.byref(d), g.data_ptr(), y.data_ptr() if d.relu else None, x.data_ptr(),
+                                    gamma.data_ptr(), mean.data_ptr(), invstd.data_ptr(), ptr(dx), ptr(dr),
+                                    ptr(dgamma), ptr(dbeta), L.stream()), 'bn1_bwd')
+            return dx, dgamma, dbeta, dr, None, None, None, None, None, None, None
         partial = torch.empty(d.C, d.S, 2, dtype=torch.float64, device=g.device)
         yp = y.data_ptr() if d.relu else None
         L.check(lib.vfd_bn_bwd_stats(ctypes.byref(d), g.data_ptr(), yp, x.data_ptr(), mean.data_ptr(),
@@ -997,33 +1027,70 @@ class EluUpPad(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, y, up):
-        lib = L.load()
-        _check_device(y, 'elu_up_pad input')
-        y = y.contiguous()
-        *lead, h, w = y.shape
-        u = 1 if up else 0
-        out = torch.empty(*lead, (h << u) + 2, (w << u) + 2, device=y.device)
-        planes = y.numel() // (h * w)
-        L.check(lib.vfd_elu_up_pad1_fwd(y.data_ptr(), out.data_ptr(), planes, h, w, u, L.stream()), 'elu_up_pad1_fwd')
-        if L.PROF_ON:
-            L.ALG_BYTES['elu_pad'] += (y.numel() + out.numel()) * 4
-        ctx.u = u
+        ctx.u = 1 if up else 0
         ctx.save_for_backward(y)
-        return out
+        return _elu_up_pad_fwd(y, ctx.u)
 
     @staticmethod
     def backward(ctx, g):
-        lib = L.load()
         y, = ctx.saved_tensors
-        g = g.contiguous()
-        h, w = y.shape[-2:]
-        dy = torch.empty_like(y)
-        planes = y.numel() // (h * w)
-        L.check(lib.vfd_elu_up_pad1_bwd(g.data_ptr(), y.data_ptr(), dy.data_ptr(), planes, h, w, ctx.u, L.stream()),
-                'elu_up_pad1_bwd')
-        if L.PROF_ON:
-            L.ALG_BYTES['elu_pad'] += (g.numel() + 2 * y.numel()) * 4
-        return dy, None
+        return _elu_up_pad_bwd(g, y, ctx.u)[0], None
+
+
+def _elu_up_pad_fwd(y, u):
+    lib = L.load()
+    _check_device(y, 'elu_up_pad input')
+    y = y.contiguous()
+    *lead, h, w = y.shape
+    out = torch.empty(*lead, (h << u) + 2, (w << u) + 2, device=y.device)
+    planes = y.numel() // (h * w)
+    L.check(lib.vfd_elu_up_pad1_fwd(y.data_ptr(), out.data_ptr(), planes, h, w, u, L.stream()), 'elu_up_pad1_fwd')
+    if L.PROF_ON:
+        L.ALG_BYTES['elu_pad'] += (y.numel() + out.numel()) * 4
+    return out
+
+
+def _elu_up_pad_bwd(g, y, u, bias_grad=False):
+    """d y of the fused ELU [+ up] + pad, and (bias_grad) the per-plane block partial sums of d y
+    [planes, blocks] (the producing conv's bias gradient before its fixed-order sum)."""
+    lib = L.load()
+    g = g.contiguous()
+    h, w = y.shape[-2:]
+    dy = torch.empty_like(y)
+    planes = y.numel() // (h * w)
+    psum = torch.empty(planes, lib.vfd_elu_up_pad1_bwd_blocks(h, w), device=y.device) if bias_grad else None
+    L.check(lib.vfd_elu_up_pad1_bwd(g.data_ptr(), y.data_ptr(), dy.data_ptr(), planes, h, w, u,
+                                    psum.data_ptr() if psum is not None else None, L.stream()), 'elu_up_pad1_bwd')
+    if L.PROF_ON:
+        L.ALG_BYTES['elu_pad'] += (g.numel() + 2 * y.numel()) * 4
+    return dy, psum
+
+
+class ConvEluUpPad(torch.autograd.Function):
+    """One decoder block (fusion_depthnet.py:97-145): the reflect conv 3x3 on an already padded
+    map xp (MIOpen, padding 0), then ELU [+ nearest 2x] + the next conv's reflect pad (HIP).  The
+    backward takes the conv's bias gradient from the ELU kernel's per-block sums (fixed order)
+    instead of an ATen reduction over d y, and asks MIOpen for the data / weight gradients only."""
+
+    @staticmethod
+    def forward(ctx, xp, weight, bias, up):
+        with torch.no_grad():
+            y = F.conv2d(xp, weight, bias)
+        ctx.u = 1 if up else 0
+        ctx.save_for_backward(xp, weight, y)
+        return _elu_up_pad_fwd(y, ctx.u)
+
+    @staticmethod
+    def backward(ctx, g):
+        xp, weight, y = ctx.saved_tensors
+        need = ctx.needs_input_grad
+        dy, psum = _elu_up_pad_bwd(g, y, ctx.u, bias_grad=need[2])
+        db = psum.view(y.shape[0], y.shape[1], -1).sum((0, 2)) if need[2] else None
+        dx = dw = None
+        if need[0] or need[1]:
+            dx, dw, _ = torch.ops.aten.convolution_backward(dy, xp, weight, None, [1, 1], [0, 0], [1, 1], False,
+                                                            [0, 0], 1, [need[0], need[1], False])
+        return dx, dw, db, None
 
 
 # =============================================================================================

@@ -89,9 +89,9 @@ class FusionDepthDecoder(nn.Module):
         xp = KN.ReflectPad1.apply(input_features[-1])
         for i in range(self.level_in, -1, -1):
             c0 = self.convs[('upconv', i, 0)][0]
-            xp = KN.EluUpPad.apply(F.conv2d(xp, c0.weight, c0.bias), True)
+            xp = KN.ConvEluUpPad.apply(xp, c0.weight, c0.bias, True)
             c1 = self.convs[('upconv', i, 1)][0]
-            xp = KN.EluUpPad.apply(F.conv2d(xp, c1.weight, c1.bias), False)
+            xp = KN.ConvEluUpPad.apply(xp, c1.weight, c1.bias, False)
             if i in self.scales:
                 cd = self.convs[('dispconv', i)][0]
                 out[('disp', i)] = self.sigmoid(F.conv2d(xp, cd.weight, cd.bias))

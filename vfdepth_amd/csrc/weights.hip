@@ -68,14 +68,29 @@ __global__ __launch_bounds__(256) void weight_frag_k(WrArgs a, const float* __re
   for (int k = 0; k < WR_TAPS; ++k) dst[off + (flip ? WR_TAPS - 1 - k : k) * plane] = v[k];
 }
 
+// swap as a tiled transpose of 16 x 16 (a, b) blocks of tap rows through LDS: both the reads
+// (16 rows of 16 * taps contiguous floats) and the writes are contiguous runs
+constexpr int WS_T = 16;
 __global__ __launch_bounds__(256) void weight_swap_k(const float* __restrict__ w, float* __restrict__ dst, int O,
-                                                     int A, int Bn, int taps) {
-  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;   // destination row (o, b, a)
-  if (t >= (long long)O * A * Bn) return;
-  const int ai = (int)(t % A), bi = (int)((t / A) % Bn), o = (int)(t / ((long long)A * Bn));
-  const float* p = w + (((long long)o * A + ai) * Bn + bi) * taps;
-  float* q = dst + t * taps;
-  for (int k = 0; k < taps; ++k) q[k] = p[k];
+                                                     int A, int Bn, int taps, int tiles_b) {
+  __shared__ float tile[WS_T * WS_T * WR_TAPS + WS_T];
+  const int o = blockIdx.y;
+  const int a0 = (blockIdx.x / tiles_b) * WS_T, b0 = (blockIdx.x % tiles_b) * WS_T;
+  const int t = threadIdx.x;
+  // read: row a0 + t / WS_T holds tap rows b0 .. b0 + 15 contiguously
+  for (int k = t; k < WS_T * WS_T * taps; k += 256) {
+    const int al = k / (WS_T * taps), rem = k - al * WS_T * taps;
+    const int bl = rem / taps, tp = rem - bl * taps;
+    const int a = a0 + al, b = b0 + bl;
+    if (a < A && b < Bn) tile[(al * WS_T + bl) * taps + tp] = w[(((size_t)o * A + a) * Bn + b) * taps + tp];
+  }
+  __syncthreads();
+  for (int k = t; k < WS_T * WS_T * taps; k += 256) {
+    const int bl = k / (WS_T * taps), rem = k - bl * WS_T * taps;
+    const int al = rem / taps, tp = rem - al * taps;
+    const int a = a0 + al, b = b0 + bl;
+    if (a < A && b < Bn) dst[(((size_t)o * Bn + b) * A + a) * taps + tp] = tile[(al * WS_T + bl) * taps + tp];
+  }
 }
 
 }  // namespace vfd
@@ -111,10 +126,11 @@ int vfd_weight_fragments(int mode, const float* w, float* dst, int O, int C, int
 }
 
 int vfd_weight_swap(const float* w, float* dst, int O, int A, int B, int taps, void* stream) {
-  VFD_REQUIRE(w && dst && O > 0 && A > 0 && B > 0 && taps > 0, "weight_swap: bad arguments");
+  VFD_REQUIRE(w && dst && O > 0 && O < 65536 && A > 0 && B > 0 && taps > 0 && taps <= WR_TAPS,
+              "weight_swap: bad arguments (taps <= %d)", WR_TAPS);
   hipStream_t s = (hipStream_t)stream;
-  const long long n = (long long)O * A * B;
-  weight_swap_k<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(w, dst, O, A, B, taps);
+  const int ta = (A + WS_T - 1) / WS_T, tb = (B + WS_T - 1) / WS_T;
+  weight_swap_k<<<dim3((unsigned)(ta * tb), (unsigned)O), 256, 0, s>>>(w, dst, O, A, B, taps, tb);
   return fail_launch("weight_swap");
 }
 

@@ -402,8 +402,24 @@ def pose_conv_fragments(w, C1, Z):
     return pad_conv_weight_fragments(w, C1, Z)
 
 
-def weight_swap(w, A, B):
-    """w [O, A*B, kh, kw] with channel a*B + b -> channel b*A + a (weights.hip, one launch)."""
+_SWAP_CACHE = {}
+
+
+def weight_swap(w, A, B, cache=False):
+    """w [O, A*B, kh, kw] with channel a*B + b -> channel b*A + a (weights.hip, one launch).
+    cache: reuse the last result for the same tensor and version (the pose weight, swapped once
+    per step for both pose calls' backward)."""
+    key = (w.data_ptr(), w._version, tuple(w.shape), A, B) if cache else None
+    if key is not None and key in _SWAP_CACHE:
+        return _SWAP_CACHE[key]
+    out = _weight_swap(w, A, B)
+    if key is not None:
+        _SWAP_CACHE.clear()
+        _SWAP_CACHE[key] = out
+    return out
+
+
+def _weight_swap(w, A, B):
     lib = L.load()
     w = _dev(w, 'conv weight').contiguous()
     O, _, kh, kw = w.shape
@@ -459,7 +475,7 @@ class PadConv(torch.autograd.Function):
         s = ctx.stride
         if ctx.perm:        # MIOpen works in the map's channel order: swap in, and the gradient back
             C1, Z = ctx.perm
-            w = weight_swap(w, C1, Z)
+            w = weight_swap(w, C1, Z, cache=True)
         dx, dw, db = torch.ops.aten.convolution_backward(g_pre, x, w, [w.shape[0]], [s, s], [0, 0], [1, 1],
                                                          False, [0, 0], 1, mask)
         if ctx.perm and dw is not None:

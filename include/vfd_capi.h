@@ -206,6 +206,19 @@ int vfd_bn1_bwd(const vfd_bn_desc* d, const float* g, const float* y, const floa
                 const float* mean, const float* invstd, float* dx, float* dresidual, float* dgamma, float* dbeta,
                 void* stream);
 
+/* ------------------------------------------------------------------ disparity head (dispconv.hip) */
+/* disp = sigmoid(conv3x3(xp) + b) for the decoder's full-resolution ('dispconv', 0) block
+ * (fusion_depthnet.py:117-118, 139-141): xp [N, 16, H+2, W+2] already reflect-padded, w [1, 16, 3, 3],
+ * out [N, 1, H, W].  Backward from g = d disp and the saved output: dxp [N, 16, H+2, W+2] (fully
+ * written; NULL to skip) and partial [vfd_disp_conv_wgrad_blocks][145] = per-block sums of the 144
+ * weight and the bias gradient terms (NULL to skip; the caller sums the blocks). */
+int vfd_disp_conv_supported(int N, int C, int H, int W);
+int vfd_disp_conv_wgrad_blocks(int N, int H, int W);
+int vfd_disp_conv_fwd(const float* xp, const float* w, const float* bias, float* out, int N, int C, int H, int W,
+                      void* stream);
+int vfd_disp_conv_bwd(const float* g, const float* out, const float* xp, const float* w, float* dxp, float* partial,
+                      int N, int C, int H, int W, void* stream);
+
 /* ------------------------------------------------------------------ weight relayouts (weights.hip) */
 /* Once-per-step copies of reduce_dim's first-conv weight w [O, C, 3, 3] for the MFMA kernels
  * (volumetric_fusionnet.py:59-60; replace ATen permute/flip/pad chains):

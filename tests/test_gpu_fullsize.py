@@ -679,6 +679,28 @@ def test_weight_relayouts_match_torch_chains():
         assert torch.equal(KN.weight_swap(wz, Z, C1), wp)
 
 
+def test_disp_conv_matches_aten():
+    """The full-resolution disparity head sigmoid(conv3x3(xp) + b) (16 -> 1 channels, padded input)
+    against F.conv2d + sigmoid: output, d xp, d w, d b, at the config-2 shape and a ragged one."""
+    from vfdepth_amd import kernels as KN
+    gen = torch.Generator(device=DEV).manual_seed(23)
+    for shape in ((6, 16, 386, 642), (2, 16, 9, 14)):
+        xp = torch.randn(shape, device=DEV, generator=gen).requires_grad_(True)
+        w = (0.1 * torch.randn(1, 16, 3, 3, device=DEV, generator=gen)).requires_grad_(True)
+        b = torch.randn(1, device=DEV, generator=gen).requires_grad_(True)
+        assert KN.DispConvSigmoid.supported(xp, w)
+        out = KN.DispConvSigmoid.apply(xp, w, b)
+        xr, wr, br = (t.detach().clone().requires_grad_(True) for t in (xp, w, b))
+        ref = torch.sigmoid(F.conv2d(xr, wr, br))
+        close(out, ref, f'disp conv {shape}', atol=1e-6, rtol=1e-5)
+        g = torch.randn(out.shape, device=DEV, generator=gen)
+        out.backward(g)
+        ref.backward(g)
+        close(xp.grad, xr.grad, f'disp conv d xp {shape}', atol=1e-6, rtol=1e-5)
+        close(w.grad, wr.grad, f'disp conv d w {shape}', atol=1e-3 * float(wr.grad.abs().max()), rtol=1e-4)
+        close(b.grad, br.grad, f'disp conv d b {shape}', atol=1e-3 * float(br.grad.abs().max()), rtol=1e-4)
+
+
 def test_stem_max_pool_matches_aten():
     """MaxPool2d(3, 2, 1) with the one-byte argmax: forward bit-identical to ATen (ties of a ReLU
     map's zeros go to the first maximum in scan order), backward equal to ATen's (fixed-order sum of

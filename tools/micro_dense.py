@@ -64,7 +64,7 @@ def main():
         dyy = torch.empty_like(yy)
         nbe = (yy.numel() + op.numel()) * 4
         line(f'elu_up_pad fwd {shape} up={up}', timeit(lambda: lib.vfd_elu_up_pad1_fwd(yy.data_ptr(), op.data_ptr(), n * c, h, w, up, L.stream())), nbe)
-        line(f'elu_up_pad bwd {shape} up={up}', timeit(lambda: lib.vfd_elu_up_pad1_bwd(op.data_ptr(), yy.data_ptr(), dyy.data_ptr(), n * c, h, w, up, L.stream())), nbe + yy.numel() * 4)
+        line(f'elu_up_pad bwd {shape} up={up}', timeit(lambda: lib.vfd_elu_up_pad1_bwd(op.data_ptr(), yy.data_ptr(), dyy.data_ptr(), n * c, h, w, up, None, L.stream())), nbe + yy.numel() * 4)
 
         def aten_chain():
             a = F.elu(yy)
@@ -72,6 +72,16 @@ def main():
                 a = F.interpolate(a, scale_factor=2, mode='nearest')
             return F.pad(a, (1, 1, 1, 1), mode='reflect')
         line(f'  ATen elu->up->pad fwd {shape}', timeit(aten_chain), nbe)
+    # decoder disparity head 16 -> 1 at full resolution vs MIOpen
+    xpd = torch.randn(6, 16, 386, 642, device=dev, requires_grad=True)
+    wd = (0.1 * torch.randn(1, 16, 3, 3, device=dev)).requires_grad_(True)
+    bd = torch.zeros(1, device=dev, requires_grad=True)
+    od = KN.DispConvSigmoid.apply(xpd, wd, bd)
+    gd = torch.randn_like(od)
+    line('disp conv fwd (HIP)', timeit(lambda: KN.DispConvSigmoid.apply(xpd, wd, bd)), xpd.numel() * 4)
+    line('disp conv fwd+bwd (HIP)', timeit(lambda: torch.autograd.grad(KN.DispConvSigmoid.apply(xpd, wd, bd), (xpd, wd, bd), gd)), xpd.numel() * 12)
+    line('disp conv fwd (MIOpen)', timeit(lambda: torch.sigmoid(F.conv2d(xpd, wd, bd))), xpd.numel() * 4)
+    line('disp conv fwd+bwd (MIOpen)', timeit(lambda: torch.autograd.grad(torch.sigmoid(F.conv2d(xpd, wd, bd)), (xpd, wd, bd), gd)), xpd.numel() * 12)
     d = torch.randn(6, 256, 48, 80, device=dev)
     for hs, ws in ((24, 40), (12, 20), (6, 10)):
         dl = torch.empty(6, 256, hs, ws, device=dev)

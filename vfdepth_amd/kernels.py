@@ -1109,6 +1109,58 @@ class ConvEluUpPad(torch.autograd.Function):
         return dx, dw, db, None
 
 
+class DispConvSigmoid(torch.autograd.Function):
+    """sigmoid(conv3x3(xp) + b) for the decoder's full-resolution disparity head (16 -> 1 channels,
+    xp already reflect-padded): one HIP sweep forward, one data-gradient and one weight/bias
+    gradient sweep backward (dispconv.hip) instead of MIOpen's one-output-channel solvers."""
+
+    @staticmethod
+    def supported(xp, weight):
+        N, C, Hp, Wp = xp.shape
+        return (xp.is_cuda and xp.dtype == torch.float32 and tuple(weight.shape) == (1, C, 3, 3)
+                and bool(L.load().vfd_disp_conv_supported(N, C, Hp - 2, Wp - 2)))
+
+    @staticmethod
+    def forward(ctx, xp, weight, bias):
+        lib = L.load()
+        xp = _dev(xp, 'disp conv input')
+        w = weight.contiguous()
+        N, C, Hp, Wp = xp.shape
+        H, W = Hp - 2, Wp - 2
+        out = torch.empty(N, 1, H, W, device=xp.device)
+        L.check(lib.vfd_disp_conv_fwd(xp.data_ptr(), w.data_ptr(), bias.data_ptr(), out.data_ptr(), N, C, H, W,
+                                      L.stream()), 'disp_conv_fwd')
+        if L.PROF_ON:
+            L.ALG_BYTES['disp_conv'] += (xp.numel() + out.numel()) * 4
+        ctx.save_for_backward(xp, w, out)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        lib = L.load()
+        xp, w, out = ctx.saved_tensors
+        g = g.contiguous()
+        N, C, Hp, Wp = xp.shape
+        H, W = Hp - 2, Wp - 2
+        need = ctx.needs_input_grad
+        dxp = torch.empty_like(xp) if need[0] else None
+        part = (torch.empty(lib.vfd_disp_conv_wgrad_blocks(N, H, W), C * 9 + 1, device=xp.device)
+                if need[1] or need[2] else None)
+        L.check(lib.vfd_disp_conv_bwd(g.data_ptr(), out.data_ptr(), xp.data_ptr(), w.data_ptr(),
+                                      dxp.data_ptr() if dxp is not None else None,
+                                      part.data_ptr() if part is not None else None, N, C, H, W, L.stream()),
+                'disp_conv_bwd')
+        if L.PROF_ON:
+            L.ALG_BYTES['disp_conv'] += (2 * out.numel() + (dxp is not None) * xp.numel()
+                                         + (part is not None) * xp.numel()) * 4
+        dw = db = None
+        if part is not None:
+            tot = part.sum(0)
+            dw = tot[:C * 9].view(1, C, 3, 3) if need[1] else None
+            db = tot[C * 9:] if need[2] else None
+        return dxp, dw, db
+
+
 # =============================================================================================
 # ResNet stem max pool (3x3, stride 2, padding 1) with a one-byte argmax and a gather backward
 # =============================================================================================

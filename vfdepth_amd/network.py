@@ -94,7 +94,10 @@ class FusionDepthDecoder(nn.Module):
             xp = KN.ConvEluUpPad.apply(xp, c1.weight, c1.bias, False)
             if i in self.scales:
                 cd = self.convs[('dispconv', i)][0]
-                out[('disp', i)] = self.sigmoid(F.conv2d(xp, cd.weight, cd.bias))
+                if KN.DispConvSigmoid.supported(xp, cd.weight) and cd.bias is not None:
+                    out[('disp', i)] = KN.DispConvSigmoid.apply(xp, cd.weight, cd.bias)
+                else:
+                    out[('disp', i)] = self.sigmoid(F.conv2d(xp, cd.weight, cd.bias))
         return out
 
     def forward(self, input_features):

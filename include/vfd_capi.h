@@ -219,6 +219,19 @@ int vfd_disp_conv_fwd(const float* xp, const float* w, const float* bias, float*
 int vfd_disp_conv_bwd(const float* g, const float* out, const float* xp, const float* w, float* dxp, float* partial,
                       int N, int C, int H, int W, void* stream);
 
+/* ------------------------------------------------------------------ decoder convs (decconv.hip) */
+/* The decoder's narrow reflect 3x3 convs (fusion_depthnet.py:97-145 upconv blocks, CI, CO in {16, 32},
+ * W % 16 == 0) on fp32 MFMA (v_mfma_f32_16x16x4_f32), input already reflect-padded:
+ * y [N, CO, H, W] = conv(xp [N, CI, H+2, W+2], w [CO, CI, 3, 3]) + b.  Backward from dy: dxp (all
+ * padded positions; NULL to skip) and partial [vfd_dec_conv_wgrad_blocks][CO][CI][9] per-block weight
+ * gradient sums (NULL to skip; the caller sums the blocks, bias gradient from the ELU kernel). */
+int vfd_dec_conv_supported(int N, int CI, int CO, int H, int W);
+int vfd_dec_conv_wgrad_blocks(int N, int H, int W);
+int vfd_dec_conv_fwd(const float* xp, const float* w, const float* bias, float* y, int N, int CI, int CO, int H, int W,
+                     void* stream);
+int vfd_dec_conv_bwd(const float* dy, const float* xp, const float* w, float* dxp, float* partial, int N, int CI, int CO,
+                     int H, int W, void* stream);
+
 /* ------------------------------------------------------------------ weight relayouts (weights.hip) */
 /* Once-per-step copies of reduce_dim's first-conv weight w [O, C, 3, 3] for the MFMA kernels
  * (volumetric_fusionnet.py:59-60; replace ATen permute/flip/pad chains):

@@ -701,6 +701,32 @@ def test_disp_conv_matches_aten():
         close(b.grad, br.grad, f'disp conv d b {shape}', atol=1e-3 * float(br.grad.abs().max()), rtol=1e-4)
 
 
+@pytest.mark.parametrize('shape,co,up', [((6, 16, 386, 642), 16, False), ((6, 32, 194, 322), 16, True),
+                                         ((6, 32, 194, 322), 32, False), ((2, 16, 9, 18), 32, True)])
+def test_decoder_conv_mfma_matches_aten(shape, co, up):
+    """A decoder block on the MFMA conv (decconv.hip) + fused ELU/up/pad against F.conv2d ->
+    F.elu -> F.interpolate -> F.pad(reflect): output, d xp, d w, d b (config-2 decoder shapes)."""
+    from vfdepth_amd import kernels as KN
+    gen = torch.Generator(device=DEV).manual_seed(31)
+    ci = shape[1]
+    xp = torch.randn(shape, device=DEV, generator=gen).requires_grad_(True)
+    w = (torch.randn(co, ci, 3, 3, device=DEV, generator=gen) / (3 * ci ** 0.5)).requires_grad_(True)
+    b = (0.1 * torch.randn(co, device=DEV, generator=gen)).requires_grad_(True)
+    out = KN.ConvEluUpPad.apply(xp, w, b, up)
+    xr, wr, br = (t.detach().clone().requires_grad_(True) for t in (xp, w, b))
+    ref = F.elu(F.conv2d(xr, wr, br))
+    if up:
+        ref = F.interpolate(ref, scale_factor=2, mode='nearest')
+    ref = F.pad(ref, (1, 1, 1, 1), mode='reflect')
+    close(out, ref, f'dec conv {shape}->{co}', atol=1e-5, rtol=1e-4)
+    g = torch.randn(out.shape, device=DEV, generator=gen)
+    out.backward(g)
+    ref.backward(g)
+    close(xp.grad, xr.grad, f'dec conv d xp {shape}', atol=1e-5 * float(xr.grad.abs().max()), rtol=1e-4)
+    close(w.grad, wr.grad, f'dec conv d w {shape}', atol=1e-4 * float(wr.grad.abs().max()), rtol=1e-4)
+    close(b.grad, br.grad, f'dec conv d b {shape}', atol=1e-4 * float(br.grad.abs().max()), rtol=1e-4)
+
+
 def test_stem_max_pool_matches_aten():
     """MaxPool2d(3, 2, 1) with the one-byte argmax: forward bit-identical to ATen (ties of a ReLU
     map's zeros go to the first maximum in scan order), backward equal to ATen's (fixed-order sum of

@@ -887,6 +887,7 @@ class AggregateUp(torch.autograd.Function):
 # Fused training-mode BatchNorm (+ residual) (+ ReLU) of the ResNet encoders (bnact.hip)
 # =============================================================================================
 _BN_ONE = os.environ.get('VFD_BN_ONE', '1') != '0'      # one-launch BN for small layers
+_DEC_CONV = os.environ.get('VFD_DEC_CONV', '1') != '0'   # decoder's narrow convs on MFMA (decconv.hip)
 
 
 def _bn_group(bn):
@@ -1090,8 +1091,21 @@ class ConvEluUpPad(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, xp, weight, bias, up):
-        with torch.no_grad():
-            y = F.conv2d(xp, weight, bias)
+        lib = L.load()
+        N, CI, Hp, Wp = xp.shape
+        CO = weight.shape[0]
+        ctx.mfma = (_DEC_CONV and bias is not None and xp.is_contiguous()
+                    and bool(lib.vfd_dec_conv_supported(N, CI, CO, Hp - 2, Wp - 2)))
+        if ctx.mfma:      # decconv.hip: the narrow conv on fp32 MFMA
+            w = weight.detach().contiguous()
+            y = torch.empty(N, CO, Hp - 2, Wp - 2, device=xp.device)
+            L.check(lib.vfd_dec_conv_fwd(xp.data_ptr(), w.data_ptr(), bias.data_ptr(), y.data_ptr(), N, CI, CO,
+                                         Hp - 2, Wp - 2, L.stream()), 'dec_conv_fwd')
+            if L.PROF_ON:
+                L.ALG_BYTES['dec_conv'] += (xp.numel() + y.numel()) * 4
+        else:
+            with torch.no_grad():
+                y = F.conv2d(xp, weight, bias)
         ctx.u = 1 if up else 0
         ctx.save_for_backward(xp, weight, y)
         return _elu_up_pad_fwd(y, ctx.u)
@@ -1103,7 +1117,24 @@ class ConvEluUpPad(torch.autograd.Function):
         dy, psum = _elu_up_pad_bwd(g, y, ctx.u, bias_grad=need[2])
         db = psum.view(y.shape[0], y.shape[1], -1).sum((0, 2)) if need[2] else None
         dx = dw = None
-        if need[0] or need[1]:
+        N, CI, Hp, Wp = xp.shape
+        CO = weight.shape[0]
+        # the backward on MFMA where it beats MIOpen (tools/micro_decconv.py): 16 output channels
+        if ctx.mfma and CO == 16 and (need[0] or need[1]):
+            lib = L.load()
+            w = weight.detach().contiguous()
+            dx = torch.empty_like(xp) if need[0] else None
+            part = (torch.empty(lib.vfd_dec_conv_wgrad_blocks(N, Hp - 2, Wp - 2), CO, CI, 9, device=xp.device)
+                    if need[1] else None)
+            L.check(lib.vfd_dec_conv_bwd(dy.data_ptr(), xp.data_ptr(), w.data_ptr(),
+                                         dx.data_ptr() if dx is not None else None,
+                                         part.data_ptr() if part is not None else None, N, CI, CO, Hp - 2, Wp - 2,
+                                         L.stream()), 'dec_conv_bwd')
+            if L.PROF_ON:
+                L.ALG_BYTES['dec_conv'] += (dy.numel() + (dx is not None) * xp.numel()
+                                            + (part is not None) * (dy.numel() + xp.numel())) * 4
+            dw = part.sum(0).view(CO, CI, 3, 3) if part is not None else None
+        elif need[0] or need[1]:
             dx, dw, _ = torch.ops.aten.convolution_backward(dy, xp, weight, None, [1, 1], [0, 0], [1, 1], False,
                                                             [0, 0], 1, [need[0], need[1], False])
         return dx, dw, db, None

@@ -221,7 +221,7 @@ int vfd_disp_conv_bwd(const float* g, const float* out, const float* xp, const f
 
 /* ------------------------------------------------------------------ decoder convs (decconv.hip) */
 /* The decoder's narrow reflect 3x3 convs (fusion_depthnet.py:97-145 upconv blocks, CI, CO in {16, 32},
- * W % 16 == 0) on fp32 MFMA (v_mfma_f32_16x16x4_f32), input already reflect-padded:
+ * W % 64 == 0) on fp32 MFMA (v_mfma_f32_16x16x4_f32), input already reflect-padded:
  * y [N, CO, H, W] = conv(xp [N, CI, H+2, W+2], w [CO, CI, 3, 3]) + b.  Backward from dy: dxp (all
  * padded positions; NULL to skip) and partial [vfd_dec_conv_wgrad_blocks][CO][CI][9] per-block weight
  * gradient sums (NULL to skip; the caller sums the blocks, bias gradient from the ELU kernel). */

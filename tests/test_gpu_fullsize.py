@@ -702,7 +702,8 @@ def test_disp_conv_matches_aten():
 
 
 @pytest.mark.parametrize('shape,co,up', [((6, 16, 386, 642), 16, False), ((6, 32, 194, 322), 16, True),
-                                         ((6, 32, 194, 322), 32, False), ((2, 16, 9, 18), 32, True)])
+                                         ((6, 32, 194, 322), 32, False), ((2, 16, 9, 66), 32, True),
+                                         ((2, 16, 5, 130), 16, False)])
 def test_decoder_conv_mfma_matches_aten(shape, co, up):
     """A decoder block on the MFMA conv (decconv.hip) + fused ELU/up/pad against F.conv2d ->
     F.elu -> F.interpolate -> F.pad(reflect): output, d xp, d w, d b (config-2 decoder shapes)."""

@@ -136,21 +136,35 @@ __global__ __launch_bounds__(DK_THREADS) void dconv_dgrad_k(const float* __restr
   }
 }
 
-// weight gradient: a block walks a contiguous range of 4-pixel groups (rows of W % 4 == 0); each
-// wave accumulates dW tiles for all taps in registers; waves are combined in LDS in wave order and
-// the block writes partial[block][CO][CI][9]
+// weight gradient: a block walks strips of 64 consecutive output pixels of one row (W % 64 == 0).
+// A strip's xp rows (3 x 66 columns x CI) and dy (CO x 64) are staged in LDS with coalesced loads
+// (the MFMA operands are channel-strided: read straight from global memory every 16-lane group
+// touches 16 planes); the next strip's loads are issued into registers before the current strip's
+// MFMAs.  Each wave owns 16 of the strip's pixels (4 k-steps) and keeps the dW tiles of all taps
+// in registers; waves are combined in LDS in wave order and the block writes
+// partial[block][CO][CI][9].
+constexpr int DW_S = 64;                        // pixels per strip
+constexpr int DW_XS = DW_S + 3;                 // LDS row stride of the xp rows (66 used; bank spread)
+constexpr int DW_GS = DW_S + 1;                 // LDS row stride of dy
+
 template <int CI, int CO>
 __global__ __launch_bounds__(DK_THREADS) void dconv_wgrad_k(const float* __restrict__ dy, const float* __restrict__ xp,
                                                             float* __restrict__ partial, int N, int H, int W,
-                                                            long long groups_per_block) {
+                                                            long long strips_per_block) {
   constexpr int NO = CO / 16, NC = CI / 16;
-  __shared__ float red[CO * CI * 9];
+  constexpr int XN = CI * 3 * (DW_S + 2), GN = CO * DW_S;           // staged floats
+  constexpr int XPT = (XN + DK_THREADS - 1) / DK_THREADS, GPT = (GN + DK_THREADS - 1) / DK_THREADS;
+  constexpr int LDS0 = CI * 3 * DW_XS + CO * DW_GS;
+  constexpr int LDS = LDS0 > CO * CI * 9 ? LDS0 : CO * CI * 9;   // staging, then the wave reduction
+  __shared__ float lds[LDS];
+  float* xs = lds;
+  float* gs = lds + CI * 3 * DW_XS;
   const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4, wv = threadIdx.x >> 6;
   const int wp = W + 2, hp = H + 2;
-  const int gpr = W / 4;                                      // 4-pixel groups per row
-  const long long ngroup = (long long)N * H * gpr;
-  const long long g0 = (long long)blockIdx.x * groups_per_block;
-  const long long g1 = g0 + groups_per_block < ngroup ? g0 + groups_per_block : ngroup;
+  const int spr = W / DW_S;
+  const long long nstrip = (long long)N * H * spr;
+  const long long s0 = (long long)blockIdx.x * strips_per_block;
+  const long long s1 = s0 + strips_per_block < nstrip ? s0 + strips_per_block : nstrip;
   f32x4 acc[NO][9][NC];
 #pragma unroll
   for (int a = 0; a < NO; ++a)
@@ -158,28 +172,66 @@ __global__ __launch_bounds__(DK_THREADS) void dconv_wgrad_k(const float* __restr
     for (int tap = 0; tap < 9; ++tap)
 #pragma unroll
       for (int b = 0; b < NC; ++b) acc[a][tap][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (long long g = g0 + wv; g < g1; g += DK_THREADS / 64) {
-    const int x0 = (int)(g % gpr) * 4;
-    const int yy = (int)((g / gpr) % H), n = (int)(g / ((long long)gpr * H));
-    // A[i = o][k = pixel x0 + k] = dy[o][yy][x0 + k]
-    float av[NO];
+  float rx[XPT], rg[GPT];
+  auto fetch = [&](long long s) {               // strip s -> registers (coalesced along columns)
+    const int x0 = (int)(s % spr) * DW_S;
+    const int yy = (int)((s / spr) % H), n = (int)(s / ((long long)spr * H));
 #pragma unroll
-    for (int a = 0; a < NO; ++a) av[a] = dy[(((size_t)n * CO + 16 * a + li) * H + yy) * W + x0 + lk];
-    // B[k = pixel][j = c] = xp[c][yy + ky][x0 + k + kx]
-    const float* xb = xp + (((size_t)n * CI + li) * hp + yy) * wp + x0 + lk;
+    for (int i = 0; i < XPT; ++i) {
+      const int k = threadIdx.x + i * DK_THREADS;
+      const int kk = k < XN ? k : 0;
+      const int col = kk % (DW_S + 2), row = kk / (DW_S + 2);            // row = c * 3 + ky
+      const int c = row / 3, ky = row - 3 * c;
+      rx[i] = xp[(((size_t)n * CI + c) * hp + yy + ky) * wp + x0 + col];
+    }
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const int ky = tap / 3, kx = tap - 3 * ky;
-      float bv[NC];
+    for (int i = 0; i < GPT; ++i) {
+      const int k = threadIdx.x + i * DK_THREADS;
+      const int kk = k < GN ? k : 0;
+      const int col = kk % DW_S, o = kk / DW_S;
+      rg[i] = dy[(((size_t)n * CO + o) * H + yy) * W + x0 + col];
+    }
+  };
+  auto stage = [&]() {
 #pragma unroll
-      for (int b = 0; b < NC; ++b) bv[b] = xb[((size_t)(16 * b) * hp + ky) * wp + kx];
+    for (int i = 0; i < XPT; ++i) {
+      const int k = threadIdx.x + i * DK_THREADS;
+      if (k < XN) xs[(k / (DW_S + 2)) * DW_XS + k % (DW_S + 2)] = rx[i];
+    }
 #pragma unroll
-      for (int a = 0; a < NO; ++a)
+    for (int i = 0; i < GPT; ++i) {
+      const int k = threadIdx.x + i * DK_THREADS;
+      if (k < GN) gs[(k / DW_S) * DW_GS + k % DW_S] = rg[i];
+    }
+  };
+  if (s0 < s1) fetch(s0);
+  for (long long s = s0; s < s1; ++s) {
+    __syncthreads();                            // the previous strip's operands are consumed
+    stage();
+    __syncthreads();
+    if (s + 1 < s1) fetch(s + 1);               // in flight during this strip's MFMAs
 #pragma unroll
-        for (int b = 0; b < NC; ++b) acc[a][tap][b] = mfma16(av[a], bv[b], acc[a][tap][b]);
+    for (int ks = 0; ks < 4; ++ks) {
+      const int px = 16 * wv + 4 * ks + lk;     // this lane's k (pixel of the strip)
+      float av[NO];
+#pragma unroll
+      for (int a = 0; a < NO; ++a) av[a] = gs[(16 * a + li) * DW_GS + px];          // A[i = o][k]
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int ky = tap / 3, kx = tap - 3 * ky;
+        float bv[NC];
+#pragma unroll
+        for (int b = 0; b < NC; ++b) bv[b] = xs[((16 * b + li) * 3 + ky) * DW_XS + px + kx];   // B[k][j = c]
+#pragma unroll
+        for (int a = 0; a < NO; ++a)
+#pragma unroll
+          for (int b = 0; b < NC; ++b) acc[a][tap][b] = mfma16(av[a], bv[b], acc[a][tap][b]);
+      }
     }
   }
   // D[i = o (row)][j = c (column)]: lane holds o = 16 a + 4 lk + r, c = 16 b + li
+  float* red = lds;
+  __syncthreads();
   for (int w = 0; w < DK_THREADS / 64; ++w) {
     if (wv == w) {
 #pragma unroll
@@ -216,7 +268,7 @@ extern "C" {
 
 int vfd_dec_conv_supported(int N, int CI, int CO, int H, int W) {
   const bool ch = (CI == 16 || CI == 32) && (CO == 16 || CO == 32);
-  return N > 0 && ch && H > 0 && W > 0 && W % 16 == 0 && (long long)N * (CI > CO ? CI : CO) * (H + 2) * (W + 2) < (1LL << 31);
+  return N > 0 && ch && H > 0 && W > 0 && W % 64 == 0 && (long long)N * (CI > CO ? CI : CO) * (H + 2) * (W + 2) < (1LL << 31);
 }
 
 int vfd_dec_conv_wgrad_blocks(int N, int H, int W) { (void)N; (void)H; (void)W; return dk_blocks() / 4; }
@@ -231,7 +283,7 @@ int vfd_dec_conv_wgrad_blocks(int N, int H, int W) { (void)N; (void)H; (void)W; 
 
 int vfd_dec_conv_fwd(const float* xp, const float* w, const float* bias, float* y, int N, int CI, int CO, int H, int W,
                      void* stream) {
-  VFD_REQUIRE(vfd_dec_conv_supported(N, CI, CO, H, W), "dec_conv: unsupported shape (CI, CO in {16, 32}, W %% 16 == 0)");
+  VFD_REQUIRE(vfd_dec_conv_supported(N, CI, CO, H, W), "dec_conv: unsupported shape (CI, CO in {16, 32}, W %% 64 == 0)");
   VFD_REQUIRE(xp && w && bias && y && ((uintptr_t)y & 15) == 0, "dec_conv_fwd: bad argument");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_DEC_CONV, s);
@@ -244,7 +296,7 @@ int vfd_dec_conv_fwd(const float* xp, const float* w, const float* bias, float* 
 
 int vfd_dec_conv_bwd(const float* dy, const float* xp, const float* w, float* dxp, float* partial, int N, int CI, int CO,
                      int H, int W, void* stream) {
-  VFD_REQUIRE(vfd_dec_conv_supported(N, CI, CO, H, W), "dec_conv: unsupported shape (CI, CO in {16, 32}, W %% 16 == 0)");
+  VFD_REQUIRE(vfd_dec_conv_supported(N, CI, CO, H, W), "dec_conv: unsupported shape (CI, CO in {16, 32}, W %% 64 == 0)");
   VFD_REQUIRE(dy && w && (!partial || xp), "dec_conv_bwd: bad argument");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_DEC_CONV, s);
@@ -255,9 +307,10 @@ int vfd_dec_conv_bwd(const float* dy, const float* xp, const float* w, float* dx
     DK_DISPATCH(dconv_dgrad_k, dy, w, dxp, N, H, W);
   }
   if (partial) {
+    VFD_REQUIRE(W % DW_S == 0, "dec_conv_bwd: weight gradient needs W %% %d == 0", DW_S);
     const unsigned grid = (unsigned)vfd_dec_conv_wgrad_blocks(N, H, W);
-    const long long ngroup = (long long)N * H * (W / 4);
-    const long long per = (ngroup + grid - 1) / grid;
+    const long long nstrip = (long long)N * H * (W / DW_S);
+    const long long per = (nstrip + grid - 1) / grid;
     DK_DISPATCH(dconv_wgrad_k, dy, xp, partial, N, H, W, per);
   }
   return fail_launch("dec_conv_bwd");

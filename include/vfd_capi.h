@@ -244,6 +244,10 @@ int vfd_weight_fragments(int mode, const float* w, float* dst, int O, int C, int
 /* dst[o][b][a][t] = w[o][a][b][t] (w [O][A][B][taps]): the pose weight between the reference channel
  * order c*Z + z (A = C1, B = Z) and K2's map order z*C1 + c, and back for its gradient. */
 int vfd_weight_swap(const float* w, float* dst, int O, int A, int B, int taps, void* stream);
+/* Element (o, a, b, t) (t < T <= 9) copied from w[o*s0 + a*s1 + b*s2 + t*s3] to dst[o*d0 + a*d1 + b*d2 + t*d3]
+ * (strides in floats): the swap between any NCHW / channels-last pair of layouts. */
+int vfd_weight_permute(const float* w, float* dst, int O, int A, int B, int T, const long long* src_strides,
+                       const long long* dst_strides, void* stream);
 
 /* ELU(alpha 1) [+ nearest 2x upsample (up = 1)] + the one-pixel reflect pad, NCHW fp32: the
  * decoders' conv -> ELU -> upsample -> next reflect conv chain (fusion_depthnet.py:97-145,

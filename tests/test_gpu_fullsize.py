@@ -677,6 +677,10 @@ def test_weight_relayouts_match_torch_chains():
         assert torch.equal(KN.pad_conv_weight_fragments(wz), ref)
         assert torch.equal(KN.weight_swap(wp, C1, Z), wz)
         assert torch.equal(KN.weight_swap(wz, Z, C1), wp)
+        cl = torch.channels_last
+        sw = KN.weight_swap(wp, C1, Z, memory_format=cl)            # NCHW -> channels-last
+        assert sw.is_contiguous(memory_format=cl) and torch.equal(sw, wz)
+        assert torch.equal(KN.weight_swap(wz.contiguous(memory_format=cl), Z, C1), wp)   # and back
 
 
 def test_disp_conv_matches_aten():

@@ -110,6 +110,7 @@ _SIGS = {
     'vfd_dec_conv_bwd': (c_int, [c_fp] * 5 + [c_int] * 5 + [c_void_p]),
     'vfd_weight_fragments': (c_int, [c_int, c_fp, c_fp] + [c_int] * 6 + [c_void_p]),
     'vfd_weight_swap': (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_void_p]),
+    'vfd_weight_permute': (c_int, [c_fp, c_fp] + [c_int] * 4 + [ctypes.POINTER(ctypes.c_longlong)] * 2 + [c_void_p]),
     'vfd_elu_up_pad1_fwd': (c_int, [c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_int, c_void_p]),
     'vfd_elu_up_pad1_bwd': (c_int, [c_fp, c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_int, c_fp, c_void_p]),
     'vfd_elu_up_pad1_bwd_blocks': (c_int, [c_int, c_int]),

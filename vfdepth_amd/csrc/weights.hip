@@ -13,8 +13,9 @@
 //           (projconv.hip pcv_main_k; reference channel c*D + d, :261-265)
 //   mode 2  K3C data-gradient copy  dst[8 - tap][oq][n][h][s] = w[4oq + 2h + s][c*D + d][tap]
 //           (projconv.hip pcd_main_k; n = d*Cv + c, zero for n >= Cv*D)
-//   swap    dst[o][b][a][t] = w[o][a][b][t]: the pose weight between the reference channel order
-//           (c*Z + z) and the map's (z*C1 + c), for MIOpen's data / weight gradients
+//   permute element (o, a, b, t) between any two strided layouts (the pose weight between the
+//           reference channel order c*Z + z and the map's z*C1 + c, NCHW or channels-last for MIOpen);
+//           swap = the NCHW -> NCHW instance dst[o][b][a][t] = w[o][a][b][t]
 #include "vfd_common.h"
 
 namespace vfd {
@@ -68,28 +69,54 @@ __global__ __launch_bounds__(256) void weight_frag_k(WrArgs a, const float* __re
   for (int k = 0; k < WR_TAPS; ++k) dst[off + (flip ? WR_TAPS - 1 - k : k) * plane] = v[k];
 }
 
-// swap as a tiled transpose of 16 x 16 (a, b) blocks of tap rows through LDS: both the reads
-// (16 rows of 16 * taps contiguous floats) and the writes are contiguous runs
+// Generic 4-D permuted copy of a weight, element (o, a, b, t) from src[o so + a sa + b sb + t st]
+// to dst[o do + a da + b db + t dt] (t <= 9 taps): tiles of 16 x 16 (a, b) x all taps go through
+// LDS so that whichever of a / b is contiguous on either side is walked by consecutive lanes.
+// The pose weight's channel-order swap (reference c*Z + z <-> K2's map order z*C1 + c) and its
+// NCHW <-> channels-last conversions for MIOpen are instances.
 constexpr int WS_T = 16;
-__global__ __launch_bounds__(256) void weight_swap_k(const float* __restrict__ w, float* __restrict__ dst, int O,
-                                                     int A, int Bn, int taps, int tiles_b) {
+struct WpArgs {
+  long long so, sa, sb, st, dO, da, db, dt;
+  int O, A, B, T, tiles_b;
+};
+__global__ __launch_bounds__(256) void weight_permute_k(WpArgs p, const float* __restrict__ w, float* __restrict__ dst) {
   __shared__ float tile[WS_T * WS_T * WR_TAPS + WS_T];
   const int o = blockIdx.y;
-  const int a0 = (blockIdx.x / tiles_b) * WS_T, b0 = (blockIdx.x % tiles_b) * WS_T;
+  const int a0 = (blockIdx.x / p.tiles_b) * WS_T, b0 = (blockIdx.x % p.tiles_b) * WS_T;
   const int t = threadIdx.x;
-  // read: row a0 + t / WS_T holds tap rows b0 .. b0 + 15 contiguously
-  for (int k = t; k < WS_T * WS_T * taps; k += 256) {
-    const int al = k / (WS_T * taps), rem = k - al * WS_T * taps;
-    const int bl = rem / taps, tp = rem - bl * taps;
+  const int n = WS_T * WS_T * p.T;
+  // read order: the faster-moving of a / b on the source side fastest (after t if t is contiguous)
+  const bool b_fast_src = p.sb <= p.sa;
+  for (int k = t; k < n; k += 256) {
+    int al, bl, tp;
+    if (p.st == 1) {
+      tp = k % p.T;
+      const int r = k / p.T;
+      if (b_fast_src) { bl = r % WS_T; al = r / WS_T; } else { al = r % WS_T; bl = r / WS_T; }
+    } else {
+      const int r = k % (WS_T * WS_T);
+      tp = k / (WS_T * WS_T);
+      if (b_fast_src) { bl = r % WS_T; al = r / WS_T; } else { al = r % WS_T; bl = r / WS_T; }
+    }
     const int a = a0 + al, b = b0 + bl;
-    if (a < A && b < Bn) tile[(al * WS_T + bl) * taps + tp] = w[(((size_t)o * A + a) * Bn + b) * taps + tp];
+    if (a < p.A && b < p.B)
+      tile[(al * WS_T + bl) * WR_TAPS + tp] = w[o * p.so + a * p.sa + b * p.sb + tp * p.st];
   }
   __syncthreads();
-  for (int k = t; k < WS_T * WS_T * taps; k += 256) {
-    const int bl = k / (WS_T * taps), rem = k - bl * WS_T * taps;
-    const int al = rem / taps, tp = rem - al * taps;
+  const bool b_fast_dst = p.db <= p.da;
+  for (int k = t; k < n; k += 256) {
+    int al, bl, tp;
+    if (p.dt == 1) {
+      tp = k % p.T;
+      const int r = k / p.T;
+      if (b_fast_dst) { bl = r % WS_T; al = r / WS_T; } else { al = r % WS_T; bl = r / WS_T; }
+    } else {
+      const int r = k % (WS_T * WS_T);
+      tp = k / (WS_T * WS_T);
+      if (b_fast_dst) { bl = r % WS_T; al = r / WS_T; } else { al = r % WS_T; bl = r / WS_T; }
+    }
     const int a = a0 + al, b = b0 + bl;
-    if (a < A && b < Bn) dst[(((size_t)o * Bn + b) * A + a) * taps + tp] = tile[(al * WS_T + bl) * taps + tp];
+    if (a < p.A && b < p.B) dst[o * p.dO + a * p.da + b * p.db + tp * p.dt] = tile[(al * WS_T + bl) * WR_TAPS + tp];
   }
 }
 
@@ -125,13 +152,26 @@ int vfd_weight_fragments(int mode, const float* w, float* dst, int O, int C, int
   return fail_launch("weight_fragments");
 }
 
-int vfd_weight_swap(const float* w, float* dst, int O, int A, int B, int taps, void* stream) {
-  VFD_REQUIRE(w && dst && O > 0 && O < 65536 && A > 0 && B > 0 && taps > 0 && taps <= WR_TAPS,
-              "weight_swap: bad arguments (taps <= %d)", WR_TAPS);
+int vfd_weight_permute(const float* w, float* dst, int O, int A, int B, int T, const long long* src_strides,
+                       const long long* dst_strides, void* stream) {
+  VFD_REQUIRE(w && dst && src_strides && dst_strides && O > 0 && O < 65536 && A > 0 && B > 0 && T > 0 && T <= WR_TAPS,
+              "weight_permute: bad arguments (taps <= %d)", WR_TAPS);
+  WpArgs p;
+  p.so = src_strides[0]; p.sa = src_strides[1]; p.sb = src_strides[2]; p.st = src_strides[3];
+  p.dO = dst_strides[0]; p.da = dst_strides[1]; p.db = dst_strides[2]; p.dt = dst_strides[3];
+  p.O = O; p.A = A; p.B = B; p.T = T;
+  const int ta = (A + WS_T - 1) / WS_T;
+  p.tiles_b = (B + WS_T - 1) / WS_T;
   hipStream_t s = (hipStream_t)stream;
-  const int ta = (A + WS_T - 1) / WS_T, tb = (B + WS_T - 1) / WS_T;
-  weight_swap_k<<<dim3((unsigned)(ta * tb), (unsigned)O), 256, 0, s>>>(w, dst, O, A, B, taps, tb);
-  return fail_launch("weight_swap");
+  weight_permute_k<<<dim3((unsigned)(ta * p.tiles_b), (unsigned)O), 256, 0, s>>>(p, w, dst);
+  return fail_launch("weight_permute");
+}
+
+int vfd_weight_swap(const float* w, float* dst, int O, int A, int B, int taps, void* stream) {
+  const long long T = taps;
+  const long long ss[4] = {(long long)A * B * T, B * T, T, 1};
+  const long long ds[4] = {(long long)A * B * T, T, (long long)A * T, 1};
+  return vfd_weight_permute(w, dst, O, A, B, taps, ss, ds, stream);
 }
 
 }  // extern "C"

@@ -405,26 +405,37 @@ def pose_conv_fragments(w, C1, Z):
 _SWAP_CACHE = {}
 
 
-def weight_swap(w, A, B, cache=False):
-    """w [O, A*B, kh, kw] with channel a*B + b -> channel b*A + a (weights.hip, one launch).
-    cache: reuse the last result for the same tensor and version (the pose weight, swapped once
-    per step for both pose calls' backward)."""
-    key = (w.data_ptr(), w._version, tuple(w.shape), A, B) if cache else None
+def weight_swap(w, A, B, cache=False, memory_format=torch.contiguous_format):
+    """w [O, A*B, kh, kw] (any layout) with channel a*B + b -> channel b*A + a, written in
+    `memory_format` (weights.hip, one launch; NCHW and channels-last on either side, so MIOpen's
+    channels-last convolutions get their weight without a conversion copy).  cache: reuse the last
+    result for the same tensor, version and format (the pose weight, swapped once per step for both
+    pose calls' backward)."""
+    key = (w.data_ptr(), w._version, tuple(w.shape), A, B, memory_format) if cache else None
     if key is not None and key in _SWAP_CACHE:
         return _SWAP_CACHE[key]
-    out = _weight_swap(w, A, B)
+    out = _weight_permute_swap(w, A, B, memory_format)
     if key is not None:
         _SWAP_CACHE.clear()
         _SWAP_CACHE[key] = out
     return out
 
 
-def _weight_swap(w, A, B):
+def _weight_permute_swap(w, A, B, memory_format):
     lib = L.load()
-    w = _dev(w, 'conv weight').contiguous()
-    O, _, kh, kw = w.shape
-    out = torch.empty_like(w)
-    L.check(lib.vfd_weight_swap(w.data_ptr(), out.data_ptr(), O, A, B, kh * kw, L.stream()), 'weight_swap')
+    w = _dev(w, 'conv weight')
+    O, C, kh, kw = w.shape
+    T = kh * kw
+    out = torch.empty(O, C, kh, kw, device=w.device, memory_format=memory_format)
+    so, sc, sy, sx = w.stride()
+    if sy != kw * sx:
+        w = w.contiguous()
+        so, sc, sy, sx = w.stride()
+    do, dc, dy_, dx_ = out.stride()
+    # element (o, a, b, t): source channel a*B + b, destination channel b*A + a, tap t = y*kw + x
+    src = (ctypes.c_longlong * 4)(so, B * sc, sc, sx)
+    dst = (ctypes.c_longlong * 4)(do, dc, A * dc, dx_)
+    L.check(lib.vfd_weight_permute(w.data_ptr(), out.data_ptr(), O, A, B, T, src, dst, L.stream()), 'weight_permute')
     return out
 
 
@@ -473,9 +484,9 @@ class PadConv(torch.autograd.Function):
         g_pre = lrelu_pad_backward(g, out)
         mask = [ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]]
         s = ctx.stride
-        if ctx.perm:        # MIOpen works in the map's channel order: swap in, and the gradient back
-            C1, Z = ctx.perm
-            w = weight_swap(w, C1, Z, cache=True)
+        if ctx.perm:        # MIOpen works in the map's channel order (channels-last like x): swap
+            C1, Z = ctx.perm  # in, and the gradient back to the reference order (NCHW)
+            w = weight_swap(w, C1, Z, cache=True, memory_format=torch.channels_last)
         dx, dw, db = torch.ops.aten.convolution_backward(g_pre, x, w, [w.shape[0]], [s, s], [0, 0], [1, 1],
                                                          False, [0, 0], 1, mask)
         if ctx.perm and dw is not None:

@@ -232,6 +232,18 @@ int vfd_dec_conv_fwd(const float* xp, const float* w, const float* bias, float* 
 int vfd_dec_conv_bwd(const float* dy, const float* xp, const float* w, float* dxp, float* partial, int N, int CI, int CO,
                      int H, int W, void* stream);
 
+/* ------------------------------------------------------------------ encoder stem (stemconv.hip) */
+/* y [N, 64, Ho, Wo] = conv7x7 stride 2 pad 3 of ((img - 0.45) / 0.225), img [N, C, H, W] raw, C in {3, 6},
+ * w [64, C, 7, 7], no bias (the ResNet encoders' conv1 + the packnet input normalisation,
+ * fusion_depthnet.py:24, fusion_posenet.py:22); Wo % 16 == 0.  Weight gradient only (the image needs
+ * none): partial [vfd_stem_conv_wgrad_groups()][ceil(ktiles / 4) * 4][64][16], k = c*49 + ky*7 + kx
+ * columns in tiles of 16 (zero past C*49); the caller sums the groups. */
+int vfd_stem_conv_supported(int N, int C, int H, int W, int O);
+int vfd_stem_conv_ktiles(int C);
+int vfd_stem_conv_wgrad_groups(void);
+int vfd_stem_conv_fwd(const float* img, const float* w, float* y, int N, int C, int H, int W, void* stream);
+int vfd_stem_conv_wgrad(const float* img, const float* dy, float* partial, int N, int C, int H, int W, void* stream);
+
 /* ------------------------------------------------------------------ weight relayouts (weights.hip) */
 /* Once-per-step copies of reduce_dim's first-conv weight w [O, C, 3, 3] for the MFMA kernels
  * (volumetric_fusionnet.py:59-60; replace ATen permute/flip/pad chains):

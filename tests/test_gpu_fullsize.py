@@ -732,6 +732,25 @@ def test_decoder_conv_mfma_matches_aten(shape, co, up):
     close(b.grad, br.grad, f'dec conv d b {shape}', atol=1e-4 * float(br.grad.abs().max()), rtol=1e-4)
 
 
+@pytest.mark.parametrize('shape', [(6, 6, 384, 640), (6, 3, 384, 640), (2, 6, 64, 96)])
+def test_stem_conv_matches_aten(shape):
+    """The encoders' normalisation + 7x7/2 stem conv on MFMA (stemconv.hip) against
+    F.conv2d((x - 0.45) / 0.225, w, stride 2, padding 3): output and weight gradient."""
+    from vfdepth_amd import kernels as KN
+    gen = torch.Generator(device=DEV).manual_seed(37)
+    img = torch.rand(shape, device=DEV, generator=gen)
+    w = (torch.randn(64, shape[1], 7, 7, device=DEV, generator=gen) / (7 * shape[1] ** 0.5)).requires_grad_(True)
+    assert KN.StemConv.supported(img, w)
+    y = KN.StemConv.apply(img, w)
+    wr = w.detach().clone().requires_grad_(True)
+    ref = F.conv2d((img - 0.45) / 0.225, wr, None, 2, 3)
+    close(y, ref, f'stem conv {shape}', atol=1e-4, rtol=1e-4)
+    g = torch.randn(y.shape, device=DEV, generator=gen)
+    y.backward(g)
+    ref.backward(g)
+    close(w.grad, wr.grad, f'stem conv d w {shape}', atol=1e-4 * float(wr.grad.abs().max()), rtol=1e-4)
+
+
 def test_stem_max_pool_matches_aten():
     """MaxPool2d(3, 2, 1) with the one-byte argmax: forward bit-identical to ATen (ties of a ReLU
     map's zeros go to the first maximum in scan order), backward equal to ATen's (fixed-order sum of

@@ -16,7 +16,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, 'csrc')
 INCLUDE = os.path.join(ROOT, 'include')
 LIB = os.path.join(HERE, 'libvfd_hip.so')
-SOURCES = ['capi.hip', 'fusion.hip', 'view.hip', 'photo.hip', 'aggregate.hip', 'projconv.hip', 'depthsyn.hip', 'padconv.hip', 'bnact.hip', 'reflectpad.hip', 'geometry.hip', 'maxpool.hip', 'weights.hip', 'dispconv.hip', 'decconv.hip']
+SOURCES = ['capi.hip', 'fusion.hip', 'view.hip', 'photo.hip', 'aggregate.hip', 'projconv.hip', 'depthsyn.hip', 'padconv.hip', 'bnact.hip', 'reflectpad.hip', 'geometry.hip', 'maxpool.hip', 'weights.hip', 'dispconv.hip', 'decconv.hip', 'stemconv.hip']
 ARCH = os.environ.get('VFD_OFFLOAD_ARCH', 'gfx950')
 FLAGS = ['-O3', f'--offload-arch={ARCH}', '-std=c++17', '-fPIC', '-ffp-contract=off',
          '-Wno-unused-result', '-I', INCLUDE, '-I', CSRC]

@@ -1204,6 +1204,55 @@ class DispConvSigmoid(torch.autograd.Function):
         return dxp, dw, db
 
 
+class StemConv(torch.autograd.Function):
+    """conv1 (7x7, stride 2, padding 3, 64 outputs, no bias) of the normalised image
+    (image - 0.45) / 0.225 — the ResNet encoders' input normalisation and stem conv in one fp32
+    MFMA kernel (stemconv.hip); backward: the weight gradient (the image takes none)."""
+
+    @staticmethod
+    def supported(image, weight):
+        if not (image.is_cuda and image.dim() == 4 and image.dtype == torch.float32 and not image.requires_grad
+                and weight.dim() == 4 and tuple(weight.shape[2:]) == (7, 7) and weight.shape[1] == image.shape[1]):
+            return False
+        N, C, H, W = image.shape
+        return bool(L.load().vfd_stem_conv_supported(N, C, H, W, weight.shape[0]))
+
+    @staticmethod
+    def forward(ctx, image, weight):
+        lib = L.load()
+        image = _dev(image, 'stem conv image')
+        w = weight.detach().contiguous()
+        N, C, H, W = image.shape
+        Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+        y = torch.empty(N, 64, Ho, Wo, device=image.device)
+        L.check(lib.vfd_stem_conv_fwd(image.data_ptr(), w.data_ptr(), y.data_ptr(), N, C, H, W, L.stream()),
+                'stem_conv_fwd')
+        if L.PROF_ON:
+            L.ALG_BYTES['stem_conv'] += (image.numel() + y.numel()) * 4
+        ctx.save_for_backward(image)
+        ctx.C = C
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        lib = L.load()
+        image, = ctx.saved_tensors
+        if not ctx.needs_input_grad[1]:
+            return None, None
+        g = g.contiguous()
+        N, C, H, W = image.shape
+        kt = lib.vfd_stem_conv_ktiles(C)
+        nkt = (kt + 3) // 4 * 4
+        part = torch.empty(lib.vfd_stem_conv_wgrad_groups(), nkt, 64, 16, device=g.device)
+        L.check(lib.vfd_stem_conv_wgrad(image.data_ptr(), g.data_ptr(), part.data_ptr(), N, C, H, W, L.stream()),
+                'stem_conv_wgrad')
+        if L.PROF_ON:
+            L.ALG_BYTES['stem_conv'] += (image.numel() + g.numel()) * 4
+        K = C * 49
+        dw = part.sum(0).permute(1, 0, 2).reshape(64, nkt * 16)[:, :K].reshape(64, C, 7, 7)
+        return None, dw
+
+
 # =============================================================================================
 # ResNet stem max pool (3x3, stride 2, padding 1) with a one-byte argmax and a gather backward
 # =============================================================================================

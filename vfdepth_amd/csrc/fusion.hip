@@ -1574,12 +1574,24 @@ __global__ __launch_bounds__(128) void fuse_depth_combine_k(vfd_voxel_desc d, co
     const int x0 = (tile % ntx) * PT, y0 = (tile / ntx) * PT;
     const float* p0 = pool + (size_t)cb.y * PT2 * POSE_MAXC + ch;
     float* db = dP + (size_t)bc * hw * ROW + ch;
-    for (int p = 0; p < PT2; ++p) {
-      const int x = x0 + p % PT, y = y0 + p / PT;
-      if (x >= d.w || y >= d.h) continue;
-      float a = p0[(size_t)p * POSE_MAXC];
-      for (int s2 = 1; s2 < cb.z; ++s2) a += p0[((size_t)s2 * PT2 + p) * POSE_MAXC];
-      db[((size_t)y * d.w + x) * ROW] = a;
+    // one tile row at a time with all PT x PBW_MAXS slot loads in flight (absent parts re-read
+    // the last slot and add +0: every load unconditional, summed in part order)
+    for (int py = 0; py < PT; ++py) {
+      const int y = y0 + py;
+      if (y >= d.h) break;
+      float v[PT][PBW_MAXS];
+#pragma unroll
+      for (int px = 0; px < PT; ++px)
+#pragma unroll
+        for (int s2 = 0; s2 < PBW_MAXS; ++s2)
+          v[px][s2] = p0[((size_t)min(s2, cb.z - 1) * PT2 + py * PT + px) * POSE_MAXC];
+#pragma unroll
+      for (int px = 0; px < PT; ++px) {
+        float a = v[px][0];
+#pragma unroll
+        for (int s2 = 1; s2 < PBW_MAXS; ++s2) a += (s2 < cb.z ? 1.f : 0.f) * v[px][s2];
+        if (x0 + px < d.w) db[((size_t)y * d.w + x0 + px) * ROW] = a;
+      }
     }
   }
 }

@@ -162,10 +162,14 @@ int vfd_bn_sum(const vfd_bn_desc* d, const double* partial, double* sums, void* 
 /* sums: the [C][S][2] partials (ns = S) or reduced [C][2] sums (ns = 1); residual / running stats
  * / num_batches_tracked (int64, += 1) nullable.  Writes y and the per-channel mean / invstd the
  * backward reads. */
+/* relu_mask (optional, N*C*HW bytes): the forward also stores [y > 0] per element; a backward call
+ * with d->relu == 2 then takes that mask in place of y (a quarter of the bytes). */
 int vfd_bn_fwd_apply(const vfd_bn_desc* d, const float* x, const float* residual, const double* sums, int ns,
                      double count, const float* gamma, const float* beta, float* y, float* mean, float* invstd,
-                     float* running_mean, float* running_var, long long* num_batches_tracked, void* stream);
-/* g = d y; y = the forward's output (ReLU mask; unused without ReLU) */
+                     float* running_mean, float* running_var, long long* num_batches_tracked,
+                     unsigned char* relu_mask, void* stream);
+/* g = d y; y = the forward's output (ReLU mask; unused without ReLU), or with d->relu == 2 the
+ * forward's byte mask */
 int vfd_bn_bwd_stats(const vfd_bn_desc* d, const float* g, const float* y, const float* x, const float* mean,
                      double* partial, void* stream);
 /* dx, d residual, d gamma, d beta nullable (not requested) */
@@ -191,9 +195,6 @@ int vfd_maxpool3s2_bwd(const float* g, const uint8_t* arg, float* dx, long long 
  * of each pixel's copies (deterministic, no atomics). */
 int vfd_reflect_pad1_fwd(const float* x, float* y, long long planes, int h, int w, void* stream);
 int vfd_reflect_pad1_bwd(const float* g, float* dx, long long planes, int h, int w, void* stream);
-/* backward of LeakyReLU(slope) + the one-pixel reflect pad for channels-last maps (the K3C / K2C
- * outputs): g, out [n, h+2, w+2, C] (out = the padded forward output) -> gp [n, h, w, C] =
- * (sum of g's copies) * (out > 0 ? 1 : slope); C % 4 == 0, 16-B aligned. */
 /* One-launch BatchNorm(+residual)(+ReLU) forward / backward for channels of at most 8192 elements
  * with local statistics (the small ResNet layers): one workgroup per channel computes the fp64
  * statistics and applies them; same arguments and results as bn_fwd_stats + bn_fwd_apply /
@@ -201,7 +202,7 @@ int vfd_reflect_pad1_bwd(const float* g, float* dx, long long planes, int h, int
 int vfd_bn1_fits(const vfd_bn_desc* d);
 int vfd_bn1_fwd(const vfd_bn_desc* d, const float* x, const float* residual, const float* gamma, const float* beta,
                 float* y, float* mean, float* invstd, float* running_mean, float* running_var,
-                long long* num_batches_tracked, void* stream);
+                long long* num_batches_tracked, unsigned char* relu_mask, void* stream);
 int vfd_bn1_bwd(const vfd_bn_desc* d, const float* g, const float* y, const float* x, const float* gamma,
                 const float* mean, const float* invstd, float* dx, float* dresidual, float* dgamma, float* dbeta,
                 void* stream);
@@ -272,6 +273,9 @@ int vfd_elu_up_pad1_bwd(const float* g, const float* y, float* dy, long long pla
 /* psum (optional, [planes][vfd_elu_up_pad1_bwd_blocks(h, w)]): per-block sums of dy per plane —
  * the partials of the producing conv's bias gradient (summed in fixed order by the caller) */
 int vfd_elu_up_pad1_bwd_blocks(int h, int w);
+/* backward of LeakyReLU(slope) + the one-pixel reflect pad for channels-last maps (the K3C / K2C
+ * outputs): g, out [n, h+2, w+2, C] (out = the padded forward output) -> gp [n, h, w, C] =
+ * (sum of g's copies) * (out > 0 ? 1 : slope); C % 4 == 0, 16-B aligned. */
 int vfd_lrelu_pad1_bwd_nhwc(const float* g, const float* out, float* gp, long long n_img, int h, int w, int C,
                             float slope, void* stream);
 

@@ -87,7 +87,7 @@ _SIGS = {
     'vfd_bn_splits': (c_int, [ctypes.POINTER(BnDesc)]),
     'vfd_bn_fwd_stats': (c_int, [ctypes.POINTER(BnDesc), c_fp, c_fp, c_void_p]),
     'vfd_bn_sum': (c_int, [ctypes.POINTER(BnDesc), c_fp, c_fp, c_void_p]),
-    'vfd_bn_fwd_apply': (c_int, [ctypes.POINTER(BnDesc), c_fp, c_fp, c_fp, c_int, c_double] + [c_fp] * 8 + [c_void_p]),
+    'vfd_bn_fwd_apply': (c_int, [ctypes.POINTER(BnDesc), c_fp, c_fp, c_fp, c_int, c_double] + [c_fp] * 9 + [c_void_p]),
     'vfd_bn_bwd_stats': (c_int, [ctypes.POINTER(BnDesc)] + [c_fp] * 5 + [c_void_p]),
     'vfd_bn_bwd_apply': (c_int, [ctypes.POINTER(BnDesc), c_fp, c_fp, c_fp, c_fp, c_int, c_double] + [c_fp] * 7
                          + [c_void_p]),
@@ -98,7 +98,7 @@ _SIGS = {
     'vfd_reflect_pad1_fwd': (c_int, [c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_void_p]),
     'vfd_reflect_pad1_bwd': (c_int, [c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_void_p]),
     'vfd_bn1_fits': (c_int, [ctypes.POINTER(BnDesc)]),
-    'vfd_bn1_fwd': (c_int, [ctypes.POINTER(BnDesc)] + [c_fp] * 10 + [c_void_p]),
+    'vfd_bn1_fwd': (c_int, [ctypes.POINTER(BnDesc)] + [c_fp] * 11 + [c_void_p]),
     'vfd_bn1_bwd': (c_int, [ctypes.POINTER(BnDesc)] + [c_fp] * 10 + [c_void_p]),
     'vfd_disp_conv_supported': (c_int, [c_int] * 4),
     'vfd_disp_conv_wgrad_blocks': (c_int, [c_int] * 3),

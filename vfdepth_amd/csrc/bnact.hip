@@ -59,6 +59,28 @@ __device__ __forceinline__ void bn_visit(const vfd_bn_desc& d, int c, BnRange r,
   }
 }
 
+// ReLU mask in the backward: from the forward output y (d.relu == 1) or from the forward's byte
+// mask (d.relu == 2: `y` then points at N*C*HW bytes, 1 = positive output) — a quarter of the bytes
+__device__ __forceinline__ void relu_mask4(const vfd_bn_desc& d, const float* __restrict__ y, size_t o, float4& gv) {
+  if (d.relu == 2) {
+    const uchar4 m = *reinterpret_cast<const uchar4*>(reinterpret_cast<const unsigned char*>(y) + o);
+    gv.x = m.x ? gv.x : 0.f;
+    gv.y = m.y ? gv.y : 0.f;
+    gv.z = m.z ? gv.z : 0.f;
+    gv.w = m.w ? gv.w : 0.f;
+  } else {
+    const float4 yv = *reinterpret_cast<const float4*>(y + o);
+    gv.x = yv.x > 0.f ? gv.x : 0.f;
+    gv.y = yv.y > 0.f ? gv.y : 0.f;
+    gv.z = yv.z > 0.f ? gv.z : 0.f;
+    gv.w = yv.w > 0.f ? gv.w : 0.f;
+  }
+}
+
+__device__ __forceinline__ bool relu_on(const vfd_bn_desc& d, const float* __restrict__ y, size_t o) {
+  return d.relu == 2 ? reinterpret_cast<const unsigned char*>(y)[o] != 0 : y[o] > 0.f;
+}
+
 // partial[(c*S + split)*2 + {0,1}] = sum x, sum x^2 over the range
 __global__ __launch_bounds__(BN_THREADS) void bn_stats_k(vfd_bn_desc d, const float* __restrict__ x,
                                                          double* __restrict__ partial) {
@@ -118,7 +140,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_apply_k(vfd_bn_desc d, const fl
                                                          const float* __restrict__ beta, float* __restrict__ y,
                                                          float* __restrict__ mean_out, float* __restrict__ invstd_out,
                                                          float* __restrict__ run_mean, float* __restrict__ run_var,
-                                                         long long* __restrict__ nbt) {
+                                                         long long* __restrict__ nbt, unsigned char* __restrict__ mk) {
   const int c = blockIdx.y, split = blockIdx.x;
   if (nbt && c == 0 && split == 0 && threadIdx.x == 0) nbt[0] += 1;   // num_batches_tracked
   double s1, s2;
@@ -161,11 +183,13 @@ __global__ __launch_bounds__(BN_THREADS) void bn_apply_k(vfd_bn_desc d, const fl
         v.w = fmaxf(v.w, 0.f);
       }
       *reinterpret_cast<float4*>(y + o) = v;
+      if (mk) *reinterpret_cast<uchar4*>(mk + o) = make_uchar4(v.x > 0.f, v.y > 0.f, v.z > 0.f, v.w > 0.f);
     } else {
       float v = x[o] * sc + sh;
       if (r) v += r[o];
       if (relu) v = fmaxf(v, 0.f);
       y[o] = v;
+      if (mk) mk[o] = v > 0.f;
     }
   });
 }
@@ -184,19 +208,13 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_stats_k(vfd_bn_desc d, cons
     if (n == 4) {
       float4 gv = *reinterpret_cast<const float4*>(g + o);
       const float4 xv = *reinterpret_cast<const float4*>(x + o);
-      if (relu) {
-        const float4 yv = *reinterpret_cast<const float4*>(y + o);
-        gv.x = yv.x > 0.f ? gv.x : 0.f;
-        gv.y = yv.y > 0.f ? gv.y : 0.f;
-        gv.z = yv.z > 0.f ? gv.z : 0.f;
-        gv.w = yv.w > 0.f ? gv.w : 0.f;
-      }
+      if (relu) relu_mask4(d, y, o, gv);
       s1 += ((double)gv.x + (double)gv.y) + ((double)gv.z + (double)gv.w);
       s2 += ((double)gv.x * (double)(xv.x - mean) + (double)gv.y * (double)(xv.y - mean)) +
             ((double)gv.z * (double)(xv.z - mean) + (double)gv.w * (double)(xv.w - mean));
     } else {
       float gv = g[o];
-      if (relu && !(y[o] > 0.f)) gv = 0.f;
+      if (relu && !relu_on(d, y, o)) gv = 0.f;
       s1 += gv;
       s2 += (double)gv * (double)(x[o] - mean);
     }
@@ -235,13 +253,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply_k(vfd_bn_desc d, cons
     if (n == 4) {
       float4 gv = *reinterpret_cast<const float4*>(g + o);
       const float4 xv = *reinterpret_cast<const float4*>(x + o);
-      if (relu) {
-        const float4 yv = *reinterpret_cast<const float4*>(y + o);
-        gv.x = yv.x > 0.f ? gv.x : 0.f;
-        gv.y = yv.y > 0.f ? gv.y : 0.f;
-        gv.z = yv.z > 0.f ? gv.z : 0.f;
-        gv.w = yv.w > 0.f ? gv.w : 0.f;
-      }
+      if (relu) relu_mask4(d, y, o, gv);
       if (dr) *reinterpret_cast<float4*>(dr + o) = gv;
       if (dx) {
         float4 o4;
@@ -253,7 +265,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply_k(vfd_bn_desc d, cons
       }
     } else {
       float gv = g[o];
-      if (relu && !(y[o] > 0.f)) gv = 0.f;
+      if (relu && !relu_on(d, y, o)) gv = 0.f;
       if (dr) dr[o] = gv;
       if (dx) dx[o] = k * (gv - mg - (x[o] - mean) * mx);
     }
@@ -294,7 +306,7 @@ __global__ __launch_bounds__(BN1_THREADS) void bn1_fwd_k(vfd_bn_desc d, const fl
                                                          const float* __restrict__ beta, float* __restrict__ y,
                                                          float* __restrict__ mean_out, float* __restrict__ invstd_out,
                                                          float* __restrict__ run_mean, float* __restrict__ run_var,
-                                                         long long* __restrict__ nbt) {
+                                                         long long* __restrict__ nbt, unsigned char* __restrict__ mk) {
   __shared__ double sh[BN1_THREADS / 64];
   const int c = blockIdx.x;
   if (nbt && c == 0 && threadIdx.x == 0) nbt[0] += 1;
@@ -352,11 +364,13 @@ __global__ __launch_bounds__(BN1_THREADS) void bn1_fwd_k(vfd_bn_desc d, const fl
         v.w = fmaxf(v.w, 0.f);
       }
       *reinterpret_cast<float4*>(y + o) = v;
+      if (mk) *reinterpret_cast<uchar4*>(mk + o) = make_uchar4(v.x > 0.f, v.y > 0.f, v.z > 0.f, v.w > 0.f);
     } else {
       float v = x[o] * sc + shf;
       if (r) v += r[o];
       if (relu) v = fmaxf(v, 0.f);
       y[o] = v;
+      if (mk) mk[o] = v > 0.f;
     }
   });
 }
@@ -377,19 +391,13 @@ __global__ __launch_bounds__(BN1_THREADS) void bn1_bwd_k(vfd_bn_desc d, const fl
     if (n == 4) {
       float4 gv = *reinterpret_cast<const float4*>(g + o);
       const float4 xv = *reinterpret_cast<const float4*>(x + o);
-      if (relu) {
-        const float4 yv = *reinterpret_cast<const float4*>(y + o);
-        gv.x = yv.x > 0.f ? gv.x : 0.f;
-        gv.y = yv.y > 0.f ? gv.y : 0.f;
-        gv.z = yv.z > 0.f ? gv.z : 0.f;
-        gv.w = yv.w > 0.f ? gv.w : 0.f;
-      }
+      if (relu) relu_mask4(d, y, o, gv);
       s1 += ((double)gv.x + (double)gv.y) + ((double)gv.z + (double)gv.w);
       s2 += ((double)gv.x * (double)(xv.x - mean) + (double)gv.y * (double)(xv.y - mean)) +
             ((double)gv.z * (double)(xv.z - mean) + (double)gv.w * (double)(xv.w - mean));
     } else {
       float gv = g[o];
-      if (relu && !(y[o] > 0.f)) gv = 0.f;
+      if (relu && !relu_on(d, y, o)) gv = 0.f;
       s1 += gv;
       s2 += (double)gv * (double)(x[o] - mean);
     }
@@ -407,13 +415,7 @@ __global__ __launch_bounds__(BN1_THREADS) void bn1_bwd_k(vfd_bn_desc d, const fl
     if (n == 4) {
       float4 gv = *reinterpret_cast<const float4*>(g + o);
       const float4 xv = *reinterpret_cast<const float4*>(x + o);
-      if (relu) {
-        const float4 yv = *reinterpret_cast<const float4*>(y + o);
-        gv.x = yv.x > 0.f ? gv.x : 0.f;
-        gv.y = yv.y > 0.f ? gv.y : 0.f;
-        gv.z = yv.z > 0.f ? gv.z : 0.f;
-        gv.w = yv.w > 0.f ? gv.w : 0.f;
-      }
+      if (relu) relu_mask4(d, y, o, gv);
       if (dr) *reinterpret_cast<float4*>(dr + o) = gv;
       if (dx) {
         float4 o4;
@@ -425,7 +427,7 @@ __global__ __launch_bounds__(BN1_THREADS) void bn1_bwd_k(vfd_bn_desc d, const fl
       }
     } else {
       float gv = g[o];
-      if (relu && !(y[o] > 0.f)) gv = 0.f;
+      if (relu && !relu_on(d, y, o)) gv = 0.f;
       if (dr) dr[o] = gv;
       if (dx) dx[o] = k * (gv - mg - (x[o] - mean) * mx);
     }
@@ -475,7 +477,8 @@ int vfd_bn_sum(const vfd_bn_desc* d, const double* partial, double* sums, void* 
 
 int vfd_bn_fwd_apply(const vfd_bn_desc* d, const float* x, const float* residual, const double* sums, int ns,
                      double count, const float* gamma, const float* beta, float* y, float* mean, float* invstd,
-                     float* running_mean, float* running_var, long long* num_batches_tracked, void* stream) {
+                     float* running_mean, float* running_var, long long* num_batches_tracked,
+                     unsigned char* relu_mask, void* stream) {
   if (int e = bn_check(d, "bn_fwd_apply")) return e;
   VFD_REQUIRE(x && sums && gamma && beta && y && mean && invstd && (ns == 1 || ns == d->S) && count > 0.0,
               "bn_fwd_apply: bad argument");
@@ -483,7 +486,8 @@ int vfd_bn_fwd_apply(const vfd_bn_desc* d, const float* x, const float* residual
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_BN_FWD, s);
   bn_apply_k<<<dim3(d->S, d->C), BN_THREADS, 0, s>>>(*d, x, residual, sums, ns, count, gamma, beta, y, mean, invstd,
-                                                     running_mean, running_var, num_batches_tracked);
+                                                     running_mean, running_var, num_batches_tracked,
+                                                     d->relu ? relu_mask : nullptr);
   return fail_launch("bn_fwd_apply");
 }
 
@@ -517,13 +521,13 @@ int vfd_bn1_fits(const vfd_bn_desc* d) {
 
 int vfd_bn1_fwd(const vfd_bn_desc* d, const float* x, const float* residual, const float* gamma, const float* beta,
                 float* y, float* mean, float* invstd, float* running_mean, float* running_var,
-                long long* num_batches_tracked, void* stream) {
+                long long* num_batches_tracked, unsigned char* relu_mask, void* stream) {
   VFD_REQUIRE(vfd_bn1_fits(d), "bn1_fwd: channel larger than %u elements", BN1_MAX);
   VFD_REQUIRE(x && gamma && beta && y && mean && invstd && !running_mean == !running_var, "bn1_fwd: bad argument");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_BN_FWD, s);
   bn1_fwd_k<<<d->C, BN1_THREADS, 0, s>>>(*d, x, residual, gamma, beta, y, mean, invstd, running_mean, running_var,
-                                         num_batches_tracked);
+                                         num_batches_tracked, d->relu ? relu_mask : nullptr);
   return fail_launch("bn1_fwd");
 }
 

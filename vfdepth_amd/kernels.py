@@ -940,6 +940,9 @@ class BatchNormAct(torch.autograd.Function):
         d.S = lib.vfd_bn_splits(ctypes.byref(d))
         r = residual.contiguous() if residual is not None else None
         ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+        # with ReLU the forward also stores [y > 0] as one byte per element: the backward reads
+        # that mask instead of y (d.relu == 2 there), a quarter of the bytes
+        mk = torch.empty(x.shape, dtype=torch.uint8, device=x.device) if relu else None
         ctx.one = pg is None and _BN_ONE and bool(lib.vfd_bn1_fits(ctypes.byref(d)))
         if ctx.one:       # small layer, local statistics: one launch (bnact.hip bn1_fwd_k)
             y = torch.empty_like(x)
@@ -947,11 +950,11 @@ class BatchNormAct(torch.autograd.Function):
             invstd = torch.empty(C, device=x.device)
             L.check(lib.vfd_bn1_fwd(ctypes.byref(d), x.data_ptr(), ptr(r), gamma.data_ptr(), beta.data_ptr(),
                                     y.data_ptr(), mean.data_ptr(), invstd.data_ptr(), ptr(running_mean),
-                                    ptr(running_var), ptr(nbt), L.stream()), 'bn1_fwd')
+                                    ptr(running_var), ptr(nbt), ptr(mk), L.stream()), 'bn1_fwd')
             ctx.d, ctx.pg, ctx.count, ctx.has_res = (d.N, d.C, d.HW, d.S, d.relu, d.eps, d.momentum), pg, float(N * H * W), r is not None
             if L.PROF_ON:
-                L.ALG_BYTES['bn_fwd'] += x.numel() * 4 * (2 + (r is not None))
-            ctx.save_for_backward(x, y, gamma, mean, invstd)
+                L.ALG_BYTES['bn_fwd'] += x.numel() * (8 + 4 * (r is not None) + (mk is not None))
+            ctx.save_for_backward(x, mk, gamma, mean, invstd)
             return y
         partial = torch.empty(C, d.S, 2, dtype=torch.float64, device=x.device)
         L.check(lib.vfd_bn_fwd_stats(ctypes.byref(d), x.data_ptr(), partial.data_ptr(), L.stream()), 'bn_fwd_stats')
@@ -966,19 +969,21 @@ class BatchNormAct(torch.autograd.Function):
                                      mean.data_ptr(), invstd.data_ptr(),
                                      running_mean.data_ptr() if running_mean is not None else None,
                                      running_var.data_ptr() if running_var is not None else None,
-                                     nbt.data_ptr() if nbt is not None else None, L.stream()),
+                                     nbt.data_ptr() if nbt is not None else None, ptr(mk), L.stream()),
                 'bn_fwd_apply')
         ctx.d, ctx.pg, ctx.count, ctx.has_res = (d.N, d.C, d.HW, d.S, d.relu, d.eps, d.momentum), pg, count, r is not None
-        if L.PROF_ON:                        # compulsory: x (+ r) in, y out
-            L.ALG_BYTES['bn_fwd'] += x.numel() * 4 * (2 + (r is not None))
-        ctx.save_for_backward(x, y, gamma, mean, invstd)
+        if L.PROF_ON:                        # compulsory: x (+ r) in, y (+ the ReLU byte mask) out
+            L.ALG_BYTES['bn_fwd'] += x.numel() * (8 + 4 * (r is not None) + (mk is not None))
+        ctx.save_for_backward(x, mk, gamma, mean, invstd)
         return y
 
     @staticmethod
     def backward(ctx, g):
         lib = L.load()
-        x, y, gamma, mean, invstd = ctx.saved_tensors
+        x, mk, gamma, mean, invstd = ctx.saved_tensors
         d = L.BnDesc(*ctx.d)
+        if d.relu:
+            d.relu = 2                       # the ReLU mask is the forward's byte mask
         g = g.contiguous()
         need = ctx.needs_input_grad
         ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
@@ -988,13 +993,13 @@ class BatchNormAct(torch.autograd.Function):
             dgamma = torch.empty_like(gamma) if need[1] else None
             dbeta = torch.empty_like(gamma) if need[2] else None
             if L.PROF_ON:
-                L.ALG_BYTES['bn_bwd'] += x.numel() * 4 * (2 + d.relu + (dx is not None) + (dr is not None))
-            L.check(lib.vfd_bn1_bwd(ctypes.byref(d), g.data_ptr(), y.data_ptr() if d.relu else None, x.data_ptr(),
+                L.ALG_BYTES['bn_bwd'] += x.numel() * (8 + (d.relu != 0) + 4 * ((dx is not None) + (dr is not None)))
+            L.check(lib.vfd_bn1_bwd(ctypes.byref(d), g.data_ptr(), mk.data_ptr() if d.relu else None, x.data_ptr(),
                                     gamma.data_ptr(), mean.data_ptr(), invstd.data_ptr(), ptr(dx), ptr(dr),
                                     ptr(dgamma), ptr(dbeta), L.stream()), 'bn1_bwd')
             return dx, dgamma, dbeta, dr, None, None, None, None, None, None, None
         partial = torch.empty(d.C, d.S, 2, dtype=torch.float64, device=g.device)
-        yp = y.data_ptr() if d.relu else None
+        yp = mk.data_ptr() if d.relu else None
         L.check(lib.vfd_bn_bwd_stats(ctypes.byref(d), g.data_ptr(), yp, x.data_ptr(), mean.data_ptr(),
                                      partial.data_ptr(), L.stream()), 'bn_bwd_stats')
         sums, ns, count = partial, d.S, ctx.count
@@ -1006,8 +1011,8 @@ class BatchNormAct(torch.autograd.Function):
         dgamma = torch.empty_like(gamma) if need[1] else None
         dbeta = torch.empty_like(gamma) if need[2] else None
         ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
-        if L.PROF_ON:                        # compulsory: g, x (, y) in, dx (, dr) out
-            L.ALG_BYTES['bn_bwd'] += x.numel() * 4 * (2 + d.relu + (dx is not None) + (dr is not None))
+        if L.PROF_ON:                        # compulsory: g, x (, the mask) in, dx (, dr) out
+            L.ALG_BYTES['bn_bwd'] += x.numel() * (8 + (d.relu != 0) + 4 * ((dx is not None) + (dr is not None)))
         L.check(lib.vfd_bn_bwd_apply(ctypes.byref(d), g.data_ptr(), yp, x.data_ptr(), sums.data_ptr(), ns, count,
                                      gamma.data_ptr(), mean.data_ptr(), invstd.data_ptr(), ptr(dx), ptr(dr),
                                      ptr(dgamma), ptr(dbeta), L.stream()), 'bn_bwd_apply')

@@ -188,6 +188,10 @@ int vfd_inverse4x4(const float* m, float* out, int n, void* stream);
  * and NaN rules.  Backward: a fixed-order gather of the winners' gradients (no atomics). */
 int vfd_maxpool3s2_fwd(const float* x, float* y, uint8_t* arg, long long planes, int h, int w, void* stream);
 int vfd_maxpool3s2_bwd(const float* g, const uint8_t* arg, float* dx, long long planes, int h, int w, void* stream);
+/* The encoders' input normalisation (x - 0.45) / 0.225 of cat([a, b], channels) in one pass:
+ * a [n_img, ca, hw], b [n_img, cb, hw] (cb = 0: a alone) -> dst [n_img, ca + cb, hw]; hw % 4 == 0. */
+int vfd_normalize_cat(const float* a, const float* b, float* dst, long long n_img, int ca, int cb, int hw,
+                      void* stream);
 
 /* ------------------------------------------------------------------ reflect padding (decoders) */
 /* nn.Conv2d(padding_mode='reflect', padding=1) of the decoders' 3x3 blocks (network/blocks.py):

@@ -751,6 +751,17 @@ def test_stem_conv_matches_aten(shape):
     close(w.grad, wr.grad, f'stem conv d w {shape}', atol=1e-4 * float(wr.grad.abs().max()), rtol=1e-4)
 
 
+def test_normalize_cat_bit_identical():
+    """The encoders' input: (cat(frames) - 0.45) / 0.225 in one HIP pass, bit-identical to the ATen
+    ops (pose: two frames, depth: one)."""
+    from vfdepth_amd import kernels as KN
+    gen = torch.Generator(device=DEV).manual_seed(3)
+    a = torch.rand(6, 3, 384, 640, device=DEV, generator=gen)
+    b = torch.rand(6, 3, 384, 640, device=DEV, generator=gen)
+    assert torch.equal(KN.normalize_cat(a, b), (torch.cat([a, b], 1) - 0.45) / 0.225)
+    assert torch.equal(KN.normalize_cat(a), (a - 0.45) / 0.225)
+
+
 def test_stem_max_pool_matches_aten():
     """MaxPool2d(3, 2, 1) with the one-byte argmax: forward bit-identical to ATen (ties of a ReLU
     map's zeros go to the first maximum in scan order), backward equal to ATen's (fixed-order sum of

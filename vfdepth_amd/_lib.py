@@ -93,6 +93,7 @@ _SIGS = {
                          + [c_void_p]),
     'vfd_inverse4x4': (c_int, [c_fp, c_fp, c_int, c_void_p]),
     'vfd_maxpool3s2_fwd': (c_int, [c_fp, c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_void_p]),
+    'vfd_normalize_cat': (c_int, [c_fp, c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_int, c_void_p]),
     'vfd_maxpool3s2_bwd': (c_int, [c_fp, c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_void_p]),
     'vfd_upsample_ac_bwd': (c_int, [c_fp, c_fp, c_fp, ctypes.c_longlong] + [c_int] * 4 + [c_void_p]),
     'vfd_reflect_pad1_fwd': (c_int, [c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_void_p]),

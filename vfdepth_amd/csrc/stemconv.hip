@@ -28,11 +28,11 @@ __device__ __forceinline__ f32x4s mfma16s(float a, float b, f32x4s c) {
 }
 
 // normalised input value at (n, c, iy, ix) (zero outside the image): the reference's
-// (image - 0.45) / 0.225, evaluated with the same two fp32 operations
+// (image - 0.45) / 0.225, evaluated as ATen's GPU kernels do (multiply by the fp32 reciprocal)
 __device__ __forceinline__ float sc_in(const float* __restrict__ img, int C, int H, int W, int n, int c, int iy, int ix) {
   const bool ok = iy >= 0 && iy < H && ix >= 0 && ix < W;
   const float v = img[(((size_t)n * C + c) * H + (ok ? iy : 0)) * W + (ok ? ix : 0)];
-  return ok ? (v - 0.45f) / 0.225f : 0.f;
+  return ok ? (v - 0.45f) * (1.0f / 0.225f) : 0.f;
 }
 
 constexpr int SC_OH = 32;                        // output channels per block (grid.y = 64 / 32)

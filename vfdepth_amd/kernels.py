@@ -1258,6 +1258,20 @@ class StemConv(torch.autograd.Function):
         return None, dw
 
 
+def normalize_cat(a, b=None):
+    """(cat([a, b], dim=1) - 0.45) / 0.225 for image batches [n, c, h, w] without gradient, in one
+    HIP pass (maxpool.hip norm_cat_k; the encoders' input normalisation, bit-identical)."""
+    lib = L.load()
+    a = _dev(a, 'image').contiguous()
+    b = _dev(b, 'image').contiguous() if b is not None else None
+    n, ca, h, w = a.shape
+    cb = b.shape[1] if b is not None else 0
+    out = torch.empty(n, ca + cb, h, w, device=a.device)
+    L.check(lib.vfd_normalize_cat(a.data_ptr(), b.data_ptr() if b is not None else None, out.data_ptr(), n, ca, cb,
+                                  h * w, L.stream()), 'normalize_cat')
+    return out
+
+
 # =============================================================================================
 # ResNet stem max pool (3x3, stride 2, padding 1) with a one-byte argmax and a gather backward
 # =============================================================================================

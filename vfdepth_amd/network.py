@@ -16,12 +16,23 @@ from .layers import (MonoDepthDecoder, PoseDecoder, ResnetEncoder, conv2d_block,
                      unpack_cam_feat, upsample)
 
 
-def _aggregate(encoder, conv1x1, images, lvl, B, N):
+def _encoder_input(frames):
+    """cat(frames, channels) of [B, N, 3, H, W] batches, packed to [B*N, ...]: the fused nets' encoder
+    input.  On the GPU (fp32, no gradient, H*W % 4 == 0) it comes normalised from one HIP pass
+    (`kernels.normalize_cat`, bit-identical to cat + (x - 0.45) / 0.225); returns (x, normalized)."""
+    f = [pack_cam_feat(t) for t in frames]
+    if (len(f) <= 2 and all(t.is_cuda and t.dtype == torch.float32 and not t.requires_grad for t in f)
+            and (f[0].shape[-1] * f[0].shape[-2]) % 4 == 0 and os.environ.get('VFD_NORM_CAT', '1') != '0'):
+        return KN.normalize_cat(*f), True
+    return (torch.cat(f, 1) if len(f) > 1 else f[0]), False
+
+
+def _aggregate(encoder, conv1x1, images, lvl, B, N, normalized=False):
     """Encoder pyramid -> fusion-level aggregate [B,N,C,h,w] (fusion_depthnet.py:53-65,
     fusion_posenet.py:55-67): LReLU(conv1x1(cat(f_lvl, up(f_lvl+1), ...))) evaluated as
     LReLU(W_lvl f_lvl + sum up(W_k f_k) + b) — each slice of the 1x1 conv at its own resolution,
     one fused upsample-add-bias-LReLU kernel (same parameters, same result up to fp32 rounding)."""
-    feats = encoder(images)
+    feats = encoder(images, normalized)
     conv = conv1x1[0]
     off, parts = 0, []
     for f in feats[lvl:]:
@@ -139,7 +150,8 @@ class FusedDepthNet(nn.Module):
         imgs = inputs[('color_aug', 0, 0)]
         B, N = imgs.shape[:2]
         with net_autocast(self, imgs):
-            feats, agg = _aggregate(self.encoder, self.conv1x1, pack_cam_feat(imgs), self.fusion_level, B, N)
+            x, normed = _encoder_input([imgs]) if not torch.is_autocast_enabled('cuda') else (pack_cam_feat(imgs), False)
+            feats, agg = _aggregate(self.encoder, self.conv1x1, x, self.fusion_level, B, N, normed)
             fusion = self.fusion_net(inputs, agg)
             disp = self.decoder(feats[:self.fusion_level] + [fusion['proj_feat']])
             # depth synthesis: a second decoder pass on the augmented view (fusion_depthnet.py:79-86)
@@ -178,10 +190,14 @@ class FusedPoseNet(nn.Module):
         self.bf16 = cfg['training'].get('net_precision', 'fp32') == 'bf16'
 
     def forward(self, inputs, frame_ids, _cam=None):
-        imgs = torch.cat([inputs[('color_aug', frame_ids[0], 0)], inputs[('color_aug', frame_ids[1], 0)]], 2)
-        B, N = imgs.shape[:2]
-        with net_autocast(self, imgs):
-            _, agg = _aggregate(self.encoder, self.conv1x1, pack_cam_feat(imgs), self.fusion_level, B, N)
+        frames = [inputs[('color_aug', frame_ids[0], 0)], inputs[('color_aug', frame_ids[1], 0)]]
+        B, N = frames[0].shape[:2]
+        with net_autocast(self, frames[0]):
+            if torch.is_autocast_enabled('cuda'):
+                x, normed = pack_cam_feat(torch.cat(frames, 2)), False
+            else:
+                x, normed = _encoder_input(frames)
+            _, agg = _aggregate(self.encoder, self.conv1x1, x, self.fusion_level, B, N, normed)
             bev = self.fusion_net(inputs, agg)
             axis_angle, translation = self.pose_decoder([[bev]])
         return axis_angle.float(), torch.clamp(translation.float(), -4.0, 4.0)

@@ -17,7 +17,11 @@ def main():
     out_dir = os.path.join('/tmp', 'vfd_variants', name)
     os.makedirs(out_dir, exist_ok=True)
     objs = []
+    only = os.environ.get('VFD_VARIANT_SRCS')      # e.g. "fusion.hip": the rest from the main build
     for src in B.SOURCES:
+        if only and src not in only.split(','):
+            objs.append(os.path.join(B.HERE, 'build', src.replace('.hip', '.o')))
+            continue
         o = os.path.join(out_dir, src.replace('.hip', '.o'))
         subprocess.check_call([B._hipcc()] + B.FLAGS + defs + ['-c', os.path.join(B.CSRC, src), '-o', o])
         objs.append(o)

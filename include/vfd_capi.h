@@ -410,6 +410,13 @@ int vfd_smooth_bwd(int B, int N, int H, int W, const float* disp, const float* c
 int vfd_aggregate_fwd(int BN, int C, int h, int w, const float* base, int n_levels,
                       const float* const* levels, const int* level_hw, const float* bias, float* out,
                       void* stream);
+/* backward of vfd_aggregate_fwd in one launch (one workgroup per plane, LDS-resident):
+ * d = g * LReLU'(out) [BN, C, h, w] (the base's gradient), psum [BN * C] = its plane sums (the
+ * caller sums them over n for the bias gradient), dlevels[k] [BN, C, level_hw[2k], level_hw[2k+1]]
+ * = the upsample adjoint of d (the fixed-order separable gather of vfd_upsample_ac_bwd).
+ * Needs (h * w + h * max_k level_w) * 4 <= 64 KiB (else VFD_EINVAL). */
+int vfd_aggregate_bwd(int BN, int C, int h, int w, const float* g, const float* out, float* d, int n_levels,
+                      float* const* dlevels, const int* level_hw, float* psum, void* stream);
 /* backward of the align_corners bilinear upsample (the aggregation's levels): g [planes, h, w] ->
  * dsrc [planes, hs, ws] as a separable fixed-order gather (deterministic, no atomics);
  * tmp: [planes, h, ws] scratch */

@@ -612,6 +612,37 @@ def test_reflect_pad_upsample_and_lrelu_pad_backward():
         close(dl, ref, f'upsample backward {hs}x{ws}', atol=1e-5, rtol=1e-5)
 
 
+def test_aggregate_matches_aten():
+    """The fusion-level aggregation LReLU_0.1(base + sum_k up_align_corners(level_k) + bias)
+    (fusion_depthnet.py:53-63) forward and backward (the one-launch per-plane backward: base,
+    bias and level gradients) against the ATen chain, at the config-2 shapes, config-5 shapes and
+    ragged ones."""
+    from vfdepth_amd import kernels as KN
+    gen = torch.Generator(device=DEV).manual_seed(41)
+    cases = (((6, 256, 48, 80), ((24, 40), (12, 20), (6, 10))),
+             ((2, 32, 80, 120), ((40, 60), (20, 30), (10, 15))),
+             ((3, 5, 7, 9), ((4, 5), (2, 3))),
+             ((1, 4, 6, 6), ((6, 6),)))
+    for shape, lv in cases:
+        BN, C, h, w = shape
+        base = torch.randn(shape, device=DEV, generator=gen).requires_grad_(True)
+        bias = torch.randn(C, device=DEV, generator=gen).requires_grad_(True)
+        levels = [torch.randn(BN, C, hs, ws, device=DEV, generator=gen).requires_grad_(True) for hs, ws in lv]
+        out = KN.AggregateUp.apply(base, bias, *levels)
+        rb, rbias = base.detach().clone().requires_grad_(True), bias.detach().clone().requires_grad_(True)
+        rl = [t.detach().clone().requires_grad_(True) for t in levels]
+        ref = rb + sum(F.interpolate(t, size=(h, w), mode='bilinear', align_corners=True) for t in rl)
+        ref = F.leaky_relu(ref + rbias.view(1, -1, 1, 1), 0.1)
+        close(out, ref, f'aggregate forward {shape}', atol=1e-5, rtol=1e-5)
+        g = torch.randn(shape, device=DEV, generator=gen)
+        out.backward(g)
+        ref.backward(g)
+        close(base.grad, rb.grad, f'aggregate d base {shape}', atol=1e-6, rtol=1e-6)
+        close(bias.grad, rbias.grad, f'aggregate d bias {shape}', atol=1e-3, rtol=1e-5)
+        for t, r in zip(levels, rl):
+            close(t.grad, r.grad, f'aggregate d level {tuple(t.shape)}', atol=1e-5, rtol=1e-5)
+
+
 def test_elu_upsample_pad_matches_aten():
     """The decoders' fused ELU [+ nearest 2x upsample] + reflect pad against F.elu ->
     F.interpolate(nearest) -> F.pad(reflect), forward and backward, at the config-2 decoder shapes

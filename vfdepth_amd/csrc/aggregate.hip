@@ -128,7 +128,128 @@ __global__ __launch_bounds__(256) void up_ac_bwd_y_k(const float* __restrict__ t
   }
 }
 
+// ---- one workgroup per (n, c) plane, for planes whose working set fits LDS (every config here)
+// Forward: the plane's level maps are staged in LDS once, so the 4 taps per level of every output
+// read LDS instead of L2 (the flat kernel above issued 12 global loads per output element).
+// Backward: d = g * LReLU'(out) is written once and kept in LDS; its plane sum (the bias gradient's
+// partial) and, per level, the separable gather (rows -> LDS tmp -> columns) all run from LDS.
+// Same arithmetic and summation order as aggregate_fwd_k / up_ac_bwd_{x,y}_k.
+constexpr int AGG_T = 256;
+constexpr int AGG_LDS_MAX = 64 * 1024;
+
+struct AggLevels {
+  const float* src[3];
+  float* dst[3];
+  int hs[3], ws[3];
+};
+
+template <int NL>
+__global__ __launch_bounds__(AGG_T) void aggregate_plane_fwd_k(int C, int h, int w, const float* __restrict__ base,
+                                                               AggLevels lv, const float* __restrict__ bias,
+                                                               float* __restrict__ out) {
+  extern __shared__ float agg_sm[];
+  const size_t p = blockIdx.x;                       // n * C + c
+  float* lp[3] = {agg_sm, agg_sm, agg_sm};
+  int off = 0;
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {
+    const int n = lv.hs[k] * lv.ws[k];
+    lp[k] = agg_sm + off;
+    const float* src = lv.src[k] + p * n;
+    for (int i = threadIdx.x; i < n; i += AGG_T) lp[k][i] = src[i];
+    off += n;
+  }
+  __syncthreads();
+  const float bc = bias[p % C];
+  const int hw = h * w;
+  const float* bp = base + p * hw;
+  float* op = out + p * hw;
+  for (int i = threadIdx.x; i < hw; i += AGG_T) {
+    const int x = i % w, y = i / w;
+    float v = bp[i];
+#pragma unroll
+    for (int k = 0; k < NL; ++k) v += up_ac(lp[k], lv.hs[k], lv.ws[k], h, w, y, x);
+    v += bc;
+    op[i] = v > 0.f ? v : v * 0.1f;
+  }
+}
+
+template <int NL>
+__global__ __launch_bounds__(AGG_T) void aggregate_plane_bwd_k(int h, int w, const float* __restrict__ g,
+                                                               const float* __restrict__ out, float* __restrict__ d,
+                                                               AggLevels lv, float* __restrict__ psum) {
+  extern __shared__ float agg_sm[];
+  __shared__ float wsum[AGG_T / 64];
+  const size_t p = blockIdx.x;
+  const int hw = h * w;
+  float* dp = agg_sm;
+  float* tmp = agg_sm + hw;
+  float s = 0.f;
+  for (int i = threadIdx.x; i < hw; i += AGG_T) {
+    const float ov = out[p * hw + i];
+    const float dv = g[p * hw + i] * (ov > 0.f ? 1.f : 0.1f);
+    d[p * hw + i] = dv;
+    dp[i] = dv;
+    s += dv;
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) psum[p] = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {
+    const int hs = lv.hs[k], ws = lv.ws[k];
+    for (int j = threadIdx.x; j < h * ws; j += AGG_T) {
+      const int y = j / ws, xs = j - y * ws;
+      int lo, hi;
+      up_range(xs, ws, w, &lo, &hi);
+      const float* gr = dp + y * w;
+      float acc = 0.f;
+      for (int x = lo; x <= hi; ++x) acc += up_weight(ws, w, x, xs) * gr[x];
+      tmp[j] = acc;
+    }
+    __syncthreads();
+    float* dst = lv.dst[k] + p * hs * ws;
+    for (int j = threadIdx.x; j < hs * ws; j += AGG_T) {
+      const int ys = j / ws, xs = j - ys * ws;
+      int lo, hi;
+      up_range(ys, hs, h, &lo, &hi);
+      float acc = 0.f;
+      for (int y = lo; y <= hi; ++y) acc += up_weight(hs, h, y, ys) * tmp[y * ws + xs];
+      dst[j] = acc;
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace vfd
+
+extern "C" int vfd_aggregate_bwd(int BN, int C, int h, int w, const float* g, const float* out, float* d,
+                                 int n_levels, float* const* dlevels, const int* level_hw, float* psum, void* stream) {
+  VFD_REQUIRE(BN > 0 && C > 0 && h > 0 && w > 0 && g && out && d && psum, "aggregate_bwd: bad arguments");
+  VFD_REQUIRE(n_levels >= 0 && n_levels <= 3, "up to 3 upsampled levels supported (got %d)", n_levels);
+  vfd::AggLevels lv{};
+  int wsmax = 0;
+  for (int k = 0; k < n_levels; ++k) {
+    lv.dst[k] = dlevels[k];
+    lv.hs[k] = level_hw[2 * k];
+    lv.ws[k] = level_hw[2 * k + 1];
+    VFD_REQUIRE(lv.dst[k] && lv.hs[k] > 0 && lv.ws[k] > 0 && lv.hs[k] <= h && lv.ws[k] <= w, "aggregate_bwd: level %d", k);
+    wsmax = lv.ws[k] > wsmax ? lv.ws[k] : wsmax;
+  }
+  const size_t lds = ((size_t)h * w + (size_t)h * wsmax) * 4;
+  VFD_REQUIRE(lds <= (size_t)vfd::AGG_LDS_MAX, "aggregate_bwd: plane %dx%d too large for LDS", h, w);
+  hipStream_t s = (hipStream_t)stream;
+  vfd::ProfScope ps(vfd::K_UPSAMPLE_BWD, s);
+  const unsigned nb = (unsigned)((long long)BN * C);
+  switch (n_levels) {
+    case 0: vfd::aggregate_plane_bwd_k<0><<<nb, vfd::AGG_T, lds, s>>>(h, w, g, out, d, lv, psum); break;
+    case 1: vfd::aggregate_plane_bwd_k<1><<<nb, vfd::AGG_T, lds, s>>>(h, w, g, out, d, lv, psum); break;
+    case 2: vfd::aggregate_plane_bwd_k<2><<<nb, vfd::AGG_T, lds, s>>>(h, w, g, out, d, lv, psum); break;
+    default: vfd::aggregate_plane_bwd_k<3><<<nb, vfd::AGG_T, lds, s>>>(h, w, g, out, d, lv, psum); break;
+  }
+  return vfd::fail_launch("aggregate_bwd");
+}
 
 extern "C" int vfd_upsample_ac_bwd(const float* g, float* dsrc, float* tmp, long long planes, int h, int w, int hs,
                                    int ws, void* stream) {
@@ -153,6 +274,24 @@ extern "C" int vfd_aggregate_fwd(int BN, int C, int h, int w, const float* base,
   hipStream_t s = (hipStream_t)stream;
   const size_t n = (size_t)BN * C * h * w;
   ProfScope ps(K_AGGREGATE, s);
+  size_t lds = 0;
+  AggLevels al{};
+  for (int k = 0; k < n_levels; ++k) {
+    al.src[k] = lv[k].src;
+    al.hs[k] = lv[k].h;
+    al.ws[k] = lv[k].w;
+    lds += (size_t)lv[k].h * lv[k].w * 4;
+  }
+  if (lds <= (size_t)AGG_LDS_MAX / 2) {          // per-plane form (levels staged in LDS)
+    const unsigned nb = (unsigned)((long long)BN * C);
+    switch (n_levels) {
+      case 0: aggregate_plane_fwd_k<0><<<nb, AGG_T, lds, s>>>(C, h, w, base, al, bias, out); break;
+      case 1: aggregate_plane_fwd_k<1><<<nb, AGG_T, lds, s>>>(C, h, w, base, al, bias, out); break;
+      case 2: aggregate_plane_fwd_k<2><<<nb, AGG_T, lds, s>>>(C, h, w, base, al, bias, out); break;
+      default: aggregate_plane_fwd_k<3><<<nb, AGG_T, lds, s>>>(C, h, w, base, al, bias, out); break;
+    }
+    return fail_launch("aggregate_fwd");
+  }
   switch (n_levels) {
     case 0: aggregate_fwd_k<0><<<cdiv(n, 256), 256, 0, s>>>(BN, C, h, w, base, lv[0], lv[1], lv[2], bias, out); break;
     case 1: aggregate_fwd_k<1><<<cdiv(n, 256), 256, 0, s>>>(BN, C, h, w, base, lv[0], lv[1], lv[2], bias, out); break;

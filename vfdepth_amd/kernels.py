@@ -880,8 +880,22 @@ class AggregateUp(torch.autograd.Function):
     def backward(ctx, g):
         lib = L.load()
         out, = ctx.saved_tensors
+        g = g.contiguous()
+        BN, C, h, w = g.shape
+        wsmax = max([shp[-1] for shp in ctx.level_shapes] + [0])
+        if (h * w + h * wsmax) * 4 <= 64 * 1024:     # one launch: d, its plane sums, every level
+            d = torch.empty_like(g)
+            psum = torch.empty(BN * C, device=g.device)
+            grads = [torch.empty(shp, device=g.device) for shp in ctx.level_shapes]
+            n = len(grads)
+            ptrs = (L.c_fp * max(n, 1))(*[t.data_ptr() for t in grads])
+            hw = (L.c_int * max(2 * n, 1))(*[v for shp in ctx.level_shapes for v in shp[-2:]])
+            L.check(lib.vfd_aggregate_bwd(BN, C, h, w, g.data_ptr(), out.data_ptr(), d.data_ptr(), n, ptrs, hw,
+                                          psum.data_ptr(), L.stream()), 'aggregate_bwd')
+            if L.PROF_ON:
+                L.ALG_BYTES['upsample_bwd'] += (3 * g.numel() + sum(t.numel() for t in grads)) * 4
+            return (d, psum.view(BN, C).sum(0)) + tuple(grads)
         d = (g * torch.where(out > 0, 1.0, 0.1)).contiguous()
-        BN, C, h, w = d.shape
         grads = []
         for shp in ctx.level_shapes:          # the upsample's adjoint as a gather (deterministic)
             dl = torch.empty(shp, device=d.device)

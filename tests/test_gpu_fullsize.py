@@ -690,15 +690,18 @@ def test_weight_relayouts_match_torch_chains():
     import torch.nn.functional as F
     from vfdepth_amd import kernels as KN
     gen = torch.Generator(device=DEV).manual_seed(5)
-    O, Cv, D = 256, 64, 50
-    w = torch.randn(O, Cv * D, 3, 3, device=DEV, generator=gen)
-    ref = w.reshape(O, Cv // 4, 2, 2, D, 3, 3).permute(4, 5, 6, 1, 0, 2, 3).contiguous()
-    assert torch.equal(KN.proj_conv_weight_fragments(w, Cv, D), ref)
-    n, npad = Cv * D, (Cv * D + 255) // 256 * 256
-    wd = F.pad(w.reshape(O, Cv, D, 3, 3).flip(3, 4).permute(3, 4, 0, 2, 1).reshape(9, O, n), (0, npad - n))
-    ref = wd.reshape(9, O // 4, 2, 2, npad).permute(0, 1, 4, 2, 3).contiguous()
-    assert torch.equal(KN.proj_conv_dgrad_weight(w, Cv, D), ref)
-    for C1, Z in ((257, 20), (13, 3)):
+    # tiled kernels (O % 16, Cv % 16) at the config-2 shape and ragged depth chunks / padding; the
+    # row-per-thread kernel for the other shapes
+    for O, Cv, D in ((256, 64, 50), (32, 16, 23), (20, 12, 7)):
+        w = torch.randn(O, Cv * D, 3, 3, device=DEV, generator=gen)
+        ref = w.reshape(O, Cv // 4, 2, 2, D, 3, 3).permute(4, 5, 6, 1, 0, 2, 3).contiguous()
+        assert torch.equal(KN.proj_conv_weight_fragments(w, Cv, D), ref), (O, Cv, D)
+        n, npad = Cv * D, (Cv * D + 255) // 256 * 256
+        wd = F.pad(w.reshape(O, Cv, D, 3, 3).flip(3, 4).permute(3, 4, 0, 2, 1).reshape(9, O, n), (0, npad - n))
+        ref = wd.reshape(9, O // 4, 2, 2, npad).permute(0, 1, 4, 2, 3).contiguous()
+        assert torch.equal(KN.proj_conv_dgrad_weight(w, Cv, D), ref), (O, Cv, D)
+    O = 256
+    for C1, Z in ((256, 20), (8, 6), (257, 20), (13, 3)):
         wp = torch.randn(O, C1 * Z, 3, 3, device=DEV, generator=gen)
         wz = wp.view(O, C1, Z, 3, 3).transpose(1, 2).reshape(O, Z * C1, 3, 3)
         cpad = (C1 * Z + 15) // 16 * 16

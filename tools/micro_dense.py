@@ -96,6 +96,15 @@ def main():
         go = torch.randn_like(out)
         line(f'bn+relu fwd {shape}', timeit(lambda: bn_act(bn, t)), t.numel() * 12)
         line(f'bn+relu fwd+bwd {shape}', timeit(lambda: torch.autograd.grad(bn_act(bn, t), t, go)), t.numel() * 32)
+    # per-step weight relayouts (weights.hip) at the config-2 reduce_dim weights
+    wk = torch.randn(256, 64 * 50, 3, 3, device=dev)
+    line('K3C fwd fragments 256x3200x9', timeit(lambda: KN.proj_conv_weight_fragments(wk, 64, 50)), wk.numel() * 8)
+    line('K3C dgrad copy 256x3200x9', timeit(lambda: KN.proj_conv_dgrad_weight(wk, 64, 50)), wk.numel() * 8)
+    wp = torch.randn(256, 256 * 20, 3, 3, device=dev)
+    line('K2C pose fragments 256x5120x9', timeit(lambda: KN.pose_conv_fragments(wp, 256, 20)), wp.numel() * 8)
+    line('pose swap -> channels-last', timeit(lambda: KN.weight_swap(wp, 256, 20, memory_format=torch.channels_last)), wp.numel() * 8)
+    wpc = wp.contiguous(memory_format=torch.channels_last)
+    line('pose swap channels-last -> NCHW', timeit(lambda: KN.weight_swap(wpc, 20, 256)), wp.numel() * 8)
 
 
 if __name__ == '__main__':

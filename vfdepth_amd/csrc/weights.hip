@@ -69,6 +69,97 @@ __global__ __launch_bounds__(256) void weight_frag_k(WrArgs a, const float* __re
   for (int k = 0; k < WR_TAPS; ++k) dst[off + (flip ? WR_TAPS - 1 - k : k) * plane] = v[k];
 }
 
+// Tiled forms of the three fragment modes for the step's large weights: a workgroup stages a
+// tile whose source rows are contiguous runs (a 9-tap row per (out, in)-channel, several rows in
+// a run) through LDS, then writes destination runs of 32-64 consecutive floats.  Same values and
+// placement as weight_frag_k (a copy: bit-identical); weight_frag_k stays for shapes the tiles do
+// not cover.
+constexpr int WT_DT = 10;                 // depth bins per tile (modes 1, 2)
+constexpr int WT_TILE = 64 * WT_DT * WR_TAPS;
+
+// mode 1: tile = 16 out-channels x one channel quad q x WT_DT depth bins; source runs
+// w[o][(4q + c) * D + d0 .. + nd][taps] (nd * 9 floats), destination runs (d, tap, q): 16 o x 4 c
+__global__ __launch_bounds__(256) void wfrag1_k(const float* __restrict__ w, float* __restrict__ dst, int O, int Cv,
+                                                int D) {
+  __shared__ float tile[WT_TILE];
+  const int o0 = blockIdx.x * 16, q = blockIdx.y, d0 = blockIdx.z * WT_DT;
+  const int nd = min(WT_DT, D - d0), K = Cv * D, Q = Cv / 4;
+  const int seg = nd * WR_TAPS, no = min(16, O - o0);
+  for (int i = threadIdx.x; i < 64 * seg; i += 256) {
+    const int r = i / seg, k = i - r * seg;          // r = o_l * 4 + c_l
+    if ((r >> 2) < no)
+      tile[r * WT_DT * WR_TAPS + k] = w[((size_t)(o0 + (r >> 2)) * K + (size_t)(4 * q + (r & 3)) * D + d0) * WR_TAPS + k];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < seg * 64; i += 256) {
+    const int r = i & 63, dt = i >> 6;               // dt = d_l * 9 + tap
+    const int d_l = dt / WR_TAPS, tap = dt - d_l * WR_TAPS;
+    if ((r >> 2) < no)
+      dst[(((size_t)(d0 + d_l) * WR_TAPS + tap) * Q + q) * O * 4 + (size_t)o0 * 4 + r] = tile[r * WT_DT * WR_TAPS + dt];
+  }
+}
+
+// mode 2: tile = one out-channel quad oq x 16 channels x WT_DT depth bins; source runs
+// w[4 oq + o][(c0 + c) * D + d0 .. + nd][taps], destination runs (8 - tap, oq, d): 16 c x 4 o
+// (n = d * Cv + c); the zero rows n >= Cv * D are written by wfrag2_pad_k
+__global__ __launch_bounds__(256) void wfrag2_k(const float* __restrict__ w, float* __restrict__ dst, int O, int Cv,
+                                                int D, int npad) {
+  __shared__ float tile[WT_TILE];
+  const int oq = blockIdx.x, c0 = blockIdx.y * 16, d0 = blockIdx.z * WT_DT;
+  const int nd = min(WT_DT, D - d0), K = Cv * D, OQ = O / 4;
+  const int seg = nd * WR_TAPS, nc = min(16, Cv - c0);
+  for (int i = threadIdx.x; i < 64 * seg; i += 256) {
+    const int r = i / seg, k = i - r * seg;          // r = o_l * 16 + c_l
+    const int o_l = r >> 4, c_l = r & 15;
+    if (c_l < nc)
+      tile[r * WT_DT * WR_TAPS + k] = w[((size_t)(4 * oq + o_l) * K + (size_t)(c0 + c_l) * D + d0) * WR_TAPS + k];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < seg * 64; i += 256) {
+    const int r = i & 63, dt = i >> 6;
+    const int c_l = r >> 2, o_l = r & 3;
+    const int d_l = dt / WR_TAPS, tap = dt - d_l * WR_TAPS;
+    if (c_l < nc) {
+      const size_t n = (size_t)(d0 + d_l) * Cv + c0 + c_l;
+      dst[(((size_t)(WR_TAPS - 1 - tap) * OQ + oq) * npad + n) * 4 + o_l] = tile[(o_l * 16 + c_l) * WT_DT * WR_TAPS + dt];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void wfrag2_pad_k(float* __restrict__ dst, int OQ, int K, int npad) {
+  const long long per = (long long)(npad - K) * 4;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)WR_TAPS * OQ * per) return;
+  const long long plane = i / per, r = i - plane * per;    // plane = tap' * OQ + oq
+  dst[(plane * npad + K) * 4 + r] = 0.f;
+}
+
+// mode 0 with the pose map's channel order (cz = z * C1 + c, reference channel c * Z + z):
+// tile = 8 out-channels x 4 map channels c0 .. c0 + 3 x all Z; source runs w[o][c0 * Z .. (c0 + 4) * Z][taps]
+// (4 Z rows), destination runs (tap, q = (z C1 + c0) / 4): 8 o x 4 cz.  Needs C1 % 4 == 0 and
+// C1 * Z % 16 == 0 (no zero rows).  Dynamic LDS: 8 * 4 * Z * 9 floats.
+__global__ __launch_bounds__(256) void wfrag0z_k(const float* __restrict__ w, float* __restrict__ dst, int O, int C1,
+                                                 int Z) {
+  extern __shared__ float wt_sm[];
+  const int o0 = blockIdx.x * 8, c0 = blockIdx.y * 4;
+  const int C = C1 * Z, seg = 4 * Z * WR_TAPS, no = min(8, O - o0);
+  for (int i = threadIdx.x; i < 8 * seg; i += 256) {
+    const int o_l = i / seg, k = i - o_l * seg;
+    if (o_l < no) wt_sm[i] = w[((size_t)(o0 + o_l) * C + (size_t)c0 * Z) * WR_TAPS + k];
+  }
+  __syncthreads();
+  const int qn = C / 4;
+  for (int i = threadIdx.x; i < Z * WR_TAPS * 32; i += 256) {
+    const int r = i & 31, zt = i >> 5;
+    const int o_l = r >> 2, c_l = r & 3;
+    const int z = zt / WR_TAPS, tap = zt - z * WR_TAPS;
+    if (o_l < no) {
+      const int q = (z * C1 + c0) >> 2;
+      dst[(((size_t)tap * qn + q) * O + o0 + o_l) * 4 + c_l] = wt_sm[o_l * seg + ((c_l * Z) + z) * WR_TAPS + tap];
+    }
+  }
+}
+
 // Generic 4-D permuted copy of a weight, element (o, a, b, t) from src[o so + a sa + b sb + t st]
 // to dst[o do + a da + b db + t dt] (t <= 9 taps): tiles of 16 x 16 (a, b) x all taps go through
 // LDS so that whichever of a / b is contiguous on either side is walked by consecutive lanes.
@@ -148,6 +239,24 @@ int vfd_weight_fragments(int mode, const float* w, float* dst, int O, int C, int
     return VFD_EINVAL;
   }
   hipStream_t s = (hipStream_t)stream;
+  if (mode == 1 && O % 16 == 0) {
+    wfrag1_k<<<dim3((unsigned)(O / 16), (unsigned)(Cv / 4), (unsigned)((D + WT_DT - 1) / WT_DT)), 256, 0, s>>>(w, dst, O, Cv, D);
+    return fail_launch("weight_fragments");
+  }
+  if (mode == 2 && Cv % 16 == 0) {
+    wfrag2_k<<<dim3((unsigned)(O / 4), (unsigned)(Cv / 16), (unsigned)((D + WT_DT - 1) / WT_DT)), 256, 0, s>>>(w, dst, O, Cv, D,
+                                                                                                        a.npad);
+    if (a.npad > Cv * D) {
+      const long long n = (long long)WR_TAPS * (O / 4) * (a.npad - Cv * D) * 4;
+      wfrag2_pad_k<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(dst, O / 4, Cv * D, a.npad);
+    }
+    return fail_launch("weight_fragments");
+  }
+  if (mode == 0 && a.refperm && C1 % 4 == 0 && C % 16 == 0 && Z <= 40) {
+    const size_t lds = (size_t)8 * 4 * Z * WR_TAPS * 4;
+    wfrag0z_k<<<dim3((unsigned)((O + 7) / 8), (unsigned)(C1 / 4)), 256, lds, s>>>(w, dst, O, C1, Z);
+    return fail_launch("weight_fragments");
+  }
   weight_frag_k<<<(unsigned)((nrow + 255) / 256), 256, 0, s>>>(a, w, dst, nrow);
   return fail_launch("weight_fragments");
 }

@@ -414,7 +414,7 @@ int vfd_aggregate_fwd(int BN, int C, int h, int w, const float* base, int n_leve
  * d = g * LReLU'(out) [BN, C, h, w] (the base's gradient), psum [BN * C] = its plane sums (the
  * caller sums them over n for the bias gradient), dlevels[k] [BN, C, level_hw[2k], level_hw[2k+1]]
  * = the upsample adjoint of d (the fixed-order separable gather of vfd_upsample_ac_bwd).
- * Needs (h * w + h * max_k level_w) * 4 <= 64 KiB (else VFD_EINVAL). */
+ * Needs (h * w + h * max_k level_w + 5 * (h + w)) * 4 <= 64 KiB (else VFD_EINVAL). */
 int vfd_aggregate_bwd(int BN, int C, int h, int w, const float* g, const float* out, float* d, int n_levels,
                       float* const* dlevels, const int* level_hw, float* psum, void* stream);
 /* backward of the align_corners bilinear upsample (the aggregation's levels): g [planes, h, w] ->

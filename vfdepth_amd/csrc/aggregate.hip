@@ -164,14 +164,31 @@ __global__ __launch_bounds__(AGG_T) void aggregate_plane_fwd_k(int C, int h, int
   const int hw = h * w;
   const float* bp = base + p * hw;
   float* op = out + p * hw;
-  for (int i = threadIdx.x; i < hw; i += AGG_T) {
-    const int x = i % w, y = i / w;
-    float v = bp[i];
+  constexpr int U = 4;                               // base loads in flight per thread
+  for (int i0 = threadIdx.x; i0 < hw; i0 += U * AGG_T) {
+    float bv[U];
 #pragma unroll
-    for (int k = 0; k < NL; ++k) v += up_ac(lp[k], lv.hs[k], lv.ws[k], h, w, y, x);
-    v += bc;
-    op[i] = v > 0.f ? v : v * 0.1f;
+    for (int u = 0; u < U; ++u) bv[u] = bp[min(i0 + u * AGG_T, hw - 1)];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * AGG_T;
+      if (i < hw) {
+        const int x = i % w, y = i / w;
+        float v = bv[u];
+#pragma unroll
+        for (int k = 0; k < NL; ++k) v += up_ac(lp[k], lv.hs[k], lv.ws[k], h, w, y, x);
+        v += bc;
+        op[i] = v > 0.f ? v : v * 0.1f;
+      }
+    }
   }
+}
+
+// floats of the backward's gather scratch: h x the widest level
+__device__ __forceinline__ int agg_tmp_floats(int h, const AggLevels& lv, int nl) {
+  int m = 0;
+  for (int k = 0; k < nl; ++k) m = max(m, lv.ws[k]);
+  return h * m;
 }
 
 template <int NL>
@@ -185,37 +202,79 @@ __global__ __launch_bounds__(AGG_T) void aggregate_plane_bwd_k(int h, int w, con
   float* dp = agg_sm;
   float* tmp = agg_sm + hw;
   float s = 0.f;
-  for (int i = threadIdx.x; i < hw; i += AGG_T) {
-    const float ov = out[p * hw + i];
-    const float dv = g[p * hw + i] * (ov > 0.f ? 1.f : 0.1f);
-    d[p * hw + i] = dv;
-    dp[i] = dv;
-    s += dv;
+  constexpr int U = 4;                               // loads in flight per thread
+  const float* gp = g + p * hw;
+  const float* opl = out + p * hw;
+  for (int i0 = threadIdx.x; i0 < hw; i0 += U * AGG_T) {
+    float gv[U], ov[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = min(i0 + u * AGG_T, hw - 1);
+      gv[u] = gp[i];
+      ov[u] = opl[i];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * AGG_T;
+      if (i < hw) {
+        const float dv = gv[u] * (ov[u] > 0.f ? 1.f : 0.1f);
+        d[p * hw + i] = dv;
+        dp[i] = dv;
+        s += dv;
+      }
+    }
   }
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = s;
   __syncthreads();
   if (threadIdx.x == 0) psum[p] = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+  // per level: the forward's taps of every output column / row and each source's candidate
+  // range, once per plane in LDS (the gathers then read tables instead of redoing up_axis per tap)
+  int* xt0 = reinterpret_cast<int*>(tmp + agg_tmp_floats(h, lv, NL));
+  int* xt1 = xt0 + w;
+  float* xl = reinterpret_cast<float*>(xt1 + w);
+  int* yt0 = reinterpret_cast<int*>(xl + w);
+  int* yt1 = yt0 + h;
+  float* yl = reinterpret_cast<float*>(yt1 + h);
+  int* xlo = reinterpret_cast<int*>(yl + h);
+  int* xhi = xlo + w;
+  int* ylo = xhi + w;
+  int* yhi = ylo + h;
 #pragma unroll
   for (int k = 0; k < NL; ++k) {
     const int hs = lv.hs[k], ws = lv.ws[k];
+    for (int i = threadIdx.x; i < w + h; i += AGG_T) {
+      if (i < w) {
+        up_axis(ws, w, i, &xt0[i], &xt1[i], &xl[i]);
+        if (i < ws) up_range(i, ws, w, &xlo[i], &xhi[i]);
+      } else {
+        const int y = i - w;
+        up_axis(hs, h, y, &yt0[y], &yt1[y], &yl[y]);
+        if (y < hs) up_range(y, hs, h, &ylo[y], &yhi[y]);
+      }
+    }
+    __syncthreads();
     for (int j = threadIdx.x; j < h * ws; j += AGG_T) {
       const int y = j / ws, xs = j - y * ws;
-      int lo, hi;
-      up_range(xs, ws, w, &lo, &hi);
+      const int lo = xlo[xs], hi = xhi[xs];
       const float* gr = dp + y * w;
       float acc = 0.f;
-      for (int x = lo; x <= hi; ++x) acc += up_weight(ws, w, x, xs) * gr[x];
+      for (int x = lo; x <= hi; ++x) {
+        const float l = xl[x];
+        acc += ((xt0[x] == xs ? 1.f - l : 0.f) + (xt1[x] == xs ? l : 0.f)) * gr[x];
+      }
       tmp[j] = acc;
     }
     __syncthreads();
     float* dst = lv.dst[k] + p * hs * ws;
     for (int j = threadIdx.x; j < hs * ws; j += AGG_T) {
       const int ys = j / ws, xs = j - ys * ws;
-      int lo, hi;
-      up_range(ys, hs, h, &lo, &hi);
+      const int lo = ylo[ys], hi = yhi[ys];
       float acc = 0.f;
-      for (int y = lo; y <= hi; ++y) acc += up_weight(hs, h, y, ys) * tmp[y * ws + xs];
+      for (int y = lo; y <= hi; ++y) {
+        const float l = yl[y];
+        acc += ((yt0[y] == ys ? 1.f - l : 0.f) + (yt1[y] == ys ? l : 0.f)) * tmp[y * ws + xs];
+      }
       dst[j] = acc;
     }
     __syncthreads();
@@ -237,7 +296,7 @@ extern "C" int vfd_aggregate_bwd(int BN, int C, int h, int w, const float* g, co
     VFD_REQUIRE(lv.dst[k] && lv.hs[k] > 0 && lv.ws[k] > 0 && lv.hs[k] <= h && lv.ws[k] <= w, "aggregate_bwd: level %d", k);
     wsmax = lv.ws[k] > wsmax ? lv.ws[k] : wsmax;
   }
-  const size_t lds = ((size_t)h * w + (size_t)h * wsmax) * 4;
+  const size_t lds = ((size_t)h * w + (size_t)h * wsmax + 5 * (size_t)(w + h)) * 4;   // d, tmp, tap tables
   VFD_REQUIRE(lds <= (size_t)vfd::AGG_LDS_MAX, "aggregate_bwd: plane %dx%d too large for LDS", h, w);
   hipStream_t s = (hipStream_t)stream;
   vfd::ProfScope ps(vfd::K_UPSAMPLE_BWD, s);

@@ -883,7 +883,7 @@ class AggregateUp(torch.autograd.Function):
         g = g.contiguous()
         BN, C, h, w = g.shape
         wsmax = max([shp[-1] for shp in ctx.level_shapes] + [0])
-        if (h * w + h * wsmax) * 4 <= 64 * 1024:     # one launch: d, its plane sums, every level
+        if (h * w + h * wsmax + 5 * (h + w)) * 4 <= 64 * 1024:     # one launch: d, its plane sums, every level
             d = torch.empty_like(g)
             psum = torch.empty(BN * C, device=g.device)
             grads = [torch.empty(shp, device=g.device) for shp in ctx.level_shapes]

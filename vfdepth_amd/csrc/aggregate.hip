@@ -135,6 +135,7 @@ __global__ __launch_bounds__(256) void up_ac_bwd_y_k(const float* __restrict__ t
 // partial) and, per level, the separable gather (rows -> LDS tmp -> columns) all run from LDS.
 // Same arithmetic and summation order as aggregate_fwd_k / up_ac_bwd_{x,y}_k.
 constexpr int AGG_T = 256;
+constexpr int AGG_BT = 512;                        // backward: more lanes per plane for its serial phases
 constexpr int AGG_LDS_MAX = 64 * 1024;
 
 struct AggLevels {
@@ -192,11 +193,11 @@ __device__ __forceinline__ int agg_tmp_floats(int h, const AggLevels& lv, int nl
 }
 
 template <int NL>
-__global__ __launch_bounds__(AGG_T) void aggregate_plane_bwd_k(int h, int w, const float* __restrict__ g,
+__global__ __launch_bounds__(AGG_BT) void aggregate_plane_bwd_k(int h, int w, const float* __restrict__ g,
                                                                const float* __restrict__ out, float* __restrict__ d,
                                                                AggLevels lv, float* __restrict__ psum) {
   extern __shared__ float agg_sm[];
-  __shared__ float wsum[AGG_T / 64];
+  __shared__ float wsum[AGG_BT / 64];
   const size_t p = blockIdx.x;
   const int hw = h * w;
   float* dp = agg_sm;
@@ -205,17 +206,17 @@ __global__ __launch_bounds__(AGG_T) void aggregate_plane_bwd_k(int h, int w, con
   constexpr int U = 4;                               // loads in flight per thread
   const float* gp = g + p * hw;
   const float* opl = out + p * hw;
-  for (int i0 = threadIdx.x; i0 < hw; i0 += U * AGG_T) {
+  for (int i0 = threadIdx.x; i0 < hw; i0 += U * AGG_BT) {
     float gv[U], ov[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int i = min(i0 + u * AGG_T, hw - 1);
+      const int i = min(i0 + u * AGG_BT, hw - 1);
       gv[u] = gp[i];
       ov[u] = opl[i];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int i = i0 + u * AGG_T;
+      const int i = i0 + u * AGG_BT;
       if (i < hw) {
         const float dv = gv[u] * (ov[u] > 0.f ? 1.f : 0.1f);
         d[p * hw + i] = dv;
@@ -227,7 +228,12 @@ __global__ __launch_bounds__(AGG_T) void aggregate_plane_bwd_k(int h, int w, con
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) psum[p] = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < AGG_BT / 64; ++k) t += wsum[k];
+    psum[p] = t;
+  }
   // per level: the forward's taps of every output column / row and each source's candidate
   // range, once per plane in LDS (the gathers then read tables instead of redoing up_axis per tap)
   int* xt0 = reinterpret_cast<int*>(tmp + agg_tmp_floats(h, lv, NL));
@@ -243,7 +249,7 @@ __global__ __launch_bounds__(AGG_T) void aggregate_plane_bwd_k(int h, int w, con
 #pragma unroll
   for (int k = 0; k < NL; ++k) {
     const int hs = lv.hs[k], ws = lv.ws[k];
-    for (int i = threadIdx.x; i < w + h; i += AGG_T) {
+    for (int i = threadIdx.x; i < w + h; i += AGG_BT) {
       if (i < w) {
         up_axis(ws, w, i, &xt0[i], &xt1[i], &xl[i]);
         if (i < ws) up_range(i, ws, w, &xlo[i], &xhi[i]);
@@ -254,7 +260,7 @@ __global__ __launch_bounds__(AGG_T) void aggregate_plane_bwd_k(int h, int w, con
       }
     }
     __syncthreads();
-    for (int j = threadIdx.x; j < h * ws; j += AGG_T) {
+    for (int j = threadIdx.x; j < h * ws; j += AGG_BT) {
       const int y = j / ws, xs = j - y * ws;
       const int lo = xlo[xs], hi = xhi[xs];
       const float* gr = dp + y * w;
@@ -267,7 +273,7 @@ __global__ __launch_bounds__(AGG_T) void aggregate_plane_bwd_k(int h, int w, con
     }
     __syncthreads();
     float* dst = lv.dst[k] + p * hs * ws;
-    for (int j = threadIdx.x; j < hs * ws; j += AGG_T) {
+    for (int j = threadIdx.x; j < hs * ws; j += AGG_BT) {
       const int ys = j / ws, xs = j - ys * ws;
       const int lo = ylo[ys], hi = yhi[ys];
       float acc = 0.f;
@@ -302,10 +308,10 @@ extern "C" int vfd_aggregate_bwd(int BN, int C, int h, int w, const float* g, co
   vfd::ProfScope ps(vfd::K_UPSAMPLE_BWD, s);
   const unsigned nb = (unsigned)((long long)BN * C);
   switch (n_levels) {
-    case 0: vfd::aggregate_plane_bwd_k<0><<<nb, vfd::AGG_T, lds, s>>>(h, w, g, out, d, lv, psum); break;
-    case 1: vfd::aggregate_plane_bwd_k<1><<<nb, vfd::AGG_T, lds, s>>>(h, w, g, out, d, lv, psum); break;
-    case 2: vfd::aggregate_plane_bwd_k<2><<<nb, vfd::AGG_T, lds, s>>>(h, w, g, out, d, lv, psum); break;
-    default: vfd::aggregate_plane_bwd_k<3><<<nb, vfd::AGG_T, lds, s>>>(h, w, g, out, d, lv, psum); break;
+    case 0: vfd::aggregate_plane_bwd_k<0><<<nb, vfd::AGG_BT, lds, s>>>(h, w, g, out, d, lv, psum); break;
+    case 1: vfd::aggregate_plane_bwd_k<1><<<nb, vfd::AGG_BT, lds, s>>>(h, w, g, out, d, lv, psum); break;
+    case 2: vfd::aggregate_plane_bwd_k<2><<<nb, vfd::AGG_BT, lds, s>>>(h, w, g, out, d, lv, psum); break;
+    default: vfd::aggregate_plane_bwd_k<3><<<nb, vfd::AGG_BT, lds, s>>>(h, w, g, out, d, lv, psum); break;
   }
   return vfd::fail_launch("aggregate_bwd");
 }

@@ -799,10 +799,11 @@ def test_normalize_cat_bit_identical():
 def test_stem_max_pool_matches_aten():
     """MaxPool2d(3, 2, 1) with the one-byte argmax: forward bit-identical to ATen (ties of a ReLU
     map's zeros go to the first maximum in scan order), backward equal to ATen's (fixed-order sum of
-    the <= 4 windows a pixel wins); odd and even sizes, the bench's stem shapes included."""
+    the <= 4 windows a pixel wins); odd and even sizes, the bench's stem shapes included (even
+    widths with wo % 4 == 0 take the four-outputs-per-thread forward)."""
     from vfdepth_amd import kernels as KN
     gen = torch.Generator(device=DEV).manual_seed(41)
-    for shape in ((6, 64, 192, 320), (2, 64, 96, 160), (3, 5, 37, 53), (1, 2, 1, 1), (2, 3, 2, 7)):
+    for shape in ((6, 64, 192, 320), (2, 64, 96, 160), (2, 3, 8, 16), (3, 5, 37, 53), (1, 2, 1, 1), (2, 3, 2, 7)):
         x = torch.relu(torch.randn(shape, device=DEV, generator=gen)).requires_grad_(True)
         if shape[-1] > 10:
             x.data[:, :, ::3, ::2] = 0.5                                  # equal maxima in one window

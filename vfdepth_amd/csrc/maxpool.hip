@@ -43,6 +43,57 @@ __global__ __launch_bounds__(256) void maxpool_fwd_k(const float* __restrict__ x
   }
 }
 
+// Four consecutive outputs per thread (wo % 4 == 0, w == 2 wo): each of the 3 window rows is one
+// scalar (column 2 ox0 - 1) and two 16-B loads (columns 2 ox0 .. 2 ox0 + 7), 9 load instructions
+// for 4 outputs instead of 36; the taps, their order and the selection are maxpool_fwd_k's.
+__global__ __launch_bounds__(256) void maxpool_fwd4_k(const float* __restrict__ x, float* __restrict__ y,
+                                                      uint8_t* __restrict__ arg, long long planes, int h, int w,
+                                                      int ho, int wo) {
+  const int wq = wo / 4;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= ho * wq) return;
+  const int oy = j / wq, ox0 = (j - oy * wq) * 4;
+  for (long long p = blockIdx.y; p < planes; p += gridDim.y) {
+    const float* xp = x + (size_t)p * h * w;
+    float r[3][9];
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const float* row = xp + min(max(2 * oy - 1 + ky, 0), h - 1) * w;
+      const float4 a = *reinterpret_cast<const float4*>(row + 2 * ox0);
+      const float4 b = *reinterpret_cast<const float4*>(row + 2 * ox0 + 4);
+      r[ky][0] = row[max(2 * ox0 - 1, 0)];
+      r[ky][1] = a.x; r[ky][2] = a.y; r[ky][3] = a.z; r[ky][4] = a.w;
+      r[ky][5] = b.x; r[ky][6] = b.y; r[ky][7] = b.z; r[ky][8] = b.w;
+    }
+    float best4[4];
+    unsigned code = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int ox = ox0 + e;
+      float best = -INFINITY;
+      int bi = 4;
+      bool first = true;
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        const int ky = k / 3, kx = k % 3;
+        const int yy = 2 * oy - 1 + ky, xx = 2 * ox - 1 + kx;
+        const bool ok = yy >= 0 && yy < h && xx >= 0 && xx < w;
+        const float v = r[ky][2 * e + kx];
+        if (ok && (first || v > best || isnan(v))) {
+          best = v;
+          bi = k;
+          first = false;
+        }
+      }
+      best4[e] = best;
+      code |= (unsigned)bi << (8 * e);
+    }
+    const size_t i = (size_t)p * ho * wo + (size_t)oy * wo + ox0;
+    *reinterpret_cast<float4*>(y + i) = make_float4(best4[0], best4[1], best4[2], best4[3]);
+    *reinterpret_cast<unsigned*>(arg + i) = code;
+  }
+}
+
 // One thread per 2x2 input block (rows 2i, 2i+1; columns 2j, 2j+1): the block's pixels are covered
 // by the output windows (i, j), (i, j+1), (i+1, j), (i+1, j+1) only (pixel 2i sits in window i's
 // centre row, pixel 2i+1 in window i's last row and window i+1's first), so 4 gradient and 4 index
@@ -120,6 +171,10 @@ int vfd_maxpool3s2_fwd(const float* x, float* y, uint8_t* arg, long long planes,
   vfd::ProfScope ps(vfd::K_MAXPOOL, s);
   const int ho = (h - 1) / 2 + 1, wo = (w - 1) / 2 + 1;
   const unsigned gy = (unsigned)(planes < 65535 ? planes : 65535);
+  if (wo % 4 == 0 && w == 2 * wo && (((uintptr_t)x | (uintptr_t)y) & 15) == 0 && ((uintptr_t)arg & 3) == 0) {
+    vfd::maxpool_fwd4_k<<<dim3((unsigned)((ho * (wo / 4) + 255) / 256), gy), 256, 0, s>>>(x, y, arg, planes, h, w, ho, wo);
+    return vfd::fail_launch("maxpool3s2_fwd");
+  }
   vfd::maxpool_fwd_k<<<dim3((unsigned)((ho * wo + 255) / 256), gy), 256, 0, s>>>(x, y, arg, planes, h, w, ho, wo);
   return vfd::fail_launch("maxpool3s2_fwd");
 }

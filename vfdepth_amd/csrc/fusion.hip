@@ -589,8 +589,8 @@ template <int NC>
 __global__ __launch_bounds__(256) void fusion_plan_k(vfd_voxel_desc d, const float* __restrict__ mlo,
                                                      const float* __restrict__ K, const float* __restrict__ Einv,
                                                      PlanEntry* __restrict__ plan, int* __restrict__ counts) {
-  __shared__ int wave_cnt[4];
-  __shared__ int block_base;
+  __shared__ int wave_cnt[NC][4];
+  __shared__ int block_base[NC];
   const int V = d.X * d.Y * d.Z;
   const int b = blockIdx.y;
   const int v = blockIdx.x * blockDim.x + threadIdx.x;
@@ -617,20 +617,27 @@ __global__ __launch_bounds__(256) void fusion_plan_k(vfd_voxel_desc d, const flo
 #pragma unroll
     for (int c = 0; c < NC; ++c) val[c] = false;
   }
+  // every camera's wave counts, then one thread per camera reserves the block's run of entries:
+  // the NC counter atomics are in flight together (two barriers instead of three per camera)
+  int before[NC];
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     const unsigned long long m = __ballot(val[c]);
-    const int before = __popcll(m & ((1ull << lane) - 1ull));
-    if (lane == 0) wave_cnt[wv] = __popcll(m);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const int tot = wave_cnt[0] + wave_cnt[1] + wave_cnt[2] + wave_cnt[3];
-      block_base = tot ? atomicAdd(counts + b * NC + c, tot) : 0;
-    }
-    __syncthreads();
+    before[c] = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) wave_cnt[c][wv] = __popcll(m);
+  }
+  __syncthreads();
+  if (threadIdx.x < NC) {
+    const int c = threadIdx.x;
+    const int tot = wave_cnt[c][0] + wave_cnt[c][1] + wave_cnt[c][2] + wave_cnt[c][3];
+    block_base[c] = tot ? atomicAdd(counts + b * NC + c, tot) : 0;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
     if (val[c]) {
-      int off = block_base + before;
-      for (int k = 0; k < wv; ++k) off += wave_cnt[k];
+      int off = block_base[c] + before[c];
+      for (int k = 0; k < wv; ++k) off += wave_cnt[c][k];
       Bilinear bl = bilinear_taps(g[c].ix, g[c].iy, d.w, d.h);
       PlanEntry e;
       unsigned in = 0;
@@ -647,7 +654,6 @@ __global__ __launch_bounds__(256) void fusion_plan_k(vfd_voxel_desc d, const flo
       e.pad = 0;
       plan[((size_t)b * NC + c) * V + off] = e;
     }
-    __syncthreads();
   }
 }
 

@@ -146,9 +146,12 @@ int vfd_proj_conv_fwd(const vfd_voxel_desc* d, const float* vox, const float* in
 /* Training-mode BatchNorm2d of the ResNet encoders (fusion_depthnet.py:24-36, fusion_posenet.py:
  * 22-35; torchvision BasicBlock/Bottleneck/stem), fused with the block's residual add and ReLU:
  * y = relu((x - mean) * invstd * gamma + beta [+ r]), NCHW fp32.  Statistics in fp64, per
- * (channel, split) partials [C][S][2] summed in a fixed order.  SyncBatchNorm (DDP): vfd_bn_sum
- * reduces the partials to [C][2] sums that the host all-reduces, then the apply passes take
- * ns = 1 and the global element count. */
+ * (channel, split) partials [C][S][2] summed in a fixed order.  SyncBatchNorm (DDP,
+ * models/vfdepth.py:68 convert_sync_batchnorm): vfd_bn_sum reduces the partials to [C+1][2] sums
+ * whose row C carries the local element count; the host all-reduces that buffer (ONE collective per
+ * direction, like torch's SyncBatchNorm: one all_gather forward, one all_reduce backward) and the
+ * apply passes take ns = 1 and count = 0, which makes them read the global count from row C on the
+ * device (no host synchronisation). */
 typedef struct vfd_bn_desc {
   int32_t N, C, HW;      /* images, channels, H*W                                        */
   int32_t S;             /* splits per channel: vfd_bn_splits(desc)                      */
@@ -158,8 +161,13 @@ typedef struct vfd_bn_desc {
 
 int vfd_bn_splits(const vfd_bn_desc* d);
 int vfd_bn_fwd_stats(const vfd_bn_desc* d, const float* x, double* partial, void* stream);
-int vfd_bn_sum(const vfd_bn_desc* d, const double* partial, double* sums, void* stream);
-/* sums: the [C][S][2] partials (ns = S) or reduced [C][2] sums (ns = 1); residual / running stats
+/* count > 0: also writes row C = (count, 0).  invstd / dgamma / dbeta (backward, nullable): d gamma
+ * = sum g'(x - mean) * invstd and d beta = sum g' from this rank's LOCAL sums (SyncBatchNorm's
+ * parameter gradients are local; DDP averages them). */
+int vfd_bn_sum(const vfd_bn_desc* d, const double* partial, double count, double* sums, const float* invstd,
+               float* dgamma, float* dbeta, void* stream);
+/* sums: the [C][S][2] partials (ns = S) or reduced [C][2] sums (ns = 1; count <= 0: the element
+ * count is read from row C of the reduced sums, see vfd_bn_sum); residual / running stats
  * / num_batches_tracked (int64, += 1) nullable.  Writes y and the per-channel mean / invstd the
  * backward reads. */
 /* relu_mask (optional, N*C*HW bytes): the forward also stores [y > 0] per element; a backward call
@@ -236,18 +244,6 @@ int vfd_dec_conv_fwd(const float* xp, const float* w, const float* bias, float* 
                      void* stream);
 int vfd_dec_conv_bwd(const float* dy, const float* xp, const float* w, float* dxp, float* partial, int N, int CI, int CO,
                      int H, int W, void* stream);
-
-/* ------------------------------------------------------------------ encoder stem (stemconv.hip) */
-/* y [N, 64, Ho, Wo] = conv7x7 stride 2 pad 3 of ((img - 0.45) / 0.225), img [N, C, H, W] raw, C in {3, 6},
- * w [64, C, 7, 7], no bias (the ResNet encoders' conv1 + the packnet input normalisation,
- * fusion_depthnet.py:24, fusion_posenet.py:22); Wo % 16 == 0.  Weight gradient only (the image needs
- * none): partial [vfd_stem_conv_wgrad_groups()][ceil(ktiles / 4) * 4][64][16], k = c*49 + ky*7 + kx
- * columns in tiles of 16 (zero past C*49); the caller sums the groups. */
-int vfd_stem_conv_supported(int N, int C, int H, int W, int O);
-int vfd_stem_conv_ktiles(int C);
-int vfd_stem_conv_wgrad_groups(void);
-int vfd_stem_conv_fwd(const float* img, const float* w, float* y, int N, int C, int H, int W, void* stream);
-int vfd_stem_conv_wgrad(const float* img, const float* dy, float* partial, int N, int C, int H, int W, void* stream);
 
 /* ------------------------------------------------------------------ weight relayouts (weights.hip) */
 /* Once-per-step copies of reduce_dim's first-conv weight w [O, C, 3, 3] for the MFMA kernels

@@ -4,6 +4,8 @@ Large inputs and upstream gradients are NOT stored in the fixtures: they are reg
 bit-identically from CPU `torch.Generator` seeds here (same torch build in the build container
 and on the GPU box), and every fixture stores a checksum of them so that drift is detected.
 """
+import math
+
 import numpy as np
 import torch
 
@@ -244,3 +246,25 @@ def data_align_case():
               'splitname': 'train_0000000000'}
     m = (torch.rand(97, 151, generator=gen) * 255).to(torch.uint8).numpy()
     return sample, pil.fromarray(m, 'L'), [-1, 1], np.arange(4)
+
+
+def perturb_rig(batch, seed):
+    """Per-batch-element geometry.  The synthetic rig is the same for every element, which would
+    hide a kernel that reads element 0's K / E for all of them: element b gets its focal lengths
+    scaled by 1 + 0.03 b (K, inv_K at every scale) and its whole rig turned by 2b degrees about
+    the vertical axis and shifted by (0.1 b, -0.05 b, 0) m (extrinsics, extrinsics_inv)."""
+    B = batch['extrinsics'].shape[0]
+    gen = torch.Generator().manual_seed(seed)
+    for b in range(B):
+        a = math.radians(2.0 * b)
+        R = torch.eye(4)
+        R[0, 0], R[0, 1], R[1, 0], R[1, 1] = math.cos(a), -math.sin(a), math.sin(a), math.cos(a)
+        R[:3, 3] = torch.tensor([0.1 * b, -0.05 * b, 0.0]) + 0.01 * torch.randn(3, generator=gen)
+        batch['extrinsics'][b] = R @ batch['extrinsics'][b]
+        for k in [k for k in batch if isinstance(k, tuple) and k[0] == 'K']:
+            batch[k][b, :, 0, 0] *= 1 + 0.03 * b
+            batch[k][b, :, 1, 1] *= 1 + 0.03 * b
+    for k in [k for k in batch if isinstance(k, tuple) and k[0] == 'K']:
+        batch[('inv_K', k[1])] = torch.inverse(batch[k].double()).float()
+    batch['extrinsics_inv'] = torch.inverse(batch['extrinsics'])
+    return batch

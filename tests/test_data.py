@@ -47,7 +47,7 @@ def test_transform_mask_sample_matches_reference():
 
 def _cfg(path, dataset='ddad', h=40, w=64, **data):
     cfg = C.surround_fusion_cfg(height=h, width=w)
-    cfg['data'].update({'data_path': path, 'dataset': dataset, **data})
+    cfg['data'].update({'data_path': path, 'dataset': dataset, 'mask_path': D.ALL_ONES_MASK, **data})
     return cfg
 
 
@@ -176,3 +176,67 @@ def test_threaded_loader(tmp_path):
     batches = list(D.ThreadedLoader(ds, batch_size=2))
     assert len(batches) == 1 and batches[0][('color', 0, 0)].shape == (2, 6, 3, 40, 64)
     torch.testing.assert_close(batches[0][('color', 0, 0)][1], ds[1][('color', 0, 0)])
+
+
+def _write_masks(root, cams, sets):
+    """<root>/<set>/<CAM>_mask.png, set k filled with value 10 * (k + 1) (distinguishable)."""
+    for k in sets:
+        os.makedirs(os.path.join(root, str(k)), exist_ok=True)
+        for cam in cams:
+            pil.new('L', (128, 80), 10 * (k + 1)).save(os.path.join(root, str(k), cam.upper() + '_mask.png'))
+
+
+def test_ddad_mask_set_lookup(tmp_path):
+    """The scene directory '000000' is looked up as int('000000') -> '0' in the JSON dump of the
+    reference's mask_idx_dict (ddad_dataset_sf.py:102); a mapping without the scene is an error;
+    no mask_path at all is an error unless 'all_ones' asks for the all-255 mask."""
+    import json
+    from vfdepth_amd.config import DDAD_CAMERAS
+    path, _, _ = data_fake.write_ddad(str(tmp_path / 'ddad'), h=80, w=128, n_samples=4)
+    masks = str(tmp_path / 'masks')
+    _write_masks(masks, DDAD_CAMERAS, (0, 2))
+    mj = str(tmp_path / 'mask_idx.json')
+    with open(mj, 'w') as f:
+        json.dump({'0': 2, '150': 0}, f)
+    cfg = _cfg(path, mask_path=masks, mask_idx_json=mj, h=80, w=128)
+    s = D.construct_dataset(cfg, 'val', **D.augmentation(cfg, 'val'))[0]
+    np.testing.assert_allclose(s['mask'].numpy(), 30 / 255.0, rtol=1e-6)        # set 2, not set 0
+    with open(mj, 'w') as f:
+        json.dump({'150': 0}, f)
+    with pytest.raises(KeyError):
+        D.construct_dataset(cfg, 'val', **D.augmentation(cfg, 'val'))[0]
+    cfg = _cfg(path)
+    del cfg['data']['mask_path']
+    with pytest.raises(ValueError, match='mask_path'):
+        D.construct_dataset(cfg, 'val', **D.augmentation(cfg, 'val'))
+
+
+def test_nuscenes_depth_cache_is_read(tmp_path):
+    """nuscenes_dataset.py:108-116: the cached map <dirname(path)>/samples/DEPTH_MAP/<CAM>/<file>.npz
+    is read (arrays only) instead of re-projecting the lidar sweep."""
+    root, _, _ = data_fake.write_nuscenes(str(tmp_path / 'nusc'), h=80, w=128, n_samples=4)
+    cam = data_fake.NUSC_CAMERAS[0]
+    cdir = os.path.join(str(tmp_path), 'samples', 'DEPTH_MAP', cam, 'samples', cam)
+    os.makedirs(cdir)
+    np.savez_compressed(os.path.join(cdir, '0.png.npz'), depth=np.full((80, 128), 9.0))
+    cfg = _cfg(root, 'nuscenes', h=80, w=128, nusc_version='v1.0-mini',
+               cameras=[c.lower() for c in data_fake.NUSC_CAMERAS])
+    s = D.construct_dataset(cfg, 'val', **D.augmentation(cfg, 'val'))[0]
+    assert torch.all(s['depth'][0] == 9.0)
+    assert not torch.all(s['depth'][1] == 9.0)                # other cameras: projected lidar
+
+
+def test_threaded_loader_propagates_errors():
+    class Bad(torch.utils.data.Dataset):
+        def __len__(self):
+            return 4
+
+        def __getitem__(self, i):
+            if i == 2:
+                raise RuntimeError('corrupt sample 2')
+            return {'x': torch.full((2,), float(i))}
+    it = iter(D.ThreadedLoader(Bad(), batch_size=1, pin=False))
+    assert float(next(it)['x'][0, 0]) == 0.0
+    assert float(next(it)['x'][0, 0]) == 1.0
+    with pytest.raises(RuntimeError, match='corrupt sample 2'):
+        next(it)

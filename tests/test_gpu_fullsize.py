@@ -106,19 +106,23 @@ def _near_grid_lines(O, batch, depth_c, co, c, cfg, tol=2e-3):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize('config', [2, 4])
+@pytest.mark.parametrize('config', [2, 4, 5])
 def test_view_synthesis_and_losses_full_size(config):
     """K4 (Projection + get_virtual_image + intensity alignment + overlap sums, every warp of
     all six cameras) and K5 (SSIM/photometric, auto-mask, masked means, spatial and
-    spatio-temporal terms, smoothness) at 384x640 / 352x640, forward and backward, against the
-    oracle (view_rendering.py:118-243, loss_util.py:6-78, multi_cam_loss.py:16-138)."""
+    spatio-temporal terms, smoothness) at 384x640 / 352x640 (B=1) and config 5's 640x960 at its
+    per-GPU batch B=4 (every element with its own rig geometry, G.perturb_rig), forward and
+    backward, against the oracle (view_rendering.py:118-243, loss_util.py:6-78,
+    multi_cam_loss.py:16-138)."""
     from oracle import vfd_oracle as O
     from vfdepth_amd.geometry import Pose, ViewRendering
     from vfdepth_amd.losses import MultiCamLoss
-    cfg = full_cfg(config)
+    cfg = full_cfg(config, 4 if config == 5 else 1)
     t = cfg['training']
     N, frames, H, W = cfg['data']['num_cams'], t['frame_ids'], t['height'], t['width']
     batch, depth, poses = G.view_case_cfg(cfg, seed=60 + config)
+    if config == 5:
+        batch = G.perturb_rig(batch, 65)
     keys = G.VIEW_IMG_KEYS
     # ---- K4, oracle.  The backward is checked with a random linear functional of the planes
     # whose weights are zero on pixels that sample near a source grid line (_near_grid_lines),
@@ -222,12 +226,13 @@ def _fusion_inputs(cfg, seed):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize('config,k1', [(2, 'gather'), (2, 'scatter'), (5, 'gather')])
+@pytest.mark.parametrize('config,k1', [(2, 'gather'), (2, 'scatter'), (4, 'gather'), (5, 'gather')])
 def test_fuse_depth_full_size(config, k1, monkeypatch):
     """K1 (depth-mode backproject_into_voxel + the overlap / non-overlap 1x1 MLPs,
     volumetric_fusionnet.py:116-230) on the full grid: 100x100x20 (config 2) and 200x200x20
     (config 5), C=256 -> Cv=64, forward against the oracle; backward too at config 2, through the
-    atomic-free gather over the fusion plan (the default) and the atomic scatter."""
+    atomic-free gather over the fusion plan (the default) and the atomic scatter; config 4's
+    44x80 map (NuScenes 352x640) forward + backward.  B = 4 at config 5: test_fusion_ops_batch4_config5."""
     from oracle import vfd_oracle as O
     from vfdepth_amd import kernels as KN
     from vfdepth_amd.fusion import VFNet
@@ -241,7 +246,7 @@ def test_fuse_depth_full_size(config, k1, monkeypatch):
     net = VFNet(cfg, C, 128, model='depth')
     net.load_state_dict(seeded_state_dict(net, seed=92))
     c_no, c_o = net.conv_non_overlap[0], net.conv_overlap[0]
-    grad = config == 2
+    grad = config in (2, 4)
     fr = feats.clone().requires_grad_(grad)
     ref = O.fuse_depth(spec, fr, batch['mask'], batch[('K', lvl)], Einv, c_no.weight, c_no.bias, c_o.weight, c_o.bias)
     if grad:
@@ -263,6 +268,76 @@ def test_fuse_depth_full_size(config, k1, monkeypatch):
         for k, p in gnet.named_parameters():
             if k in ref_grads:
                 gclose(p.grad, ref_grads[k], f'K1 d {k}')
+
+
+@pytest.mark.timeout(900)
+def test_fusion_ops_batch4_config5():
+    """Config 5's per-GPU batch, B = 4, on the 200x200x20 grid (80x120 feature map, C=256, Cv=64,
+    D=50), every element with its own geometry (G.perturb_rig) and mask: K1 forward + backward
+    (the plan gather), K2 forward and K3 forward on all four elements, against the oracle on
+    elements 1 and 3 (volumetric_fusionnet.py:116-262; the elements are independent, so the
+    other two get a zero gradient functional and must come out with exactly zero gradients)."""
+    from oracle import vfd_oracle as O
+    from vfdepth_amd import kernels as KN
+    from vfdepth_amd.fusion import VFNet
+    from vfdepth_amd.layers import seeded_state_dict
+    cfg = full_cfg(5, 4)
+    spec = O.VoxelSpec(cfg)
+    batch, lvl, _ = _fusion_inputs(cfg, 190)
+    batch = G.perturb_rig(batch, 191)
+    Einv = batch['extrinsics_inv']
+    B, sub, rest = 4, [1, 3], [0, 2]
+    C, Cv = int(cfg['model']['fusion_feat_in_dim']), int(cfg['model']['voxel_pre_dim'][-1])
+    feats = G.seeded_randn((B, 6, C, spec.h, spec.w), 192)
+    net = VFNet(cfg, C, 128, model='depth')
+    net.load_state_dict(seeded_state_dict(net, seed=193))
+    c_no, c_o = net.conv_non_overlap[0], net.conv_overlap[0]
+    K, mask = batch[('K', lvl)], batch['mask']
+    # ---- K1, oracle on the subset
+    fr = feats[sub].clone().requires_grad_(True)
+    ref = O.fuse_depth(spec, fr, mask[sub], K[sub], Einv[sub], c_no.weight, c_no.bias, c_o.weight, c_o.bias)
+    g = G.seeded_randn(ref.shape, 194)
+    (ref * g).sum().backward()
+    ref_grads = {k: p.grad.clone() for k, p in net.named_parameters() if p.grad is not None}
+    net.zero_grad(set_to_none=True)
+    ref, d_ref = ref.detach(), fr.grad
+    del fr
+    # ---- K1, product on all four elements
+    gnet = net.to(DEV)
+    inputs = {('K', lvl): K.to(DEV), 'extrinsics_inv': Einv.to(DEV), 'mask': mask.to(DEV)}
+    fg = feats.to(DEV).requires_grad_(True)
+    vox = gnet.backproject_depth(inputs, fg)                       # [B, V, Cv]
+    close(vox.permute(0, 2, 1)[sub], ref, 'K1 voxel features (B=4, elements 1, 3)')
+    for b in range(B):
+        assert int(((vox[b] != 0).sum(1) > 0).sum()) > 0.05 * spec.V, f'element {b}: too few voxels carry features'
+    gfull = torch.zeros(B, *ref.shape[1:])
+    gfull[sub] = g
+    (vox.permute(0, 2, 1) * gfull.to(DEV)).sum().backward()
+    gclose(fg.grad[sub], d_ref, 'K1 d feats (B=4)')
+    assert not bool(fg.grad[rest].any()), 'K1: gradient leaked into elements with a zero functional'
+    for k, p in gnet.named_parameters():
+        if k in ref_grads:
+            gclose(p.grad, ref_grads[k], f'K1 d {k} (B=4)')
+    del vox, fg, gfull, ref, d_ref
+    # ---- K2 (pose fusion) forward
+    space = KN.VoxelSpace(cfg, DEV)
+    feats_p = G.seeded_randn((B, 6, C, spec.h, spec.w), 195)
+    ref = O.fuse_pose(spec, feats_p[sub], mask[sub], K[sub], Einv[sub])                    # [2, C+1, V]
+    mask_lo = KN.mask_lowres(space, mask.to(DEV))
+    plan = KN.FusionPlan(space, mask_lo, K.to(DEV), Einv.to(DEV), build=False)
+    out = KN.pose_to_reference(KN.FusePose.apply(space, plan, feats_p.to(DEV)), C + 1, space.Z)
+    inner = out[:, :, 1:-1, 1:-1].reshape(B, C + 1, -1)
+    close(inner[sub], ref, 'K2 pose voxels (B=4, elements 1, 3)')
+    del out, inner, ref, feats_p
+    # ---- K3 (voxel -> frustum) forward
+    invK, E = batch[('inv_K', lvl)], batch['extrinsics']
+    vin = G.seeded_randn((B, Cv, spec.V), 196)
+    refs = O.project_voxels(spec, vin[sub], invK[sub], E[sub])                            # N x [2, Cv*D, h, w]
+    out = KN.proj_to_reference(KN.VoxelProject.apply(space, vin.permute(0, 2, 1).contiguous().to(DEV),
+                                                     invK.to(DEV), E.to(DEV)), Cv, space.D)
+    out = out.view(B, 6, *out.shape[1:])
+    for c in range(6):
+        close(out[sub, c, :, 1:-1, 1:-1], refs[c], f'K3 frustum features cam {c} (B=4, elements 1, 3)')
 
 
 @pytest.mark.timeout(900)
@@ -462,23 +537,24 @@ def test_config3_step_b2(prec):
 
 # ------------------------------------------------------------------------------------ K3C
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize('config', ['small', 2, 5])
-def test_proj_conv_matches_k3_plus_conv(config):
+@pytest.mark.parametrize('config,B', [('small', 1), (2, 1), (4, 1), (5, 1), (5, 4)])
+def test_proj_conv_matches_k3_plus_conv(config, B):
     """K3C (K3 fused into reduce_dim's first conv, fp32 MFMA implicit GEMM) against the unfused
     path it replaces — K3 (pinned by the golden fixtures) + the reflect-padded 3x3 conv + bias +
     LeakyReLU (volumetric_fusionnet.py:59-60, 232-267) — forward (every reflect-halo copy too) and
     backward (d voxels, d weight, d bias).  'small': the reduced step config (12x20 feature map:
-    partial pixel tiles, D=16); 2: 48x80, D=50; 5: 80x120 (partial column tiles), 200x200x20."""
+    partial pixel tiles, D=16); 2: 48x80, D=50; 4: 44x80 (partial row tiles); 5: 80x120 (partial
+    column tiles), 200x200x20, at B=1 and at config 5's B=4 with per-element geometry."""
     from vfdepth_amd import kernels as KN
     from vfdepth_amd import synth
     cfg = G.step_cfg() if config == 'small' else full_cfg(config)
     space = KN.VoxelSpace(cfg, DEV)
-    b = synth.make_batch(cfg, seed=71, batch_size=1, device=DEV)
+    b = G.perturb_rig(synth.make_batch(cfg, seed=71, batch_size=B), 70)
     lvl = cfg['model']['fusion_level'] + 1
-    invK, E = b['inv_K', lvl], b['extrinsics']
+    invK, E = b['inv_K', lvl].to(DEV), b['extrinsics'].to(DEV)
     gen = torch.Generator(device=DEV).manual_seed(72)
     Cv, D, O = 64, space.D, 256
-    vox = torch.randn(1, space.V, Cv, device=DEV, generator=gen)
+    vox = torch.randn(B, space.V, Cv, device=DEV, generator=gen)
     w0 = torch.randn(O, Cv * D, 3, 3, device=DEV, generator=gen) * (Cv * D * 9) ** -0.5
     bias = 0.1 * torch.randn(O, device=DEV, generator=gen)
     leaves = [t.clone().requires_grad_(True) for t in (vox, w0, bias)]
@@ -491,7 +567,7 @@ def test_proj_conv_matches_k3_plus_conv(config):
     # which the forward tolerates but would move the gradient by 0.9 g there
     pos = y.detach()[:, :, 1:-1, 1:-1] > 0
     y_ref = F.pad(torch.where(pos, pre, 0.1 * pre), (1, 1, 1, 1), mode='reflect')
-    close(y, y_ref, f'K3C output (config {config})')
+    close(y, y_ref, f'K3C output (config {config}, B={B})')
     close(F.leaky_relu(pre, 0.1), y[:, :, 1:-1, 1:-1], f'K3C output vs its own LeakyReLU (config {config})')
     # the frustum features the kernel writes for the backward (K3's padded layout, halo included)
     close(y.grad_fn.saved_tensors[2], x.detach(), f'K3C frustum-feature side output (config {config})')
@@ -764,25 +840,6 @@ def test_decoder_conv_mfma_matches_aten(shape, co, up):
     close(xp.grad, xr.grad, f'dec conv d xp {shape}', atol=1e-5 * float(xr.grad.abs().max()), rtol=1e-4)
     close(w.grad, wr.grad, f'dec conv d w {shape}', atol=1e-4 * float(wr.grad.abs().max()), rtol=1e-4)
     close(b.grad, br.grad, f'dec conv d b {shape}', atol=1e-4 * float(br.grad.abs().max()), rtol=1e-4)
-
-
-@pytest.mark.parametrize('shape', [(6, 6, 384, 640), (6, 3, 384, 640), (2, 6, 64, 96)])
-def test_stem_conv_matches_aten(shape):
-    """The encoders' normalisation + 7x7/2 stem conv on MFMA (stemconv.hip) against
-    F.conv2d((x - 0.45) / 0.225, w, stride 2, padding 3): output and weight gradient."""
-    from vfdepth_amd import kernels as KN
-    gen = torch.Generator(device=DEV).manual_seed(37)
-    img = torch.rand(shape, device=DEV, generator=gen)
-    w = (torch.randn(64, shape[1], 7, 7, device=DEV, generator=gen) / (7 * shape[1] ** 0.5)).requires_grad_(True)
-    assert KN.StemConv.supported(img, w)
-    y = KN.StemConv.apply(img, w)
-    wr = w.detach().clone().requires_grad_(True)
-    ref = F.conv2d((img - 0.45) / 0.225, wr, None, 2, 3)
-    close(y, ref, f'stem conv {shape}', atol=1e-4, rtol=1e-4)
-    g = torch.randn(y.shape, device=DEV, generator=gen)
-    y.backward(g)
-    ref.backward(g)
-    close(w.grad, wr.grad, f'stem conv d w {shape}', atol=1e-4 * float(wr.grad.abs().max()), rtol=1e-4)
 
 
 def test_normalize_cat_bit_identical():

@@ -423,6 +423,23 @@ def test_full_step_against_reference(which):
         assert rel < 1e-2, f'{key}: gradient rel diff {rel:.3g} vs the reference'
 
 
+def test_step_depth_metrics_against_reference_logger():
+    """A24 on the GPU: the fusion step's depth maps scored by `compute_depth_metrics` (all 7
+    metrics, plain and median-scaled; reference utils/logger.py:193-247 + utils/misc.py:85-98)
+    against the reference Logger's values on the reference step's own depths
+    (tests/golden/depth_metrics.npz 'step_*'), at 1e-4 relative."""
+    from vfdepth_amd.metrics import METRIC_NAMES
+    cfg, fx, algo, inputs, outputs, losses = _step(G.step_cfg, 'step_small.npz', 5)
+    torch.cuda.synchronize()
+    fm = golden('depth_metrics.npz')
+    metric, median = algo.compute_depth_metrics(inputs, outputs)
+    assert METRIC_NAMES == ['abs_rel', 'sq_rel', 'rms', 'log_rms', 'a1', 'a2', 'a3']
+    for k in METRIC_NAMES:
+        for what, got in (('metric', metric[k]), ('median', median[k])):
+            ref = float(fm[f'step_{what}_{k}'])
+            assert abs(float(got) - ref) <= 1e-4 * abs(ref) + 1e-7, f'{what} {k}: GPU step {float(got):.8g} vs reference {ref:.8g}'
+
+
 def _fro(a, b):
     a, b = a.detach().double().cpu(), b.detach().double().cpu().reshape(a.shape)
     return float((a - b).norm() / max(float(b.norm()), 1e-30)), float((a - b).abs().max() / max(float(b.abs().max()), 1e-30))
@@ -677,8 +694,8 @@ def test_bf16_nets_step_tracks_fp32():
 
 @pytest.mark.parametrize('config', [2, 4, 5])
 def test_fusion_adjoint_at_full_size(config):
-    """Size-independent property at BASELINE.json's full sizes (configs 2, 4, 5 at B=1), where the
-    oracle is too slow: K2 (pose fusion, affine in the features) and K3 (voxel -> frustum, linear)
+    """Size-independent property at BASELINE.json's full sizes (configs 2 and 4 at B=1, config 5 at
+    its per-GPU batch B=4), where the oracle is too slow: K2 (pose fusion, affine in the features) and K3 (voxel -> frustum, linear)
     backward kernels are the exact adjoints of their forward kernels,
     <fwd(x) - fwd(0), g> == <x, bwd(g)>, reflect-pad copies and zero padding included.  Inner
     products in fp64 over fp32 values; tolerance 1e-5 of sum |fwd(x) * g| (fp32 rounding of the
@@ -687,9 +704,12 @@ def test_fusion_adjoint_at_full_size(config):
     from vfdepth_amd import kernels as KN
     from vfdepth_amd import synth
     from vfdepth_amd.geometry import inverse4x4
-    cfg, _ = bench.make_cfg(config, 1)
+    B = 4 if config == 5 else 1
+    cfg, _ = bench.make_cfg(config, B)
     space = KN.VoxelSpace(cfg, DEV)
     b = synth.make_batch(cfg, seed=3, device=DEV)
+    if B > 1:                      # per-element geometry (common.perturb_rig)
+        b = {k: (v.to(DEV) if torch.is_tensor(v) else v) for k, v in G.perturb_rig(synth.make_batch(cfg, seed=3), 4).items()}
     lvl = cfg['model']['fusion_level'] + 1
     Einv = inverse4x4(b['extrinsics'])
     mask_lo = KN.mask_lowres(space, b['mask'])
@@ -703,7 +723,7 @@ def test_fusion_adjoint_at_full_size(config):
 
     # K2: features [B, N, C, h, w] -> padded pose volume (affine: the depth channel is constant)
     plan = KN.FusionPlan(space, mask_lo, b['K', lvl], Einv)
-    feats = torch.randn(1, 6, C, space.h, space.w, device=DEV, generator=gen, requires_grad=True)
+    feats = torch.randn(B, 6, C, space.h, space.w, device=DEV, generator=gen, requires_grad=True)
     out = KN.FusePose.apply(space, plan, feats)
     with torch.no_grad():
         out0 = KN.FusePose.apply(space, plan, torch.zeros_like(feats))
@@ -712,7 +732,7 @@ def test_fusion_adjoint_at_full_size(config):
     check((out.detach() - out0) * g, float((feats.detach().double() * feats.grad.double()).sum()), 'K2')
     del out, out0, g, feats
     # K3: voxels [B, V, Cv] -> frustum features (linear)
-    vox = torch.randn(1, space.V, Cv, device=DEV, generator=gen, requires_grad=True)
+    vox = torch.randn(B, space.V, Cv, device=DEV, generator=gen, requires_grad=True)
     out = KN.VoxelProject.apply(space, vox, b['inv_K', lvl], b['extrinsics'])
     g = torch.randn(out.shape, device=DEV, generator=gen).contiguous(memory_format=torch.channels_last)
     out.backward(g)

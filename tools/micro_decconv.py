@@ -51,27 +51,5 @@ def main():
               f'MIOpen fwd {t_mf:7.1f}  bwd(d+w) {t_mb:7.1f}', flush=True)
 
 
-def stem():
-    from vfdepth_amd import _lib as L
-    lib = L.load()
-    dev = 'cuda:0'
-    for c in (6, 3):
-        img = torch.rand(6, c, 384, 640, device=dev)
-        wt = torch.randn(64, c, 7, 7, device=dev)
-        y = torch.empty(6, 64, 192, 320, device=dev)
-        g = torch.randn_like(y)
-        part = torch.empty(lib.vfd_stem_conv_wgrad_groups(), (lib.vfd_stem_conv_ktiles(c) + 3) // 4 * 4, 64, 16, device=dev)
-        st = L.stream()
-        gf = 2 * 6 * 192 * 320 * 64 * c * 49 / 1e9
-        t_f = timeit(lambda: lib.vfd_stem_conv_fwd(img.data_ptr(), wt.data_ptr(), y.data_ptr(), 6, c, 384, 640, st))
-        t_w = timeit(lambda: lib.vfd_stem_conv_wgrad(img.data_ptr(), g.data_ptr(), part.data_ptr(), 6, c, 384, 640, st))
-        xn = (img - 0.45) / 0.225
-        t_mf = timeit(lambda: F.conv2d((img - 0.45) / 0.225, wt, None, 2, 3))
-        t_mw = timeit(lambda: torch.ops.aten.convolution_backward(g, xn, wt, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1, [False, True, False]))
-        print(f'stem {c}->64 @384x640: HIP fwd (incl. normalise) {t_f:7.1f} us ({gf / t_f * 1e3:6.1f} TF)  wgrad {t_w:7.1f} | '
-              f'MIOpen normalise+fwd {t_mf:7.1f}  wgrad {t_mw:7.1f}', flush=True)
-
-
 if __name__ == '__main__':
-    stem()
     main()

@@ -86,7 +86,7 @@ _SIGS = {
     'vfd_proj_conv_dgrad': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 4 + [c_size_t, c_void_p]),
     'vfd_bn_splits': (c_int, [ctypes.POINTER(BnDesc)]),
     'vfd_bn_fwd_stats': (c_int, [ctypes.POINTER(BnDesc), c_fp, c_fp, c_void_p]),
-    'vfd_bn_sum': (c_int, [ctypes.POINTER(BnDesc), c_fp, c_fp, c_void_p]),
+    'vfd_bn_sum': (c_int, [ctypes.POINTER(BnDesc), c_fp, c_double, c_fp, c_fp, c_fp, c_fp, c_void_p]),
     'vfd_bn_fwd_apply': (c_int, [ctypes.POINTER(BnDesc), c_fp, c_fp, c_fp, c_int, c_double] + [c_fp] * 9 + [c_void_p]),
     'vfd_bn_bwd_stats': (c_int, [ctypes.POINTER(BnDesc)] + [c_fp] * 5 + [c_void_p]),
     'vfd_bn_bwd_apply': (c_int, [ctypes.POINTER(BnDesc), c_fp, c_fp, c_fp, c_fp, c_int, c_double] + [c_fp] * 7
@@ -110,11 +110,6 @@ _SIGS = {
     'vfd_dec_conv_wgrad_blocks': (c_int, [c_int] * 3),
     'vfd_dec_conv_fwd': (c_int, [c_fp] * 4 + [c_int] * 5 + [c_void_p]),
     'vfd_dec_conv_bwd': (c_int, [c_fp] * 5 + [c_int] * 5 + [c_void_p]),
-    'vfd_stem_conv_supported': (c_int, [c_int] * 5),
-    'vfd_stem_conv_ktiles': (c_int, [c_int]),
-    'vfd_stem_conv_wgrad_groups': (c_int, []),
-    'vfd_stem_conv_fwd': (c_int, [c_fp] * 3 + [c_int] * 4 + [c_void_p]),
-    'vfd_stem_conv_wgrad': (c_int, [c_fp] * 3 + [c_int] * 4 + [c_void_p]),
     'vfd_weight_fragments': (c_int, [c_int, c_fp, c_fp] + [c_int] * 6 + [c_void_p]),
     'vfd_weight_swap': (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_void_p]),
     'vfd_weight_permute': (c_int, [c_fp, c_fp] + [c_int] * 4 + [ctypes.POINTER(ctypes.c_longlong)] * 2 + [c_void_p]),
@@ -174,7 +169,7 @@ KERNEL_IDS = {
     'voxel_project_fwd': 5, 'voxel_project_bwd': 6, 'view_stats': 7, 'view_apply': 8, 'view_bwd': 9,
     'photo_fwd': 10, 'photo_bwd': 11, 'smooth_fwd': 12, 'smooth_bwd': 13, 'fusion_plan': 14,
     'aggregate': 15, 'voxel_project_plan': 16, 'proj_conv_fwd': 17,
-    'depth_syn_fwd': 18, 'depth_syn_bwd': 19, 'proj_conv_dgrad': 20, 'pad_conv_fwd': 21, 'bn_fwd': 22, 'bn_bwd': 23, 'reflect_pad': 24, 'upsample_bwd': 25, 'maxpool': 26, 'elu_pad': 27, 'disp_conv': 28, 'dec_conv': 29, 'stem_conv': 30,
+    'depth_syn_fwd': 18, 'depth_syn_bwd': 19, 'proj_conv_dgrad': 20, 'pad_conv_fwd': 21, 'bn_fwd': 22, 'bn_bwd': 23, 'reflect_pad': 24, 'upsample_bwd': 25, 'maxpool': 26, 'elu_pad': 27, 'disp_conv': 28, 'dec_conv': 29,
 }
 
 
@@ -197,7 +192,7 @@ def prof_enable(kernel='all'):
 # Algorithmic bytes of the shape-varying dense-net kernels (fused BN, reflect pads, upsample
 # backward), accumulated by their Python wrappers while profiling is on (bench.py's rooflines).
 PROF_ON = False
-ALG_BYTES = {'bn_fwd': 0, 'bn_bwd': 0, 'reflect_pad': 0, 'upsample_bwd': 0, 'maxpool': 0, 'elu_pad': 0, 'disp_conv': 0, 'dec_conv': 0, 'stem_conv': 0}
+ALG_BYTES = {'bn_fwd': 0, 'bn_bwd': 0, 'reflect_pad': 0, 'upsample_bwd': 0, 'maxpool': 0, 'elu_pad': 0, 'disp_conv': 0, 'dec_conv': 0}
 
 
 def prof_read():

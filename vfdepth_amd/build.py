@@ -16,7 +16,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, 'csrc')
 INCLUDE = os.path.join(ROOT, 'include')
 LIB = os.path.join(HERE, 'libvfd_hip.so')
-SOURCES = ['capi.hip', 'fusion.hip', 'view.hip', 'photo.hip', 'aggregate.hip', 'projconv.hip', 'depthsyn.hip', 'padconv.hip', 'bnact.hip', 'reflectpad.hip', 'geometry.hip', 'maxpool.hip', 'weights.hip', 'dispconv.hip', 'decconv.hip', 'stemconv.hip']
+SOURCES = ['capi.hip', 'fusion.hip', 'view.hip', 'photo.hip', 'aggregate.hip', 'projconv.hip', 'depthsyn.hip', 'padconv.hip', 'bnact.hip', 'reflectpad.hip', 'geometry.hip', 'maxpool.hip', 'weights.hip', 'dispconv.hip', 'decconv.hip']
 ARCH = os.environ.get('VFD_OFFLOAD_ARCH', 'gfx950')
 FLAGS = ['-O3', f'--offload-arch={ARCH}', '-std=c++17', '-fPIC', '-ffp-contract=off',
          '-Wno-unused-result', '-I', INCLUDE, '-I', CSRC]
@@ -39,17 +39,23 @@ def _stale(out, deps):
 def build(force=False, verbose=True):
     hipcc = _hipcc()
     headers = [os.path.join(CSRC, 'vfd_common.h'), os.path.join(INCLUDE, 'vfd_capi.h')]
-    objs = []
+    objs, cmds = [], []
     os.makedirs(os.path.join(HERE, 'build'), exist_ok=True)
     for src in SOURCES:
         s = os.path.join(CSRC, src)
         o = os.path.join(HERE, 'build', src.replace('.hip', '.o'))
         objs.append(o)
         if force or _stale(o, [s] + headers):
-            cmd = [hipcc] + FLAGS + ['-c', s, '-o', o]
-            if verbose:
-                print(' '.join(cmd), flush=True)
-            subprocess.check_call(cmd)
+            cmds.append([hipcc] + FLAGS + ['-c', s, '-o', o])
+    # translation units compile in parallel (at most 8 hipcc processes)
+    from concurrent.futures import ThreadPoolExecutor
+
+    def run(cmd):
+        if verbose:
+            print(' '.join(cmd), flush=True)
+        subprocess.check_call(cmd)
+    with ThreadPoolExecutor(max_workers=max(1, min(8, os.cpu_count() or 1))) as ex:
+        list(ex.map(run, cmds))
     if force or _stale(LIB, objs):
         cmd = [hipcc, f'--offload-arch={ARCH}', '-shared', '-fPIC', '-o', LIB] + objs
         if verbose:

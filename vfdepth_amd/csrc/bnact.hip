@@ -8,7 +8,8 @@
 // (plus three more for their backward); these kernels do one statistics pass and one apply pass
 // each way.  Statistics accumulate in fp64 (as the reference's CPU batch norm does), per
 // (channel, split) partials summed in a fixed order: deterministic.  For SyncBatchNorm the host
-// all-reduces the per-channel sums between the two passes (vfd_bn_sum).
+// all-reduces the per-channel sums between the two passes (vfd_bn_sum): one collective per
+// direction, the element count riding along as an extra row (no host synchronisation).
 //
 // Work split: a channel's N*HW elements (N images of HW contiguous floats) are cut into S
 // equal float4-aligned ranges; block (split, channel) of every kernel owns one range.
@@ -107,9 +108,18 @@ __global__ __launch_bounds__(BN_THREADS) void bn_stats_k(vfd_bn_desc d, const fl
   }
 }
 
-// sums[c*2 + k] = sum over splits of partial (fixed order); one thread per channel
-__global__ void bn_sum_k(vfd_bn_desc d, const double* __restrict__ partial, double* __restrict__ sums) {
+// sums[c*2 + k] = sum over splits of partial (fixed order); one thread per channel.  SyncBatchNorm:
+// thread C writes the local element count as row C (count > 0), so ONE all-reduce of the [C+1][2]
+// buffer gives the global sums and the global count together (no host round trip for the count);
+// dgamma / dbeta (backward, nullable) take this rank's LOCAL sums, as torch's SyncBatchNorm
+// returns local parameter gradients that DDP then averages.
+__global__ void bn_sum_k(vfd_bn_desc d, const double* __restrict__ partial, double count, double* __restrict__ sums,
+                         const float* __restrict__ invstd, float* __restrict__ dgamma, float* __restrict__ dbeta) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c == d.C && count > 0.0) {
+    sums[c * 2] = count;
+    sums[c * 2 + 1] = 0.0;
+  }
   if (c >= d.C) return;
   double a = 0.0, b = 0.0;
   for (int s = 0; s < d.S; ++s) {
@@ -118,6 +128,8 @@ __global__ void bn_sum_k(vfd_bn_desc d, const double* __restrict__ partial, doub
   }
   sums[c * 2] = a;
   sums[c * 2 + 1] = b;
+  if (dgamma) dgamma[c] = (float)(b * invstd[c]);
+  if (dbeta) dbeta[c] = (float)a;
 }
 
 // per-channel sums of the block's channel: from the S partials, or (ns == 1) already reduced
@@ -143,6 +155,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_apply_k(vfd_bn_desc d, const fl
                                                          long long* __restrict__ nbt, unsigned char* __restrict__ mk) {
   const int c = blockIdx.y, split = blockIdx.x;
   if (nbt && c == 0 && split == 0 && threadIdx.x == 0) nbt[0] += 1;   // num_batches_tracked
+  if (count <= 0.0) count = sums[2 * d.C];                          // all-reduced count row (ns == 1)
   double s1, s2;
   bn_channel_sums(sums, ns, c, &s1, &s2);
   const double mean_d = s1 / count;
@@ -238,6 +251,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply_k(vfd_bn_desc d, cons
                                                              float* __restrict__ dx, float* __restrict__ dr,
                                                              float* __restrict__ dgamma, float* __restrict__ dbeta) {
   const int c = blockIdx.y, split = blockIdx.x;
+  if (count <= 0.0) count = sums[2 * d.C];                          // all-reduced count row (ns == 1)
   double sg, sgx;
   bn_channel_sums(sums, ns, c, &sg, &sgx);
   const float mean = mean_in[c], invstd = invstd_in[c];
@@ -467,11 +481,13 @@ int vfd_bn_fwd_stats(const vfd_bn_desc* d, const float* x, double* partial, void
   return fail_launch("bn_fwd_stats");
 }
 
-int vfd_bn_sum(const vfd_bn_desc* d, const double* partial, double* sums, void* stream) {
+int vfd_bn_sum(const vfd_bn_desc* d, const double* partial, double count, double* sums, const float* invstd,
+               float* dgamma, float* dbeta, void* stream) {
   if (int e = bn_check(d, "bn_sum")) return e;
   VFD_REQUIRE(partial && sums, "bn_sum: null argument");
+  VFD_REQUIRE(invstd || (!dgamma && !dbeta), "bn_sum: dgamma / dbeta need invstd");
   hipStream_t s = (hipStream_t)stream;
-  bn_sum_k<<<(d->C + 255) / 256, 256, 0, s>>>(*d, partial, sums);
+  bn_sum_k<<<(d->C + 1 + 255) / 256, 256, 0, s>>>(*d, partial, count, sums, invstd, dgamma, dbeta);
   return fail_launch("bn_sum");
 }
 
@@ -480,8 +496,9 @@ int vfd_bn_fwd_apply(const vfd_bn_desc* d, const float* x, const float* residual
                      float* running_mean, float* running_var, long long* num_batches_tracked,
                      unsigned char* relu_mask, void* stream) {
   if (int e = bn_check(d, "bn_fwd_apply")) return e;
-  VFD_REQUIRE(x && sums && gamma && beta && y && mean && invstd && (ns == 1 || ns == d->S) && count > 0.0,
-              "bn_fwd_apply: bad argument");
+  VFD_REQUIRE(x && sums && gamma && beta && y && mean && invstd && (ns == 1 || ns == d->S) &&
+                  (count > 0.0 || ns == 1),
+              "bn_fwd_apply: bad argument (count <= 0 reads the count row of reduced sums: ns must be 1)");
   VFD_REQUIRE(!running_mean == !running_var, "bn_fwd_apply: running mean / var must come together");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_BN_FWD, s);
@@ -506,8 +523,8 @@ int vfd_bn_bwd_apply(const vfd_bn_desc* d, const float* g, const float* y, const
                      float* dresidual, float* dgamma, float* dbeta, void* stream) {
   if (int e = bn_check(d, "bn_bwd_apply")) return e;
   VFD_REQUIRE(g && x && sums && gamma && mean && invstd && (y || !d->relu) && (ns == 1 || ns == d->S) &&
-                  count > 0.0,
-              "bn_bwd_apply: bad argument");
+                  (count > 0.0 || ns == 1),
+              "bn_bwd_apply: bad argument (count <= 0 reads the count row of reduced sums: ns must be 1)");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_BN_BWD, s);
   bn_bwd_apply_k<<<dim3(d->S, d->C), BN_THREADS, 0, s>>>(*d, g, y, x, sums, ns, count, gamma, mean, invstd, dx,

@@ -1728,26 +1728,15 @@ __global__ __launch_bounds__(256) void voxel_project_fwd_k(vfd_voxel_desc d, con
 #define VFD_VPB_PQ 8
 #endif
 constexpr int VB_X = 8, VB_Y = 4;                  // voxel tile (one z layer) per wave task
-// VFD_VPB_WALK 1: one wave per task walks the task's VB_LG voxel layers bottom-up (vpb_walk_k),
-// reading every cell layer's gradient rows once for both voxel layers it touches; 0 (default):
-// one wave per voxel layer (vpb_main_k), each reading the two cell layers around it.  The walk
-// reads 1.25-1.5x rows per voxel layer instead of 2x but needs two LDS layer slots per wave, which
-// halves the resident waves of this latency-bound loop: 315-370 us vs 207 us at config 2 for
-// VB_LG 2-4 and VB_S 512-2048.
-#ifndef VFD_VPB_WALK
-#define VFD_VPB_WALK 0
-#endif
+// One wave per voxel layer (vpb_main_k), each reading the two cell layers around it.  (A z-walk
+// form — one wave sweeping a brick column, each gradient row read once for both voxel layers it
+// feeds — measured 315-370 us vs 207 us at config 2: its second LDS layer slot halves the resident
+// waves of this latency-bound loop; DESIGN.md section 4.  Removed from the library, in git history.)
 #ifndef VFD_VPB_LG
-#if VFD_VPB_WALK
-#define VFD_VPB_LG 4
-#else
 #define VFD_VPB_LG 2          // 4 and 5 measured slower (219, 263 us vs 209 us at config 2)
-#endif
 #endif
 constexpr int VB_LG = VFD_VPB_LG;                  // voxel layers (waves) per workgroup task
 constexpr int VB_RY = VB_Y + 1, VB_NSEG = 2 * VB_RY;   // cell rows per layer, entry ranges per tile
-constexpr int VB_WSEG = (VB_LG + 1) * VB_RY;           // entry ranges of a walk task (cell layers x rows)
-static_assert(VB_WSEG <= 32, "walk: one lane per entry range within a half-wave scan");
 #ifndef VFD_VPB_S
 #define VFD_VPB_S 1024
 #endif
@@ -2117,20 +2106,6 @@ __global__ __launch_bounds__(64) void vpb_tile_k(vfd_voxel_desc d, const int* __
   int xb, yb, zp;
   vpb_tile_pos(d, g, tl, &xb, &yb, &zp);
   static_assert(VB_LG * VB_NSEG <= 64, "one lane per entry range");
-#if VFD_VPB_WALK
-  {
-    int n = 0;
-    if (lane < VB_WSEG) {
-      int s0, s1;
-      vpb_segment(d, g, ptr, boff, b, VB_LG * zp - 1 + lane / VB_RY, yb - 1 + lane % VB_RY, xb, &s0, &s1);
-      n = s1 - s0;
-    }
-    const int tot = wave_sum(n);
-    const int np = d.deterministic ? 1 : max(1, (tot + VB_S - 1) / VB_S);
-    if (lane == 0) parts[tile] = np;
-    return;
-  }
-#endif
   int n = 0, wl = -1;
   if (lane < VB_LG * VB_NSEG) {
     const int w = lane / VB_NSEG, k = lane % VB_NSEG;
@@ -2378,220 +2353,6 @@ __global__ __launch_bounds__(64 * VB_LG) void vpb_main_k(vfd_voxel_desc d, const
         }
       }
     }
-  }
-}
-
-// ---- z-walk form (VFD_VPB_WALK): a task = one 8x4 brick column over VB_LG voxel layers
-// [zbase, zend), one wave.  Its entry list is the (VB_LG + 1) cell layers zbase - 1 .. zend - 1
-// x 5 cell rows, in ascending cell layer; a sample of cell layer z0 adds to the 4 corners of voxel
-// layer z0 (weight az0) and of z0 + 1 (az1), so each gradient row is read once per task instead of
-// once per voxel layer.  Two LDS layer slots roll up the column (layer z in slot z & 1): when the
-// walk reaches cell layer z0, every voxel layer below z0 has all its samples and is written out
-// (plain stores, or atomics into pre-zeroed voxels for split tasks) and its slot cleared.
-constexpr int VW_LAYER = VB_Y * VB_X * 64;
-__shared__ float vw_lacc[2 * VW_LAYER + 64];          // two layer slots + a scratch row (masked corners)
-
-// write voxel layer zl of the task from its slot, clear the slot
-template <int CV>
-__device__ __noinline__ void vw_writeout(float* __restrict__ dvox_b, int zl, int xb, int yb, int X, int Y, int split) {
-  const int lane = threadIdx.x;
-  float* lay = vw_lacc + (zl & 1) * VW_LAYER;
-  constexpr int QPV = CV / 4, VPI = 64 / QPV;
-  const int q = lane % QPV, vsub = lane / QPV;
-  for (int v0 = 0; v0 < VB_X * VB_Y; v0 += VPI) {
-    const int vl = v0 + vsub;
-    const int x = xb + vl % VB_X, y = yb + vl / VB_X;
-    const float4 a = *reinterpret_cast<const float4*>(lay + vl * 64 + q * 4);
-    if (x < X && y < Y) {
-      float* dst = dvox_b + ((size_t)(zl * Y + y) * X + x) * CV + q * 4;
-      if (!split) {
-        *reinterpret_cast<float4*>(dst) = a;
-      } else {
-        unsafeAtomicAdd(dst + 0, a.x);
-        unsafeAtomicAdd(dst + 1, a.y);
-        unsafeAtomicAdd(dst + 2, a.z);
-        unsafeAtomicAdd(dst + 3, a.w);
-      }
-    }
-  }
-  // the whole slot, channel lanes >= CV included (they accumulate copies of channel 0)
-  for (int i = lane; i < VW_LAYER / 4; i += 64) reinterpret_cast<float4*>(lay)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-}
-
-template <int CV>
-__global__ __launch_bounds__(64) void vpb_walk_k(vfd_voxel_desc d, const int* __restrict__ ptr,
-                                                 const int* __restrict__ boff, const float4* __restrict__ entries,
-                                                 const int2* __restrict__ tasks, int* __restrict__ ctrl,
-                                                 const float* __restrict__ dout, const float* __restrict__ fbz,
-                                                 float* __restrict__ dvox) {
-  const VpbGeom g = vpb_geom(d);
-  const int lane = threadIdx.x;
-  const int cl = lane < CV ? lane : 0;
-  const int V = d.X * d.Y * d.Z;
-  const int ntask = ctrl[0];
-  float* trash = vw_lacc + 2 * VW_LAYER;
-  for (int i = lane; i < 2 * VW_LAYER / 4; i += 64) reinterpret_cast<float4*>(vw_lacc)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (;;) {
-    int tk0 = 0;
-    if (lane == 0) tk0 = atomicAdd(ctrl + 8, 1);
-    const int t = __shfl(tk0, 0, 64);
-    if (t >= ntask) break;
-    const int2 tk = tasks[t];
-    const int tile = tk.x, part = tk.y & 0xFFFF, np = tk.y >> 16;
-    const int b = tile / g.ntile, tl = tile % g.ntile;
-    int xb, yb, zp;
-    vpb_tile_pos(d, g, tl, &xb, &yb, &zp);
-    const int zbase = VB_LG * zp, zend = min(zbase + VB_LG, d.Z);
-    float* dvox_b = dvox + (size_t)b * V * CV;
-    // entry ranges (lanes 0 .. VB_WSEG-1), cell layer major
-    int s0 = 0, s1 = 0;
-    if (lane < VB_WSEG) vpb_segment(d, g, ptr, boff, b, zbase - 1 + lane / VB_RY, yb - 1 + lane % VB_RY, xb, &s0, &s1);
-    const int len = s1 - s0;
-    int inc = len;
-#pragma unroll
-    for (int off = 1; off < 32; off <<= 1) {
-      const int tt = __shfl_up(inc, off, 64);
-      if (lane >= off) inc += tt;
-    }
-    const int total = __builtin_amdgcn_readlane(inc, VB_WSEG - 1);
-    const int lo = (int)((long long)total * part / np), hi = (int)((long long)total * (part + 1) / np);
-    auto entry_of = [&](int gi) {
-      gi = min(gi, hi - 1);
-      int seg = 0;
-#pragma unroll
-      for (int k = 0; k < VB_WSEG - 1; ++k) seg += gi >= __builtin_amdgcn_readlane(inc, k) ? 1 : 0;
-      const int ss = __shfl(s0, seg, 64), ex = __shfl(inc - len, seg, 64);
-      return entries[ss + gi - ex];
-    };
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f, a4 = 0.f, a5 = 0.f, a6 = 0.f, a7 = 0.f;
-    int cur = -1;                  // current cell key (wave-uniform)
-    unsigned cmask = 0;            // corners: bits 0-3 layer z0, 4-7 layer z0 + 1
-    // split parts only write the layers they touched; a whole task writes every layer
-    int zlo = zbase, ztop = np == 1 ? zend : zbase;
-    bool started = np == 1;
-    auto flush = [&]() {
-      const int z0 = zbase - 1 + (cur >> 8);
-      const int lx = (cur & 15) - 1, ly = ((cur >> 4) & 15) - 1;
-      const int ro = (ly * VB_X + lx) * 64;
-      float* r0 = vw_lacc + (z0 & 1) * VW_LAYER + ro;
-      float* r1 = vw_lacc + ((z0 + 1) & 1) * VW_LAYER + ro;
-      float* p0 = (cmask & 1u) ? r0 : trash;
-      float* p1 = (cmask & 2u) ? r0 + 64 : trash;
-      float* p2 = (cmask & 4u) ? r0 + VB_X * 64 : trash;
-      float* p3 = (cmask & 8u) ? r0 + VB_X * 64 + 64 : trash;
-      float* p4 = (cmask & 16u) ? r1 : trash;
-      float* p5 = (cmask & 32u) ? r1 + 64 : trash;
-      float* p6 = (cmask & 64u) ? r1 + VB_X * 64 : trash;
-      float* p7 = (cmask & 128u) ? r1 + VB_X * 64 + 64 : trash;
-      const float v0 = p0[lane], v1 = p1[lane], v2 = p2[lane], v3 = p3[lane];
-      const float v4 = p4[lane], v5 = p5[lane], v6 = p6[lane], v7 = p7[lane];
-      p0[lane] = v0 + a0;
-      p1[lane] = v1 + a1;
-      p2[lane] = v2 + a2;
-      p3[lane] = v3 + a3;
-      p4[lane] = v4 + a4;
-      p5[lane] = v5 + a5;
-      p6[lane] = v6 + a6;
-      p7[lane] = v7 + a7;
-      a0 = a1 = a2 = a3 = a4 = a5 = a6 = a7 = 0.f;
-    };
-    struct Prm {
-      int key, m;
-      float w[8];
-      unsigned row;
-    };
-    auto setup = [&](const float4& e, int g0) {
-      Prm q;
-      const bool valid = g0 + lane < hi;
-      const float fx0 = floorf(e.x), fy0 = floorf(e.y), fz0 = floorf(e.z);
-      const float ax0 = fx0 + 1.f - e.x, ax1 = e.x - fx0, ay0 = fy0 + 1.f - e.y, ay1 = e.y - fy0;
-      const float az0 = fz0 + 1.f - e.z, az1 = e.z - fz0;
-      const int x0 = (int)fx0, y0 = (int)fy0, z0 = valid ? (int)fz0 : zbase;
-      // ATen trilinear weights (ax[dx] * ay[dy]) * az[dz], as in frustum_sample
-      const float xy0 = ax0 * ay0, xy1 = ax1 * ay0, xy2 = ax0 * ay1, xy3 = ax1 * ay1;
-      q.w[0] = xy0 * az0;
-      q.w[1] = xy1 * az0;
-      q.w[2] = xy2 * az0;
-      q.w[3] = xy3 * az0;
-      q.w[4] = xy0 * az1;
-      q.w[5] = xy1 * az1;
-      q.w[6] = xy2 * az1;
-      q.w[7] = xy3 * az1;
-      const bool xin0 = x0 >= max(xb, 0), xin1 = x0 + 1 < min(xb + VB_X, d.X);
-      const bool yin0 = y0 >= max(yb, 0), yin1 = y0 + 1 < min(yb + VB_Y, d.Y);
-      const unsigned mxy = (xin0 && yin0 ? 1u : 0u) | (xin1 && yin0 ? 2u : 0u) | (xin0 && yin1 ? 4u : 0u) |
-                           (xin1 && yin1 ? 8u : 0u);
-      const unsigned lay = (z0 >= zbase ? mxy : 0u) | (z0 + 1 < zend ? mxy << 4 : 0u);
-      q.m = valid ? (int)lay : 0;
-      q.key = valid ? ((z0 - zbase + 1) << 8) | ((y0 - yb + 1) << 4) | (x0 - xb + 1) : -1;
-      q.row = valid ? __float_as_uint(e.w) : 0x80000000u;     // past the end: the zero row
-      return q;
-    };
-    constexpr int PQ = VFD_VPB_PQ;
-    auto load_part = [&](const Prm& q, int h, float* gr) {
-#pragma unroll
-      for (int j = 0; j < PQ; ++j) {
-        const unsigned rj = (unsigned)__builtin_amdgcn_readlane((int)q.row, h * PQ + j);
-        const float* src = (rj >> 31) ? fbz : dout;
-        gr[j] = src[(size_t)(rj & 0x7FFFFFFFu) * CV + cl];
-      }
-    };
-    auto rl = [](float v, int j) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j)); };
-    auto process_part = [&](const Prm& q, int h, const float* gr) {
-#pragma unroll
-      for (int j = 0; j < PQ; ++j) {
-        const int jj = h * PQ + j;
-        const float gj = gr[j];
-        const int kj = __builtin_amdgcn_readlane(q.key, jj);
-        if (kj != cur) {
-          flush();
-          cur = kj;
-          cmask = (unsigned)__builtin_amdgcn_readlane(q.m, jj);
-          if (kj >= 0) {
-            const int z0 = zbase - 1 + (kj >> 8);
-            if (!started) {
-              zlo = max(zbase, z0);
-              started = true;
-            }
-            ztop = max(ztop, min(zend, z0 + 2));
-            while (zlo < z0) vw_writeout<CV>(dvox_b, zlo++, xb, yb, d.X, d.Y, np > 1);
-          }
-        }
-        a0 += rl(q.w[0], jj) * gj;
-        a1 += rl(q.w[1], jj) * gj;
-        a2 += rl(q.w[2], jj) * gj;
-        a3 += rl(q.w[3], jj) * gj;
-        a4 += rl(q.w[4], jj) * gj;
-        a5 += rl(q.w[5], jj) * gj;
-        a6 += rl(q.w[6], jj) * gj;
-        a7 += rl(q.w[7], jj) * gj;
-      }
-    };
-    if (lo < hi) {
-      constexpr int NST = 64 / PQ;
-      float4 en = entry_of(lo + lane);
-      Prm P = setup(en, lo);
-      en = entry_of(lo + 64 + lane);
-      float gr[2][PQ];
-      load_part(P, 0, gr[0]);
-      for (int g0 = lo; g0 < hi; g0 += 64) {
-        Prm Pn = P;
-#pragma unroll
-        for (int st = 0; st < NST; ++st) {
-          if (st + 1 < NST) {
-            load_part(P, st + 1, gr[(st + 1) & 1]);
-          } else {
-            Pn = setup(en, g0 + 64);
-            en = entry_of(g0 + 128 + lane);
-            load_part(Pn, 0, gr[(st + 1) & 1]);
-          }
-          process_part(P, st, gr[st & 1]);
-        }
-        P = Pn;
-      }
-    }
-    flush();
-    while (zlo < ztop) vw_writeout<CV>(dvox_b, zlo++, xb, yb, d.X, d.Y, np > 1);
   }
 }
 
@@ -2945,10 +2706,7 @@ static void vpb_bwd_launch(const vfd_voxel_desc* d, const float* d_out, void* ws
 #define VPB_LAUNCH(CVV)                                                                                         \
   case CVV:                                                                                                     \
     vpb_fold_zero_k<CVV><<<nf + nb + 1, 256, 0, s>>>(*d, d_out, p.fb, nf, p.parts, nb, p.ctrl, d_vox);            \
-    if (VFD_VPB_WALK)                                                                                           \
-      vpb_walk_k<CVV><<<VPB_WORKERS, 64, 0, s>>>(*d, p.ptr, p.boff, p.entries, p.tasks, p.ctrl, d_out, p.zrow, d_vox); \
-    else                                                                                                        \
-      vpb_main_k<CVV><<<VPB_WORKERS / VB_LG, 64 * VB_LG, 0, s>>>(*d, p.ptr, p.boff, p.entries, p.tasks, p.ctrl, d_out, \
+    vpb_main_k<CVV><<<VPB_WORKERS / VB_LG, 64 * VB_LG, 0, s>>>(*d, p.ptr, p.boff, p.entries, p.tasks, p.ctrl, d_out, \
                                                                  p.zrow, d_vox);                                \
     break;
     VPB_LAUNCH(8)

@@ -198,11 +198,7 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pcv_main_k(vfd_voxel_desc d, Pc
   if (!compute) {
     // producer: atom a+1 into the other buffer while the compute waves run atom a
     for (int atom = a_lo; atom < a_hi; ++atom) {
-#ifdef VFD_PC_NOGATHER
-      if (false)                                      // experiment: no gather after the first atom
-#else
       if (atom + 1 < a_hi)
-#endif
         gather(atom + 1, xs[(atom + 1 - a_lo) & 1]);
       __syncthreads();
     }
@@ -229,11 +225,7 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pcv_main_k(vfd_voxel_desc d, Pc
   int pf_atom = a_lo, pf_it = 0;
   auto prefetch = [&](int slot) {
     if (pf_atom < a_hi) {
-#ifdef VFD_PC_SAMEW
-      const int di = 0;                               // experiment: every atom reads bin 0's weights
-#else
       const int di = pf_atom % d.D;
-#endif
       const float2* w = wlane + ((size_t)di * PC_ITERS + pf_it) * (2 * PC_O);
       bq[slot][0] = w[0];
       bq[slot][1] = w[64];

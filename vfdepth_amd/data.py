@@ -409,13 +409,28 @@ class DDADDataset(Dataset):
         cam_pts = (np.linalg.inv(E) @ E_l @ hom.T).T[:, :3]          # lidar -> vehicle -> camera
         return project_depth_map(cam_pts, K, size[1], size[0])
 
+    def _mask_set(self, scene_name):
+        """The scene's self-occlusion mask set: the reference looks up `mask_idx_dict[int(scene)]`
+        (ddad_dataset_sf.py:102), so a JSON dump of its dict has keys like '150' for directory
+        '000150'.  No mapping given: every scene uses set 0 (documented in the module header); a
+        mapping that lacks the scene is an error, not a silent fallback."""
+        if not self.mask_idx:
+            return 0
+        keys = [scene_name]
+        if scene_name.isdigit():
+            keys = [str(int(scene_name)), int(scene_name), scene_name]
+        for k in keys:
+            if k in self.mask_idx:
+                return self.mask_idx[k]
+        raise KeyError(f'scene {scene_name!r} is not in the mask-set mapping (tried {keys})')
+
     def __getitem__(self, idx):
         si, i = self.items[idx]
         scene = self.scenes[si]
         contexts = _contexts(self.bwd, self.fwd)
         calib = self._calibration(scene, scene['samples'][i]['calibration_key'])
         scene_name = os.path.basename(scene['_dir'])
-        mask_idx = self.mask_idx.get(scene_name, self.mask_idx.get(str(scene_name), 0))
+        mask_idx = self._mask_set(scene_name)
         sample = []
         for cam in self.cameras:
             K, E = calib[cam]
@@ -429,8 +444,8 @@ class DDADDataset(Dataset):
             if self.with_pose:
                 data['extrinsics'] = E.astype(np.float32)
             if self.with_mask:
-                data['mask'] = (mask_loader_scene(self.mask_path, mask_idx, cam) if self.mask_path
-                                else pil.new('L', rgb.size, 255))
+                data['mask'] = (pil.new('L', rgb.size, 255) if self.mask_path == ALL_ONES_MASK
+                                else mask_loader_scene(self.mask_path, mask_idx, cam))
             if self.has_context:
                 data['rgb_context'] = ([self._image(scene, i - 1, cam)] if self.bwd else []) + \
                                       ([self._image(scene, i + 1, cam)] if self.fwd else [])
@@ -496,13 +511,21 @@ class NuScenesDataset(Dataset):
         return pose_matrix(quat_to_matrix(*r), cs['translation']).astype(np.float32)
 
     def _depth(self, sample, cam_sd):
+        """nuscenes_dataset.py:103-210: the cached map `<dirname(path)>/samples/DEPTH_MAP/<CAM>/
+        <image file>.npz` when it exists (read with allow_pickle=False: arrays only), else the
+        LIDAR_TOP sweep projected; the homogeneous ego-frame points are rounded to fp32 before the
+        lidar -> camera transform, as the reference's `torch.from_numpy(...).float()` does."""
+        cam = cam_sd['filename'].split('/')[-2] if '/' in cam_sd['filename'] else ''
+        cache = os.path.join(os.path.dirname(self.path), 'samples', 'DEPTH_MAP', cam, cam_sd['filename'] + '.npz')
+        if os.path.exists(cache):
+            return _load_depth_npz(cache)
         lid = self.get('sample_data', sample['data']['LIDAR_TOP'])
         pts = np.fromfile(os.path.join(self.path, lid['filename']), dtype=np.float32).reshape(-1, 5)[:, :3]
         lp = self.get('ego_pose', lid['ego_pose_token'])
         lidar_to_world = pose_matrix(quat_to_matrix(*lp['rotation']), lp['translation'])
         ls = self.get('calibrated_sensor', lid['calibrated_sensor_token'])
         ego_pts = pts.astype(np.float64) @ quat_to_matrix(*ls['rotation']).T + np.asarray(ls['translation'])
-        hom = np.concatenate([ego_pts, np.ones((len(ego_pts), 1))], 1)
+        hom = np.concatenate([ego_pts, np.ones((len(ego_pts), 1))], 1).astype(np.float32).astype(np.float64)
         ep = self.get('ego_pose', cam_sd['ego_pose_token'])
         world_to_ego = np.linalg.inv(pose_matrix(quat_to_matrix(*ep['rotation']), ep['translation']))
         cs = self.get('calibrated_sensor', cam_sd['calibrated_sensor_token'])
@@ -527,8 +550,8 @@ class NuScenesDataset(Dataset):
             if self.with_pose:
                 data['extrinsics'] = self._extrinsics(cs)
             if self.with_mask:
-                data['mask'] = (mask_loader_scene(self.mask_path, '', cam) if self.mask_path
-                                else pil.new('L', data['rgb'].size, 255))
+                data['mask'] = (pil.new('L', data['rgb'].size, 255) if self.mask_path == ALL_ONES_MASK
+                                else mask_loader_scene(self.mask_path, '', cam))
             if self.has_context:
                 ctx = []
                 for k, on in (('prev', self.bwd), ('next', self.fwd)):
@@ -549,6 +572,20 @@ def augmentation(cfg, mode):
             'crop_train_borders': (), 'crop_eval_borders': ()}
 
 
+ALL_ONES_MASK = 'all_ones'
+
+
+def _mask_path(d, req):
+    """`data.mask_path` when the requirements include 'mask'.  The reference always loads the
+    self-occlusion masks (dataset/ddad_mask, dataset/nuscenes_mask); training without them changes
+    the loss, so it must be asked for explicitly: `data.mask_path: 'all_ones'`."""
+    path = d.get('mask_path')
+    if 'mask' in req and not path:
+        raise ValueError("data.mask_path is not set but the requirements include 'mask': point it at the "
+                         "self-occlusion mask directory, or set it to 'all_ones' to train without masks")
+    return path
+
+
 def construct_dataset(cfg, mode, **kwargs):
     """base_dataset.py:5-50 (both modes use the 'train' transform, as the reference)."""
     d, m = cfg['data'], cfg['model']
@@ -563,10 +600,10 @@ def construct_dataset(cfg, mode, **kwargs):
         if d.get('mask_idx_json'):
             with open(d['mask_idx_json']) as f:
                 mask_idx = json.load(f)
-        return DDADDataset(d['data_path'], mode, mask_path=d.get('mask_path'), mask_idx=mask_idx, **args)
+        return DDADDataset(d['data_path'], mode, mask_path=_mask_path(d, req), mask_idx=mask_idx, **args)
     if d['dataset'] == 'nuscenes':
         return NuScenesDataset(d['data_path'], mode, version=d.get('nusc_version', 'v1.0-trainval'),
-                               split_dir=d.get('split_dir'), mask_path=d.get('mask_path'), **args)
+                               split_dir=d.get('split_dir'), mask_path=_mask_path(d, req), **args)
     raise ValueError('Unknown dataset: ' + d['dataset'])
 
 
@@ -645,6 +682,11 @@ class DevicePrefetcher:
         return len(self.loader)
 
 
+class _LoaderError:
+    def __init__(self, exc):
+        self.exc = exc
+
+
 class ThreadedLoader:
     """Background-thread batch producer (queue depth `depth`) for map-style datasets when
     DataLoader worker processes are unwanted (e.g. inside a process that already owns the GPU)."""
@@ -663,16 +705,22 @@ class ThreadedLoader:
         n = len(self)
 
         def work():
-            for b in range(n):
-                items = [self.dataset[i] for i in self.indices[b * self.batch_size:(b + 1) * self.batch_size]]
-                batch = self.collate(items)
-                if self.pin and torch.cuda.is_available():
-                    batch = {k: (v.pin_memory() if torch.is_tensor(v) else v) for k, v in batch.items()}
-                q.put(batch)
-            q.put(None)
+            try:
+                for b in range(n):
+                    items = [self.dataset[i] for i in self.indices[b * self.batch_size:(b + 1) * self.batch_size]]
+                    batch = self.collate(items)
+                    if self.pin and torch.cuda.is_available():
+                        batch = {k: (v.pin_memory() if torch.is_tensor(v) else v) for k, v in batch.items()}
+                    q.put(batch)
+            except BaseException as e:          # a bad sample fails the consumer, never hangs it
+                q.put(_LoaderError(e))
+            finally:
+                q.put(None)
         threading.Thread(target=work, daemon=True).start()
         while True:
             b = q.get()
             if b is None:
                 return
+            if isinstance(b, _LoaderError):
+                raise b.exc
             yield b

@@ -925,18 +925,18 @@ def _bn_group(bn):
     return pg if dist.get_world_size(pg) > 1 else None
 
 
-def _bn_sync(lib, d, partial, pg, what, count=None):
-    """Per-channel [C, 2] fp64 sums reduced over the group (+ the global element count when the
-    local one is given: ranks may hold different batch sizes, as SyncBatchNorm allows)."""
+def _bn_sync(lib, d, partial, pg, count, what, invstd=None, dgamma=None, dbeta=None):
+    """SyncBatchNorm exchange: the per-channel fp64 sums [C, 2] plus the local element count as row
+    C, reduced over the group in ONE all-reduce (ranks may hold different batch sizes, as
+    SyncBatchNorm allows; the apply kernels read the global count from row C on the device, so
+    nothing waits on the host).  Backward (invstd given): d gamma / d beta from this rank's LOCAL
+    sums first, as torch's SyncBatchNorm returns them (DDP then averages them over ranks)."""
     import torch.distributed as dist
-    sums = torch.empty(d.C, 2, dtype=torch.float64, device=partial.device)
-    L.check(lib.vfd_bn_sum(ctypes.byref(d), partial.data_ptr(), sums.data_ptr(), L.stream()), what)
+    sums = torch.empty(d.C + 1, 2, dtype=torch.float64, device=partial.device)
+    L.check(lib.vfd_bn_sum(ctypes.byref(d), partial.data_ptr(), float(count), sums.data_ptr(), L.ptr(invstd),
+                           L.ptr(dgamma), L.ptr(dbeta), L.stream()), what)
     dist.all_reduce(sums, group=pg)
-    if count is None:
-        return sums, None
-    cnt = torch.tensor([float(count)], dtype=torch.float64, device=partial.device)
-    dist.all_reduce(cnt, group=pg)
-    return sums, float(cnt.item())
+    return sums
 
 
 class BatchNormAct(torch.autograd.Function):
@@ -973,8 +973,9 @@ class BatchNormAct(torch.autograd.Function):
         partial = torch.empty(C, d.S, 2, dtype=torch.float64, device=x.device)
         L.check(lib.vfd_bn_fwd_stats(ctypes.byref(d), x.data_ptr(), partial.data_ptr(), L.stream()), 'bn_fwd_stats')
         count, sums, ns = float(N * H * W), partial, d.S
-        if pg is not None:
-            (sums, count), ns = _bn_sync(lib, d, partial, pg, 'bn_sum', count), 1
+        if pg is not None:          # global sums and count from the group; count 0 = read on device
+            sums, ns = _bn_sync(lib, d, partial, pg, count, 'bn_sum'), 1
+            count = 0.0
         y = torch.empty_like(x)
         mean = torch.empty(C, device=x.device)
         invstd = torch.empty(C, device=x.device)
@@ -1016,20 +1017,22 @@ class BatchNormAct(torch.autograd.Function):
         yp = mk.data_ptr() if d.relu else None
         L.check(lib.vfd_bn_bwd_stats(ctypes.byref(d), g.data_ptr(), yp, x.data_ptr(), mean.data_ptr(),
                                      partial.data_ptr(), L.stream()), 'bn_bwd_stats')
-        sums, ns, count = partial, d.S, ctx.count
-        if ctx.pg is not None:
-            sums, ns = _bn_sync(lib, d, partial, ctx.pg, 'bn_sum')[0], 1
         need = ctx.needs_input_grad
         dx = torch.empty_like(x) if need[0] else None
         dr = torch.empty_like(x) if ctx.has_res and need[3] else None
         dgamma = torch.empty_like(gamma) if need[1] else None
         dbeta = torch.empty_like(gamma) if need[2] else None
         ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+        sums, ns, count = partial, d.S, ctx.count
+        pg_dgamma, pg_dbeta = dgamma, dbeta
+        if ctx.pg is not None:      # local d gamma / d beta, then the global sums (+ count row)
+            sums, ns = _bn_sync(lib, d, partial, ctx.pg, x.shape[0] * d.HW, 'bn_sum', invstd, dgamma, dbeta), 1
+            count, pg_dgamma, pg_dbeta = 0.0, None, None
         if L.PROF_ON:                        # compulsory: g, x (, the mask) in, dx (, dr) out
             L.ALG_BYTES['bn_bwd'] += x.numel() * (8 + (d.relu != 0) + 4 * ((dx is not None) + (dr is not None)))
         L.check(lib.vfd_bn_bwd_apply(ctypes.byref(d), g.data_ptr(), yp, x.data_ptr(), sums.data_ptr(), ns, count,
                                      gamma.data_ptr(), mean.data_ptr(), invstd.data_ptr(), ptr(dx), ptr(dr),
-                                     ptr(dgamma), ptr(dbeta), L.stream()), 'bn_bwd_apply')
+                                     ptr(pg_dgamma), ptr(pg_dbeta), L.stream()), 'bn_bwd_apply')
         return dx, dgamma, dbeta, dr, None, None, None, None, None, None, None
 
 
@@ -1221,55 +1224,6 @@ class DispConvSigmoid(torch.autograd.Function):
             dw = tot[:C * 9].view(1, C, 3, 3) if need[1] else None
             db = tot[C * 9:] if need[2] else None
         return dxp, dw, db
-
-
-class StemConv(torch.autograd.Function):
-    """conv1 (7x7, stride 2, padding 3, 64 outputs, no bias) of the normalised image
-    (image - 0.45) / 0.225 — the ResNet encoders' input normalisation and stem conv in one fp32
-    MFMA kernel (stemconv.hip); backward: the weight gradient (the image takes none)."""
-
-    @staticmethod
-    def supported(image, weight):
-        if not (image.is_cuda and image.dim() == 4 and image.dtype == torch.float32 and not image.requires_grad
-                and weight.dim() == 4 and tuple(weight.shape[2:]) == (7, 7) and weight.shape[1] == image.shape[1]):
-            return False
-        N, C, H, W = image.shape
-        return bool(L.load().vfd_stem_conv_supported(N, C, H, W, weight.shape[0]))
-
-    @staticmethod
-    def forward(ctx, image, weight):
-        lib = L.load()
-        image = _dev(image, 'stem conv image')
-        w = weight.detach().contiguous()
-        N, C, H, W = image.shape
-        Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
-        y = torch.empty(N, 64, Ho, Wo, device=image.device)
-        L.check(lib.vfd_stem_conv_fwd(image.data_ptr(), w.data_ptr(), y.data_ptr(), N, C, H, W, L.stream()),
-                'stem_conv_fwd')
-        if L.PROF_ON:
-            L.ALG_BYTES['stem_conv'] += (image.numel() + y.numel()) * 4
-        ctx.save_for_backward(image)
-        ctx.C = C
-        return y
-
-    @staticmethod
-    def backward(ctx, g):
-        lib = L.load()
-        image, = ctx.saved_tensors
-        if not ctx.needs_input_grad[1]:
-            return None, None
-        g = g.contiguous()
-        N, C, H, W = image.shape
-        kt = lib.vfd_stem_conv_ktiles(C)
-        nkt = (kt + 3) // 4 * 4
-        part = torch.empty(lib.vfd_stem_conv_wgrad_groups(), nkt, 64, 16, device=g.device)
-        L.check(lib.vfd_stem_conv_wgrad(image.data_ptr(), g.data_ptr(), part.data_ptr(), N, C, H, W, L.stream()),
-                'stem_conv_wgrad')
-        if L.PROF_ON:
-            L.ALG_BYTES['stem_conv'] += (image.numel() + g.numel()) * 4
-        K = C * 49
-        dw = part.sum(0).permute(1, 0, 2).reshape(64, nkt * 16)[:, :K].reshape(64, C, 7, 7)
-        return None, dw
 
 
 def normalize_cat(a, b=None):

@@ -212,17 +212,8 @@ class ResnetEncoder(nn.Module):
         """image: [n, 3*num_input_images, H, W] in [0, 1]; normalized=True: already (x - 0.45) / 0.225
         (the fused nets normalise while concatenating frames: kernels.normalize_cat)."""
         e = self.encoder
-        from . import kernels as KN
-        # opt-in (VFD_STEM_CONV=1): correct, but its per-lane gathers run the pose stem at 613 us
-        # forward vs MIOpen's 286 (tools/micro_decconv.py); MIOpen stays the default
-        if (not normalized and os.environ.get('VFD_STEM_CONV', '0') == '1' and not torch.is_autocast_enabled('cuda')
-                and e.conv1.bias is None and e.conv1.stride == (2, 2) and e.conv1.padding == (3, 3)
-                and KN.StemConv.supported(image, e.conv1.weight)):
-            # normalisation + conv1 in one MFMA kernel (stemconv.hip)
-            f0 = bn_act(e.bn1, KN.StemConv.apply(image, e.conv1.weight))
-        else:
-            x = image if normalized else (image - 0.45) / 0.225
-            f0 = bn_act(e.bn1, e.conv1(x))
+        x = image if normalized else (image - 0.45) / 0.225
+        f0 = bn_act(e.bn1, e.conv1(x))
         f1 = e.layer1(max_pool_stem(e.maxpool, f0))
         f2 = e.layer2(f1)
         f3 = e.layer3(f2)

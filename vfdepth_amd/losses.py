@@ -205,6 +205,15 @@ class DepthSynLoss(MultiCamLoss):
     clamp(|a - t| / (a + t + 1e-8), 0, 1) as one masked mean over all sources, and plain-gradient
     smoothness of disp_aug / mean; weighted by depth_con_coeff / depth_sm_coeff."""
 
+    def __init__(self, cfg, rank):
+        super().__init__(cfg, rank)
+        if list(self.scales) != [0]:
+            # the reference adds the depth-synthesis terms of every scale before dividing by the
+            # scale count (depth_synthesis_loss.py:66-89); this build renders the augmented view
+            # at scale 0 only (every shipped config uses scales [0]), so refuse rather than
+            # silently weight the terms differently
+            raise NotImplementedError(f'aug_depth supports scales [0] only, got {list(self.scales)}')
+
     @staticmethod
     def syn_terms(aug_depth, tform, tmask, disp_aug):
         """aug_depth, disp_aug [B, N, H, W]; tform, tmask [B, N, S, H, W] -> (con [N], sm [N])."""

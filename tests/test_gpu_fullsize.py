@@ -35,7 +35,9 @@ def _need_gpu():
     torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
 
 
-def close(a, b, what, atol=1e-4, rtol=1e-4, where=None, max_off=0):
+def close(a, b, what, atol=1e-4, rtol=1e-4, where=None, max_off=0, cap=None):
+    """|a - b| <= atol + rtol |b| everywhere except at most `max_off` elements, which must still
+    lie within `cap` (absolute) when given."""
     a = a.detach().float().cpu() if torch.is_tensor(a) else torch.as_tensor(a)
     b = b.detach().float().cpu() if torch.is_tensor(b) else torch.as_tensor(b)
     assert a.shape == b.shape, f'{what}: shape {tuple(a.shape)} vs {tuple(b.shape)}'
@@ -44,6 +46,8 @@ def close(a, b, what, atol=1e-4, rtol=1e-4, where=None, max_off=0):
     if where is not None:
         bad &= where
     assert int(bad.sum()) <= max_off, f'{what}: {int(bad.sum())}/{bad.numel()} off, max err {float(err.max()):.3g}'
+    if cap is not None:
+        assert float(err.max()) <= cap, f'{what}: max err {float(err.max()):.3g} > cap {cap}'
 
 
 def gclose(a, b, what, rel=2e-4, where=None):
@@ -156,10 +160,16 @@ def test_view_synthesis_and_losses_full_size(config):
     rel = {c: pose.compute_relative_cam_poses(bd, outputs, c) for c in range(N)}
     vr.render_all(bd, outputs, rel, {0: d[:, :, 0]})
     gloss = 0.0
+    # 640x960 (config 5): one fp32 ulp of a source x coordinate is 6e-5 px, 2x that at 640 px;
+    # times the local image gradient, the GPU's and the CPU's differently associated projection
+    # products move a warped value by up to ~2e-4 — a handful of pixels in 10^6 cross the 1e-4
+    # bound (8 of 7.4 M in round 3); allow 1 in 10^5, each within 1e-3
+    max_off = 0 if config != 5 else None
     for c in range(N):
         out = outputs[('cam', c)]
         for i, k in enumerate(keys):
-            close(out[k], ref[c][k], f'{k} cam {c}')
+            close(out[k], ref[c][k], f'{k} cam {c}', max_off=max_off if max_off is not None else out[k].numel() // 100000,
+                  cap=1e-3)
             gloss = gloss + (out[k] * gw[(c, i)].to(DEV)).sum()
         for k in G.VIEW_MSK_KEYS:
             close(out[k], ref[c][k], f'{k} cam {c}', atol=0, rtol=0)
@@ -225,6 +235,15 @@ def _fusion_inputs(cfg, seed):
     return batch, lvl, Einv
 
 
+def _off_kink(ref, tol=1e-4):
+    """Zero the gradient functional on voxel channels whose K1 output lies within `tol` of the
+    LeakyReLU kink (0 < |out| < tol): there the fp32 GPU and CPU pre-activations (different
+    summation orders) may take different slopes (1 vs 0.1), a legitimate decision discontinuity
+    that moves the gradient by 0.9 g (config 4's d feats differed by 0.9 % of max without this mask)."""
+    a = ref.detach().abs()
+    return ((a == 0) | (a >= tol)).to(ref.dtype)
+
+
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize('config,k1', [(2, 'gather'), (2, 'scatter'), (4, 'gather'), (5, 'gather')])
 def test_fuse_depth_full_size(config, k1, monkeypatch):
@@ -250,7 +269,7 @@ def test_fuse_depth_full_size(config, k1, monkeypatch):
     fr = feats.clone().requires_grad_(grad)
     ref = O.fuse_depth(spec, fr, batch['mask'], batch[('K', lvl)], Einv, c_no.weight, c_no.bias, c_o.weight, c_o.bias)
     if grad:
-        g = G.seeded_randn(ref.shape, 93)
+        g = G.seeded_randn(ref.shape, 93) * _off_kink(ref)
         (ref * g).sum().backward()
         ref_grads = {k: p.grad.clone() for k, p in net.named_parameters() if p.grad is not None}
         net.zero_grad(set_to_none=True)
@@ -296,7 +315,7 @@ def test_fusion_ops_batch4_config5():
     # ---- K1, oracle on the subset
     fr = feats[sub].clone().requires_grad_(True)
     ref = O.fuse_depth(spec, fr, mask[sub], K[sub], Einv[sub], c_no.weight, c_no.bias, c_o.weight, c_o.bias)
-    g = G.seeded_randn(ref.shape, 194)
+    g = G.seeded_randn(ref.shape, 194) * _off_kink(ref)
     (ref * g).sum().backward()
     ref_grads = {k: p.grad.clone() for k, p in net.named_parameters() if p.grad is not None}
     net.zero_grad(set_to_none=True)
@@ -561,7 +580,10 @@ def test_proj_conv_matches_k3_plus_conv(config, B):
     y = KN.ProjConv.apply(space, leaves[0], invK, E, leaves[1], leaves[2])
     refs = [t.clone().requires_grad_(True) for t in (vox, w0, bias)]
     x = KN.VoxelProject.apply(space, refs[0], invK, E)
-    pre = F.conv2d(x, KN.proj_conv_weight(refs[1], Cv, D), refs[2])
+    wref = KN.proj_conv_weight(refs[1], Cv, D)
+    # per batch element (6 images each): the conv problems MIOpen already knows from B = 1, so no
+    # new solver search for a 24-image problem
+    pre = torch.cat([F.conv2d(xb, wref, refs[2]) for xb in x.split(6)], 0)
     # LeakyReLU with the fused kernel's own sign decisions: a pre-activation within fp32 rounding
     # of 0 may take the other branch in the two GEMM summation orders (the kink: slope 1 vs 0.1),
     # which the forward tolerates but would move the gradient by 0.9 g there

@@ -141,6 +141,13 @@ size_t vfd_proj_conv_fwd_workspace(const vfd_voxel_desc* d);
 int vfd_proj_conv_fwd(const vfd_voxel_desc* d, const float* vox, const float* invK, const float* E,
                       const float* Wq, const float* bias, int out_channels, float* out, float* x_out,
                       void* workspace, size_t ws_bytes, void* stream);
+/* bf16 form (config 3's autocast, volumetric_fusionnet.py:105-114): the same computation with the
+ * halo samples rounded to bf16 and bf16 weights on v_mfma_f32_32x32x16_bf16 (fp32 accumulation,
+ * bias and LeakyReLU in fp32).  vox / invK / E / bias fp32; Wq = vfd_weight_fragments_bf16 mode 3;
+ * out and x_out (nullable) bf16, same layouts as vfd_proj_conv_fwd; same workspace size. */
+int vfd_proj_conv_fwd_bf16(const vfd_voxel_desc* d, const float* vox, const float* invK, const float* E,
+                           const void* Wq, const float* bias, int out_channels, void* out, void* x_out,
+                           void* workspace, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------ fused BatchNorm (+res)(+ReLU) */
 /* Training-mode BatchNorm2d of the ResNet encoders (fusion_depthnet.py:24-36, fusion_posenet.py:
@@ -157,10 +164,12 @@ typedef struct vfd_bn_desc {
   int32_t S;             /* splits per channel: vfd_bn_splits(desc)                      */
   int32_t relu;          /* 1: ReLU after the (residual) add                              */
   float eps, momentum;   /* nn.BatchNorm2d eps / momentum                                 */
+  int32_t dtype;         /* activations x / residual / y / g / dx / d residual: 0 fp32,
+                            1 bf16 (config 3's autocast; statistics and parameters stay fp32 / fp64) */
 } vfd_bn_desc;
 
 int vfd_bn_splits(const vfd_bn_desc* d);
-int vfd_bn_fwd_stats(const vfd_bn_desc* d, const float* x, double* partial, void* stream);
+int vfd_bn_fwd_stats(const vfd_bn_desc* d, const void* x, double* partial, void* stream);
 /* count > 0: also writes row C = (count, 0).  invstd / dgamma / dbeta (backward, nullable): d gamma
  * = sum g'(x - mean) * invstd and d beta = sum g' from this rank's LOCAL sums (SyncBatchNorm's
  * parameter gradients are local; DDP averages them). */
@@ -172,30 +181,33 @@ int vfd_bn_sum(const vfd_bn_desc* d, const double* partial, double count, double
  * backward reads. */
 /* relu_mask (optional, N*C*HW bytes): the forward also stores [y > 0] per element; a backward call
  * with d->relu == 2 then takes that mask in place of y (a quarter of the bytes). */
-int vfd_bn_fwd_apply(const vfd_bn_desc* d, const float* x, const float* residual, const double* sums, int ns,
-                     double count, const float* gamma, const float* beta, float* y, float* mean, float* invstd,
+int vfd_bn_fwd_apply(const vfd_bn_desc* d, const void* x, const void* residual, const double* sums, int ns,
+                     double count, const float* gamma, const float* beta, void* y, float* mean, float* invstd,
                      float* running_mean, float* running_var, long long* num_batches_tracked,
                      unsigned char* relu_mask, void* stream);
 /* g = d y; y = the forward's output (ReLU mask; unused without ReLU), or with d->relu == 2 the
  * forward's byte mask */
-int vfd_bn_bwd_stats(const vfd_bn_desc* d, const float* g, const float* y, const float* x, const float* mean,
+int vfd_bn_bwd_stats(const vfd_bn_desc* d, const void* g, const void* y, const void* x, const float* mean,
                      double* partial, void* stream);
 /* dx, d residual, d gamma, d beta nullable (not requested) */
-int vfd_bn_bwd_apply(const vfd_bn_desc* d, const float* g, const float* y, const float* x, const double* sums,
-                     int ns, double count, const float* gamma, const float* mean, const float* invstd, float* dx,
-                     float* dresidual, float* dgamma, float* dbeta, void* stream);
+int vfd_bn_bwd_apply(const vfd_bn_desc* d, const void* g, const void* y, const void* x, const double* sums,
+                     int ns, double count, const float* gamma, const float* mean, const float* invstd, void* dx,
+                     void* dresidual, float* dgamma, float* dbeta, void* stream);
 
 /* ------------------------------------------------------------------ geometry */
 /* batched 4x4 inverse of n row-major matrices (torch.inverse of the extrinsics, models/vfdepth.py:211):
  * cofactors in geometry.inverse4x4's operation order (bit-identical to it), one thread per matrix */
 int vfd_inverse4x4(const float* m, float* out, int n, void* stream);
 
+/* dtype (max pool, reflect pad, ELU + up + pad): 0 = fp32 maps, 1 = bf16 maps (config 3's autocast;
+ * arithmetic in fp32, one round-to-nearest-even per output). */
 /* ------------------------------------------------------------------ ResNet stem max pool */
 /* MaxPool2d(3, 2, 1) of the encoders' stem, NCHW fp32: x [planes, h, w] -> y [planes, ho, wo]
  * (ho = (h-1)/2 + 1) and the winning window position (0..8) per output as one byte; ATen's tie
  * and NaN rules.  Backward: a fixed-order gather of the winners' gradients (no atomics). */
-int vfd_maxpool3s2_fwd(const float* x, float* y, uint8_t* arg, long long planes, int h, int w, void* stream);
-int vfd_maxpool3s2_bwd(const float* g, const uint8_t* arg, float* dx, long long planes, int h, int w, void* stream);
+int vfd_maxpool3s2_fwd(const void* x, void* y, uint8_t* arg, long long planes, int h, int w, int dtype, void* stream);
+int vfd_maxpool3s2_bwd(const void* g, const uint8_t* arg, void* dx, long long planes, int h, int w, int dtype,
+                       void* stream);
 /* The encoders' input normalisation (x - 0.45) / 0.225 of cat([a, b], channels) in one pass:
  * a [n_img, ca, hw], b [n_img, cb, hw] (cb = 0: a alone) -> dst [n_img, ca + cb, hw]; hw % 4 == 0. */
 int vfd_normalize_cat(const float* a, const float* b, float* dst, long long n_img, int ca, int cb, int hw,
@@ -205,18 +217,18 @@ int vfd_normalize_cat(const float* a, const float* b, float* dst, long long n_im
 /* nn.Conv2d(padding_mode='reflect', padding=1) of the decoders' 3x3 blocks (network/blocks.py):
  * x [planes, h, w] -> y [planes, h+2, w+2] (NCHW fp32), and its backward as a fixed-order gather
  * of each pixel's copies (deterministic, no atomics). */
-int vfd_reflect_pad1_fwd(const float* x, float* y, long long planes, int h, int w, void* stream);
-int vfd_reflect_pad1_bwd(const float* g, float* dx, long long planes, int h, int w, void* stream);
+int vfd_reflect_pad1_fwd(const void* x, void* y, long long planes, int h, int w, int dtype, void* stream);
+int vfd_reflect_pad1_bwd(const void* g, void* dx, long long planes, int h, int w, int dtype, void* stream);
 /* One-launch BatchNorm(+residual)(+ReLU) forward / backward for channels of at most 8192 elements
  * with local statistics (the small ResNet layers): one workgroup per channel computes the fp64
  * statistics and applies them; same arguments and results as bn_fwd_stats + bn_fwd_apply /
  * bn_bwd_stats + bn_bwd_apply (d->S unused).  vfd_bn1_fits: 1 when the shape qualifies. */
 int vfd_bn1_fits(const vfd_bn_desc* d);
-int vfd_bn1_fwd(const vfd_bn_desc* d, const float* x, const float* residual, const float* gamma, const float* beta,
-                float* y, float* mean, float* invstd, float* running_mean, float* running_var,
+int vfd_bn1_fwd(const vfd_bn_desc* d, const void* x, const void* residual, const float* gamma, const float* beta,
+                void* y, float* mean, float* invstd, float* running_mean, float* running_var,
                 long long* num_batches_tracked, unsigned char* relu_mask, void* stream);
-int vfd_bn1_bwd(const vfd_bn_desc* d, const float* g, const float* y, const float* x, const float* gamma,
-                const float* mean, const float* invstd, float* dx, float* dresidual, float* dgamma, float* dbeta,
+int vfd_bn1_bwd(const vfd_bn_desc* d, const void* g, const void* y, const void* x, const float* gamma,
+                const float* mean, const float* invstd, void* dx, void* dresidual, float* dgamma, float* dbeta,
                 void* stream);
 
 /* ------------------------------------------------------------------ disparity head (dispconv.hip) */
@@ -254,6 +266,13 @@ int vfd_dec_conv_bwd(const float* dy, const float* xp, const float* w, float* dx
  *   mode 2: K3C data-gradient copy [9 flipped taps][O/4][ceil256(Cv*D)][2][2] (n = d*Cv + c). */
 int vfd_weight_fragments(int mode, const float* w, float* dst, int O, int C, int C1, int Z, int Cv, int D,
                          void* stream);
+/* bf16 fragment copies (dst: bf16 elements, rounded to nearest even):
+ *   mode 3: K3C forward [D][9][Cv/16][O/32][64 lanes][8]: lane l of block ob holds
+ *           w[32 ob + (l & 31)][(16 q + 8 (l >> 5) + j) * D + d][tap], j = 0..7;
+ *   mode 4: K2C [9][ceil32(C)/16][O/32][64 lanes][8] over the map's channel order, built from
+ *           w = the fp32 mode-0 fragment copy (vfd_weight_fragments mode 0, same C / C1 / Z). */
+int vfd_weight_fragments_bf16(int mode, const float* w, void* dst, int O, int C, int C1, int Z, int Cv, int D,
+                              void* stream);
 /* dst[o][b][a][t] = w[o][a][b][t] (w [O][A][B][taps]): the pose weight between the reference channel
  * order c*Z + z (A = C1, B = Z) and K2's map order z*C1 + c, and back for its gradient. */
 int vfd_weight_swap(const float* w, float* dst, int O, int A, int B, int taps, void* stream);
@@ -267,9 +286,9 @@ int vfd_weight_permute(const float* w, float* dst, int O, int A, int B, int T, c
  * blocks.py:33-38 upsample, nn.Conv2d(padding_mode='reflect')) from the conv's pre-activation
  * y [planes, h, w] straight to the next conv's padded input out [planes, (h<<up)+2, (w<<up)+2];
  * backward dy = elu'(y) * (gather of the up-block's reflect copies of g), no atomics. */
-int vfd_elu_up_pad1_fwd(const float* y, float* out, long long planes, int h, int w, int up, void* stream);
-int vfd_elu_up_pad1_bwd(const float* g, const float* y, float* dy, long long planes, int h, int w, int up,
-                        float* psum, void* stream);
+int vfd_elu_up_pad1_fwd(const void* y, void* out, long long planes, int h, int w, int up, int dtype, void* stream);
+int vfd_elu_up_pad1_bwd(const void* g, const void* y, void* dy, long long planes, int h, int w, int up,
+                        float* psum, int dtype, void* stream);
 /* psum (optional, [planes][vfd_elu_up_pad1_bwd_blocks(h, w)]): per-block sums of dy per plane —
  * the partials of the producing conv's bias gradient (summed in fixed order by the caller) */
 int vfd_elu_up_pad1_bwd_blocks(int h, int w);
@@ -298,6 +317,12 @@ typedef struct vfd_conv_desc {
 size_t vfd_pad_conv_fwd_workspace(const vfd_conv_desc* d);
 int vfd_pad_conv_fwd(const vfd_conv_desc* d, const float* x, const float* Wf, const float* bias, float* out,
                      void* workspace, size_t ws_bytes, void* stream);
+/* bf16 form (config 3's autocast): the map rounded to bf16 as it is staged, bf16 weights
+ * (vfd_weight_fragments_bf16 mode 4), v_mfma_f32_32x32x16_bf16 with fp32 accumulation, bias and
+ * LeakyReLU in fp32; x fp32, out bf16 (same layout as vfd_pad_conv_fwd). */
+size_t vfd_pad_conv_fwd_bf16_workspace(const vfd_conv_desc* d);
+int vfd_pad_conv_fwd_bf16(const vfd_conv_desc* d, const float* x, const void* Wf, const float* bias, void* out,
+                          void* workspace, size_t ws_bytes, void* stream);
 
 /* K3C data gradient (volumetric_fusionnet.py:59-60, 265 backward): d of reduce_dim's first conv
  * w.r.t. its reflect-padded input, dx [B*N, h+2, w+2, D*Cv] (channel d*Cv + c: the layout

@@ -398,10 +398,10 @@ class OpRecorder:
         self.calls = {'k1': [], 'k2': [], 'k3': [], 'k3c': []}
         self._saved = [(owner, name, owner.__dict__.get(name)) for owner, name in
                        ((VFNet, 'backproject_depth'), (KN.FusePose, 'apply'), (KN.VoxelProject, 'apply'),
-                        (KN.ProjConv, 'apply'))]
+                        (KN.ProjConv, 'apply'), (KN.ProjConvBF16, 'apply'))]
         rec = self
         k1, k2, k3 = VFNet.backproject_depth, KN.FusePose.apply, KN.VoxelProject.apply
-        k3c = KN.ProjConv.apply
+        k3c, k3cb = KN.ProjConv.apply, KN.ProjConvBF16.apply
 
         def backproject_depth(net, inputs, feats):
             out = k1(net, inputs, feats)
@@ -422,10 +422,16 @@ class OpRecorder:
             out = k3c(space, vox, invK, E, w0, bias)
             rec.calls['k3c'].append((vox.detach().float(), invK, E, w0.detach(), bias.detach(), out.detach()))
             return out
+
+        def proj_conv_bf16(space, vox, invK, E, w0, bias):
+            out = k3cb(space, vox, invK, E, w0, bias)
+            rec.calls['k3c'].append((vox.detach().float(), invK, E, w0.detach(), bias.detach(), out.detach()))
+            return out
         VFNet.backproject_depth = backproject_depth
         KN.FusePose.apply = staticmethod(fuse_pose)
         KN.VoxelProject.apply = staticmethod(voxel_project)
         KN.ProjConv.apply = staticmethod(proj_conv)
+        KN.ProjConvBF16.apply = staticmethod(proj_conv_bf16)
 
     def restore(self):
         for owner, name, orig in self._saved:
@@ -470,10 +476,16 @@ def _check_recorded_ops(O, cfg, rec, inputs_cpu):
         B = vox.shape[0]
         with torch.no_grad():
             refs = O.project_voxels(spec, vox.cpu().permute(0, 2, 1), invK.cpu(), E.cpu())
-            got = out.view(B, 6, *out.shape[1:])
+            got = out.float().view(B, 6, *out.shape[1:])
             for c in range(6):
-                y = F.conv2d(F.pad(refs[c], (1, 1, 1, 1), mode='reflect'), w0.cpu(), bias.cpu())
-                close(got[:, c, :, 1:-1, 1:-1], F.leaky_relu(y, 0.1), f'K3C cam {c} in the step')
+                y = F.leaky_relu(F.conv2d(F.pad(refs[c], (1, 1, 1, 1), mode='reflect'), w0.cpu(), bias.cpu()), 0.1)
+                if out.dtype == torch.bfloat16:
+                    # the bf16 K3C (config 3): bf16 operands, fp32 accumulation, bf16 output — within
+                    # 2^-8 of each output plus the operand rounding's 1 % of the output scale
+                    close(got[:, c, :, 1:-1, 1:-1], y, f'bf16 K3C cam {c} in the step', atol=1e-2 * float(y.abs().max()),
+                          rtol=2.0 ** -8)
+                else:
+                    close(got[:, c, :, 1:-1, 1:-1], y, f'K3C cam {c} in the step')
 
 
 def _check_loss_path(O, cfg, inputs_cpu, outputs, losses, noise):
@@ -600,6 +612,60 @@ def test_proj_conv_matches_k3_plus_conv(config, B):
         gclose(a.grad, r.grad, f'K3C {name} (config {config})')
 
 
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize('config', ['small', 2])
+def test_proj_conv_bf16(config):
+    """K3C's bf16 form (config 3's autocast of the fusion features, volumetric_fusionnet.py:105-114)
+    against the same conv computed in fp32 on the bf16-rounded operands: the side output equals K3's
+    fp32 frustum features rounded to bf16 (the same fp32 arithmetic, then round to nearest even);
+    the output equals LeakyReLU(conv(bf16(x), bf16(w)) + b) up to fp32 summation order and the final
+    bf16 rounding (2^-8 relative); the gradients track the fp32 K3C's within bf16 precision."""
+    from vfdepth_amd import kernels as KN
+    from vfdepth_amd import synth
+    cfg = G.step_cfg() if config == 'small' else full_cfg(config)
+    space = KN.VoxelSpace(cfg, DEV)
+    b = G.perturb_rig(synth.make_batch(cfg, seed=171, batch_size=1), 170)
+    lvl = cfg['model']['fusion_level'] + 1
+    invK, E = b['inv_K', lvl].to(DEV), b['extrinsics'].to(DEV)
+    gen = torch.Generator(device=DEV).manual_seed(172)
+    Cv, D, O = 64, space.D, 256
+    vox = torch.randn(1, space.V, Cv, device=DEV, generator=gen)
+    w0 = torch.randn(O, Cv * D, 3, 3, device=DEV, generator=gen) * (Cv * D * 9) ** -0.5
+    bias = 0.1 * torch.randn(O, device=DEV, generator=gen)
+    leaves = [t.clone().requires_grad_(True) for t in (vox, w0, bias)]
+    y = KN.ProjConvBF16.apply(space, leaves[0], invK, E, leaves[1], leaves[2])
+    assert y.dtype == torch.bfloat16 and y.is_contiguous(memory_format=torch.channels_last)
+    with torch.no_grad():
+        x = KN.VoxelProject.apply(space, vox, invK, E)                    # fp32 frustum features (K3)
+        xs = y.grad_fn.saved_tensors[2]
+        diff = (xs.float() - x.to(torch.bfloat16).float()).abs()
+        assert float(diff.max()) == 0.0, f'bf16 side output vs bf16(K3): max diff {float(diff.max()):.3g}'
+        wq = KN.proj_conv_weight(w0, Cv, D).to(torch.bfloat16).float()
+        pre = F.conv2d(x.to(torch.bfloat16).float(), wq, bias)
+        ref = F.leaky_relu(pre, 0.1)
+        got = y[:, :, 1:-1, 1:-1].float()
+        err = (got - ref).abs()
+        bound = 2.0 ** -8 * ref.abs() + 1e-4 * float(ref.abs().max())
+        assert bool((err <= bound).all()), f'bf16 K3C output: max err {float(err.max()):.3g} (scale {float(ref.abs().max()):.3g})'
+        assert torch.equal(y[:, :, 0, 1:-1], y[:, :, 2, 1:-1]) and torch.equal(y[:, :, 1:-1, -1], y[:, :, 1:-1, -3])
+    # gradients: the same function in fp32 on the bf16-rounded operands (rounding passed straight
+    # through to K3 and the master weight) with the kernel's own LeakyReLU decisions (a
+    # pre-activation within the operands' bf16 rounding of 0 may take the other slope)
+    g = torch.randn(y.shape, device=DEV, generator=gen)
+    (y.float() * g).sum().backward()
+    refs = [t.clone().requires_grad_(True) for t in (vox, w0, bias)]
+    xf = KN.VoxelProject.apply(space, refs[0], invK, E)
+    xr = xf + (xf.to(torch.bfloat16).float() - xf).detach()
+    wf = KN.proj_conv_weight(refs[1], Cv, D)
+    wr = wf + (wf.to(torch.bfloat16).float() - wf).detach()
+    pre = F.conv2d(xr, wr, refs[2])
+    pos = y.detach()[:, :, 1:-1, 1:-1] > 0
+    yr = F.pad(torch.where(pos, pre, 0.1 * pre), (1, 1, 1, 1), mode='reflect')
+    (yr * g).sum().backward()
+    for name, a, r in zip(('d voxels', 'd weight', 'd bias'), leaves, refs):
+        gclose(a.grad, r.grad, f'bf16 K3C {name} (config {config})', rel=2e-2)
+
+
 # ------------------------------------------------------------------------------------ K2C
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize('shape', [(1, 5140, 102, 102, 2),     # config 2 pose: (C+1)*Z, padded 100x100 BEV
@@ -630,6 +696,48 @@ def test_pad_conv_matches_conv(shape):
     (y_ref * g).sum().backward()
     for name, a, r in zip(('d input', 'd weight', 'd bias'), leaves, refs):
         gclose(a.grad, r.grad, f'K2C {name} {shape}')
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize('shape', [(2, 5140, 102, 102, 2, (257, 20)),   # config 3 pose: B=2, reference-order weight
+                                   (2, 20, 13, 11, 2, None),           # odd sizes, partial channel chunk
+                                   (1, 44, 9, 30, 1, None)])           # stride 1
+def test_pad_conv_bf16(shape):
+    """K2C's bf16 form (config 3) against F.conv2d in fp32 on the bf16-rounded map and weight (+ bias,
+    LeakyReLU, the next conv's reflect pad): equal up to fp32 summation order and the final bf16
+    rounding; gradients track the fp32 K2C's within bf16 precision (volumetric_fusionnet.py:59-60,
+    338-343).  With `perm` the weight is in the reference channel order c*Z + z."""
+    from vfdepth_amd import kernels as KN
+    B, C, H, W, s, perm = shape
+    gen = torch.Generator(device=DEV).manual_seed(181)
+    x = torch.randn(B, C, H, W, device=DEV, generator=gen).contiguous(memory_format=torch.channels_last)
+    w = torch.randn(256, C, 3, 3, device=DEV, generator=gen) * (C * 9) ** -0.5
+    b = 0.1 * torch.randn(256, device=DEV, generator=gen)
+    assert KN.pad_conv_bf16_supported(x, s, 256)
+    leaves = [t.clone().requires_grad_(True) for t in (x, w, b)]
+    y = KN.PadConvBF16.apply(leaves[0], leaves[1], leaves[2], s, None, perm)
+    assert y.dtype == torch.bfloat16
+    wm = KN.pose_conv_weight(w, *perm) if perm else w            # the map's channel order
+    with torch.no_grad():
+        pre = F.conv2d(x.to(torch.bfloat16).float(), wm.to(torch.bfloat16).float(), b, stride=s)
+        ref = F.pad(F.leaky_relu(pre, 0.1), (1, 1, 1, 1), mode='reflect')
+        err = (y.float() - ref).abs()
+        bound = 2.0 ** -8 * ref.abs() + 1e-4 * float(ref.abs().max())
+        assert bool((err <= bound).all()), f'bf16 K2C {shape}: max err {float(err.max()):.3g}'
+    # gradients: fp32 on the bf16-rounded operands (straight through) with the kernel's own
+    # LeakyReLU decisions (see test_proj_conv_bf16)
+    g = torch.randn(y.shape, device=DEV, generator=gen)
+    (y.float() * g).sum().backward()
+    refs = [t.clone().requires_grad_(True) for t in (x, w, b)]
+    xr = refs[0] + (refs[0].to(torch.bfloat16).float() - refs[0]).detach()
+    wmr = KN.pose_conv_weight(refs[1], *perm) if perm else refs[1]
+    wr = wmr + (wmr.to(torch.bfloat16).float() - wmr).detach()
+    pre = F.conv2d(xr, wr, refs[2], stride=s)
+    pos = y.detach()[:, :, 1:-1, 1:-1] > 0
+    yr = F.pad(torch.where(pos, pre, 0.1 * pre), (1, 1, 1, 1), mode='reflect')
+    (yr * g).sum().backward()
+    for name, a, r in zip(('d input', 'd weight', 'd bias'), leaves, refs):
+        gclose(a.grad, r.grad, f'bf16 K2C {name} {shape}', rel=2e-2)
 
 
 # ------------------------------------------------------------------------------------ fused BN
@@ -676,6 +784,90 @@ def test_batchnorm_act_matches_torch(shape, res, relu):
     gclose(bn.bias.grad, bn_ref.bias.grad, 'BN d beta', rel=1e-4)
     if res:
         gclose(ra.grad, rr.grad, 'BN d residual', rel=1e-6)
+
+
+@pytest.mark.parametrize('shape,res,relu', [((6, 64, 96, 160), True, True), ((6, 256, 24, 40), True, True),
+                                            ((6, 512, 12, 20), False, False), ((3, 8, 5, 7), True, True)])
+def test_batchnorm_act_bf16(shape, res, relu):
+    """The fused BN's bf16 activations (config 3: under bf16 autocast the convs hand it bf16 maps):
+    statistics in fp64 over the bf16 values, output rounded to bf16 once, fp32 parameters and
+    running statistics; against nn.BatchNorm2d.train() in fp32 on the same (bf16-valued) inputs:
+    outputs within one bf16 rounding, running stats and gradients at fp32 / bf16-rounding level."""
+    import copy
+    from vfdepth_amd.layers import bn_act
+    gen = torch.Generator(device=DEV).manual_seed(191)
+    x = (2.0 * torch.randn(shape, device=DEV, generator=gen) + 0.5).to(torch.bfloat16)
+    r = torch.randn(shape, device=DEV, generator=gen).to(torch.bfloat16) if res else None
+    bn = torch.nn.BatchNorm2d(shape[1]).to(DEV).train()
+    with torch.no_grad():
+        bn.weight.copy_(1 + 0.1 * torch.randn(shape[1], device=DEV, generator=gen))
+        bn.bias.copy_(0.1 * torch.randn(shape[1], device=DEV, generator=gen))
+    bn_ref = copy.deepcopy(bn)
+    xa, xr = x.clone().requires_grad_(True), x.float().requires_grad_(True)
+    ra = r.clone().requires_grad_(True) if res else None
+    rr = r.float().requires_grad_(True) if res else None
+    with torch.autocast(device_type='cuda', dtype=torch.bfloat16):
+        y = bn_act(bn, xa, ra, relu)
+    assert y.dtype == torch.bfloat16 and 'BatchNormAct' in type(y.grad_fn).__name__
+    yr = bn_ref(xr)
+    if res:
+        yr = yr + rr
+    if relu:
+        yr = torch.relu(yr)
+    close(y.float(), yr, f'bf16 BN output {shape}', atol=1e-5, rtol=2.0 ** -8)
+    close(bn.running_mean, bn_ref.running_mean, 'running_mean', atol=1e-6, rtol=1e-5)
+    close(bn.running_var, bn_ref.running_var, 'running_var', atol=1e-6, rtol=1e-5)
+    g = torch.randn(shape, device=DEV, generator=gen).to(torch.bfloat16)
+    (y.float() * g.float()).sum().backward()
+    (yr * g.float()).sum().backward()
+    gclose(xa.grad.float(), xr.grad, f'bf16 BN d input {shape}', rel=2e-2)
+    gclose(bn.weight.grad, bn_ref.weight.grad, f'bf16 BN d gamma {shape}', rel=2e-2)
+    gclose(bn.bias.grad, bn_ref.bias.grad, f'bf16 BN d beta {shape}', rel=2e-2)
+    if res:
+        gclose(ra.grad.float(), rr.grad, f'bf16 BN d residual {shape}', rel=2e-2)
+
+
+def test_dense_maps_bf16():
+    """bf16 maps (config 3) through the reflect pad, the decoders' ELU + upsample + pad chain and the
+    stem max pool: forward bit-identical to ATen's bf16 ops (copies, fp32-computed ELU rounded once,
+    max selection), backward equal to the fp32 gather of the bf16 gradient rounded once."""
+    from vfdepth_amd import kernels as KN
+    gen = torch.Generator(device=DEV).manual_seed(193)
+    x = torch.randn(6, 16, 37, 53, device=DEV, generator=gen).to(torch.bfloat16).requires_grad_(True)
+    y = KN.ReflectPad1.apply(x)
+    assert y.dtype == torch.bfloat16 and torch.equal(y, F.pad(x.detach(), (1, 1, 1, 1), mode='reflect'))
+    g = torch.randn(y.shape, device=DEV, generator=gen).to(torch.bfloat16)
+    y.backward(g)
+    xr = x.detach().float().requires_grad_(True)
+    F.pad(xr, (1, 1, 1, 1), mode='reflect').backward(g.float())
+    assert torch.equal(x.grad, xr.grad.to(torch.bfloat16)), 'reflect pad bf16 backward'
+    for shape, up in (((6, 16, 48, 80), True), ((6, 32, 24, 40), False), ((2, 3, 5, 7), True)):
+        t = torch.randn(shape, device=DEV, generator=gen).to(torch.bfloat16).requires_grad_(True)
+        out = KN.EluUpPad.apply(t, up)
+        ref = F.elu(t.detach())
+        if up:
+            ref = F.interpolate(ref, scale_factor=2, mode='nearest')
+        ref = F.pad(ref, (1, 1, 1, 1), mode='reflect')
+        assert out.dtype == torch.bfloat16 and torch.equal(out, ref), f'elu_up_pad bf16 {shape}'
+        go = torch.randn(out.shape, device=DEV, generator=gen).to(torch.bfloat16)
+        out.backward(go)
+        tr = t.detach().float().requires_grad_(True)
+        rr = F.elu(tr)
+        if up:
+            rr = F.interpolate(rr, scale_factor=2, mode='nearest')
+        F.pad(rr, (1, 1, 1, 1), mode='reflect').backward(go.float())
+        close(t.grad.float(), tr.grad, f'elu_up_pad bf16 backward {shape}', atol=1e-6, rtol=2.0 ** -8)
+    for shape in ((6, 64, 192, 320), (3, 5, 37, 53)):
+        m = torch.relu(torch.randn(shape, device=DEV, generator=gen)).to(torch.bfloat16).requires_grad_(True)
+        ym = KN.MaxPool3s2.apply(m)
+        mr = m.detach().clone().requires_grad_(True)
+        yr = F.max_pool2d(mr, 3, 2, 1)
+        assert ym.dtype == torch.bfloat16 and torch.equal(ym, yr), f'maxpool bf16 {shape}'
+        gm = torch.randn(ym.shape, device=DEV, generator=gen).to(torch.bfloat16)
+        ym.backward(gm)
+        mf = m.detach().float().requires_grad_(True)
+        F.max_pool2d(mf, 3, 2, 1).backward(gm.float())
+        assert torch.equal(m.grad, mf.grad.to(torch.bfloat16)), f'maxpool bf16 backward {shape}'
 
 
 # ------------------------------------------------------------------------------------ pads / upsample

@@ -42,8 +42,8 @@ def main():
     g = torch.randn_like(y)
     dx = torch.empty_like(x)
     nb = x.numel() * 4 + y.numel() * 5
-    line('maxpool fwd (HIP)', timeit(lambda: lib.vfd_maxpool3s2_fwd(x.data_ptr(), y.data_ptr(), arg.data_ptr(), 384, 192, 320, L.stream())), nb)
-    line('maxpool bwd (HIP)', timeit(lambda: lib.vfd_maxpool3s2_bwd(g.data_ptr(), arg.data_ptr(), dx.data_ptr(), 384, 192, 320, L.stream())), nb)
+    line('maxpool fwd (HIP)', timeit(lambda: lib.vfd_maxpool3s2_fwd(x.data_ptr(), y.data_ptr(), arg.data_ptr(), 384, 192, 320, 0, L.stream())), nb)
+    line('maxpool bwd (HIP)', timeit(lambda: lib.vfd_maxpool3s2_bwd(g.data_ptr(), arg.data_ptr(), dx.data_ptr(), 384, 192, 320, 0, L.stream())), nb)
     yr, idx = F.max_pool2d(x, 3, 2, 1, return_indices=True)
     line('maxpool fwd (ATen)', timeit(lambda: F.max_pool2d(x, 3, 2, 1, return_indices=True)), x.numel() * 4 + y.numel() * 12)
     line('maxpool bwd (ATen)', timeit(lambda: torch.ops.aten.max_pool2d_with_indices_backward(g, x, [3, 3], [2, 2], [1, 1], [1, 1], False, idx)),
@@ -54,8 +54,8 @@ def main():
         n, c, h, w = shape
         tp = torch.empty(n, c, h + 2, w + 2, device=dev)
         nbp = (t.numel() + tp.numel()) * 4
-        line(f'reflect pad fwd {shape}', timeit(lambda: lib.vfd_reflect_pad1_fwd(t.data_ptr(), tp.data_ptr(), n * c, h, w, L.stream())), nbp)
-        line(f'reflect pad bwd {shape}', timeit(lambda: lib.vfd_reflect_pad1_bwd(tp.data_ptr(), t.data_ptr(), n * c, h, w, L.stream())), nbp)
+        line(f'reflect pad fwd {shape}', timeit(lambda: lib.vfd_reflect_pad1_fwd(t.data_ptr(), tp.data_ptr(), n * c, h, w, 0, L.stream())), nbp)
+        line(f'reflect pad bwd {shape}', timeit(lambda: lib.vfd_reflect_pad1_bwd(tp.data_ptr(), t.data_ptr(), n * c, h, w, 0, L.stream())), nbp)
     # decoder ELU [+ nearest 2x] + reflect pad (config-2 decoder shapes) vs the ATen chain
     for shape, up in (((6, 16, 192, 320), 1), ((6, 16, 384, 640), 0), ((6, 32, 96, 160), 1), ((6, 64, 48, 80), 1)):
         n, c, h, w = shape
@@ -63,8 +63,8 @@ def main():
         op = torch.empty(n, c, (h << up) + 2, (w << up) + 2, device=dev)
         dyy = torch.empty_like(yy)
         nbe = (yy.numel() + op.numel()) * 4
-        line(f'elu_up_pad fwd {shape} up={up}', timeit(lambda: lib.vfd_elu_up_pad1_fwd(yy.data_ptr(), op.data_ptr(), n * c, h, w, up, L.stream())), nbe)
-        line(f'elu_up_pad bwd {shape} up={up}', timeit(lambda: lib.vfd_elu_up_pad1_bwd(op.data_ptr(), yy.data_ptr(), dyy.data_ptr(), n * c, h, w, up, None, L.stream())), nbe + yy.numel() * 4)
+        line(f'elu_up_pad fwd {shape} up={up}', timeit(lambda: lib.vfd_elu_up_pad1_fwd(yy.data_ptr(), op.data_ptr(), n * c, h, w, up, 0, L.stream())), nbe)
+        line(f'elu_up_pad bwd {shape} up={up}', timeit(lambda: lib.vfd_elu_up_pad1_bwd(op.data_ptr(), yy.data_ptr(), dyy.data_ptr(), n * c, h, w, up, None, 0, L.stream())), nbe + yy.numel() * 4)
 
         def aten_chain():
             a = F.elu(yy)

@@ -48,7 +48,7 @@ class ConvDesc(ctypes.Structure):
 
 class BnDesc(ctypes.Structure):
     _fields_ = [('N', c_int), ('C', c_int), ('HW', c_int), ('S', c_int), ('relu', c_int),
-                ('eps', c_float), ('momentum', c_float)]
+                ('eps', c_float), ('momentum', c_float), ('dtype', c_int)]
 
 
 _SIGS = {
@@ -82,6 +82,7 @@ _SIGS = {
     'vfd_aggregate_fwd': (c_int, [c_int] * 4 + [c_fp, c_int, ctypes.POINTER(c_fp), ctypes.POINTER(c_int), c_fp, c_fp, c_void_p]),
     'vfd_proj_conv_fwd_workspace': (c_size_t, [ctypes.POINTER(VoxelDesc)]),
     'vfd_proj_conv_fwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 5 + [c_int, c_fp, c_fp, c_fp, c_size_t, c_void_p]),
+    'vfd_proj_conv_fwd_bf16': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 5 + [c_int, c_fp, c_fp, c_fp, c_size_t, c_void_p]),
     'vfd_proj_conv_dgrad_workspace': (c_size_t, [ctypes.POINTER(VoxelDesc)]),
     'vfd_proj_conv_dgrad': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 4 + [c_size_t, c_void_p]),
     'vfd_bn_splits': (c_int, [ctypes.POINTER(BnDesc)]),
@@ -92,13 +93,13 @@ _SIGS = {
     'vfd_bn_bwd_apply': (c_int, [ctypes.POINTER(BnDesc), c_fp, c_fp, c_fp, c_fp, c_int, c_double] + [c_fp] * 7
                          + [c_void_p]),
     'vfd_inverse4x4': (c_int, [c_fp, c_fp, c_int, c_void_p]),
-    'vfd_maxpool3s2_fwd': (c_int, [c_fp, c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_void_p]),
+    'vfd_maxpool3s2_fwd': (c_int, [c_fp, c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_int, c_void_p]),
     'vfd_normalize_cat': (c_int, [c_fp, c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_int, c_void_p]),
-    'vfd_maxpool3s2_bwd': (c_int, [c_fp, c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_void_p]),
+    'vfd_maxpool3s2_bwd': (c_int, [c_fp, c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_int, c_void_p]),
     'vfd_aggregate_bwd': (c_int, [c_int] * 4 + [c_fp, c_fp, c_fp, c_int, ctypes.POINTER(c_fp), ctypes.POINTER(c_int), c_fp, c_void_p]),
     'vfd_upsample_ac_bwd': (c_int, [c_fp, c_fp, c_fp, ctypes.c_longlong] + [c_int] * 4 + [c_void_p]),
-    'vfd_reflect_pad1_fwd': (c_int, [c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_void_p]),
-    'vfd_reflect_pad1_bwd': (c_int, [c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_void_p]),
+    'vfd_reflect_pad1_fwd': (c_int, [c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_int, c_void_p]),
+    'vfd_reflect_pad1_bwd': (c_int, [c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_int, c_void_p]),
     'vfd_bn1_fits': (c_int, [ctypes.POINTER(BnDesc)]),
     'vfd_bn1_fwd': (c_int, [ctypes.POINTER(BnDesc)] + [c_fp] * 11 + [c_void_p]),
     'vfd_bn1_bwd': (c_int, [ctypes.POINTER(BnDesc)] + [c_fp] * 10 + [c_void_p]),
@@ -111,14 +112,17 @@ _SIGS = {
     'vfd_dec_conv_fwd': (c_int, [c_fp] * 4 + [c_int] * 5 + [c_void_p]),
     'vfd_dec_conv_bwd': (c_int, [c_fp] * 5 + [c_int] * 5 + [c_void_p]),
     'vfd_weight_fragments': (c_int, [c_int, c_fp, c_fp] + [c_int] * 6 + [c_void_p]),
+    'vfd_weight_fragments_bf16': (c_int, [c_int, c_fp, c_fp] + [c_int] * 6 + [c_void_p]),
     'vfd_weight_swap': (c_int, [c_fp, c_fp, c_int, c_int, c_int, c_int, c_void_p]),
     'vfd_weight_permute': (c_int, [c_fp, c_fp] + [c_int] * 4 + [ctypes.POINTER(ctypes.c_longlong)] * 2 + [c_void_p]),
-    'vfd_elu_up_pad1_fwd': (c_int, [c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_int, c_void_p]),
-    'vfd_elu_up_pad1_bwd': (c_int, [c_fp, c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_int, c_fp, c_void_p]),
+    'vfd_elu_up_pad1_fwd': (c_int, [c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_int, c_int, c_void_p]),
+    'vfd_elu_up_pad1_bwd': (c_int, [c_fp, c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_int, c_fp, c_int, c_void_p]),
     'vfd_elu_up_pad1_bwd_blocks': (c_int, [c_int, c_int]),
     'vfd_lrelu_pad1_bwd_nhwc': (c_int, [c_fp, c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_int, c_float, c_void_p]),
     'vfd_pad_conv_fwd_workspace': (c_size_t, [ctypes.POINTER(ConvDesc)]),
     'vfd_pad_conv_fwd': (c_int, [ctypes.POINTER(ConvDesc)] + [c_fp] * 5 + [c_size_t, c_void_p]),
+    'vfd_pad_conv_fwd_bf16_workspace': (c_size_t, [ctypes.POINTER(ConvDesc)]),
+    'vfd_pad_conv_fwd_bf16': (c_int, [ctypes.POINTER(ConvDesc)] + [c_fp] * 5 + [c_size_t, c_void_p]),
     'vfd_depth_syn_fwd': (c_int, [ctypes.POINTER(DepthSynDesc)] + [c_fp] * 8 + [c_void_p]),
     'vfd_depth_syn_bwd': (c_int, [ctypes.POINTER(DepthSynDesc)] + [c_fp] * 9 + [c_void_p]),
     'vfd_smooth_workspace_bytes': (c_size_t, [c_int] * 4),

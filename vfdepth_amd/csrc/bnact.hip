@@ -62,7 +62,8 @@ __device__ __forceinline__ void bn_visit(const vfd_bn_desc& d, int c, BnRange r,
 
 // ReLU mask in the backward: from the forward output y (d.relu == 1) or from the forward's byte
 // mask (d.relu == 2: `y` then points at N*C*HW bytes, 1 = positive output) — a quarter of the bytes
-__device__ __forceinline__ void relu_mask4(const vfd_bn_desc& d, const float* __restrict__ y, size_t o, float4& gv) {
+template <typename T>
+__device__ __forceinline__ void relu_mask4(const vfd_bn_desc& d, const T* __restrict__ y, size_t o, float4& gv) {
   if (d.relu == 2) {
     const uchar4 m = *reinterpret_cast<const uchar4*>(reinterpret_cast<const unsigned char*>(y) + o);
     gv.x = m.x ? gv.x : 0.f;
@@ -70,7 +71,7 @@ __device__ __forceinline__ void relu_mask4(const vfd_bn_desc& d, const float* __
     gv.z = m.z ? gv.z : 0.f;
     gv.w = m.w ? gv.w : 0.f;
   } else {
-    const float4 yv = *reinterpret_cast<const float4*>(y + o);
+    const float4 yv = ld4(y + o);
     gv.x = yv.x > 0.f ? gv.x : 0.f;
     gv.y = yv.y > 0.f ? gv.y : 0.f;
     gv.z = yv.z > 0.f ? gv.z : 0.f;
@@ -78,24 +79,26 @@ __device__ __forceinline__ void relu_mask4(const vfd_bn_desc& d, const float* __
   }
 }
 
-__device__ __forceinline__ bool relu_on(const vfd_bn_desc& d, const float* __restrict__ y, size_t o) {
-  return d.relu == 2 ? reinterpret_cast<const unsigned char*>(y)[o] != 0 : y[o] > 0.f;
+template <typename T>
+__device__ __forceinline__ bool relu_on(const vfd_bn_desc& d, const T* __restrict__ y, size_t o) {
+  return d.relu == 2 ? reinterpret_cast<const unsigned char*>(y)[o] != 0 : ld1(y + o) > 0.f;
 }
 
 // partial[(c*S + split)*2 + {0,1}] = sum x, sum x^2 over the range
-__global__ __launch_bounds__(BN_THREADS) void bn_stats_k(vfd_bn_desc d, const float* __restrict__ x,
+template <typename T>
+__global__ __launch_bounds__(BN_THREADS) void bn_stats_k(vfd_bn_desc d, const T* __restrict__ x,
                                                          double* __restrict__ partial) {
   __shared__ double sh[BN_THREADS / 64];
   const int c = blockIdx.y, split = blockIdx.x;
   double s1 = 0.0, s2 = 0.0;
   bn_visit(d, c, bn_range(d, split), [&](size_t o, int n) {
     if (n == 4) {
-      const float4 v = *reinterpret_cast<const float4*>(x + o);
+      const float4 v = ld4(x + o);
       const double a = v.x, b = v.y, e = v.z, f = v.w;
       s1 += (a + b) + (e + f);
       s2 += (a * a + b * b) + (e * e + f * f);
     } else {
-      const double a = x[o];
+      const double a = ld1(x + o);
       s1 += a;
       s2 += a * a;
     }
@@ -146,10 +149,11 @@ __device__ __forceinline__ void bn_channel_sums(const double* __restrict__ part,
 
 // y = relu((x - mean) * invstd * gamma + beta [+ r]); block (0, c) also stores mean / invstd and
 // updates the running statistics (momentum, unbiased variance), as nn.BatchNorm2d.train() does.
-__global__ __launch_bounds__(BN_THREADS) void bn_apply_k(vfd_bn_desc d, const float* __restrict__ x,
-                                                         const float* __restrict__ r, const double* __restrict__ sums,
+template <typename T>
+__global__ __launch_bounds__(BN_THREADS) void bn_apply_k(vfd_bn_desc d, const T* __restrict__ x,
+                                                         const T* __restrict__ r, const double* __restrict__ sums,
                                                          int ns, double count, const float* __restrict__ gamma,
-                                                         const float* __restrict__ beta, float* __restrict__ y,
+                                                         const float* __restrict__ beta, T* __restrict__ y,
                                                          float* __restrict__ mean_out, float* __restrict__ invstd_out,
                                                          float* __restrict__ run_mean, float* __restrict__ run_var,
                                                          long long* __restrict__ nbt, unsigned char* __restrict__ mk) {
@@ -177,13 +181,13 @@ __global__ __launch_bounds__(BN_THREADS) void bn_apply_k(vfd_bn_desc d, const fl
   const bool relu = d.relu != 0;
   bn_visit(d, c, bn_range(d, split), [&](size_t o, int n) {
     if (n == 4) {
-      float4 v = *reinterpret_cast<const float4*>(x + o);
+      float4 v = ld4(x + o);
       v.x = v.x * sc + sh;
       v.y = v.y * sc + sh;
       v.z = v.z * sc + sh;
       v.w = v.w * sc + sh;
       if (r) {
-        const float4 q = *reinterpret_cast<const float4*>(r + o);
+        const float4 q = ld4(r + o);
         v.x += q.x;
         v.y += q.y;
         v.z += q.z;
@@ -195,21 +199,22 @@ __global__ __launch_bounds__(BN_THREADS) void bn_apply_k(vfd_bn_desc d, const fl
         v.z = fmaxf(v.z, 0.f);
         v.w = fmaxf(v.w, 0.f);
       }
-      *reinterpret_cast<float4*>(y + o) = v;
+      st4(y + o, v);
       if (mk) *reinterpret_cast<uchar4*>(mk + o) = make_uchar4(v.x > 0.f, v.y > 0.f, v.z > 0.f, v.w > 0.f);
     } else {
-      float v = x[o] * sc + sh;
-      if (r) v += r[o];
+      float v = ld1(x + o) * sc + sh;
+      if (r) v += ld1(r + o);
       if (relu) v = fmaxf(v, 0.f);
-      y[o] = v;
+      st1(y + o, v);
       if (mk) mk[o] = v > 0.f;
     }
   });
 }
 
 // backward statistics: sum g', sum g' * (x - mean), g' = g * [y > 0] (relu) or g
-__global__ __launch_bounds__(BN_THREADS) void bn_bwd_stats_k(vfd_bn_desc d, const float* __restrict__ g,
-                                                             const float* __restrict__ y, const float* __restrict__ x,
+template <typename T>
+__global__ __launch_bounds__(BN_THREADS) void bn_bwd_stats_k(vfd_bn_desc d, const T* __restrict__ g,
+                                                             const T* __restrict__ y, const T* __restrict__ x,
                                                              const float* __restrict__ mean_in,
                                                              double* __restrict__ partial) {
   __shared__ double sh[BN_THREADS / 64];
@@ -219,17 +224,17 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_stats_k(vfd_bn_desc d, cons
   double s1 = 0.0, s2 = 0.0;
   bn_visit(d, c, bn_range(d, split), [&](size_t o, int n) {
     if (n == 4) {
-      float4 gv = *reinterpret_cast<const float4*>(g + o);
-      const float4 xv = *reinterpret_cast<const float4*>(x + o);
+      float4 gv = ld4(g + o);
+      const float4 xv = ld4(x + o);
       if (relu) relu_mask4(d, y, o, gv);
       s1 += ((double)gv.x + (double)gv.y) + ((double)gv.z + (double)gv.w);
       s2 += ((double)gv.x * (double)(xv.x - mean) + (double)gv.y * (double)(xv.y - mean)) +
             ((double)gv.z * (double)(xv.z - mean) + (double)gv.w * (double)(xv.w - mean));
     } else {
-      float gv = g[o];
+      float gv = ld1(g + o);
       if (relu && !relu_on(d, y, o)) gv = 0.f;
       s1 += gv;
-      s2 += (double)gv * (double)(x[o] - mean);
+      s2 += (double)gv * (double)(ld1(x + o) - mean);
     }
   });
   s1 = block_sum(s1, sh);
@@ -242,13 +247,14 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_stats_k(vfd_bn_desc d, cons
 
 // dx = gamma * invstd * (g' - sum g'/n - (x - mean) * invstd^2 * sum g'(x - mean) / n); dr = g';
 // block (0, c) stores d gamma = invstd * sum g'(x - mean), d beta = sum g'
-__global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply_k(vfd_bn_desc d, const float* __restrict__ g,
-                                                             const float* __restrict__ y, const float* __restrict__ x,
+template <typename T>
+__global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply_k(vfd_bn_desc d, const T* __restrict__ g,
+                                                             const T* __restrict__ y, const T* __restrict__ x,
                                                              const double* __restrict__ sums, int ns, double count,
                                                              const float* __restrict__ gamma,
                                                              const float* __restrict__ mean_in,
                                                              const float* __restrict__ invstd_in,
-                                                             float* __restrict__ dx, float* __restrict__ dr,
+                                                             T* __restrict__ dx, T* __restrict__ dr,
                                                              float* __restrict__ dgamma, float* __restrict__ dbeta) {
   const int c = blockIdx.y, split = blockIdx.x;
   if (count <= 0.0) count = sums[2 * d.C];                          // all-reduced count row (ns == 1)
@@ -265,23 +271,23 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply_k(vfd_bn_desc d, cons
   const bool relu = d.relu != 0;
   bn_visit(d, c, bn_range(d, split), [&](size_t o, int n) {
     if (n == 4) {
-      float4 gv = *reinterpret_cast<const float4*>(g + o);
-      const float4 xv = *reinterpret_cast<const float4*>(x + o);
+      float4 gv = ld4(g + o);
+      const float4 xv = ld4(x + o);
       if (relu) relu_mask4(d, y, o, gv);
-      if (dr) *reinterpret_cast<float4*>(dr + o) = gv;
+      if (dr) st4(dr + o, gv);
       if (dx) {
         float4 o4;
         o4.x = k * (gv.x - mg - (xv.x - mean) * mx);
         o4.y = k * (gv.y - mg - (xv.y - mean) * mx);
         o4.z = k * (gv.z - mg - (xv.z - mean) * mx);
         o4.w = k * (gv.w - mg - (xv.w - mean) * mx);
-        *reinterpret_cast<float4*>(dx + o) = o4;
+        st4(dx + o, o4);
       }
     } else {
-      float gv = g[o];
+      float gv = ld1(g + o);
       if (relu && !relu_on(d, y, o)) gv = 0.f;
-      if (dr) dr[o] = gv;
-      if (dx) dx[o] = k * (gv - mg - (x[o] - mean) * mx);
+      if (dr) st1(dr + o, gv);
+      if (dx) st1(dx + o, k * (gv - mg - (ld1(x + o) - mean) * mx));
     }
   });
 }
@@ -315,9 +321,10 @@ __device__ __forceinline__ void bn1_visit(const vfd_bn_desc& d, int c, F&& f) {
   }
 }
 
-__global__ __launch_bounds__(BN1_THREADS) void bn1_fwd_k(vfd_bn_desc d, const float* __restrict__ x,
-                                                         const float* __restrict__ r, const float* __restrict__ gamma,
-                                                         const float* __restrict__ beta, float* __restrict__ y,
+template <typename T>
+__global__ __launch_bounds__(BN1_THREADS) void bn1_fwd_k(vfd_bn_desc d, const T* __restrict__ x,
+                                                         const T* __restrict__ r, const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta, T* __restrict__ y,
                                                          float* __restrict__ mean_out, float* __restrict__ invstd_out,
                                                          float* __restrict__ run_mean, float* __restrict__ run_var,
                                                          long long* __restrict__ nbt, unsigned char* __restrict__ mk) {
@@ -327,12 +334,12 @@ __global__ __launch_bounds__(BN1_THREADS) void bn1_fwd_k(vfd_bn_desc d, const fl
   double s1 = 0.0, s2 = 0.0;
   bn1_visit(d, c, [&](size_t o, int n) {
     if (n == 4) {
-      const float4 v = *reinterpret_cast<const float4*>(x + o);
+      const float4 v = ld4(x + o);
       const double a = v.x, b = v.y, e = v.z, f = v.w;
       s1 += (a + b) + (e + f);
       s2 += (a * a + b * b) + (e * e + f * f);
     } else {
-      const double a = x[o];
+      const double a = ld1(x + o);
       s1 += a;
       s2 += a * a;
     }
@@ -359,13 +366,13 @@ __global__ __launch_bounds__(BN1_THREADS) void bn1_fwd_k(vfd_bn_desc d, const fl
   const bool relu = d.relu != 0;
   bn1_visit(d, c, [&](size_t o, int n) {
     if (n == 4) {
-      float4 v = *reinterpret_cast<const float4*>(x + o);
+      float4 v = ld4(x + o);
       v.x = v.x * sc + shf;
       v.y = v.y * sc + shf;
       v.z = v.z * sc + shf;
       v.w = v.w * sc + shf;
       if (r) {
-        const float4 q = *reinterpret_cast<const float4*>(r + o);
+        const float4 q = ld4(r + o);
         v.x += q.x;
         v.y += q.y;
         v.z += q.z;
@@ -377,24 +384,25 @@ __global__ __launch_bounds__(BN1_THREADS) void bn1_fwd_k(vfd_bn_desc d, const fl
         v.z = fmaxf(v.z, 0.f);
         v.w = fmaxf(v.w, 0.f);
       }
-      *reinterpret_cast<float4*>(y + o) = v;
+      st4(y + o, v);
       if (mk) *reinterpret_cast<uchar4*>(mk + o) = make_uchar4(v.x > 0.f, v.y > 0.f, v.z > 0.f, v.w > 0.f);
     } else {
-      float v = x[o] * sc + shf;
-      if (r) v += r[o];
+      float v = ld1(x + o) * sc + shf;
+      if (r) v += ld1(r + o);
       if (relu) v = fmaxf(v, 0.f);
-      y[o] = v;
+      st1(y + o, v);
       if (mk) mk[o] = v > 0.f;
     }
   });
 }
 
-__global__ __launch_bounds__(BN1_THREADS) void bn1_bwd_k(vfd_bn_desc d, const float* __restrict__ g,
-                                                         const float* __restrict__ y, const float* __restrict__ x,
+template <typename T>
+__global__ __launch_bounds__(BN1_THREADS) void bn1_bwd_k(vfd_bn_desc d, const T* __restrict__ g,
+                                                         const T* __restrict__ y, const T* __restrict__ x,
                                                          const float* __restrict__ gamma,
                                                          const float* __restrict__ mean_in,
-                                                         const float* __restrict__ invstd_in, float* __restrict__ dx,
-                                                         float* __restrict__ dr, float* __restrict__ dgamma,
+                                                         const float* __restrict__ invstd_in, T* __restrict__ dx,
+                                                         T* __restrict__ dr, float* __restrict__ dgamma,
                                                          float* __restrict__ dbeta) {
   __shared__ double sh[BN1_THREADS / 64];
   const int c = blockIdx.x;
@@ -403,17 +411,17 @@ __global__ __launch_bounds__(BN1_THREADS) void bn1_bwd_k(vfd_bn_desc d, const fl
   double s1 = 0.0, s2 = 0.0;
   bn1_visit(d, c, [&](size_t o, int n) {
     if (n == 4) {
-      float4 gv = *reinterpret_cast<const float4*>(g + o);
-      const float4 xv = *reinterpret_cast<const float4*>(x + o);
+      float4 gv = ld4(g + o);
+      const float4 xv = ld4(x + o);
       if (relu) relu_mask4(d, y, o, gv);
       s1 += ((double)gv.x + (double)gv.y) + ((double)gv.z + (double)gv.w);
       s2 += ((double)gv.x * (double)(xv.x - mean) + (double)gv.y * (double)(xv.y - mean)) +
             ((double)gv.z * (double)(xv.z - mean) + (double)gv.w * (double)(xv.w - mean));
     } else {
-      float gv = g[o];
+      float gv = ld1(g + o);
       if (relu && !relu_on(d, y, o)) gv = 0.f;
       s1 += gv;
-      s2 += (double)gv * (double)(x[o] - mean);
+      s2 += (double)gv * (double)(ld1(x + o) - mean);
     }
   });
   const double sg = block_sum1(s1, sh), sgx = block_sum1(s2, sh);
@@ -427,23 +435,23 @@ __global__ __launch_bounds__(BN1_THREADS) void bn1_bwd_k(vfd_bn_desc d, const fl
   const float mx = (float)(sgx / count) * invstd * invstd;
   bn1_visit(d, c, [&](size_t o, int n) {
     if (n == 4) {
-      float4 gv = *reinterpret_cast<const float4*>(g + o);
-      const float4 xv = *reinterpret_cast<const float4*>(x + o);
+      float4 gv = ld4(g + o);
+      const float4 xv = ld4(x + o);
       if (relu) relu_mask4(d, y, o, gv);
-      if (dr) *reinterpret_cast<float4*>(dr + o) = gv;
+      if (dr) st4(dr + o, gv);
       if (dx) {
         float4 o4;
         o4.x = k * (gv.x - mg - (xv.x - mean) * mx);
         o4.y = k * (gv.y - mg - (xv.y - mean) * mx);
         o4.z = k * (gv.z - mg - (xv.z - mean) * mx);
         o4.w = k * (gv.w - mg - (xv.w - mean) * mx);
-        *reinterpret_cast<float4*>(dx + o) = o4;
+        st4(dx + o, o4);
       }
     } else {
-      float gv = g[o];
+      float gv = ld1(g + o);
       if (relu && !relu_on(d, y, o)) gv = 0.f;
-      if (dr) dr[o] = gv;
-      if (dx) dx[o] = k * (gv - mg - (x[o] - mean) * mx);
+      if (dr) st1(dr + o, gv);
+      if (dx) st1(dx + o, k * (gv - mg - (ld1(x + o) - mean) * mx));
     }
   });
 }
@@ -472,12 +480,13 @@ static int bn_check(const vfd_bn_desc* d, const char* what) {
   return VFD_OK;
 }
 
-int vfd_bn_fwd_stats(const vfd_bn_desc* d, const float* x, double* partial, void* stream) {
+int vfd_bn_fwd_stats(const vfd_bn_desc* d, const void* x, double* partial, void* stream) {
   if (int e = bn_check(d, "bn_fwd_stats")) return e;
   VFD_REQUIRE(x && partial, "bn_fwd_stats: null argument");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_BN_FWD, s);
-  bn_stats_k<<<dim3(d->S, d->C), BN_THREADS, 0, s>>>(*d, x, partial);
+  if (d->dtype == 1) bn_stats_k<__bf16><<<dim3(d->S, d->C), BN_THREADS, 0, s>>>(*d, (const __bf16*)x, partial);
+  else bn_stats_k<float><<<dim3(d->S, d->C), BN_THREADS, 0, s>>>(*d, (const float*)x, partial);
   return fail_launch("bn_fwd_stats");
 }
 
@@ -491,8 +500,8 @@ int vfd_bn_sum(const vfd_bn_desc* d, const double* partial, double count, double
   return fail_launch("bn_sum");
 }
 
-int vfd_bn_fwd_apply(const vfd_bn_desc* d, const float* x, const float* residual, const double* sums, int ns,
-                     double count, const float* gamma, const float* beta, float* y, float* mean, float* invstd,
+int vfd_bn_fwd_apply(const vfd_bn_desc* d, const void* x, const void* residual, const double* sums, int ns,
+                     double count, const float* gamma, const float* beta, void* y, float* mean, float* invstd,
                      float* running_mean, float* running_var, long long* num_batches_tracked,
                      unsigned char* relu_mask, void* stream) {
   if (int e = bn_check(d, "bn_fwd_apply")) return e;
@@ -502,33 +511,51 @@ int vfd_bn_fwd_apply(const vfd_bn_desc* d, const float* x, const float* residual
   VFD_REQUIRE(!running_mean == !running_var, "bn_fwd_apply: running mean / var must come together");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_BN_FWD, s);
-  bn_apply_k<<<dim3(d->S, d->C), BN_THREADS, 0, s>>>(*d, x, residual, sums, ns, count, gamma, beta, y, mean, invstd,
-                                                     running_mean, running_var, num_batches_tracked,
-                                                     d->relu ? relu_mask : nullptr);
+  if (d->dtype == 1)
+    bn_apply_k<__bf16><<<dim3(d->S, d->C), BN_THREADS, 0, s>>>(*d, (const __bf16*)x, (const __bf16*)residual, sums, ns,
+                                                               count, gamma, beta, (__bf16*)y, mean, invstd, running_mean,
+                                                               running_var, num_batches_tracked,
+                                                               d->relu ? relu_mask : nullptr);
+  else
+    bn_apply_k<float><<<dim3(d->S, d->C), BN_THREADS, 0, s>>>(*d, (const float*)x, (const float*)residual, sums, ns,
+                                                              count, gamma, beta, (float*)y, mean, invstd, running_mean,
+                                                              running_var, num_batches_tracked,
+                                                              d->relu ? relu_mask : nullptr);
   return fail_launch("bn_fwd_apply");
 }
 
-int vfd_bn_bwd_stats(const vfd_bn_desc* d, const float* g, const float* y, const float* x, const float* mean,
+int vfd_bn_bwd_stats(const vfd_bn_desc* d, const void* g, const void* y, const void* x, const float* mean,
                      double* partial, void* stream) {
   if (int e = bn_check(d, "bn_bwd_stats")) return e;
   VFD_REQUIRE(g && x && mean && partial && (y || !d->relu), "bn_bwd_stats: null argument");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_BN_BWD, s);
-  bn_bwd_stats_k<<<dim3(d->S, d->C), BN_THREADS, 0, s>>>(*d, g, y, x, mean, partial);
+  if (d->dtype == 1)
+    bn_bwd_stats_k<__bf16><<<dim3(d->S, d->C), BN_THREADS, 0, s>>>(*d, (const __bf16*)g, (const __bf16*)y,
+                                                                   (const __bf16*)x, mean, partial);
+  else
+    bn_bwd_stats_k<float><<<dim3(d->S, d->C), BN_THREADS, 0, s>>>(*d, (const float*)g, (const float*)y,
+                                                                  (const float*)x, mean, partial);
   return fail_launch("bn_bwd_stats");
 }
 
-int vfd_bn_bwd_apply(const vfd_bn_desc* d, const float* g, const float* y, const float* x, const double* sums,
-                     int ns, double count, const float* gamma, const float* mean, const float* invstd, float* dx,
-                     float* dresidual, float* dgamma, float* dbeta, void* stream) {
+int vfd_bn_bwd_apply(const vfd_bn_desc* d, const void* g, const void* y, const void* x, const double* sums,
+                     int ns, double count, const float* gamma, const float* mean, const float* invstd, void* dx,
+                     void* dresidual, float* dgamma, float* dbeta, void* stream) {
   if (int e = bn_check(d, "bn_bwd_apply")) return e;
   VFD_REQUIRE(g && x && sums && gamma && mean && invstd && (y || !d->relu) && (ns == 1 || ns == d->S) &&
                   (count > 0.0 || ns == 1),
               "bn_bwd_apply: bad argument (count <= 0 reads the count row of reduced sums: ns must be 1)");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_BN_BWD, s);
-  bn_bwd_apply_k<<<dim3(d->S, d->C), BN_THREADS, 0, s>>>(*d, g, y, x, sums, ns, count, gamma, mean, invstd, dx,
-                                                         dresidual, dgamma, dbeta);
+  if (d->dtype == 1)
+    bn_bwd_apply_k<__bf16><<<dim3(d->S, d->C), BN_THREADS, 0, s>>>(*d, (const __bf16*)g, (const __bf16*)y,
+                                                                   (const __bf16*)x, sums, ns, count, gamma, mean, invstd,
+                                                                   (__bf16*)dx, (__bf16*)dresidual, dgamma, dbeta);
+  else
+    bn_bwd_apply_k<float><<<dim3(d->S, d->C), BN_THREADS, 0, s>>>(*d, (const float*)g, (const float*)y,
+                                                                  (const float*)x, sums, ns, count, gamma, mean, invstd,
+                                                                  (float*)dx, (float*)dresidual, dgamma, dbeta);
   return fail_launch("bn_bwd_apply");
 }
 
@@ -536,26 +563,37 @@ int vfd_bn1_fits(const vfd_bn_desc* d) {
   return d && d->N > 0 && d->C > 0 && d->HW > 0 && (long long)d->N * d->HW <= (long long)BN1_MAX ? 1 : 0;
 }
 
-int vfd_bn1_fwd(const vfd_bn_desc* d, const float* x, const float* residual, const float* gamma, const float* beta,
-                float* y, float* mean, float* invstd, float* running_mean, float* running_var,
+int vfd_bn1_fwd(const vfd_bn_desc* d, const void* x, const void* residual, const float* gamma, const float* beta,
+                void* y, float* mean, float* invstd, float* running_mean, float* running_var,
                 long long* num_batches_tracked, unsigned char* relu_mask, void* stream) {
   VFD_REQUIRE(vfd_bn1_fits(d), "bn1_fwd: channel larger than %u elements", BN1_MAX);
   VFD_REQUIRE(x && gamma && beta && y && mean && invstd && !running_mean == !running_var, "bn1_fwd: bad argument");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_BN_FWD, s);
-  bn1_fwd_k<<<d->C, BN1_THREADS, 0, s>>>(*d, x, residual, gamma, beta, y, mean, invstd, running_mean, running_var,
-                                         num_batches_tracked, d->relu ? relu_mask : nullptr);
+  if (d->dtype == 1)
+    bn1_fwd_k<__bf16><<<d->C, BN1_THREADS, 0, s>>>(*d, (const __bf16*)x, (const __bf16*)residual, gamma, beta,
+                                                   (__bf16*)y, mean, invstd, running_mean, running_var,
+                                                   num_batches_tracked, d->relu ? relu_mask : nullptr);
+  else
+    bn1_fwd_k<float><<<d->C, BN1_THREADS, 0, s>>>(*d, (const float*)x, (const float*)residual, gamma, beta, (float*)y,
+                                                  mean, invstd, running_mean, running_var, num_batches_tracked,
+                                                  d->relu ? relu_mask : nullptr);
   return fail_launch("bn1_fwd");
 }
 
-int vfd_bn1_bwd(const vfd_bn_desc* d, const float* g, const float* y, const float* x, const float* gamma,
-                const float* mean, const float* invstd, float* dx, float* dresidual, float* dgamma, float* dbeta,
+int vfd_bn1_bwd(const vfd_bn_desc* d, const void* g, const void* y, const void* x, const float* gamma,
+                const float* mean, const float* invstd, void* dx, void* dresidual, float* dgamma, float* dbeta,
                 void* stream) {
   VFD_REQUIRE(vfd_bn1_fits(d), "bn1_bwd: channel larger than %u elements", BN1_MAX);
   VFD_REQUIRE(g && x && gamma && mean && invstd && (y || !d->relu), "bn1_bwd: bad argument");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_BN_BWD, s);
-  bn1_bwd_k<<<d->C, BN1_THREADS, 0, s>>>(*d, g, y, x, gamma, mean, invstd, dx, dresidual, dgamma, dbeta);
+  if (d->dtype == 1)
+    bn1_bwd_k<__bf16><<<d->C, BN1_THREADS, 0, s>>>(*d, (const __bf16*)g, (const __bf16*)y, (const __bf16*)x, gamma,
+                                                   mean, invstd, (__bf16*)dx, (__bf16*)dresidual, dgamma, dbeta);
+  else
+    bn1_bwd_k<float><<<d->C, BN1_THREADS, 0, s>>>(*d, (const float*)g, (const float*)y, (const float*)x, gamma, mean,
+                                                  invstd, (float*)dx, (float*)dresidual, dgamma, dbeta);
   return fail_launch("bn1_bwd");
 }
 

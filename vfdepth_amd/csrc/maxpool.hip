@@ -1,5 +1,6 @@
 // MaxPool2d(3, stride 2, padding 1) of the ResNet stem (torchvision / packnet ResnetEncoder,
-// fusion_depthnet.py:24-36, fusion_posenet.py:22-35), NCHW fp32, forward and backward.
+// fusion_depthnet.py:24-36, fusion_posenet.py:22-35), NCHW fp32 or bf16 (config 3's autocast;
+// compared and summed in fp32), forward and backward.
 // The forward keeps the winning window position as one byte (ATen stores an int64 index: 8x the
 // bytes); ties go to the first maximum in window scan order and NaN wins, as ATen's `val > max ||
 // isnan(val)` does.  The backward is a gather: every input pixel sums the gradients of the (<= 4)
@@ -8,7 +9,8 @@
 
 namespace vfd {
 
-__global__ __launch_bounds__(256) void maxpool_fwd_k(const float* __restrict__ x, float* __restrict__ y,
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool_fwd_k(const T* __restrict__ x, T* __restrict__ y,
                                                      uint8_t* __restrict__ arg, long long planes, int h, int w,
                                                      int ho, int wo) {
   // grid (cdiv(ho*wo, 256), planes): 32-bit index math inside a plane (64-bit division is a
@@ -18,12 +20,12 @@ __global__ __launch_bounds__(256) void maxpool_fwd_k(const float* __restrict__ x
   const int oy = j / wo, ox = j - oy * wo;
   for (long long p = blockIdx.y; p < planes; p += gridDim.y) {
     const size_t i = (size_t)p * ho * wo + j;
-    const float* xp = x + (size_t)p * h * w;
+    const T* xp = x + (size_t)p * h * w;
     float v[9];
 #pragma unroll
     for (int k = 0; k < 9; ++k) {                    // unconditional loads at clamped taps
       const int yy = min(max(2 * oy - 1 + k / 3, 0), h - 1), xx = min(max(2 * ox - 1 + k % 3, 0), w - 1);
-      v[k] = xp[yy * w + xx];
+      v[k] = ld1(xp + yy * w + xx);
     }
     float best = -INFINITY;
     int bi = 4;                                      // centre (always inside the image)
@@ -38,7 +40,7 @@ __global__ __launch_bounds__(256) void maxpool_fwd_k(const float* __restrict__ x
         first = false;
       }
     }
-    y[i] = best;
+    st1(y + i, best);
     arg[i] = (uint8_t)bi;
   }
 }
@@ -46,7 +48,8 @@ __global__ __launch_bounds__(256) void maxpool_fwd_k(const float* __restrict__ x
 // Four consecutive outputs per thread (wo % 4 == 0, w == 2 wo): each of the 3 window rows is one
 // scalar (column 2 ox0 - 1) and two 16-B loads (columns 2 ox0 .. 2 ox0 + 7), 9 load instructions
 // for 4 outputs instead of 36; the taps, their order and the selection are maxpool_fwd_k's.
-__global__ __launch_bounds__(256) void maxpool_fwd4_k(const float* __restrict__ x, float* __restrict__ y,
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool_fwd4_k(const T* __restrict__ x, T* __restrict__ y,
                                                       uint8_t* __restrict__ arg, long long planes, int h, int w,
                                                       int ho, int wo) {
   const int wq = wo / 4;
@@ -54,14 +57,14 @@ __global__ __launch_bounds__(256) void maxpool_fwd4_k(const float* __restrict__ 
   if (j >= ho * wq) return;
   const int oy = j / wq, ox0 = (j - oy * wq) * 4;
   for (long long p = blockIdx.y; p < planes; p += gridDim.y) {
-    const float* xp = x + (size_t)p * h * w;
+    const T* xp = x + (size_t)p * h * w;
     float r[3][9];
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky) {
-      const float* row = xp + min(max(2 * oy - 1 + ky, 0), h - 1) * w;
-      const float4 a = *reinterpret_cast<const float4*>(row + 2 * ox0);
-      const float4 b = *reinterpret_cast<const float4*>(row + 2 * ox0 + 4);
-      r[ky][0] = row[max(2 * ox0 - 1, 0)];
+      const T* row = xp + min(max(2 * oy - 1 + ky, 0), h - 1) * w;
+      const float4 a = ld4(row + 2 * ox0);
+      const float4 b = ld4(row + 2 * ox0 + 4);
+      r[ky][0] = ld1(row + max(2 * ox0 - 1, 0));
       r[ky][1] = a.x; r[ky][2] = a.y; r[ky][3] = a.z; r[ky][4] = a.w;
       r[ky][5] = b.x; r[ky][6] = b.y; r[ky][7] = b.z; r[ky][8] = b.w;
     }
@@ -89,7 +92,7 @@ __global__ __launch_bounds__(256) void maxpool_fwd4_k(const float* __restrict__ 
       code |= (unsigned)bi << (8 * e);
     }
     const size_t i = (size_t)p * ho * wo + (size_t)oy * wo + ox0;
-    *reinterpret_cast<float4*>(y + i) = make_float4(best4[0], best4[1], best4[2], best4[3]);
+    st4(y + i, make_float4(best4[0], best4[1], best4[2], best4[3]));
     *reinterpret_cast<unsigned*>(arg + i) = code;
   }
 }
@@ -98,8 +101,9 @@ __global__ __launch_bounds__(256) void maxpool_fwd4_k(const float* __restrict__ 
 // by the output windows (i, j), (i, j+1), (i+1, j), (i+1, j+1) only (pixel 2i sits in window i's
 // centre row, pixel 2i+1 in window i's last row and window i+1's first), so 4 gradient and 4 index
 // loads serve 4 pixels; each pixel sums its winning windows in ATen's (row, column) order.
-__global__ __launch_bounds__(256) void maxpool_bwd_k(const float* __restrict__ g, const uint8_t* __restrict__ arg,
-                                                     float* __restrict__ dx, long long planes, int h, int w, int ho,
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool_bwd_k(const T* __restrict__ g, const uint8_t* __restrict__ arg,
+                                                     T* __restrict__ dx, long long planes, int h, int w, int ho,
                                                      int wo) {
   const int hb = (h + 1) / 2, wb = (w + 1) / 2;
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -110,12 +114,12 @@ __global__ __launch_bounds__(256) void maxpool_bwd_k(const float* __restrict__ g
   const int y0 = 2 * bi, x0 = 2 * bj;
   const bool y1in = y0 + 1 < h, x1in = x0 + 1 < w;
   for (long long p = blockIdx.y; p < planes; p += gridDim.y) {
-    const float* gp = g + (size_t)p * ho * wo;
+    const T* gp = g + (size_t)p * ho * wo;
     const uint8_t* ap = arg + (size_t)p * ho * wo;
     // unconditional loads at clamped offsets; windows past the edge get index 255 (never wins)
     const int o01 = c1 ? o + 1 : o, o10 = r1 ? o + wo : o, o11 = (r1 && c1) ? o + wo + 1 : o;
     const int l00 = ap[o], l01 = ap[o01], l10 = ap[o10], l11 = ap[o11];
-    const float g00 = gp[o], g01 = gp[o01], g10 = gp[o10], g11 = gp[o11];
+    const float g00 = ld1(gp + o), g01 = ld1(gp + o01), g10 = ld1(gp + o10), g11 = ld1(gp + o11);
     const int a00 = l00, a01 = c1 ? l01 : 255, a10 = r1 ? l10 : 255, a11 = (r1 && c1) ? l11 : 255;
     // window positions (ky * 3 + kx): pixel (2i, 2j) is (1,1) of (i,j); (2i, 2j+1) is (1,2) of
     // (i,j) and (1,0) of (i,j+1); (2i+1, 2j) is (2,1) of (i,j) and (0,1) of (i+1,j); (2i+1, 2j+1)
@@ -130,12 +134,12 @@ __global__ __launch_bounds__(256) void maxpool_bwd_k(const float* __restrict__ g
     if (a01 == 6) d11 += g01;
     if (a10 == 2) d11 += g10;
     if (a11 == 0) d11 += g11;
-    float* dp = dx + (size_t)p * h * w + (size_t)y0 * w + x0;
-    dp[0] = d00;
-    if (x1in) dp[1] = d01;
+    T* dp = dx + (size_t)p * h * w + (size_t)y0 * w + x0;
+    st1(dp, d00);
+    if (x1in) st1(dp + 1, d01);
     if (y1in) {
-      dp[w] = d10;
-      if (x1in) dp[w + 1] = d11;
+      st1(dp + w, d10);
+      if (x1in) st1(dp + w + 1, d11);
     }
   }
 }
@@ -162,32 +166,44 @@ __global__ __launch_bounds__(256) void norm_cat_k(const float4* __restrict__ a, 
 
 }  // namespace vfd
 
-extern "C" {
-
-int vfd_maxpool3s2_fwd(const float* x, float* y, uint8_t* arg, long long planes, int h, int w, void* stream) {
-  VFD_REQUIRE(x && y && arg && planes > 0 && h > 0 && w > 0 && (long long)h * w < (1LL << 31),
-              "maxpool3s2: bad arguments");
-  hipStream_t s = (hipStream_t)stream;
-  vfd::ProfScope ps(vfd::K_MAXPOOL, s);
+template <typename T>
+static int maxpool_fwd_launch(const T* x, T* y, uint8_t* arg, long long planes, int h, int w, hipStream_t s) {
   const int ho = (h - 1) / 2 + 1, wo = (w - 1) / 2 + 1;
   const unsigned gy = (unsigned)(planes < 65535 ? planes : 65535);
-  if (wo % 4 == 0 && w == 2 * wo && (((uintptr_t)x | (uintptr_t)y) & 15) == 0 && ((uintptr_t)arg & 3) == 0) {
-    vfd::maxpool_fwd4_k<<<dim3((unsigned)((ho * (wo / 4) + 255) / 256), gy), 256, 0, s>>>(x, y, arg, planes, h, w, ho, wo);
-    return vfd::fail_launch("maxpool3s2_fwd");
+  const uintptr_t al = 4 * sizeof(T) - 1;
+  if (wo % 4 == 0 && w == 2 * wo && (((uintptr_t)x | (uintptr_t)y) & al) == 0 && ((uintptr_t)arg & 3) == 0) {
+    vfd::maxpool_fwd4_k<T><<<dim3((unsigned)((ho * (wo / 4) + 255) / 256), gy), 256, 0, s>>>(x, y, arg, planes, h, w, ho, wo);
+  } else {
+    vfd::maxpool_fwd_k<T><<<dim3((unsigned)((ho * wo + 255) / 256), gy), 256, 0, s>>>(x, y, arg, planes, h, w, ho, wo);
   }
-  vfd::maxpool_fwd_k<<<dim3((unsigned)((ho * wo + 255) / 256), gy), 256, 0, s>>>(x, y, arg, planes, h, w, ho, wo);
   return vfd::fail_launch("maxpool3s2_fwd");
 }
 
-int vfd_maxpool3s2_bwd(const float* g, const uint8_t* arg, float* dx, long long planes, int h, int w, void* stream) {
-  VFD_REQUIRE(g && arg && dx && planes > 0 && h > 0 && w > 0 && (long long)h * w < (1LL << 31),
+extern "C" {
+
+int vfd_maxpool3s2_fwd(const void* x, void* y, uint8_t* arg, long long planes, int h, int w, int dtype, void* stream) {
+  VFD_REQUIRE(x && y && arg && planes > 0 && h > 0 && w > 0 && (long long)h * w < (1LL << 31) && (dtype == 0 || dtype == 1),
+              "maxpool3s2: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  vfd::ProfScope ps(vfd::K_MAXPOOL, s);
+  if (dtype == 1) return maxpool_fwd_launch((const __bf16*)x, (__bf16*)y, arg, planes, h, w, s);
+  return maxpool_fwd_launch((const float*)x, (float*)y, arg, planes, h, w, s);
+}
+
+int vfd_maxpool3s2_bwd(const void* g, const uint8_t* arg, void* dx, long long planes, int h, int w, int dtype,
+                       void* stream) {
+  VFD_REQUIRE(g && arg && dx && planes > 0 && h > 0 && w > 0 && (long long)h * w < (1LL << 31) && (dtype == 0 || dtype == 1),
               "maxpool3s2: bad arguments");
   hipStream_t s = (hipStream_t)stream;
   vfd::ProfScope ps(vfd::K_MAXPOOL, s);
   const int ho = (h - 1) / 2 + 1, wo = (w - 1) / 2 + 1;
   const unsigned gy = (unsigned)(planes < 65535 ? planes : 65535);
   const int nblk2 = ((h + 1) / 2) * ((w + 1) / 2);
-  vfd::maxpool_bwd_k<<<dim3((unsigned)((nblk2 + 255) / 256), gy), 256, 0, s>>>(g, arg, dx, planes, h, w, ho, wo);
+  const dim3 grid((unsigned)((nblk2 + 255) / 256), gy);
+  if (dtype == 1)
+    vfd::maxpool_bwd_k<__bf16><<<grid, 256, 0, s>>>((const __bf16*)g, arg, (__bf16*)dx, planes, h, w, ho, wo);
+  else
+    vfd::maxpool_bwd_k<float><<<grid, 256, 0, s>>>((const float*)g, arg, (float*)dx, planes, h, w, ho, wo);
   return vfd::fail_launch("maxpool3s2_bwd");
 }
 

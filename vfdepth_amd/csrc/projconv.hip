@@ -89,10 +89,26 @@ struct PcTri {
   float w[8];
 };
 
-__device__ __forceinline__ void pc_gather(const vfd_voxel_desc& d, float* __restrict__ xs, PcTri* __restrict__ tw,
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// one (position, channel quad) sample into a row of T: fp32 (float4, 16 B) or bf16 (8 B, the
+// fp32 trilinear sum rounded to nearest even, as torch's .to(bfloat16) of K3's fp32 output)
+__device__ __forceinline__ void pc_put(float* dst, float4 v) { *reinterpret_cast<float4*>(dst) = v; }
+__device__ __forceinline__ void pc_put(__bf16* dst, float4 v) {
+  bf16x4 b;
+  b[0] = (__bf16)v.x;
+  b[1] = (__bf16)v.y;
+  b[2] = (__bf16)v.z;
+  b[3] = (__bf16)v.w;
+  *reinterpret_cast<bf16x4*>(dst) = b;
+}
+
+template <typename T, int XS>
+__device__ __forceinline__ void pc_gather(const vfd_voxel_desc& d, T* __restrict__ xs, PcTri* __restrict__ tw,
                                           const float* __restrict__ vox_b, const float* __restrict__ iK,
                                           const float* __restrict__ E, int y0, int x0, int di, int gw,
-                                          float* __restrict__ xo) {
+                                          T* __restrict__ xo) {
   const int lane = threadIdx.x & 63;
   // (1) the wave's positions p = gw*4 + (k & 3) + 16*(k >> 2): lane k evaluates slot k's trilinear
   //     cell once (wave-private LDS slice, no workgroup barrier)
@@ -113,7 +129,7 @@ __device__ __forceinline__ void pc_gather(const vfd_voxel_desc& d, float* __rest
   // (2) lanes = (position, channel quad): 16 quads per 64-channel row, 4 positions per instruction
   const int q = lane & 15, sub = lane >> 4;
   const float4* vb = reinterpret_cast<const float4*>(vox_b) + q;
-  const int ho = d.h + 2, wo = d.w + 2;
+  const int wo = d.w + 2;
   for (int it = 0; it < PC_GPOS / 4; ++it) {
     const int p = gw * 4 + sub + 16 * it;
     if (p >= PC_NPOS) break;
@@ -135,7 +151,7 @@ __device__ __forceinline__ void pc_gather(const vfd_voxel_desc& d, float* __rest
       acc.z += v[k].z * w;
       acc.w += v[k].w * w;
     }
-    *reinterpret_cast<float4*>(&xs[p * PC_XS + 4 * q]) = acc;
+    pc_put(&xs[p * XS + 4 * q], acc);
     if (xo) {
       const int hr = p / PC_HC, hc = p - hr * PC_HC;
       const int py = y0 + hr - 1, px = x0 + hc - 1;
@@ -144,12 +160,10 @@ __device__ __forceinline__ void pc_gather(const vfd_voxel_desc& d, float* __rest
         pad_sets(py, d.h, true, rows, &nr);
         pad_sets(px, d.w, true, cols, &nc);
         for (int r = 0; r < nr; ++r)
-          for (int c = 0; c < nc; ++c)
-            *reinterpret_cast<float4*>(xo + (((size_t)rows[r] * wo + cols[c]) * d.D + di) * PC_CV + 4 * q) = acc;
+          for (int c = 0; c < nc; ++c) pc_put(xo + (((size_t)rows[r] * wo + cols[c]) * d.D + di) * PC_CV + 4 * q, acc);
       }
     }
   }
-  (void)ho;
 }
 
 struct PcAtom {
@@ -190,8 +204,8 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pcv_main_k(vfd_voxel_desc d, Pc
   auto gather = [&](int atom, float* dst) {
     const PcAtom a = pc_atom(d, g, atom);
     float* xo = xout ? xout + (size_t)a.bc * (d.h + 2) * (d.w + 2) * d.D * PC_CV : nullptr;
-    pc_gather(d, dst, tri[wv - PC_WAVES], vox + (size_t)(a.bc / d.N) * V * PC_CV, invK + a.bc * 16,
-              E + a.bc * 16, a.y0, a.x0, a.di, wv - PC_WAVES, xo);
+    pc_gather<float, PC_XS>(d, dst, tri[wv - PC_WAVES], vox + (size_t)(a.bc / d.N) * V * PC_CV, invK + a.bc * 16,
+                            E + a.bc * 16, a.y0, a.x0, a.di, wv - PC_WAVES, xo);
   };
   if (!compute) gather(a_lo, xs[0]);
   __syncthreads();
@@ -298,12 +312,151 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pcv_main_k(vfd_voxel_desc d, Pc
       for (int r = 0; r < 16; ++r) dst[((a * 2 + b) * 16 + r) * 64 + lane] = acc[a][b][r];
 }
 
+// ---------------------------------------------------------------------------------------------
+// bf16 form (config 3's mixed precision: the reference autocasts the fusion features,
+// volumetric_fusionnet.py:105-114): the same atoms, gather waves and stream-K ranges, with the
+// halo samples rounded to bf16 in LDS and the MFMA on v_mfma_f32_32x32x16_bf16 (fp32
+// accumulation; 16x the fp32 rate).  K = 16 per instruction: one (tap, 16-channel chunk) step is
+// 8 MFMAs per compute wave (4 pixel blocks x 2 output blocks); lane (r, h) of a pixel block reads
+// the 8 channels 16q + 8h .. +7 of its halo position (one 16-B LDS read).  Weights: the fragment
+// copy `vfd_proj_conv_weight_bf16`: [D][9 taps][Cv/16][O/32 blocks][64 lanes][8], lane (r, h) of
+// block ob holding W[o = 32 ob + r][c = 16 q + 8 h + j] (rounded to nearest even).
+constexpr int PCB_XS = PC_CV + 8;               // bf16 per LDS row (144 B: 16-B aligned, staggered banks)
+constexpr int PCB_ITERS = 9 * (PC_CV / 16);     // (tap, 16-channel chunk) steps per atom
+#ifndef VFD_PCB_PF
+#define VFD_PCB_PF 2
+#endif
+constexpr int PCB_PF = VFD_PCB_PF;              // weight-fragment prefetch distance (steps; 4 spills)
+
+__global__ __launch_bounds__(PC_THREADS, 2) void pcvb_main_k(vfd_voxel_desc d, PcGeom g,
+                                                            const float* __restrict__ vox,
+                                                            const float* __restrict__ invK,
+                                                            const float* __restrict__ E,
+                                                            const bf16x8* __restrict__ Wq,
+                                                            float* __restrict__ partial,
+                                                            __bf16* __restrict__ xout) {
+  __shared__ __attribute__((aligned(16))) __bf16 xs[2][PC_NPOS * PCB_XS];
+  __shared__ PcTri tri[PC_WAVES][PC_GPOS];
+  const int grp = blockIdx.x;
+  const int a_lo = pc_lo(g, grp), a_hi = pc_lo(g, grp + 1);
+  if (a_lo >= a_hi) return;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int V = d.X * d.Y * d.Z;
+  const bool compute = wv < PC_WAVES;
+  auto gather = [&](int atom, __bf16* dst) {
+    const PcAtom a = pc_atom(d, g, atom);
+    __bf16* xo = xout ? xout + (size_t)a.bc * (d.h + 2) * (d.w + 2) * d.D * PC_CV : nullptr;
+    pc_gather<__bf16, PCB_XS>(d, dst, tri[wv - PC_WAVES], vox + (size_t)(a.bc / d.N) * V * PC_CV,
+                              invK + a.bc * 16, E + a.bc * 16, a.y0, a.x0, a.di, wv - PC_WAVES, xo);
+  };
+  if (!compute) gather(a_lo, xs[0]);
+  __syncthreads();
+  if (!compute) {
+    for (int atom = a_lo; atom < a_hi; ++atom) {
+      if (atom + 1 < a_hi) gather(atom + 1, xs[(atom + 1 - a_lo) & 1]);
+      __syncthreads();
+    }
+    return;
+  }
+  const int li = lane & 31, lh = lane >> 5;
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  // LDS offset of the lane's A row at tap (0, 0), + 8h; pixel block a adds 32 pixels = exactly
+  // two tile rows, a compile-time offset
+  const int aoff0 = ((li >> 4) * PC_HC + (li & 15)) * PCB_XS + 8 * lh;
+  constexpr int ABLK = 2 * PC_HC * PCB_XS;
+  // weight fragments of the flattened (atom, step) stream, PCB_PF steps ahead
+  // running pointer into the weight stream: one (tap, chunk) step = 8 blocks x 64 lanes; the next
+  // depth bin follows contiguously, except after the last bin (back to bin 0)
+  const bf16x8* wbase = Wq + (size_t)(2 * wv) * 64 + lane;
+  const bf16x8* wp = wbase + (size_t)(a_lo % d.D) * PCB_ITERS * (PC_O / 32) * 64;
+  const bf16x8* wend = wbase + (size_t)d.D * PCB_ITERS * (PC_O / 32) * 64;
+  bf16x8 bq[PCB_PF][2];
+  int pf_left = (a_hi - a_lo) * PCB_ITERS;         // steps still to prefetch
+  auto prefetch = [&](int slot) {
+    if (pf_left > 0) {
+      bq[slot][0] = wp[0];
+      bq[slot][1] = wp[64];
+      wp += (PC_O / 32) * 64;
+      if (wp == wend) wp = wbase;
+      --pf_left;
+    }
+  };
+#pragma unroll
+  for (int k = 0; k < PCB_PF; ++k) prefetch(k);
+  int slot = 0;
+  int tile = a_lo / d.D;
+  for (int atom = a_lo; atom < a_hi; ++atom) {
+    const int t = atom / d.D;
+    if (t != tile) {                                  // flush the finished tile's partial
+      float* dst = partial + ((size_t)grp * 2 + slot) * PC_FRAG + (size_t)wv * (PC_FRAG / PC_WAVES);
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            dst[((a * 2 + b) * 16 + r) * 64 + lane] = acc[a][b][r];
+            acc[a][b][r] = 0.f;
+          }
+      slot = 1;
+      tile = t;
+    }
+    const __bf16* xb = xs[(atom - a_lo) & 1];
+    // A fragments software-pipelined one step ahead (LDS latency off the MFMA path)
+    bf16x8 afc[4], afn[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) afc[a] = *reinterpret_cast<const bf16x8*>(&xb[aoff0 + a * ABLK]);
+#pragma unroll 1
+    for (int tap = 0; tap < 9; ++tap) {
+      const int ky = tap / 3, kx = tap - 3 * ky;
+      const __bf16* xt = xb + (ky * PC_HC + kx) * PCB_XS;
+      const int tn = tap + 1, kyn = tn / 3, kxn = tn - 3 * kyn;
+      const __bf16* xn = xb + (kyn * PC_HC + kxn) * PCB_XS;      // next tap (unused after tap 8)
+#pragma unroll
+      for (int q = 0; q < PC_CV / 16; ++q) {
+        const int ring = q % PCB_PF;                  // (PC_CV / 16) % PCB_PF == 0: static ring slots
+        const bf16x8 b0 = bq[ring][0], b1 = bq[ring][1];
+        prefetch(ring);
+        if (q < PC_CV / 16 - 1) {
+#pragma unroll
+          for (int a = 0; a < 4; ++a) afn[a] = *reinterpret_cast<const bf16x8*>(&xt[aoff0 + a * ABLK + 16 * (q + 1)]);
+        } else if (tap < 8) {
+#pragma unroll
+          for (int a = 0; a < 4; ++a) afn[a] = *reinterpret_cast<const bf16x8*>(&xn[aoff0 + a * ABLK]);
+        }
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          acc[a][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afc[a], b0, acc[a][0], 0, 0, 0);
+          acc[a][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afc[a], b1, acc[a][1], 0, 0, 0);
+        }
+#pragma unroll
+        for (int a = 0; a < 4; ++a) afc[a] = afn[a];
+      }
+    }
+    __syncthreads();                                  // buffer handed back to the gather waves
+  }
+  float* dst = partial + ((size_t)grp * 2 + slot) * PC_FRAG + (size_t)wv * (PC_FRAG / PC_WAVES);
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dst[((a * 2 + b) * 16 + r) * 64 + lane] = acc[a][b][r];
+}
+
 // Sum of each tile's partials (in workgroup order) + bias, LeakyReLU(0.1), stored into the
 // reflect-padded NHWC map out [B*N, h+2, w+2, O] (the input of reduce_dim's second conv).
 constexpr int PC_MAXC = 72;     // contributors of one tile (<= D + 1, D <= 64)
 constexpr int PC_FSL = 8;       // fragment slices per tile (grid.y of the reduce kernels)
+template <typename TO>
 __global__ __launch_bounds__(256) void pcv_reduce_k(vfd_voxel_desc d, PcGeom g, const float* __restrict__ partial,
-                                                    const float* __restrict__ bias, float* __restrict__ out) {
+                                                    const float* __restrict__ bias, TO* __restrict__ out) {
   __shared__ int contrib[PC_MAXC];
   __shared__ int ncontrib;
   const int t = blockIdx.x;
@@ -328,7 +481,7 @@ __global__ __launch_bounds__(256) void pcv_reduce_k(vfd_voxel_desc d, PcGeom g, 
   const int bc = t / g.tiles_img, ti = t - bc * g.tiles_img;
   const int y0 = (ti / g.tc) * PC_TR, x0 = (ti % g.tc) * PC_TC;
   const int ho = d.h + 2, wo = d.w + 2;
-  float* ob = out + (size_t)bc * ho * wo * PC_O;
+  TO* ob = out + (size_t)bc * ho * wo * PC_O;
   constexpr int FPS = 4 * 2 * 16 / PC_FSL;
   for (int f = blockIdx.y * FPS; f < (blockIdx.y + 1) * FPS; ++f) {
     const int a = f >> 5, bb = (f >> 4) & 1, r = f & 15;
@@ -347,7 +500,7 @@ __global__ __launch_bounds__(256) void pcv_reduce_k(vfd_voxel_desc d, PcGeom g, 
     pad_sets(py, d.h, true, rows, &nr);
     pad_sets(px, d.w, true, cols, &ncol);
     for (int i = 0; i < nr; ++i)
-      for (int j = 0; j < ncol; ++j) ob[((size_t)rows[i] * wo + cols[j]) * PC_O + o] = v;
+      for (int j = 0; j < ncol; ++j) ob[((size_t)rows[i] * wo + cols[j]) * PC_O + o] = (TO)v;
   }
 }
 
@@ -645,8 +798,28 @@ int vfd_proj_conv_fwd(const vfd_voxel_desc* d, const float* vox, const float* in
   const PcGeom g = pc_plan(*d);
   float* partial = (float*)ws;
   pcv_main_k<<<g.ngroup, PC_THREADS, 0, s>>>(*d, g, vox, invK, E, Wq, partial, x_out);
-  pcv_reduce_k<<<dim3(g.ntile, PC_FSL), 256, 0, s>>>(*d, g, partial, bias, out);
+  pcv_reduce_k<float><<<dim3(g.ntile, PC_FSL), 256, 0, s>>>(*d, g, partial, bias, out);
   return fail_launch("proj_conv_fwd");
+}
+
+// bf16 form: same workspace; vox / invK / E fp32, Wq = vfd_weight_fragments mode 3, bias fp32,
+// out / x_out bf16 (x_out optional: the frustum features for the weight gradient)
+int vfd_proj_conv_fwd_bf16(const vfd_voxel_desc* d, const float* vox, const float* invK, const float* E,
+                           const void* Wq, const float* bias, int out_channels, void* out, void* x_out, void* ws,
+                           size_t ws_bytes, void* stream) {
+  VFD_REQUIRE(d && vox && invK && E && Wq && bias && out, "proj_conv_fwd_bf16: null argument");
+  VFD_REQUIRE(d->Cv == PC_CV, "proj_conv_fwd_bf16: Cv must be %d (got %d)", PC_CV, d->Cv);
+  VFD_REQUIRE(out_channels == PC_O, "proj_conv_fwd_bf16: output channels must be %d (got %d)", PC_O, out_channels);
+  VFD_REQUIRE(d->B > 0 && d->N > 0 && d->h >= 2 && d->w >= 2 && d->D > 0 && d->D <= 64,
+              "proj_conv_fwd_bf16: bad shape (h, w >= 2, 0 < D <= 64)");
+  VFD_REQUIRE(ws && ws_bytes >= vfd_proj_conv_fwd_workspace(d), "proj_conv_fwd_bf16: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  ProfScope ps(K_PROJ_CONV_FWD, s);
+  const PcGeom g = pc_plan(*d);
+  float* partial = (float*)ws;
+  pcvb_main_k<<<g.ngroup, PC_THREADS, 0, s>>>(*d, g, vox, invK, E, (const bf16x8*)Wq, partial, (__bf16*)x_out);
+  pcv_reduce_k<__bf16><<<dim3(g.ntile, PC_FSL), 256, 0, s>>>(*d, g, partial, bias, (__bf16*)out);
+  return fail_launch("proj_conv_fwd_bf16");
 }
 
 size_t vfd_proj_conv_dgrad_workspace(const vfd_voxel_desc* d) {

@@ -1,5 +1,6 @@
 // Reflect padding by one pixel (nn.Conv2d(padding_mode='reflect', padding=1): the decoders'
-// 3x3 convs, network/blocks.py conv2d blocks) for NCHW fp32 maps, forward and backward, alone
+// 3x3 convs, network/blocks.py conv2d blocks) for NCHW fp32 or bf16 maps (config 3's autocast;
+// arithmetic in fp32, one rounding per output), forward and backward, alone
 // or fused with the ELU [+ nearest 2x upsample] in front of it (elu_up_pad_*: the plain pad is
 // the <UP = 0, ACT = false> instance).  The backward is a gather: every input pixel sums its
 // (up to four) padded copies in a fixed order, so it needs no atomics and is deterministic
@@ -57,8 +58,8 @@ __global__ __launch_bounds__(256) void lrelu_pad_bwd_nhwc_k(const float4* __rest
 constexpr int EPT = 4, PPT = 4;
 __device__ __forceinline__ float elu1(float v) { return v <= 0.f ? expm1f(v) : v; }
 
-template <int UP, bool ACT>
-__global__ __launch_bounds__(256) void elu_up_pad_fwd_k(const float* __restrict__ y, float* __restrict__ out,
+template <int UP, bool ACT, typename T>
+__global__ __launch_bounds__(256) void elu_up_pad_fwd_k(const T* __restrict__ y, T* __restrict__ out,
                                                         long long planes, int h, int w) {
   const int Hu = h << UP, Wu = w << UP;
   const int ho = Hu + 2, wo = Wu + 2, hwo = ho * wo;
@@ -77,17 +78,17 @@ __global__ __launch_bounds__(256) void elu_up_pad_fwd_k(const float* __restrict_
   for (int q = 0; q < PPT; ++q) {
     const long long p = p0 + q;
     if (p >= planes) break;
-    const float* yp = y + p * h * w;
+    const T* yp = y + p * h * w;
     float v[EPT];
 #pragma unroll
-    for (int e = 0; e < EPT; ++e) v[e] = ACT ? elu1(yp[src[e]]) : yp[src[e]];
-    float* op = out + p * hwo + j0;
+    for (int e = 0; e < EPT; ++e) v[e] = ACT ? elu1(ld1(yp + src[e])) : ld1(yp + src[e]);
+    T* op = out + p * hwo + j0;
     if (vec) {
-      *reinterpret_cast<float4*>(op) = make_float4(v[0], v[1], v[2], v[3]);
+      st4(op, make_float4(v[0], v[1], v[2], v[3]));
     } else {
 #pragma unroll
       for (int e = 0; e < EPT; ++e)
-        if (j0 + e < hwo) op[e] = v[e];
+        if (j0 + e < hwo) st1(op + e, v[e]);
     }
   }
 }
@@ -116,19 +117,19 @@ __device__ __forceinline__ EupIdx eup_idx(int s, int n) {
   return r;
 }
 
-template <int UP>
-__device__ __forceinline__ float eup_row(const float* __restrict__ gr, const EupIdx& C) {
-  float t = gr[C.a];
-  if (UP) t += gr[C.b];
-  if (C.fma != 0.f || C.fmb != 0.f) t = (t + C.fma * gr[C.ma]) + C.fmb * gr[C.mb];
+template <int UP, typename T>
+__device__ __forceinline__ float eup_row(const T* __restrict__ gr, const EupIdx& C) {
+  float t = ld1(gr + C.a);
+  if (UP) t += ld1(gr + C.b);
+  if (C.fma != 0.f || C.fmb != 0.f) t = (t + C.fma * ld1(gr + C.ma)) + C.fmb * ld1(gr + C.mb);
   return t;
 }
 
 // psum (optional): psum[p * gridDim.x + blockIdx.x] = the block's sum of dy over plane p (the
 // conv bias gradient's partials, summed in a fixed order by the caller: no ATen reduction pass)
-template <int UP, bool ACT>
-__global__ __launch_bounds__(256) void elu_up_pad_bwd_k(const float* __restrict__ g, const float* __restrict__ y,
-                                                        float* __restrict__ dy, long long planes, int h, int w,
+template <int UP, bool ACT, typename T>
+__global__ __launch_bounds__(256) void elu_up_pad_bwd_k(const T* __restrict__ g, const T* __restrict__ y,
+                                                        T* __restrict__ dy, long long planes, int h, int w,
                                                         float* __restrict__ psum) {
   __shared__ float red[256 / 64];
   const int Hu = h << UP, Wu = w << UP;
@@ -149,9 +150,9 @@ __global__ __launch_bounds__(256) void elu_up_pad_bwd_k(const float* __restrict_
   for (int q = 0; q < PPT; ++q) {
     const long long p = p0 + q;
     if (p >= planes) break;
-    const float* gp = g + p * (Hu + 2) * wo;
-    const float* ga = gp + (size_t)R.a * wo;
-    const float* gb = gp + (size_t)R.b * wo;
+    const T* gp = g + p * (Hu + 2) * wo;
+    const T* ga = gp + (size_t)R.a * wo;
+    const T* gb = gp + (size_t)R.b * wo;
     float s[EPT];
 #pragma unroll
     for (int e = 0; e < EPT; ++e) {
@@ -166,11 +167,11 @@ __global__ __launch_bounds__(256) void elu_up_pad_bwd_k(const float* __restrict_
     float v[EPT] = {};
     if (!ACT) {
     } else if (vec) {
-      const float4 t = *reinterpret_cast<const float4*>(y + o);
+      const float4 t = ld4(y + o);
       v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
     } else {
 #pragma unroll
-      for (int e = 0; e < EPT; ++e) v[e] = y[o + (sx0 + e < w ? e : 0)];
+      for (int e = 0; e < EPT; ++e) v[e] = ld1(y + o + (sx0 + e < w ? e : 0));
     }
     float r[EPT];
 #pragma unroll
@@ -180,11 +181,11 @@ __global__ __launch_bounds__(256) void elu_up_pad_bwd_k(const float* __restrict_
     }
     if (live) {
       if (vec) {
-        *reinterpret_cast<float4*>(dy + o) = make_float4(r[0], r[1], r[2], r[3]);
+        st4(dy + o, make_float4(r[0], r[1], r[2], r[3]));
       } else {
 #pragma unroll
         for (int e = 0; e < EPT; ++e)
-          if (sx0 + e < w) dy[o + e] = r[e];
+          if (sx0 + e < w) st1(dy + o + e, r[e]);
       }
     }
     if (psum) {                                              // block-uniform branch
@@ -206,25 +207,33 @@ using namespace vfd;
 
 extern "C" {
 
-int vfd_reflect_pad1_fwd(const float* x, float* y, long long planes, int h, int w, void* stream) {
-  VFD_REQUIRE(x && y && planes > 0 && h >= 2 && w >= 2 && (long long)(h + 2) * (w + 2) < (1LL << 31),
+int vfd_reflect_pad1_fwd(const void* x, void* y, long long planes, int h, int w, int dtype, void* stream) {
+  VFD_REQUIRE(x && y && planes > 0 && h >= 2 && w >= 2 && (long long)(h + 2) * (w + 2) < (1LL << 31) &&
+                  (dtype == 0 || dtype == 1),
               "reflect_pad1: bad arguments (h, w >= 2)");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_REFLECT_PAD, s);
   VFD_REQUIRE(planes / PPT < 65535, "reflect_pad1: too many planes");
   const dim3 grid((unsigned)(((h + 2) * (w + 2) + 256 * EPT - 1) / (256 * EPT)), (unsigned)((planes + PPT - 1) / PPT));
-  elu_up_pad_fwd_k<0, false><<<grid, 256, 0, s>>>(x, y, planes, h, w);
+  if (dtype == 1) elu_up_pad_fwd_k<0, false><<<grid, 256, 0, s>>>((const __bf16*)x, (__bf16*)y, planes, h, w);
+  else elu_up_pad_fwd_k<0, false><<<grid, 256, 0, s>>>((const float*)x, (float*)y, planes, h, w);
   return fail_launch("reflect_pad1_fwd");
 }
 
-int vfd_reflect_pad1_bwd(const float* g, float* dx, long long planes, int h, int w, void* stream) {
-  VFD_REQUIRE(g && dx && planes > 0 && h >= 2 && w >= 2 && (long long)(h + 2) * (w + 2) < (1LL << 31),
+int vfd_reflect_pad1_bwd(const void* g, void* dx, long long planes, int h, int w, int dtype, void* stream) {
+  VFD_REQUIRE(g && dx && planes > 0 && h >= 2 && w >= 2 && (long long)(h + 2) * (w + 2) < (1LL << 31) &&
+                  (dtype == 0 || dtype == 1),
               "reflect_pad1: bad arguments (h, w >= 2)");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_REFLECT_PAD, s);
   VFD_REQUIRE(planes / PPT < 65535, "reflect_pad1: too many planes");
   const dim3 grid((unsigned)((h * ((w + EPT - 1) / EPT) + 255) / 256), (unsigned)((planes + PPT - 1) / PPT));
-  elu_up_pad_bwd_k<0, false><<<grid, 256, 0, s>>>(g, nullptr, dx, planes, h, w, nullptr);
+  if (dtype == 1)
+    elu_up_pad_bwd_k<0, false><<<grid, 256, 0, s>>>((const __bf16*)g, (const __bf16*)nullptr, (__bf16*)dx, planes, h,
+                                                    w, nullptr);
+  else
+    elu_up_pad_bwd_k<0, false><<<grid, 256, 0, s>>>((const float*)g, (const float*)nullptr, (float*)dx, planes, h, w,
+                                                    nullptr);
   return fail_launch("reflect_pad1_bwd");
 }
 
@@ -242,31 +251,45 @@ int vfd_lrelu_pad1_bwd_nhwc(const float* g, const float* out, float* gp, long lo
   return fail_launch("lrelu_pad1_bwd_nhwc");
 }
 
-int vfd_elu_up_pad1_fwd(const float* y, float* out, long long planes, int h, int w, int up, void* stream) {
+int vfd_elu_up_pad1_fwd(const void* y, void* out, long long planes, int h, int w, int up, int dtype, void* stream) {
   VFD_REQUIRE(y && out && planes > 0 && planes / PPT < 65535 && h >= 1 && w >= 1 && (up == 0 || up == 1) && (h << up) >= 2 &&
+                  (dtype == 0 || dtype == 1) &&
                   (w << up) >= 2 && (long long)((h << up) + 2) * ((w << up) + 2) < (1LL << 31),
               "elu_up_pad1: bad arguments (up in {0, 1}, padded side >= 2)");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_ELU_PAD, s);
   const unsigned gx = (unsigned)((((h << up) + 2) * ((w << up) + 2) + 256 * EPT - 1) / (256 * EPT));
   const dim3 grid(gx, (unsigned)((planes + PPT - 1) / PPT));
-  if (up) elu_up_pad_fwd_k<1, true><<<grid, 256, 0, s>>>(y, out, planes, h, w);
-  else elu_up_pad_fwd_k<0, true><<<grid, 256, 0, s>>>(y, out, planes, h, w);
+  if (dtype == 1) {
+    if (up) elu_up_pad_fwd_k<1, true><<<grid, 256, 0, s>>>((const __bf16*)y, (__bf16*)out, planes, h, w);
+    else elu_up_pad_fwd_k<0, true><<<grid, 256, 0, s>>>((const __bf16*)y, (__bf16*)out, planes, h, w);
+  } else {
+    if (up) elu_up_pad_fwd_k<1, true><<<grid, 256, 0, s>>>((const float*)y, (float*)out, planes, h, w);
+    else elu_up_pad_fwd_k<0, true><<<grid, 256, 0, s>>>((const float*)y, (float*)out, planes, h, w);
+  }
   return fail_launch("elu_up_pad1_fwd");
 }
 
 int vfd_elu_up_pad1_bwd_blocks(int h, int w) { return (h * ((w + EPT - 1) / EPT) + 255) / 256; }
 
-int vfd_elu_up_pad1_bwd(const float* g, const float* y, float* dy, long long planes, int h, int w, int up,
-                        float* psum, void* stream) {
+int vfd_elu_up_pad1_bwd(const void* g, const void* y, void* dy, long long planes, int h, int w, int up,
+                        float* psum, int dtype, void* stream) {
   VFD_REQUIRE(g && y && dy && planes > 0 && planes / PPT < 65535 && h >= 1 && w >= 1 && (up == 0 || up == 1) && (h << up) >= 2 &&
+                  (dtype == 0 || dtype == 1) &&
                   (w << up) >= 2 && (long long)((h << up) + 2) * ((w << up) + 2) < (1LL << 31),
               "elu_up_pad1: bad arguments (up in {0, 1}, padded side >= 2)");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_ELU_PAD, s);
   const dim3 grid((unsigned)((h * ((w + EPT - 1) / EPT) + 255) / 256), (unsigned)((planes + PPT - 1) / PPT));
-  if (up) elu_up_pad_bwd_k<1, true><<<grid, 256, 0, s>>>(g, y, dy, planes, h, w, psum);
-  else elu_up_pad_bwd_k<0, true><<<grid, 256, 0, s>>>(g, y, dy, planes, h, w, psum);
+  if (dtype == 1) {
+    const __bf16 *gb = (const __bf16*)g, *yb = (const __bf16*)y;
+    if (up) elu_up_pad_bwd_k<1, true><<<grid, 256, 0, s>>>(gb, yb, (__bf16*)dy, planes, h, w, psum);
+    else elu_up_pad_bwd_k<0, true><<<grid, 256, 0, s>>>(gb, yb, (__bf16*)dy, planes, h, w, psum);
+  } else {
+    const float *gf = (const float*)g, *yf = (const float*)y;
+    if (up) elu_up_pad_bwd_k<1, true><<<grid, 256, 0, s>>>(gf, yf, (float*)dy, planes, h, w, psum);
+    else elu_up_pad_bwd_k<0, true><<<grid, 256, 0, s>>>(gf, yf, (float*)dy, planes, h, w, psum);
+  }
   return fail_launch("elu_up_pad1_bwd");
 }
 

@@ -161,6 +161,29 @@ __device__ __forceinline__ T block_sum_all(T v, T* lds) {
   return lds[0] + lds[1] + lds[2] + lds[3];
 }
 
+// ---------------------------------------------------------------- activation element types
+// The dense-net kernels read / write their activations as fp32 or bf16 (config 3's autocast) and
+// compute in fp32: loads widen exactly, stores round to nearest even (= torch's .to(bfloat16)).
+typedef __bf16 vfd_bf16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float ld1(const float* p) { return *p; }
+__device__ __forceinline__ float ld1(const __bf16* p) { return (float)*p; }
+__device__ __forceinline__ void st1(float* p, float v) { *p = v; }
+__device__ __forceinline__ void st1(__bf16* p, float v) { *p = (__bf16)v; }
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ float4 ld4(const __bf16* p) {
+  const vfd_bf16x4 v = *reinterpret_cast<const vfd_bf16x4*>(p);
+  return make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
+}
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+__device__ __forceinline__ void st4(__bf16* p, float4 v) {
+  vfd_bf16x4 b;
+  b[0] = (__bf16)v.x;
+  b[1] = (__bf16)v.y;
+  b[2] = (__bf16)v.z;
+  b[3] = (__bf16)v.w;
+  *reinterpret_cast<vfd_bf16x4*>(p) = b;
+}
+
 // ---------------------------------------------------------------- K3 geometry (frustum samples)
 struct Tri {
   int x0, y0, z0;

@@ -13,6 +13,10 @@
 //           (projconv.hip pcv_main_k; reference channel c*D + d, :261-265)
 //   mode 2  K3C data-gradient copy  dst[8 - tap][oq][n][h][s] = w[4oq + 2h + s][c*D + d][tap]
 //           (projconv.hip pcd_main_k; n = d*Cv + c, zero for n >= Cv*D)
+//   mode 3  K3C forward, bf16       dst[d][tap][q16][ob][lane][j] = bf16(w[o][c*D + d][tap]),
+//           o = 32 ob + (lane & 31), c = 16 q16 + 8 (lane >> 5) + j (projconv.hip pcvb_main_k)
+//   mode 4  K2C, bf16 (from the mode-0 copy f0): dst[tap][q16][ob][lane][j] = bf16(f0 of channel
+//           16 q16 + 8 (lane >> 5) + j, out-channel 32 ob + (lane & 31)), q16 < ceil32(C) / 16
 //   permute element (o, a, b, t) between any two strided layouts (the pose weight between the
 //           reference channel order c*Z + z and the map's z*C1 + c, NCHW or channels-last for MIOpen);
 //           swap = the NCHW -> NCHW instance dst[o][b][a][t] = w[o][a][b][t]
@@ -132,6 +136,65 @@ __global__ __launch_bounds__(256) void wfrag2_pad_k(float* __restrict__ dst, int
   if (i >= (long long)WR_TAPS * OQ * per) return;
   const long long plane = i / per, r = i - plane * per;    // plane = tap' * OQ + oq
   dst[(plane * npad + K) * 4 + r] = 0.f;
+}
+
+// mode 3 (bf16, projconv.hip pcvb_main_k): dst[d][tap][q16][ob][lane][j] = bf16(w[o][c*D + d][tap])
+// with o = 32 ob + (lane & 31), c = 16 q16 + 8 (lane >> 5) + j (round to nearest even).  Tile = one
+// 32-out-channel block x one 16-channel chunk x WT_D3 depth bins, source runs of WT_D3 * 9 floats
+// staged through LDS; each thread writes one lane's 16-B fragment.
+constexpr int WT_D3 = 4;
+typedef __bf16 wbf16x8 __attribute__((ext_vector_type(8)));
+__global__ __launch_bounds__(256) void wfrag3_k(const float* __restrict__ w, wbf16x8* __restrict__ dst, int O, int Cv,
+                                                int D) {
+  __shared__ float tile[32 * 16 * WT_D3 * WR_TAPS];
+  const int ob = blockIdx.x, q16 = blockIdx.y, d0 = blockIdx.z * WT_D3;
+  const int nd = min(WT_D3, D - d0), K = Cv * D, seg = nd * WR_TAPS;
+  for (int i = threadIdx.x; i < 32 * 16 * seg; i += 256) {
+    const int r = i / seg, k = i - r * seg;          // r = o_l * 16 + c_l
+    const int o_l = r >> 4, c_l = r & 15;
+    tile[r * WT_D3 * WR_TAPS + k] = w[((size_t)(32 * ob + o_l) * K + (size_t)(16 * q16 + c_l) * D + d0) * WR_TAPS + k];
+  }
+  __syncthreads();
+  const int Q16 = Cv / 16, OB = O / 32;
+  for (int i = threadIdx.x; i < seg * 64; i += 256) {
+    const int lane = i & 63, dt = i >> 6;            // dt = d_l * 9 + tap
+    const int d_l = dt / WR_TAPS, tap = dt - d_l * WR_TAPS;
+    const int o_l = lane & 31, h = lane >> 5;
+    wbf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (__bf16)tile[(o_l * 16 + 8 * h + j) * WT_D3 * WR_TAPS + dt];
+    dst[((((size_t)(d0 + d_l) * WR_TAPS + tap) * Q16 + q16) * OB + ob) * 64 + lane] = v;
+  }
+}
+
+// mode 4 (bf16, padconv.hip ppcb_main_k) from the fp32 mode-0 fragment copy f0 [9][cpad16/4][O][2][2]:
+// dst[tap][q16][ob][lane][j] = bf16(f0 element of channel cz = 16 q16 + 8 (lane >> 5) + j, out-channel
+// 32 ob + (lane & 31)), zero for cz >= cpad16; one thread per destination lane fragment: two
+// 16-B reads (channel quads 4 q16 + 2h, +1), coalesced over the 32 out-channels of a block
+__global__ __launch_bounds__(256) void wfrag4_k(const float4* __restrict__ f0, wbf16x8* __restrict__ dst, int O,
+                                                int cq4, int nq16) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int OB = O / 32;
+  const long long total = (long long)WR_TAPS * nq16 * OB * 64;
+  if (i >= total) return;
+  const int lane = (int)(i & 63);
+  long long r = i >> 6;
+  const int ob = (int)(r % OB);
+  r /= OB;
+  const int q16 = (int)(r % nq16), tap = (int)(r / nq16);
+  const int o = 32 * ob + (lane & 31), h = lane >> 5;
+  wbf16x8 v;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int q4 = 4 * q16 + 2 * h + k;
+    float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (q4 < cq4) f = f0[((size_t)tap * cq4 + q4) * O + o];
+    v[4 * k + 0] = (__bf16)f.x;
+    v[4 * k + 1] = (__bf16)f.y;
+    v[4 * k + 2] = (__bf16)f.z;
+    v[4 * k + 3] = (__bf16)f.w;
+  }
+  dst[i] = v;
 }
 
 // mode 0 with the pose map's channel order (cz = z * C1 + c, reference channel c * Z + z):
@@ -259,6 +322,30 @@ int vfd_weight_fragments(int mode, const float* w, float* dst, int O, int C, int
   }
   weight_frag_k<<<(unsigned)((nrow + 255) / 256), 256, 0, s>>>(a, w, dst, nrow);
   return fail_launch("weight_fragments");
+}
+
+// bf16 fragment copies of the MFMA convolutions' weights (mode 3: K3C forward, projconv.hip
+// pcvb_main_k); dst holds bf16 elements
+int vfd_weight_fragments_bf16(int mode, const float* w, void* dst, int O, int C, int C1, int Z, int Cv, int D,
+                              void* stream) {
+  (void)C; (void)C1; (void)Z;
+  VFD_REQUIRE(w && dst && O > 0, "weight_fragments_bf16: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  if (mode == 3) {
+    VFD_REQUIRE(O % 32 == 0 && Cv > 0 && Cv % 16 == 0 && D > 0, "weight_fragments_bf16: mode 3 needs O %% 32, Cv %% 16");
+    wfrag3_k<<<dim3((unsigned)(O / 32), (unsigned)(Cv / 16), (unsigned)((D + WT_D3 - 1) / WT_D3)), 256, 0, s>>>(
+        w, (wbf16x8*)dst, O, Cv, D);
+    return fail_launch("weight_fragments_bf16");
+  }
+  if (mode == 4) {          // w = the fp32 mode-0 fragment copy [9][ceil16(C)/4][O][2][2]
+    VFD_REQUIRE(O % 32 == 0 && C > 0, "weight_fragments_bf16: mode 4 needs O %% 32");
+    const int cq4 = (C + 15) / 16 * 4, nq16 = (C + 31) / 32 * 2;
+    const long long n = (long long)WR_TAPS * nq16 * (O / 32) * 64;
+    wfrag4_k<<<(unsigned)((n + 255) / 256), 256, 0, s>>>((const float4*)w, (wbf16x8*)dst, O, cq4, nq16);
+    return fail_launch("weight_fragments_bf16");
+  }
+  set_error("weight_fragments_bf16: mode %d", mode);
+  return VFD_EINVAL;
 }
 
 int vfd_weight_permute(const float* w, float* dst, int O, int A, int B, int T, const long long* src_strides,

@@ -132,6 +132,14 @@ class VFNet(nn.Module):
             w0 = KN.proj_conv_weight(c0.weight, self.v_dim_o[-1], self.proj_d_bins)
         else:
             C1, Z = self.feat_in_dim + 1, self.z_dim
+            if self.pad_conv_bf16(x_padded):
+                # K2C's bf16 form under config 3's autocast (padconv.hip ppcb_main_k); fragments from
+                # the fp32 mode-0 copy, shared by the step's pose calls
+                wf = _GEOMETRY_CACHE.get(('pose_wf_bf16', id(c0.weight)), (c0.weight,),
+                                         lambda: KN.pad_conv_weight_fragments_bf16(c0.weight.detach(), C1, Z))
+                y0 = KN.PadConvBF16.apply(x_padded, c0.weight, c0.bias, self.stride, wf, (C1, Z))
+                return F.leaky_relu(F.conv2d(y0, c1.weight, c1.bias, stride=self.stride), 0.1,
+                                    inplace=True).contiguous()
             if self.pad_conv(x_padded):
                 # K2C: the first conv on MFMA (padconv.hip), written reflect-padded for the second;
                 # it takes the weight in the reference channel order (relayouts in weights.hip);
@@ -144,6 +152,14 @@ class VFNet(nn.Module):
             w0 = KN.pose_conv_weight(c0.weight, C1, Z)
         x = F.leaky_relu(F.conv2d(x_padded, w0, c0.bias, stride=self.stride), 0.1, inplace=True)
         return F.leaky_relu(c1(x), 0.1, inplace=True).contiguous()
+
+    def pad_conv_bf16(self, x_padded):
+        """K2C's bf16 form applies: 256 outputs, bf16 autocast (config 3), a supported shape, not
+        disabled by VFD_PAD_CONV=0 / VFD_PAD_CONV_BF16=0."""
+        return (os.environ.get('VFD_PAD_CONV', '1') != '0' and os.environ.get('VFD_PAD_CONV_BF16', '1') != '0'
+                and self.reduce_dim[0].out_channels == 256 and torch.is_autocast_enabled('cuda')
+                and torch.get_autocast_dtype('cuda') == torch.bfloat16
+                and KN.pad_conv_bf16_supported(x_padded, self.stride, 256))
 
     def pad_conv(self, x_padded):
         """K2C (the pose reduce_dim's first conv as an fp32 MFMA kernel) applies: 256 outputs, fp32
@@ -189,12 +205,21 @@ class VFNet(nn.Module):
                 and c0.out_channels == 256 and self.proj_d_bins <= 64
                 and not torch.is_autocast_enabled('cuda'))
 
+    def fused_projection_bf16(self, voxel_feat):
+        """K3C's bf16 form applies: as fused_projection, under bf16 autocast (config 3), not
+        disabled by VFD_PROJ_CONV_BF16=0."""
+        c0 = self.reduce_dim[0]
+        return (os.environ.get('VFD_PROJ_CONV', '1') != '0' and os.environ.get('VFD_PROJ_CONV_BF16', '1') != '0'
+                and voxel_feat.shape[-1] == 64 and c0.out_channels == 256 and self.proj_d_bins <= 64
+                and torch.is_autocast_enabled('cuda') and torch.get_autocast_dtype('cuda') == torch.bfloat16)
+
     def project_voxel_into_image(self, voxel_feat, inv_K, extrinsics):
         """K3 + reduce_dim: voxel features [B,V,Cv] -> [B*N, feat_out, h, w]."""
         space = self.space(voxel_feat.device)
-        if self.fused_projection(voxel_feat):
+        if self.fused_projection(voxel_feat) or self.fused_projection_bf16(voxel_feat):
             c0, c1 = self.reduce_dim[0], self.reduce_dim[3]
-            y0 = KN.ProjConv.apply(space, voxel_feat, inv_K, extrinsics, c0.weight, c0.bias)
+            fn = KN.ProjConv if self.fused_projection(voxel_feat) else KN.ProjConvBF16
+            y0 = fn.apply(space, voxel_feat.float(), inv_K, extrinsics, c0.weight, c0.bias)
             return F.leaky_relu(F.conv2d(y0, c1.weight, c1.bias), 0.1, inplace=True).contiguous()
         return self._reduce(KN.VoxelProject.apply(space, voxel_feat, inv_K, extrinsics))
 

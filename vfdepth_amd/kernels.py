@@ -37,6 +37,15 @@ _amp_fwd = torch.amp.custom_fwd(device_type='cuda', cast_inputs=torch.float32)
 _amp_bwd = torch.amp.custom_bwd(device_type='cuda')
 
 
+def _dt(t):
+    """C-ABI activation dtype code of a dense-net map: 0 fp32, 1 bf16."""
+    if t.dtype == torch.float32:
+        return 0
+    if t.dtype == torch.bfloat16:
+        return 1
+    raise RuntimeError(f'dense-net kernels take fp32 or bf16 maps, got {t.dtype}')
+
+
 def _ws(nbytes, device):
     return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
 
@@ -494,6 +503,72 @@ class PadConv(torch.autograd.Function):
         return dx, dw, db, None, None, None
 
 
+def pad_conv_weight_fragments_bf16(w, C1=0, Z=0, f0=None):
+    """Conv weight [O, C, 3, 3] -> the bf16 K2C kernel's copy [9, ceil32(C)/16, O/32, 64, 8] over the
+    map's channel order (padconv.hip ppcb_main_k), through the fp32 mode-0 fragments `f0` (built
+    here unless given)."""
+    lib = L.load()
+    O, C = w.shape[:2]
+    if f0 is None:
+        f0 = pad_conv_weight_fragments(w, C1, Z)
+    out = torch.empty(9, (C + 31) // 32 * 2, O // 32, 64, 8, dtype=torch.bfloat16, device=w.device)
+    L.check(lib.vfd_weight_fragments_bf16(4, f0.data_ptr(), out.data_ptr(), O, C, C1, Z, 0, 0, L.stream()),
+            'weight_fragments_bf16')
+    return out
+
+
+def pad_conv_bf16_supported(x, stride, out_channels):
+    return bool(L.load().vfd_pad_conv_fwd_bf16_workspace(ctypes.byref(pad_conv_desc(x, stride, out_channels))))
+
+
+class PadConvBF16(torch.autograd.Function):
+    """K2C in bf16 (config 3): the fp32 reflect-padded channels-last map rounded to bf16 as it is
+    staged, bf16 weights, v_mfma_f32_32x32x16_bf16 with fp32 accumulation, bias + LeakyReLU in fp32,
+    output bf16 (reflect-padded channels-last, the input of the next conv, which autocast runs in
+    bf16).  Backward: MIOpen's bf16 data / weight gradients on bf16 copies of the map and weight,
+    gradients returned in fp32 (the map, the master weight, the bias)."""
+
+    @staticmethod
+    def forward(ctx, x, w, bias, stride, wf=None, perm=None):
+        lib = L.load()
+        x = _channels_last(x, 'pad_conv input')
+        bias = _dev(bias, 'pad_conv bias')
+        O = w.shape[0]
+        d = pad_conv_desc(x, stride, O)
+        nbytes = lib.vfd_pad_conv_fwd_bf16_workspace(ctypes.byref(d))
+        if not nbytes:
+            raise RuntimeError(f'pad_conv_fwd_bf16: unsupported shape {tuple(x.shape)}, stride {stride}, {O} outputs')
+        ho, wo = (x.shape[2] - 3) // stride + 1, (x.shape[3] - 3) // stride + 1
+        out = torch.empty(x.shape[0], O, ho + 2, wo + 2, dtype=torch.bfloat16, device=x.device,
+                          memory_format=torch.channels_last)
+        if wf is None:
+            wf = pad_conv_weight_fragments_bf16(_dev(w.detach(), 'pad_conv weight'), *(perm or (0, 0)))
+        ws = _ws(nbytes, x.device)
+        L.check(lib.vfd_pad_conv_fwd_bf16(ctypes.byref(d), x.data_ptr(), wf.data_ptr(), bias.data_ptr(), out.data_ptr(),
+                                          ws.data_ptr(), nbytes, L.stream()), 'pad_conv_fwd_bf16')
+        ctx.stride, ctx.perm = stride, perm
+        ctx.save_for_backward(x, w, out)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w, out = ctx.saved_tensors
+        g_pre = lrelu_pad_backward(g.float(), out.float()).to(torch.bfloat16)
+        mask = [ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]]
+        s = ctx.stride
+        wd = w.detach()
+        if ctx.perm:        # MIOpen works in the map's channel order (channels-last like x)
+            C1, Z = ctx.perm
+            wd = weight_swap(wd, C1, Z, cache=True, memory_format=torch.channels_last)
+        dx, dw, db = torch.ops.aten.convolution_backward(g_pre, x.to(torch.bfloat16), wd.to(torch.bfloat16), [w.shape[0]],
+                                                         [s, s], [0, 0], [1, 1], False, [0, 0], 1, mask)
+        if dw is not None:
+            dw = dw.float()
+            if ctx.perm:
+                dw = weight_swap(dw, Z, C1)
+        return (dx.float() if dx is not None else None), dw, (db.float() if db is not None else None), None, None, None
+
+
 def lrelu_pad_backward(g, out, slope=0.1):
     """d pre-activation of LeakyReLU(slope) + reflect pad(1) from the channels-last gradient of the
     padded output g and that output (fused, deterministic: reflectpad.hip) -> NHWC [n, C, h, w]."""
@@ -600,6 +675,84 @@ class ProjConv(torch.autograd.Function):
             dw0 = weight_swap(dw, space.D, Cv)      # d*Cv + c -> the reference's c*D + d
         ctx.plan = None
         return None, dvox, None, None, dw0, db if mask[2] else None
+
+
+def proj_conv_weight_fragments_bf16(w, Cv, D):
+    """reduce_dim[0] weight [O, Cv*D, 3, 3] (reference channel c*D + d) -> the bf16 K3C kernel's
+    fragment copy [D, 9, Cv/16, O/32, 64, 8] (projconv.hip pcvb_main_k), rounded to nearest even."""
+    lib = L.load()
+    w = _dev(w.detach(), 'conv weight')
+    O = w.shape[0]
+    out = torch.empty(D, 9, Cv // 16, O // 32, 64, 8, dtype=torch.bfloat16, device=w.device)
+    L.check(lib.vfd_weight_fragments_bf16(3, w.data_ptr(), out.data_ptr(), O, Cv * D, 0, 0, Cv, D, L.stream()),
+            'weight_fragments_bf16')
+    return out
+
+
+class ProjConvBF16(torch.autograd.Function):
+    """K3C in bf16 (config 3: the reference autocasts the fusion features to bf16,
+    volumetric_fusionnet.py:105-114): the fp32 trilinear samples of the fp32 voxel grid rounded to
+    bf16 in LDS, bf16 weights, v_mfma_f32_32x32x16_bf16 with fp32 accumulation, bias + LeakyReLU
+    in fp32, output bf16 (the reflect-padded channels-last input of reduce_dim's second conv,
+    which autocast runs in bf16).  Backward: MIOpen's bf16 data / weight gradients on the bf16
+    frustum features the kernel writes as its side output, then K3's fp32 planned backward.
+    Gradients to the fp32 voxels / master weight / bias come back in fp32."""
+
+    @staticmethod
+    def forward(ctx, space, vox, invK, E, w0, bias):
+        lib = L.load()
+        vox, invK, E = (_dev(t, n) for t, n in ((vox, 'voxel'), (invK, 'inv_K'), (E, 'extrinsics')))
+        bias = _dev(bias, 'reduce_dim bias')
+        B, V, Cv = vox.shape
+        N, O = E.shape[1], w0.shape[0]
+        wq = proj_conv_weight_fragments_bf16(w0, Cv, space.D)
+        cl = torch.channels_last
+        out = torch.empty(B * N, O, space.h + 2, space.w + 2, dtype=torch.bfloat16, device=vox.device, memory_format=cl)
+        need_x = ctx.needs_input_grad[1] or ctx.needs_input_grad[4]
+        x = (torch.empty(B * N, Cv * space.D, space.h + 2, space.w + 2, dtype=torch.bfloat16, device=vox.device,
+                         memory_format=cl) if need_x else None)
+        d = space.desc(B, N, Cv=Cv)
+        nbytes = lib.vfd_proj_conv_fwd_workspace(ctypes.byref(d))
+        ws = _ws(nbytes, vox.device)
+        L.check(lib.vfd_proj_conv_fwd_bf16(ctypes.byref(d), vox.data_ptr(), invK.data_ptr(), E.data_ptr(),
+                                           wq.data_ptr(), bias.data_ptr(), O, out.data_ptr(),
+                                           x.data_ptr() if need_x else None, ws.data_ptr(), nbytes, L.stream()),
+                'proj_conv_fwd_bf16')
+        ctx.space, ctx.shape = space, (B, N, V, Cv, O)
+        ctx.plan = None
+        if ctx.needs_input_grad[1]:
+            nbytes = lib.vfd_voxel_project_plan_bytes(ctypes.byref(d))
+            ctx.plan = torch.empty(nbytes, dtype=torch.uint8, device=vox.device)
+            L.check(lib.vfd_voxel_project_plan(ctypes.byref(d), invK.data_ptr(), E.data_ptr(), ctx.plan.data_ptr(),
+                                               nbytes, L.stream()), 'voxel_project_plan')
+        ctx.save_for_backward(w0, out, x)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        lib = L.load()
+        w0, out, x = ctx.saved_tensors
+        space = ctx.space
+        B, N, V, Cv, O = ctx.shape
+        d = space.desc(B, N, Cv=Cv)
+        # adjoint of the reflect padding and the LeakyReLU in fp32 (sign from the bf16 output), then
+        # the bf16 operand of MIOpen's gradients
+        g_pre = lrelu_pad_backward(g.float(), out.float()).to(torch.bfloat16)
+        mask = (ctx.needs_input_grad[1], ctx.needs_input_grad[4], ctx.needs_input_grad[5])
+        wb = proj_conv_weight(w0.detach(), Cv, space.D).to(torch.bfloat16)
+        dx, dw, db = torch.ops.aten.convolution_backward(g_pre, x, wb, [O], [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
+                                                         [mask[0], mask[1], mask[2]])
+        dvox = dw0 = None
+        if mask[0]:
+            dxf = dx.float().contiguous(memory_format=torch.channels_last)
+            dvox = torch.empty(B, V, Cv, device=g.device)
+            L.check(lib.vfd_voxel_project_bwd_planned(ctypes.byref(d), dxf.data_ptr(), ctx.plan.data_ptr(),
+                                                      ctx.plan.numel(), dvox.data_ptr(), L.stream()),
+                    'voxel_project_bwd')
+        if mask[1]:
+            dw0 = weight_swap(dw.float(), space.D, Cv)      # d*Cv + c -> the reference's c*D + d
+        ctx.plan = None
+        return None, dvox, None, None, dw0, db.float() if mask[2] else None
 
 
 # =============================================================================================
@@ -948,11 +1101,14 @@ class BatchNormAct(torch.autograd.Function):
     def forward(ctx, x, gamma, beta, residual, running_mean, running_var, eps, momentum, relu, pg, nbt=None):
         lib = L.load()
         _check_device(x, 'batch norm input')
+        if x.dtype not in (torch.float32, torch.bfloat16):
+            raise RuntimeError(f'fused batch norm: fp32 or bf16 activations, got {x.dtype}')
         x = x.contiguous()
         N, C, H, W = x.shape
-        d = L.BnDesc(N, C, H * W, 0, int(relu), float(eps), float(momentum))
+        # bf16 activations (config 3's autocast: the conv outputs are bf16), fp32 parameters / stats
+        d = L.BnDesc(N, C, H * W, 0, int(relu), float(eps), float(momentum), int(x.dtype == torch.bfloat16))
         d.S = lib.vfd_bn_splits(ctypes.byref(d))
-        r = residual.contiguous() if residual is not None else None
+        r = residual.to(x.dtype).contiguous() if residual is not None else None
         ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
         # with ReLU the forward also stores [y > 0] as one byte per element: the backward reads
         # that mask instead of y (d.relu == 2 there), a quarter of the bytes
@@ -965,9 +1121,10 @@ class BatchNormAct(torch.autograd.Function):
             L.check(lib.vfd_bn1_fwd(ctypes.byref(d), x.data_ptr(), ptr(r), gamma.data_ptr(), beta.data_ptr(),
                                     y.data_ptr(), mean.data_ptr(), invstd.data_ptr(), ptr(running_mean),
                                     ptr(running_var), ptr(nbt), ptr(mk), L.stream()), 'bn1_fwd')
-            ctx.d, ctx.pg, ctx.count, ctx.has_res = (d.N, d.C, d.HW, d.S, d.relu, d.eps, d.momentum), pg, float(N * H * W), r is not None
+            ctx.d, ctx.pg, ctx.count, ctx.has_res = (d.N, d.C, d.HW, d.S, d.relu, d.eps, d.momentum, d.dtype), pg, float(N * H * W), r is not None
             if L.PROF_ON:
-                L.ALG_BYTES['bn_fwd'] += x.numel() * (8 + 4 * (r is not None) + (mk is not None))
+                L.ALG_BYTES['bn_fwd'] += x.numel() * (2 * x.element_size() + x.element_size() * (r is not None)
+                                                      + (mk is not None))
             ctx.save_for_backward(x, mk, gamma, mean, invstd)
             return y
         partial = torch.empty(C, d.S, 2, dtype=torch.float64, device=x.device)
@@ -986,9 +1143,10 @@ class BatchNormAct(torch.autograd.Function):
                                      running_var.data_ptr() if running_var is not None else None,
                                      nbt.data_ptr() if nbt is not None else None, ptr(mk), L.stream()),
                 'bn_fwd_apply')
-        ctx.d, ctx.pg, ctx.count, ctx.has_res = (d.N, d.C, d.HW, d.S, d.relu, d.eps, d.momentum), pg, count, r is not None
+        ctx.d, ctx.pg, ctx.count, ctx.has_res = (d.N, d.C, d.HW, d.S, d.relu, d.eps, d.momentum, d.dtype), pg, count, r is not None
         if L.PROF_ON:                        # compulsory: x (+ r) in, y (+ the ReLU byte mask) out
-            L.ALG_BYTES['bn_fwd'] += x.numel() * (8 + 4 * (r is not None) + (mk is not None))
+            L.ALG_BYTES['bn_fwd'] += x.numel() * (2 * x.element_size() + x.element_size() * (r is not None)
+                                                  + (mk is not None))
         ctx.save_for_backward(x, mk, gamma, mean, invstd)
         return y
 
@@ -999,7 +1157,7 @@ class BatchNormAct(torch.autograd.Function):
         d = L.BnDesc(*ctx.d)
         if d.relu:
             d.relu = 2                       # the ReLU mask is the forward's byte mask
-        g = g.contiguous()
+        g = g.to(x.dtype).contiguous()
         need = ctx.needs_input_grad
         ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
         if ctx.one:
@@ -1008,7 +1166,8 @@ class BatchNormAct(torch.autograd.Function):
             dgamma = torch.empty_like(gamma) if need[1] else None
             dbeta = torch.empty_like(gamma) if need[2] else None
             if L.PROF_ON:
-                L.ALG_BYTES['bn_bwd'] += x.numel() * (8 + (d.relu != 0) + 4 * ((dx is not None) + (dr is not None)))
+                es = x.element_size()
+                L.ALG_BYTES['bn_bwd'] += x.numel() * (2 * es + (d.relu != 0) + es * ((dx is not None) + (dr is not None)))
             L.check(lib.vfd_bn1_bwd(ctypes.byref(d), g.data_ptr(), mk.data_ptr() if d.relu else None, x.data_ptr(),
                                     gamma.data_ptr(), mean.data_ptr(), invstd.data_ptr(), ptr(dx), ptr(dr),
                                     ptr(dgamma), ptr(dbeta), L.stream()), 'bn1_bwd')
@@ -1029,7 +1188,8 @@ class BatchNormAct(torch.autograd.Function):
             sums, ns = _bn_sync(lib, d, partial, ctx.pg, x.shape[0] * d.HW, 'bn_sum', invstd, dgamma, dbeta), 1
             count, pg_dgamma, pg_dbeta = 0.0, None, None
         if L.PROF_ON:                        # compulsory: g, x (, the mask) in, dx (, dr) out
-            L.ALG_BYTES['bn_bwd'] += x.numel() * (8 + (d.relu != 0) + 4 * ((dx is not None) + (dr is not None)))
+            es = x.element_size()
+            L.ALG_BYTES['bn_bwd'] += x.numel() * (2 * es + (d.relu != 0) + es * ((dx is not None) + (dr is not None)))
         L.check(lib.vfd_bn_bwd_apply(ctypes.byref(d), g.data_ptr(), yp, x.data_ptr(), sums.data_ptr(), ns, count,
                                      gamma.data_ptr(), mean.data_ptr(), invstd.data_ptr(), ptr(dx), ptr(dr),
                                      ptr(pg_dgamma), ptr(pg_dbeta), L.stream()), 'bn_bwd_apply')
@@ -1040,8 +1200,9 @@ class BatchNormAct(torch.autograd.Function):
 # Reflect padding by one pixel (the decoders' reflect 3x3 convs), deterministic backward
 # =============================================================================================
 class ReflectPad1(torch.autograd.Function):
-    """F.pad(x, (1, 1, 1, 1), mode='reflect') for NCHW fp32 x (reflectpad.hip); the backward
-    gathers each pixel's copies in a fixed order (ATen's scatters with atomics)."""
+    """F.pad(x, (1, 1, 1, 1), mode='reflect') for NCHW fp32 or bf16 x (reflectpad.hip); the backward
+    gathers each pixel's copies in a fixed order in fp32 (ATen's scatters with atomics, in bf16
+    under autocast: 0.5 ms per decoder pad at config 3)."""
 
     @staticmethod
     def forward(ctx, x):
@@ -1049,24 +1210,24 @@ class ReflectPad1(torch.autograd.Function):
         _check_device(x, 'reflect pad input')
         x = x.contiguous()
         *lead, h, w = x.shape
-        y = torch.empty(*lead, h + 2, w + 2, device=x.device)
+        y = torch.empty(*lead, h + 2, w + 2, dtype=x.dtype, device=x.device)
         planes = x.numel() // (h * w)
-        L.check(lib.vfd_reflect_pad1_fwd(x.data_ptr(), y.data_ptr(), planes, h, w, L.stream()), 'reflect_pad1_fwd')
+        L.check(lib.vfd_reflect_pad1_fwd(x.data_ptr(), y.data_ptr(), planes, h, w, _dt(x), L.stream()), 'reflect_pad1_fwd')
         if L.PROF_ON:
-            L.ALG_BYTES['reflect_pad'] += (x.numel() + y.numel()) * 4
-        ctx.shape = tuple(x.shape)
+            L.ALG_BYTES['reflect_pad'] += (x.numel() + y.numel()) * x.element_size()
+        ctx.shape, ctx.dtype = tuple(x.shape), x.dtype
         return y
 
     @staticmethod
     def backward(ctx, g):
         lib = L.load()
-        g = g.contiguous()
+        g = g.to(ctx.dtype).contiguous()
         h, w = ctx.shape[-2:]
-        dx = torch.empty(ctx.shape, device=g.device)
+        dx = torch.empty(ctx.shape, dtype=ctx.dtype, device=g.device)
         planes = dx.numel() // (h * w)
-        L.check(lib.vfd_reflect_pad1_bwd(g.data_ptr(), dx.data_ptr(), planes, h, w, L.stream()), 'reflect_pad1_bwd')
+        L.check(lib.vfd_reflect_pad1_bwd(g.data_ptr(), dx.data_ptr(), planes, h, w, _dt(dx), L.stream()), 'reflect_pad1_bwd')
         if L.PROF_ON:
-            L.ALG_BYTES['reflect_pad'] += (g.numel() + dx.numel()) * 4
+            L.ALG_BYTES['reflect_pad'] += (g.numel() + dx.numel()) * dx.element_size()
         return dx
 
 
@@ -1092,11 +1253,12 @@ def _elu_up_pad_fwd(y, u):
     _check_device(y, 'elu_up_pad input')
     y = y.contiguous()
     *lead, h, w = y.shape
-    out = torch.empty(*lead, (h << u) + 2, (w << u) + 2, device=y.device)
+    out = torch.empty(*lead, (h << u) + 2, (w << u) + 2, dtype=y.dtype, device=y.device)
     planes = y.numel() // (h * w)
-    L.check(lib.vfd_elu_up_pad1_fwd(y.data_ptr(), out.data_ptr(), planes, h, w, u, L.stream()), 'elu_up_pad1_fwd')
+    L.check(lib.vfd_elu_up_pad1_fwd(y.data_ptr(), out.data_ptr(), planes, h, w, u, _dt(y), L.stream()),
+            'elu_up_pad1_fwd')
     if L.PROF_ON:
-        L.ALG_BYTES['elu_pad'] += (y.numel() + out.numel()) * 4
+        L.ALG_BYTES['elu_pad'] += (y.numel() + out.numel()) * y.element_size()
     return out
 
 
@@ -1104,15 +1266,16 @@ def _elu_up_pad_bwd(g, y, u, bias_grad=False):
     """d y of the fused ELU [+ up] + pad, and (bias_grad) the per-plane block partial sums of d y
     [planes, blocks] (the producing conv's bias gradient before its fixed-order sum)."""
     lib = L.load()
-    g = g.contiguous()
+    g = g.to(y.dtype).contiguous()
     h, w = y.shape[-2:]
     dy = torch.empty_like(y)
     planes = y.numel() // (h * w)
     psum = torch.empty(planes, lib.vfd_elu_up_pad1_bwd_blocks(h, w), device=y.device) if bias_grad else None
     L.check(lib.vfd_elu_up_pad1_bwd(g.data_ptr(), y.data_ptr(), dy.data_ptr(), planes, h, w, u,
-                                    psum.data_ptr() if psum is not None else None, L.stream()), 'elu_up_pad1_bwd')
+                                    psum.data_ptr() if psum is not None else None, _dt(y), L.stream()),
+            'elu_up_pad1_bwd')
     if L.PROF_ON:
-        L.ALG_BYTES['elu_pad'] += (g.numel() + 2 * y.numel()) * 4
+        L.ALG_BYTES['elu_pad'] += (g.numel() + 2 * y.numel()) * y.element_size()
     return dy, psum
 
 
@@ -1127,7 +1290,7 @@ class ConvEluUpPad(torch.autograd.Function):
         lib = L.load()
         N, CI, Hp, Wp = xp.shape
         CO = weight.shape[0]
-        ctx.mfma = (_DEC_CONV and bias is not None and xp.is_contiguous()
+        ctx.mfma = (_DEC_CONV and bias is not None and xp.is_contiguous() and xp.dtype == torch.float32
                     and bool(lib.vfd_dec_conv_supported(N, CI, CO, Hp - 2, Wp - 2)))
         if ctx.mfma:      # decconv.hip: the narrow conv on fp32 MFMA
             w = weight.detach().contiguous()
@@ -1137,8 +1300,10 @@ class ConvEluUpPad(torch.autograd.Function):
             if L.PROF_ON:
                 L.ALG_BYTES['dec_conv'] += (xp.numel() + y.numel()) * 4
         else:
+            # MIOpen; a bf16 map (config 3's autocast) takes the weight / bias in bf16, as autocast's
+            # conv2d would
             with torch.no_grad():
-                y = F.conv2d(xp, weight, bias)
+                y = F.conv2d(xp, weight.to(xp.dtype), bias.to(xp.dtype) if bias is not None else None)
         ctx.u = 1 if up else 0
         ctx.save_for_backward(xp, weight, y)
         return _elu_up_pad_fwd(y, ctx.u)
@@ -1169,8 +1334,10 @@ class ConvEluUpPad(torch.autograd.Function):
                                             + (part is not None) * (dy.numel() + xp.numel())) * 4
             dw = part.sum(0).view(CO, CI, 3, 3) if part is not None else None
         elif need[0] or need[1]:
-            dx, dw, _ = torch.ops.aten.convolution_backward(dy, xp, weight, None, [1, 1], [0, 0], [1, 1], False,
-                                                            [0, 0], 1, [need[0], need[1], False])
+            dx, dw, _ = torch.ops.aten.convolution_backward(dy, xp, weight.to(xp.dtype), None, [1, 1], [0, 0], [1, 1],
+                                                            False, [0, 0], 1, [need[0], need[1], False])
+            if dw is not None:
+                dw = dw.to(weight.dtype)
         return dx, dw, db, None
 
 
@@ -1244,8 +1411,8 @@ def normalize_cat(a, b=None):
 # ResNet stem max pool (3x3, stride 2, padding 1) with a one-byte argmax and a gather backward
 # =============================================================================================
 class MaxPool3s2(torch.autograd.Function):
-    """F.max_pool2d(x, 3, 2, 1) for NCHW fp32 x (maxpool.hip): one byte of window index per
-    output instead of ATen's int64 indices; deterministic gather backward."""
+    """F.max_pool2d(x, 3, 2, 1) for NCHW fp32 or bf16 x (maxpool.hip): one byte of window index
+    per output instead of ATen's int64 indices; deterministic gather backward."""
 
     @staticmethod
     def forward(ctx, x):
@@ -1254,14 +1421,14 @@ class MaxPool3s2(torch.autograd.Function):
         x = x.contiguous()
         *lead, h, w = x.shape
         ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
-        y = torch.empty(*lead, ho, wo, device=x.device)
+        y = torch.empty(*lead, ho, wo, dtype=x.dtype, device=x.device)
         arg = torch.empty(*lead, ho, wo, dtype=torch.uint8, device=x.device)
         planes = x.numel() // (h * w)
-        L.check(lib.vfd_maxpool3s2_fwd(x.data_ptr(), y.data_ptr(), arg.data_ptr(), planes, h, w, L.stream()),
+        L.check(lib.vfd_maxpool3s2_fwd(x.data_ptr(), y.data_ptr(), arg.data_ptr(), planes, h, w, _dt(x), L.stream()),
                 'maxpool3s2_fwd')
         if L.PROF_ON:
-            L.ALG_BYTES['maxpool'] += (x.numel() + y.numel()) * 4 + arg.numel()
-        ctx.shape = tuple(x.shape)
+            L.ALG_BYTES['maxpool'] += (x.numel() + y.numel()) * x.element_size() + arg.numel()
+        ctx.shape, ctx.dtype = tuple(x.shape), x.dtype
         ctx.save_for_backward(arg)
         return y
 
@@ -1269,12 +1436,12 @@ class MaxPool3s2(torch.autograd.Function):
     def backward(ctx, g):
         lib = L.load()
         arg, = ctx.saved_tensors
-        g = g.contiguous()
+        g = g.to(ctx.dtype).contiguous()
         h, w = ctx.shape[-2:]
-        dx = torch.empty(ctx.shape, device=g.device)
+        dx = torch.empty(ctx.shape, dtype=ctx.dtype, device=g.device)
         planes = dx.numel() // (h * w)
-        L.check(lib.vfd_maxpool3s2_bwd(g.data_ptr(), arg.data_ptr(), dx.data_ptr(), planes, h, w, L.stream()),
+        L.check(lib.vfd_maxpool3s2_bwd(g.data_ptr(), arg.data_ptr(), dx.data_ptr(), planes, h, w, _dt(dx), L.stream()),
                 'maxpool3s2_bwd')
         if L.PROF_ON:
-            L.ALG_BYTES['maxpool'] += (g.numel() + dx.numel()) * 4 + arg.numel()
+            L.ALG_BYTES['maxpool'] += (g.numel() + dx.numel()) * dx.element_size() + arg.numel()
         return dx

@@ -30,15 +30,23 @@ def _activation(nonlin):
     return nn.Identity()
 
 
+def _fused_dtype_ok(x):
+    """fp32 outside autocast, or the bf16 activations of config 3's bf16 autocast."""
+    if torch.is_autocast_enabled('cuda'):
+        return x.dtype == torch.bfloat16 and torch.get_autocast_dtype('cuda') == torch.bfloat16
+    return x.dtype == torch.float32
+
+
 class ReflectConv2d(nn.Conv2d):
     """nn.Conv2d(padding_mode='reflect') (same parameters and state-dict keys) whose one-pixel
-    reflect padding runs on the HIP pad kernels for fp32 GPU maps: a deterministic backward
-    (ATen's reflection_pad2d backward scatters with atomics) and one launch each way."""
+    reflect padding runs on the HIP pad kernels for GPU maps (fp32, or bf16 under config 3's
+    autocast): a deterministic backward (ATen's reflection_pad2d backward scatters with atomics)
+    and one launch each way."""
 
     def _conv_forward(self, x, weight, bias):
         if (self.padding_mode == 'reflect' and tuple(self.padding) == (1, 1) and x.is_cuda and x.dim() == 4
-                and x.dtype == torch.float32 and x.shape[-1] >= 2 and x.shape[-2] >= 2
-                and not torch.is_autocast_enabled('cuda') and os.environ.get('VFD_REFLECT_PAD', '1') != '0'):
+                and _fused_dtype_ok(x) and x.shape[-1] >= 2 and x.shape[-2] >= 2
+                and os.environ.get('VFD_REFLECT_PAD', '1') != '0'):
             from . import kernels as KN
             return F.conv2d(KN.ReflectPad1.apply(x), weight, bias, self.stride, 0, self.dilation, self.groups)
         return super()._conv_forward(x, weight, bias)
@@ -87,12 +95,12 @@ def upsample(x):
 # ----------------------------------------------------------------------------- ResNet encoder
 def bn_act(bn, x, residual=None, relu=True):
     """relu(bn(x) [+ residual]): one fused HIP kernel pair (bnact.hip, SyncBatchNorm-aware) for a
-    training-mode fp32 BatchNorm2d on the GPU; the module + torch ops otherwise (eval mode, bf16
-    autocast, CPU).  VFD_FUSED_BN=0 disables the fused path."""
+    training-mode BatchNorm2d on the GPU, fp32 activations or (under bf16 autocast) bf16 ones with
+    fp32 statistics; the module + torch ops otherwise (eval mode, CPU).  VFD_FUSED_BN=0 disables
+    the fused path."""
     if (bn.training and bn.track_running_stats and bn.affine and bn.momentum is not None and x.is_cuda
-            and x.dim() == 4 and x.dtype == torch.float32 and not torch.is_autocast_enabled('cuda')
-            and os.environ.get('VFD_FUSED_BN', '1') != '0'
-            and (residual is None or residual.shape == x.shape and residual.dtype == x.dtype)):
+            and x.dim() == 4 and _fused_dtype_ok(x) and os.environ.get('VFD_FUSED_BN', '1') != '0'
+            and (residual is None or residual.shape == x.shape)):
         from . import kernels as KN
         return KN.BatchNormAct.apply(x, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var,
                                      bn.eps, bn.momentum, relu, KN._bn_group(bn),
@@ -104,9 +112,9 @@ def bn_act(bn, x, residual=None, relu=True):
 
 
 def max_pool_stem(pool, x):
-    """The stem's MaxPool2d(3, 2, 1): the HIP kernel pair for fp32 GPU maps (one-byte argmax,
-    gather backward), the module otherwise."""
-    if (x.is_cuda and x.dim() == 4 and x.dtype == torch.float32 and pool.kernel_size in (3, (3, 3))
+    """The stem's MaxPool2d(3, 2, 1): the HIP kernel pair for GPU maps, fp32 or bf16 under bf16
+    autocast (one-byte argmax, gather backward), the module otherwise."""
+    if (x.is_cuda and x.dim() == 4 and _fused_dtype_ok(x) and pool.kernel_size in (3, (3, 3))
             and pool.stride in (2, (2, 2)) and pool.padding in (1, (1, 1)) and pool.dilation in (1, (1, 1))
             and not pool.ceil_mode and os.environ.get('VFD_MAXPOOL', '1') != '0'):
         from . import kernels as KN

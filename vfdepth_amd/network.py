@@ -74,10 +74,11 @@ class FusionDepthDecoder(nn.Module):
         self.sigmoid = nn.Sigmoid()
 
     def _fused_ok(self, x):
-        """The HIP chain applies: fp32 GPU maps outside autocast, no skip concatenation, and the
-        blocks are the stock (reflect conv 3x3, Identity, ELU(1.0)) — VFD_ELU_PAD=0 disables it."""
-        if not (x.is_cuda and x.dtype == torch.float32 and not torch.is_autocast_enabled('cuda')
-                and not self.use_skips and os.environ.get('VFD_ELU_PAD', '1') != '0'):
+        """The HIP chain applies: GPU maps (fp32, or bf16 under config 3's bf16 autocast), no skip
+        concatenation, and the blocks are the stock (reflect conv 3x3, Identity, ELU(1.0)) —
+        VFD_ELU_PAD=0 disables it."""
+        from .layers import _fused_dtype_ok
+        if not (x.is_cuda and _fused_dtype_ok(x) and not self.use_skips and os.environ.get('VFD_ELU_PAD', '1') != '0'):
             return False
         for k, blk in self.convs.items():
             conv, norm, act = blk
@@ -150,7 +151,7 @@ class FusedDepthNet(nn.Module):
         imgs = inputs[('color_aug', 0, 0)]
         B, N = imgs.shape[:2]
         with net_autocast(self, imgs):
-            x, normed = _encoder_input([imgs]) if not torch.is_autocast_enabled('cuda') else (pack_cam_feat(imgs), False)
+            x, normed = _encoder_input([imgs])          # fp32, normalised (the stem conv casts under autocast)
             feats, agg = _aggregate(self.encoder, self.conv1x1, x, self.fusion_level, B, N, normed)
             fusion = self.fusion_net(inputs, agg)
             disp = self.decoder(feats[:self.fusion_level] + [fusion['proj_feat']])
@@ -193,10 +194,7 @@ class FusedPoseNet(nn.Module):
         frames = [inputs[('color_aug', frame_ids[0], 0)], inputs[('color_aug', frame_ids[1], 0)]]
         B, N = frames[0].shape[:2]
         with net_autocast(self, frames[0]):
-            if torch.is_autocast_enabled('cuda'):
-                x, normed = pack_cam_feat(torch.cat(frames, 2)), False
-            else:
-                x, normed = _encoder_input(frames)
+            x, normed = _encoder_input(frames)
             _, agg = _aggregate(self.encoder, self.conv1x1, x, self.fusion_level, B, N, normed)
             bev = self.fusion_net(inputs, agg)
             axis_angle, translation = self.pose_decoder([[bev]])

@@ -133,9 +133,9 @@ def pose_hw(s):
 
 def mfma_flops(kernel, s):
     """Dense fp32 MFMA flops of one launch of the matrix-bound ops (None for the HBM-bound ones):
-    K3C = reduce_dim's first conv, 2 * pixels * 256 * (Cv * D * 9); its data gradient the same;
-    K2C = the pose reduce_dim's first conv."""
-    if kernel in ('proj_conv_fwd', 'proj_conv_dgrad'):
+    K3C = reduce_dim's first conv, 2 * pixels * 256 * (Cv * D * 9); its data and weight gradients
+    the same; K2C = the pose reduce_dim's first conv."""
+    if kernel in ('proj_conv_fwd', 'proj_conv_dgrad', 'proj_conv_wgrad'):
         return 2.0 * s['B'] * s['N'] * s['h'] * s['w'] * 256 * s['Cv'] * s['D'] * 9
     if kernel == 'pad_conv_fwd':                                  # K2C, pose reduce_dim[0]: K = (C+1)*Z*9
         return 2.0 * s['B'] * pose_hw(s) * 256 * (s['C'] + 1) * s['Z'] * 9

@@ -334,6 +334,16 @@ size_t vfd_proj_conv_dgrad_workspace(const vfd_voxel_desc* d);
 int vfd_proj_conv_dgrad(const vfd_voxel_desc* d, const float* g_pre, const float* Wd, float* dx, void* workspace,
                         size_t ws_bytes, void* stream);
 
+/* K3C weight / bias gradient (volumetric_fusionnet.py:59-60, 265 backward; replaces the
+ * reference's cudnn weight-gradient of reduce_dim[0]): dw [O = 256, Cv*D, 3, 3] in the reference
+ * channel order c*D + d, db [O], from g_pre [B*N, h, w, O] (NHWC) and the frustum features x
+ * [B*N, h+2, w+2, D*Cv] that vfd_proj_conv_fwd wrote as x_out.  fp32 MFMA, stream-K with a
+ * fixed-order partial sum (deterministic).  dw or db may be null (not computed).
+ * Workspace 0 = shape unsupported (Cv != 64 or D > 64). */
+size_t vfd_proj_conv_wgrad_workspace(const vfd_voxel_desc* d);
+int vfd_proj_conv_wgrad(const vfd_voxel_desc* d, const float* g_pre, const float* x, float* dw, float* db,
+                        void* workspace, size_t ws_bytes, void* stream);
+
 /* ------------------------------------------------------------------ view synthesis (K4) */
 typedef struct vfd_view_desc {
   int32_t B, N, H, W;

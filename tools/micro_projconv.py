@@ -111,6 +111,29 @@ def main():
     derr = float((dx - ref).abs().max()) / float(ref.abs().max())
     print(f'config {a.config}: dgrad kernel {t_dg:.3f} ms (kernel {ms2 / n2:.3f} ms, {flop / (ms2 / n2) / 1e9:.1f} TFLOP/s, '
           f'weight copy incl.); MIOpen dgrad {t_mi:.3f} ms, MIOpen wgrad {t_wg:.3f} ms; max rel err {derr:.2e}', flush=True)
+    # weight / bias gradient: the MFMA kernel (reference channel order) vs MIOpen's + the channel swap
+    nbytes = lib.vfd_proj_conv_wgrad_workspace(ctypes.byref(d))
+    ws2 = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    dw = torch.empty(O, Cv * D, 3, 3, device=dev)
+    db = torch.empty(O, device=dev)
+
+    def wgrad():
+        _lib.check(lib.vfd_proj_conv_wgrad(ctypes.byref(d), g_pre.data_ptr(), xcl.data_ptr(), dw.data_ptr(),
+                                           db.data_ptr(), ws2.data_ptr(), nbytes, _lib.stream()), 'proj_conv_wgrad')
+    t_wk = timed(wgrad, a.iters)
+    _lib.prof_enable('proj_conv_wgrad')
+    for _ in range(a.iters):
+        wgrad()
+    torch.cuda.synchronize()
+    prof = _lib.prof_read()
+    _lib.prof_enable('off')
+    n3, ms3 = prof.get('proj_conv_wgrad', (1, float('nan')))
+    _, dw_ref, db_ref = cb(g_pre, xcl, w0, *args, [False, True, True])
+    dw_ref = KN.weight_swap(dw_ref, D, Cv)
+    werr = float((dw - dw_ref).abs().max()) / float(dw_ref.abs().max())
+    berr = float((db - db_ref).abs().max()) / float(db_ref.abs().max())
+    print(f'config {a.config}: wgrad kernel {t_wk:.3f} ms (kernel {ms3 / n3:.3f} ms, {flop / (ms3 / n3) / 1e9:.1f} TFLOP/s, '
+          f'bias incl.); max rel err dw {werr:.2e} db {berr:.2e}', flush=True)
 
 
 if __name__ == '__main__':

@@ -35,6 +35,7 @@ OPS = {
     'aggregate': ['aggregate_fwd_k'],
     'proj_conv_fwd': ['pcv_main_k', 'pcv_reduce_k'],
     'proj_conv_dgrad': ['pcd_main_k', 'pcd_reduce_k'],
+    'proj_conv_wgrad': ['pcw_main_k', 'pcw_reduce_k', 'pcw_bias_k', 'pcw_bias_fin_k'],
     'pad_conv_fwd': ['ppc_main_k', 'ppc_reduce_k'],
     'depth_syn_fwd': ['depth_syn_fwd_k'],
     'depth_syn_bwd': ['depth_syn_bwd_k'],

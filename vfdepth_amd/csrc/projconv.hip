@@ -529,8 +529,13 @@ static PcGeom pc_plan(const vfd_voxel_desc& d) {
 //   dXp[bc, Y, X, n] = sum_{ty, tx, o} G[bc, Y - ty, X - tx, o] * W[o, n, ty, tx]
 //
 // G = d pre-activation [B*N, h, w, O] (zero outside the h x w grid), n = d*Cv + c (K3's channel
-// order).  M = padded positions (row-major, 128 per tile), N = D*Cv (256 per tile, zero-padded
-// weights past D*Cv), K = 9 taps x O.  An atom = (tile, 32-channel chunk of O): the loader waves
+// order).  M = padded positions of ALL cameras, flattened (row-major, 128 per tile): the cameras'
+// (h+2)-row padded grids are stacked into one tall grid of B*N*(h+2) rows, on which camera bc's
+// G rows y < h sit at virtual rows bc*(h+2) + y and rows h, h+1 are zero, so a tap reaching above
+// a camera's first row reads the previous camera's two zero rows — the stacked problem is exactly
+// the B*N per-camera ones, with one ragged tile in total instead of one per camera (config 2:
+// 193 tiles of 128 for 24 600 positions, 3 % fewer than 6 x 33).  N = D*Cv (256 per tile,
+// zero-padded weights past D*Cv), K = 9 taps x O.  An atom = (tile, 32-channel chunk of O): the loader waves
 // stage the chunk's G rows under the tile (<= hrows rows x (w + 4) columns, zero margins) in LDS
 // while the compute waves run the previous atom's 9 taps x 8 channel quads (same wave roles and
 // fragment pipeline as the forward).  Stream-K over atoms: a tile whole inside one workgroup's
@@ -544,7 +549,7 @@ constexpr int PD_ITERS = 9 * (PD_OC / 4);       // (tap, quad) iterations per at
 constexpr int PD_LDS_MAX = 160 * 1024;
 
 struct PdGeom {
-  int nbc, h, w, wo, npix, mtiles, ntot, np, ntile, natom, ngroup, hrows, cols, lds_floats;
+  int nbc, h, w, wo, npix, mtot, mtiles, ntot, np, ntile, natom, ngroup, hrows, cols, lds_floats;
 };
 
 __host__ __device__ inline int pd_lo(const PdGeom& g, int grp) {
@@ -552,39 +557,41 @@ __host__ __device__ inline int pd_lo(const PdGeom& g, int grp) {
 }
 
 struct PdTile {
-  int nt, bc, mt, m0, ymin;
+  int nt, mt, m0, ymin;
 };
 
-// tile order: n-tile outermost (a workgroup's consecutive tiles share the n-tile's weights)
+// tile order: n-tile outermost (a workgroup's consecutive tiles share the n-tile's weights);
+// m0 / ymin are positions / rows of the stacked grid
 __device__ __forceinline__ PdTile pd_tile(const PdGeom& g, int t) {
   PdTile r;
   r.mt = t % g.mtiles;
-  const int rest = t / g.mtiles;
-  r.bc = rest % g.nbc;
-  r.nt = rest / g.nbc;
+  r.nt = t / g.mtiles;
   r.m0 = r.mt * PC_PIX;
   r.ymin = r.m0 / g.wo;
   return r;
 }
 
-// loader waves (tid 0..255): G rows ymin-2 .. ymin-2+hrows-1, columns -2 .. w+1, channels of chunk ch
+// loader waves (tid 0..255): stacked G rows ymin-2 .. ymin-2+hrows-1, columns -2 .. w+1, channels
+// of chunk ch (zero outside a camera's h x w grid)
 __device__ __forceinline__ void pd_stage(const PdGeom& g, float* __restrict__ dst, const float* __restrict__ gp,
                                          int atom, int tid) {
   const int t = atom / PD_CHUNKS, ch = atom - t * PD_CHUNKS;
   const PdTile tl = pd_tile(g, t);
   const int npos = g.hrows * g.cols;
   const int q = tid & 7;
-  const float* src = gp + (size_t)tl.bc * g.h * g.w * PC_O + ch * PD_OC + 4 * q;
+  const int hp = g.h + 2;
+  const float* src = gp + ch * PD_OC + 4 * q;
   for (int p0 = tid >> 3; p0 < npos; p0 += 4 * 32) {
     float4 v[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int p = p0 + 32 * u;
       const int hr = p / g.cols, c = p - hr * g.cols;
-      const int y = tl.ymin - 2 + hr, x = c - 2;
+      const int r = tl.ymin - 2 + hr, x = c - 2;
+      const int bc = r >= 0 ? r / hp : 0, y = r - bc * hp;
       v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (p < npos && y >= 0 && y < g.h && x >= 0 && x < g.w)
-        v[u] = *reinterpret_cast<const float4*>(src + ((size_t)y * g.w + x) * PC_O);
+      if (p < npos && r >= 0 && bc < g.nbc && y < g.h && x >= 0 && x < g.w)
+        v[u] = *reinterpret_cast<const float4*>(src + (((size_t)bc * g.h + y) * g.w + x) * PC_O);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -633,7 +640,7 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pcd_main_k(PdGeom g, const floa
   auto prefetch = [&](int slot) {
     if (pf_atom < a_hi) {
       const int t = pf_atom / PD_CHUNKS, ch = pf_atom - t * PD_CHUNKS;
-      const int nt = t / (g.mtiles * g.nbc);
+      const int nt = t / g.mtiles;
       const int tap = pf_it >> 3, q = pf_it & 7;
       const float2* w = wlane + ((size_t)(tap * (PC_O / 4) + ch * (PD_OC / 4) + q) * g.np + nt * PD_N) * 2;
       bq[slot][0] = w[0];
@@ -650,7 +657,7 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pcd_main_k(PdGeom g, const floa
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
       int m = tl.m0 + 32 * a + li;
-      m = m < g.npix ? m : g.npix - 1;                 // rows past the grid: computed, never stored
+      m = m < g.mtot ? m : g.mtot - 1;                 // rows past the grid: computed, never stored
       const int Y = m / g.wo, X = m - Y * g.wo;
       aoff[a] = ((Y - tl.ymin) * g.cols + X) * PD_XS + 2 * lh;
     }
@@ -692,7 +699,6 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pcd_main_k(PdGeom g, const floa
     if (ch == PD_CHUNKS - 1 || atom == a_hi - 1) {
       const int ts = t * PD_CHUNKS;
       if (ts >= a_lo && ts + PD_CHUNKS <= a_hi) {     // whole tile in this range: store
-        float* ob = dx + (size_t)tl.bc * g.npix * g.ntot;
 #pragma unroll
         for (int a = 0; a < 4; ++a)
 #pragma unroll
@@ -701,7 +707,7 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pcd_main_k(PdGeom g, const floa
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
               const int m = tl.m0 + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * lh;
-              if (m < g.npix && n < g.ntot) ob[(size_t)m * g.ntot + n] = acc[a][b][r];
+              if (m < g.mtot && n < g.ntot) dx[(size_t)m * g.ntot + n] = acc[a][b][r];
               acc[a][b][r] = 0.f;
             }
           }
@@ -733,7 +739,6 @@ __global__ __launch_bounds__(256) void pcd_reduce_k(PdGeom g, const float* __res
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int c0 = (grp - 1) * 2 + (t == pd_lo(g, grp - 1) / PD_CHUNKS ? 0 : 1), c1 = grp * 2;
   const PdTile tl = pd_tile(g, t);
-  float* ob = dx + (size_t)tl.bc * g.npix * g.ntot;
   constexpr int FPS = 4 * 2 * 16 / PC_FSL;
   for (int f = blockIdx.y * FPS; f < (blockIdx.y + 1) * FPS; ++f) {
     const int a = f >> 5, bb = (f >> 4) & 1, r = f & 15;
@@ -741,7 +746,7 @@ __global__ __launch_bounds__(256) void pcd_reduce_k(PdGeom g, const float* __res
     const float s = partial[(size_t)c0 * PC_FRAG + off] + partial[(size_t)c1 * PC_FRAG + off];
     const int m = tl.m0 + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
     const int n = tl.nt * PD_N + wv * 64 + bb * 32 + (lane & 31);
-    if (m < g.npix && n < g.ntot) ob[(size_t)m * g.ntot + n] = s;
+    if (m < g.mtot && n < g.ntot) dx[(size_t)m * g.ntot + n] = s;
   }
 }
 
@@ -753,10 +758,11 @@ static PdGeom pd_plan(const vfd_voxel_desc& d) {
   g.w = d.w;
   g.wo = d.w + 2;
   g.npix = (d.h + 2) * g.wo;
-  g.mtiles = (g.npix + PC_PIX - 1) / PC_PIX;
+  g.mtot = g.nbc * g.npix;
+  g.mtiles = (g.mtot + PC_PIX - 1) / PC_PIX;
   g.ntot = d.D * PC_CV;
   g.np = (g.ntot + PD_N - 1) / PD_N * PD_N;
-  g.ntile = (g.np / PD_N) * g.nbc * g.mtiles;
+  g.ntile = (g.np / PD_N) * g.mtiles;
   g.natom = g.ntile * PD_CHUNKS;
   g.hrows = 3 + (g.wo + PC_PIX - 2) / g.wo;           // rows under 128 consecutive positions + 2
   g.cols = d.w + 4;
@@ -771,6 +777,221 @@ static bool pd_supported(const vfd_voxel_desc& d) {
   if (d.Cv != PC_CV || d.B <= 0 || d.N <= 0 || d.h < 2 || d.w < 2 || d.D <= 0 || d.D > 64) return false;
   const PdGeom g = pd_plan(d);
   return (size_t)2 * g.lds_floats * sizeof(float) <= PD_LDS_MAX;
+}
+
+// =============================================================================================
+// K3C weight gradient — reduce_dim's first conv, d weight and d bias (volumetric_fusionnet.py:59-60,
+// 265 backward), as an fp32 MFMA GEMM over the pixels of all cameras:
+//
+//   dW[o, n, ky, kx] = sum_{bc, y, x} G[bc, y, x, o] * Xp[bc, y + ky, x + kx, n],   db[o] = sum G
+//
+// G = d pre-activation [B*N, h, w, O] (NHWC), Xp = the frustum features K3C's forward wrote as its
+// side output [B*N, h+2, w+2, D*Cv] (n = d*Cv + c).  M = the 256 output channels, N = 32 frustum
+// channels x 9 taps, K = pixels: an output tile (one 32-channel block of n) is 8 x 9 MFMA blocks;
+// wave w of the 8 owns o-block w and all 9 taps (9 f32x16 accumulators), so one A fragment (G)
+// feeds 9 MFMAs whose B fragments are the 9 tap-shifted X positions of the same LDS halo.  All 8
+// waves compute (two per SIMD, so one wave's LDS waits are covered by the other's MFMAs) and all
+// stage: an atom = (tile, camera, 2 x 16 pixel tile); during atom a each thread's global loads of
+// atom a+1 (its share of 32 G rows x 256 o and the 4 x 18 x 32 Xp halo) are in flight, and land
+// in the other half of a double-buffered LDS image after the wave's MFMAs (one barrier per atom).
+// Stream-K over the atoms (one workgroup per CU, contiguous equal ranges, tile-major): every tile
+// a range meets leaves a partial in MFMA fragment order; `pcw_reduce_k` sums a tile's partials in
+// workgroup order (deterministic) and writes dW straight into the reference layout
+// [O, Cv*D (c*D + d), 3, 3].
+constexpr int PW_WAVES = 8;
+constexpr int PW_NT = 32;                       // frustum channels per tile
+constexpr int PW_TR = 2, PW_TC = 16;            // pixel tile of an atom
+constexpr int PW_PIX = PW_TR * PW_TC;
+constexpr int PW_HR = PW_TR + 2, PW_HC = PW_TC + 2;
+constexpr int PW_NPOS = PW_HR * PW_HC;          // 72 halo positions
+constexpr int PW_GS = PC_O + 32;                // LDS floats per staged G pixel (lane halves on other banks)
+constexpr int PW_XS = PW_NT;                    // LDS floats per staged X position
+constexpr int PW_BUF = PW_PIX * PW_GS + PW_NPOS * PW_XS;
+constexpr int PW_FRAG = PW_WAVES * 9 * 16 * 64;  // floats of one tile's partial
+constexpr int PW_BIAS_BLOCKS = 64;
+constexpr int PW_GV = PW_PIX * PC_O / 4 / PC_THREADS;                    // 4 float4 of G per thread
+constexpr int PW_XV = (PW_NPOS * PW_XS / 4 + PC_THREADS - 1) / PC_THREADS;  // 2 float4 of Xp per thread
+
+struct PwGeom {
+  int nbc, h, w, ntot, D, tc, tiles_img, L, ntile, natom, ngroup, slots;
+};
+
+__host__ __device__ inline long long pw_lo(const PwGeom& g, int grp) {
+  return ((long long)grp * g.natom) / g.ngroup;
+}
+
+struct PwStage {
+  float4 gv[PW_GV], xv[PW_XV];
+};
+
+// a thread's share of atom `atom`: G rows of its 32 pixels and the Xp halo, into registers
+__device__ __forceinline__ void pw_fetch(const PwGeom& g, PwStage& st, const float* __restrict__ gp,
+                                         const float* __restrict__ xp, int atom, int tid) {
+  const int t = atom / g.L, within = atom - t * g.L;
+  const int bc = within / g.tiles_img, ti = within - bc * g.tiles_img;
+  const int y0 = (ti / g.tc) * PW_TR, x0 = (ti % g.tc) * PW_TC;
+  const int wo = g.w + 2;
+#pragma unroll
+  for (int u = 0; u < PW_GV; ++u) {
+    const int e = tid + PC_THREADS * u, px = e >> 6, q = e & 63;
+    const int y = y0 + (px >> 4), x = x0 + (px & 15);
+    st.gv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (y < g.h && x < g.w)
+      st.gv[u] = *reinterpret_cast<const float4*>(gp + (((size_t)bc * g.h + y) * g.w + x) * PC_O + 4 * q);
+  }
+#pragma unroll
+  for (int u = 0; u < PW_XV; ++u) {
+    const int e = tid + PC_THREADS * u, pos = e >> 3, q = e & 7;
+    const int r = pos / PW_HC, c = pos - r * PW_HC;
+    const int Y = y0 + r, X = x0 + c;
+    st.xv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (pos < PW_NPOS && Y < g.h + 2 && X < wo)
+      st.xv[u] = *reinterpret_cast<const float4*>(xp + (((size_t)bc * (g.h + 2) + Y) * wo + X) * g.ntot + t * PW_NT + 4 * q);
+  }
+}
+
+__device__ __forceinline__ void pw_put(const PwStage& st, float* __restrict__ dst, int tid) {
+#pragma unroll
+  for (int u = 0; u < PW_GV; ++u) {
+    const int e = tid + PC_THREADS * u, px = e >> 6, q = e & 63;
+    *reinterpret_cast<float4*>(dst + px * PW_GS + 4 * q) = st.gv[u];
+  }
+  float* xd = dst + PW_PIX * PW_GS;
+#pragma unroll
+  for (int u = 0; u < PW_XV; ++u) {
+    const int e = tid + PC_THREADS * u, pos = e >> 3, q = e & 7;
+    if (pos < PW_NPOS) *reinterpret_cast<float4*>(xd + pos * PW_XS + 4 * q) = st.xv[u];
+  }
+}
+
+__global__ __launch_bounds__(PC_THREADS, 2) void pcw_main_k(PwGeom g, const float* __restrict__ gp,
+                                                           const float* __restrict__ xp,
+                                                           float* __restrict__ partial) {
+  __shared__ float lds[2][PW_BUF];
+  const int grp = blockIdx.x;
+  const int a_lo = (int)pw_lo(g, grp), a_hi = (int)pw_lo(g, grp + 1);
+  if (a_lo >= a_hi) return;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int li = lane & 31, kk = lane >> 5;
+  {
+    PwStage st;
+    pw_fetch(g, st, gp, xp, a_lo, tid);
+    pw_put(st, lds[0], tid);
+  }
+  __syncthreads();
+  f32x16 acc[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[k][r] = 0.f;
+  const int first_tile = a_lo / g.L;
+  int tile = first_tile;
+  auto flush = [&](int tl) {
+    float* dst = partial + (((size_t)grp * g.slots + (tl - first_tile)) * PW_WAVES + wv) * (9 * 16 * 64) + lane;
+#pragma unroll
+    for (int k = 0; k < 9; ++k)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        dst[(k * 16 + r) * 64] = acc[k][r];
+        acc[k][r] = 0.f;
+      }
+  };
+  for (int atom = a_lo; atom < a_hi; ++atom) {
+    const int t = atom / g.L;
+    if (t != tile) {
+      flush(tile);
+      tile = t;
+    }
+    PwStage st;
+    const bool more = atom + 1 < a_hi;
+    if (more) pw_fetch(g, st, gp, xp, atom + 1, tid);        // in flight during this atom's MFMAs
+    const float* gb = lds[(atom - a_lo) & 1] + kk * PW_GS + 32 * wv + li;       // lane's G column
+    const float* xb = lds[(atom - a_lo) & 1] + PW_PIX * PW_GS + kk * PW_XS + li;  // lane's X column
+    // pixel pair s: pixels 2s (lanes 0-31) and 2s+1 (lanes 32-63), one tile row
+#pragma unroll
+    for (int s = 0; s < PW_PIX / 2; ++s) {
+      const int p = 2 * s, py = p >> 4, px = p & 15;
+      const float a = gb[p * PW_GS];
+#pragma unroll
+      for (int k = 0; k < 9; ++k)
+        acc[k] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, xb[((py + k / 3) * PW_HC + px + (k % 3)) * PW_XS], acc[k],
+                                                      0, 0, 0);
+    }
+    if (more) pw_put(st, lds[(atom + 1 - a_lo) & 1], tid);
+    __syncthreads();
+  }
+  flush(tile);
+}
+
+// the workgroup whose range holds atom a
+__device__ __forceinline__ int pw_owner(const PwGeom& g, long long a) {
+  int grp = (int)((a * g.ngroup) / g.natom);
+  while (grp + 1 < g.ngroup && pw_lo(g, grp + 1) <= a) ++grp;
+  while (grp > 0 && pw_lo(g, grp) > a) --grp;
+  return grp;
+}
+
+// one workgroup per (tile, o-block): the tile's partials summed in workgroup order into LDS, then
+// written as dW[o][c*D + d][tap] (runs of 9 taps)
+__global__ __launch_bounds__(256) void pcw_reduce_k(PwGeom g, const float* __restrict__ partial,
+                                                    float* __restrict__ dw) {
+  constexpr int TS = 16 * 64 + 1;                     // LDS floats per tap (odd: taps on other banks)
+  __shared__ float sm[9 * TS];
+  const int t = blockIdx.x, wb = blockIdx.y;
+  const int g0 = pw_owner(g, (long long)t * g.L), g1 = pw_owner(g, (long long)(t + 1) * g.L - 1);
+  for (int f = threadIdx.x; f < 9 * 16 * 64; f += 256) {
+    float s = 0.f;
+    for (int grp = g0; grp <= g1; ++grp) {
+      const int slot = t - (int)(pw_lo(g, grp) / g.L);
+      s += partial[(((size_t)grp * g.slots + slot) * PW_WAVES + wb) * (9 * 16 * 64) + f];
+    }
+    sm[(f >> 10) * TS + (f & 1023)] = s;
+  }
+  __syncthreads();
+  const int cvd = g.ntot;                              // Cv * D
+  for (int e = threadIdx.x; e < 32 * 32 * 9; e += 256) {
+    const int tap = e % 9, cl = (e / 9) & 31, ol = e / 288;
+    const int r = (ol & 3) + 4 * (ol >> 3), ln = cl + 32 * ((ol >> 2) & 1);
+    const int o = 32 * wb + ol;
+    const int n = t * PW_NT + cl, d = n / PC_CV, c = n - d * PC_CV;
+    dw[((size_t)o * cvd + c * g.D + d) * 9 + tap] = sm[tap * TS + r * 64 + ln];
+  }
+}
+
+// d bias: fixed-order column sums of G, PW_BIAS_BLOCKS partial rows then one final row
+__global__ __launch_bounds__(256) void pcw_bias_k(int rows, const float* __restrict__ gp, float* __restrict__ part) {
+  float s = 0.f;
+  for (int r = blockIdx.x; r < rows; r += PW_BIAS_BLOCKS) s += gp[(size_t)r * PC_O + threadIdx.x];
+  part[blockIdx.x * PC_O + threadIdx.x] = s;
+}
+
+__global__ __launch_bounds__(256) void pcw_bias_fin_k(const float* __restrict__ part, float* __restrict__ db) {
+  float s = 0.f;
+  for (int b = 0; b < PW_BIAS_BLOCKS; ++b) s += part[b * PC_O + threadIdx.x];
+  db[threadIdx.x] = s;
+}
+
+static PwGeom pw_plan(const vfd_voxel_desc& d) {
+  PwGeom g;
+  g.nbc = d.B * d.N;
+  g.h = d.h;
+  g.w = d.w;
+  g.D = d.D;
+  g.ntot = d.D * PC_CV;
+  g.tc = (d.w + PW_TC - 1) / PW_TC;
+  g.tiles_img = ((d.h + PW_TR - 1) / PW_TR) * g.tc;
+  g.L = g.nbc * g.tiles_img;
+  g.ntile = g.ntot / PW_NT;
+  g.natom = g.ntile * g.L;
+  const int res = pc_resident();
+  g.ngroup = g.natom < res ? g.natom : res;
+  const long long range = (g.natom + g.ngroup - 1) / g.ngroup;
+  g.slots = (int)((range - 1) / g.L) + 2;
+  return g;
+}
+
+static bool pw_supported(const vfd_voxel_desc& d) {
+  return d.Cv == PC_CV && d.B > 0 && d.N > 0 && d.h >= 1 && d.w >= 1 && d.D > 0 && d.D <= 64;
 }
 
 }  // namespace vfd
@@ -846,6 +1067,33 @@ int vfd_proj_conv_dgrad(const vfd_voxel_desc* d, const float* g_pre, const float
   pcd_main_k<<<g.ngroup, PC_THREADS, lds, s>>>(g, g_pre, Wd, dx, partial);
   pcd_reduce_k<<<dim3(g.ngroup, PC_FSL), 256, 0, s>>>(g, partial, dx);
   return fail_launch("proj_conv_dgrad");
+}
+
+size_t vfd_proj_conv_wgrad_workspace(const vfd_voxel_desc* d) {
+  if (!d || !pw_supported(*d)) return 0;
+  const PwGeom g = pw_plan(*d);
+  return ((size_t)g.ngroup * g.slots * PW_FRAG + PW_BIAS_BLOCKS * PC_O) * sizeof(float);
+}
+
+int vfd_proj_conv_wgrad(const vfd_voxel_desc* d, const float* g_pre, const float* x, float* dw, float* db, void* ws,
+                        size_t ws_bytes, void* stream) {
+  VFD_REQUIRE(d && g_pre && x && (dw || db), "proj_conv_wgrad: null argument");
+  VFD_REQUIRE(pw_supported(*d), "proj_conv_wgrad: unsupported shape (Cv = %d, 0 < D <= 64)", PC_CV);
+  VFD_REQUIRE(ws && ws_bytes >= vfd_proj_conv_wgrad_workspace(d), "proj_conv_wgrad: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  ProfScope ps(K_PROJ_CONV_WGRAD, s);
+  const PwGeom g = pw_plan(*d);
+  float* partial = (float*)ws;
+  if (dw) {
+    pcw_main_k<<<g.ngroup, PC_THREADS, 0, s>>>(g, g_pre, x, partial);
+    pcw_reduce_k<<<dim3(g.ntile, PW_WAVES), 256, 0, s>>>(g, partial, dw);
+  }
+  if (db) {
+    float* part = partial + (size_t)g.ngroup * g.slots * PW_FRAG;
+    pcw_bias_k<<<PW_BIAS_BLOCKS, PC_O, 0, s>>>(g.nbc * g.h * g.w, g_pre, part);
+    pcw_bias_fin_k<<<1, PC_O, 0, s>>>(part, db);
+  }
+  return fail_launch("proj_conv_wgrad");
 }
 
 }  // extern "C"

@@ -394,6 +394,7 @@ def proj_conv_dgrad_weight(w, Cv, D):
 
 
 _PC_DGRAD = os.environ.get('VFD_PC_DGRAD', '1') != '0'
+_PC_WGRAD = os.environ.get('VFD_PC_WGRAD', '1') != '0'
 
 
 def pad_conv_weight_fragments(w, C1=0, Z=0):
@@ -590,8 +591,9 @@ class ProjConv(torch.autograd.Function):
     channels-last input of reduce_dim's second conv, logical [B*N, O, h+2, w+2].
 
     When a gradient is needed the kernel also writes the frustum features themselves (K3's padded
-    channels-last layout) as a side output, so the backward is exactly the unfused one: MIOpen's
-    data / weight gradients and K3's planned backward give d voxel, d weight, d bias."""
+    channels-last layout) as a side output.  Backward: the LeakyReLU + pad adjoint, the data
+    gradient (`vfd_proj_conv_dgrad`) into K3's planned backward (d voxel), and the weight / bias
+    gradient (`vfd_proj_conv_wgrad`, over the side output); all fp32 MFMA, fixed summation order."""
 
     @staticmethod
     @_amp_fwd
@@ -643,38 +645,56 @@ class ProjConv(torch.autograd.Function):
         if mask[0] and _PC_DGRAD:
             nbytes = lib.vfd_proj_conv_dgrad_workspace(ctypes.byref(d))
             if nbytes:
-                # the fused data gradient (fp32 MFMA, projconv.hip); MIOpen then only does d weight
+                # the fused data gradient (fp32 MFMA, projconv.hip)
                 wd = proj_conv_dgrad_weight(w0, Cv, space.D)
                 dx = torch.empty(B * N, Cv * space.D, space.h + 2, space.w + 2, device=g.device,
                                  memory_format=torch.channels_last)
                 ws = _ws(nbytes, g.device)
                 L.check(lib.vfd_proj_conv_dgrad(ctypes.byref(d), g_pre.data_ptr(), wd.data_ptr(), dx.data_ptr(),
                                                 ws.data_ptr(), nbytes, L.stream()), 'proj_conv_dgrad')
+        dw0 = db0 = None
+        wmask = [mask[1], mask[2]]          # what MIOpen still has to compute
+        if (mask[1] or mask[2]) and _PC_WGRAD:
+            nbytes = lib.vfd_proj_conv_wgrad_workspace(ctypes.byref(d))
+            if nbytes:
+                # the fused weight / bias gradient (fp32 MFMA, projconv.hip), straight into the
+                # reference's channel order c*D + d (no swap)
+                dw0 = torch.empty(w0.shape, device=g.device) if mask[1] else None
+                db0 = torch.empty(O, device=g.device) if mask[2] else None
+                ws = _ws(nbytes, g.device)
+                L.check(lib.vfd_proj_conv_wgrad(ctypes.byref(d), g_pre.data_ptr(), x.data_ptr(),
+                                                dw0.data_ptr() if mask[1] else None,
+                                                db0.data_ptr() if mask[2] else None, ws.data_ptr(), nbytes,
+                                                L.stream()), 'proj_conv_wgrad')
+                wmask = [False, False]
+        dw = db = None
         if dx is not None:
-            dw = db = None
-            if mask[1] or mask[2]:
+            if any(wmask):
                 # the weight gradient reads only the weight's shape: w0 has it (no permuted copy)
-                _, dw, db = cb(g_pre, x, w0, *args, [False, mask[1], mask[2]])
+                _, dw, db = cb(g_pre, x, w0, *args, [False] + wmask)
         elif _DGRAD_LAYOUT == 'nchw' and mask[0]:
             # MIOpen's NCHW data-gradient solver (the NHWC one is ~1.5x slower at this shape);
             # the input tensor only supplies shape / memory format to the data gradient
             w_perm = proj_conv_weight(w0, Cv, space.D)
             shape_only = torch.empty(x.shape, device=x.device)
             dx = cb(g_pre.contiguous(), shape_only, w_perm.contiguous(), *args, [True, False, False])[0]
-            _, dw, db = cb(g_pre, x, w0, *args, [False, mask[1], mask[2]])
-        else:
-            dx, dw, db = cb(g_pre, x, proj_conv_weight(w0, Cv, space.D), *args, [mask[0], mask[1], mask[2]])
-        dvox = dw0 = None
+            if any(wmask):
+                _, dw, db = cb(g_pre, x, w0, *args, [False] + wmask)
+        elif mask[0] or any(wmask):
+            dx, dw, db = cb(g_pre, x, proj_conv_weight(w0, Cv, space.D), *args, [mask[0]] + wmask)
+        dvox = None
         if mask[0]:
             dx = _channels_last(dx, 'd frustum features')
             dvox = torch.empty(B, V, Cv, device=g.device)
             L.check(lib.vfd_voxel_project_bwd_planned(ctypes.byref(d), dx.data_ptr(), ctx.plan.data_ptr(),
                                                       ctx.plan.numel(), dvox.data_ptr(), L.stream()),
                     'voxel_project_bwd')
-        if mask[1]:
+        if dw is not None:
             dw0 = weight_swap(dw, space.D, Cv)      # d*Cv + c -> the reference's c*D + d
+        if db is not None:
+            db0 = db
         ctx.plan = None
-        return None, dvox, None, None, dw0, db if mask[2] else None
+        return None, dvox, None, None, dw0, db0
 
 
 def proj_conv_weight_fragments_bf16(w, Cv, D):

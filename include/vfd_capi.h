@@ -166,6 +166,11 @@ typedef struct vfd_bn_desc {
   float eps, momentum;   /* nn.BatchNorm2d eps / momentum                                 */
   int32_t dtype;         /* activations x / residual / y / g / dx / d residual: 0 fp32,
                             1 bf16 (config 3's autocast; statistics and parameters stay fp32 / fp64) */
+  const void* g2;        /* backward (nullable): a second gradient of y, summed into g on load — the
+                            next block's identity branch, so autograd's residual-gradient add and the
+                            d residual tensor of that block never materialise (one rounding of the
+                            sum to the activation type, as autograd's add)                     */
+  const uint8_t* m2;     /* nullable: the next block's ReLU byte mask; g2 counts where it is 1    */
 } vfd_bn_desc;
 
 int vfd_bn_splits(const vfd_bn_desc* d);

@@ -1103,3 +1103,50 @@ def test_inverse4x4_kernel_matches_torch_ops():
     t = geometry.inverse4x4(Eg.clone().requires_grad_(True)).detach()    # torch-ops path (grad)
     assert torch.equal(k, t)
     close(k, torch.linalg.inv(E.double()).float(), '4x4 inverse vs linalg.inv', atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize('blocks,bf16', [(2, False), (4, False), (2, True)])
+def test_residual_join_matches_autograd_add(blocks, bf16):
+    """Residual join (identity blocks: the d residual of block k is summed into block k-1's fused BN
+    backward on load, instead of autograd materialising it and adding the conv branch's gradient):
+    a chain of identity BasicBlocks behind a fused BN gives the same outputs and input / parameter
+    gradients with and without the join (fp32; bf16 under autocast, where the sum is rounded to
+    bf16 once, as autograd's add); bit-identity is checked by the deterministic full-step test.  4 blocks exercise the chain fold (a block that both
+    receives and hands on a join)."""
+    import copy
+    from vfdepth_amd import kernels as KN
+    from vfdepth_amd.layers import BasicBlock, bn_act
+    gen = torch.Generator(device=DEV).manual_seed(301)
+    C = 64
+    stem_bn = torch.nn.BatchNorm2d(C).to(DEV).train()
+    chain = torch.nn.Sequential(*[BasicBlock(C, C) for _ in range(blocks)]).to(DEV).train()
+    with torch.no_grad():
+        for m in chain.modules():
+            if isinstance(m, torch.nn.BatchNorm2d):
+                m.weight.copy_(1 + 0.1 * torch.randn(C, device=DEV, generator=gen))
+                m.bias.copy_(0.1 * torch.randn(C, device=DEV, generator=gen))
+    mods = [(stem_bn, chain), (copy.deepcopy(stem_bn), copy.deepcopy(chain))]
+    x = torch.randn(2, C, 24, 40, device=DEV, generator=gen)
+    gy = torch.randn(2, C, 24, 40, device=DEV, generator=gen)
+    res = []
+    saved = KN._BN_JOIN
+    try:
+        for join, (sb, ch) in zip((True, False), mods):
+            KN._BN_JOIN = join
+            xa = x.clone().requires_grad_(True)
+            with torch.autocast(device_type='cuda', dtype=torch.bfloat16, enabled=bf16):
+                y = ch(bn_act(sb, xa.to(torch.bfloat16) if bf16 else xa))
+            (y.float() * gy).sum().backward()
+            params = [p.grad for p in list(sb.parameters()) + list(ch.parameters())]
+            res.append((y.detach().float(), xa.grad, params))
+    finally:
+        KN._BN_JOIN = saved
+    (ya, ga, pa), (yb, gb, pb) = res
+    # the join itself is exact (the same adds); MIOpen's conv gradients may sum with atomics run to
+    # run (outside deterministic mode: its bf16 weight gradients differ at bf16 rounding level),
+    # hence a rounding-level tolerance
+    rel = 1e-2 if bf16 else 1e-5
+    assert torch.equal(ya, yb), 'outputs differ'
+    gclose(ga, gb, 'input gradient (join vs autograd add)', rel=rel)
+    for i, (a, b) in enumerate(zip(pa, pb)):
+        gclose(a, b, f'parameter {i} gradient (join vs autograd add)', rel=rel)

@@ -79,6 +79,39 @@ __device__ __forceinline__ void relu_mask4(const vfd_bn_desc& d, const T* __rest
   }
 }
 
+// the incoming gradient at element offset o (4 or 1 elements): g, plus the next block's identity-
+// branch gradient g2 (masked by its ReLU byte mask m2) when d.g2 is set — summed in fp32 and
+// rounded once to the activation type, exactly autograd's add of the two tensors
+__device__ __forceinline__ float bn_rnd(float v, const float*) { return v; }
+__device__ __forceinline__ float bn_rnd(float v, const __bf16*) { return (float)(__bf16)v; }
+
+template <typename T>
+__device__ __forceinline__ float4 bn_g4(const vfd_bn_desc& d, const T* __restrict__ g, size_t o) {
+  float4 gv = ld4(g + o);
+  if (d.g2) {
+    float4 h = ld4(reinterpret_cast<const T*>(d.g2) + o);
+    if (d.m2) {
+      const uchar4 m = *reinterpret_cast<const uchar4*>(d.m2 + o);
+      h.x = m.x ? h.x : 0.f;
+      h.y = m.y ? h.y : 0.f;
+      h.z = m.z ? h.z : 0.f;
+      h.w = m.w ? h.w : 0.f;
+    }
+    gv.x = bn_rnd(gv.x + h.x, g);
+    gv.y = bn_rnd(gv.y + h.y, g);
+    gv.z = bn_rnd(gv.z + h.z, g);
+    gv.w = bn_rnd(gv.w + h.w, g);
+  }
+  return gv;
+}
+
+template <typename T>
+__device__ __forceinline__ float bn_g1(const vfd_bn_desc& d, const T* __restrict__ g, size_t o) {
+  float gv = ld1(g + o);
+  if (d.g2 && (!d.m2 || d.m2[o])) gv = bn_rnd(gv + ld1(reinterpret_cast<const T*>(d.g2) + o), g);
+  return gv;
+}
+
 template <typename T>
 __device__ __forceinline__ bool relu_on(const vfd_bn_desc& d, const T* __restrict__ y, size_t o) {
   return d.relu == 2 ? reinterpret_cast<const unsigned char*>(y)[o] != 0 : ld1(y + o) > 0.f;
@@ -224,14 +257,14 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_stats_k(vfd_bn_desc d, cons
   double s1 = 0.0, s2 = 0.0;
   bn_visit(d, c, bn_range(d, split), [&](size_t o, int n) {
     if (n == 4) {
-      float4 gv = ld4(g + o);
+      float4 gv = bn_g4(d, g, o);
       const float4 xv = ld4(x + o);
       if (relu) relu_mask4(d, y, o, gv);
       s1 += ((double)gv.x + (double)gv.y) + ((double)gv.z + (double)gv.w);
       s2 += ((double)gv.x * (double)(xv.x - mean) + (double)gv.y * (double)(xv.y - mean)) +
             ((double)gv.z * (double)(xv.z - mean) + (double)gv.w * (double)(xv.w - mean));
     } else {
-      float gv = ld1(g + o);
+      float gv = bn_g1(d, g, o);
       if (relu && !relu_on(d, y, o)) gv = 0.f;
       s1 += gv;
       s2 += (double)gv * (double)(ld1(x + o) - mean);
@@ -271,7 +304,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply_k(vfd_bn_desc d, cons
   const bool relu = d.relu != 0;
   bn_visit(d, c, bn_range(d, split), [&](size_t o, int n) {
     if (n == 4) {
-      float4 gv = ld4(g + o);
+      float4 gv = bn_g4(d, g, o);
       const float4 xv = ld4(x + o);
       if (relu) relu_mask4(d, y, o, gv);
       if (dr) st4(dr + o, gv);
@@ -284,7 +317,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply_k(vfd_bn_desc d, cons
         st4(dx + o, o4);
       }
     } else {
-      float gv = ld1(g + o);
+      float gv = bn_g1(d, g, o);
       if (relu && !relu_on(d, y, o)) gv = 0.f;
       if (dr) st1(dr + o, gv);
       if (dx) st1(dx + o, k * (gv - mg - (ld1(x + o) - mean) * mx));
@@ -411,14 +444,14 @@ __global__ __launch_bounds__(BN1_THREADS) void bn1_bwd_k(vfd_bn_desc d, const T*
   double s1 = 0.0, s2 = 0.0;
   bn1_visit(d, c, [&](size_t o, int n) {
     if (n == 4) {
-      float4 gv = ld4(g + o);
+      float4 gv = bn_g4(d, g, o);
       const float4 xv = ld4(x + o);
       if (relu) relu_mask4(d, y, o, gv);
       s1 += ((double)gv.x + (double)gv.y) + ((double)gv.z + (double)gv.w);
       s2 += ((double)gv.x * (double)(xv.x - mean) + (double)gv.y * (double)(xv.y - mean)) +
             ((double)gv.z * (double)(xv.z - mean) + (double)gv.w * (double)(xv.w - mean));
     } else {
-      float gv = ld1(g + o);
+      float gv = bn_g1(d, g, o);
       if (relu && !relu_on(d, y, o)) gv = 0.f;
       s1 += gv;
       s2 += (double)gv * (double)(ld1(x + o) - mean);
@@ -435,7 +468,7 @@ __global__ __launch_bounds__(BN1_THREADS) void bn1_bwd_k(vfd_bn_desc d, const T*
   const float mx = (float)(sgx / count) * invstd * invstd;
   bn1_visit(d, c, [&](size_t o, int n) {
     if (n == 4) {
-      float4 gv = ld4(g + o);
+      float4 gv = bn_g4(d, g, o);
       const float4 xv = ld4(x + o);
       if (relu) relu_mask4(d, y, o, gv);
       if (dr) st4(dr + o, gv);
@@ -448,7 +481,7 @@ __global__ __launch_bounds__(BN1_THREADS) void bn1_bwd_k(vfd_bn_desc d, const T*
         st4(dx + o, o4);
       }
     } else {
-      float gv = ld1(g + o);
+      float gv = bn_g1(d, g, o);
       if (relu && !relu_on(d, y, o)) gv = 0.f;
       if (dr) st1(dr + o, gv);
       if (dx) st1(dx + o, k * (gv - mg - (ld1(x + o) - mean) * mx));

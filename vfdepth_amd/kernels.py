@@ -1085,6 +1085,7 @@ class AggregateUp(torch.autograd.Function):
 # Fused training-mode BatchNorm (+ residual) (+ ReLU) of the ResNet encoders (bnact.hip)
 # =============================================================================================
 _BN_ONE = os.environ.get('VFD_BN_ONE', '1') != '0'      # one-launch BN for small layers
+_BN_JOIN = os.environ.get('VFD_BN_JOIN', '1') != '0'    # residual join (BatchNormAct.forward)
 _DEC_CONV = os.environ.get('VFD_DEC_CONV', '1') != '0'   # decoder's narrow convs on MFMA (decconv.hip)
 
 
@@ -1118,7 +1119,8 @@ class BatchNormAct(torch.autograd.Function):
     (None = local statistics)."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, residual, running_mean, running_var, eps, momentum, relu, pg, nbt=None):
+    def forward(ctx, x, gamma, beta, residual, running_mean, running_var, eps, momentum, relu, pg, nbt=None,
+                join=False):
         lib = L.load()
         _check_device(x, 'batch norm input')
         if x.dtype not in (torch.float32, torch.bfloat16):
@@ -1129,6 +1131,15 @@ class BatchNormAct(torch.autograd.Function):
         d = L.BnDesc(N, C, H * W, 0, int(relu), float(eps), float(momentum), int(x.dtype == torch.bfloat16))
         d.S = lib.vfd_bn_splits(ctypes.byref(d))
         r = residual.to(x.dtype).contiguous() if residual is not None else None
+        # residual join: when the residual is the output of the previous block's fused BN (an
+        # identity block), this layer's d residual (= g masked by its ReLU) is handed to that BN's
+        # backward, which sums it into its own incoming gradient on load — no d residual tensor and
+        # no autograd add of the two branches (the sum is the same fp32 add autograd performs)
+        ctx.pending = []
+        ctx.res_node = None
+        if (join and _BN_JOIN and r is residual and residual.requires_grad
+                and type(residual.grad_fn).__name__ == 'BatchNormActBackward'):
+            ctx.res_node = residual.grad_fn
         ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
         # with ReLU the forward also stores [y > 0] as one byte per element: the backward reads
         # that mask instead of y (d.relu == 2 there), a quarter of the bytes
@@ -1180,25 +1191,38 @@ class BatchNormAct(torch.autograd.Function):
         g = g.to(x.dtype).contiguous()
         need = ctx.needs_input_grad
         ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+        # the next block's identity-branch gradient, deposited by its backward (residual join)
+        pending, ctx.pending = ctx.pending, []
+        joined = ctx.res_node is not None and need[3]
+        # a join chain (this block both receives and hands on an identity-branch gradient, deeper
+        # ResNets) and extra deposits fold with autograd's own adds; one deposit rides in the kernel
+        for g2, m2 in (pending if joined else pending[1:]):
+            g = g + (g2 * m2 if m2 is not None else g2)
+        if pending and not joined:
+            d.g2, d.m2 = pending[0][0].data_ptr(), ptr(pending[0][1])
+        if joined:      # hand d residual = g (ReLU-masked on load) to the block that produced r
+            ctx.res_node.pending.append((g, mk if d.relu else None))
+            ctx.res_node = None
+        want_dr = ctx.has_res and need[3] and not joined
         if ctx.one:
             dx = torch.empty_like(x) if need[0] else None
-            dr = torch.empty_like(x) if ctx.has_res and need[3] else None
+            dr = torch.empty_like(x) if want_dr else None
             dgamma = torch.empty_like(gamma) if need[1] else None
             dbeta = torch.empty_like(gamma) if need[2] else None
             if L.PROF_ON:
                 es = x.element_size()
-                L.ALG_BYTES['bn_bwd'] += x.numel() * (2 * es + (d.relu != 0) + es * ((dx is not None) + (dr is not None)))
+                L.ALG_BYTES['bn_bwd'] += x.numel() * (2 * es + (d.relu != 0) + es * ((dx is not None) + (dr is not None))
+                                                      + (es + (d.m2 is not None)) * (d.g2 is not None))
             L.check(lib.vfd_bn1_bwd(ctypes.byref(d), g.data_ptr(), mk.data_ptr() if d.relu else None, x.data_ptr(),
                                     gamma.data_ptr(), mean.data_ptr(), invstd.data_ptr(), ptr(dx), ptr(dr),
                                     ptr(dgamma), ptr(dbeta), L.stream()), 'bn1_bwd')
-            return dx, dgamma, dbeta, dr, None, None, None, None, None, None, None
+            return dx, dgamma, dbeta, dr, None, None, None, None, None, None, None, None
         partial = torch.empty(d.C, d.S, 2, dtype=torch.float64, device=g.device)
         yp = mk.data_ptr() if d.relu else None
         L.check(lib.vfd_bn_bwd_stats(ctypes.byref(d), g.data_ptr(), yp, x.data_ptr(), mean.data_ptr(),
                                      partial.data_ptr(), L.stream()), 'bn_bwd_stats')
-        need = ctx.needs_input_grad
         dx = torch.empty_like(x) if need[0] else None
-        dr = torch.empty_like(x) if ctx.has_res and need[3] else None
+        dr = torch.empty_like(x) if want_dr else None
         dgamma = torch.empty_like(gamma) if need[1] else None
         dbeta = torch.empty_like(gamma) if need[2] else None
         ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
@@ -1209,11 +1233,12 @@ class BatchNormAct(torch.autograd.Function):
             count, pg_dgamma, pg_dbeta = 0.0, None, None
         if L.PROF_ON:                        # compulsory: g, x (, the mask) in, dx (, dr) out
             es = x.element_size()
-            L.ALG_BYTES['bn_bwd'] += x.numel() * (2 * es + (d.relu != 0) + es * ((dx is not None) + (dr is not None)))
+            L.ALG_BYTES['bn_bwd'] += x.numel() * (2 * es + (d.relu != 0) + es * ((dx is not None) + (dr is not None))
+                                                  + (es + (d.m2 is not None)) * (d.g2 is not None))
         L.check(lib.vfd_bn_bwd_apply(ctypes.byref(d), g.data_ptr(), yp, x.data_ptr(), sums.data_ptr(), ns, count,
                                      gamma.data_ptr(), mean.data_ptr(), invstd.data_ptr(), ptr(dx), ptr(dr),
                                      ptr(pg_dgamma), ptr(pg_dbeta), L.stream()), 'bn_bwd_apply')
-        return dx, dgamma, dbeta, dr, None, None, None, None, None, None, None
+        return dx, dgamma, dbeta, dr, None, None, None, None, None, None, None, None
 
 
 # =============================================================================================

@@ -93,18 +93,19 @@ def upsample(x):
 
 
 # ----------------------------------------------------------------------------- ResNet encoder
-def bn_act(bn, x, residual=None, relu=True):
+def bn_act(bn, x, residual=None, relu=True, join=False):
     """relu(bn(x) [+ residual]): one fused HIP kernel pair (bnact.hip, SyncBatchNorm-aware) for a
     training-mode BatchNorm2d on the GPU, fp32 activations or (under bf16 autocast) bf16 ones with
     fp32 statistics; the module + torch ops otherwise (eval mode, CPU).  VFD_FUSED_BN=0 disables
-    the fused path."""
+    the fused path.  join: the residual is this block's input and also feeds its first conv (an
+    identity block): its gradient is summed inside the producing BN's backward kernels."""
     if (bn.training and bn.track_running_stats and bn.affine and bn.momentum is not None and x.is_cuda
             and x.dim() == 4 and _fused_dtype_ok(x) and os.environ.get('VFD_FUSED_BN', '1') != '0'
             and (residual is None or residual.shape == x.shape)):
         from . import kernels as KN
         return KN.BatchNormAct.apply(x, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var,
                                      bn.eps, bn.momentum, relu, KN._bn_group(bn),
-                                     bn.num_batches_tracked)      # += 1 inside the apply kernel
+                                     bn.num_batches_tracked, join)      # += 1 inside the apply kernel
     y = bn(x)
     if residual is not None:
         y = y + residual
@@ -137,7 +138,7 @@ class BasicBlock(nn.Module):
     def forward(self, x):
         idt = x if self.downsample is None else bn_act(self.downsample[1], self.downsample[0](x), relu=False)
         y = bn_act(self.bn1, self.conv1(x))
-        return bn_act(self.bn2, self.conv2(y), residual=idt)
+        return bn_act(self.bn2, self.conv2(y), residual=idt, join=self.downsample is None)
 
 
 class Bottleneck(nn.Module):
@@ -158,7 +159,7 @@ class Bottleneck(nn.Module):
         idt = x if self.downsample is None else bn_act(self.downsample[1], self.downsample[0](x), relu=False)
         y = bn_act(self.bn1, self.conv1(x))
         y = bn_act(self.bn2, self.conv2(y))
-        return bn_act(self.bn3, self.conv3(y), residual=idt)
+        return bn_act(self.bn3, self.conv3(y), residual=idt, join=self.downsample is None)
 
 
 _RESNET_SPECS = {18: (BasicBlock, [2, 2, 2, 2]), 34: (BasicBlock, [3, 4, 6, 3]),

@@ -808,7 +808,6 @@ constexpr int PW_GS = PC_O + 32;                // LDS floats per staged G pixel
 constexpr int PW_XS = PW_NT;                    // LDS floats per staged X position
 constexpr int PW_BUF = PW_PIX * PW_GS + PW_NPOS * PW_XS;
 constexpr int PW_FRAG = PW_WAVES * 9 * 16 * 64;  // floats of one tile's partial
-constexpr int PW_BIAS_BLOCKS = 64;
 constexpr int PW_GV = PW_PIX * PC_O / 4 / PC_THREADS;                    // 4 float4 of G per thread
 constexpr int PW_XV = (PW_NPOS * PW_XS / 4 + PC_THREADS - 1) / PC_THREADS;  // 2 float4 of Xp per thread
 
@@ -931,44 +930,100 @@ __device__ __forceinline__ int pw_owner(const PwGeom& g, long long a) {
   return grp;
 }
 
-// one workgroup per (tile, o-block): the tile's partials summed in workgroup order into LDS, then
-// written as dW[o][c*D + d][tap] (runs of 9 taps)
+// Workgroup (o quad, c half, chunk of PW_DC depth bins): the partials of the chunk's tiles (tile =
+// 32-channel block n / 32 = 2d + c half) for the quad's 4 output channels, summed in workgroup
+// order into LDS (128-B runs of the fragments), then written as dW[o][c*D + d][tap]: runs of
+// PW_DC * 9 consecutive floats per (o, c), whole cache lines instead of 36-B pieces.
+constexpr int PW_DC = 10;
+
+constexpr int PW_MAXC = 16;     // contributors of one tile the reduce handles (host-checked)
+
 __global__ __launch_bounds__(256) void pcw_reduce_k(PwGeom g, const float* __restrict__ partial,
                                                     float* __restrict__ dw) {
-  constexpr int TS = 16 * 64 + 1;                     // LDS floats per tap (odd: taps on other banks)
-  __shared__ float sm[9 * TS];
-  const int t = blockIdx.x, wb = blockIdx.y;
-  const int g0 = pw_owner(g, (long long)t * g.L), g1 = pw_owner(g, (long long)(t + 1) * g.L - 1);
-  for (int f = threadIdx.x; f < 9 * 16 * 64; f += 256) {
-    float s = 0.f;
+  __shared__ float sm[PW_DC * 4 * 32 * 9];
+  __shared__ long long off[PW_DC][PW_MAXC];
+  __shared__ int ncon[PW_DC];
+  const int oq = blockIdx.x, ch = blockIdx.y & 1, d0 = (blockIdx.y >> 1) * PW_DC;
+  const int nd = g.D - d0 < PW_DC ? g.D - d0 : PW_DC;
+  const int wb = oq >> 3, lh = oq & 1, rb = ((oq & 7) >> 1) * 4;
+  if (threadIdx.x < nd) {          // the chunk's tiles: contributing workgroups, in order
+    const int dl = threadIdx.x, t = 2 * (d0 + dl) + ch;
+    const int g0 = pw_owner(g, (long long)t * g.L), g1 = pw_owner(g, (long long)(t + 1) * g.L - 1);
+    ncon[dl] = g1 - g0 + 1;
     for (int grp = g0; grp <= g1; ++grp) {
       const int slot = t - (int)(pw_lo(g, grp) / g.L);
-      s += partial[(((size_t)grp * g.slots + slot) * PW_WAVES + wb) * (9 * 16 * 64) + f];
+      off[dl][grp - g0] = (((long long)grp * g.slots + slot) * PW_WAVES + wb) * (9 * 16 * 64);
     }
-    sm[(f >> 10) * TS + (f & 1023)] = s;
   }
   __syncthreads();
-  const int cvd = g.ntot;                              // Cv * D
-  for (int e = threadIdx.x; e < 32 * 32 * 9; e += 256) {
-    const int tap = e % 9, cl = (e / 9) & 31, ol = e / 288;
-    const int r = (ol & 3) + 4 * (ol >> 3), ln = cl + 32 * ((ol >> 2) & 1);
-    const int o = 32 * wb + ol;
-    const int n = t * PW_NT + cl, d = n / PC_CV, c = n - d * PC_CV;
-    dw[((size_t)o * cvd + c * g.D + d) * 9 + tap] = sm[tap * TS + r * 64 + ln];
+  // 4 elements per thread per pass, every contributor load of the 4 in flight before the sums
+  // (contributors beyond the fourth: a plain loop; they occur only for very short ranges)
+  constexpr int U = 4;
+  const int total = nd * 4 * 32 * 9;
+  for (int e0 = threadIdx.x; e0 < total; e0 += 256 * U) {
+    float a[U][4];
+    int fo[U], dls[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + 256 * u;
+      const int ee = e < total ? e : total - 1;
+      const int cl = ee & 31, ol = (ee >> 5) & 3, tap = (ee >> 7) % 9, dl = ee / (4 * 32 * 9);
+      fo[u] = (tap * 16 + rb + ol) * 64 + cl + 32 * lh;
+      dls[u] = dl;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a[u][k] = k < ncon[dl] ? partial[off[dl][k] + fo[u]] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + 256 * u;
+      if (e >= total) break;
+      float v = ((a[u][0] + a[u][1]) + a[u][2]) + a[u][3];
+      for (int k = 4; k < ncon[dls[u]]; ++k) v += partial[off[dls[u]][k] + fo[u]];
+      const int cl = e & 31, ol = (e >> 5) & 3, tap = (e >> 7) % 9;
+      sm[((dls[u] * 4 + ol) * 32 + cl) * 9 + tap] = v;
+    }
+  }
+  __syncthreads();
+  const int run = nd * 9;
+  for (int e = threadIdx.x; e < 4 * 32 * run; e += 256) {
+    const int k = e % run, oc = e / run, cl = oc & 31, ol = oc >> 5;
+    const int dl = k / 9, tap = k - dl * 9;
+    const int o = 4 * oq + ol, c = 32 * ch + cl;
+    dw[((size_t)o * g.ntot + c * g.D + d0) * 9 + k] = sm[((dl * 4 + ol) * 32 + cl) * 9 + tap];
   }
 }
 
-// d bias: fixed-order column sums of G, PW_BIAS_BLOCKS partial rows then one final row
+// d bias: fixed-order column sums of G — blocks of PW_BIAS_ROWS rows, then the block partials
+constexpr int PW_BIAS_ROWS = 64;
+
 __global__ __launch_bounds__(256) void pcw_bias_k(int rows, const float* __restrict__ gp, float* __restrict__ part) {
+  const int r0 = blockIdx.x * PW_BIAS_ROWS;
+  const int r1 = r0 + PW_BIAS_ROWS < rows ? r0 + PW_BIAS_ROWS : rows;
   float s = 0.f;
-  for (int r = blockIdx.x; r < rows; r += PW_BIAS_BLOCKS) s += gp[(size_t)r * PC_O + threadIdx.x];
+  for (int r = r0; r < r1; r += 8) {            // 8 rows in flight, summed in row order
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = r + k < r1 ? gp[(size_t)(r + k) * PC_O + threadIdx.x] : 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += v[k];
+  }
   part[blockIdx.x * PC_O + threadIdx.x] = s;
 }
 
-__global__ __launch_bounds__(256) void pcw_bias_fin_k(const float* __restrict__ part, float* __restrict__ db) {
+// workgroup = 4 channels x 64 lanes: lane j sums partial rows j, j + 64, ... of its channel, then
+// the 64 lane sums are added in lane order
+__global__ __launch_bounds__(256) void pcw_bias_fin_k(int nblk, const float* __restrict__ part, float* __restrict__ db) {
+  __shared__ float sh[4][64];
+  const int c = 4 * blockIdx.x + (threadIdx.x & 3), j = threadIdx.x >> 2;
   float s = 0.f;
-  for (int b = 0; b < PW_BIAS_BLOCKS; ++b) s += part[b * PC_O + threadIdx.x];
-  db[threadIdx.x] = s;
+  for (int b = j; b < nblk; b += 64) s += part[b * PC_O + c];
+  sh[threadIdx.x & 3][j] = s;
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    float t = 0.f;
+    for (int k = 0; k < 64; ++k) t += sh[threadIdx.x][k];
+    db[4 * blockIdx.x + threadIdx.x] = t;
+  }
 }
 
 static PwGeom pw_plan(const vfd_voxel_desc& d) {
@@ -991,7 +1046,10 @@ static PwGeom pw_plan(const vfd_voxel_desc& d) {
 }
 
 static bool pw_supported(const vfd_voxel_desc& d) {
-  return d.Cv == PC_CV && d.B > 0 && d.N > 0 && d.h >= 1 && d.w >= 1 && d.D > 0 && d.D <= 64;
+  if (!(d.Cv == PC_CV && d.B > 0 && d.N > 0 && d.h >= 1 && d.w >= 1 && d.D > 0 && d.D <= 64)) return false;
+  const PwGeom g = pw_plan(d);
+  const long long range = g.natom / g.ngroup;           // shortest range
+  return range > 0 && (g.L + range - 1) / range + 1 <= PW_MAXC;   // workgroups meeting one tile
 }
 
 }  // namespace vfd
@@ -1072,7 +1130,8 @@ int vfd_proj_conv_dgrad(const vfd_voxel_desc* d, const float* g_pre, const float
 size_t vfd_proj_conv_wgrad_workspace(const vfd_voxel_desc* d) {
   if (!d || !pw_supported(*d)) return 0;
   const PwGeom g = pw_plan(*d);
-  return ((size_t)g.ngroup * g.slots * PW_FRAG + PW_BIAS_BLOCKS * PC_O) * sizeof(float);
+  const int nblk = (g.nbc * g.h * g.w + PW_BIAS_ROWS - 1) / PW_BIAS_ROWS;
+  return ((size_t)g.ngroup * g.slots * PW_FRAG + (size_t)nblk * PC_O) * sizeof(float);
 }
 
 int vfd_proj_conv_wgrad(const vfd_voxel_desc* d, const float* g_pre, const float* x, float* dw, float* db, void* ws,
@@ -1086,12 +1145,13 @@ int vfd_proj_conv_wgrad(const vfd_voxel_desc* d, const float* g_pre, const float
   float* partial = (float*)ws;
   if (dw) {
     pcw_main_k<<<g.ngroup, PC_THREADS, 0, s>>>(g, g_pre, x, partial);
-    pcw_reduce_k<<<dim3(g.ntile, PW_WAVES), 256, 0, s>>>(g, partial, dw);
+    pcw_reduce_k<<<dim3(PC_O / 4, 2 * ((d->D + PW_DC - 1) / PW_DC)), 256, 0, s>>>(g, partial, dw);
   }
   if (db) {
     float* part = partial + (size_t)g.ngroup * g.slots * PW_FRAG;
-    pcw_bias_k<<<PW_BIAS_BLOCKS, PC_O, 0, s>>>(g.nbc * g.h * g.w, g_pre, part);
-    pcw_bias_fin_k<<<1, PC_O, 0, s>>>(part, db);
+    const int rows = g.nbc * g.h * g.w, nblk = (rows + PW_BIAS_ROWS - 1) / PW_BIAS_ROWS;
+    pcw_bias_k<<<nblk, PC_O, 0, s>>>(rows, g_pre, part);
+    pcw_bias_fin_k<<<PC_O / 4, 256, 0, s>>>(nblk, part, db);
   }
   return fail_launch("proj_conv_wgrad");
 }

@@ -32,32 +32,48 @@ OPS = {
     'photo_bwd': ['photo_bwd_k'],
     'smooth_fwd': ['smooth_fwd_k', 'smooth_finalize_k'],
     'smooth_bwd': ['smooth_bwd_k'],
-    'aggregate': ['aggregate_fwd_k'],
-    'proj_conv_fwd': ['pcv_main_k', 'pcv_reduce_k'],
+    'aggregate': ['aggregate_fwd_k', 'aggregate_plane_fwd_k'],
+    'proj_conv_fwd': ['pcv_main_k', 'pcvb_main_k', 'pcv_reduce_k'],
     'proj_conv_dgrad': ['pcd_main_k', 'pcd_reduce_k'],
     'proj_conv_wgrad': ['pcw_main_k', 'pcw_reduce_k', 'pcw_bias_k', 'pcw_bias_fin_k'],
-    'pad_conv_fwd': ['ppc_main_k', 'ppc_reduce_k'],
+    'pad_conv_fwd': ['ppc_main_k', 'ppcb_main_k', 'ppc_reduce_k'],
     'depth_syn_fwd': ['depth_syn_fwd_k'],
     'depth_syn_bwd': ['depth_syn_bwd_k'],
-    'bn_fwd': ['bn_stats_k', 'bn_sum_k', 'bn_apply_k'],
-    'bn_bwd': ['bn_bwd_stats_k', 'bn_bwd_apply_k'],
+    'bn_fwd': ['bn_stats_k', 'bn_sum_k', 'bn_apply_k', 'bn1_fwd_k'],
+    'bn_bwd': ['bn_bwd_stats_k', 'bn_bwd_apply_k', 'bn1_bwd_k'],
     'reflect_pad': ['reflect_pad_fwd_k', 'reflect_pad_bwd_k', 'lrelu_pad_bwd_nhwc_k'],
-    'upsample_bwd': ['up_ac_bwd_x_k', 'up_ac_bwd_y_k'],
+    'upsample_bwd': ['up_ac_bwd_x_k', 'up_ac_bwd_y_k', 'aggregate_plane_bwd_k'],
     'maxpool': ['maxpool_fwd_k', 'maxpool_bwd_k'],
+    'elu_pad': ['elu_up_pad_fwd_k', 'elu_up_pad_bwd_k'],
+    'disp_conv': ['disp_conv_fwd_k', 'disp_conv_dgrad_k', 'disp_conv_wgrad_k'],
+    'dec_conv': ['dconv_fwd_k', 'dconv_dgrad_k', 'dconv_wgrad_k'],
 }
 # Ops timed as several separate C-ABI calls (one ProfScope each, the bench's launch unit): the
 # traffic is per call of any of these kernels, not per launch of the first one.
 ENTRY = {
-    'bn_fwd': ['bn_stats_k', 'bn_apply_k'],
-    'bn_bwd': ['bn_bwd_stats_k', 'bn_bwd_apply_k'],
+    'aggregate': ['aggregate_fwd_k', 'aggregate_plane_fwd_k'],
+    'bn_fwd': ['bn_stats_k', 'bn_apply_k', 'bn1_fwd_k'],
+    'bn_bwd': ['bn_bwd_stats_k', 'bn_bwd_apply_k', 'bn1_bwd_k'],
+    'upsample_bwd': ['up_ac_bwd_x_k', 'aggregate_plane_bwd_k'],
+    'elu_pad': ['elu_up_pad_fwd_k', 'elu_up_pad_bwd_k'],
+    'disp_conv': ['disp_conv_fwd_k', 'disp_conv_dgrad_k'],
+    'dec_conv': ['dconv_fwd_k', 'dconv_dgrad_k'],
     'reflect_pad': ['reflect_pad_fwd_k', 'reflect_pad_bwd_k', 'lrelu_pad_bwd_nhwc_k'],
     'maxpool': ['maxpool_fwd_k', 'maxpool_bwd_k'],
 }
 
 
 def kernel_of(name):
+    """vfd kernel base name from a demangled ('vfd::bn_apply_k<float>(...)') or, as rocprofv3
+    leaves the bf16 template instances, mangled ('_ZN3vfd10bn_apply_kIDF16bEEv...') name."""
     m = re.search(r'vfd::(\w+)', name)
-    return m.group(1) if m else None
+    if m:
+        return m.group(1)
+    m = re.match(r'_ZN3vfd(\d+)', name)
+    if m:
+        n = int(m.group(1))
+        return name[m.end():m.end() + n]
+    return None
 
 
 def load(path, counter):

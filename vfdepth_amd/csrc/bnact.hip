@@ -54,6 +54,7 @@ __device__ __forceinline__ double block_sum(double v, double* sh) {
 template <typename F>
 __device__ __forceinline__ void bn_visit(const vfd_bn_desc& d, int c, BnRange r, F&& f) {
   if ((d.HW & 3) == 0) {
+#pragma unroll 2
     for (unsigned e = r.lo + 4 * threadIdx.x; e < r.hi; e += 4 * BN_THREADS) f(bn_off(d, c, e), 4);
   } else {
     for (unsigned e = r.lo + threadIdx.x; e < r.hi; e += BN_THREADS) f(bn_off(d, c, e), 1);
@@ -169,15 +170,19 @@ __global__ void bn_sum_k(vfd_bn_desc d, const double* __restrict__ partial, doub
 }
 
 // per-channel sums of the block's channel: from the S partials, or (ns == 1) already reduced
+// channel c's sums from its ns partials, by the whole block: thread i loads partial i (ns <= a few
+// hundred), then a fixed-order block reduction — one round of loads instead of a serial chain of
+// ns dependent ones in every thread (which dominated the apply kernels of the small layers)
 __device__ __forceinline__ void bn_channel_sums(const double* __restrict__ part, int ns, int c, double* a,
                                                 double* b) {
+  __shared__ double sh[BN_THREADS / 64];
   double s1 = 0.0, s2 = 0.0;
-  for (int s = 0; s < ns; ++s) {
+  for (int s = threadIdx.x; s < ns; s += BN_THREADS) {
     s1 += part[((size_t)c * ns + s) * 2];
     s2 += part[((size_t)c * ns + s) * 2 + 1];
   }
-  *a = s1;
-  *b = s2;
+  *a = block_sum(s1, sh);
+  *b = block_sum(s2, sh);
 }
 
 // y = relu((x - mean) * invstd * gamma + beta [+ r]); block (0, c) also stores mean / invstd and

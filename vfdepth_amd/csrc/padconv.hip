@@ -29,7 +29,7 @@ constexpr int PP_PF = 4;                        // weight-fragment prefetch dist
 constexpr int PP_FRAG = PP_PIX * PP_O;          // floats of one tile's partial
 constexpr int PP_LDS_MAX = 160 * 1024;
 constexpr int PP_MAXC = 96;                     // contributors of one tile
-constexpr int PP_FSL = 8;                       // fragment slices per tile in the reduce
+constexpr int PP_FSL = 32;                      // fragment slices per tile in the reduce
 
 struct PpGeom {
   int B, hp, wp, cin, s, ho, wo, mimg, mtiles, nchunk, cq, ntile, natom, ngroup, hrows, lds_floats;
@@ -383,13 +383,14 @@ __global__ __launch_bounds__(256) void ppc_reduce_k(PpGeom g, const float* __res
   const int nc = ncontrib;
   const PpTile tl = pp_tile(g, t);
   constexpr int FPS = 4 * 2 * 16 / PP_FSL;
-  for (int f = blockIdx.y * FPS; f < (blockIdx.y + 1) * FPS; ++f) {
+  float su[FPS];
+  frag_sums<FPS>(partial, contrib, nc, PP_FRAG, (size_t)wv * (PP_FRAG / PP_WAVES) + (blockIdx.y * FPS * 64 + lane), su);
+#pragma unroll
+  for (int u = 0; u < FPS; ++u) {
+    const int f = blockIdx.y * FPS + u;
     const int a = f >> 5, bb = (f >> 4) & 1, r = f & 15;
-    float s = 0.f;
-    for (int k = 0; k < nc; ++k)
-      s += partial[(size_t)contrib[k] * PP_FRAG + (size_t)wv * (PP_FRAG / PP_WAVES) + (f * 64 + lane)];
     const int m = tl.m0 + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-    pp_store(g, out, bias, tl.b, m, wv * 64 + bb * 32 + (lane & 31), s);
+    pp_store(g, out, bias, tl.b, m, wv * 64 + bb * 32 + (lane & 31), su[u]);
   }
 }
 

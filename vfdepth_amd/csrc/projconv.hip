@@ -483,11 +483,15 @@ __global__ __launch_bounds__(256) void pcv_reduce_k(vfd_voxel_desc d, PcGeom g, 
   const int ho = d.h + 2, wo = d.w + 2;
   TO* ob = out + (size_t)bc * ho * wo * PC_O;
   constexpr int FPS = 4 * 2 * 16 / PC_FSL;
-  for (int f = blockIdx.y * FPS; f < (blockIdx.y + 1) * FPS; ++f) {
+  constexpr int U = 4;
+  for (int fu = blockIdx.y * FPS; fu < (blockIdx.y + 1) * FPS; fu += U) {
+    float su[U];
+    frag_sums<U>(partial, contrib, nc, PC_FRAG, (size_t)wv * (PC_FRAG / PC_WAVES) + (fu * 64 + lane), su);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+    const int f = fu + u;
+    const float s = su[u];
     const int a = f >> 5, bb = (f >> 4) & 1, r = f & 15;
-    float s = 0.f;
-    for (int k = 0; k < nc; ++k)
-      s += partial[(size_t)contrib[k] * PC_FRAG + (size_t)wv * (PC_FRAG / PC_WAVES) + (f * 64 + lane)];
     // fragment -> (pixel, channel): C/D layout of v_mfma_f32_32x32x2_f32
     const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
     const int ip = 32 * a + row;
@@ -501,6 +505,7 @@ __global__ __launch_bounds__(256) void pcv_reduce_k(vfd_voxel_desc d, PcGeom g, 
     pad_sets(px, d.w, true, cols, &ncol);
     for (int i = 0; i < nr; ++i)
       for (int j = 0; j < ncol; ++j) ob[((size_t)rows[i] * wo + cols[j]) * PC_O + o] = (TO)v;
+    }
   }
 }
 
@@ -740,13 +745,20 @@ __global__ __launch_bounds__(256) void pcd_reduce_k(PdGeom g, const float* __res
   const int c0 = (grp - 1) * 2 + (t == pd_lo(g, grp - 1) / PD_CHUNKS ? 0 : 1), c1 = grp * 2;
   const PdTile tl = pd_tile(g, t);
   constexpr int FPS = 4 * 2 * 16 / PC_FSL;
-  for (int f = blockIdx.y * FPS; f < (blockIdx.y + 1) * FPS; ++f) {
+  constexpr int U = 4;
+  const int contrib[2] = {c0, c1};
+  for (int fu = blockIdx.y * FPS; fu < (blockIdx.y + 1) * FPS; fu += U) {
+    float su[U];
+    frag_sums<U>(partial, contrib, 2, PC_FRAG, (size_t)wv * (PC_FRAG / PC_WAVES) + (fu * 64 + lane), su);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+    const int f = fu + u;
     const int a = f >> 5, bb = (f >> 4) & 1, r = f & 15;
-    const size_t off = (size_t)wv * (PC_FRAG / PC_WAVES) + (f * 64 + lane);
-    const float s = partial[(size_t)c0 * PC_FRAG + off] + partial[(size_t)c1 * PC_FRAG + off];
+    const float s = su[u];
     const int m = tl.m0 + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
     const int n = tl.nt * PD_N + wv * 64 + bb * 32 + (lane & 31);
     if (m < g.mtot && n < g.ntot) dx[(size_t)m * g.ntot + n] = s;
+    }
   }
 }
 

@@ -53,6 +53,32 @@ __device__ __forceinline__ int reflect1(int i, int n) {
 
 __device__ __forceinline__ bool finitef(float x) { return __builtin_isfinite(x); }
 
+// Stream-K partial sums: s[u] = sum over contributors k (in order) of p_k[u * 64], where p_k =
+// partial + contrib[k] * frag + base — U fragment elements of one lane; the loads of two
+// contributors x U elements are issued before any add (the reduce kernels are latency-bound), the
+// adds keep contributor order (the same sums as a plain loop)
+template <int U>
+__device__ __forceinline__ void frag_sums(const float* __restrict__ partial, const int* contrib, int nc,
+                                          size_t frag, size_t base, float (&s)[U]) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) s[u] = 0.f;
+  for (int k = 0; k < nc; k += 2) {
+    float v0[U], v1[U];
+    const float* p0 = partial + (size_t)contrib[k] * frag + base;
+    const float* p1 = partial + (size_t)contrib[k + 1 < nc ? k + 1 : k] * frag + base;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      v0[u] = p0[u * 64];
+      v1[u] = p1[u * 64];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      s[u] += v0[u];
+      if (k + 1 < nc) s[u] += v1[u];
+    }
+  }
+}
+
 // Positions of source index i along an axis of length n in a reflect-padded (+1 each side) copy:
 // {i+1}, plus 0 when i == 1 and n+1 when i == n-2 (ReflectionPad(1)).  Without padding: {i}.
 __device__ __forceinline__ void pad_sets(int i, int n, bool pad, int* idx, int* cnt) {

@@ -41,7 +41,11 @@ typedef struct vfd_voxel_desc {
   float str[3];          /* model.voxel_str_p                                            */
   float len[3];          /* voxel_end_p - voxel_str_p                                    */
   float z_scale;         /* model.voxel_size[0]: divisor of the appended depth feature   */
-  int32_t pad_out;       /* 1: outputs consumed by a 3x3 reflect conv are written padded */
+  int32_t pad_out;       /* 1: outputs consumed by a 3x3 reflect conv are written padded;
+                            2 (K3C only): padded layout, and the gradient of that padded map
+                            arrives with its reflect copies already folded into the interior
+                            (vfd_proj_conv_dgrad's folded form): the K3 plan / backward read every
+                            sample from the interior, no fold pass */
   const float* axis_x;   /* [X] voxel centres (torch.linspace fp32), device              */
   const float* axis_y;   /* [Y]                                                          */
   const float* axis_z;   /* [Z]                                                          */
@@ -334,7 +338,10 @@ int vfd_pad_conv_fwd_bf16(const vfd_conv_desc* d, const float* x, const void* Wf
  * vfd_voxel_project_bwd_planned reads) from g_pre [B*N, h, w, O = 256] (d pre-activation, NHWC)
  * and Wd = the weight [O, Cv*D, 3, 3] as [9 flipped taps][O/4][np][2][2] (np = D*Cv rounded up
  * to 256, zero-padded).  fp32 MFMA, stream-K with a fixed-order partial sum (deterministic).
- * Workspace 0 = shape unsupported (Cv != 64, D > 64, or the padded rows of a tile exceed LDS). */
+ * d->pad_out == 2: the folded form — only the interior of dx is written, each border-adjacent pixel
+ * holding the sum of its reflect copies (the plan for vfd_voxel_project_bwd_planned must be built
+ * with the same pad_out); h >= 6, w >= 64.
+ * Workspace 0 = shape unsupported (Cv != 64, D > 64, or the staged rows of a tile exceed LDS). */
 size_t vfd_proj_conv_dgrad_workspace(const vfd_voxel_desc* d);
 int vfd_proj_conv_dgrad(const vfd_voxel_desc* d, const float* g_pre, const float* Wd, float* dx, void* workspace,
                         size_t ws_bytes, void* stream);

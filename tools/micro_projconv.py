@@ -111,6 +111,35 @@ def main():
     derr = float((dx - ref).abs().max()) / float(ref.abs().max())
     print(f'config {a.config}: dgrad kernel {t_dg:.3f} ms (kernel {ms2 / n2:.3f} ms, {flop / (ms2 / n2) / 1e9:.1f} TFLOP/s, '
           f'weight copy incl.); MIOpen dgrad {t_mi:.3f} ms, MIOpen wgrad {t_wg:.3f} ms; max rel err {derr:.2e}', flush=True)
+    # the folded form (pad_out = 2): interior only, reflect copies folded in; check against the
+    # padded result folded on the host side
+    df = space.desc(B, N, Cv=Cv, pad_out=2)
+    nbf = lib.vfd_proj_conv_dgrad_workspace(ctypes.byref(df))
+    if nbf:
+        wsf = torch.empty(nbf, dtype=torch.uint8, device=dev)
+        dxf = torch.zeros_like(dx)
+
+        def dgrad_f():
+            wd = KN.proj_conv_dgrad_weight(w0, Cv, D)
+            _lib.check(lib.vfd_proj_conv_dgrad(ctypes.byref(df), g_pre.data_ptr(), wd.data_ptr(), dxf.data_ptr(),
+                                               wsf.data_ptr(), nbf, _lib.stream()), 'proj_conv_dgrad folded')
+        _lib.prof_enable('proj_conv_dgrad')
+        for _ in range(a.iters):
+            dgrad_f()
+        torch.cuda.synchronize()
+        prof = _lib.prof_read()
+        _lib.prof_enable('off')
+        n4, ms4 = prof.get('proj_conv_dgrad', (1, float('nan')))
+        dgrad()
+        ref = dx.clone()                                   # padded, unfolded: fold it here
+        ref[:, :, 2, :] += ref[:, :, 0, :]
+        ref[:, :, h - 1, :] += ref[:, :, h + 1, :]
+        ref[:, :, :, 2] += ref[:, :, :, 0]
+        ref[:, :, :, w - 1] += ref[:, :, :, w + 1]
+        inner = (slice(None), slice(None), slice(1, h + 1), slice(1, w + 1))
+        ferr = float((dxf[inner] - ref[inner]).abs().max()) / float(ref[inner].abs().max())
+        print(f'config {a.config}: folded dgrad kernel {ms4 / n4:.3f} ms ({flop / (ms4 / n4) / 1e9:.1f} TFLOP/s); '
+              f'max rel err vs folded padded {ferr:.2e}', flush=True)
     # weight / bias gradient: the MFMA kernel (reference channel order) vs MIOpen's + the channel swap
     nbytes = lib.vfd_proj_conv_wgrad_workspace(ctypes.byref(d))
     ws2 = torch.empty(nbytes, dtype=torch.uint8, device=dev)

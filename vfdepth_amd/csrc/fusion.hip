@@ -1929,7 +1929,7 @@ __global__ __launch_bounds__(256) void vpb_fill_k(vfd_voxel_desc d, const float*
   const int c = vpb_cell(d, g, ix, iy, iz);
   const int n = d.B * g.ncell;
   const int Pd = d.pad_out ? 1 : 0;
-  const int fs = Pd ? vpb_fold_slot(d, px, py) : -1;
+  const int fs = d.pad_out == 1 ? vpb_fold_slot(d, px, py) : -1;   // pad_out 2: d_out arrives folded
   const unsigned row = fs >= 0 ? 0x80000000u | (unsigned)(1 + (bc * 2 * (d.w + d.h) + fs) * d.D + di)
                                : (unsigned)(((bc * (d.h + 2 * Pd) + py + Pd) * (d.w + 2 * Pd) + px + Pd) * d.D + di);
   entries[vpb_ptr(ptr, boff, n, b * g.ncell + c) + r] = make_float4(ix, iy, iz, __uint_as_float(row));
@@ -2701,7 +2701,7 @@ static void vpb_bwd_launch(const vfd_voxel_desc* d, const float* d_out, void* ws
   const VpbGeom g = vpb_geom(*d);
   const VpbPtrs p = vpb_ptrs(w, ws);
   const int nb = d->B * g.ntile;
-  const int nf = d->pad_out ? d->B * d->N * 2 * (d->w + d->h) : 0;
+  const int nf = d->pad_out == 1 ? d->B * d->N * 2 * (d->w + d->h) : 0;
   switch (d->Cv) {
 #define VPB_LAUNCH(CVV)                                                                                         \
   case CVV:                                                                                                     \

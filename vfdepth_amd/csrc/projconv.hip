@@ -546,6 +546,10 @@ static PcGeom pc_plan(const vfd_voxel_desc& d) {
 // fragment pipeline as the forward).  Stream-K over atoms: a tile whole inside one workgroup's
 // range is stored directly; the (at most two) split tiles of a range go to partial slots that
 // `pcd_reduce_k` sums in workgroup order (deterministic).
+#ifndef VFD_PD_PF
+#define VFD_PD_PF 4
+#endif
+constexpr int PD_PF = VFD_PD_PF;                // weight-fragment prefetch distance of the data gradient
 constexpr int PD_OC = 32;                       // O channels per atom
 constexpr int PD_XS = PD_OC + 4;                // LDS floats per staged position
 constexpr int PD_N = PC_WAVES * 64;             // n per tile
@@ -640,7 +644,7 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pcd_main_k(PdGeom g, const floa
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
   const float2* wlane = reinterpret_cast<const float2*>(Wd) + (size_t)(wv * 64 + li) * 2 + lh;
-  float2 bq[PC_PF][2];
+  float2 bq[PD_PF][2];
   int pf_atom = a_lo, pf_it = 0;
   auto prefetch = [&](int slot) {
     if (pf_atom < a_hi) {
@@ -654,7 +658,7 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pcd_main_k(PdGeom g, const floa
     }
   };
 #pragma unroll
-  for (int k = 0; k < PC_PF; ++k) prefetch(k);
+  for (int k = 0; k < PD_PF; ++k) prefetch(k);
   for (int atom = a_lo; atom < a_hi; ++atom) {
     const int t = atom / PD_CHUNKS, ch = atom - t * PD_CHUNKS;
     const PdTile tl = pd_tile(g, t);
@@ -678,7 +682,7 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pcd_main_k(PdGeom g, const floa
       const float* xn = xb + (kyn * g.cols + kxn) * PD_XS;
 #pragma unroll
       for (int q = 0; q < PD_OC / 4; ++q) {
-        const int ring = q % PC_PF;
+        const int ring = q % PD_PF;
         const float2 b0 = bq[ring][0], b1 = bq[ring][1];
         prefetch(ring);
         if (q < PD_OC / 4 - 1) {
@@ -760,6 +764,293 @@ __global__ __launch_bounds__(256) void pcd_reduce_k(PdGeom g, const float* __res
     if (m < g.mtot && n < g.ntot) dx[(size_t)m * g.ntot + n] = s;
     }
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Folded form (vfd_voxel_desc.pad_out == 2): the data gradient of the reflect-padded input with the
+// reflect-pad adjoint folded in, so only the h x w interior is computed.  A padded border position's
+// gradient belongs to its mirror pixel (pad_sets); with the flipped taps,
+//   dX[y=1]    = dXp[2] + dXp[0],        dXp[0]   = G[0] W_(ky=2)     (only that tap row reaches G)
+//   dX[y=h-2]  = dXp[h-1] + dXp[h+1],    dXp[h+1] = G[h-1] W_(ky=0)
+// (columns alike), i.e. the A operand of row 1 at ky = 2 is G[2] + G[0] and of row h-2 at ky = 0 is
+// G[h-3] + G[h-1].  Column folds ride in two extra staged columns per row (E1 = G[.][2] + G[.][0]
+// read by x = 1 at kx = 2, E2 = G[.][w-3] + G[.][w-1] by x = w-2 at kx = 0); the row fold in one
+// extra staged row per tile (a tile spans <= 3 pixel rows, so with h >= 6 it holds row 1 or row h-2,
+// never both), read by those lanes at those taps instead of their plain row — one A read per lane
+// as in the padded form; the fold row's E columns carry the corner terms.  Tiles are 128 consecutive interior pixels of ONE camera (config 2:
+// 30 per camera, 180 in all against 193 padded ones), written into the interior of the padded
+// layout; K3's backward then reads every sample straight from it (its plan built with pad_out = 2:
+// no fold buffer, no fold launch).
+struct PfGeom {
+  int nbc, h, w, ntot, np, tpc, mtiles, ntile, natom, ngroup, hrows, cols, lds_floats;
+};
+
+__host__ __device__ inline int pf_lo(const PfGeom& g, int grp) {
+  return (int)(((long long)grp * g.natom) / g.ngroup);
+}
+
+struct PfTile {
+  int nt, bc, m0, y0;
+};
+
+__device__ __forceinline__ PfTile pf_tile(const PfGeom& g, int t) {
+  PfTile r;
+  const int mt = t % g.mtiles;
+  r.nt = t / g.mtiles;
+  r.bc = mt / g.tpc;
+  r.m0 = (mt - r.bc * g.tpc) * PC_PIX;
+  r.y0 = r.m0 / g.w;
+  return r;
+}
+
+// one staged element: G row y (zero outside [0, h)) at staged column c (G column c - 2; E1 / E2)
+__device__ __forceinline__ float4 pf_elem(const PfGeom& g, const float* __restrict__ src, int y, int c) {
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (y < 0 || y >= g.h) return v;
+  const float* row = src + (size_t)y * g.w * PC_O;
+  if (c < g.w + 4) {
+    const int x = c - 2;
+    if (x >= 0 && x < g.w) v = *reinterpret_cast<const float4*>(row + (size_t)x * PC_O);
+  } else {
+    const int xa = c == g.w + 4 ? 2 : g.w - 3, xb = c == g.w + 4 ? 0 : g.w - 1;
+    const float4 a = *reinterpret_cast<const float4*>(row + (size_t)xa * PC_O);
+    const float4 b = *reinterpret_cast<const float4*>(row + (size_t)xb * PC_O);
+    v = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+  }
+  return v;
+}
+
+// loader waves (tid 0..255): staged row r < hrows = G row y0 - 1 + r of the tile's camera,
+// columns 0 .. w+3 = G columns -2 .. w+1, then E1, E2; row hrows = the tile's fold row (G[2] + G[0]
+// when the tile holds pixel row 1, G[h-3] + G[h-1] when it holds row h-2; h >= 6: never both);
+// channels of chunk ch
+__device__ __forceinline__ void pf_stage(const PfGeom& g, float* __restrict__ dst, const float* __restrict__ gp,
+                                         int atom, int tid) {
+  const int t = atom / PD_CHUNKS, ch = atom - t * PD_CHUNKS;
+  const PfTile tl = pf_tile(g, t);
+  const int hw = g.h * g.w;
+  const int ylast = (tl.m0 + PC_PIX - 1 < hw ? tl.m0 + PC_PIX - 1 : hw - 1) / g.w;
+  const int fa = tl.y0 <= 1 && ylast >= 1 ? 2 : (tl.y0 <= g.h - 2 && ylast >= g.h - 2 ? g.h - 3 : -1);
+  const int fb = fa == 2 ? 0 : g.h - 1;
+  const int npos = (g.hrows + (fa >= 0 ? 1 : 0)) * g.cols;
+  const int q = tid & 7;
+  const float* src = gp + (size_t)tl.bc * g.h * g.w * PC_O + ch * PD_OC + 4 * q;
+  for (int p0 = tid >> 3; p0 < npos; p0 += 4 * 32) {
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int p = p0 + 32 * u;
+      const int hr = p / g.cols, c = p - hr * g.cols;
+      v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (p < npos) {
+        if (hr < g.hrows) {
+          v[u] = pf_elem(g, src, tl.y0 - 1 + hr, c);
+        } else {
+          const float4 a = pf_elem(g, src, fa, c), b = pf_elem(g, src, fb, c);
+          v[u] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int p = p0 + 32 * u;
+      if (p < npos) *reinterpret_cast<float4*>(dst + p * PD_XS + 4 * q) = v[u];
+    }
+  }
+}
+
+__global__ __launch_bounds__(PC_THREADS, 2) void pcdf_main_k(PfGeom g, const float* __restrict__ gp,
+                                                            const float* __restrict__ Wd,
+                                                            float* __restrict__ dx,
+                                                            float* __restrict__ partial) {
+  extern __shared__ float pd_lds[];
+  const int grp = (g.ngroup % 8 == 0) ? (blockIdx.x % 8) * (g.ngroup / 8) + blockIdx.x / 8 : blockIdx.x;
+  const int a_lo = pf_lo(g, grp), a_hi = pf_lo(g, grp + 1);
+  if (a_lo >= a_hi) return;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const bool compute = wv < PC_WAVES;
+  if (!compute) pf_stage(g, pd_lds, gp, a_lo, threadIdx.x - 64 * PC_WAVES);
+  __syncthreads();
+  if (!compute) {
+    for (int atom = a_lo; atom < a_hi; ++atom) {
+      if (atom + 1 < a_hi)
+        pf_stage(g, pd_lds + ((atom + 1 - a_lo) & 1) * g.lds_floats, gp, atom + 1, threadIdx.x - 64 * PC_WAVES);
+      __syncthreads();
+    }
+    return;
+  }
+  const int li = lane & 31, lh = lane >> 5;
+  const int hw = g.h * g.w;
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  const float2* wlane = reinterpret_cast<const float2*>(Wd) + (size_t)(wv * 64 + li) * 2 + lh;
+  float2 bq[PD_PF][2];
+  int pf_atom = a_lo, pf_it = 0;
+  auto prefetch = [&](int slot) {
+    if (pf_atom < a_hi) {
+      const int t = pf_atom / PD_CHUNKS, ch = pf_atom - t * PD_CHUNKS;
+      const int nt = t / g.mtiles;
+      const int tap = pf_it >> 3, q = pf_it & 7;
+      const float2* w = wlane + ((size_t)(tap * (PC_O / 4) + ch * (PD_OC / 4) + q) * g.np + nt * PD_N) * 2;
+      bq[slot][0] = w[0];
+      bq[slot][1] = w[64];
+      if (++pf_it == PD_ITERS) { pf_it = 0; ++pf_atom; }
+    }
+  };
+#pragma unroll
+  for (int k = 0; k < PD_PF; ++k) prefetch(k);
+  for (int atom = a_lo; atom < a_hi; ++atom) {
+    const int t = atom / PD_CHUNKS, ch = atom - t * PD_CHUNKS;
+    const PfTile tl = pf_tile(g, t);
+    int pyx[4];                                       // (row << 16) | column of the lane's pixels
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      int m = tl.m0 + 32 * a + li;
+      m = m < hw ? m : hw - 1;                        // pixels past the camera: computed, never stored
+      const int y = m / g.w;
+      pyx[a] = (y << 16) | (m - y * g.w);
+    }
+    const float* xb = pd_lds + ((atom - a_lo) & 1) * g.lds_floats;
+    // per-lane LDS offset of tap `tap`: the A row (the fold row for row 1 at ky = 2 and row h-2 at
+    // ky = 0) and column (E1 / E2 for the column folds)
+    auto offsets = [&](int tap, int* o1) {
+      const int ky = tap / 3, kx = tap - 3 * ky;
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        const int px = pyx[a] & 0xFFFF, py = pyx[a] >> 16;
+        const int col = (px == 1 && kx == 2) ? g.w + 4 : (px == g.w - 2 && kx == 0) ? g.w + 5 : px + 1 + kx;
+        const bool frow = (py == 1 && ky == 2) || (py == g.h - 2 && ky == 0);
+        o1[a] = ((frow ? g.hrows : py - tl.y0 + ky) * g.cols + col) * PD_XS + 2 * lh;
+      }
+    };
+    int o1c[4];
+    offsets(0, o1c);
+    float2 afc[4], afn[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) afc[a] = *reinterpret_cast<const float2*>(&xb[o1c[a]]);
+#pragma unroll 1
+    for (int tap = 0; tap < 9; ++tap) {
+#pragma unroll
+      for (int q = 0; q < PD_OC / 4; ++q) {
+        const int ring = q % PD_PF;
+        const float2 b0 = bq[ring][0], b1 = bq[ring][1];
+        prefetch(ring);
+        if (q < PD_OC / 4 - 1) {
+#pragma unroll
+          for (int a = 0; a < 4; ++a) afn[a] = *reinterpret_cast<const float2*>(&xb[o1c[a] + 4 * (q + 1)]);
+        } else if (tap < 8) {                         // the current tap's loads are all issued
+          offsets(tap + 1, o1c);
+#pragma unroll
+          for (int a = 0; a < 4; ++a) afn[a] = *reinterpret_cast<const float2*>(&xb[o1c[a]]);
+        }
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int a = 0; a < 4; ++a) {
+            const float v = s ? afc[a].y : afc[a].x;
+            acc[a][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(v, s ? b0.y : b0.x, acc[a][0], 0, 0, 0);
+            acc[a][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(v, s ? b1.y : b1.x, acc[a][1], 0, 0, 0);
+          }
+#pragma unroll
+        for (int a = 0; a < 4; ++a) afc[a] = afn[a];
+      }
+    }
+    __syncthreads();                                  // buffer handed back to the loader waves
+    if (ch == PD_CHUNKS - 1 || atom == a_hi - 1) {
+      const int ts = t * PD_CHUNKS;
+      if (ts >= a_lo && ts + PD_CHUNKS <= a_hi) {     // whole tile in this range: store
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            const int n = tl.nt * PD_N + wv * 64 + b * 32 + li;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int m = tl.m0 + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * lh;
+              if (m < hw && n < g.ntot) {
+                const int y = m / g.w, x = m - y * g.w;
+                dx[(((size_t)tl.bc * (g.h + 2) + y + 1) * (g.w + 2) + x + 1) * g.ntot + n] = acc[a][b][r];
+              }
+              acc[a][b][r] = 0.f;
+            }
+          }
+      } else {                                        // split tile: partial slot
+        const int slot = t == a_lo / PD_CHUNKS ? 0 : 1;
+        float* dst = partial + ((size_t)grp * 2 + slot) * PC_FRAG + (size_t)wv * (PC_FRAG / PC_WAVES);
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              dst[((a * 2 + b) * 16 + r) * 64 + lane] = acc[a][b][r];
+              acc[a][b][r] = 0.f;
+            }
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void pcdf_reduce_k(PfGeom g, const float* __restrict__ partial,
+                                                     float* __restrict__ dx) {
+  const int grp = blockIdx.x;
+  const int lo = pf_lo(g, grp);
+  if (grp == 0 || lo % PD_CHUNKS == 0) return;        // boundary on a tile edge: nothing split
+  const int t = lo / PD_CHUNKS;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c0 = (grp - 1) * 2 + (t == pf_lo(g, grp - 1) / PD_CHUNKS ? 0 : 1), c1 = grp * 2;
+  const PfTile tl = pf_tile(g, t);
+  const int hw = g.h * g.w;
+  constexpr int FPS = 4 * 2 * 16 / PC_FSL;
+  constexpr int U = 4;
+  const int contrib[2] = {c0, c1};
+  for (int fu = blockIdx.y * FPS; fu < (blockIdx.y + 1) * FPS; fu += U) {
+    float su[U];
+    frag_sums<U>(partial, contrib, 2, PC_FRAG, (size_t)wv * (PC_FRAG / PC_WAVES) + (fu * 64 + lane), su);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int f = fu + u;
+      const int a = f >> 5, bb = (f >> 4) & 1, r = f & 15;
+      const int m = tl.m0 + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      const int n = tl.nt * PD_N + wv * 64 + bb * 32 + (lane & 31);
+      if (m < hw && n < g.ntot) {
+        const int y = m / g.w, x = m - y * g.w;
+        dx[(((size_t)tl.bc * (g.h + 2) + y + 1) * (g.w + 2) + x + 1) * g.ntot + n] = su[u];
+      }
+    }
+  }
+}
+
+static PfGeom pf_plan(const vfd_voxel_desc& d) {
+  PfGeom g;
+  g.nbc = d.B * d.N;
+  g.h = d.h;
+  g.w = d.w;
+  g.ntot = d.D * PC_CV;
+  g.np = (g.ntot + PD_N - 1) / PD_N * PD_N;
+  g.tpc = (d.h * d.w + PC_PIX - 1) / PC_PIX;
+  g.mtiles = g.nbc * g.tpc;
+  g.ntile = (g.np / PD_N) * g.mtiles;
+  g.natom = g.ntile * PD_CHUNKS;
+  g.hrows = (d.w + PC_PIX - 2) / d.w + 3;             // G rows under 128 consecutive pixels + 2
+  g.cols = d.w + 6;                                   // 2 + w + 2 columns, E1, E2
+  g.lds_floats = (g.hrows + 1) * g.cols * PD_XS;      // + the fold row
+  const int res = pc_resident();
+  const int most = g.natom / PD_CHUNKS;
+  g.ngroup = most < res ? (most > 0 ? most : 1) : res;
+  return g;
+}
+
+static bool pf_supported(const vfd_voxel_desc& d) {
+  if (d.Cv != PC_CV || d.B <= 0 || d.N <= 0 || d.h < 6 || d.w < 3 || d.D <= 0 || d.D > 64) return false;
+  const PfGeom g = pf_plan(d);
+  if (g.hrows > 5) return false;                      // a tile spans <= 3 pixel rows (w >= 64)
+  return (size_t)2 * g.lds_floats * sizeof(float) <= PD_LDS_MAX;
 }
 
 // one workgroup per CU, ranges of >= PD_CHUNKS atoms (a tile meets at most two groups per side)
@@ -1114,17 +1405,32 @@ int vfd_proj_conv_fwd_bf16(const vfd_voxel_desc* d, const float* vox, const floa
 }
 
 size_t vfd_proj_conv_dgrad_workspace(const vfd_voxel_desc* d) {
-  if (!d || !pd_supported(*d)) return 0;
+  if (!d) return 0;
+  if (d->pad_out == 2) return pf_supported(*d) ? (size_t)pf_plan(*d).ngroup * 2 * PC_FRAG * sizeof(float) : 0;
+  if (!pd_supported(*d)) return 0;
   return (size_t)pd_plan(*d).ngroup * 2 * PC_FRAG * sizeof(float);
 }
 
 int vfd_proj_conv_dgrad(const vfd_voxel_desc* d, const float* g_pre, const float* Wd, float* dx, void* ws,
                         size_t ws_bytes, void* stream) {
   VFD_REQUIRE(d && g_pre && Wd && dx, "proj_conv_dgrad: null argument");
-  VFD_REQUIRE(pd_supported(*d), "proj_conv_dgrad: unsupported shape (Cv = %d, 0 < D <= 64, padded rows in LDS)", PC_CV);
+  VFD_REQUIRE(d->pad_out == 2 ? pf_supported(*d) : pd_supported(*d),
+              "proj_conv_dgrad: unsupported shape (Cv = %d, 0 < D <= 64, staged rows in LDS; folded: h >= 6, w >= 64)", PC_CV);
   VFD_REQUIRE(ws && ws_bytes >= vfd_proj_conv_dgrad_workspace(d), "proj_conv_dgrad: workspace too small");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_PROJ_CONV_DGRAD, s);
+  if (d->pad_out == 2) {
+    const PfGeom g = pf_plan(*d);
+    static bool fattr = false;
+    if (!fattr) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(pcdf_main_k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                PD_LDS_MAX);
+      fattr = true;
+    }
+    pcdf_main_k<<<g.ngroup, PC_THREADS, (size_t)2 * g.lds_floats * sizeof(float), s>>>(g, g_pre, Wd, dx, (float*)ws);
+    pcdf_reduce_k<<<dim3(g.ngroup, PC_FSL), 256, 0, s>>>(g, (const float*)ws, dx);
+    return fail_launch("proj_conv_dgrad");
+  }
   const PdGeom g = pd_plan(*d);
   float* partial = (float*)ws;
   const size_t lds = (size_t)2 * g.lds_floats * sizeof(float);

@@ -395,6 +395,7 @@ def proj_conv_dgrad_weight(w, Cv, D):
 
 _PC_DGRAD = os.environ.get('VFD_PC_DGRAD', '1') != '0'
 _PC_WGRAD = os.environ.get('VFD_PC_WGRAD', '1') != '0'
+_PC_FOLD = os.environ.get('VFD_PC_FOLD', '1') != '0'    # K3C data gradient with the reflect fold inside
 
 
 def pad_conv_weight_fragments(w, C1=0, Z=0):
@@ -625,6 +626,11 @@ class ProjConv(torch.autograd.Function):
                                       bias.data_ptr(), O, out.data_ptr(), x.data_ptr() if need_x else None,
                                       ws.data_ptr(), nbytes, L.stream()),
                 'proj_conv_fwd')
+        # the data gradient's folded form (reflect-pad adjoint inside the GEMM, interior only) when
+        # it applies; K3's plan is then built for a folded d_out (pad_out = 2)
+        d.pad_out = 2 if (_PC_DGRAD and _PC_FOLD and lib.vfd_proj_conv_dgrad_workspace(ctypes.byref(
+            space.desc(B, N, Cv=Cv, pad_out=2)))) else 1
+        ctx.pad_out = d.pad_out
         ctx.space, ctx.shape = space, (B, N, V, Cv, O)
         ctx.plan = None
         if ctx.needs_input_grad[1]:
@@ -642,7 +648,7 @@ class ProjConv(torch.autograd.Function):
         w0, out, x = ctx.saved_tensors
         space = ctx.space
         B, N, V, Cv, O = ctx.shape
-        d = space.desc(B, N, Cv=Cv)
+        d = space.desc(B, N, Cv=Cv, pad_out=ctx.pad_out)
         # adjoint of the reflect padding, then of the LeakyReLU (its sign from the output): one kernel
         g_pre = lrelu_pad_backward(g, out)
         if x is None:   # only the bias gradient was asked for

@@ -1150,3 +1150,39 @@ def test_residual_join_matches_autograd_add(blocks, bf16):
     gclose(ga, gb, 'input gradient (join vs autograd add)', rel=rel)
     for i, (a, b) in enumerate(zip(pa, pb)):
         gclose(a, b, f'parameter {i} gradient (join vs autograd add)', rel=rel)
+
+
+@pytest.mark.parametrize('config', [2, 4])
+def test_proj_conv_dgrad_folded_matches_padded(config):
+    """The K3C data gradient's folded form (pad_out = 2: the reflect-pad adjoint inside the GEMM,
+    interior only; projconv.hip pcdf_main_k) against its padded form with the reflect copies folded
+    on the host (rows 0 / h+1 into 2 / h-1, then columns 0 / w+1 into 2 / w-1, as pad_sets pairs them),
+    through the C ABI at the config's shape."""
+    import ctypes
+    from vfdepth_amd import _lib as L
+    from vfdepth_amd import kernels as KN
+    cfg = full_cfg(config)
+    space = KN.VoxelSpace(cfg, DEV)
+    lib = L.load()
+    gen = torch.Generator(device=DEV).manual_seed(401)
+    B, N, Cv, D, O, h, w = 1, 6, 64, space.D, 256, space.h, space.w
+    g_pre = torch.randn(B * N, O, h, w, device=DEV, generator=gen).contiguous(memory_format=torch.channels_last)
+    w0 = torch.randn(O, Cv * D, 3, 3, device=DEV, generator=gen) * (O * 9) ** -0.5
+    wd = KN.proj_conv_dgrad_weight(w0, Cv, D)
+    out = {}
+    for pad_out in (1, 2):
+        d = space.desc(B, N, Cv=Cv, pad_out=pad_out)
+        nbytes = lib.vfd_proj_conv_dgrad_workspace(ctypes.byref(d))
+        assert nbytes, f'pad_out={pad_out} unsupported at config {config}'
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=DEV)
+        dx = torch.zeros(B * N, Cv * D, h + 2, w + 2, device=DEV).contiguous(memory_format=torch.channels_last)
+        L.check(lib.vfd_proj_conv_dgrad(ctypes.byref(d), g_pre.data_ptr(), wd.data_ptr(), dx.data_ptr(),
+                                        ws.data_ptr(), nbytes, L.stream()), 'proj_conv_dgrad')
+        out[pad_out] = dx
+    ref = out[1].clone()
+    ref[:, :, 2, :] += ref[:, :, 0, :]
+    ref[:, :, h - 1, :] += ref[:, :, h + 1, :]
+    ref[:, :, :, 2] += ref[:, :, :, 0]
+    ref[:, :, :, w - 1] += ref[:, :, :, w + 1]
+    inner = (slice(None), slice(None), slice(1, h + 1), slice(1, w + 1))
+    close(out[2][inner], ref[inner], f'folded K3C data gradient (config {config})', atol=1e-5, rtol=1e-4)

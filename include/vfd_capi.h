@@ -175,6 +175,10 @@ typedef struct vfd_bn_desc {
                             d residual tensor of that block never materialise (one rounding of the
                             sum to the activation type, as autograd's add)                     */
   const uint8_t* m2;     /* nullable: the next block's ReLU byte mask; g2 counts where it is 1    */
+  int32_t nhwc;          /* 1: channels-last maps [N*HW][C] (C/4 a power of two, C <= 2048) — config
+                            3's bf16 encoders, whose MIOpen convs then skip their NCHW<->NHWC
+                            transposes.  The apply passes then take reduced sums only (ns = 1: call
+                            vfd_bn_sum first); the one-launch bn1 kernels do not apply (fits = 0). */
 } vfd_bn_desc;
 
 int vfd_bn_splits(const vfd_bn_desc* d);
@@ -217,6 +221,12 @@ int vfd_inverse4x4(const float* m, float* out, int n, void* stream);
 int vfd_maxpool3s2_fwd(const void* x, void* y, uint8_t* arg, long long planes, int h, int w, int dtype, void* stream);
 int vfd_maxpool3s2_bwd(const void* g, const uint8_t* arg, void* dx, long long planes, int h, int w, int dtype,
                        void* stream);
+/* Channels-last variants (config 3's bf16 encoders): x [n][h][w][c] -> y, arg [n][ho][wo][c], c % 4 == 0;
+ * same taps, tie / NaN rules and fixed-order gather backward. */
+int vfd_maxpool3s2_nhwc_fwd(const void* x, void* y, uint8_t* arg, int n, int c, int h, int w, int dtype,
+                            void* stream);
+int vfd_maxpool3s2_nhwc_bwd(const void* g, const uint8_t* arg, void* dx, int n, int c, int h, int w, int dtype,
+                            void* stream);
 /* The encoders' input normalisation (x - 0.45) / 0.225 of cat([a, b], channels) in one pass:
  * a [n_img, ca, hw], b [n_img, cb, hw] (cb = 0: a alone) -> dst [n_img, ca + cb, hw]; hw % 4 == 0. */
 int vfd_normalize_cat(const float* a, const float* b, float* dst, long long n_img, int ca, int cb, int hw,

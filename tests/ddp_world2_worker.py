@@ -62,39 +62,42 @@ def bn_layer_checks(rank, world):
         if relu:
             yr = torch.relu(yr)
         (yr * g).sum().backward()
-        # this rank's half on the GPU through a SyncBatchNorm module (fused synchronised path)
-        half = slice(rank * shape[0] // world, (rank + 1) * shape[0] // world)
-        bn = torch.nn.SyncBatchNorm(C).to(DEV).train()
-        with torch.no_grad():
-            bn.weight.copy_(gamma.float())
-            bn.bias.copy_(beta.float())
-            bn.running_mean.copy_(rmean.float())
-        xh = x[half].float().to(DEV).requires_grad_(True)
-        rh = r[half].float().to(DEV).requires_grad_(True) if res else None
-        y = bn_act(bn, xh, rh, relu)
-        assert y.grad_fn is not None and 'BatchNormAct' in type(y.grad_fn).__name__, type(y.grad_fn).__name__
-        (y * g[half].float().to(DEV)).sum().backward()
-        torch.cuda.synchronize()
+        # this rank's half on the GPU through a SyncBatchNorm module (fused synchronised path), NCHW
+        # and channels-last (bnact.hip's NHWC kernels, config 3's bf16 encoders)
+        for fmt in (torch.contiguous_format, torch.channels_last):
+            half = slice(rank * shape[0] // world, (rank + 1) * shape[0] // world)
+            bn = torch.nn.SyncBatchNorm(C).to(DEV).train()
+            with torch.no_grad():
+                bn.weight.copy_(gamma.float())
+                bn.bias.copy_(beta.float())
+                bn.running_mean.copy_(rmean.float())
+            xh = x[half].float().to(DEV).contiguous(memory_format=fmt).requires_grad_(True)
+            rh = r[half].float().to(DEV).contiguous(memory_format=fmt).requires_grad_(True) if res else None
+            y = bn_act(bn, xh, rh, relu)
+            assert y.grad_fn is not None and 'BatchNormAct' in type(y.grad_fn).__name__, type(y.grad_fn).__name__
+            assert y.is_contiguous(memory_format=fmt)
+            (y * g[half].float().to(DEV)).sum().backward()
+            torch.cuda.synchronize()
 
-        def err(a, b, what, tol):
-            nonlocal worst
-            a, b = a.detach().double().cpu(), b.detach().double().cpu()
-            e = float((a - b).abs().max()) / max(float(b.abs().max()), 1e-12)
-            worst = max(worst, e)
-            assert e <= tol, f'rank {rank} {shape}: {what} rel err {e:.3g} > {tol}'
-        err(y, yr[half], 'output', 2e-6)
-        err(bn.running_mean, ref.running_mean, 'running_mean', 1e-6)
-        err(bn.running_var, ref.running_var, 'running_var', 1e-6)
-        assert int(bn.num_batches_tracked) == 1
-        err(xh.grad, xr.grad[half], 'd input', 2e-5)
-        if res:
-            err(rh.grad, rr.grad[half], 'd residual', 1e-6)
-        # SyncBatchNorm's parameter gradients are this rank's local sums: they add up to the whole batch's
-        dg, db = bn.weight.grad.clone(), bn.bias.grad.clone()
-        dist.all_reduce(dg)
-        dist.all_reduce(db)
-        err(dg, ref.weight.grad, 'sum over ranks of d gamma', 2e-5)
-        err(db, ref.bias.grad, 'sum over ranks of d beta', 2e-5)
+            def err(a, b, what, tol):
+                nonlocal worst
+                a, b = a.detach().double().cpu(), b.detach().double().cpu()
+                e = float((a - b).abs().max()) / max(float(b.abs().max()), 1e-12)
+                worst = max(worst, e)
+                assert e <= tol, f'rank {rank} {shape} {fmt}: {what} rel err {e:.3g} > {tol}'
+            err(y, yr[half], 'output', 2e-6)
+            err(bn.running_mean, ref.running_mean, 'running_mean', 1e-6)
+            err(bn.running_var, ref.running_var, 'running_var', 1e-6)
+            assert int(bn.num_batches_tracked) == 1
+            err(xh.grad, xr.grad[half], 'd input', 2e-5)
+            if res:
+                err(rh.grad, rr.grad[half], 'd residual', 1e-6)
+            # SyncBatchNorm's parameter gradients are this rank's local sums: they add up to the whole batch's
+            dg, db = bn.weight.grad.clone(), bn.bias.grad.clone()
+            dist.all_reduce(dg)
+            dist.all_reduce(db)
+            err(dg, ref.weight.grad, 'sum over ranks of d gamma', 2e-5)
+            err(db, ref.bias.grad, 'sum over ranks of d beta', 2e-5)
     return worst
 
 

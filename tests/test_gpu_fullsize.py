@@ -827,6 +827,114 @@ def test_batchnorm_act_bf16(shape, res, relu):
         gclose(ra.grad.float(), rr.grad, f'bf16 BN d residual {shape}', rel=2e-2)
 
 
+@pytest.mark.parametrize('shape,res,relu,bf16', [((12, 64, 96, 160), True, True, True),    # config-3 layer1
+                                                 ((12, 64, 192, 320), False, True, True),  # config-3 stem
+                                                 ((12, 128, 48, 80), True, True, False),
+                                                 ((12, 512, 12, 20), False, False, True),  # downsample BN
+                                                 ((2, 2048, 6, 10), True, True, False),    # ResNet-50 width
+                                                 ((3, 16, 5, 7), True, True, False)])      # odd spatial size
+def test_batchnorm_act_channels_last(shape, res, relu, bf16):
+    """The fused BN's channels-last kernels (d.nhwc: config 3's bf16 encoders keep NHWC maps) against
+    nn.BatchNorm2d.train() (+ add + ReLU) on the same channels-last input in fp32: the output and
+    the input / residual gradients stay channels-last; values, running statistics and gradients
+    as in the NCHW tests (fp32 at fp32 rounding, bf16 within its rounding)."""
+    import copy
+    from vfdepth_amd.layers import bn_act
+    cl = torch.channels_last
+    gen = torch.Generator(device=DEV).manual_seed(97)
+    dt = torch.bfloat16 if bf16 else torch.float32
+    x = (2.0 * torch.randn(shape, device=DEV, generator=gen) + 0.5).to(dt).contiguous(memory_format=cl)
+    r = torch.randn(shape, device=DEV, generator=gen).to(dt).contiguous(memory_format=cl) if res else None
+    C = shape[1]
+    bn = torch.nn.BatchNorm2d(C).to(DEV).train()
+    with torch.no_grad():
+        bn.weight.copy_(1 + 0.1 * torch.randn(C, device=DEV, generator=gen))
+        bn.bias.copy_(0.1 * torch.randn(C, device=DEV, generator=gen))
+        bn.running_mean.copy_(0.2 * torch.randn(C, device=DEV, generator=gen))
+    bn_ref = copy.deepcopy(bn)
+    xa, xr = x.clone().requires_grad_(True), x.float().requires_grad_(True)
+    ra = r.clone().requires_grad_(True) if res else None
+    rr = r.float().requires_grad_(True) if res else None
+    with torch.autocast(device_type='cuda', dtype=torch.bfloat16, enabled=bf16):
+        y = bn_act(bn, xa, ra, relu)
+    assert 'BatchNormAct' in type(y.grad_fn).__name__ and y.dtype == dt
+    assert y.is_contiguous(memory_format=cl) and not y.is_contiguous()
+    yr = bn_ref(xr)
+    if res:
+        yr = yr + rr
+    if relu:
+        yr = torch.relu(yr)
+    tol = dict(atol=1e-5, rtol=2.0 ** -8) if bf16 else dict(atol=2e-5, rtol=2e-5)
+    close(y.float(), yr, f'channels-last BN output {shape}', **tol)
+    close(bn.running_mean, bn_ref.running_mean, 'running_mean', atol=1e-6, rtol=1e-5)
+    close(bn.running_var, bn_ref.running_var, 'running_var', atol=1e-6, rtol=1e-5)
+    assert int(bn.num_batches_tracked) == 1
+    g = torch.randn(shape, device=DEV, generator=gen).to(dt).contiguous(memory_format=cl)
+    (y.float() * g.float()).sum().backward()
+    (yr * g.float()).sum().backward()
+    rel = 2e-2 if bf16 else 1e-4
+    assert xa.grad.is_contiguous(memory_format=cl)
+    gclose(xa.grad.float(), xr.grad, f'channels-last BN d input {shape}', rel=rel)
+    gclose(bn.weight.grad, bn_ref.weight.grad, f'channels-last BN d gamma {shape}', rel=rel)
+    gclose(bn.bias.grad, bn_ref.bias.grad, f'channels-last BN d beta {shape}', rel=rel)
+    if res:
+        gclose(ra.grad.float(), rr.grad, f'channels-last BN d residual {shape}', rel=rel if bf16 else 1e-6)
+
+
+def _fro(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+@pytest.mark.parametrize('bf16', [False, True])
+def test_channels_last_encoder_matches_nchw(bf16):
+    """The encoder channels-last (ResnetEncoder.use_channels_last: NHWC weights, maps and BN
+    kernels; config 3 runs it under bf16 autocast) against the same encoder NCHW.  fp32: the
+    pyramid agrees at fp32 rounding level and the gradients within 1e-2 in Frobenius norm (the
+    train-mode BN backward cancels and a ReLU / max-pool kink crossed by a last-bit forward
+    difference moves single entries; see test_gpu_parity's encoder tolerance).  bf16: both layouts
+    against the fp32 NCHW encoder — channels-last may not be further from it than NCHW bf16 is
+    (x1.5 + 1e-3: MIOpen picks different bf16 algorithms per layout).  The fused BN took the NHWC
+    path."""
+    import copy
+    from vfdepth_amd.layers import ResnetEncoder
+    gen = torch.Generator(device=DEV).manual_seed(98)
+    enc = ResnetEncoder(18, False, 2).to(DEV).train()
+    enc_cl = copy.deepcopy(enc).use_channels_last()
+    assert enc_cl.encoder.conv1.weight.is_contiguous(memory_format=torch.channels_last)
+    x = torch.randn(12, 6, 96, 160, device=DEV, generator=gen)
+    runs = [(copy.deepcopy(enc), False)] if bf16 else []
+    runs += [(enc, bf16), (enc_cl, bf16)]
+    outs = []
+    for e, amp in runs:
+        xa = x.clone().requires_grad_(True)
+        with torch.autocast(device_type='cuda', dtype=torch.bfloat16, enabled=amp):
+            feats = e(xa, normalized=True)
+        loss = sum((f.float() * (k + 1)).mean() for k, f in enumerate(feats))
+        loss.backward()
+        outs.append(([f.float() for f in feats], xa.grad, e.encoder.conv1.weight.grad,
+                     e.encoder.layer4[1].bn2.weight.grad))
+    fb = outs[-1][0]
+    assert fb[1].is_contiguous(memory_format=torch.channels_last) and not fb[1].is_contiguous()
+    names = ['level 0', 'level 1', 'level 2', 'level 3', 'level 4', 'd input', 'stem conv d weight',
+             'layer4 bn2 d gamma']
+    flat = [o[0] + list(o[1:]) for o in outs]
+    if not bf16:
+        (fa, ga, wa, ba), (fb, gb, wb, bb) = outs
+        for k, (a, b) in enumerate(zip(fa, fb)):
+            gclose(b, a, f'encoder level {k}', rel=1e-4)
+        for what, a, b in (('d input', gb, ga), ('stem conv d weight', wb, wa), ('layer4 bn2 d gamma', bb, ba)):
+            fro = _fro(a, b)
+            print(f'{what}: fro {fro:.3g}')
+            assert fro < 1e-2, f'{what}: relative Frobenius error {fro:.3g}'
+        return
+    ref, nchw, cl = flat
+    for what, r, n, c in zip(names, ref, nchw, cl):
+        en, ec = _fro(n, r), _fro(c, r)
+        print(f'{what}: bf16 NCHW {en:.3g}, bf16 channels-last {ec:.3g} (vs fp32)')
+        assert ec <= 1.5 * en + 1e-3, f'{what}: channels-last {ec:.3g} vs NCHW {en:.3g} from fp32'
+
+
 def test_dense_maps_bf16():
     """bf16 maps (config 3) through the reflect pad, the decoders' ELU + upsample + pad chain and the
     stem max pool: forward bit-identical to ATen's bf16 ops (copies, fp32-computed ELU rounded once,
@@ -1086,6 +1194,35 @@ def test_stem_max_pool_matches_aten():
         y.backward(g)
         yr.backward(g)
         assert torch.equal(x.grad, xr.grad), shape
+
+
+@pytest.mark.parametrize('bf16', [False, True])
+def test_stem_max_pool_channels_last(bf16):
+    """The channels-last max pool (maxpool.hip maxpool_nhwc_*: config 3's bf16 encoders) against
+    ATen on the same channels-last input: forward bit-identical (same tie / NaN rules), backward
+    equal (fixed-order sum of the <= 4 winning windows; in bf16 ATen accumulates in fp32 as well),
+    output and input gradient channels-last; odd and even sizes."""
+    from vfdepth_amd import kernels as KN
+    cl = torch.channels_last
+    gen = torch.Generator(device=DEV).manual_seed(42)
+    dt = torch.bfloat16 if bf16 else torch.float32
+    for shape in ((12, 64, 192, 320), (2, 8, 37, 53), (2, 4, 2, 7), (1, 12, 5, 5)):
+        x = torch.relu(torch.randn(shape, device=DEV, generator=gen)).to(dt)
+        if shape[-1] > 10:
+            x[:, :, ::3, ::2] = 0.5                                         # equal maxima in one window
+        x = x.contiguous(memory_format=cl).requires_grad_(True)
+        xr = x.detach().clone().requires_grad_(True)
+        y = KN.MaxPool3s2.apply(x)
+        yr = F.max_pool2d(xr, 3, 2, 1)
+        assert y.is_contiguous(memory_format=cl) and torch.equal(y, yr), shape
+        g = torch.randn(y.shape, device=DEV, generator=gen).to(dt).contiguous(memory_format=cl)
+        y.backward(g)
+        yr.backward(g)
+        assert x.grad.is_contiguous(memory_format=cl), shape
+        if bf16:       # <= 4 fp32 terms rounded once; the summation order may differ from ATen's
+            close(x.grad, xr.grad, f'bf16 channels-last max pool d input {shape}', atol=1e-6, rtol=2.0 ** -7)
+        else:
+            assert torch.equal(x.grad, xr.grad), shape
 
 
 def test_inverse4x4_kernel_matches_torch_ops():

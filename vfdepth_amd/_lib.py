@@ -48,7 +48,8 @@ class ConvDesc(ctypes.Structure):
 
 class BnDesc(ctypes.Structure):
     _fields_ = [('N', c_int), ('C', c_int), ('HW', c_int), ('S', c_int), ('relu', c_int),
-                ('eps', c_float), ('momentum', c_float), ('dtype', c_int), ('g2', c_void_p), ('m2', c_void_p)]
+                ('eps', c_float), ('momentum', c_float), ('dtype', c_int), ('g2', c_void_p), ('m2', c_void_p),
+                ('nhwc', c_int)]
 
 
 _SIGS = {
@@ -98,6 +99,8 @@ _SIGS = {
     'vfd_maxpool3s2_fwd': (c_int, [c_fp, c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_int, c_void_p]),
     'vfd_normalize_cat': (c_int, [c_fp, c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_int, c_void_p]),
     'vfd_maxpool3s2_bwd': (c_int, [c_fp, c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_int, c_void_p]),
+    'vfd_maxpool3s2_nhwc_fwd': (c_int, [c_fp, c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_void_p]),
+    'vfd_maxpool3s2_nhwc_bwd': (c_int, [c_fp, c_fp, c_fp, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     'vfd_aggregate_bwd': (c_int, [c_int] * 4 + [c_fp, c_fp, c_fp, c_int, ctypes.POINTER(c_fp), ctypes.POINTER(c_int), c_fp, c_void_p]),
     'vfd_upsample_ac_bwd': (c_int, [c_fp, c_fp, c_fp, ctypes.c_longlong] + [c_int] * 4 + [c_void_p]),
     'vfd_reflect_pad1_fwd': (c_int, [c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_int, c_void_p]),

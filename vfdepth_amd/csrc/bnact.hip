@@ -494,14 +494,265 @@ __global__ __launch_bounds__(BN1_THREADS) void bn1_bwd_k(vfd_bn_desc d, const T*
   });
 }
 
+// ---- channels-last (d.nhwc = 1): config 3's bf16 encoders keep their maps NHWC so MIOpen's
+// convolutions run without their NCHW <-> NHWC transposes.  x is [R = N*HW rows][C]; a row's C
+// channels are contiguous, so a channel's statistics cannot be one block's contiguous range:
+// block `split` of the statistics kernels owns rows [split*chunk, ...) of ALL channels, thread t
+// the channel quad(s) q = t % QW (+ 256 j) of every RP-th row, and the per-(channel, split)
+// partials keep the NCHW path's [C][S][2] layout (vfd_bn_sum reduces them in a fixed order).
+// The apply passes read reduced sums (ns = 1): each block first turns them into per-channel
+// coefficients in LDS, then streams float4s of [R][C] (quad = index mod C/4).
+constexpr int NH_MAXC = 2048;        // ResNet-50's widest stage; C/4 a power of two
+
+struct NhGeom {
+  unsigned rows, chunk;   // R = N*HW, rows per split
+  int Q, QW, QT, RP;      // quads per row, quads per thread-row group (<= 256), quads per thread, rows per sweep
+};
+
+__device__ __forceinline__ NhGeom nh_geom(const vfd_bn_desc& d) {
+  NhGeom g;
+  g.rows = (unsigned)d.N * (unsigned)d.HW;
+  g.chunk = (g.rows + d.S - 1) / d.S;
+  g.Q = d.C >> 2;
+  g.QW = g.Q < BN_THREADS ? g.Q : BN_THREADS;
+  g.QT = g.Q / g.QW;
+  g.RP = BN_THREADS / g.QW;
+  return g;
+}
+
+// per-thread channel accumulators (QT <= 2) -> per-(channel, split) partials, rows summed in order
+__device__ __forceinline__ void nh_store_partials(const vfd_bn_desc& d, const NhGeom& g, double (&a)[2][4],
+                                                  double (&b)[2][4], double* __restrict__ partial) {
+  const int q0 = threadIdx.x % g.QW, rs = threadIdx.x / g.QW;
+  if (g.RP == 1) {        // C >= 1024: every thread owns whole channels
+    for (int j = 0; j < g.QT; ++j)
+      for (int k = 0; k < 4; ++k) {
+        const int c = 4 * (q0 + j * g.QW) + k;
+        partial[((size_t)c * d.S + blockIdx.x) * 2] = a[j][k];
+        partial[((size_t)c * d.S + blockIdx.x) * 2 + 1] = b[j][k];
+      }
+    return;
+  }
+  __shared__ double s1[4 * BN_THREADS];     // [RP][C], RP * C = 4 * BN_THREADS when C < 1024
+  __shared__ double s2[4 * BN_THREADS];
+  for (int j = 0; j < g.QT; ++j)
+    for (int k = 0; k < 4; ++k) {
+      const int slot = rs * d.C + 4 * (q0 + j * g.QW) + k;    // [RP][C]
+      s1[slot] = a[j][k];
+      s2[slot] = b[j][k];
+    }
+  __syncthreads();
+  for (int c = threadIdx.x; c < d.C; c += BN_THREADS) {
+    double u = 0.0, v = 0.0;
+    for (int r = 0; r < g.RP; ++r) {
+      u += s1[r * d.C + c];
+      v += s2[r * d.C + c];
+    }
+    partial[((size_t)c * d.S + blockIdx.x) * 2] = u;
+    partial[((size_t)c * d.S + blockIdx.x) * 2 + 1] = v;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(BN_THREADS) void bn_stats_nhwc_k(vfd_bn_desc d, const T* __restrict__ x,
+                                                              double* __restrict__ partial) {
+  const NhGeom g = nh_geom(d);
+  const int q0 = threadIdx.x % g.QW, rs = threadIdx.x / g.QW;
+  const unsigned lo = blockIdx.x * g.chunk, hi = lo + g.chunk < g.rows ? lo + g.chunk : g.rows;
+  double a[2][4] = {}, b[2][4] = {};
+  for (unsigned r = lo + rs; r < hi; r += g.RP)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (j >= g.QT) break;
+      const float4 v = ld4(x + (size_t)r * d.C + 4 * (q0 + j * g.QW));
+      a[j][0] += v.x; a[j][1] += v.y; a[j][2] += v.z; a[j][3] += v.w;
+      b[j][0] += (double)v.x * v.x; b[j][1] += (double)v.y * v.y;
+      b[j][2] += (double)v.z * v.z; b[j][3] += (double)v.w * v.w;
+    }
+  nh_store_partials(d, g, a, b, partial);
+}
+
+template <typename T>
+__global__ __launch_bounds__(BN_THREADS) void bn_bwd_stats_nhwc_k(vfd_bn_desc d, const T* __restrict__ gr,
+                                                                  const T* __restrict__ y, const T* __restrict__ x,
+                                                                  const float* __restrict__ mean_in,
+                                                                  double* __restrict__ partial) {
+  const NhGeom g = nh_geom(d);
+  const int q0 = threadIdx.x % g.QW, rs = threadIdx.x / g.QW;
+  const unsigned lo = blockIdx.x * g.chunk, hi = lo + g.chunk < g.rows ? lo + g.chunk : g.rows;
+  float4 mu[2];
+  for (int j = 0; j < g.QT; ++j) mu[j] = *reinterpret_cast<const float4*>(mean_in + 4 * (q0 + j * g.QW));
+  const bool relu = d.relu != 0;
+  double a[2][4] = {}, b[2][4] = {};
+  for (unsigned r = lo + rs; r < hi; r += g.RP)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (j >= g.QT) break;
+      const size_t o = (size_t)r * d.C + 4 * (q0 + j * g.QW);
+      float4 gv = bn_g4(d, gr, o);
+      const float4 xv = ld4(x + o);
+      if (relu) relu_mask4(d, y, o, gv);
+      a[j][0] += gv.x; a[j][1] += gv.y; a[j][2] += gv.z; a[j][3] += gv.w;
+      b[j][0] += (double)gv.x * (double)(xv.x - mu[j].x);
+      b[j][1] += (double)gv.y * (double)(xv.y - mu[j].y);
+      b[j][2] += (double)gv.z * (double)(xv.z - mu[j].z);
+      b[j][3] += (double)gv.w * (double)(xv.w - mu[j].w);
+    }
+  nh_store_partials(d, g, a, b, partial);
+}
+
+// sums[c] from the S partials by one block per channel (the NHWC path has hundreds of splits: a
+// serial chain per thread would dominate); block C writes the count row
+__global__ __launch_bounds__(BN_THREADS) void bn_sum_blk_k(vfd_bn_desc d, const double* __restrict__ partial,
+                                                           double count, double* __restrict__ sums,
+                                                           const float* __restrict__ invstd,
+                                                           float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  const int c = blockIdx.x;
+  if (c == d.C) {
+    if (count > 0.0 && threadIdx.x == 0) {
+      sums[c * 2] = count;
+      sums[c * 2 + 1] = 0.0;
+    }
+    return;
+  }
+  double a, b;
+  bn_channel_sums(partial, d.S, c, &a, &b);
+  if (threadIdx.x == 0) {
+    sums[c * 2] = a;
+    sums[c * 2 + 1] = b;
+    if (dgamma) dgamma[c] = (float)(b * invstd[c]);
+    if (dbeta) dbeta[c] = (float)a;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(BN_THREADS) void bn_apply_nhwc_k(vfd_bn_desc d, const T* __restrict__ x,
+                                                              const T* __restrict__ r, const double* __restrict__ sums,
+                                                              double count, const float* __restrict__ gamma,
+                                                              const float* __restrict__ beta, T* __restrict__ y,
+                                                              float* __restrict__ mean_out,
+                                                              float* __restrict__ invstd_out,
+                                                              float* __restrict__ run_mean, float* __restrict__ run_var,
+                                                              long long* __restrict__ nbt,
+                                                              unsigned char* __restrict__ mk) {
+  __shared__ float2 coef[NH_MAXC];
+  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] += 1;
+  if (count <= 0.0) count = sums[2 * d.C];
+  for (int c = threadIdx.x; c < d.C; c += BN_THREADS) {     // the NCHW apply's per-channel arithmetic
+    const double mean_d = sums[2 * c] / count;
+    double var_d = sums[2 * c + 1] / count - mean_d * mean_d;
+    var_d = var_d > 0.0 ? var_d : 0.0;
+    const float mean = (float)mean_d;
+    const float invstd = (float)(1.0 / sqrt(var_d + (double)d.eps));
+    const float sc = invstd * gamma[c];
+    coef[c] = make_float2(sc, beta[c] - mean * sc);
+    if (blockIdx.x == 0) {
+      mean_out[c] = mean;
+      invstd_out[c] = invstd;
+      if (run_mean) {
+        const double unbiased = count > 1.0 ? var_d * count / (count - 1.0) : var_d;
+        run_mean[c] = (float)((1.0 - d.momentum) * run_mean[c] + d.momentum * mean_d);
+        run_var[c] = (float)((1.0 - d.momentum) * run_var[c] + d.momentum * unbiased);
+      }
+    }
+  }
+  __syncthreads();
+  const unsigned qm = (unsigned)(d.C >> 2) - 1u;
+  const unsigned total4 = (unsigned)d.N * (unsigned)d.HW * (unsigned)(d.C >> 2);
+  const bool relu = d.relu != 0;
+  for (unsigned i = blockIdx.x * BN_THREADS + threadIdx.x; i < total4; i += gridDim.x * BN_THREADS) {
+    const size_t o = 4 * (size_t)i;
+    const int c = 4 * (i & qm);
+    float4 v = ld4(x + o);
+    const float2 k0 = coef[c], k1 = coef[c + 1], k2 = coef[c + 2], k3 = coef[c + 3];
+    v.x = v.x * k0.x + k0.y;
+    v.y = v.y * k1.x + k1.y;
+    v.z = v.z * k2.x + k2.y;
+    v.w = v.w * k3.x + k3.y;
+    if (r) {
+      const float4 q = ld4(r + o);
+      v.x += q.x;
+      v.y += q.y;
+      v.z += q.z;
+      v.w += q.w;
+    }
+    if (relu) {
+      v.x = fmaxf(v.x, 0.f);
+      v.y = fmaxf(v.y, 0.f);
+      v.z = fmaxf(v.z, 0.f);
+      v.w = fmaxf(v.w, 0.f);
+    }
+    st4(y + o, v);
+    if (mk) *reinterpret_cast<uchar4*>(mk + o) = make_uchar4(v.x > 0.f, v.y > 0.f, v.z > 0.f, v.w > 0.f);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply_nhwc_k(vfd_bn_desc d, const T* __restrict__ g,
+                                                                  const T* __restrict__ y, const T* __restrict__ x,
+                                                                  const double* __restrict__ sums, double count,
+                                                                  const float* __restrict__ gamma,
+                                                                  const float* __restrict__ mean_in,
+                                                                  const float* __restrict__ invstd_in,
+                                                                  T* __restrict__ dx, T* __restrict__ dr,
+                                                                  float* __restrict__ dgamma,
+                                                                  float* __restrict__ dbeta) {
+  __shared__ float4 coef[NH_MAXC];     // k, mean g', mx, mean
+  if (count <= 0.0) count = sums[2 * d.C];
+  for (int c = threadIdx.x; c < d.C; c += BN_THREADS) {
+    const double sg = sums[2 * c], sgx = sums[2 * c + 1];
+    const float mean = mean_in[c], invstd = invstd_in[c];
+    if (blockIdx.x == 0) {
+      if (dgamma) dgamma[c] = (float)(sgx * invstd);
+      if (dbeta) dbeta[c] = (float)sg;
+    }
+    coef[c] = make_float4(gamma[c] * invstd, (float)(sg / count), (float)(sgx / count) * invstd * invstd, mean);
+  }
+  __syncthreads();
+  const unsigned qm = (unsigned)(d.C >> 2) - 1u;
+  const unsigned total4 = (unsigned)d.N * (unsigned)d.HW * (unsigned)(d.C >> 2);
+  const bool relu = d.relu != 0;
+  for (unsigned i = blockIdx.x * BN_THREADS + threadIdx.x; i < total4; i += gridDim.x * BN_THREADS) {
+    const size_t o = 4 * (size_t)i;
+    const int c = 4 * (i & qm);
+    float4 gv = bn_g4(d, g, o);
+    if (relu) relu_mask4(d, y, o, gv);
+    if (dr) st4(dr + o, gv);
+    if (dx) {
+      const float4 xv = ld4(x + o);
+      const float4 k0 = coef[c], k1 = coef[c + 1], k2 = coef[c + 2], k3 = coef[c + 3];
+      float4 o4;
+      o4.x = k0.x * (gv.x - k0.y - (xv.x - k0.w) * k0.z);
+      o4.y = k1.x * (gv.y - k1.y - (xv.y - k1.w) * k1.z);
+      o4.z = k2.x * (gv.z - k2.y - (xv.z - k2.w) * k2.z);
+      o4.w = k3.x * (gv.w - k3.y - (xv.w - k3.w) * k3.z);
+      st4(dx + o, o4);
+    }
+  }
+}
+
 }  // namespace vfd
 
 using namespace vfd;
+
+// grid of the NHWC apply passes: ~4 float4 per thread, at most 4096 blocks
+static int nh_apply_blocks(const vfd_bn_desc* d) {
+  const long long total4 = (long long)d->N * d->HW * (d->C >> 2);
+  long long b = (total4 + 4 * BN_THREADS - 1) / (4 * BN_THREADS);
+  return (int)(b < 1 ? 1 : b > 4096 ? 4096 : b);
+}
 
 extern "C" {
 
 int vfd_bn_splits(const vfd_bn_desc* d) {
   if (!d || d->N <= 0 || d->C <= 0 || d->HW <= 0) return 0;
+  if (d->nhwc) {          // row splits over all channels: ~4k elements per block, at most 2048
+    const long long rows = (long long)d->N * d->HW;
+    long long s = (rows * d->C + 4095) / 4096;
+    if (s > 2048) s = 2048;
+    if (s > rows) s = rows;
+    return (int)(s < 1 ? 1 : s);
+  }
   // ~4096 blocks per pass, >= 2048 elements per block
   const long long total = (long long)d->N * d->HW;
   long long s = (4096 + d->C - 1) / d->C;
@@ -515,6 +766,10 @@ static int bn_check(const vfd_bn_desc* d, const char* what) {
   VFD_REQUIRE(d && d->N > 0 && d->C > 0 && d->HW > 0 && d->S > 0 && d->S == vfd_bn_splits(d),
               "%s: bad descriptor (S must be vfd_bn_splits)", what);
   VFD_REQUIRE((long long)d->N * d->HW < (1LL << 31), "%s: more than 2^31 elements per channel", what);
+  if (d->nhwc)
+    VFD_REQUIRE(d->C % 4 == 0 && d->C <= NH_MAXC && ((d->C >> 2) & ((d->C >> 2) - 1)) == 0 &&
+                    (long long)d->N * d->HW * d->C < (1LL << 31),
+                "%s: channels-last needs C/4 a power of two, C <= %d and < 2^31 elements", what, NH_MAXC);
   return VFD_OK;
 }
 
@@ -523,6 +778,11 @@ int vfd_bn_fwd_stats(const vfd_bn_desc* d, const void* x, double* partial, void*
   VFD_REQUIRE(x && partial, "bn_fwd_stats: null argument");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_BN_FWD, s);
+  if (d->nhwc) {
+    if (d->dtype == 1) bn_stats_nhwc_k<__bf16><<<d->S, BN_THREADS, 0, s>>>(*d, (const __bf16*)x, partial);
+    else bn_stats_nhwc_k<float><<<d->S, BN_THREADS, 0, s>>>(*d, (const float*)x, partial);
+    return fail_launch("bn_fwd_stats");
+  }
   if (d->dtype == 1) bn_stats_k<__bf16><<<dim3(d->S, d->C), BN_THREADS, 0, s>>>(*d, (const __bf16*)x, partial);
   else bn_stats_k<float><<<dim3(d->S, d->C), BN_THREADS, 0, s>>>(*d, (const float*)x, partial);
   return fail_launch("bn_fwd_stats");
@@ -534,6 +794,10 @@ int vfd_bn_sum(const vfd_bn_desc* d, const double* partial, double count, double
   VFD_REQUIRE(partial && sums, "bn_sum: null argument");
   VFD_REQUIRE(invstd || (!dgamma && !dbeta), "bn_sum: dgamma / dbeta need invstd");
   hipStream_t s = (hipStream_t)stream;
+  if (d->S > 64) {
+    bn_sum_blk_k<<<d->C + 1, BN_THREADS, 0, s>>>(*d, partial, count, sums, invstd, dgamma, dbeta);
+    return fail_launch("bn_sum");
+  }
   bn_sum_k<<<(d->C + 1 + 255) / 256, 256, 0, s>>>(*d, partial, count, sums, invstd, dgamma, dbeta);
   return fail_launch("bn_sum");
 }
@@ -547,8 +811,21 @@ int vfd_bn_fwd_apply(const vfd_bn_desc* d, const void* x, const void* residual, 
                   (count > 0.0 || ns == 1),
               "bn_fwd_apply: bad argument (count <= 0 reads the count row of reduced sums: ns must be 1)");
   VFD_REQUIRE(!running_mean == !running_var, "bn_fwd_apply: running mean / var must come together");
+  VFD_REQUIRE(!d->nhwc || ns == 1, "bn_fwd_apply: channels-last takes reduced sums (vfd_bn_sum, ns = 1)");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_BN_FWD, s);
+  if (d->nhwc) {
+    unsigned char* mk = d->relu ? relu_mask : nullptr;
+    if (d->dtype == 1)
+      bn_apply_nhwc_k<__bf16><<<nh_apply_blocks(d), BN_THREADS, 0, s>>>(
+          *d, (const __bf16*)x, (const __bf16*)residual, sums, count, gamma, beta, (__bf16*)y, mean, invstd,
+          running_mean, running_var, num_batches_tracked, mk);
+    else
+      bn_apply_nhwc_k<float><<<nh_apply_blocks(d), BN_THREADS, 0, s>>>(
+          *d, (const float*)x, (const float*)residual, sums, count, gamma, beta, (float*)y, mean, invstd, running_mean,
+          running_var, num_batches_tracked, mk);
+    return fail_launch("bn_fwd_apply");
+  }
   if (d->dtype == 1)
     bn_apply_k<__bf16><<<dim3(d->S, d->C), BN_THREADS, 0, s>>>(*d, (const __bf16*)x, (const __bf16*)residual, sums, ns,
                                                                count, gamma, beta, (__bf16*)y, mean, invstd, running_mean,
@@ -568,6 +845,15 @@ int vfd_bn_bwd_stats(const vfd_bn_desc* d, const void* g, const void* y, const v
   VFD_REQUIRE(g && x && mean && partial && (y || !d->relu), "bn_bwd_stats: null argument");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_BN_BWD, s);
+  if (d->nhwc) {
+    if (d->dtype == 1)
+      bn_bwd_stats_nhwc_k<__bf16><<<d->S, BN_THREADS, 0, s>>>(*d, (const __bf16*)g, (const __bf16*)y,
+                                                              (const __bf16*)x, mean, partial);
+    else
+      bn_bwd_stats_nhwc_k<float><<<d->S, BN_THREADS, 0, s>>>(*d, (const float*)g, (const float*)y, (const float*)x,
+                                                             mean, partial);
+    return fail_launch("bn_bwd_stats");
+  }
   if (d->dtype == 1)
     bn_bwd_stats_k<__bf16><<<dim3(d->S, d->C), BN_THREADS, 0, s>>>(*d, (const __bf16*)g, (const __bf16*)y,
                                                                    (const __bf16*)x, mean, partial);
@@ -584,8 +870,20 @@ int vfd_bn_bwd_apply(const vfd_bn_desc* d, const void* g, const void* y, const v
   VFD_REQUIRE(g && x && sums && gamma && mean && invstd && (y || !d->relu) && (ns == 1 || ns == d->S) &&
                   (count > 0.0 || ns == 1),
               "bn_bwd_apply: bad argument (count <= 0 reads the count row of reduced sums: ns must be 1)");
+  VFD_REQUIRE(!d->nhwc || ns == 1, "bn_bwd_apply: channels-last takes reduced sums (vfd_bn_sum, ns = 1)");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_BN_BWD, s);
+  if (d->nhwc) {
+    if (d->dtype == 1)
+      bn_bwd_apply_nhwc_k<__bf16><<<nh_apply_blocks(d), BN_THREADS, 0, s>>>(
+          *d, (const __bf16*)g, (const __bf16*)y, (const __bf16*)x, sums, count, gamma, mean, invstd, (__bf16*)dx,
+          (__bf16*)dresidual, dgamma, dbeta);
+    else
+      bn_bwd_apply_nhwc_k<float><<<nh_apply_blocks(d), BN_THREADS, 0, s>>>(
+          *d, (const float*)g, (const float*)y, (const float*)x, sums, count, gamma, mean, invstd, (float*)dx,
+          (float*)dresidual, dgamma, dbeta);
+    return fail_launch("bn_bwd_apply");
+  }
   if (d->dtype == 1)
     bn_bwd_apply_k<__bf16><<<dim3(d->S, d->C), BN_THREADS, 0, s>>>(*d, (const __bf16*)g, (const __bf16*)y,
                                                                    (const __bf16*)x, sums, ns, count, gamma, mean, invstd,
@@ -598,7 +896,7 @@ int vfd_bn_bwd_apply(const vfd_bn_desc* d, const void* g, const void* y, const v
 }
 
 int vfd_bn1_fits(const vfd_bn_desc* d) {
-  return d && d->N > 0 && d->C > 0 && d->HW > 0 && (long long)d->N * d->HW <= (long long)BN1_MAX ? 1 : 0;
+  return d && !d->nhwc && d->N > 0 && d->C > 0 && d->HW > 0 && (long long)d->N * d->HW <= (long long)BN1_MAX ? 1 : 0;
 }
 
 int vfd_bn1_fwd(const vfd_bn_desc* d, const void* x, const void* residual, const float* gamma, const float* beta,

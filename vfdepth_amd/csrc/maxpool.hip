@@ -144,6 +144,102 @@ __global__ __launch_bounds__(256) void maxpool_bwd_k(const T* __restrict__ g, co
   }
 }
 
+// ---- channels-last (config 3's bf16 encoders, layers.ResnetEncoder.use_channels_last): x [n][h][w][C],
+// y / arg [n][ho][wo][C].  One thread per (output pixel, channel quad): every tap is one 4-channel
+// load contiguous across the wave; the taps, their order and the selection are maxpool_fwd_k's,
+// per channel.
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool_nhwc_fwd_k(const T* __restrict__ x, T* __restrict__ y,
+                                                          uint8_t* __restrict__ arg, int n, int C, int h, int w,
+                                                          int ho, int wo) {
+  // 32-bit index math (host-checked < 2^31 work items): 64-bit division is a long software sequence
+  const unsigned Q = (unsigned)C >> 2;
+  const unsigned total = (unsigned)n * ho * wo * Q;
+  for (unsigned t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+    const unsigned q = t % Q;
+    const unsigned pix = t / Q;                        // (img, oy, ox)
+    const int ox = (int)(pix % (unsigned)wo);
+    const unsigned r = pix / (unsigned)wo;
+    const int oy = (int)(r % (unsigned)ho);
+    const unsigned img = r / (unsigned)ho;
+    const T* xp = x + (size_t)img * h * w * C + 4 * q;
+    float best[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    int bi[4] = {4, 4, 4, 4};
+    bool first[4] = {true, true, true, true};
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const int yy = 2 * oy - 1 + k / 3, xx = 2 * ox - 1 + k % 3;
+      if (yy < 0 || yy >= h || xx < 0 || xx >= w) continue;
+      const float4 v4 = ld4(xp + ((size_t)yy * w + xx) * C);
+      const float v[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (first[e] || v[e] > best[e] || isnan(v[e])) {
+          best[e] = v[e];
+          bi[e] = k;
+          first[e] = false;
+        }
+    }
+    const size_t o = (size_t)pix * C + 4 * q;
+    st4(y + o, make_float4(best[0], best[1], best[2], best[3]));
+    *reinterpret_cast<uchar4*>(arg + o) = make_uchar4(bi[0], bi[1], bi[2], bi[3]);
+  }
+}
+
+// channels-last backward: one thread per (2x2 input block, channel quad), maxpool_bwd_k's gather
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool_nhwc_bwd_k(const T* __restrict__ g, const uint8_t* __restrict__ arg,
+                                                          T* __restrict__ dx, int n, int C, int h, int w, int ho,
+                                                          int wo) {
+  const unsigned Q = (unsigned)C >> 2, hb = (h + 1) / 2, wb = (w + 1) / 2;
+  const unsigned total = (unsigned)n * hb * wb * Q;
+  for (unsigned t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+    const unsigned q = t % Q;
+    const unsigned blk = t / Q;
+    const int bj = (int)(blk % wb);
+    const unsigned r = blk / wb;
+    const int bi = (int)(r % hb);
+    const unsigned img = r / hb;
+    const bool r1 = bi + 1 < ho, c1 = bj + 1 < wo;
+    const size_t base = (size_t)img * ho * wo;
+    const size_t o00 = base + (size_t)bi * wo + bj;
+    const size_t o01 = c1 ? o00 + 1 : o00, o10 = r1 ? o00 + wo : o00, o11 = (r1 && c1) ? o00 + wo + 1 : o00;
+    const size_t cq = 4 * (size_t)q;
+    const uchar4 l00 = *reinterpret_cast<const uchar4*>(arg + o00 * C + cq);
+    const uchar4 l01 = *reinterpret_cast<const uchar4*>(arg + o01 * C + cq);
+    const uchar4 l10 = *reinterpret_cast<const uchar4*>(arg + o10 * C + cq);
+    const uchar4 l11 = *reinterpret_cast<const uchar4*>(arg + o11 * C + cq);
+    const float4 g00 = ld4(g + o00 * C + cq), g01 = ld4(g + o01 * C + cq);
+    const float4 g10 = ld4(g + o10 * C + cq), g11 = ld4(g + o11 * C + cq);
+    const unsigned char A00[4] = {l00.x, l00.y, l00.z, l00.w}, A01[4] = {l01.x, l01.y, l01.z, l01.w};
+    const unsigned char A10[4] = {l10.x, l10.y, l10.z, l10.w}, A11[4] = {l11.x, l11.y, l11.z, l11.w};
+    const float G00[4] = {g00.x, g00.y, g00.z, g00.w}, G01[4] = {g01.x, g01.y, g01.z, g01.w};
+    const float G10[4] = {g10.x, g10.y, g10.z, g10.w}, G11[4] = {g11.x, g11.y, g11.z, g11.w};
+    float d00[4], d01[4], d10[4], d11[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int a00 = A00[e], a01 = c1 ? A01[e] : 255, a10 = r1 ? A10[e] : 255, a11 = (r1 && c1) ? A11[e] : 255;
+      d00[e] = 0.f; d01[e] = 0.f; d10[e] = 0.f; d11[e] = 0.f;
+      if (a00 == 4) d00[e] += G00[e];
+      if (a00 == 5) d01[e] += G00[e];
+      if (a01 == 3) d01[e] += G01[e];
+      if (a00 == 7) d10[e] += G00[e];
+      if (a10 == 1) d10[e] += G10[e];
+      if (a00 == 8) d11[e] += G00[e];
+      if (a01 == 6) d11[e] += G01[e];
+      if (a10 == 2) d11[e] += G10[e];
+      if (a11 == 0) d11[e] += G11[e];
+    }
+    const int y0 = 2 * bi, x0 = 2 * bj;
+    T* dp = dx + (((size_t)img * h + y0) * w + x0) * C + cq;
+    st4(dp, make_float4(d00[0], d00[1], d00[2], d00[3]));
+    if (x0 + 1 < w) st4(dp + C, make_float4(d01[0], d01[1], d01[2], d01[3]));
+    if (y0 + 1 < h) {
+      st4(dp + (size_t)w * C, make_float4(d10[0], d10[1], d10[2], d10[3]));
+      if (x0 + 1 < w) st4(dp + (size_t)w * C + C, make_float4(d11[0], d11[1], d11[2], d11[3]));
+    }
+  }
+}
 
 // The encoders' input normalisation (image - 0.45) / 0.225 (packnet ResnetEncoder), fused with the
 // pose net's frame concatenation torch.cat([frame_a, frame_b], dim=channels) (fusion_posenet.py:
@@ -217,6 +313,40 @@ int vfd_normalize_cat(const float* a, const float* b, float* dst, long long n_im
   vfd::norm_cat_k<<<(unsigned)((n + 255) / 256), 256, 0, s>>>((const float4*)a, (const float4*)(b ? b : a),
                                                               (float4*)dst, n_img, ca, cb, hw / 4);
   return vfd::fail_launch("normalize_cat");
+}
+
+int vfd_maxpool3s2_nhwc_fwd(const void* x, void* y, uint8_t* arg, int n, int c, int h, int w, int dtype,
+                            void* stream) {
+  VFD_REQUIRE(x && y && arg && n > 0 && c > 0 && c % 4 == 0 && h > 0 && w > 0 && (dtype == 0 || dtype == 1) &&
+                  (long long)n * h * w * c < (1LL << 31),
+              "maxpool3s2_nhwc: bad arguments (C % 4 == 0)");
+  hipStream_t s = (hipStream_t)stream;
+  vfd::ProfScope ps(vfd::K_MAXPOOL, s);
+  const int ho = (h - 1) / 2 + 1, wo = (w - 1) / 2 + 1;
+  const long long total = (long long)n * ho * wo * (c / 4);
+  const unsigned grid = (unsigned)std::min<long long>((total + 255) / 256, 16384);
+  if (dtype == 1)
+    vfd::maxpool_nhwc_fwd_k<__bf16><<<grid, 256, 0, s>>>((const __bf16*)x, (__bf16*)y, arg, n, c, h, w, ho, wo);
+  else
+    vfd::maxpool_nhwc_fwd_k<float><<<grid, 256, 0, s>>>((const float*)x, (float*)y, arg, n, c, h, w, ho, wo);
+  return vfd::fail_launch("maxpool3s2_nhwc_fwd");
+}
+
+int vfd_maxpool3s2_nhwc_bwd(const void* g, const uint8_t* arg, void* dx, int n, int c, int h, int w, int dtype,
+                            void* stream) {
+  VFD_REQUIRE(g && arg && dx && n > 0 && c > 0 && c % 4 == 0 && h > 0 && w > 0 && (dtype == 0 || dtype == 1) &&
+                  (long long)n * h * w * c < (1LL << 31),
+              "maxpool3s2_nhwc: bad arguments (C % 4 == 0)");
+  hipStream_t s = (hipStream_t)stream;
+  vfd::ProfScope ps(vfd::K_MAXPOOL, s);
+  const int ho = (h - 1) / 2 + 1, wo = (w - 1) / 2 + 1;
+  const long long total = (long long)n * ((h + 1) / 2) * ((w + 1) / 2) * (c / 4);
+  const unsigned grid = (unsigned)std::min<long long>((total + 255) / 256, 16384);
+  if (dtype == 1)
+    vfd::maxpool_nhwc_bwd_k<__bf16><<<grid, 256, 0, s>>>((const __bf16*)g, arg, (__bf16*)dx, n, c, h, w, ho, wo);
+  else
+    vfd::maxpool_nhwc_bwd_k<float><<<grid, 256, 0, s>>>((const float*)g, arg, (float*)dx, n, c, h, w, ho, wo);
+  return vfd::fail_launch("maxpool3s2_nhwc_bwd");
 }
 
 }  // extern "C"

@@ -1102,6 +1102,7 @@ class AggregateUp(torch.autograd.Function):
 # =============================================================================================
 _BN_ONE = os.environ.get('VFD_BN_ONE', '1') != '0'      # one-launch BN for small layers
 _BN_JOIN = os.environ.get('VFD_BN_JOIN', '1') != '0'    # residual join (BatchNormAct.forward)
+_BN_NHWC = os.environ.get('VFD_BN_NHWC', '1') != '0'    # channels-last maps stay channels-last
 _DEC_CONV = os.environ.get('VFD_DEC_CONV', '1') != '0'   # decoder's narrow convs on MFMA (decconv.hip)
 
 
@@ -1129,6 +1130,25 @@ def _bn_sync(lib, d, partial, pg, count, what, invstd=None, dgamma=None, dbeta=N
     return sums
 
 
+def _bn_reduce(lib, d, partial, count, what, invstd=None, dgamma=None, dbeta=None):
+    """The [C][S][2] partials reduced to [C + 1][2] sums (row C = the element count) on this rank."""
+    sums = torch.empty(d.C + 1, 2, dtype=torch.float64, device=partial.device)
+    L.check(lib.vfd_bn_sum(ctypes.byref(d), partial.data_ptr(), float(count), sums.data_ptr(), L.ptr(invstd),
+                           L.ptr(dgamma), L.ptr(dbeta), L.stream()), what)
+    return sums
+
+
+def _bn_nhwc(x):
+    """x is a channels-last map the NHWC kernels take (C/4 a power of two, C <= 2048)."""
+    C = x.shape[1]
+    return (_BN_NHWC and x.dim() == 4 and not x.is_contiguous() and x.is_contiguous(memory_format=torch.channels_last)
+            and C % 4 == 0 and C <= 2048 and ((C >> 2) & ((C >> 2) - 1)) == 0)
+
+
+def _bn_fields(d):
+    return (d.N, d.C, d.HW, d.S, d.relu, d.eps, d.momentum, d.dtype, None, None, d.nhwc)
+
+
 class BatchNormAct(torch.autograd.Function):
     """y = relu(batch_norm_train(x) [+ r]) for NCHW fp32 x (one statistics + one apply pass each
     way; running statistics updated like nn.BatchNorm2d.train()).  `pg`: the SyncBatchNorm group
@@ -1141,12 +1161,16 @@ class BatchNormAct(torch.autograd.Function):
         _check_device(x, 'batch norm input')
         if x.dtype not in (torch.float32, torch.bfloat16):
             raise RuntimeError(f'fused batch norm: fp32 or bf16 activations, got {x.dtype}')
-        x = x.contiguous()
         N, C, H, W = x.shape
+        # channels-last maps (config 3's bf16 encoders, layers.ResnetEncoder) stay channels-last
+        fmt = torch.channels_last if _bn_nhwc(x) else torch.contiguous_format
+        x = x.contiguous(memory_format=fmt)
         # bf16 activations (config 3's autocast: the conv outputs are bf16), fp32 parameters / stats
         d = L.BnDesc(N, C, H * W, 0, int(relu), float(eps), float(momentum), int(x.dtype == torch.bfloat16))
+        d.nhwc = int(fmt is torch.channels_last)
         d.S = lib.vfd_bn_splits(ctypes.byref(d))
-        r = residual.to(x.dtype).contiguous() if residual is not None else None
+        ctx.fmt = fmt
+        r = residual.to(x.dtype).contiguous(memory_format=fmt) if residual is not None else None
         # residual join: when the residual is the output of the previous block's fused BN (an
         # identity block), this layer's d residual (= g masked by its ReLU) is handed to that BN's
         # backward, which sums it into its own incoming gradient on load — no d residual tensor and
@@ -1159,7 +1183,7 @@ class BatchNormAct(torch.autograd.Function):
         ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
         # with ReLU the forward also stores [y > 0] as one byte per element: the backward reads
         # that mask instead of y (d.relu == 2 there), a quarter of the bytes
-        mk = torch.empty(x.shape, dtype=torch.uint8, device=x.device) if relu else None
+        mk = torch.empty_like(x, dtype=torch.uint8) if relu else None
         ctx.one = pg is None and _BN_ONE and bool(lib.vfd_bn1_fits(ctypes.byref(d)))
         if ctx.one:       # small layer, local statistics: one launch (bnact.hip bn1_fwd_k)
             y = torch.empty_like(x)
@@ -1168,7 +1192,7 @@ class BatchNormAct(torch.autograd.Function):
             L.check(lib.vfd_bn1_fwd(ctypes.byref(d), x.data_ptr(), ptr(r), gamma.data_ptr(), beta.data_ptr(),
                                     y.data_ptr(), mean.data_ptr(), invstd.data_ptr(), ptr(running_mean),
                                     ptr(running_var), ptr(nbt), ptr(mk), L.stream()), 'bn1_fwd')
-            ctx.d, ctx.pg, ctx.count, ctx.has_res = (d.N, d.C, d.HW, d.S, d.relu, d.eps, d.momentum, d.dtype), pg, float(N * H * W), r is not None
+            ctx.d, ctx.pg, ctx.count, ctx.has_res = _bn_fields(d), pg, float(N * H * W), r is not None
             if L.PROF_ON:
                 L.ALG_BYTES['bn_fwd'] += x.numel() * (2 * x.element_size() + x.element_size() * (r is not None)
                                                       + (mk is not None))
@@ -1180,6 +1204,8 @@ class BatchNormAct(torch.autograd.Function):
         if pg is not None:          # global sums and count from the group; count 0 = read on device
             sums, ns = _bn_sync(lib, d, partial, pg, count, 'bn_sum'), 1
             count = 0.0
+        elif d.nhwc:                # channels-last apply passes take reduced sums
+            sums, ns = _bn_reduce(lib, d, partial, count, 'bn_sum'), 1
         y = torch.empty_like(x)
         mean = torch.empty(C, device=x.device)
         invstd = torch.empty(C, device=x.device)
@@ -1190,7 +1216,7 @@ class BatchNormAct(torch.autograd.Function):
                                      running_var.data_ptr() if running_var is not None else None,
                                      nbt.data_ptr() if nbt is not None else None, ptr(mk), L.stream()),
                 'bn_fwd_apply')
-        ctx.d, ctx.pg, ctx.count, ctx.has_res = (d.N, d.C, d.HW, d.S, d.relu, d.eps, d.momentum, d.dtype), pg, count, r is not None
+        ctx.d, ctx.pg, ctx.count, ctx.has_res = _bn_fields(d), pg, count, r is not None
         if L.PROF_ON:                        # compulsory: x (+ r) in, y (+ the ReLU byte mask) out
             L.ALG_BYTES['bn_fwd'] += x.numel() * (2 * x.element_size() + x.element_size() * (r is not None)
                                                   + (mk is not None))
@@ -1204,7 +1230,7 @@ class BatchNormAct(torch.autograd.Function):
         d = L.BnDesc(*ctx.d)
         if d.relu:
             d.relu = 2                       # the ReLU mask is the forward's byte mask
-        g = g.to(x.dtype).contiguous()
+        g = g.to(x.dtype).contiguous(memory_format=ctx.fmt)
         need = ctx.needs_input_grad
         ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
         # the next block's identity-branch gradient, deposited by its backward (residual join)
@@ -1247,6 +1273,9 @@ class BatchNormAct(torch.autograd.Function):
         if ctx.pg is not None:      # local d gamma / d beta, then the global sums (+ count row)
             sums, ns = _bn_sync(lib, d, partial, ctx.pg, x.shape[0] * d.HW, 'bn_sum', invstd, dgamma, dbeta), 1
             count, pg_dgamma, pg_dbeta = 0.0, None, None
+        elif d.nhwc:                # channels-last: reduced sums (d gamma / d beta written there)
+            sums, ns = _bn_reduce(lib, d, partial, count, 'bn_sum', invstd, dgamma, dbeta), 1
+            pg_dgamma, pg_dbeta = None, None
         if L.PROF_ON:                        # compulsory: g, x (, the mask) in, dx (, dr) out
             es = x.element_size()
             L.ALG_BYTES['bn_bwd'] += x.numel() * (2 * es + (d.relu != 0) + es * ((dx is not None) + (dr is not None))
@@ -1473,23 +1502,31 @@ def normalize_cat(a, b=None):
 # =============================================================================================
 class MaxPool3s2(torch.autograd.Function):
     """F.max_pool2d(x, 3, 2, 1) for NCHW fp32 or bf16 x (maxpool.hip): one byte of window index
-    per output instead of ATen's int64 indices; deterministic gather backward."""
+    per output instead of ATen's int64 indices; deterministic gather backward.  A channels-last x
+    (config 3's bf16 encoders, C % 4 == 0) takes the NHWC kernels and gives a channels-last y."""
 
     @staticmethod
     def forward(ctx, x):
         lib = L.load()
         _check_device(x, 'max pool input')
-        x = x.contiguous()
+        cl = (x.dim() == 4 and x.shape[1] % 4 == 0 and not x.is_contiguous()
+              and x.is_contiguous(memory_format=torch.channels_last))
+        fmt = torch.channels_last if cl else torch.contiguous_format
+        x = x.contiguous(memory_format=fmt)
         *lead, h, w = x.shape
         ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
-        y = torch.empty(*lead, ho, wo, dtype=x.dtype, device=x.device)
-        arg = torch.empty(*lead, ho, wo, dtype=torch.uint8, device=x.device)
-        planes = x.numel() // (h * w)
-        L.check(lib.vfd_maxpool3s2_fwd(x.data_ptr(), y.data_ptr(), arg.data_ptr(), planes, h, w, _dt(x), L.stream()),
-                'maxpool3s2_fwd')
+        y = torch.empty(*lead, ho, wo, dtype=x.dtype, device=x.device, memory_format=fmt)
+        arg = torch.empty(*lead, ho, wo, dtype=torch.uint8, device=x.device, memory_format=fmt)
+        if cl:
+            L.check(lib.vfd_maxpool3s2_nhwc_fwd(x.data_ptr(), y.data_ptr(), arg.data_ptr(), x.shape[0], x.shape[1],
+                                                h, w, _dt(x), L.stream()), 'maxpool3s2_nhwc_fwd')
+        else:
+            planes = x.numel() // (h * w)
+            L.check(lib.vfd_maxpool3s2_fwd(x.data_ptr(), y.data_ptr(), arg.data_ptr(), planes, h, w, _dt(x),
+                                           L.stream()), 'maxpool3s2_fwd')
         if L.PROF_ON:
             L.ALG_BYTES['maxpool'] += (x.numel() + y.numel()) * x.element_size() + arg.numel()
-        ctx.shape, ctx.dtype = tuple(x.shape), x.dtype
+        ctx.shape, ctx.dtype, ctx.fmt = tuple(x.shape), x.dtype, fmt
         ctx.save_for_backward(arg)
         return y
 
@@ -1497,12 +1534,16 @@ class MaxPool3s2(torch.autograd.Function):
     def backward(ctx, g):
         lib = L.load()
         arg, = ctx.saved_tensors
-        g = g.to(ctx.dtype).contiguous()
+        g = g.to(ctx.dtype).contiguous(memory_format=ctx.fmt)
         h, w = ctx.shape[-2:]
-        dx = torch.empty(ctx.shape, dtype=ctx.dtype, device=g.device)
-        planes = dx.numel() // (h * w)
-        L.check(lib.vfd_maxpool3s2_bwd(g.data_ptr(), arg.data_ptr(), dx.data_ptr(), planes, h, w, _dt(dx), L.stream()),
-                'maxpool3s2_bwd')
+        dx = torch.empty(ctx.shape, dtype=ctx.dtype, device=g.device, memory_format=ctx.fmt)
+        if ctx.fmt is torch.channels_last:
+            L.check(lib.vfd_maxpool3s2_nhwc_bwd(g.data_ptr(), arg.data_ptr(), dx.data_ptr(), ctx.shape[0],
+                                                ctx.shape[1], h, w, _dt(dx), L.stream()), 'maxpool3s2_nhwc_bwd')
+        else:
+            planes = dx.numel() // (h * w)
+            L.check(lib.vfd_maxpool3s2_bwd(g.data_ptr(), arg.data_ptr(), dx.data_ptr(), planes, h, w, _dt(dx),
+                                           L.stream()), 'maxpool3s2_bwd')
         if L.PROF_ON:
             L.ALG_BYTES['maxpool'] += (g.numel() + dx.numel()) * dx.element_size() + arg.numel()
         return dx

@@ -216,6 +216,17 @@ class ResnetEncoder(nn.Module):
         if num_layers > 34:
             self.num_ch_enc[1:] *= 4
         self.encoder = ResNetTrunk(num_layers, num_input_images)
+        self.channels_last = False
+
+    def use_channels_last(self):
+        """Config 3's bf16 encoders run channels-last: the conv weights (and through them every map:
+        ATen's MIOpen convs take the channels-last layout when input or weight has it) live NHWC,
+        so MIOpen's bf16 convs skip their NCHW <-> NHWC transposes and the fused BN kernels take
+        the maps as they are (bnact.hip, d.nhwc).  The returned pyramid is channels-last; its
+        consumers (1x1 aggregation slices, HIP ops via .contiguous()) accept either layout."""
+        self.channels_last = True
+        self.to(memory_format=torch.channels_last)
+        return self
 
     def forward(self, image, normalized=False):
         """image: [n, 3*num_input_images, H, W] in [0, 1]; normalized=True: already (x - 0.45) / 0.225

@@ -16,6 +16,10 @@ from .layers import (MonoDepthDecoder, PoseDecoder, ResnetEncoder, conv2d_block,
                      unpack_cam_feat, upsample)
 
 
+# config 3 (bf16 nets): channels-last encoders unless training.channels_last says otherwise
+_CL_DEFAULT = os.environ.get('VFD_CHANNELS_LAST', '1') != '0'
+
+
 def _encoder_input(frames):
     """cat(frames, channels) of [B, N, 3, H, W] batches, packed to [B*N, ...]: the fused nets' encoder
     input.  On the GPU (fp32, no gradient, H*W % 4 == 0) it comes normalised from one HIP pass
@@ -145,6 +149,8 @@ class FusedDepthNet(nn.Module):
         self.decoder = FusionDepthDecoder(lvl, self.encoder.num_ch_enc[:lvl + 1], [16, 32, 64, 128, 256],
                                           self.scales, use_skips=bool(m['use_skips']))
         self.bf16 = t.get('net_precision', 'fp32') == 'bf16'
+        if self.bf16 and t.get('channels_last', _CL_DEFAULT):
+            self.encoder.use_channels_last()
 
     def forward(self, inputs):
         outputs = {('cam', c): {} for c in range(self.num_cams)}
@@ -189,6 +195,8 @@ class FusedPoseNet(nn.Module):
         self.pose_decoder = PoseDecoder(num_ch_enc=[out_dim], num_input_features=1,
                                         num_frames_to_predict_for=1, stride=2)
         self.bf16 = cfg['training'].get('net_precision', 'fp32') == 'bf16'
+        if self.bf16 and cfg['training'].get('channels_last', _CL_DEFAULT):
+            self.encoder.use_channels_last()
 
     def forward(self, inputs, frame_ids, _cam=None):
         frames = [inputs[('color_aug', frame_ids[0], 0)], inputs[('color_aug', frame_ids[1], 0)]]

@@ -32,6 +32,7 @@ def timed(fn, iters):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--iters', type=int, default=10)
+    ap.add_argument('--batch', type=int, default=1, help='>1: also the data gradient at that batch vs per image')
     a = ap.parse_args()
     dev = torch.device('cuda:0')
     C, Y, X, O = 5140, 100, 100, 256
@@ -66,6 +67,21 @@ def main():
         dcols = torch.mm(w2.t(), g.reshape(O, -1))
         return F.fold(dcols[None], (Y + 2, X + 2), 3, stride=2)
     res['dgrad_gemm_fold'] = timed(dgrad_gemm, a.iters)
+    if a.batch > 1:     # config 3 (B = 2): one call over the batch vs one call per image
+        nb = a.batch
+        xb = torch.randn(nb, C, Y + 2, X + 2, device=dev).contiguous(memory_format=torch.channels_last)
+        gb = torch.randn(nb, O, 50, 50, device=dev).contiguous(memory_format=torch.channels_last)
+        res[f'dgrad_cl_n{nb}'] = timed(lambda: cb(gb, xb, w, *args, [True, False, False]), a.iters) / nb
+        res[f'dgrad_cl_per_image_n{nb}'] = timed(
+            lambda: [cb(gb[i:i + 1], xb[i:i + 1], w, *args, [True, False, False]) for i in range(nb)], a.iters) / nb
+        w16, xb16, gb16 = w.bfloat16(), xb.bfloat16(), gb.bfloat16()
+        res[f'wgrad_cl_bf16_n{nb}'] = timed(lambda: cb(gb16, xb16, w16, *args, [False, True, True]), a.iters) / nb
+        res[f'wgrad_cl_bf16_per_image_n{nb}'] = timed(
+            lambda: [cb(gb16[i:i + 1], xb16[i:i + 1], w16, *args, [False, True, True]) for i in range(nb)], a.iters) / nb
+        da = cb(gb, xb, w, *args, [True, False, False])[0]
+        dp = torch.cat([cb(gb[i:i + 1], xb[i:i + 1], w, *args, [True, False, False])[0] for i in range(nb)])
+        print(f'per-image vs batched dgrad max rel err {float((da - dp).abs().max() / da.abs().max()):.2e} '
+              '(times per image below)', flush=True)
     ref = F.conv2d(x_cl, w, b, stride=2)
     err = float((fwd_gemm().reshape(1, O, 50, 50) - ref).abs().max() / ref.abs().max())
     for k, v in res.items():

@@ -16,8 +16,16 @@ from .layers import (MonoDepthDecoder, PoseDecoder, ResnetEncoder, conv2d_block,
                      unpack_cam_feat, upsample)
 
 
-# config 3 (bf16 nets): channels-last encoders unless training.channels_last says otherwise
-_CL_DEFAULT = os.environ.get('VFD_CHANNELS_LAST', '1') != '0'
+# channels-last encoders: training.channels_last when set, else VFD_CHANNELS_LAST — '1' (default):
+# the bf16 nets (config 3) only, 'all': fp32 ones too, '0': never
+_CL_ENV = os.environ.get('VFD_CHANNELS_LAST', '1')
+
+
+def _use_channels_last(training, bf16):
+    cl = training.get('channels_last')
+    if cl is None:
+        cl = _CL_ENV == 'all' or (bf16 and _CL_ENV != '0')
+    return bool(cl)
 
 
 def _encoder_input(frames):
@@ -149,7 +157,7 @@ class FusedDepthNet(nn.Module):
         self.decoder = FusionDepthDecoder(lvl, self.encoder.num_ch_enc[:lvl + 1], [16, 32, 64, 128, 256],
                                           self.scales, use_skips=bool(m['use_skips']))
         self.bf16 = t.get('net_precision', 'fp32') == 'bf16'
-        if self.bf16 and t.get('channels_last', _CL_DEFAULT):
+        if _use_channels_last(t, self.bf16):
             self.encoder.use_channels_last()
 
     def forward(self, inputs):
@@ -195,7 +203,7 @@ class FusedPoseNet(nn.Module):
         self.pose_decoder = PoseDecoder(num_ch_enc=[out_dim], num_input_features=1,
                                         num_frames_to_predict_for=1, stride=2)
         self.bf16 = cfg['training'].get('net_precision', 'fp32') == 'bf16'
-        if self.bf16 and cfg['training'].get('channels_last', _CL_DEFAULT):
+        if _use_channels_last(cfg['training'], self.bf16):
             self.encoder.use_channels_last()
 
     def forward(self, inputs, frame_ids, _cam=None):

@@ -85,6 +85,32 @@ def test_net_precision_flag():
         VFDepthAlgo(C.surround_fusion_cfg(net_precision='fp16'), 'cpu')
 
 
+def test_channels_last_encoder_switch():
+    """The bf16 nets (config 3) build channels-last encoders (NHWC conv weights: MIOpen then runs
+    their convs without layout transposes, the fused BN / max pool take their NHWC kernels); the
+    fp32 nets stay NCHW; `training.channels_last` overrides either way.  Same values either way:
+    the state dict round-trips between the layouts."""
+    from vfdepth_amd import config as C
+    from vfdepth_amd.network import FusedDepthNet, FusedPoseNet
+    cl = torch.channels_last
+
+    def is_cl(net):
+        w = net.encoder.encoder.layer1[0].conv1.weight
+        return w.is_contiguous(memory_format=cl) and not w.is_contiguous()
+    fp32, bf16 = C.surround_fusion_cfg(), C.surround_fusion_cfg(net_precision='bf16')
+    assert not is_cl(FusedDepthNet(fp32)) and not is_cl(FusedPoseNet(fp32))
+    assert is_cl(FusedDepthNet(bf16)) and is_cl(FusedPoseNet(bf16))
+    bf16['training']['channels_last'] = False
+    assert not is_cl(FusedPoseNet(bf16))
+    fp32['training']['channels_last'] = True
+    a = FusedPoseNet(fp32)
+    assert is_cl(a)
+    b = FusedPoseNet(C.surround_fusion_cfg())
+    b.load_state_dict(a.state_dict())
+    for (k, va), vb in zip(a.state_dict().items(), b.state_dict().values()):
+        assert torch.equal(va, vb), k
+
+
 def test_batched_pose_and_warp_matrices_match_per_camera():
     """The batched pose distribution + warp-matrix chain (one gather + batched products) equals the
     per-camera reference formulation (pose.py:66-96, view_rendering.py:118-198) bit for bit."""

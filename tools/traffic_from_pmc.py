@@ -34,16 +34,16 @@ OPS = {
     'smooth_bwd': ['smooth_bwd_k'],
     'aggregate': ['aggregate_fwd_k', 'aggregate_plane_fwd_k'],
     'proj_conv_fwd': ['pcv_main_k', 'pcvb_main_k', 'pcv_reduce_k'],
-    'proj_conv_dgrad': ['pcd_main_k', 'pcd_reduce_k'],
+    'proj_conv_dgrad': ['pcd_main_k', 'pcd_reduce_k', 'pcdf_main_k', 'pcdf_reduce_k'],
     'proj_conv_wgrad': ['pcw_main_k', 'pcw_reduce_k', 'pcw_bias_k', 'pcw_bias_fin_k'],
     'pad_conv_fwd': ['ppc_main_k', 'ppcb_main_k', 'ppc_reduce_k'],
     'depth_syn_fwd': ['depth_syn_fwd_k'],
     'depth_syn_bwd': ['depth_syn_bwd_k'],
-    'bn_fwd': ['bn_stats_k', 'bn_sum_k', 'bn_apply_k', 'bn1_fwd_k'],
-    'bn_bwd': ['bn_bwd_stats_k', 'bn_bwd_apply_k', 'bn1_bwd_k'],
+    'bn_fwd': ['bn_stats_k', 'bn_sum_k', 'bn_apply_k', 'bn1_fwd_k', 'bn_stats_nhwc_k', 'bn_sum_blk_k', 'bn_apply_nhwc_k'],
+    'bn_bwd': ['bn_bwd_stats_k', 'bn_bwd_apply_k', 'bn1_bwd_k', 'bn_bwd_stats_nhwc_k', 'bn_bwd_apply_nhwc_k'],
     'reflect_pad': ['reflect_pad_fwd_k', 'reflect_pad_bwd_k', 'lrelu_pad_bwd_nhwc_k'],
     'upsample_bwd': ['up_ac_bwd_x_k', 'up_ac_bwd_y_k', 'aggregate_plane_bwd_k'],
-    'maxpool': ['maxpool_fwd_k', 'maxpool_bwd_k'],
+    'maxpool': ['maxpool_fwd_k', 'maxpool_fwd4_k', 'maxpool_bwd_k', 'maxpool_nhwc_fwd_k', 'maxpool_nhwc_bwd_k'],
     'elu_pad': ['elu_up_pad_fwd_k', 'elu_up_pad_bwd_k'],
     'disp_conv': ['disp_conv_fwd_k', 'disp_conv_dgrad_k', 'disp_conv_wgrad_k'],
     'dec_conv': ['dconv_fwd_k', 'dconv_dgrad_k', 'dconv_wgrad_k'],
@@ -52,14 +52,14 @@ OPS = {
 # traffic is per call of any of these kernels, not per launch of the first one.
 ENTRY = {
     'aggregate': ['aggregate_fwd_k', 'aggregate_plane_fwd_k'],
-    'bn_fwd': ['bn_stats_k', 'bn_apply_k', 'bn1_fwd_k'],
-    'bn_bwd': ['bn_bwd_stats_k', 'bn_bwd_apply_k', 'bn1_bwd_k'],
+    'bn_fwd': ['bn_stats_k', 'bn_apply_k', 'bn1_fwd_k', 'bn_stats_nhwc_k', 'bn_apply_nhwc_k'],
+    'bn_bwd': ['bn_bwd_stats_k', 'bn_bwd_apply_k', 'bn1_bwd_k', 'bn_bwd_stats_nhwc_k', 'bn_bwd_apply_nhwc_k'],
     'upsample_bwd': ['up_ac_bwd_x_k', 'aggregate_plane_bwd_k'],
     'elu_pad': ['elu_up_pad_fwd_k', 'elu_up_pad_bwd_k'],
     'disp_conv': ['disp_conv_fwd_k', 'disp_conv_dgrad_k'],
     'dec_conv': ['dconv_fwd_k', 'dconv_dgrad_k'],
     'reflect_pad': ['reflect_pad_fwd_k', 'reflect_pad_bwd_k', 'lrelu_pad_bwd_nhwc_k'],
-    'maxpool': ['maxpool_fwd_k', 'maxpool_bwd_k'],
+    'maxpool': ['maxpool_fwd_k', 'maxpool_fwd4_k', 'maxpool_bwd_k', 'maxpool_nhwc_fwd_k', 'maxpool_nhwc_bwd_k'],
 }
 
 

@@ -3,6 +3,8 @@
 #include <stdarg.h>
 
 #include <mutex>
+#include <set>
+#include <utility>
 #include <vector>
 
 #include "vfd_common.h"
@@ -27,6 +29,16 @@ int fail_launch(const char* what) {
     return VFD_ELAUNCH;
   }
   return VFD_OK;
+}
+
+void lds_attr(const void* fn, int bytes) {
+  static std::mutex mu;
+  static std::set<std::pair<const void*, int>> done;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(mu);
+  if (done.insert({fn, dev}).second)
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
 }
 
 // ---------------------------------------------------------------- profiling

@@ -457,12 +457,7 @@ int vfd_pad_conv_fwd(const vfd_conv_desc* d, const float* x, const float* Wf, co
   VFD_REQUIRE(ws && ws_bytes >= vfd_pad_conv_fwd_workspace(d), "pad_conv_fwd: workspace too small");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_PAD_CONV_FWD, s);
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(ppc_main_k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              PP_LDS_MAX);
-    attr = true;
-  }
+  lds_attr(reinterpret_cast<const void*>(ppc_main_k), PP_LDS_MAX);
   float* partial = (float*)ws;
   ppc_main_k<<<g.ngroup, PP_THREADS, (size_t)2 * g.lds_floats * sizeof(float), s>>>(g, x, Wf, bias, out, partial);
   ppc_reduce_k<float><<<dim3(g.ntile, PP_FSL), 256, 0, s>>>(g, partial, bias, out);
@@ -484,12 +479,7 @@ int vfd_pad_conv_fwd_bf16(const vfd_conv_desc* d, const float* x, const void* Wf
   VFD_REQUIRE(ws && ws_bytes >= vfd_pad_conv_fwd_bf16_workspace(d), "pad_conv_fwd_bf16: workspace too small");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_PAD_CONV_FWD, s);
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(ppcb_main_k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              PP_LDS_MAX);
-    attr = true;
-  }
+  lds_attr(reinterpret_cast<const void*>(ppcb_main_k), PP_LDS_MAX);
   float* partial = (float*)ws;
   const size_t lds = (size_t)2 * g.hrows * g.wp * PPB_XS * 2;
   ppcb_main_k<<<g.ngroup, PP_THREADS, lds, s>>>(g, x, (const bf16x8*)Wf, partial);

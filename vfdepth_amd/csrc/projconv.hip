@@ -1421,12 +1421,7 @@ int vfd_proj_conv_dgrad(const vfd_voxel_desc* d, const float* g_pre, const float
   ProfScope ps(K_PROJ_CONV_DGRAD, s);
   if (d->pad_out == 2) {
     const PfGeom g = pf_plan(*d);
-    static bool fattr = false;
-    if (!fattr) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(pcdf_main_k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                PD_LDS_MAX);
-      fattr = true;
-    }
+    lds_attr(reinterpret_cast<const void*>(pcdf_main_k), PD_LDS_MAX);
     pcdf_main_k<<<g.ngroup, PC_THREADS, (size_t)2 * g.lds_floats * sizeof(float), s>>>(g, g_pre, Wd, dx, (float*)ws);
     pcdf_reduce_k<<<dim3(g.ngroup, PC_FSL), 256, 0, s>>>(g, (const float*)ws, dx);
     return fail_launch("proj_conv_dgrad");
@@ -1434,12 +1429,7 @@ int vfd_proj_conv_dgrad(const vfd_voxel_desc* d, const float* g_pre, const float
   const PdGeom g = pd_plan(*d);
   float* partial = (float*)ws;
   const size_t lds = (size_t)2 * g.lds_floats * sizeof(float);
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(pcd_main_k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                        PD_LDS_MAX);
-    attr = true;
-  }
+  lds_attr(reinterpret_cast<const void*>(pcd_main_k), PD_LDS_MAX);
   pcd_main_k<<<g.ngroup, PC_THREADS, lds, s>>>(g, g_pre, Wd, dx, partial);
   pcd_reduce_k<<<dim3(g.ngroup, PC_FSL), 256, 0, s>>>(g, partial, dx);
   return fail_launch("proj_conv_dgrad");

@@ -22,6 +22,10 @@ int fail_launch(const char* what);   // reads hipGetLastError, returns VFD_ELAUN
     }                                     \
   } while (0)
 
+// Raise kernel `fn`'s dynamic-LDS limit to `bytes` on the CURRENT device (the attribute is per
+// device): set once per (kernel, device), thread-safe (capi.hip).
+void lds_attr(const void* fn, int bytes);
+
 // ---------------------------------------------------------------- profiling hook
 enum KernelId {
   K_MASK_DOWN = 0, K_FUSE_DEPTH_FWD, K_FUSE_DEPTH_BWD, K_FUSE_POSE_FWD, K_FUSE_POSE_BWD,

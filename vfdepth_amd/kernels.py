@@ -6,6 +6,7 @@ missing library or a non-HIP tensor raises.
 """
 import ctypes
 import os
+import weakref
 
 import torch
 import torch.nn.functional as F
@@ -776,8 +777,11 @@ class ProjConvBF16(torch.autograd.Function):
         g_pre = lrelu_pad_backward(g.float(), out.float()).to(torch.bfloat16)
         mask = (ctx.needs_input_grad[1], ctx.needs_input_grad[4], ctx.needs_input_grad[5])
         wb = proj_conv_weight(w0.detach(), Cv, space.D).to(torch.bfloat16)
-        dx, dw, db = torch.ops.aten.convolution_backward(g_pre, x, wb, [O], [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
-                                                         [mask[0], mask[1], mask[2]])
+        if x is None:   # only the bias gradient was asked for (the forward wrote no side output)
+            dx, dw, db = None, None, g_pre.float().sum((0, 2, 3))
+        else:
+            dx, dw, db = torch.ops.aten.convolution_backward(g_pre, x, wb, [O], [1, 1], [0, 0], [1, 1], False, [0, 0],
+                                                             1, [mask[0], mask[1], mask[2]])
         dvox = dw0 = None
         if mask[0]:
             dxf = dx.float().contiguous(memory_format=torch.channels_last)
@@ -1149,6 +1153,11 @@ def _bn_fields(d):
     return (d.N, d.C, d.HW, d.S, d.relu, d.eps, d.momentum, d.dtype, None, None, d.nhwc)
 
 
+def _observed(t):
+    """Something reads t's gradient outside the autograd graph: a tensor hook or retain_grad."""
+    return bool(t.retains_grad or getattr(t, '_backward_hooks', None))
+
+
 class BatchNormAct(torch.autograd.Function):
     """y = relu(batch_norm_train(x) [+ r]) for NCHW fp32 x (one statistics + one apply pass each
     way; running statistics updated like nn.BatchNorm2d.train()).  `pg`: the SyncBatchNorm group
@@ -1175,11 +1184,18 @@ class BatchNormAct(torch.autograd.Function):
         # identity block), this layer's d residual (= g masked by its ReLU) is handed to that BN's
         # backward, which sums it into its own incoming gradient on load — no d residual tensor and
         # no autograd add of the two branches (the sum is the same fp32 add autograd performs)
+        # The join bypasses autograd's delivery of d residual to the residual tensor, so it is only
+        # taken when nothing observes that gradient: no tensor hooks and no retain_grad, checked
+        # here and again at backward time (through a weak reference).  A partial autograd.grad(...,
+        # inputs=[block output]) cannot be detected: set VFD_BN_JOIN=0 to inspect gradients of
+        # intermediate encoder tensors.
         ctx.pending = []
         ctx.res_node = None
+        ctx.res_ref = None
         if (join and _BN_JOIN and r is residual and residual.requires_grad
-                and type(residual.grad_fn).__name__ == 'BatchNormActBackward'):
+                and type(residual.grad_fn).__name__ == 'BatchNormActBackward' and not _observed(residual)):
             ctx.res_node = residual.grad_fn
+            ctx.res_ref = weakref.ref(residual)
         ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
         # with ReLU the forward also stores [y > 0] as one byte per element: the backward reads
         # that mask instead of y (d.relu == 2 there), a quarter of the bytes
@@ -1235,7 +1251,9 @@ class BatchNormAct(torch.autograd.Function):
         ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
         # the next block's identity-branch gradient, deposited by its backward (residual join)
         pending, ctx.pending = ctx.pending, []
-        joined = ctx.res_node is not None and need[3]
+        res = ctx.res_ref() if ctx.res_ref is not None else None
+        joined = ctx.res_node is not None and need[3] and not (res is not None and _observed(res))
+        ctx.res_ref = None
         # a join chain (this block both receives and hands on an identity-branch gradient, deeper
         # ResNets) and extra deposits fold with autograd's own adds; one deposit rides in the kernel
         for g2, m2 in (pending if joined else pending[1:]):
@@ -1244,7 +1262,7 @@ class BatchNormAct(torch.autograd.Function):
             d.g2, d.m2 = pending[0][0].data_ptr(), ptr(pending[0][1])
         if joined:      # hand d residual = g (ReLU-masked on load) to the block that produced r
             ctx.res_node.pending.append((g, mk if d.relu else None))
-            ctx.res_node = None
+        ctx.res_node = None
         want_dr = ctx.has_res and need[3] and not joined
         if ctx.one:
             dx = torch.empty_like(x) if need[0] else None

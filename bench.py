@@ -60,7 +60,14 @@ def job_throughput(elapsed, steps, world, batch_per_rank=1):
 
 
 def make_cfg(config, batch=None):
-    if config == 2:
+    if config == 0:
+        # the reduced 6-camera fusion step of the parity fixtures (tests/golden/common.step_cfg):
+        # multi-rank plumbing rehearsals, not a bench line
+        cfg = C.surround_fusion_cfg(height=96, width=160, batch_size=batch or 1, voxel_size=[40, 40, 10],
+                                    voxel_unit_size=[2.5, 2.5, 3.0], voxel_str_p=[-50.0, -50.0, -15.0],
+                                    proj_d_bins=16, focal_length_scale=30)
+        name = 'reduced 6-cam 96x160 fusion, voxel 40x40x10, D=16, fp32 (rehearsal)'
+    elif config == 2:
         cfg = C.surround_fusion_cfg(batch_size=batch or 1)
         name = '6-cam DDAD 384x640 fusion, voxel 100x100x20, D=50, fp32'
     elif config == 3:
@@ -294,8 +301,14 @@ def main():
     local = int(os.environ.get('LOCAL_RANK', '0'))
     if world != args.gpus:
         raise SystemExit(f'bench.py --gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU')
+    # test-only overrides (tests/test_gpu_0_bench_world2.py rehearses the multi-rank path on one
+    # GPU): VFD_BENCH_BACKEND=gloo, VFD_BENCH_ONE_DEVICE=1 puts every rank on cuda:0 (RCCL does not
+    # run two ranks on one device); the driver's runs set neither
+    backend = os.environ.get('VFD_BENCH_BACKEND', 'nccl')
+    if os.environ.get('VFD_BENCH_ONE_DEVICE') == '1':
+        local = 0
     if world > 1:
-        dist.init_process_group('nccl', init_method='env://')
+        dist.init_process_group(backend, init_method='env://')
     torch.cuda.set_device(local)
     torch.backends.cudnn.benchmark = bool(args.conv_autotune)
     _lib.load()
@@ -347,10 +360,13 @@ def main():
     # graph replays could not fire them); kernel durations do not depend on how they were issued
     n_prof = min(args.steps, 5)
     torch.cuda.synchronize()
+    from vfdepth_amd import kernels as KN
+    KN.syncbn_stats(reset=True)
     _lib.prof_enable('all')
     for _ in range(n_prof):
         losses = eager_step()
     torch.cuda.synchronize()
+    sbn = KN.syncbn_stats(reset=True)
     prof = _lib.prof_read()
     dense_bytes = {k: v * args.steps / n_prof for k, v in _lib.ALG_BYTES.items()}
     _lib.prof_enable('off')
@@ -440,6 +456,10 @@ def main():
         'hot_path_ms_per_step': sum(t for _, t in prof.values()) / args.steps,
         'dense_fused': {k: roofline_any(k) for k in dense},
         'execution': 'hip-graph replay of the whole step' if use_graph else 'eager',
+        'syncbn': ({'backend': dist.get_backend(), 'allreduce_per_step': sbn['calls'] / n_prof,
+                    'bytes_per_step': sbn['bytes'] / n_prof, 'host_ms_per_step': sbn['host_s'] * 1e3 / n_prof,
+                    'what': 'the fused BN kernels\' SyncBatchNorm exchange: one all-reduce of [C+1][2] fp64 per '
+                            'layer and direction (host time = enqueue for RCCL)'} if world > 1 else None),
         'parity': parity,
         'cpu_baseline': base,
     }

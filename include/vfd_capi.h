@@ -316,6 +316,10 @@ int vfd_elu_up_pad1_bwd_blocks(int h, int w);
  * (sum of g's copies) * (out > 0 ? 1 : slope); C % 4 == 0, 16-B aligned. */
 int vfd_lrelu_pad1_bwd_nhwc(const float* g, const float* out, float* gp, long long n_img, int h, int w, int C,
                             float slope, void* stream);
+/* the same with element types: dtype_in (g, out) / dtype_out (gp) 0 = fp32, 1 = bf16 (fp32 arithmetic,
+ * one rounding of the result) */
+int vfd_lrelu_pad1_bwd_nhwc_t(const void* g, const void* out, void* gp, long long n_img, int h, int w, int C,
+                              float slope, int dtype_in, int dtype_out, void* stream);
 
 /* ------------------------------------------------------------------ padded 3x3 conv (K2C) */
 typedef struct vfd_conv_desc {
@@ -350,11 +354,20 @@ int vfd_pad_conv_fwd_bf16(const vfd_conv_desc* d, const float* x, const void* Wf
  * to 256, zero-padded).  fp32 MFMA, stream-K with a fixed-order partial sum (deterministic).
  * d->pad_out == 2: the folded form — only the interior of dx is written, each border-adjacent pixel
  * holding the sum of its reflect copies (the plan for vfd_voxel_project_bwd_planned must be built
- * with the same pad_out); h >= 6, w >= 64.
+ * with the same pad_out): tiles of 256 interior pixels x 128 channels, any h, w >= 2 whose staged
+ * rows fit LDS (w <= 128; config 5's 80 x 120 included).
  * Workspace 0 = shape unsupported (Cv != 64, D > 64, or the staged rows of a tile exceed LDS). */
 size_t vfd_proj_conv_dgrad_workspace(const vfd_voxel_desc* d);
 int vfd_proj_conv_dgrad(const vfd_voxel_desc* d, const float* g_pre, const float* Wd, float* dx, void* workspace,
                         size_t ws_bytes, void* stream);
+
+/* bf16 form of the folded K3C data gradient (config 3; d->pad_out must be 2): g_pre bf16
+ * [B*N, h, w, O] NHWC, Wd = vfd_weight_fragments_bf16 mode 5 of the mode-2 copy, v_mfma_f32_32x32x16_bf16
+ * with fp32 accumulation, dx fp32 (the interior of [B*N, h+2, w+2, D*Cv], as vfd_proj_conv_dgrad).
+ * Workspace 0 = shape unsupported. */
+size_t vfd_proj_conv_dgrad_bf16_workspace(const vfd_voxel_desc* d);
+int vfd_proj_conv_dgrad_bf16(const vfd_voxel_desc* d, const void* g_pre, const void* Wd, float* dx, void* workspace,
+                             size_t ws_bytes, void* stream);
 
 /* K3C weight / bias gradient (volumetric_fusionnet.py:59-60, 265 backward; replaces the
  * reference's cudnn weight-gradient of reduce_dim[0]): dw [O = 256, Cv*D, 3, 3] in the reference

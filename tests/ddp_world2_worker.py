@@ -63,21 +63,40 @@ def bn_layer_checks(rank, world):
             yr = torch.relu(yr)
         (yr * g).sum().backward()
         # this rank's half on the GPU through a SyncBatchNorm module (fused synchronised path), NCHW
-        # and channels-last (bnact.hip's NHWC kernels, config 3's bf16 encoders)
-        for fmt in (torch.contiguous_format, torch.channels_last):
+        # and channels-last (bnact.hip's NHWC kernels), fp32 and — config 3's encoders — bf16
+        # channels-last maps (fp32 statistics and arithmetic, outputs / input gradients rounded once)
+        for fmt, dt in ((torch.contiguous_format, torch.float32), (torch.channels_last, torch.float32),
+                        (torch.channels_last, torch.bfloat16)):
+            bf = dt == torch.bfloat16
             half = slice(rank * shape[0] // world, (rank + 1) * shape[0] // world)
             bn = torch.nn.SyncBatchNorm(C).to(DEV).train()
             with torch.no_grad():
                 bn.weight.copy_(gamma.float())
                 bn.bias.copy_(beta.float())
                 bn.running_mean.copy_(rmean.float())
-            xh = x[half].float().to(DEV).contiguous(memory_format=fmt).requires_grad_(True)
-            rh = r[half].float().to(DEV).contiguous(memory_format=fmt).requires_grad_(True) if res else None
+            xh = x[half].to(dt).to(DEV).contiguous(memory_format=fmt).requires_grad_(True)
+            rh = r[half].to(dt).to(DEV).contiguous(memory_format=fmt).requires_grad_(True) if res else None
             y = bn_act(bn, xh, rh, relu)
             assert y.grad_fn is not None and 'BatchNormAct' in type(y.grad_fn).__name__, type(y.grad_fn).__name__
-            assert y.is_contiguous(memory_format=fmt)
-            (y * g[half].float().to(DEV)).sum().backward()
+            assert y.is_contiguous(memory_format=fmt) and y.dtype == dt
+            (y.float() * g[half].to(dt).float().to(DEV)).sum().backward()
             torch.cuda.synchronize()
+            if bf:
+                # the bf16 check runs against the same fp64 reference on the bf16-rounded inputs
+                # (statistics of the rounded maps), at bf16 output precision
+                xb = x.to(dt).double().requires_grad_(True)
+                rb = r.to(dt).double().requires_grad_(True) if res else None
+                refb = torch.nn.BatchNorm2d(C).double().train()
+                with torch.no_grad():
+                    refb.weight.copy_(gamma.float().double())
+                    refb.bias.copy_(beta.float().double())
+                    refb.running_mean.copy_(rmean.float().double())
+                yb = refb(xb)
+                if res:
+                    yb = yb + rb
+                if relu:
+                    yb = torch.relu(yb)
+                (yb * g.to(dt).double()).sum().backward()
 
             def err(a, b, what, tol):
                 nonlocal worst
@@ -85,6 +104,20 @@ def bn_layer_checks(rank, world):
                 e = float((a - b).abs().max()) / max(float(b.abs().max()), 1e-12)
                 worst = max(worst, e)
                 assert e <= tol, f'rank {rank} {shape} {fmt}: {what} rel err {e:.3g} > {tol}'
+            if bf:
+                e8 = 2.0 ** -7          # one bf16 rounding of the output / gradient (+ fp32 sums)
+                err(y, yb[half], 'bf16 output', e8)
+                err(bn.running_mean, refb.running_mean, 'bf16 running_mean', 1e-5)
+                err(bn.running_var, refb.running_var, 'bf16 running_var', 1e-5)
+                err(xh.grad, xb.grad[half], 'bf16 d input', 2 * e8)
+                if res:
+                    err(rh.grad, rb.grad[half], 'bf16 d residual', e8)
+                dg, db = bn.weight.grad.clone(), bn.bias.grad.clone()
+                dist.all_reduce(dg)
+                dist.all_reduce(db)
+                err(dg, refb.weight.grad, 'bf16 sum over ranks of d gamma', 1e-3)
+                err(db, refb.bias.grad, 'bf16 sum over ranks of d beta', 1e-3)
+                continue
             err(y, yr[half], 'output', 2e-6)
             err(bn.running_mean, ref.running_mean, 'running_mean', 1e-6)
             err(bn.running_var, ref.running_var, 'running_var', 1e-6)
@@ -121,19 +154,29 @@ def _bn_stats(models):
     return out
 
 
-def step_checks(rank, world):
+def step_checks(rank, world, bf16=False):
+    """bf16=True: config 3's precision — bf16 nets under autocast with channels-last encoders (the
+    NHWC bf16 SyncBatchNorm branch inside a DDP step), B = 2 per rank."""
     import common as G
     from torch.nn.parallel import DistributedDataParallel as DDP
+    from vfdepth_amd import kernels as KN
     from vfdepth_amd import synth
     from vfdepth_amd.layers import seeded_state_dict
     from vfdepth_amd.vfdepth import VFDepthAlgo
-    cfg = G.step_cfg()
-    inputs = synth.make_batch(cfg, seed=50 + rank, device=DEV)        # each rank its own sample
-    noise = 1e-5 * torch.randn(6, 1, 2, cfg['training']['height'], cfg['training']['width'],
+
+    def make_cfg():
+        c = G.step_cfg()
+        if bf16:
+            c['training'].update(net_precision='bf16', batch_size=2)
+        return c
+    cfg = make_cfg()
+    B = cfg['training']['batch_size']
+    inputs = synth.make_batch(cfg, seed=50 + rank, device=DEV)        # each rank its own samples
+    noise = 1e-5 * torch.randn(6, B, 2, cfg['training']['height'], cfg['training']['width'],
                                generator=torch.Generator().manual_seed(60 + rank)).to(DEV)
 
     def run(ddp):
-        c = G.step_cfg()
+        c = make_cfg()
         c['ddp'].update({'ddp_enable': ddp, 'world_size': world, 'gpus': list(range(world))})
         algo = VFDepthAlgo(c, DEV)
         for m in algo.models.values():
@@ -148,8 +191,14 @@ def step_checks(rank, world):
         torch.cuda.synchronize()
         return algo, losses
     run(False)                  # warm-up: MIOpen's solver picks on first use
+    KN.syncbn_stats(reset=True)
     algo_d, loss_d = run(True)
+    sbn = KN.syncbn_stats(reset=True)
+    assert sbn['calls'] > 0, 'the DDP step issued no SyncBatchNorm collective'
     assert all(isinstance(m, DDP) for m in algo_d.models.values())
+    if bf16:                    # the encoders really run channels-last bf16 (the NHWC SyncBN kernels)
+        encs = [m.module.encoder for m in algo_d.models.values() if hasattr(m.module, 'encoder')]
+        assert encs and all(e.channels_last for e in encs)
     for m in algo_d.models.values():
         assert any(isinstance(x, torch.nn.SyncBatchNorm) for x in m.module.modules())
         assert not any(type(x) is torch.nn.BatchNorm2d for x in m.module.modules())
@@ -178,7 +227,7 @@ def step_checks(rank, world):
         assert torch.equal(peers[0], peers[1]), f'{k} differs between ranks'
         e = float((s_ddp[k] - s_loc[k]).abs().max())
         assert e <= 1e-5 * max(float(s_loc[k].abs().max()), 1.0), f'{k}: DDP vs local-step statistics {e:.3g}'
-    return rel, len(keys)
+    return rel, len(keys), sbn
 
 
 def main():
@@ -189,11 +238,14 @@ def main():
     from vfdepth_amd import _lib
     _lib.load()
     worst = bn_layer_checks(rank, world)
-    rel, n = step_checks(rank, world)
+    rel, n, sbn = step_checks(rank, world)
+    rel3, n3, sbn3 = step_checks(rank, world, bf16=True)
     dist.barrier()
     dist.destroy_process_group()
-    print(f'OK rank {rank}: syncbn worst rel err {worst:.3g}; DDP step {n} gradients, rel vs mean of local {rel:.3g}',
-          flush=True)
+    print(f'OK rank {rank}: syncbn worst rel err {worst:.3g}; DDP step {n} gradients, rel vs mean of local {rel:.3g} '
+          f'({sbn["calls"]} SyncBN all-reduces, {sbn["bytes"] / 1e3:.1f} KB, {sbn["host_s"] * 1e3:.1f} ms host); '
+          f'bf16 channels-last B=2 DDP step {n3} gradients, rel {rel3:.3g} ({sbn3["calls"]} all-reduces, '
+          f'{sbn3["host_s"] * 1e3:.1f} ms host)', flush=True)
 
 
 if __name__ == '__main__':

@@ -606,7 +606,18 @@ def test_proj_conv_matches_k3_plus_conv(config, B):
     # the frustum features the kernel writes for the backward (K3's padded layout, halo included)
     close(y.grad_fn.saved_tensors[2], x.detach(), f'K3C frustum-feature side output (config {config})')
     g = torch.randn(y.shape, device=DEV, generator=gen)
-    (y * g).sum().backward()
+    from vfdepth_amd import _lib as L
+    torch.cuda.synchronize()
+    L.prof_enable('all')
+    try:
+        (y * g).sum().backward()
+        torch.cuda.synchronize()
+        ran = L.prof_read()
+    finally:
+        L.prof_enable('off')
+    # the hand-written data / weight gradients ran (no MIOpen fallback at this shape)
+    assert ran.get('proj_conv_dgrad', (0, 0))[0] == 1, f'K3C data gradient not on the HIP path: {sorted(ran)}'
+    assert ran.get('proj_conv_wgrad', (0, 0))[0] == 1, f'K3C weight gradient not on the HIP path: {sorted(ran)}'
     (y_ref * g).sum().backward()
     for name, a, r in zip(('d voxels', 'd weight', 'd bias'), leaves, refs):
         gclose(a.grad, r.grad, f'K3C {name} (config {config})')
@@ -671,7 +682,8 @@ def test_proj_conv_bf16(config):
 @pytest.mark.parametrize('shape', [(1, 5140, 102, 102, 2),     # config 2 pose: (C+1)*Z, padded 100x100 BEV
                                    (2, 20, 13, 11, 2),         # odd sizes, partial channel chunk
                                    (1, 44, 9, 30, 1),          # stride 1
-                                   (2, 1028, 22, 22, 2)])      # small-config pose shape, B=2
+                                   (2, 1028, 22, 22, 2),       # small-config pose shape, B=2
+                                   (4, 5140, 202, 202, 2)])    # config 5 pose: B=4, 200x200 BEV
 def test_pad_conv_matches_conv(shape):
     """K2C (the pose reduce_dim's first conv, volumetric_fusionnet.py:59-60, 338-343) against
     F.conv2d on the same reflect-padded map + bias + LeakyReLU + the reflect pad of the next conv:
@@ -701,7 +713,8 @@ def test_pad_conv_matches_conv(shape):
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize('shape', [(2, 5140, 102, 102, 2, (257, 20)),   # config 3 pose: B=2, reference-order weight
                                    (2, 20, 13, 11, 2, None),           # odd sizes, partial channel chunk
-                                   (1, 44, 9, 30, 1, None)])           # stride 1
+                                   (1, 44, 9, 30, 1, None),            # stride 1
+                                   (2, 5140, 202, 202, 2, (257, 20))])  # config 5's pose shape in bf16, B=2
 def test_pad_conv_bf16(shape):
     """K2C's bf16 form (config 3) against F.conv2d in fp32 on the bf16-rounded map and weight (+ bias,
     LeakyReLU, the next conv's reflect pad): equal up to fp32 summation order and the final bf16
@@ -1323,3 +1336,84 @@ def test_proj_conv_dgrad_folded_matches_padded(config):
     ref[:, :, :, w - 1] += ref[:, :, :, w + 1]
     inner = (slice(None), slice(None), slice(1, h + 1), slice(1, w + 1))
     close(out[2][inner], ref[inner], f'folded K3C data gradient (config {config})', atol=1e-5, rtol=1e-4)
+
+
+def _folded_dgrad_ref(g_pre, wn, h, w):
+    """d of a 3x3 conv (no padding) w.r.t. its reflect-padded input, folded onto the interior:
+    conv_transpose2d gives d Xp [n, K, h+2, w+2]; then rows 0 / h+1 add into 2 / h-1 and columns
+    0 / w+1 into 2 / w-1 (pad_sets' pairing), in that order (a corner folds twice)."""
+    ref = F.conv_transpose2d(g_pre, wn)
+    ref[:, :, 2, :] += ref[:, :, 0, :]
+    ref[:, :, h - 1, :] += ref[:, :, h + 1, :]
+    ref[:, :, :, 2] += ref[:, :, :, 0]
+    ref[:, :, :, w - 1] += ref[:, :, :, w + 1]
+    return ref[:, :, 1:h + 1, 1:w + 1]
+
+
+# (config, B, h, w, D): the step shapes (configs 2 / 3 (B=2) / 4 / 5) and small / odd ones where
+# one tile holds both fold rows (h <= 5), w < 64 (tiles spanning many rows), h or w = 2 / 3
+_DGRAD_SHAPES = [('c2', 1, 48, 80, 50), ('c3', 2, 48, 80, 50), ('c4', 1, 44, 80, 50), ('c5', 4, 80, 120, 50),
+                 ('small', 1, 12, 20, 16), ('odd', 1, 5, 7, 3), ('thin', 1, 2, 3, 2), ('flat', 1, 3, 2, 5),
+                 ('wide', 1, 6, 128, 4)]
+
+
+def _dgrad_case(B, h, w, D, seed):
+    from vfdepth_amd import kernels as KN
+    space = KN.VoxelSpace(G.step_cfg(), DEV)
+    N, Cv, O = 6, 64, 256
+    d = space.desc(B, N, Cv=Cv, pad_out=2)
+    d.h, d.w, d.D = h, w, D
+    gen = torch.Generator(device=DEV).manual_seed(seed)
+    g_pre = torch.randn(B * N, O, h, w, device=DEV, generator=gen).contiguous(memory_format=torch.channels_last)
+    w0 = torch.randn(O, Cv * D, 3, 3, device=DEV, generator=gen) * (O * 9) ** -0.5
+    return KN, d, g_pre, w0, KN.proj_conv_weight(w0, Cv, D)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize('name,B,h,w,D', _DGRAD_SHAPES)
+def test_proj_conv_dgrad_matches_conv_transpose(name, B, h, w, D):
+    """The folded K3C data gradient (projconv.hip pcg_main_k, fp32 MFMA; volumetric_fusionnet.py:
+    59-60, 261-265 backward) through the C ABI against MIOpen's conv_transpose2d of the same operands
+    + the reflect-pad adjoint, at the step shapes (config 5's 80x120 at B=4 included: the form that
+    fits LDS there) and at small / odd shapes that exercise both fold rows in one tile."""
+    import ctypes
+    from vfdepth_amd import _lib as L
+    KN, d, g_pre, w0, wn = _dgrad_case(B, h, w, D, 501)
+    lib = L.load()
+    nbytes = lib.vfd_proj_conv_dgrad_workspace(ctypes.byref(d))
+    assert nbytes, f'{name}: folded data gradient unsupported'
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=DEV)
+    dx = torch.zeros(B * 6, 64 * D, h + 2, w + 2, device=DEV).contiguous(memory_format=torch.channels_last)
+    wd = KN.proj_conv_dgrad_weight(w0, 64, D)
+    L.check(lib.vfd_proj_conv_dgrad(ctypes.byref(d), g_pre.data_ptr(), wd.data_ptr(), dx.data_ptr(), ws.data_ptr(),
+                                    nbytes, L.stream()), 'proj_conv_dgrad')
+    ref = _folded_dgrad_ref(g_pre.contiguous(), wn, h, w)
+    close(dx[:, :, 1:h + 1, 1:w + 1], ref, f'folded K3C data gradient ({name})', atol=1e-5, rtol=1e-4)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize('name,B,h,w,D', _DGRAD_SHAPES)
+def test_proj_conv_dgrad_bf16_matches_conv_transpose(name, B, h, w, D):
+    """The bf16 folded K3C data gradient (pcg_main_k<bf16>: bf16 G and weight fragments,
+    v_mfma_f32_32x32x16_bf16, fp32 accumulation and output) against the fp32 conv_transpose2d of the
+    bf16-rounded operands + the reflect-pad adjoint.  The kernel rounds the fold sums (G[2] + G[0], ...)
+    once more to bf16 and sums in another order: |err| <= 2^-8 * (the same transpose of |G| and |W|)
+    + 1e-5 * max|ref|."""
+    import ctypes
+    from vfdepth_amd import _lib as L
+    KN, d, g_pre, w0, wn = _dgrad_case(B, h, w, D, 502)
+    lib = L.load()
+    nbytes = lib.vfd_proj_conv_dgrad_bf16_workspace(ctypes.byref(d))
+    assert nbytes, f'{name}: bf16 folded data gradient unsupported'
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=DEV)
+    dx = torch.zeros(B * 6, 64 * D, h + 2, w + 2, device=DEV).contiguous(memory_format=torch.channels_last)
+    gb = g_pre.to(torch.bfloat16)
+    wd = KN.proj_conv_dgrad_weight_bf16(w0, 64, D)
+    L.check(lib.vfd_proj_conv_dgrad_bf16(ctypes.byref(d), gb.data_ptr(), wd.data_ptr(), dx.data_ptr(), ws.data_ptr(),
+                                         nbytes, L.stream()), 'proj_conv_dgrad_bf16')
+    gr, wr = gb.float().contiguous(), wn.to(torch.bfloat16).float()
+    ref = _folded_dgrad_ref(gr, wr, h, w)
+    mag = _folded_dgrad_ref(gr.abs(), wr.abs(), h, w)
+    err = (dx[:, :, 1:h + 1, 1:w + 1] - ref).abs()
+    bound = 2.0 ** -8 * mag + 1e-5 * float(ref.abs().max())
+    assert bool((err <= bound).all()), f'bf16 folded K3C data gradient ({name}): max err/mag {float((err / (mag + 1e-12)).max()):.3g}'

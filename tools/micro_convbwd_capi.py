@@ -1,0 +1,76 @@
+"""Time the hand-written reduce_dim gradient kernels through the C ABI (HIP events on the launching
+stream, the bench's own scopes), fp32 and bf16, at the step shapes.
+
+    python tools/micro_convbwd_capi.py [--iters 10] [--ops dgrad,dgrad_bf16] [--shapes c2,c3,c5]
+Run a variant build with VFD_LIB=/path/libvfd_X.so (tools/build_variant.py)."""
+import argparse
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+SHAPES = {'c2': (1, 48, 80, 50), 'c3': (2, 48, 80, 50), 'c4': (1, 44, 80, 50), 'c5': (4, 80, 120, 50)}
+PEAK = {'fp32': 157.3, 'bf16': 2516.6}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--iters', type=int, default=10)
+    ap.add_argument('--ops', default='dgrad,dgrad_bf16')
+    ap.add_argument('--shapes', default='c2,c3,c5')
+    a = ap.parse_args()
+    from vfdepth_amd import _lib as L
+    from vfdepth_amd import kernels as KN
+    sys.path.insert(0, os.path.join(ROOT, 'tests', 'golden'))
+    import common as G
+    lib = L.load()
+    dev = torch.device('cuda:0')
+    space = KN.VoxelSpace(G.step_cfg(), dev)
+    for sh in a.shapes.split(','):
+        B, h, w, D = SHAPES[sh]
+        N, Cv, O = 6, 64, 256
+        d = space.desc(B, N, Cv=Cv, pad_out=2)
+        d.h, d.w, d.D = h, w, D
+        g_pre = torch.randn(B * N, O, h, w, device=dev).contiguous(memory_format=torch.channels_last)
+        w0 = torch.randn(O, Cv * D, 3, 3, device=dev) * (O * 9) ** -0.5
+        dx = torch.empty(B * N, Cv * D, h + 2, w + 2, device=dev).contiguous(memory_format=torch.channels_last)
+        flop = 2.0 * B * N * h * w * O * Cv * D * 9
+        for op in a.ops.split(','):
+            if op == 'dgrad':
+                wd, gp, kind = KN.proj_conv_dgrad_weight(w0, Cv, D), g_pre, 'fp32'
+                nb = lib.vfd_proj_conv_dgrad_workspace(ctypes.byref(d))
+                fn = lib.vfd_proj_conv_dgrad
+            elif op == 'dgrad_bf16':
+                wd, gp, kind = KN.proj_conv_dgrad_weight_bf16(w0, Cv, D), g_pre.to(torch.bfloat16), 'bf16'
+                nb = lib.vfd_proj_conv_dgrad_bf16_workspace(ctypes.byref(d))
+                fn = lib.vfd_proj_conv_dgrad_bf16
+            else:
+                raise SystemExit(f'unknown op {op}')
+            if not nb:
+                print(f'{sh} {op}: unsupported', flush=True)
+                continue
+            ws = torch.empty(nb, dtype=torch.uint8, device=dev)
+
+            def call():
+                L.check(fn(ctypes.byref(d), gp.data_ptr(), wd.data_ptr(), dx.data_ptr(), ws.data_ptr(), nb,
+                           L.stream()), op)
+            for _ in range(2):
+                call()
+            torch.cuda.synchronize()
+            L.prof_enable('proj_conv_dgrad')
+            for _ in range(a.iters):
+                call()
+            torch.cuda.synchronize()
+            n, ms = L.prof_read()['proj_conv_dgrad']
+            L.prof_enable('off')
+            us = ms / n * 1e3
+            tf = flop / (us * 1e-6) / 1e12
+            print(f'{sh} {op:11s} {us:9.1f} us  {tf:7.1f} TF/s  {tf / PEAK[kind]:.3f} of {kind} peak', flush=True)
+
+
+if __name__ == '__main__':
+    main()

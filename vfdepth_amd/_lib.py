@@ -86,6 +86,8 @@ _SIGS = {
     'vfd_proj_conv_fwd_bf16': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 5 + [c_int, c_fp, c_fp, c_fp, c_size_t, c_void_p]),
     'vfd_proj_conv_dgrad_workspace': (c_size_t, [ctypes.POINTER(VoxelDesc)]),
     'vfd_proj_conv_dgrad': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 4 + [c_size_t, c_void_p]),
+    'vfd_proj_conv_dgrad_bf16_workspace': (c_size_t, [ctypes.POINTER(VoxelDesc)]),
+    'vfd_proj_conv_dgrad_bf16': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 4 + [c_size_t, c_void_p]),
     'vfd_proj_conv_wgrad_workspace': (c_size_t, [ctypes.POINTER(VoxelDesc)]),
     'vfd_proj_conv_wgrad': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 5 + [c_size_t, c_void_p]),
     'vfd_bn_splits': (c_int, [ctypes.POINTER(BnDesc)]),
@@ -124,6 +126,8 @@ _SIGS = {
     'vfd_elu_up_pad1_bwd': (c_int, [c_fp, c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_int, c_fp, c_int, c_void_p]),
     'vfd_elu_up_pad1_bwd_blocks': (c_int, [c_int, c_int]),
     'vfd_lrelu_pad1_bwd_nhwc': (c_int, [c_fp, c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_int, c_float, c_void_p]),
+    'vfd_lrelu_pad1_bwd_nhwc_t': (c_int, [c_fp, c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_int, c_float, c_int, c_int,
+                                          c_void_p]),
     'vfd_pad_conv_fwd_workspace': (c_size_t, [ctypes.POINTER(ConvDesc)]),
     'vfd_pad_conv_fwd': (c_int, [ctypes.POINTER(ConvDesc)] + [c_fp] * 5 + [c_size_t, c_void_p]),
     'vfd_pad_conv_fwd_bf16_workspace': (c_size_t, [ctypes.POINTER(ConvDesc)]),

@@ -20,6 +20,8 @@
 // sums go to a per-(workgroup, slot) buffer in MFMA fragment order; `pcv_reduce_k` sums each tile's
 // partials in workgroup order (deterministic), adds the bias, applies the LeakyReLU and writes the
 // reflect-padded NHWC input of reduce_dim's second conv.
+#include <type_traits>
+
 #include "vfd_common.h"
 
 namespace vfd {
@@ -1083,6 +1085,664 @@ static bool pd_supported(const vfd_voxel_desc& d) {
 }
 
 // =============================================================================================
+// K3C data gradient, round 4 ("pcg"): the folded form (reflect-pad adjoint inside the GEMM, interior
+// only, as pcdf) on tiles of 256 interior pixels x 128 frustum channels, fp32 and bf16.
+//
+// Each of the 4 compute waves owns 8 pixel blocks (256 pixels) x ONE 32-channel block of n, so a
+// weight fragment feeds 8 pixel blocks (pcdf: 4) — half the weight bytes streamed from L2 per MFMA
+// — and N = D*Cv = 3200 splits into 25 tiles of 128 with no zero padding (pcdf: 13 x 256, 4 %
+// zero work).  Tiles are 256 consecutive interior pixels of one camera (config 2: 15 per camera,
+// exact), whose staged G rows (the whole rows under the tile, columns -1 .. w, then the E1 / E2
+// column folds) and both fold rows (F1 = G[2] + G[0] for pixel row 1 at ky' = 2, F2 = G[h-3] +
+// G[h-1] for row h-2 at ky' = 0; staged only when the tile holds that row) fit LDS double-buffered
+// for w <= 128 (config 5: w = 120, 158.7 KB), because an atom carries only OC output channels:
+// fp32 16 (9 taps x 4 channel quads of v_mfma_f32_32x32x2_f32, 16 MFMAs per step), bf16 32 (9 taps
+// x 2 sixteen-channel steps of v_mfma_f32_32x32x16_bf16, 8 MFMAs per step).  Same loader / compute
+// wave split, stream-K ranges (>= OC atoms: a split tile meets two groups) and XCD-contiguous
+// group numbering as pcdf; split tiles summed in group order by pcg_reduce_k (deterministic).
+// bf16 (config 3): G staged as bf16 (the adjoint's bf16 output, or fp32 rounded), the fold sums in
+// fp32 rounded once; weights = vfd_weight_fragments_bf16 mode 5; dx fp32 (K3's backward input).
+#ifndef VFD_PG_BF_PF
+#define VFD_PG_BF_PF 6      // bf16 B-fragment prefetch distance (steps; divides 18)
+#endif
+template <typename T>
+struct PgCfg;
+template <>
+struct PgCfg<float> {
+  static constexpr int OC = 16, XS = 20, STEPS = 4, PF = 4;   // o per atom, LDS elems / position, k-steps per tap
+};
+template <>
+struct PgCfg<__bf16> {
+  static constexpr int OC = 32, XS = 40, STEPS = 2, PF = VFD_PG_BF_PF;
+};
+
+constexpr int PG_PIX = 256;                     // interior pixels per tile (8 blocks of 32)
+constexpr int PG_N = 128;                       // frustum channels per tile (4 waves x 32)
+constexpr int PG_FRAG = PG_PIX * PG_N;          // floats of one tile's partial
+
+struct PgGeom {
+  int nbc, h, w, ntot, np, tpc, mtiles, ntn, ntile, och, natom, ngroup, hrows, cols, lds_elems;
+};
+
+__host__ __device__ inline int pg_lo(const PgGeom& g, int grp) {
+  return (int)(((long long)grp * g.natom) / g.ngroup);
+}
+
+struct PgTile {
+  int nt, bc, m0, y0;
+};
+
+// tile order: n-tile outermost (a group's consecutive tiles share the n-tile's weights)
+__device__ __forceinline__ PgTile pg_tile(const PgGeom& g, int t) {
+  PgTile r;
+  const int mt = t % g.mtiles;
+  r.nt = t / g.mtiles;
+  r.bc = mt / g.tpc;
+  r.m0 = (mt - r.bc * g.tpc) * PG_PIX;
+  r.y0 = r.m0 / g.w;
+  return r;
+}
+
+// 16-byte vectors of G: fp32 4 channels, bf16 8 channels; loads widen to fp32, the staging store
+// rounds once to the LDS type
+template <typename TG>
+struct PgVec;
+template <>
+struct PgVec<float> {
+  static constexpr int CH = 4;
+  struct V { float x[4]; };
+  static __device__ __forceinline__ V zero() { return V{{0.f, 0.f, 0.f, 0.f}}; }
+  static __device__ __forceinline__ V load(const float* p) {
+    const float4 f = *reinterpret_cast<const float4*>(p);
+    return V{{f.x, f.y, f.z, f.w}};
+  }
+};
+template <>
+struct PgVec<__bf16> {
+  static constexpr int CH = 8;
+  struct V { float x[8]; };
+  static __device__ __forceinline__ V zero() { return V{{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}}; }
+  static __device__ __forceinline__ V load(const __bf16* p) {
+    const bf16x8 b = *reinterpret_cast<const bf16x8*>(p);
+    V v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v.x[j] = (float)b[j];
+    return v;
+  }
+};
+
+template <typename T, typename V, int CH>
+__device__ __forceinline__ void pg_put(T* dst, const V& v) {
+  if constexpr (sizeof(T) == 4) {
+#pragma unroll
+    for (int j = 0; j < CH; j += 4)
+      *reinterpret_cast<float4*>(dst + j) = make_float4(v.x[j], v.x[j + 1], v.x[j + 2], v.x[j + 3]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < CH; j += 8) {
+      bf16x8 b;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) b[k] = (__bf16)v.x[j + k];
+      *reinterpret_cast<bf16x8*>(dst + j) = b;
+    }
+  }
+}
+
+// loader waves (tid 0..255): staged rows 0 .. hrows-1 = G rows y0 - 1 .. (zero outside the camera),
+// row hrows = F1 = G[2] + G[0], row hrows + 1 = F2 = G[h-3] + G[h-1] (each only when the tile holds
+// pixel row 1 / h - 2); staged columns 0 .. w + 1 = G columns -1 .. w, w + 2 = E1 = G[.][2] + G[.][0],
+// w + 3 = E2 = G[.][w-3] + G[.][w-1]; channels ch * OC .. + OC - 1.  A thread owns one (column,
+// channel vector) and walks the rows: each staged element is the sum of <= 2 x 2 G vectors
+// (rows ya / yb, columns xa / xb; -1 = absent), four rows' loads in flight.
+template <typename T, typename TG>
+__device__ __forceinline__ void pg_stage(const PgGeom& g, T* __restrict__ dst, const TG* __restrict__ gp, int atom,
+                                         int tid) {
+  typedef PgVec<TG> PV;
+  constexpr int OC = PgCfg<T>::OC, XS = PgCfg<T>::XS, CH = PV::CH, QP = OC / CH, CPP = 256 / QP;
+  const int t = atom / g.och, ch = atom - t * g.och;
+  const PgTile tl = pg_tile(g, t);
+  const int hw = g.h * g.w;
+  const int ylast = ((tl.m0 + PG_PIX < hw ? tl.m0 + PG_PIX : hw) - 1) / g.w;
+  const bool f1 = tl.y0 <= 1 && ylast >= 1, f2 = tl.y0 <= g.h - 2 && ylast >= g.h - 2;
+  const int nrow = g.hrows + 2;
+  const int q = tid % QP;
+  const TG* src = gp + (size_t)tl.bc * hw * PC_O + ch * OC + CH * q;
+#ifdef VFD_PG_NOSTAGE
+  return;                                             // timing experiment only: LDS left as is
+#endif
+  for (int c = tid / QP; c < g.cols; c += CPP) {
+    int xa, xb = -1;
+    if (c < g.w + 2) {
+      xa = c - 1 < g.w ? c - 1 : -1;                 // -1 for c = 0 too
+    } else if (c == g.w + 2) {
+      xa = 2 < g.w ? 2 : -1;
+      xb = 0;
+    } else {
+      xa = g.w - 3;
+      xb = g.w - 1;
+    }
+    T* dcol = dst + c * XS + CH * q;
+    for (int r0 = 0; r0 < nrow; r0 += 4) {
+      typename PV::V v[4][4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int r = r0 + u;
+        int ya = -1, yb = -1;
+        if (r < g.hrows) {
+          const int y = tl.y0 - 1 + r;
+          ya = y >= 0 && y < g.h ? y : -1;
+        } else if (r == g.hrows && f1) {
+          ya = 2 < g.h ? 2 : -1;
+          yb = 0;
+        } else if (r == g.hrows + 1 && f2) {
+          ya = g.h - 3;
+          yb = g.h - 1;
+        }
+        const int ys[2] = {ya, yb}, xs[2] = {xa, xb};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int yy = ys[k >> 1], xx = xs[k & 1];
+          v[u][k] = (r < nrow && yy >= 0 && xx >= 0) ? PV::load(src + ((size_t)yy * g.w + xx) * PC_O) : PV::zero();
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (r0 + u < nrow) {
+          typename PV::V s = v[u][0];
+#pragma unroll
+          for (int j = 0; j < CH; ++j) s.x[j] = (s.x[j] + v[u][1].x[j]) + (v[u][2].x[j] + v[u][3].x[j]);
+          pg_put<T, typename PV::V, CH>(dcol + (r0 + u) * g.cols * XS, s);
+        }
+      }
+    }
+  }
+}
+
+// fp32 weights: vfd_weight_fragments mode 2, float2 (s = 0, 1) at ((tap' * O/4 + oq) * np + n) * 2 + h;
+// bf16: mode 5, bf16x8 at ((tap' * O/16 + q16) * np/32 + nb) * 64 + lane (o = 16 q16 + 8 h + j)
+template <typename T, typename TG>
+__global__ __launch_bounds__(PC_THREADS, 2) void pcg_main_k(PgGeom g, const TG* __restrict__ gp,
+                                                           const void* __restrict__ Wd, float* __restrict__ dx,
+                                                           float* __restrict__ partial) {
+  constexpr int OC = PgCfg<T>::OC, XS = PgCfg<T>::XS, STEPS = PgCfg<T>::STEPS, PF = PgCfg<T>::PF;
+  constexpr int ITERS = 9 * STEPS;
+  constexpr bool BF = sizeof(T) == 2;
+  typedef typename std::conditional<BF, bf16x8, float2>::type BFrag;
+  typedef typename std::conditional<BF, bf16x8, float2>::type AFrag;
+  extern __shared__ __attribute__((aligned(16))) unsigned char pg_raw[];
+  T* lds = reinterpret_cast<T*>(pg_raw);
+  const int grp = (g.ngroup % 8 == 0) ? (blockIdx.x % 8) * (g.ngroup / 8) + blockIdx.x / 8 : blockIdx.x;
+  const int a_lo = pg_lo(g, grp), a_hi = pg_lo(g, grp + 1);
+  if (a_lo >= a_hi) return;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const bool compute = wv < PC_WAVES;
+  if (!compute) pg_stage<T, TG>(g, lds, gp, a_lo, threadIdx.x - 64 * PC_WAVES);
+  __syncthreads();
+  if (!compute) {
+    for (int atom = a_lo; atom < a_hi; ++atom) {
+      if (atom + 1 < a_hi)
+        pg_stage<T, TG>(g, lds + ((atom + 1 - a_lo) & 1) * g.lds_elems, gp, atom + 1, threadIdx.x - 64 * PC_WAVES);
+      __syncthreads();
+    }
+    return;
+  }
+  const int li = lane & 31, lh = lane >> 5;
+  const int hw = g.h * g.w;
+  f32x16 acc[8];
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[a][r] = 0.f;
+  // B fragments: the lane's stream of atom a starts at bbase(a); iteration j = tap * STEPS + q adds
+  // tap * tstride + q * qstride; prefetched PF iterations ahead (ITERS % PF == 0: static ring slots)
+  static_assert(ITERS % PF == 0, "prefetch ring");
+  const BFrag* wf = reinterpret_cast<const BFrag*>(Wd);
+  const size_t qstride = BF ? (size_t)(g.np / 32) * 64 : (size_t)g.np * 2;
+  const size_t tstride = (size_t)(BF ? PC_O / 16 : PC_O / 4) * qstride;
+  auto bbase = [&](int atom) -> const BFrag* {
+    const int t = atom / g.och, ch = atom - t * g.och;
+    const int nt = t / g.mtiles;
+    if constexpr (BF)
+      return wf + (size_t)ch * STEPS * qstride + (size_t)(nt * (PG_N / 32) + wv) * 64 + lane;
+    else
+      return wf + (size_t)ch * STEPS * qstride + (size_t)(nt * PG_N + wv * 32 + li) * 2 + lh;
+  };
+  BFrag bq[PF];
+  const BFrag* bcur = bbase(a_lo);
+#pragma unroll
+  for (int j = 0; j < PF; ++j) bq[j] = bcur[(j / STEPS) * tstride + (j % STEPS) * qstride];
+  constexpr int LH = BF ? 8 : 2;                      // the lane half's element offset within a step
+  for (int atom = a_lo; atom < a_hi; ++atom) {
+    const int t = atom / g.och, ch = atom - t * g.och;
+    const PgTile tl = pg_tile(g, t);
+    const bool more = atom + 1 < a_hi;
+    const BFrag* bnext = more ? bbase(atom + 1) : bcur;
+    int pyx[8];                                       // (row << 16) | column of the lane's pixels
+#pragma unroll
+    for (int a = 0; a < 8; ++a) {
+      int m = tl.m0 + 32 * a + li;
+      m = m < hw ? m : hw - 1;                        // pixels past the camera: computed, never stored
+      const int y = m / g.w;
+      pyx[a] = (y << 16) | (m - y * g.w);
+    }
+    const T* xb = lds + ((atom - a_lo) & 1) * g.lds_elems;
+    auto offsets = [&](int tap, int* o1) {
+      const int ky = tap / 3, kx = tap - 3 * ky;
+#pragma unroll
+      for (int a = 0; a < 8; ++a) {
+        const int px = pyx[a] & 0xFFFF, py = pyx[a] >> 16;
+        const int col = (px == 1 && kx == 2) ? g.w + 2 : (px == g.w - 2 && kx == 0) ? g.w + 3 : px + kx;
+        const int row = (py == 1 && ky == 2) ? g.hrows : (py == g.h - 2 && ky == 0) ? g.hrows + 1 : py - tl.y0 + ky;
+        o1[a] = (row * g.cols + col) * XS + LH * lh;
+      }
+    };
+    int o1c[8];
+    offsets(0, o1c);
+    AFrag afc[8], afn[8];
+#pragma unroll
+    for (int a = 0; a < 8; ++a) afc[a] = *reinterpret_cast<const AFrag*>(&xb[o1c[a]]);
+#pragma unroll
+    for (int j = 0; j < ITERS; ++j) {
+      const int tap = j / STEPS, q = j % STEPS;
+      const BFrag b = bq[j % PF];
+      {                                               // refill the slot with iteration j + PF
+        const int jn = j + PF;
+#ifdef VFD_PG_NOB
+        if (jn < 0)                                   // timing experiment only: B loaded once
+#else
+        if (jn < ITERS)
+#endif
+          bq[j % PF] = bcur[(jn / STEPS) * tstride + (jn % STEPS) * qstride];
+#ifndef VFD_PG_NOB
+        else if (more)
+          bq[j % PF] = bnext[((jn - ITERS) / STEPS) * tstride + ((jn - ITERS) % STEPS) * qstride];
+#endif
+      }
+      if (q < STEPS - 1) {
+#pragma unroll
+        for (int a = 0; a < 8; ++a) afn[a] = *reinterpret_cast<const AFrag*>(&xb[o1c[a] + (OC / STEPS) * (q + 1)]);
+      } else if (tap < 8) {                           // the current tap's loads are all issued
+        offsets(tap + 1, o1c);
+#pragma unroll
+        for (int a = 0; a < 8; ++a) afn[a] = *reinterpret_cast<const AFrag*>(&xb[o1c[a]]);
+      }
+      if constexpr (BF) {
+#pragma unroll
+        for (int a = 0; a < 8; ++a) acc[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afc[a], b, acc[a], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int a = 0; a < 8; ++a)
+            acc[a] = __builtin_amdgcn_mfma_f32_32x32x2f32(s2 ? afc[a].y : afc[a].x, s2 ? b.y : b.x, acc[a], 0, 0, 0);
+      }
+#pragma unroll
+      for (int a = 0; a < 8; ++a) afc[a] = afn[a];
+    }
+    bcur = bnext;
+    __syncthreads();                                  // buffer handed back to the loader waves
+    if (ch == g.och - 1 || atom == a_hi - 1) {
+      const int ts = t * g.och;
+      const int n = tl.nt * PG_N + wv * 32 + li;
+      if (ts >= a_lo && ts + g.och <= a_hi) {         // whole tile in this range: store
+#pragma unroll
+        for (int a = 0; a < 8; ++a)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = tl.m0 + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            if (m < hw && n < g.ntot) {
+              const int y = m / g.w, x = m - y * g.w;
+              dx[(((size_t)tl.bc * (g.h + 2) + y + 1) * (g.w + 2) + x + 1) * g.ntot + n] = acc[a][r];
+            }
+            acc[a][r] = 0.f;
+          }
+      } else {                                        // split tile: partial slot
+        const int slot = t == a_lo / g.och ? 0 : 1;
+        float* dst = partial + ((size_t)grp * 2 + slot) * PG_FRAG + (size_t)wv * (PG_FRAG / PC_WAVES) + lane;
+#pragma unroll
+        for (int a = 0; a < 8; ++a)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            dst[(a * 16 + r) * 64] = acc[a][r];
+            acc[a][r] = 0.f;
+          }
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void pcg_reduce_k(PgGeom g, const float* __restrict__ partial,
+                                                    float* __restrict__ dx) {
+  const int grp = blockIdx.x;
+  const int lo = pg_lo(g, grp);
+  if (grp == 0 || lo % g.och == 0) return;           // boundary on a tile edge: nothing split
+  const int t = lo / g.och;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c0 = (grp - 1) * 2 + (t == pg_lo(g, grp - 1) / g.och ? 0 : 1), c1 = grp * 2;
+  const PgTile tl = pg_tile(g, t);
+  const int hw = g.h * g.w;
+  constexpr int FPS = 8 * 16 / PC_FSL;
+  constexpr int U = 4;
+  const int contrib[2] = {c0, c1};
+  const int n = tl.nt * PG_N + wv * 32 + (lane & 31);
+  for (int fu = blockIdx.y * FPS; fu < (blockIdx.y + 1) * FPS; fu += U) {
+    float su[U];
+    frag_sums<U>(partial, contrib, 2, PG_FRAG, (size_t)wv * (PG_FRAG / PC_WAVES) + (fu * 64 + lane), su);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int f = fu + u;
+      const int a = f >> 4, r = f & 15;
+      const int m = tl.m0 + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (m < hw && n < g.ntot) {
+        const int y = m / g.w, x = m - y * g.w;
+        dx[(((size_t)tl.bc * (g.h + 2) + y + 1) * (g.w + 2) + x + 1) * g.ntot + n] = su[u];
+      }
+    }
+  }
+}
+
+template <typename T>
+static PgGeom pg_plan(const vfd_voxel_desc& d) {
+  constexpr int OC = PgCfg<T>::OC, XS = PgCfg<T>::XS;
+  PgGeom g;
+  g.nbc = d.B * d.N;
+  g.h = d.h;
+  g.w = d.w;
+  g.ntot = d.D * PC_CV;
+  g.np = (g.ntot + 255) / 256 * 256;                  // the weight copies' n stride (mode 2 / 5)
+  g.tpc = (d.h * d.w + PG_PIX - 1) / PG_PIX;
+  g.mtiles = g.nbc * g.tpc;
+  g.ntn = (g.ntot + PG_N - 1) / PG_N;
+  g.ntile = g.ntn * g.mtiles;
+  g.och = PC_O / OC;
+  g.natom = g.ntile * g.och;
+  int rows = d.w > 0 ? (PG_PIX - 1 + d.w - 1) / d.w + 1 : 1;   // pixel rows under 256 consecutive pixels
+  rows = rows < d.h ? rows : d.h;
+  g.hrows = rows + 2;
+  g.cols = d.w + 4;
+  g.lds_elems = (g.hrows + 2) * g.cols * XS;
+  const int res = pc_resident();
+  const int most = g.natom / g.och;
+  g.ngroup = most < res ? (most > 0 ? most : 1) : res;
+  return g;
+}
+
+template <typename T>
+static bool pg_supported(const vfd_voxel_desc& d) {
+  if (d.Cv != PC_CV || d.B <= 0 || d.N <= 0 || d.h < 2 || d.w < 2 || d.D <= 0 || d.D > 64) return false;
+  if ((long long)d.h * d.w >= (1 << 16) * 256LL) return false;    // 16-bit row / column packing
+  const PgGeom g = pg_plan<T>(d);
+  return (size_t)2 * g.lds_elems * sizeof(T) <= PD_LDS_MAX;
+}
+
+// ---------------------------------------------------------------------------------------------
+// bf16 folded data gradient on 2-D tiles ("pch", config 3): 16 x 16 interior pixels per tile, so an
+// atom stages only the tile's 18 x 18 G halo (+ F1 / F2 rows and E1 / E2 columns when the tile holds
+// pixel row / column 1 or h-2 / w-2): 400 positions per 256 pixels against pcg's whole rows (756 at
+// w = 80) — at the bf16 MFMA rate pcg spends its time in the loader waves (timing without staging:
+// 895 -> 458 us at config 2).  Pixel block a = tile rows 2a, 2a+1 (lane li: row 2a + li/16, column
+// li%16).  LDS image [20 rows][RP][XS]: row pitch PH_RP elements = 448 dwords (a multiple of 64
+// dwords), so the two tile rows of a pixel block fall into complementary bank slots for
+// ds_read_b128 (positions 20 dwords apart within a row).  Same B fragments (mode 5), stream-K,
+// prefetch ring, split-tile partials as pcg; ragged edge tiles (w or h not a multiple of 16) compute
+// clamped pixels they never store.
+constexpr int PH_T = 16;                        // tile side (pixels)
+constexpr int PH_S = PH_T + 4;                  // staged rows / columns: 18 halo + the two fold slots
+constexpr int PH_XS = 40;                       // bf16 per staged position (32 o + pad: 20 dwords)
+constexpr int PH_RP = 896;                      // bf16 per staged row (448 dwords)
+constexpr int PH_OC = 32;                       // o channels per atom
+constexpr int PH_ELEMS = PH_S * PH_RP;          // bf16 per LDS buffer (35.8 KB)
+
+struct PhGeom {
+  int nbc, h, w, ntot, np, tpw, tpc, mtiles, ntile, och, natom, ngroup;
+};
+
+__host__ __device__ inline int ph_lo(const PhGeom& g, int grp) {
+  return (int)(((long long)grp * g.natom) / g.ngroup);
+}
+
+struct PhTile {
+  int nt, bc, y0, x0;
+};
+
+__device__ __forceinline__ PhTile ph_tile(const PhGeom& g, int t) {
+  PhTile r;
+  const int mt = t % g.mtiles;
+  r.nt = t / g.mtiles;
+  r.bc = mt / g.tpc;
+  const int ti = mt - r.bc * g.tpc;
+  r.y0 = (ti / g.tpw) * PH_T;
+  r.x0 = (ti % g.tpw) * PH_T;
+  return r;
+}
+
+// loader waves (tid 0..255): 400 positions x 4 eight-channel vectors, each the sum of <= 2 x 2 G
+// vectors (rows ya / yb x columns xa / xb, -1 = absent); every load of a thread in flight together
+__device__ __forceinline__ void ph_stage(const PhGeom& g, __bf16* __restrict__ dst, const __bf16* __restrict__ gp,
+                                         int atom, int tid) {
+  constexpr int NP = PH_S * PH_S, PER = (NP * 4 + 255) / 256;     // 7 items per thread
+  const int t = atom / g.och, ch = atom - t * g.och;
+  const PhTile tl = ph_tile(g, t);
+  const bool f1 = tl.y0 == 0, f2 = tl.y0 <= g.h - 2 && tl.y0 + PH_T > g.h - 2;
+  const bool e1 = tl.x0 == 0, e2 = tl.x0 <= g.w - 2 && tl.x0 + PH_T > g.w - 2;
+  const int q = tid & 3;
+  const __bf16* src = gp + (size_t)tl.bc * g.h * g.w * PC_O + ch * PH_OC + 8 * q;
+  bf16x8 v[PER][4];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int p = (tid >> 2) + 64 * k;
+    const int r = p / PH_S, c = p - r * PH_S;
+    int ya = -1, yb = -1, xa = -1, xb = -1;
+    if (p < NP) {
+      if (r < PH_T + 2) {
+        const int y = tl.y0 - 1 + r;
+        ya = y >= 0 && y < g.h ? y : -1;
+      } else if (r == PH_T + 2 ? f1 : f2) {
+        ya = r == PH_T + 2 ? (2 < g.h ? 2 : -1) : g.h - 3;
+        yb = r == PH_T + 2 ? 0 : g.h - 1;
+      }
+      if (c < PH_T + 2) {
+        const int x = tl.x0 - 1 + c;
+        xa = x >= 0 && x < g.w ? x : -1;
+      } else if (c == PH_T + 2 ? e1 : e2) {
+        xa = c == PH_T + 2 ? (2 < g.w ? 2 : -1) : g.w - 3;
+        xb = c == PH_T + 2 ? 0 : g.w - 1;
+      }
+    }
+    const int ys[2] = {ya, yb}, xs[2] = {xa, xb};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int yy = ys[j >> 1], xx = xs[j & 1];
+      bf16x8 z;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) z[e] = (__bf16)0.f;
+      v[k][j] = (yy >= 0 && xx >= 0) ? *reinterpret_cast<const bf16x8*>(src + ((size_t)yy * g.w + xx) * PC_O) : z;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int p = (tid >> 2) + 64 * k;
+    if (p < NP) {
+      const int r = p / PH_S, c = p - r * PH_S;
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        o[e] = (__bf16)(((float)v[k][0][e] + (float)v[k][1][e]) + ((float)v[k][2][e] + (float)v[k][3][e]));
+      *reinterpret_cast<bf16x8*>(dst + r * PH_RP + c * PH_XS + 8 * q) = o;
+    }
+  }
+}
+
+__global__ __launch_bounds__(PC_THREADS, 2) void pch_main_k(PhGeom g, const __bf16* __restrict__ gp,
+                                                           const bf16x8* __restrict__ Wd, float* __restrict__ dx,
+                                                           float* __restrict__ partial) {
+  constexpr int STEPS = PH_OC / 16, PF = VFD_PG_BF_PF, ITERS = 9 * STEPS;
+  static_assert(ITERS % PF == 0, "prefetch ring");
+  __shared__ __attribute__((aligned(16))) __bf16 lds[2 * PH_ELEMS];
+  const int grp = (g.ngroup % 8 == 0) ? (blockIdx.x % 8) * (g.ngroup / 8) + blockIdx.x / 8 : blockIdx.x;
+  const int a_lo = ph_lo(g, grp), a_hi = ph_lo(g, grp + 1);
+  if (a_lo >= a_hi) return;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const bool compute = wv < PC_WAVES;
+  if (!compute) ph_stage(g, lds, gp, a_lo, threadIdx.x - 64 * PC_WAVES);
+  __syncthreads();
+  if (!compute) {
+    for (int atom = a_lo; atom < a_hi; ++atom) {
+      if (atom + 1 < a_hi) ph_stage(g, lds + ((atom + 1 - a_lo) & 1) * PH_ELEMS, gp, atom + 1, threadIdx.x - 64 * PC_WAVES);
+      __syncthreads();
+    }
+    return;
+  }
+  const int li = lane & 31, lh = lane >> 5;
+  f32x16 acc[8];
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[a][r] = 0.f;
+  const size_t qstride = (size_t)(g.np / 32) * 64, tstride = (size_t)(PC_O / 16) * qstride;
+  auto bbase = [&](int atom) -> const bf16x8* {
+    const int t = atom / g.och, ch = atom - t * g.och;
+    const int nt = t / g.mtiles;
+    return Wd + (size_t)ch * STEPS * qstride + (size_t)(nt * (PG_N / 32) + wv) * 64 + lane;
+  };
+  bf16x8 bq[PF];
+  const bf16x8* bcur = bbase(a_lo);
+#pragma unroll
+  for (int j = 0; j < PF; ++j) bq[j] = bcur[(j / STEPS) * tstride + (j % STEPS) * qstride];
+  const int ly = li >> 4, lx = li & 15;
+  for (int atom = a_lo; atom < a_hi; ++atom) {
+    const int t = atom / g.och, ch = atom - t * g.och;
+    const PhTile tl = ph_tile(g, t);
+    const bool more = atom + 1 < a_hi;
+    const bf16x8* bnext = more ? bbase(atom + 1) : bcur;
+    // the lane's pixel column (clamped into the camera) and, per block, its row
+    const int px = min(tl.x0 + lx, g.w - 1);
+    int py[8];
+#pragma unroll
+    for (int a = 0; a < 8; ++a) py[a] = min(tl.y0 + 2 * a + ly, g.h - 1);
+    const __bf16* xb = lds + ((atom - a_lo) & 1) * PH_ELEMS;
+    auto offsets = [&](int tap, int* o1) {
+      const int ky = tap / 3, kx = tap - 3 * ky;
+      const int col = (px == 1 && kx == 2) ? PH_T + 2 : (px == g.w - 2 && kx == 0) ? PH_T + 3 : px - tl.x0 + kx;
+#pragma unroll
+      for (int a = 0; a < 8; ++a) {
+        const int row = (py[a] == 1 && ky == 2) ? PH_T + 2 : (py[a] == g.h - 2 && ky == 0) ? PH_T + 3 : py[a] - tl.y0 + ky;
+        o1[a] = row * PH_RP + col * PH_XS + 8 * lh;
+      }
+    };
+    int o1c[8];
+    offsets(0, o1c);
+    bf16x8 afc[8], afn[8];
+#pragma unroll
+    for (int a = 0; a < 8; ++a) afc[a] = *reinterpret_cast<const bf16x8*>(&xb[o1c[a]]);
+#pragma unroll
+    for (int j = 0; j < ITERS; ++j) {
+      const int tap = j / STEPS, q = j % STEPS;
+      const bf16x8 b = bq[j % PF];
+      {
+        const int jn = j + PF;
+        if (jn < ITERS)
+          bq[j % PF] = bcur[(jn / STEPS) * tstride + (jn % STEPS) * qstride];
+        else if (more)
+          bq[j % PF] = bnext[((jn - ITERS) / STEPS) * tstride + ((jn - ITERS) % STEPS) * qstride];
+      }
+      if (q < STEPS - 1) {
+#pragma unroll
+        for (int a = 0; a < 8; ++a) afn[a] = *reinterpret_cast<const bf16x8*>(&xb[o1c[a] + 16 * (q + 1)]);
+      } else if (tap < 8) {
+        offsets(tap + 1, o1c);
+#pragma unroll
+        for (int a = 0; a < 8; ++a) afn[a] = *reinterpret_cast<const bf16x8*>(&xb[o1c[a]]);
+      }
+#pragma unroll
+      for (int a = 0; a < 8; ++a) acc[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afc[a], b, acc[a], 0, 0, 0);
+#pragma unroll
+      for (int a = 0; a < 8; ++a) afc[a] = afn[a];
+    }
+    bcur = bnext;
+    __syncthreads();                                  // buffer handed back to the loader waves
+    if (ch == g.och - 1 || atom == a_hi - 1) {
+      const int ts = t * g.och;
+      const int n = tl.nt * PG_N + wv * 32 + li;
+      if (ts >= a_lo && ts + g.och <= a_hi) {         // whole tile in this range: store
+#pragma unroll
+        for (int a = 0; a < 8; ++a)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int rr = (r & 3) + 8 * (r >> 2) + 4 * lh;       // pixel of block a: tile row 2a + rr/16
+            const int y = tl.y0 + 2 * a + (rr >> 4), x = tl.x0 + (rr & 15);
+            if (y < g.h && x < g.w && n < g.ntot)
+              dx[(((size_t)tl.bc * (g.h + 2) + y + 1) * (g.w + 2) + x + 1) * g.ntot + n] = acc[a][r];
+            acc[a][r] = 0.f;
+          }
+      } else {
+        const int slot = t == a_lo / g.och ? 0 : 1;
+        float* dst = partial + ((size_t)grp * 2 + slot) * PG_FRAG + (size_t)wv * (PG_FRAG / PC_WAVES) + lane;
+#pragma unroll
+        for (int a = 0; a < 8; ++a)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            dst[(a * 16 + r) * 64] = acc[a][r];
+            acc[a][r] = 0.f;
+          }
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void pch_reduce_k(PhGeom g, const float* __restrict__ partial,
+                                                    float* __restrict__ dx) {
+  const int grp = blockIdx.x;
+  const int lo = ph_lo(g, grp);
+  if (grp == 0 || lo % g.och == 0) return;
+  const int t = lo / g.och;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c0 = (grp - 1) * 2 + (t == ph_lo(g, grp - 1) / g.och ? 0 : 1), c1 = grp * 2;
+  const PhTile tl = ph_tile(g, t);
+  constexpr int FPS = 8 * 16 / PC_FSL;
+  constexpr int U = 4;
+  const int contrib[2] = {c0, c1};
+  const int n = tl.nt * PG_N + wv * 32 + (lane & 31);
+  for (int fu = blockIdx.y * FPS; fu < (blockIdx.y + 1) * FPS; fu += U) {
+    float su[U];
+    frag_sums<U>(partial, contrib, 2, PG_FRAG, (size_t)wv * (PG_FRAG / PC_WAVES) + (fu * 64 + lane), su);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int f = fu + u;
+      const int a = f >> 4, r = f & 15;
+      const int rr = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      const int y = tl.y0 + 2 * a + (rr >> 4), x = tl.x0 + (rr & 15);
+      if (y < g.h && x < g.w && n < g.ntot)
+        dx[(((size_t)tl.bc * (g.h + 2) + y + 1) * (g.w + 2) + x + 1) * g.ntot + n] = su[u];
+    }
+  }
+}
+
+static PhGeom ph_plan(const vfd_voxel_desc& d) {
+  PhGeom g;
+  g.nbc = d.B * d.N;
+  g.h = d.h;
+  g.w = d.w;
+  g.ntot = d.D * PC_CV;
+  g.np = (g.ntot + 255) / 256 * 256;
+  g.tpw = (d.w + PH_T - 1) / PH_T;
+  g.tpc = ((d.h + PH_T - 1) / PH_T) * g.tpw;
+  g.mtiles = g.nbc * g.tpc;
+  g.ntile = ((g.ntot + PG_N - 1) / PG_N) * g.mtiles;
+  g.och = PC_O / PH_OC;
+  g.natom = g.ntile * g.och;
+  const int res = pc_resident();
+  const int most = g.natom / g.och;
+  g.ngroup = most < res ? (most > 0 ? most : 1) : res;
+  return g;
+}
+
+static bool ph_supported(const vfd_voxel_desc& d) {
+  return d.Cv == PC_CV && d.B > 0 && d.N > 0 && d.h >= 2 && d.w >= 2 && d.D > 0 && d.D <= 64 &&
+         (long long)d.B * d.N * d.h * d.w < (1LL << 31) / 256;
+}
+
+// =============================================================================================
 // K3C weight gradient — reduce_dim's first conv, d weight and d bias (volumetric_fusionnet.py:59-60,
 // 265 backward), as an fp32 MFMA GEMM over the pixels of all cameras:
 //
@@ -1404,8 +2064,19 @@ int vfd_proj_conv_fwd_bf16(const vfd_voxel_desc* d, const float* vox, const floa
   return fail_launch("proj_conv_fwd_bf16");
 }
 
+#ifndef VFD_PCD_GEN
+#define VFD_PCD_GEN 1       // folded fp32 data gradient: 1 = pcdf where its staged rows fit LDS (configs
+#endif                      // 2-4: 3.08 vs pcg's 3.15 ms at config 2), pcg otherwise (config 5); 2 = pcg always
+
+// pcg for the folded form: always at VFD_PCD_GEN 2, else where pcdf does not fit
+static bool pcd_use_pcg(const vfd_voxel_desc& d) {
+  return d.pad_out == 2 && pg_supported<float>(d) && (VFD_PCD_GEN >= 2 || !pf_supported(d));
+}
+
 size_t vfd_proj_conv_dgrad_workspace(const vfd_voxel_desc* d) {
   if (!d) return 0;
+  if (pcd_use_pcg(*d))
+    return (size_t)pg_plan<float>(*d).ngroup * 2 * PG_FRAG * sizeof(float);
   if (d->pad_out == 2) return pf_supported(*d) ? (size_t)pf_plan(*d).ngroup * 2 * PC_FRAG * sizeof(float) : 0;
   if (!pd_supported(*d)) return 0;
   return (size_t)pd_plan(*d).ngroup * 2 * PC_FRAG * sizeof(float);
@@ -1414,11 +2085,20 @@ size_t vfd_proj_conv_dgrad_workspace(const vfd_voxel_desc* d) {
 int vfd_proj_conv_dgrad(const vfd_voxel_desc* d, const float* g_pre, const float* Wd, float* dx, void* ws,
                         size_t ws_bytes, void* stream) {
   VFD_REQUIRE(d && g_pre && Wd && dx, "proj_conv_dgrad: null argument");
-  VFD_REQUIRE(d->pad_out == 2 ? pf_supported(*d) : pd_supported(*d),
+  const bool gen2 = pcd_use_pcg(*d);
+  VFD_REQUIRE(gen2 || (d->pad_out == 2 ? pf_supported(*d) : pd_supported(*d)),
               "proj_conv_dgrad: unsupported shape (Cv = %d, 0 < D <= 64, staged rows in LDS; folded: h >= 6, w >= 64)", PC_CV);
   VFD_REQUIRE(ws && ws_bytes >= vfd_proj_conv_dgrad_workspace(d), "proj_conv_dgrad: workspace too small");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_PROJ_CONV_DGRAD, s);
+  if (gen2) {
+    const PgGeom g = pg_plan<float>(*d);
+    lds_attr(reinterpret_cast<const void*>(pcg_main_k<float, float>), PD_LDS_MAX);
+    pcg_main_k<float, float><<<g.ngroup, PC_THREADS, (size_t)2 * g.lds_elems * sizeof(float), s>>>(g, g_pre, Wd, dx,
+                                                                                                  (float*)ws);
+    pcg_reduce_k<<<dim3(g.ngroup, PC_FSL), 256, 0, s>>>(g, (const float*)ws, dx);
+    return fail_launch("proj_conv_dgrad");
+  }
   if (d->pad_out == 2) {
     const PfGeom g = pf_plan(*d);
     lds_attr(reinterpret_cast<const void*>(pcdf_main_k), PD_LDS_MAX);
@@ -1433,6 +2113,43 @@ int vfd_proj_conv_dgrad(const vfd_voxel_desc* d, const float* g_pre, const float
   pcd_main_k<<<g.ngroup, PC_THREADS, lds, s>>>(g, g_pre, Wd, dx, partial);
   pcd_reduce_k<<<dim3(g.ngroup, PC_FSL), 256, 0, s>>>(g, partial, dx);
   return fail_launch("proj_conv_dgrad");
+}
+
+// bf16 form (config 3): g_pre bf16 [B*N, h, w, O] NHWC, Wd = vfd_weight_fragments_bf16 mode 5, dx fp32
+// (the folded interior, pad_out == 2 only)
+#ifndef VFD_PCD_BF_2D
+#define VFD_PCD_BF_2D 1     // bf16 folded data gradient on 16 x 16 tiles (pch); 0 = pcg's row tiles
+#endif
+
+size_t vfd_proj_conv_dgrad_bf16_workspace(const vfd_voxel_desc* d) {
+  if (!d || d->pad_out != 2) return 0;
+  if (VFD_PCD_BF_2D && ph_supported(*d)) return (size_t)ph_plan(*d).ngroup * 2 * PG_FRAG * sizeof(float);
+  if (!pg_supported<__bf16>(*d)) return 0;
+  return (size_t)pg_plan<__bf16>(*d).ngroup * 2 * PG_FRAG * sizeof(float);
+}
+
+int vfd_proj_conv_dgrad_bf16(const vfd_voxel_desc* d, const void* g_pre, const void* Wd, float* dx, void* ws,
+                             size_t ws_bytes, void* stream) {
+  VFD_REQUIRE(d && g_pre && Wd && dx, "proj_conv_dgrad_bf16: null argument");
+  const bool two_d = VFD_PCD_BF_2D && d->pad_out == 2 && ph_supported(*d);
+  VFD_REQUIRE(two_d || (d->pad_out == 2 && pg_supported<__bf16>(*d)),
+              "proj_conv_dgrad_bf16: unsupported shape (folded form pad_out = 2, Cv = %d, 0 < D <= 64, staged rows in LDS)",
+              PC_CV);
+  VFD_REQUIRE(ws && ws_bytes >= vfd_proj_conv_dgrad_bf16_workspace(d), "proj_conv_dgrad_bf16: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  ProfScope ps(K_PROJ_CONV_DGRAD, s);
+  if (two_d) {
+    const PhGeom g = ph_plan(*d);
+    pch_main_k<<<g.ngroup, PC_THREADS, 0, s>>>(g, (const __bf16*)g_pre, (const bf16x8*)Wd, dx, (float*)ws);
+    pch_reduce_k<<<dim3(g.ngroup, PC_FSL), 256, 0, s>>>(g, (const float*)ws, dx);
+    return fail_launch("proj_conv_dgrad_bf16");
+  }
+  const PgGeom g = pg_plan<__bf16>(*d);
+  lds_attr(reinterpret_cast<const void*>(pcg_main_k<__bf16, __bf16>), PD_LDS_MAX);
+  pcg_main_k<__bf16, __bf16><<<g.ngroup, PC_THREADS, (size_t)2 * g.lds_elems * sizeof(__bf16), s>>>(
+      g, (const __bf16*)g_pre, Wd, dx, (float*)ws);
+  pcg_reduce_k<<<dim3(g.ngroup, PC_FSL), 256, 0, s>>>(g, (const float*)ws, dx);
+  return fail_launch("proj_conv_dgrad_bf16");
 }
 
 size_t vfd_proj_conv_wgrad_workspace(const vfd_voxel_desc* d) {

@@ -16,10 +16,11 @@ __device__ __forceinline__ int rp_src(int i, int n) {       // padded index -> s
 // Backward of LeakyReLU(slope) followed by the one-pixel reflect pad, channels-last (the fused
 // reduce_dim convs' outputs, projconv.hip / padconv.hip): gp[n][y][x][c] = (sum of the copies of
 // g at pixel (y, x)) * (out[n][y+1][x+1][c] > 0 ? 1 : slope); float4 lanes over channels.
-__global__ __launch_bounds__(256) void lrelu_pad_bwd_nhwc_k(const float4* __restrict__ g, const float4* __restrict__ out,
-                                                            float4* __restrict__ gp, long long n_img, int h, int w,
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void lrelu_pad_bwd_nhwc_k(const TI* __restrict__ g, const TI* __restrict__ out,
+                                                            TO* __restrict__ gp, long long n_img, int h, int w,
                                                             int c4, float slope) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;       // (pixel, float4) of image blockIdx.y
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;       // (pixel, channel quad) of image blockIdx.y
   if (j >= h * w * c4) return;
   const long long n = blockIdx.y;
   const int pix = j / c4, q = j - pix * c4;
@@ -29,22 +30,22 @@ __global__ __launch_bounds__(256) void lrelu_pad_bwd_nhwc_k(const float4* __rest
   int rows[3], cols[3], nr, nc;
   pad_sets(yy, h, true, rows, &nr);
   pad_sets(x, w, true, cols, &nc);
-  const float4* gb = g + n * (h + 2) * wo * c4 + q;
+  const TI* gb = g + ((size_t)n * (h + 2) * wo * c4 + q) * 4;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int a = 0; a < nr; ++a)
     for (int b = 0; b < nc; ++b) {
-      const float4 v = gb[((size_t)rows[a] * wo + cols[b]) * c4];
+      const float4 v = ld4(gb + ((size_t)rows[a] * wo + cols[b]) * c4 * 4);
       s.x += v.x;
       s.y += v.y;
       s.z += v.z;
       s.w += v.w;
     }
-  const float4 o = out[((n * (h + 2) + yy + 1) * wo + x + 1) * c4 + q];
+  const float4 o = ld4(out + (((n * (h + 2) + yy + 1) * wo + x + 1) * c4 + q) * 4);
   s.x *= o.x > 0.f ? 1.f : slope;
   s.y *= o.y > 0.f ? 1.f : slope;
   s.z *= o.z > 0.f ? 1.f : slope;
   s.w *= o.w > 0.f ? 1.f : slope;
-  gp[i] = s;
+  st4(gp + i * 4, s);
 }
 
 
@@ -246,9 +247,29 @@ int vfd_lrelu_pad1_bwd_nhwc(const float* g, const float* out, float* gp, long lo
   ProfScope ps(K_REFLECT_PAD, s);
   VFD_REQUIRE(n_img < 65536 && (long long)h * w * C < (1LL << 31), "lrelu_pad1_bwd_nhwc: too large");
   const dim3 grid((unsigned)(((long long)h * w * (C / 4) + 255) / 256), (unsigned)n_img);
-  lrelu_pad_bwd_nhwc_k<<<grid, 256, 0, s>>>((const float4*)g, (const float4*)out, (float4*)gp,
-                                                                  n_img, h, w, C / 4, slope);
+  lrelu_pad_bwd_nhwc_k<float, float><<<grid, 256, 0, s>>>(g, out, gp, n_img, h, w, C / 4, slope);
   return fail_launch("lrelu_pad1_bwd_nhwc");
+}
+
+int vfd_lrelu_pad1_bwd_nhwc_t(const void* g, const void* out, void* gp, long long n_img, int h, int w, int C,
+                              float slope, int dtype_in, int dtype_out, void* stream) {
+  VFD_REQUIRE(g && out && gp && n_img > 0 && h >= 2 && w >= 2 && C > 0 && C % 4 == 0 && (dtype_in == 0 || dtype_in == 1) &&
+                  (dtype_out == 0 || dtype_out == 1),
+              "lrelu_pad1_bwd_nhwc_t: bad arguments (h, w >= 2, C %% 4 == 0, dtypes 0 fp32 / 1 bf16)");
+  VFD_REQUIRE((((uintptr_t)g | (uintptr_t)out | (uintptr_t)gp) & 7) == 0, "lrelu_pad1_bwd_nhwc_t: 8-B alignment");
+  VFD_REQUIRE(n_img < 65536 && (long long)h * w * C < (1LL << 31), "lrelu_pad1_bwd_nhwc_t: too large");
+  hipStream_t s = (hipStream_t)stream;
+  ProfScope ps(K_REFLECT_PAD, s);
+  const dim3 grid((unsigned)(((long long)h * w * (C / 4) + 255) / 256), (unsigned)n_img);
+  if (dtype_in == 0 && dtype_out == 0)
+    lrelu_pad_bwd_nhwc_k<float, float><<<grid, 256, 0, s>>>((const float*)g, (const float*)out, (float*)gp, n_img, h, w, C / 4, slope);
+  else if (dtype_in == 0)
+    lrelu_pad_bwd_nhwc_k<float, __bf16><<<grid, 256, 0, s>>>((const float*)g, (const float*)out, (__bf16*)gp, n_img, h, w, C / 4, slope);
+  else if (dtype_out == 0)
+    lrelu_pad_bwd_nhwc_k<__bf16, float><<<grid, 256, 0, s>>>((const __bf16*)g, (const __bf16*)out, (float*)gp, n_img, h, w, C / 4, slope);
+  else
+    lrelu_pad_bwd_nhwc_k<__bf16, __bf16><<<grid, 256, 0, s>>>((const __bf16*)g, (const __bf16*)out, (__bf16*)gp, n_img, h, w, C / 4, slope);
+  return fail_launch("lrelu_pad1_bwd_nhwc_t");
 }
 
 int vfd_elu_up_pad1_fwd(const void* y, void* out, long long planes, int h, int w, int up, int dtype, void* stream) {

@@ -17,6 +17,8 @@
 //           o = 32 ob + (lane & 31), c = 16 q16 + 8 (lane >> 5) + j (projconv.hip pcvb_main_k)
 //   mode 4  K2C, bf16 (from the mode-0 copy f0): dst[tap][q16][ob][lane][j] = bf16(f0 of channel
 //           16 q16 + 8 (lane >> 5) + j, out-channel 32 ob + (lane & 31)), q16 < ceil32(C) / 16
+//   mode 5  K3C data gradient, bf16 (from the mode-2 copy f2): dst[tap'][q16][nb][lane][j] = bf16(f2 of
+//           out-channel 16 q16 + 8 (lane >> 5) + j, n = 32 nb + (lane & 31)) (projconv.hip pcg_main_k)
 //   permute element (o, a, b, t) between any two strided layouts (the pose weight between the
 //           reference channel order c*Z + z and the map's z*C1 + c, NCHW or channels-last for MIOpen);
 //           swap = the NCHW -> NCHW instance dst[o][b][a][t] = w[o][a][b][t]
@@ -197,6 +199,34 @@ __global__ __launch_bounds__(256) void wfrag4_k(const float4* __restrict__ f0, w
   dst[i] = v;
 }
 
+// mode 5 (bf16, projconv.hip pcg_main_k<bf16>) from the fp32 mode-2 copy f2 [9][O/4][npad][2][2]:
+// dst[tap'][q16][nb][lane][j] = bf16(f2 element of out-channel o = 16 q16 + 8 (lane >> 5) + j, n = 32 nb +
+// (lane & 31)); one thread per destination lane fragment: two 16-B reads (out-channel quads
+// 4 q16 + 2h, +1), coalesced over the 32 n of a block
+__global__ __launch_bounds__(256) void wfrag5_k(const float4* __restrict__ f2, wbf16x8* __restrict__ dst, int OQ,
+                                                int npad) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int NB = npad / 32, Q16 = OQ / 4;
+  const long long total = (long long)WR_TAPS * Q16 * NB * 64;
+  if (i >= total) return;
+  const int lane = (int)(i & 63);
+  long long r = i >> 6;
+  const int nb = (int)(r % NB);
+  r /= NB;
+  const int q16 = (int)(r % Q16), tap = (int)(r / Q16);
+  const int n = 32 * nb + (lane & 31), h = lane >> 5;
+  wbf16x8 v;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const float4 f = f2[((size_t)tap * OQ + 4 * q16 + 2 * h + k) * npad + n];
+    v[4 * k + 0] = (__bf16)f.x;
+    v[4 * k + 1] = (__bf16)f.y;
+    v[4 * k + 2] = (__bf16)f.z;
+    v[4 * k + 3] = (__bf16)f.w;
+  }
+  dst[i] = v;
+}
+
 // mode 0 with the pose map's channel order (cz = z * C1 + c, reference channel c * Z + z):
 // tile = 8 out-channels x 4 map channels c0 .. c0 + 3 x all Z; source runs w[o][c0 * Z .. (c0 + 4) * Z][taps]
 // (4 Z rows), destination runs (tap, q = (z C1 + c0) / 4): 8 o x 4 cz.  Needs C1 % 4 == 0 and
@@ -342,6 +372,13 @@ int vfd_weight_fragments_bf16(int mode, const float* w, void* dst, int O, int C,
     const int cq4 = (C + 15) / 16 * 4, nq16 = (C + 31) / 32 * 2;
     const long long n = (long long)WR_TAPS * nq16 * (O / 32) * 64;
     wfrag4_k<<<(unsigned)((n + 255) / 256), 256, 0, s>>>((const float4*)w, (wbf16x8*)dst, O, cq4, nq16);
+    return fail_launch("weight_fragments_bf16");
+  }
+  if (mode == 5) {          // w = the fp32 mode-2 copy [9][O/4][npad][2][2] (K3C data gradient)
+    VFD_REQUIRE(O % 16 == 0 && Cv > 0 && D > 0, "weight_fragments_bf16: mode 5 needs O %% 16");
+    const int npad = (Cv * D + 255) / 256 * 256;
+    const long long n = (long long)WR_TAPS * (O / 16) * (npad / 32) * 64;
+    wfrag5_k<<<(unsigned)((n + 255) / 256), 256, 0, s>>>((const float4*)w, (wbf16x8*)dst, O / 4, npad);
     return fail_launch("weight_fragments_bf16");
   }
   set_error("weight_fragments_bf16: mode %d", mode);

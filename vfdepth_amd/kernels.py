@@ -397,6 +397,7 @@ def proj_conv_dgrad_weight(w, Cv, D):
 _PC_DGRAD = os.environ.get('VFD_PC_DGRAD', '1') != '0'
 _PC_WGRAD = os.environ.get('VFD_PC_WGRAD', '1') != '0'
 _PC_FOLD = os.environ.get('VFD_PC_FOLD', '1') != '0'    # K3C data gradient with the reflect fold inside
+_PC_BF16_BWD = os.environ.get('VFD_PC_BF16_BWD', '1') != '0'   # hand-written bf16 K3C / K2C backward (config 3)
 
 
 def pad_conv_weight_fragments(w, C1=0, Z=0):
@@ -582,17 +583,23 @@ class PadConvBF16(torch.autograd.Function):
         return dx, dw, (db.float() if db is not None else None), None, None, None
 
 
-def lrelu_pad_backward(g, out, slope=0.1):
+_DT = {torch.float32: 0, torch.bfloat16: 1}
+
+
+def lrelu_pad_backward(g, out, slope=0.1, dtype=None):
     """d pre-activation of LeakyReLU(slope) + reflect pad(1) from the channels-last gradient of the
-    padded output g and that output (fused, deterministic: reflectpad.hip) -> NHWC [n, C, h, w]."""
+    padded output g and that output (fused, deterministic: reflectpad.hip) -> NHWC [n, C, h, w].
+    g and out fp32 or bf16 (the same type); the result in `dtype` (default g's), computed in fp32."""
     lib = L.load()
     g = _channels_last(g, 'grad')
+    out = _channels_last(out.to(g.dtype), 'output')
+    dtype = dtype or g.dtype
     n, C, hp, wp = g.shape
-    gp = torch.empty(n, C, hp - 2, wp - 2, device=g.device, memory_format=torch.channels_last)
-    L.check(lib.vfd_lrelu_pad1_bwd_nhwc(g.data_ptr(), out.data_ptr(), gp.data_ptr(), n, hp - 2, wp - 2, C, slope,
-                                        L.stream()), 'lrelu_pad1_bwd_nhwc')
+    gp = torch.empty(n, C, hp - 2, wp - 2, device=g.device, dtype=dtype, memory_format=torch.channels_last)
+    L.check(lib.vfd_lrelu_pad1_bwd_nhwc_t(g.data_ptr(), out.data_ptr(), gp.data_ptr(), n, hp - 2, wp - 2, C, slope,
+                                          _DT[g.dtype], _DT[dtype], L.stream()), 'lrelu_pad1_bwd_nhwc')
     if L.PROF_ON:                            # g in, the output's interior in, gp out
-        L.ALG_BYTES['reflect_pad'] += (g.numel() + 2 * gp.numel()) * 4
+        L.ALG_BYTES['reflect_pad'] += (g.numel() + gp.numel()) * g.element_size() + gp.numel() * gp.element_size()
     return gp
 
 
@@ -714,6 +721,20 @@ class ProjConv(torch.autograd.Function):
         return None, dvox, None, None, dw0, db0
 
 
+def proj_conv_dgrad_weight_bf16(w, Cv, D):
+    """reduce_dim[0] weight -> the bf16 data-gradient kernel's copy [9 flipped taps, O/16, np/32, 64, 8]
+    (projconv.hip pcg_main_k<bf16>; through the fp32 mode-2 copy), rounded to nearest even."""
+    lib = L.load()
+    w = _dev(w.detach(), 'conv weight')
+    O = w.shape[0]
+    f2 = proj_conv_dgrad_weight(w, Cv, D)
+    npad = f2.shape[2]
+    out = torch.empty(9, O // 16, npad // 32, 64, 8, dtype=torch.bfloat16, device=w.device)
+    L.check(lib.vfd_weight_fragments_bf16(5, f2.data_ptr(), out.data_ptr(), O, 0, 0, 0, Cv, D, L.stream()),
+            'weight_fragments_bf16')
+    return out
+
+
 def proj_conv_weight_fragments_bf16(w, Cv, D):
     """reduce_dim[0] weight [O, Cv*D, 3, 3] (reference channel c*D + d) -> the bf16 K3C kernel's
     fragment copy [D, 9, Cv/16, O/32, 64, 8] (projconv.hip pcvb_main_k), rounded to nearest even."""
@@ -751,6 +772,9 @@ class ProjConvBF16(torch.autograd.Function):
         d = space.desc(B, N, Cv=Cv)
         nbytes = lib.vfd_proj_conv_fwd_workspace(ctypes.byref(d))
         ws = _ws(nbytes, vox.device)
+        # the bf16 data gradient is the folded form: K3's plan built for a folded d_out (pad_out = 2)
+        ctx.pad_out = 2 if (_PC_DGRAD and _PC_BF16_BWD and lib.vfd_proj_conv_dgrad_bf16_workspace(ctypes.byref(
+            space.desc(B, N, Cv=Cv, pad_out=2)))) else 1
         L.check(lib.vfd_proj_conv_fwd_bf16(ctypes.byref(d), vox.data_ptr(), invK.data_ptr(), E.data_ptr(),
                                            wq.data_ptr(), bias.data_ptr(), O, out.data_ptr(),
                                            x.data_ptr() if need_x else None, ws.data_ptr(), nbytes, L.stream()),
@@ -758,6 +782,7 @@ class ProjConvBF16(torch.autograd.Function):
         ctx.space, ctx.shape = space, (B, N, V, Cv, O)
         ctx.plan = None
         if ctx.needs_input_grad[1]:
+            d.pad_out = ctx.pad_out
             nbytes = lib.vfd_voxel_project_plan_bytes(ctypes.byref(d))
             ctx.plan = torch.empty(nbytes, dtype=torch.uint8, device=vox.device)
             L.check(lib.vfd_voxel_project_plan(ctypes.byref(d), invK.data_ptr(), E.data_ptr(), ctx.plan.data_ptr(),
@@ -771,17 +796,30 @@ class ProjConvBF16(torch.autograd.Function):
         w0, out, x = ctx.saved_tensors
         space = ctx.space
         B, N, V, Cv, O = ctx.shape
-        d = space.desc(B, N, Cv=Cv)
-        # adjoint of the reflect padding and the LeakyReLU in fp32 (sign from the bf16 output), then
-        # the bf16 operand of MIOpen's gradients
-        g_pre = lrelu_pad_backward(g.float(), out.float()).to(torch.bfloat16)
+        d = space.desc(B, N, Cv=Cv, pad_out=ctx.pad_out)
+        # adjoint of the reflect padding and the LeakyReLU (fp32 arithmetic, sign from the bf16
+        # output), one bf16 rounding: the bf16 operand of the gradients
+        g_pre = lrelu_pad_backward(g.to(torch.bfloat16), out, dtype=torch.bfloat16)
         mask = (ctx.needs_input_grad[1], ctx.needs_input_grad[4], ctx.needs_input_grad[5])
-        wb = proj_conv_weight(w0.detach(), Cv, space.D).to(torch.bfloat16)
+        dx = dw = db = None
+        if mask[0] and ctx.pad_out == 2:
+            # the folded bf16 data gradient (bf16 MFMA, fp32 accumulation, projconv.hip pcg_main_k)
+            wd = proj_conv_dgrad_weight_bf16(w0, Cv, space.D)
+            nbytes = lib.vfd_proj_conv_dgrad_bf16_workspace(ctypes.byref(d))
+            dx = torch.empty(B * N, Cv * space.D, space.h + 2, space.w + 2, device=g.device,
+                             memory_format=torch.channels_last)
+            ws = _ws(nbytes, g.device)
+            L.check(lib.vfd_proj_conv_dgrad_bf16(ctypes.byref(d), g_pre.data_ptr(), wd.data_ptr(), dx.data_ptr(),
+                                                 ws.data_ptr(), nbytes, L.stream()), 'proj_conv_dgrad_bf16')
+        need_dx = mask[0] and dx is None
         if x is None:   # only the bias gradient was asked for (the forward wrote no side output)
-            dx, dw, db = None, None, g_pre.float().sum((0, 2, 3))
-        else:
-            dx, dw, db = torch.ops.aten.convolution_backward(g_pre, x, wb, [O], [1, 1], [0, 0], [1, 1], False, [0, 0],
-                                                             1, [mask[0], mask[1], mask[2]])
+            db = g_pre.float().sum((0, 2, 3))
+        elif need_dx or mask[1] or mask[2]:
+            wb = proj_conv_weight(w0.detach(), Cv, space.D).to(torch.bfloat16)
+            dx2, dw, db = torch.ops.aten.convolution_backward(g_pre, x, wb, [O], [1, 1], [0, 0], [1, 1], False, [0, 0],
+                                                              1, [need_dx, mask[1], mask[2]])
+            if need_dx:
+                dx = dx2
         dvox = dw0 = None
         if mask[0]:
             dxf = dx.float().contiguous(memory_format=torch.channels_last)
@@ -1126,12 +1164,30 @@ def _bn_sync(lib, d, partial, pg, count, what, invstd=None, dgamma=None, dbeta=N
     SyncBatchNorm allows; the apply kernels read the global count from row C on the device, so
     nothing waits on the host).  Backward (invstd given): d gamma / d beta from this rank's LOCAL
     sums first, as torch's SyncBatchNorm returns them (DDP then averages them over ranks)."""
+    import time
     import torch.distributed as dist
     sums = torch.empty(d.C + 1, 2, dtype=torch.float64, device=partial.device)
     L.check(lib.vfd_bn_sum(ctypes.byref(d), partial.data_ptr(), float(count), sums.data_ptr(), L.ptr(invstd),
                            L.ptr(dgamma), L.ptr(dbeta), L.stream()), what)
+    t0 = time.perf_counter()
     dist.all_reduce(sums, group=pg)
+    SYNCBN_STATS['calls'] += 1
+    SYNCBN_STATS['bytes'] += sums.numel() * sums.element_size()
+    SYNCBN_STATS['host_s'] += time.perf_counter() - t0
     return sums
+
+
+# SyncBatchNorm collectives issued by the fused BN (one all-reduce of [C+1][2] fp64 per layer and
+# direction): count, payload and the host time spent in dist.all_reduce (for RCCL the enqueue, for
+# gloo the whole exchange).  syncbn_stats(reset=True) reads them.
+SYNCBN_STATS = {'calls': 0, 'bytes': 0, 'host_s': 0.0}
+
+
+def syncbn_stats(reset=True):
+    out = dict(SYNCBN_STATS)
+    if reset:
+        SYNCBN_STATS.update(calls=0, bytes=0, host_s=0.0)
+    return out
 
 
 def _bn_reduce(lib, d, partial, count, what, invstd=None, dgamma=None, dbeta=None):

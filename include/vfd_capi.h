@@ -347,6 +347,21 @@ size_t vfd_pad_conv_fwd_bf16_workspace(const vfd_conv_desc* d);
 int vfd_pad_conv_fwd_bf16(const vfd_conv_desc* d, const float* x, const void* Wf, const float* bias, void* out,
                           void* workspace, size_t ws_bytes, void* stream);
 
+/* K2C data gradient (volumetric_fusionnet.py:59-60, 338-343 backward; replaces the cudnn / MIOpen
+ * backward-data of the pose reduce_dim[0]): dx [B, H, W, C] (the full reflect-padded map's gradient,
+ * channels-last, every position written) from g_pre [B, Ho, Wo, 256] (d pre-activation, NHWC) and Wd =
+ * the weight in the MAP's channel order as vfd_weight_fragments mode 2 with Cv = C1, D = Z (the pose
+ * map's z*C1 + c order; [9 flipped taps][64][np][2][2], np = C rounded up to 256).  Stride 2 by parity
+ * class (4 / 2 / 2 / 1 taps), stride-K over work units, fixed-order partial sums (deterministic).
+ * bf16: g_pre bf16, Wd = vfd_weight_fragments_bf16 mode 5 of that copy; dx fp32.
+ * Workspace 0 = shape unsupported. */
+size_t vfd_pad_conv_dgrad_workspace(const vfd_conv_desc* d);
+int vfd_pad_conv_dgrad(const vfd_conv_desc* d, const float* g_pre, const float* Wd, float* dx, void* workspace,
+                       size_t ws_bytes, void* stream);
+size_t vfd_pad_conv_dgrad_bf16_workspace(const vfd_conv_desc* d);
+int vfd_pad_conv_dgrad_bf16(const vfd_conv_desc* d, const void* g_pre, const void* Wd, float* dx, void* workspace,
+                            size_t ws_bytes, void* stream);
+
 /* K3C data gradient (volumetric_fusionnet.py:59-60, 265 backward): d of reduce_dim's first conv
  * w.r.t. its reflect-padded input, dx [B*N, h+2, w+2, D*Cv] (channel d*Cv + c: the layout
  * vfd_voxel_project_bwd_planned reads) from g_pre [B*N, h, w, O = 256] (d pre-activation, NHWC)
@@ -495,7 +510,7 @@ int vfd_upsample_ac_bwd(const float* g, float* dsrc, float* tmp, long long plane
  * recorded; vfd_prof_read_kernels: the same per kernel id into arrays of `count` entries.
  * Both reset the record. */
 #define VFD_PROF_ALL (-1)
-#define VFD_KERNEL_COUNT 27
+#define VFD_KERNEL_COUNT 32
 const char* vfd_kernel_name(int kernel_id);
 int vfd_prof_enable(int kernel_id);
 int vfd_prof_read(int* launches, double* total_ms);

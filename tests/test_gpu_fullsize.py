@@ -740,7 +740,17 @@ def test_pad_conv_bf16(shape):
     # gradients: fp32 on the bf16-rounded operands (straight through) with the kernel's own
     # LeakyReLU decisions (see test_proj_conv_bf16)
     g = torch.randn(y.shape, device=DEV, generator=gen)
-    (y.float() * g).sum().backward()
+    from vfdepth_amd import _lib as L
+    torch.cuda.synchronize()
+    L.prof_enable('pad_conv_dgrad')
+    try:
+        (y.float() * g).sum().backward()
+        torch.cuda.synchronize()
+        ran = L.prof_read()
+    finally:
+        L.prof_enable('off')
+    # the bf16 data gradient runs on the HIP path (no MIOpen backward-data in config 3's pose conv)
+    assert ran.get('pad_conv_dgrad', (0, 0))[0] == 1, f'bf16 K2C data gradient not on the HIP path {shape}'
     refs = [t.clone().requires_grad_(True) for t in (x, w, b)]
     xr = refs[0] + (refs[0].to(torch.bfloat16).float() - refs[0]).detach()
     wmr = KN.pose_conv_weight(refs[1], *perm) if perm else refs[1]
@@ -1417,3 +1427,42 @@ def test_proj_conv_dgrad_bf16_matches_conv_transpose(name, B, h, w, D):
     err = (dx[:, :, 1:h + 1, 1:w + 1] - ref).abs()
     bound = 2.0 ** -8 * mag + 1e-5 * float(ref.abs().max())
     assert bool((err <= bound).all()), f'bf16 folded K3C data gradient ({name}): max err/mag {float((err / (mag + 1e-12)).max()):.3g}'
+
+
+# (B, C, H, W, stride, perm): the pose reduce_dim[0] shapes of configs 2 / 3 / 5 (reference-order
+# weight, the map's z-major channels), odd sizes with a ragged channel tile, stride 1
+_PAD_DGRAD_SHAPES = [(1, 5140, 102, 102, 2, (257, 20)), (2, 5140, 102, 102, 2, (257, 20)),
+                     (4, 5140, 202, 202, 2, (257, 20)), (2, 20, 13, 11, 2, None), (1, 44, 9, 30, 1, None),
+                     (2, 1028, 22, 22, 2, None), (1, 36, 4, 5, 2, None)]
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize('bf16', [False, True])
+@pytest.mark.parametrize('shape', _PAD_DGRAD_SHAPES)
+def test_pad_conv_dgrad_matches_conv_transpose(shape, bf16):
+    """K2C's data gradient (padconv.hip ppd_main_k: parity-class tiles for stride 2, stream-K over
+    work units; volumetric_fusionnet.py:59-60, 338-343 backward) through the C ABI against
+    conv_transpose2d of the same operands (the map-order weight), every padded position (the
+    positions no output reads must come out exactly 0).  bf16: against the fp32 transpose of the
+    bf16-rounded operands, |err| <= 2^-8 * (the transpose of |G|, |W|) + 1e-5 max|ref|."""
+    from vfdepth_amd import kernels as KN
+    B, C, H, W, s, perm = shape
+    gen = torch.Generator(device=DEV).manual_seed(601)
+    ho, wo = (H - 3) // s + 1, (W - 3) // s + 1
+    g = torch.randn(B, 256, ho, wo, device=DEV, generator=gen).contiguous(memory_format=torch.channels_last)
+    w = torch.randn(256, C, 3, 3, device=DEV, generator=gen) * (256 * 9) ** -0.5
+    wm = KN.pose_conv_weight(w, *perm) if perm else w          # the map's channel order
+    gk = g.to(torch.bfloat16) if bf16 else g
+    dx = KN.pad_conv_dgrad(gk, (B, C, H, W), w, s, perm)
+    assert dx is not None, f'{shape}: unsupported'
+    op = (H - ((ho - 1) * s + 3), W - ((wo - 1) * s + 3))
+    if not bf16:
+        ref = F.conv_transpose2d(g.contiguous(), wm, stride=s, output_padding=op)
+        close(dx, ref, f'K2C data gradient {shape}', atol=1e-5, rtol=1e-4)
+        return
+    gr, wr = gk.float().contiguous(), wm.to(torch.bfloat16).float()
+    ref = F.conv_transpose2d(gr, wr, stride=s, output_padding=op)
+    mag = F.conv_transpose2d(gr.abs(), wr.abs(), stride=s, output_padding=op)
+    err = (dx - ref).abs()
+    bound = 2.0 ** -8 * mag + 1e-5 * float(ref.abs().max())
+    assert bool((err <= bound).all()), f'bf16 K2C data gradient {shape}: max err/mag {float((err / (mag + 1e-12)).max()):.3g}'

@@ -14,6 +14,7 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 SHAPES = {'c2': (1, 48, 80, 50), 'c3': (2, 48, 80, 50), 'c4': (1, 44, 80, 50), 'c5': (4, 80, 120, 50)}
+POSE = {'c2': (1, 102), 'c3': (2, 102), 'c4': (1, 102), 'c5': (4, 202)}     # (B, padded BEV side), C = 257 * 20
 PEAK = {'fp32': 157.3, 'bf16': 2516.6}
 
 
@@ -31,6 +32,11 @@ def main():
     dev = torch.device('cuda:0')
     space = KN.VoxelSpace(G.step_cfg(), dev)
     for sh in a.shapes.split(','):
+        pose_ops = [o for o in a.ops.split(',') if o.startswith('pdgrad')]
+        if pose_ops:
+            pose(lib, L, KN, dev, sh, pose_ops, a.iters)
+        if all(o.startswith('pdgrad') for o in a.ops.split(',')):
+            continue
         B, h, w, D = SHAPES[sh]
         N, Cv, O = 6, 64, 256
         d = space.desc(B, N, Cv=Cv, pad_out=2)
@@ -40,6 +46,8 @@ def main():
         dx = torch.empty(B * N, Cv * D, h + 2, w + 2, device=dev).contiguous(memory_format=torch.channels_last)
         flop = 2.0 * B * N * h * w * O * Cv * D * 9
         for op in a.ops.split(','):
+            if op.startswith('pdgrad'):
+                continue
             if op == 'dgrad':
                 wd, gp, kind = KN.proj_conv_dgrad_weight(w0, Cv, D), g_pre, 'fp32'
                 nb = lib.vfd_proj_conv_dgrad_workspace(ctypes.byref(d))
@@ -70,6 +78,49 @@ def main():
             us = ms / n * 1e3
             tf = flop / (us * 1e-6) / 1e12
             print(f'{sh} {op:11s} {us:9.1f} us  {tf:7.1f} TF/s  {tf / PEAK[kind]:.3f} of {kind} peak', flush=True)
+
+
+def pose(lib, L, KN, dev, sh, ops, iters):
+    """K2C (pose reduce_dim[0], stride 2) data gradient: the HIP kernel (fp32 / bf16) vs MIOpen's
+    backward-data of the same conv (fp32, torch events)."""
+    import torch.nn.functional as F
+    B, S = POSE[sh]
+    C, C1, Z = 5140, 257, 20
+    ho = (S - 3) // 2 + 1
+    g = torch.randn(B, 256, ho, ho, device=dev).contiguous(memory_format=torch.channels_last)
+    w = torch.randn(256, C, 3, 3, device=dev) * (256 * 9) ** -0.5
+    x = torch.randn(B, C, S, S, device=dev).contiguous(memory_format=torch.channels_last)
+    flop = 2.0 * B * ho * ho * 256 * C * 9
+    for op in ops:
+        if op == 'pdgrad_miopen':
+            wm = KN.pose_conv_weight(w, C1, Z).contiguous(memory_format=torch.channels_last)
+            fn = lambda: torch.ops.aten.convolution_backward(g, x, wm, [256], [2, 2], [0, 0], [1, 1], False, [0, 0], 1,
+                                                             [True, False, False])  # noqa: E731
+            for _ in range(2):
+                fn()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(iters):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            us, kind = e0.elapsed_time(e1) / iters * 1e3, 'fp32'
+        else:
+            gk = g.to(torch.bfloat16) if op == 'pdgrad_bf16' else g
+            kind = 'bf16' if op == 'pdgrad_bf16' else 'fp32'
+            for _ in range(2):
+                KN.pad_conv_dgrad(gk, x.shape, w, 2, (C1, Z))
+            torch.cuda.synchronize()
+            L.prof_enable('pad_conv_dgrad')
+            for _ in range(iters):
+                KN.pad_conv_dgrad(gk, x.shape, w, 2, (C1, Z))
+            torch.cuda.synchronize()
+            n, ms = L.prof_read()['pad_conv_dgrad']
+            L.prof_enable('off')
+            us = ms / n * 1e3
+        tf = flop / (us * 1e-6) / 1e12
+        print(f'{sh} pose {op:14s} {us:9.1f} us  {tf:7.1f} TF/s  {tf / PEAK[kind]:.3f} of {kind} peak', flush=True)
 
 
 if __name__ == '__main__':

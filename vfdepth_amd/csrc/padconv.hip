@@ -12,6 +12,8 @@
 // positions) into one half of a double-buffered LDS image while the compute waves run the
 // previous atom's 9 taps x 4 channel quads.  Split tiles are summed by `ppc_reduce_k` in
 // workgroup order (deterministic), which also applies the epilogue to every tile.
+#include <type_traits>
+
 #include "vfd_common.h"
 
 namespace vfd {
@@ -52,30 +54,32 @@ __device__ __forceinline__ PpTile pp_tile(const PpGeom& g, int t) {
 }
 
 // loader waves (tid 0..255): input rows s*ymin .. s*ymin + hrows - 1 (all Wp columns), channels
-// ch*16 .. ch*16 + 15 (zero past Cin)
+// ch*CC .. ch*CC + CC - 1 (zero past Cin)
+template <int CC>
 __device__ __forceinline__ void pp_stage(const PpGeom& g, float* __restrict__ dst, const float* __restrict__ x,
                                          int atom, int tid) {
+  constexpr int QP = CC / 4, PPP = 256 / QP, XS = CC + 4;
   const int t = atom / g.nchunk, ch = atom - t * g.nchunk;
   const PpTile tl = pp_tile(g, t);
   const int npos = g.hrows * g.wp;
-  const int q = tid & 3;
-  const int c = ch * PP_CC + 4 * q;
+  const int q = tid % QP;
+  const int c = ch * CC + 4 * q;
   const int r0 = g.s * tl.ymin;
   const float* src = x + ((size_t)tl.b * g.hp + r0) * g.wp * g.cin + c;
   const bool cok = c < g.cin;
-  for (int p0 = tid >> 2; p0 < npos; p0 += 4 * 64) {
+  for (int p0 = tid / QP; p0 < npos; p0 += 4 * PPP) {
     float4 v[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int p = p0 + 64 * u;
+      const int p = p0 + PPP * u;
       v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (cok && p < npos && r0 + p / g.wp < g.hp)
         v[u] = *reinterpret_cast<const float4*>(src + (size_t)p * g.cin);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int p = p0 + 64 * u;
-      if (p < npos) *reinterpret_cast<float4*>(dst + p * PP_XS + 4 * q) = v[u];
+      const int p = p0 + PPP * u;
+      if (p < npos) *reinterpret_cast<float4*>(dst + p * XS + 4 * q) = v[u];
     }
   }
 }
@@ -97,24 +101,27 @@ __device__ __forceinline__ void pp_store(const PpGeom& g, TO* __restrict__ out, 
 }
 
 // Weight layout Wf: [9 taps][cq = Cin_pad/4 quads][O][2 (h)][2 (s)], c = 4*quad + 2*h + s
-// (channels past Cin zero).
+// (channels past Cin zero).  CC = channels per atom: 16, or 8 where the staged rows of 16 do not
+// fit LDS (config 5's 202-wide BEV map).
+template <int CC>
 __global__ __launch_bounds__(PP_THREADS, 2) void ppc_main_k(PpGeom g, const float* __restrict__ x,
                                                            const float* __restrict__ Wf,
                                                            const float* __restrict__ bias,
                                                            float* __restrict__ out,
                                                            float* __restrict__ partial) {
+  constexpr int XS = CC + 4, ITERS = 9 * (CC / 4), PF = CC / 4 < PP_PF ? CC / 4 : PP_PF;
   extern __shared__ float pp_lds[];
   const int grp = blockIdx.x;
   const int a_lo = pp_lo(g, grp), a_hi = pp_lo(g, grp + 1);
   if (a_lo >= a_hi) return;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const bool compute = wv < PP_WAVES;
-  if (!compute) pp_stage(g, pp_lds, x, a_lo, threadIdx.x - 64 * PP_WAVES);
+  if (!compute) pp_stage<CC>(g, pp_lds, x, a_lo, threadIdx.x - 64 * PP_WAVES);
   __syncthreads();
   if (!compute) {
     for (int atom = a_lo; atom < a_hi; ++atom) {
       if (atom + 1 < a_hi)
-        pp_stage(g, pp_lds + ((atom + 1 - a_lo) & 1) * g.lds_floats, x, atom + 1, threadIdx.x - 64 * PP_WAVES);
+        pp_stage<CC>(g, pp_lds + ((atom + 1 - a_lo) & 1) * g.lds_floats, x, atom + 1, threadIdx.x - 64 * PP_WAVES);
       __syncthreads();
     }
     return;
@@ -128,20 +135,20 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppc_main_k(PpGeom g, const floa
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
   const float2* wlane = reinterpret_cast<const float2*>(Wf) + (size_t)(wv * 64 + li) * 2 + lh;
-  float2 bq[PP_PF][2];
+  float2 bq[PF][2];
   int pf_atom = a_lo, pf_it = 0;
   auto prefetch = [&](int slot) {
     if (pf_atom < a_hi) {
       const int ch = pf_atom % g.nchunk;
-      const int tap = pf_it >> 2, q = pf_it & 3;
-      const float2* w = wlane + (size_t)(tap * g.cq + ch * (PP_CC / 4) + q) * (2 * PP_O);
+      const int tap = pf_it / (CC / 4), q = pf_it % (CC / 4);
+      const float2* w = wlane + (size_t)(tap * g.cq + ch * (CC / 4) + q) * (2 * PP_O);
       bq[slot][0] = w[0];
       bq[slot][1] = w[64];
-      if (++pf_it == PP_ITERS) { pf_it = 0; ++pf_atom; }
+      if (++pf_it == ITERS) { pf_it = 0; ++pf_atom; }
     }
   };
 #pragma unroll
-  for (int k = 0; k < PP_PF; ++k) prefetch(k);
+  for (int k = 0; k < PF; ++k) prefetch(k);
   for (int atom = a_lo; atom < a_hi; ++atom) {
     const int t = atom / g.nchunk, ch = atom - t * g.nchunk;
     const PpTile tl = pp_tile(g, t);
@@ -151,7 +158,7 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppc_main_k(PpGeom g, const floa
       int m = tl.m0 + 32 * a + li;
       m = m < g.mimg ? m : g.mimg - 1;                 // pixels past the image: computed, never stored
       const int y = m / g.wo, xx = m - y * g.wo;
-      aoff[a] = (g.s * (y - tl.ymin) * g.wp + g.s * xx) * PP_XS + 2 * lh;
+      aoff[a] = (g.s * (y - tl.ymin) * g.wp + g.s * xx) * XS + 2 * lh;
     }
     const float* xb = pp_lds + ((atom - a_lo) & 1) * g.lds_floats;
     float2 afc[4], afn[4];
@@ -160,15 +167,15 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppc_main_k(PpGeom g, const floa
 #pragma unroll 1
     for (int tap = 0; tap < 9; ++tap) {
       const int ky = tap / 3, kx = tap - 3 * ky;
-      const float* xt = xb + (ky * g.wp + kx) * PP_XS;
+      const float* xt = xb + (ky * g.wp + kx) * XS;
       const int tn = tap + 1, kyn = tn / 3, kxn = tn - 3 * kyn;
-      const float* xn = xb + (kyn * g.wp + kxn) * PP_XS;
+      const float* xn = xb + (kyn * g.wp + kxn) * XS;
 #pragma unroll
-      for (int q = 0; q < PP_CC / 4; ++q) {
-        const int ring = q % PP_PF;
+      for (int q = 0; q < CC / 4; ++q) {
+        const int ring = q % PF;                      // (CC / 4) % PF == 0: static ring slots
         const float2 b0 = bq[ring][0], b1 = bq[ring][1];
         prefetch(ring);
-        if (q < PP_CC / 4 - 1) {
+        if (q < CC / 4 - 1) {
 #pragma unroll
           for (int a = 0; a < 4; ++a) afn[a] = *reinterpret_cast<const float2*>(&xt[aoff[a] + 4 * (q + 1)]);
         } else if (tap < 8) {
@@ -217,62 +224,65 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppc_main_k(PpGeom g, const floa
 // block ob holding W[32 ob + r][16 q + 8 h + j] (cpad = C rounded up to 32, zero past C).
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-constexpr int PPB_CC = 32;                      // input channels per atom
+constexpr int PPB_CC = 32;                      // input channels per atom (16 where 32 do not fit LDS)
 constexpr int PPB_XS = PPB_CC + 8;              // bf16 per staged position (80 B: 16-B aligned)
-constexpr int PPB_STEPS = 9 * (PPB_CC / 16);    // (tap, 16-channel) MFMA steps per atom
 constexpr int PPB_PF = 2;                       // weight-fragment prefetch distance (steps)
 
+template <int CC>
 __device__ __forceinline__ void ppb_stage(const PpGeom& g, __bf16* __restrict__ dst, const float* __restrict__ x,
                                           int atom, int tid) {
-  const int nchunk = (g.cin + PPB_CC - 1) / PPB_CC;
+  constexpr int QP = CC / 4, PPP = 256 / QP, XS = CC + 8;
+  const int nchunk = (g.cin + CC - 1) / CC;
   const int t = atom / nchunk, ch = atom - t * nchunk;
   const PpTile tl = pp_tile(g, t);
   const int npos = g.hrows * g.wp;
-  const int q = tid & 7;                        // channel quad of the 32-channel chunk
-  const int c = ch * PPB_CC + 4 * q;
+  const int q = tid % QP;                       // channel quad of the chunk
+  const int c = ch * CC + 4 * q;
   const int r0 = g.s * tl.ymin;
   const float* src = x + ((size_t)tl.b * g.hp + r0) * g.wp * g.cin + c;
   const bool cok = c < g.cin;                   // cin % 4 == 0: a quad is all in or all out
-  for (int p0 = tid >> 3; p0 < npos; p0 += 4 * 32) {
+  for (int p0 = tid / QP; p0 < npos; p0 += 4 * PPP) {
     float4 v[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int p = p0 + 32 * u;
+      const int p = p0 + PPP * u;
       v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (cok && p < npos && r0 + p / g.wp < g.hp)
         v[u] = *reinterpret_cast<const float4*>(src + (size_t)p * g.cin);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int p = p0 + 32 * u;
+      const int p = p0 + PPP * u;
       if (p < npos) {
         bf16x4 b;
         b[0] = (__bf16)v[u].x;
         b[1] = (__bf16)v[u].y;
         b[2] = (__bf16)v[u].z;
         b[3] = (__bf16)v[u].w;
-        *reinterpret_cast<bf16x4*>(dst + p * PPB_XS + 4 * q) = b;
+        *reinterpret_cast<bf16x4*>(dst + p * XS + 4 * q) = b;
       }
     }
   }
 }
 
+template <int CC>
 __global__ __launch_bounds__(PP_THREADS, 2) void ppcb_main_k(PpGeom g, const float* __restrict__ x,
                                                             const bf16x8* __restrict__ Wf,
                                                             float* __restrict__ partial) {
+  constexpr int XS = CC + 8, STEPS = 9 * (CC / 16), PF = CC / 16 < PPB_PF ? CC / 16 : PPB_PF;
   extern __shared__ __attribute__((aligned(16))) __bf16 ppb_lds[];
   const int grp = blockIdx.x;
   const int a_lo = pp_lo(g, grp), a_hi = pp_lo(g, grp + 1);
   if (a_lo >= a_hi) return;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const bool compute = wv < PP_WAVES;
-  const int lds_elems = g.hrows * g.wp * PPB_XS;
-  if (!compute) ppb_stage(g, ppb_lds, x, a_lo, threadIdx.x - 64 * PP_WAVES);
+  const int lds_elems = g.hrows * g.wp * XS;
+  if (!compute) ppb_stage<CC>(g, ppb_lds, x, a_lo, threadIdx.x - 64 * PP_WAVES);
   __syncthreads();
   if (!compute) {
     for (int atom = a_lo; atom < a_hi; ++atom) {
       if (atom + 1 < a_hi)
-        ppb_stage(g, ppb_lds + ((atom + 1 - a_lo) & 1) * lds_elems, x, atom + 1, threadIdx.x - 64 * PP_WAVES);
+        ppb_stage<CC>(g, ppb_lds + ((atom + 1 - a_lo) & 1) * lds_elems, x, atom + 1, threadIdx.x - 64 * PP_WAVES);
       __syncthreads();
     }
     return;
@@ -285,23 +295,23 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppcb_main_k(PpGeom g, const flo
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-  const int nchunk = g.nchunk;                  // 32-channel chunks (host-set for the bf16 form)
-  const int nq16 = nchunk * (PPB_CC / 16);
+  const int nchunk = g.nchunk;                  // CC-channel chunks (host-set for the bf16 form)
+  const int nq16 = (g.cin + 31) / 32 * 2;       // 16-channel steps per tap of the fragment copy (C to 32)
   const bf16x8* wlane = Wf + (size_t)(2 * wv) * 64 + lane;
-  bf16x8 bq[PPB_PF][2];
+  bf16x8 bq[PF][2];
   int pf_atom = a_lo, pf_it = 0;
   auto prefetch = [&](int slot) {
     if (pf_atom < a_hi) {
       const int ch = pf_atom % nchunk;
-      const int tap = pf_it >> 1, q = pf_it & 1;
-      const bf16x8* w = wlane + ((size_t)tap * nq16 + ch * (PPB_CC / 16) + q) * (PP_O / 32) * 64;
+      const int tap = pf_it / (CC / 16), q = pf_it % (CC / 16);
+      const bf16x8* w = wlane + ((size_t)tap * nq16 + ch * (CC / 16) + q) * (PP_O / 32) * 64;
       bq[slot][0] = w[0];
       bq[slot][1] = w[64];
-      if (++pf_it == PPB_STEPS) { pf_it = 0; ++pf_atom; }
+      if (++pf_it == STEPS) { pf_it = 0; ++pf_atom; }
     }
   };
 #pragma unroll
-  for (int k = 0; k < PPB_PF; ++k) prefetch(k);
+  for (int k = 0; k < PF; ++k) prefetch(k);
   for (int atom = a_lo; atom < a_hi; ++atom) {
     const int t = atom / nchunk, ch = atom - t * nchunk;
     const PpTile tl = pp_tile(g, t);
@@ -311,19 +321,19 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppcb_main_k(PpGeom g, const flo
       int m = tl.m0 + 32 * a + li;
       m = m < g.mimg ? m : g.mimg - 1;                 // pixels past the image: computed, never stored
       const int y = m / g.wo, xx = m - y * g.wo;
-      aoff[a] = (g.s * (y - tl.ymin) * g.wp + g.s * xx) * PPB_XS + 8 * lh;
+      aoff[a] = (g.s * (y - tl.ymin) * g.wp + g.s * xx) * XS + 8 * lh;
     }
     const __bf16* xb = ppb_lds + ((atom - a_lo) & 1) * lds_elems;
 #pragma unroll 1
     for (int tap = 0; tap < 9; ++tap) {
       const int ky = tap / 3, kx = tap - 3 * ky;
-      const __bf16* xt = xb + (ky * g.wp + kx) * PPB_XS;
+      const __bf16* xt = xb + (ky * g.wp + kx) * XS;
 #pragma unroll
-      for (int q = 0; q < PPB_CC / 16; ++q) {
+      for (int q = 0; q < CC / 16; ++q) {
         bf16x8 af[4];
 #pragma unroll
         for (int a = 0; a < 4; ++a) af[a] = *reinterpret_cast<const bf16x8*>(&xt[aoff[a] + 16 * q]);
-        const int ring = q % PPB_PF;
+        const int ring = q % PF;
         const bf16x8 b0 = bq[ring][0], b1 = bq[ring][1];
         prefetch(ring);
 #pragma unroll
@@ -418,13 +428,13 @@ static bool pp_plan(const vfd_conv_desc& d, PpGeom* out, int cc = PP_CC, int xs_
   g.mimg = g.ho * g.wo;
   g.mtiles = (g.mimg + PP_PIX - 1) / PP_PIX;
   g.nchunk = (d.C + cc - 1) / cc;
-  g.cq = g.nchunk * (cc / 4);
+  g.cq = (d.C + 15) / 16 * 4;            // channel quads per tap of the fp32 fragment copy (C rounded to 16)
   g.ntile = g.B * g.mtiles;
   g.natom = g.ntile * g.nchunk;
   // output rows under 128 consecutive pixels, and the input rows they read
   const int orows = 1 + (g.wo - 1 + PP_PIX - 1) / g.wo;
   g.hrows = g.s * (orows - 1) + 3;
-  g.lds_floats = g.hrows * g.wp * PP_XS;
+  g.lds_floats = g.hrows * g.wp * (xs_bytes / 4);
   if ((size_t)2 * g.hrows * g.wp * xs_bytes > PP_LDS_MAX) return false;
   // ranges of >= ceil(nchunk / (PP_MAXC - 2)) atoms keep a tile's contributors <= PP_MAXC - 1
   const int res = pp_resident();
@@ -436,15 +446,407 @@ static bool pp_plan(const vfd_conv_desc& d, PpGeom* out, int cc = PP_CC, int xs_
   return true;
 }
 
+// 16-byte vectors of G (fp32 4 channels, bf16 8), widened to fp32; put<T> rounds once to the LDS type
+template <typename TG>
+struct PgVecP;
+template <>
+struct PgVecP<float> {
+  static constexpr int CH = 4;
+  typedef float4 V;
+  static __device__ __forceinline__ V zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+  static __device__ __forceinline__ V load(const float* p) { return *reinterpret_cast<const float4*>(p); }
+  template <typename T>
+  static __device__ __forceinline__ void put(T* dst, const V& v) { st4(dst, v); }
+};
+template <>
+struct PgVecP<__bf16> {
+  static constexpr int CH = 8;
+  typedef bf16x8 V;
+  static __device__ __forceinline__ V zero() {
+    V z;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) z[e] = (__bf16)0.f;
+    return z;
+  }
+  static __device__ __forceinline__ V load(const __bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
+  template <typename T>
+  static __device__ __forceinline__ void put(T* dst, const V& v) {
+    static_assert(sizeof(T) == 2, "bf16 G staged as bf16");
+    *reinterpret_cast<bf16x8*>(dst) = v;
+  }
+};
+
+// =============================================================================================
+// K2C data gradient ("ppd"): d of the stride-s 3x3 conv w.r.t. its reflect-padded input map, the
+// backward of ppc_main_k (volumetric_fusionnet.py:59-60, 338-343; the reference's cudnn backward-data
+// of reduce_dim[0] under DDP):
+//
+//   dXp[b, Y, X, c] = sum_{ky, kx: Y = s y + ky, X = s x + kx} sum_o G[b, y, x, o] W[o, c, ky, kx]
+//
+// For stride 2 a padded position's taps depend on its parity class (Y % 2, X % 2): even rows take
+// ky in {0, 2} (G rows Y/2 and Y/2 - 1), odd rows ky = 1 (G row (Y-1)/2); columns alike — 4, 2, 2
+// and 1 taps.  Positions are tiled by class: a tile = 256 consecutive positions of one class grid
+// (class row i -> Y = 2i + py) of one image, so every pixel of a tile has the same tap list; M =
+// those positions, N = 128 map channels per tile (4 waves x 32), K = taps x O.  Atom = (tile,
+// OC-channel chunk of O), its trip count = taps x OC / (MFMA k); stream-K ranges are cut in WORK
+// units (an atom of a t-tap class costs t) so every workgroup gets the same MFMA count.  The loader
+// waves stage the G rows under the tile (rows i0 - 1 .. i1, columns -1 .. wo - 1, zero outside) for
+// the atom's chunk; compute waves as pcg (projconv.hip): 8 pixel blocks x one 32-channel block,
+// B fragments from the weight's data-gradient copy (vfd_weight_fragments mode 2 with Cv = C1,
+// D = Z over the map's channel order; bf16: mode 5 of it), PF steps ahead.  Stride 1 is the same
+// with one class of 9 taps.  Whole tiles are stored directly (every padded position belongs to
+// exactly one class, so dXp is written in full, zeros included); split tiles summed in group order
+// by ppd_reduce_k (deterministic).
+template <typename T>
+struct PdCfg;
+template <>
+struct PdCfg<float> {
+  static constexpr int OC = 16, XS = 20, STEPS = 4, PF = 4;   // o per atom, LDS elems / position, k-steps per tap,
+};                                                            // B prefetch distance (steps, <= STEPS)
+template <>
+struct PdCfg<__bf16> {
+  static constexpr int OC = 64, XS = 72, STEPS = 4, PF = 2;
+};
+
+constexpr int PD2_PIX = 256;                    // positions per tile (8 blocks of 32)
+constexpr int PD2_N = 128;                      // map channels per tile (4 waves x 32)
+constexpr int PD2_FRAG = PD2_PIX * PD2_N;
+
+struct PdcGeom {
+  int B, hp, wp, cin, ho, wo, s, np, ntn, och;
+  int nclass, py[4], px[4], hc[4], wc[4], tpc[4], ntap[4], ct_start[5], cu_start[5];
+  int tiles_nt, units_nt, ntile, natom, ngroup, hrows, cols, lds_elems;
+  long long units;
+};
+
+__host__ __device__ inline int pdc_class(const PdcGeom& g, int tl) {
+  int c = 0;
+  while (c + 1 < g.nclass && tl >= g.ct_start[c + 1]) ++c;
+  return c;
+}
+
+// first atom whose work-unit start is >= u
+__host__ __device__ inline int pdc_atom_at(const PdcGeom& g, long long u) {
+  if (u >= g.units) return g.natom;
+  const int nt = (int)(u / g.units_nt);
+  const int ru = (int)(u - (long long)nt * g.units_nt);
+  int c = 0;
+  while (c + 1 < g.nclass && ru >= g.cu_start[c + 1]) ++c;
+  const int k = (ru - g.cu_start[c] + g.ntap[c] - 1) / g.ntap[c];
+  return (nt * g.tiles_nt + g.ct_start[c]) * g.och + k;
+}
+
+__host__ __device__ inline int pdc_lo(const PdcGeom& g, int grp) {
+  return pdc_atom_at(g, (g.units * grp) / g.ngroup);
+}
+
+struct PdcTile {
+  int nt, c, b, m0, i0;
+};
+
+__device__ __forceinline__ PdcTile pdc_tile(const PdcGeom& g, int t) {
+  PdcTile r;
+  r.nt = t / g.tiles_nt;
+  const int tl = t - r.nt * g.tiles_nt;
+  r.c = pdc_class(g, tl);
+  const int k = tl - g.ct_start[r.c];
+  r.b = k / g.tpc[r.c];
+  r.m0 = (k - r.b * g.tpc[r.c]) * PD2_PIX;
+  r.i0 = r.m0 / g.wc[r.c];
+  return r;
+}
+
+// tap tl of class c -> (ky, kx); its G offset (dy, dx): G row = i - dy
+__device__ __forceinline__ void pdc_tap(const PdcGeom& g, int c, int tl, int* ky, int* kx) {
+  if (g.s == 1) {
+    *ky = tl / 3;
+    *kx = tl - 3 * *ky;
+    return;
+  }
+  const int nkx = g.px[c] ? 1 : 2;
+  const int a = tl / nkx, b = tl - a * nkx;
+  *ky = g.py[c] ? 1 : 2 * a;
+  *kx = g.px[c] ? 1 : 2 * b;
+}
+
+// loader waves (tid 0..255): staged row r = G row i0 - 1 + r (stride 1: i0 - 2 + r), staged column
+// c = G column c - 1 (stride 1: c - 2); channels ch * OC ..
+template <typename T, typename TG>
+__device__ __forceinline__ void pdc_stage(const PdcGeom& g, T* __restrict__ dst, const TG* __restrict__ gp, int atom,
+                                          int tid) {
+  typedef PgVecP<TG> PV;
+  constexpr int OC = PdCfg<T>::OC, XS = PdCfg<T>::XS, CH = PV::CH, QP = OC / CH, PPP = 256 / QP;
+  const int t = atom / g.och, ch = atom - t * g.och;
+  const PdcTile tl = pdc_tile(g, t);
+  const int r0 = tl.i0 - (g.s == 1 ? 2 : 1), c0 = g.s == 1 ? 2 : 1;
+  const int npos = g.hrows * g.cols;
+  const int q = tid % QP;
+  const TG* src = gp + (size_t)tl.b * g.ho * g.wo * PP_O + ch * OC + CH * q;
+  for (int p0 = tid / QP; p0 < npos; p0 += 8 * PPP) {
+    typename PV::V v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int p = p0 + PPP * u;
+      const int r = p / g.cols, c = p - r * g.cols;
+      const int y = r0 + r, x = c - c0;
+      v[u] = (p < npos && y >= 0 && y < g.ho && x >= 0 && x < g.wo) ? PV::load(src + ((size_t)y * g.wo + x) * PP_O)
+                                                                   : PV::zero();
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int p = p0 + PPP * u;
+      if (p < npos) PV::template put<T>(dst + p * XS + CH * q, v[u]);
+    }
+  }
+}
+
+template <typename T, typename TG>
+__global__ __launch_bounds__(PP_THREADS, 2) void ppd_main_k(PdcGeom g, const TG* __restrict__ gp,
+                                                           const void* __restrict__ Wd, float* __restrict__ dx,
+                                                           float* __restrict__ partial) {
+  constexpr int OC = PdCfg<T>::OC, XS = PdCfg<T>::XS, STEPS = PdCfg<T>::STEPS, PF = PdCfg<T>::PF;
+  static_assert(STEPS % PF == 0, "prefetch ring");
+  constexpr bool BF = sizeof(T) == 2;
+  typedef typename std::conditional<BF, bf16x8, float2>::type Frag;
+  extern __shared__ __attribute__((aligned(16))) unsigned char pd_raw[];
+  T* lds = reinterpret_cast<T*>(pd_raw);
+  const int grp = (g.ngroup % 8 == 0) ? (blockIdx.x % 8) * (g.ngroup / 8) + blockIdx.x / 8 : blockIdx.x;
+  const int a_lo = pdc_lo(g, grp), a_hi = pdc_lo(g, grp + 1);
+  if (a_lo >= a_hi) return;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const bool compute = wv < PP_WAVES;
+  if (!compute) pdc_stage<T, TG>(g, lds, gp, a_lo, threadIdx.x - 64 * PP_WAVES);
+  __syncthreads();
+  if (!compute) {
+    for (int atom = a_lo; atom < a_hi; ++atom) {
+      if (atom + 1 < a_hi)
+        pdc_stage<T, TG>(g, lds + ((atom + 1 - a_lo) & 1) * g.lds_elems, gp, atom + 1, threadIdx.x - 64 * PP_WAVES);
+      __syncthreads();
+    }
+    return;
+  }
+  const int li = lane & 31, lh = lane >> 5;
+  f32x16 acc[8];
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[a][r] = 0.f;
+  const Frag* wf = reinterpret_cast<const Frag*>(Wd);
+  // B fragment of (atom, tap tl, step q): the weight copy's tap slot 8 - (3 ky + kx)
+  auto bptr = [&](int atom, int tl) -> const Frag* {
+    const int t = atom / g.och, ch = atom - t * g.och;
+    const PdcTile tt = pdc_tile(g, t);
+    int ky, kx;
+    pdc_tap(g, tt.c, tl, &ky, &kx);
+    const int slot = 8 - (3 * ky + kx);
+    if constexpr (BF)
+      return wf + (((size_t)slot * (PP_O / 16) + ch * STEPS) * (g.np / 32) + tt.nt * (PD2_N / 32) + wv) * 64 + lane;
+    else
+      return wf + (((size_t)slot * (PP_O / 4) + ch * STEPS) * g.np + tt.nt * PD2_N + wv * 32 + li) * 2 + lh;
+  };
+  const size_t qstride = BF ? (size_t)(g.np / 32) * 64 : (size_t)g.np * 2;
+  Frag bq[PF];
+  const Frag* btap = bptr(a_lo, 0);                  // the current tap's fragments (step 0)
+#pragma unroll
+  for (int q = 0; q < PF; ++q) bq[q] = btap[q * qstride];
+  constexpr int LH = BF ? 8 : 2;
+  for (int atom = a_lo; atom < a_hi; ++atom) {
+    const int t = atom / g.och, ch = atom - t * g.och;
+    const PdcTile tl = pdc_tile(g, t);
+    const int hw = g.hc[tl.c] * g.wc[tl.c], wcc = g.wc[tl.c];
+    const int ntap = g.ntap[tl.c];
+    const int rbase = tl.i0 - (g.s == 1 ? 2 : 1), cbase = g.s == 1 ? 2 : 1;
+    int pij[8];                                       // (class row << 16) | class column of the lane's positions
+#pragma unroll
+    for (int a = 0; a < 8; ++a) {
+      int m = tl.m0 + 32 * a + li;
+      m = m < hw ? m : hw - 1;
+      const int i = m / wcc;
+      pij[a] = (i << 16) | (m - i * wcc);
+    }
+    const T* xb = lds + ((atom - a_lo) & 1) * g.lds_elems;
+    auto offsets = [&](int tp, int* o1) {
+      int ky, kx;
+      pdc_tap(g, tl.c, tp, &ky, &kx);
+      // G row of class row i at tap ky: stride 2: i - (ky == 2) (even rows) / i (odd rows, ky = 1);
+      // stride 1: Y - ky with Y = i (staged from row i0 - 2)
+      const int dy = g.s == 1 ? ky : (ky == 2 ? 1 : 0), dxo = g.s == 1 ? kx : (kx == 2 ? 1 : 0);
+#pragma unroll
+      for (int a = 0; a < 8; ++a) {
+        const int i = pij[a] >> 16, j = pij[a] & 0xFFFF;
+        o1[a] = ((i - dy - rbase) * g.cols + (j - dxo + cbase)) * XS + LH * lh;
+      }
+    };
+    int o1c[8];
+    offsets(0, o1c);
+    Frag afc[8], afn[8];
+#pragma unroll
+    for (int a = 0; a < 8; ++a) afc[a] = *reinterpret_cast<const Frag*>(&xb[o1c[a]]);
+    const bool more = atom + 1 < a_hi;
+#pragma unroll 1
+    for (int tp = 0; tp < ntap; ++tp) {
+      // refill pointer: this atom's next tap, or the next atom's first
+      const Frag* bn = tp + 1 < ntap ? bptr(atom, tp + 1) : (more ? bptr(atom + 1, 0) : nullptr);
+#pragma unroll
+      for (int q = 0; q < STEPS; ++q) {
+        const Frag b = bq[q % PF];
+        if (q + PF < STEPS)
+          bq[q % PF] = btap[(q + PF) * qstride];
+        else if (bn)
+          bq[q % PF] = bn[(q + PF - STEPS) * qstride];
+        if (q < STEPS - 1) {
+#pragma unroll
+          for (int a = 0; a < 8; ++a) afn[a] = *reinterpret_cast<const Frag*>(&xb[o1c[a] + (OC / STEPS) * (q + 1)]);
+        } else if (tp + 1 < ntap) {
+          offsets(tp + 1, o1c);
+#pragma unroll
+          for (int a = 0; a < 8; ++a) afn[a] = *reinterpret_cast<const Frag*>(&xb[o1c[a]]);
+        }
+        if constexpr (BF) {
+#pragma unroll
+          for (int a = 0; a < 8; ++a) acc[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afc[a], b, acc[a], 0, 0, 0);
+        } else {
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+            for (int a = 0; a < 8; ++a)
+              acc[a] = __builtin_amdgcn_mfma_f32_32x32x2f32(s2 ? afc[a].y : afc[a].x, s2 ? b.y : b.x, acc[a], 0, 0, 0);
+        }
+#pragma unroll
+        for (int a = 0; a < 8; ++a) afc[a] = afn[a];
+      }
+      btap = bn;
+    }
+    __syncthreads();                                  // buffer handed back to the loader waves
+    if (ch == g.och - 1 || atom == a_hi - 1) {
+      const int ts = t * g.och;
+      const int n = tl.nt * PD2_N + wv * 32 + li;
+      const int py = g.py[tl.c], px = g.px[tl.c], st = g.s;
+      if (ts >= a_lo && ts + g.och <= a_hi) {         // whole tile in this range: store
+#pragma unroll
+        for (int a = 0; a < 8; ++a)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = tl.m0 + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            if (m < hw && n < g.cin) {
+              const int i = m / wcc, j = m - i * wcc;
+              dx[(((size_t)tl.b * g.hp + st * i + py) * g.wp + st * j + px) * g.cin + n] = acc[a][r];
+            }
+            acc[a][r] = 0.f;
+          }
+      } else {
+        const int slot = t == a_lo / g.och ? 0 : 1;
+        float* dst = partial + ((size_t)grp * 2 + slot) * PD2_FRAG + (size_t)wv * (PD2_FRAG / PP_WAVES) + lane;
+#pragma unroll
+        for (int a = 0; a < 8; ++a)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            dst[(a * 16 + r) * 64] = acc[a][r];
+            acc[a][r] = 0.f;
+          }
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void ppd_reduce_k(PdcGeom g, const float* __restrict__ partial, float* __restrict__ dx) {
+  const int grp = blockIdx.x;
+  const int lo = pdc_lo(g, grp);
+  if (grp == 0 || lo % g.och == 0 || lo >= g.natom) return;
+  const int t = lo / g.och;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c0 = (grp - 1) * 2 + (t == pdc_lo(g, grp - 1) / g.och ? 0 : 1), c1 = grp * 2;
+  const PdcTile tl = pdc_tile(g, t);
+  const int hw = g.hc[tl.c] * g.wc[tl.c], wcc = g.wc[tl.c];
+  constexpr int FSL = 8, FPS = 8 * 16 / FSL, U = 4;
+  const int contrib[2] = {c0, c1};
+  const int n = tl.nt * PD2_N + wv * 32 + (lane & 31);
+  for (int fu = blockIdx.y * FPS; fu < (blockIdx.y + 1) * FPS; fu += U) {
+    float su[U];
+    frag_sums<U>(partial, contrib, 2, PD2_FRAG, (size_t)wv * (PD2_FRAG / PP_WAVES) + (fu * 64 + lane), su);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int f = fu + u;
+      const int a = f >> 4, r = f & 15;
+      const int m = tl.m0 + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (m < hw && n < g.cin) {
+        const int i = m / wcc, j = m - i * wcc;
+        dx[(((size_t)tl.b * g.hp + g.s * i + g.py[tl.c]) * g.wp + g.s * j + g.px[tl.c]) * g.cin + n] = su[u];
+      }
+    }
+  }
+}
+
+template <typename T>
+static bool pdc_plan(const vfd_conv_desc& d, PdcGeom* out) {
+  constexpr int OC = PdCfg<T>::OC, XS = PdCfg<T>::XS;
+  if (d.B <= 0 || d.C <= 0 || d.C % 4 || d.stride < 1 || d.stride > 2 || d.H < 3 || d.W < 3 || d.out_channels != PP_O)
+    return false;
+  PdcGeom g{};
+  g.B = d.B;
+  g.hp = d.H;
+  g.wp = d.W;
+  g.cin = d.C;
+  g.s = d.stride;
+  g.ho = (d.H - 3) / d.stride + 1;
+  g.wo = (d.W - 3) / d.stride + 1;
+  if (g.ho < 1 || g.wo < 1) return false;
+  g.np = (d.C + 255) / 256 * 256;
+  g.ntn = (d.C + PD2_N - 1) / PD2_N;
+  g.och = PP_O / OC;
+  g.nclass = d.stride == 2 ? 4 : 1;
+  int wmax = 0, rows_max = 0;
+  g.ct_start[0] = g.cu_start[0] = 0;
+  for (int c = 0; c < g.nclass; ++c) {
+    g.py[c] = d.stride == 2 ? c >> 1 : 0;
+    g.px[c] = d.stride == 2 ? c & 1 : 0;
+    g.hc[c] = d.stride == 2 ? (d.H - g.py[c] + 1) / 2 : d.H;
+    g.wc[c] = d.stride == 2 ? (d.W - g.px[c] + 1) / 2 : d.W;
+    g.tpc[c] = (g.hc[c] * g.wc[c] + PD2_PIX - 1) / PD2_PIX;
+    g.ntap[c] = d.stride == 2 ? (g.py[c] ? 1 : 2) * (g.px[c] ? 1 : 2) : 9;
+    g.ct_start[c + 1] = g.ct_start[c] + d.B * g.tpc[c];
+    g.cu_start[c + 1] = g.cu_start[c] + d.B * g.tpc[c] * g.och * g.ntap[c];
+    wmax = g.wc[c] > wmax ? g.wc[c] : wmax;
+    const int rows = (PD2_PIX - 1 + g.wc[c] - 1) / g.wc[c] + 1;
+    rows_max = (rows < g.hc[c] ? rows : g.hc[c]) > rows_max ? (rows < g.hc[c] ? rows : g.hc[c]) : rows_max;
+  }
+  g.tiles_nt = g.ct_start[g.nclass];
+  g.units_nt = g.cu_start[g.nclass];
+  g.ntile = g.ntn * g.tiles_nt;
+  g.natom = g.ntile * g.och;
+  g.units = (long long)g.ntn * g.units_nt;
+  // staged rows: stride 2 the tile's class rows + 1 above (ky = 2); stride 1 + 2 above
+  g.hrows = rows_max + (d.stride == 1 ? 2 : 1);
+  g.cols = wmax + (d.stride == 1 ? 2 : 1);
+  g.lds_elems = g.hrows * g.cols * XS;
+  if ((size_t)2 * g.lds_elems * sizeof(T) > PP_LDS_MAX) return false;
+  // groups: every range must hold >= och atoms (a split tile meets two groups) -> units per group
+  // >= max taps x och
+  const int res = pp_resident();
+  const long long most = g.units / (9LL * g.och);
+  g.ngroup = (int)(most < res ? (most > 0 ? most : 1) : res);
+  for (int k = 0; k < g.ngroup; ++k)
+    if (pdc_lo(g, k + 1) - pdc_lo(g, k) < g.och && pdc_lo(g, k + 1) < g.natom) return false;
+  *out = g;
+  return true;
+}
+
 }  // namespace vfd
 
 using namespace vfd;
 
 extern "C" {
 
+// channels per atom of the fp32 forward: 16, or 8 when 16 do not fit LDS
+static int pp_cc(const vfd_conv_desc& d, PpGeom* g) {
+  if (pp_plan(d, g)) return PP_CC;
+  if (pp_plan(d, g, 8, 12 * 4)) return 8;
+  return 0;
+}
+
 size_t vfd_pad_conv_fwd_workspace(const vfd_conv_desc* d) {
   PpGeom g;
-  if (!d || !pp_plan(*d, &g)) return 0;
+  if (!d || !pp_cc(*d, &g)) return 0;
   return ((size_t)g.ngroup * 2 + g.ntile) * PP_FRAG * sizeof(float);
 }
 
@@ -452,21 +854,35 @@ int vfd_pad_conv_fwd(const vfd_conv_desc* d, const float* x, const float* Wf, co
                      void* ws, size_t ws_bytes, void* stream) {
   VFD_REQUIRE(d && x && Wf && bias && out, "pad_conv_fwd: null argument");
   PpGeom g;
-  VFD_REQUIRE(pp_plan(*d, &g), "pad_conv_fwd: unsupported shape (C %% 4 == 0, stride 1 or 2, %d outputs, "
+  const int cc = pp_cc(*d, &g);
+  VFD_REQUIRE(cc, "pad_conv_fwd: unsupported shape (C %% 4 == 0, stride 1 or 2, %d outputs, "
               "input rows of a tile in LDS)", PP_O);
   VFD_REQUIRE(ws && ws_bytes >= vfd_pad_conv_fwd_workspace(d), "pad_conv_fwd: workspace too small");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_PAD_CONV_FWD, s);
-  lds_attr(reinterpret_cast<const void*>(ppc_main_k), PP_LDS_MAX);
   float* partial = (float*)ws;
-  ppc_main_k<<<g.ngroup, PP_THREADS, (size_t)2 * g.lds_floats * sizeof(float), s>>>(g, x, Wf, bias, out, partial);
+  if (cc == 8) {
+    lds_attr(reinterpret_cast<const void*>(ppc_main_k<8>), PP_LDS_MAX);
+    ppc_main_k<8><<<g.ngroup, PP_THREADS, (size_t)2 * g.lds_floats * sizeof(float), s>>>(g, x, Wf, bias, out, partial);
+  } else {
+    lds_attr(reinterpret_cast<const void*>(ppc_main_k<PP_CC>), PP_LDS_MAX);
+    ppc_main_k<PP_CC><<<g.ngroup, PP_THREADS, (size_t)2 * g.lds_floats * sizeof(float), s>>>(g, x, Wf, bias, out,
+                                                                                           partial);
+  }
   ppc_reduce_k<float><<<dim3(g.ntile, PP_FSL), 256, 0, s>>>(g, partial, bias, out);
   return fail_launch("pad_conv_fwd");
 }
 
+// channels per atom of the bf16 forward: 32, or 16 when 32 do not fit LDS
+static int ppb_cc(const vfd_conv_desc& d, PpGeom* g) {
+  if (pp_plan(d, g, PPB_CC, PPB_XS * 2)) return PPB_CC;
+  if (pp_plan(d, g, 16, 24 * 2)) return 16;
+  return 0;
+}
+
 size_t vfd_pad_conv_fwd_bf16_workspace(const vfd_conv_desc* d) {
   PpGeom g;
-  if (!d || !pp_plan(*d, &g, PPB_CC, PPB_XS * 2)) return 0;
+  if (!d || !ppb_cc(*d, &g)) return 0;
   return ((size_t)g.ngroup * 2 + g.ntile) * PP_FRAG * sizeof(float);
 }
 
@@ -474,17 +890,66 @@ int vfd_pad_conv_fwd_bf16(const vfd_conv_desc* d, const float* x, const void* Wf
                           void* ws, size_t ws_bytes, void* stream) {
   VFD_REQUIRE(d && x && Wf && bias && out, "pad_conv_fwd_bf16: null argument");
   PpGeom g;
-  VFD_REQUIRE(pp_plan(*d, &g, PPB_CC, PPB_XS * 2), "pad_conv_fwd_bf16: unsupported shape (C %% 4 == 0, stride 1 or 2, "
+  const int cc = ppb_cc(*d, &g);
+  VFD_REQUIRE(cc, "pad_conv_fwd_bf16: unsupported shape (C %% 4 == 0, stride 1 or 2, "
               "%d outputs, input rows of a tile in LDS)", PP_O);
   VFD_REQUIRE(ws && ws_bytes >= vfd_pad_conv_fwd_bf16_workspace(d), "pad_conv_fwd_bf16: workspace too small");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_PAD_CONV_FWD, s);
-  lds_attr(reinterpret_cast<const void*>(ppcb_main_k), PP_LDS_MAX);
   float* partial = (float*)ws;
-  const size_t lds = (size_t)2 * g.hrows * g.wp * PPB_XS * 2;
-  ppcb_main_k<<<g.ngroup, PP_THREADS, lds, s>>>(g, x, (const bf16x8*)Wf, partial);
+  const size_t lds = (size_t)2 * g.hrows * g.wp * (cc + 8) * 2;
+  if (cc == 16) {
+    lds_attr(reinterpret_cast<const void*>(ppcb_main_k<16>), PP_LDS_MAX);
+    ppcb_main_k<16><<<g.ngroup, PP_THREADS, lds, s>>>(g, x, (const bf16x8*)Wf, partial);
+  } else {
+    lds_attr(reinterpret_cast<const void*>(ppcb_main_k<PPB_CC>), PP_LDS_MAX);
+    ppcb_main_k<PPB_CC><<<g.ngroup, PP_THREADS, lds, s>>>(g, x, (const bf16x8*)Wf, partial);
+  }
   ppc_reduce_k<__bf16><<<dim3(g.ntile, PP_FSL), 256, 0, s>>>(g, partial, bias, (__bf16*)out);
   return fail_launch("pad_conv_fwd_bf16");
+}
+
+size_t vfd_pad_conv_dgrad_workspace(const vfd_conv_desc* d) {
+  PdcGeom g;
+  if (!d || !pdc_plan<float>(*d, &g)) return 0;
+  return (size_t)g.ngroup * 2 * PD2_FRAG * sizeof(float);
+}
+
+int vfd_pad_conv_dgrad(const vfd_conv_desc* d, const float* g_pre, const float* Wd, float* dx, void* ws,
+                       size_t ws_bytes, void* stream) {
+  VFD_REQUIRE(d && g_pre && Wd && dx, "pad_conv_dgrad: null argument");
+  PdcGeom g;
+  VFD_REQUIRE(pdc_plan<float>(*d, &g), "pad_conv_dgrad: unsupported shape (C %% 4 == 0, stride 1 or 2, %d outputs)", PP_O);
+  VFD_REQUIRE(ws && ws_bytes >= vfd_pad_conv_dgrad_workspace(d), "pad_conv_dgrad: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  ProfScope ps(K_PAD_CONV_DGRAD, s);
+  lds_attr(reinterpret_cast<const void*>(ppd_main_k<float, float>), PP_LDS_MAX);
+  ppd_main_k<float, float><<<g.ngroup, PP_THREADS, (size_t)2 * g.lds_elems * sizeof(float), s>>>(g, g_pre, Wd, dx,
+                                                                                                 (float*)ws);
+  ppd_reduce_k<<<dim3(g.ngroup, 8), 256, 0, s>>>(g, (const float*)ws, dx);
+  return fail_launch("pad_conv_dgrad");
+}
+
+size_t vfd_pad_conv_dgrad_bf16_workspace(const vfd_conv_desc* d) {
+  PdcGeom g;
+  if (!d || !pdc_plan<__bf16>(*d, &g)) return 0;
+  return (size_t)g.ngroup * 2 * PD2_FRAG * sizeof(float);
+}
+
+int vfd_pad_conv_dgrad_bf16(const vfd_conv_desc* d, const void* g_pre, const void* Wd, float* dx, void* ws,
+                            size_t ws_bytes, void* stream) {
+  VFD_REQUIRE(d && g_pre && Wd && dx, "pad_conv_dgrad_bf16: null argument");
+  PdcGeom g;
+  VFD_REQUIRE(pdc_plan<__bf16>(*d, &g), "pad_conv_dgrad_bf16: unsupported shape (C %% 4 == 0, stride 1 or 2, %d outputs)",
+              PP_O);
+  VFD_REQUIRE(ws && ws_bytes >= vfd_pad_conv_dgrad_bf16_workspace(d), "pad_conv_dgrad_bf16: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  ProfScope ps(K_PAD_CONV_DGRAD, s);
+  lds_attr(reinterpret_cast<const void*>(ppd_main_k<__bf16, __bf16>), PP_LDS_MAX);
+  ppd_main_k<__bf16, __bf16><<<g.ngroup, PP_THREADS, (size_t)2 * g.lds_elems * sizeof(__bf16), s>>>(
+      g, (const __bf16*)g_pre, Wd, dx, (float*)ws);
+  ppd_reduce_k<<<dim3(g.ngroup, 8), 256, 0, s>>>(g, (const float*)ws, dx);
+  return fail_launch("pad_conv_dgrad_bf16");
 }
 
 }  // extern "C"

@@ -462,6 +462,61 @@ def pad_conv_supported(x, stride, out_channels):
     return bool(L.load().vfd_pad_conv_fwd_workspace(ctypes.byref(pad_conv_desc(x, stride, out_channels))))
 
 
+# K2C data gradient on the HIP path: '1' (default) the bf16 form (config 3: 0.71 vs MIOpen's fp32
+# 1.91 ms per call at B = 2), 'all' the fp32 form too (slower than MIOpen's at configs 2 / 5: 1.09 vs
+# 0.91 ms, 15.9 vs 9.3 ms — profiles/r4/pdgrad_micro.txt), '0' never
+_PAD_DGRAD_ENV = os.environ.get('VFD_PAD_DGRAD', '1')
+_PAD_DGRAD = _PAD_DGRAD_ENV != '0'
+_PAD_DGRAD_FP32 = _PAD_DGRAD_ENV == 'all'
+_PDW_CACHE = {}
+
+
+def pad_conv_dgrad_weight(w, perm=None, bf16=False, cache=True):
+    """K2C weight [O, C, 3, 3] -> the data-gradient kernel's copy over the MAP's channel order:
+    mode 2 [9 flipped taps, O/4, np, 2, 2] with Cv = C1, D = Z (perm = (C1, Z): reference channel
+    c*Z + z at map channel z*C1 + c) or Cv = C, D = 1; bf16: mode 5 of it.  Cached per (tensor,
+    version): the step's two pose calls share one copy (padconv.hip ppd_main_k)."""
+    lib = L.load()
+    w = _dev(w.detach(), 'pad_conv weight')
+    O, C = w.shape[:2]
+    Cv, D = perm if perm else (C, 1)
+    key = (w.data_ptr(), w._version, tuple(w.shape), Cv, D, bf16)
+    if cache and key in _PDW_CACHE:
+        return _PDW_CACHE[key]
+    npad = (C + 255) // 256 * 256
+    f2 = torch.empty(9, O // 4, npad, 2, 2, device=w.device)
+    L.check(lib.vfd_weight_fragments(2, w.data_ptr(), f2.data_ptr(), O, 0, 0, 0, Cv, D, L.stream()),
+            'weight_fragments')
+    out = f2
+    if bf16:
+        out = torch.empty(9, O // 16, npad // 32, 64, 8, dtype=torch.bfloat16, device=w.device)
+        L.check(lib.vfd_weight_fragments_bf16(5, f2.data_ptr(), out.data_ptr(), O, 0, 0, 0, Cv, D, L.stream()),
+                'weight_fragments_bf16')
+    if cache:
+        _PDW_CACHE.clear()
+        _PDW_CACHE[key] = out
+    return out
+
+
+def pad_conv_dgrad(g_pre, x_shape, w, stride, perm=None):
+    """K2C's data gradient through the C ABI: g_pre [B, 256, Ho, Wo] channels-last (fp32 or bf16) ->
+    d x [B, C, H, W] channels-last fp32 (every padded position written); None when unsupported."""
+    lib = L.load()
+    B, C, H, W = x_shape
+    d = L.ConvDesc(B, H, W, C, stride, g_pre.shape[1])
+    bf16 = g_pre.dtype == torch.bfloat16
+    nbytes = (lib.vfd_pad_conv_dgrad_bf16_workspace if bf16 else lib.vfd_pad_conv_dgrad_workspace)(ctypes.byref(d))
+    if not nbytes:
+        return None
+    wd = pad_conv_dgrad_weight(w, perm, bf16)
+    dx = torch.empty(B, C, H, W, device=g_pre.device, memory_format=torch.channels_last)
+    ws = _ws(nbytes, g_pre.device)
+    fn = lib.vfd_pad_conv_dgrad_bf16 if bf16 else lib.vfd_pad_conv_dgrad
+    L.check(fn(ctypes.byref(d), g_pre.data_ptr(), wd.data_ptr(), dx.data_ptr(), ws.data_ptr(), nbytes, L.stream()),
+            'pad_conv_dgrad')
+    return dx
+
+
 class PadConv(torch.autograd.Function):
     """K2C: reflect-padded channels-last map x [B, C, H, W] -> LeakyReLU(conv3x3_stride(x) + bias)
     as the reflect-padded channels-last input of the next reflect conv, logical
@@ -497,11 +552,19 @@ class PadConv(torch.autograd.Function):
         g_pre = lrelu_pad_backward(g, out)
         mask = [ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]]
         s = ctx.stride
+        dx = None
+        if mask[0] and _PAD_DGRAD_FP32:
+            # the data gradient on fp32 MFMA (padconv.hip ppd_main_k), straight from the
+            # reference-order weight (opt-in: MIOpen's is faster at these shapes)
+            dx = pad_conv_dgrad(g_pre, x.shape, w, s, ctx.perm)
+            mask[0] = dx is None
         if ctx.perm:        # MIOpen works in the map's channel order (channels-last like x): swap
             C1, Z = ctx.perm  # in, and the gradient back to the reference order (NCHW)
             w = weight_swap(w, C1, Z, cache=True, memory_format=torch.channels_last)
-        dx, dw, db = torch.ops.aten.convolution_backward(g_pre, x, w, [w.shape[0]], [s, s], [0, 0], [1, 1],
-                                                         False, [0, 0], 1, mask)
+        dx2, dw, db = torch.ops.aten.convolution_backward(g_pre, x, w, [w.shape[0]], [s, s], [0, 0], [1, 1],
+                                                          False, [0, 0], 1, mask) if any(mask) else (None,) * 3
+        if dx is None:
+            dx = dx2
         if ctx.perm and dw is not None:
             dw = weight_swap(dw, Z, C1)
         return dx, dw, db, None, None, None
@@ -558,24 +621,32 @@ class PadConvBF16(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         x, w, out = ctx.saved_tensors
-        g32 = lrelu_pad_backward(g.float(), out.float())
         mask = [ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]]
         s = ctx.stride
-        wd = w.detach()
-        if ctx.perm:        # MIOpen works in the map's channel order (channels-last like x)
-            C1, Z = ctx.perm
-            wd = weight_swap(wd, C1, Z, cache=True, memory_format=torch.channels_last)
+        # d pre-activation (LeakyReLU + pad adjoint in fp32, sign from the bf16 output) rounded once
+        # to bf16: the operand of both gradients
+        gb = lrelu_pad_backward(g.to(torch.bfloat16), out, dtype=torch.bfloat16)
         cb = torch.ops.aten.convolution_backward
         args = ([w.shape[0]], [s, s], [0, 0], [1, 1], False, [0, 0], 1)
         dx = dw = db = None
-        if mask[0]:
-            # the map's gradient in fp32 from the fp32 pre-activation gradient: MIOpen's bf16 data
-            # gradient of this shape accumulates in an fp32 workspace and then casts it to bf16
-            # (which the fp32 map's gradient would cast back) — 1.6 ms vs ~1.2 ms per call at config 3
+        if mask[0] and _PC_BF16_BWD and _PAD_DGRAD:
+            # the bf16 data gradient (padconv.hip ppd_main_k<bf16>: bf16 operands, fp32 accumulation
+            # and output — the fp32 map's gradient, as autocast's bf16 conv gradient cast back)
+            dx = pad_conv_dgrad(gb, x.shape, w, s, ctx.perm)
+        wd = None
+        if (mask[0] and dx is None) or mask[1] or mask[2]:
+            wd = w.detach()
+            if ctx.perm:    # MIOpen works in the map's channel order (channels-last like x)
+                C1, Z = ctx.perm
+                wd = weight_swap(wd, C1, Z, cache=True, memory_format=torch.channels_last)
+        if mask[0] and dx is None:
+            # MIOpen's data gradient in fp32 from the fp32 pre-activation gradient (its bf16 data
+            # gradient of this shape accumulates in an fp32 workspace and then casts to bf16, which
+            # the fp32 map's gradient would cast back)
+            g32 = lrelu_pad_backward(g.float(), out.float())
             dx = cb(g32, x, wd, *args, [True, False, False])[0]
         if mask[1] or mask[2]:
-            _, dw, db = cb(g32.to(torch.bfloat16), x.to(torch.bfloat16), wd.to(torch.bfloat16), *args,
-                           [False, mask[1], mask[2]])
+            _, dw, db = cb(gb, x.to(torch.bfloat16), wd.to(torch.bfloat16), *args, [False, mask[1], mask[2]])
         if dw is not None:
             dw = dw.float()
             if ctx.perm:

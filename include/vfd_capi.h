@@ -384,6 +384,19 @@ size_t vfd_proj_conv_dgrad_bf16_workspace(const vfd_voxel_desc* d);
 int vfd_proj_conv_dgrad_bf16(const vfd_voxel_desc* d, const void* g_pre, const void* Wd, float* dx, void* workspace,
                              size_t ws_bytes, void* stream);
 
+/* bf16 weight / bias gradients (config 3; MIOpen's bf16 weight gradient before): K3C from g_pre bf16
+ * [B*N, h, w, O] and the bf16 frustum side output x [B*N, h+2, w+2, D*Cv] into dw [O, Cv*D, 3, 3] fp32
+ * in the reference channel order c*D + d; K2C from g_pre bf16 [B, Ho, Wo, 256] and the fp32 padded BEV
+ * map x [B, H, W, C] (rounded to bf16 as staged) into dw_map [256, C, 3, 3] fp32 in the MAP's channel
+ * order (the caller swaps it to the reference's c*Z + z).  db [O] fp32 (nullable, as dw).
+ * v_mfma_f32_32x32x16_bf16 on transposed LDS reads, stream-K, fixed-order sums (deterministic). */
+size_t vfd_proj_conv_wgrad_bf16_workspace(const vfd_voxel_desc* d);
+int vfd_proj_conv_wgrad_bf16(const vfd_voxel_desc* d, const void* g_pre, const void* x, float* dw, float* db,
+                             void* workspace, size_t ws_bytes, void* stream);
+size_t vfd_pad_conv_wgrad_bf16_workspace(const vfd_conv_desc* d);
+int vfd_pad_conv_wgrad_bf16(const vfd_conv_desc* d, const void* g_pre, const float* x, float* dw_map, float* db,
+                            void* workspace, size_t ws_bytes, void* stream);
+
 /* K3C weight / bias gradient (volumetric_fusionnet.py:59-60, 265 backward; replaces the
  * reference's cudnn weight-gradient of reduce_dim[0]): dw [O = 256, Cv*D, 3, 3] in the reference
  * channel order c*D + d, db [O], from g_pre [B*N, h, w, O] (NHWC) and the frustum features x
@@ -510,7 +523,7 @@ int vfd_upsample_ac_bwd(const float* g, float* dsrc, float* tmp, long long plane
  * recorded; vfd_prof_read_kernels: the same per kernel id into arrays of `count` entries.
  * Both reset the record. */
 #define VFD_PROF_ALL (-1)
-#define VFD_KERNEL_COUNT 32
+#define VFD_KERNEL_COUNT 33
 const char* vfd_kernel_name(int kernel_id);
 int vfd_prof_enable(int kernel_id);
 int vfd_prof_read(int* launches, double* total_ms);

@@ -76,7 +76,9 @@ def bn_layer_checks(rank, world):
                 bn.running_mean.copy_(rmean.float())
             xh = x[half].to(dt).to(DEV).contiguous(memory_format=fmt).requires_grad_(True)
             rh = r[half].to(dt).to(DEV).contiguous(memory_format=fmt).requires_grad_(True) if res else None
-            y = bn_act(bn, xh, rh, relu)
+            # bf16 maps take the fused path under config 3's bf16 autocast (layers._fused_dtype_ok)
+            with torch.autocast('cuda', dtype=torch.bfloat16, enabled=bf):
+                y = bn_act(bn, xh, rh, relu)
             assert y.grad_fn is not None and 'BatchNormAct' in type(y.grad_fn).__name__, type(y.grad_fn).__name__
             assert y.is_contiguous(memory_format=fmt) and y.dtype == dt
             (y.float() * g[half].to(dt).float().to(DEV)).sum().backward()

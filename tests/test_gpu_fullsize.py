@@ -1466,3 +1466,66 @@ def test_pad_conv_dgrad_matches_conv_transpose(shape, bf16):
     err = (dx - ref).abs()
     bound = 2.0 ** -8 * mag + 1e-5 * float(ref.abs().max())
     assert bool((err <= bound).all()), f'bf16 K2C data gradient {shape}: max err/mag {float((err / (mag + 1e-12)).max()):.3g}'
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize('kind,B,h,w,D', [('k3c', 2, 48, 80, 50), ('k3c', 1, 12, 20, 16), ('k3c', 1, 7, 5, 3)])
+def test_proj_conv_wgrad_bf16_matches_conv(kind, B, h, w, D):
+    """K3C's bf16 weight / bias gradient (projconv.hip pwb_main_k: bf16 operands by transposed LDS
+    reads, v_mfma_f32_32x32x16_bf16, fp32 partial sums in a fixed order) through the C ABI against the
+    fp32 gradient of the same conv on the bf16 operands (MIOpen), in the reference channel order c*D + d;
+    config 3's shape (B = 2) and small / ragged tiles.  |err| <= 1e-4 * (the gradient of |G|, |X|)."""
+    import ctypes
+    from vfdepth_amd import _lib as L
+    from vfdepth_amd import kernels as KN
+    space = KN.VoxelSpace(G.step_cfg(), DEV)
+    N, Cv, O = 6, 64, 256
+    d = space.desc(B, N, Cv=Cv)
+    d.h, d.w, d.D = h, w, D
+    gen = torch.Generator(device=DEV).manual_seed(701)
+    gb = torch.randn(B * N, O, h, w, device=DEV, generator=gen).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    xb = torch.randn(B * N, Cv * D, h + 2, w + 2, device=DEV, generator=gen).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    lib = L.load()
+    nbytes = lib.vfd_proj_conv_wgrad_bf16_workspace(ctypes.byref(d))
+    assert nbytes
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=DEV)
+    dw = torch.empty(O, Cv * D, 3, 3, device=DEV)
+    db = torch.empty(O, device=DEV)
+    L.check(lib.vfd_proj_conv_wgrad_bf16(ctypes.byref(d), gb.data_ptr(), xb.data_ptr(), dw.data_ptr(), db.data_ptr(),
+                                         ws.data_ptr(), nbytes, L.stream()), 'proj_conv_wgrad_bf16')
+    gf, xf = gb.float(), xb.float()
+    wshape = [O, Cv * D, 3, 3]
+    cb = torch.ops.aten.convolution_backward
+    args = ([O], [1, 1], [0, 0], [1, 1], False, [0, 0], 1, [False, True, True])
+    _, ref, rb = cb(gf, xf, torch.empty(wshape, device=DEV), *args)
+    _, mag, _ = cb(gf.abs(), xf.abs(), torch.empty(wshape, device=DEV), *args)
+    # kernel channel order n = d*Cv + c (the frustum features) -> the reference's c*D + d
+    ref, mag = KN.weight_swap(ref, D, Cv), KN.weight_swap(mag, D, Cv)
+    err = (dw - ref).abs()
+    assert bool((err <= 1e-4 * mag + 1e-6).all()), f'bf16 K3C d weight: max err/mag {float((err / (mag + 1e-12)).max()):.3g}'
+    close(db, rb, f'bf16 K3C d bias {kind}', atol=1e-3, rtol=1e-4)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize('shape', [(2, 5140, 102, 102, 2), (1, 40, 13, 11, 2), (1, 48, 9, 30, 1), (4, 5140, 202, 202, 2)])
+def test_pad_conv_wgrad_bf16_matches_conv(shape):
+    """K2C's bf16 weight / bias gradient (pwb_main_k at stride 2 / 1: the fp32 map rounded to bf16 as
+    it is staged) through the C ABI against the fp32 gradient of the same conv on the bf16-rounded
+    operands, in the map's channel order; config 3's and config 5's pose shapes, ragged tiles."""
+    from vfdepth_amd import kernels as KN
+    B, C, H, W, s = shape
+    gen = torch.Generator(device=DEV).manual_seed(702)
+    ho, wo = (H - 3) // s + 1, (W - 3) // s + 1
+    gb = torch.randn(B, 256, ho, wo, device=DEV, generator=gen).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x = torch.randn(B, C, H, W, device=DEV, generator=gen).contiguous(memory_format=torch.channels_last)
+    w = torch.empty(256, C, 3, 3, device=DEV)
+    dw, db = KN.pad_conv_wgrad_bf16(gb, x, w, s)
+    gf, xf = gb.float(), x.to(torch.bfloat16).float()
+    cb = torch.ops.aten.convolution_backward
+    args = ([256], [s, s], [0, 0], [1, 1], False, [0, 0], 1, [False, True, True])
+    _, ref, rb = cb(gf, xf, w, *args)
+    _, mag, _ = cb(gf.abs(), xf.abs(), w, *args)
+    err = (dw - ref).abs()
+    assert bool((err <= 1e-4 * mag + 1e-6).all()), f'bf16 K2C d weight {shape}: max err/mag {float((err / (mag + 1e-12)).max()):.3g}'
+    close(db, rb, f'bf16 K2C d bias {shape}', atol=1e-3, rtol=1e-4)

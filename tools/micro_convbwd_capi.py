@@ -32,10 +32,10 @@ def main():
     dev = torch.device('cuda:0')
     space = KN.VoxelSpace(G.step_cfg(), dev)
     for sh in a.shapes.split(','):
-        pose_ops = [o for o in a.ops.split(',') if o.startswith('pdgrad')]
+        pose_ops = [o for o in a.ops.split(',') if o.startswith(('pdgrad', 'pwgrad'))]
         if pose_ops:
             pose(lib, L, KN, dev, sh, pose_ops, a.iters)
-        if all(o.startswith('pdgrad') for o in a.ops.split(',')):
+        if all(o.startswith(('pdgrad', 'pwgrad')) for o in a.ops.split(',')):
             continue
         B, h, w, D = SHAPES[sh]
         N, Cv, O = 6, 64, 256
@@ -46,12 +46,15 @@ def main():
         dx = torch.empty(B * N, Cv * D, h + 2, w + 2, device=dev).contiguous(memory_format=torch.channels_last)
         flop = 2.0 * B * N * h * w * O * Cv * D * 9
         for op in a.ops.split(','):
-            if op.startswith('pdgrad'):
+            if op.startswith(('pdgrad', 'pwgrad')):
                 continue
             if op == 'dgrad':
                 wd, gp, kind = KN.proj_conv_dgrad_weight(w0, Cv, D), g_pre, 'fp32'
                 nb = lib.vfd_proj_conv_dgrad_workspace(ctypes.byref(d))
                 fn = lib.vfd_proj_conv_dgrad
+            elif op in ('wgrad_bf16', 'wgrad_bf16_miopen'):
+                time_wgrad(lib, L, KN, dev, d, sh, B, N, h, w, D, op, a.iters)
+                continue
             elif op == 'dgrad_bf16':
                 wd, gp, kind = KN.proj_conv_dgrad_weight_bf16(w0, Cv, D), g_pre.to(torch.bfloat16), 'bf16'
                 nb = lib.vfd_proj_conv_dgrad_bf16_workspace(ctypes.byref(d))
@@ -80,6 +83,45 @@ def main():
             print(f'{sh} {op:11s} {us:9.1f} us  {tf:7.1f} TF/s  {tf / PEAK[kind]:.3f} of {kind} peak', flush=True)
 
 
+def _events(fn, iters):
+    for _ in range(2):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e3
+
+
+def time_wgrad(lib, L, KN, dev, d, sh, B, N, h, w, D, op, iters):
+    """K3C bf16 weight + bias gradient: the HIP kernel vs MIOpen's bf16 wrw of the same conv."""
+    Cv, O = 64, 256
+    gb = torch.randn(B * N, O, h, w, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    xb = torch.randn(B * N, Cv * D, h + 2, w + 2, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    flop = 2.0 * B * N * h * w * O * Cv * D * 9
+    if op == 'wgrad_bf16':
+        nb = lib.vfd_proj_conv_wgrad_bf16_workspace(ctypes.byref(d))
+        ws = torch.empty(nb, dtype=torch.uint8, device=dev)
+        dw = torch.empty(O, Cv * D, 3, 3, device=dev)
+        db = torch.empty(O, device=dev)
+
+        def call():
+            L.check(lib.vfd_proj_conv_wgrad_bf16(ctypes.byref(d), gb.data_ptr(), xb.data_ptr(), dw.data_ptr(),
+                                                 db.data_ptr(), ws.data_ptr(), nb, L.stream()), op)
+    else:
+        wb = torch.empty(O, Cv * D, 3, 3, device=dev, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+
+        def call():
+            torch.ops.aten.convolution_backward(gb, xb, wb, [O], [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
+                                                [False, True, True])
+    us = _events(call, iters)
+    tf = flop / (us * 1e-6) / 1e12
+    print(f'{sh} {op:17s} {us:9.1f} us  {tf:7.1f} TF/s  {tf / PEAK["bf16"]:.3f} of bf16 peak', flush=True)
+
+
 def pose(lib, L, KN, dev, sh, ops, iters):
     """K2C (pose reduce_dim[0], stride 2) data gradient: the HIP kernel (fp32 / bf16) vs MIOpen's
     backward-data of the same conv (fp32, torch events)."""
@@ -92,6 +134,18 @@ def pose(lib, L, KN, dev, sh, ops, iters):
     x = torch.randn(B, C, S, S, device=dev).contiguous(memory_format=torch.channels_last)
     flop = 2.0 * B * ho * ho * 256 * C * 9
     for op in ops:
+        if op in ('pwgrad_bf16', 'pwgrad_bf16_miopen'):
+            gb = g.to(torch.bfloat16)
+            if op == 'pwgrad_bf16':
+                call = lambda: KN.pad_conv_wgrad_bf16(gb, x, w, 2)  # noqa: E731
+            else:
+                wm = KN.pose_conv_weight(w, C1, Z).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+                call = lambda: torch.ops.aten.convolution_backward(gb, x.to(torch.bfloat16), wm, [256], [2, 2], [0, 0],  # noqa: E731
+                                                                   [1, 1], False, [0, 0], 1, [False, True, True])
+            us = _events(call, iters)
+            tf = flop / (us * 1e-6) / 1e12
+            print(f'{sh} pose {op:18s} {us:9.1f} us  {tf:7.1f} TF/s  {tf / PEAK["bf16"]:.3f} of bf16 peak', flush=True)
+            continue
         if op == 'pdgrad_miopen':
             wm = KN.pose_conv_weight(w, C1, Z).contiguous(memory_format=torch.channels_last)
             fn = lambda: torch.ops.aten.convolution_backward(g, x, wm, [256], [2, 2], [0, 0], [1, 1], False, [0, 0], 1,

@@ -88,6 +88,10 @@ _SIGS = {
     'vfd_proj_conv_dgrad': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 4 + [c_size_t, c_void_p]),
     'vfd_proj_conv_dgrad_bf16_workspace': (c_size_t, [ctypes.POINTER(VoxelDesc)]),
     'vfd_proj_conv_dgrad_bf16': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 4 + [c_size_t, c_void_p]),
+    'vfd_proj_conv_wgrad_bf16_workspace': (c_size_t, [ctypes.POINTER(VoxelDesc)]),
+    'vfd_proj_conv_wgrad_bf16': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 5 + [c_size_t, c_void_p]),
+    'vfd_pad_conv_wgrad_bf16_workspace': (c_size_t, [ctypes.POINTER(ConvDesc)]),
+    'vfd_pad_conv_wgrad_bf16': (c_int, [ctypes.POINTER(ConvDesc)] + [c_fp] * 5 + [c_size_t, c_void_p]),
     'vfd_proj_conv_wgrad_workspace': (c_size_t, [ctypes.POINTER(VoxelDesc)]),
     'vfd_proj_conv_wgrad': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 5 + [c_size_t, c_void_p]),
     'vfd_bn_splits': (c_int, [ctypes.POINTER(BnDesc)]),
@@ -186,7 +190,7 @@ KERNEL_IDS = {
     'voxel_project_fwd': 5, 'voxel_project_bwd': 6, 'view_stats': 7, 'view_apply': 8, 'view_bwd': 9,
     'photo_fwd': 10, 'photo_bwd': 11, 'smooth_fwd': 12, 'smooth_bwd': 13, 'fusion_plan': 14,
     'aggregate': 15, 'voxel_project_plan': 16, 'proj_conv_fwd': 17,
-    'depth_syn_fwd': 18, 'depth_syn_bwd': 19, 'proj_conv_dgrad': 20, 'pad_conv_fwd': 21, 'bn_fwd': 22, 'bn_bwd': 23, 'reflect_pad': 24, 'upsample_bwd': 25, 'maxpool': 26, 'elu_pad': 27, 'disp_conv': 28, 'dec_conv': 29, 'proj_conv_wgrad': 30, 'pad_conv_dgrad': 31,
+    'depth_syn_fwd': 18, 'depth_syn_bwd': 19, 'proj_conv_dgrad': 20, 'pad_conv_fwd': 21, 'bn_fwd': 22, 'bn_bwd': 23, 'reflect_pad': 24, 'upsample_bwd': 25, 'maxpool': 26, 'elu_pad': 27, 'disp_conv': 28, 'dec_conv': 29, 'proj_conv_wgrad': 30, 'pad_conv_dgrad': 31, 'pad_conv_wgrad': 32,
 }
 
 

@@ -2015,6 +2015,265 @@ static bool pw_supported(const vfd_voxel_desc& d) {
   return range > 0 && (g.L + range - 1) / range + 1 <= PW_MAXC;   // workgroups meeting one tile
 }
 
+// =============================================================================================
+// bf16 weight / bias gradient of a 3x3 conv (stride 1 or 2) on MFMA — K3C's reduce_dim[0] (stride 1,
+// the bf16 frustum side output) and K2C's pose reduce_dim[0] (stride 2, the fp32 BEV map rounded to
+// bf16 as it is staged) under config 3's autocast (volumetric_fusionnet.py:59-60, 105-114, 265,
+// 338-343 backward; MIOpen's bf16 weight gradient before):
+//
+//   dW[o, n, ky, kx] = sum_{img, y, x} G[img, y, x, o] * X[img, s y + ky, s x + kx, n]
+//
+// M = the 256 output channels (8 waves x one 32-channel block), N = 32 input channels x 9 taps per
+// tile (9 accumulators per wave), K = pixels, 16 per v_mfma_f32_32x32x16_bf16.  An atom = (tile,
+// image, 4 x 16 output pixels): the G rows (64 pixels x 256 o) and the X halo ((3s + 3) x (15s + 3)
+// positions x 32 n) staged in LDS in their natural [pixel][channel] layouts and read as MFMA operands
+// with ds_read_b64_tr_b16 (the transpose read delivers 4 consecutive pixels of one channel per lane;
+// a tap is only a different per-lane row address, so no shifted copies).  G rows padded to 576 B and X
+// positions at 64 B make both transposed reads conflict-free for stride 1.  Every wave stages its share
+// of the next atom into registers during the current atom's MFMAs (as pcw_main_k).  Stream-K over atoms;
+// partials in pcw_main_k's fragment layout (pcw_reduce_k sums them for K3C in the reference channel order;
+// pwb_reduce_map_k in the map's order for K2C, then the pose weight swap).
+constexpr int WB_TR = 4, WB_TC = 16, WB_PIX = WB_TR * WB_TC;
+constexpr int WB_GP = 288;                      // bf16 per staged G pixel (256 o + pad: 576 B)
+constexpr int WB_XP = 32;                       // bf16 per staged X position (64 B)
+constexpr int WB_XMAX = (3 * 2 + 3) * (15 * 2 + 3);   // halo positions at stride 2 (297)
+constexpr int WB_BUF = WB_PIX * WB_GP + WB_XMAX * WB_XP;   // bf16 per buffer (55.9 KB)
+
+struct WbGeom {
+  int nimg, ho, wo, hp, wp, s, C, tc, tiles_img, L, ntile, natom, ngroup, slots, hr, hc;
+};
+
+__host__ __device__ inline long long wb_lo(const WbGeom& g, int grp) { return ((long long)grp * g.natom) / g.ngroup; }
+
+typedef short wb_s4 __attribute__((ext_vector_type(4)));
+
+template <typename TX>
+struct WbStage {
+  uint4 gv[WB_PIX * PC_O / 8 / PC_THREADS];                         // 4 x 8 bf16 of G
+  typename std::conditional<sizeof(TX) == 2, uint4, float4>::type xv[(WB_XMAX * WB_XP / (16 / sizeof(TX)) + PC_THREADS - 1) / PC_THREADS];
+};
+
+template <typename TX>
+__device__ __forceinline__ void wb_fetch(const WbGeom& g, WbStage<TX>& st, const __bf16* __restrict__ gp,
+                                         const TX* __restrict__ xp, int atom, int tid) {
+  constexpr int XV = 16 / sizeof(TX);                               // channels per 16-B vector of X
+  constexpr int NXV = sizeof(st.xv) / sizeof(st.xv[0]);
+  const int t = atom / g.L, within = atom - t * g.L;
+  const int img = within / g.tiles_img, ti = within - img * g.tiles_img;
+  const int y0 = (ti / g.tc) * WB_TR, x0 = (ti % g.tc) * WB_TC;
+#pragma unroll
+  for (int u = 0; u < (int)(sizeof(st.gv) / sizeof(st.gv[0])); ++u) {
+    const int e = tid + PC_THREADS * u, px = e >> 5, q = e & 31;     // 32 vectors of 8 o per pixel
+    const int y = y0 + (px >> 4), x = x0 + (px & 15);
+    st.gv[u] = make_uint4(0u, 0u, 0u, 0u);
+    if (y < g.ho && x < g.wo)
+      st.gv[u] = *reinterpret_cast<const uint4*>(gp + (((size_t)img * g.ho + y) * g.wo + x) * PC_O + 8 * q);
+  }
+  const int npos = g.hr * g.hc, vpp = WB_XP / XV;
+#pragma unroll
+  for (int u = 0; u < NXV; ++u) {
+    const int e = tid + PC_THREADS * u, pos = e / vpp, q = e - pos * vpp;
+    const int r = pos / g.hc, c = pos - r * g.hc;
+    const int Y = g.s * y0 + r, X = g.s * x0 + c, n = t * 32 + XV * q;
+    memset(&st.xv[u], 0, sizeof(st.xv[u]));
+    if (pos < npos && Y < g.hp && X < g.wp && n < g.C)
+      st.xv[u] = *reinterpret_cast<const typename std::remove_reference<decltype(st.xv[0])>::type*>(
+          xp + (((size_t)img * g.hp + Y) * g.wp + X) * g.C + n);
+  }
+}
+
+template <typename TX>
+__device__ __forceinline__ void wb_put(const WbGeom& g, const WbStage<TX>& st, __bf16* __restrict__ dst, int tid) {
+  constexpr int XV = 16 / sizeof(TX);
+  constexpr int NXV = sizeof(st.xv) / sizeof(st.xv[0]);
+#pragma unroll
+  for (int u = 0; u < (int)(sizeof(st.gv) / sizeof(st.gv[0])); ++u) {
+    const int e = tid + PC_THREADS * u, px = e >> 5, q = e & 31;
+    *reinterpret_cast<uint4*>(dst + px * WB_GP + 8 * q) = st.gv[u];
+  }
+  __bf16* xd = dst + WB_PIX * WB_GP;
+  const int npos = g.hr * g.hc, vpp = WB_XP / XV;
+#pragma unroll
+  for (int u = 0; u < NXV; ++u) {
+    const int e = tid + PC_THREADS * u, pos = e / vpp, q = e - pos * vpp;
+    if (pos < npos) {
+      if constexpr (sizeof(TX) == 2) {
+        *reinterpret_cast<uint4*>(xd + pos * WB_XP + XV * q) = st.xv[u];
+      } else {
+        bf16x4 b;
+        b[0] = (__bf16)st.xv[u].x;
+        b[1] = (__bf16)st.xv[u].y;
+        b[2] = (__bf16)st.xv[u].z;
+        b[3] = (__bf16)st.xv[u].w;
+        *reinterpret_cast<bf16x4*>(xd + pos * WB_XP + XV * q) = b;
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ bf16x8 wb_tr8(const __bf16* p0, const __bf16* p1) {
+  typedef __attribute__((address_space(3))) wb_s4 lds_s4;
+  const wb_s4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(p0));
+  const wb_s4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(p1));
+  bf16x8 r;
+  __builtin_memcpy(&r, &a, 8);
+  __builtin_memcpy(reinterpret_cast<char*>(&r) + 8, &b, 8);
+  return r;
+}
+
+template <typename TX>
+__global__ __launch_bounds__(PC_THREADS, 2) void pwb_main_k(WbGeom g, const __bf16* __restrict__ gp,
+                                                           const TX* __restrict__ xp, float* __restrict__ partial) {
+  __shared__ __attribute__((aligned(16))) __bf16 lds[2 * WB_BUF];
+  const int grp = blockIdx.x;
+  const int a_lo = (int)wb_lo(g, grp), a_hi = (int)wb_lo(g, grp + 1);
+  if (a_lo >= a_hi) return;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  {
+    WbStage<TX> st;
+    wb_fetch<TX>(g, st, gp, xp, a_lo, tid);
+    wb_put<TX>(g, st, lds, tid);
+  }
+  __syncthreads();
+  f32x16 acc[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[k][r] = 0.f;
+  const int first_tile = a_lo / g.L;
+  int tile = first_tile;
+  auto flush = [&](int tl) {
+    float* dst = partial + (((size_t)grp * g.slots + (tl - first_tile)) * PW_WAVES + wv) * (9 * 16 * 64) + lane;
+#pragma unroll
+    for (int k = 0; k < 9; ++k)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        dst[(k * 16 + r) * 64] = acc[k][r];
+        acc[k][r] = 0.f;
+      }
+  };
+  // transposed-read lane roles: group gq = lane >> 4 (column half gq & 1, row half gq >> 1); within
+  // the group lane 4q + p supplies row q, columns 4p .. 4p + 3
+  const int gq = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int colh = 16 * (gq & 1) + 4 * p, rowh = 8 * (gq >> 1) + q;
+  for (int atom = a_lo; atom < a_hi; ++atom) {
+    const int t = atom / g.L;
+    if (t != tile) {
+      flush(tile);
+      tile = t;
+    }
+    WbStage<TX> st;
+    const bool more = atom + 1 < a_hi;
+    if (more) wb_fetch<TX>(g, st, gp, xp, atom + 1, tid);           // in flight during this atom's MFMAs
+    const __bf16* gb = lds + ((atom - a_lo) & 1) * WB_BUF;
+    const __bf16* xb = gb + WB_PIX * WB_GP;
+#pragma unroll 1
+    for (int ks = 0; ks < WB_TR; ++ks) {
+      // A = G^T: rows = pixels 16 ks + rowh (+4), columns = this wave's o block
+      const __bf16* ga = gb + (16 * ks + rowh) * WB_GP + 32 * wv + colh;
+      const bf16x8 a = wb_tr8(ga, ga + 4 * WB_GP);
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        const int ky = k / 3, kx = k % 3;
+        // B = X: rows = the tap-shifted positions of pixels (ks, rowh (+4)), columns = n
+        const __bf16* xa = xb + ((g.s * ks + ky) * g.hc + g.s * rowh + kx) * WB_XP + colh;
+        const bf16x8 b = wb_tr8(xa, xa + 4 * g.s * WB_XP);
+        acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[k], 0, 0, 0);
+      }
+    }
+    if (more) wb_put<TX>(g, st, lds + ((atom + 1 - a_lo) & 1) * WB_BUF, tid);
+    __syncthreads();
+  }
+  flush(tile);
+}
+
+// K2C: the partials of every tile (32 map channels) summed in workgroup order into dW in the MAP's
+// channel order [O][C][9] (the pose weight swap then gives the reference order)
+__global__ __launch_bounds__(256) void pwb_reduce_map_k(WbGeom g, const float* __restrict__ partial,
+                                                        float* __restrict__ dw) {
+  const int t = blockIdx.x;                          // tile: map channels 32 t ..
+  const int ob = blockIdx.y;                         // o block (32 o)
+  PwGeom pg;                                         // pw_owner's view of the ranges
+  pg.natom = g.natom;
+  pg.ngroup = g.ngroup;
+  const int g0 = pw_owner(pg, (long long)t * g.L), g1 = pw_owner(pg, (long long)(t + 1) * g.L - 1);
+  for (int e = threadIdx.x; e < 32 * 32 * 9; e += 256) {
+    const int tap = e % 9, nl = (e / 9) % 32, ol = e / (9 * 32);
+    const int n = 32 * t + nl;
+    if (n >= g.C) continue;
+    // C/D layout of the 32 x 32 block: row (o) = (r & 3) + 8 (r >> 2) + 4 lh, column (n) = lane & 31
+    const int lh = (ol >> 2) & 1, r = (ol & 3) + 4 * (ol >> 3), ln = nl + 32 * lh;
+    float v = 0.f;
+    for (int grp = g0; grp <= g1; ++grp) {
+      const int slot = t - (int)(wb_lo(g, grp) / g.L);
+      v += partial[((((size_t)grp * g.slots + slot) * PW_WAVES + ob) * 9 + tap) * 16 * 64 + r * 64 + ln];
+    }
+    dw[((size_t)(32 * ob + ol) * g.C + n) * 9 + tap] = v;
+  }
+}
+
+// d bias of bf16 G: fixed-order column sums (blocks of PW_BIAS_ROWS rows), then pcw_bias_fin_k
+__global__ __launch_bounds__(256) void pwb_bias_k(int rows, const __bf16* __restrict__ gp, float* __restrict__ part) {
+  const int r0 = blockIdx.x * PW_BIAS_ROWS;
+  const int r1 = r0 + PW_BIAS_ROWS < rows ? r0 + PW_BIAS_ROWS : rows;
+  float s = 0.f;
+  for (int r = r0; r < r1; r += 8) {
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = r + k < r1 ? (float)gp[(size_t)(r + k) * PC_O + threadIdx.x] : 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += v[k];
+  }
+  part[blockIdx.x * PC_O + threadIdx.x] = s;
+}
+
+static WbGeom wb_plan(int nimg, int ho, int wo, int hp, int wp, int s, int C) {
+  WbGeom g;
+  g.nimg = nimg;
+  g.ho = ho;
+  g.wo = wo;
+  g.hp = hp;
+  g.wp = wp;
+  g.s = s;
+  g.C = C;
+  g.tc = (wo + WB_TC - 1) / WB_TC;
+  g.tiles_img = ((ho + WB_TR - 1) / WB_TR) * g.tc;
+  g.L = nimg * g.tiles_img;
+  g.ntile = (C + 31) / 32;
+  g.natom = g.ntile * g.L;
+  const int res = pc_resident();
+  g.ngroup = g.natom < res ? g.natom : res;
+  const long long range = (g.natom + g.ngroup - 1) / g.ngroup;
+  g.slots = (int)((range - 1) / g.L) + 2;
+  g.hr = s * (WB_TR - 1) + 3;
+  g.hc = s * (WB_TC - 1) + 3;
+  return g;
+}
+
+// vec: channels per 16-B load of X (bf16 8, fp32 4): C a multiple of it
+static bool wb_supported(const WbGeom& g, int vec) {
+  if (g.nimg <= 0 || g.ho <= 0 || g.wo <= 0 || (g.s != 1 && g.s != 2) || g.C <= 0 || g.C % vec) return false;
+  const long long range = g.natom / g.ngroup;
+  return range > 0 && (g.L + range - 1) / range + 1 <= PW_MAXC;   // workgroups meeting one tile (reduce)
+}
+
+static PwGeom wb_as_pw(const WbGeom& w, int D) {
+  PwGeom g;
+  g.nbc = w.nimg;
+  g.h = w.ho;
+  g.w = w.wo;
+  g.ntot = w.C;
+  g.D = D;
+  g.tc = w.tc;
+  g.tiles_img = w.tiles_img;
+  g.L = w.L;
+  g.ntile = w.ntile;
+  g.natom = w.natom;
+  g.ngroup = w.ngroup;
+  g.slots = w.slots;
+  return g;
+}
+
 }  // namespace vfd
 
 using namespace vfd;
@@ -2179,6 +2438,81 @@ int vfd_proj_conv_wgrad(const vfd_voxel_desc* d, const float* g_pre, const float
     pcw_bias_fin_k<<<PC_O / 4, 256, 0, s>>>(nblk, part, db);
   }
   return fail_launch("proj_conv_wgrad");
+}
+
+// bf16 K3C weight / bias gradient (config 3): g_pre bf16 [B*N, h, w, O], x = the bf16 frustum side
+// output [B*N, h+2, w+2, D*Cv]; dw [O, Cv*D, 3, 3] fp32 in the reference channel order, db [O] fp32
+static WbGeom pwb_k3c(const vfd_voxel_desc& d) {
+  return wb_plan(d.B * d.N, d.h, d.w, d.h + 2, d.w + 2, 1, d.D * PC_CV);
+}
+
+size_t vfd_proj_conv_wgrad_bf16_workspace(const vfd_voxel_desc* d) {
+  if (!d || d->Cv != PC_CV || d->D <= 0 || d->D > 64 || d->B <= 0 || d->N <= 0 || d->h < 1 || d->w < 1) return 0;
+  const WbGeom g = pwb_k3c(*d);
+  if (!wb_supported(g, 8)) return 0;
+  const int nblk = (g.nimg * g.ho * g.wo + PW_BIAS_ROWS - 1) / PW_BIAS_ROWS;
+  return ((size_t)g.ngroup * g.slots * PW_FRAG + (size_t)nblk * PC_O) * sizeof(float);
+}
+
+int vfd_proj_conv_wgrad_bf16(const vfd_voxel_desc* d, const void* g_pre, const void* x, float* dw, float* db,
+                             void* ws, size_t ws_bytes, void* stream) {
+  VFD_REQUIRE(d && g_pre && x && (dw || db), "proj_conv_wgrad_bf16: null argument");
+  const size_t need = vfd_proj_conv_wgrad_bf16_workspace(d);
+  VFD_REQUIRE(need, "proj_conv_wgrad_bf16: unsupported shape (Cv = %d, 0 < D <= 64)", PC_CV);
+  VFD_REQUIRE(ws && ws_bytes >= need, "proj_conv_wgrad_bf16: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  ProfScope ps(K_PROJ_CONV_WGRAD, s);
+  const WbGeom g = pwb_k3c(*d);
+  float* partial = (float*)ws;
+  if (dw) {
+    pwb_main_k<__bf16><<<g.ngroup, PC_THREADS, 0, s>>>(g, (const __bf16*)g_pre, (const __bf16*)x, partial);
+    const PwGeom pg = wb_as_pw(g, d->D);
+    pcw_reduce_k<<<dim3(PC_O / 4, 2 * ((d->D + PW_DC - 1) / PW_DC)), 256, 0, s>>>(pg, partial, dw);
+  }
+  if (db) {
+    float* part = partial + (size_t)g.ngroup * g.slots * PW_FRAG;
+    const int rows = g.nimg * g.ho * g.wo, nblk = (rows + PW_BIAS_ROWS - 1) / PW_BIAS_ROWS;
+    pwb_bias_k<<<nblk, PC_O, 0, s>>>(rows, (const __bf16*)g_pre, part);
+    pcw_bias_fin_k<<<PC_O / 4, 256, 0, s>>>(nblk, part, db);
+  }
+  return fail_launch("proj_conv_wgrad_bf16");
+}
+
+// bf16 K2C weight / bias gradient (config 3; the pose reduce_dim[0], stride d->stride): g_pre bf16
+// [B, Ho, Wo, 256], x = the fp32 reflect-padded BEV map [B, H, W, C] (rounded to bf16 as staged);
+// dw_map [256, C, 3, 3] fp32 in the MAP's channel order (the caller swaps it to the reference order),
+// db [256] fp32
+size_t vfd_pad_conv_wgrad_bf16_workspace(const vfd_conv_desc* d) {
+  if (!d || d->out_channels != PC_O || d->B <= 0 || d->H < 3 || d->W < 3 || (d->stride != 1 && d->stride != 2)) return 0;
+  const int ho = (d->H - 3) / d->stride + 1, wo = (d->W - 3) / d->stride + 1;
+  const WbGeom g = wb_plan(d->B, ho, wo, d->H, d->W, d->stride, d->C);
+  if (!wb_supported(g, 4)) return 0;
+  const int nblk = (g.nimg * g.ho * g.wo + PW_BIAS_ROWS - 1) / PW_BIAS_ROWS;
+  return ((size_t)g.ngroup * g.slots * PW_FRAG + (size_t)nblk * PC_O) * sizeof(float);
+}
+
+int vfd_pad_conv_wgrad_bf16(const vfd_conv_desc* d, const void* g_pre, const float* x, float* dw_map, float* db,
+                            void* ws, size_t ws_bytes, void* stream) {
+  VFD_REQUIRE(d && g_pre && x && (dw_map || db), "pad_conv_wgrad_bf16: null argument");
+  const size_t need = vfd_pad_conv_wgrad_bf16_workspace(d);
+  VFD_REQUIRE(need, "pad_conv_wgrad_bf16: unsupported shape (C %% 4 == 0, stride 1 or 2, %d outputs)", PC_O);
+  VFD_REQUIRE(ws && ws_bytes >= need, "pad_conv_wgrad_bf16: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  ProfScope ps(K_PAD_CONV_WGRAD, s);
+  const int ho = (d->H - 3) / d->stride + 1, wo = (d->W - 3) / d->stride + 1;
+  const WbGeom g = wb_plan(d->B, ho, wo, d->H, d->W, d->stride, d->C);
+  float* partial = (float*)ws;
+  if (dw_map) {
+    pwb_main_k<float><<<g.ngroup, PC_THREADS, 0, s>>>(g, (const __bf16*)g_pre, x, partial);
+    pwb_reduce_map_k<<<dim3(g.ntile, PC_O / 32), 256, 0, s>>>(g, partial, dw_map);
+  }
+  if (db) {
+    float* part = partial + (size_t)g.ngroup * g.slots * PW_FRAG;
+    const int rows = g.nimg * g.ho * g.wo, nblk = (rows + PW_BIAS_ROWS - 1) / PW_BIAS_ROWS;
+    pwb_bias_k<<<nblk, PC_O, 0, s>>>(rows, (const __bf16*)g_pre, part);
+    pcw_bias_fin_k<<<PC_O / 4, 256, 0, s>>>(nblk, part, db);
+  }
+  return fail_launch("pad_conv_wgrad_bf16");
 }
 
 }  // extern "C"

@@ -517,6 +517,28 @@ def pad_conv_dgrad(g_pre, x_shape, w, stride, perm=None):
     return dx
 
 
+_PAD_WGRAD = os.environ.get('VFD_PAD_WGRAD', '1') != '0'    # bf16 K2C weight gradient on the HIP path
+
+
+def pad_conv_wgrad_bf16(gb, x, w, stride, need_w=True, need_b=True):
+    """K2C's bf16 weight / bias gradient through the C ABI: gb [B, 256, Ho, Wo] bf16 channels-last
+    (d pre-activation), x the fp32 channels-last map [B, C, H, W] -> (d w in the MAP's channel
+    order [256, C, 3, 3] fp32, d b [256] fp32); (None, None) parts not asked for."""
+    lib = L.load()
+    B, C, H, W = x.shape
+    d = L.ConvDesc(B, H, W, C, stride, gb.shape[1])
+    nbytes = lib.vfd_pad_conv_wgrad_bf16_workspace(ctypes.byref(d))
+    if not nbytes:
+        raise RuntimeError(f'pad_conv_wgrad_bf16: unsupported shape {tuple(x.shape)}, stride {stride}')
+    dw = torch.empty(gb.shape[1], C, 3, 3, device=gb.device) if need_w else None
+    db = torch.empty(gb.shape[1], device=gb.device) if need_b else None
+    ws = _ws(nbytes, gb.device)
+    L.check(lib.vfd_pad_conv_wgrad_bf16(ctypes.byref(d), _channels_last(gb, 'grad').data_ptr(),
+                                        _channels_last(x, 'map').data_ptr(), L.ptr(dw), L.ptr(db), ws.data_ptr(),
+                                        nbytes, L.stream()), 'pad_conv_wgrad_bf16')
+    return dw, db
+
+
 class PadConv(torch.autograd.Function):
     """K2C: reflect-padded channels-last map x [B, C, H, W] -> LeakyReLU(conv3x3_stride(x) + bias)
     as the reflect-padded channels-last input of the next reflect conv, logical
@@ -634,7 +656,7 @@ class PadConvBF16(torch.autograd.Function):
             # and output — the fp32 map's gradient, as autocast's bf16 conv gradient cast back)
             dx = pad_conv_dgrad(gb, x.shape, w, s, ctx.perm)
         wd = None
-        if (mask[0] and dx is None) or mask[1] or mask[2]:
+        if (mask[0] and dx is None) or ((mask[1] or mask[2]) and not (_PC_BF16_BWD and _PAD_WGRAD)):
             wd = w.detach()
             if ctx.perm:    # MIOpen works in the map's channel order (channels-last like x)
                 C1, Z = ctx.perm
@@ -645,12 +667,23 @@ class PadConvBF16(torch.autograd.Function):
             # the fp32 map's gradient would cast back)
             g32 = lrelu_pad_backward(g.float(), out.float())
             dx = cb(g32, x, wd, *args, [True, False, False])[0]
+        if (mask[1] or mask[2]) and _PC_BF16_BWD and _PAD_WGRAD:
+            # the bf16 weight / bias gradient on MFMA (projconv.hip pwb_main_k: the fp32 map rounded
+            # to bf16 as it is staged), d weight in the map's channel order, then the pose swap
+            dw, db = pad_conv_wgrad_bf16(gb, x, w, s, mask[1], mask[2])
+            if dw is not None and ctx.perm:
+                dw = weight_swap(dw, ctx.perm[1], ctx.perm[0])
+            return dx, dw, db, None, None, None
         if mask[1] or mask[2]:
+            if wd is None:
+                wd = w.detach()
+                if ctx.perm:
+                    wd = weight_swap(wd, ctx.perm[0], ctx.perm[1], cache=True, memory_format=torch.channels_last)
             _, dw, db = cb(gb, x.to(torch.bfloat16), wd.to(torch.bfloat16), *args, [False, mask[1], mask[2]])
         if dw is not None:
             dw = dw.float()
             if ctx.perm:
-                dw = weight_swap(dw, Z, C1)
+                dw = weight_swap(dw, ctx.perm[1], ctx.perm[0])
         return dx, dw, (db.float() if db is not None else None), None, None, None
 
 
@@ -883,6 +916,19 @@ class ProjConvBF16(torch.autograd.Function):
             L.check(lib.vfd_proj_conv_dgrad_bf16(ctypes.byref(d), g_pre.data_ptr(), wd.data_ptr(), dx.data_ptr(),
                                                  ws.data_ptr(), nbytes, L.stream()), 'proj_conv_dgrad_bf16')
         need_dx = mask[0] and dx is None
+        dw0 = None
+        if (mask[1] or mask[2]) and _PC_BF16_BWD and x is not None:
+            # the bf16 weight / bias gradient on MFMA (projconv.hip pwb_main_k), d weight straight
+            # into the reference channel order c*D + d
+            nbytes = lib.vfd_proj_conv_wgrad_bf16_workspace(ctypes.byref(d))
+            if nbytes:
+                dw0 = torch.empty(w0.shape, device=g.device) if mask[1] else None
+                db = torch.empty(O, device=g.device) if mask[2] else None
+                ws = _ws(nbytes, g.device)
+                L.check(lib.vfd_proj_conv_wgrad_bf16(ctypes.byref(d), g_pre.data_ptr(), x.data_ptr(), L.ptr(dw0),
+                                                     L.ptr(db), ws.data_ptr(), nbytes, L.stream()),
+                        'proj_conv_wgrad_bf16')
+                mask = (mask[0], False, False)
         if x is None:   # only the bias gradient was asked for (the forward wrote no side output)
             db = g_pre.float().sum((0, 2, 3))
         elif need_dx or mask[1] or mask[2]:
@@ -891,17 +937,17 @@ class ProjConvBF16(torch.autograd.Function):
                                                               1, [need_dx, mask[1], mask[2]])
             if need_dx:
                 dx = dx2
-        dvox = dw0 = None
-        if mask[0]:
+        dvox = None
+        if ctx.needs_input_grad[1]:
             dxf = dx.float().contiguous(memory_format=torch.channels_last)
             dvox = torch.empty(B, V, Cv, device=g.device)
             L.check(lib.vfd_voxel_project_bwd_planned(ctypes.byref(d), dxf.data_ptr(), ctx.plan.data_ptr(),
                                                       ctx.plan.numel(), dvox.data_ptr(), L.stream()),
                     'voxel_project_bwd')
-        if mask[1]:
-            dw0 = weight_swap(dw.float(), space.D, Cv)      # d*Cv + c -> the reference's c*D + d
+        if mask[1]:         # MIOpen's d weight: d*Cv + c -> the reference's c*D + d
+            dw0 = weight_swap(dw.float(), space.D, Cv)
         ctx.plan = None
-        return None, dvox, None, None, dw0, db.float() if mask[2] else None
+        return None, dvox, None, None, dw0, (db.float() if ctx.needs_input_grad[5] and db is not None else None)
 
 
 # =============================================================================================

@@ -248,6 +248,12 @@ def _channels_last(t, what):
     return t.contiguous(memory_format=torch.channels_last)
 
 
+def _nhwc(t, what):
+    """Device tensor in channels-last (NHWC) memory order, its dtype kept (no copy when it already is)."""
+    _check_device(t, what)
+    return t.contiguous(memory_format=torch.channels_last)
+
+
 def pose_conv_weight(w, C1, Z):
     """reduce_dim[0] weight [O, C1*Z, kh, kw] (reference channel c*Z + z) -> the z-major order
     z*C1 + c of FusePose's output; differentiable (a view + one gather)."""
@@ -533,9 +539,10 @@ def pad_conv_wgrad_bf16(gb, x, w, stride, need_w=True, need_b=True):
     dw = torch.empty(gb.shape[1], C, 3, 3, device=gb.device) if need_w else None
     db = torch.empty(gb.shape[1], device=gb.device) if need_b else None
     ws = _ws(nbytes, gb.device)
-    L.check(lib.vfd_pad_conv_wgrad_bf16(ctypes.byref(d), _channels_last(gb, 'grad').data_ptr(),
-                                        _channels_last(x, 'map').data_ptr(), L.ptr(dw), L.ptr(db), ws.data_ptr(),
-                                        nbytes, L.stream()), 'pad_conv_wgrad_bf16')
+    gb = _nhwc(gb.to(torch.bfloat16), 'grad')
+    x = _nhwc(x.float(), 'map')
+    L.check(lib.vfd_pad_conv_wgrad_bf16(ctypes.byref(d), gb.data_ptr(), x.data_ptr(), L.ptr(dw), L.ptr(db),
+                                        ws.data_ptr(), nbytes, L.stream()), 'pad_conv_wgrad_bf16')
     return dw, db
 
 
@@ -695,8 +702,10 @@ def lrelu_pad_backward(g, out, slope=0.1, dtype=None):
     padded output g and that output (fused, deterministic: reflectpad.hip) -> NHWC [n, C, h, w].
     g and out fp32 or bf16 (the same type); the result in `dtype` (default g's), computed in fp32."""
     lib = L.load()
-    g = _channels_last(g, 'grad')
-    out = _channels_last(out.to(g.dtype), 'output')
+    if g.dtype not in _DT:
+        g = g.float()
+    g = _nhwc(g, 'grad')
+    out = _nhwc(out.to(g.dtype), 'output')
     dtype = dtype or g.dtype
     n, C, hp, wp = g.shape
     gp = torch.empty(n, C, hp - 2, wp - 2, device=g.device, dtype=dtype, memory_format=torch.channels_last)

@@ -144,7 +144,7 @@ def mfma_flops(kernel, s):
     the same; K2C = the pose reduce_dim's first conv."""
     if kernel in ('proj_conv_fwd', 'proj_conv_dgrad', 'proj_conv_wgrad'):
         return 2.0 * s['B'] * s['N'] * s['h'] * s['w'] * 256 * s['Cv'] * s['D'] * 9
-    if kernel == 'pad_conv_fwd':                                  # K2C, pose reduce_dim[0]: K = (C+1)*Z*9
+    if kernel in ('pad_conv_fwd', 'pad_conv_dgrad', 'pad_conv_wgrad'):   # K2C, pose reduce_dim[0]: K = (C+1)*Z*9
         return 2.0 * s['B'] * pose_hw(s) * 256 * (s['C'] + 1) * s['Z'] * 9
     return None
 
@@ -385,8 +385,10 @@ def main():
         fl = mfma_flops(k, s)
         if fl is not None:
             ach = fl / avg_s / 1e12
-            # config 3 runs K3C / K2C's forward on bf16 MFMA (the data gradients stay fp32 / MIOpen)
-            bf16 = cfg['training']['net_precision'] == 'bf16' and k in ('proj_conv_fwd', 'pad_conv_fwd')
+            # config 3 runs K3C / K2C (forward, data and weight gradients) on bf16 MFMA
+            bf16 = cfg['training']['net_precision'] == 'bf16'
+            if bf16 and os.environ.get('VFD_PC_BF16_BWD', '1') == '0':
+                bf16 = k in ('proj_conv_fwd', 'pad_conv_fwd')
             peak = MFMA_BF16_PEAK_TFS if bf16 else MFMA_F32_PEAK_TFS
             return {'kernel': k, 'bound': 'mfma', 'mfma_dtype': 'bf16' if bf16 else 'fp32', 'achieved': ach,
                     'peak': peak, 'unit': 'TFLOP/s', 'frac': ach / peak, 'traffic': traffic_tab.get(k),

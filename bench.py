@@ -97,9 +97,10 @@ def shapes(cfg):
 
 
 def algorithmic_bytes(kernel, s):
-    """Compulsory HBM bytes of ONE launch at the kernel's own boundary (fp32 = 4 B), with the
-    unpadded tensor sizes of SURVEY.md §8(d) (the reflect-pad halos the K2/K3 kernels also write
-    for the consumer convs are NOT counted: they are extra work, not algorithmic bytes)."""
+    """Compulsory HBM bytes of ONE launch at the kernel's own boundary (fp32 = 4 B; the pose BEV
+    map 2 B where K2 writes it in bf16, s['map_bytes']), with the unpadded tensor sizes of
+    SURVEY.md §8(d) (the reflect-pad halos the K2/K3 kernels also write for the consumer convs are
+    NOT counted: they are extra work, not algorithmic bytes)."""
     B, N, C, Cv, p, P = s['B'], s['N'], s['C'], s['Cv'], s['h'] * s['w'], s['H'] * s['W']
     V, D, T, F = s['V'], s['D'], s['T'], s['F']
     pose_out = B * (C + 1) * V                                    # [B, C+1, V] mean voxel features
@@ -130,6 +131,8 @@ def algorithmic_bytes(kernel, s):
         'depth_syn_fwd': B * N * P * 3 + 2 * B * N * 3 * P,        # depths + mask in, 3 sources x (depth, mask) out
         'depth_syn_bwd': B * N * P * 3 + B * N * 3 * P + 2 * B * N * P,
     }
+    if kernel in ('fuse_pose_fwd', 'pad_conv_fwd') and s.get('map_bytes', 4) != 4:
+        return (planes[kernel] - pose_out) * 4 + pose_out * s['map_bytes']
     return planes[kernel] * 4
 
 
@@ -377,6 +380,8 @@ def main():
         return 0
 
     s = shapes(cfg)
+    if cfg['training']['net_precision'] == 'bf16' and os.environ.get('VFD_POSE_BF16_MAP', '1') != '0':
+        s['map_bytes'] = 2            # config 3: K2 writes the pose map in bf16 (kernels.PoseConvBF16)
     traffic_tab = load_traffic(args.config)
 
     def roofline_of(k):

@@ -100,6 +100,10 @@ int vfd_fusion_plan(const vfd_voxel_desc* d, const float* mask_lo, const float* 
  * the conv weight's input channels are permuted the same way, so the convolution is unchanged). */
 int vfd_fuse_pose_fwd(const vfd_voxel_desc* d, const float* mask_lo, const float* K, const float* Einv,
                       const float* feats_cl, float* out, void* stream);
+/* As vfd_fuse_pose_fwd with the map stored as dtype_out (0 fp32, 1 bf16 rounded to nearest even:
+ * config 3, whose only consumer, the bf16 K2C, stages exactly those rounded values). */
+int vfd_fuse_pose_fwd_t(const vfd_voxel_desc* d, const float* mask_lo, const float* K, const float* Einv,
+                        const float* feats_cl, void* out, int dtype_out, void* stream);
 /* d_out in the forward's output layout -> d_feats [B,N,C,h,w] (every element written).
  * Atomic-free gather over the plan's 4x4-pixel tile buckets, pulled from the plan's task queue
  * (heavy tiles split by channel group); the call resets the queue's work counter inside `plan`,
@@ -346,6 +350,9 @@ int vfd_pad_conv_fwd(const vfd_conv_desc* d, const float* x, const float* Wf, co
 size_t vfd_pad_conv_fwd_bf16_workspace(const vfd_conv_desc* d);
 int vfd_pad_conv_fwd_bf16(const vfd_conv_desc* d, const float* x, const void* Wf, const float* bias, void* out,
                           void* workspace, size_t ws_bytes, void* stream);
+/* x of type dtype_x (0 fp32, 1 bf16: the map vfd_fuse_pose_fwd_t writes under config 3, C % 4 == 0). */
+int vfd_pad_conv_fwd_bf16_t(const vfd_conv_desc* d, const void* x, int dtype_x, const void* Wf, const float* bias,
+                            void* out, void* workspace, size_t ws_bytes, void* stream);
 
 /* K2C data gradient (volumetric_fusionnet.py:59-60, 338-343 backward; replaces the cudnn / MIOpen
  * backward-data of the pose reduce_dim[0]): dx [B, H, W, C] (the full reflect-padded map's gradient,
@@ -396,6 +403,9 @@ int vfd_proj_conv_wgrad_bf16(const vfd_voxel_desc* d, const void* g_pre, const v
 size_t vfd_pad_conv_wgrad_bf16_workspace(const vfd_conv_desc* d);
 int vfd_pad_conv_wgrad_bf16(const vfd_conv_desc* d, const void* g_pre, const float* x, float* dw_map, float* db,
                             void* workspace, size_t ws_bytes, void* stream);
+/* x of type dtype_x (0 fp32, 1 bf16 map). */
+int vfd_pad_conv_wgrad_bf16_t(const vfd_conv_desc* d, const void* g_pre, const void* x, int dtype_x, float* dw_map,
+                              float* db, void* workspace, size_t ws_bytes, void* stream);
 
 /* K3C weight / bias gradient (volumetric_fusionnet.py:59-60, 265 backward; replaces the
  * reference's cudnn weight-gradient of reduce_dim[0]): dw [O = 256, Cv*D, 3, 3] in the reference

@@ -763,6 +763,45 @@ def test_pad_conv_bf16(shape):
         gclose(a.grad, r.grad, f'bf16 K2C {name} {shape}', rel=2e-2)
 
 
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize('config,B', [(2, 2), (5, 1)])
+def test_pose_conv_bf16_map_matches_two_nodes(config, B):
+    """Config 3's K2 + K2C on the bf16 map (PoseConvBF16: K2 writes the map in bf16, the conv's
+    forward and weight gradient read it) against FusePose (fp32 map) -> PadConvBF16 (the map
+    rounded to bf16 as it is staged): the same staged values, so the map, the conv output and
+    every gradient (d feats through the fp32 K2C data gradient and K2's backward, d weight, d bias)
+    are BIT-identical (volumetric_fusionnet.py:116-162, 338-343 under autocast)."""
+    from vfdepth_amd import kernels as KN
+    cfg = full_cfg(config)
+    batch, lvl, Einv = _fusion_inputs(cfg, 91)
+    C = int(cfg['model']['fusion_feat_in_dim'])
+    space = KN.VoxelSpace(cfg, DEV)
+    rep = (lambda t: t.to(DEV).repeat(B, *([1] * (t.dim() - 1)))) if B > 1 else (lambda t: t.to(DEV))
+    K, E, mask = rep(batch[('K', lvl)]), rep(Einv), rep(batch['mask'])
+    plan = KN.FusionPlan(space, KN.mask_lowres(space, mask), K, E, build=False)
+    C1, Z = C + 1, space.Z
+    gen = torch.Generator(device=DEV).manual_seed(92)
+    feats = torch.randn(B, 6, C, space.h, space.w, device=DEV, generator=gen)
+    w = torch.randn(256, C1 * Z, 3, 3, device=DEV, generator=gen) * (C1 * Z * 9) ** -0.5
+    b = 0.1 * torch.randn(256, device=DEV, generator=gen)
+    assert KN.pose_conv_bf16_supported(space, B, C, 2, 256)
+    with torch.no_grad():
+        x32 = KN.FusePose.apply(space, plan, feats)
+        x16 = KN._pose_fuse_t(space, plan, feats, torch.bfloat16)
+        assert torch.equal(x16, x32.to(torch.bfloat16)), 'bf16 map != the fp32 map rounded to nearest even'
+    wf = KN.pad_conv_weight_fragments_bf16(w, C1, Z)
+    la = [t.clone().requires_grad_(True) for t in (feats, w, b)]
+    lb = [t.clone().requires_grad_(True) for t in (feats, w, b)]
+    ya = KN.PadConvBF16.apply(KN.FusePose.apply(space, plan, la[0]), la[1], la[2], 2, wf, (C1, Z))
+    yb = KN.PoseConvBF16.apply(space, plan, lb[0], lb[1], lb[2], 2, wf, (C1, Z))
+    assert yb.dtype == torch.bfloat16 and torch.equal(ya, yb), 'K2C output differs on the bf16 map'
+    g = torch.randn(ya.shape, device=DEV, generator=gen).to(torch.bfloat16)
+    ya.backward(g)
+    yb.backward(g)
+    for name, p, q in zip(('d feats', 'd weight', 'd bias'), la, lb):
+        assert torch.equal(p.grad, q.grad), f'{name} differs on the bf16 map (max {float((p.grad - q.grad).abs().max()):.3g})'
+
+
 # ------------------------------------------------------------------------------------ fused BN
 @pytest.mark.parametrize('shape,res,relu', [((6, 64, 96, 160), True, True),      # layer1 block tail
                                             ((6, 64, 192, 320), False, True),    # stem

@@ -32,10 +32,10 @@ def main():
     dev = torch.device('cuda:0')
     space = KN.VoxelSpace(G.step_cfg(), dev)
     for sh in a.shapes.split(','):
-        pose_ops = [o for o in a.ops.split(',') if o.startswith(('pdgrad', 'pwgrad'))]
+        pose_ops = [o for o in a.ops.split(',') if o.startswith(('pdgrad', 'pwgrad', 'pfwd'))]
         if pose_ops:
             pose(lib, L, KN, dev, sh, pose_ops, a.iters)
-        if all(o.startswith(('pdgrad', 'pwgrad')) for o in a.ops.split(',')):
+        if all(o.startswith(('pdgrad', 'pwgrad', 'pfwd')) for o in a.ops.split(',')):
             continue
         B, h, w, D = SHAPES[sh]
         N, Cv, O = 6, 64, 256
@@ -46,7 +46,7 @@ def main():
         dx = torch.empty(B * N, Cv * D, h + 2, w + 2, device=dev).contiguous(memory_format=torch.channels_last)
         flop = 2.0 * B * N * h * w * O * Cv * D * 9
         for op in a.ops.split(','):
-            if op.startswith(('pdgrad', 'pwgrad')):
+            if op.startswith(('pdgrad', 'pwgrad', 'pfwd')):
                 continue
             if op == 'dgrad':
                 wd, gp, kind = KN.proj_conv_dgrad_weight(w0, Cv, D), g_pre, 'fp32'
@@ -134,10 +134,46 @@ def pose(lib, L, KN, dev, sh, ops, iters):
     x = torch.randn(B, C, S, S, device=dev).contiguous(memory_format=torch.channels_last)
     flop = 2.0 * B * ho * ho * 256 * C * 9
     for op in ops:
-        if op in ('pwgrad_bf16', 'pwgrad_bf16_miopen'):
+        if op in ('pfwd', 'pfwd_bf16', 'pfwd_bf16m'):
+            bf = op != 'pfwd'
+            xm = x.to(torch.bfloat16) if op == 'pfwd_bf16m' else x    # the bf16 map of PoseConvBF16
+            d = KN.pad_conv_desc(x, 2, 256)
+            bias = torch.randn(256, device=dev)
+            wf = KN.pad_conv_weight_fragments_bf16(w, C1, Z) if bf else KN.pad_conv_weight_fragments(w, C1, Z)
+            fn = lib.vfd_pad_conv_fwd_bf16 if bf else lib.vfd_pad_conv_fwd
+            nb = (lib.vfd_pad_conv_fwd_bf16_workspace if bf else lib.vfd_pad_conv_fwd_workspace)(ctypes.byref(d))
+            ws = torch.empty(nb, dtype=torch.uint8, device=dev)
+            out = torch.empty(B, 256, ho + 2, ho + 2, device=dev, dtype=torch.bfloat16 if bf else torch.float32,
+                              memory_format=torch.channels_last)
+
+            def fcall():
+                if op == 'pfwd_bf16m':
+                    L.check(lib.vfd_pad_conv_fwd_bf16_t(ctypes.byref(d), xm.data_ptr(), 1, wf.data_ptr(), bias.data_ptr(),
+                                                        out.data_ptr(), ws.data_ptr(), nb, L.stream()), op)
+                    return
+                L.check(fn(ctypes.byref(d), x.data_ptr(), wf.data_ptr(), bias.data_ptr(), out.data_ptr(),
+                           ws.data_ptr(), nb, L.stream()), op)
+            for _ in range(2):
+                fcall()
+            torch.cuda.synchronize()
+            L.prof_enable('pad_conv_fwd')
+            for _ in range(iters):
+                fcall()
+            torch.cuda.synchronize()
+            n, ms = L.prof_read()['pad_conv_fwd']
+            L.prof_enable('off')
+            us = ms / n * 1e3
+            kind = 'bf16' if bf else 'fp32'
+            tf = flop / (us * 1e-6) / 1e12
+            print(f'{sh} pose {op:14s} {us:9.1f} us  {tf:7.1f} TF/s  {tf / PEAK[kind]:.3f} of {kind} peak', flush=True)
+            continue
+        if op in ('pwgrad_bf16', 'pwgrad_bf16m', 'pwgrad_bf16_miopen'):
             gb = g.to(torch.bfloat16)
             if op == 'pwgrad_bf16':
                 call = lambda: KN.pad_conv_wgrad_bf16(gb, x, w, 2)  # noqa: E731
+            elif op == 'pwgrad_bf16m':
+                xm = x.to(torch.bfloat16)
+                call = lambda: KN.pad_conv_wgrad_bf16(gb, xm, w, 2)  # noqa: E731
             else:
                 wm = KN.pose_conv_weight(w, C1, Z).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
                 call = lambda: torch.ops.aten.convolution_backward(gb, x.to(torch.bfloat16), wm, [256], [2, 2], [0, 0],  # noqa: E731

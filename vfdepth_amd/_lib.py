@@ -67,6 +67,7 @@ _SIGS = {
     'vfd_fusion_plan_bytes': (c_size_t, [ctypes.POINTER(VoxelDesc)]),
     'vfd_fusion_plan': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 5 + [c_void_p]),
     'vfd_fuse_pose_fwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 5 + [c_void_p]),
+    'vfd_fuse_pose_fwd_t': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 5 + [c_int, c_void_p]),
     'vfd_fuse_pose_bwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 4 + [c_void_p]),
     'vfd_voxel_project_fwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 4 + [c_void_p]),
     'vfd_voxel_project_plan_bytes': (c_size_t, [ctypes.POINTER(VoxelDesc)]),
@@ -92,6 +93,8 @@ _SIGS = {
     'vfd_proj_conv_wgrad_bf16': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 5 + [c_size_t, c_void_p]),
     'vfd_pad_conv_wgrad_bf16_workspace': (c_size_t, [ctypes.POINTER(ConvDesc)]),
     'vfd_pad_conv_wgrad_bf16': (c_int, [ctypes.POINTER(ConvDesc)] + [c_fp] * 5 + [c_size_t, c_void_p]),
+    'vfd_pad_conv_wgrad_bf16_t': (c_int, [ctypes.POINTER(ConvDesc)] + [c_fp] * 2 + [c_int] + [c_fp] * 3
+                                  + [c_size_t, c_void_p]),
     'vfd_proj_conv_wgrad_workspace': (c_size_t, [ctypes.POINTER(VoxelDesc)]),
     'vfd_proj_conv_wgrad': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 5 + [c_size_t, c_void_p]),
     'vfd_bn_splits': (c_int, [ctypes.POINTER(BnDesc)]),
@@ -136,6 +139,7 @@ _SIGS = {
     'vfd_pad_conv_fwd': (c_int, [ctypes.POINTER(ConvDesc)] + [c_fp] * 5 + [c_size_t, c_void_p]),
     'vfd_pad_conv_fwd_bf16_workspace': (c_size_t, [ctypes.POINTER(ConvDesc)]),
     'vfd_pad_conv_fwd_bf16': (c_int, [ctypes.POINTER(ConvDesc)] + [c_fp] * 5 + [c_size_t, c_void_p]),
+    'vfd_pad_conv_fwd_bf16_t': (c_int, [ctypes.POINTER(ConvDesc), c_fp, c_int] + [c_fp] * 4 + [c_size_t, c_void_p]),
     'vfd_pad_conv_dgrad_workspace': (c_size_t, [ctypes.POINTER(ConvDesc)]),
     'vfd_pad_conv_dgrad': (c_int, [ctypes.POINTER(ConvDesc)] + [c_fp] * 4 + [c_size_t, c_void_p]),
     'vfd_pad_conv_dgrad_bf16_workspace': (c_size_t, [ctypes.POINTER(ConvDesc)]),

@@ -673,10 +673,10 @@ constexpr int POSE_TV = 32;
 #endif
 constexpr int POSE_MAXC = 256;      // channels held per lane: ceil(C / 64) <= 4
 
-template <int NC>
+template <int NC, typename TO>
 __global__ __launch_bounds__(256) void fuse_pose_fwd_k(vfd_voxel_desc d, const float* __restrict__ mlo,
                                                        const float* __restrict__ K, const float* __restrict__ Einv,
-                                                       const float* __restrict__ feats, float* __restrict__ out) {
+                                                       const float* __restrict__ feats, TO* __restrict__ out) {
   constexpr int CPL = POSE_MAXC / 64;
   __shared__ int s_base[POSE_TV][NC];
   __shared__ float s_w[POSE_TV][NC][4];
@@ -737,7 +737,7 @@ __global__ __launch_bounds__(256) void fuse_pose_fwd_k(vfd_voxel_desc d, const f
   const int P = d.pad_out ? 2 : 0;
   const int Yo = d.Y + P, Xo = d.X + P;
   const size_t pix_stride = (size_t)d.Z * C1;
-  float* ob = out + (size_t)b * Yo * Xo * pix_stride;
+  TO* ob = out + (size_t)b * Yo * Xo * pix_stride;
   for (int t0 = wv * 2; t0 < POSE_TV; t0 += 8) {
     float acc[2][CPL];
 #pragma unroll
@@ -796,13 +796,13 @@ __global__ __launch_bounds__(256) void fuse_pose_fwd_k(vfd_voxel_desc d, const f
       const float zf = s_zf[t];
       for (int a = 0; a < nr; ++a)
         for (int c2 = 0; c2 < nc; ++c2) {
-          float* row = ob + ((size_t)rows[a] * Xo + cols[c2]) * pix_stride + (size_t)zi * C1;
+          TO* row = ob + ((size_t)rows[a] * Xo + cols[c2]) * pix_stride + (size_t)zi * C1;
 #pragma unroll
           for (int k = 0; k < CPL; ++k) {
             const int ch = lane + 64 * k;
-            if (ch < C) row[ch] = o[k];
+            if (ch < C) row[ch] = (TO)o[k];
           }
-          if (lane == 0) row[C] = zf;
+          if (lane == 0) row[C] = (TO)zf;
         }
     }
   }
@@ -2512,22 +2512,30 @@ int vfd_fusion_plan(const vfd_voxel_desc* d, const float* mask_lo, const float* 
   return fail_launch("fusion_plan");
 }
 
-int vfd_fuse_pose_fwd(const vfd_voxel_desc* d, const float* mask_lo, const float* K, const float* Einv,
-                      const float* feats_cl, float* out, void* stream) {
+int vfd_fuse_pose_fwd_t(const vfd_voxel_desc* d, const float* mask_lo, const float* K, const float* Einv,
+                        const float* feats_cl, void* out, int dtype_out, void* stream) {
   int st = check_voxel_desc(d);
   if (st) return st;
   VFD_REQUIRE(d->C >= 1 && d->C <= POSE_MAXC, "fuse_pose: C=%d outside [1, %d]", d->C, POSE_MAXC);
   VFD_REQUIRE(d->N >= 1 && d->N <= 8, "fuse_pose: N=%d outside [1, 8]", d->N);
+  VFD_REQUIRE(dtype_out == 0 || dtype_out == 1, "fuse_pose: dtype_out %d (0 fp32, 1 bf16)", dtype_out);
   hipStream_t s = (hipStream_t)stream;
   const int V = d->X * d->Y * d->Z;
   dim3 grid(VFD_POSE_XCD ? 8 * cdiv(cdiv(V, POSE_TV), 8) : cdiv(V, POSE_TV), d->B);
   ProfScope ps(K_FUSE_POSE_FWD, s);
-  switch (d->N) {
-#define VFD_CASE(n) case n: fuse_pose_fwd_k<n><<<grid, 256, 0, s>>>(*d, mask_lo, K, Einv, feats_cl, out); break;
+  switch (d->N * 2 + dtype_out) {
+#define VFD_CASE(n)                                                                                        \
+  case 2 * n: fuse_pose_fwd_k<n, float><<<grid, 256, 0, s>>>(*d, mask_lo, K, Einv, feats_cl, (float*)out); break; \
+  case 2 * n + 1: fuse_pose_fwd_k<n, __bf16><<<grid, 256, 0, s>>>(*d, mask_lo, K, Einv, feats_cl, (__bf16*)out); break;
     VFD_CASE(1) VFD_CASE(2) VFD_CASE(3) VFD_CASE(4) VFD_CASE(5) VFD_CASE(6) VFD_CASE(7) VFD_CASE(8)
 #undef VFD_CASE
   }
   return fail_launch("fuse_pose_fwd");
+}
+
+int vfd_fuse_pose_fwd(const vfd_voxel_desc* d, const float* mask_lo, const float* K, const float* Einv,
+                      const float* feats_cl, float* out, void* stream) {
+  return vfd_fuse_pose_fwd_t(d, mask_lo, K, Einv, feats_cl, out, 0, stream);
 }
 
 int vfd_fuse_pose_bwd(const vfd_voxel_desc* d, const void* plan, const int* counts, const float* d_out,

@@ -32,6 +32,15 @@ constexpr int PP_FRAG = PP_PIX * PP_O;          // floats of one tile's partial
 constexpr int PP_LDS_MAX = 160 * 1024;
 constexpr int PP_MAXC = 96;                     // contributors of one tile
 constexpr int PP_FSL = 32;                      // fragment slices per tile in the reduce
+#ifndef VFD_PP_ALIGN
+#define VFD_PP_ALIGN 1                          // tile-aligned stream-K splits + XCD numbering (pp_plan)
+#endif
+
+// workgroup -> stream-K group: with ngroup % 8 == 0 XCD k (workgroups k, k + 8, ...) takes the
+// contiguous groups [k ngroup / 8, (k+1) ngroup / 8)
+__device__ __forceinline__ int pp_group(int ngroup) {
+  return (VFD_PP_ALIGN && ngroup % 8 == 0) ? (blockIdx.x % 8) * (ngroup / 8) + blockIdx.x / 8 : blockIdx.x;
+}
 
 struct PpGeom {
   int B, hp, wp, cin, s, ho, wo, mimg, mtiles, nchunk, cq, ntile, natom, ngroup, hrows, lds_floats;
@@ -111,7 +120,7 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppc_main_k(PpGeom g, const floa
                                                            float* __restrict__ partial) {
   constexpr int XS = CC + 4, ITERS = 9 * (CC / 4), PF = CC / 4 < PP_PF ? CC / 4 : PP_PF;
   extern __shared__ float pp_lds[];
-  const int grp = blockIdx.x;
+  const int grp = pp_group(g.ngroup);
   const int a_lo = pp_lo(g, grp), a_hi = pp_lo(g, grp + 1);
   if (a_lo >= a_hi) return;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -226,12 +235,54 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 constexpr int PPB_CC = 32;                      // input channels per atom (16 where 32 do not fit LDS)
 constexpr int PPB_XS = PPB_CC + 8;              // bf16 per staged position (80 B: 16-B aligned)
-constexpr int PPB_PF = 2;                       // weight-fragment prefetch distance (steps)
+#ifndef VFD_PPB_PF
+#define VFD_PPB_PF 3                            // weight-fragment prefetch distance (steps; divides 18)
+#endif
+#ifndef VFD_PPB_U
+#define VFD_PPB_U 16                            // loader: 16-B loads in flight per lane
+#endif
+// The staged rows (~120 KB of the fp32 map per atom) and the weight steps (147 KB) both come from
+// L2 / HBM at ~2 us latency: a CU keeps U x 4 KB of rows and PF steps of fragments in flight, the
+// loader waves having the VGPRs the compute waves need anyway (one workgroup per CU).
 
-template <int CC>
-__device__ __forceinline__ void ppb_stage(const PpGeom& g, __bf16* __restrict__ dst, const float* __restrict__ x,
+// one channel quad of the map as bf16: the fp32 map rounded to nearest even (16-B loads), or the
+// bf16 map K2 writes under config 3 (8-B loads of the same rounded values: C % 4 == 0 keeps a quad
+// 8-B aligned at any position)
+template <typename TX>
+struct PbQuad;
+template <>
+struct PbQuad<float> {
+  typedef float4 V;
+  static __device__ __forceinline__ V zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+  static __device__ __forceinline__ V load(const float* p) { return *reinterpret_cast<const float4*>(p); }
+  static __device__ __forceinline__ bf16x4 cvt(const V& v) {
+    bf16x4 b;
+    b[0] = (__bf16)v.x;
+    b[1] = (__bf16)v.y;
+    b[2] = (__bf16)v.z;
+    b[3] = (__bf16)v.w;
+    return b;
+  }
+};
+template <>
+struct PbQuad<__bf16> {
+  typedef bf16x4 V;
+  static __device__ __forceinline__ V zero() {
+    V z;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) z[e] = (__bf16)0.f;
+    return z;
+  }
+  static __device__ __forceinline__ V load(const __bf16* p) { return *reinterpret_cast<const bf16x4*>(p); }
+  static __device__ __forceinline__ bf16x4 cvt(const V& v) { return v; }
+};
+
+template <int CC, typename TX>
+__device__ __forceinline__ void ppb_stage(const PpGeom& g, __bf16* __restrict__ dst, const TX* __restrict__ x,
                                           int atom, int tid) {
-  constexpr int QP = CC / 4, PPP = 256 / QP, XS = CC + 8;
+  typedef PbQuad<TX> PQ;
+  // loads in flight per lane: U 16-B vectors of the fp32 map, 2U 8-B vectors of the bf16 one
+  constexpr int QP = CC / 4, PPP = 256 / QP, XS = CC + 8, U = VFD_PPB_U * 4 / (int)sizeof(TX);
   const int nchunk = (g.cin + CC - 1) / CC;
   const int t = atom / nchunk, ch = atom - t * nchunk;
   const PpTile tl = pp_tile(g, t);
@@ -239,50 +290,46 @@ __device__ __forceinline__ void ppb_stage(const PpGeom& g, __bf16* __restrict__ 
   const int q = tid % QP;                       // channel quad of the chunk
   const int c = ch * CC + 4 * q;
   const int r0 = g.s * tl.ymin;
-  const float* src = x + ((size_t)tl.b * g.hp + r0) * g.wp * g.cin + c;
+  const TX* src = x + ((size_t)tl.b * g.hp + r0) * g.wp * g.cin + c;
   const bool cok = c < g.cin;                   // cin % 4 == 0: a quad is all in or all out
-  for (int p0 = tid / QP; p0 < npos; p0 += 4 * PPP) {
-    float4 v[4];
+  const int pval = min(npos, (g.hp - r0) * g.wp);  // positions inside the map
+  for (int p0 = tid / QP; p0 < npos; p0 += U * PPP) {
+    typename PQ::V v[U];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int p = p0 + PPP * u;
-      v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (cok && p < npos && r0 + p / g.wp < g.hp)
-        v[u] = *reinterpret_cast<const float4*>(src + (size_t)p * g.cin);
+      v[u] = PQ::zero();
+#ifndef VFD_PPB_NOSTAGE
+      if (cok && p < pval) v[u] = PQ::load(src + (size_t)p * g.cin);
+#endif
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int p = p0 + PPP * u;
-      if (p < npos) {
-        bf16x4 b;
-        b[0] = (__bf16)v[u].x;
-        b[1] = (__bf16)v[u].y;
-        b[2] = (__bf16)v[u].z;
-        b[3] = (__bf16)v[u].w;
-        *reinterpret_cast<bf16x4*>(dst + p * XS + 4 * q) = b;
-      }
+      if (p < npos) *reinterpret_cast<bf16x4*>(dst + p * XS + 4 * q) = PQ::cvt(v[u]);
     }
   }
 }
 
-template <int CC>
-__global__ __launch_bounds__(PP_THREADS, 2) void ppcb_main_k(PpGeom g, const float* __restrict__ x,
+template <int CC, typename TX>
+__global__ __launch_bounds__(PP_THREADS, 2) void ppcb_main_k(PpGeom g, const TX* __restrict__ x,
                                                             const bf16x8* __restrict__ Wf,
                                                             float* __restrict__ partial) {
-  constexpr int XS = CC + 8, STEPS = 9 * (CC / 16), PF = CC / 16 < PPB_PF ? CC / 16 : PPB_PF;
+  constexpr int XS = CC + 8, SPT = CC / 16, STEPS = 9 * SPT, PF = SPT == 2 ? VFD_PPB_PF : 3;
+  static_assert(STEPS % PF == 0, "prefetch ring");
   extern __shared__ __attribute__((aligned(16))) __bf16 ppb_lds[];
-  const int grp = blockIdx.x;
+  const int grp = pp_group(g.ngroup);
   const int a_lo = pp_lo(g, grp), a_hi = pp_lo(g, grp + 1);
   if (a_lo >= a_hi) return;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const bool compute = wv < PP_WAVES;
   const int lds_elems = g.hrows * g.wp * XS;
-  if (!compute) ppb_stage<CC>(g, ppb_lds, x, a_lo, threadIdx.x - 64 * PP_WAVES);
+  if (!compute) ppb_stage<CC, TX>(g, ppb_lds, x, a_lo, threadIdx.x - 64 * PP_WAVES);
   __syncthreads();
   if (!compute) {
     for (int atom = a_lo; atom < a_hi; ++atom) {
       if (atom + 1 < a_hi)
-        ppb_stage<CC>(g, ppb_lds + ((atom + 1 - a_lo) & 1) * lds_elems, x, atom + 1, threadIdx.x - 64 * PP_WAVES);
+        ppb_stage<CC, TX>(g, ppb_lds + ((atom + 1 - a_lo) & 1) * lds_elems, x, atom + 1, threadIdx.x - 64 * PP_WAVES);
       __syncthreads();
     }
     return;
@@ -297,22 +344,26 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppcb_main_k(PpGeom g, const flo
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
   const int nchunk = g.nchunk;                  // CC-channel chunks (host-set for the bf16 form)
   const int nq16 = (g.cin + 31) / 32 * 2;       // 16-channel steps per tap of the fragment copy (C to 32)
-  const bf16x8* wlane = Wf + (size_t)(2 * wv) * 64 + lane;
-  bf16x8 bq[PF][2];
-  int pf_atom = a_lo, pf_it = 0;
-  auto prefetch = [&](int slot) {
-    if (pf_atom < a_hi) {
-      const int ch = pf_atom % nchunk;
-      const int tap = pf_it / (CC / 16), q = pf_it % (CC / 16);
-      const bf16x8* w = wlane + ((size_t)tap * nq16 + ch * (CC / 16) + q) * (PP_O / 32) * 64;
-      bq[slot][0] = w[0];
-      bq[slot][1] = w[64];
-      if (++pf_it == STEPS) { pf_it = 0; ++pf_atom; }
-    }
+  // weight fragments addressed as the uniform base + a 32-bit per-lane byte offset (the fragment
+  // copy is < 4 GB): one VGPR per in-flight step instead of a 64-bit pointer
+  const char* wbase = reinterpret_cast<const char*>(Wf);
+  constexpr unsigned QS = (PP_O / 32) * 64 * 16;   // bytes of one 16-channel step of the copy
+  const unsigned tstride = (unsigned)nq16 * QS;     // one tap
+  const unsigned wlane = (unsigned)(2 * wv * 64 + lane) * 16u;
+  auto wsrc = [&](int atom) { return wlane + (unsigned)(atom % nchunk) * SPT * QS; };
+  // B fragments of step s (tap s / SPT, step s % SPT) of the atom whose fragments start at w
+  auto wld = [&](unsigned w, int s, bf16x8* b) {
+    const unsigned o = w + (unsigned)(s / SPT) * tstride + (unsigned)(s % SPT) * QS;
+    b[0] = *reinterpret_cast<const bf16x8*>(wbase + o);
+    b[1] = *reinterpret_cast<const bf16x8*>(wbase + o + 64u * 16u);
   };
+  bf16x8 bq[PF][2];
+  unsigned wc = wsrc(a_lo);
 #pragma unroll
-  for (int k = 0; k < PF; ++k) prefetch(k);
+  for (int k = 0; k < PF; ++k) wld(wc, k, bq[k]);
   for (int atom = a_lo; atom < a_hi; ++atom) {
+    const bool more = atom + 1 < a_hi;
+    const unsigned wn = more ? wsrc(atom + 1) : 0u;
     const int t = atom / nchunk, ch = atom - t * nchunk;
     const PpTile tl = pp_tile(g, t);
     int aoff[4];
@@ -325,24 +376,33 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppcb_main_k(PpGeom g, const flo
     }
     const __bf16* xb = ppb_lds + ((atom - a_lo) & 1) * lds_elems;
 #pragma unroll 1
-    for (int tap = 0; tap < 9; ++tap) {
-      const int ky = tap / 3, kx = tap - 3 * ky;
+    for (int s0 = 0; s0 < STEPS; s0 += PF)
+#pragma unroll
+    for (int ring = 0; ring < PF; ++ring) {         // STEPS % PF == 0: static ring slots across atoms
+      const int st = s0 + ring;
+      const int tap = st / SPT, q = st % SPT, ky = tap / 3, kx = tap - 3 * ky;
       const __bf16* xt = xb + (ky * g.wp + kx) * XS;
+      bf16x8 af[4];
 #pragma unroll
-      for (int q = 0; q < CC / 16; ++q) {
-        bf16x8 af[4];
+      for (int a = 0; a < 4; ++a) af[a] = *reinterpret_cast<const bf16x8*>(&xt[aoff[a] + 16 * q]);
 #pragma unroll
-        for (int a = 0; a < 4; ++a) af[a] = *reinterpret_cast<const bf16x8*>(&xt[aoff[a] + 16 * q]);
-        const int ring = q % PF;
-        const bf16x8 b0 = bq[ring][0], b1 = bq[ring][1];
-        prefetch(ring);
-#pragma unroll
-        for (int a = 0; a < 4; ++a) {
-          acc[a][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], b0, acc[a][0], 0, 0, 0);
-          acc[a][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], b1, acc[a][1], 0, 0, 0);
-        }
+      for (int a = 0; a < 4; ++a) {
+        acc[a][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bq[ring][0], acc[a][0], 0, 0, 0);
+        acc[a][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bq[ring][1], acc[a][1], 0, 0, 0);
       }
+      // the refill lands in the slot the MFMAs above just read: no register copy, so no wait on
+      // the younger loads of the ring (a copy-out would need them all: s_waitcnt vmcnt(0))
+#ifndef VFD_PPB_NOB
+      if (st + PF < STEPS)
+        wld(wc, st + PF, bq[ring]);
+      else if (more)
+        wld(wn, st + PF - STEPS, bq[ring]);
+#endif
+      // keep the scheduler from hoisting later steps' LDS reads above these MFMAs (register
+      // pressure: the prefetch ring, not the A fragments, is what should hold VGPRs)
+      __builtin_amdgcn_sched_barrier(0);
     }
+    wc = wn;
     __syncthreads();                                  // buffer handed back to the loader waves
     if (ch == nchunk - 1 || atom == a_hi - 1) {
       const int ts = t * nchunk;
@@ -442,6 +502,18 @@ static bool pp_plan(const vfd_conv_desc& d, PpGeom* out, int cc = PP_CC, int xs_
   int most = g.natom / min_range;
   most = most > 0 ? most : 1;
   g.ngroup = res < most ? res : most;
+#if VFD_PP_ALIGN
+  // fewer tiles than CUs: every tile cut into the same ksplit chunk ranges (group t * ksplit + j
+  // takes chunks [j nchunk / ksplit, (j+1) nchunk / ksplit) of tile t), so the groups of one split
+  // read the same weight fragments at the same time; with the XCD numbering of the main kernels
+  // the tiles of one XCD share its L2 copy instead of every CU streaming its own from HBM / MALL
+  if (g.ntile <= res) {
+    int ks = res / g.ntile;
+    ks = ks < g.nchunk ? ks : g.nchunk;
+    ks = ks < PP_MAXC - 1 ? ks : PP_MAXC - 1;
+    g.ngroup = g.ntile * ks;
+  }
+#endif
   *out = g;
   return true;
 }
@@ -497,6 +569,12 @@ struct PgVecP<__bf16> {
 // with one class of 9 taps.  Whole tiles are stored directly (every padded position belongs to
 // exactly one class, so dXp is written in full, zeros included); split tiles summed in group order
 // by ppd_reduce_k (deterministic).
+#ifndef VFD_PD_U
+#define VFD_PD_U 12                             // loader: 16-B loads in flight per lane (one batch per atom)
+#endif
+#ifndef VFD_PD_BF_PF
+#define VFD_PD_BF_PF 4                          // bf16 B-fragment prefetch distance (steps: one tap ahead)
+#endif
 template <typename T>
 struct PdCfg;
 template <>
@@ -505,7 +583,7 @@ struct PdCfg<float> {
 };                                                            // B prefetch distance (steps, <= STEPS)
 template <>
 struct PdCfg<__bf16> {
-  static constexpr int OC = 64, XS = 72, STEPS = 4, PF = 2;
+  static constexpr int OC = 64, XS = 72, STEPS = 4, PF = VFD_PD_BF_PF;
 };
 
 constexpr int PD2_PIX = 256;                    // positions per tile (8 blocks of 32)
@@ -582,18 +660,23 @@ __device__ __forceinline__ void pdc_stage(const PdcGeom& g, T* __restrict__ dst,
   const int npos = g.hrows * g.cols;
   const int q = tid % QP;
   const TG* src = gp + (size_t)tl.b * g.ho * g.wo * PP_O + ch * OC + CH * q;
-  for (int p0 = tid / QP; p0 < npos; p0 += 8 * PPP) {
-    typename PV::V v[8];
+  constexpr int U = VFD_PD_U;
+  for (int p0 = tid / QP; p0 < npos; p0 += U * PPP) {
+    typename PV::V v[U];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int p = p0 + PPP * u;
       const int r = p / g.cols, c = p - r * g.cols;
       const int y = r0 + r, x = c - c0;
+#ifdef VFD_PD_NOSTAGE
+      v[u] = PV::zero();
+#else
       v[u] = (p < npos && y >= 0 && y < g.ho && x >= 0 && x < g.wo) ? PV::load(src + ((size_t)y * g.wo + x) * PP_O)
                                                                    : PV::zero();
+#endif
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int p = p0 + PPP * u;
       if (p < npos) PV::template put<T>(dst + p * XS + CH * q, v[u]);
     }
@@ -626,13 +709,20 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppd_main_k(PdcGeom g, const TG*
     return;
   }
   const int li = lane & 31, lh = lane >> 5;
-  f32x16 acc[8];
+  // 2 x 2 wave grid over the 256 x 128 tile: wave (wm, wn) owns pixel blocks 4 wm .. 4 wm + 3 and
+  // map-channel blocks 2 wn, 2 wn + 1 — every A fragment read from LDS feeds two MFMAs
+  constexpr int MB = 4, NB = 2;
+  const int wm = wv >> 1, wn = wv & 1;
+  f32x16 acc[MB][NB];
 #pragma unroll
-  for (int a = 0; a < 8; ++a)
+  for (int a = 0; a < MB; ++a)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[a][r] = 0.f;
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
   const Frag* wf = reinterpret_cast<const Frag*>(Wd);
-  // B fragment of (atom, tap tl, step q): the weight copy's tap slot 8 - (3 ky + kx)
+  // B fragments of (atom, tap tl, step q): the weight copy's tap slot 8 - (3 ky + kx); the wave's
+  // second channel block 64 fragments on
   auto bptr = [&](int atom, int tl) -> const Frag* {
     const int t = atom / g.och, ch = atom - t * g.och;
     const PdcTile tt = pdc_tile(g, t);
@@ -640,15 +730,17 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppd_main_k(PdcGeom g, const TG*
     pdc_tap(g, tt.c, tl, &ky, &kx);
     const int slot = 8 - (3 * ky + kx);
     if constexpr (BF)
-      return wf + (((size_t)slot * (PP_O / 16) + ch * STEPS) * (g.np / 32) + tt.nt * (PD2_N / 32) + wv) * 64 + lane;
+      return wf + (((size_t)slot * (PP_O / 16) + ch * STEPS) * (g.np / 32) + tt.nt * (PD2_N / 32) + 2 * wn) * 64 + lane;
     else
-      return wf + (((size_t)slot * (PP_O / 4) + ch * STEPS) * g.np + tt.nt * PD2_N + wv * 32 + li) * 2 + lh;
+      return wf + (((size_t)slot * (PP_O / 4) + ch * STEPS) * g.np + tt.nt * PD2_N + wn * 64 + li) * 2 + lh;
   };
   const size_t qstride = BF ? (size_t)(g.np / 32) * 64 : (size_t)g.np * 2;
-  Frag bq[PF];
+  Frag bq[PF][NB];
   const Frag* btap = bptr(a_lo, 0);                  // the current tap's fragments (step 0)
 #pragma unroll
-  for (int q = 0; q < PF; ++q) bq[q] = btap[q * qstride];
+  for (int q = 0; q < PF; ++q)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) bq[q][b] = btap[q * qstride + 64 * b];
   constexpr int LH = BF ? 8 : 2;
   for (int atom = a_lo; atom < a_hi; ++atom) {
     const int t = atom / g.och, ch = atom - t * g.och;
@@ -656,10 +748,11 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppd_main_k(PdcGeom g, const TG*
     const int hw = g.hc[tl.c] * g.wc[tl.c], wcc = g.wc[tl.c];
     const int ntap = g.ntap[tl.c];
     const int rbase = tl.i0 - (g.s == 1 ? 2 : 1), cbase = g.s == 1 ? 2 : 1;
-    int pij[8];                                       // (class row << 16) | class column of the lane's positions
+    const int m0w = tl.m0 + 32 * MB * wm;             // the wave's first position
+    int pij[MB];                                      // (class row << 16) | class column of the lane's positions
 #pragma unroll
-    for (int a = 0; a < 8; ++a) {
-      int m = tl.m0 + 32 * a + li;
+    for (int a = 0; a < MB; ++a) {
+      int m = m0w + 32 * a + li;
       m = m < hw ? m : hw - 1;
       const int i = m / wcc;
       pij[a] = (i << 16) | (m - i * wcc);
@@ -672,16 +765,16 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppd_main_k(PdcGeom g, const TG*
       // stride 1: Y - ky with Y = i (staged from row i0 - 2)
       const int dy = g.s == 1 ? ky : (ky == 2 ? 1 : 0), dxo = g.s == 1 ? kx : (kx == 2 ? 1 : 0);
 #pragma unroll
-      for (int a = 0; a < 8; ++a) {
+      for (int a = 0; a < MB; ++a) {
         const int i = pij[a] >> 16, j = pij[a] & 0xFFFF;
         o1[a] = ((i - dy - rbase) * g.cols + (j - dxo + cbase)) * XS + LH * lh;
       }
     };
-    int o1c[8];
+    int o1c[MB];
     offsets(0, o1c);
-    Frag afc[8], afn[8];
+    Frag afc[MB], afn[MB];
 #pragma unroll
-    for (int a = 0; a < 8; ++a) afc[a] = *reinterpret_cast<const Frag*>(&xb[o1c[a]]);
+    for (int a = 0; a < MB; ++a) afc[a] = *reinterpret_cast<const Frag*>(&xb[o1c[a]]);
     const bool more = atom + 1 < a_hi;
 #pragma unroll 1
     for (int tp = 0; tp < ntap; ++tp) {
@@ -689,61 +782,88 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppd_main_k(PdcGeom g, const TG*
       const Frag* bn = tp + 1 < ntap ? bptr(atom, tp + 1) : (more ? bptr(atom + 1, 0) : nullptr);
 #pragma unroll
       for (int q = 0; q < STEPS; ++q) {
-        const Frag b = bq[q % PF];
-        if (q + PF < STEPS)
-          bq[q % PF] = btap[(q + PF) * qstride];
-        else if (bn)
-          bq[q % PF] = bn[(q + PF - STEPS) * qstride];
         if (q < STEPS - 1) {
 #pragma unroll
-          for (int a = 0; a < 8; ++a) afn[a] = *reinterpret_cast<const Frag*>(&xb[o1c[a] + (OC / STEPS) * (q + 1)]);
+          for (int a = 0; a < MB; ++a) afn[a] = *reinterpret_cast<const Frag*>(&xb[o1c[a] + (OC / STEPS) * (q + 1)]);
         } else if (tp + 1 < ntap) {
           offsets(tp + 1, o1c);
 #pragma unroll
-          for (int a = 0; a < 8; ++a) afn[a] = *reinterpret_cast<const Frag*>(&xb[o1c[a]]);
+          for (int a = 0; a < MB; ++a) afn[a] = *reinterpret_cast<const Frag*>(&xb[o1c[a]]);
         }
         if constexpr (BF) {
 #pragma unroll
-          for (int a = 0; a < 8; ++a) acc[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afc[a], b, acc[a], 0, 0, 0);
+          for (int a = 0; a < MB; ++a)
+#pragma unroll
+            for (int b = 0; b < NB; ++b)
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afc[a], bq[q % PF][b], acc[a][b], 0, 0, 0);
         } else {
 #pragma unroll
           for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-            for (int a = 0; a < 8; ++a)
-              acc[a] = __builtin_amdgcn_mfma_f32_32x32x2f32(s2 ? afc[a].y : afc[a].x, s2 ? b.y : b.x, acc[a], 0, 0, 0);
-        }
+            for (int a = 0; a < MB; ++a)
 #pragma unroll
-        for (int a = 0; a < 8; ++a) afc[a] = afn[a];
+              for (int b = 0; b < NB; ++b)
+                acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(s2 ? afc[a].y : afc[a].x,
+                                                                 s2 ? bq[q % PF][b].y : bq[q % PF][b].x, acc[a][b], 0, 0, 0);
+        }
+        // refill the slots just read (no copy-out of the ring: see ppcb_main_k)
+#ifndef VFD_PD_NOB
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+          if (q + PF < STEPS)
+            bq[q % PF][b] = btap[(q + PF) * qstride + 64 * b];
+          else if (bn)
+            bq[q % PF][b] = bn[(q + PF - STEPS) * qstride + 64 * b];
+        }
+#endif
+#pragma unroll
+        for (int a = 0; a < MB; ++a) afc[a] = afn[a];
       }
       btap = bn;
     }
     __syncthreads();                                  // buffer handed back to the loader waves
     if (ch == g.och - 1 || atom == a_hi - 1) {
       const int ts = t * g.och;
-      const int n = tl.nt * PD2_N + wv * 32 + li;
+      const int n0 = tl.nt * PD2_N + wn * 64 + li;
       const int py = g.py[tl.c], px = g.px[tl.c], st = g.s;
       if (ts >= a_lo && ts + g.och <= a_hi) {         // whole tile in this range: store
+        // one division per pixel block: element r sits d = (r & 3) + 8 (r >> 2) <= 27 positions
+        // after the block's first, at most one class-row wrap when the class grid is >= 28 wide
+        const long long rowp = (long long)st * g.wp * g.cin, colp = (long long)st * g.cin;
 #pragma unroll
-        for (int a = 0; a < 8; ++a)
+        for (int a = 0; a < MB; ++a) {
+          const int mb = m0w + 32 * a + 4 * lh;
+          const int ib = mb / wcc, jb = mb - ib * wcc;
+          float* pa = dx + (((size_t)tl.b * g.hp + st * ib + py) * g.wp + st * jb + px) * g.cin + n0;
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const int m = tl.m0 + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * lh;
-            if (m < hw && n < g.cin) {
-              const int i = m / wcc, j = m - i * wcc;
-              dx[(((size_t)tl.b * g.hp + st * i + py) * g.wp + st * j + px) * g.cin + n] = acc[a][r];
+            const int d = (r & 3) + 8 * (r >> 2);
+            long long off;
+            if (wcc >= 28) {
+              off = d * colp + (jb + d >= wcc ? rowp - wcc * colp : 0);
+            } else {
+              const int i2 = (mb + d) / wcc, j2 = mb + d - i2 * wcc;
+              off = (i2 - ib) * rowp + (j2 - jb) * colp;
             }
-            acc[a][r] = 0.f;
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+              if (mb + d < hw && n0 + 32 * b < g.cin) pa[off + 32 * b] = acc[a][b][r];
+              acc[a][b][r] = 0.f;
+            }
           }
+        }
       } else {
         const int slot = t == a_lo / g.och ? 0 : 1;
         float* dst = partial + ((size_t)grp * 2 + slot) * PD2_FRAG + (size_t)wv * (PD2_FRAG / PP_WAVES) + lane;
 #pragma unroll
-        for (int a = 0; a < 8; ++a)
+        for (int a = 0; a < MB; ++a)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            dst[(a * 16 + r) * 64] = acc[a][r];
-            acc[a][r] = 0.f;
-          }
+          for (int b = 0; b < NB; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              dst[((a * NB + b) * 16 + r) * 64] = acc[a][b][r];
+              acc[a][b][r] = 0.f;
+            }
       }
     }
   }
@@ -760,15 +880,18 @@ __global__ __launch_bounds__(256) void ppd_reduce_k(PdcGeom g, const float* __re
   const int hw = g.hc[tl.c] * g.wc[tl.c], wcc = g.wc[tl.c];
   constexpr int FSL = 8, FPS = 8 * 16 / FSL, U = 4;
   const int contrib[2] = {c0, c1};
-  const int n = tl.nt * PD2_N + wv * 32 + (lane & 31);
+  // slice wv = wave (wm, wn) of ppd_main_k: fragment f = (a, b, r) -> pixel block 4 wm + a,
+  // channel block 2 wn + b
+  const int wm = wv >> 1, wn = wv & 1;
   for (int fu = blockIdx.y * FPS; fu < (blockIdx.y + 1) * FPS; fu += U) {
     float su[U];
     frag_sums<U>(partial, contrib, 2, PD2_FRAG, (size_t)wv * (PD2_FRAG / PP_WAVES) + (fu * 64 + lane), su);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int f = fu + u;
-      const int a = f >> 4, r = f & 15;
-      const int m = tl.m0 + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      const int a = f >> 5, b = (f >> 4) & 1, r = f & 15;
+      const int n = tl.nt * PD2_N + wn * 64 + 32 * b + (lane & 31);
+      const int m = tl.m0 + 32 * (4 * wm + a) + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
       if (m < hw && n < g.cin) {
         const int i = m / wcc, j = m - i * wcc;
         dx[(((size_t)tl.b * g.hp + g.s * i + g.py[tl.c]) * g.wp + g.s * j + g.px[tl.c]) * g.cin + n] = su[u];
@@ -886,9 +1009,10 @@ size_t vfd_pad_conv_fwd_bf16_workspace(const vfd_conv_desc* d) {
   return ((size_t)g.ngroup * 2 + g.ntile) * PP_FRAG * sizeof(float);
 }
 
-int vfd_pad_conv_fwd_bf16(const vfd_conv_desc* d, const float* x, const void* Wf, const float* bias, void* out,
-                          void* ws, size_t ws_bytes, void* stream) {
+int vfd_pad_conv_fwd_bf16_t(const vfd_conv_desc* d, const void* x, int dtype_x, const void* Wf, const float* bias,
+                            void* out, void* ws, size_t ws_bytes, void* stream) {
   VFD_REQUIRE(d && x && Wf && bias && out, "pad_conv_fwd_bf16: null argument");
+  VFD_REQUIRE(dtype_x == 0 || dtype_x == 1, "pad_conv_fwd_bf16: dtype_x %d (0 fp32, 1 bf16)", dtype_x);
   PpGeom g;
   const int cc = ppb_cc(*d, &g);
   VFD_REQUIRE(cc, "pad_conv_fwd_bf16: unsupported shape (C %% 4 == 0, stride 1 or 2, "
@@ -898,15 +1022,27 @@ int vfd_pad_conv_fwd_bf16(const vfd_conv_desc* d, const float* x, const void* Wf
   ProfScope ps(K_PAD_CONV_FWD, s);
   float* partial = (float*)ws;
   const size_t lds = (size_t)2 * g.hrows * g.wp * (cc + 8) * 2;
-  if (cc == 16) {
-    lds_attr(reinterpret_cast<const void*>(ppcb_main_k<16>), PP_LDS_MAX);
-    ppcb_main_k<16><<<g.ngroup, PP_THREADS, lds, s>>>(g, x, (const bf16x8*)Wf, partial);
+  const bf16x8* wf = (const bf16x8*)Wf;
+#define VFD_PPB_LAUNCH(CCV, TXT)                                                              \
+  lds_attr(reinterpret_cast<const void*>(ppcb_main_k<CCV, TXT>), PP_LDS_MAX);                 \
+  ppcb_main_k<CCV, TXT><<<g.ngroup, PP_THREADS, lds, s>>>(g, (const TXT*)x, wf, partial);
+  if (cc == 16 && dtype_x == 0) {
+    VFD_PPB_LAUNCH(16, float)
+  } else if (cc == 16) {
+    VFD_PPB_LAUNCH(16, __bf16)
+  } else if (dtype_x == 0) {
+    VFD_PPB_LAUNCH(PPB_CC, float)
   } else {
-    lds_attr(reinterpret_cast<const void*>(ppcb_main_k<PPB_CC>), PP_LDS_MAX);
-    ppcb_main_k<PPB_CC><<<g.ngroup, PP_THREADS, lds, s>>>(g, x, (const bf16x8*)Wf, partial);
+    VFD_PPB_LAUNCH(PPB_CC, __bf16)
   }
+#undef VFD_PPB_LAUNCH
   ppc_reduce_k<__bf16><<<dim3(g.ntile, PP_FSL), 256, 0, s>>>(g, partial, bias, (__bf16*)out);
   return fail_launch("pad_conv_fwd_bf16");
+}
+
+int vfd_pad_conv_fwd_bf16(const vfd_conv_desc* d, const float* x, const void* Wf, const float* bias, void* out,
+                          void* ws, size_t ws_bytes, void* stream) {
+  return vfd_pad_conv_fwd_bf16_t(d, x, 0, Wf, bias, out, ws, ws_bytes, stream);
 }
 
 size_t vfd_pad_conv_dgrad_workspace(const vfd_conv_desc* d) {

@@ -2047,17 +2047,25 @@ __host__ __device__ inline long long wb_lo(const WbGeom& g, int grp) { return ((
 
 typedef short wb_s4 __attribute__((ext_vector_type(4)));
 
-template <typename TX>
-struct WbStage {
-  uint4 gv[WB_PIX * PC_O / 8 / PC_THREADS];                         // 4 x 8 bf16 of G
-  typename std::conditional<sizeof(TX) == 2, uint4, float4>::type xv[(WB_XMAX * WB_XP / (16 / sizeof(TX)) + PC_THREADS - 1) / PC_THREADS];
+// X vectors: XV channels of TX per load — 8 bf16 (16 B) or 4 fp32 (16 B, rounded when put), or
+// 4 bf16 (8 B) for the bf16 BEV map of K2C (C = 5140: a multiple of 4, not of 8)
+template <typename TX, int XV>
+struct WbXVec {
+  typedef typename std::conditional<sizeof(TX) == 2, typename std::conditional<XV == 8, uint4, uint2>::type,
+                                    float4>::type type;
 };
 
-template <typename TX>
-__device__ __forceinline__ void wb_fetch(const WbGeom& g, WbStage<TX>& st, const __bf16* __restrict__ gp,
+template <typename TX, int XV>
+struct WbStage {
+  uint4 gv[WB_PIX * PC_O / 8 / PC_THREADS];                         // 4 x 8 bf16 of G
+  typename WbXVec<TX, XV>::type xv[(WB_XMAX * WB_XP / XV + PC_THREADS - 1) / PC_THREADS];
+};
+
+template <typename TX, int XV>
+__device__ __forceinline__ void wb_fetch(const WbGeom& g, WbStage<TX, XV>& st, const __bf16* __restrict__ gp,
                                          const TX* __restrict__ xp, int atom, int tid) {
-  constexpr int XV = 16 / sizeof(TX);                               // channels per 16-B vector of X
   constexpr int NXV = sizeof(st.xv) / sizeof(st.xv[0]);
+  typedef typename WbXVec<TX, XV>::type XT;
   const int t = atom / g.L, within = atom - t * g.L;
   const int img = within / g.tiles_img, ti = within - img * g.tiles_img;
   const int y0 = (ti / g.tc) * WB_TR, x0 = (ti % g.tc) * WB_TC;
@@ -2077,15 +2085,14 @@ __device__ __forceinline__ void wb_fetch(const WbGeom& g, WbStage<TX>& st, const
     const int Y = g.s * y0 + r, X = g.s * x0 + c, n = t * 32 + XV * q;
     memset(&st.xv[u], 0, sizeof(st.xv[u]));
     if (pos < npos && Y < g.hp && X < g.wp && n < g.C)
-      st.xv[u] = *reinterpret_cast<const typename std::remove_reference<decltype(st.xv[0])>::type*>(
-          xp + (((size_t)img * g.hp + Y) * g.wp + X) * g.C + n);
+      st.xv[u] = *reinterpret_cast<const XT*>(xp + (((size_t)img * g.hp + Y) * g.wp + X) * g.C + n);
   }
 }
 
-template <typename TX>
-__device__ __forceinline__ void wb_put(const WbGeom& g, const WbStage<TX>& st, __bf16* __restrict__ dst, int tid) {
-  constexpr int XV = 16 / sizeof(TX);
+template <typename TX, int XV>
+__device__ __forceinline__ void wb_put(const WbGeom& g, const WbStage<TX, XV>& st, __bf16* __restrict__ dst, int tid) {
   constexpr int NXV = sizeof(st.xv) / sizeof(st.xv[0]);
+  typedef typename WbXVec<TX, XV>::type XT;
 #pragma unroll
   for (int u = 0; u < (int)(sizeof(st.gv) / sizeof(st.gv[0])); ++u) {
     const int e = tid + PC_THREADS * u, px = e >> 5, q = e & 31;
@@ -2098,7 +2105,7 @@ __device__ __forceinline__ void wb_put(const WbGeom& g, const WbStage<TX>& st, _
     const int e = tid + PC_THREADS * u, pos = e / vpp, q = e - pos * vpp;
     if (pos < npos) {
       if constexpr (sizeof(TX) == 2) {
-        *reinterpret_cast<uint4*>(xd + pos * WB_XP + XV * q) = st.xv[u];
+        *reinterpret_cast<XT*>(xd + pos * WB_XP + XV * q) = st.xv[u];
       } else {
         bf16x4 b;
         b[0] = (__bf16)st.xv[u].x;
@@ -2121,7 +2128,7 @@ __device__ __forceinline__ bf16x8 wb_tr8(const __bf16* p0, const __bf16* p1) {
   return r;
 }
 
-template <typename TX>
+template <typename TX, int XV = 16 / sizeof(TX)>
 __global__ __launch_bounds__(PC_THREADS, 2) void pwb_main_k(WbGeom g, const __bf16* __restrict__ gp,
                                                            const TX* __restrict__ xp, float* __restrict__ partial) {
   __shared__ __attribute__((aligned(16))) __bf16 lds[2 * WB_BUF];
@@ -2130,9 +2137,9 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pwb_main_k(WbGeom g, const __bf
   if (a_lo >= a_hi) return;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   {
-    WbStage<TX> st;
-    wb_fetch<TX>(g, st, gp, xp, a_lo, tid);
-    wb_put<TX>(g, st, lds, tid);
+    WbStage<TX, XV> st;
+    wb_fetch<TX, XV>(g, st, gp, xp, a_lo, tid);
+    wb_put<TX, XV>(g, st, lds, tid);
   }
   __syncthreads();
   f32x16 acc[9];
@@ -2162,9 +2169,9 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pwb_main_k(WbGeom g, const __bf
       flush(tile);
       tile = t;
     }
-    WbStage<TX> st;
+    WbStage<TX, XV> st;
     const bool more = atom + 1 < a_hi;
-    if (more) wb_fetch<TX>(g, st, gp, xp, atom + 1, tid);           // in flight during this atom's MFMAs
+    if (more) wb_fetch<TX, XV>(g, st, gp, xp, atom + 1, tid);           // in flight during this atom's MFMAs
     const __bf16* gb = lds + ((atom - a_lo) & 1) * WB_BUF;
     const __bf16* xb = gb + WB_PIX * WB_GP;
 #pragma unroll 1
@@ -2181,7 +2188,7 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pwb_main_k(WbGeom g, const __bf
         acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[k], 0, 0, 0);
       }
     }
-    if (more) wb_put<TX>(g, st, lds + ((atom + 1 - a_lo) & 1) * WB_BUF, tid);
+    if (more) wb_put<TX, XV>(g, st, lds + ((atom + 1 - a_lo) & 1) * WB_BUF, tid);
     __syncthreads();
   }
   flush(tile);
@@ -2491,9 +2498,10 @@ size_t vfd_pad_conv_wgrad_bf16_workspace(const vfd_conv_desc* d) {
   return ((size_t)g.ngroup * g.slots * PW_FRAG + (size_t)nblk * PC_O) * sizeof(float);
 }
 
-int vfd_pad_conv_wgrad_bf16(const vfd_conv_desc* d, const void* g_pre, const float* x, float* dw_map, float* db,
-                            void* ws, size_t ws_bytes, void* stream) {
+int vfd_pad_conv_wgrad_bf16_t(const vfd_conv_desc* d, const void* g_pre, const void* x, int dtype_x, float* dw_map,
+                              float* db, void* ws, size_t ws_bytes, void* stream) {
   VFD_REQUIRE(d && g_pre && x && (dw_map || db), "pad_conv_wgrad_bf16: null argument");
+  VFD_REQUIRE(dtype_x == 0 || dtype_x == 1, "pad_conv_wgrad_bf16: dtype_x %d (0 fp32, 1 bf16)", dtype_x);
   const size_t need = vfd_pad_conv_wgrad_bf16_workspace(d);
   VFD_REQUIRE(need, "pad_conv_wgrad_bf16: unsupported shape (C %% 4 == 0, stride 1 or 2, %d outputs)", PC_O);
   VFD_REQUIRE(ws && ws_bytes >= need, "pad_conv_wgrad_bf16: workspace too small");
@@ -2503,7 +2511,12 @@ int vfd_pad_conv_wgrad_bf16(const vfd_conv_desc* d, const void* g_pre, const flo
   const WbGeom g = wb_plan(d->B, ho, wo, d->H, d->W, d->stride, d->C);
   float* partial = (float*)ws;
   if (dw_map) {
-    pwb_main_k<float><<<g.ngroup, PC_THREADS, 0, s>>>(g, (const __bf16*)g_pre, x, partial);
+    if (dtype_x == 0)
+      pwb_main_k<float><<<g.ngroup, PC_THREADS, 0, s>>>(g, (const __bf16*)g_pre, (const float*)x, partial);
+    else if (d->C % 8 == 0)
+      pwb_main_k<__bf16, 8><<<g.ngroup, PC_THREADS, 0, s>>>(g, (const __bf16*)g_pre, (const __bf16*)x, partial);
+    else
+      pwb_main_k<__bf16, 4><<<g.ngroup, PC_THREADS, 0, s>>>(g, (const __bf16*)g_pre, (const __bf16*)x, partial);
     pwb_reduce_map_k<<<dim3(g.ntile, PC_O / 32), 256, 0, s>>>(g, partial, dw_map);
   }
   if (db) {
@@ -2513,6 +2526,11 @@ int vfd_pad_conv_wgrad_bf16(const vfd_conv_desc* d, const void* g_pre, const flo
     pcw_bias_fin_k<<<PC_O / 4, 256, 0, s>>>(nblk, part, db);
   }
   return fail_launch("pad_conv_wgrad_bf16");
+}
+
+int vfd_pad_conv_wgrad_bf16(const vfd_conv_desc* d, const void* g_pre, const float* x, float* dw_map, float* db,
+                            void* ws, size_t ws_bytes, void* stream) {
+  return vfd_pad_conv_wgrad_bf16_t(d, g_pre, x, 0, dw_map, db, ws, ws_bytes, stream);
 }
 
 }  // extern "C"

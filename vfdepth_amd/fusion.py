@@ -252,8 +252,27 @@ class VFNet(nn.Module):
                 inputs['extrinsics_aug'] = fusion_dict['extrinsics_aug'] = ext_aug
                 fusion_dict['proj_feat_aug'] = self.project_voxel_into_image(vox, inv_K, ext_aug)
             return fusion_dict
+        if self.pose_conv_bf16(space, feats_agg):
+            # config 3: K2 writes the map in bf16 for the bf16 K2C, one autograd node (kernels.py)
+            c0, c1 = self.reduce_dim[0], self.reduce_dim[3]
+            C1, Z = self.feat_in_dim + 1, self.z_dim
+            wf = _GEOMETRY_CACHE.get(('pose_wf_bf16', id(c0.weight)), (c0.weight,),
+                                     lambda: KN.pad_conv_weight_fragments_bf16(c0.weight.detach(), C1, Z))
+            y0 = KN.PoseConvBF16.apply(space, self._plan(inputs, space), feats_agg, c0.weight, c0.bias,
+                                       self.stride, wf, (C1, Z))
+            return F.leaky_relu(F.conv2d(y0, c1.weight, c1.bias, stride=self.stride), 0.1,
+                                inplace=True).contiguous()
         vox = KN.FusePose.apply(space, self._plan(inputs, space), feats_agg)
         return self._reduce(vox)
+
+    def pose_conv_bf16(self, space, feats_agg):
+        """K2 + K2C on the bf16 map (PoseConvBF16) applies: K2C's bf16 form would run (bf16
+        autocast, 256 outputs), its three kernels accept the map, not disabled by
+        VFD_POSE_BF16_MAP=0 (or VFD_PAD_CONV / VFD_PAD_CONV_BF16 = 0)."""
+        return (os.environ.get('VFD_POSE_BF16_MAP', '1') != '0' and os.environ.get('VFD_PAD_CONV', '1') != '0'
+                and os.environ.get('VFD_PAD_CONV_BF16', '1') != '0' and self.reduce_dim[0].out_channels == 256
+                and torch.is_autocast_enabled('cuda') and torch.get_autocast_dtype('cuda') == torch.bfloat16
+                and KN.pose_conv_bf16_supported(space, feats_agg.shape[0], feats_agg.shape[2], self.stride, 256))
 
 
 __all__ = ['VFNet', 'pack_cam_feat']

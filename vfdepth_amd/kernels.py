@@ -528,8 +528,9 @@ _PAD_WGRAD = os.environ.get('VFD_PAD_WGRAD', '1') != '0'    # bf16 K2C weight gr
 
 def pad_conv_wgrad_bf16(gb, x, w, stride, need_w=True, need_b=True):
     """K2C's bf16 weight / bias gradient through the C ABI: gb [B, 256, Ho, Wo] bf16 channels-last
-    (d pre-activation), x the fp32 channels-last map [B, C, H, W] -> (d w in the MAP's channel
-    order [256, C, 3, 3] fp32, d b [256] fp32); (None, None) parts not asked for."""
+    (d pre-activation), x the channels-last map [B, C, H, W] (fp32, or the bf16 map of PoseConvBF16)
+    -> (d w in the MAP's channel order [256, C, 3, 3] fp32, d b [256] fp32); (None, None) parts not
+    asked for."""
     lib = L.load()
     B, C, H, W = x.shape
     d = L.ConvDesc(B, H, W, C, stride, gb.shape[1])
@@ -540,9 +541,9 @@ def pad_conv_wgrad_bf16(gb, x, w, stride, need_w=True, need_b=True):
     db = torch.empty(gb.shape[1], device=gb.device) if need_b else None
     ws = _ws(nbytes, gb.device)
     gb = _nhwc(gb.to(torch.bfloat16), 'grad')
-    x = _nhwc(x.float(), 'map')
-    L.check(lib.vfd_pad_conv_wgrad_bf16(ctypes.byref(d), gb.data_ptr(), x.data_ptr(), L.ptr(dw), L.ptr(db),
-                                        ws.data_ptr(), nbytes, L.stream()), 'pad_conv_wgrad_bf16')
+    x = _nhwc(x if x.dtype == torch.bfloat16 else x.float(), 'map')
+    L.check(lib.vfd_pad_conv_wgrad_bf16_t(ctypes.byref(d), gb.data_ptr(), x.data_ptr(), _DT[x.dtype], L.ptr(dw),
+                                          L.ptr(db), ws.data_ptr(), nbytes, L.stream()), 'pad_conv_wgrad_bf16')
     return dw, db
 
 
@@ -695,6 +696,92 @@ class PadConvBF16(torch.autograd.Function):
 
 
 _DT = {torch.float32: 0, torch.bfloat16: 1}
+
+
+def _pose_fuse_t(space, plan, feats, dtype):
+    """K2 forward into a fresh map of `dtype` (fusion.hip fuse_pose_fwd_k) -> (map, desc shape)."""
+    lib = L.load()
+    feats = _dev(feats, 'feats')
+    B, N, C = feats.shape[:3]
+    feats_cl = feats.flatten(3).transpose(2, 3).contiguous()        # [B, N, h*w, C]
+    out = torch.empty(B, (C + 1) * space.Z, space.Y + 2, space.X + 2, device=feats.device, dtype=dtype,
+                      memory_format=torch.channels_last)
+    d = space.desc(B, N, C=C)
+    L.check(lib.vfd_fuse_pose_fwd_t(ctypes.byref(d), plan.mask_lo.data_ptr(), plan.K.data_ptr(),
+                                    plan.Einv.data_ptr(), feats_cl.data_ptr(), out.data_ptr(), _DT[dtype],
+                                    L.stream()), 'fuse_pose_fwd')
+    return out
+
+
+def _pose_unfuse(space, plan, shape, g):
+    """K2 backward: d map (fp32 channels-last) -> d feats [B, N, C, h, w] (fuse_pose_bwd_k)."""
+    lib = L.load()
+    B, N, C = shape[:3]
+    g = _channels_last(g, 'grad')
+    dfeats = torch.empty(shape, device=g.device)
+    d = space.desc(B, N, C=C)
+    plan.build().wait()
+    L.check(lib.vfd_fuse_pose_bwd(ctypes.byref(d), plan.buf.data_ptr(), plan.counts.data_ptr(),
+                                  g.data_ptr(), dfeats.data_ptr(), L.stream()), 'fuse_pose_bwd')
+    return dfeats
+
+
+def pose_conv_bf16_supported(space, B, C, stride, out_channels):
+    """PoseConvBF16 applies: the bf16 map's K2C forward / weight gradient accept its shape."""
+    shape = (B, (C + 1) * space.Z, space.Y + 2, space.X + 2)
+    d = L.ConvDesc(shape[0], shape[2], shape[3], shape[1], stride, out_channels)
+    lib = L.load()
+    return bool(_PC_BF16_BWD and _PAD_DGRAD and _PAD_WGRAD and lib.vfd_pad_conv_fwd_bf16_workspace(ctypes.byref(d))
+                and lib.vfd_pad_conv_wgrad_bf16_workspace(ctypes.byref(d))
+                and lib.vfd_pad_conv_dgrad_bf16_workspace(ctypes.byref(d)))
+
+
+class PoseConvBF16(torch.autograd.Function):
+    """K2 + K2C under config 3 as one autograd node: the pose gather writes the BEV map in bf16 —
+    exactly the values the bf16 K2C stages from the fp32 map (rounded to nearest even), so the conv,
+    its weight gradient and the map's gradient are those of FusePose -> PadConvBF16 — at half the
+    map's bytes (written by K2, read by the conv's forward and weight gradient).  The map stays
+    inside this node, so its gradient (the K2C data gradient, fp32) goes straight into K2's
+    backward with no dtype round trip.  Output: LeakyReLU(conv + bias) bf16, reflect-padded
+    channels-last [B, 256, Ho+2, Wo+2] (as PadConvBF16)."""
+
+    @staticmethod
+    def forward(ctx, space, plan, feats, w, bias, stride, wf, perm):
+        lib = L.load()
+        feats = feats.float()
+        x = _pose_fuse_t(space, plan, feats, torch.bfloat16)
+        if ctx.needs_input_grad[2]:
+            plan.build()            # the backward's index (kept in the order the step issued it)
+        bias = _dev(bias, 'pad_conv bias').float()
+        O = w.shape[0]
+        d = pad_conv_desc(x, stride, O)
+        nbytes = lib.vfd_pad_conv_fwd_bf16_workspace(ctypes.byref(d))
+        if not nbytes:
+            raise RuntimeError(f'pad_conv_fwd_bf16: unsupported shape {tuple(x.shape)}, stride {stride}, {O} outputs')
+        ho, wo = (x.shape[2] - 3) // stride + 1, (x.shape[3] - 3) // stride + 1
+        out = torch.empty(x.shape[0], O, ho + 2, wo + 2, dtype=torch.bfloat16, device=x.device,
+                          memory_format=torch.channels_last)
+        ws = _ws(nbytes, x.device)
+        L.check(lib.vfd_pad_conv_fwd_bf16_t(ctypes.byref(d), x.data_ptr(), 1, wf.data_ptr(), bias.data_ptr(),
+                                            out.data_ptr(), ws.data_ptr(), nbytes, L.stream()), 'pad_conv_fwd_bf16')
+        ctx.space, ctx.plan, ctx.shape, ctx.stride, ctx.perm = space, plan, tuple(feats.shape), stride, perm
+        ctx.save_for_backward(x, w, out)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w, out = ctx.saved_tensors
+        s = ctx.stride
+        gb = lrelu_pad_backward(g.to(torch.bfloat16), out, dtype=torch.bfloat16)
+        dfeats = dw = db = None
+        if ctx.needs_input_grad[2]:
+            # the bf16 data gradient (ppd_main_k, fp32 output) straight into K2's backward
+            dfeats = _pose_unfuse(ctx.space, ctx.plan, ctx.shape, pad_conv_dgrad(gb, x.shape, w, s, ctx.perm))
+        if ctx.needs_input_grad[3] or ctx.needs_input_grad[4]:
+            dw, db = pad_conv_wgrad_bf16(gb, x, w, s, ctx.needs_input_grad[3], ctx.needs_input_grad[4])
+            if dw is not None and ctx.perm:
+                dw = weight_swap(dw, ctx.perm[1], ctx.perm[0])
+        return None, None, dfeats, dw, db, None, None, None
 
 
 def lrelu_pad_backward(g, out, slope=0.1, dtype=None):

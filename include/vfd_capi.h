@@ -101,9 +101,13 @@ int vfd_fusion_plan(const vfd_voxel_desc* d, const float* mask_lo, const float* 
 int vfd_fuse_pose_fwd(const vfd_voxel_desc* d, const float* mask_lo, const float* K, const float* Einv,
                       const float* feats_cl, float* out, void* stream);
 /* As vfd_fuse_pose_fwd with the map stored as dtype_out (0 fp32, 1 bf16 rounded to nearest even:
- * config 3, whose only consumer, the bf16 K2C, stages exactly those rounded values). */
+ * config 3, whose only consumer, the bf16 K2C, stages exactly those rounded values) and an
+ * optional voxel order (nullable): [8][order_cap] voxel indices by azimuth sector around the rig,
+ * -1 padding, every voxel exactly once; workgroup k takes sector k % 8, i.e. one XCD per sector
+ * (its L2 then caches the features of the cameras facing it).  The output does not depend on it. */
 int vfd_fuse_pose_fwd_t(const vfd_voxel_desc* d, const float* mask_lo, const float* K, const float* Einv,
-                        const float* feats_cl, void* out, int dtype_out, void* stream);
+                        const float* feats_cl, void* out, int dtype_out, const int* order, int order_cap,
+                        void* stream);
 /* d_out in the forward's output layout -> d_feats [B,N,C,h,w] (every element written).
  * Atomic-free gather over the plan's 4x4-pixel tile buckets, pulled from the plan's task queue
  * (heavy tiles split by channel group); the call resets the queue's work counter inside `plan`,

@@ -765,7 +765,7 @@ def test_pad_conv_bf16(shape):
 
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize('config,B', [(2, 2), (5, 1)])
-def test_pose_conv_bf16_map_matches_two_nodes(config, B):
+def test_pose_conv_bf16_map_matches_two_nodes(config, B, monkeypatch):
     """Config 3's K2 + K2C on the bf16 map (PoseConvBF16: K2 writes the map in bf16, the conv's
     forward and weight gradient read it) against FusePose (fp32 map) -> PadConvBF16 (the map
     rounded to bf16 as it is staged): the same staged values, so the map, the conv output and
@@ -789,6 +789,12 @@ def test_pose_conv_bf16_map_matches_two_nodes(config, B):
         x32 = KN.FusePose.apply(space, plan, feats)
         x16 = KN._pose_fuse_t(space, plan, feats, torch.bfloat16)
         assert torch.equal(x16, x32.to(torch.bfloat16)), 'bf16 map != the fp32 map rounded to nearest even'
+        # K2's azimuth-sector voxel order (one XCD per sector) only reorders work: the map is the
+        # index-order launch's, bit for bit
+        monkeypatch.setenv('VFD_POSE_SECTORS', '1')
+        assert space.pose_order() is not None
+        assert torch.equal(KN.FusePose.apply(space, plan, feats), x32), 'sector order changed the map'
+        monkeypatch.delenv('VFD_POSE_SECTORS')
     wf = KN.pad_conv_weight_fragments_bf16(w, C1, Z)
     la = [t.clone().requires_grad_(True) for t in (feats, w, b)]
     lb = [t.clone().requires_grad_(True) for t in (feats, w, b)]

@@ -67,7 +67,7 @@ _SIGS = {
     'vfd_fusion_plan_bytes': (c_size_t, [ctypes.POINTER(VoxelDesc)]),
     'vfd_fusion_plan': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 5 + [c_void_p]),
     'vfd_fuse_pose_fwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 5 + [c_void_p]),
-    'vfd_fuse_pose_fwd_t': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 5 + [c_int, c_void_p]),
+    'vfd_fuse_pose_fwd_t': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 5 + [c_int, c_fp, c_int, c_void_p]),
     'vfd_fuse_pose_bwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 4 + [c_void_p]),
     'vfd_voxel_project_fwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 4 + [c_void_p]),
     'vfd_voxel_project_plan_bytes': (c_size_t, [ctypes.POINTER(VoxelDesc)]),

@@ -668,15 +668,18 @@ __global__ __launch_bounds__(256) void fusion_plan_k(vfd_voxel_desc d, const flo
 // the voxel's C+1 values as one contiguous row at each of its (reflect-padded) positions.  Every
 // output element is written exactly once: no memset, no atomics.
 constexpr int POSE_TV = 32;
-#ifndef VFD_POSE_XCD          // XCD-aware z-slab numbering: measured 112 vs 108 us per launch, off
-#define VFD_POSE_XCD 0
-#endif
 constexpr int POSE_MAXC = 256;      // channels held per lane: ceil(C / 64) <= 4
 
+// order (nullable): the voxels by azimuth sector around the rig, [8][ocap] (-1 = padding,
+// kernels.VoxelSpace.pose_order).  Workgroup k runs sector k % 8 — one XCD (the hardware deals
+// workgroups round-robin over the 8 XCDs) — so an XCD gathers the feature rows of the one or two
+// cameras facing its sector and each row comes into one L2, instead of every XCD caching every
+// camera's map.  Null: voxels in index order, POSE_TV per workgroup.
 template <int NC, typename TO>
 __global__ __launch_bounds__(256) void fuse_pose_fwd_k(vfd_voxel_desc d, const float* __restrict__ mlo,
                                                        const float* __restrict__ K, const float* __restrict__ Einv,
-                                                       const float* __restrict__ feats, TO* __restrict__ out) {
+                                                       const float* __restrict__ feats, const int* __restrict__ order,
+                                                       int ocap, TO* __restrict__ out) {
   constexpr int CPL = POSE_MAXC / 64;
   __shared__ int s_base[POSE_TV][NC];
   __shared__ float s_w[POSE_TV][NC][4];
@@ -685,26 +688,25 @@ __global__ __launch_bounds__(256) void fuse_pose_fwd_k(vfd_voxel_desc d, const f
   __shared__ int s_cnt[POSE_TV];
   __shared__ float s_den[POSE_TV];
   __shared__ float s_zf[POSE_TV];
+  __shared__ int s_v[POSE_TV];
   const int V = d.X * d.Y * d.Z;
   const int b = blockIdx.y;
-#if VFD_POSE_XCD
-  // XCD-aware numbering: XCD k (workgroups k, k+8, ...) takes the contiguous voxel range
-  // [k*per, (k+1)*per) blocks — a z slab, whose taps fall in one band of each camera's rows, so
-  // the feature rows it gathers stay in that XCD's L2 instead of every XCD caching every map
-  const int per = gridDim.x / 8;
-  const int blk = (blockIdx.x % 8) * per + blockIdx.x / 8;
-  if (blk * POSE_TV >= V) return;
-  const int v0 = blk * POSE_TV;
-#else
-  const int v0 = blockIdx.x * POSE_TV;
-#endif
   const int hw = d.h * d.w;
   const int C = d.C, C1 = d.C + 1;
   if (threadIdx.x < POSE_TV) {
-    const int t = threadIdx.x, v = v0 + t;
+    const int t = threadIdx.x;
+    int v;
+    if (order) {
+      const int i = (blockIdx.x / 8) * POSE_TV + t;
+      v = i < ocap ? order[(blockIdx.x % 8) * ocap + i] : -1;
+    } else {
+      v = blockIdx.x * POSE_TV + t;
+      v = v < V ? v : -1;
+    }
+    s_v[t] = v;
     int cnt = 0;
     float zsum = 0.f;
-    if (v < V) {
+    if (v >= 0) {
       const float x = d.axis_x[v % d.X], y = d.axis_y[(v / d.X) % d.Y], z = d.axis_z[v / (d.X * d.Y)];
       VoxProj pj[NC];
       float occ[NC];
@@ -783,8 +785,8 @@ __global__ __launch_bounds__(256) void fuse_pose_fwd_k(vfd_voxel_desc d, const f
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const int t = t0 + u, v = v0 + t;
-      if (v >= V) continue;
+      const int t = t0 + u, v = s_v[t];
+      if (v < 0) continue;
       const float den = s_den[t];
       const int xi = v % d.X, yi = (v / d.X) % d.Y, zi = v / (d.X * d.Y);
       int rows[3], cols[3], nr, nc;
@@ -2513,7 +2515,8 @@ int vfd_fusion_plan(const vfd_voxel_desc* d, const float* mask_lo, const float* 
 }
 
 int vfd_fuse_pose_fwd_t(const vfd_voxel_desc* d, const float* mask_lo, const float* K, const float* Einv,
-                        const float* feats_cl, void* out, int dtype_out, void* stream) {
+                        const float* feats_cl, void* out, int dtype_out, const int* order, int order_cap,
+                        void* stream) {
   int st = check_voxel_desc(d);
   if (st) return st;
   VFD_REQUIRE(d->C >= 1 && d->C <= POSE_MAXC, "fuse_pose: C=%d outside [1, %d]", d->C, POSE_MAXC);
@@ -2521,12 +2524,16 @@ int vfd_fuse_pose_fwd_t(const vfd_voxel_desc* d, const float* mask_lo, const flo
   VFD_REQUIRE(dtype_out == 0 || dtype_out == 1, "fuse_pose: dtype_out %d (0 fp32, 1 bf16)", dtype_out);
   hipStream_t s = (hipStream_t)stream;
   const int V = d->X * d->Y * d->Z;
-  dim3 grid(VFD_POSE_XCD ? 8 * cdiv(cdiv(V, POSE_TV), 8) : cdiv(V, POSE_TV), d->B);
+  VFD_REQUIRE(!order || (order_cap > 0 && 8 * (long long)order_cap >= V),
+              "fuse_pose: order holds 8 x %d slots for %d voxels", order_cap, V);
+  dim3 grid(order ? 8 * cdiv(order_cap, POSE_TV) : cdiv(V, POSE_TV), d->B);
   ProfScope ps(K_FUSE_POSE_FWD, s);
   switch (d->N * 2 + dtype_out) {
-#define VFD_CASE(n)                                                                                        \
-  case 2 * n: fuse_pose_fwd_k<n, float><<<grid, 256, 0, s>>>(*d, mask_lo, K, Einv, feats_cl, (float*)out); break; \
-  case 2 * n + 1: fuse_pose_fwd_k<n, __bf16><<<grid, 256, 0, s>>>(*d, mask_lo, K, Einv, feats_cl, (__bf16*)out); break;
+#define VFD_CASE(n)                                                                                               \
+  case 2 * n: fuse_pose_fwd_k<n, float><<<grid, 256, 0, s>>>(*d, mask_lo, K, Einv, feats_cl, order, order_cap,    \
+                                                             (float*)out); break;                                 \
+  case 2 * n + 1: fuse_pose_fwd_k<n, __bf16><<<grid, 256, 0, s>>>(*d, mask_lo, K, Einv, feats_cl, order, order_cap, \
+                                                                  (__bf16*)out); break;
     VFD_CASE(1) VFD_CASE(2) VFD_CASE(3) VFD_CASE(4) VFD_CASE(5) VFD_CASE(6) VFD_CASE(7) VFD_CASE(8)
 #undef VFD_CASE
   }
@@ -2535,7 +2542,7 @@ int vfd_fuse_pose_fwd_t(const vfd_voxel_desc* d, const float* mask_lo, const flo
 
 int vfd_fuse_pose_fwd(const vfd_voxel_desc* d, const float* mask_lo, const float* K, const float* Einv,
                       const float* feats_cl, float* out, void* stream) {
-  return vfd_fuse_pose_fwd_t(d, mask_lo, K, Einv, feats_cl, out, 0, stream);
+  return vfd_fuse_pose_fwd_t(d, mask_lo, K, Einv, feats_cl, out, 0, nullptr, 0, stream);
 }
 
 int vfd_fuse_pose_bwd(const vfd_voxel_desc* d, const void* plan, const int* counts, const float* d_out,

@@ -32,19 +32,22 @@ constexpr int PP_FRAG = PP_PIX * PP_O;          // floats of one tile's partial
 constexpr int PP_LDS_MAX = 160 * 1024;
 constexpr int PP_MAXC = 96;                     // contributors of one tile
 constexpr int PP_FSL = 32;                      // fragment slices per tile in the reduce
+#ifndef VFD_RING_EARLY
+#define VFD_RING_EARLY 0                        // B-fragment ring: refill before (1) or after (0) the MFMAs
+#endif
 #ifndef VFD_PP_ALIGN
 #define VFD_PP_ALIGN 1                          // tile-aligned stream-K splits + XCD numbering (pp_plan)
 #endif
 
 // workgroup -> stream-K group: with ngroup % 8 == 0 XCD k (workgroups k, k + 8, ...) takes the
 // contiguous groups [k ngroup / 8, (k+1) ngroup / 8)
-__device__ __forceinline__ int pp_group(int ngroup) {
-  return (VFD_PP_ALIGN && ngroup % 8 == 0) ? (blockIdx.x % 8) * (ngroup / 8) + blockIdx.x / 8 : blockIdx.x;
-}
-
 struct PpGeom {
-  int B, hp, wp, cin, s, ho, wo, mimg, mtiles, nchunk, cq, ntile, natom, ngroup, hrows, lds_floats;
+  int B, hp, wp, cin, s, ho, wo, mimg, mtiles, nchunk, cq, ntile, natom, ngroup, hrows, lds_floats, xcd;
 };
+
+__device__ __forceinline__ int pp_group(const PpGeom& g) {
+  return g.xcd ? (blockIdx.x % 8) * (g.ngroup / 8) + blockIdx.x / 8 : blockIdx.x;
+}
 
 __host__ __device__ inline int pp_lo(const PpGeom& g, int grp) {
   return (int)(((long long)grp * g.natom) / g.ngroup);
@@ -120,7 +123,7 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppc_main_k(PpGeom g, const floa
                                                            float* __restrict__ partial) {
   constexpr int XS = CC + 4, ITERS = 9 * (CC / 4), PF = CC / 4 < PP_PF ? CC / 4 : PP_PF;
   extern __shared__ float pp_lds[];
-  const int grp = pp_group(g.ngroup);
+  const int grp = pp_group(g);
   const int a_lo = pp_lo(g, grp), a_hi = pp_lo(g, grp + 1);
   if (a_lo >= a_hi) return;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -318,7 +321,7 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppcb_main_k(PpGeom g, const TX*
   constexpr int XS = CC + 8, SPT = CC / 16, STEPS = 9 * SPT, PF = SPT == 2 ? VFD_PPB_PF : 3;
   static_assert(STEPS % PF == 0, "prefetch ring");
   extern __shared__ __attribute__((aligned(16))) __bf16 ppb_lds[];
-  const int grp = pp_group(g.ngroup);
+  const int grp = pp_group(g);
   const int a_lo = pp_lo(g, grp), a_hi = pp_lo(g, grp + 1);
   if (a_lo >= a_hi) return;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -385,18 +388,30 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppcb_main_k(PpGeom g, const TX*
       bf16x8 af[4];
 #pragma unroll
       for (int a = 0; a < 4; ++a) af[a] = *reinterpret_cast<const bf16x8*>(&xt[aoff[a] + 16 * q]);
+#if VFD_RING_EARLY                                     // A/B: copy the slot out, refill, then the MFMAs
+      bf16x8 bc[2] = {bq[ring][0], bq[ring][1]};
+      if (st + PF < STEPS)
+        wld(wc, st + PF, bq[ring]);
+      else if (more)
+        wld(wn, st + PF - STEPS, bq[ring]);
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        acc[a][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bc[0], acc[a][0], 0, 0, 0);
+        acc[a][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bc[1], acc[a][1], 0, 0, 0);
+      }
+#else
 #pragma unroll
       for (int a = 0; a < 4; ++a) {
         acc[a][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bq[ring][0], acc[a][0], 0, 0, 0);
         acc[a][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bq[ring][1], acc[a][1], 0, 0, 0);
       }
-      // the refill lands in the slot the MFMAs above just read: no register copy, so no wait on
-      // the younger loads of the ring (a copy-out would need them all: s_waitcnt vmcnt(0))
+      // the refill lands in the slot the MFMAs above just read (no register copy of the slot)
 #ifndef VFD_PPB_NOB
       if (st + PF < STEPS)
         wld(wc, st + PF, bq[ring]);
       else if (more)
         wld(wn, st + PF - STEPS, bq[ring]);
+#endif
 #endif
       // keep the scheduler from hoisting later steps' LDS reads above these MFMAs (register
       // pressure: the prefetch ring, not the A fragments, is what should hold VGPRs)
@@ -472,7 +487,9 @@ static int pp_resident() {
   return cus;
 }
 
-static bool pp_plan(const vfd_conv_desc& d, PpGeom* out, int cc = PP_CC, int xs_bytes = PP_XS * 4) {
+// align: tile-aligned splits + XCD numbering (the bf16 forward: 441 vs 476 us at config 3; the fp32
+// forward is MFMA-bound and a little faster without, 550 vs 557 us at config 2)
+static bool pp_plan(const vfd_conv_desc& d, PpGeom* out, int cc = PP_CC, int xs_bytes = PP_XS * 4, bool align = false) {
   if (d.B <= 0 || d.C <= 0 || d.C % 4 || d.stride < 1 || d.stride > 2 || d.H < 3 || d.W < 3 ||
       d.out_channels != PP_O)
     return false;
@@ -502,17 +519,19 @@ static bool pp_plan(const vfd_conv_desc& d, PpGeom* out, int cc = PP_CC, int xs_
   int most = g.natom / min_range;
   most = most > 0 ? most : 1;
   g.ngroup = res < most ? res : most;
+  g.xcd = 0;
 #if VFD_PP_ALIGN
   // fewer tiles than CUs: every tile cut into the same ksplit chunk ranges (group t * ksplit + j
   // takes chunks [j nchunk / ksplit, (j+1) nchunk / ksplit) of tile t), so the groups of one split
   // read the same weight fragments at the same time; with the XCD numbering of the main kernels
   // the tiles of one XCD share its L2 copy instead of every CU streaming its own from HBM / MALL
-  if (g.ntile <= res) {
+  if (align && g.ntile <= res) {
     int ks = res / g.ntile;
     ks = ks < g.nchunk ? ks : g.nchunk;
     ks = ks < PP_MAXC - 1 ? ks : PP_MAXC - 1;
     g.ngroup = g.ntile * ks;
   }
+  g.xcd = align && g.ngroup % 8 == 0;
 #endif
   *out = g;
   return true;
@@ -790,12 +809,26 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppd_main_k(PdcGeom g, const TG*
 #pragma unroll
           for (int a = 0; a < MB; ++a) afn[a] = *reinterpret_cast<const Frag*>(&xb[o1c[a]]);
         }
+#if VFD_RING_EARLY
+        Frag bc[NB];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+          bc[b] = bq[q % PF][b];
+          if (q + PF < STEPS)
+            bq[q % PF][b] = btap[(q + PF) * qstride + 64 * b];
+          else if (bn)
+            bq[q % PF][b] = bn[(q + PF - STEPS) * qstride + 64 * b];
+        }
+#define VFD_PD_B(b) bc[b]
+#else
+#define VFD_PD_B(b) bq[q % PF][b]
+#endif
         if constexpr (BF) {
 #pragma unroll
           for (int a = 0; a < MB; ++a)
 #pragma unroll
             for (int b = 0; b < NB; ++b)
-              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afc[a], bq[q % PF][b], acc[a][b], 0, 0, 0);
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afc[a], VFD_PD_B(b), acc[a][b], 0, 0, 0);
         } else {
 #pragma unroll
           for (int s2 = 0; s2 < 2; ++s2)
@@ -804,10 +837,11 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppd_main_k(PdcGeom g, const TG*
 #pragma unroll
               for (int b = 0; b < NB; ++b)
                 acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(s2 ? afc[a].y : afc[a].x,
-                                                                 s2 ? bq[q % PF][b].y : bq[q % PF][b].x, acc[a][b], 0, 0, 0);
+                                                                 s2 ? VFD_PD_B(b).y : VFD_PD_B(b).x, acc[a][b], 0, 0, 0);
         }
+#undef VFD_PD_B
         // refill the slots just read (no copy-out of the ring: see ppcb_main_k)
-#ifndef VFD_PD_NOB
+#if !defined(VFD_PD_NOB) && !VFD_RING_EARLY
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
           if (q + PF < STEPS)
@@ -998,8 +1032,8 @@ int vfd_pad_conv_fwd(const vfd_conv_desc* d, const float* x, const float* Wf, co
 
 // channels per atom of the bf16 forward: 32, or 16 when 32 do not fit LDS
 static int ppb_cc(const vfd_conv_desc& d, PpGeom* g) {
-  if (pp_plan(d, g, PPB_CC, PPB_XS * 2)) return PPB_CC;
-  if (pp_plan(d, g, 16, 24 * 2)) return 16;
+  if (pp_plan(d, g, PPB_CC, PPB_XS * 2, true)) return PPB_CC;
+  if (pp_plan(d, g, 16, 24 * 2, true)) return 16;
   return 0;
 }
 

@@ -84,6 +84,9 @@ constexpr int PC_ITERS = 9 * (PC_CV / 4);       // (tap, channel quad) iteration
 // when `xo` is given — the tile's own (interior) samples into the padded NHWC frustum-feature map
 // the conv's backward reads (K3's output layout; written once, reflect copies included).
 constexpr int PC_GPOS = (PC_NPOS + 15) / 16 * 4;   // halo positions per gather wave (48)
+#ifndef VFD_PCG_U
+#define VFD_PCG_U 4                                 // gather: positions' corner rows in flight per lane
+#endif
 
 struct PcTri {
   int base;
@@ -128,41 +131,64 @@ __device__ __forceinline__ void pc_gather(const vfd_voxel_desc& d, T* __restrict
   }
   __threadfence_block();
   __builtin_amdgcn_wave_barrier();
-  // (2) lanes = (position, channel quad): 16 quads per 64-channel row, 4 positions per instruction
+  // (2) lanes = (position, channel quad): 16 quads per 64-channel row, 4 positions per instruction;
+  //     U positions' 8 corner rows in flight together (the voxel rows come from L2 / MALL at ~1 us:
+  //     one position at a time made the bf16 kernel's gather, not its MFMAs, the bound)
   const int q = lane & 15, sub = lane >> 4;
   const float4* vb = reinterpret_cast<const float4*>(vox_b) + q;
   const int wo = d.w + 2;
-  for (int it = 0; it < PC_GPOS / 4; ++it) {
-    const int p = gw * 4 + sub + 16 * it;
-    if (p >= PC_NPOS) break;
-    const PcTri& t = tw[it * 4 + sub];
-    const unsigned in = t.in;
-    const int base = t.base;
-    float4 v[8];
+  constexpr int U = VFD_PCG_U;
+  static_assert((PC_GPOS / 4) % U == 0, "gather unroll");
+  for (int i0 = 0; i0 < PC_GPOS / 4; i0 += U) {
+    float4 v[U][8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const bool ok = (in >> k & 1u) != 0u;
-      v[k] = vb[(size_t)(ok ? base + corner_offset(d, k) : 0) * (PC_CV / 4)];
-    }
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int u = 0; u < U; ++u) {
+      const int it = i0 + u;
+      const int p = gw * 4 + sub + 16 * it;
+      const PcTri& t = tw[it * 4 + sub];
+      const unsigned in = p < PC_NPOS ? t.in : 0u;
+      const int base = t.base;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {           // K3's arithmetic: corner order, weight 0 when out of range
-      const float w = (in >> k & 1u) ? t.w[k] : 0.f;
-      acc.x += v[k].x * w;
-      acc.y += v[k].y * w;
-      acc.z += v[k].z * w;
-      acc.w += v[k].w * w;
+      for (int k = 0; k < 8; ++k) {
+        const bool ok = (in >> k & 1u) != 0u;
+#ifdef VFD_PCV_NOGATHER                       // timing experiment only: no corner loads
+        v[u][k] = make_float4(0.f, 0.f, 0.f, (float)(ok ? base : 0));
+#else
+        v[u][k] = vb[(size_t)(ok ? base + corner_offset(d, k) : 0) * (PC_CV / 4)];
+#endif
+      }
     }
-    pc_put(&xs[p * XS + 4 * q], acc);
-    if (xo) {
-      const int hr = p / PC_HC, hc = p - hr * PC_HC;
-      const int py = y0 + hr - 1, px = x0 + hc - 1;
-      if (hr >= 1 && hr <= PC_TR && hc >= 1 && hc <= PC_TC && py < d.h && px < d.w) {
-        int rows[3], cols[3], nr, nc;
-        pad_sets(py, d.h, true, rows, &nr);
-        pad_sets(px, d.w, true, cols, &nc);
-        for (int r = 0; r < nr; ++r)
-          for (int c = 0; c < nc; ++c) pc_put(xo + (((size_t)rows[r] * wo + cols[c]) * d.D + di) * PC_CV + 4 * q, acc);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int it = i0 + u;
+      const int p = gw * 4 + sub + 16 * it;
+      if (p >= PC_NPOS) break;
+      const PcTri& t = tw[it * 4 + sub];
+      const unsigned in = t.in;
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {           // K3's arithmetic: corner order, weight 0 when out of range
+        const float w = (in >> k & 1u) ? t.w[k] : 0.f;
+        acc.x += v[u][k].x * w;
+        acc.y += v[u][k].y * w;
+        acc.z += v[u][k].z * w;
+        acc.w += v[u][k].w * w;
+      }
+      pc_put(&xs[p * XS + 4 * q], acc);
+#ifdef VFD_PCV_NOXO                           // timing experiment only: no side output
+      if (false) {
+#else
+      if (xo) {
+#endif
+        const int hr = p / PC_HC, hc = p - hr * PC_HC;
+        const int py = y0 + hr - 1, px = x0 + hc - 1;
+        if (hr >= 1 && hr <= PC_TR && hc >= 1 && hc <= PC_TC && py < d.h && px < d.w) {
+          int rows[3], cols[3], nr, nc;
+          pad_sets(py, d.h, true, rows, &nr);
+          pad_sets(px, d.w, true, cols, &nc);
+          for (int r = 0; r < nr; ++r)
+            for (int c = 0; c < nc; ++c) pc_put(xo + (((size_t)rows[r] * wo + cols[c]) * d.D + di) * PC_CV + 4 * q, acc);
+        }
       }
     }
   }
@@ -379,11 +405,16 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pcvb_main_k(vfd_voxel_desc d, P
   const bf16x8* wp = wbase + (size_t)(a_lo % d.D) * PCB_ITERS * (PC_O / 32) * 64;
   const bf16x8* wend = wbase + (size_t)d.D * PCB_ITERS * (PC_O / 32) * 64;
   bf16x8 bq[PCB_PF][2];
+#ifdef VFD_PCV_NOB
+  for (int k = 0; k < PCB_PF; ++k) bq[k][0] = bq[k][1] = wbase[64 * k];
+#endif
   int pf_left = (a_hi - a_lo) * PCB_ITERS;         // steps still to prefetch
   auto prefetch = [&](int slot) {
     if (pf_left > 0) {
+#ifndef VFD_PCV_NOB                           // timing experiment only: B fragments loaded once
       bq[slot][0] = wp[0];
       bq[slot][1] = wp[64];
+#endif
       wp += (PC_O / 32) * 64;
       if (wp == wend) wp = wbase;
       --pf_left;

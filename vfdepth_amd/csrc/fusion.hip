@@ -669,6 +669,14 @@ __global__ __launch_bounds__(256) void fusion_plan_k(vfd_voxel_desc d, const flo
 // output element is written exactly once: no memset, no atomics.
 constexpr int POSE_TV = 32;
 constexpr int POSE_MAXC = 256;      // channels held per lane: ceil(C / 64) <= 4
+#ifndef VFD_POSE_QUAD
+#define VFD_POSE_QUAD 1             // lanes = channel quads (C % 4 == 0): 166 vs 188 us (config 3), 91 vs 101 (2)
+#endif
+#ifndef VFD_POSE_VU
+#define VFD_POSE_VU 2                 // voxels per wave round: 166 vs 170 (1) / 202 (4) us at config 3
+#endif
+constexpr int POSE_VU = VFD_POSE_VU;
+static_assert(POSE_TV % (4 * POSE_VU) == 0, "K2 forward: voxels per wave round");
 
 // order (nullable): the voxels by azimuth sector around the rig, [8][ocap] (-1 = padding,
 // kernels.VoxelSpace.pose_order).  Workgroup k runs sector k % 8 — one XCD (the hardware deals
@@ -740,6 +748,84 @@ __global__ __launch_bounds__(256) void fuse_pose_fwd_k(vfd_voxel_desc d, const f
   const int Yo = d.Y + P, Xo = d.X + P;
   const size_t pix_stride = (size_t)d.Z * C1;
   TO* ob = out + (size_t)b * Yo * Xo * pix_stride;
+#if VFD_POSE_QUAD
+  if ((C & 3) == 0) {
+    // lanes = channel quads: one 16-B load per lane brings a whole tap row (C <= 256), the wave
+    // works on POSE_VU voxels at a time (wave-uniform: their camera loops are uniform branches) and
+    // issues all their tap rows of one camera round before summing any.  The per-channel arithmetic
+    // is the lane-per-channel form's, in the same order (taps, then cameras), so the map is
+    // bit-identical to it
+    const int cq = min(lane, C / 4 - 1) * 4;        // idle lanes (C < 256) re-read the last quad
+    const bool own = lane < C / 4;
+    for (int t0 = wv * POSE_VU; t0 < POSE_TV; t0 += 4 * POSE_VU) {
+      float4 acc[POSE_VU];
+      int cmax = 0;
+#pragma unroll
+      for (int u = 0; u < POSE_VU; ++u) {
+        acc[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        cmax = max(cmax, s_cnt[t0 + u]);
+      }
+      for (int j = 0; j < cmax; ++j) {
+        float4 f[POSE_VU][4];
+#pragma unroll
+        for (int u = 0; u < POSE_VU; ++u) {
+          const int t = t0 + u;
+          const bool act = j < s_cnt[t];
+          const float* fc = fb + (size_t)(act ? s_cam[t][j] : 0) * hw * C + cq;
+          const int base = act ? s_base[t][j] : 0;
+          const unsigned in = act ? s_in[t][j] : 0u;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const bool ok = (in >> q & 1u) != 0u;
+            f[u][q] = *reinterpret_cast<const float4*>(fc + (size_t)(ok ? base + tap_offset(q, d.w) : 0) * C);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < POSE_VU; ++u) {
+          const int t = t0 + u;
+          if (j >= s_cnt[t]) continue;
+          const unsigned in = s_in[t][j];
+          float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float w = (in >> q & 1u) ? s_w[t][j][q] : 0.f;
+            val.x += f[u][q].x * w;
+            val.y += f[u][q].y * w;
+            val.z += f[u][q].z * w;
+            val.w += f[u][q].w * w;
+          }
+          acc[u].x += val.x;
+          acc[u].y += val.y;
+          acc[u].z += val.z;
+          acc[u].w += val.w;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < POSE_VU; ++u) {
+        const int t = t0 + u, v = s_v[t];
+        if (v < 0) continue;
+        const float den = s_den[t];
+        const int xi = v % d.X, yi = (v / d.X) % d.Y, zi = v / (d.X * d.Y);
+        int rows[3], cols[3], nr, nc;
+        pad_sets(yi, d.Y, d.pad_out, rows, &nr);
+        pad_sets(xi, d.X, d.pad_out, cols, &nc);
+        const float o[4] = {acc[u].x / den, acc[u].y / den, acc[u].z / den, acc[u].w / den};
+        const float zf = s_zf[t];
+        for (int a = 0; a < nr; ++a)
+          for (int c2 = 0; c2 < nc; ++c2) {
+            TO* row = ob + ((size_t)rows[a] * Xo + cols[c2]) * pix_stride + (size_t)zi * C1;
+            if (own) {
+              // rows start at any element (C + 1 per z): element stores, consecutive across lanes
+#pragma unroll
+              for (int e = 0; e < 4; ++e) row[cq + e] = (TO)o[e];
+            }
+            if (lane == 0) row[C] = (TO)zf;
+          }
+      }
+    }
+    return;
+  }
+#endif
   for (int t0 = wv * 2; t0 < POSE_TV; t0 += 8) {
     float acc[2][CPL];
 #pragma unroll

@@ -34,9 +34,12 @@ OPS = {
     'smooth_bwd': ['smooth_bwd_k'],
     'aggregate': ['aggregate_fwd_k', 'aggregate_plane_fwd_k'],
     'proj_conv_fwd': ['pcv_main_k', 'pcvb_main_k', 'pcv_reduce_k'],
-    'proj_conv_dgrad': ['pcd_main_k', 'pcd_reduce_k', 'pcdf_main_k', 'pcdf_reduce_k'],
-    'proj_conv_wgrad': ['pcw_main_k', 'pcw_reduce_k', 'pcw_bias_k', 'pcw_bias_fin_k'],
+    'proj_conv_dgrad': ['pcd_main_k', 'pcd_reduce_k', 'pcdf_main_k', 'pcdf_reduce_k', 'pcg_main_k', 'pcg_reduce_k',
+                        'pch_main_k', 'pch_reduce_k'],
+    'proj_conv_wgrad': ['pcw_main_k', 'pwb_main_k8', 'pcw_reduce_k', 'pcw_bias_k', 'pwb_bias_k', 'pcw_bias_fin_k'],
     'pad_conv_fwd': ['ppc_main_k', 'ppcb_main_k', 'ppc_reduce_k'],
+    'pad_conv_dgrad': ['ppd_main_k', 'ppd_reduce_k'],
+    'pad_conv_wgrad': ['pwb_main_k4', 'pwb_reduce_map_k'],
     'depth_syn_fwd': ['depth_syn_fwd_k'],
     'depth_syn_bwd': ['depth_syn_bwd_k'],
     'bn_fwd': ['bn_stats_k', 'bn_sum_k', 'bn_apply_k', 'bn1_fwd_k', 'bn_stats_nhwc_k', 'bn_sum_blk_k', 'bn_apply_nhwc_k'],
@@ -65,15 +68,21 @@ ENTRY = {
 
 def kernel_of(name):
     """vfd kernel base name from a demangled ('vfd::bn_apply_k<float>(...)') or, as rocprofv3
-    leaves the bf16 template instances, mangled ('_ZN3vfd10bn_apply_kIDF16bEEv...') name."""
+    leaves the bf16 template instances, mangled ('_ZN3vfd10bn_apply_kIDF16bEEv...') name.  The bf16
+    weight-gradient kernel serves two ops: K3C's instance (8 channels per X load) is
+    'pwb_main_k8', K2C's (4: the pose map) 'pwb_main_k4'."""
+    base = None
     m = re.search(r'vfd::(\w+)', name)
     if m:
-        return m.group(1)
-    m = re.match(r'_ZN3vfd(\d+)', name)
-    if m:
-        n = int(m.group(1))
-        return name[m.end():m.end() + n]
-    return None
+        base = m.group(1)
+    else:
+        m = re.match(r'_ZN3vfd(\d+)', name)
+        if m:
+            n = int(m.group(1))
+            base = name[m.end():m.end() + n]
+    if base == 'pwb_main_k':
+        base += '8' if ('Li8E' in name or ', 8>' in name) else '4'
+    return base
 
 
 def load(path, counter):

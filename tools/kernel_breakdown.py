@@ -15,10 +15,13 @@ def main():
     ap.add_argument('--marker', default='mask_downsample_k')
     ap.add_argument('--last', type=int, default=5)
     ap.add_argument('--top', type=int, default=40)
+    ap.add_argument('--skip', type=int, default=0, help='ignore the last N marker launches (the bench\'s parity step)')
     a = ap.parse_args()
-    rows = list(csv.DictReader(open(a.csv)))
+    import gzip
+    rows = list(csv.DictReader(gzip.open(a.csv, 'rt') if a.csv.endswith('.gz') else open(a.csv)))
     rows.sort(key=lambda r: int(r['Start_Timestamp']))
     marks = [i for i, r in enumerate(rows) if a.marker in r['Kernel_Name']]
+    marks = marks[:len(marks) - a.skip] if a.skip else marks
     if len(marks) < a.last + 1:
         raise SystemExit(f'only {len(marks)} marker launches')
     lo, hi = marks[-a.last - 1], marks[-1]

@@ -84,6 +84,9 @@ constexpr int PC_ITERS = 9 * (PC_CV / 4);       // (tap, channel quad) iteration
 // when `xo` is given — the tile's own (interior) samples into the padded NHWC frustum-feature map
 // the conv's backward reads (K3's output layout; written once, reflect copies included).
 constexpr int PC_GPOS = (PC_NPOS + 15) / 16 * 4;   // halo positions per gather wave (48)
+#ifndef VFD_PCVB_XO_COMPUTE
+#define VFD_PCVB_XO_COMPUTE 1                       // bf16 K3C: side output written by the compute waves
+#endif
 #ifndef VFD_PCG_U
 #define VFD_PCG_U 4                                 // gather: positions' corner rows in flight per lane
 #endif
@@ -373,7 +376,7 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pcvb_main_k(vfd_voxel_desc d, P
   const bool compute = wv < PC_WAVES;
   auto gather = [&](int atom, __bf16* dst) {
     const PcAtom a = pc_atom(d, g, atom);
-    __bf16* xo = xout ? xout + (size_t)a.bc * (d.h + 2) * (d.w + 2) * d.D * PC_CV : nullptr;
+    __bf16* xo = (xout && !VFD_PCVB_XO_COMPUTE) ? xout + (size_t)a.bc * (d.h + 2) * (d.w + 2) * d.D * PC_CV : nullptr;
     pc_gather<__bf16, PCB_XS>(d, dst, tri[wv - PC_WAVES], vox + (size_t)(a.bc / d.N) * V * PC_CV,
                               invK + a.bc * 16, E + a.bc * 16, a.y0, a.x0, a.di, wv - PC_WAVES, xo);
   };
@@ -472,6 +475,30 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pcvb_main_k(vfd_voxel_desc d, P
         for (int a = 0; a < 4; ++a) afc[a] = afn[a];
       }
     }
+#if VFD_PCVB_XO_COMPUTE
+    if (xout) {
+      // the frustum side output (K3's layout, reflect copies included) for the weight gradient,
+      // written by the compute waves from the staged image after this atom's MFMAs: the gather
+      // waves bound the bf16 kernel (0.18 ms of its 0.99 at config 3 were these stores), the
+      // compute waves wait for them at the barrier anyway.  Same bf16 values as the gather's.
+      const PcAtom pa = pc_atom(d, g, atom);
+      __bf16* xo = xout + (size_t)pa.bc * (d.h + 2) * (d.w + 2) * d.D * PC_CV;
+      const int wo = d.w + 2;
+      for (int e = threadIdx.x; e < PC_PIX * (PC_CV / 8); e += PC_WAVES * 64) {
+        const int px = e >> 3, k = e & 7;                 // tile position, channel octet
+        const int ty = px / PC_TC, tx = px - ty * PC_TC;
+        const int py = pa.y0 + ty, pxx = pa.x0 + tx;
+        if (py >= d.h || pxx >= d.w) continue;
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(&xb[((ty + 1) * PC_HC + tx + 1) * PCB_XS + 8 * k]);
+        int rows[3], cols[3], nr, nc;
+        pad_sets(py, d.h, true, rows, &nr);
+        pad_sets(pxx, d.w, true, cols, &nc);
+        for (int r = 0; r < nr; ++r)
+          for (int c = 0; c < nc; ++c)
+            *reinterpret_cast<bf16x8*>(xo + (((size_t)rows[r] * wo + cols[c]) * d.D + pa.di) * PC_CV + 8 * k) = v;
+      }
+    }
+#endif
     __syncthreads();                                  // buffer handed back to the gather waves
   }
   float* dst = partial + ((size_t)grp * 2 + slot) * PC_FRAG + (size_t)wv * (PC_FRAG / PC_WAVES);

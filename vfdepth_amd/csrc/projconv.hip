@@ -84,6 +84,9 @@ constexpr int PC_ITERS = 9 * (PC_CV / 4);       // (tap, channel quad) iteration
 // when `xo` is given — the tile's own (interior) samples into the padded NHWC frustum-feature map
 // the conv's backward reads (K3's output layout; written once, reflect copies included).
 constexpr int PC_GPOS = (PC_NPOS + 15) / 16 * 4;   // halo positions per gather wave (48)
+#ifndef VFD_PH_PIPE
+#define VFD_PH_PIPE 0                               // bf16 K3C dgrad loader two atoms ahead: 965 vs 932 us, off
+#endif
 #ifndef VFD_PCVB_XO_COMPUTE
 #define VFD_PCVB_XO_COMPUTE 1                       // bf16 K3C: side output written by the compute waves
 #endif
@@ -1576,16 +1579,19 @@ __device__ __forceinline__ PhTile ph_tile(const PhGeom& g, int t) {
 
 // loader waves (tid 0..255): 400 positions x 4 eight-channel vectors, each the sum of <= 2 x 2 G
 // vectors (rows ya / yb x columns xa / xb, -1 = absent); every load of a thread in flight together
-__device__ __forceinline__ void ph_stage(const PhGeom& g, __bf16* __restrict__ dst, const __bf16* __restrict__ gp,
-                                         int atom, int tid) {
-  constexpr int NP = PH_S * PH_S, PER = (NP * 4 + 255) / 256;     // 7 items per thread
+constexpr int PH_PER = (PH_S * PH_S * 4 + 255) / 256;   // staged 16-B items per loader thread (7)
+typedef bf16x8 PhRegs[PH_PER][4];
+
+// loader waves (tid 0..255), phase 1: the atom's G rows (and fold partners) into registers
+__device__ __forceinline__ void ph_fetch(const PhGeom& g, const __bf16* __restrict__ gp, int atom, int tid,
+                                         PhRegs& v) {
+  constexpr int NP = PH_S * PH_S, PER = PH_PER;
   const int t = atom / g.och, ch = atom - t * g.och;
   const PhTile tl = ph_tile(g, t);
   const bool f1 = tl.y0 == 0, f2 = tl.y0 <= g.h - 2 && tl.y0 + PH_T > g.h - 2;
   const bool e1 = tl.x0 == 0, e2 = tl.x0 <= g.w - 2 && tl.x0 + PH_T > g.w - 2;
   const int q = tid & 3;
   const __bf16* src = gp + (size_t)tl.bc * g.h * g.w * PC_O + ch * PH_OC + 8 * q;
-  bf16x8 v[PER][4];
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     const int p = (tid >> 2) + 64 * k;
@@ -1608,27 +1614,54 @@ __device__ __forceinline__ void ph_stage(const PhGeom& g, __bf16* __restrict__ d
       }
     }
     const int ys[2] = {ya, yb}, xs[2] = {xa, xb};
+    bf16x8 z;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int yy = ys[j >> 1], xx = xs[j & 1];
-      bf16x8 z;
+    for (int e = 0; e < 8; ++e) z[e] = (__bf16)0.f;
+#ifdef VFD_PH_NOSTAGE                       // timing experiment only: no G loads
+    v[k][0] = v[k][1] = v[k][2] = v[k][3] = z;
+    (void)ys; (void)xs;
+#else
+    // only the two fold rows / columns have partners (yb / xb): the interior's 3 partner slots are
+    // zero without a load or its address arithmetic
+    v[k][0] = (ya >= 0 && xa >= 0) ? *reinterpret_cast<const bf16x8*>(src + ((size_t)ya * g.w + xa) * PC_O) : z;
+    v[k][1] = v[k][2] = v[k][3] = z;
+    if (yb >= 0 || xb >= 0) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) z[e] = (__bf16)0.f;
-      v[k][j] = (yy >= 0 && xx >= 0) ? *reinterpret_cast<const bf16x8*>(src + ((size_t)yy * g.w + xx) * PC_O) : z;
+      for (int j = 1; j < 4; ++j) {
+        const int yy = ys[j >> 1], xx = xs[j & 1];
+        if (yy >= 0 && xx >= 0) v[k][j] = *reinterpret_cast<const bf16x8*>(src + ((size_t)yy * g.w + xx) * PC_O);
+      }
     }
+#endif
   }
+}
+
+// phase 2: the registers (fold partners summed) into one LDS image
+__device__ __forceinline__ void ph_put(__bf16* __restrict__ dst, const PhRegs& v, int tid) {
+  constexpr int NP = PH_S * PH_S, PER = PH_PER;
+  const int q = tid & 3;
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     const int p = (tid >> 2) + 64 * k;
     if (p < NP) {
       const int r = p / PH_S, c = p - r * PH_S;
-      bf16x8 o;
+      bf16x8 o = v[k][0];
+      if (r >= PH_T + 2 || c >= PH_T + 2) {     // fold row / column: the partners' fp32 sum, rounded once
 #pragma unroll
-      for (int e = 0; e < 8; ++e)
-        o[e] = (__bf16)(((float)v[k][0][e] + (float)v[k][1][e]) + ((float)v[k][2][e] + (float)v[k][3][e]));
+        for (int e = 0; e < 8; ++e)
+          o[e] = (__bf16)(((float)v[k][0][e] + (float)v[k][1][e]) + ((float)v[k][2][e] + (float)v[k][3][e]));
+      }
       *reinterpret_cast<bf16x8*>(dst + r * PH_RP + c * PH_XS + 8 * q) = o;
     }
   }
+}
+
+
+__device__ __forceinline__ void ph_stage(const PhGeom& g, __bf16* __restrict__ dst, const __bf16* __restrict__ gp,
+                                         int atom, int tid) {
+  PhRegs v;
+  ph_fetch(g, gp, atom, tid, v);
+  ph_put(dst, v, tid);
 }
 
 __global__ __launch_bounds__(PC_THREADS, 2) void pch_main_k(PhGeom g, const __bf16* __restrict__ gp,
@@ -1642,6 +1675,29 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pch_main_k(PhGeom g, const __bf
   if (a_lo >= a_hi) return;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const bool compute = wv < PC_WAVES;
+#if VFD_PH_PIPE
+  // loader waves two atoms ahead: the rows of atom k + 2 are fetched into registers right after
+  // atom k + 1's are put in LDS, so their L2 / MALL round trip overlaps a whole atom of MFMAs and
+  // the barrier (one atom ahead, the round trip was exposed on every atom: 0.23 of 0.91 ms)
+  PhRegs pv;
+  const int ltid = threadIdx.x - 64 * PC_WAVES;
+  if (!compute) {
+    ph_fetch(g, gp, a_lo, ltid, pv);
+    ph_put(lds, pv, ltid);
+    if (a_lo + 1 < a_hi) ph_fetch(g, gp, a_lo + 1, ltid, pv);
+  }
+  __syncthreads();
+  if (!compute) {
+    for (int atom = a_lo; atom < a_hi; ++atom) {
+      if (atom + 1 < a_hi) {
+        ph_put(lds + ((atom + 1 - a_lo) & 1) * PH_ELEMS, pv, ltid);
+        if (atom + 2 < a_hi) ph_fetch(g, gp, atom + 2, ltid, pv);
+      }
+      __syncthreads();
+    }
+    return;
+  }
+#else
   if (!compute) ph_stage(g, lds, gp, a_lo, threadIdx.x - 64 * PC_WAVES);
   __syncthreads();
   if (!compute) {
@@ -1651,6 +1707,7 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pch_main_k(PhGeom g, const __bf
     }
     return;
   }
+#endif
   const int li = lane & 31, lh = lane >> 5;
   f32x16 acc[8];
 #pragma unroll
@@ -1699,7 +1756,11 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pch_main_k(PhGeom g, const __bf
       const bf16x8 b = bq[j % PF];
       {
         const int jn = j + PF;
+#ifdef VFD_PH_NOB                            // timing experiment only: B fragments loaded once
+        if (jn < 0)
+#else
         if (jn < ITERS)
+#endif
           bq[j % PF] = bcur[(jn / STEPS) * tstride + (jn % STEPS) * qstride];
         else if (more)
           bq[j % PF] = bnext[((jn - ITERS) / STEPS) * tstride + ((jn - ITERS) % STEPS) * qstride];
@@ -2132,8 +2193,10 @@ __device__ __forceinline__ void wb_fetch(const WbGeom& g, WbStage<TX, XV>& st, c
     const int e = tid + PC_THREADS * u, px = e >> 5, q = e & 31;     // 32 vectors of 8 o per pixel
     const int y = y0 + (px >> 4), x = x0 + (px & 15);
     st.gv[u] = make_uint4(0u, 0u, 0u, 0u);
+#ifndef VFD_PWB_NOFETCH                       // timing experiment only: no G / X loads
     if (y < g.ho && x < g.wo)
       st.gv[u] = *reinterpret_cast<const uint4*>(gp + (((size_t)img * g.ho + y) * g.wo + x) * PC_O + 8 * q);
+#endif
   }
   const int npos = g.hr * g.hc, vpp = WB_XP / XV;
 #pragma unroll
@@ -2142,7 +2205,11 @@ __device__ __forceinline__ void wb_fetch(const WbGeom& g, WbStage<TX, XV>& st, c
     const int r = pos / g.hc, c = pos - r * g.hc;
     const int Y = g.s * y0 + r, X = g.s * x0 + c, n = t * 32 + XV * q;
     memset(&st.xv[u], 0, sizeof(st.xv[u]));
+#ifdef VFD_PWB_NOFETCH
+    if (false)
+#else
     if (pos < npos && Y < g.hp && X < g.wp && n < g.C)
+#endif
       st.xv[u] = *reinterpret_cast<const XT*>(xp + (((size_t)img * g.hp + Y) * g.wp + X) * g.C + n);
   }
 }

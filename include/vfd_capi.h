@@ -319,6 +319,17 @@ int vfd_elu_up_pad1_bwd(const void* g, const void* y, void* dy, long long planes
 /* psum (optional, [planes][vfd_elu_up_pad1_bwd_blocks(h, w)]): per-block sums of dy per plane —
  * the partials of the producing conv's bias gradient (summed in fixed order by the caller) */
 int vfd_elu_up_pad1_bwd_blocks(int h, int w);
+/* The same chain for channels-last maps (config 3's bf16 decoders, VFD_DEC_CL): y [n_img, h, w, C]
+ * -> out [n_img, (h<<up)+2, (w<<up)+2, C]; act = 0 is the plain reflect pad (ReflectPad1 on a
+ * channels-last map).  C % 4 == 0, dtype 0 fp32 (16-B aligned) / 1 bf16 (8-B aligned); the
+ * backward needs C / 4 to divide 256 and sums each channel's copies in the NCHW kernel's order
+ * (identical d y).  y may be NULL for act 0. */
+int vfd_elu_up_pad1_nhwc_fwd(const void* y, void* out, long long n_img, int h, int w, int C, int up, int act,
+                             int dtype, void* stream);
+int vfd_elu_up_pad1_nhwc_bwd(const void* g, const void* y, void* dy, long long n_img, int h, int w, int C, int up,
+                             int act, float* part, int dtype, void* stream);
+/* part (optional, [vfd_elu_up_pad1_nhwc_bwd_blocks(...)][C]): per-block channel sums of d y (bias partials) */
+int vfd_elu_up_pad1_nhwc_bwd_blocks(long long n_img, int h, int w, int C);
 /* backward of LeakyReLU(slope) + the one-pixel reflect pad for channels-last maps (the K3C / K2C
  * outputs): g, out [n, h+2, w+2, C] (out = the padded forward output) -> gp [n, h, w, C] =
  * (sum of g's copies) * (out > 0 ? 1 : slope); C % 4 == 0, 16-B aligned. */

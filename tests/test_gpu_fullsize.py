@@ -1164,6 +1164,69 @@ def test_elu_upsample_pad_matches_aten():
     close(gf, gm, 'fused decoder input gradient', atol=1e-5 * float(gm.abs().max()), rtol=1e-4)
 
 
+def test_channels_last_decoder_bf16():
+    """Config 3's channels-last bf16 decoder (VFD_DEC_CL): the NHWC reflect pad and ELU [+ up] + pad
+    kernels bit-identical to the NCHW ones (forward and d y: the same per-channel sums in the same
+    order), the bias partials equal to the NCHW block sums up to fp32 summation order; then the
+    whole fused decoder under bf16 autocast, channels-last against NCHW, both against the fp32
+    decoder (channels-last no further from it than NCHW, x1.5 + 1e-3: MIOpen's per-layout bf16
+    algorithms differ), and its maps stayed channels-last."""
+    import copy
+    from vfdepth_amd import kernels as KN
+    from vfdepth_amd.network import FusionDepthDecoder
+    cl = torch.channels_last
+    gen = torch.Generator(device=DEV).manual_seed(211)
+    for shape in ((6, 256, 48, 80), (2, 4, 3, 2), (3, 16, 37, 53)):
+        x = torch.randn(shape, device=DEV, generator=gen).to(torch.bfloat16)
+        a = x.clone().requires_grad_(True)
+        b = x.contiguous(memory_format=cl).requires_grad_(True)
+        ya, yb = KN.ReflectPad1.apply(a), KN.ReflectPad1.apply(b)
+        assert yb.is_contiguous(memory_format=cl) and not yb.is_contiguous() and torch.equal(ya, yb), shape
+        g = torch.randn(ya.shape, device=DEV, generator=gen).to(torch.bfloat16)
+        ya.backward(g)
+        yb.backward(g)
+        assert torch.equal(a.grad, b.grad), f'reflect pad NHWC backward {shape}'
+    for shape, up in (((6, 32, 96, 160), True), ((6, 16, 192, 320), False), ((2, 8, 1, 1), True),
+                      ((3, 4, 5, 7), True), ((2, 64, 3, 5), False)):
+        for dt in (torch.bfloat16, torch.float32):
+            y = torch.randn(shape, device=DEV, generator=gen).to(dt)
+            g = torch.randn(shape[0], shape[1], (shape[2] << up) + 2, (shape[3] << up) + 2, device=DEV,
+                            generator=gen).to(dt)
+            oa = KN._elu_up_pad_fwd(y, int(up))
+            ob = KN._elu_up_pad_fwd(y.contiguous(memory_format=cl), int(up))
+            # (a 1x1 map is NCHW- and channels-last-contiguous at once: it takes the NCHW kernels)
+            assert ob.is_contiguous(memory_format=cl) or shape[2] * shape[3] == 1
+            assert torch.equal(oa, ob), f'elu_up_pad NHWC {shape} {dt}'
+            da, dba = KN._elu_up_pad_bwd(g, y, int(up), bias_grad=True)
+            db_, dbb = KN._elu_up_pad_bwd(g.contiguous(memory_format=cl), y.contiguous(memory_format=cl), int(up),
+                                          bias_grad=True)
+            assert torch.equal(da, db_), f'elu_up_pad NHWC backward {shape} {dt}'
+            # fp32 sums of up to 92k terms in two orders: cancelling channels judged on the sum of |d y|
+            close(dbb, dba, f'elu_up_pad NHWC bias sums {shape} {dt}', rtol=1e-5,
+                  atol=1e-6 * float(da.float().abs().sum((0, 2, 3)).max()))
+    dec = FusionDepthDecoder(2, [64, 64, 128], [16, 32, 64, 128, 256], [0], use_skips=False).to(DEV)
+    feat = torch.randn(6, 128, 48, 80, device=DEV, generator=gen)
+    gd = torch.randn(6, 1, 384, 640, device=DEV, generator=gen)
+    outs = []
+    for amp, dec_cl in ((False, False), (True, False), (True, True)):
+        d = copy.deepcopy(dec)
+        f = feat.to(torch.bfloat16 if amp else torch.float32, copy=True).requires_grad_(True)
+        KN._DEC_CL = dec_cl
+        try:
+            with torch.autocast(device_type='cuda', dtype=torch.bfloat16, enabled=amp):
+                assert d._fused_ok(f)
+                disp = d([None, None, f])[('disp', 0)]
+        finally:
+            KN._DEC_CL = True
+        disp.float().backward(gd)
+        outs.append([disp.float(), f.grad.float(), d.convs[('upconv', 2, 0)][0].weight.grad,
+                     d.convs[('upconv', 0, 1)][0].bias.grad])
+    for what, r, n, c in zip(['disparity', 'd input', 'first conv d weight', 'last conv d bias'], *outs):
+        en, ec = _fro(n, r), _fro(c, r)
+        print(f'decoder {what}: bf16 NCHW {en:.3g}, bf16 channels-last {ec:.3g} (vs fp32)')
+        assert ec <= 1.5 * en + 1e-3, f'decoder {what}: channels-last {ec:.3g} vs NCHW {en:.3g} from fp32'
+
+
 def test_weight_relayouts_match_torch_chains():
     """weights.hip against the ATen permute / flip / pad chains it replaces (pure data movement:
     bit-identical): K3C forward fragments, K3C data-gradient copy, K2C fragments over the pose map's

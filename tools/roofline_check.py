@@ -9,6 +9,7 @@ last --prof-calls calls of each kernel only (the bench's profiled steps are its 
 both fractions and their ratio; exit 1 if they differ by more than 2 %."""
 import argparse
 import csv
+import gzip
 import json
 import sys
 
@@ -18,7 +19,8 @@ OP_KERNELS = {
     'proj_conv_dgrad': ('vfd::pcdf_main_k', 'vfd::pcdf_reduce_k', 'vfd::pcd_main_k', 'vfd::pcd_reduce_k',
                         'vfd::pct_main_k', 'vfd::pct_reduce_k'),
     'proj_conv_wgrad': ('vfd::pcw_main_k', 'vfd::pcw_reduce_k', 'vfd::pcw_bias_k', 'vfd::pcw_bias_fin_k'),
-    'pad_conv_fwd': ('vfd::ppc_main_k', 'vfd::ppcb_main_k', 'void vfd::ppc_reduce_k'),
+    'pad_conv_fwd': ('vfd::ppc_main_k', 'vfd::ppcb_main_k', 'void vfd::ppc_reduce_k', '_ZN3vfd11ppcb_main_k'),
+    'pad_conv_dgrad': ('_ZN3vfd10ppd_main_k', 'vfd::ppd_reduce_k'),
     'fuse_pose_fwd': ('void vfd::fuse_pose_fwd_k',),
     'voxel_project_bwd': ('void vfd::vpb_main_k', 'vfd::vpb_fold_k', 'vfd::vpb_split_k'),
 }
@@ -63,7 +65,8 @@ def main():
            'rocprof_per_call_min_us': per_call_min}
     if a.trace:
         names = {x['Name'] for x in mine}
-        tr = [x for x in csv.DictReader(open(a.trace)) if x['Kernel_Name'] in names]
+        fh = gzip.open(a.trace, 'rt') if a.trace.endswith('.gz') else open(a.trace)
+        tr = [x for x in csv.DictReader(fh) if x['Kernel_Name'] in names]
         by = {}
         for x in sorted(tr, key=lambda x: int(x['Start_Timestamp'])):
             by.setdefault(x['Kernel_Name'], []).append((int(x['End_Timestamp']) - int(x['Start_Timestamp'])) / 1e3)

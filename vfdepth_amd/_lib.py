@@ -132,6 +132,11 @@ _SIGS = {
     'vfd_elu_up_pad1_fwd': (c_int, [c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_int, c_int, c_void_p]),
     'vfd_elu_up_pad1_bwd': (c_int, [c_fp, c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_int, c_fp, c_int, c_void_p]),
     'vfd_elu_up_pad1_bwd_blocks': (c_int, [c_int, c_int]),
+    'vfd_elu_up_pad1_nhwc_fwd': (c_int, [c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_int, c_int, c_int, c_int,
+                                         c_void_p]),
+    'vfd_elu_up_pad1_nhwc_bwd': (c_int, [c_fp, c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_int, c_int, c_int, c_fp,
+                                         c_int, c_void_p]),
+    'vfd_elu_up_pad1_nhwc_bwd_blocks': (c_int, [ctypes.c_longlong, c_int, c_int, c_int]),
     'vfd_lrelu_pad1_bwd_nhwc': (c_int, [c_fp, c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_int, c_float, c_void_p]),
     'vfd_lrelu_pad1_bwd_nhwc_t': (c_int, [c_fp, c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_int, c_float, c_int, c_int,
                                           c_void_p]),

@@ -202,6 +202,109 @@ __global__ __launch_bounds__(256) void elu_up_pad_bwd_k(const T* __restrict__ g,
   }
 }
 
+// ---- channels-last forms (config 3's bf16 decoders keep their maps NHWC, so MIOpen's convolutions
+// run without their NCHW <-> NHWC transposes).  Same per-channel arithmetic as the NCHW kernels:
+// thread = (padded output pixel | source pixel, channel quad), 8-B bf16 / 16-B fp32 accesses.
+template <int UP, bool ACT, typename T>
+__global__ __launch_bounds__(256) void elu_up_pad_fwd_nhwc_k(const T* __restrict__ y, T* __restrict__ out,
+                                                             long long n_img, int h, int w, int Q) {
+  const int Hu = h << UP, Wu = w << UP;
+  const int ho = Hu + 2, wo = Wu + 2;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_img * ho * wo * Q) return;
+  const int q = (int)(i % Q);
+  const long long pix = i / Q;
+  const int X = (int)(pix % wo);
+  const long long r = pix / wo;
+  const int Y = (int)(r % ho);
+  const long long n = r / ho;
+  const int sy = rp_src(Y, Hu) >> UP, sx = rp_src(X, Wu) >> UP;
+  float4 v = ld4(y + ((n * h + sy) * w + sx) * (4LL * Q) + 4 * q);
+  if (ACT) {
+    v.x = elu1(v.x);
+    v.y = elu1(v.y);
+    v.z = elu1(v.z);
+    v.w = elu1(v.w);
+  }
+  st4(out + pix * (4LL * Q) + 4 * q, v);
+}
+
+template <int UP, typename T>
+__device__ __forceinline__ float4 eup_row_nhwc(const T* __restrict__ gr, const EupIdx& C, int ld) {
+  // eup_row's order per channel: a (+ b) then (+ fma * ma) + fmb * mb
+  float4 t = ld4(gr + (size_t)C.a * ld);
+  if (UP) {
+    const float4 b = ld4(gr + (size_t)C.b * ld);
+    t.x += b.x; t.y += b.y; t.z += b.z; t.w += b.w;
+  }
+  if (C.fma != 0.f || C.fmb != 0.f) {
+    const float4 ma = ld4(gr + (size_t)C.ma * ld), mb = ld4(gr + (size_t)C.mb * ld);
+    t.x = (t.x + C.fma * ma.x) + C.fmb * mb.x;
+    t.y = (t.y + C.fma * ma.y) + C.fmb * mb.y;
+    t.z = (t.z + C.fma * ma.z) + C.fmb * mb.z;
+    t.w = (t.w + C.fma * ma.w) + C.fmb * mb.w;
+  }
+  return t;
+}
+
+// part (optional, [gridDim.x][4 Q]): the block's per-channel sums of dy (conv bias partials; a block
+// covers whole pixels: 256 / Q of them), summed over blocks by the caller
+template <int UP, bool ACT, typename T>
+__global__ __launch_bounds__(256) void elu_up_pad_bwd_nhwc_k(const T* __restrict__ g, const T* __restrict__ y,
+                                                             T* __restrict__ dy, long long n_img, int h, int w, int Q,
+                                                             float* __restrict__ part) {
+  __shared__ float4 red[256];
+  const int Hu = h << UP, Wu = w << UP;
+  const int wo = Wu + 2, ld = 4 * Q;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = i < n_img * h * w * Q;
+  float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (live) {
+    const int q = (int)(i % Q);
+    const long long pix = i / Q;
+    const int sx = (int)(pix % w);
+    const long long rr = pix / w;
+    const int sy = (int)(rr % h);
+    const long long n = rr / h;
+    const EupIdx R = eup_idx<UP>(sy, h), C = eup_idx<UP>(sx, w);
+    const T* gp = g + (size_t)n * (Hu + 2) * wo * ld + 4 * q;
+    // per row: eup_row over the columns; rows a (+ b) then the mirrors, as elu_up_pad_bwd_k
+    float4 s = eup_row_nhwc<UP>(gp + (size_t)R.a * wo * ld, C, ld);
+    if (UP) {
+      const float4 t = eup_row_nhwc<UP>(gp + (size_t)R.b * wo * ld, C, ld);
+      s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
+    }
+    if (R.fma != 0.f || R.fmb != 0.f) {
+      const float4 ta = eup_row_nhwc<UP>(gp + (size_t)R.ma * wo * ld, C, ld);
+      s.x += R.fma * ta.x; s.y += R.fma * ta.y; s.z += R.fma * ta.z; s.w += R.fma * ta.w;
+      const float4 tb = eup_row_nhwc<UP>(gp + (size_t)R.mb * wo * ld, C, ld);
+      s.x += R.fmb * tb.x; s.y += R.fmb * tb.y; s.z += R.fmb * tb.z; s.w += R.fmb * tb.w;
+    }
+    r = s;
+    const size_t o = (size_t)pix * ld + 4 * q;
+    if (ACT) {
+      const float4 v = ld4(y + o);
+      float ov;
+      ov = elu1(v.x); r.x = ov <= 0.f ? s.x * (ov + 1.f) : s.x;
+      ov = elu1(v.y); r.y = ov <= 0.f ? s.y * (ov + 1.f) : s.y;
+      ov = elu1(v.z); r.z = ov <= 0.f ? s.z * (ov + 1.f) : s.z;
+      ov = elu1(v.w); r.w = ov <= 0.f ? s.w * (ov + 1.f) : s.w;
+    }
+    st4(dy + o, r);
+  }
+  if (part) {                                  // block-uniform: fixed-order sums over the block's pixels
+    red[threadIdx.x] = r;
+    __syncthreads();
+    if (threadIdx.x < Q) {
+      float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int k = threadIdx.x; k < 256; k += Q) {
+        t.x += red[k].x; t.y += red[k].y; t.z += red[k].z; t.w += red[k].w;
+      }
+      *reinterpret_cast<float4*>(part + (size_t)blockIdx.x * ld + 4 * threadIdx.x) = t;
+    }
+  }
+}
+
 }  // namespace vfd
 
 using namespace vfd;
@@ -312,6 +415,58 @@ int vfd_elu_up_pad1_bwd(const void* g, const void* y, void* dy, long long planes
     else elu_up_pad_bwd_k<0, true><<<grid, 256, 0, s>>>(gf, yf, (float*)dy, planes, h, w, psum);
   }
   return fail_launch("elu_up_pad1_bwd");
+}
+
+// channels-last [n_img, h, w, C] -> [n_img, Hu + 2, Wu + 2, C], C % 4 == 0 (act 0: the plain pad)
+int vfd_elu_up_pad1_nhwc_fwd(const void* y, void* out, long long n_img, int h, int w, int C, int up, int act,
+                             int dtype, void* stream) {
+  VFD_REQUIRE(y && out && n_img > 0 && h >= 1 && w >= 1 && C > 0 && C % 4 == 0 && (up == 0 || up == 1) &&
+                  (act == 0 || act == 1) && (dtype == 0 || dtype == 1) && (h << up) >= 2 && (w << up) >= 2 &&
+                  (((uintptr_t)y | (uintptr_t)out) & (dtype ? 7 : 15)) == 0,
+              "elu_up_pad1_nhwc: bad arguments (C %% 4 == 0, up in {0, 1}, padded side >= 2, aligned maps)");
+  hipStream_t s = (hipStream_t)stream;
+  ProfScope ps(act ? K_ELU_PAD : K_REFLECT_PAD, s);
+  const long long total = n_img * (long long)((h << up) + 2) * ((w << up) + 2) * (C / 4);
+  const unsigned grid = (unsigned)((total + 255) / 256);
+#define VFD_EUP_N(U, A, T) elu_up_pad_fwd_nhwc_k<U, A, T><<<grid, 256, 0, s>>>((const T*)y, (T*)out, n_img, h, w, C / 4)
+  if (dtype == 1) {
+    if (up) { if (act) VFD_EUP_N(1, true, __bf16); else VFD_EUP_N(1, false, __bf16); }
+    else { if (act) VFD_EUP_N(0, true, __bf16); else VFD_EUP_N(0, false, __bf16); }
+  } else {
+    if (up) { if (act) VFD_EUP_N(1, true, float); else VFD_EUP_N(1, false, float); }
+    else { if (act) VFD_EUP_N(0, true, float); else VFD_EUP_N(0, false, float); }
+  }
+#undef VFD_EUP_N
+  return fail_launch("elu_up_pad1_nhwc_fwd");
+}
+
+int vfd_elu_up_pad1_nhwc_bwd_blocks(long long n_img, int h, int w, int C) {
+  return (int)((n_img * h * w * (C / 4) + 255) / 256);
+}
+
+// y (act 1: the conv's pre-activation, channels-last [n_img, h, w, C]) may be NULL for act 0
+int vfd_elu_up_pad1_nhwc_bwd(const void* g, const void* y, void* dy, long long n_img, int h, int w, int C, int up,
+                             int act, float* part, int dtype, void* stream) {
+  VFD_REQUIRE(g && dy && (y || !act) && n_img > 0 && h >= 1 && w >= 1 && C > 0 && C % 4 == 0 && 256 % (C / 4) == 0 &&
+                  (up == 0 || up == 1) && (act == 0 || act == 1) && (dtype == 0 || dtype == 1) &&
+                  (h << up) >= 2 && (w << up) >= 2 &&
+                  (((uintptr_t)g | (uintptr_t)y | (uintptr_t)dy | (uintptr_t)part) & (dtype ? 7 : 15)) == 0,
+              "elu_up_pad1_nhwc_bwd: bad arguments (C %% 4 == 0, C / 4 divides 256, up in {0, 1}, padded side >= 2, "
+              "aligned maps)");
+  hipStream_t s = (hipStream_t)stream;
+  ProfScope ps(act ? K_ELU_PAD : K_REFLECT_PAD, s);
+  const unsigned grid = (unsigned)vfd_elu_up_pad1_nhwc_bwd_blocks(n_img, h, w, C);
+#define VFD_EUPB_N(U, A, T) \
+  elu_up_pad_bwd_nhwc_k<U, A, T><<<grid, 256, 0, s>>>((const T*)g, (const T*)y, (T*)dy, n_img, h, w, C / 4, part)
+  if (dtype == 1) {
+    if (up) { if (act) VFD_EUPB_N(1, true, __bf16); else VFD_EUPB_N(1, false, __bf16); }
+    else { if (act) VFD_EUPB_N(0, true, __bf16); else VFD_EUPB_N(0, false, __bf16); }
+  } else {
+    if (up) { if (act) VFD_EUPB_N(1, true, float); else VFD_EUPB_N(1, false, float); }
+    else { if (act) VFD_EUPB_N(0, true, float); else VFD_EUPB_N(0, false, float); }
+  }
+#undef VFD_EUPB_N
+  return fail_launch("elu_up_pad1_nhwc_bwd");
 }
 
 }  // extern "C"

@@ -1593,15 +1593,52 @@ class BatchNormAct(torch.autograd.Function):
 # =============================================================================================
 # Reflect padding by one pixel (the decoders' reflect 3x3 convs), deterministic backward
 # =============================================================================================
+_DEC_CL = os.environ.get('VFD_DEC_CL', '1') != '0'       # bf16 decoders keep their maps channels-last
+
+
+def _nhwc_ok(t):
+    """The channels-last reflectpad.hip kernels apply: a 4-d channels-last (not also NCHW-contiguous)
+    map whose channel count is a multiple of 4 with C / 4 dividing 256 (the bias partials' blocks
+    cover whole pixels)."""
+    if t.dim() != 4 or t.is_contiguous() or not t.is_contiguous(memory_format=torch.channels_last):
+        return False
+    q, r = divmod(t.shape[1], 4)
+    return r == 0 and 256 % q == 0 and t.data_ptr() % 16 == 0
+
+
+def _as_nhwc(t, like):
+    """t in the layout of `like` (channels-last), 16-B aligned, for the NHWC kernels."""
+    t = t.to(like.dtype).contiguous(memory_format=torch.channels_last)
+    return t if t.data_ptr() % 16 == 0 else t.clone(memory_format=torch.channels_last)
+
+
+def decoder_channels_last(x):
+    """Whether a bf16 decoder input goes channels-last (VFD_DEC_CL, default on): MIOpen's bf16
+    convs then read / write NHWC directly instead of transposing every NCHW map around an NHWC
+    solver (config 3's batched_transpose_* kernels)."""
+    return _DEC_CL and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[1] % 4 == 0 and \
+        256 % (x.shape[1] // 4) == 0
+
+
 class ReflectPad1(torch.autograd.Function):
-    """F.pad(x, (1, 1, 1, 1), mode='reflect') for NCHW fp32 or bf16 x (reflectpad.hip); the backward
-    gathers each pixel's copies in a fixed order in fp32 (ATen's scatters with atomics, in bf16
-    under autocast: 0.5 ms per decoder pad at config 3)."""
+    """F.pad(x, (1, 1, 1, 1), mode='reflect') for NCHW or channels-last fp32 or bf16 x
+    (reflectpad.hip); the backward gathers each pixel's copies in a fixed order in fp32 (ATen's
+    scatters with atomics, in bf16 under autocast: 0.5 ms per decoder pad at config 3)."""
 
     @staticmethod
     def forward(ctx, x):
         lib = L.load()
         _check_device(x, 'reflect pad input')
+        ctx.nhwc = _nhwc_ok(x)
+        if ctx.nhwc:
+            n, c, h, w = x.shape
+            y = torch.empty(n, c, h + 2, w + 2, dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+            L.check(lib.vfd_elu_up_pad1_nhwc_fwd(x.data_ptr(), y.data_ptr(), n, h, w, c, 0, 0, _dt(x), L.stream()),
+                    'elu_up_pad1_nhwc_fwd')
+            if L.PROF_ON:
+                L.ALG_BYTES['reflect_pad'] += (x.numel() + y.numel()) * x.element_size()
+            ctx.shape, ctx.dtype = tuple(x.shape), x.dtype
+            return y
         x = x.contiguous()
         *lead, h, w = x.shape
         y = torch.empty(*lead, h + 2, w + 2, dtype=x.dtype, device=x.device)
@@ -1615,6 +1652,15 @@ class ReflectPad1(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         lib = L.load()
+        if ctx.nhwc:
+            n, c, h, w = ctx.shape
+            dx = torch.empty(ctx.shape, dtype=ctx.dtype, device=g.device, memory_format=torch.channels_last)
+            g = _as_nhwc(g, dx)
+            L.check(lib.vfd_elu_up_pad1_nhwc_bwd(g.data_ptr(), None, dx.data_ptr(), n, h, w, c, 0, 0, None, _dt(dx),
+                                                 L.stream()), 'elu_up_pad1_nhwc_bwd')
+            if L.PROF_ON:
+                L.ALG_BYTES['reflect_pad'] += (g.numel() + dx.numel()) * dx.element_size()
+            return dx
         g = g.to(ctx.dtype).contiguous()
         h, w = ctx.shape[-2:]
         dx = torch.empty(ctx.shape, dtype=ctx.dtype, device=g.device)
@@ -1645,6 +1691,15 @@ class EluUpPad(torch.autograd.Function):
 def _elu_up_pad_fwd(y, u):
     lib = L.load()
     _check_device(y, 'elu_up_pad input')
+    if _nhwc_ok(y):
+        n, c, h, w = y.shape
+        out = torch.empty(n, c, (h << u) + 2, (w << u) + 2, dtype=y.dtype, device=y.device,
+                          memory_format=torch.channels_last)
+        L.check(lib.vfd_elu_up_pad1_nhwc_fwd(y.data_ptr(), out.data_ptr(), n, h, w, c, u, 1, _dt(y), L.stream()),
+                'elu_up_pad1_nhwc_fwd')
+        if L.PROF_ON:
+            L.ALG_BYTES['elu_pad'] += (y.numel() + out.numel()) * y.element_size()
+        return out
     y = y.contiguous()
     *lead, h, w = y.shape
     out = torch.empty(*lead, (h << u) + 2, (w << u) + 2, dtype=y.dtype, device=y.device)
@@ -1657,9 +1712,21 @@ def _elu_up_pad_fwd(y, u):
 
 
 def _elu_up_pad_bwd(g, y, u, bias_grad=False):
-    """d y of the fused ELU [+ up] + pad, and (bias_grad) the per-plane block partial sums of d y
-    [planes, blocks] (the producing conv's bias gradient before its fixed-order sum)."""
+    """d y of the fused ELU [+ up] + pad, and (bias_grad) its per-channel sum [C] in fp32 (the
+    producing conv's bias gradient: fixed-order block partials from the kernel, then one sum)."""
     lib = L.load()
+    if _nhwc_ok(y):
+        n, c, h, w = y.shape
+        dy = torch.empty_like(y, memory_format=torch.channels_last)
+        g = _as_nhwc(g, y)
+        part = (torch.empty(lib.vfd_elu_up_pad1_nhwc_bwd_blocks(n, h, w, c), c, device=y.device)
+                if bias_grad else None)
+        L.check(lib.vfd_elu_up_pad1_nhwc_bwd(g.data_ptr(), y.data_ptr(), dy.data_ptr(), n, h, w, c, u, 1,
+                                             part.data_ptr() if part is not None else None, _dt(y), L.stream()),
+                'elu_up_pad1_nhwc_bwd')
+        if L.PROF_ON:
+            L.ALG_BYTES['elu_pad'] += (g.numel() + 2 * y.numel()) * y.element_size()
+        return dy, (part.sum(0) if part is not None else None)
     g = g.to(y.dtype).contiguous()
     h, w = y.shape[-2:]
     dy = torch.empty_like(y)
@@ -1670,7 +1737,7 @@ def _elu_up_pad_bwd(g, y, u, bias_grad=False):
             'elu_up_pad1_bwd')
     if L.PROF_ON:
         L.ALG_BYTES['elu_pad'] += (g.numel() + 2 * y.numel()) * y.element_size()
-    return dy, psum
+    return dy, (psum.view(y.shape[0], y.shape[1], -1).sum((0, 2)) if psum is not None else None)
 
 
 class ConvEluUpPad(torch.autograd.Function):
@@ -1706,8 +1773,7 @@ class ConvEluUpPad(torch.autograd.Function):
     def backward(ctx, g):
         xp, weight, y = ctx.saved_tensors
         need = ctx.needs_input_grad
-        dy, psum = _elu_up_pad_bwd(g, y, ctx.u, bias_grad=need[2])
-        db = psum.view(y.shape[0], y.shape[1], -1).sum((0, 2)) if need[2] else None
+        dy, db = _elu_up_pad_bwd(g, y, ctx.u, bias_grad=need[2])
         dx = dw = None
         N, CI, Hp, Wp = xp.shape
         CO = weight.shape[0]

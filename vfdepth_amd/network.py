@@ -110,7 +110,10 @@ class FusionDepthDecoder(nn.Module):
         previous block's kernel wrote (padding 0), the ELU / upsample / pad intermediates never
         exist."""
         out = {}
-        xp = KN.ReflectPad1.apply(input_features[-1])
+        x = input_features[-1]
+        if KN.decoder_channels_last(x):
+            x = x.contiguous(memory_format=torch.channels_last)
+        xp = KN.ReflectPad1.apply(x)
         for i in range(self.level_in, -1, -1):
             c0 = self.convs[('upconv', i, 0)][0]
             xp = KN.ConvEluUpPad.apply(xp, c0.weight, c0.bias, True)

@@ -667,10 +667,19 @@ __device__ __forceinline__ void pdc_tap(const PdcGeom& g, int c, int tl, int* ky
 }
 
 // loader waves (tid 0..255): staged row r = G row i0 - 1 + r (stride 1: i0 - 2 + r), staged column
-// c = G column c - 1 (stride 1: c - 2); channels ch * OC ..
+// c = G column c - 1 (stride 1: c - 2); channels ch * OC ..  The thread's staged positions p = p0 +
+// PPP k are the same for every atom: their (row, column) walk starts from (rc0 >> 16, rc0 & 0xFFFF)
+// (one division per thread per kernel, pdc_rc0) and steps by PPP without dividing.
+template <typename T, typename TG>
+__device__ __forceinline__ int pdc_rc0(const PdcGeom& g, int tid) {
+  constexpr int QP = PdCfg<T>::OC / PgVecP<TG>::CH;
+  const int p0 = tid / QP;
+  return ((p0 / g.cols) << 16) | (p0 % g.cols);
+}
+
 template <typename T, typename TG>
 __device__ __forceinline__ void pdc_stage(const PdcGeom& g, T* __restrict__ dst, const TG* __restrict__ gp, int atom,
-                                          int tid) {
+                                          int tid, int rc0) {
   typedef PgVecP<TG> PV;
   constexpr int OC = PdCfg<T>::OC, XS = PdCfg<T>::XS, CH = PV::CH, QP = OC / CH, PPP = 256 / QP;
   const int t = atom / g.och, ch = atom - t * g.och;
@@ -680,26 +689,41 @@ __device__ __forceinline__ void pdc_stage(const PdcGeom& g, T* __restrict__ dst,
   const int q = tid % QP;
   const TG* src = gp + (size_t)tl.b * g.ho * g.wo * PP_O + ch * OC + CH * q;
   constexpr int U = VFD_PD_U;
+  const int cstep = PPP % g.cols, rstep = PPP / g.cols;   // uniform
+  int r = rc0 >> 16, c = rc0 & 0xFFFF;
   for (int p0 = tid / QP; p0 < npos; p0 += U * PPP) {
     typename PV::V v[U];
+    int pos[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int p = p0 + PPP * u;
-      const int r = p / g.cols, c = p - r * g.cols;
       const int y = r0 + r, x = c - c0;
+      pos[u] = p;
 #ifdef VFD_PD_NOSTAGE
       v[u] = PV::zero();
 #else
       v[u] = (p < npos && y >= 0 && y < g.ho && x >= 0 && x < g.wo) ? PV::load(src + ((size_t)y * g.wo + x) * PP_O)
                                                                    : PV::zero();
 #endif
+      c += cstep;
+      r += rstep;
+      if (c >= g.cols) {
+        c -= g.cols;
+        ++r;
+      }
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int p = p0 + PPP * u;
-      if (p < npos) PV::template put<T>(dst + p * XS + CH * q, v[u]);
-    }
+    for (int u = 0; u < U; ++u)
+      if (pos[u] < npos) PV::template put<T>(dst + pos[u] * XS + CH * q, v[u]);
   }
+}
+
+// m / d for 0 <= m < 2^22, d >= 1, with rd = 1 / d: float quotient plus one correction step
+__device__ __forceinline__ int pdc_div(int m, int d, float rd) {
+  int q = (int)((float)m * rd);
+  const int rem = m - q * d;
+  q += (rem >= d) - (rem < 0);
+  return q;
 }
 
 template <typename T, typename TG>
@@ -717,12 +741,14 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppd_main_k(PdcGeom g, const TG*
   if (a_lo >= a_hi) return;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const bool compute = wv < PP_WAVES;
-  if (!compute) pdc_stage<T, TG>(g, lds, gp, a_lo, threadIdx.x - 64 * PP_WAVES);
+  const int rc0 = compute ? 0 : pdc_rc0<T, TG>(g, threadIdx.x - 64 * PP_WAVES);
+  if (!compute) pdc_stage<T, TG>(g, lds, gp, a_lo, threadIdx.x - 64 * PP_WAVES, rc0);
   __syncthreads();
   if (!compute) {
     for (int atom = a_lo; atom < a_hi; ++atom) {
       if (atom + 1 < a_hi)
-        pdc_stage<T, TG>(g, lds + ((atom + 1 - a_lo) & 1) * g.lds_elems, gp, atom + 1, threadIdx.x - 64 * PP_WAVES);
+        pdc_stage<T, TG>(g, lds + ((atom + 1 - a_lo) & 1) * g.lds_elems, gp, atom + 1, threadIdx.x - 64 * PP_WAVES,
+                         rc0);
       __syncthreads();
     }
     return;
@@ -769,11 +795,12 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppd_main_k(PdcGeom g, const TG*
     const int rbase = tl.i0 - (g.s == 1 ? 2 : 1), cbase = g.s == 1 ? 2 : 1;
     const int m0w = tl.m0 + 32 * MB * wm;             // the wave's first position
     int pij[MB];                                      // (class row << 16) | class column of the lane's positions
+    const float rw = 1.f / (float)wcc;
 #pragma unroll
     for (int a = 0; a < MB; ++a) {
       int m = m0w + 32 * a + li;
       m = m < hw ? m : hw - 1;
-      const int i = m / wcc;
+      const int i = pdc_div(m, wcc, rw);
       pij[a] = (i << 16) | (m - i * wcc);
     }
     const T* xb = lds + ((atom - a_lo) & 1) * g.lds_elems;
@@ -867,7 +894,7 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppd_main_k(PdcGeom g, const TG*
 #pragma unroll
         for (int a = 0; a < MB; ++a) {
           const int mb = m0w + 32 * a + 4 * lh;
-          const int ib = mb / wcc, jb = mb - ib * wcc;
+          const int ib = pdc_div(mb, wcc, rw), jb = mb - ib * wcc;
           float* pa = dx + (((size_t)tl.b * g.hp + st * ib + py) * g.wp + st * jb + px) * g.cin + n0;
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
@@ -876,12 +903,14 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppd_main_k(PdcGeom g, const TG*
             if (wcc >= 28) {
               off = d * colp + (jb + d >= wcc ? rowp - wcc * colp : 0);
             } else {
-              const int i2 = (mb + d) / wcc, j2 = mb + d - i2 * wcc;
+              const int i2 = pdc_div(mb + d, wcc, rw), j2 = mb + d - i2 * wcc;
               off = (i2 - ib) * rowp + (j2 - jb) * colp;
             }
 #pragma unroll
             for (int b = 0; b < NB; ++b) {
+#ifndef VFD_PD_NOSTORE
               if (mb + d < hw && n0 + 32 * b < g.cin) pa[off + 32 * b] = acc[a][b][r];
+#endif
               acc[a][b][r] = 0.f;
             }
           }

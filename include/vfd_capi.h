@@ -529,6 +529,11 @@ int vfd_smooth_bwd(int B, int N, int H, int W, const float* disp, const float* c
 int vfd_aggregate_fwd(int BN, int C, int h, int w, const float* base, int n_levels,
                       const float* const* levels, const int* level_hw, const float* bias, float* out,
                       void* stream);
+/* the same with channels-last inputs read in place: base [BN, h, w, C], levels[k] [BN, hs, ws, C] of
+ * dtype 0 fp32 / 1 bf16 (config 3's bf16 1x1-conv products), out NCHW fp32 [BN, C, h, w]; per
+ * element the arithmetic of vfd_aggregate_fwd on the fp32 values (bit-identical). */
+int vfd_aggregate_fwd_cl(int BN, int C, int h, int w, const void* base, int n_levels, const void* const* levels,
+                         const int* level_hw, const float* bias, float* out, int dtype, void* stream);
 /* backward of vfd_aggregate_fwd in one launch (one workgroup per plane, LDS-resident):
  * d = g * LReLU'(out) [BN, C, h, w] (the base's gradient), psum [BN * C] = its plane sums (the
  * caller sums them over n for the bias gradient), dlevels[k] [BN, C, level_hw[2k], level_hw[2k+1]]

@@ -1124,6 +1124,36 @@ def test_aggregate_matches_aten():
             close(t.grad, r.grad, f'aggregate d level {tuple(t.shape)}', atol=1e-5, rtol=1e-5)
 
 
+def test_aggregate_channels_last_bit_identical():
+    """AggregateUp on channels-last fp32 / bf16 products (config 3's encoders) read in place
+    (vfd_aggregate_fwd_cl) against the NCHW fp32 path on the same values: forward bit-identical
+    (same fp32 arithmetic per element), backward unchanged (same kernel); config-3 shapes, a
+    ragged one and a level of the base's own size."""
+    from vfdepth_amd import kernels as KN
+    cl = torch.channels_last
+    gen = torch.Generator(device=DEV).manual_seed(77)
+    cases = (((12, 256, 48, 80), ((24, 40), (12, 20), (6, 10))), ((3, 20, 7, 45), ((4, 23), (7, 45))),
+             ((2, 64, 5, 6), ()))
+    for shape, lv in cases:
+        BN, C, h, w = shape
+        for dt in (torch.bfloat16, torch.float32):
+            base = torch.randn(shape, device=DEV, generator=gen).to(dt).contiguous(memory_format=cl)
+            levels = [torch.randn(BN, C, hs, ws, device=DEV, generator=gen).to(dt).contiguous(memory_format=cl)
+                      for hs, ws in lv]
+            bias = torch.randn(C, device=DEV, generator=gen)
+            assert KN._agg_cl_ok(base, levels)
+            a = [t.detach().clone().requires_grad_(True) for t in [base] + levels]
+            r = [t.detach().float().contiguous().requires_grad_(True) for t in [base] + levels]
+            out = KN.AggregateUp.apply(a[0], bias, *a[1:])
+            ref = KN.AggregateUp.apply(r[0], bias, *r[1:])
+            assert out.dtype == torch.float32 and out.is_contiguous() and torch.equal(out, ref), (shape, dt)
+            g = torch.randn(shape, device=DEV, generator=gen)
+            out.backward(g)
+            ref.backward(g)
+            for t, u in zip(a, r):
+                assert t.grad.dtype == dt and torch.equal(t.grad, u.grad.to(dt)), (shape, dt, tuple(t.shape))
+
+
 def test_elu_upsample_pad_matches_aten():
     """The decoders' fused ELU [+ nearest 2x upsample] + reflect pad against F.elu ->
     F.interpolate(nearest) -> F.pad(reflect), forward and backward, at the config-2 decoder shapes

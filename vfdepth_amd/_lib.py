@@ -82,6 +82,8 @@ _SIGS = {
     'vfd_photo_fwd': (c_int, [ctypes.POINTER(PhotoDesc)] + [c_fp] * 13 + [c_size_t, c_void_p]),
     'vfd_photo_bwd': (c_int, [ctypes.POINTER(PhotoDesc)] + [c_fp] * 9 + [c_void_p]),
     'vfd_aggregate_fwd': (c_int, [c_int] * 4 + [c_fp, c_int, ctypes.POINTER(c_fp), ctypes.POINTER(c_int), c_fp, c_fp, c_void_p]),
+    'vfd_aggregate_fwd_cl': (c_int, [c_int] * 4 + [c_fp, c_int, ctypes.POINTER(c_fp), ctypes.POINTER(c_int), c_fp, c_fp,
+                                                   c_int, c_void_p]),
     'vfd_proj_conv_fwd_workspace': (c_size_t, [ctypes.POINTER(VoxelDesc)]),
     'vfd_proj_conv_fwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 5 + [c_int, c_fp, c_fp, c_fp, c_size_t, c_void_p]),
     'vfd_proj_conv_fwd_bf16': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 5 + [c_int, c_fp, c_fp, c_fp, c_size_t, c_void_p]),

@@ -287,7 +287,107 @@ __global__ __launch_bounds__(AGG_BT) void aggregate_plane_bwd_k(int h, int w, co
   }
 }
 
+// ---- channels-last inputs (config 3: the bf16 1x1-conv products of the channels-last encoders),
+// NCHW fp32 output as aggregate_plane_fwd_k.  A workgroup takes (image n, row y, 32 columns, 64
+// channels): lanes run over channels for the base / level reads (128-B bf16 rows), the results go
+// through an LDS tile [64][33] and leave with lanes over columns (128-B NCHW rows).  Per element the
+// arithmetic of aggregate_fwd_k / up_ac (level taps of the same fp32 values in the same order):
+// bit-identical to the NCHW path on the fp32-converted inputs.
+constexpr int AGC_X = 32, AGC_C = 64;
+
+struct AggLevelsT {
+  const void* src[3];
+  int hs[3], ws[3];
+};
+
+template <int NL, typename TI>
+__global__ __launch_bounds__(256) void aggregate_cl_fwd_k(int C, int h, int w, const TI* __restrict__ base,
+                                                          AggLevelsT lv, const float* __restrict__ bias,
+                                                          float* __restrict__ out) {
+  __shared__ float tile[AGC_C][AGC_X + 1];
+  const int ncx = (w + AGC_X - 1) / AGC_X;
+  const int x0 = (blockIdx.x % ncx) * AGC_X, c0 = (blockIdx.x / ncx) * AGC_C;
+  const int y = blockIdx.y;
+  const long long n = blockIdx.z;
+  const int cl = threadIdx.x & (AGC_C - 1), xq = threadIdx.x >> 6;
+  const int c = c0 + cl;
+  if (c < C) {
+    // the vertical taps of every level (the same for all of this thread's columns)
+    int ya[3], yb[3];
+    float lyv[3];
+#pragma unroll
+    for (int k = 0; k < NL; ++k) up_axis(lv.hs[k], h, y, &ya[k], &yb[k], &lyv[k]);
+    const TI* bp = base + ((n * h + y) * w) * C + c;
+    const float bc = bias[c];
+#pragma unroll 2
+    for (int xl = xq; xl < AGC_X; xl += 4) {
+      const int x = x0 + xl;
+      if (x >= w) break;
+      float v = ld1(bp + (size_t)x * C);
+#pragma unroll
+      for (int k = 0; k < NL; ++k) {
+        const int hs = lv.hs[k], ws = lv.ws[k];
+        int xa, xb;
+        float lx;
+        up_axis(ws, w, x, &xa, &xb, &lx);
+        const TI* lp = reinterpret_cast<const TI*>(lv.src[k]) + (n * hs * ws) * C + c;
+        const float top = (1.f - lx) * ld1(lp + ((size_t)ya[k] * ws + xa) * C) + lx * ld1(lp + ((size_t)ya[k] * ws + xb) * C);
+        const float bot = (1.f - lx) * ld1(lp + ((size_t)yb[k] * ws + xa) * C) + lx * ld1(lp + ((size_t)yb[k] * ws + xb) * C);
+        v += (1.f - lyv[k]) * top + lyv[k] * bot;
+      }
+      v += bc;
+      tile[cl][xl] = v > 0.f ? v : v * 0.1f;
+    }
+  }
+  __syncthreads();
+  const int xo = threadIdx.x & (AGC_X - 1), cr = threadIdx.x >> 5;
+  if (x0 + xo < w) {
+#pragma unroll
+    for (int j = 0; j < AGC_C / 8; ++j) {
+      const int cc = cr + 8 * j;
+      if (c0 + cc < C) out[((n * C + c0 + cc) * h + y) * w + x0 + xo] = tile[cc][xo];
+    }
+  }
+}
+
 }  // namespace vfd
+
+// base / levels channels-last [BN, h, w, C] / [BN, hs, ws, C] of dtype (0 fp32, 1 bf16), out NCHW fp32
+extern "C" int vfd_aggregate_fwd_cl(int BN, int C, int h, int w, const void* base, int n_levels,
+                                    const void* const* levels, const int* level_hw, const float* bias, float* out,
+                                    int dtype, void* stream) {
+  VFD_REQUIRE(BN > 0 && C > 0 && h > 0 && w > 0 && base && bias && out && (dtype == 0 || dtype == 1) && BN < 65536 &&
+                  h < 65536,
+              "aggregate_fwd_cl: bad arguments");
+  VFD_REQUIRE(n_levels >= 0 && n_levels <= 3, "up to 3 upsampled levels supported (got %d)", n_levels);
+  vfd::AggLevelsT lv{};
+  for (int k = 0; k < n_levels; ++k) {
+    lv.src[k] = levels[k];
+    lv.hs[k] = level_hw[2 * k];
+    lv.ws[k] = level_hw[2 * k + 1];
+    VFD_REQUIRE(lv.src[k] && lv.hs[k] > 0 && lv.ws[k] > 0, "aggregate_fwd_cl: level %d", k);
+  }
+  hipStream_t s = (hipStream_t)stream;
+  vfd::ProfScope ps(vfd::K_AGGREGATE, s);
+  const dim3 grid((unsigned)(((w + vfd::AGC_X - 1) / vfd::AGC_X) * ((C + vfd::AGC_C - 1) / vfd::AGC_C)), (unsigned)h,
+                  (unsigned)BN);
+#define VFD_AGC(NL, T) vfd::aggregate_cl_fwd_k<NL, T><<<grid, 256, 0, s>>>(C, h, w, (const T*)base, lv, bias, out)
+#define VFD_AGC_T(T)                      \
+  switch (n_levels) {                     \
+    case 0: VFD_AGC(0, T); break;         \
+    case 1: VFD_AGC(1, T); break;         \
+    case 2: VFD_AGC(2, T); break;         \
+    default: VFD_AGC(3, T); break;        \
+  }
+  if (dtype == 1) {
+    VFD_AGC_T(__bf16)
+  } else {
+    VFD_AGC_T(float)
+  }
+#undef VFD_AGC_T
+#undef VFD_AGC
+  return vfd::fail_launch("aggregate_fwd_cl");
+}
 
 extern "C" int vfd_aggregate_bwd(int BN, int C, int h, int w, const float* g, const float* out, float* d,
                                  int n_levels, float* const* dlevels, const int* level_hw, float* psum, void* stream) {

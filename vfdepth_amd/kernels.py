@@ -37,6 +37,7 @@ def _dev(t, what):
 # with autocast off; their gradients are cast back to the callers' dtypes by autograd.
 _amp_fwd = torch.amp.custom_fwd(device_type='cuda', cast_inputs=torch.float32)
 _amp_bwd = torch.amp.custom_bwd(device_type='cuda')
+_amp_keep = torch.amp.custom_fwd(device_type='cuda')     # autocast-aware, inputs as given
 
 
 def _dt(t):
@@ -1317,19 +1318,42 @@ class Smoothness(torch.autograd.Function):
 # =============================================================================================
 # Fusion-level feature aggregation (fusion_depthnet.py:53-63)
 # =============================================================================================
+_AGG_CL = os.environ.get('VFD_AGG_CL', '1') != '0'     # channels-last products read in place
+
+
+def _agg_cl_ok(base, levels):
+    """AggregateUp reads its inputs in place (vfd_aggregate_fwd_cl): all channels-last (and not also
+    NCHW-contiguous) maps of one dtype, fp32 or bf16."""
+    return _AGG_CL and all(t.is_cuda and t.dim() == 4 and t.dtype == base.dtype and t.dtype in _DT
+                           and not t.is_contiguous() and t.is_contiguous(memory_format=torch.channels_last)
+                           for t in (base,) + tuple(levels))
+
+
 class AggregateUp(torch.autograd.Function):
-    """LReLU_0.1(base + sum_k up_align_corners(level_k) + bias), NCHW; levels are upsampled to base's size."""
+    """LReLU_0.1(base + sum_k up_align_corners(level_k) + bias) -> NCHW fp32; levels are upsampled to
+    base's size.  NCHW inputs are taken in fp32 (the cast autocast's custom_fwd(cast_inputs=float32)
+    did); channels-last fp32 / bf16 inputs (config 3's bf16 1x1-conv products) are read in place —
+    the same fp32 values and arithmetic, without the cast and NCHW copies."""
 
     @staticmethod
-    @_amp_fwd
+    @_amp_keep
     def forward(ctx, base, bias, *levels):
         lib = L.load()
+        BN, C, h, w = base.shape
+        hw = (L.c_int * max(2 * len(levels), 1))(*[v for t in levels for v in t.shape[-2:]])
+        if _agg_cl_ok(base, levels):
+            bias = _dev(bias, 'bias')
+            out = torch.empty(BN, C, h, w, device=base.device)
+            ptrs = (L.c_fp * max(len(levels), 1))(*[t.data_ptr() for t in levels])
+            L.check(lib.vfd_aggregate_fwd_cl(BN, C, h, w, base.data_ptr(), len(levels), ptrs, hw, bias.data_ptr(),
+                                             out.data_ptr(), _DT[base.dtype], L.stream()), 'aggregate_fwd_cl')
+            ctx.save_for_backward(out)
+            ctx.level_shapes = [tuple(t.shape) for t in levels]
+            return out
         base, bias = _dev(base, 'aggregate base'), _dev(bias, 'bias')
         levels = [_dev(t, 'aggregate level') for t in levels]
-        BN, C, h, w = base.shape
         out = torch.empty_like(base)
         ptrs = (L.c_fp * max(len(levels), 1))(*[t.data_ptr() for t in levels])
-        hw = (L.c_int * max(2 * len(levels), 1))(*[v for t in levels for v in t.shape[-2:]])
         L.check(lib.vfd_aggregate_fwd(BN, C, h, w, base.data_ptr(), len(levels), ptrs, hw, bias.data_ptr(),
                                       out.data_ptr(), L.stream()), 'aggregate_fwd')
         ctx.save_for_backward(out)

@@ -114,6 +114,10 @@ int vfd_fuse_pose_fwd_t(const vfd_voxel_desc* d, const float* mask_lo, const flo
  * so calls sharing one plan must be stream-ordered. */
 int vfd_fuse_pose_bwd(const vfd_voxel_desc* d, const void* plan, const int* counts, const float* d_out,
                       float* d_feats, void* stream);
+/* the same with d_out of dtype_out (0 fp32, 1 bf16: the bf16 K2C data gradient, read 4 channels per
+ * 8-B load and summed in fp32; the reflect copies are folded in fp32) */
+int vfd_fuse_pose_bwd_t(const vfd_voxel_desc* d, const void* plan, const int* counts, const void* d_out,
+                        int dtype_out, float* d_feats, void* stream);
 
 /* K3 — voxel -> camera-frustum trilinear resampling (volumetric_fusionnet.py:232-262).
  * vox [B,V,Cv] (Cv <= 64), invK, E [B,N,4,4] (fusion scale) -> out [B*N, h(+2), w(+2), D*Cv]:
@@ -383,6 +387,10 @@ int vfd_pad_conv_dgrad(const vfd_conv_desc* d, const float* g_pre, const float* 
 size_t vfd_pad_conv_dgrad_bf16_workspace(const vfd_conv_desc* d);
 int vfd_pad_conv_dgrad_bf16(const vfd_conv_desc* d, const void* g_pre, const void* Wd, float* dx, void* workspace,
                             size_t ws_bytes, void* stream);
+/* dtype_dx 0: fp32 dx (as vfd_pad_conv_dgrad_bf16), 1: bf16 dx — the fp32 sums rounded once to
+ * nearest even, as a bf16 convolution's input gradient under autocast (config 3's pose map) */
+int vfd_pad_conv_dgrad_bf16_t(const vfd_conv_desc* d, const void* g_pre, const void* Wd, void* dx, int dtype_dx,
+                              void* workspace, size_t ws_bytes, void* stream);
 
 /* K3C data gradient (volumetric_fusionnet.py:59-60, 265 backward): d of reduce_dim's first conv
  * w.r.t. its reflect-padded input, dx [B*N, h+2, w+2, D*Cv] (channel d*Cv + c: the layout
@@ -532,6 +540,9 @@ int vfd_aggregate_fwd(int BN, int C, int h, int w, const float* base, int n_leve
 /* the same with channels-last inputs read in place: base [BN, h, w, C], levels[k] [BN, hs, ws, C] of
  * dtype 0 fp32 / 1 bf16 (config 3's bf16 1x1-conv products), out NCHW fp32 [BN, C, h, w]; per
  * element the arithmetic of vfd_aggregate_fwd on the fp32 values (bit-identical). */
+/* x NCHW fp32 [n][C][hw] -> y channels-last [n][hw][C] of dtype_out (0 fp32, 1 bf16, rounded to
+ * nearest even): AggregateUp's input gradients in the layout / dtype of its channels-last inputs */
+int vfd_nchw_to_nhwc(const float* x, void* y, long long n, int C, int hw, int dtype_out, void* stream);
 int vfd_aggregate_fwd_cl(int BN, int C, int h, int w, const void* base, int n_levels, const void* const* levels,
                          const int* level_hw, const float* bias, float* out, int dtype, void* stream);
 /* backward of vfd_aggregate_fwd in one launch (one workgroup per plane, LDS-resident):

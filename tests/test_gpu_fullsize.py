@@ -784,8 +784,9 @@ def test_pose_conv_bf16_map_matches_two_nodes(config, B, monkeypatch):
     """Config 3's K2 + K2C on the bf16 map (PoseConvBF16: K2 writes the map in bf16, the conv's
     forward and weight gradient read it) against FusePose (fp32 map) -> PadConvBF16 (the map
     rounded to bf16 as it is staged): the same staged values, so the map, the conv output and
-    every gradient (d feats through the fp32 K2C data gradient and K2's backward, d weight, d bias)
-    are BIT-identical (volumetric_fusionnet.py:116-162, 338-343 under autocast)."""
+    every gradient (d feats through the K2C data gradient — rounded to bf16 in both, VFD_PD_DX_BF16 —
+    and K2's backward, d weight, d bias) are BIT-identical (volumetric_fusionnet.py:116-162, 338-343
+    under autocast)."""
     from vfdepth_amd import kernels as KN
     cfg = full_cfg(config)
     batch, lvl, Einv = _fusion_inputs(cfg, 91)
@@ -821,6 +822,12 @@ def test_pose_conv_bf16_map_matches_two_nodes(config, B, monkeypatch):
     yb.backward(g)
     for name, p, q in zip(('d feats', 'd weight', 'd bias'), la, lb):
         assert torch.equal(p.grad, q.grad), f'{name} differs on the bf16 map (max {float((p.grad - q.grad).abs().max()):.3g})'
+    # K2's backward on a bf16 map gradient (the bf16 K2C data gradient's output) equals its fp32 form
+    # on the same values, bit for bit (loads widened exactly, the same fp32 sums)
+    gm = torch.randn(x32.shape, device=DEV, generator=gen).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    with torch.no_grad():
+        assert torch.equal(KN._pose_unfuse(space, plan, feats.shape, gm),
+                           KN._pose_unfuse(space, plan, feats.shape, gm.float())), 'K2 backward on a bf16 map gradient'
 
 
 # ------------------------------------------------------------------------------------ fused BN
@@ -1152,6 +1159,7 @@ def test_aggregate_channels_last_bit_identical():
             ref.backward(g)
             for t, u in zip(a, r):
                 assert t.grad.dtype == dt and torch.equal(t.grad, u.grad.to(dt)), (shape, dt, tuple(t.shape))
+                assert t.grad.is_contiguous(memory_format=cl), 'gradient handed back channels-last'
 
 
 def test_elu_upsample_pad_matches_aten():

@@ -69,6 +69,7 @@ _SIGS = {
     'vfd_fuse_pose_fwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 5 + [c_void_p]),
     'vfd_fuse_pose_fwd_t': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 5 + [c_int, c_fp, c_int, c_void_p]),
     'vfd_fuse_pose_bwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 4 + [c_void_p]),
+    'vfd_fuse_pose_bwd_t': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 3 + [c_int, c_fp, c_void_p]),
     'vfd_voxel_project_fwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 4 + [c_void_p]),
     'vfd_voxel_project_plan_bytes': (c_size_t, [ctypes.POINTER(VoxelDesc)]),
     'vfd_voxel_project_plan': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 2 + [c_void_p, c_size_t, c_void_p]),
@@ -82,6 +83,7 @@ _SIGS = {
     'vfd_photo_fwd': (c_int, [ctypes.POINTER(PhotoDesc)] + [c_fp] * 13 + [c_size_t, c_void_p]),
     'vfd_photo_bwd': (c_int, [ctypes.POINTER(PhotoDesc)] + [c_fp] * 9 + [c_void_p]),
     'vfd_aggregate_fwd': (c_int, [c_int] * 4 + [c_fp, c_int, ctypes.POINTER(c_fp), ctypes.POINTER(c_int), c_fp, c_fp, c_void_p]),
+    'vfd_nchw_to_nhwc': (c_int, [c_fp, c_fp, ctypes.c_longlong, c_int, c_int, c_int, c_void_p]),
     'vfd_aggregate_fwd_cl': (c_int, [c_int] * 4 + [c_fp, c_int, ctypes.POINTER(c_fp), ctypes.POINTER(c_int), c_fp, c_fp,
                                                    c_int, c_void_p]),
     'vfd_proj_conv_fwd_workspace': (c_size_t, [ctypes.POINTER(VoxelDesc)]),
@@ -151,6 +153,7 @@ _SIGS = {
     'vfd_pad_conv_dgrad': (c_int, [ctypes.POINTER(ConvDesc)] + [c_fp] * 4 + [c_size_t, c_void_p]),
     'vfd_pad_conv_dgrad_bf16_workspace': (c_size_t, [ctypes.POINTER(ConvDesc)]),
     'vfd_pad_conv_dgrad_bf16': (c_int, [ctypes.POINTER(ConvDesc)] + [c_fp] * 4 + [c_size_t, c_void_p]),
+    'vfd_pad_conv_dgrad_bf16_t': (c_int, [ctypes.POINTER(ConvDesc)] + [c_fp] * 3 + [c_int, c_fp, c_size_t, c_void_p]),
     'vfd_depth_syn_fwd': (c_int, [ctypes.POINTER(DepthSynDesc)] + [c_fp] * 8 + [c_void_p]),
     'vfd_depth_syn_bwd': (c_int, [ctypes.POINTER(DepthSynDesc)] + [c_fp] * 9 + [c_void_p]),
     'vfd_smooth_workspace_bytes': (c_size_t, [c_int] * 4),

@@ -352,6 +352,38 @@ __global__ __launch_bounds__(256) void aggregate_cl_fwd_k(int C, int h, int w, c
 
 }  // namespace vfd
 
+namespace vfd {
+// NCHW fp32 [n][C][hw] -> channels-last [n][hw][C] of TO (one rounding): the aggregation's input
+// gradients handed back in the layout / dtype of its channels-last inputs (what autograd's cast and
+// the convolution backward's layout copy would otherwise do in two passes).  64 x 64 tiles through
+// LDS: lanes over pixels on the read, over channels on the write.
+template <typename TO>
+__global__ __launch_bounds__(256) void nchw_to_nhwc_k(const float* __restrict__ x, TO* __restrict__ y, int C, int hw) {
+  __shared__ float t[64][65];
+  const int p0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+  const long long n = blockIdx.z;
+  const int l = threadIdx.x & 63, r = threadIdx.x >> 6;
+#pragma unroll 4
+  for (int k = r; k < 64; k += 4)
+    if (c0 + k < C && p0 + l < hw) t[k][l] = x[(n * C + c0 + k) * hw + p0 + l];
+  __syncthreads();
+#pragma unroll 4
+  for (int k = r; k < 64; k += 4)
+    if (p0 + k < hw && c0 + l < C) y[(n * hw + p0 + k) * C + c0 + l] = (TO)t[l][k];
+}
+}  // namespace vfd
+
+extern "C" int vfd_nchw_to_nhwc(const float* x, void* y, long long n, int C, int hw, int dtype_out, void* stream) {
+  VFD_REQUIRE(x && y && n > 0 && n < 65536 && C > 0 && hw > 0 && (dtype_out == 0 || dtype_out == 1),
+              "nchw_to_nhwc: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  vfd::ProfScope ps(vfd::K_UPSAMPLE_BWD, s);
+  const dim3 grid((unsigned)((hw + 63) / 64), (unsigned)((C + 63) / 64), (unsigned)n);
+  if (dtype_out == 1) vfd::nchw_to_nhwc_k<__bf16><<<grid, 256, 0, s>>>(x, (__bf16*)y, C, hw);
+  else vfd::nchw_to_nhwc_k<float><<<grid, 256, 0, s>>>(x, (float*)y, C, hw);
+  return vfd::fail_launch("nchw_to_nhwc");
+}
+
 // base / levels channels-last [BN, h, w, C] / [BN, hs, ws, C] of dtype (0 fp32, 1 bf16), out NCHW fp32
 extern "C" int vfd_aggregate_fwd_cl(int BN, int C, int h, int w, const void* base, int n_levels,
                                     const void* const* levels, const int* level_hw, const float* bias, float* out,

@@ -1255,7 +1255,8 @@ constexpr int PBW_U = VFD_PBW_U;       // voxel rows (1 KB each) in flight per w
 // grid = B * nslot * POSE_FOLD_SPLIT: each slot's Z * (C + 1) floats are split over
 // POSE_FOLD_SPLIT workgroups (a slot per workgroup leaves 400 workgroups on 256 CUs, latency-bound)
 constexpr int POSE_FOLD_SPLIT = 4;
-__global__ __launch_bounds__(256) void pose_fold_k(vfd_voxel_desc d, const float* __restrict__ dout,
+template <typename TG>
+__global__ __launch_bounds__(256) void pose_fold_k(vfd_voxel_desc d, const TG* __restrict__ dout,
                                                    float* __restrict__ fb, int aligned16) {
   const int nslot = 2 * (d.X + d.Y);
   const int part = blockIdx.x % POSE_FOLD_SPLIT, sb = blockIdx.x / POSE_FOLD_SPLIT;
@@ -1268,17 +1269,17 @@ __global__ __launch_bounds__(256) void pose_fold_k(vfd_voxel_desc d, const float
   if (pose_fold_slot(xi, yi, d.X, d.Y) != slot) return;     // owned by an earlier slot
   // a padded position's Z rows are contiguous: sum the (up to 4) copies' Z * (C + 1) floats
   const int n = d.Z * (d.C + 1), Xo = d.X + 2;
-  const float* gb = dout + (size_t)b * (d.Y + 2) * Xo * n;
+  const TG* gb = dout + (size_t)b * (d.Y + 2) * Xo * n;
   const int ex = xi == 1 ? 0 : (xi == d.X - 2 ? d.X + 1 : -1);   // x-mirror column (padded)
   const int ey = yi == 1 ? 0 : (yi == d.Y - 2 ? d.Y + 1 : -1);
-  const float* p0 = gb + ((size_t)(yi + 1) * Xo + xi + 1) * n;
-  const float* p1 = gb + ((size_t)(yi + 1) * Xo + max(ex, 0)) * n;
-  const float* p2 = gb + ((size_t)max(ey, 0) * Xo + xi + 1) * n;
-  const float* p3 = gb + ((size_t)max(ey, 0) * Xo + max(ex, 0)) * n;
+  const TG* p0 = gb + ((size_t)(yi + 1) * Xo + xi + 1) * n;
+  const TG* p1 = gb + ((size_t)(yi + 1) * Xo + max(ex, 0)) * n;
+  const TG* p2 = gb + ((size_t)max(ey, 0) * Xo + xi + 1) * n;
+  const TG* p3 = gb + ((size_t)max(ey, 0) * Xo + max(ex, 0)) * n;
   const float f1 = ex >= 0 ? 1.f : 0.f, f2 = ey >= 0 ? 1.f : 0.f, f3 = f1 * f2;
   float* dst = fb + ((size_t)b * nslot + slot) * n;
   // ((primary + x-copy) + y-copy) + xy-copy, absent copies weighted 0 (loads stay in range)
-  if ((n & 3) == 0 && aligned16) {          // rows start 16-B aligned: float4 lanes
+  if (sizeof(TG) == 4 && (n & 3) == 0 && aligned16) {   // fp32 rows start 16-B aligned: float4 lanes
     const int n4 = n >> 2, c4 = (n4 + POSE_FOLD_SPLIT - 1) / POSE_FOLD_SPLIT;
     const int e4 = min(n4, (part + 1) * c4);
     const float4 *q0 = reinterpret_cast<const float4*>(p0), *q1 = reinterpret_cast<const float4*>(p1);
@@ -1296,10 +1297,10 @@ __global__ __launch_bounds__(256) void pose_fold_k(vfd_voxel_desc d, const float
   }
   const int cn = (n + POSE_FOLD_SPLIT - 1) / POSE_FOLD_SPLIT, e = min(n, (part + 1) * cn);
   for (int i = part * cn + threadIdx.x; i < e; i += blockDim.x) {
-    float s = p0[i];
-    s += f1 * p1[i];
-    s += f2 * p2[i];
-    s += f3 * p3[i];
+    float s = ld1(p0 + i);
+    s += f1 * ld1(p1 + i);
+    s += f2 * ld1(p2 + i);
+    s += f3 * ld1(p3 + i);
     dst[i] = s;
   }
 }
@@ -1319,9 +1320,10 @@ extern "C" int vfd_pbw_trace_read(void* dst, size_t bytes) {
 // batch ahead), sums each footprint run in registers and flushes it into its LDS tile
 // [PT2 + 1][256] (row PT2 takes taps outside the tile).  Rows start at any 4-B offset (C + 1
 // floats per row): the 16-B loads run unaligned, which gfx9's unaligned access mode allows.
+template <typename TG>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void fuse_pose_bwd_k(vfd_voxel_desc d, const int4* __restrict__ tasks,
                                                       const int* __restrict__ ctrl, const TileItem* __restrict__ items,
-                                                      const float* __restrict__ dout, const float* __restrict__ fbuf,
+                                                      const TG* __restrict__ dout, const float* __restrict__ fbuf,
                                                       float* __restrict__ pool, float* __restrict__ dfeats) {
   constexpr int U = PBW_U;
   constexpr int PR = PT2 + 1;
@@ -1339,7 +1341,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void fu
   const int bc = bct / nt, b = bc / d.N, tile = bct % nt;
   const int V = d.X * d.Y * d.Z, hw = d.h * d.w;
   const int P = d.pad_out ? 2 : 0;
-  const float* gb = dout + (size_t)b * (d.Y + P) * (d.X + P) * d.Z * C1;
+  const TG* gb = dout + (size_t)b * (d.Y + P) * (d.X + P) * d.Z * C1;
   const float* fb = fbuf + (size_t)b * 2 * (d.X + d.Y) * d.Z * C1;
   const TileItem* ib = items + (size_t)bc * 4 * V;
   const int cq = min(lane, C / 4 - 1) * 4;         // this lane's first channel (idle lanes re-read)
@@ -1378,7 +1380,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void fu
   // (buffer loads: the row offset is a scalar soffset and the lane's channel offset a constant
   // voffset, so an item costs no VGPR address arithmetic)
   const __amdgpu_buffer_rsrc_t rs_g = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)gb, 0, (int)((size_t)(d.Y + P) * (d.X + P) * d.Z * C1 * sizeof(float)), 0x00020000);
+      (void*)gb, 0, (int)((size_t)(d.Y + P) * (d.X + P) * d.Z * C1 * sizeof(TG)), 0x00020000);
   const __amdgpu_buffer_rsrc_t rs_f = __builtin_amdgcn_make_buffer_rsrc(
       (void*)fb, 0, (int)((size_t)2 * (d.X + d.Y) * d.Z * C1 * sizeof(float)), 0x00020000);
   const int voff = cq * (int)sizeof(float);
@@ -1386,9 +1388,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void fu
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)m.pz, k * U + u);
-      const int soff = (int)((r & 0x7FFFFFFFu) * (uint32_t)C1 * (uint32_t)sizeof(float));
-      const auto v = __builtin_amdgcn_raw_buffer_load_b128((r >> 31) ? rs_f : rs_g, voff, soff, 0);
-      gr[u] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+      if constexpr (sizeof(TG) == 4) {
+        const int soff = (int)((r & 0x7FFFFFFFu) * (uint32_t)C1 * (uint32_t)sizeof(float));
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128((r >> 31) ? rs_f : rs_g, voff, soff, 0);
+        gr[u] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+      } else if (r >> 31) {                      // folded border row: fp32 sums (wave-uniform branch)
+        const int soff = (int)((r & 0x7FFFFFFFu) * (uint32_t)C1 * (uint32_t)sizeof(float));
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs_f, voff, soff, 0);
+        gr[u] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+      } else {                                   // bf16 gradient row: 4 channels in 8 B
+        const int soff = (int)(r * (uint32_t)C1 * 2u);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs_g, cq * 2, soff, 0);
+        gr[u] = make_float4(__uint_as_float((uint32_t)v[0] << 16), __uint_as_float((uint32_t)v[0] & 0xFFFF0000u),
+                            __uint_as_float((uint32_t)v[1] << 16), __uint_as_float((uint32_t)v[1] & 0xFFFF0000u));
+      }
     }
   };
   auto consume = [&](int jb, const TileItem& m, int k, const float4 (&gr)[U]) {
@@ -2631,12 +2644,14 @@ int vfd_fuse_pose_fwd(const vfd_voxel_desc* d, const float* mask_lo, const float
   return vfd_fuse_pose_fwd_t(d, mask_lo, K, Einv, feats_cl, out, 0, nullptr, 0, stream);
 }
 
-int vfd_fuse_pose_bwd(const vfd_voxel_desc* d, const void* plan, const int* counts, const float* d_out,
-                      float* d_feats, void* stream) {
+// d_out of dtype_out (0 fp32, 1 bf16: the bf16 K2C data gradient)
+int vfd_fuse_pose_bwd_t(const vfd_voxel_desc* d, const void* plan, const int* counts, const void* d_out, int dtype_out,
+                        float* d_feats, void* stream) {
   int st = check_voxel_desc(d);
   if (st) return st;
   (void)counts;
   VFD_REQUIRE(d->C >= 4 && d->C <= POSE_MAXC && d->C % 4 == 0, "fuse_pose_bwd: C=%d must be a multiple of 4 in [4, %d]", d->C, POSE_MAXC);
+  VFD_REQUIRE(dtype_out == 0 || dtype_out == 1, "fuse_pose_bwd: dtype_out %d (0 fp32, 1 bf16)", dtype_out);
   hipStream_t s = (hipStream_t)stream;
   const int hw = d->h * d->w;
   const int* row_ptr = (const int*)((const char*)plan + plan_entries_bytes(d));
@@ -2647,12 +2662,24 @@ int vfd_fuse_pose_bwd(const vfd_voxel_desc* d, const void* plan, const int* coun
   float* fbuf = (float*)((char*)ctrl + 256);                   // folded border rows (plan scratch)
   float* pool = (float*)((char*)fbuf + plan_fold_bytes(d));    // split tiles' partials
   ProfScope ps(K_FUSE_POSE_BWD, s);
-  if (d->pad_out) pose_fold_k<<<d->B * 2 * (d->X + d->Y) * POSE_FOLD_SPLIT, 256, 0, s>>>(
-      *d, d_out, fbuf, (((uintptr_t)d_out | (uintptr_t)fbuf) & 15) == 0);
+  const unsigned nfold = d->B * 2 * (d->X + d->Y) * POSE_FOLD_SPLIT;
+  const int al16 = (((uintptr_t)d_out | (uintptr_t)fbuf) & 15) == 0;
   const int ntask_max = host_tiles(d) * d->B * d->N + PBW_POOL;
-  fuse_pose_bwd_k<<<128 * cdiv(ntask_max, 128), 64, 0, s>>>(*d, tasks, ctrl, csr, d_out, fbuf, pool, d_feats);
+  const unsigned ntask = 128 * cdiv(ntask_max, 128);
+  if (dtype_out == 1) {
+    if (d->pad_out) pose_fold_k<__bf16><<<nfold, 256, 0, s>>>(*d, (const __bf16*)d_out, fbuf, al16);
+    fuse_pose_bwd_k<__bf16><<<ntask, 64, 0, s>>>(*d, tasks, ctrl, csr, (const __bf16*)d_out, fbuf, pool, d_feats);
+  } else {
+    if (d->pad_out) pose_fold_k<float><<<nfold, 256, 0, s>>>(*d, (const float*)d_out, fbuf, al16);
+    fuse_pose_bwd_k<float><<<ntask, 64, 0, s>>>(*d, tasks, ctrl, csr, (const float*)d_out, fbuf, pool, d_feats);
+  }
   pose_combine_k<<<std::min(PBW_POOL / 2, host_tiles(d) * d->B * d->N), 256, 0, s>>>(*d, combos, ctrl, pool, d_feats);
   return fail_launch("fuse_pose_bwd");
+}
+
+int vfd_fuse_pose_bwd(const vfd_voxel_desc* d, const void* plan, const int* counts, const float* d_out,
+                      float* d_feats, void* stream) {
+  return vfd_fuse_pose_bwd_t(d, plan, counts, d_out, 0, d_feats, stream);
 }
 
 int vfd_fuse_depth_bwd_planned(const vfd_voxel_desc* d, const void* plan, const float* d_vox, const float* vox,

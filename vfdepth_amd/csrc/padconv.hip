@@ -726,9 +726,9 @@ __device__ __forceinline__ int pdc_div(int m, int d, float rd) {
   return q;
 }
 
-template <typename T, typename TG>
+template <typename T, typename TG, typename TO = float>
 __global__ __launch_bounds__(PP_THREADS, 2) void ppd_main_k(PdcGeom g, const TG* __restrict__ gp,
-                                                           const void* __restrict__ Wd, float* __restrict__ dx,
+                                                           const void* __restrict__ Wd, TO* __restrict__ dx,
                                                            float* __restrict__ partial) {
   constexpr int OC = PdCfg<T>::OC, XS = PdCfg<T>::XS, STEPS = PdCfg<T>::STEPS, PF = PdCfg<T>::PF;
   static_assert(STEPS % PF == 0, "prefetch ring");
@@ -895,7 +895,7 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppd_main_k(PdcGeom g, const TG*
         for (int a = 0; a < MB; ++a) {
           const int mb = m0w + 32 * a + 4 * lh;
           const int ib = pdc_div(mb, wcc, rw), jb = mb - ib * wcc;
-          float* pa = dx + (((size_t)tl.b * g.hp + st * ib + py) * g.wp + st * jb + px) * g.cin + n0;
+          TO* pa = dx + (((size_t)tl.b * g.hp + st * ib + py) * g.wp + st * jb + px) * g.cin + n0;
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int d = (r & 3) + 8 * (r >> 2);
@@ -909,7 +909,7 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppd_main_k(PdcGeom g, const TG*
 #pragma unroll
             for (int b = 0; b < NB; ++b) {
 #ifndef VFD_PD_NOSTORE
-              if (mb + d < hw && n0 + 32 * b < g.cin) pa[off + 32 * b] = acc[a][b][r];
+              if (mb + d < hw && n0 + 32 * b < g.cin) st1(pa + off + 32 * b, acc[a][b][r]);
 #endif
               acc[a][b][r] = 0.f;
             }
@@ -932,7 +932,8 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppd_main_k(PdcGeom g, const TG*
   }
 }
 
-__global__ __launch_bounds__(256) void ppd_reduce_k(PdcGeom g, const float* __restrict__ partial, float* __restrict__ dx) {
+template <typename TO>
+__global__ __launch_bounds__(256) void ppd_reduce_k(PdcGeom g, const float* __restrict__ partial, TO* __restrict__ dx) {
   const int grp = blockIdx.x;
   const int lo = pdc_lo(g, grp);
   if (grp == 0 || lo % g.och == 0 || lo >= g.natom) return;
@@ -957,7 +958,7 @@ __global__ __launch_bounds__(256) void ppd_reduce_k(PdcGeom g, const float* __re
       const int m = tl.m0 + 32 * (4 * wm + a) + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
       if (m < hw && n < g.cin) {
         const int i = m / wcc, j = m - i * wcc;
-        dx[(((size_t)tl.b * g.hp + g.s * i + g.py[tl.c]) * g.wp + g.s * j + g.px[tl.c]) * g.cin + n] = su[u];
+        st1(dx + (((size_t)tl.b * g.hp + g.s * i + g.py[tl.c]) * g.wp + g.s * j + g.px[tl.c]) * g.cin + n, su[u]);
       }
     }
   }
@@ -1125,7 +1126,7 @@ int vfd_pad_conv_dgrad(const vfd_conv_desc* d, const float* g_pre, const float* 
   lds_attr(reinterpret_cast<const void*>(ppd_main_k<float, float>), PP_LDS_MAX);
   ppd_main_k<float, float><<<g.ngroup, PP_THREADS, (size_t)2 * g.lds_elems * sizeof(float), s>>>(g, g_pre, Wd, dx,
                                                                                                  (float*)ws);
-  ppd_reduce_k<<<dim3(g.ngroup, 8), 256, 0, s>>>(g, (const float*)ws, dx);
+  ppd_reduce_k<float><<<dim3(g.ngroup, 8), 256, 0, s>>>(g, (const float*)ws, dx);
   return fail_launch("pad_conv_dgrad");
 }
 
@@ -1135,20 +1136,34 @@ size_t vfd_pad_conv_dgrad_bf16_workspace(const vfd_conv_desc* d) {
   return (size_t)g.ngroup * 2 * PD2_FRAG * sizeof(float);
 }
 
-int vfd_pad_conv_dgrad_bf16(const vfd_conv_desc* d, const void* g_pre, const void* Wd, float* dx, void* ws,
-                            size_t ws_bytes, void* stream) {
-  VFD_REQUIRE(d && g_pre && Wd && dx, "pad_conv_dgrad_bf16: null argument");
+// dtype_dx 0: fp32 d X, 1: bf16 (rounded once from the fp32 sums, as a bf16 conv's input gradient)
+int vfd_pad_conv_dgrad_bf16_t(const vfd_conv_desc* d, const void* g_pre, const void* Wd, void* dx, int dtype_dx,
+                              void* ws, size_t ws_bytes, void* stream) {
+  VFD_REQUIRE(d && g_pre && Wd && dx && (dtype_dx == 0 || dtype_dx == 1), "pad_conv_dgrad_bf16: bad argument");
   PdcGeom g;
   VFD_REQUIRE(pdc_plan<__bf16>(*d, &g), "pad_conv_dgrad_bf16: unsupported shape (C %% 4 == 0, stride 1 or 2, %d outputs)",
               PP_O);
   VFD_REQUIRE(ws && ws_bytes >= vfd_pad_conv_dgrad_bf16_workspace(d), "pad_conv_dgrad_bf16: workspace too small");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_PAD_CONV_DGRAD, s);
-  lds_attr(reinterpret_cast<const void*>(ppd_main_k<__bf16, __bf16>), PP_LDS_MAX);
-  ppd_main_k<__bf16, __bf16><<<g.ngroup, PP_THREADS, (size_t)2 * g.lds_elems * sizeof(__bf16), s>>>(
-      g, (const __bf16*)g_pre, Wd, dx, (float*)ws);
-  ppd_reduce_k<<<dim3(g.ngroup, 8), 256, 0, s>>>(g, (const float*)ws, dx);
+  const size_t lds = (size_t)2 * g.lds_elems * sizeof(__bf16);
+  if (dtype_dx == 1) {
+    lds_attr(reinterpret_cast<const void*>(ppd_main_k<__bf16, __bf16, __bf16>), PP_LDS_MAX);
+    ppd_main_k<__bf16, __bf16, __bf16><<<g.ngroup, PP_THREADS, lds, s>>>(g, (const __bf16*)g_pre, Wd, (__bf16*)dx,
+                                                                         (float*)ws);
+    ppd_reduce_k<__bf16><<<dim3(g.ngroup, 8), 256, 0, s>>>(g, (const float*)ws, (__bf16*)dx);
+  } else {
+    lds_attr(reinterpret_cast<const void*>(ppd_main_k<__bf16, __bf16, float>), PP_LDS_MAX);
+    ppd_main_k<__bf16, __bf16, float><<<g.ngroup, PP_THREADS, lds, s>>>(g, (const __bf16*)g_pre, Wd, (float*)dx,
+                                                                        (float*)ws);
+    ppd_reduce_k<float><<<dim3(g.ngroup, 8), 256, 0, s>>>(g, (const float*)ws, (float*)dx);
+  }
   return fail_launch("pad_conv_dgrad_bf16");
+}
+
+int vfd_pad_conv_dgrad_bf16(const vfd_conv_desc* d, const void* g_pre, const void* Wd, float* dx, void* ws,
+                            size_t ws_bytes, void* stream) {
+  return vfd_pad_conv_dgrad_bf16_t(d, g_pre, Wd, dx, 0, ws, ws_bytes, stream);
 }
 
 }  // extern "C"

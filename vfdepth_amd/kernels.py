@@ -520,9 +520,14 @@ def pad_conv_dgrad_weight(w, perm=None, bf16=False, cache=True):
     return out
 
 
-def pad_conv_dgrad(g_pre, x_shape, w, stride, perm=None):
+_PD_DX_BF16 = os.environ.get('VFD_PD_DX_BF16', '0') == '1'  # bf16 K2C: d map rounded to bf16 (autocast's)
+
+
+def pad_conv_dgrad(g_pre, x_shape, w, stride, perm=None, out_dtype=torch.float32):
     """K2C's data gradient through the C ABI: g_pre [B, 256, Ho, Wo] channels-last (fp32 or bf16) ->
-    d x [B, C, H, W] channels-last fp32 (every padded position written); None when unsupported."""
+    d x [B, C, H, W] channels-last (every padded position written), fp32 or — bf16 g_pre only —
+    bf16 (the fp32 sums rounded once, as a bf16 convolution's input gradient is); None when
+    unsupported."""
     lib = L.load()
     B, C, H, W = x_shape
     d = L.ConvDesc(B, H, W, C, stride, g_pre.shape[1])
@@ -531,11 +536,15 @@ def pad_conv_dgrad(g_pre, x_shape, w, stride, perm=None):
     if not nbytes:
         return None
     wd = pad_conv_dgrad_weight(w, perm, bf16)
-    dx = torch.empty(B, C, H, W, device=g_pre.device, memory_format=torch.channels_last)
+    out_dtype = out_dtype if bf16 else torch.float32
+    dx = torch.empty(B, C, H, W, device=g_pre.device, dtype=out_dtype, memory_format=torch.channels_last)
     ws = _ws(nbytes, g_pre.device)
-    fn = lib.vfd_pad_conv_dgrad_bf16 if bf16 else lib.vfd_pad_conv_dgrad
-    L.check(fn(ctypes.byref(d), g_pre.data_ptr(), wd.data_ptr(), dx.data_ptr(), ws.data_ptr(), nbytes, L.stream()),
-            'pad_conv_dgrad')
+    if bf16:
+        L.check(lib.vfd_pad_conv_dgrad_bf16_t(ctypes.byref(d), g_pre.data_ptr(), wd.data_ptr(), dx.data_ptr(),
+                                              _DT[out_dtype], ws.data_ptr(), nbytes, L.stream()), 'pad_conv_dgrad')
+    else:
+        L.check(lib.vfd_pad_conv_dgrad(ctypes.byref(d), g_pre.data_ptr(), wd.data_ptr(), dx.data_ptr(), ws.data_ptr(),
+                                       nbytes, L.stream()), 'pad_conv_dgrad')
     return dx
 
 
@@ -676,9 +685,11 @@ class PadConvBF16(torch.autograd.Function):
         args = ([w.shape[0]], [s, s], [0, 0], [1, 1], False, [0, 0], 1)
         dx = dw = db = None
         if mask[0] and _PC_BF16_BWD and _PAD_DGRAD:
-            # the bf16 data gradient (padconv.hip ppd_main_k<bf16>: bf16 operands, fp32 accumulation
-            # and output — the fp32 map's gradient, as autocast's bf16 conv gradient cast back)
-            dx = pad_conv_dgrad(gb, x.shape, w, s, ctx.perm)
+            # the bf16 data gradient (padconv.hip ppd_main_k<bf16>: bf16 operands, fp32 accumulation,
+            # rounded to bf16 as autocast's bf16 conv gradient is, then cast back for an fp32 map)
+            dx = pad_conv_dgrad(gb, x.shape, w, s, ctx.perm, torch.bfloat16 if _PD_DX_BF16 else torch.float32)
+            if dx is not None:
+                dx = dx.to(x.dtype)
         wd = None
         if (mask[0] and dx is None) or ((mask[1] or mask[2]) and not (_PC_BF16_BWD and _PAD_WGRAD)):
             wd = w.detach()
@@ -732,15 +743,15 @@ def _pose_fuse_t(space, plan, feats, dtype):
 
 
 def _pose_unfuse(space, plan, shape, g):
-    """K2 backward: d map (fp32 channels-last) -> d feats [B, N, C, h, w] (fuse_pose_bwd_k)."""
+    """K2 backward: d map (fp32 or bf16, channels-last) -> d feats [B, N, C, h, w] fp32 (fuse_pose_bwd_k)."""
     lib = L.load()
     B, N, C = shape[:3]
-    g = _channels_last(g, 'grad')
+    g = _nhwc(g, 'grad') if g.dtype in _DT else _channels_last(g, 'grad')
     dfeats = torch.empty(shape, device=g.device)
     d = space.desc(B, N, C=C)
     plan.build().wait()
-    L.check(lib.vfd_fuse_pose_bwd(ctypes.byref(d), plan.buf.data_ptr(), plan.counts.data_ptr(),
-                                  g.data_ptr(), dfeats.data_ptr(), L.stream()), 'fuse_pose_bwd')
+    L.check(lib.vfd_fuse_pose_bwd_t(ctypes.byref(d), plan.buf.data_ptr(), plan.counts.data_ptr(),
+                                    g.data_ptr(), _DT[g.dtype], dfeats.data_ptr(), L.stream()), 'fuse_pose_bwd')
     return dfeats
 
 
@@ -793,8 +804,10 @@ class PoseConvBF16(torch.autograd.Function):
         gb = lrelu_pad_backward(g.to(torch.bfloat16), out, dtype=torch.bfloat16)
         dfeats = dw = db = None
         if ctx.needs_input_grad[2]:
-            # the bf16 data gradient (ppd_main_k, fp32 output) straight into K2's backward
-            dfeats = _pose_unfuse(ctx.space, ctx.plan, ctx.shape, pad_conv_dgrad(gb, x.shape, w, s, ctx.perm))
+            # the bf16 data gradient (ppd_main_k: fp32 sums rounded to bf16 as autocast's conv gradient
+            # is, VFD_PD_DX_BF16=0 keeps them fp32) straight into K2's backward
+            dmap = pad_conv_dgrad(gb, x.shape, w, s, ctx.perm, torch.bfloat16 if _PD_DX_BF16 else torch.float32)
+            dfeats = _pose_unfuse(ctx.space, ctx.plan, ctx.shape, dmap)
         if ctx.needs_input_grad[3] or ctx.needs_input_grad[4]:
             dw, db = pad_conv_wgrad_bf16(gb, x, w, s, ctx.needs_input_grad[3], ctx.needs_input_grad[4])
             if dw is not None and ctx.perm:
@@ -1319,6 +1332,7 @@ class Smoothness(torch.autograd.Function):
 # Fusion-level feature aggregation (fusion_depthnet.py:53-63)
 # =============================================================================================
 _AGG_CL = os.environ.get('VFD_AGG_CL', '1') != '0'     # channels-last products read in place
+_AGG_CL_GRAD = os.environ.get('VFD_AGG_CL_GRAD', '0') == '1'   # their gradients handed back channels-last
 
 
 def _agg_cl_ok(base, levels):
@@ -1327,6 +1341,15 @@ def _agg_cl_ok(base, levels):
     return _AGG_CL and all(t.is_cuda and t.dim() == 4 and t.dtype == base.dtype and t.dtype in _DT
                            and not t.is_contiguous() and t.is_contiguous(memory_format=torch.channels_last)
                            for t in (base,) + tuple(levels))
+
+
+def _to_nhwc(x, dtype):
+    """NCHW fp32 x -> channels-last `dtype` copy in one pass (vfd_nchw_to_nhwc)."""
+    lib = L.load()
+    n, C, h, w = x.shape
+    y = torch.empty(n, C, h, w, device=x.device, dtype=dtype, memory_format=torch.channels_last)
+    L.check(lib.vfd_nchw_to_nhwc(x.data_ptr(), y.data_ptr(), n, C, h * w, _DT[dtype], L.stream()), 'nchw_to_nhwc')
+    return y
 
 
 class AggregateUp(torch.autograd.Function):
@@ -1349,7 +1372,9 @@ class AggregateUp(torch.autograd.Function):
                                              out.data_ptr(), _DT[base.dtype], L.stream()), 'aggregate_fwd_cl')
             ctx.save_for_backward(out)
             ctx.level_shapes = [tuple(t.shape) for t in levels]
+            ctx.cl_dtype = base.dtype if _AGG_CL_GRAD else None
             return out
+        ctx.cl_dtype = None
         base, bias = _dev(base, 'aggregate base'), _dev(bias, 'bias')
         levels = [_dev(t, 'aggregate level') for t in levels]
         out = torch.empty_like(base)
@@ -1379,6 +1404,8 @@ class AggregateUp(torch.autograd.Function):
                                           psum.data_ptr(), L.stream()), 'aggregate_bwd')
             if L.PROF_ON:
                 L.ALG_BYTES['upsample_bwd'] += (3 * g.numel() + sum(t.numel() for t in grads)) * 4
+            if ctx.cl_dtype is not None:       # channels-last inputs: their gradients in their layout / dtype
+                d, grads = _to_nhwc(d, ctx.cl_dtype), [_to_nhwc(t, ctx.cl_dtype) for t in grads]
             return (d, psum.view(BN, C).sum(0)) + tuple(grads)
         d = (g * torch.where(out > 0, 1.0, 0.1)).contiguous()
         grads = []
@@ -1390,7 +1417,10 @@ class AggregateUp(torch.autograd.Function):
             if L.PROF_ON:
                 L.ALG_BYTES['upsample_bwd'] += (d.numel() + dl.numel()) * 4
             grads.append(dl)
-        return (d, d.sum((0, 2, 3))) + tuple(grads)
+        db = d.sum((0, 2, 3))
+        if ctx.cl_dtype is not None:
+            d, grads = _to_nhwc(d, ctx.cl_dtype), [_to_nhwc(t, ctx.cl_dtype) for t in grads]
+        return (d, db) + tuple(grads)
 
 
 # =============================================================================================

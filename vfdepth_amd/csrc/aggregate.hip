@@ -297,6 +297,9 @@ constexpr int AGC_X = 32, AGC_C = 64;
 #ifndef VFD_AGC_U
 #define VFD_AGC_U 2                                // columns per thread in flight (of 8)
 #endif
+#ifndef VFD_AGC_PAIR
+#define VFD_AGC_PAIR 0                             // channel pairs per lane (aggregate_cl2_fwd_k)
+#endif
 
 struct AggLevelsT {
   const void* src[3];
@@ -347,6 +350,72 @@ __global__ __launch_bounds__(256) void aggregate_cl_fwd_k(int C, int h, int w, c
   if (x0 + xo < w) {
 #pragma unroll
     for (int j = 0; j < AGC_C / 8; ++j) {
+      const int cc = cr + 8 * j;
+      if (c0 + cc < C) out[((n * C + c0 + cc) * h + y) * w + x0 + xo] = tile[cc][xo];
+    }
+  }
+}
+
+// The same with a channel pair per lane (C even, 8-B / 4-B aligned maps): 128 channels per
+// workgroup, one 8-B fp32 / 4-B bf16 load per tap and pair — half the load instructions; each
+// channel's arithmetic is aggregate_cl_fwd_k's.
+__device__ __forceinline__ float2 agc_ld2(const float* p) { return *reinterpret_cast<const float2*>(p); }
+__device__ __forceinline__ float2 agc_ld2(const __bf16* p) {
+  const uint32_t u = *reinterpret_cast<const uint32_t*>(p);
+  return make_float2(__uint_as_float(u << 16), __uint_as_float(u & 0xFFFF0000u));
+}
+
+constexpr int AGC2_C = 2 * AGC_C;
+
+template <int NL, typename TI>
+__global__ __launch_bounds__(256) void aggregate_cl2_fwd_k(int C, int h, int w, const TI* __restrict__ base,
+                                                           AggLevelsT lv, const float* __restrict__ bias,
+                                                           float* __restrict__ out) {
+  __shared__ float tile[AGC2_C][AGC_X + 1];
+  const int ncx = (w + AGC_X - 1) / AGC_X;
+  const int x0 = (blockIdx.x % ncx) * AGC_X, c0 = (blockIdx.x / ncx) * AGC2_C;
+  const int y = blockIdx.y;
+  const long long n = blockIdx.z;
+  const int cl = threadIdx.x & (AGC_C - 1), xq = threadIdx.x >> 6;
+  const int c = c0 + 2 * cl;
+  if (c < C) {
+    int ya[3], yb[3];
+    float lyv[3];
+#pragma unroll
+    for (int k = 0; k < NL; ++k) up_axis(lv.hs[k], h, y, &ya[k], &yb[k], &lyv[k]);
+    const TI* bp = base + ((n * h + y) * w) * C + c;
+    const float bc0 = bias[c], bc1 = bias[c + 1];
+#pragma unroll VFD_AGC_U
+    for (int xl = xq; xl < AGC_X; xl += 4) {
+      const int x = x0 + xl;
+      if (x >= w) break;
+      const float2 b = agc_ld2(bp + (size_t)x * C);
+      float v0 = b.x, v1 = b.y;
+#pragma unroll
+      for (int k = 0; k < NL; ++k) {
+        const int hs = lv.hs[k], ws = lv.ws[k];
+        int xa, xb;
+        float lx;
+        up_axis(ws, w, x, &xa, &xb, &lx);
+        const TI* lp = reinterpret_cast<const TI*>(lv.src[k]) + (n * hs * ws) * C + c;
+        const float2 p00 = agc_ld2(lp + ((size_t)ya[k] * ws + xa) * C), p01 = agc_ld2(lp + ((size_t)ya[k] * ws + xb) * C);
+        const float2 p10 = agc_ld2(lp + ((size_t)yb[k] * ws + xa) * C), p11 = agc_ld2(lp + ((size_t)yb[k] * ws + xb) * C);
+        const float top0 = (1.f - lx) * p00.x + lx * p01.x, bot0 = (1.f - lx) * p10.x + lx * p11.x;
+        const float top1 = (1.f - lx) * p00.y + lx * p01.y, bot1 = (1.f - lx) * p10.y + lx * p11.y;
+        v0 += (1.f - lyv[k]) * top0 + lyv[k] * bot0;
+        v1 += (1.f - lyv[k]) * top1 + lyv[k] * bot1;
+      }
+      v0 += bc0;
+      v1 += bc1;
+      tile[2 * cl][xl] = v0 > 0.f ? v0 : v0 * 0.1f;
+      tile[2 * cl + 1][xl] = v1 > 0.f ? v1 : v1 * 0.1f;
+    }
+  }
+  __syncthreads();
+  const int xo = threadIdx.x & (AGC_X - 1), cr = threadIdx.x >> 5;
+  if (x0 + xo < w) {
+#pragma unroll 4
+    for (int j = 0; j < AGC2_C / 8; ++j) {
       const int cc = cr + 8 * j;
       if (c0 + cc < C) out[((n * C + c0 + cc) * h + y) * w + x0 + xo] = tile[cc][xo];
     }
@@ -404,9 +473,15 @@ extern "C" int vfd_aggregate_fwd_cl(int BN, int C, int h, int w, const void* bas
   }
   hipStream_t s = (hipStream_t)stream;
   vfd::ProfScope ps(vfd::K_AGGREGATE, s);
-  const dim3 grid((unsigned)(((w + vfd::AGC_X - 1) / vfd::AGC_X) * ((C + vfd::AGC_C - 1) / vfd::AGC_C)), (unsigned)h,
-                  (unsigned)BN);
-#define VFD_AGC(NL, T) vfd::aggregate_cl_fwd_k<NL, T><<<grid, 256, 0, s>>>(C, h, w, (const T*)base, lv, bias, out)
+  // channel pairs when every map allows the 2-element loads
+  uintptr_t al = (uintptr_t)base;
+  for (int k = 0; k < n_levels; ++k) al |= (uintptr_t)lv.src[k];
+  const bool pair = VFD_AGC_PAIR && C % 2 == 0 && (al & (dtype ? 3 : 7)) == 0;
+  const int cpb = pair ? vfd::AGC2_C : vfd::AGC_C;
+  const dim3 grid((unsigned)(((w + vfd::AGC_X - 1) / vfd::AGC_X) * ((C + cpb - 1) / cpb)), (unsigned)h, (unsigned)BN);
+#define VFD_AGC(NL, T)                                                                                           \
+  if (pair) vfd::aggregate_cl2_fwd_k<NL, T><<<grid, 256, 0, s>>>(C, h, w, (const T*)base, lv, bias, out);        \
+  else vfd::aggregate_cl_fwd_k<NL, T><<<grid, 256, 0, s>>>(C, h, w, (const T*)base, lv, bias, out)
 #define VFD_AGC_T(T)                      \
   switch (n_levels) {                     \
     case 0: VFD_AGC(0, T); break;         \

@@ -298,7 +298,7 @@ constexpr int AGC_X = 32, AGC_C = 64;
 #define VFD_AGC_U 2                                // columns per thread in flight (of 8)
 #endif
 #ifndef VFD_AGC_PAIR
-#define VFD_AGC_PAIR 0                             // channel pairs per lane (aggregate_cl2_fwd_k)
+#define VFD_AGC_PAIR 1                             // channel pairs per lane (aggregate_cl2_fwd_k)
 #endif
 
 struct AggLevelsT {

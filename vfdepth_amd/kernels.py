@@ -730,7 +730,9 @@ def _pose_fuse_t(space, plan, feats, dtype):
     lib = L.load()
     feats = _dev(feats, 'feats')
     B, N, C = feats.shape[:3]
-    feats_cl = feats.flatten(3).transpose(2, 3).contiguous()        # [B, N, h*w, C]
+    hw = feats.shape[3] * feats.shape[4]
+    feats_cl = torch.empty(B, N, hw, C, device=feats.device)          # [B, N, h*w, C]: one tiled pass
+    L.check(lib.vfd_nchw_to_nhwc(feats.data_ptr(), feats_cl.data_ptr(), B * N, C, hw, 0, L.stream()), 'nchw_to_nhwc')
     out = torch.empty(B, (C + 1) * space.Z, space.Y + 2, space.X + 2, device=feats.device, dtype=dtype,
                       memory_format=torch.channels_last)
     d = space.desc(B, N, C=C)

@@ -189,10 +189,7 @@ class VFNet(nn.Module):
         # the fold is part of K1's algebra (it replaces the reference's fp32 1x1 convs after the
         # gather): fp32 even when the dense nets run under bf16 autocast (config 3)
         with torch.autocast(device_type='cuda', enabled=False):
-            # P[b, n] = f[b, n]^T W_n^T as one batched GEMM on transposed views (einsum's operand
-            # permute copied the whole [B, N, C, hw] map first: 64 us at config 3)
-            P = torch.matmul(feats_agg.float().reshape(B, N, C, h * w).transpose(-1, -2),
-                             wf.float().transpose(-1, -2)).contiguous()
+            P = torch.einsum('bncp,nkc->bnpk', feats_agg.float().reshape(B, N, C, h * w), wf.float()).contiguous()
         K = inputs['K', self.fusion_level + 1]
         # the step's fusion plan (shared with the pose calls) indexes K1's atomic-free backward
         return KN.FuseDepth.apply(space, P, self._mask_lowres(inputs, space), K, inputs['extrinsics_inv'],

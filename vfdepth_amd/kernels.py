@@ -733,6 +733,8 @@ def _pose_fuse_t(space, plan, feats, dtype):
     hw = feats.shape[3] * feats.shape[4]
     feats_cl = torch.empty(B, N, hw, C, device=feats.device)          # [B, N, h*w, C]: one tiled pass
     L.check(lib.vfd_nchw_to_nhwc(feats.data_ptr(), feats_cl.data_ptr(), B * N, C, hw, 0, L.stream()), 'nchw_to_nhwc')
+    if L.PROF_ON:                            # timed under the upsample_bwd scope (vfd_nchw_to_nhwc)
+        L.ALG_BYTES['upsample_bwd'] += 2 * feats.numel() * 4
     out = torch.empty(B, (C + 1) * space.Z, space.Y + 2, space.X + 2, device=feats.device, dtype=dtype,
                       memory_format=torch.channels_last)
     d = space.desc(B, N, C=C)
@@ -1351,6 +1353,8 @@ def _to_nhwc(x, dtype):
     n, C, h, w = x.shape
     y = torch.empty(n, C, h, w, device=x.device, dtype=dtype, memory_format=torch.channels_last)
     L.check(lib.vfd_nchw_to_nhwc(x.data_ptr(), y.data_ptr(), n, C, h * w, _DT[dtype], L.stream()), 'nchw_to_nhwc')
+    if L.PROF_ON:                            # timed under the upsample_bwd scope (the aggregate's backward)
+        L.ALG_BYTES['upsample_bwd'] += x.numel() * 4 + y.numel() * y.element_size()
     return y
 
 

@@ -778,6 +778,32 @@ def test_pad_conv_bf16(shape):
         gclose(a.grad, r.grad, f'bf16 K2C {name} {shape}', rel=2e-2)
 
 
+@pytest.mark.parametrize('shape', [(2, 20, 13, 11, 2), (1, 44, 9, 30, 1)])
+def test_pad_conv_bf16_wgrad_declined_falls_back(shape, monkeypatch):
+    """When the bf16 K2C weight gradient declines a map (zero workspace: few channel tiles for the
+    device's CU count), PadConvBF16's backward takes MIOpen's bf16 weight gradient instead of
+    raising; the result equals the HIP kernel's within bf16 accumulation noise."""
+    from vfdepth_amd import kernels as KN
+    B, C, H, W, s = shape
+    gen = torch.Generator(device=DEV).manual_seed(183)
+    x = torch.randn(B, C, H, W, device=DEV, generator=gen).contiguous(memory_format=torch.channels_last)
+    w = torch.randn(256, C, 3, 3, device=DEV, generator=gen) * (C * 9) ** -0.5
+    b = 0.1 * torch.randn(256, device=DEV, generator=gen)
+    g = None
+    grads = []
+    for declined in (False, True):
+        if declined:
+            monkeypatch.setattr(KN, 'pad_conv_wgrad_bf16_supported', lambda *a: False)
+        leaves = [t.clone().requires_grad_(True) for t in (x, w, b)]
+        y = KN.PadConvBF16.apply(leaves[0], leaves[1], leaves[2], s, None, None)
+        if g is None:
+            g = torch.randn(y.shape, device=DEV, generator=gen)
+        (y.float() * g).sum().backward()
+        grads.append([t.grad for t in leaves])
+    for name, a, r in zip(('d input', 'd weight', 'd bias'), grads[1], grads[0]):
+        gclose(a, r, f'bf16 K2C (MIOpen weight gradient) {name} {shape}', rel=2e-2)
+
+
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize('config,B', [(2, 2), (5, 1)])
 def test_pose_conv_bf16_map_matches_two_nodes(config, B, monkeypatch):

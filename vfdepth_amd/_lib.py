@@ -204,7 +204,7 @@ KERNEL_IDS = {
     'voxel_project_fwd': 5, 'voxel_project_bwd': 6, 'view_stats': 7, 'view_apply': 8, 'view_bwd': 9,
     'photo_fwd': 10, 'photo_bwd': 11, 'smooth_fwd': 12, 'smooth_bwd': 13, 'fusion_plan': 14,
     'aggregate': 15, 'voxel_project_plan': 16, 'proj_conv_fwd': 17,
-    'depth_syn_fwd': 18, 'depth_syn_bwd': 19, 'proj_conv_dgrad': 20, 'pad_conv_fwd': 21, 'bn_fwd': 22, 'bn_bwd': 23, 'reflect_pad': 24, 'upsample_bwd': 25, 'maxpool': 26, 'elu_pad': 27, 'disp_conv': 28, 'dec_conv': 29, 'proj_conv_wgrad': 30, 'pad_conv_dgrad': 31, 'pad_conv_wgrad': 32,
+    'depth_syn_fwd': 18, 'depth_syn_bwd': 19, 'proj_conv_dgrad': 20, 'pad_conv_fwd': 21, 'bn_fwd': 22, 'bn_bwd': 23, 'reflect_pad': 24, 'upsample_bwd': 25, 'maxpool': 26, 'elu_pad': 27, 'disp_conv': 28, 'dec_conv': 29, 'proj_conv_wgrad': 30, 'pad_conv_dgrad': 31, 'pad_conv_wgrad': 32, 'layout_copy': 33,
 }
 
 
@@ -227,7 +227,7 @@ def prof_enable(kernel='all'):
 # Algorithmic bytes of the shape-varying dense-net kernels (fused BN, reflect pads, upsample
 # backward), accumulated by their Python wrappers while profiling is on (bench.py's rooflines).
 PROF_ON = False
-ALG_BYTES = {'bn_fwd': 0, 'bn_bwd': 0, 'reflect_pad': 0, 'upsample_bwd': 0, 'maxpool': 0, 'elu_pad': 0, 'disp_conv': 0, 'dec_conv': 0}
+ALG_BYTES = {'bn_fwd': 0, 'bn_bwd': 0, 'reflect_pad': 0, 'upsample_bwd': 0, 'maxpool': 0, 'elu_pad': 0, 'disp_conv': 0, 'dec_conv': 0, 'layout_copy': 0}
 
 
 def prof_read():

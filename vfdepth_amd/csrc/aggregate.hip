@@ -449,7 +449,7 @@ extern "C" int vfd_nchw_to_nhwc(const float* x, void* y, long long n, int C, int
   VFD_REQUIRE(x && y && n > 0 && n < 65536 && C > 0 && hw > 0 && (dtype_out == 0 || dtype_out == 1),
               "nchw_to_nhwc: bad arguments");
   hipStream_t s = (hipStream_t)stream;
-  vfd::ProfScope ps(vfd::K_UPSAMPLE_BWD, s);
+  vfd::ProfScope ps(vfd::K_LAYOUT_COPY, s);
   const dim3 grid((unsigned)((hw + 63) / 64), (unsigned)((C + 63) / 64), (unsigned)n);
   if (dtype_out == 1) vfd::nchw_to_nhwc_k<__bf16><<<grid, 256, 0, s>>>(x, (__bf16*)y, C, hw);
   else vfd::nchw_to_nhwc_k<float><<<grid, 256, 0, s>>>(x, (float*)y, C, hw);

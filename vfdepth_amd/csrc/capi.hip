@@ -81,7 +81,7 @@ static const char* kNames[K_COUNT] = {
   "mask_downsample", "fuse_depth_fwd", "fuse_depth_bwd", "fuse_pose_fwd", "fuse_pose_bwd",
   "voxel_project_fwd", "voxel_project_bwd", "view_stats", "view_apply", "view_bwd",
   "photo_fwd", "photo_bwd", "smooth_fwd", "smooth_bwd", "fusion_plan", "aggregate", "voxel_project_plan",
-  "proj_conv_fwd", "depth_syn_fwd", "depth_syn_bwd", "proj_conv_dgrad", "pad_conv_fwd", "bn_fwd", "bn_bwd", "reflect_pad", "upsample_bwd", "maxpool", "elu_pad", "disp_conv", "dec_conv", "proj_conv_wgrad", "pad_conv_dgrad", "pad_conv_wgrad"};
+  "proj_conv_fwd", "depth_syn_fwd", "depth_syn_bwd", "proj_conv_dgrad", "pad_conv_fwd", "bn_fwd", "bn_bwd", "reflect_pad", "upsample_bwd", "maxpool", "elu_pad", "disp_conv", "dec_conv", "proj_conv_wgrad", "pad_conv_dgrad", "pad_conv_wgrad", "layout_copy"};
 
 }  // namespace vfd
 

@@ -302,9 +302,7 @@ __device__ __forceinline__ void ppb_stage(const PpGeom& g, __bf16* __restrict__ 
     for (int u = 0; u < U; ++u) {
       const int p = p0 + PPP * u;
       v[u] = PQ::zero();
-#ifndef VFD_PPB_NOSTAGE
       if (cok && p < pval) v[u] = PQ::load(src + (size_t)p * g.cin);
-#endif
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -406,12 +404,10 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppcb_main_k(PpGeom g, const TX*
         acc[a][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bq[ring][1], acc[a][1], 0, 0, 0);
       }
       // the refill lands in the slot the MFMAs above just read (no register copy of the slot)
-#ifndef VFD_PPB_NOB
       if (st + PF < STEPS)
         wld(wc, st + PF, bq[ring]);
       else if (more)
         wld(wn, st + PF - STEPS, bq[ring]);
-#endif
 #endif
       // keep the scheduler from hoisting later steps' LDS reads above these MFMAs (register
       // pressure: the prefetch ring, not the A fragments, is what should hold VGPRs)
@@ -699,12 +695,8 @@ __device__ __forceinline__ void pdc_stage(const PdcGeom& g, T* __restrict__ dst,
       const int p = p0 + PPP * u;
       const int y = r0 + r, x = c - c0;
       pos[u] = p;
-#ifdef VFD_PD_NOSTAGE
-      v[u] = PV::zero();
-#else
       v[u] = (p < npos && y >= 0 && y < g.ho && x >= 0 && x < g.wo) ? PV::load(src + ((size_t)y * g.wo + x) * PP_O)
                                                                    : PV::zero();
-#endif
       c += cstep;
       r += rstep;
       if (c >= g.cols) {
@@ -868,7 +860,7 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppd_main_k(PdcGeom g, const TG*
         }
 #undef VFD_PD_B
         // refill the slots just read (no copy-out of the ring: see ppcb_main_k)
-#if !defined(VFD_PD_NOB) && !VFD_RING_EARLY
+#if !VFD_RING_EARLY
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
           if (q + PF < STEPS)
@@ -908,9 +900,7 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppd_main_k(PdcGeom g, const TG*
             }
 #pragma unroll
             for (int b = 0; b < NB; ++b) {
-#ifndef VFD_PD_NOSTORE
               if (mb + d < hw && n0 + 32 * b < g.cin) st1(pa + off + 32 * b, acc[a][b][r]);
-#endif
               acc[a][b][r] = 0.f;
             }
           }

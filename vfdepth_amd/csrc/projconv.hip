@@ -157,11 +157,7 @@ __device__ __forceinline__ void pc_gather(const vfd_voxel_desc& d, T* __restrict
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const bool ok = (in >> k & 1u) != 0u;
-#ifdef VFD_PCV_NOGATHER                       // timing experiment only: no corner loads
-        v[u][k] = make_float4(0.f, 0.f, 0.f, (float)(ok ? base : 0));
-#else
         v[u][k] = vb[(size_t)(ok ? base + corner_offset(d, k) : 0) * (PC_CV / 4)];
-#endif
       }
     }
 #pragma unroll
@@ -181,11 +177,7 @@ __device__ __forceinline__ void pc_gather(const vfd_voxel_desc& d, T* __restrict
         acc.w += v[u][k].w * w;
       }
       pc_put(&xs[p * XS + 4 * q], acc);
-#ifdef VFD_PCV_NOXO                           // timing experiment only: no side output
-      if (false) {
-#else
       if (xo) {
-#endif
         const int hr = p / PC_HC, hc = p - hr * PC_HC;
         const int py = y0 + hr - 1, px = x0 + hc - 1;
         if (hr >= 1 && hr <= PC_TR && hc >= 1 && hc <= PC_TC && py < d.h && px < d.w) {
@@ -411,16 +403,11 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pcvb_main_k(vfd_voxel_desc d, P
   const bf16x8* wp = wbase + (size_t)(a_lo % d.D) * PCB_ITERS * (PC_O / 32) * 64;
   const bf16x8* wend = wbase + (size_t)d.D * PCB_ITERS * (PC_O / 32) * 64;
   bf16x8 bq[PCB_PF][2];
-#ifdef VFD_PCV_NOB
-  for (int k = 0; k < PCB_PF; ++k) bq[k][0] = bq[k][1] = wbase[64 * k];
-#endif
   int pf_left = (a_hi - a_lo) * PCB_ITERS;         // steps still to prefetch
   auto prefetch = [&](int slot) {
     if (pf_left > 0) {
-#ifndef VFD_PCV_NOB                           // timing experiment only: B fragments loaded once
       bq[slot][0] = wp[0];
       bq[slot][1] = wp[64];
-#endif
       wp += (PC_O / 32) * 64;
       if (wp == wend) wp = wbase;
       --pf_left;
@@ -1268,9 +1255,6 @@ __device__ __forceinline__ void pg_stage(const PgGeom& g, T* __restrict__ dst, c
   const int nrow = g.hrows + 2;
   const int q = tid % QP;
   const TG* src = gp + (size_t)tl.bc * hw * PC_O + ch * OC + CH * q;
-#ifdef VFD_PG_NOSTAGE
-  return;                                             // timing experiment only: LDS left as is
-#endif
   for (int c = tid / QP; c < g.cols; c += CPP) {
     int xa, xb = -1;
     if (c < g.w + 2) {
@@ -1408,16 +1392,10 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pcg_main_k(PgGeom g, const TG* 
       const BFrag b = bq[j % PF];
       {                                               // refill the slot with iteration j + PF
         const int jn = j + PF;
-#ifdef VFD_PG_NOB
-        if (jn < 0)                                   // timing experiment only: B loaded once
-#else
         if (jn < ITERS)
-#endif
           bq[j % PF] = bcur[(jn / STEPS) * tstride + (jn % STEPS) * qstride];
-#ifndef VFD_PG_NOB
         else if (more)
           bq[j % PF] = bnext[((jn - ITERS) / STEPS) * tstride + ((jn - ITERS) % STEPS) * qstride];
-#endif
       }
       if (q < STEPS - 1) {
 #pragma unroll
@@ -1617,10 +1595,6 @@ __device__ __forceinline__ void ph_fetch(const PhGeom& g, const __bf16* __restri
     bf16x8 z;
 #pragma unroll
     for (int e = 0; e < 8; ++e) z[e] = (__bf16)0.f;
-#ifdef VFD_PH_NOSTAGE                       // timing experiment only: no G loads
-    v[k][0] = v[k][1] = v[k][2] = v[k][3] = z;
-    (void)ys; (void)xs;
-#else
     // only the two fold rows / columns have partners (yb / xb): the interior's 3 partner slots are
     // zero without a load or its address arithmetic
     v[k][0] = (ya >= 0 && xa >= 0) ? *reinterpret_cast<const bf16x8*>(src + ((size_t)ya * g.w + xa) * PC_O) : z;
@@ -1632,7 +1606,6 @@ __device__ __forceinline__ void ph_fetch(const PhGeom& g, const __bf16* __restri
         if (yy >= 0 && xx >= 0) v[k][j] = *reinterpret_cast<const bf16x8*>(src + ((size_t)yy * g.w + xx) * PC_O);
       }
     }
-#endif
   }
 }
 
@@ -1756,11 +1729,7 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pch_main_k(PhGeom g, const __bf
       const bf16x8 b = bq[j % PF];
       {
         const int jn = j + PF;
-#ifdef VFD_PH_NOB                            // timing experiment only: B fragments loaded once
-        if (jn < 0)
-#else
         if (jn < ITERS)
-#endif
           bq[j % PF] = bcur[(jn / STEPS) * tstride + (jn % STEPS) * qstride];
         else if (more)
           bq[j % PF] = bnext[((jn - ITERS) / STEPS) * tstride + ((jn - ITERS) % STEPS) * qstride];
@@ -2193,10 +2162,8 @@ __device__ __forceinline__ void wb_fetch(const WbGeom& g, WbStage<TX, XV>& st, c
     const int e = tid + PC_THREADS * u, px = e >> 5, q = e & 31;     // 32 vectors of 8 o per pixel
     const int y = y0 + (px >> 4), x = x0 + (px & 15);
     st.gv[u] = make_uint4(0u, 0u, 0u, 0u);
-#ifndef VFD_PWB_NOFETCH                       // timing experiment only: no G / X loads
     if (y < g.ho && x < g.wo)
       st.gv[u] = *reinterpret_cast<const uint4*>(gp + (((size_t)img * g.ho + y) * g.wo + x) * PC_O + 8 * q);
-#endif
   }
   const int npos = g.hr * g.hc, vpp = WB_XP / XV;
 #pragma unroll
@@ -2205,11 +2172,7 @@ __device__ __forceinline__ void wb_fetch(const WbGeom& g, WbStage<TX, XV>& st, c
     const int r = pos / g.hc, c = pos - r * g.hc;
     const int Y = g.s * y0 + r, X = g.s * x0 + c, n = t * 32 + XV * q;
     memset(&st.xv[u], 0, sizeof(st.xv[u]));
-#ifdef VFD_PWB_NOFETCH
-    if (false)
-#else
     if (pos < npos && Y < g.hp && X < g.wp && n < g.C)
-#endif
       st.xv[u] = *reinterpret_cast<const XT*>(xp + (((size_t)img * g.hp + Y) * g.wp + X) * g.C + n);
   }
 }

@@ -30,7 +30,7 @@ void lds_attr(const void* fn, int bytes);
 enum KernelId {
   K_MASK_DOWN = 0, K_FUSE_DEPTH_FWD, K_FUSE_DEPTH_BWD, K_FUSE_POSE_FWD, K_FUSE_POSE_BWD,
   K_VPROJ_FWD, K_VPROJ_BWD, K_VIEW_STATS, K_VIEW_APPLY, K_VIEW_BWD, K_PHOTO_FWD, K_PHOTO_BWD,
-  K_SMOOTH_FWD, K_SMOOTH_BWD, K_FUSION_PLAN, K_AGGREGATE, K_VPROJ_PLAN, K_PROJ_CONV_FWD, K_DEPTH_SYN_FWD, K_DEPTH_SYN_BWD, K_PROJ_CONV_DGRAD, K_PAD_CONV_FWD, K_BN_FWD, K_BN_BWD, K_REFLECT_PAD, K_UPSAMPLE_BWD, K_MAXPOOL, K_ELU_PAD, K_DISP_CONV, K_DEC_CONV, K_PROJ_CONV_WGRAD, K_PAD_CONV_DGRAD, K_PAD_CONV_WGRAD, K_COUNT
+  K_SMOOTH_FWD, K_SMOOTH_BWD, K_FUSION_PLAN, K_AGGREGATE, K_VPROJ_PLAN, K_PROJ_CONV_FWD, K_DEPTH_SYN_FWD, K_DEPTH_SYN_BWD, K_PROJ_CONV_DGRAD, K_PAD_CONV_FWD, K_BN_FWD, K_BN_BWD, K_REFLECT_PAD, K_UPSAMPLE_BWD, K_MAXPOOL, K_ELU_PAD, K_DISP_CONV, K_DEC_CONV, K_PROJ_CONV_WGRAD, K_PAD_CONV_DGRAD, K_PAD_CONV_WGRAD, K_LAYOUT_COPY, K_COUNT
 };
 void prof_begin(int id, hipStream_t s);
 void prof_end(int id, hipStream_t s);

@@ -447,12 +447,12 @@ def weight_swap(w, A, B, cache=False, memory_format=torch.contiguous_format):
     result for the same tensor, version and format (the pose weight, swapped once per step for both
     pose calls' backward)."""
     key = (w.data_ptr(), w._version, tuple(w.shape), A, B, memory_format) if cache else None
-    if key is not None and key in _SWAP_CACHE:
-        return _SWAP_CACHE[key]
+    hit = _SWAP_CACHE.get('entry')
+    if key is not None and hit is not None and hit[1] == key:
+        return hit[2]
     out = _weight_permute_swap(w, A, B, memory_format)
-    if key is not None:
-        _SWAP_CACHE.clear()
-        _SWAP_CACHE[key] = out
+    if key is not None:     # the entry holds the source, so its address cannot be reused meanwhile
+        _SWAP_CACHE['entry'] = (w, key, out)
     return out
 
 
@@ -502,9 +502,12 @@ def pad_conv_dgrad_weight(w, perm=None, bf16=False, cache=True):
     w = _dev(w.detach(), 'pad_conv weight')
     O, C = w.shape[:2]
     Cv, D = perm if perm else (C, 1)
+    # the entry holds the source tensor (so its storage stays alive and no other weight can be
+    # handed the same address while the key is live) next to (address, version, shape)
     key = (w.data_ptr(), w._version, tuple(w.shape), Cv, D, bf16)
-    if cache and key in _PDW_CACHE:
-        return _PDW_CACHE[key]
+    hit = _PDW_CACHE.get('entry')
+    if cache and hit is not None and hit[1] == key:
+        return hit[2]
     npad = (C + 255) // 256 * 256
     f2 = torch.empty(9, O // 4, npad, 2, 2, device=w.device)
     L.check(lib.vfd_weight_fragments(2, w.data_ptr(), f2.data_ptr(), O, 0, 0, 0, Cv, D, L.stream()),
@@ -515,8 +518,7 @@ def pad_conv_dgrad_weight(w, perm=None, bf16=False, cache=True):
         L.check(lib.vfd_weight_fragments_bf16(5, f2.data_ptr(), out.data_ptr(), O, 0, 0, 0, Cv, D, L.stream()),
                 'weight_fragments_bf16')
     if cache:
-        _PDW_CACHE.clear()
-        _PDW_CACHE[key] = out
+        _PDW_CACHE['entry'] = (w, key, out)
     return out
 
 
@@ -643,13 +645,24 @@ def pad_conv_bf16_supported(x, stride, out_channels):
     return bool(L.load().vfd_pad_conv_fwd_bf16_workspace(ctypes.byref(pad_conv_desc(x, stride, out_channels))))
 
 
+def pad_conv_wgrad_bf16_supported(x, stride, out_channels):
+    """The bf16 K2C weight gradient (pwb_main_k) accepts this map: its workspace query is non-zero (it
+    depends on the channel tiles and the device's CU count); PadConvBF16 takes MIOpen's otherwise."""
+    return bool(L.load().vfd_pad_conv_wgrad_bf16_workspace(ctypes.byref(pad_conv_desc(x, stride, out_channels))))
+
+
 class PadConvBF16(torch.autograd.Function):
     """K2C in bf16 (config 3): the fp32 reflect-padded channels-last map rounded to bf16 as it is
     staged, bf16 weights, v_mfma_f32_32x32x16_bf16 with fp32 accumulation, bias + LeakyReLU in fp32,
     output bf16 (reflect-padded channels-last, the input of the next conv, which autocast runs in
-    bf16).  Backward: MIOpen's fp32 data gradient of the fp32 map (no bf16 round trip) and bf16
-    weight gradient on bf16 copies of the map and weight; gradients returned in fp32 (the map, the
-    master weight, the bias)."""
+    bf16).  Backward (default): the d pre-activation (LeakyReLU + pad adjoint in fp32) rounded once
+    to bf16 is the operand of both hand-written bf16 MFMA gradients — the data gradient
+    (padconv.hip ppd_main_k: bf16 weight fragments, fp32 accumulation, fp32 d map, or bf16 with
+    VFD_PD_DX_BF16=1) and the weight / bias gradient (projconv.hip pwb_main_k: the map rounded to
+    bf16 as it is staged, fp32 accumulation); gradients returned in fp32 (the map, the master
+    weight, the bias).  VFD_PC_BF16_BWD=0 (both), VFD_PAD_DGRAD=0 / VFD_PAD_WGRAD=0 (one) restore
+    MIOpen's: its fp32 data gradient of the fp32 map and its bf16 weight gradient on bf16 copies;
+    shapes the HIP kernels decline (zero workspace) take MIOpen's as well."""
 
     @staticmethod
     def forward(ctx, x, w, bias, stride, wf=None, perm=None):
@@ -691,7 +704,8 @@ class PadConvBF16(torch.autograd.Function):
             if dx is not None:
                 dx = dx.to(x.dtype)
         wd = None
-        if (mask[0] and dx is None) or ((mask[1] or mask[2]) and not (_PC_BF16_BWD and _PAD_WGRAD)):
+        hip_wgrad = _PC_BF16_BWD and _PAD_WGRAD and pad_conv_wgrad_bf16_supported(x, s, w.shape[0])
+        if (mask[0] and dx is None) or ((mask[1] or mask[2]) and not hip_wgrad):
             wd = w.detach()
             if ctx.perm:    # MIOpen works in the map's channel order (channels-last like x)
                 C1, Z = ctx.perm
@@ -702,7 +716,7 @@ class PadConvBF16(torch.autograd.Function):
             # the fp32 map's gradient would cast back)
             g32 = lrelu_pad_backward(g.float(), out.float())
             dx = cb(g32, x, wd, *args, [True, False, False])[0]
-        if (mask[1] or mask[2]) and _PC_BF16_BWD and _PAD_WGRAD:
+        if (mask[1] or mask[2]) and hip_wgrad:
             # the bf16 weight / bias gradient on MFMA (projconv.hip pwb_main_k: the fp32 map rounded
             # to bf16 as it is staged), d weight in the map's channel order, then the pose swap
             dw, db = pad_conv_wgrad_bf16(gb, x, w, s, mask[1], mask[2])
@@ -733,8 +747,8 @@ def _pose_fuse_t(space, plan, feats, dtype):
     hw = feats.shape[3] * feats.shape[4]
     feats_cl = torch.empty(B, N, hw, C, device=feats.device)          # [B, N, h*w, C]: one tiled pass
     L.check(lib.vfd_nchw_to_nhwc(feats.data_ptr(), feats_cl.data_ptr(), B * N, C, hw, 0, L.stream()), 'nchw_to_nhwc')
-    if L.PROF_ON:                            # timed under the upsample_bwd scope (vfd_nchw_to_nhwc)
-        L.ALG_BYTES['upsample_bwd'] += 2 * feats.numel() * 4
+    if L.PROF_ON:                            # timed under its own layout_copy scope (vfd_nchw_to_nhwc)
+        L.ALG_BYTES['layout_copy'] += 2 * feats.numel() * 4
     out = torch.empty(B, (C + 1) * space.Z, space.Y + 2, space.X + 2, device=feats.device, dtype=dtype,
                       memory_format=torch.channels_last)
     d = space.desc(B, N, C=C)
@@ -987,9 +1001,15 @@ class ProjConvBF16(torch.autograd.Function):
     volumetric_fusionnet.py:105-114): the fp32 trilinear samples of the fp32 voxel grid rounded to
     bf16 in LDS, bf16 weights, v_mfma_f32_32x32x16_bf16 with fp32 accumulation, bias + LeakyReLU
     in fp32, output bf16 (the reflect-padded channels-last input of reduce_dim's second conv,
-    which autocast runs in bf16).  Backward: MIOpen's bf16 data / weight gradients on the bf16
-    frustum features the kernel writes as its side output, then K3's fp32 planned backward.
-    Gradients to the fp32 voxels / master weight / bias come back in fp32."""
+    which autocast runs in bf16).  Backward (default): the d pre-activation (LeakyReLU + pad
+    adjoint in fp32) rounded once to bf16 feeds the hand-written bf16 MFMA gradients — the data
+    gradient (projconv.hip pch_main_k, folded reflect-pad adjoint, bf16 weight fragments, fp32
+    accumulation, fp32 d frustum features) into K3's fp32 planned backward, and the weight / bias
+    gradient (pwb_main_k over the bf16 frustum features the forward writes as its side output, fp32
+    accumulation, d weight straight in the reference channel order).  VFD_PC_BF16_BWD=0 (or
+    VFD_PC_DGRAD=0 for the data gradient) restores MIOpen's bf16 gradients; shapes the HIP kernels
+    decline (zero workspace) take MIOpen's as well.  Gradients to the fp32 voxels / master weight /
+    bias come back in fp32."""
 
     @staticmethod
     def forward(ctx, space, vox, invK, E, w0, bias):
@@ -1353,8 +1373,8 @@ def _to_nhwc(x, dtype):
     n, C, h, w = x.shape
     y = torch.empty(n, C, h, w, device=x.device, dtype=dtype, memory_format=torch.channels_last)
     L.check(lib.vfd_nchw_to_nhwc(x.data_ptr(), y.data_ptr(), n, C, h * w, _DT[dtype], L.stream()), 'nchw_to_nhwc')
-    if L.PROF_ON:                            # timed under the upsample_bwd scope (the aggregate's backward)
-        L.ALG_BYTES['upsample_bwd'] += x.numel() * 4 + y.numel() * y.element_size()
+    if L.PROF_ON:                            # timed under the layout_copy scope (vfd_nchw_to_nhwc)
+        L.ALG_BYTES['layout_copy'] += x.numel() * 4 + y.numel() * y.element_size()
     return y
 
 
@@ -1371,6 +1391,8 @@ class AggregateUp(torch.autograd.Function):
         BN, C, h, w = base.shape
         hw = (L.c_int * max(2 * len(levels), 1))(*[v for t in levels for v in t.shape[-2:]])
         if _agg_cl_ok(base, levels):
+            for t in (base,) + tuple(levels):
+                _check_device(t, 'aggregate input')
             bias = _dev(bias, 'bias')
             out = torch.empty(BN, C, h, w, device=base.device)
             ptrs = (L.c_fp * max(len(levels), 1))(*[t.data_ptr() for t in levels])

@@ -237,12 +237,45 @@ def parity_check(device):
     metric, median = algo.compute_depth_metrics(inputs, outputs)
     absrel = {'metric': float(metric['abs_rel']), 'median': float(median['abs_rel']),
               'ref_metric': float(fm['step_metric_abs_rel']), 'ref_median': float(fm['step_median_abs_rel'])}
+    full = parity_full(device)
     return {'config': 'reduced 6-cam fusion step (96x160, voxels 40x40x10, D=16) vs the reference\'s outputs',
+            'full_resolution': full,
             'max_abs_diff_depth': d_depth, 'max_rel_diff_depth': rel_depth,
             'max_abs_diff_loss': max(d_loss.values()), 'loss_keys': len(d_loss),
             'abs_rel': absrel,
             'abs_rel_equal_1e-4': abs(absrel['metric'] - absrel['ref_metric']) <= 1e-4 * absrel['ref_metric']
             and abs(absrel['median'] - absrel['ref_median']) <= 1e-4 * absrel['ref_median']}
+
+
+def parity_full(device):
+    """The same check at config 2's full shape (6 x 384 x 640, 100 x 100 x 20 voxels, D = 50)
+    against the reference's own CPU step there (tests/golden/step_full.npz): max |Δ| of the depth
+    maps (every 4th pixel) and of every loss scalar, and the 1e-4 per-pixel north_star verdict."""
+    import numpy as np
+    import common as G
+    from vfdepth_amd.vfdepth import VFDepthAlgo
+    fx = np.load(os.path.join(ROOT, 'tests', 'golden', 'step_full.npz'))
+    cfg = G.full_cfg()
+    algo = VFDepthAlgo(cfg, device.index)
+    for m in algo.models.values():
+        m.load_state_dict(seeded_state_dict(m, seed=G.STEP_SEED))
+    algo.set_train()
+    inputs = synth.make_batch(cfg, seed=G.FULL_SEED, with_depth=True)
+    t = cfg['training']
+    noise = torch.stack(G.full_noise(fx, (t['batch_size'], len(t['frame_ids']) - 1, t['height'], t['width'])))
+    outputs, losses = algo.process_batch(inputs, device.index, noise=noise.to(device))
+    losses['total_loss'].backward()
+    torch.cuda.synchronize()
+    s, N = G.FULL_SUB, cfg['data']['num_cams']
+    dd = [(outputs[('cam', c)][('depth', 0)][..., ::s, ::s].cpu().double(), torch.tensor(fx[f'depth_sub_c{c}']).double())
+          for c in range(N)]
+    d_depth = max(float((a - b).abs().max()) for a, b in dd)
+    within = all(bool(((a - b).abs() <= 1e-4 + 1e-4 * b.abs()).all()) for a, b in dd)
+    d_loss = {k[5:]: abs(float(losses[k[5:]]) - float(fx[k])) for k in fx.files if k.startswith('loss_')}
+    within = within and all(v <= 1e-4 + 1e-4 * abs(float(fx['loss_' + k])) for k, v in d_loss.items())
+    return {'config': '6-cam 384x640, voxels 100x100x20, D=50 (config 2) vs the reference\'s CPU step',
+            'max_abs_diff_depth': d_depth, 'max_abs_diff_loss': max(d_loss.values()), 'loss_keys': len(d_loss),
+            'within_1e-4': within}
 
 
 def load_traffic(config):

@@ -173,6 +173,34 @@ def depth_metric_case():
 # ------------------------------------------------------------------------------------ full step
 STEP_SEED = 7
 
+# ------------------------------------------------------------------------------------ full resolution
+# config 2 of BASELINE.json (6-cam DDAD 384x640, B=1, 100x100x20 voxels, D=50, fp32): the headline
+# shape, pinned against the reference's own CPU step (tests/golden/step_full.npz)
+FULL_SEED = 15            # synth.make_batch seed of the inputs
+FULL_NOISE_SEED = 1234    # the reference step's torch.manual_seed before its identity-noise draws
+FULL_SUB = 4              # depth maps stored at every FULL_SUB-th pixel (plus full-map checksums)
+
+
+def full_cfg():
+    return C.surround_fusion_cfg(batch_size=1)
+
+
+def full_noise(fx, shape, n_cams=6):
+    """The identity-loss noise of the full-resolution fixture, rebuilt bit-identically: the
+    reference's raw torch.randn draws (one [B, T, H, W] block per camera, in camera order, from a
+    CPU generator seeded FULL_NOISE_SEED, checked against the stored checksums) plus the sparse
+    tie-breaking nudges of gen_golden._untie_noise, times the reference's 1e-5."""
+    gen = torch.Generator().manual_seed(FULL_NOISE_SEED)
+    out = []
+    for c in range(n_cams):
+        raw = torch.randn(tuple(shape), generator=gen)
+        np.testing.assert_allclose(checksum(raw), fx[f'cs_noise_raw_c{c}'], rtol=1e-12)   # host SIMD: last bit
+        flat = raw.flatten().clone()
+        idx = torch.from_numpy(fx[f'noise_idx_c{c}'].astype(np.int64))
+        flat[idx] += torch.from_numpy(fx[f'noise_add_c{c}'])
+        out.append(flat.view(raw.shape) * 1e-5)
+    return out
+
 
 def step_cfg():
     return C.surround_fusion_cfg(height=96, width=160, batch_size=1, voxel_size=[40, 40, 10],

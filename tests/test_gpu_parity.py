@@ -452,6 +452,51 @@ def test_full_step_against_reference(which):
         assert rel < 1e-2, f'{key}: gradient rel diff {rel:.3g} vs the reference'
 
 
+def test_full_resolution_step_against_reference():
+    """BASELINE config 2's full shape (6 x 384 x 640, 100 x 100 x 20 voxels, D = 50, fp32) against
+    the reference's own CPU step there (tests/golden/step_full.npz, same seeded weights, inputs
+    and identity noise): every loss scalar, the 12 poses, the depth maps at every 4th pixel at
+    the north_star tolerance (1e-4 abs + 1e-4 rel per pixel) and their full-map checksums; the
+    small parameter gradients within the end-to-end sanity bound of
+    test_full_step_against_reference (models/vfdepth.py:191-313)."""
+    from vfdepth_amd import synth
+    from vfdepth_amd.layers import seeded_state_dict
+    from vfdepth_amd.vfdepth import VFDepthAlgo
+    fx = golden('step_full.npz')
+    cfg = G.full_cfg()
+    algo = VFDepthAlgo(cfg, 0)
+    for m in algo.models.values():
+        m.load_state_dict(seeded_state_dict(m, seed=G.STEP_SEED))
+    algo.set_train()
+    inputs = synth.make_batch(cfg, seed=G.FULL_SEED, with_depth=True)
+    # full-size double sums: the host's SIMD width changes the last bit (inputs drift would be gross)
+    np.testing.assert_allclose(G.checksum(inputs[('color', 0, 0)]), fx['cs_color'], rtol=1e-12)
+    t = cfg['training']
+    noise = torch.stack(G.full_noise(fx, (t['batch_size'], len(t['frame_ids']) - 1, t['height'], t['width']))).to(DEV)
+    outputs, losses = algo.process_batch(inputs, 0, noise=noise)
+    losses['total_loss'].backward()
+    torch.cuda.synchronize()
+    for k in [k for k in fx.files if k.startswith('loss_')]:
+        close(losses[k[5:]], fx[k], k)
+    s = G.FULL_SUB
+    for c in range(cfg['data']['num_cams']):
+        d = outputs[('cam', c)][('depth', 0)]
+        close(d[..., ::s, ::s], fx[f'depth_sub_c{c}'], f'depth cam {c} (every {s}th pixel)')
+        cs, ref = G.checksum(d.cpu()), fx[f'cs_depth_c{c}']
+        assert abs(cs[0] - ref[0]) <= 1e-5 * abs(ref[0]) and abs(cs[1] - ref[1]) <= 1e-5 * abs(ref[1]), \
+            f'depth cam {c}: full-map checksum {cs[:2]} vs reference {ref[:2]}'
+        for f in cfg['training']['frame_ids'][1:]:
+            close(outputs[('cam', c)][('cam_T_cam', 0, f)], fx[f'cam_T_cam_{f}_c{c}'], f'T{f} cam {c}', atol=1e-5)
+    named = {}
+    for mname, m in algo.models.items():
+        for pname, p in m.named_parameters():
+            named[f'{mname}.{pname}'] = p
+    for key in [k for k in fx.files if k.startswith('grad__')]:
+        a, b = named[key[6:]].grad.detach().double().cpu(), torch.tensor(fx[key]).double()
+        rel = float((a - b).norm() / b.norm())
+        assert rel < 1e-2, f'{key}: gradient rel diff {rel:.3g} vs the reference (full resolution)'
+
+
 def test_step_depth_metrics_against_reference_logger():
     """A24 on the GPU: the fusion step's depth maps scored by `compute_depth_metrics` (all 7
     metrics, plain and median-scaled; reference utils/logger.py:193-247 + utils/misc.py:85-98)

@@ -197,3 +197,36 @@ def test_step_oracle(aug):
             for j, (d, m) in enumerate(zip(o[('tform_depth', 0)], o[('tform_depth_mask', 0)])):
                 close_most(d, fx[f'tform_depth_c{c}_{j}'], what=f'tform depth cam {c} src {j}')
                 close(m, fx[f'tform_mask_c{c}_{j}'], rtol=0, atol=0, what=f'tform mask cam {c} src {j}')
+
+
+def test_step_oracle_full_resolution():
+    """The oracle's whole step at BASELINE config 2's full shape (6 x 384 x 640, 100 x 100 x 20
+    voxels, D = 50) against the reference's own CPU step there (tests/golden/step_full.npz):
+    every loss scalar, the 12 poses and the depth maps (every 4th pixel, plus full-map checksums)
+    at the north_star tolerance 1e-4 (models/vfdepth.py:191-313)."""
+    from vfdepth_amd import synth
+    from vfdepth_amd.layers import seeded_state_dict
+    from vfdepth_amd.network import FusedDepthNet, FusedPoseNet
+    torch.set_num_threads(8)
+    fx = golden('step_full.npz')
+    cfg = G.full_cfg()
+    inputs = synth.make_batch(cfg, seed=G.FULL_SEED, with_depth=True)
+    # full-size double sums: the host's SIMD width changes the last bit (inputs drift would be gross)
+    np.testing.assert_allclose(G.checksum(inputs[('color', 0, 0)]), fx['cs_color'], rtol=1e-12)
+    t = cfg['training']
+    noise = G.full_noise(fx, (t['batch_size'], len(t['frame_ids']) - 1, t['height'], t['width']))
+    dn, pn = FusedDepthNet(cfg), FusedPoseNet(cfg)
+    dn.load_state_dict(seeded_state_dict(dn, seed=G.STEP_SEED))
+    pn.load_state_dict(seeded_state_dict(pn, seed=G.STEP_SEED))
+    with torch.no_grad():
+        out, losses = O.process_batch(O.nets_from_modules(dn, pn), inputs, cfg, noise)
+    for k in [k for k in fx.files if k.startswith('loss_')]:
+        close(losses[k[5:]], fx[k], what=k)
+    s = G.FULL_SUB
+    for c in range(6):
+        d = out[('cam', c)][('depth', 0)]
+        close(d[..., ::s, ::s], fx[f'depth_sub_c{c}'], what=f'depth cam {c}')
+        cs = G.checksum(d)
+        close(cs[:2], fx[f'cs_depth_c{c}'][:2], rtol=1e-5, atol=0, what=f'depth checksum cam {c}')
+        for f in cfg['training']['frame_ids'][1:]:
+            close(out[('cam', c)][('cam_T_cam', 0, f)], fx[f'cam_T_cam_{f}_c{c}'], what=f'T{f} cam {c}')

@@ -191,6 +191,13 @@ typedef struct vfd_bn_desc {
                             3's bf16 encoders, whose MIOpen convs then skip their NCHW<->NHWC
                             transposes.  The apply passes then take reduced sums only (ns = 1: call
                             vfd_bn_sum first); the one-launch bn1 kernels do not apply (fits = 0). */
+  int32_t groups;        /* 0 / 1: one batch.  G > 1: the maps hold G consecutive batches of N images
+                            each (N is the per-group count), normalised with their own statistics —
+                            G separate train-mode calls of the layer in one launch (the pose net's two
+                            frame pairs, models/geometry/pose.py:33-42).  partial [G][C][S][2], sums
+                            [G][C+1][2] (one all-reduce for SyncBatchNorm), mean / invstd [G][C];
+                            running statistics updated G times in group order, num_batches_tracked
+                            += G; d gamma / d beta summed over the groups (fp32, group order). */
 } vfd_bn_desc;
 
 int vfd_bn_splits(const vfd_bn_desc* d);

@@ -35,10 +35,10 @@ def test_descriptor_layouts_match_c(tmp_path):
     from vfdepth_amd import _lib
     src = tmp_path / 'sz.c'
     src.write_text('#include "vfd_capi.h"\n#include <stdio.h>\n#include <stddef.h>\n'
-                   'int main(){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(vfd_voxel_desc), sizeof(vfd_view_desc),'
+                   'int main(){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(vfd_voxel_desc), sizeof(vfd_view_desc),'
                    ' sizeof(vfd_photo_desc), offsetof(vfd_voxel_desc, axis_x), offsetof(vfd_view_desc, color),'
                    ' offsetof(vfd_photo_desc, ident), sizeof(vfd_depthsyn_desc), offsetof(vfd_depthsyn_desc, src_tab),'
-                   ' sizeof(vfd_bn_desc), offsetof(vfd_bn_desc, dtype));'
+                   ' sizeof(vfd_bn_desc), offsetof(vfd_bn_desc, dtype), offsetof(vfd_bn_desc, groups));'
                    'return 0;}\n')
     exe = tmp_path / 'sz'
     subprocess.check_call(['gcc', '-I', os.path.dirname(HEADER), str(src), '-o', str(exe)])
@@ -46,7 +46,7 @@ def test_descriptor_layouts_match_c(tmp_path):
     want = [ctypes.sizeof(_lib.VoxelDesc), ctypes.sizeof(_lib.ViewDesc), ctypes.sizeof(_lib.PhotoDesc),
             _lib.VoxelDesc.axis_x.offset, _lib.ViewDesc.color.offset, _lib.PhotoDesc.ident.offset,
             ctypes.sizeof(_lib.DepthSynDesc), _lib.DepthSynDesc.src_tab.offset,
-            ctypes.sizeof(_lib.BnDesc), _lib.BnDesc.dtype.offset]
+            ctypes.sizeof(_lib.BnDesc), _lib.BnDesc.dtype.offset, _lib.BnDesc.groups.offset]
     assert got == want
 
 

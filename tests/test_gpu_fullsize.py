@@ -902,6 +902,65 @@ def test_batchnorm_act_matches_torch(shape, res, relu):
         gclose(ra.grad, rr.grad, 'BN d residual', rel=1e-6)
 
 
+@pytest.mark.parametrize('shape,res,relu,layout', [((12, 64, 96, 160), True, True, 'nchw'),      # split path
+                                                   ((12, 256, 24, 40), True, True, 'nchw'),      # one-launch path
+                                                   ((12, 512, 12, 20), False, False, 'nchw'),
+                                                   ((6, 8, 5, 7), True, True, 'nchw'),           # HW % 4 != 0
+                                                   ((12, 64, 96, 160), True, True, 'nhwc_bf16'),
+                                                   ((12, 512, 12, 20), False, False, 'nhwc_bf16'),
+                                                   ((6, 16, 5, 7), True, True, 'nhwc')])
+def test_batchnorm_act_groups_equal_separate_calls(shape, res, relu, layout):
+    """vfd_bn_desc.groups (the pose net's two frame pairs as one batch, models/geometry/pose.py:33-42):
+    the grouped launch equals two separate calls of the fused BN on the halves BIT FOR BIT — output,
+    ReLU decisions, running statistics (updated twice, in order), num_batches_tracked (+2), d input,
+    d residual — and d gamma / d beta equal the two calls' gradients summed (autograd's accumulation);
+    and it matches nn.BatchNorm2d.train() called on each half."""
+    import copy
+    from vfdepth_amd.layers import bn_act, bn_groups
+    gen = torch.Generator(device=DEV).manual_seed(93)
+    bf16 = layout == 'nhwc_bf16'
+    dt = torch.bfloat16 if bf16 else torch.float32
+    fmt = torch.contiguous_format if layout == 'nchw' else torch.channels_last
+    x = (2.0 * torch.randn(shape, device=DEV, generator=gen) + 0.5).to(dt).contiguous(memory_format=fmt)
+    r = torch.randn(shape, device=DEV, generator=gen).to(dt).contiguous(memory_format=fmt) if res else None
+    C, half = shape[1], shape[0] // 2
+    bn = torch.nn.BatchNorm2d(C).to(DEV).train()
+    with torch.no_grad():
+        bn.weight.copy_(1 + 0.1 * torch.randn(C, device=DEV, generator=gen))
+        bn.bias.copy_(0.1 * torch.randn(C, device=DEV, generator=gen))
+        bn.running_mean.copy_(0.2 * torch.randn(C, device=DEV, generator=gen))
+    bn_sep, bn_ref = copy.deepcopy(bn), copy.deepcopy(bn)
+    g = torch.randn(shape, device=DEV, generator=gen).to(dt).contiguous(memory_format=fmt)
+    with torch.autocast(device_type='cuda', dtype=torch.bfloat16, enabled=bf16):
+        xa = x.clone().requires_grad_(True)
+        ra = r.clone().requires_grad_(True) if res else None
+        with bn_groups(2):
+            y = bn_act(bn, xa, ra, relu)
+        assert 'BatchNormAct' in type(y.grad_fn).__name__
+        (y.float() * g.float()).sum().backward()
+        xs = [x[:half].clone().requires_grad_(True), x[half:].clone().requires_grad_(True)]
+        rs = [r[:half].clone().requires_grad_(True), r[half:].clone().requires_grad_(True)] if res else [None, None]
+        ys = [bn_act(bn_sep, xs[k].contiguous(memory_format=fmt), rs[k], relu) for k in range(2)]
+        sum((ys[k].float() * g[k * half:(k + 1) * half].float()).sum() for k in range(2)).backward()
+    assert torch.equal(y, torch.cat(ys)), 'grouped BN output differs from two calls'
+    assert torch.equal(bn.running_mean, bn_sep.running_mean) and torch.equal(bn.running_var, bn_sep.running_var)
+    assert int(bn.num_batches_tracked) == int(bn_sep.num_batches_tracked) == 2
+    assert torch.equal(xa.grad, torch.cat([t.grad for t in xs])), 'grouped BN d input differs'
+    if res:
+        assert torch.equal(ra.grad, torch.cat([t.grad for t in rs])), 'grouped BN d residual differs'
+    assert torch.equal(bn.weight.grad, bn_sep.weight.grad) and torch.equal(bn.bias.grad, bn_sep.bias.grad)
+    # and the module semantics: nn.BatchNorm2d.train() once per half
+    yr = torch.cat([bn_ref(x[k * half:(k + 1) * half].float()) for k in range(2)])
+    if res:
+        yr = yr + r.float()
+    if relu:
+        yr = torch.relu(yr)
+    tol = dict(atol=1e-5, rtol=2.0 ** -8) if bf16 else dict(atol=2e-5, rtol=2e-5)
+    close(y.float(), yr, f'grouped BN output {shape} {layout}', **tol)
+    close(bn.running_mean, bn_ref.running_mean, 'running_mean', atol=1e-6, rtol=1e-5)
+    close(bn.running_var, bn_ref.running_var, 'running_var', atol=1e-6, rtol=1e-5)
+
+
 @pytest.mark.parametrize('shape,res,relu', [((6, 64, 96, 160), True, True), ((6, 256, 24, 40), True, True),
                                             ((6, 512, 12, 20), False, False), ((3, 8, 5, 7), True, True)])
 def test_batchnorm_act_bf16(shape, res, relu):

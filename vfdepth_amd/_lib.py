@@ -49,7 +49,7 @@ class ConvDesc(ctypes.Structure):
 class BnDesc(ctypes.Structure):
     _fields_ = [('N', c_int), ('C', c_int), ('HW', c_int), ('S', c_int), ('relu', c_int),
                 ('eps', c_float), ('momentum', c_float), ('dtype', c_int), ('g2', c_void_p), ('m2', c_void_p),
-                ('nhwc', c_int)]
+                ('nhwc', c_int), ('groups', c_int)]
 
 
 _SIGS = {

@@ -13,6 +13,14 @@
 //
 // Work split: a channel's N*HW elements (N images of HW contiguous floats) are cut into S
 // equal float4-aligned ranges; block (split, channel) of every kernel owns one range.
+//
+// Groups (d.groups = G > 1): the tensors hold G consecutive batches of N images, each normalised
+// with its OWN statistics — what G separate train-mode calls of the layer compute (the pose net's
+// two frame-pair calls of a step run as one batch this way, fusion_posenet.py:42-72 /
+// models/geometry/pose.py:33-42).  Block z = group; partials [G][C][S][2], reduced sums
+// [G][C+1][2], mean / invstd [G][C]; the running statistics are updated G times in group order and
+// num_batches_tracked grows by G (as after G calls); d gamma / d beta are the groups' values summed
+// in fp32 in group order (autograd's accumulation over the calls).
 #include "vfd_common.h"
 
 namespace vfd {
@@ -39,6 +47,18 @@ __device__ __forceinline__ size_t bn_off(const vfd_bn_desc& d, int c, unsigned e
   return ((size_t)n * d.C + c) * d.HW + (e - n * (unsigned)d.HW);
 }
 
+__device__ __forceinline__ int bn_groups(const vfd_bn_desc& d) { return d.groups > 1 ? d.groups : 1; }
+// elements of one group (N images)
+__device__ __forceinline__ size_t bn_gsz(const vfd_bn_desc& d) { return (size_t)d.N * d.C * d.HW; }
+
+// the running-statistics update of nn.BatchNorm2d.train() from one group's mean / biased variance
+__device__ __forceinline__ void bn_running(const vfd_bn_desc& d, int c, double count, double mean_d, double var_d,
+                                           float* __restrict__ run_mean, float* __restrict__ run_var) {
+  const double unbiased = count > 1.0 ? var_d * count / (count - 1.0) : var_d;
+  run_mean[c] = (float)((1.0 - d.momentum) * run_mean[c] + d.momentum * mean_d);
+  run_var[c] = (float)((1.0 - d.momentum) * run_var[c] + d.momentum * unbiased);
+}
+
 __device__ __forceinline__ double block_sum(double v, double* sh) {
   v = wave_sum(v);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -52,12 +72,12 @@ __device__ __forceinline__ double block_sum(double v, double* sh) {
 
 // Visit every element of a range: f(offset_of_float4, 4 values) with float4 loads when HW % 4 == 0.
 template <typename F>
-__device__ __forceinline__ void bn_visit(const vfd_bn_desc& d, int c, BnRange r, F&& f) {
+__device__ __forceinline__ void bn_visit(const vfd_bn_desc& d, int c, BnRange r, size_t gb, F&& f) {
   if ((d.HW & 3) == 0) {
 #pragma unroll 2
-    for (unsigned e = r.lo + 4 * threadIdx.x; e < r.hi; e += 4 * BN_THREADS) f(bn_off(d, c, e), 4);
+    for (unsigned e = r.lo + 4 * threadIdx.x; e < r.hi; e += 4 * BN_THREADS) f(gb + bn_off(d, c, e), 4);
   } else {
-    for (unsigned e = r.lo + threadIdx.x; e < r.hi; e += BN_THREADS) f(bn_off(d, c, e), 1);
+    for (unsigned e = r.lo + threadIdx.x; e < r.hi; e += BN_THREADS) f(gb + bn_off(d, c, e), 1);
   }
 }
 
@@ -123,9 +143,9 @@ template <typename T>
 __global__ __launch_bounds__(BN_THREADS) void bn_stats_k(vfd_bn_desc d, const T* __restrict__ x,
                                                          double* __restrict__ partial) {
   __shared__ double sh[BN_THREADS / 64];
-  const int c = blockIdx.y, split = blockIdx.x;
+  const int c = blockIdx.y, split = blockIdx.x, grp = blockIdx.z;
   double s1 = 0.0, s2 = 0.0;
-  bn_visit(d, c, bn_range(d, split), [&](size_t o, int n) {
+  bn_visit(d, c, bn_range(d, split), grp * bn_gsz(d), [&](size_t o, int n) {
     if (n == 4) {
       const float4 v = ld4(x + o);
       const double a = v.x, b = v.y, e = v.z, f = v.w;
@@ -140,8 +160,8 @@ __global__ __launch_bounds__(BN_THREADS) void bn_stats_k(vfd_bn_desc d, const T*
   s1 = block_sum(s1, sh);
   s2 = block_sum(s2, sh);
   if (threadIdx.x == 0) {
-    partial[((size_t)c * d.S + split) * 2] = s1;
-    partial[((size_t)c * d.S + split) * 2 + 1] = s2;
+    partial[(((size_t)grp * d.C + c) * d.S + split) * 2] = s1;
+    partial[(((size_t)grp * d.C + c) * d.S + split) * 2 + 1] = s2;
   }
 }
 
@@ -153,20 +173,30 @@ __global__ __launch_bounds__(BN_THREADS) void bn_stats_k(vfd_bn_desc d, const T*
 __global__ void bn_sum_k(vfd_bn_desc d, const double* __restrict__ partial, double count, double* __restrict__ sums,
                          const float* __restrict__ invstd, float* __restrict__ dgamma, float* __restrict__ dbeta) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int G = bn_groups(d);
+  const size_t sst = (size_t)(d.C + 1) * 2;          // one group's reduced sums
   if (c == d.C && count > 0.0) {
-    sums[c * 2] = count;
-    sums[c * 2 + 1] = 0.0;
+    for (int k = 0; k < G; ++k) {
+      sums[k * sst + c * 2] = count;
+      sums[k * sst + c * 2 + 1] = 0.0;
+    }
   }
   if (c >= d.C) return;
-  double a = 0.0, b = 0.0;
-  for (int s = 0; s < d.S; ++s) {
-    a += partial[((size_t)c * d.S + s) * 2];
-    b += partial[((size_t)c * d.S + s) * 2 + 1];
+  float dg = 0.f, db = 0.f;
+  for (int k = 0; k < G; ++k) {
+    const double* pk = partial + (size_t)k * d.C * d.S * 2;
+    double a = 0.0, b = 0.0;
+    for (int s = 0; s < d.S; ++s) {
+      a += pk[((size_t)c * d.S + s) * 2];
+      b += pk[((size_t)c * d.S + s) * 2 + 1];
+    }
+    sums[k * sst + c * 2] = a;
+    sums[k * sst + c * 2 + 1] = b;
+    if (dgamma) dg += (float)(b * invstd[(size_t)k * d.C + c]);
+    if (dbeta) db += (float)a;
   }
-  sums[c * 2] = a;
-  sums[c * 2 + 1] = b;
-  if (dgamma) dgamma[c] = (float)(b * invstd[c]);
-  if (dbeta) dbeta[c] = (float)a;
+  if (dgamma) dgamma[c] = dg;
+  if (dbeta) dbeta[c] = db;
 }
 
 // per-channel sums of the block's channel: from the S partials, or (ns == 1) already reduced
@@ -195,29 +225,38 @@ __global__ __launch_bounds__(BN_THREADS) void bn_apply_k(vfd_bn_desc d, const T*
                                                          float* __restrict__ mean_out, float* __restrict__ invstd_out,
                                                          float* __restrict__ run_mean, float* __restrict__ run_var,
                                                          long long* __restrict__ nbt, unsigned char* __restrict__ mk) {
-  const int c = blockIdx.y, split = blockIdx.x;
-  if (nbt && c == 0 && split == 0 && threadIdx.x == 0) nbt[0] += 1;   // num_batches_tracked
-  if (count <= 0.0) count = sums[2 * d.C];                          // all-reduced count row (ns == 1)
+  const int c = blockIdx.y, split = blockIdx.x, grp = blockIdx.z, G = bn_groups(d);
+  if (nbt && c == 0 && split == 0 && grp == 0 && threadIdx.x == 0) nbt[0] += G;   // num_batches_tracked
+  const size_t sst = ns == 1 ? (size_t)(d.C + 1) * 2 : (size_t)d.C * d.S * 2;   // one group's sums
+  const double cnt = count > 0.0 ? count : sums[grp * sst + 2 * d.C];   // all-reduced count row (ns == 1)
   double s1, s2;
-  bn_channel_sums(sums, ns, c, &s1, &s2);
-  const double mean_d = s1 / count;
-  double var_d = s2 / count - mean_d * mean_d;
+  bn_channel_sums(sums + grp * sst, ns, c, &s1, &s2);
+  const double mean_d = s1 / cnt;
+  double var_d = s2 / cnt - mean_d * mean_d;
   var_d = var_d > 0.0 ? var_d : 0.0;
   const float mean = (float)mean_d;
   const float invstd = (float)(1.0 / sqrt(var_d + (double)d.eps));
   if (split == 0 && threadIdx.x == 0) {
-    mean_out[c] = mean;
-    invstd_out[c] = invstd;
-    if (run_mean) {
-      const double unbiased = count > 1.0 ? var_d * count / (count - 1.0) : var_d;
-      run_mean[c] = (float)((1.0 - d.momentum) * run_mean[c] + d.momentum * mean_d);
-      run_var[c] = (float)((1.0 - d.momentum) * run_var[c] + d.momentum * unbiased);
+    mean_out[(size_t)grp * d.C + c] = mean;
+    invstd_out[(size_t)grp * d.C + c] = invstd;
+  }
+  if (run_mean && split == 0 && grp == 0) {      // block-uniform: the groups' updates in order
+    for (int k = 0; k < G; ++k) {
+      double a = s1, b = s2, ck = cnt;
+      if (k > 0) {
+        ck = count > 0.0 ? count : sums[k * sst + 2 * d.C];
+        bn_channel_sums(sums + k * sst, ns, c, &a, &b);
+      }
+      const double mk_d = a / ck;
+      double vk = b / ck - mk_d * mk_d;
+      vk = vk > 0.0 ? vk : 0.0;
+      if (threadIdx.x == 0) bn_running(d, c, ck, mk_d, vk, run_mean, run_var);
     }
   }
   const float sc = invstd * gamma[c];
   const float sh = beta[c] - mean * sc;
   const bool relu = d.relu != 0;
-  bn_visit(d, c, bn_range(d, split), [&](size_t o, int n) {
+  bn_visit(d, c, bn_range(d, split), grp * bn_gsz(d), [&](size_t o, int n) {
     if (n == 4) {
       float4 v = ld4(x + o);
       v.x = v.x * sc + sh;
@@ -256,11 +295,11 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_stats_k(vfd_bn_desc d, cons
                                                              const float* __restrict__ mean_in,
                                                              double* __restrict__ partial) {
   __shared__ double sh[BN_THREADS / 64];
-  const int c = blockIdx.y, split = blockIdx.x;
-  const float mean = mean_in[c];
+  const int c = blockIdx.y, split = blockIdx.x, grp = blockIdx.z;
+  const float mean = mean_in[(size_t)grp * d.C + c];
   const bool relu = d.relu != 0;
   double s1 = 0.0, s2 = 0.0;
-  bn_visit(d, c, bn_range(d, split), [&](size_t o, int n) {
+  bn_visit(d, c, bn_range(d, split), grp * bn_gsz(d), [&](size_t o, int n) {
     if (n == 4) {
       float4 gv = bn_g4(d, g, o);
       const float4 xv = ld4(x + o);
@@ -278,8 +317,8 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_stats_k(vfd_bn_desc d, cons
   s1 = block_sum(s1, sh);
   s2 = block_sum(s2, sh);
   if (threadIdx.x == 0) {
-    partial[((size_t)c * d.S + split) * 2] = s1;
-    partial[((size_t)c * d.S + split) * 2 + 1] = s2;
+    partial[(((size_t)grp * d.C + c) * d.S + split) * 2] = s1;
+    partial[(((size_t)grp * d.C + c) * d.S + split) * 2 + 1] = s2;
   }
 }
 
@@ -294,20 +333,30 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply_k(vfd_bn_desc d, cons
                                                              const float* __restrict__ invstd_in,
                                                              T* __restrict__ dx, T* __restrict__ dr,
                                                              float* __restrict__ dgamma, float* __restrict__ dbeta) {
-  const int c = blockIdx.y, split = blockIdx.x;
-  if (count <= 0.0) count = sums[2 * d.C];                          // all-reduced count row (ns == 1)
+  const int c = blockIdx.y, split = blockIdx.x, grp = blockIdx.z, G = bn_groups(d);
+  const size_t sst = ns == 1 ? (size_t)(d.C + 1) * 2 : (size_t)d.C * d.S * 2;   // one group's sums
+  const double cnt = count > 0.0 ? count : sums[grp * sst + 2 * d.C];   // all-reduced count row (ns == 1)
   double sg, sgx;
-  bn_channel_sums(sums, ns, c, &sg, &sgx);
-  const float mean = mean_in[c], invstd = invstd_in[c];
-  if (split == 0 && threadIdx.x == 0) {
-    if (dgamma) dgamma[c] = (float)(sgx * invstd);
-    if (dbeta) dbeta[c] = (float)sg;
+  bn_channel_sums(sums + grp * sst, ns, c, &sg, &sgx);
+  const float mean = mean_in[(size_t)grp * d.C + c], invstd = invstd_in[(size_t)grp * d.C + c];
+  if (split == 0 && grp == 0 && (dgamma || dbeta)) {   // block-uniform: the groups' values, fp32, in order
+    float dg = 0.f, db = 0.f;
+    for (int k = 0; k < G; ++k) {
+      double a = sg, b = sgx;
+      if (k > 0) bn_channel_sums(sums + k * sst, ns, c, &a, &b);
+      dg += (float)(b * invstd_in[(size_t)k * d.C + c]);
+      db += (float)a;
+    }
+    if (threadIdx.x == 0) {
+      if (dgamma) dgamma[c] = dg;
+      if (dbeta) dbeta[c] = db;
+    }
   }
   const float k = gamma[c] * invstd;
-  const float mg = (float)(sg / count);
-  const float mx = (float)(sgx / count) * invstd * invstd;
+  const float mg = (float)(sg / cnt);
+  const float mx = (float)(sgx / cnt) * invstd * invstd;
   const bool relu = d.relu != 0;
-  bn_visit(d, c, bn_range(d, split), [&](size_t o, int n) {
+  bn_visit(d, c, bn_range(d, split), grp * bn_gsz(d), [&](size_t o, int n) {
     if (n == 4) {
       float4 gv = bn_g4(d, g, o);
       const float4 xv = ld4(x + o);
@@ -354,12 +403,12 @@ __device__ __forceinline__ double block_sum1(double v, double* sh) {
 }
 
 template <typename F>
-__device__ __forceinline__ void bn1_visit(const vfd_bn_desc& d, int c, F&& f) {
+__device__ __forceinline__ void bn1_visit(const vfd_bn_desc& d, int c, size_t gb, F&& f) {
   const unsigned total = (unsigned)d.N * (unsigned)d.HW;
   if ((d.HW & 3) == 0) {
-    for (unsigned e = 4 * threadIdx.x; e < total; e += 4 * BN1_THREADS) f(bn_off(d, c, e), 4);
+    for (unsigned e = 4 * threadIdx.x; e < total; e += 4 * BN1_THREADS) f(gb + bn_off(d, c, e), 4);
   } else {
-    for (unsigned e = threadIdx.x; e < total; e += BN1_THREADS) f(bn_off(d, c, e), 1);
+    for (unsigned e = threadIdx.x; e < total; e += BN1_THREADS) f(gb + bn_off(d, c, e), 1);
   }
 }
 
@@ -371,10 +420,12 @@ __global__ __launch_bounds__(BN1_THREADS) void bn1_fwd_k(vfd_bn_desc d, const T*
                                                          float* __restrict__ run_mean, float* __restrict__ run_var,
                                                          long long* __restrict__ nbt, unsigned char* __restrict__ mk) {
   __shared__ double sh[BN1_THREADS / 64];
-  const int c = blockIdx.x;
-  if (nbt && c == 0 && threadIdx.x == 0) nbt[0] += 1;
+  const int c = blockIdx.x, G = bn_groups(d);
+  if (nbt && c == 0 && threadIdx.x == 0) nbt[0] += G;
+  for (int grp = 0; grp < G; ++grp) {          // the groups in order (running statistics)
+  const size_t gb = grp * bn_gsz(d);
   double s1 = 0.0, s2 = 0.0;
-  bn1_visit(d, c, [&](size_t o, int n) {
+  bn1_visit(d, c, gb, [&](size_t o, int n) {
     if (n == 4) {
       const float4 v = ld4(x + o);
       const double a = v.x, b = v.y, e = v.z, f = v.w;
@@ -395,18 +446,14 @@ __global__ __launch_bounds__(BN1_THREADS) void bn1_fwd_k(vfd_bn_desc d, const T*
   const float mean = (float)mean_d;
   const float invstd = (float)(1.0 / sqrt(var_d + (double)d.eps));
   if (threadIdx.x == 0) {
-    mean_out[c] = mean;
-    invstd_out[c] = invstd;
-    if (run_mean) {
-      const double unbiased = count > 1.0 ? var_d * count / (count - 1.0) : var_d;
-      run_mean[c] = (float)((1.0 - d.momentum) * run_mean[c] + d.momentum * mean_d);
-      run_var[c] = (float)((1.0 - d.momentum) * run_var[c] + d.momentum * unbiased);
-    }
+    mean_out[(size_t)grp * d.C + c] = mean;
+    invstd_out[(size_t)grp * d.C + c] = invstd;
+    if (run_mean) bn_running(d, c, count, mean_d, var_d, run_mean, run_var);
   }
   const float sc = invstd * gamma[c];
   const float shf = beta[c] - mean * sc;
   const bool relu = d.relu != 0;
-  bn1_visit(d, c, [&](size_t o, int n) {
+  bn1_visit(d, c, gb, [&](size_t o, int n) {
     if (n == 4) {
       float4 v = ld4(x + o);
       v.x = v.x * sc + shf;
@@ -436,6 +483,7 @@ __global__ __launch_bounds__(BN1_THREADS) void bn1_fwd_k(vfd_bn_desc d, const T*
       if (mk) mk[o] = v > 0.f;
     }
   });
+  }
 }
 
 template <typename T>
@@ -447,11 +495,14 @@ __global__ __launch_bounds__(BN1_THREADS) void bn1_bwd_k(vfd_bn_desc d, const T*
                                                          T* __restrict__ dr, float* __restrict__ dgamma,
                                                          float* __restrict__ dbeta) {
   __shared__ double sh[BN1_THREADS / 64];
-  const int c = blockIdx.x;
-  const float mean = mean_in[c], invstd = invstd_in[c];
+  const int c = blockIdx.x, G = bn_groups(d);
   const bool relu = d.relu != 0;
+  float dg = 0.f, db = 0.f;
+  for (int grp = 0; grp < G; ++grp) {
+  const size_t gb = grp * bn_gsz(d);
+  const float mean = mean_in[(size_t)grp * d.C + c], invstd = invstd_in[(size_t)grp * d.C + c];
   double s1 = 0.0, s2 = 0.0;
-  bn1_visit(d, c, [&](size_t o, int n) {
+  bn1_visit(d, c, gb, [&](size_t o, int n) {
     if (n == 4) {
       float4 gv = bn_g4(d, g, o);
       const float4 xv = ld4(x + o);
@@ -467,15 +518,13 @@ __global__ __launch_bounds__(BN1_THREADS) void bn1_bwd_k(vfd_bn_desc d, const T*
     }
   });
   const double sg = block_sum1(s1, sh), sgx = block_sum1(s2, sh);
-  if (threadIdx.x == 0) {
-    if (dgamma) dgamma[c] = (float)(sgx * invstd);
-    if (dbeta) dbeta[c] = (float)sg;
-  }
+  dg += (float)(sgx * invstd);
+  db += (float)sg;
   const double count = (double)d.N * d.HW;
   const float k = gamma[c] * invstd;
   const float mg = (float)(sg / count);
   const float mx = (float)(sgx / count) * invstd * invstd;
-  bn1_visit(d, c, [&](size_t o, int n) {
+  bn1_visit(d, c, gb, [&](size_t o, int n) {
     if (n == 4) {
       float4 gv = bn_g4(d, g, o);
       const float4 xv = ld4(x + o);
@@ -496,6 +545,11 @@ __global__ __launch_bounds__(BN1_THREADS) void bn1_bwd_k(vfd_bn_desc d, const T*
       if (dx) st1(dx + o, k * (gv - mg - (ld1(x + o) - mean) * mx));
     }
   });
+  }
+  if (threadIdx.x == 0) {
+    if (dgamma) dgamma[c] = dg;
+    if (dbeta) dbeta[c] = db;
+  }
 }
 
 // ---- channels-last (d.nhwc = 1): config 3's bf16 encoders keep their maps NHWC so MIOpen's
@@ -561,19 +615,20 @@ template <typename T>
 __global__ __launch_bounds__(BN_THREADS) void bn_stats_nhwc_k(vfd_bn_desc d, const T* __restrict__ x,
                                                               double* __restrict__ partial) {
   const NhGeom g = nh_geom(d);
-  const int q0 = threadIdx.x % g.QW, rs = threadIdx.x / g.QW;
+  const int q0 = threadIdx.x % g.QW, rs = threadIdx.x / g.QW, grp = blockIdx.y;
   const unsigned lo = blockIdx.x * g.chunk, hi = lo + g.chunk < g.rows ? lo + g.chunk : g.rows;
+  const size_t gb = grp * bn_gsz(d);
   double a[2][4] = {}, b[2][4] = {};
   for (unsigned r = lo + rs; r < hi; r += g.RP)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       if (j >= g.QT) break;
-      const float4 v = ld4(x + (size_t)r * d.C + 4 * (q0 + j * g.QW));
+      const float4 v = ld4(x + gb + (size_t)r * d.C + 4 * (q0 + j * g.QW));
       a[j][0] += v.x; a[j][1] += v.y; a[j][2] += v.z; a[j][3] += v.w;
       b[j][0] += (double)v.x * v.x; b[j][1] += (double)v.y * v.y;
       b[j][2] += (double)v.z * v.z; b[j][3] += (double)v.w * v.w;
     }
-  nh_store_partials(d, g, a, b, partial);
+  nh_store_partials(d, g, a, b, partial + (size_t)grp * d.C * d.S * 2);
 }
 
 template <typename T>
@@ -582,17 +637,19 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_stats_nhwc_k(vfd_bn_desc d,
                                                                   const float* __restrict__ mean_in,
                                                                   double* __restrict__ partial) {
   const NhGeom g = nh_geom(d);
-  const int q0 = threadIdx.x % g.QW, rs = threadIdx.x / g.QW;
+  const int q0 = threadIdx.x % g.QW, rs = threadIdx.x / g.QW, grp = blockIdx.y;
   const unsigned lo = blockIdx.x * g.chunk, hi = lo + g.chunk < g.rows ? lo + g.chunk : g.rows;
+  const size_t gb = grp * bn_gsz(d);
   float4 mu[2];
-  for (int j = 0; j < g.QT; ++j) mu[j] = *reinterpret_cast<const float4*>(mean_in + 4 * (q0 + j * g.QW));
+  for (int j = 0; j < g.QT; ++j)
+    mu[j] = *reinterpret_cast<const float4*>(mean_in + (size_t)grp * d.C + 4 * (q0 + j * g.QW));
   const bool relu = d.relu != 0;
   double a[2][4] = {}, b[2][4] = {};
   for (unsigned r = lo + rs; r < hi; r += g.RP)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       if (j >= g.QT) break;
-      const size_t o = (size_t)r * d.C + 4 * (q0 + j * g.QW);
+      const size_t o = gb + (size_t)r * d.C + 4 * (q0 + j * g.QW);
       float4 gv = bn_g4(d, gr, o);
       const float4 xv = ld4(x + o);
       if (relu) relu_mask4(d, y, o, gv);
@@ -602,7 +659,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_stats_nhwc_k(vfd_bn_desc d,
       b[j][2] += (double)gv.z * (double)(xv.z - mu[j].z);
       b[j][3] += (double)gv.w * (double)(xv.w - mu[j].w);
     }
-  nh_store_partials(d, g, a, b, partial);
+  nh_store_partials(d, g, a, b, partial + (size_t)grp * d.C * d.S * 2);
 }
 
 // sums[c] from the S partials by one block per channel (the NHWC path has hundreds of splits: a
@@ -611,21 +668,30 @@ __global__ __launch_bounds__(BN_THREADS) void bn_sum_blk_k(vfd_bn_desc d, const 
                                                            double count, double* __restrict__ sums,
                                                            const float* __restrict__ invstd,
                                                            float* __restrict__ dgamma, float* __restrict__ dbeta) {
-  const int c = blockIdx.x;
+  const int c = blockIdx.x, G = bn_groups(d);
+  const size_t sst = (size_t)(d.C + 1) * 2;          // one group's reduced sums
   if (c == d.C) {
-    if (count > 0.0 && threadIdx.x == 0) {
-      sums[c * 2] = count;
-      sums[c * 2 + 1] = 0.0;
-    }
+    if (count > 0.0 && threadIdx.x == 0)
+      for (int k = 0; k < G; ++k) {
+        sums[k * sst + c * 2] = count;
+        sums[k * sst + c * 2 + 1] = 0.0;
+      }
     return;
   }
-  double a, b;
-  bn_channel_sums(partial, d.S, c, &a, &b);
+  float dg = 0.f, db = 0.f;
+  for (int k = 0; k < G; ++k) {
+    double a, b;
+    bn_channel_sums(partial + (size_t)k * d.C * d.S * 2, d.S, c, &a, &b);
+    if (threadIdx.x == 0) {
+      sums[k * sst + c * 2] = a;
+      sums[k * sst + c * 2 + 1] = b;
+      if (dgamma) dg += (float)(b * invstd[(size_t)k * d.C + c]);
+      if (dbeta) db += (float)a;
+    }
+  }
   if (threadIdx.x == 0) {
-    sums[c * 2] = a;
-    sums[c * 2 + 1] = b;
-    if (dgamma) dgamma[c] = (float)(b * invstd[c]);
-    if (dbeta) dbeta[c] = (float)a;
+    if (dgamma) dgamma[c] = dg;
+    if (dbeta) dbeta[c] = db;
   }
 }
 
@@ -640,32 +706,40 @@ __global__ __launch_bounds__(BN_THREADS) void bn_apply_nhwc_k(vfd_bn_desc d, con
                                                               long long* __restrict__ nbt,
                                                               unsigned char* __restrict__ mk) {
   __shared__ float2 coef[NH_MAXC];
-  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] += 1;
-  if (count <= 0.0) count = sums[2 * d.C];
+  const int grp = blockIdx.y, G = bn_groups(d);
+  if (nbt && blockIdx.x == 0 && grp == 0 && threadIdx.x == 0) nbt[0] += G;
+  const size_t sst = (size_t)(d.C + 1) * 2;          // one group's reduced sums
+  const double* sg = sums + grp * sst;
+  const double cnt = count > 0.0 ? count : sg[2 * d.C];
   for (int c = threadIdx.x; c < d.C; c += BN_THREADS) {     // the NCHW apply's per-channel arithmetic
-    const double mean_d = sums[2 * c] / count;
-    double var_d = sums[2 * c + 1] / count - mean_d * mean_d;
+    const double mean_d = sg[2 * c] / cnt;
+    double var_d = sg[2 * c + 1] / cnt - mean_d * mean_d;
     var_d = var_d > 0.0 ? var_d : 0.0;
     const float mean = (float)mean_d;
     const float invstd = (float)(1.0 / sqrt(var_d + (double)d.eps));
     const float sc = invstd * gamma[c];
     coef[c] = make_float2(sc, beta[c] - mean * sc);
     if (blockIdx.x == 0) {
-      mean_out[c] = mean;
-      invstd_out[c] = invstd;
-      if (run_mean) {
-        const double unbiased = count > 1.0 ? var_d * count / (count - 1.0) : var_d;
-        run_mean[c] = (float)((1.0 - d.momentum) * run_mean[c] + d.momentum * mean_d);
-        run_var[c] = (float)((1.0 - d.momentum) * run_var[c] + d.momentum * unbiased);
-      }
+      mean_out[(size_t)grp * d.C + c] = mean;
+      invstd_out[(size_t)grp * d.C + c] = invstd;
+      if (run_mean && grp == 0)                  // the groups' updates in order
+        for (int k = 0; k < G; ++k) {
+          const double* sk = sums + k * sst;
+          const double ck = count > 0.0 ? count : sk[2 * d.C];
+          const double mk_d = sk[2 * c] / ck;
+          double vk = sk[2 * c + 1] / ck - mk_d * mk_d;
+          vk = vk > 0.0 ? vk : 0.0;
+          bn_running(d, c, ck, mk_d, vk, run_mean, run_var);
+        }
     }
   }
   __syncthreads();
   const unsigned qm = (unsigned)(d.C >> 2) - 1u;
   const unsigned total4 = (unsigned)d.N * (unsigned)d.HW * (unsigned)(d.C >> 2);
   const bool relu = d.relu != 0;
+  const size_t gb = grp * bn_gsz(d);
   for (unsigned i = blockIdx.x * BN_THREADS + threadIdx.x; i < total4; i += gridDim.x * BN_THREADS) {
-    const size_t o = 4 * (size_t)i;
+    const size_t o = gb + 4 * (size_t)i;
     const int c = 4 * (i & qm);
     float4 v = ld4(x + o);
     const float2 k0 = coef[c], k1 = coef[c + 1], k2 = coef[c + 2], k3 = coef[c + 3];
@@ -702,22 +776,30 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply_nhwc_k(vfd_bn_desc d,
                                                                   float* __restrict__ dgamma,
                                                                   float* __restrict__ dbeta) {
   __shared__ float4 coef[NH_MAXC];     // k, mean g', mx, mean
-  if (count <= 0.0) count = sums[2 * d.C];
+  const int grp = blockIdx.y, G = bn_groups(d);
+  const size_t sst = (size_t)(d.C + 1) * 2;          // one group's reduced sums
+  const double cnt = count > 0.0 ? count : sums[grp * sst + 2 * d.C];
   for (int c = threadIdx.x; c < d.C; c += BN_THREADS) {
-    const double sg = sums[2 * c], sgx = sums[2 * c + 1];
-    const float mean = mean_in[c], invstd = invstd_in[c];
-    if (blockIdx.x == 0) {
-      if (dgamma) dgamma[c] = (float)(sgx * invstd);
-      if (dbeta) dbeta[c] = (float)sg;
+    const double sg = sums[grp * sst + 2 * c], sgx = sums[grp * sst + 2 * c + 1];
+    const float mean = mean_in[(size_t)grp * d.C + c], invstd = invstd_in[(size_t)grp * d.C + c];
+    if (blockIdx.x == 0 && grp == 0 && (dgamma || dbeta)) {   // the groups' values, fp32, in order
+      float dg = 0.f, db = 0.f;
+      for (int k = 0; k < G; ++k) {
+        dg += (float)(sums[k * sst + 2 * c + 1] * invstd_in[(size_t)k * d.C + c]);
+        db += (float)sums[k * sst + 2 * c];
+      }
+      if (dgamma) dgamma[c] = dg;
+      if (dbeta) dbeta[c] = db;
     }
-    coef[c] = make_float4(gamma[c] * invstd, (float)(sg / count), (float)(sgx / count) * invstd * invstd, mean);
+    coef[c] = make_float4(gamma[c] * invstd, (float)(sg / cnt), (float)(sgx / cnt) * invstd * invstd, mean);
   }
   __syncthreads();
   const unsigned qm = (unsigned)(d.C >> 2) - 1u;
   const unsigned total4 = (unsigned)d.N * (unsigned)d.HW * (unsigned)(d.C >> 2);
   const bool relu = d.relu != 0;
+  const size_t gb = grp * bn_gsz(d);
   for (unsigned i = blockIdx.x * BN_THREADS + threadIdx.x; i < total4; i += gridDim.x * BN_THREADS) {
-    const size_t o = 4 * (size_t)i;
+    const size_t o = gb + 4 * (size_t)i;
     const int c = 4 * (i & qm);
     float4 gv = bn_g4(d, g, o);
     if (relu) relu_mask4(d, y, o, gv);
@@ -947,6 +1029,7 @@ static int bn_check(const vfd_bn_desc* d, const char* what) {
   VFD_REQUIRE(d && d->N > 0 && d->C > 0 && d->HW > 0 && d->S > 0 && d->S == vfd_bn_splits(d),
               "%s: bad descriptor (S must be vfd_bn_splits)", what);
   VFD_REQUIRE((long long)d->N * d->HW < (1LL << 31), "%s: more than 2^31 elements per channel", what);
+  VFD_REQUIRE(d->groups >= 0 && d->groups <= 64, "%s: groups must be in [0, 64]", what);
   if (d->nhwc)
     VFD_REQUIRE(d->C % 4 == 0 && d->C <= NH_MAXC && ((d->C >> 2) & ((d->C >> 2) - 1)) == 0 &&
                     (long long)d->N * d->HW * d->C < (1LL << 31),
@@ -958,14 +1041,15 @@ int vfd_bn_fwd_stats(const vfd_bn_desc* d, const void* x, double* partial, void*
   if (int e = bn_check(d, "bn_fwd_stats")) return e;
   VFD_REQUIRE(x && partial, "bn_fwd_stats: null argument");
   hipStream_t s = (hipStream_t)stream;
+  const int G = d->groups > 1 ? d->groups : 1;
   ProfScope ps(K_BN_FWD, s);
   if (d->nhwc) {
-    if (d->dtype == 1) bn_stats_nhwc_k<__bf16><<<d->S, BN_THREADS, 0, s>>>(*d, (const __bf16*)x, partial);
-    else bn_stats_nhwc_k<float><<<d->S, BN_THREADS, 0, s>>>(*d, (const float*)x, partial);
+    if (d->dtype == 1) bn_stats_nhwc_k<__bf16><<<dim3(d->S, G), BN_THREADS, 0, s>>>(*d, (const __bf16*)x, partial);
+    else bn_stats_nhwc_k<float><<<dim3(d->S, G), BN_THREADS, 0, s>>>(*d, (const float*)x, partial);
     return fail_launch("bn_fwd_stats");
   }
-  if (d->dtype == 1) bn_stats_k<__bf16><<<dim3(d->S, d->C), BN_THREADS, 0, s>>>(*d, (const __bf16*)x, partial);
-  else bn_stats_k<float><<<dim3(d->S, d->C), BN_THREADS, 0, s>>>(*d, (const float*)x, partial);
+  if (d->dtype == 1) bn_stats_k<__bf16><<<dim3(d->S, d->C, G), BN_THREADS, 0, s>>>(*d, (const __bf16*)x, partial);
+  else bn_stats_k<float><<<dim3(d->S, d->C, G), BN_THREADS, 0, s>>>(*d, (const float*)x, partial);
   return fail_launch("bn_fwd_stats");
 }
 
@@ -988,6 +1072,7 @@ int vfd_bn_fwd_apply(const vfd_bn_desc* d, const void* x, const void* residual, 
                      float* running_mean, float* running_var, long long* num_batches_tracked,
                      unsigned char* relu_mask, void* stream) {
   if (int e = bn_check(d, "bn_fwd_apply")) return e;
+  const int G = d->groups > 1 ? d->groups : 1;
   VFD_REQUIRE(x && sums && gamma && beta && y && mean && invstd && (ns == 1 || ns == d->S) &&
                   (count > 0.0 || ns == 1),
               "bn_fwd_apply: bad argument (count <= 0 reads the count row of reduced sums: ns must be 1)");
@@ -998,22 +1083,22 @@ int vfd_bn_fwd_apply(const vfd_bn_desc* d, const void* x, const void* residual, 
   if (d->nhwc) {
     unsigned char* mk = d->relu ? relu_mask : nullptr;
     if (d->dtype == 1)
-      bn_apply_nhwc_k<__bf16><<<nh_apply_blocks(d), BN_THREADS, 0, s>>>(
+      bn_apply_nhwc_k<__bf16><<<dim3(nh_apply_blocks(d), G), BN_THREADS, 0, s>>>(
           *d, (const __bf16*)x, (const __bf16*)residual, sums, count, gamma, beta, (__bf16*)y, mean, invstd,
           running_mean, running_var, num_batches_tracked, mk);
     else
-      bn_apply_nhwc_k<float><<<nh_apply_blocks(d), BN_THREADS, 0, s>>>(
+      bn_apply_nhwc_k<float><<<dim3(nh_apply_blocks(d), G), BN_THREADS, 0, s>>>(
           *d, (const float*)x, (const float*)residual, sums, count, gamma, beta, (float*)y, mean, invstd, running_mean,
           running_var, num_batches_tracked, mk);
     return fail_launch("bn_fwd_apply");
   }
   if (d->dtype == 1)
-    bn_apply_k<__bf16><<<dim3(d->S, d->C), BN_THREADS, 0, s>>>(*d, (const __bf16*)x, (const __bf16*)residual, sums, ns,
+    bn_apply_k<__bf16><<<dim3(d->S, d->C, G), BN_THREADS, 0, s>>>(*d, (const __bf16*)x, (const __bf16*)residual, sums, ns,
                                                                count, gamma, beta, (__bf16*)y, mean, invstd, running_mean,
                                                                running_var, num_batches_tracked,
                                                                d->relu ? relu_mask : nullptr);
   else
-    bn_apply_k<float><<<dim3(d->S, d->C), BN_THREADS, 0, s>>>(*d, (const float*)x, (const float*)residual, sums, ns,
+    bn_apply_k<float><<<dim3(d->S, d->C, G), BN_THREADS, 0, s>>>(*d, (const float*)x, (const float*)residual, sums, ns,
                                                               count, gamma, beta, (float*)y, mean, invstd, running_mean,
                                                               running_var, num_batches_tracked,
                                                               d->relu ? relu_mask : nullptr);
@@ -1023,23 +1108,24 @@ int vfd_bn_fwd_apply(const vfd_bn_desc* d, const void* x, const void* residual, 
 int vfd_bn_bwd_stats(const vfd_bn_desc* d, const void* g, const void* y, const void* x, const float* mean,
                      double* partial, void* stream) {
   if (int e = bn_check(d, "bn_bwd_stats")) return e;
+  const int G = d->groups > 1 ? d->groups : 1;
   VFD_REQUIRE(g && x && mean && partial && (y || !d->relu), "bn_bwd_stats: null argument");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_BN_BWD, s);
   if (d->nhwc) {
     if (d->dtype == 1)
-      bn_bwd_stats_nhwc_k<__bf16><<<d->S, BN_THREADS, 0, s>>>(*d, (const __bf16*)g, (const __bf16*)y,
+      bn_bwd_stats_nhwc_k<__bf16><<<dim3(d->S, G), BN_THREADS, 0, s>>>(*d, (const __bf16*)g, (const __bf16*)y,
                                                               (const __bf16*)x, mean, partial);
     else
-      bn_bwd_stats_nhwc_k<float><<<d->S, BN_THREADS, 0, s>>>(*d, (const float*)g, (const float*)y, (const float*)x,
+      bn_bwd_stats_nhwc_k<float><<<dim3(d->S, G), BN_THREADS, 0, s>>>(*d, (const float*)g, (const float*)y, (const float*)x,
                                                              mean, partial);
     return fail_launch("bn_bwd_stats");
   }
   if (d->dtype == 1)
-    bn_bwd_stats_k<__bf16><<<dim3(d->S, d->C), BN_THREADS, 0, s>>>(*d, (const __bf16*)g, (const __bf16*)y,
+    bn_bwd_stats_k<__bf16><<<dim3(d->S, d->C, G), BN_THREADS, 0, s>>>(*d, (const __bf16*)g, (const __bf16*)y,
                                                                    (const __bf16*)x, mean, partial);
   else
-    bn_bwd_stats_k<float><<<dim3(d->S, d->C), BN_THREADS, 0, s>>>(*d, (const float*)g, (const float*)y,
+    bn_bwd_stats_k<float><<<dim3(d->S, d->C, G), BN_THREADS, 0, s>>>(*d, (const float*)g, (const float*)y,
                                                                   (const float*)x, mean, partial);
   return fail_launch("bn_bwd_stats");
 }
@@ -1048,6 +1134,7 @@ int vfd_bn_bwd_apply(const vfd_bn_desc* d, const void* g, const void* y, const v
                      int ns, double count, const float* gamma, const float* mean, const float* invstd, void* dx,
                      void* dresidual, float* dgamma, float* dbeta, void* stream) {
   if (int e = bn_check(d, "bn_bwd_apply")) return e;
+  const int G = d->groups > 1 ? d->groups : 1;
   VFD_REQUIRE(g && x && sums && gamma && mean && invstd && (y || !d->relu) && (ns == 1 || ns == d->S) &&
                   (count > 0.0 || ns == 1),
               "bn_bwd_apply: bad argument (count <= 0 reads the count row of reduced sums: ns must be 1)");
@@ -1056,21 +1143,21 @@ int vfd_bn_bwd_apply(const vfd_bn_desc* d, const void* g, const void* y, const v
   ProfScope ps(K_BN_BWD, s);
   if (d->nhwc) {
     if (d->dtype == 1)
-      bn_bwd_apply_nhwc_k<__bf16><<<nh_apply_blocks(d), BN_THREADS, 0, s>>>(
+      bn_bwd_apply_nhwc_k<__bf16><<<dim3(nh_apply_blocks(d), G), BN_THREADS, 0, s>>>(
           *d, (const __bf16*)g, (const __bf16*)y, (const __bf16*)x, sums, count, gamma, mean, invstd, (__bf16*)dx,
           (__bf16*)dresidual, dgamma, dbeta);
     else
-      bn_bwd_apply_nhwc_k<float><<<nh_apply_blocks(d), BN_THREADS, 0, s>>>(
+      bn_bwd_apply_nhwc_k<float><<<dim3(nh_apply_blocks(d), G), BN_THREADS, 0, s>>>(
           *d, (const float*)g, (const float*)y, (const float*)x, sums, count, gamma, mean, invstd, (float*)dx,
           (float*)dresidual, dgamma, dbeta);
     return fail_launch("bn_bwd_apply");
   }
   if (d->dtype == 1)
-    bn_bwd_apply_k<__bf16><<<dim3(d->S, d->C), BN_THREADS, 0, s>>>(*d, (const __bf16*)g, (const __bf16*)y,
+    bn_bwd_apply_k<__bf16><<<dim3(d->S, d->C, G), BN_THREADS, 0, s>>>(*d, (const __bf16*)g, (const __bf16*)y,
                                                                    (const __bf16*)x, sums, ns, count, gamma, mean, invstd,
                                                                    (__bf16*)dx, (__bf16*)dresidual, dgamma, dbeta);
   else
-    bn_bwd_apply_k<float><<<dim3(d->S, d->C), BN_THREADS, 0, s>>>(*d, (const float*)g, (const float*)y,
+    bn_bwd_apply_k<float><<<dim3(d->S, d->C, G), BN_THREADS, 0, s>>>(*d, (const float*)g, (const float*)y,
                                                                   (const float*)x, sums, ns, count, gamma, mean, invstd,
                                                                   (float*)dx, (float*)dresidual, dgamma, dbeta);
   return fail_launch("bn_bwd_apply");
@@ -1078,7 +1165,9 @@ int vfd_bn_bwd_apply(const vfd_bn_desc* d, const void* g, const void* y, const v
 
 int vfd_bn1_fits(const vfd_bn_desc* d) {
   if (!d || d->N <= 0 || d->C <= 0 || d->HW <= 0 || (long long)d->N * d->HW > (long long)BN1_MAX) return 0;
-  return !d->nhwc || (VFD_BN1_NHWC && d->C % BN1N_CG == 0) ? 1 : 0;
+  if (d->groups < 0 || d->groups > 64) return 0;
+  // groups: the NCHW one-launch kernels loop over them; the opt-in NHWC ones take one group
+  return !d->nhwc || (VFD_BN1_NHWC && d->C % BN1N_CG == 0 && d->groups <= 1) ? 1 : 0;
 }
 
 int vfd_bn1_fwd(const vfd_bn_desc* d, const void* x, const void* residual, const float* gamma, const float* beta,

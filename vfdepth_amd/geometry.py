@@ -6,6 +6,8 @@
   reference's per-camera API; `render_all(inputs, outputs, rel_poses)` renders every camera's
   warps in one fused launch sequence and is what `VFDepthAlgo` uses.
 """
+import os
+
 import torch
 import torch.nn as nn
 
@@ -60,6 +62,11 @@ def vec_to_matrix(rot_angle, trans_vec, invert=False):
     return torch.matmul(R, Tm) if invert else torch.matmul(Tm, R)
 
 
+# the fused pose net's frame pairs as one batch: opt-in (VFD_POSE_PAIRS=1) until the illegal
+# address its first HIP-graph replay hit in round 5 is understood
+_POSE_PAIRS = os.environ.get('VFD_POSE_PAIRS', '0') == '1'
+
+
 class Pose:
     """Multi-camera pose handling (pose.py:7-96)."""
 
@@ -70,6 +77,9 @@ class Pose:
         self.num_cams = int(dt['num_cams'])
         self.rel_cam_list = dt['rel_cam_list']
         self.spatio, self.spatio_temporal = bool(t['spatio']), bool(t['spatio_temporal'])
+        # the frame pairs as one batch (eager steps); VFDepthAlgo.graphed_train_step turns it off for
+        # the captured step (the stacked-pair step faulted on its first HIP-graph replay)
+        self.batch_pairs = True
 
     def compute_pose(self, net, inputs):
         if self.pose_model == 'fusion':
@@ -78,9 +88,17 @@ class Pose:
         return {('cam', c): self.get_single_pose(net, inputs, c) for c in range(self.num_cams)}
 
     def get_single_pose(self, net, inputs, cam):
+        """pose.py:31-42: one net call per context frame (pairs in temporal order).  With
+        VFD_POSE_PAIRS=1 the fused pose net takes all pairs in ONE call: its stacked-batch forward
+        gives each pair exactly the reference call's BatchNorm statistics."""
         out = {}
-        for f in self.frame_ids[1:]:
-            pair = [-1, 0] if f < 0 else [0, 1]
+        fids = self.frame_ids[1:]
+        pairs = [[-1, 0] if f < 0 else [0, 1] for f in fids]
+        if cam is None and self.pose_model == 'fusion' and len(pairs) > 1 and _POSE_PAIRS and self.batch_pairs:
+            for f, (axisangle, translation) in zip(fids, net(inputs, pairs, cam)):
+                out[('cam_T_cam', 0, f)] = vec_to_matrix(axisangle[:, 0], translation[:, 0], invert=(f < 0))
+            return out
+        for f, pair in zip(fids, pairs):
             axisangle, translation = net(inputs, pair, cam)
             out[('cam_T_cam', 0, f)] = vec_to_matrix(axisangle[:, 0], translation[:, 0], invert=(f < 0))
         return out

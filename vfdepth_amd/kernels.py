@@ -321,15 +321,7 @@ class FusePose(torch.autograd.Function):
     @staticmethod
     @_amp_bwd
     def backward(ctx, g):
-        lib = L.load()
-        B, N, C = ctx.shape[:3]
-        g = _channels_last(g, 'grad')
-        dfeats = torch.empty(ctx.shape, device=g.device)
-        d = ctx.space.desc(B, N, C=C)
-        ctx.plan.build().wait()
-        L.check(lib.vfd_fuse_pose_bwd(ctypes.byref(d), ctx.plan.buf.data_ptr(), ctx.plan.counts.data_ptr(),
-                                      g.data_ptr(), dfeats.data_ptr(), L.stream()), 'fuse_pose_bwd')
-        return None, None, dfeats
+        return None, None, _pose_unfuse(ctx.space, ctx.plan, ctx.shape, _channels_last(g, 'grad'))
 
 
 class VoxelProject(torch.autograd.Function):
@@ -739,11 +731,21 @@ class PadConvBF16(torch.autograd.Function):
 _DT = {torch.float32: 0, torch.bfloat16: 1}
 
 
+def _pose_pairs(plan, B):
+    """Frame pairs stacked in a pose batch of B elements over a plan (geometry) of plan.B elements."""
+    if B % plan.B:
+        raise RuntimeError(f'pose fusion: batch {B} is not a multiple of the geometry batch {plan.B}')
+    return B // plan.B
+
+
 def _pose_fuse_t(space, plan, feats, dtype):
-    """K2 forward into a fresh map of `dtype` (fusion.hip fuse_pose_fwd_k) -> (map, desc shape)."""
+    """K2 forward into a fresh map of `dtype` (fusion.hip fuse_pose_fwd_k) -> (map, desc shape).
+    feats may stack P frame pairs over the plan's geometry batch ([P * plan.B, N, C, h, w], the
+    pose net's pairs in one batch): K2 runs once per pair on its slice with the plan's geometry."""
     lib = L.load()
     feats = _dev(feats, 'feats')
     B, N, C = feats.shape[:3]
+    P, Bg = _pose_pairs(plan, B), plan.B
     hw = feats.shape[3] * feats.shape[4]
     feats_cl = torch.empty(B, N, hw, C, device=feats.device)          # [B, N, h*w, C]: one tiled pass
     L.check(lib.vfd_nchw_to_nhwc(feats.data_ptr(), feats_cl.data_ptr(), B * N, C, hw, 0, L.stream()), 'nchw_to_nhwc')
@@ -751,25 +753,33 @@ def _pose_fuse_t(space, plan, feats, dtype):
         L.ALG_BYTES['layout_copy'] += 2 * feats.numel() * 4
     out = torch.empty(B, (C + 1) * space.Z, space.Y + 2, space.X + 2, device=feats.device, dtype=dtype,
                       memory_format=torch.channels_last)
-    d = space.desc(B, N, C=C)
+    d = space.desc(Bg, N, C=C)
     order = space.pose_order()
-    L.check(lib.vfd_fuse_pose_fwd_t(ctypes.byref(d), plan.mask_lo.data_ptr(), plan.K.data_ptr(),
-                                    plan.Einv.data_ptr(), feats_cl.data_ptr(), out.data_ptr(), _DT[dtype],
-                                    L.ptr(order), order.shape[1] if order is not None else 0, L.stream()),
-            'fuse_pose_fwd')
+    fstep, ostep = Bg * N * hw * C * 4, Bg * out[0].numel() * out.element_size()     # bytes per pair
+    for p in range(P):
+        L.check(lib.vfd_fuse_pose_fwd_t(ctypes.byref(d), plan.mask_lo.data_ptr(), plan.K.data_ptr(),
+                                        plan.Einv.data_ptr(), feats_cl.data_ptr() + p * fstep,
+                                        out.data_ptr() + p * ostep, _DT[dtype],
+                                        L.ptr(order), order.shape[1] if order is not None else 0, L.stream()),
+                'fuse_pose_fwd')
     return out
 
 
 def _pose_unfuse(space, plan, shape, g):
-    """K2 backward: d map (fp32 or bf16, channels-last) -> d feats [B, N, C, h, w] fp32 (fuse_pose_bwd_k)."""
+    """K2 backward: d map (fp32 or bf16, channels-last) -> d feats [B, N, C, h, w] fp32 (fuse_pose_bwd_k);
+    once per stacked frame pair, as the forward."""
     lib = L.load()
     B, N, C = shape[:3]
+    P, Bg = _pose_pairs(plan, B), plan.B
     g = _nhwc(g, 'grad') if g.dtype in _DT else _channels_last(g, 'grad')
     dfeats = torch.empty(shape, device=g.device)
-    d = space.desc(B, N, C=C)
+    d = space.desc(Bg, N, C=C)
     plan.build().wait()
-    L.check(lib.vfd_fuse_pose_bwd_t(ctypes.byref(d), plan.buf.data_ptr(), plan.counts.data_ptr(),
-                                    g.data_ptr(), _DT[g.dtype], dfeats.data_ptr(), L.stream()), 'fuse_pose_bwd')
+    gstep, fstep = Bg * g[0].numel() * g.element_size(), Bg * dfeats[0].numel() * 4       # bytes per pair
+    for p in range(P):
+        L.check(lib.vfd_fuse_pose_bwd_t(ctypes.byref(d), plan.buf.data_ptr(), plan.counts.data_ptr(),
+                                        g.data_ptr() + p * gstep, _DT[g.dtype], dfeats.data_ptr() + p * fstep,
+                                        L.stream()), 'fuse_pose_bwd')
     return dfeats
 
 
@@ -1478,7 +1488,7 @@ def _bn_sync(lib, d, partial, pg, count, what, invstd=None, dgamma=None, dbeta=N
     sums first, as torch's SyncBatchNorm returns them (DDP then averages them over ranks)."""
     import time
     import torch.distributed as dist
-    sums = torch.empty(d.C + 1, 2, dtype=torch.float64, device=partial.device)
+    sums = torch.empty(max(d.groups, 1), d.C + 1, 2, dtype=torch.float64, device=partial.device)
     L.check(lib.vfd_bn_sum(ctypes.byref(d), partial.data_ptr(), float(count), sums.data_ptr(), L.ptr(invstd),
                            L.ptr(dgamma), L.ptr(dbeta), L.stream()), what)
     t0 = time.perf_counter()
@@ -1503,8 +1513,8 @@ def syncbn_stats(reset=True):
 
 
 def _bn_reduce(lib, d, partial, count, what, invstd=None, dgamma=None, dbeta=None):
-    """The [C][S][2] partials reduced to [C + 1][2] sums (row C = the element count) on this rank."""
-    sums = torch.empty(d.C + 1, 2, dtype=torch.float64, device=partial.device)
+    """The [G][C][S][2] partials reduced to [G][C + 1][2] sums (row C = the element count) on this rank."""
+    sums = torch.empty(max(d.groups, 1), d.C + 1, 2, dtype=torch.float64, device=partial.device)
     L.check(lib.vfd_bn_sum(ctypes.byref(d), partial.data_ptr(), float(count), sums.data_ptr(), L.ptr(invstd),
                            L.ptr(dgamma), L.ptr(dbeta), L.stream()), what)
     return sums
@@ -1518,7 +1528,7 @@ def _bn_nhwc(x):
 
 
 def _bn_fields(d):
-    return (d.N, d.C, d.HW, d.S, d.relu, d.eps, d.momentum, d.dtype, None, None, d.nhwc)
+    return (d.N, d.C, d.HW, d.S, d.relu, d.eps, d.momentum, d.dtype, None, None, d.nhwc, d.groups)
 
 
 def _observed(t):
@@ -1529,22 +1539,29 @@ def _observed(t):
 class BatchNormAct(torch.autograd.Function):
     """y = relu(batch_norm_train(x) [+ r]) for NCHW fp32 x (one statistics + one apply pass each
     way; running statistics updated like nn.BatchNorm2d.train()).  `pg`: the SyncBatchNorm group
-    (None = local statistics)."""
+    (None = local statistics).  `groups` G > 1: x holds G consecutive batches normalised with their
+    own statistics, exactly G train-mode calls of the layer (running statistics updated G times in
+    order, num_batches_tracked += G, parameter gradients summed) in the launches of one
+    (bnact.hip, vfd_bn_desc.groups)."""
 
     @staticmethod
     def forward(ctx, x, gamma, beta, residual, running_mean, running_var, eps, momentum, relu, pg, nbt=None,
-                join=False):
+                join=False, groups=1):
         lib = L.load()
         _check_device(x, 'batch norm input')
         if x.dtype not in (torch.float32, torch.bfloat16):
             raise RuntimeError(f'fused batch norm: fp32 or bf16 activations, got {x.dtype}')
         N, C, H, W = x.shape
+        G = int(groups)
+        if G < 1 or N % G:
+            raise RuntimeError(f'fused batch norm: {N} images do not split into {G} groups')
         # channels-last maps (config 3's bf16 encoders, layers.ResnetEncoder) stay channels-last
         fmt = torch.channels_last if _bn_nhwc(x) else torch.contiguous_format
         x = x.contiguous(memory_format=fmt)
         # bf16 activations (config 3's autocast: the conv outputs are bf16), fp32 parameters / stats
-        d = L.BnDesc(N, C, H * W, 0, int(relu), float(eps), float(momentum), int(x.dtype == torch.bfloat16))
+        d = L.BnDesc(N // G, C, H * W, 0, int(relu), float(eps), float(momentum), int(x.dtype == torch.bfloat16))
         d.nhwc = int(fmt is torch.channels_last)
+        d.groups = G
         d.S = lib.vfd_bn_splits(ctypes.byref(d))
         ctx.fmt = fmt
         r = residual.to(x.dtype).contiguous(memory_format=fmt) if residual is not None else None
@@ -1571,28 +1588,28 @@ class BatchNormAct(torch.autograd.Function):
         ctx.one = pg is None and _BN_ONE and bool(lib.vfd_bn1_fits(ctypes.byref(d)))
         if ctx.one:       # small layer, local statistics: one launch (bnact.hip bn1_fwd_k)
             y = torch.empty_like(x)
-            mean = torch.empty(C, device=x.device)
-            invstd = torch.empty(C, device=x.device)
+            mean = torch.empty(G, C, device=x.device)
+            invstd = torch.empty(G, C, device=x.device)
             L.check(lib.vfd_bn1_fwd(ctypes.byref(d), x.data_ptr(), ptr(r), gamma.data_ptr(), beta.data_ptr(),
                                     y.data_ptr(), mean.data_ptr(), invstd.data_ptr(), ptr(running_mean),
                                     ptr(running_var), ptr(nbt), ptr(mk), L.stream()), 'bn1_fwd')
-            ctx.d, ctx.pg, ctx.count, ctx.has_res = _bn_fields(d), pg, float(N * H * W), r is not None
+            ctx.d, ctx.pg, ctx.count, ctx.has_res = _bn_fields(d), pg, float(N // G * H * W), r is not None
             if L.PROF_ON:
                 L.ALG_BYTES['bn_fwd'] += x.numel() * (2 * x.element_size() + x.element_size() * (r is not None)
                                                       + (mk is not None))
             ctx.save_for_backward(x, mk, gamma, mean, invstd)
             return y
-        partial = torch.empty(C, d.S, 2, dtype=torch.float64, device=x.device)
+        partial = torch.empty(G, C, d.S, 2, dtype=torch.float64, device=x.device)
         L.check(lib.vfd_bn_fwd_stats(ctypes.byref(d), x.data_ptr(), partial.data_ptr(), L.stream()), 'bn_fwd_stats')
-        count, sums, ns = float(N * H * W), partial, d.S
+        count, sums, ns = float(N // G * H * W), partial, d.S
         if pg is not None:          # global sums and count from the group; count 0 = read on device
             sums, ns = _bn_sync(lib, d, partial, pg, count, 'bn_sum'), 1
             count = 0.0
         elif d.nhwc:                # channels-last apply passes take reduced sums
             sums, ns = _bn_reduce(lib, d, partial, count, 'bn_sum'), 1
         y = torch.empty_like(x)
-        mean = torch.empty(C, device=x.device)
-        invstd = torch.empty(C, device=x.device)
+        mean = torch.empty(G, C, device=x.device)
+        invstd = torch.empty(G, C, device=x.device)
         L.check(lib.vfd_bn_fwd_apply(ctypes.byref(d), x.data_ptr(), r.data_ptr() if r is not None else None,
                                      sums.data_ptr(), ns, count, gamma.data_ptr(), beta.data_ptr(), y.data_ptr(),
                                      mean.data_ptr(), invstd.data_ptr(),
@@ -1644,8 +1661,8 @@ class BatchNormAct(torch.autograd.Function):
             L.check(lib.vfd_bn1_bwd(ctypes.byref(d), g.data_ptr(), mk.data_ptr() if d.relu else None, x.data_ptr(),
                                     gamma.data_ptr(), mean.data_ptr(), invstd.data_ptr(), ptr(dx), ptr(dr),
                                     ptr(dgamma), ptr(dbeta), L.stream()), 'bn1_bwd')
-            return dx, dgamma, dbeta, dr, None, None, None, None, None, None, None, None
-        partial = torch.empty(d.C, d.S, 2, dtype=torch.float64, device=g.device)
+            return dx, dgamma, dbeta, dr, None, None, None, None, None, None, None, None, None
+        partial = torch.empty(max(d.groups, 1), d.C, d.S, 2, dtype=torch.float64, device=g.device)
         yp = mk.data_ptr() if d.relu else None
         L.check(lib.vfd_bn_bwd_stats(ctypes.byref(d), g.data_ptr(), yp, x.data_ptr(), mean.data_ptr(),
                                      partial.data_ptr(), L.stream()), 'bn_bwd_stats')
@@ -1657,7 +1674,7 @@ class BatchNormAct(torch.autograd.Function):
         sums, ns, count = partial, d.S, ctx.count
         pg_dgamma, pg_dbeta = dgamma, dbeta
         if ctx.pg is not None:      # local d gamma / d beta, then the global sums (+ count row)
-            sums, ns = _bn_sync(lib, d, partial, ctx.pg, x.shape[0] * d.HW, 'bn_sum', invstd, dgamma, dbeta), 1
+            sums, ns = _bn_sync(lib, d, partial, ctx.pg, d.N * d.HW, 'bn_sum', invstd, dgamma, dbeta), 1
             count, pg_dgamma, pg_dbeta = 0.0, None, None
         elif d.nhwc:                # channels-last: reduced sums (d gamma / d beta written there)
             sums, ns = _bn_reduce(lib, d, partial, count, 'bn_sum', invstd, dgamma, dbeta), 1
@@ -1669,7 +1686,7 @@ class BatchNormAct(torch.autograd.Function):
         L.check(lib.vfd_bn_bwd_apply(ctypes.byref(d), g.data_ptr(), yp, x.data_ptr(), sums.data_ptr(), ns, count,
                                      gamma.data_ptr(), mean.data_ptr(), invstd.data_ptr(), ptr(dx), ptr(dr),
                                      ptr(pg_dgamma), ptr(pg_dbeta), L.stream()), 'bn_bwd_apply')
-        return dx, dgamma, dbeta, dr, None, None, None, None, None, None, None, None
+        return dx, dgamma, dbeta, dr, None, None, None, None, None, None, None, None, None
 
 
 # =============================================================================================
@@ -1935,15 +1952,19 @@ class DispConvSigmoid(torch.autograd.Function):
         return dxp, dw, db
 
 
-def normalize_cat(a, b=None):
+def normalize_cat(a, b=None, out=None):
     """(cat([a, b], dim=1) - 0.45) / 0.225 for image batches [n, c, h, w] without gradient, in one
-    HIP pass (maxpool.hip norm_cat_k; the encoders' input normalisation, bit-identical)."""
+    HIP pass (maxpool.hip norm_cat_k; the encoders' input normalisation, bit-identical).  `out`: a
+    contiguous [n, ca + cb, h, w] slot to write (one frame pair's part of a stacked batch)."""
     lib = L.load()
     a = _dev(a, 'image').contiguous()
     b = _dev(b, 'image').contiguous() if b is not None else None
     n, ca, h, w = a.shape
     cb = b.shape[1] if b is not None else 0
-    out = torch.empty(n, ca + cb, h, w, device=a.device)
+    if out is None:
+        out = torch.empty(n, ca + cb, h, w, device=a.device)
+    elif tuple(out.shape) != (n, ca + cb, h, w) or not out.is_contiguous() or out.dtype != torch.float32:
+        raise RuntimeError(f'normalize_cat: out {tuple(out.shape)} does not fit {(n, ca + cb, h, w)}')
     L.check(lib.vfd_normalize_cat(a.data_ptr(), b.data_ptr() if b is not None else None, out.data_ptr(), n, ca, cb,
                                   h * w, L.stream()), 'normalize_cat')
     return out

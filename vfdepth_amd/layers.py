@@ -93,20 +93,44 @@ def upsample(x):
 
 
 # ----------------------------------------------------------------------------- ResNet encoder
+_BN_GROUPS = [1]
+
+
+class bn_groups:
+    """Inside the block every training-mode BatchNorm of `bn_act` treats its batch as G consecutive
+    groups with their own statistics — exactly G separate calls of the layer (running statistics
+    updated G times in order).  The fused pose net runs its two frame pairs as one batch this way
+    (models/geometry/pose.py:33-42 calls it once per pair)."""
+
+    def __init__(self, groups):
+        self.groups = int(groups)
+
+    def __enter__(self):
+        _BN_GROUPS.append(self.groups)
+        return self
+
+    def __exit__(self, *exc):
+        _BN_GROUPS.pop()
+
+
 def bn_act(bn, x, residual=None, relu=True, join=False):
     """relu(bn(x) [+ residual]): one fused HIP kernel pair (bnact.hip, SyncBatchNorm-aware) for a
     training-mode BatchNorm2d on the GPU, fp32 activations or (under bf16 autocast) bf16 ones with
     fp32 statistics; the module + torch ops otherwise (eval mode, CPU).  VFD_FUSED_BN=0 disables
     the fused path.  join: the residual is this block's input and also feeds its first conv (an
     identity block): its gradient is summed inside the producing BN's backward kernels."""
+    G = _BN_GROUPS[-1]
     if (bn.training and bn.track_running_stats and bn.affine and bn.momentum is not None and x.is_cuda
             and x.dim() == 4 and _fused_dtype_ok(x) and os.environ.get('VFD_FUSED_BN', '1') != '0'
             and (residual is None or residual.shape == x.shape)):
         from . import kernels as KN
         return KN.BatchNormAct.apply(x, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var,
                                      bn.eps, bn.momentum, relu, KN._bn_group(bn),
-                                     bn.num_batches_tracked, join)      # += 1 inside the apply kernel
-    y = bn(x)
+                                     bn.num_batches_tracked, join, G)   # += G inside the apply kernel
+    if G > 1 and bn.training:
+        y = torch.cat([bn(xc) for xc in x.chunk(G)])        # G calls, in group order
+    else:
+        y = bn(x)
     if residual is not None:
         y = y + residual
     return F.relu(y, inplace=True) if relu else y
@@ -228,18 +252,23 @@ class ResnetEncoder(nn.Module):
         self.to(memory_format=torch.channels_last)
         return self
 
-    def forward(self, image, normalized=False):
+    def forward(self, image, normalized=False, groups=1):
         """image: [n, 3*num_input_images, H, W] in [0, 1]; normalized=True: already (x - 0.45) / 0.225
-        (the fused nets normalise while concatenating frames: kernels.normalize_cat)."""
+        (the fused nets normalise while concatenating frames: kernels.normalize_cat).  groups G: the
+        batch is G stacked calls' batches, each BatchNorm'd on its own (`bn_groups`)."""
         e = self.encoder
         x = image if normalized else (image - 0.45) / 0.225
-        f0 = bn_act(e.bn1, e.conv1(x))
-        f1 = e.layer1(max_pool_stem(e.maxpool, f0))
-        f2 = e.layer2(f1)
-        f3 = e.layer3(f2)
-        f4 = e.layer4(f3)
-        self.features = [f0, f1, f2, f3, f4]
-        return self.features
+        with bn_groups(groups):
+            f0 = bn_act(e.bn1, e.conv1(x))
+            f1 = e.layer1(max_pool_stem(e.maxpool, f0))
+            f2 = e.layer2(f1)
+            f3 = e.layer3(f2)
+            f4 = e.layer4(f3)
+        # returned, not kept as a module attribute (monodepth2's encoder stores `self.features`):
+        # a kept pyramid would hold this step's autograd graph — and its AccumulateGrad nodes, with
+        # the stream they were created on — alive into the next step (a captured HIP-graph step
+        # after eager warm-up steps on a side stream then accumulates on that stream)
+        return [f0, f1, f2, f3, f4]
 
 
 # ----------------------------------------------------------------------------- decoders

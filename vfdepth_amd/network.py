@@ -28,23 +28,33 @@ def _use_channels_last(training, bf16):
     return bool(cl)
 
 
-def _encoder_input(frames):
+def _encoder_input(frames, pairs=None):
     """cat(frames, channels) of [B, N, 3, H, W] batches, packed to [B*N, ...]: the fused nets' encoder
     input.  On the GPU (fp32, no gradient, H*W % 4 == 0) it comes normalised from one HIP pass
-    (`kernels.normalize_cat`, bit-identical to cat + (x - 0.45) / 0.225); returns (x, normalized)."""
-    f = [pack_cam_feat(t) for t in frames]
-    if (len(f) <= 2 and all(t.is_cuda and t.dtype == torch.float32 and not t.requires_grad for t in f)
-            and (f[0].shape[-1] * f[0].shape[-2]) % 4 == 0 and os.environ.get('VFD_NORM_CAT', '1') != '0'):
-        return KN.normalize_cat(*f), True
-    return (torch.cat(f, 1) if len(f) > 1 else f[0]), False
+    (`kernels.normalize_cat`, bit-identical to cat + (x - 0.45) / 0.225); returns (x, normalized).
+    pairs: a list of frame lists, stacked along the batch ([P*B*N, ...], pair-major)."""
+    groups = pairs if pairs is not None else [frames]
+    fs = [[pack_cam_feat(t) for t in fr] for fr in groups]
+    if (all(len(f) <= 2 for f in fs) and all(t.is_cuda and t.dtype == torch.float32 and not t.requires_grad
+                                             for f in fs for t in f)
+            and (fs[0][0].shape[-1] * fs[0][0].shape[-2]) % 4 == 0 and os.environ.get('VFD_NORM_CAT', '1') != '0'):
+        if len(fs) == 1:
+            return KN.normalize_cat(*fs[0]), True
+        n, _, h, w = fs[0][0].shape
+        out = torch.empty(len(fs) * n, sum(t.shape[1] for t in fs[0]), h, w, device=fs[0][0].device)
+        for p, f in enumerate(fs):
+            KN.normalize_cat(*f, out=out[p * n:(p + 1) * n])
+        return out, True
+    cat = [torch.cat(f, 1) if len(f) > 1 else f[0] for f in fs]
+    return (torch.cat(cat, 0) if len(cat) > 1 else cat[0]), False
 
 
-def _aggregate(encoder, conv1x1, images, lvl, B, N, normalized=False):
+def _aggregate(encoder, conv1x1, images, lvl, B, N, normalized=False, groups=1):
     """Encoder pyramid -> fusion-level aggregate [B,N,C,h,w] (fusion_depthnet.py:53-65,
     fusion_posenet.py:55-67): LReLU(conv1x1(cat(f_lvl, up(f_lvl+1), ...))) evaluated as
     LReLU(W_lvl f_lvl + sum up(W_k f_k) + b) — each slice of the 1x1 conv at its own resolution,
     one fused upsample-add-bias-LReLU kernel (same parameters, same result up to fp32 rounding)."""
-    feats = encoder(images, normalized)
+    feats = encoder(images, normalized, groups)
     conv = conv1x1[0]
     off, parts = 0, []
     for f in feats[lvl:]:
@@ -210,14 +220,26 @@ class FusedPoseNet(nn.Module):
             self.encoder.use_channels_last()
 
     def forward(self, inputs, frame_ids, _cam=None):
-        frames = [inputs[('color_aug', frame_ids[0], 0)], inputs[('color_aug', frame_ids[1], 0)]]
-        B, N = frames[0].shape[:2]
-        with net_autocast(self, frames[0]):
-            x, normed = _encoder_input(frames)
-            _, agg = _aggregate(self.encoder, self.conv1x1, x, self.fusion_level, B, N, normed)
+        """frame_ids: one pair [f0, f1] -> (axis_angle, translation), the reference's call; or a list
+        of pairs -> one (axis_angle, translation) per pair, computed as ONE batch: the pairs are
+        stacked along the batch (pair-major), every encoder BatchNorm normalises each pair's part on
+        its own (`layers.bn_groups`: the statistics, running-statistics updates and parameter
+        gradients of one call per pair), K2 fuses each pair with the step's geometry, and the
+        convolutions / K2C / decoder run once on the stacked batch."""
+        batched = isinstance(frame_ids[0], (list, tuple))
+        pairs = [list(p) for p in frame_ids] if batched else [list(frame_ids)]
+        P = len(pairs)
+        frames = [[inputs[('color_aug', f, 0)] for f in p] for p in pairs]
+        B, N = frames[0][0].shape[:2]
+        with net_autocast(self, frames[0][0]):
+            x, normed = _encoder_input(None, frames)
+            _, agg = _aggregate(self.encoder, self.conv1x1, x, self.fusion_level, P * B, N, normed, groups=P)
             bev = self.fusion_net(inputs, agg)
             axis_angle, translation = self.pose_decoder([[bev]])
-        return axis_angle.float(), torch.clamp(translation.float(), -4.0, 4.0)
+        axis_angle, translation = axis_angle.float(), torch.clamp(translation.float(), -4.0, 4.0)
+        if not batched:
+            return axis_angle, translation
+        return [(axis_angle[p * B:(p + 1) * B], translation[p * B:(p + 1) * B]) for p in range(P)]
 
 
 class MonoDepthNet(nn.Module):

@@ -300,6 +300,10 @@ class VFDepthAlgo:
             raise NotImplementedError('graph capture of the DDP step is not supported; use train_step')
         static = {k: (v.to(self.device) if torch.is_tensor(v) else v) for k, v in batch.items()}
         self.losses.device_seed = True
+        # the captured step calls the pose net once per frame pair (pose.batch_pairs off): the
+        # stacked-pair form's first replay hit an illegal address — eager steps
+        # keep the stacked pairs
+        self.pose.batch_pairs = False
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):

@@ -1388,6 +1388,45 @@ def _to_nhwc(x, dtype):
     return y
 
 
+class LevelConv1x1(torch.autograd.Function):
+    """The aggregation's 1x1 conv (fusion_depthnet.py:57-63, fusion_posenet.py:58-66: conv1x1 over the
+    channel concatenation of the upsampled levels) evaluated per pyramid level at its own
+    resolution with the level's input-channel slice of ONE weight [O, sum C_k, 1, 1] (MIOpen, as
+    F.conv2d on each slice).  Backward: each level's data and weight gradient from one
+    convolution_backward, and the weight gradient as the concatenation of the slices' gradients —
+    autograd's per-slice chain (a zero fill of the whole weight, a copy into the slice, an add of
+    the slices: eight launches per call) becomes one concatenation.  Under bf16 autocast the slices
+    run in bf16 as autocast casts them; their gradients come back fp32 (the master weight's)."""
+
+    @staticmethod
+    def forward(ctx, w, *feats):
+        outs, off = [], 0
+        for f in feats:
+            c = f.shape[1]
+            outs.append(F.conv2d(f, w[:, off:off + c]))
+            off += c
+        ctx.save_for_backward(w, *feats)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *gs):
+        w, *feats = ctx.saved_tensors
+        dws, dfs, off = [], [], 0
+        for i, (f, g) in enumerate(zip(feats, gs)):
+            c = f.shape[1]
+            wk = w[:, off:off + c].to(f.dtype)
+            off += c
+            if g is None:
+                g = torch.zeros(f.shape[0], w.shape[0], *f.shape[2:], device=f.device, dtype=f.dtype)
+            mask = [ctx.needs_input_grad[1 + i], ctx.needs_input_grad[0], False]
+            df, dw, _ = torch.ops.aten.convolution_backward(g.to(f.dtype), f, wk, None, [1, 1], [0, 0], [1, 1],
+                                                            False, [0, 0], 1, mask)
+            dfs.append(df)
+            dws.append(dw)
+        dW = torch.cat([t.to(w.dtype) for t in dws], 1) if ctx.needs_input_grad[0] else None
+        return (dW, *dfs)
+
+
 class AggregateUp(torch.autograd.Function):
     """LReLU_0.1(base + sum_k up_align_corners(level_k) + bias) -> NCHW fp32; levels are upsampled to
     base's size.  NCHW inputs are taken in fp32 (the cast autocast's custom_fwd(cast_inputs=float32)

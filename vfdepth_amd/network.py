@@ -56,11 +56,14 @@ def _aggregate(encoder, conv1x1, images, lvl, B, N, normalized=False, groups=1):
     one fused upsample-add-bias-LReLU kernel (same parameters, same result up to fp32 rounding)."""
     feats = encoder(images, normalized, groups)
     conv = conv1x1[0]
-    off, parts = 0, []
-    for f in feats[lvl:]:
-        c = f.shape[1]
-        parts.append(F.conv2d(f, conv.weight[:, off:off + c]))
-        off += c
+    if images.is_cuda and os.environ.get('VFD_LEVEL_CONV', '1') != '0':
+        parts = KN.LevelConv1x1.apply(conv.weight, *feats[lvl:])
+    else:
+        off, parts = 0, []
+        for f in feats[lvl:]:
+            c = f.shape[1]
+            parts.append(F.conv2d(f, conv.weight[:, off:off + c]))
+            off += c
     agg = KN.AggregateUp.apply(parts[0], conv.bias, *parts[1:])
     return feats, unpack_cam_feat(agg, B, N)
 

@@ -295,9 +295,16 @@ class VFDepthAlgo:
 
         Returns step(new_batch=None) -> losses: copies new_batch (same shapes) into the static
         input buffers and replays the graph: ~2000 kernel launches per step become one.  Needs a
-        capturable optimizer (set_optimizer(capturable=True)); single process (no DDP)."""
+        capturable optimizer (set_optimizer(capturable=True)).
+
+        Under DDP (trainer/vfdepth_trainer.py:61-66 with models/vfdepth.py:56-71's wrapping) the
+        captured step holds DDP's bucketed gradient all-reduces and the fused BN's SyncBatchNorm
+        all-reduces (RCCL kernels on the ranks' streams, captured with the step): DDP settles its
+        buckets during its first iterations, so at least 11 eager DDP steps run (on the side
+        stream) before the capture, as PyTorch requires for a DDP capture.  Every rank captures and
+        replays the same step, so the collectives stay matched."""
         if self.ddp_enable:
-            raise NotImplementedError('graph capture of the DDP step is not supported; use train_step')
+            warmup = max(warmup, 11)
         static = {k: (v.to(self.device) if torch.is_tensor(v) else v) for k, v in batch.items()}
         self.losses.device_seed = True
         # the captured step calls the pose net once per frame pair (pose.batch_pairs off): the

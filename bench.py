@@ -310,8 +310,9 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--kernel-table', action='store_true', help='print per-kernel times to stderr')
     ap.add_argument('--graph', type=int, default=0, help='1: replay the step as a captured HIP graph (single GPU)')
-    ap.add_argument('--conv-autotune', type=int, default=0,
-                    help='1: let MIOpen benchmark conv algorithms per shape (torch.backends.cudnn.benchmark)')
+    ap.add_argument('--conv-autotune', type=int, default=1,
+                    help='1 (default): MIOpen picks each conv algorithm by measured time (torch.backends.cudnn.'
+                         'benchmark; the committed find-db answers config 2 without a search); 0: immediate mode')
     ap.add_argument('--channels-last', type=int, default=0, help='1: NHWC memory format for the dense nets')
     ap.add_argument('--cpu-steps', type=int, default=3, help='timed CPU-baseline steps (after 1 warm-up)')
     ap.add_argument('--no-parity', action='store_true')
@@ -463,6 +464,8 @@ def main():
     agg_s = sum(prof[k][1] for k in hbm_ops) / 1e3
     parity = None
     if not args.no_parity:
+        # the parity steps run other shapes (96x160, the fixture's): immediate mode, no MIOpen search
+        torch.backends.cudnn.benchmark = False
         parity = parity_check(torch.device(f'cuda:{local}'))
     base = None
     if world == 1 and not args.no_cpu_baseline:
@@ -496,6 +499,11 @@ def main():
         'hot_path_ms_per_step': sum(t for _, t in prof.values()) / args.steps,
         'dense_fused': {k: roofline_any(k) for k in dense},
         'execution': 'hip-graph replay of the whole step' if use_graph else 'eager',
+        'miopen': ('benchmark mode (algorithm per shape by measured time, find-db miopen_db/)' if args.conv_autotune
+                   else 'immediate mode (find-db miopen_db/)'),
+        'encoder_layout': 'channels-last' if any(getattr(m, 'channels_last', False) for net in algo.models.values()
+                                                  for m in (net.module if hasattr(net, 'module') else net).modules())
+                          else 'NCHW',
         'syncbn': ({'backend': dist.get_backend(), 'allreduce_per_step': sbn['calls'] / n_prof,
                     'bytes_per_step': sbn['bytes'] / n_prof, 'host_ms_per_step': sbn['host_s'] * 1e3 / n_prof,
                     'what': 'the fused BN kernels\' SyncBatchNorm exchange: one all-reduce of [C+1][2] fp64 per '

@@ -86,10 +86,11 @@ def test_net_precision_flag():
 
 
 def test_channels_last_encoder_switch():
-    """The bf16 nets (config 3) build channels-last encoders (NHWC conv weights: MIOpen then runs
-    their convs without layout transposes, the fused BN / max pool take their NHWC kernels); the
-    fp32 nets stay NCHW; `training.channels_last` overrides either way.  Same values either way:
-    the state dict round-trips between the layouts."""
+    """The bf16 nets always, and the fp32 nets when MIOpen picks algorithms by measured time
+    (torch.backends.cudnn.benchmark), build channels-last encoders (NHWC conv weights: MIOpen then
+    runs their convs without layout transposes, the fused BN / max pool take their NHWC kernels;
+    VFD_CHANNELS_LAST='auto'); `training.channels_last` overrides either way.  Same values either
+    way: the state dict round-trips between the layouts."""
     from vfdepth_amd import config as C
     from vfdepth_amd.network import FusedDepthNet, FusedPoseNet
     cl = torch.channels_last
@@ -98,14 +99,24 @@ def test_channels_last_encoder_switch():
         w = net.encoder.encoder.layer1[0].conv1.weight
         return w.is_contiguous(memory_format=cl) and not w.is_contiguous()
     fp32, bf16 = C.surround_fusion_cfg(), C.surround_fusion_cfg(net_precision='bf16')
-    assert not is_cl(FusedDepthNet(fp32)) and not is_cl(FusedPoseNet(fp32))
+    bench = torch.backends.cudnn.benchmark
+    try:
+        torch.backends.cudnn.benchmark = False      # immediate mode: fp32 encoders stay NCHW
+        assert not is_cl(FusedDepthNet(fp32)) and not is_cl(FusedPoseNet(fp32))
+        torch.backends.cudnn.benchmark = True       # measured algorithm choice: channels-last
+        assert is_cl(FusedDepthNet(fp32)) and is_cl(FusedPoseNet(fp32))
+    finally:
+        torch.backends.cudnn.benchmark = bench
     assert is_cl(FusedDepthNet(bf16)) and is_cl(FusedPoseNet(bf16))
     bf16['training']['channels_last'] = False
     assert not is_cl(FusedPoseNet(bf16))
     fp32['training']['channels_last'] = True
     a = FusedPoseNet(fp32)
     assert is_cl(a)
-    b = FusedPoseNet(C.surround_fusion_cfg())
+    nchw = C.surround_fusion_cfg()
+    nchw['training']['channels_last'] = False
+    b = FusedPoseNet(nchw)
+    assert not is_cl(b)
     b.load_state_dict(a.state_dict())
     for (k, va), vb in zip(a.state_dict().items(), b.state_dict().values()):
         assert torch.equal(va, vb), k

@@ -172,9 +172,11 @@ class VFNet(nn.Module):
     def folded_weights(self):
         """Per-camera [N, 2Cv, C] feature columns of (W_no, W_o[group]) and the [3, Cv] depth columns."""
         C = self.feat_in_dim
-        w_no = self.conv_non_overlap[0].weight[:, :, 0]
-        w_o = self.conv_overlap[0].weight[:, :, 0]
         groups = KN.overlap_group_table(self.num_cams)
+        w_no, w_o = self.conv_non_overlap[0].weight, self.conv_overlap[0].weight
+        if w_no.is_cuda and os.environ.get('VFD_FOLD_WEIGHTS', '1') != '0':
+            return KN.FoldWeights.apply(w_no, w_o, groups)
+        w_no, w_o = w_no[:, :, 0], w_o[:, :, 0]
         halves = [w_o[:, :C], w_o[:, C + 1:2 * C + 1]]
         wf = torch.stack([torch.cat([w_no[:, :C], halves[g]], 0) for g in groups], 0)
         wz = torch.stack([w_no[:, C], w_o[:, C], w_o[:, 2 * C + 1]], 0)

@@ -1388,6 +1388,46 @@ def _to_nhwc(x, dtype):
     return y
 
 
+class FoldWeights(torch.autograd.Function):
+    """K1's folded 1x1-conv columns (VFNet.folded_weights): from conv_non_overlap's weight W_no
+    [Cv, C+1, 1] and conv_overlap's W_o [Cv, 2C+2, 1] (volumetric_fusionnet.py:197-230) ->
+    wf [N, 2Cv, C] (per camera: W_no's feature columns over W_o's half of the camera's overlap
+    group) and wz [3, Cv] (the depth-feature columns).  The forward is the slices / cat / stack of
+    VFNet.folded_weights; the backward writes both weight gradients directly (column sums over the
+    cameras of each group, one copy per depth column) instead of autograd's zero fill + copy + add
+    per slice and camera."""
+
+    @staticmethod
+    def forward(ctx, w_no, w_o, groups):
+        Cv, C1 = w_no.shape[:2]
+        C = C1 - 1
+        wn, wo = w_no[:, :, 0], w_o[:, :, 0]
+        halves = [wo[:, :C], wo[:, C + 1:2 * C + 1]]
+        wf = torch.stack([torch.cat([wn[:, :C], halves[g]], 0) for g in groups], 0)
+        wz = torch.stack([wn[:, C], wo[:, C], wo[:, 2 * C + 1]], 0)
+        ctx.groups, ctx.shapes = tuple(groups), (tuple(w_no.shape), tuple(w_o.shape))
+        return wf, wz
+
+    @staticmethod
+    def backward(ctx, dwf, dwz):
+        (Cv, C1, _), so = ctx.shapes
+        C = C1 - 1
+        dev, dt = (dwf if dwf is not None else dwz).device, (dwf if dwf is not None else dwz).dtype
+        dno = torch.zeros(Cv, C1, device=dev, dtype=dt)
+        do = torch.zeros(so[0], so[1], device=dev, dtype=dt)
+        if dwf is not None:
+            torch.sum(dwf[:, :Cv, :], 0, out=dno[:, :C])
+            for g, lo in ((0, 0), (1, C + 1)):
+                cams = [n for n, gg in enumerate(ctx.groups) if gg == g]
+                if cams:
+                    torch.sum(dwf[cams, Cv:, :], 0, out=do[:, lo:lo + C])
+        if dwz is not None:
+            dno[:, C] = dwz[0]
+            do[:, C] = dwz[1]
+            do[:, 2 * C + 1] = dwz[2]
+        return dno.unsqueeze(-1), do.unsqueeze(-1), None
+
+
 class LevelConv1x1(torch.autograd.Function):
     """The aggregation's 1x1 conv (fusion_depthnet.py:57-63, fusion_posenet.py:58-66: conv1x1 over the
     channel concatenation of the upsampled levels) evaluated per pyramid level at its own

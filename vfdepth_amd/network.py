@@ -16,15 +16,21 @@ from .layers import (MonoDepthDecoder, PoseDecoder, ResnetEncoder, conv2d_block,
                      unpack_cam_feat, upsample)
 
 
-# channels-last encoders: training.channels_last when set, else VFD_CHANNELS_LAST — '1' (default):
-# the bf16 nets (config 3) only, 'all': fp32 ones too, '0': never
-_CL_ENV = os.environ.get('VFD_CHANNELS_LAST', '1')
+# channels-last encoders: training.channels_last when set, else VFD_CHANNELS_LAST — 'auto' (default):
+# the bf16 nets always, the fp32 nets when MIOpen picks its algorithms by measured time
+# (torch.backends.cudnn.benchmark at construction); 'all': always, '1': the bf16 nets only, '0':
+# never.  With the find-db tuned for the NHWC fp32 shapes (miopen_db/, round 5) MIOpen's
+# channels-last fp32 convolutions in benchmark mode beat its NCHW Winograd + transposed implicit
+# GEMMs at config 2 (33.2 vs 34.3 ms/step; NCHW immediate mode 35.5), but its immediate-mode picks
+# for them do not (37.1, profiles/r5/ab/); round 3's NCHW-wins result ran them untuned
+_CL_ENV = os.environ.get('VFD_CHANNELS_LAST', 'auto')
 
 
 def _use_channels_last(training, bf16):
     cl = training.get('channels_last')
     if cl is None:
-        cl = _CL_ENV == 'all' or (bf16 and _CL_ENV != '0')
+        cl = (_CL_ENV == 'all' or (bf16 and _CL_ENV != '0')
+              or (_CL_ENV == 'auto' and bool(torch.backends.cudnn.benchmark)))
     return bool(cl)
 
 

@@ -23,9 +23,12 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 # MIOpen's user find/perf database: a committed one (tuned on MI355X) makes conv-solver choice
-# reproducible and skips the per-shape search on a fresh box.  Must be set before MIOpen loads.
-if os.path.isdir(os.path.join(ROOT, 'miopen_db')):
-    os.environ.setdefault('MIOPEN_USER_DB_PATH', os.path.join(ROOT, 'miopen_db'))
+# reproducible and skips the per-shape search on a fresh box.  Must be set before MIOpen loads; a
+# private copy per process, so records other runs write never reach the committed picks
+# (vfdepth_amd/miopen_db.py).
+sys.path.insert(0, ROOT)
+from vfdepth_amd.miopen_db import use_private_copy  # noqa: E402
+use_private_copy()
 
 import threading  # noqa: E402
 

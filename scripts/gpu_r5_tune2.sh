@@ -7,6 +7,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 OUT=gpurun_out/r5/tune2
 mkdir -p $OUT
 export PYTHONUNBUFFERED=1
+export MIOPEN_USER_DB_PATH=$GRAFT_REPO_ROOT/miopen_db   # the tuning run writes the committed db
 B="--no-cpu-baseline --no-parity --steps 10 --warmup 3"
 VFD_CHANNELS_LAST=all timeout -k 10 900 python bench.py $B --conv-autotune 1 > $OUT/cl_tune.json 2> $OUT/cl_tune.err || exit $?
 mkdir -p $OUT/db && cp miopen_db/* $OUT/db/

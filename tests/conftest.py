@@ -8,6 +8,11 @@ for p in (ROOT, os.path.join(ROOT, 'tests', 'golden')):
     if p not in sys.path:
         sys.path.insert(0, p)
 
+# the tests' MIOpen runs work on a private copy of the committed find-db (they would otherwise
+# write their immediate-mode records into it, vfdepth_amd/miopen_db.py)
+from vfdepth_amd.miopen_db import use_private_copy  # noqa: E402
+use_private_copy()
+
 
 def pytest_configure(config):
     config.addinivalue_line('markers', 'gpu: needs an MI355X (HIP) device')

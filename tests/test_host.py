@@ -160,3 +160,28 @@ def test_batched_pose_and_warp_matrices_match_per_camera():
     batched = vr.warp_matrices(inputs, outputs, None, list(range(N)))
     assert batched.shape == per_cam.shape
     assert torch.equal(batched, per_cam)
+
+
+def test_fold_weights_backward_matches_autograd_slices():
+    """kernels.FoldWeights (K1's folded 1x1 columns, one direct backward) against autograd through
+    VFNet.folded_weights' slice / cat / stack form, on the CPU in float64."""
+    from vfdepth_amd import kernels as KN
+    torch.manual_seed(0)
+    Cv, C = 5, 7
+    groups = KN.overlap_group_table(6)
+    w_no = torch.randn(Cv, C + 1, 1, dtype=torch.float64, requires_grad=True)
+    w_o = torch.randn(Cv, 2 * C + 2, 1, dtype=torch.float64, requires_grad=True)
+    gf = torch.randn(6, 2 * Cv, C, dtype=torch.float64)
+    gz = torch.randn(3, Cv, dtype=torch.float64)
+    wf, wz = KN.FoldWeights.apply(w_no, w_o, groups)
+    ((wf * gf).sum() + (wz * gz).sum()).backward()
+    a_no, a_o = w_no.grad.clone(), w_o.grad.clone()
+    w_no.grad = w_o.grad = None
+    wn, wo = w_no[:, :, 0], w_o[:, :, 0]
+    halves = [wo[:, :C], wo[:, C + 1:2 * C + 1]]
+    rf = torch.stack([torch.cat([wn[:, :C], halves[g]], 0) for g in groups], 0)
+    rz = torch.stack([wn[:, C], wo[:, C], wo[:, 2 * C + 1]], 0)
+    assert torch.equal(wf, rf) and torch.equal(wz, rz)
+    ((rf * gf).sum() + (rz * gz).sum()).backward()
+    torch.testing.assert_close(a_no, w_no.grad, rtol=1e-12, atol=1e-12)
+    torch.testing.assert_close(a_o, w_o.grad, rtol=1e-12, atol=1e-12)

@@ -45,12 +45,12 @@ def _flat(x):
 
 def report(kind, name, ins, outs):
     torch.cuda.synchronize()
-    if FIRST:
+    if len(FIRST) >= 30:
         return
     bi, bo = _nan(_flat(ins)), _nan(_flat(outs))
     if bo and not bi:
         FIRST.append(f'{kind} {name}: NaN-free inputs, NaN in outputs {bo}')
-        print('FIRST NaN PRODUCER:', FIRST[-1], flush=True)
+        print('NaN PRODUCER:', FIRST[-1], flush=True)
 
 
 def wrap_functions():
@@ -77,7 +77,7 @@ def wrap_functions():
 class AtenCheck(TorchDispatchMode):
     def __torch_dispatch__(self, func, types, args=(), kwargs=None):
         out = func(*args, **(kwargs or {}))
-        if not FIRST and 'fill' not in str(func) and 'empty' not in str(func):
+        if len(FIRST) < 30 and 'fill' not in str(func) and 'empty' not in str(func):
             report('aten', str(func), list(args) + list((kwargs or {}).values()), out)
         return out
 
@@ -94,7 +94,11 @@ def main():
     from vfdepth_amd.layers import seeded_state_dict
     from vfdepth_amd.vfdepth import VFDepthAlgo
     _lib.load()
-    cfg, name = bench.make_cfg(a.config)
+    if a.config < 0:                       # the graph-replay test's configuration
+        import common as G
+        cfg = G.step_cfg()
+    else:
+        cfg, name = bench.make_cfg(a.config)
     algo = VFDepthAlgo(cfg, 0)
     for m in algo.models.values():
         m.load_state_dict(seeded_state_dict(m, seed=7))
@@ -108,8 +112,12 @@ def main():
     free, _ = torch.cuda.mem_get_info()
     poison = torch.empty(int(free * 0.7) // 4, dtype=torch.int32, device='cuda:0')
     poison.fill_(-1)
+    # the small pool (blocks <= 1 MB, 2 MB segments) is separate: poison 4 GB of it too
+    small = [torch.empty(256 * 1024, dtype=torch.int32, device='cuda:0') for _ in range(4096)]
+    for t in small:
+        t.fill_(-1)
     torch.cuda.synchronize()
-    del poison
+    del poison, small
     algo.optimizer.zero_grad(set_to_none=True)
     if a.aten:
         with AtenCheck():
@@ -122,7 +130,9 @@ def main():
     bad = [n for n, p in ((n, p) for m in algo.models.values() for n, p in m.named_parameters())
            if p.grad is not None and bool(torch.isnan(p.grad).any())]
     print('poisoned step total_loss', float(losses['total_loss']), 'NaN grads in', len(bad), 'params', bad[:5], flush=True)
-    print('first NaN producer:', FIRST[0] if FIRST else 'none', flush=True)
+    print('NaN producers:', len(FIRST), flush=True)
+    for f in FIRST:
+        print('  ', f, flush=True)
 
 
 if __name__ == '__main__':

@@ -30,7 +30,9 @@ def main():
     ap.add_argument('--config', type=int, default=2)
     ap.add_argument('--top', type=int, default=60)
     ap.add_argument('--match', default='transpose,SubTensor,add,copy,Fill,reduce')
+    ap.add_argument('--autotune', type=int, default=1, help='MIOpen benchmark mode, as bench.py defaults')
     a = ap.parse_args()
+    torch.backends.cudnn.benchmark = bool(a.autotune)
     _lib.load()
     cfg, name = bench.make_cfg(a.config)
     algo = VFDepthAlgo(cfg, 0)
@@ -38,7 +40,7 @@ def main():
         m.load_state_dict(seeded_state_dict(m, seed=7))
     algo.set_train()
     batch = synth.make_batch(cfg, seed=1234, device='cuda:0')
-    for _ in range(3):
+    for _ in range(4):
         algo.train_step(dict(batch))
     torch.cuda.synchronize()
     from torch.profiler import ProfilerActivity, profile

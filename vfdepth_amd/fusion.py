@@ -228,13 +228,16 @@ class VFNet(nn.Module):
     def augment_extrinsics(self, ext):
         """Random rotation in front of every camera (volumetric_fusionnet.py:269-287): the angles
         are the reference's `torch.rand(b, cam, 3)` draw on the CPU global generator, scaled by
-        `aug_angle` (used as radians, as the reference does); no gradient."""
+        `aug_angle` (used as radians, as the reference does); no gradient.  Under HIP-graph
+        capture the draw is on the device generator instead (a CPU draw and its host->device copy
+        would be frozen into the graph: every replay would reuse the capture step's rotation)."""
         with torch.no_grad():
             b, cam = ext.shape[:2]
-            angle = torch.rand(b, cam, 3)
+            capturing = ext.is_cuda and torch.cuda.is_current_stream_capturing()
+            angle = torch.rand(b, cam, 3, device=ext.device if capturing else 'cpu')
             for i in range(3):
                 angle[:, :, i] = (angle[:, :, i] - 0.5) * self.aug_angle[i]
-            tform = torch.eye(4).repeat(b, cam, 1, 1)
+            tform = torch.eye(4, device=angle.device).repeat(b, cam, 1, 1)
             tform[:, :, :3, :3] = axis_angle_to_matrix(angle)
             return tform.to(device=ext.device, dtype=ext.dtype) @ ext
 

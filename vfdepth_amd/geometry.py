@@ -62,9 +62,9 @@ def vec_to_matrix(rot_angle, trans_vec, invert=False):
     return torch.matmul(R, Tm) if invert else torch.matmul(Tm, R)
 
 
-# the fused pose net's frame pairs as one batch: opt-in (VFD_POSE_PAIRS=1) until the illegal
-# address its first HIP-graph replay hit in round 5 is understood
-_POSE_PAIRS = os.environ.get('VFD_POSE_PAIRS', '0') == '1'
+# the fused pose net's frame pairs as one batch in eager steps (VFD_POSE_PAIRS=0 turns it off):
+# config 2 31.3/32.2 vs 34.5/33.9 ms/step on one box, alternating runs (round 5)
+_POSE_PAIRS = os.environ.get('VFD_POSE_PAIRS', '1') == '1'
 
 
 class Pose:
@@ -88,8 +88,8 @@ class Pose:
         return {('cam', c): self.get_single_pose(net, inputs, c) for c in range(self.num_cams)}
 
     def get_single_pose(self, net, inputs, cam):
-        """pose.py:31-42: one net call per context frame (pairs in temporal order).  With
-        VFD_POSE_PAIRS=1 the fused pose net takes all pairs in ONE call: its stacked-batch forward
+        """pose.py:31-42: one net call per context frame (pairs in temporal order).  By default
+        (VFD_POSE_PAIRS=1) the fused pose net takes all pairs in ONE call: its stacked-batch forward
         gives each pair exactly the reference call's BatchNorm statistics."""
         out = {}
         fids = self.frame_ids[1:]

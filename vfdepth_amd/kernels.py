@@ -1388,6 +1388,19 @@ def _to_nhwc(x, dtype):
     return y
 
 
+_GROUP_CAMS = {}
+
+
+def _group_cams(groups, g, device):
+    """Device index of the cameras in overlap group g, made once per (groups, device): the first
+    (eager) step builds it, so a captured step holds no host->device copy."""
+    key = (tuple(groups), g, str(device))
+    if key not in _GROUP_CAMS:
+        cams = [n for n, gg in enumerate(groups) if gg == g]
+        _GROUP_CAMS[key] = torch.tensor(cams, dtype=torch.long, device=device) if cams else None
+    return _GROUP_CAMS[key]
+
+
 class FoldWeights(torch.autograd.Function):
     """K1's folded 1x1-conv columns (VFNet.folded_weights): from conv_non_overlap's weight W_no
     [Cv, C+1, 1] and conv_overlap's W_o [Cv, 2C+2, 1] (volumetric_fusionnet.py:197-230) ->
@@ -1418,9 +1431,9 @@ class FoldWeights(torch.autograd.Function):
         if dwf is not None:
             torch.sum(dwf[:, :Cv, :], 0, out=dno[:, :C])
             for g, lo in ((0, 0), (1, C + 1)):
-                cams = [n for n, gg in enumerate(ctx.groups) if gg == g]
-                if cams:
-                    torch.sum(dwf[cams, Cv:, :], 0, out=do[:, lo:lo + C])
+                cams = _group_cams(ctx.groups, g, dev)
+                if cams is not None:
+                    torch.sum(dwf.index_select(0, cams)[:, Cv:, :], 0, out=do[:, lo:lo + C])
         if dwz is not None:
             dno[:, C] = dwz[0]
             do[:, C] = dwz[1]

@@ -13,6 +13,7 @@ for the GPU:
   default) or, for bit-level parity with the reference, from the CPU global RNG exactly as the
   reference draws it (`noise_mode='cpu_global'`).
 """
+import contextlib
 import os
 from collections import defaultdict
 
@@ -20,6 +21,7 @@ import torch
 import torch.distributed as dist
 import torch.nn.functional as F
 import torch.optim as optim
+from torch.utils._python_dispatch import TorchDispatchMode
 from torch.utils.data import DataLoader
 
 from . import fusion
@@ -27,10 +29,49 @@ from .config import flatten
 from .geometry import Pose, ViewRendering, inverse4x4
 from .losses import DepthSynLoss, MultiCamLoss, SingleCamLoss
 from .network import FusedDepthNet, FusedPoseNet, MonoDepthNet, MonoPoseNet
+from .rotation import _qm_consts
 from .synth import SyntheticSurroundDataset
 
 _NO_DEVICE_KEYS = ['idx', 'dataset_idx', 'sensor_name', 'filename']
 _OPTIMIZER_NAME = 'adam'
+
+
+class _CaptureCheck(TorchDispatchMode):
+    """VFD_GRAPH_CHECK=1: every framework op of the captured step whose tensors are on both the host
+    and the device is recorded.  A host->device copy inside a capture is a graph node that reads the
+    host buffer at every replay — long after the temporary it copied from was freed — and its value
+    is frozen at the capture step's.  The captured step must have none."""
+
+    def __init__(self):
+        super().__init__()
+        self.found = []
+
+    def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+        out = func(*args, **(kwargs or {}))
+        devs = set()
+        for t in torch.utils._pytree.tree_leaves((args, kwargs or {}, out)):
+            if torch.is_tensor(t):
+                devs.add(t.device.type)
+        if 'cpu' in devs and 'cuda' in devs:
+            shapes = [tuple(t.shape) for t in torch.utils._pytree.tree_leaves(args) if torch.is_tensor(t)]
+            self.found.append(f'{func} {shapes}')
+        return out
+
+    def live_graph_before_capture(self):
+        """Tensors of an earlier step's autograd graph still alive when the capture starts keep
+        that step's AccumulateGrad nodes (and their stream) in use by the captured backward."""
+        import gc
+        gc.collect()
+        for o in gc.get_objects():
+            try:
+                if torch.is_tensor(o) and o.grad_fn is not None:
+                    self.found.append(f'live autograd graph before capture: {tuple(o.shape)} {type(o.grad_fn).__name__}')
+            except Exception:       # objects that refuse inspection
+                continue
+
+    def raise_if_any(self):
+        if self.found:
+            raise RuntimeError('host<->device transfers inside the captured step:\n  ' + '\n  '.join(self.found[:20]))
 
 
 class VFDepthAlgo:
@@ -317,12 +358,26 @@ class VFDepthAlgo:
             for _ in range(warmup):
                 self.train_step(dict(static))
         torch.cuda.current_stream(self.device).wait_stream(side)
+        # constants the captured step builds on the device (the augmented view's rotation is drawn
+        # on the device generator under capture): made here, so no host->device copy is captured
+        _qm_consts(self.device, torch.float32)
         graph = torch.cuda.CUDAGraph()
+        dump = os.environ.get('VFD_GRAPH_DUMP')          # diagnostics: the captured graph as DOT
+        if dump:
+            graph.enable_debug_mode()
         self.optimizer.zero_grad(set_to_none=True)
+        check = _CaptureCheck() if os.environ.get('VFD_GRAPH_CHECK') == '1' else contextlib.nullcontext()
+        if isinstance(check, _CaptureCheck):
+            check.live_graph_before_capture()
         with torch.cuda.graph(graph):
-            static_outputs, static_losses = self.process_batch(dict(static), self.rank)
-            static_losses['total_loss'].backward()
-            self.optimizer.step()
+            with check:
+                static_outputs, static_losses = self.process_batch(dict(static), self.rank)
+                static_losses['total_loss'].backward()
+                self.optimizer.step()
+        if isinstance(check, _CaptureCheck):
+            check.raise_if_any()
+        if dump:
+            graph.debug_dump(dump)
 
         def step(new_batch=None):
             if new_batch is not None:

@@ -495,6 +495,15 @@ int vfd_depth_syn_fwd(const vfd_depthsyn_desc* d, const float* aug_depth, const 
 int vfd_depth_syn_bwd(const vfd_depthsyn_desc* d, const float* aug_depth, const float* depth, const float* mask,
                       const float* invK, const float* M, const float* zrow, const float* g, float* d_aug,
                       float* d_depth, void* stream);
+/* The same backward with d_depth summed in exact 128-bit fixed point (2^-100 resolution, |sum| < 2^26;
+ * integer adds, so the result does not depend on the order the scattered contributions land in):
+ * the deterministic mode's form (torch.backends.cudnn.deterministic / VFD_DETERMINISTIC=1).
+ * workspace >= vfd_depth_syn_bwd_ordered_workspace(d) bytes (16 per source pixel). */
+size_t vfd_depth_syn_bwd_ordered_workspace(const vfd_depthsyn_desc* d);
+int vfd_depth_syn_bwd_ordered(const vfd_depthsyn_desc* d, const float* aug_depth, const float* depth,
+                              const float* mask, const float* invK, const float* M, const float* zrow,
+                              const float* g, float* d_aug, float* d_depth, void* workspace, size_t ws_bytes,
+                              void* stream);
 
 /* ------------------------------------------------------------------ photometric losses (K5) */
 typedef struct vfd_photo_desc {

@@ -846,6 +846,40 @@ def test_depth_synthesis_kernel_against_reference():
     gclose(td.grad, fx['d_tar_depth'], 'd augmented-view depth')
 
 
+def test_depth_synthesis_ordered_backward(monkeypatch):
+    """The deterministic mode's depth-synthesis backward (vfd_depth_syn_bwd_ordered: the scattered
+    source-depth gradient summed in 128-bit fixed point) against the reference fixture, bitwise
+    equal over repeated runs, and within fp32 summation error of the atomic form."""
+    from vfdepth_amd import kernels as KN
+    fx = golden('virtual_depth.npz')
+    c = G.virtual_depth_case()
+    B = c['src_depth'].shape[0]
+    T = c['T'].to(DEV)
+    M = (c['src_K'].to(DEV) @ torch.inverse(T))[:, :3, :].reshape(B, 1, 1, 3, 4).contiguous()
+    zrow = T[:, 2, :].reshape(B, 1, 1, 4).contiguous()
+    tab = torch.zeros(1, 1, dtype=torch.int32, device=DEV)
+    invK = c['tar_invK'].to(DEV).reshape(B, 1, 4, 4)
+    gout = G.seeded_randn(fx['depth'].shape, 61).to(DEV)
+
+    def grads(det):
+        monkeypatch.setenv('VFD_DETERMINISTIC', '1' if det else '0')
+        sd = c['src_depth'].to(DEV).requires_grad_(True)
+        td = c['tar_depth'].to(DEV).requires_grad_(True)
+        d, _ = KN.DepthSynthesis.apply(tab, c['min_depth'], c['max_depth'], td, sd,
+                                       c['src_mask'].to(DEV)[:, 0:1], invK, M, zrow)
+        (d[:, :, 0] * gout).sum().backward()
+        return sd.grad.clone(), td.grad.clone()
+
+    ref_s, ref_t = grads(False)
+    runs = [grads(True) for _ in range(3)]
+    for s_, t_ in runs[1:]:
+        assert torch.equal(s_, runs[0][0]) and torch.equal(t_, runs[0][1]), 'ordered backward not reproducible'
+    gclose(runs[0][0], fx['d_src_depth'], 'd source depth (ordered)')
+    gclose(runs[0][1], fx['d_tar_depth'], 'd augmented-view depth (ordered)')
+    assert torch.equal(runs[0][1], ref_t)             # the per-pixel gradient has no scatter
+    torch.testing.assert_close(runs[0][0], ref_s, rtol=1e-5, atol=1e-7)
+
+
 def test_full_step_depth_synthesis_against_reference():
     """The aug_depth step (ddad_surround_fusion_augdepth.yaml: augment_extrinsics, second K3C +
     decoder pass, depth synthesis, DepthSynLoss) against the reference's step fixture: every loss

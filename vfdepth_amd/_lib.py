@@ -156,6 +156,8 @@ _SIGS = {
     'vfd_pad_conv_dgrad_bf16_t': (c_int, [ctypes.POINTER(ConvDesc)] + [c_fp] * 3 + [c_int, c_fp, c_size_t, c_void_p]),
     'vfd_depth_syn_fwd': (c_int, [ctypes.POINTER(DepthSynDesc)] + [c_fp] * 8 + [c_void_p]),
     'vfd_depth_syn_bwd': (c_int, [ctypes.POINTER(DepthSynDesc)] + [c_fp] * 9 + [c_void_p]),
+    'vfd_depth_syn_bwd_ordered_workspace': (ctypes.c_size_t, [ctypes.POINTER(DepthSynDesc)]),
+    'vfd_depth_syn_bwd_ordered': (c_int, [ctypes.POINTER(DepthSynDesc)] + [c_fp] * 10 + [ctypes.c_size_t, c_void_p]),
     'vfd_smooth_workspace_bytes': (c_size_t, [c_int] * 4),
     'vfd_smooth_fwd': (c_int, [c_int] * 4 + [c_fp] * 5 + [c_size_t, c_void_p]),
     'vfd_smooth_bwd': (c_int, [c_int] * 4 + [c_fp] * 5 + [c_void_p]),

@@ -10,7 +10,9 @@
 // materialised (each bilinear tap recomputes its source pixel's z from the source depth).
 //   depth_syn_fwd_k  -> tform_depth [B,N,S,H,W], tform_mask [B,N,S,H,W]
 //   depth_syn_bwd_k  -> d aug_depth (per pixel, summed over the sources: no atomics) and
-//                       d depth of the sources (the bilinear transpose: f32 atomics)
+//                       d depth of the sources (the bilinear transpose: f32 atomics, or — the
+//                       ordered form — exact 128-bit fixed-point integer sums, whose value does
+//                       not depend on the order the atomics land in)
 #include "vfd_common.h"
 
 namespace vfd {
@@ -121,11 +123,57 @@ __global__ __launch_bounds__(256) void depth_syn_fwd_k(vfd_depthsyn_desc d, cons
   }
 }
 
+// Ordered (deterministic) accumulation: a contribution v is the signed 128-bit integer
+// round-toward-zero(v * 2^DS_FRAC) (exact for |v| >= 2^-DS_FRAC+23, |v| < 2^26), added to the
+// pixel's (hi, lo) pair by two 64-bit integer atomics with the low word's carry passed on.
+// Integer addition is associative, so the pair ends the same whatever order the adds land in.
+constexpr int DS_FRAC = 100;
+
+__device__ __forceinline__ void ds_fixed_add(unsigned long long* __restrict__ cell, float v) {
+  const unsigned u = __float_as_uint(v);
+  const int ex = (int)((u >> 23) & 255u);
+  if (ex == 0) return;                               // zero / denormal (< 1.2e-38): nothing
+  const int sh = ex - 127 - 23 + DS_FRAC;            // v = m * 2^(ex - 150), m < 2^24
+  if (sh <= -24) return;                             // below the fixed-point resolution
+  const unsigned long long m = (unsigned long long)((u & 0x7FFFFFu) | 0x800000u);
+  unsigned long long lo, hi;
+  if (sh < 0) {
+    lo = m >> -sh;
+    hi = 0ull;
+  } else if (sh < 64) {
+    lo = m << sh;
+    hi = sh > 40 ? m >> (64 - sh) : 0ull;
+  } else {
+    lo = 0ull;
+    hi = m << (sh - 64);                               // sh <= 102 for |v| < 2^26
+  }
+  if (u >> 31) {                                     // two's complement of the 128-bit value
+    lo = ~lo + 1ull;
+    hi = ~hi + (lo == 0ull ? 1ull : 0ull);
+  }
+  const unsigned long long old = atomicAdd(cell + 1, lo);
+  const unsigned long long carry = old + lo < old ? 1ull : 0ull;
+  atomicAdd(cell, hi + carry);
+}
+
+// d_depth from the fixed-point pairs [hi, lo]
+__global__ __launch_bounds__(256) void depth_syn_fixed_k(const unsigned long long* __restrict__ acc, size_t n,
+                                                         float* __restrict__ d_depth) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const long long hi = (long long)acc[2 * i];
+  const unsigned long long lo = acc[2 * i + 1];
+  // + the non-finite contributions, which went to d_depth itself (0 when there were none)
+  d_depth[i] = (float)((double)hi * 0x1p-36 + (double)lo * 0x1p-100) + d_depth[i];
+}
+
+template <bool ORDERED>
 __global__ __launch_bounds__(256) void depth_syn_bwd_k(vfd_depthsyn_desc d, const float* __restrict__ aug_depth,
                                                        const float* __restrict__ depth, const float* __restrict__ mask,
                                                        const float* __restrict__ invK, const float* __restrict__ M,
                                                        const float* __restrict__ zrow, const float* __restrict__ g,
-                                                       float* __restrict__ d_aug, float* __restrict__ d_depth) {
+                                                       float* __restrict__ d_aug, float* __restrict__ d_depth,
+                                                       unsigned long long* __restrict__ fixed) {
   const int HW = d.H * d.W;
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   const int bc = blockIdx.y, b = bc / d.N, c = bc % d.N;
@@ -149,7 +197,11 @@ __global__ __launch_bounds__(256) void depth_syn_bwd_k(vfd_depthsyn_desc d, cons
     // values: d z_k = g w_k -> d source depth = g w_k dz/ddepth (grid_sampler_2d_backward's scatter)
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-      if (sm.q[k] >= 0) atomicAdd(d_depth + sb * HW + sm.q[k], gv * sm.bl.w[k] * sm.dz[k]);
+      if (sm.q[k] >= 0) {
+        const float v = gv * sm.bl.w[k] * sm.dz[k];
+        if (ORDERED && isfinite(v)) ds_fixed_add(fixed + 2 * (sb * HW + sm.q[k]), v);
+        else atomicAdd(d_depth + sb * HW + sm.q[k], v);   // (ordered form: non-finite values only)
+      }
     // coordinates (zeros padding: out-of-range taps contribute nothing)
     const float x0 = floorf(sm.ix), y0 = floorf(sm.iy), x1 = x0 + 1.f, y1 = y0 + 1.f;
     float gix = 0.f, giy = 0.f;
@@ -202,8 +254,34 @@ int vfd_depth_syn_bwd(const vfd_depthsyn_desc* d, const float* aug_depth, const 
   ProfScope ps(K_DEPTH_SYN_BWD, s);
   (void)hipMemsetAsync(d_depth, 0, sizeof(float) * (size_t)d->B * d->N * d->H * d->W, s);
   dim3 grid(cdiv(d->H * d->W, 256), d->B * d->N);
-  depth_syn_bwd_k<<<grid, 256, 0, s>>>(*d, aug_depth, depth, mask, invK, M, zrow, g, d_aug, d_depth);
+  depth_syn_bwd_k<false><<<grid, 256, 0, s>>>(*d, aug_depth, depth, mask, invK, M, zrow, g, d_aug, d_depth, nullptr);
   return fail_launch("depth_syn_bwd");
+}
+
+size_t vfd_depth_syn_bwd_ordered_workspace(const vfd_depthsyn_desc* d) {
+  if (!d || d->B <= 0 || d->N <= 0 || d->H <= 0 || d->W <= 0) return 0;
+  return (size_t)d->B * d->N * d->H * d->W * 2 * sizeof(unsigned long long);
+}
+
+int vfd_depth_syn_bwd_ordered(const vfd_depthsyn_desc* d, const float* aug_depth, const float* depth,
+                              const float* mask, const float* invK, const float* M, const float* zrow,
+                              const float* g, float* d_aug, float* d_depth, void* workspace, size_t ws_bytes,
+                              void* stream) {
+  if (int e = check_ds(d)) return e;
+  VFD_REQUIRE(aug_depth && depth && mask && invK && M && zrow && g && d_aug && d_depth && workspace,
+              "depth_syn_bwd_ordered: null argument");
+  const size_t need = vfd_depth_syn_bwd_ordered_workspace(d);
+  VFD_REQUIRE(ws_bytes >= need, "depth_syn_bwd_ordered: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  ProfScope ps(K_DEPTH_SYN_BWD, s);
+  auto* fixed = (unsigned long long*)workspace;
+  (void)hipMemsetAsync(fixed, 0, need, s);
+  (void)hipMemsetAsync(d_depth, 0, sizeof(float) * (size_t)d->B * d->N * d->H * d->W, s);
+  dim3 grid(cdiv(d->H * d->W, 256), d->B * d->N);
+  depth_syn_bwd_k<true><<<grid, 256, 0, s>>>(*d, aug_depth, depth, mask, invK, M, zrow, g, d_aug, d_depth, fixed);
+  const size_t n = (size_t)d->B * d->N * d->H * d->W;
+  depth_syn_fixed_k<<<(unsigned)cdiv((long long)n, 256), 256, 0, s>>>(fixed, n, d_depth);
+  return fail_launch("depth_syn_bwd_ordered");
 }
 
 }  // extern "C"

@@ -1255,9 +1255,17 @@ class DepthSynthesis(torch.autograd.Function):
         g = _dev(g, 'grad')
         d_aug = torch.empty_like(aug_depth)
         d_depth = torch.empty_like(depth)
-        L.check(lib.vfd_depth_syn_bwd(ctypes.byref(d), aug_depth.data_ptr(), depth.data_ptr(), mask.data_ptr(),
-                                      invK.data_ptr(), M.data_ptr(), zrow.data_ptr(), g.data_ptr(), d_aug.data_ptr(),
-                                      d_depth.data_ptr(), L.stream()), 'depth_syn_bwd')
+        if deterministic():          # exact fixed-point sums of the scattered source-depth gradient
+            nbytes = lib.vfd_depth_syn_bwd_ordered_workspace(ctypes.byref(d))
+            ws = _ws(nbytes, depth.device)
+            L.check(lib.vfd_depth_syn_bwd_ordered(ctypes.byref(d), aug_depth.data_ptr(), depth.data_ptr(),
+                                                  mask.data_ptr(), invK.data_ptr(), M.data_ptr(), zrow.data_ptr(),
+                                                  g.data_ptr(), d_aug.data_ptr(), d_depth.data_ptr(), ws.data_ptr(),
+                                                  nbytes, L.stream()), 'depth_syn_bwd_ordered')
+        else:
+            L.check(lib.vfd_depth_syn_bwd(ctypes.byref(d), aug_depth.data_ptr(), depth.data_ptr(), mask.data_ptr(),
+                                          invK.data_ptr(), M.data_ptr(), zrow.data_ptr(), g.data_ptr(),
+                                          d_aug.data_ptr(), d_depth.data_ptr(), L.stream()), 'depth_syn_bwd')
         return None, None, None, d_aug, d_depth, None, None, None, None
 
 

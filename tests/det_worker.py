@@ -9,6 +9,12 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.dirname(HERE), os.path.join(HERE, 'golden')]
 
+# MIOpen's deterministic switch selects among its deterministic solvers, but a find-db record (the
+# committed tuned picks include split-K weight gradients with atomics) is used as it stands: this
+# process gets an empty user db, whatever the parent (pytest's conftest copy) exported
+import tempfile  # noqa: E402
+os.environ['MIOPEN_USER_DB_PATH'] = tempfile.mkdtemp(prefix='vfd_det_db_')
+
 import torch  # noqa: E402
 
 torch.backends.cudnn.deterministic = True

@@ -460,7 +460,11 @@ def _check_recorded_ops(O, cfg, rec, inputs_cpu):
     lvl = int(cfg['model']['fusion_level']) + 1
     mask, K, Einv = inputs_cpu['mask'], inputs_cpu[('K', lvl)], torch.inverse(inputs_cpu['extrinsics'])
     C, Cv, Z = int(cfg['model']['fusion_feat_in_dim']), int(cfg['model']['voxel_pre_dim'][-1]), spec.Z
-    assert len(rec.calls['k1']) == 1 and len(rec.calls['k2']) == 2
+    # the pose net's two frame pairs: two K2 calls, or one over the stacked pairs (geometry.Pose's
+    # batched pairs, the default) — checked per pair either way
+    Bm = mask.shape[0]
+    k2 = [(f[j:j + Bm], o[j:j + Bm]) for f, o in rec.calls['k2'] for j in range(0, f.shape[0], Bm)]
+    assert len(rec.calls['k1']) == 1 and len(k2) == 2
     assert len(rec.calls['k3']) + len(rec.calls['k3c']) == 1
     net, _, _, _, feats, vox = rec.calls['k1'][0]
     c_no, c_o = net.conv_non_overlap[0], net.conv_overlap[0]
@@ -468,7 +472,7 @@ def _check_recorded_ops(O, cfg, rec, inputs_cpu):
         ref = O.fuse_depth(spec, feats.cpu(), mask, K, Einv, c_no.weight.cpu(), c_no.bias.cpu(),
                            c_o.weight.cpu(), c_o.bias.cpu())
     close(vox.permute(0, 2, 1), ref, 'K1 in the step')
-    for i, (feats, out) in enumerate(rec.calls['k2']):
+    for i, (feats, out) in enumerate(k2):
         with torch.no_grad():
             ref = O.fuse_pose(spec, feats.cpu(), mask, K, Einv)
         B = ref.shape[0]

@@ -252,7 +252,7 @@ int vfd_depth_syn_bwd(const vfd_depthsyn_desc* d, const float* aug_depth, const 
   VFD_REQUIRE(aug_depth && depth && mask && invK && M && zrow && g && d_aug && d_depth, "depth_syn_bwd: null argument");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_DEPTH_SYN_BWD, s);
-  (void)hipMemsetAsync(d_depth, 0, sizeof(float) * (size_t)d->B * d->N * d->H * d->W, s);
+  zero_async(d_depth, sizeof(float) * (size_t)d->B * d->N * d->H * d->W, s);
   dim3 grid(cdiv(d->H * d->W, 256), d->B * d->N);
   depth_syn_bwd_k<false><<<grid, 256, 0, s>>>(*d, aug_depth, depth, mask, invK, M, zrow, g, d_aug, d_depth, nullptr);
   return fail_launch("depth_syn_bwd");
@@ -275,8 +275,8 @@ int vfd_depth_syn_bwd_ordered(const vfd_depthsyn_desc* d, const float* aug_depth
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_DEPTH_SYN_BWD, s);
   auto* fixed = (unsigned long long*)workspace;
-  (void)hipMemsetAsync(fixed, 0, need, s);
-  (void)hipMemsetAsync(d_depth, 0, sizeof(float) * (size_t)d->B * d->N * d->H * d->W, s);
+  zero_async(fixed, need, s);
+  zero_async(d_depth, sizeof(float) * (size_t)d->B * d->N * d->H * d->W, s);
   dim3 grid(cdiv(d->H * d->W, 256), d->B * d->N);
   depth_syn_bwd_k<true><<<grid, 256, 0, s>>>(*d, aug_depth, depth, mask, invK, M, zrow, g, d_aug, d_depth, fixed);
   const size_t n = (size_t)d->B * d->N * d->H * d->W;

@@ -2523,7 +2523,7 @@ int vfd_fuse_depth_bwd(const vfd_voxel_desc* d, const float* d_vox, const float*
   hipStream_t s = (hipStream_t)stream;
   const int V = d->X * d->Y * d->Z;
   ProfScope ps(K_FUSE_DEPTH_BWD, s);         // the op: zero dP, scatter, partial reduction
-  (void)hipMemsetAsync(dP, 0, (size_t)d->B * d->N * d->h * d->w * 2 * d->Cv * sizeof(float), s);
+  zero_async(dP, (size_t)d->B * d->N * d->h * d->w * 2 * d->Cv * sizeof(float), s);
   dim3 grid(cdiv(cdiv(V, 64), 4), d->B);
   float* partial = (float*)ws;
   if (d->Cv <= 64)
@@ -2579,7 +2579,7 @@ int vfd_fusion_plan(const vfd_voxel_desc* d, const float* mask_lo, const float* 
   VFD_REQUIRE(2 * (size_t)host_tiles(d) * PSUB * sizeof(int) <= 160 * 1024, "feature map %dx%d too large for the tile index", d->h, d->w);
   hipStream_t s = (hipStream_t)stream;
   const int V = d->X * d->Y * d->Z;
-  (void)hipMemsetAsync(counts, 0, (size_t)d->B * d->N * sizeof(int), s);
+  zero_async(counts, (size_t)d->B * d->N * sizeof(int), s);
   dim3 grid(cdiv(V, 256), d->B);
   ProfScope ps(K_FUSION_PLAN, s);
   switch (d->N) {
@@ -2590,7 +2590,7 @@ int vfd_fusion_plan(const vfd_voxel_desc* d, const float* mask_lo, const float* 
   int* row_ptr = (int*)((char*)plan + plan_entries_bytes(d));
   int* cursor = (int*)((char*)row_ptr + plan_rowptr_bytes(d));
   TileItem* csr = (TileItem*)((char*)cursor + plan_cursor_bytes(d));
-  (void)hipMemsetAsync(cursor, 0, (size_t)d->B * d->N * host_tiles(d) * PSUB * sizeof(int), s);
+  zero_async(cursor, (size_t)d->B * d->N * host_tiles(d) * PSUB * sizeof(int), s);
   const dim3 egrid(cdiv(V, 256), d->B * d->N);
   const size_t hist = (size_t)host_tiles(d) * PSUB * sizeof(int);
   if (2 * hist > 64 * 1024) {
@@ -2810,7 +2810,7 @@ static void vpb_plan_launch(const vfd_voxel_desc* d, const float* invK, const fl
   const VpbPtrs p = vpb_ptrs(w, ws);
   const int ncell = d->B * g.ncell, nblk = cdiv(ncell, VB_SCAN), nb = d->B * g.ntile;
   const int hwD = d->h * d->w * d->D;
-  (void)hipMemsetAsync(p.cnt, 0, w.fold, s);   // counters + zero row
+  zero_async(p.cnt, w.fold, s);   // counters + zero row
   const int cpb = cdiv(hwD, 256);
   vpb_count_k<<<cpb * d->B * d->N, 256, 0, s>>>(*d, invK, E, p.cnt, p.rank, cpb);
   vpb_scan1_k<<<nblk, 256, 0, s>>>(p.cnt, ncell, p.ptr, p.bsum);

@@ -270,4 +270,26 @@ __device__ __forceinline__ int corner_offset(const vfd_voxel_desc& d, int k) {
 
 __host__ __device__ inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
 
+// Zero fill as a kernel (instead of hipMemsetAsync): a plain kernel node when a step is captured into
+// a HIP graph, 16-B stores, byte tail.  Zeroed counters / accumulators ahead of atomics use it.
+template <int Unused = 0>
+__global__ __launch_bounds__(256) void zero_fill_k(unsigned char* __restrict__ p, size_t bytes) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  const size_t mis = (size_t)((16u - ((uintptr_t)p & 15u)) & 15u);
+  const size_t head = mis < bytes ? mis : bytes;            // bytes up to the first 16-B boundary
+  unsigned char* q = p + head;
+  const size_t n16 = (bytes - head) / 16, tail = bytes - head - n16 * 16;
+  if (i < head) p[i] = 0;
+  for (size_t k = i; k < n16; k += stride) reinterpret_cast<uint4*>(q)[k] = make_uint4(0u, 0u, 0u, 0u);
+  if (i < tail) q[n16 * 16 + i] = 0;
+}
+
+static inline void zero_async(void* p, size_t bytes, hipStream_t s) {
+  if (bytes == 0) return;
+  size_t blocks = (bytes / 16 + 255) / 256;
+  blocks = blocks < 1 ? 1 : (blocks > 2048 ? 2048 : blocks);
+  zero_fill_k<<<(unsigned)blocks, 256, 0, s>>>((unsigned char*)p, bytes);
+}
+
 }  // namespace vfd

@@ -14,6 +14,7 @@ for the GPU:
   reference draws it (`noise_mode='cpu_global'`).
 """
 import contextlib
+import gc
 import os
 from collections import defaultdict
 
@@ -352,6 +353,9 @@ class VFDepthAlgo:
         # stacked-pair form's first replay hit an illegal address — eager steps
         # keep the stacked pairs
         self.pose.batch_pairs = False
+        # no autograd graph of an earlier step may survive into the warm-up or the capture: its
+        # AccumulateGrad nodes would carry their stream into the captured backward
+        gc.collect()
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):
@@ -361,6 +365,7 @@ class VFDepthAlgo:
         # constants the captured step builds on the device (the augmented view's rotation is drawn
         # on the device generator under capture): made here, so no host->device copy is captured
         _qm_consts(self.device, torch.float32)
+        gc.collect()
         graph = torch.cuda.CUDAGraph()
         dump = os.environ.get('VFD_GRAPH_DUMP')          # diagnostics: the captured graph as DOT
         if dump:

@@ -13,7 +13,7 @@ timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $OUT/stats -o run --output
 cd $GRAFT_REPO_ROOT
 TRACE=$(ls $OUT/stats/*/run_kernel_trace.csv $OUT/stats/run_kernel_trace.csv 2>/dev/null | head -1)
 STATS=$(ls $OUT/stats/*/run_kernel_stats.csv $OUT/stats/run_kernel_stats.csv 2>/dev/null | head -1)
-python tools/kernel_breakdown.py $TRACE --last 5 --skip ${SKIP_MARKS:-1} --top 70 > $OUT/breakdown.txt   # --skip 1: the parity step after the timed ones
+python tools/kernel_breakdown.py $TRACE --last 5 --skip ${SKIP_MARKS:-2} --top 70 > $OUT/breakdown.txt   # --skip 1: the parity step after the timed ones
 python tools/roofline_check.py $OUT/bench.json $STATS --trace $TRACE > $OUT/roofline_check.json
 echo "roofline_check rc=$?"
 gzip -f $TRACE

@@ -941,41 +941,64 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pcdf_main_k(PfGeom g, const flo
   const float2* wlane = reinterpret_cast<const float2*>(Wd) + (size_t)(wv * 64 + li) * 2 + lh;
   float2 bq[PD_PF][2];
   int pf_atom = a_lo, pf_it = 0;
+  // the prefetched atom's weight base (its channel chunk and n-tile), advanced once per atom: the
+  // per-iteration address is then one multiply-add
+  // (a uniform float2 offset, kept scalar; the lane's part is wlane)
+  unsigned pf_off = 0;
+  auto pf_set = [&]() {
+    const int t = pf_atom / PD_CHUNKS, ch = pf_atom - t * PD_CHUNKS;
+    pf_off = ((unsigned)(ch * (PD_OC / 4)) * (unsigned)g.np + (unsigned)(t / g.mtiles) * PD_N) * 2u;
+  };
+  pf_set();
   auto prefetch = [&](int slot) {
     if (pf_atom < a_hi) {
-      const int t = pf_atom / PD_CHUNKS, ch = pf_atom - t * PD_CHUNKS;
-      const int nt = t / g.mtiles;
       const int tap = pf_it >> 3, q = pf_it & 7;
-      const float2* w = wlane + ((size_t)(tap * (PC_O / 4) + ch * (PD_OC / 4) + q) * g.np + nt * PD_N) * 2;
+      const float2* w = wlane + (pf_off + (unsigned)(tap * (PC_O / 4) + q) * (unsigned)g.np * 2u);
       bq[slot][0] = w[0];
       bq[slot][1] = w[64];
-      if (++pf_it == PD_ITERS) { pf_it = 0; ++pf_atom; }
+      if (++pf_it == PD_ITERS) {
+        pf_it = 0;
+        ++pf_atom;
+        if (pf_atom < a_hi) pf_set();
+      }
     }
   };
 #pragma unroll
   for (int k = 0; k < PD_PF; ++k) prefetch(k);
+  int cur_t = -1;
+  int pyx[4];                                         // (row << 16) | column of the lane's pixels
   for (int atom = a_lo; atom < a_hi; ++atom) {
     const int t = atom / PD_CHUNKS, ch = atom - t * PD_CHUNKS;
     const PfTile tl = pf_tile(g, t);
-    int pyx[4];                                       // (row << 16) | column of the lane's pixels
+    if (t != cur_t) {                                 // pixel geometry once per tile (8 atoms)
+      cur_t = t;
 #pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      int m = tl.m0 + 32 * a + li;
-      m = m < hw ? m : hw - 1;                        // pixels past the camera: computed, never stored
-      const int y = m / g.w;
-      pyx[a] = (y << 16) | (m - y * g.w);
+      for (int a = 0; a < 4; ++a) {
+        int m = tl.m0 + 32 * a + li;
+        m = m < hw ? m : hw - 1;                      // pixels past the camera: computed, never stored
+        const int y = m / g.w;
+        pyx[a] = (y << 16) | (m - y * g.w);
+      }
     }
     const float* xb = pd_lds + ((atom - a_lo) & 1) * g.lds_floats;
     // per-lane LDS offset of tap `tap`: the A row (the fold row for row 1 at ky = 2 and row h-2 at
-    // ky = 0) and column (E1 / E2 for the column folds)
+    // ky = 0) and column (E1 / E2 for the column folds).  Plain position: base + the tap's uniform
+    // (ky, kx) step; a fold replaces the column (px = 1 at kx = 2 -> E1 = column w+4, px = w-2 at
+    // kx = 0 -> E2 = column w+5) or the row (the staged fold row hrows) — uniform deltas per tap
+    // and tile, added where the lane's pixel matches the tap's fold column / row
     auto offsets = [&](int tap, int* o1) {
       const int ky = tap / 3, kx = tap - 3 * ky;
+      const int step = (ky * g.cols + kx) * PD_XS;
+      const int fcol = kx == 2 ? 1 : (kx == 0 ? g.w - 2 : -1);
+      const int dcol = (kx == 2 ? g.w : 6) * PD_XS;
+      const int frow = ky == 2 ? 1 : (ky == 0 ? g.h - 2 : -1);
+      const int drow = (g.hrows - (ky == 2 ? 3 - tl.y0 : g.h - 2 - tl.y0)) * g.cols * PD_XS;
+      const int r1 = g.cols * PD_XS, r2 = 2 * g.cols * PD_XS;   // a tile's pixels sit in rows y0 .. y0+2
 #pragma unroll
       for (int a = 0; a < 4; ++a) {
-        const int px = pyx[a] & 0xFFFF, py = pyx[a] >> 16;
-        const int col = (px == 1 && kx == 2) ? g.w + 4 : (px == g.w - 2 && kx == 0) ? g.w + 5 : px + 1 + kx;
-        const bool frow = (py == 1 && ky == 2) || (py == g.h - 2 && ky == 0);
-        o1[a] = ((frow ? g.hrows : py - tl.y0 + ky) * g.cols + col) * PD_XS + 2 * lh;
+        const int px = pyx[a] & 0xFFFF, py = pyx[a] >> 16, dy = py - tl.y0;
+        const int rowo = dy == 0 ? 0 : (dy == 1 ? r1 : r2);
+        o1[a] = rowo + (px + 1) * PD_XS + 2 * lh + step + (px == fcol ? dcol : 0) + (py == frow ? drow : 0);
       }
     };
     int o1c[4];
@@ -1014,6 +1037,10 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pcdf_main_k(PfGeom g, const flo
     if (ch == PD_CHUNKS - 1 || atom == a_hi - 1) {
       const int ts = t * PD_CHUNKS;
       if (ts >= a_lo && ts + PD_CHUNKS <= a_hi) {     // whole tile in this range: store
+        // the tile's 128 pixels span <= 3 rows from y0 (w >= 64): row / column by two compares;
+        // element indices within the camera in 32 bits (pf_supported: one camera's padded map < 2^32)
+        const int mr0 = tl.m0 - tl.y0 * g.w;          // the tile's first pixel within row y0
+        float* dcam = dx + (size_t)tl.bc * (g.h + 2) * (g.w + 2) * g.ntot;
 #pragma unroll
         for (int a = 0; a < 4; ++a)
 #pragma unroll
@@ -1021,10 +1048,14 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pcdf_main_k(PfGeom g, const flo
             const int n = tl.nt * PD_N + wv * 64 + b * 32 + li;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-              const int m = tl.m0 + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * lh;
-              if (m < hw && n < g.ntot) {
-                const int y = m / g.w, x = m - y * g.w;
-                dx[(((size_t)tl.bc * (g.h + 2) + y + 1) * (g.w + 2) + x + 1) * g.ntot + n] = acc[a][b][r];
+              const int mo = 32 * a + (r & 3) + 8 * (r >> 2) + 4 * lh;
+              const int mr = mr0 + mo;
+              const int dy = (mr >= g.w ? 1 : 0) + (mr >= 2 * g.w ? 1 : 0);
+              const int x = mr - dy * g.w;
+              if (tl.m0 + mo < hw && n < g.ntot) {
+                const unsigned e = ((unsigned)(tl.y0 + dy + 1) * (unsigned)(g.w + 2) + (unsigned)(x + 1)) *
+                                   (unsigned)g.ntot + (unsigned)n;
+                dcam[e] = acc[a][b][r];
               }
               acc[a][b][r] = 0.f;
             }
@@ -1100,6 +1131,7 @@ static bool pf_supported(const vfd_voxel_desc& d) {
   if (d.Cv != PC_CV || d.B <= 0 || d.N <= 0 || d.h < 6 || d.w < 3 || d.D <= 0 || d.D > 64) return false;
   const PfGeom g = pf_plan(d);
   if (g.hrows > 5) return false;                      // a tile spans <= 3 pixel rows (w >= 64)
+  if ((size_t)(d.h + 2) * (d.w + 2) * g.ntot >= ((size_t)1 << 32)) return false;
   return (size_t)2 * g.lds_floats * sizeof(float) <= PD_LDS_MAX;
 }
 

@@ -79,13 +79,15 @@ __device__ __forceinline__ void pp_stage(const PpGeom& g, float* __restrict__ ds
   const int r0 = g.s * tl.ymin;
   const float* src = x + ((size_t)tl.b * g.hp + r0) * g.wp * g.cin + c;
   const bool cok = c < g.cin;
+  // positions p < plim lie in rows r0 + p / wp < hp (no per-position division)
+  const int plim = min(npos, (g.hp - r0) * g.wp);
   for (int p0 = tid / QP; p0 < npos; p0 += 4 * PPP) {
     float4 v[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int p = p0 + PPP * u;
       v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (cok && p < npos && r0 + p / g.wp < g.hp)
+      if (cok && p < plim)
         v[u] = *reinterpret_cast<const float4*>(src + (size_t)p * g.cin);
     }
 #pragma unroll
@@ -149,28 +151,36 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppc_main_k(PpGeom g, const floa
   const float2* wlane = reinterpret_cast<const float2*>(Wf) + (size_t)(wv * 64 + li) * 2 + lh;
   float2 bq[PF][2];
   int pf_atom = a_lo, pf_it = 0;
+  int pf_ch = a_lo % g.nchunk;                        // the prefetched atom's channel chunk
   auto prefetch = [&](int slot) {
     if (pf_atom < a_hi) {
-      const int ch = pf_atom % g.nchunk;
       const int tap = pf_it / (CC / 4), q = pf_it % (CC / 4);
-      const float2* w = wlane + (size_t)(tap * g.cq + ch * (CC / 4) + q) * (2 * PP_O);
+      const float2* w = wlane + (size_t)(tap * g.cq + pf_ch * (CC / 4) + q) * (2 * PP_O);
       bq[slot][0] = w[0];
       bq[slot][1] = w[64];
-      if (++pf_it == ITERS) { pf_it = 0; ++pf_atom; }
+      if (++pf_it == ITERS) {
+        pf_it = 0;
+        ++pf_atom;
+        pf_ch = pf_ch + 1 == g.nchunk ? 0 : pf_ch + 1;
+      }
     }
   };
 #pragma unroll
   for (int k = 0; k < PF; ++k) prefetch(k);
+  int cur_t = -1;
+  int aoff[4];                                        // the lane's pixels' LDS offsets (per tile)
   for (int atom = a_lo; atom < a_hi; ++atom) {
     const int t = atom / g.nchunk, ch = atom - t * g.nchunk;
     const PpTile tl = pp_tile(g, t);
-    int aoff[4];
+    if (t != cur_t) {                                 // pixel geometry once per tile
+      cur_t = t;
 #pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      int m = tl.m0 + 32 * a + li;
-      m = m < g.mimg ? m : g.mimg - 1;                 // pixels past the image: computed, never stored
-      const int y = m / g.wo, xx = m - y * g.wo;
-      aoff[a] = (g.s * (y - tl.ymin) * g.wp + g.s * xx) * XS + 2 * lh;
+      for (int a = 0; a < 4; ++a) {
+        int m = tl.m0 + 32 * a + li;
+        m = m < g.mimg ? m : g.mimg - 1;               // pixels past the image: computed, never stored
+        const int y = m / g.wo, xx = m - y * g.wo;
+        aoff[a] = (g.s * (y - tl.ymin) * g.wp + g.s * xx) * XS + 2 * lh;
+      }
     }
     const float* xb = pp_lds + ((atom - a_lo) & 1) * g.lds_floats;
     float2 afc[4], afn[4];

@@ -134,9 +134,12 @@ def algorithmic_bytes(kernel, s):
         'depth_syn_fwd': B * N * P * 3 + 2 * B * N * 3 * P,        # depths + mask in, 3 sources x (depth, mask) out
         'depth_syn_bwd': B * N * P * 3 + B * N * 3 * P + 2 * B * N * P,
     }
+    # K2C runs once over the stacked frame pairs (geometry.Pose's batched pairs): pose_pairs samples
+    # of B per launch (K2 itself still launches per pair)
+    k2c = s.get('pose_pairs', 1) if kernel == 'pad_conv_fwd' else 1
     if kernel in ('fuse_pose_fwd', 'pad_conv_fwd') and s.get('map_bytes', 4) != 4:
-        return (planes[kernel] - pose_out) * 4 + pose_out * s['map_bytes']
-    return planes[kernel] * 4
+        return ((planes[kernel] - pose_out) * 4 + pose_out * s['map_bytes']) * k2c
+    return planes[kernel] * 4 * k2c
 
 
 def pose_hw(s):
@@ -151,7 +154,8 @@ def mfma_flops(kernel, s):
     if kernel in ('proj_conv_fwd', 'proj_conv_dgrad', 'proj_conv_wgrad'):
         return 2.0 * s['B'] * s['N'] * s['h'] * s['w'] * 256 * s['Cv'] * s['D'] * 9
     if kernel in ('pad_conv_fwd', 'pad_conv_dgrad', 'pad_conv_wgrad'):   # K2C, pose reduce_dim[0]: K = (C+1)*Z*9
-        return 2.0 * s['B'] * pose_hw(s) * 256 * (s['C'] + 1) * s['Z'] * 9
+        # one launch over the stacked frame pairs (pose_pairs x B samples)
+        return 2.0 * s['B'] * s.get('pose_pairs', 1) * pose_hw(s) * 256 * (s['C'] + 1) * s['Z'] * 9
     return None
 
 
@@ -417,6 +421,9 @@ def main():
         return 0
 
     s = shapes(cfg)
+    from vfdepth_amd import geometry as GEO
+    if cfg['model']['pose_model'] == 'fusion' and GEO._POSE_PAIRS and algo.pose.batch_pairs and not use_graph:
+        s['pose_pairs'] = s['T']          # the frame pairs' K2C convs as one launch
     if cfg['training']['net_precision'] == 'bf16' and os.environ.get('VFD_POSE_BF16_MAP', '1') != '0':
         s['map_bytes'] = 2            # config 3: K2 writes the pose map in bf16 (kernels.PoseConvBF16)
     traffic_tab = load_traffic(args.config)

@@ -88,7 +88,7 @@ __device__ __forceinline__ void pp_stage(const PpGeom& g, float* __restrict__ ds
       const int p = p0 + PPP * u;
       v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (cok && p < plim)
-        v[u] = *reinterpret_cast<const float4*>(src + (size_t)p * g.cin);
+        v[u] = *reinterpret_cast<const float4*>(src + (unsigned)(p * g.cin));   // p * cin < 2^31
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -312,7 +312,7 @@ __device__ __forceinline__ void ppb_stage(const PpGeom& g, __bf16* __restrict__ 
     for (int u = 0; u < U; ++u) {
       const int p = p0 + PPP * u;
       v[u] = PQ::zero();
-      if (cok && p < pval) v[u] = PQ::load(src + (size_t)p * g.cin);
+      if (cok && p < pval) v[u] = PQ::load(src + (unsigned)(p * g.cin));   // p * cin < 2^31: 32-bit offsets
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -372,18 +372,22 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppcb_main_k(PpGeom g, const TX*
   unsigned wc = wsrc(a_lo);
 #pragma unroll
   for (int k = 0; k < PF; ++k) wld(wc, k, bq[k]);
+  int cur_t = -1;
+  int aoff[4];                                        // the lane's pixels' LDS offsets (per tile)
   for (int atom = a_lo; atom < a_hi; ++atom) {
     const bool more = atom + 1 < a_hi;
     const unsigned wn = more ? wsrc(atom + 1) : 0u;
     const int t = atom / nchunk, ch = atom - t * nchunk;
     const PpTile tl = pp_tile(g, t);
-    int aoff[4];
+    if (t != cur_t) {                                 // pixel geometry once per tile
+      cur_t = t;
 #pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      int m = tl.m0 + 32 * a + li;
-      m = m < g.mimg ? m : g.mimg - 1;                 // pixels past the image: computed, never stored
-      const int y = m / g.wo, xx = m - y * g.wo;
-      aoff[a] = (g.s * (y - tl.ymin) * g.wp + g.s * xx) * XS + 8 * lh;
+      for (int a = 0; a < 4; ++a) {
+        int m = tl.m0 + 32 * a + li;
+        m = m < g.mimg ? m : g.mimg - 1;               // pixels past the image: computed, never stored
+        const int y = m / g.wo, xx = m - y * g.wo;
+        aoff[a] = (g.s * (y - tl.ymin) * g.wp + g.s * xx) * XS + 8 * lh;
+      }
     }
     const __bf16* xb = ppb_lds + ((atom - a_lo) & 1) * lds_elems;
 #pragma unroll 1
@@ -519,6 +523,7 @@ static bool pp_plan(const vfd_conv_desc& d, PpGeom* out, int cc = PP_CC, int xs_
   g.hrows = g.s * (orows - 1) + 3;
   g.lds_floats = g.hrows * g.wp * (xs_bytes / 4);
   if ((size_t)2 * g.hrows * g.wp * xs_bytes > PP_LDS_MAX) return false;
+  if ((size_t)g.hrows * g.wp * g.cin >= ((size_t)1 << 31)) return false;   // loaders' 32-bit offsets
   // ranges of >= ceil(nchunk / (PP_MAXC - 2)) atoms keep a tile's contributors <= PP_MAXC - 1
   const int res = pp_resident();
   const int min_range = (g.nchunk + PP_MAXC - 3) / (PP_MAXC - 2);
@@ -770,9 +775,7 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppd_main_k(PdcGeom g, const TG*
   const Frag* wf = reinterpret_cast<const Frag*>(Wd);
   // B fragments of (atom, tap tl, step q): the weight copy's tap slot 8 - (3 ky + kx); the wave's
   // second channel block 64 fragments on
-  auto bptr = [&](int atom, int tl) -> const Frag* {
-    const int t = atom / g.och, ch = atom - t * g.och;
-    const PdcTile tt = pdc_tile(g, t);
+  auto bptr_t = [&](const PdcTile& tt, int ch, int tl) -> const Frag* {
     int ky, kx;
     pdc_tap(g, tt.c, tl, &ky, &kx);
     const int slot = 8 - (3 * ky + kx);
@@ -780,6 +783,10 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppd_main_k(PdcGeom g, const TG*
       return wf + (((size_t)slot * (PP_O / 16) + ch * STEPS) * (g.np / 32) + tt.nt * (PD2_N / 32) + 2 * wn) * 64 + lane;
     else
       return wf + (((size_t)slot * (PP_O / 4) + ch * STEPS) * g.np + tt.nt * PD2_N + wn * 64 + li) * 2 + lh;
+  };
+  auto bptr = [&](int atom, int tl) -> const Frag* {
+    const int t = atom / g.och;
+    return bptr_t(pdc_tile(g, t), atom - t * g.och, tl);
   };
   const size_t qstride = BF ? (size_t)(g.np / 32) * 64 : (size_t)g.np * 2;
   Frag bq[PF][NB];
@@ -789,6 +796,8 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppd_main_k(PdcGeom g, const TG*
 #pragma unroll
     for (int b = 0; b < NB; ++b) bq[q][b] = btap[q * qstride + 64 * b];
   constexpr int LH = BF ? 8 : 2;
+  int cur_t = -1;
+  int pij[MB];                                        // (class row << 16) | class column of the lane's positions
   for (int atom = a_lo; atom < a_hi; ++atom) {
     const int t = atom / g.och, ch = atom - t * g.och;
     const PdcTile tl = pdc_tile(g, t);
@@ -796,14 +805,16 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppd_main_k(PdcGeom g, const TG*
     const int ntap = g.ntap[tl.c];
     const int rbase = tl.i0 - (g.s == 1 ? 2 : 1), cbase = g.s == 1 ? 2 : 1;
     const int m0w = tl.m0 + 32 * MB * wm;             // the wave's first position
-    int pij[MB];                                      // (class row << 16) | class column of the lane's positions
     const float rw = 1.f / (float)wcc;
+    if (t != cur_t) {                                 // position geometry once per tile (och atoms)
+      cur_t = t;
 #pragma unroll
-    for (int a = 0; a < MB; ++a) {
-      int m = m0w + 32 * a + li;
-      m = m < hw ? m : hw - 1;
-      const int i = pdc_div(m, wcc, rw);
-      pij[a] = (i << 16) | (m - i * wcc);
+      for (int a = 0; a < MB; ++a) {
+        int m = m0w + 32 * a + li;
+        m = m < hw ? m : hw - 1;
+        const int i = pdc_div(m, wcc, rw);
+        pij[a] = (i << 16) | (m - i * wcc);
+      }
     }
     const T* xb = lds + ((atom - a_lo) & 1) * g.lds_elems;
     auto offsets = [&](int tp, int* o1) {
@@ -827,7 +838,7 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppd_main_k(PdcGeom g, const TG*
 #pragma unroll 1
     for (int tp = 0; tp < ntap; ++tp) {
       // refill pointer: this atom's next tap, or the next atom's first
-      const Frag* bn = tp + 1 < ntap ? bptr(atom, tp + 1) : (more ? bptr(atom + 1, 0) : nullptr);
+      const Frag* bn = tp + 1 < ntap ? bptr_t(tl, ch, tp + 1) : (more ? bptr(atom + 1, 0) : nullptr);
 #pragma unroll
       for (int q = 0; q < STEPS; ++q) {
         if (q < STEPS - 1) {

@@ -263,13 +263,17 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pcv_main_k(vfd_voxel_desc d, Pc
   // weight fragments of the flattened (atom, iteration) stream, PC_PF iterations ahead
   float2 bq[PC_PF][2];
   int pf_atom = a_lo, pf_it = 0;
+  int pf_di = a_lo % d.D;                             // the prefetched atom's depth bin
   auto prefetch = [&](int slot) {
     if (pf_atom < a_hi) {
-      const int di = pf_atom % d.D;
-      const float2* w = wlane + ((size_t)di * PC_ITERS + pf_it) * (2 * PC_O);
+      const float2* w = wlane + ((size_t)pf_di * PC_ITERS + pf_it) * (2 * PC_O);
       bq[slot][0] = w[0];
       bq[slot][1] = w[64];
-      if (++pf_it == PC_ITERS) { pf_it = 0; ++pf_atom; }
+      if (++pf_it == PC_ITERS) {
+        pf_it = 0;
+        ++pf_atom;
+        pf_di = pf_di + 1 == d.D ? 0 : pf_di + 1;
+      }
     }
   };
 #pragma unroll

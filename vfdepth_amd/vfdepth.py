@@ -37,6 +37,19 @@ _NO_DEVICE_KEYS = ['idx', 'dataset_idx', 'sensor_name', 'filename']
 _OPTIMIZER_NAME = 'adam'
 
 
+def _record_stream(obj, stream):
+    """record_stream(stream) on every CUDA tensor of a nested dict / list / tuple."""
+    if torch.is_tensor(obj):
+        if obj.is_cuda:
+            obj.record_stream(stream)
+    elif isinstance(obj, dict):
+        for v in obj.values():
+            _record_stream(v, stream)
+    elif isinstance(obj, (list, tuple)):
+        for v in obj:
+            _record_stream(v, stream)
+
+
 class _CaptureCheck(TorchDispatchMode):
     """VFD_GRAPH_CHECK=1: every framework op of the captured step whose tensors are on both the host
     and the device is recorded.  A host->device copy inside a capture is a graph node that reads the
@@ -241,11 +254,42 @@ class VFDepthAlgo:
         losses = self.compute_losses(inputs, outputs, noise)
         return outputs, losses
 
+    def _branch_stream(self):
+        """Second stream for the pose branch of a training step (default; VFD_BRANCH_STREAMS=0 turns
+        it off): the pose net (its encoder over the frame pairs, K2 / K2C, decoder) and the depth net
+        are independent until the view synthesis, so their many small latency-bound kernels
+        (small-layer BN, small convs) fill each other's idle CUs — config 2 27.55 vs 30.27-30.50
+        ms/step on one box (round 5).  Under DDP the collectives of both branches (SyncBN, DDP's
+        buckets) go to the process group's own stream in host issue order, which is the same on every
+        rank.  Grad mode only, not under HIP-graph capture."""
+        if (self.device.type != 'cuda' or os.environ.get('VFD_BRANCH_STREAMS', '1') == '0'
+                or getattr(self, '_graphed', False)
+                or not torch.is_grad_enabled() or torch.cuda.is_current_stream_capturing()
+                or self.pose_model != 'fusion' or self.depth_model != 'fusion'):
+            return None
+        if getattr(self, '_bstream', None) is None:
+            self._bstream = torch.cuda.Stream(self.device)
+        return self._bstream
+
     def estimate_vfdepth(self, inputs):
         inputs['extrinsics_inv'] = inverse4x4(inputs['extrinsics'])
         outputs = {('cam', c): {} for c in range(self.num_cams)}
-        pose_pred = self.predict_pose(inputs)
-        depth_feats = self.predict_depth(inputs)
+        side = self._branch_stream()
+        if side is not None:
+            # the geometry both fusion nets share (1/8 mask, K2 plan object) made on this stream first
+            dn = self.models['depth_net']
+            vf = getattr(dn, 'module', dn).fusion_net
+            vf._plan(inputs, vf.space(self.device))
+            main = torch.cuda.current_stream(self.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                pose_pred = self.predict_pose(inputs)
+            depth_feats = self.predict_depth(inputs)
+            main.wait_stream(side)
+            _record_stream(pose_pred, main)     # side-stream tensors read on this stream from here on
+        else:
+            pose_pred = self.predict_pose(inputs)
+            depth_feats = self.predict_depth(inputs)
         packed = depth_feats.pop('_packed', None)
         packed_aug = depth_feats.pop('_packed_aug', None)
         if '_extrinsics_aug' in depth_feats:          # written by VFNet (travels through DDP)
@@ -329,6 +373,8 @@ class VFDepthAlgo:
         self.optimizer.zero_grad(set_to_none=True)
         _, losses = self.process_batch(inputs, self.rank)
         losses['total_loss'].backward()
+        if getattr(self, '_bstream', None) is not None:     # the pose branch's backward ran there
+            torch.cuda.current_stream(self.device).wait_stream(self._bstream)
         self.optimizer.step()
         return losses
 
@@ -353,6 +399,7 @@ class VFDepthAlgo:
         # stacked-pair form's first replay hit an illegal address — eager steps
         # keep the stacked pairs
         self.pose.batch_pairs = False
+        self._graphed = True            # one stream: the warm-up steps and the capture alike
         # no autograd graph of an earlier step may survive into the warm-up or the capture: its
         # AccumulateGrad nodes would carry their stream into the captured backward
         gc.collect()

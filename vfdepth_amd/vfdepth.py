@@ -398,6 +398,8 @@ class VFDepthAlgo:
         # the captured step calls the pose net once per frame pair (pose.batch_pairs off): the
         # stacked-pair form's first replay hit an illegal address — eager steps
         # keep the stacked pairs
+        # one stream, pairs one at a time: a capture with the pose branch's stream forked and
+        # joined inside it (and the batched pairs) crashed the host in hipStreamEndCapture (round 5)
         self.pose.batch_pairs = False
         self._graphed = True            # one stream: the warm-up steps and the capture alike
         # no autograd graph of an earlier step may survive into the warm-up or the capture: its
@@ -425,6 +427,8 @@ class VFDepthAlgo:
             with check:
                 static_outputs, static_losses = self.process_batch(dict(static), self.rank)
                 static_losses['total_loss'].backward()
+                if getattr(self, '_bstream', None) is not None:   # join the pose branch's stream
+                    torch.cuda.current_stream(self.device).wait_stream(self._bstream)
                 self.optimizer.step()
         if isinstance(check, _CaptureCheck):
             check.raise_if_any()

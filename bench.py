@@ -406,6 +406,9 @@ def main():
     torch.cuda.synchronize()
     from vfdepth_amd import kernels as KN
     KN.syncbn_stats(reset=True)
+    # one stream while the per-kernel events are recorded: with the pose branch on its own stream
+    # the two branches' kernels share the CUs, and an event pair would time the contention too
+    algo.branch_streams = False
     _lib.prof_enable('all')
     for _ in range(n_prof):
         losses = eager_step()
@@ -508,7 +511,8 @@ def main():
                                'what': 'every HBM-bound hot-path op of the step (K1-K5, plans, aggregation)'},
         'hot_path_ms_per_step': sum(t for _, t in prof.values()) / args.steps,
         'dense_fused': {k: roofline_any(k) for k in dense},
-        'execution': 'hip-graph replay of the whole step' if use_graph else 'eager',
+        'execution': ('hip-graph replay of the whole step' if use_graph else
+                      'eager, pose branch on a second stream' if getattr(algo, '_bstream', None) is not None else 'eager'),
         'miopen': ('benchmark mode (algorithm per shape by measured time, find-db miopen_db/)' if args.conv_autotune
                    else 'immediate mode (find-db miopen_db/)'),
         'encoder_layout': 'channels-last' if any(getattr(m, 'channels_last', False) for net in algo.models.values()

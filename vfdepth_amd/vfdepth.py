@@ -263,7 +263,7 @@ class VFDepthAlgo:
         buckets) go to the process group's own stream in host issue order, which is the same on every
         rank.  Grad mode only, not under HIP-graph capture."""
         if (self.device.type != 'cuda' or os.environ.get('VFD_BRANCH_STREAMS', '1') == '0'
-                or getattr(self, '_graphed', False)
+                or getattr(self, '_graphed', False) or not getattr(self, 'branch_streams', True)
                 or not torch.is_grad_enabled() or torch.cuda.is_current_stream_capturing()
                 or self.pose_model != 'fusion' or self.depth_model != 'fusion'):
             return None

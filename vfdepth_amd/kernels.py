@@ -450,7 +450,11 @@ def weight_swap(w, A, B, cache=False, memory_format=torch.contiguous_format):
 
 def _weight_permute_swap(w, A, B, memory_format):
     lib = L.load()
-    w = _dev(w, 'conv weight')
+    _check_device(w, 'conv weight')
+    if w.dtype != torch.float32:
+        w = w.float()
+    # any layout whose taps are evenly strided (NCHW, channels-last: MIOpen's NHWC weight gradient)
+    # goes in as it is — no contiguous copy of the 47-MB pose weight gradient
     O, C, kh, kw = w.shape
     T = kh * kw
     out = torch.empty(O, C, kh, kw, device=w.device, memory_format=memory_format)

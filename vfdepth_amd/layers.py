@@ -258,6 +258,10 @@ class ResnetEncoder(nn.Module):
         batch is G stacked calls' batches, each BatchNorm'd on its own (`bn_groups`)."""
         e = self.encoder
         x = image if normalized else (image - 0.45) / 0.225
+        if self.channels_last:
+            # the first conv's input in its layout once: MIOpen's NHWC forward and weight gradient
+            # would each make their own channels-last copy of it
+            x = x.contiguous(memory_format=torch.channels_last)
         with bn_groups(groups):
             f0 = bn_act(e.bn1, e.conv1(x))
             f1 = e.layer1(max_pool_stem(e.maxpool, f0))

@@ -130,9 +130,12 @@ class VFDepthAlgo:
         }
         if self.ddp_enable:
             from torch.nn.parallel import DistributedDataParallel as DDP
-            group = dist.new_group(list(range(self.world_size)))
             on_gpu = self.device.type == 'cuda'
             for k, v in models.items():
+                # one SyncBatchNorm group per net (created in the same order on every rank): the
+                # pose branch runs on its own stream, and its BN collectives then go to their own
+                # communicator (and stream) instead of queueing behind the depth branch's
+                group = dist.new_group(list(range(self.world_size)))
                 # torch's SyncBatchNorm only runs on GPU modules: the gloo/CPU rehearsal keeps
                 # per-rank BatchNorm, the GPU path converts exactly as the reference does
                 if on_gpu:

@@ -33,8 +33,9 @@ def main():
     batch = synth.make_batch(cfg, seed=99, device=dev)
     noise = 1e-5 * torch.randn(N, 1, len(frames) - 1, H, W, generator=torch.Generator().manual_seed(98)).to(dev)
     runs = []
-    for _ in range(2):
+    for i in range(3):
         algo = VFDepthAlgo(cfg, 0)
+        algo.branch_streams = i < 2          # the third run: the pose branch on the main stream
         for m in algo.models.values():
             m.load_state_dict(seeded_state_dict(m, seed=G.STEP_SEED))
         algo.set_train()
@@ -48,8 +49,9 @@ def main():
                      disp.grad.detach().clone(),
                      {f'{n}.{k}': p.grad.detach().clone() for n, m in algo.models.items()
                       for k, p in m.named_parameters() if p.grad is not None}))
-    (l0, d0, gd0, g0), (l1, d1, gd1, g1) = runs
-    out = {'env': os.environ.get('MIOPEN_DEBUG_CONVOLUTION_DETERMINISTIC'),
+    (l0, d0, gd0, g0), (l1, d1, gd1, g1), (l2, d2, gd2, g2) = runs
+    out = {'single_stream_equal': bool(torch.equal(d0, d2) and all(torch.equal(l0[k], l2[k]) for k in l0)
+                                       and torch.equal(gd0, gd2) and all(torch.equal(g0[k], g2[k]) for k in g0)),'env': os.environ.get('MIOPEN_DEBUG_CONVOLUTION_DETERMINISTIC'),
            'depth_equal': bool(torch.equal(d0, d1)),
            'loss_diff': [k for k in l0 if not torch.equal(l0[k], l1[k])],
            'd_disp_equal': bool(torch.equal(gd0, gd1)),

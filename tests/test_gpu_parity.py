@@ -920,7 +920,7 @@ def test_full_step_depth_synthesis_against_reference():
 def test_deterministic_steps_bit_identical():
     """Under torch.backends.cudnn.deterministic (set by the reference's train.py:23-24) two eager
     training steps from the same state give bit-identical losses, depth maps and parameter
-    gradients: the fusion plan's buckets and K3's cell lists are ordered by voxel / sample, K1's
+    gradients, and so does a third with the pose branch on the main stream instead of its own: the fusion plan's buckets and K3's cell lists are ordered by voxel / sample, K1's
     backward is the plan gather, K3's heavy tiles are not split, every other hot-path reduction
     already sums in a fixed order, and MIOpen runs its deterministic solvers.  In a fresh process
     (tests/det_worker.py): MIOpen reads its determinism switch once, at its first convolution."""
@@ -935,3 +935,5 @@ def test_deterministic_steps_bit_identical():
     r = json.loads(res.stdout.strip().splitlines()[-1])
     assert r['depth_equal'] and not r['loss_diff'] and r['d_disp_equal'], r
     assert not r['grad_diff'], f"{len(r['grad_diff'])} of {r['n_grads']} parameter gradients differ: {r['grad_diff']}"
+    # the pose branch on its own stream (the default) computes exactly what one stream does
+    assert r['single_stream_equal'], 'branch-stream step differs from the single-stream step'

@@ -258,11 +258,18 @@ class FusionPlan:
             t.record_stream(main)
         for t in (mask_lo, K, Einv):
             t.record_stream(self.side)
+        # the point right after the plan kernels: a consumer on another stream waits for this, not
+        # for everything queued on the building stream later (the pose branch's stream builds the
+        # plan in its forward; the depth branch's K1 backward reads it while the pose backward runs)
+        self.ready = torch.cuda.Event()
+        self.ready.record(self.side)
         return self
 
     def wait(self):
         """Make the current stream wait for the plan (before any kernel that reads its buffers)."""
-        torch.cuda.current_stream(self.buf.device).wait_stream(self.side)
+        cur = torch.cuda.current_stream(self.buf.device)
+        if cur != self.side:
+            cur.wait_event(self.ready)
 
 
 def _channels_last(t, what):

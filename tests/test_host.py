@@ -1,4 +1,5 @@
 """Host-side (non-kernel) pieces of the product on CPU: depth metrics, 4x4 inverse, config."""
+import os
 import numpy as np
 import torch
 
@@ -185,3 +186,21 @@ def test_fold_weights_backward_matches_autograd_slices():
     ((rf * gf).sum() + (rz * gz).sum()).backward()
     torch.testing.assert_close(a_no, w_no.grad, rtol=1e-12, atol=1e-12)
     torch.testing.assert_close(a_o, w_o.grad, rtol=1e-12, atol=1e-12)
+
+
+def test_miopen_private_db_copy(tmp_path, monkeypatch):
+    """vfdepth_amd.miopen_db.use_private_copy: a process works on its own copy of the committed
+    find-db (its writes cannot reach miopen_db/); an exported MIOPEN_USER_DB_PATH is kept."""
+    from vfdepth_amd import miopen_db
+    src = tmp_path / 'db'
+    src.mkdir()
+    (src / 'gfx950.ufdb.txt').write_text('record')
+    monkeypatch.delenv('MIOPEN_USER_DB_PATH', raising=False)
+    dst = miopen_db.use_private_copy(str(src))
+    assert dst != str(src) and os.environ['MIOPEN_USER_DB_PATH'] == dst
+    assert open(os.path.join(dst, 'gfx950.ufdb.txt')).read() == 'record'
+    with open(os.path.join(dst, 'gfx950.ufdb.txt'), 'a') as fh:      # MIOpen appending a record
+        fh.write('+new')
+    assert (src / 'gfx950.ufdb.txt').read_text() == 'record'
+    monkeypatch.setenv('MIOPEN_USER_DB_PATH', '/some/where')
+    assert miopen_db.use_private_copy(str(src)) == '/some/where'

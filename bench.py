@@ -425,7 +425,7 @@ def main():
 
     s = shapes(cfg)
     from vfdepth_amd import geometry as GEO
-    if cfg['model']['pose_model'] == 'fusion' and GEO._POSE_PAIRS and algo.pose.batch_pairs and not use_graph:
+    if cfg['model']['pose_model'] == 'fusion' and GEO._POSE_PAIRS and algo.pose.batch_pairs:
         s['pose_pairs'] = s['T']          # the frame pairs' K2C convs as one launch
     if cfg['training']['net_precision'] == 'bf16' and os.environ.get('VFD_POSE_BF16_MAP', '1') != '0':
         s['map_bytes'] = 2            # config 3: K2 writes the pose map in bf16 (kernels.PoseConvBF16)

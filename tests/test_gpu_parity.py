@@ -665,12 +665,15 @@ def test_graph_replay_matches_eager():
         a.set_optimizer(capturable=True)
         a.losses.device_seed = True
         algos.append(a)
-    # the eager reference runs the step as the capture does (frame pairs one at a time, one
-    # stream): the same MIOpen problems, so the comparison isolates the replay itself (the batched
-    # pairs and the branch stream are checked against the reference fixtures elsewhere)
-    algos[1].pose.batch_pairs = False
-    algos[1].branch_streams = False
+    # both run the DEFAULT step: frame pairs as one batch, the pose branch on its own stream (the
+    # capture forks and joins it); the eager side is the bench's eager step
+    assert algos[0].pose.batch_pairs and algos[1].pose.batch_pairs
+    # an eager branch-stream step first: the capture must not depend on streams an earlier eager
+    # step used (its branch stream is joined only when the step itself forked it)
+    algos[0].train_step(dict(batch))
     graphed = algos[0].graphed_train_step(batch, warmup=2)
+    assert algos[0]._bstream is not None, 'the captured step did not use the pose branch stream'
+    assert algos[0].pose.batch_pairs, 'graphed_train_step changed the pose-pair setting'
     # rewind the graphed model to the initial state, in place (the graph holds these buffers)
     for name, m in algos[0].models.items():
         m.load_state_dict(init[name])

@@ -77,8 +77,8 @@ class Pose:
         self.num_cams = int(dt['num_cams'])
         self.rel_cam_list = dt['rel_cam_list']
         self.spatio, self.spatio_temporal = bool(t['spatio']), bool(t['spatio_temporal'])
-        # the frame pairs as one batch (eager steps); VFDepthAlgo.graphed_train_step turns it off for
-        # the captured step (the stacked-pair step faulted on its first HIP-graph replay)
+        # the frame pairs as one batch (eager steps and the captured step alike); False: one pose-net
+        # call per pair, as the reference
         self.batch_pairs = True
 
     def compute_pose(self, net, inputs):

@@ -222,6 +222,17 @@ def _side_stream(device):
 _SIDE_STREAMS = {}
 
 
+def _wait_stream(dst, src):
+    """dst waits for the work queued on src so far — skipped when they are one stream.  A stream
+    waiting on its own event is a no-op on the device, but under HIP-graph capture this HIP runtime
+    (ROCm 7.x) files a non-origin capture stream that waits on an event of ITSELF (or of another
+    non-origin stream that joined through it) as its own parallel-capture child; hipStreamEndCapture
+    then recurses through that cycle until the host stack overflows (round 6: a SIGSEGV inside
+    libamdhip64 with ~170k identical frames; tools/diag_capture_patterns.py, tools/hiplog_capture.py)."""
+    if dst != src:
+        dst.wait_stream(src)
+
+
 class FusionPlan:
     """Per-(batch, camera) compacted list of visible voxels with their tap data (device buffers).
 
@@ -248,7 +259,7 @@ class FusionPlan:
         d = self.space.desc(self.B, self.N)
         nbytes = lib.vfd_fusion_plan_bytes(ctypes.byref(d))
         main, self.side = torch.cuda.current_stream(mask_lo.device), _side_stream(mask_lo.device)
-        self.side.wait_stream(main)
+        _wait_stream(self.side, main)
         with torch.cuda.stream(self.side):
             self.buf = torch.empty(nbytes, dtype=torch.uint8, device=mask_lo.device)
             self.counts = torch.empty(self.B * self.N, dtype=torch.int32, device=mask_lo.device)
@@ -357,7 +368,7 @@ class VoxelProject(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             nbytes = lib.vfd_voxel_project_plan_bytes(ctypes.byref(d))
             main, side = torch.cuda.current_stream(vox.device), _side_stream(vox.device)
-            side.wait_stream(main)                  # invK / E are ready
+            _wait_stream(side, main)                # invK / E are ready
             with torch.cuda.stream(side):
                 plan = torch.empty(nbytes, dtype=torch.uint8, device=vox.device)
                 L.check(lib.vfd_voxel_project_plan(ctypes.byref(d), invK.data_ptr(), E.data_ptr(), plan.data_ptr(),
@@ -376,7 +387,7 @@ class VoxelProject(torch.autograd.Function):
         g = _channels_last(g, 'grad')
         dvox = torch.empty(B, V, Cv, device=g.device)
         d = ctx.space.desc(B, N, Cv=Cv)
-        torch.cuda.current_stream(g.device).wait_stream(ctx.side)
+        _wait_stream(torch.cuda.current_stream(g.device), ctx.side)
         L.check(lib.vfd_voxel_project_bwd_planned(ctypes.byref(d), g.data_ptr(), ctx.plan.data_ptr(),
                                                   ctx.plan.numel(), dvox.data_ptr(), L.stream()), 'voxel_project_bwd')
         ctx.plan = None

@@ -16,6 +16,7 @@ for the GPU:
 import contextlib
 import gc
 import os
+import sys
 from collections import defaultdict
 
 import torch
@@ -48,6 +49,26 @@ def _record_stream(obj, stream):
     elif isinstance(obj, (list, tuple)):
         for v in obj:
             _record_stream(v, stream)
+
+
+def _trace(what, sync=True):
+    """VFD_GRAPH_TRACE=1: a line per stage of graphed_train_step (after a device sync when allowed),
+    so a crash is attributed to its stage."""
+    if os.environ.get('VFD_GRAPH_TRACE') == '1':
+        if sync:
+            torch.cuda.synchronize()
+        print(f'[graph] {what}', file=sys.stderr, flush=True)
+
+
+def _detach_all(obj):
+    """The same nested dict / list / tuple with every tensor detached (views of the same memory)."""
+    if torch.is_tensor(obj):
+        return obj.detach()
+    if isinstance(obj, dict):
+        return {k: _detach_all(v) for k, v in obj.items()}
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_detach_all(v) for v in obj)
+    return obj
 
 
 class _CaptureCheck(TorchDispatchMode):
@@ -264,15 +285,29 @@ class VFDepthAlgo:
         (small-layer BN, small convs) fill each other's idle CUs — config 2 27.55 vs 30.27-30.50
         ms/step on one box (round 5).  Under DDP the collectives of both branches (SyncBN, DDP's
         buckets) go to the process group's own stream in host issue order, which is the same on every
-        rank.  Grad mode only, not under HIP-graph capture."""
+        rank.  Grad mode only.  Under HIP-graph capture the branch stream is forked from the capture
+        stream and joined back (forward: `estimate_vfdepth`; backward: autograd's leaf-stream sync and
+        `_join_branch`), so the captured step has the same two-branch schedule as the eager one."""
         if (self.device.type != 'cuda' or os.environ.get('VFD_BRANCH_STREAMS', '1') == '0'
-                or getattr(self, '_graphed', False) or not getattr(self, 'branch_streams', True)
-                or not torch.is_grad_enabled() or torch.cuda.is_current_stream_capturing()
+                or not getattr(self, 'branch_streams', True) or not torch.is_grad_enabled()
                 or self.pose_model != 'fusion' or self.depth_model != 'fusion'):
+            return None
+        if torch.cuda.is_current_stream_capturing() and dist.is_initialized() and dist.get_world_size() > 1:
+            # a capture at world > 1: the pose branch's SyncBatchNorm all-reduces would make the
+            # branch stream and the process group's stream wait on each other, which this HIP
+            # runtime turns into a parent/child cycle of capture streams (kernels._wait_stream)
             return None
         if getattr(self, '_bstream', None) is None:
             self._bstream = torch.cuda.Stream(self.device)
         return self._bstream
+
+    def _join_branch(self):
+        """Make the current stream wait for the pose branch's stream if THIS step used it (its
+        backward ran there).  Only then: under capture, waiting on a stream the capture never forked
+        would be a cross-capture dependency (hipErrorStreamCaptureIsolation)."""
+        if getattr(self, '_branch_live', False):
+            torch.cuda.current_stream(self.device).wait_stream(self._bstream)
+            self._branch_live = False
 
     def estimate_vfdepth(self, inputs):
         inputs['extrinsics_inv'] = inverse4x4(inputs['extrinsics'])
@@ -285,6 +320,7 @@ class VFDepthAlgo:
             vf._plan(inputs, vf.space(self.device))
             main = torch.cuda.current_stream(self.device)
             side.wait_stream(main)
+            self._branch_live = True
             with torch.cuda.stream(side):
                 pose_pred = self.predict_pose(inputs)
             depth_feats = self.predict_depth(inputs)
@@ -372,48 +408,74 @@ class VFDepthAlgo:
 
     # ------------------------------------------------------------------ HIP graph
     def train_step(self, inputs):
-        """zero_grad -> process_batch -> backward -> optimizer step (vfdepth_trainer.py:63-66)."""
+        """zero_grad -> process_batch -> backward -> optimizer step (vfdepth_trainer.py:63-66).
+        Returns the losses DETACHED: a caller that keeps them (a logger, the bench) must not keep the
+        step's autograd graph alive — its AccumulateGrad nodes, and the streams they were created
+        on, would otherwise carry into later steps (and into a graph capture)."""
         self.optimizer.zero_grad(set_to_none=True)
         _, losses = self.process_batch(inputs, self.rank)
         losses['total_loss'].backward()
-        if getattr(self, '_bstream', None) is not None:     # the pose branch's backward ran there
-            torch.cuda.current_stream(self.device).wait_stream(self._bstream)
+        self._join_branch()
         self.optimizer.step()
-        return losses
+        return {k: (v.detach() if torch.is_tensor(v) else v) for k, v in losses.items()}
+
+    def _rewrap_ddp(self, stream):
+        """Rebuild the DDP wrappers with `stream` current.  DDP's reducer creates (and keeps) every
+        parameter's AccumulateGrad node at construction, and autograd accumulates a gradient on the
+        stream its node was created on: built on the default stream (as `prepare_model` does, like
+        the reference), the captured backward's accumulations would go to the legacy default stream,
+        which cannot join a capture.  The old wrappers are dropped first so their nodes die and
+        the new reducer makes fresh ones on `stream` (PyTorch's DDP + graph-capture recipe)."""
+        import weakref
+        from torch.nn.parallel import DistributedDataParallel as DDP
+        for k in list(self.models):
+            m = self.models[k]
+            inner, kw = m.module, dict(device_ids=m.device_ids, broadcast_buffers=m.broadcast_buffers,
+                                       process_group=m.process_group)
+            old = weakref.ref(m.reducer)
+            self.models[k] = m = None
+            gc.collect()
+            if old() is not None:
+                # its AccumulateGrad nodes (on the stream DDP was built on) would be reused
+                refs = [type(r).__name__ for r in gc.get_referrers(old())]
+                raise RuntimeError(f'{k}: the previous DDP reducer is still referenced ({refs}); '
+                                   'cannot rebuild DDP on the capture stream')
+            with torch.cuda.stream(stream):
+                self.models[k] = DDP(inner, **kw)
 
     def graphed_train_step(self, batch, warmup=3):
         """Capture one whole training step (forward, losses, backward, Adam) in a HIP graph.
 
-        Returns step(new_batch=None) -> losses: copies new_batch (same shapes) into the static
-        input buffers and replays the graph: ~2000 kernel launches per step become one.  Needs a
-        capturable optimizer (set_optimizer(capturable=True)).
+        Returns step(new_batch=None) -> losses (detached): copies new_batch (same shapes) into the
+        static input buffers and replays the graph: ~1100 kernel launches per step become one.
+        Needs a capturable optimizer (set_optimizer(capturable=True)).  The captured step is the
+        eager default one: batched frame pairs and the pose branch on its own stream (forked from
+        and joined back into the capture stream).  The warm-up steps run in that same configuration
+        on the capture stream itself, so every MIOpen problem is found / compiled before the capture
+        and every AccumulateGrad node lives on a captured stream.
 
         Under DDP (trainer/vfdepth_trainer.py:61-66 with models/vfdepth.py:56-71's wrapping) the
-        captured step holds DDP's bucketed gradient all-reduces and the fused BN's SyncBatchNorm
-        all-reduces (RCCL kernels on the ranks' streams, captured with the step): DDP settles its
-        buckets during its first iterations, so at least 11 eager DDP steps run (on the side
-        stream) before the capture, as PyTorch requires for a DDP capture.  Every rank captures and
-        replays the same step, so the collectives stay matched."""
+        wrappers are rebuilt on the capture stream (`_rewrap_ddp`) and the captured step holds DDP's
+        bucketed gradient all-reduces and the fused BN's SyncBatchNorm all-reduces (RCCL kernels on
+        the ranks' streams, captured with the step): DDP settles its buckets during its first
+        iterations, so at least 11 eager DDP steps run before the capture, as PyTorch requires.
+        Every rank captures and replays the same step, so the collectives stay matched."""
         if self.ddp_enable:
             warmup = max(warmup, 11)
         static = {k: (v.to(self.device) if torch.is_tensor(v) else v) for k, v in batch.items()}
         self.losses.device_seed = True
-        # the captured step calls the pose net once per frame pair (pose.batch_pairs off): the
-        # stacked-pair form's first replay hit an illegal address (DESIGN §2, round 5) — eager steps
-        # keep the stacked pairs
-        # one stream, pairs one at a time: a capture with the pose branch's stream forked and
-        # joined inside it (and the batched pairs) crashed the host in hipStreamEndCapture (round 5)
-        self.pose.batch_pairs = False
-        self._graphed = True            # one stream: the warm-up steps and the capture alike
         # no autograd graph of an earlier step may survive into the warm-up or the capture: its
         # AccumulateGrad nodes would carry their stream into the captured backward
         gc.collect()
-        side = torch.cuda.Stream(self.device)
-        side.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(side):
-            for _ in range(warmup):
+        cap = torch.cuda.Stream(self.device)          # warm-up AND capture stream
+        cap.wait_stream(torch.cuda.current_stream(self.device))
+        if self.ddp_enable:
+            self._rewrap_ddp(cap)
+        with torch.cuda.stream(cap):
+            for i in range(warmup):
                 self.train_step(dict(static))
-        torch.cuda.current_stream(self.device).wait_stream(side)
+                _trace(f'warm-up step {i}')
+        torch.cuda.current_stream(self.device).wait_stream(cap)
         # constants the captured step builds on the device (the augmented view's rotation is drawn
         # on the device generator under capture): made here, so no host->device copy is captured
         _qm_consts(self.device, torch.float32)
@@ -426,17 +488,34 @@ class VFDepthAlgo:
         check = _CaptureCheck() if os.environ.get('VFD_GRAPH_CHECK') == '1' else contextlib.nullcontext()
         if isinstance(check, _CaptureCheck):
             check.live_graph_before_capture()
-        with torch.cuda.graph(graph):
+        _trace(f'capture begins on stream {cap.cuda_stream:#x}, branch stream '
+               f'{getattr(getattr(self, "_bstream", None), "cuda_stream", 0):#x}, default stream '
+               f'{torch.cuda.default_stream(self.device).cuda_stream:#x}')
+        with torch.cuda.graph(graph, stream=cap):
             with check:
-                static_outputs, static_losses = self.process_batch(dict(static), self.rank)
-                static_losses['total_loss'].backward()
-                if getattr(self, '_bstream', None) is not None:   # join the pose branch's stream
-                    torch.cuda.current_stream(self.device).wait_stream(self._bstream)
-                self.optimizer.step()
+                try:
+                    static_outputs, static_losses = self.process_batch(dict(static), self.rank)
+                    _trace('captured forward', sync=False)
+                    static_losses['total_loss'].backward()
+                    _trace('captured backward', sync=False)
+                    self._join_branch()
+                    self.optimizer.step()
+                    _trace('captured optimizer step', sync=False)
+                except BaseException:
+                    # the runtime may not survive ending an invalidated capture: report first
+                    import traceback
+                    traceback.print_exc()
+                    sys.stderr.flush()
+                    raise
+        _trace('capture ended')
         if isinstance(check, _CaptureCheck):
             check.raise_if_any()
         if dump:
             graph.debug_dump(dump)
+        # keep only detached views: the captured step's autograd graph (and its AccumulateGrad nodes)
+        # must not outlive the capture
+        static_losses = {k: (v.detach() if torch.is_tensor(v) else v) for k, v in static_losses.items()}
+        static_outputs = _detach_all(static_outputs)
 
         def step(new_batch=None):
             if new_batch is not None:

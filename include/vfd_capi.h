@@ -78,7 +78,10 @@ int vfd_fuse_depth_bwd(const vfd_voxel_desc* d, const float* d_vox, const float*
                        float* d_wzb, void* workspace, size_t ws_bytes, void* stream);
 /* K1 backward as an atomic-free gather over the fusion plan's tile buckets (the plan vfd_fusion_plan
  * builds for the K2 backward; same arguments otherwise, Cv = 64): d P written with plain stores,
- * summed in bucket order (deterministic once the buckets are, see vfd_fusion_plan_sort). */
+ * summed in bucket order (deterministic once the buckets are, see vfd_fusion_plan_sort).  Its
+ * workspace (vfd_fuse_depth_bwd_planned_workspace bytes) also holds its split tiles' partials, so
+ * it may run concurrently with the K2 backward that reads the same plan (the pose branch's stream). */
+size_t vfd_fuse_depth_bwd_planned_workspace(const vfd_voxel_desc* d);
 int vfd_fuse_depth_bwd_planned(const vfd_voxel_desc* d, const void* plan, const float* d_vox, const float* vox,
                                const float* mask_lo, const float* K, const float* Einv, float* dP, float* d_wzb,
                                void* workspace, size_t ws_bytes, void* stream);

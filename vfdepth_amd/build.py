@@ -7,6 +7,7 @@ No CMake: one hipcc invocation per translation unit, then a shared link.  `-ffp-
 keeps every multiply and add separately rounded, the same operation sequence as the reference's
 CPU ATen path, so boundary decisions (OOB / mask / argmin) agree with it.
 """
+import hashlib
 import os
 import subprocess
 import sys
@@ -29,38 +30,62 @@ def _hipcc():
     raise RuntimeError('hipcc not found')
 
 
-def _stale(out, deps):
-    if not os.path.exists(out):
+def _digest(paths, extra=()):
+    """sha256 over the CONTENT of `paths` (and the compile command): what a target was built from.
+    Content, not mtimes — a checkout, a copy or a snapshot to the GPU box resets mtimes."""
+    h = hashlib.sha256()
+    for x in extra:
+        h.update(str(x).encode())
+    for p in paths:
+        with open(p, 'rb') as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def _stale(out, digest):
+    """out is missing, or was built from different content (its .sha record differs)."""
+    rec = out + '.sha'
+    if not (os.path.exists(out) and os.path.exists(rec)):
         return True
-    t = os.path.getmtime(out)
-    return any(os.path.getmtime(d) > t for d in deps)
+    with open(rec) as fh:
+        return fh.read().strip() != digest
+
+
+def _record(out, digest):
+    with open(out + '.sha', 'w') as fh:
+        fh.write(digest + '\n')
 
 
 def build(force=False, verbose=True):
     hipcc = _hipcc()
     headers = [os.path.join(CSRC, 'vfd_common.h'), os.path.join(INCLUDE, 'vfd_capi.h')]
-    objs, cmds = [], []
+    objs, jobs = [], []
     os.makedirs(os.path.join(HERE, 'build'), exist_ok=True)
     for src in SOURCES:
         s = os.path.join(CSRC, src)
         o = os.path.join(HERE, 'build', src.replace('.hip', '.o'))
         objs.append(o)
-        if force or _stale(o, [s] + headers):
-            cmds.append([hipcc] + FLAGS + ['-c', s, '-o', o])
+        dg = _digest([s] + headers, extra=FLAGS)
+        if force or _stale(o, dg):
+            jobs.append(([hipcc] + FLAGS + ['-c', s, '-o', o], o, dg))
     # translation units compile in parallel (at most 8 hipcc processes)
     from concurrent.futures import ThreadPoolExecutor
 
-    def run(cmd):
+    def run(job):
+        cmd, out, dg = job
         if verbose:
             print(' '.join(cmd), flush=True)
         subprocess.check_call(cmd)
+        _record(out, dg)
     with ThreadPoolExecutor(max_workers=max(1, min(8, os.cpu_count() or 1))) as ex:
-        list(ex.map(run, cmds))
-    if force or _stale(LIB, objs):
+        list(ex.map(run, jobs))
+    dg = _digest(objs, extra=[ARCH])
+    if force or _stale(LIB, dg):
         cmd = [hipcc, f'--offload-arch={ARCH}', '-shared', '-fPIC', '-o', LIB] + objs
         if verbose:
             print(' '.join(cmd), flush=True)
         subprocess.check_call(cmd)
+        _record(LIB, dg)
     return LIB
 
 

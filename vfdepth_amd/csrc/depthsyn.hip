@@ -127,7 +127,13 @@ __global__ __launch_bounds__(256) void depth_syn_fwd_k(vfd_depthsyn_desc d, cons
 // round-toward-zero(v * 2^DS_FRAC) (exact for |v| >= 2^-DS_FRAC+23, |v| < 2^26), added to the
 // pixel's (hi, lo) pair by two 64-bit integer atomics with the low word's carry passed on.
 // Integer addition is associative, so the pair ends the same whatever order the adds land in.
+// The pair holds sums of magnitude < 2^27 (63 - 36 integer bits in hi); contributions of
+// magnitude >= DS_FIXED_MAX (and non-finite ones) take the float atomic instead (ds_fixed_ok), so
+// the shift below never leaves [-24, 102] and the integer part cannot overflow from one add.
 constexpr int DS_FRAC = 100;
+constexpr float DS_FIXED_MAX = 0x1p25f;
+
+__device__ __forceinline__ bool ds_fixed_ok(float v) { return fabsf(v) < DS_FIXED_MAX; }   // false for NaN / inf
 
 __device__ __forceinline__ void ds_fixed_add(unsigned long long* __restrict__ cell, float v) {
   const unsigned u = __float_as_uint(v);
@@ -163,7 +169,7 @@ __global__ __launch_bounds__(256) void depth_syn_fixed_k(const unsigned long lon
   if (i >= n) return;
   const long long hi = (long long)acc[2 * i];
   const unsigned long long lo = acc[2 * i + 1];
-  // + the non-finite contributions, which went to d_depth itself (0 when there were none)
+  // + the non-finite / out-of-range contributions, which went to d_depth itself (0 when there were none)
   d_depth[i] = (float)((double)hi * 0x1p-36 + (double)lo * 0x1p-100) + d_depth[i];
 }
 
@@ -199,8 +205,8 @@ __global__ __launch_bounds__(256) void depth_syn_bwd_k(vfd_depthsyn_desc d, cons
     for (int k = 0; k < 4; ++k)
       if (sm.q[k] >= 0) {
         const float v = gv * sm.bl.w[k] * sm.dz[k];
-        if (ORDERED && isfinite(v)) ds_fixed_add(fixed + 2 * (sb * HW + sm.q[k]), v);
-        else atomicAdd(d_depth + sb * HW + sm.q[k], v);   // (ordered form: non-finite values only)
+        if (ORDERED && ds_fixed_ok(v)) ds_fixed_add(fixed + 2 * (sb * HW + sm.q[k]), v);
+        else atomicAdd(d_depth + sb * HW + sm.q[k], v);   // (ordered form: non-finite or |v| >= 2^25 only)
       }
     // coordinates (zeros padding: out-of-range taps contribute nothing)
     const float x0 = floorf(sm.ix), y0 = floorf(sm.iy), x1 = x0 + 1.f, y1 = y0 + 1.f;

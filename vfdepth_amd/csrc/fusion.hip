@@ -2682,14 +2682,28 @@ int vfd_fuse_pose_bwd(const vfd_voxel_desc* d, const void* plan, const int* coun
   return vfd_fuse_pose_bwd_t(d, plan, counts, d_out, 0, d_feats, stream);
 }
 
+// The planned K1 backward's split-tile partials live in ITS workspace, after the depth-column
+// partials — not in the plan's pool, which the K2 backward of the same step uses: with the pose
+// branch on its own stream the two backwards run concurrently, and a shared pool let each overwrite
+// the other's partial tiles (round 6: wrong d feats for both in HIP-graph replays, where the two
+// overlap most; tests/graph_det_worker.py).
+static size_t k1_partial_bytes(const vfd_voxel_desc* d) {
+  return (vfd_fuse_depth_bwd_workspace(d) + 255) / 256 * 256;
+}
+
+size_t vfd_fuse_depth_bwd_planned_workspace(const vfd_voxel_desc* d) {
+  return k1_partial_bytes(d) + PLAN_POOL_BYTES;
+}
+
 int vfd_fuse_depth_bwd_planned(const vfd_voxel_desc* d, const void* plan, const float* d_vox, const float* vox,
                                const float* mask_lo, const float* K, const float* Einv, float* dP, float* d_wzb,
                                void* ws, size_t ws_bytes, void* stream) {
   int st = check_voxel_desc(d);
   if (st) return st;
   VFD_REQUIRE(d->Cv == K1G_CV, "fuse_depth_bwd_planned: Cv=%d (the gather backward needs %d)", d->Cv, K1G_CV);
-  VFD_REQUIRE(plan && d_vox && vox && dP && d_wzb, "fuse_depth_bwd_planned: null argument");
-  VFD_REQUIRE(ws_bytes >= vfd_fuse_depth_bwd_workspace(d), "workspace too small");
+  VFD_REQUIRE(plan && d_vox && vox && dP && d_wzb && ws, "fuse_depth_bwd_planned: null argument");
+  VFD_REQUIRE(ws_bytes >= vfd_fuse_depth_bwd_planned_workspace(d),
+              "fuse_depth_bwd_planned: workspace too small (vfd_fuse_depth_bwd_planned_workspace)");
   hipStream_t s = (hipStream_t)stream;
   const int V = d->X * d->Y * d->Z;
   const int* row_ptr = (const int*)((const char*)plan + plan_entries_bytes(d));
@@ -2697,7 +2711,7 @@ int vfd_fuse_depth_bwd_planned(const vfd_voxel_desc* d, const void* plan, const 
   const int4* tasks = (const int4*)((const char*)csr + plan_items_bytes(d));
   const int* ctrl = (const int*)((const char*)tasks + plan_tasks_bytes(d));
   const int4* combos = tasks + (d->B * d->N * host_tiles(d) + PBW_POOL);
-  float* pool = (float*)((char*)ctrl + 256 + plan_fold_bytes(d));
+  float* pool = (float*)((char*)ws + k1_partial_bytes(d));      // this call's own split-tile partials
   ProfScope ps(K_FUSE_DEPTH_BWD, s);
   const int ntask_max = host_tiles(d) * d->B * d->N + PBW_POOL;
   fuse_depth_bwd_gather_k<<<128 * cdiv(ntask_max, 128), 64, 0, s>>>(*d, tasks, ctrl, csr, d_vox, vox, pool, dP);

@@ -189,7 +189,8 @@ class FuseDepth(torch.autograd.Function):
         d = ctx.space.desc(B, N, Cv=Cv)
         dP = torch.empty(B, N, hw, 2 * Cv, device=g.device)
         dwzb = torch.empty(5, Cv, device=g.device)
-        nbytes = lib.vfd_fuse_depth_bwd_workspace(ctypes.byref(d))
+        nbytes = (lib.vfd_fuse_depth_bwd_planned_workspace if ctx.plan is not None
+                  else lib.vfd_fuse_depth_bwd_workspace)(ctypes.byref(d))
         ws = _ws(nbytes, g.device)
         if ctx.plan is not None:
             plan, ctx.plan = ctx.plan.build(), None

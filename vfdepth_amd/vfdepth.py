@@ -165,8 +165,13 @@ class VFDepthAlgo:
                 # the broadcast is a self-copy whose in-place version bump on the BatchNorm running
                 # stats (saved by MIOpen's batch-norm backward) breaks the second pose-net call of
                 # the step; at world > 1 SyncBatchNorm's synchronised path saves no running stats
-                models[k] = DDP(v, device_ids=[self.device.index] if on_gpu else None,
-                                broadcast_buffers=self.world_size > 1)
+                # ddp.graph_capture: built with the capture stream current, so the AccumulateGrad
+                # nodes (and DDP's hooks) live on a stream a HIP graph can capture (_capture_stream)
+                cap = on_gpu and bool(cfg['ddp'].get('graph_capture', False))
+                with (torch.cuda.stream(self._capture_stream()) if cap else contextlib.nullcontext()):
+                    models[k] = DDP(v, device_ids=[self.device.index] if on_gpu else None,
+                                    broadcast_buffers=self.world_size > 1)
+                self._ddp_on_capture_stream = cap
         return models
 
     def _dataset(self, cfg, mode, with_depth):
@@ -419,29 +424,16 @@ class VFDepthAlgo:
         self.optimizer.step()
         return {k: (v.detach() if torch.is_tensor(v) else v) for k, v in losses.items()}
 
-    def _rewrap_ddp(self, stream):
-        """Rebuild the DDP wrappers with `stream` current.  DDP's reducer creates (and keeps) every
-        parameter's AccumulateGrad node at construction, and autograd accumulates a gradient on the
-        stream its node was created on: built on the default stream (as `prepare_model` does, like
-        the reference), the captured backward's accumulations would go to the legacy default stream,
-        which cannot join a capture.  The old wrappers are dropped first so their nodes die and
-        the new reducer makes fresh ones on `stream` (PyTorch's DDP + graph-capture recipe)."""
-        import weakref
-        from torch.nn.parallel import DistributedDataParallel as DDP
-        for k in list(self.models):
-            m = self.models[k]
-            inner, kw = m.module, dict(device_ids=m.device_ids, broadcast_buffers=m.broadcast_buffers,
-                                       process_group=m.process_group)
-            old = weakref.ref(m.reducer)
-            self.models[k] = m = None
-            gc.collect()
-            if old() is not None:
-                # its AccumulateGrad nodes (on the stream DDP was built on) would be reused
-                refs = [type(r).__name__ for r in gc.get_referrers(old())]
-                raise RuntimeError(f'{k}: the previous DDP reducer is still referenced ({refs}); '
-                                   'cannot rebuild DDP on the capture stream')
-            with torch.cuda.stream(stream):
-                self.models[k] = DDP(inner, **kw)
+    def _capture_stream(self):
+        """The stream a captured step warms up and is captured on (created once).  Under DDP with
+        `ddp.graph_capture` the DDP wrappers are BUILT with it current (prepare_model): DDP's reducer
+        creates and keeps every parameter's AccumulateGrad node at construction, and autograd
+        accumulates each gradient (and fires DDP's all-reduce hooks) on the stream its node was
+        created on — on the legacy default stream, which cannot join a capture (round 6:
+        hipErrorStreamCaptureImplicit in the captured backward), unless DDP was built on this one."""
+        if getattr(self, '_cap_stream', None) is None:
+            self._cap_stream = torch.cuda.Stream(self.device)
+        return self._cap_stream
 
     def graphed_train_step(self, batch, warmup=3):
         """Capture one whole training step (forward, losses, backward, Adam) in a HIP graph.
@@ -455,7 +447,8 @@ class VFDepthAlgo:
         and every AccumulateGrad node lives on a captured stream.
 
         Under DDP (trainer/vfdepth_trainer.py:61-66 with models/vfdepth.py:56-71's wrapping) the
-        wrappers are rebuilt on the capture stream (`_rewrap_ddp`) and the captured step holds DDP's
+        config must set `ddp.graph_capture: True` (the wrappers are then built on the capture
+        stream, `_capture_stream`), and the captured step holds DDP's
         bucketed gradient all-reduces and the fused BN's SyncBatchNorm all-reduces (RCCL kernels on
         the ranks' streams, captured with the step): DDP settles its buckets during its first
         iterations, so at least 11 eager DDP steps run before the capture, as PyTorch requires.
@@ -467,10 +460,17 @@ class VFDepthAlgo:
         # no autograd graph of an earlier step may survive into the warm-up or the capture: its
         # AccumulateGrad nodes would carry their stream into the captured backward
         gc.collect()
-        cap = torch.cuda.Stream(self.device)          # warm-up AND capture stream
+        if self.ddp_enable and not getattr(self, '_ddp_on_capture_stream', False):
+            raise RuntimeError('graphed_train_step under DDP needs the DDP wrappers built on the capture '
+                               'stream: set cfg["ddp"]["graph_capture"] = True before constructing VFDepthAlgo')
+        if self.ddp_enable and (os.environ.get('TORCH_NCCL_CUDA_EVENT_CACHE') != '0'
+                                or os.environ.get('TORCH_NCCL_ASYNC_ERROR_HANDLING') != '0'):
+            # the process group's watchdog polls its works' events; pooled events re-recorded inside
+            # the capture make that poll fail (hipErrorCapturedEvent aborts the process, round 6)
+            raise RuntimeError('graphed_train_step under DDP: export TORCH_NCCL_CUDA_EVENT_CACHE=0 and '
+                               'TORCH_NCCL_ASYNC_ERROR_HANDLING=0 before init_process_group')
+        cap = self._capture_stream()                  # warm-up AND capture stream
         cap.wait_stream(torch.cuda.current_stream(self.device))
-        if self.ddp_enable:
-            self._rewrap_ddp(cap)
         with torch.cuda.stream(cap):
             for i in range(warmup):
                 self.train_step(dict(static))

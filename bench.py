@@ -401,23 +401,31 @@ def main():
     elapsed = time.perf_counter() - t0
     # per-kernel device times: HIP events around each hot-path launch on its stream, recorded in
     # a few eager steps right after the timed region (the timed steps carry no profiling hooks;
-    # graph replays could not fire them); kernel durations do not depend on how they were issued
+    # graph replays could not fire them).  Two sets: first one-stream steps (`frac_isolated`: a
+    # kernel alone on the chip), then steps in the TIMED configuration (the pose branch on its own
+    # stream, so an event pair also times the other branch's kernels sharing the CUs): the line's
+    # `roofline` is the latter, which rocprofv3 of the same command reproduces (profiles/r6/)
     n_prof = min(args.steps, 5)
     torch.cuda.synchronize()
     from vfdepth_amd import kernels as KN
-    KN.syncbn_stats(reset=True)
-    # one stream while the per-kernel events are recorded: with the pose branch on its own stream
-    # the two branches' kernels share the CUs, and an event pair would time the contention too
-    algo.branch_streams = False
-    _lib.prof_enable('all')
-    for _ in range(n_prof):
-        losses = eager_step()
-    torch.cuda.synchronize()
-    sbn = KN.syncbn_stats(reset=True)
-    prof = _lib.prof_read()
-    dense_bytes = {k: v * args.steps / n_prof for k, v in _lib.ALG_BYTES.items()}
-    _lib.prof_enable('off')
-    prof = {k: (n * args.steps // n_prof, t * args.steps / n_prof) for k, (n, t) in prof.items()}
+
+    def profiled(branch):
+        algo.branch_streams = branch
+        KN.syncbn_stats(reset=True)
+        _lib.prof_enable('all')
+        for _ in range(n_prof):
+            last = eager_step()
+        torch.cuda.synchronize()
+        stats = KN.syncbn_stats(reset=True)
+        pr = _lib.prof_read()
+        dense = {k: v * args.steps / n_prof for k, v in _lib.ALG_BYTES.items()}
+        _lib.prof_enable('off')
+        pr = {k: (n * args.steps // n_prof, t * args.steps / n_prof) for k, (n, t) in pr.items()}
+        return pr, dense, stats, last
+    timed_branch = getattr(algo, '_bstream', None) is not None
+    prof_iso, _, _, _ = profiled(False)
+    prof, dense_bytes, sbn, losses = profiled(timed_branch)
+    algo.branch_streams = True
     elapsed = max_over_ranks(elapsed, world, f'cuda:{local}')
     if rank != 0:
         dist.destroy_process_group()
@@ -431,8 +439,8 @@ def main():
         s['map_bytes'] = 2            # config 3: K2 writes the pose map in bf16 (kernels.PoseConvBF16)
     traffic_tab = load_traffic(args.config)
 
-    def roofline_of(k):
-        n_launch, ms = prof[k]
+    def roofline_of(k, table=None):
+        n_launch, ms = (table or prof)[k]
         avg_s = ms / 1e3 / n_launch
         fl = mfma_flops(k, s)
         if fl is not None:
@@ -502,7 +510,10 @@ def main():
         'config': {'workload': name, 'config_id': args.config, 'batch_per_gpu': s['B'], 'cameras': s['N'],
                    'image': [s['H'], s['W']], 'voxels': [s['X'], s['Y'], s['Z']], 'depth_bins': s['D'],
                    'parallelism': f'dp{world}', 'net_precision': cfg['training']['net_precision']},
-        'roofline': roofline_of(dom),
+        'roofline': dict(roofline_of(dom), measured_in='the timed configuration (pose branch on its own stream)'
+                         if timed_branch else 'one stream (the timed configuration)',
+                         frac_isolated=roofline_of(dom, prof_iso)['frac'] if dom in prof_iso else None,
+                         avg_launch_us_isolated=roofline_of(dom, prof_iso)['avg_launch_us'] if dom in prof_iso else None),
         'roofline_hbm_dominant': roofline_of(dom_hbm),
         'roofline_aggregate': {'bound': 'hbm', 'achieved': agg_bytes / agg_s / 1e9, 'peak': HBM_PEAK_GBS,
                                'unit': 'GB/s', 'frac': agg_bytes / agg_s / 1e9 / HBM_PEAK_GBS,

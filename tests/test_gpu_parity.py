@@ -546,8 +546,11 @@ def _near_decisions(O, ci, co, go, c, frames, noise, margin=1e-4):
     return torch.nn.functional.max_pool2d(near.float(), 3, 1, 1) > 0
 
 
-def test_full_step_gradient_chain():
-    """Full fusion step, gradient parity stage by stage with the decisions held fixed:
+@pytest.mark.parametrize('shape', ['small', 'full'])
+def test_full_step_gradient_chain(shape):
+    """Full fusion step, gradient parity stage by stage with the decisions held fixed, at the
+    fixtures' reduced shape (96x160, 40x40x10 voxels, D=16) and at BASELINE config 2's full shape
+    (6 x 384x640, 100x100x20 voxels, D=50 — the shape the bench measures):
 
     1. loss path: d total / d disp and d total / d cam_T_cam of the GPU step against the CPU
        oracle's view synthesis + losses (view_rendering.py, multi_cam_loss.py) evaluated on the GPU's
@@ -555,17 +558,27 @@ def test_full_step_gradient_chain():
     2. nets: the GPU's upstream gradients injected into the CPU oracle step's disparity and pose
        outputs (same modules, weights and inputs) must give the GPU's parameter gradients — the
        backward of K1/K2/K3, the fused aggregation and the dense layers, with no decision between.
+    (models/vfdepth.py:191-313; network/volumetric_fusionnet.py:197-230)
     """
     from oracle import vfd_oracle as O
     from vfdepth_amd import synth
     from vfdepth_amd.layers import seeded_state_dict
     from vfdepth_amd.network import FusedDepthNet, FusedPoseNet
     from vfdepth_amd.vfdepth import VFDepthAlgo
-    fx = golden('step_small.npz')
-    cfg = G.step_cfg()
-    N, frames = cfg['data']['num_cams'], cfg['training']['frame_ids']
-    noise = torch.stack([torch.tensor(fx[f'noise_c{c}']) for c in range(N)])
-    inputs = synth.make_batch(cfg, seed=5, with_depth=True)
+    if shape == 'small':
+        fx = golden('step_small.npz')
+        cfg = G.step_cfg()
+        N = cfg['data']['num_cams']
+        noise = torch.stack([torch.tensor(fx[f'noise_c{c}']) for c in range(N)])
+        inputs = synth.make_batch(cfg, seed=5, with_depth=True)
+    else:
+        fx = golden('step_full.npz')
+        cfg = G.full_cfg()
+        N, t = cfg['data']['num_cams'], cfg['training']
+        noise = torch.stack(G.full_noise(fx, (t['batch_size'], len(t['frame_ids']) - 1, t['height'], t['width'])))
+        inputs = synth.make_batch(cfg, seed=G.FULL_SEED, with_depth=True)
+        torch.set_num_threads(max(1, min(16, len(os.sched_getaffinity(0)))))   # the CPU oracle's step
+    frames = cfg['training']['frame_ids']
     cpu_inputs = {k: v.clone() if torch.is_tensor(v) else v for k, v in inputs.items()}
     algo = VFDepthAlgo(cfg, 0)
     for m in algo.models.values():
@@ -603,7 +616,7 @@ def test_full_step_gradient_chain():
     keep = ~near
     frac_near = float(near.float().mean())
     assert frac_near < 0.5, f'{frac_near:.3f} of the pixels near a decision'
-    print(f'loss path: {int(near.sum())} of {near.numel()} px within 1e-4 of a decision')
+    print(f'loss path ({shape}): {int(near.sum())} of {near.numel()} px within 1e-4 of a decision')
     fro, mx = _fro(disp.grad[keep.to(DEV)], d_leaf.grad[keep])
     assert fro < 1e-3 and mx < 1e-2, f'd loss / d disp (outside {int(near.sum())} near-tie px): fro {fro:.3g}, max {mx:.3g}'
     for k in Ts:

@@ -1496,46 +1496,46 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void fu
 }
 
 // Split tiles: the S part slots summed in part order.  A workgroup takes split tiles in turn;
-// thread = channel, one tile row at a time with all S x 4 slot loads of the row in flight, each
-// channel's 4 pixels of the row written as one 16-B store.
-__global__ __launch_bounds__(256) void pose_combine_k(vfd_voxel_desc d, const int4* __restrict__ combos,
-                                                      const int* __restrict__ ctrl, const float* __restrict__ pool,
-                                                      float* __restrict__ dfeats) {
+// thread = (tile row, channel): all PT rows at once (one round of S x PT slot loads per thread,
+// the rows in flight together instead of one after another: 19 -> ~8 us per call at config 2),
+// each channel's 4 pixels of a row written as one 16-B store.
+constexpr int PCB_THREADS = PT * POSE_MAXC;
+__global__ __launch_bounds__(PCB_THREADS) void pose_combine_k(vfd_voxel_desc d, const int4* __restrict__ combos,
+                                                              const int* __restrict__ ctrl, const float* __restrict__ pool,
+                                                              float* __restrict__ dfeats) {
   const int nt = tiles_x(d) * tiles_y(d), ntx = tiles_x(d);
   const int hw = d.h * d.w;
-  const int ch = threadIdx.x;                      // 256 threads = POSE_MAXC channels
+  const int ch = threadIdx.x % POSE_MAXC, py = threadIdx.x / POSE_MAXC;
   const int ncombo = ctrl[1];
   const bool vec = (d.w % 4) == 0;
   for (int k = blockIdx.x; k < ncombo; k += gridDim.x) {
     const int4 cb = combos[k];
     const int bc = cb.x / nt, tile = cb.x % nt;
     const int x0 = (tile % ntx) * PT, y0 = (tile / ntx) * PT;
-    if (ch >= d.C) continue;
+    if (ch >= d.C || y0 + py >= d.h) continue;
     const float* p0 = pool + (size_t)cb.y * PT2 * POSE_MAXC + ch;
     float* db = dfeats + ((size_t)bc * d.C + ch) * hw;
-    for (int py = 0; py < PT && y0 + py < d.h; ++py) {
-      // every slot load unconditional (absent parts re-read the last slot and add +0)
-      float v[PBW_MAXS][PT];
+    // every slot load unconditional (absent parts re-read the last slot and add +0)
+    float v[PBW_MAXS][PT];
 #pragma unroll
-      for (int s = 0; s < PBW_MAXS; ++s)
+    for (int s = 0; s < PBW_MAXS; ++s)
 #pragma unroll
-        for (int px = 0; px < PT; ++px)
-          v[s][px] = p0[((size_t)min(s, cb.z - 1) * PT2 + py * PT + px) * POSE_MAXC];
-      float a[PT];
+      for (int px = 0; px < PT; ++px)
+        v[s][px] = p0[((size_t)min(s, cb.z - 1) * PT2 + py * PT + px) * POSE_MAXC];
+    float a[PT];
 #pragma unroll
-      for (int px = 0; px < PT; ++px) {
-        a[px] = v[0][px];
+    for (int px = 0; px < PT; ++px) {
+      a[px] = v[0][px];
 #pragma unroll
-        for (int s = 1; s < PBW_MAXS; ++s) a[px] += (s < cb.z ? 1.f : 0.f) * v[s][px];   // part order
-      }
-      float* dst = db + (size_t)(y0 + py) * d.w + x0;
-      if (vec && x0 + PT <= d.w) {
-        *reinterpret_cast<float4*>(dst) = make_float4(a[0], a[1], a[2], a[3]);
-      } else {
+      for (int s = 1; s < PBW_MAXS; ++s) a[px] += (s < cb.z ? 1.f : 0.f) * v[s][px];   // part order
+    }
+    float* dst = db + (size_t)(y0 + py) * d.w + x0;
+    if (vec && x0 + PT <= d.w) {
+      *reinterpret_cast<float4*>(dst) = make_float4(a[0], a[1], a[2], a[3]);
+    } else {
 #pragma unroll
-        for (int px = 0; px < PT; ++px)
-          if (x0 + px < d.w) dst[px] = a[px];
-      }
+      for (int px = 0; px < PT; ++px)
+        if (x0 + px < d.w) dst[px] = a[px];
     }
   }
 }
@@ -1666,39 +1666,37 @@ __global__ __launch_bounds__(64) void fuse_depth_bwd_gather_k(vfd_voxel_desc d, 
   }
 }
 
-// split tiles of the K1 gather: the S part slots summed in part order (thread = d P channel)
-__global__ __launch_bounds__(128) void fuse_depth_combine_k(vfd_voxel_desc d, const int4* __restrict__ combos,
-                                                            const int* __restrict__ ctrl,
-                                                            const float* __restrict__ pool, float* __restrict__ dP) {
+// split tiles of the K1 gather: the S part slots summed in part order (thread = (tile row, d P
+// channel): all PT rows' slot loads in one round)
+constexpr int K1C_THREADS = PT * 2 * K1G_CV;
+__global__ __launch_bounds__(K1C_THREADS) void fuse_depth_combine_k(vfd_voxel_desc d, const int4* __restrict__ combos,
+                                                                    const int* __restrict__ ctrl,
+                                                                    const float* __restrict__ pool, float* __restrict__ dP) {
   constexpr int ROW = 2 * K1G_CV;
   const int nt = tiles_x(d) * tiles_y(d), ntx = tiles_x(d);
   const int hw = d.h * d.w;
-  const int ch = threadIdx.x;
+  const int ch = threadIdx.x % ROW, py = threadIdx.x / ROW;
   const int ncombo = ctrl[1];
   for (int k = blockIdx.x; k < ncombo; k += gridDim.x) {
     const int4 cb = combos[k];
     const int bc = cb.x / nt, tile = cb.x % nt;
-    const int x0 = (tile % ntx) * PT, y0 = (tile / ntx) * PT;
+    const int x0 = (tile % ntx) * PT, y = (tile / ntx) * PT + py;
+    if (y >= d.h) continue;
     const float* p0 = pool + (size_t)cb.y * PT2 * POSE_MAXC + ch;
     float* db = dP + (size_t)bc * hw * ROW + ch;
-    // one tile row at a time with all PT x PBW_MAXS slot loads in flight (absent parts re-read
-    // the last slot and add +0: every load unconditional, summed in part order)
-    for (int py = 0; py < PT; ++py) {
-      const int y = y0 + py;
-      if (y >= d.h) break;
-      float v[PT][PBW_MAXS];
+    // absent parts re-read the last slot and add +0: every load unconditional, summed in part order
+    float v[PT][PBW_MAXS];
 #pragma unroll
-      for (int px = 0; px < PT; ++px)
+    for (int px = 0; px < PT; ++px)
 #pragma unroll
-        for (int s2 = 0; s2 < PBW_MAXS; ++s2)
-          v[px][s2] = p0[((size_t)min(s2, cb.z - 1) * PT2 + py * PT + px) * POSE_MAXC];
+      for (int s2 = 0; s2 < PBW_MAXS; ++s2)
+        v[px][s2] = p0[((size_t)min(s2, cb.z - 1) * PT2 + py * PT + px) * POSE_MAXC];
 #pragma unroll
-      for (int px = 0; px < PT; ++px) {
-        float a = v[px][0];
+    for (int px = 0; px < PT; ++px) {
+      float a = v[px][0];
 #pragma unroll
-        for (int s2 = 1; s2 < PBW_MAXS; ++s2) a += (s2 < cb.z ? 1.f : 0.f) * v[px][s2];
-        if (x0 + px < d.w) db[((size_t)y * d.w + x0 + px) * ROW] = a;
-      }
+      for (int s2 = 1; s2 < PBW_MAXS; ++s2) a += (s2 < cb.z ? 1.f : 0.f) * v[px][s2];
+      if (x0 + px < d.w) db[((size_t)y * d.w + x0 + px) * ROW] = a;
     }
   }
 }
@@ -2673,7 +2671,7 @@ int vfd_fuse_pose_bwd_t(const vfd_voxel_desc* d, const void* plan, const int* co
     if (d->pad_out) pose_fold_k<float><<<nfold, 256, 0, s>>>(*d, (const float*)d_out, fbuf, al16);
     fuse_pose_bwd_k<float><<<ntask, 64, 0, s>>>(*d, tasks, ctrl, csr, (const float*)d_out, fbuf, pool, d_feats);
   }
-  pose_combine_k<<<std::min(PBW_POOL / 2, host_tiles(d) * d->B * d->N), 256, 0, s>>>(*d, combos, ctrl, pool, d_feats);
+  pose_combine_k<<<std::min(PBW_POOL / 2, host_tiles(d) * d->B * d->N), PCB_THREADS, 0, s>>>(*d, combos, ctrl, pool, d_feats);
   return fail_launch("fuse_pose_bwd");
 }
 
@@ -2715,7 +2713,7 @@ int vfd_fuse_depth_bwd_planned(const vfd_voxel_desc* d, const void* plan, const 
   ProfScope ps(K_FUSE_DEPTH_BWD, s);
   const int ntask_max = host_tiles(d) * d->B * d->N + PBW_POOL;
   fuse_depth_bwd_gather_k<<<128 * cdiv(ntask_max, 128), 64, 0, s>>>(*d, tasks, ctrl, csr, d_vox, vox, pool, dP);
-  fuse_depth_combine_k<<<std::min(PBW_POOL / 2, host_tiles(d) * d->B * d->N), 2 * K1G_CV, 0, s>>>(
+  fuse_depth_combine_k<<<std::min(PBW_POOL / 2, host_tiles(d) * d->B * d->N), K1C_THREADS, 0, s>>>(
       *d, combos, ctrl, pool, dP);
   // depth-column and bias gradients: the voxel walk without the scatter
   dim3 grid(cdiv(cdiv(V, 64), 4), d->B);

@@ -942,38 +942,43 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pcdf_main_k(PfGeom g, const flo
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-  const float2* wlane = reinterpret_cast<const float2*>(Wd) + (size_t)(wv * 64 + li) * 2 + lh;
-  float2 bq[PD_PF][2];
-  int pf_atom = a_lo, pf_it = 0;
-  // the prefetched atom's weight base (its channel chunk and n-tile), advanced once per atom: the
-  // per-iteration address is then one multiply-add
-  // (a uniform float2 offset, kept scalar; the lane's part is wlane)
-  unsigned pf_off = 0;
-  auto pf_set = [&]() {
-    const int t = pf_atom / PD_CHUNKS, ch = pf_atom - t * PD_CHUNKS;
-    pf_off = ((unsigned)(ch * (PD_OC / 4)) * (unsigned)g.np + (unsigned)(t / g.mtiles) * PD_N) * 2u;
+  // Weight fragments by buffer loads: the lane's part is a constant voffset, the (atom, tap, quad)
+  // part a uniform soffset.  The B fragments of step (tap, q) are loaded four steps ahead into ring
+  // slot q & 3 (static slots: the unrolled quad loop needs no register rotation across the tap
+  // loop's back edge), issued right after step q's MFMAs have read the slot; the next tap's / next
+  // atom's items come from a base selected without a branch (the range's last atom re-reads its
+  // own, in range and unused).  Round 6: no scalar branches in the tap loop (the per-step prefetch
+  // bookkeeping split every quad step into several basic blocks, which kept the scheduler from
+  // issuing the next A fragments' LDS reads before the MFMAs).
+  constexpr int PFD_RING = 4;
+  const unsigned npb = (unsigned)g.np * 16u;          // bytes between consecutive (tap, quad) items
+  const __amdgpu_buffer_rsrc_t rs_w = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)Wd, 0, (int)(9u * (PC_O / 4) * npb), 0x00020000);
+  const int voff = ((wv * 64 + li) * 2 + lh) * 8;
+  auto wbase = [&](int at) {                          // byte offset of atom `at`'s (tap 0, quad 0) item
+    const int t = at / PD_CHUNKS, ch = at - t * PD_CHUNKS;
+    // wave-uniform (the division runs on the vector unit): readfirstlane keeps the buffer loads'
+    // soffset scalar (a VGPR soffset compiles to a waterfall loop per load)
+    return (unsigned)__builtin_amdgcn_readfirstlane(
+        (int)((unsigned)(ch * (PD_OC / 4)) * npb + (unsigned)(t / g.mtiles) * (PD_N * 16u)));
   };
-  pf_set();
-  auto prefetch = [&](int slot) {
-    if (pf_atom < a_hi) {
-      const int tap = pf_it >> 3, q = pf_it & 7;
-      const float2* w = wlane + (pf_off + (unsigned)(tap * (PC_O / 4) + q) * (unsigned)g.np * 2u);
-      bq[slot][0] = w[0];
-      bq[slot][1] = w[64];
-      if (++pf_it == PD_ITERS) {
-        pf_it = 0;
-        ++pf_atom;
-        if (pf_atom < a_hi) pf_set();
-      }
-    }
+  auto wload = [&](unsigned soff, float2 (&b)[2]) {
+    const auto v0 = __builtin_amdgcn_raw_buffer_load_b64(rs_w, voff, (int)soff, 0);
+    const auto v1 = __builtin_amdgcn_raw_buffer_load_b64(rs_w, voff + 512, (int)soff, 0);
+    b[0] = make_float2(__uint_as_float(v0[0]), __uint_as_float(v0[1]));
+    b[1] = make_float2(__uint_as_float(v1[0]), __uint_as_float(v1[1]));
   };
+  float2 bq[PFD_RING][2];
+  unsigned cbase = wbase(a_lo);
 #pragma unroll
-  for (int k = 0; k < PD_PF; ++k) prefetch(k);
+  for (int q = 0; q < PFD_RING; ++q) wload(cbase + (unsigned)q * npb, bq[q]);
+  constexpr int NQ = PD_OC / 4;                       // quads per tap (8)
   int cur_t = -1;
   int pyx[4];                                         // (row << 16) | column of the lane's pixels
   for (int atom = a_lo; atom < a_hi; ++atom) {
     const int t = atom / PD_CHUNKS, ch = atom - t * PD_CHUNKS;
     const PfTile tl = pf_tile(g, t);
+    const unsigned nbase = atom + 1 < a_hi ? wbase(atom + 1) : cbase;
     if (t != cur_t) {                                 // pixel geometry once per tile (8 atoms)
       cur_t = t;
 #pragma unroll
@@ -1012,31 +1017,37 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pcdf_main_k(PfGeom g, const flo
     for (int a = 0; a < 4; ++a) afc[a] = *reinterpret_cast<const float2*>(&xb[o1c[a]]);
 #pragma unroll 1
     for (int tap = 0; tap < 9; ++tap) {
+      // refill items: (tap, q + 4) for q < 4; (tap + 1, q - 4) of this atom, or of the next at tap 8
+      const unsigned tb = (unsigned)__builtin_amdgcn_readfirstlane((int)(cbase + (unsigned)(tap * (PC_O / 4)) * npb));
+      const unsigned nb = (unsigned)__builtin_amdgcn_readfirstlane((int)(tap < 8 ? tb + (unsigned)(PC_O / 4) * npb : nbase));
 #pragma unroll
-      for (int q = 0; q < PD_OC / 4; ++q) {
-        const int ring = q % PD_PF;
-        const float2 b0 = bq[ring][0], b1 = bq[ring][1];
-        prefetch(ring);
-        if (q < PD_OC / 4 - 1) {
+      for (int q = 0; q < NQ; ++q) {
+        if (q < NQ - 1) {
 #pragma unroll
           for (int a = 0; a < 4; ++a) afn[a] = *reinterpret_cast<const float2*>(&xb[o1c[a] + 4 * (q + 1)]);
-        } else if (tap < 8) {                         // the current tap's loads are all issued
-          offsets(tap + 1, o1c);
+        } else {                                      // the next tap's first quad (tap 8: unused)
+          offsets(tap < 8 ? tap + 1 : 8, o1c);
 #pragma unroll
           for (int a = 0; a < 4; ++a) afn[a] = *reinterpret_cast<const float2*>(&xb[o1c[a]]);
         }
 #pragma unroll
-        for (int s = 0; s < 2; ++s)
+        for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
           for (int a = 0; a < 4; ++a) {
-            const float v = s ? afc[a].y : afc[a].x;
-            acc[a][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(v, s ? b0.y : b0.x, acc[a][0], 0, 0, 0);
-            acc[a][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(v, s ? b1.y : b1.x, acc[a][1], 0, 0, 0);
+            const float v = s2 ? afc[a].y : afc[a].x;
+            acc[a][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(v, s2 ? bq[q & 3][0].y : bq[q & 3][0].x, acc[a][0], 0, 0, 0);
+            acc[a][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(v, s2 ? bq[q & 3][1].y : bq[q & 3][1].x, acc[a][1], 0, 0, 0);
           }
+        wload(q < 4 ? tb + (unsigned)(q + 4) * npb : nb + (unsigned)(q - 4) * npb, bq[q & 3]);
+        // in this step: the next A fragments' LDS reads first, then the 16 MFMAs, then the refill
+        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);   // DS read
+        __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);   // VMEM read
 #pragma unroll
         for (int a = 0; a < 4; ++a) afc[a] = afn[a];
       }
     }
+    cbase = nbase;
     __syncthreads();                                  // buffer handed back to the loader waves
     if (ch == PD_CHUNKS - 1 || atom == a_hi - 1) {
       const int ts = t * PD_CHUNKS;

@@ -483,6 +483,9 @@ def main():
     # aggregate over every HBM-bound hot-path op of the step (per-kernel and aggregate)
     agg_bytes = sum(algorithmic_bytes(k, s) * prof[k][0] for k in hbm_ops)
     agg_s = sum(prof[k][1] for k in hbm_ops) / 1e3
+    iso_ops = [k for k in hbm_ops if k in prof_iso]     # the same ops in the one-stream profiling steps
+    agg_iso = (sum(algorithmic_bytes(k, s) * prof_iso[k][0] for k in iso_ops)
+               / (sum(prof_iso[k][1] for k in iso_ops) / 1e3) / 1e9) if iso_ops else None
     parity = None
     if not args.no_parity:
         # the parity steps run other shapes (96x160, the fixture's): immediate mode, no MIOpen search
@@ -519,6 +522,9 @@ def main():
                                'unit': 'GB/s', 'frac': agg_bytes / agg_s / 1e9 / HBM_PEAK_GBS,
                                'alg_bytes_per_step': agg_bytes / args.steps,
                                'kernel_ms_per_step': agg_s * 1e3 / args.steps,
+                               'measured_in': 'the timed configuration (each op timed on its stream while the '
+                                              'other branch runs beside it)' if timed_branch else 'one stream',
+                               'frac_isolated': agg_iso / HBM_PEAK_GBS if agg_iso else None,
                                'what': 'every HBM-bound hot-path op of the step (K1-K5, plans, aggregation)'},
         'hot_path_ms_per_step': sum(t for _, t in prof.values()) / args.steps,
         'dense_fused': {k: roofline_any(k) for k in dense},

@@ -263,7 +263,8 @@ int vfd_reflect_pad1_bwd(const void* g, void* dx, long long planes, int h, int w
 /* One-launch BatchNorm(+residual)(+ReLU) forward / backward for channels of at most 8192 elements
  * with local statistics (the small ResNet layers): one workgroup per channel computes the fp64
  * statistics and applies them; same arguments and results as bn_fwd_stats + bn_fwd_apply /
- * bn_bwd_stats + bn_bwd_apply (d->S unused).  vfd_bn1_fits: 1 when the shape qualifies. */
+ * bn_bwd_stats + bn_bwd_apply (d->S unused).  vfd_bn1_fits: 1 when the shape qualifies (NCHW maps;
+ * channels-last maps take the split path). */
 int vfd_bn1_fits(const vfd_bn_desc* d);
 int vfd_bn1_fwd(const vfd_bn_desc* d, const void* x, const void* residual, const float* gamma, const float* beta,
                 void* y, float* mean, float* invstd, float* running_mean, float* running_var,

@@ -835,12 +835,10 @@ def test_pose_conv_bf16_map_matches_two_nodes(config, B, monkeypatch):
         x32 = KN.FusePose.apply(space, plan, feats)
         x16 = KN._pose_fuse_t(space, plan, feats, torch.bfloat16)
         assert torch.equal(x16, x32.to(torch.bfloat16)), 'bf16 map != the fp32 map rounded to nearest even'
-        # K2's azimuth-sector voxel order (one XCD per sector) only reorders work: the map is the
-        # index-order launch's, bit for bit
-        monkeypatch.setenv('VFD_POSE_SECTORS', '1')
-        assert space.pose_order() is not None
-        assert torch.equal(KN.FusePose.apply(space, plan, feats), x32), 'sector order changed the map'
-        monkeypatch.delenv('VFD_POSE_SECTORS')
+        # K2's azimuth-sector voxel order (the C ABI's `order`: one XCD per sector) only reorders
+        # work: the map is the index-order launch's, bit for bit
+        xs = KN._pose_fuse_t(space, plan, feats, torch.float32, order=space.pose_order())
+        assert torch.equal(xs, x32), 'sector order changed the map'
     wf = KN.pad_conv_weight_fragments_bf16(w, C1, Z)
     la = [t.clone().requires_grad_(True) for t in (feats, w, b)]
     lb = [t.clone().requires_grad_(True) for t in (feats, w, b)]

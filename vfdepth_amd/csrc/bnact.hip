@@ -385,10 +385,9 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply_k(vfd_bn_desc d, cons
 // (the second sweep re-reads the channel from L2), so a layer is one launch each way instead of
 // two, and no partials round-trip through memory.  Fixed summation order: deterministic.
 constexpr int BN1_THREADS = 512;
-#ifndef VFD_BN1_NHWC
-#define VFD_BN1_NHWC 0   // one-launch channels-last small layers (bn1n_*): opt-in — with C / 8 blocks they
-                         // lose to the 3-launch split path (config 3: BN 4.50 vs 3.86 ms/step)
-#endif
+// (channels-last maps take the 3-launch split path: a one-launch NHWC form, a block per 8 channels,
+// measured slower — config 3 BN 4.50 vs 3.86 ms/step with C / 8 blocks per layer — and was retired
+// in round 6)
 constexpr unsigned BN1_MAX = 8192;   // layer2 (23040 / channel) keeps the split path: its 128 channels alone would leave half the CUs idle
 
 __device__ __forceinline__ double block_sum1(double v, double* sh) {
@@ -817,183 +816,6 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply_nhwc_k(vfd_bn_desc d,
   }
 }
 
-// ---- one-launch channels-last variants (round 4): the small NHWC layers (<= BN1_MAX rows) took
-// three launches each way (statistics, split reduction, apply: 6-9 us each, launch-bound).  A block
-// owns BN1N_CG consecutive channels of every row: thread t the channel quad t % 4 of rows
-// t / 4, t / 4 + 128, ... (one 8-B bf16 / 16-B fp32 load per row), its row-slot partials summed in
-// LDS in row-slot order (fixed: deterministic), then the apply pass over the same elements.
-constexpr int BN1N_CG = 8;                           // channels per block (C / 8 blocks)
-constexpr int BN1N_U = 4;                            // rows' loads in flight per thread
-constexpr int BN1N_RS = BN1_THREADS / (BN1N_CG / 4);  // row slots (128)
-
-// the block's per-channel (sum a, sum b) from the threads' quad accumulators: [RS][CG] in LDS,
-// thread c < CG adds its column in row-slot order
-__device__ __forceinline__ void bn1n_reduce(const double (&a)[4], const double (&b)[4], double* sa, double* sb,
-                                            double* ca, double* cb) {
-  const int qi = threadIdx.x % (BN1N_CG / 4), rs = threadIdx.x / (BN1N_CG / 4);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    sa[rs * BN1N_CG + 4 * qi + k] = a[k];
-    sb[rs * BN1N_CG + 4 * qi + k] = b[k];
-  }
-  __syncthreads();
-  if (threadIdx.x < BN1N_CG) {
-    double u = 0.0, v = 0.0;
-    for (int r = 0; r < BN1N_RS; ++r) {
-      u += sa[r * BN1N_CG + threadIdx.x];
-      v += sb[r * BN1N_CG + threadIdx.x];
-    }
-    ca[threadIdx.x] = u;
-    cb[threadIdx.x] = v;
-  }
-  __syncthreads();
-}
-
-template <typename T>
-__global__ __launch_bounds__(BN1_THREADS) void bn1n_fwd_k(vfd_bn_desc d, const T* __restrict__ x,
-                                                          const T* __restrict__ r, const float* __restrict__ gamma,
-                                                          const float* __restrict__ beta, T* __restrict__ y,
-                                                          float* __restrict__ mean_out, float* __restrict__ invstd_out,
-                                                          float* __restrict__ run_mean, float* __restrict__ run_var,
-                                                          long long* __restrict__ nbt, unsigned char* __restrict__ mk) {
-  __shared__ double sa[BN1N_RS * BN1N_CG], sb[BN1N_RS * BN1N_CG], ca[BN1N_CG], cb[BN1N_CG];
-  __shared__ float2 coef[BN1N_CG];
-  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] += 1;
-  const int qi = threadIdx.x % (BN1N_CG / 4), rs = threadIdx.x / (BN1N_CG / 4);
-  const int c0 = blockIdx.x * BN1N_CG, cq = c0 + 4 * qi;
-  const unsigned rows = (unsigned)d.N * (unsigned)d.HW;
-  double a[4] = {}, b[4] = {};
-  for (unsigned r0 = rs; r0 < rows; r0 += BN1N_U * BN1N_RS) {
-    float4 vv[BN1N_U];
-#pragma unroll
-    for (int u = 0; u < BN1N_U; ++u) {
-      const unsigned row = r0 + u * BN1N_RS;
-      vv[u] = row < rows ? ld4(x + (size_t)row * d.C + cq) : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-#pragma unroll
-    for (int u = 0; u < BN1N_U; ++u) {       // rows in order; rows past the end add exact zeros
-      const float4 v = vv[u];
-      a[0] += v.x; a[1] += v.y; a[2] += v.z; a[3] += v.w;
-      b[0] += (double)v.x * v.x; b[1] += (double)v.y * v.y;
-      b[2] += (double)v.z * v.z; b[3] += (double)v.w * v.w;
-    }
-  }
-  bn1n_reduce(a, b, sa, sb, ca, cb);
-  if (threadIdx.x < BN1N_CG) {                 // bn1_fwd_k's per-channel arithmetic
-    const int c = c0 + threadIdx.x;
-    const double count = (double)rows;
-    const double mean_d = ca[threadIdx.x] / count;
-    double var_d = cb[threadIdx.x] / count - mean_d * mean_d;
-    var_d = var_d > 0.0 ? var_d : 0.0;
-    const float mean = (float)mean_d;
-    const float invstd = (float)(1.0 / sqrt(var_d + (double)d.eps));
-    mean_out[c] = mean;
-    invstd_out[c] = invstd;
-    if (run_mean) {
-      const double unbiased = count > 1.0 ? var_d * count / (count - 1.0) : var_d;
-      run_mean[c] = (float)((1.0 - d.momentum) * run_mean[c] + d.momentum * mean_d);
-      run_var[c] = (float)((1.0 - d.momentum) * run_var[c] + d.momentum * unbiased);
-    }
-    const float sc = invstd * gamma[c];
-    coef[threadIdx.x] = make_float2(sc, beta[c] - mean * sc);
-  }
-  __syncthreads();
-  const float2 k0 = coef[4 * qi], k1 = coef[4 * qi + 1], k2 = coef[4 * qi + 2], k3 = coef[4 * qi + 3];
-  const bool relu = d.relu != 0;
-#pragma unroll BN1N_U
-  for (unsigned row = rs; row < rows; row += BN1N_RS) {
-    const size_t o = (size_t)row * d.C + cq;
-    float4 v = ld4(x + o);
-    v.x = v.x * k0.x + k0.y;
-    v.y = v.y * k1.x + k1.y;
-    v.z = v.z * k2.x + k2.y;
-    v.w = v.w * k3.x + k3.y;
-    if (r) {
-      const float4 q = ld4(r + o);
-      v.x += q.x;
-      v.y += q.y;
-      v.z += q.z;
-      v.w += q.w;
-    }
-    if (relu) {
-      v.x = fmaxf(v.x, 0.f);
-      v.y = fmaxf(v.y, 0.f);
-      v.z = fmaxf(v.z, 0.f);
-      v.w = fmaxf(v.w, 0.f);
-    }
-    st4(y + o, v);
-    if (mk) *reinterpret_cast<uchar4*>(mk + o) = make_uchar4(v.x > 0.f, v.y > 0.f, v.z > 0.f, v.w > 0.f);
-  }
-}
-
-template <typename T>
-__global__ __launch_bounds__(BN1_THREADS) void bn1n_bwd_k(vfd_bn_desc d, const T* __restrict__ g,
-                                                          const T* __restrict__ y, const T* __restrict__ x,
-                                                          const float* __restrict__ gamma,
-                                                          const float* __restrict__ mean_in,
-                                                          const float* __restrict__ invstd_in, T* __restrict__ dx,
-                                                          T* __restrict__ dr, float* __restrict__ dgamma,
-                                                          float* __restrict__ dbeta) {
-  __shared__ double sa[BN1N_RS * BN1N_CG], sb[BN1N_RS * BN1N_CG], ca[BN1N_CG], cb[BN1N_CG];
-  __shared__ float4 coef[BN1N_CG];            // k, mean g', mx, mean
-  const int qi = threadIdx.x % (BN1N_CG / 4), rs = threadIdx.x / (BN1N_CG / 4);
-  const int c0 = blockIdx.x * BN1N_CG, cq = c0 + 4 * qi;
-  const unsigned rows = (unsigned)d.N * (unsigned)d.HW;
-  const float4 mu = *reinterpret_cast<const float4*>(mean_in + cq);
-  const bool relu = d.relu != 0;
-  double a[4] = {}, b[4] = {};
-  for (unsigned r0 = rs; r0 < rows; r0 += BN1N_U * BN1N_RS) {
-    float4 gg[BN1N_U], xx[BN1N_U];
-#pragma unroll
-    for (int u = 0; u < BN1N_U; ++u) {
-      const unsigned row = r0 + u * BN1N_RS;
-      const size_t o = (size_t)(row < rows ? row : rs) * d.C + cq;
-      gg[u] = bn_g4(d, g, o);
-      xx[u] = ld4(x + o);
-      if (relu) relu_mask4(d, y, o, gg[u]);
-    }
-#pragma unroll
-    for (int u = 0; u < BN1N_U; ++u) {
-      if (r0 + u * BN1N_RS >= rows) break;
-      const float4 gv = gg[u], xv = xx[u];
-      a[0] += gv.x; a[1] += gv.y; a[2] += gv.z; a[3] += gv.w;
-      b[0] += (double)gv.x * (double)(xv.x - mu.x);
-      b[1] += (double)gv.y * (double)(xv.y - mu.y);
-      b[2] += (double)gv.z * (double)(xv.z - mu.z);
-      b[3] += (double)gv.w * (double)(xv.w - mu.w);
-    }
-  }
-  bn1n_reduce(a, b, sa, sb, ca, cb);
-  if (threadIdx.x < BN1N_CG) {                 // bn1_bwd_k's per-channel arithmetic
-    const int c = c0 + threadIdx.x;
-    const double sg = ca[threadIdx.x], sgx = cb[threadIdx.x];
-    const float invstd = invstd_in[c];
-    if (dgamma) dgamma[c] = (float)(sgx * invstd);
-    if (dbeta) dbeta[c] = (float)sg;
-    const double count = (double)rows;
-    coef[threadIdx.x] = make_float4(gamma[c] * invstd, (float)(sg / count), (float)(sgx / count) * invstd * invstd,
-                                    mean_in[c]);
-  }
-  __syncthreads();
-  const float4 k0 = coef[4 * qi], k1 = coef[4 * qi + 1], k2 = coef[4 * qi + 2], k3 = coef[4 * qi + 3];
-#pragma unroll BN1N_U
-  for (unsigned row = rs; row < rows; row += BN1N_RS) {
-    const size_t o = (size_t)row * d.C + cq;
-    float4 gv = bn_g4(d, g, o);
-    if (relu) relu_mask4(d, y, o, gv);
-    if (dr) st4(dr + o, gv);
-    if (dx) {
-      const float4 xv = ld4(x + o);
-      float4 o4;
-      o4.x = k0.x * (gv.x - k0.y - (xv.x - k0.w) * k0.z);
-      o4.y = k1.x * (gv.y - k1.y - (xv.y - k1.w) * k1.z);
-      o4.z = k2.x * (gv.z - k2.y - (xv.z - k2.w) * k2.z);
-      o4.w = k3.x * (gv.w - k3.y - (xv.w - k3.w) * k3.z);
-      st4(dx + o, o4);
-    }
-  }
-}
-
 }  // namespace vfd
 
 using namespace vfd;
@@ -1166,8 +988,8 @@ int vfd_bn_bwd_apply(const vfd_bn_desc* d, const void* g, const void* y, const v
 int vfd_bn1_fits(const vfd_bn_desc* d) {
   if (!d || d->N <= 0 || d->C <= 0 || d->HW <= 0 || (long long)d->N * d->HW > (long long)BN1_MAX) return 0;
   if (d->groups < 0 || d->groups > 64) return 0;
-  // groups: the NCHW one-launch kernels loop over them; the opt-in NHWC ones take one group
-  return !d->nhwc || (VFD_BN1_NHWC && d->C % BN1N_CG == 0 && d->groups <= 1) ? 1 : 0;
+  // groups: the NCHW one-launch kernels loop over them; channels-last maps take the split path
+  return d->nhwc ? 0 : 1;
 }
 
 int vfd_bn1_fwd(const vfd_bn_desc* d, const void* x, const void* residual, const float* gamma, const float* beta,
@@ -1177,17 +999,6 @@ int vfd_bn1_fwd(const vfd_bn_desc* d, const void* x, const void* residual, const
   VFD_REQUIRE(x && gamma && beta && y && mean && invstd && !running_mean == !running_var, "bn1_fwd: bad argument");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_BN_FWD, s);
-  if (d->nhwc) {
-    if (d->dtype == 1)
-      bn1n_fwd_k<__bf16><<<d->C / BN1N_CG, BN1_THREADS, 0, s>>>(*d, (const __bf16*)x, (const __bf16*)residual, gamma,
-                                                                beta, (__bf16*)y, mean, invstd, running_mean, running_var,
-                                                                num_batches_tracked, d->relu ? relu_mask : nullptr);
-    else
-      bn1n_fwd_k<float><<<d->C / BN1N_CG, BN1_THREADS, 0, s>>>(*d, (const float*)x, (const float*)residual, gamma, beta,
-                                                               (float*)y, mean, invstd, running_mean, running_var,
-                                                               num_batches_tracked, d->relu ? relu_mask : nullptr);
-    return fail_launch("bn1_fwd");
-  }
   if (d->dtype == 1)
     bn1_fwd_k<__bf16><<<d->C, BN1_THREADS, 0, s>>>(*d, (const __bf16*)x, (const __bf16*)residual, gamma, beta,
                                                    (__bf16*)y, mean, invstd, running_mean, running_var,
@@ -1206,17 +1017,6 @@ int vfd_bn1_bwd(const vfd_bn_desc* d, const void* g, const void* y, const void* 
   VFD_REQUIRE(g && x && gamma && mean && invstd && (y || !d->relu), "bn1_bwd: bad argument");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(K_BN_BWD, s);
-  if (d->nhwc) {
-    if (d->dtype == 1)
-      bn1n_bwd_k<__bf16><<<d->C / BN1N_CG, BN1_THREADS, 0, s>>>(*d, (const __bf16*)g, (const __bf16*)y,
-                                                                (const __bf16*)x, gamma, mean, invstd, (__bf16*)dx,
-                                                                (__bf16*)dresidual, dgamma, dbeta);
-    else
-      bn1n_bwd_k<float><<<d->C / BN1N_CG, BN1_THREADS, 0, s>>>(*d, (const float*)g, (const float*)y, (const float*)x,
-                                                               gamma, mean, invstd, (float*)dx, (float*)dresidual,
-                                                               dgamma, dbeta);
-    return fail_launch("bn1_bwd");
-  }
   if (d->dtype == 1)
     bn1_bwd_k<__bf16><<<d->C, BN1_THREADS, 0, s>>>(*d, (const __bf16*)g, (const __bf16*)y, (const __bf16*)x, gamma,
                                                    mean, invstd, (__bf16*)dx, (__bf16*)dresidual, dgamma, dbeta);

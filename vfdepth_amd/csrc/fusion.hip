@@ -669,9 +669,6 @@ __global__ __launch_bounds__(256) void fusion_plan_k(vfd_voxel_desc d, const flo
 // output element is written exactly once: no memset, no atomics.
 constexpr int POSE_TV = 32;
 constexpr int POSE_MAXC = 256;      // channels held per lane: ceil(C / 64) <= 4
-#ifndef VFD_POSE_QUAD
-#define VFD_POSE_QUAD 1             // lanes = channel quads (C % 4 == 0): 166 vs 188 us (config 3), 91 vs 101 (2)
-#endif
 #ifndef VFD_POSE_VU
 #define VFD_POSE_VU 2                 // voxels per wave round: 166 vs 170 (1) / 202 (4) us at config 3
 #endif
@@ -748,8 +745,7 @@ __global__ __launch_bounds__(256) void fuse_pose_fwd_k(vfd_voxel_desc d, const f
   const int Yo = d.Y + P, Xo = d.X + P;
   const size_t pix_stride = (size_t)d.Z * C1;
   TO* ob = out + (size_t)b * Yo * Xo * pix_stride;
-#if VFD_POSE_QUAD
-  if ((C & 3) == 0) {
+  if ((C & 3) == 0) {     // lanes = channel quads: 166 vs 188 us (config 3), 91 vs 101 (config 2)
     // lanes = channel quads: one 16-B load per lane brings a whole tap row (C <= 256), the wave
     // works on POSE_VU voxels at a time (wave-uniform: their camera loops are uniform branches) and
     // issues all their tap rows of one camera round before summing any.  The per-channel arithmetic
@@ -825,7 +821,7 @@ __global__ __launch_bounds__(256) void fuse_pose_fwd_k(vfd_voxel_desc d, const f
     }
     return;
   }
-#endif
+  // C % 4 != 0: lanes = channels
   for (int t0 = wv * 2; t0 < POSE_TV; t0 += 8) {
     float acc[2][CPL];
 #pragma unroll

@@ -32,9 +32,6 @@ constexpr int PP_FRAG = PP_PIX * PP_O;          // floats of one tile's partial
 constexpr int PP_LDS_MAX = 160 * 1024;
 constexpr int PP_MAXC = 96;                     // contributors of one tile
 constexpr int PP_FSL = 32;                      // fragment slices per tile in the reduce
-#ifndef VFD_RING_EARLY
-#define VFD_RING_EARLY 0                        // B-fragment ring: refill before (1) or after (0) the MFMAs
-#endif
 #ifndef VFD_PP_ALIGN
 #define VFD_PP_ALIGN 1                          // tile-aligned stream-K splits + XCD numbering (pp_plan)
 #endif
@@ -400,18 +397,6 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppcb_main_k(PpGeom g, const TX*
       bf16x8 af[4];
 #pragma unroll
       for (int a = 0; a < 4; ++a) af[a] = *reinterpret_cast<const bf16x8*>(&xt[aoff[a] + 16 * q]);
-#if VFD_RING_EARLY                                     // A/B: copy the slot out, refill, then the MFMAs
-      bf16x8 bc[2] = {bq[ring][0], bq[ring][1]};
-      if (st + PF < STEPS)
-        wld(wc, st + PF, bq[ring]);
-      else if (more)
-        wld(wn, st + PF - STEPS, bq[ring]);
-#pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        acc[a][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bc[0], acc[a][0], 0, 0, 0);
-        acc[a][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bc[1], acc[a][1], 0, 0, 0);
-      }
-#else
 #pragma unroll
       for (int a = 0; a < 4; ++a) {
         acc[a][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bq[ring][0], acc[a][0], 0, 0, 0);
@@ -422,7 +407,6 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppcb_main_k(PpGeom g, const TX*
         wld(wc, st + PF, bq[ring]);
       else if (more)
         wld(wn, st + PF - STEPS, bq[ring]);
-#endif
       // keep the scheduler from hoisting later steps' LDS reads above these MFMAs (register
       // pressure: the prefetch ring, not the A fragments, is what should hold VGPRs)
       __builtin_amdgcn_sched_barrier(0);
@@ -849,20 +833,7 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppd_main_k(PdcGeom g, const TG*
 #pragma unroll
           for (int a = 0; a < MB; ++a) afn[a] = *reinterpret_cast<const Frag*>(&xb[o1c[a]]);
         }
-#if VFD_RING_EARLY
-        Frag bc[NB];
-#pragma unroll
-        for (int b = 0; b < NB; ++b) {
-          bc[b] = bq[q % PF][b];
-          if (q + PF < STEPS)
-            bq[q % PF][b] = btap[(q + PF) * qstride + 64 * b];
-          else if (bn)
-            bq[q % PF][b] = bn[(q + PF - STEPS) * qstride + 64 * b];
-        }
-#define VFD_PD_B(b) bc[b]
-#else
 #define VFD_PD_B(b) bq[q % PF][b]
-#endif
         if constexpr (BF) {
 #pragma unroll
           for (int a = 0; a < MB; ++a)
@@ -881,7 +852,6 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppd_main_k(PdcGeom g, const TG*
         }
 #undef VFD_PD_B
         // refill the slots just read (no copy-out of the ring: see ppcb_main_k)
-#if !VFD_RING_EARLY
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
           if (q + PF < STEPS)
@@ -889,7 +859,6 @@ __global__ __launch_bounds__(PP_THREADS, 2) void ppd_main_k(PdcGeom g, const TG*
           else if (bn)
             bq[q % PF][b] = bn[(q + PF - STEPS) * qstride + 64 * b];
         }
-#endif
 #pragma unroll
         for (int a = 0; a < MB; ++a) afc[a] = afn[a];
       }

@@ -91,14 +91,12 @@ class VoxelSpace:
         self._pose_order = None
 
     def pose_order(self):
-        """K2's voxel order by azimuth sector (fusion.hip fuse_pose_fwd_k): [8, cap] int32 voxel
-        indices, sector k = the voxel columns whose centre azimuth atan2(y, x) falls in
+        """K2's voxel order by azimuth sector (fusion.hip fuse_pose_fwd_k's `order`): [8, cap] int32
+        voxel indices, sector k = the voxel columns whose centre azimuth atan2(y, x) falls in
         [-pi + k pi/4, -pi + (k+1) pi/4), index order inside a sector, -1 padding to a common cap
-        (a multiple of 32).  Opt-in (VFD_POSE_SECTORS=1): measured 193 vs 186 us per call at config 3,
-        102 vs 100 at config 2 — the gather is not bound by the cross-XCD feature re-reads.  None
-        when off."""
-        if os.environ.get('VFD_POSE_SECTORS', '0') != '1':
-            return None
+        (a multiple of 32).  Not used by the step (measured 193 vs 186 us per call at config 3,
+        102 vs 100 at config 2: the gather is not bound by the cross-XCD feature re-reads); kept for
+        the C ABI's `order` argument, which test_pose_conv_bf16_map_matches_two_nodes covers."""
         if self._pose_order is None:
             v = torch.arange(self.V)
             ax, ay = (a.cpu().double() for a in self.axes[:2])
@@ -206,23 +204,6 @@ class FuseDepth(torch.autograd.Function):
         return None, dP, None, None, None, dwzb[:3], dwzb[3], dwzb[4], None
 
 
-def _side_stream(device):
-    """Stream for the geometry-only plans (K2 fusion plan, K3 backward plan).  Default: the current
-    stream (in order).  VFD_SIDE_PLANS=1 puts them on a side stream that overlaps the dense layers;
-    measured on MI355X at config 2 that is SLOWER (44.2-44.4 vs 41.9-42.1 ms/step: the plan
-    kernels co-running with MIOpen's implicit-GEMM convs cost those more than the plans take)."""
-    if os.environ.get('VFD_SIDE_PLANS', '0') != '1':
-        return torch.cuda.current_stream(device)
-    key = torch.device(device).index
-    st = _SIDE_STREAMS.get(key)
-    if st is None:
-        st = _SIDE_STREAMS[key] = torch.cuda.Stream(device=device)
-    return st
-
-
-_SIDE_STREAMS = {}
-
-
 def _wait_stream(dst, src):
     """dst waits for the work queued on src so far — skipped when they are one stream.  A stream
     waiting on its own event is a no-op on the device, but under HIP-graph capture this HIP runtime
@@ -240,8 +221,8 @@ class FusionPlan:
     Built once per step from K (fusion scale), E^-1 and the 1/8 mask; every pose-mode fusion call
     of the step reuses it (the geometry does not depend on features).  Only the backward reads the
     buffers, so they are built on demand (`build()`: by the first forward that needs a gradient;
-    a no-grad evaluation step never allocates them), on `_side_stream`'s stream; `wait()` joins
-    that stream."""
+    a no-grad evaluation step never allocates them), on the current stream; `wait()` joins that
+    stream from another (the depth branch's K1 backward reads the plan the pose branch built)."""
 
     def __init__(self, space, mask_lo, K, Einv, build=True):
         mask_lo, K, Einv = (_dev(t, n) for t, n in ((mask_lo, 'mask'), (K, 'K'), (Einv, 'Einv')))
@@ -259,17 +240,14 @@ class FusionPlan:
         mask_lo, K, Einv = self.mask_lo, self.K, self.Einv
         d = self.space.desc(self.B, self.N)
         nbytes = lib.vfd_fusion_plan_bytes(ctypes.byref(d))
-        main, self.side = torch.cuda.current_stream(mask_lo.device), _side_stream(mask_lo.device)
-        _wait_stream(self.side, main)
-        with torch.cuda.stream(self.side):
-            self.buf = torch.empty(nbytes, dtype=torch.uint8, device=mask_lo.device)
-            self.counts = torch.empty(self.B * self.N, dtype=torch.int32, device=mask_lo.device)
-            L.check(lib.vfd_fusion_plan(ctypes.byref(d), mask_lo.data_ptr(), K.data_ptr(), Einv.data_ptr(),
-                                        self.buf.data_ptr(), self.counts.data_ptr(), L.stream()), 'fusion_plan')
-        for t in (self.buf, self.counts):
-            t.record_stream(main)
-        for t in (mask_lo, K, Einv):
-            t.record_stream(self.side)
+        # built on the current stream (round 2: a side stream overlapping the dense layers measured
+        # slower at config 2, 44.2-44.4 vs 41.9-42.1 ms/step — the plan kernels co-running with
+        # MIOpen's implicit-GEMM convs cost those more than the plans take)
+        self.side = torch.cuda.current_stream(mask_lo.device)
+        self.buf = torch.empty(nbytes, dtype=torch.uint8, device=mask_lo.device)
+        self.counts = torch.empty(self.B * self.N, dtype=torch.int32, device=mask_lo.device)
+        L.check(lib.vfd_fusion_plan(ctypes.byref(d), mask_lo.data_ptr(), K.data_ptr(), Einv.data_ptr(),
+                                    self.buf.data_ptr(), self.counts.data_ptr(), L.stream()), 'fusion_plan')
         # the point right after the plan kernels: a consumer on another stream waits for this, not
         # for everything queued on the building stream later (the pose branch's stream builds the
         # plan in its forward; the depth branch's K1 backward reads it while the pose backward runs)
@@ -348,8 +326,8 @@ class VoxelProject(torch.autograd.Function):
     of reduce_dim's first conv: logical [B*N, D*Cv, h+2, w+2], channel d*Cv + c.
 
     When the voxels need a gradient, the forward also builds the backward's geometry-only plan
-    (`vfd_voxel_project_plan`: the frustum samples sorted by voxel cell; see `_side_stream` for
-    where it runs); the backward joins that stream and runs only the d_out-dependent part
+    (`vfd_voxel_project_plan`: the frustum samples sorted by voxel cell, on the forward's stream);
+    the backward joins that stream and runs only the d_out-dependent part
     (`vfd_voxel_project_bwd_planned`)."""
 
     @staticmethod
@@ -368,16 +346,10 @@ class VoxelProject(torch.autograd.Function):
         ctx.plan = ctx.side = None
         if ctx.needs_input_grad[1]:
             nbytes = lib.vfd_voxel_project_plan_bytes(ctypes.byref(d))
-            main, side = torch.cuda.current_stream(vox.device), _side_stream(vox.device)
-            _wait_stream(side, main)                # invK / E are ready
-            with torch.cuda.stream(side):
-                plan = torch.empty(nbytes, dtype=torch.uint8, device=vox.device)
-                L.check(lib.vfd_voxel_project_plan(ctypes.byref(d), invK.data_ptr(), E.data_ptr(), plan.data_ptr(),
-                                                   nbytes, L.stream()), 'voxel_project_plan')
-            plan.record_stream(main)                # consumed on the main stream by the backward
-            invK.record_stream(side)
-            E.record_stream(side)
-            ctx.plan, ctx.side = plan, side
+            plan = torch.empty(nbytes, dtype=torch.uint8, device=vox.device)
+            L.check(lib.vfd_voxel_project_plan(ctypes.byref(d), invK.data_ptr(), E.data_ptr(), plan.data_ptr(),
+                                               nbytes, L.stream()), 'voxel_project_plan')
+            ctx.plan, ctx.side = plan, torch.cuda.current_stream(vox.device)
         return out
 
     @staticmethod
@@ -395,9 +367,6 @@ class VoxelProject(torch.autograd.Function):
         return None, dvox, None, None
 
 
-# reduce_dim[0]'s data gradient in K3C's backward: 'nhwc' (one MIOpen call on the channels-last
-# tensors) or 'nchw' (the data gradient on NCHW copies of the small tensors; tools/micro_convbwd.py)
-_DGRAD_LAYOUT = os.environ.get('VFD_DGRAD_LAYOUT', 'nhwc')
 
 
 def _weight_fragments(mode, w, shape, C1=0, Z=0, Cv=0, D=0):
@@ -761,10 +730,11 @@ def _pose_pairs(plan, B):
     return B // plan.B
 
 
-def _pose_fuse_t(space, plan, feats, dtype):
+def _pose_fuse_t(space, plan, feats, dtype, order=None):
     """K2 forward into a fresh map of `dtype` (fusion.hip fuse_pose_fwd_k) -> (map, desc shape).
     feats may stack P frame pairs over the plan's geometry batch ([P * plan.B, N, C, h, w], the
-    pose net's pairs in one batch): K2 runs once per pair on its slice with the plan's geometry."""
+    pose net's pairs in one batch): K2 runs once per pair on its slice with the plan's geometry.
+    `order`: an optional voxel order (VoxelSpace.pose_order), index order when None."""
     lib = L.load()
     feats = _dev(feats, 'feats')
     B, N, C = feats.shape[:3]
@@ -777,7 +747,6 @@ def _pose_fuse_t(space, plan, feats, dtype):
     out = torch.empty(B, (C + 1) * space.Z, space.Y + 2, space.X + 2, device=feats.device, dtype=dtype,
                       memory_format=torch.channels_last)
     d = space.desc(Bg, N, C=C)
-    order = space.pose_order()
     fstep, ostep = Bg * N * hw * C * 4, Bg * out[0].numel() * out.element_size()     # bytes per pair
     for p in range(P):
         L.check(lib.vfd_fuse_pose_fwd_t(ctypes.byref(d), plan.mask_lo.data_ptr(), plan.K.data_ptr(),
@@ -977,14 +946,6 @@ class ProjConv(torch.autograd.Function):
         if dx is not None:
             if any(wmask):
                 # the weight gradient reads only the weight's shape: w0 has it (no permuted copy)
-                _, dw, db = cb(g_pre, x, w0, *args, [False] + wmask)
-        elif _DGRAD_LAYOUT == 'nchw' and mask[0]:
-            # MIOpen's NCHW data-gradient solver (the NHWC one is ~1.5x slower at this shape);
-            # the input tensor only supplies shape / memory format to the data gradient
-            w_perm = proj_conv_weight(w0, Cv, space.D)
-            shape_only = torch.empty(x.shape, device=x.device)
-            dx = cb(g_pre.contiguous(), shape_only, w_perm.contiguous(), *args, [True, False, False])[0]
-            if any(wmask):
                 _, dw, db = cb(g_pre, x, w0, *args, [False] + wmask)
         elif mask[0] or any(wmask):
             dx, dw, db = cb(g_pre, x, proj_conv_weight(w0, Cv, space.D), *args, [mask[0]] + wmask)

@@ -572,18 +572,38 @@ class _FusionDecisions:
     oracle's layouts while the step's forward runs: the fused aggregation conv (conv1x1) of each
     net, K1's folded 1x1 convs (conv_non_overlap / conv_overlap), K3C (the depth reduce_dim[0])
     and K2C (the pose reduce_dim[0]).  The pose masks are in call order, pairs stacked pair-major
-    (the batched-pairs layout; one call per pair gives the same order)."""
+    (the batched-pairs layout; one call per pair gives the same order).  Also reduce_dim's second
+    activation (both nets) and the pose decoder's ReLUs."""
 
     def __init__(self, algo):
         inner = {k: getattr(m, 'module', m) for k, m in algo.models.items()}
         self.conv = {'depth': inner['depth_net'].conv1x1, 'pose': inner['pose_net'].conv1x1}
-        self.agg, self.vox, self.y0 = {}, None, {}
+        self.relu = inner['pose_net'].pose_decoder.relu
+        self.agg, self.vox, self.y0, self.y1, self.dec = {}, None, {}, {}, []
 
     def __enter__(self):
         from vfdepth_amd import kernels as KN
         from vfdepth_amd import network as NW
-        self._orig = (NW._aggregate, KN.FuseDepth.apply, KN.ProjConv.apply, KN.PadConv.apply)
-        agg_fn, fuse_fn, proj_fn, pad_fn = self._orig
+        from vfdepth_amd.fusion import VFNet
+        self._orig = (NW._aggregate, KN.FuseDepth.apply, KN.ProjConv.apply, KN.PadConv.apply,
+                      VFNet.project_voxel_into_image, VFNet._reduce)
+        agg_fn, fuse_fn, proj_fn, pad_fn, pvi_fn, red_fn = self._orig
+        # reduce_dim's second activation: the depth net's projected features, the pose net's BEV
+        # (the returned maps are the LeakyReLU outputs: their signs are the decisions)
+
+        def project_voxel_into_image(net, *a):
+            out = pvi_fn(net, *a)
+            self.y1.setdefault('depth', []).append((out.detach() > 0).cpu())
+            return out
+
+        def reduce(net, *a):
+            out = red_fn(net, *a)
+            if net.model == 'pose':
+                self.y1.setdefault('pose', []).append((out.detach() > 0).cpu())
+            return out
+        VFNet.project_voxel_into_image, VFNet._reduce = project_voxel_into_image, reduce
+        # the pose decoder's ReLU (one module, three calls per forward)
+        self._hook = self.relu.register_forward_hook(lambda m, i, o: self.dec.append((o.detach() > 0).cpu()))
 
         def aggregate(encoder, conv1x1, *a, **kw):
             feats, agg = agg_fn(encoder, conv1x1, *a, **kw)
@@ -615,33 +635,41 @@ class _FusionDecisions:
     def __exit__(self, *exc):
         from vfdepth_amd import kernels as KN
         from vfdepth_amd import network as NW
-        NW._aggregate, KN.FuseDepth.apply, KN.ProjConv.apply, KN.PadConv.apply = self._orig
+        from vfdepth_amd.fusion import VFNet
+        (NW._aggregate, KN.FuseDepth.apply, KN.ProjConv.apply, KN.PadConv.apply,
+         VFNet.project_voxel_into_image, VFNet._reduce) = self._orig
+        self._hook.remove()
         self.agg = {k: torch.cat(v, 0) for k, v in self.agg.items()}
         self.y0 = {k: torch.cat(v, 0) for k, v in self.y0.items()}
+        self.y1 = {k: torch.cat(v, 0) for k, v in self.y1.items()}
+        # the decoder's calls in order, three per forward: regroup as [squeeze, pose 0, pose 1]
+        # masks over all of the forwards' batches (pair-major)
+        self.dec = [torch.cat(self.dec[j::3], 0) for j in range(3)] if self.dec else []
 
 
 class _MaskedLReLU(torch.nn.Module):
-    """LeakyReLU(0.1) whose slope choice follows given masks (one per call, in call order): the
-    value differs from LeakyReLU only where a mask disagrees with the sign, i.e. within fp32
-    rounding of zero; the gradient takes the recorded decisions."""
+    """LeakyReLU(slope) — ReLU for slope 0 — whose slope choice follows given masks (one per call,
+    in call order): the value differs from the activation only where a mask disagrees with the
+    sign, i.e. within fp32 rounding of zero; the gradient takes the recorded decisions."""
 
-    def __init__(self, masks):
+    def __init__(self, masks, slope=0.1):
         super().__init__()
-        self.masks, self.calls = masks, 0
+        self.masks, self.calls, self.slope = masks, 0, slope
 
     def forward(self, x):
         m = self.masks[self.calls]
         self.calls += 1
         assert m.shape == x.shape, (m.shape, x.shape)
-        return torch.where(m, x, x * 0.1)
+        return torch.where(m, x, x * self.slope)
 
 
 class _HoldFusionDecisions:
     """Runs the oracle step with the fusion-path LeakyReLU decisions of the GPU step
     (_FusionDecisions): each net's conv1x1 activation (the depth net's called once on B*N images,
     the pose net's once per frame pair), the oracle's K1 1x1-conv activation
-    (vfd_oracle._conv1x1_lrelu), reduce_dim[0]'s activation (depth: once per camera; pose: once per
-    frame pair)."""
+    (vfd_oracle._conv1x1_lrelu), reduce_dim's two activations (depth: once per camera; pose: once
+    per frame pair) and the pose decoder's ReLU (three calls per frame pair; its maps are small, so
+    one flipped ReLU there visibly moves its weight gradients)."""
 
     def __init__(self, O, dn, pn, dec, B, N):
         self.O, self.dn, self.pn, self.dec, self.B, self.N = O, dn, pn, dec, B, N
@@ -649,7 +677,17 @@ class _HoldFusionDecisions:
     def __enter__(self):
         O, dn, pn, dec, B, N = self.O, self.dn, self.pn, self.dec, self.B, self.N
         self._orig = (dn.conv1x1[2], dn.fusion_net.reduce_dim[2], pn.conv1x1[2], pn.fusion_net.reduce_dim[2],
+                      dn.fusion_net.reduce_dim[5], pn.fusion_net.reduce_dim[5], pn.pose_decoder.relu,
                       O._conv1x1_lrelu)
+        if 'depth' in dec.y1:
+            y1 = dec.y1['depth'].view(B, N, *dec.y1['depth'].shape[1:])
+            dn.fusion_net.reduce_dim[5] = _MaskedLReLU([y1[:, c] for c in range(N)])
+        if 'pose' in dec.y1:
+            pn.fusion_net.reduce_dim[5] = _MaskedLReLU(list(dec.y1['pose'].split(B)))
+        if dec.dec:                              # per pair: squeeze, pose 0, pose 1
+            P = dec.dec[0].shape[0] // B
+            pn.pose_decoder.relu = _MaskedLReLU([dec.dec[j][p * B:(p + 1) * B] for p in range(P) for j in range(3)],
+                                                slope=0.0)
         dn.conv1x1[2] = _MaskedLReLU([dec.agg['depth']])
         pn.conv1x1[2] = _MaskedLReLU(list(dec.agg['pose'].split(B * N)))
         if 'depth' in dec.y0:                    # K3C ran (fp32, 64 voxel channels, D <= 64)
@@ -666,6 +704,7 @@ class _HoldFusionDecisions:
 
     def __exit__(self, *exc):
         (self.dn.conv1x1[2], self.dn.fusion_net.reduce_dim[2], self.pn.conv1x1[2], self.pn.fusion_net.reduce_dim[2],
+         self.dn.fusion_net.reduce_dim[5], self.pn.fusion_net.reduce_dim[5], self.pn.pose_decoder.relu,
          self.O._conv1x1_lrelu) = self._orig
 
 

@@ -491,7 +491,13 @@ class VFDepthAlgo:
         _trace(f'capture begins on stream {cap.cuda_stream:#x}, branch stream '
                f'{getattr(getattr(self, "_bstream", None), "cuda_stream", 0):#x}, default stream '
                f'{torch.cuda.default_stream(self.device).cuda_stream:#x}')
-        with torch.cuda.graph(graph, stream=cap):
+        # under a process group, its watchdog thread polls the events of finished collectives while
+        # the capture runs; in the default 'global' mode any thread's event query during a capture
+        # fails (hipErrorStreamCaptureUnsupported, and the watchdog aborts the process: round 6,
+        # intermittent), so the capture checks only this thread's calls ('thread_local').  The step
+        # itself is capture-clean in 'global' mode (every single-process capture runs that way).
+        mode = 'thread_local' if dist.is_available() and dist.is_initialized() else 'global'
+        with torch.cuda.graph(graph, stream=cap, capture_error_mode=mode):
             with check:
                 try:
                     static_outputs, static_losses = self.process_batch(dict(static), self.rank)

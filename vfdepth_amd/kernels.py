@@ -723,10 +723,14 @@ class PadConvBF16(torch.autograd.Function):
 _DT = {torch.float32: 0, torch.bfloat16: 1}
 
 
-def _pose_pairs(plan, B):
-    """Frame pairs stacked in a pose batch of B elements over a plan (geometry) of plan.B elements."""
+def _pose_pairs(plan, B, N=None):
+    """Frame pairs stacked in a pose batch of B elements over a plan (geometry) of plan.B elements.
+    The per-pair slices below are raw pointer offsets into one buffer: the counts are checked here,
+    before any launch (the kernels index [plan.B, N] geometry and a pair's slice only)."""
     if B % plan.B:
         raise RuntimeError(f'pose fusion: batch {B} is not a multiple of the geometry batch {plan.B}')
+    if N is not None and N != plan.N:
+        raise RuntimeError(f'pose fusion: {N} cameras against a plan of {plan.N}')
     return B // plan.B
 
 
@@ -738,8 +742,10 @@ def _pose_fuse_t(space, plan, feats, dtype, order=None):
     lib = L.load()
     feats = _dev(feats, 'feats')
     B, N, C = feats.shape[:3]
-    P, Bg = _pose_pairs(plan, B), plan.B
+    P, Bg = _pose_pairs(plan, B, N), plan.B
     hw = feats.shape[3] * feats.shape[4]
+    if hw != space.h * space.w:
+        raise RuntimeError(f'pose fusion: feature map {tuple(feats.shape[3:])} is not {space.h}x{space.w}')
     feats_cl = torch.empty(B, N, hw, C, device=feats.device)          # [B, N, h*w, C]: one tiled pass
     L.check(lib.vfd_nchw_to_nhwc(feats.data_ptr(), feats_cl.data_ptr(), B * N, C, hw, 0, L.stream()), 'nchw_to_nhwc')
     if L.PROF_ON:                            # timed under its own layout_copy scope (vfd_nchw_to_nhwc)
@@ -762,7 +768,11 @@ def _pose_unfuse(space, plan, shape, g):
     once per stacked frame pair, as the forward."""
     lib = L.load()
     B, N, C = shape[:3]
-    P, Bg = _pose_pairs(plan, B), plan.B
+    P, Bg = _pose_pairs(plan, B, N), plan.B
+    want = (B, (C + 1) * space.Z, space.Y + 2, space.X + 2)
+    if tuple(g.shape) != want or tuple(shape[3:]) != (space.h, space.w):
+        raise RuntimeError(f'pose fusion backward: map gradient {tuple(g.shape)} / features {tuple(shape)} '
+                           f'do not match the map {want}')
     g = _nhwc(g, 'grad') if g.dtype in _DT else _channels_last(g, 'grad')
     dfeats = torch.empty(shape, device=g.device)
     d = space.desc(Bg, N, C=C)

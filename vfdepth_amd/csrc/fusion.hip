@@ -1493,7 +1493,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void fu
 
 // Split tiles: the S part slots summed in part order.  A workgroup takes split tiles in turn;
 // thread = (tile row, channel): all PT rows at once (one round of S x PT slot loads per thread,
-// the rows in flight together instead of one after another: 19 -> ~8 us per call at config 2),
+// the rows in flight together instead of one after another: 19.3 -> 17.9 us per call at config 2
+// under rocprofv3 — the row order was not what held it; it reads S partial tiles of 16 KB per split tile),
 // each channel's 4 pixels of a row written as one 16-B store.
 constexpr int PCB_THREADS = PT * POSE_MAXC;
 __global__ __launch_bounds__(PCB_THREADS) void pose_combine_k(vfd_voxel_desc d, const int4* __restrict__ combos,

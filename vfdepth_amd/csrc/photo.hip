@@ -77,7 +77,7 @@ __global__ __launch_bounds__(256) void photo_fwd_k(vfd_photo_desc d, const float
                                                    float* __restrict__ spatio_mask, uint8_t* __restrict__ sel,
                                                    double* __restrict__ partial) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  __shared__ double lds_red[4];
+  __shared__ double lds_red[6][4];
   constexpr int PT = TS + 2, PA = PT * PT;
   const int T = d.T, F = d.F;
   const int n_img = 2 * T + F;
@@ -179,12 +179,16 @@ __global__ __launch_bounds__(256) void photo_fwd_k(vfd_photo_desc d, const float
   const int nblk = gridDim.x * gridDim.y;
   const int blk = bi.y * gridDim.x + bi.x;
   double* out = partial + ((size_t)bn * nblk + blk) * 6;
+  // the six block sums in one round (same wave sums, same wave order as one round per sum)
+#pragma unroll
   for (int i = 0; i < 6; ++i) {
-    double v = wave_sum(acc[i]);
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) lds_red[threadIdx.x >> 6] = v;
-    __syncthreads();
-    if (threadIdx.x == 0) out[i] = lds_red[0] + lds_red[1] + lds_red[2] + lds_red[3];
+    const double v = wave_sum(acc[i]);
+    if ((threadIdx.x & 63) == 0) lds_red[i][threadIdx.x >> 6] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    const double* r = lds_red[threadIdx.x];
+    out[threadIdx.x] = r[0] + r[1] + r[2] + r[3];
   }
 }
 

@@ -835,12 +835,16 @@ __global__ __launch_bounds__(256) void pcd_reduce_k(PdGeom g, const float* __res
 // 30 per camera, 180 in all against 193 padded ones), written into the interior of the padded
 // layout; K3's backward then reads every sample straight from it (its plan built with pad_out = 2:
 // no fold buffer, no fold launch).
+// A launch covers the atoms [a_begin, a_end).  When at most half of the last n-tile is real
+// frustum channels (config 2: 3 200 = 12.5 x 256), that n-tile runs as a second launch of the
+// half-width form (half = 1: each wave 32 channels, one MFMA n-block, instead of 64), so the zero
+// padding costs no MFMAs; each launch splits its own atoms evenly over its groups.
 struct PfGeom {
-  int nbc, h, w, ntot, np, tpc, mtiles, ntile, natom, ngroup, hrows, cols, lds_floats;
+  int nbc, h, w, ntot, np, tpc, mtiles, ntile, natom, ngroup, hrows, cols, lds_floats, a_begin, a_end, half;
 };
 
 __host__ __device__ inline int pf_lo(const PfGeom& g, int grp) {
-  return (int)(((long long)grp * g.natom) / g.ngroup);
+  return g.a_begin + (int)(((long long)grp * (g.a_end - g.a_begin)) / g.ngroup);
 }
 
 struct PfTile {
@@ -913,6 +917,7 @@ __device__ __forceinline__ void pf_stage(const PfGeom& g, float* __restrict__ ds
   }
 }
 
+template <bool HALF>
 __global__ __launch_bounds__(PC_THREADS, 2) void pcdf_main_k(PfGeom g, const float* __restrict__ gp,
                                                             const float* __restrict__ Wd,
                                                             float* __restrict__ dx,
@@ -959,14 +964,20 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pcdf_main_k(PfGeom g, const flo
     const int t = at / PD_CHUNKS, ch = at - t * PD_CHUNKS;
     // wave-uniform (the division runs on the vector unit): readfirstlane keeps the buffer loads'
     // soffset scalar (a VGPR soffset compiles to a waterfall loop per load)
+    // (half width: wave wv's channels wv * 32 + li instead of wv * 64 + li — the same lane offset
+    // moved by a wave-uniform -512 * wv bytes, folded into the scalar base)
     return (unsigned)__builtin_amdgcn_readfirstlane(
-        (int)((unsigned)(ch * (PD_OC / 4)) * npb + (unsigned)(t / g.mtiles) * (PD_N * 16u)));
+        (int)((unsigned)(ch * (PD_OC / 4)) * npb + (unsigned)(t / g.mtiles) * (PD_N * 16u)) - (HALF ? 512 * wv : 0));
   };
   auto wload = [&](unsigned soff, float2 (&b)[2]) {
     const auto v0 = __builtin_amdgcn_raw_buffer_load_b64(rs_w, voff, (int)soff, 0);
-    const auto v1 = __builtin_amdgcn_raw_buffer_load_b64(rs_w, voff + 512, (int)soff, 0);
     b[0] = make_float2(__uint_as_float(v0[0]), __uint_as_float(v0[1]));
-    b[1] = make_float2(__uint_as_float(v1[0]), __uint_as_float(v1[1]));
+    if (!HALF) {
+      const auto v1 = __builtin_amdgcn_raw_buffer_load_b64(rs_w, voff + 512, (int)soff, 0);
+      b[1] = make_float2(__uint_as_float(v1[0]), __uint_as_float(v1[1]));
+    } else {
+      b[1] = make_float2(0.f, 0.f);
+    }
   };
   float2 bq[PFD_RING][2];
   unsigned cbase = wbase(a_lo);
@@ -1036,13 +1047,14 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pcdf_main_k(PfGeom g, const flo
           for (int a = 0; a < 4; ++a) {
             const float v = s2 ? afc[a].y : afc[a].x;
             acc[a][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(v, s2 ? bq[q & 3][0].y : bq[q & 3][0].x, acc[a][0], 0, 0, 0);
-            acc[a][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(v, s2 ? bq[q & 3][1].y : bq[q & 3][1].x, acc[a][1], 0, 0, 0);
+            if (!HALF)
+              acc[a][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(v, s2 ? bq[q & 3][1].y : bq[q & 3][1].x, acc[a][1], 0, 0, 0);
           }
         wload(q < 4 ? tb + (unsigned)(q + 4) * npb : nb + (unsigned)(q - 4) * npb, bq[q & 3]);
-        // in this step: the next A fragments' LDS reads first, then the 16 MFMAs, then the refill
-        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);   // DS read
-        __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);  // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);   // VMEM read
+        // in this step: the next A fragments' LDS reads first, then the 16 (half: 8) MFMAs, then the refill
+        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);             // DS read
+        __builtin_amdgcn_sched_group_barrier(0x008, HALF ? 8 : 16, 0); // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x020, HALF ? 1 : 2, 0);  // VMEM read
 #pragma unroll
         for (int a = 0; a < 4; ++a) afc[a] = afn[a];
       }
@@ -1060,7 +1072,8 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pcdf_main_k(PfGeom g, const flo
         for (int a = 0; a < 4; ++a)
 #pragma unroll
           for (int b = 0; b < 2; ++b) {
-            const int n = tl.nt * PD_N + wv * 64 + b * 32 + li;
+            const int n = HALF ? (b ? g.ntot : tl.nt * PD_N + wv * 32 + li)       // half width: b = 1 none
+                               : tl.nt * PD_N + wv * 64 + b * 32 + li;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
               const int mo = 32 * a + (r & 3) + 8 * (r >> 2) + 4 * lh;
@@ -1113,7 +1126,8 @@ __global__ __launch_bounds__(256) void pcdf_reduce_k(PfGeom g, const float* __re
       const int f = fu + u;
       const int a = f >> 5, bb = (f >> 4) & 1, r = f & 15;
       const int m = tl.m0 + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-      const int n = tl.nt * PD_N + wv * 64 + bb * 32 + (lane & 31);
+      const int n = g.half ? (bb ? g.ntot : tl.nt * PD_N + wv * 32 + (lane & 31))
+                           : tl.nt * PD_N + wv * 64 + bb * 32 + (lane & 31);
       if (m < hw && n < g.ntot) {
         const int y = m / g.w, x = m - y * g.w;
         dx[(((size_t)tl.bc * (g.h + 2) + y + 1) * (g.w + 2) + x + 1) * g.ntot + n] = su[u];
@@ -1136,10 +1150,39 @@ static PfGeom pf_plan(const vfd_voxel_desc& d) {
   g.hrows = (d.w + PC_PIX - 2) / d.w + 3;             // G rows under 128 consecutive pixels + 2
   g.cols = d.w + 6;                                   // 2 + w + 2 columns, E1, E2
   g.lds_floats = (g.hrows + 1) * g.cols * PD_XS;      // + the fold row
+  g.a_begin = 0;
+  g.a_end = g.natom;
+  g.half = 0;
   const int res = pc_resident();
   const int most = g.natom / PD_CHUNKS;
   g.ngroup = most < res ? (most > 0 ? most : 1) : res;
   return g;
+}
+
+// the launches of the folded data gradient: [0] the full-width n-tiles (all of them when the last
+// one is more than half real channels), [1] the half-width last n-tile (n = 1 when there is none)
+static int pf_regions(const vfd_voxel_desc& d, PfGeom (&r)[2]) {
+  const PfGeom g = pf_plan(d);
+  const int nn = g.np / PD_N;
+  if (g.ntot - (nn - 1) * PD_N > PD_N / 2) {
+    r[0] = g;
+    return 1;
+  }
+  const int nfa = (nn - 1) * g.mtiles * PD_CHUNKS;    // n-tile outermost: the last n-tile's atoms last
+  const int res = pc_resident();
+  for (int k = 0; k < 2; ++k) {
+    r[k] = g;
+    r[k].half = k;
+    r[k].a_begin = k ? nfa : 0;
+    r[k].a_end = k ? g.natom : nfa;
+    const int most = (r[k].a_end - r[k].a_begin) / PD_CHUNKS;
+    r[k].ngroup = most < res ? (most > 0 ? most : 1) : res;
+  }
+  if (nfa == 0) {                                    // a single, half-width n-tile
+    r[0] = r[1];
+    return 1;
+  }
+  return 2;
 }
 
 static bool pf_supported(const vfd_voxel_desc& d) {
@@ -2492,7 +2535,13 @@ size_t vfd_proj_conv_dgrad_workspace(const vfd_voxel_desc* d) {
   if (!d) return 0;
   if (pcd_use_pcg(*d))
     return (size_t)pg_plan<float>(*d).ngroup * 2 * PG_FRAG * sizeof(float);
-  if (d->pad_out == 2) return pf_supported(*d) ? (size_t)pf_plan(*d).ngroup * 2 * PC_FRAG * sizeof(float) : 0;
+  if (d->pad_out == 2) {
+    if (!pf_supported(*d)) return 0;
+    PfGeom r[2];
+    const int nr = pf_regions(*d, r);
+    const int ng = nr == 2 && r[1].ngroup > r[0].ngroup ? r[1].ngroup : r[0].ngroup;
+    return (size_t)ng * 2 * PC_FRAG * sizeof(float);
+  }
   if (!pd_supported(*d)) return 0;
   return (size_t)pd_plan(*d).ngroup * 2 * PC_FRAG * sizeof(float);
 }
@@ -2515,10 +2564,19 @@ int vfd_proj_conv_dgrad(const vfd_voxel_desc* d, const float* g_pre, const float
     return fail_launch("proj_conv_dgrad");
   }
   if (d->pad_out == 2) {
-    const PfGeom g = pf_plan(*d);
-    lds_attr(reinterpret_cast<const void*>(pcdf_main_k), PD_LDS_MAX);
-    pcdf_main_k<<<g.ngroup, PC_THREADS, (size_t)2 * g.lds_floats * sizeof(float), s>>>(g, g_pre, Wd, dx, (float*)ws);
-    pcdf_reduce_k<<<dim3(g.ngroup, PC_FSL), 256, 0, s>>>(g, (const float*)ws, dx);
+    PfGeom r[2];
+    const int nr = pf_regions(*d, r);
+    lds_attr(reinterpret_cast<const void*>(pcdf_main_k<false>), PD_LDS_MAX);
+    lds_attr(reinterpret_cast<const void*>(pcdf_main_k<true>), PD_LDS_MAX);
+    for (int k = 0; k < nr; ++k) {      // in order on the stream: the workspace's partial slots are reused
+      const PfGeom& g = r[k];
+      const size_t lds = (size_t)2 * g.lds_floats * sizeof(float);
+      if (g.half)
+        pcdf_main_k<true><<<g.ngroup, PC_THREADS, lds, s>>>(g, g_pre, Wd, dx, (float*)ws);
+      else
+        pcdf_main_k<false><<<g.ngroup, PC_THREADS, lds, s>>>(g, g_pre, Wd, dx, (float*)ws);
+      pcdf_reduce_k<<<dim3(g.ngroup, PC_FSL), 256, 0, s>>>(g, (const float*)ws, dx);
+    }
     return fail_launch("proj_conv_dgrad");
   }
   const PdGeom g = pd_plan(*d);

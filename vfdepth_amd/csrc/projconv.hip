@@ -835,16 +835,19 @@ __global__ __launch_bounds__(256) void pcd_reduce_k(PdGeom g, const float* __res
 // 30 per camera, 180 in all against 193 padded ones), written into the interior of the padded
 // layout; K3's backward then reads every sample straight from it (its plan built with pad_out = 2:
 // no fold buffer, no fold launch).
-// A launch covers the atoms [a_begin, a_end).  When at most half of the last n-tile is real
-// frustum channels (config 2: 3 200 = 12.5 x 256), that n-tile runs as a second launch of the
-// half-width form (half = 1: each wave 32 channels, one MFMA n-block, instead of 64), so the zero
-// padding costs no MFMAs; each launch splits its own atoms evenly over its groups.
+// When at most half of the last n-tile is real frustum channels (config 2: 3 200 = 12.5 x 256),
+// that n-tile's atoms [nfa, natom) run in the half-width form (each wave 32 channels, one MFMA
+// n-block, instead of 64), so the zero padding costs no MFMAs.  Groups [0, gfull) split the
+// full-width atoms [0, nfa), groups [gfull, ngroup) the half-width ones, the two counts in
+// proportion to the two regions' MFMA work, so every group (one per CU) finishes together.
+// No half-width region: nfa = natom, gfull = ngroup.
 struct PfGeom {
-  int nbc, h, w, ntot, np, tpc, mtiles, ntile, natom, ngroup, hrows, cols, lds_floats, a_begin, a_end, half;
+  int nbc, h, w, ntot, np, tpc, mtiles, ntile, natom, ngroup, hrows, cols, lds_floats, nfa, gfull;
 };
 
 __host__ __device__ inline int pf_lo(const PfGeom& g, int grp) {
-  return g.a_begin + (int)(((long long)grp * (g.a_end - g.a_begin)) / g.ngroup);
+  if (grp <= g.gfull) return (int)(((long long)grp * g.nfa) / g.gfull);
+  return g.nfa + (int)(((long long)(grp - g.gfull) * (g.natom - g.nfa)) / (g.ngroup - g.gfull));
 }
 
 struct PfTile {
@@ -918,12 +921,9 @@ __device__ __forceinline__ void pf_stage(const PfGeom& g, float* __restrict__ ds
 }
 
 template <bool HALF>
-__global__ __launch_bounds__(PC_THREADS, 2) void pcdf_main_k(PfGeom g, const float* __restrict__ gp,
-                                                            const float* __restrict__ Wd,
-                                                            float* __restrict__ dx,
-                                                            float* __restrict__ partial) {
-  extern __shared__ float pd_lds[];
-  const int grp = (g.ngroup % 8 == 0) ? (blockIdx.x % 8) * (g.ngroup / 8) + blockIdx.x / 8 : blockIdx.x;
+__device__ __forceinline__ void pcdf_body(const PfGeom& g, int grp, const float* __restrict__ gp,
+                                          const float* __restrict__ Wd, float* __restrict__ dx,
+                                          float* __restrict__ partial, float* __restrict__ pd_lds) {
   const int a_lo = pf_lo(g, grp), a_hi = pf_lo(g, grp + 1);
   if (a_lo >= a_hi) return;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1105,6 +1105,18 @@ __global__ __launch_bounds__(PC_THREADS, 2) void pcdf_main_k(PfGeom g, const flo
   }
 }
 
+__global__ __launch_bounds__(PC_THREADS, 2) void pcdf_main_k(PfGeom g, const float* __restrict__ gp,
+                                                            const float* __restrict__ Wd,
+                                                            float* __restrict__ dx,
+                                                            float* __restrict__ partial) {
+  extern __shared__ float pd_lds[];
+  const int grp = (g.ngroup % 8 == 0) ? (blockIdx.x % 8) * (g.ngroup / 8) + blockIdx.x / 8 : blockIdx.x;
+  if (grp < g.gfull)                                  // workgroup-uniform: one width per group
+    pcdf_body<false>(g, grp, gp, Wd, dx, partial, pd_lds);
+  else
+    pcdf_body<true>(g, grp, gp, Wd, dx, partial, pd_lds);
+}
+
 __global__ __launch_bounds__(256) void pcdf_reduce_k(PfGeom g, const float* __restrict__ partial,
                                                      float* __restrict__ dx) {
   const int grp = blockIdx.x;
@@ -1126,8 +1138,8 @@ __global__ __launch_bounds__(256) void pcdf_reduce_k(PfGeom g, const float* __re
       const int f = fu + u;
       const int a = f >> 5, bb = (f >> 4) & 1, r = f & 15;
       const int m = tl.m0 + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-      const int n = g.half ? (bb ? g.ntot : tl.nt * PD_N + wv * 32 + (lane & 31))
-                           : tl.nt * PD_N + wv * 64 + bb * 32 + (lane & 31);
+      const int n = t >= g.nfa / PD_CHUNKS ? (bb ? g.ntot : tl.nt * PD_N + wv * 32 + (lane & 31))
+                                           : tl.nt * PD_N + wv * 64 + bb * 32 + (lane & 31);
       if (m < hw && n < g.ntot) {
         const int y = m / g.w, x = m - y * g.w;
         dx[(((size_t)tl.bc * (g.h + 2) + y + 1) * (g.w + 2) + x + 1) * g.ntot + n] = su[u];
@@ -1150,40 +1162,29 @@ static PfGeom pf_plan(const vfd_voxel_desc& d) {
   g.hrows = (d.w + PC_PIX - 2) / d.w + 3;             // G rows under 128 consecutive pixels + 2
   g.cols = d.w + 6;                                   // 2 + w + 2 columns, E1, E2
   g.lds_floats = (g.hrows + 1) * g.cols * PD_XS;      // + the fold row
-  g.a_begin = 0;
-  g.a_end = g.natom;
-  g.half = 0;
   const int res = pc_resident();
   const int most = g.natom / PD_CHUNKS;
   g.ngroup = most < res ? (most > 0 ? most : 1) : res;
+  g.nfa = g.natom;
+  g.gfull = g.ngroup;
+  const int nn = g.np / PD_N;
+  if (g.ntot - (nn - 1) * PD_N <= PD_N / 2 && nn > 1 && g.ngroup > 1) {
+    // the half-width n-tile: (nn - 1) full n-tiles against half a tile's work; each region's groups
+    // keep >= PD_CHUNKS atoms (a tile then meets at most two groups)
+    const int nfa = (nn - 1) * g.mtiles * PD_CHUNKS, nha = g.natom - nfa;
+    // a half-width atom costs at least half a full one (same staging and LDS reads, half the
+    // MFMAs): the share rounded up, plus one group, so the half-width groups are not the tail
+    int gh = (int)(((long long)g.ngroup * nha + 2LL * nfa + nha - 1) / (2LL * nfa + nha)) + 1;
+    gh = gh > nha / PD_CHUNKS ? nha / PD_CHUNKS : gh;
+    const int gf = g.ngroup - gh;
+    if (gh >= 1 && gf >= 1 && gf <= nfa / PD_CHUNKS) {
+      g.nfa = nfa;
+      g.gfull = gf;
+    }
+  }
   return g;
 }
 
-// the launches of the folded data gradient: [0] the full-width n-tiles (all of them when the last
-// one is more than half real channels), [1] the half-width last n-tile (n = 1 when there is none)
-static int pf_regions(const vfd_voxel_desc& d, PfGeom (&r)[2]) {
-  const PfGeom g = pf_plan(d);
-  const int nn = g.np / PD_N;
-  if (g.ntot - (nn - 1) * PD_N > PD_N / 2) {
-    r[0] = g;
-    return 1;
-  }
-  const int nfa = (nn - 1) * g.mtiles * PD_CHUNKS;    // n-tile outermost: the last n-tile's atoms last
-  const int res = pc_resident();
-  for (int k = 0; k < 2; ++k) {
-    r[k] = g;
-    r[k].half = k;
-    r[k].a_begin = k ? nfa : 0;
-    r[k].a_end = k ? g.natom : nfa;
-    const int most = (r[k].a_end - r[k].a_begin) / PD_CHUNKS;
-    r[k].ngroup = most < res ? (most > 0 ? most : 1) : res;
-  }
-  if (nfa == 0) {                                    // a single, half-width n-tile
-    r[0] = r[1];
-    return 1;
-  }
-  return 2;
-}
 
 static bool pf_supported(const vfd_voxel_desc& d) {
   if (d.Cv != PC_CV || d.B <= 0 || d.N <= 0 || d.h < 6 || d.w < 3 || d.D <= 0 || d.D > 64) return false;
@@ -2535,13 +2536,7 @@ size_t vfd_proj_conv_dgrad_workspace(const vfd_voxel_desc* d) {
   if (!d) return 0;
   if (pcd_use_pcg(*d))
     return (size_t)pg_plan<float>(*d).ngroup * 2 * PG_FRAG * sizeof(float);
-  if (d->pad_out == 2) {
-    if (!pf_supported(*d)) return 0;
-    PfGeom r[2];
-    const int nr = pf_regions(*d, r);
-    const int ng = nr == 2 && r[1].ngroup > r[0].ngroup ? r[1].ngroup : r[0].ngroup;
-    return (size_t)ng * 2 * PC_FRAG * sizeof(float);
-  }
+  if (d->pad_out == 2) return pf_supported(*d) ? (size_t)pf_plan(*d).ngroup * 2 * PC_FRAG * sizeof(float) : 0;
   if (!pd_supported(*d)) return 0;
   return (size_t)pd_plan(*d).ngroup * 2 * PC_FRAG * sizeof(float);
 }
@@ -2564,19 +2559,10 @@ int vfd_proj_conv_dgrad(const vfd_voxel_desc* d, const float* g_pre, const float
     return fail_launch("proj_conv_dgrad");
   }
   if (d->pad_out == 2) {
-    PfGeom r[2];
-    const int nr = pf_regions(*d, r);
-    lds_attr(reinterpret_cast<const void*>(pcdf_main_k<false>), PD_LDS_MAX);
-    lds_attr(reinterpret_cast<const void*>(pcdf_main_k<true>), PD_LDS_MAX);
-    for (int k = 0; k < nr; ++k) {      // in order on the stream: the workspace's partial slots are reused
-      const PfGeom& g = r[k];
-      const size_t lds = (size_t)2 * g.lds_floats * sizeof(float);
-      if (g.half)
-        pcdf_main_k<true><<<g.ngroup, PC_THREADS, lds, s>>>(g, g_pre, Wd, dx, (float*)ws);
-      else
-        pcdf_main_k<false><<<g.ngroup, PC_THREADS, lds, s>>>(g, g_pre, Wd, dx, (float*)ws);
-      pcdf_reduce_k<<<dim3(g.ngroup, PC_FSL), 256, 0, s>>>(g, (const float*)ws, dx);
-    }
+    const PfGeom g = pf_plan(*d);
+    lds_attr(reinterpret_cast<const void*>(pcdf_main_k), PD_LDS_MAX);
+    pcdf_main_k<<<g.ngroup, PC_THREADS, (size_t)2 * g.lds_floats * sizeof(float), s>>>(g, g_pre, Wd, dx, (float*)ws);
+    pcdf_reduce_k<<<dim3(g.ngroup, PC_FSL), 256, 0, s>>>(g, (const float*)ws, dx);
     return fail_launch("proj_conv_dgrad");
   }
   const PdGeom g = pd_plan(*d);

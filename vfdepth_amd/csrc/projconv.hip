@@ -844,6 +844,9 @@ __global__ __launch_bounds__(256) void pcd_reduce_k(PdGeom g, const float* __res
 struct PfGeom {
   int nbc, h, w, ntot, np, tpc, mtiles, ntile, natom, ngroup, hrows, cols, lds_floats, nfa, gfull;
 };
+#ifndef VFD_PF_HBIAS
+#define VFD_PF_HBIAS 2          // half-width groups beyond their rounded-up share: 0 / 1 / 2 / 4 -> 2.803 / 2.787 / 2.760 / 2.767 ms (one box, C-ABI micro)
+#endif
 
 __host__ __device__ inline int pf_lo(const PfGeom& g, int grp) {
   if (grp <= g.gfull) return (int)(((long long)grp * g.nfa) / g.gfull);
@@ -1173,8 +1176,8 @@ static PfGeom pf_plan(const vfd_voxel_desc& d) {
     // keep >= PD_CHUNKS atoms (a tile then meets at most two groups)
     const int nfa = (nn - 1) * g.mtiles * PD_CHUNKS, nha = g.natom - nfa;
     // a half-width atom costs at least half a full one (same staging and LDS reads, half the
-    // MFMAs): the share rounded up, plus one group, so the half-width groups are not the tail
-    int gh = (int)(((long long)g.ngroup * nha + 2LL * nfa + nha - 1) / (2LL * nfa + nha)) + 1;
+    // MFMAs): the share rounded up, plus VFD_PF_HBIAS groups, so the half-width groups are not the tail
+    int gh = (int)(((long long)g.ngroup * nha + 2LL * nfa + nha - 1) / (2LL * nfa + nha)) + VFD_PF_HBIAS;
     gh = gh > nha / PD_CHUNKS ? nha / PD_CHUNKS : gh;
     const int gf = g.ngroup - gh;
     if (gh >= 1 && gf >= 1 && gf <= nfa / PD_CHUNKS) {
